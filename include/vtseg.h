@@ -1,0 +1,272 @@
+/*
+ * vtseg.h — C ABI of libvtseg.so, the MI355X-native long-video segmenter.
+ *
+ * This is the drop-in boundary for the reference's segmenter hot path
+ * (shizhenneko/Video-Transformer).  The reference is pure Python and reaches
+ * ffprobe/ffmpeg through subprocess; the build keeps the Python call sites
+ * (package `vtseg`, same function names and signatures as the reference
+ * modules) and puts everything below them behind this header: plain C types,
+ * caller-allocated buffers, int status codes, a thread-local error string.
+ * No exception crosses the ABI.  ctypes releases the GIL around every call.
+ *
+ * Entry point → reference interface it replaces:
+ *   vts_plan_segments      utils/video_segmenter.py:42-83   plan_segments
+ *   vts_plan_with_budget   utils/budget_planner.py:73-194   plan_segments_with_budget
+ *   vts_probe_duration     utils/video_utils.py:7-38        probe_duration (ffprobe format=duration)
+ *   vts_probe_info         utils/video_utils.py:7-38        (same probe, all stream facts)
+ *   vts_boundary_frames*   (no reference code; video_segmenter.py:157-159 snap_to_keyframe
+ *                          is the identity stub this feeds)  segment time -> frame index
+ *   vts_open/vts_score/... (no reference code; north_star)   decode + NV12 scene scoring
+ *   vts_score_nv12_dev     (no reference code)               the scoring kernel on device NV12
+ *   vts_synth_write        (no reference code; tests/test_video_segmenter.py:147-178 builds
+ *                          its only synthetic clip with `ffmpeg -f lavfi`, absent here)
+ *
+ * Status codes: 0 = ok, < 0 = error (see VTS_E_*); vts_last_error() gives a
+ * message for the calling thread's last failure.
+ */
+#ifndef VTSEG_H
+#define VTSEG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VTS_ABI_VERSION 1
+
+enum {
+  VTS_OK = 0,
+  VTS_E_INVALID = -1,        /* bad argument (NULL pointer, bad geometry ...)        */
+  VTS_E_CAPACITY = -2,       /* output too small; *n_out holds the size needed       */
+  VTS_E_NONTERMINATING = -3, /* the reference loop would never end on this input     */
+  VTS_E_RANGE = -4,          /* integer result outside int64 (Python would use bigint) */
+  VTS_E_VALUE = -5,          /* Python ValueError (e.g. math.ceil(nan))              */
+  VTS_E_OVERFLOW = -6,       /* Python OverflowError (e.g. math.ceil(inf))           */
+  VTS_E_IO = -7,             /* file cannot be opened / read / written               */
+  VTS_E_FORMAT = -8,         /* container or bitstream not understood                */
+  VTS_E_UNSUPPORTED = -9,    /* valid H.264 outside the decoder's supported subset   */
+  VTS_E_HIP = -10,           /* HIP runtime error                                    */
+  VTS_E_NODEVICE = -11,      /* no usable gfx950 device                              */
+  VTS_E_DECODE = -12,        /* bitstream error found by the device-side parser      */
+  VTS_E_ZERODIV = -13        /* Python ZeroDivisionError (max_continuations == -1)   */
+};
+
+/* ---------------------------------------------------------------- planning */
+
+/* One planned window (reference SegmentInfo, video_segmenter.py:12-18). */
+typedef struct vts_segment {
+  int64_t segment_id;
+  double start;            /* extract window start (core start - overlap)  */
+  double end;              /* extract window end   (core end + overlap)    */
+  double effective_start;  /* core start                                   */
+  double effective_end;    /* core end                                     */
+  int64_t flags;           /* bit0: `end` is the duration argument itself,
+                              bit1: `effective_end` is the duration argument
+                              (lets the host mirror return the caller's int
+                              object where the reference does)             */
+} vts_segment;
+
+/* plan_segments (video_segmenter.py:42-83), bit-exact double arithmetic in
+ * the reference's operation order.  Two-call size query: with out == NULL or
+ * cap too small returns VTS_E_CAPACITY and sets *n_out to the count needed.
+ * Returns VTS_E_NONTERMINATING where the reference `while` never ends
+ * (cursor + segment_seconds == cursor, or duration = +inf). */
+int vts_plan_segments(double duration, double segment_seconds,
+                      double overlap_seconds, vts_segment *out, int64_t cap,
+                      int64_t *n_out);
+
+/* Budget-planner inputs after the reference's _coerce_int/_coerce_bool and
+ * float(threshold) (budget_planner.py:20-40, 95-103); the host mirror does the
+ * Python-object coercion and passes plain numbers here. */
+typedef struct vts_budget_cfg {
+  int64_t default_segment_seconds; /* long_video.default_segment_seconds (480) */
+  int64_t overlap_seconds;         /* long_video.overlap_seconds (20)          */
+  int64_t min_segment_seconds;     /* long_video.min_segment_seconds (90)      */
+  int64_t hard_max_api_calls;      /* long_video.hard_max_api_calls (50)       */
+  int64_t max_continuations;       /* analyzer.max_continuations (3)           */
+  int64_t retry_times;             /* analyzer.retry_times (0)                 */
+  int32_t has_threshold;           /* duration_threshold_seconds parsed?       */
+  int32_t consolidate;             /* long_video.consolidate (True)            */
+  double duration_threshold_seconds;
+} vts_budget_cfg;
+
+/* Reference SegmentPlan (budget_planner.py:9-17). */
+typedef struct vts_plan {
+  int64_t segment_duration;
+  int64_t overlap;
+  int64_t num_segments;
+  int64_t estimated_calls;
+  int64_t available_calls;
+  int64_t hard_max_calls;
+  int32_t fits_budget;
+  int32_t _pad;
+} vts_plan;
+
+/* plan_segments_with_budget (budget_planner.py:73-194).  `duration` is the
+ * reference's float(duration).  VTS_E_VALUE / VTS_E_OVERFLOW where the
+ * reference raises ValueError / OverflowError (NaN / inf durations). */
+int vts_plan_with_budget(double duration, const vts_budget_cfg *cfg,
+                         int64_t current_api_count, vts_plan *out);
+
+/* Segment time -> frame index.  For each t in times[0..ntimes): the index of
+ * the first frame (presentation order) whose pts satisfies
+ * pts / timescale >= t, compared exactly in integer arithmetic (no rounding);
+ * n_frames when no frame qualifies.  pts must be sorted ascending. */
+int vts_boundary_frames_pts(const int64_t *pts, int64_t n_frames,
+                            int64_t timescale, const double *times,
+                            int64_t ntimes, int64_t *frame_idx);
+
+/* ---------------------------------------------------------------- probing */
+
+typedef struct vts_video_info {
+  double duration;            /* == vts_probe_duration                       */
+  int64_t duration_us;        /* av_rescale(mvhd.duration, 1e6, mvhd.timescale) */
+  int64_t movie_timescale;    /* mvhd                                        */
+  int64_t movie_duration;     /* mvhd (movie timescale units)                */
+  int64_t track_timescale;    /* mdhd of the first video track               */
+  int64_t n_frames;           /* samples of the first video track            */
+  int64_t n_sync;             /* stss entries (0 = every sample is sync)     */
+  int32_t width, height;      /* display size (SPS crop applied)             */
+  int32_t coded_width, coded_height; /* macroblock-aligned size             */
+  int32_t profile_idc, level_idc;
+  int32_t codec;              /* 1 = H.264/avc1, 0 = other                   */
+  int32_t _pad;
+} vts_video_info;
+
+/* probe_duration (video_utils.py:7-38).  Parses the ISO-BMFF `moov` box: the
+ * value is the one ffprobe prints for `format=duration` on a non-fragmented
+ * MP4, (double)av_rescale(mvhd.duration, 1000000, mvhd.timescale) / 1e6.
+ * Never fails: returns VTS_OK with *seconds = 0.0 on any error, exactly like
+ * the reference (the reason is still available from vts_last_error()). */
+int vts_probe_duration(const char *path, double *seconds);
+
+/* All container facts of the first video track. Returns < 0 on error. */
+int vts_probe_info(const char *path, vts_video_info *info);
+
+/* ------------------------------------------------- device scoring kernel */
+
+/* Per-frame scene scoring of NV12 frames already in device memory.
+ *   thumbnail (w,h) = (width/k, height/k)   (k even, divides width and height)
+ *   Y'  = box mean of the k x k luma block,        (sum + k*k/2) / (k*k)
+ *   U',V' = box mean of the (k/2)x(k/2) chroma block, rounded the same way
+ *   RGB = BT.709 limited-range 8-bit fixed point of (Y',U',V')
+ *   hist[256]  = histogram of Y' over the thumbnail (uint32)
+ *   sad        = sum |Y'_t - Y'_{t-1}| over the thumbnail (uint64; 0 for the
+ *                first frame when prev_luma == NULL)
+ *   score      = (float)(sad / (w * h * 255.0))
+ * Frame i's Y plane starts at nv12 + i*frame_stride, its interleaved UV plane
+ * at + pitch*uv_row_offset.  Outputs are device pointers; any may be NULL
+ * except sad/score.  prev_luma (w*h bytes, device) seeds frame 0's SAD and
+ * last_luma (w*h bytes, device, may be NULL) receives the last frame's Y'. */
+typedef struct vts_score_desc {
+  const uint8_t *nv12;       /* device                                      */
+  int64_t frame_stride;      /* bytes between frames                        */
+  int64_t n_frames;
+  int32_t width, height;     /* luma size scored (display size)             */
+  int32_t pitch;             /* bytes per row, Y and UV                     */
+  int32_t uv_row_offset;     /* UV plane = Y + pitch*uv_row_offset          */
+  int32_t k;                 /* downscale factor: 2, 4, 6 or 8              */
+  int32_t _pad;
+  uint8_t *rgb;              /* n_frames * w*h*3, RGB interleaved           */
+  uint32_t *hist;            /* n_frames * 256                              */
+  uint64_t *sad;             /* n_frames                                    */
+  float *score;              /* n_frames                                    */
+  const uint8_t *prev_luma;  /* w*h or NULL                                 */
+  uint8_t *last_luma;        /* w*h or NULL                                 */
+  uint8_t *workspace;        /* device scratch, vts_score_workspace_bytes() */
+  int64_t workspace_bytes;
+} vts_score_desc;
+
+int64_t vts_score_workspace_bytes(int32_t width, int32_t height, int32_t k,
+                                  int64_t n_frames);
+/* Enqueue on `hip_stream` (a hipStream_t, NULL = default stream). */
+int vts_score_nv12_dev(const vts_score_desc *desc, void *hip_stream);
+
+/* --------------------------------------------- session: decode + score */
+
+typedef struct vts_ctx vts_ctx;
+
+typedef struct vts_params {
+  int32_t k;               /* thumbnail downscale; 0 = auto (4 for <=720p, 6 above) */
+  int32_t window_frames;   /* decoded-surface ring size in frames; 0 = auto        */
+  int32_t keep_rgb;        /* 1 = keep the last window's RGB thumbnails            */
+  int32_t n_streams;       /* 1 or 2 (2 = decode/score overlap on two HIP streams) */
+  float cut_threshold;     /* scene-cut threshold on score (default 0.08 when <=0) */
+  int32_t _pad;
+} vts_params;
+
+/* Demux the file's first H.264 video track on the host (MP4 boxes and NAL
+ * length prefixes only), upload the elementary stream to device `device`
+ * and prepare the decode schedule.  Fails with VTS_E_UNSUPPORTED for streams
+ * outside the device decoder's subset (see DESIGN.md §Decoder subset). */
+int vts_open(int device, const char *path, const vts_params *params,
+             vts_ctx **out);
+/* Same, from an in-memory MP4 image (copied). */
+int vts_open_memory(int device, const uint8_t *data, int64_t size,
+                    const vts_params *params, vts_ctx **out);
+int vts_info(const vts_ctx *ctx, vts_video_info *info);
+
+/* Decode every frame on the device and score it.  Host outputs, each may be
+ * NULL except scores; cap must be >= n_frames (else VTS_E_CAPACITY with
+ * *n_frames set).  pts is in track timescale units, presentation order. */
+int vts_score(vts_ctx *ctx, float *scores, uint32_t *hist, uint64_t *sad,
+              int64_t *pts, int64_t cap, int64_t *n_frames);
+/* Device-resident variant for benchmarking: decode + score all frames,
+ * results stay on the device; returns after the work is enqueued and
+ * finished (synchronous). */
+int vts_run(vts_ctx *ctx);
+/* Scene cut frame indices (score > threshold) of the last vts_score/vts_run. */
+int vts_scene_cuts(vts_ctx *ctx, int64_t *frame_idx, int64_t cap,
+                   int64_t *n_out);
+/* Frame index of each segment time (see vts_boundary_frames_pts). */
+int vts_boundary_frames(vts_ctx *ctx, const double *times, int64_t n,
+                        int64_t *frame_idx);
+/* Copy frame i's decoded NV12 (display size, pitch = width) of the most
+ * recent window to host; only frames still resident in the ring. */
+int vts_get_frame_nv12(vts_ctx *ctx, int64_t frame, uint8_t *out,
+                       int64_t out_bytes);
+/* Timing of the last vts_run/vts_score, milliseconds, HIP events:
+ * [0] whole, [1] parse, [2] reconstruct, [3] score. */
+int vts_last_timings(const vts_ctx *ctx, double *ms4);
+int vts_close(vts_ctx *ctx);
+
+/* ------------------------------------------------ synthetic stream writer */
+
+typedef struct vts_synth_params {
+  int32_t width, height;        /* multiples of 2; coded size = 16-aligned     */
+  int32_t fps_num, fps_den;     /* frame rate, e.g. 30/1                       */
+  int64_t n_frames;
+  uint64_t seed;                /* PCG32 seed                                   */
+  double cut_min_s, cut_max_s;  /* scene length ~ U[cut_min, cut_max] seconds   */
+  double gop_max_s;             /* IDR at least every gop_max seconds           */
+  int32_t max_motion;           /* |pan| per frame in luma pixels (even)        */
+  int32_t slices_per_row;       /* 1 = one slice per macroblock row            */
+} vts_synth_params;
+
+typedef struct vts_synth_info {
+  int64_t bytes_written;
+  int64_t n_idr;
+  int64_t n_cuts;               /* scene cuts (excluding frame 0)               */
+  int64_t timescale;            /* track timescale                              */
+} vts_synth_info;
+
+/* Write a conforming H.264 (Constrained Baseline, CAVLC, I_PCM intra
+ * macroblocks, P_L0_16x16 / P_Skip integer-motion inter macroblocks without
+ * residual, deblocking disabled) elementary stream in an MP4 container.
+ * cut_frames (may be NULL, cap entries) receives the ground-truth scene-cut
+ * frame indices. */
+int vts_synth_write(const char *path, const vts_synth_params *p,
+                    vts_synth_info *info, int64_t *cut_frames, int64_t cap);
+
+/* ------------------------------------------------------------------ misc */
+const char *vts_last_error(void);
+int vts_abi_version(void);
+/* Number of visible HIP devices (0 when none); never initialises more than
+ * the HIP runtime. */
+int vts_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VTSEG_H */

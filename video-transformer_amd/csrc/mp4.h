@@ -1,0 +1,78 @@
+// mp4.h — ISO-BMFF (MP4) demuxer and muxer for H.264 video tracks.
+//
+// Demux side replaces the container half of `ffprobe`/`ffmpeg` in the
+// reference (utils/video_utils.py:9-27 probes `format=duration`;
+// utils/video_segmenter.py:118-136 stream-copies): it reads `moov` only, never
+// the media payload, and yields the per-sample table (offset, size, dts, cts,
+// sync) the device decoder schedules from.
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+namespace vts {
+
+struct EditEntry {
+  int64_t segment_duration;  // movie timescale
+  int64_t media_time;        // track timescale, -1 = empty edit
+};
+
+struct Mp4VideoTrack {
+  uint32_t track_id = 0;
+  int64_t timescale = 0;
+  int64_t duration = 0;       // mdhd, track timescale
+  int tkhd_width = 0, tkhd_height = 0;
+  std::string codec;          // sample entry fourcc ("avc1", "hvc1", ...)
+  int nal_length_size = 4;
+  std::vector<std::vector<uint8_t>> sps, pps;
+  std::vector<int64_t> offset;
+  std::vector<uint32_t> size;
+  std::vector<int64_t> dts;
+  std::vector<int32_t> cts_offset;  // ctts, 0 when absent
+  std::vector<uint8_t> sync;        // 1 = sync sample (all 1 when no stss)
+  bool has_stss = false;
+  bool has_ctts = false;
+  std::vector<EditEntry> edits;
+};
+
+struct Mp4Info {
+  int64_t movie_timescale = 0;
+  int64_t movie_duration = 0;
+  bool has_mvhd = false;
+  bool fragmented = false;   // moof/mvex present
+  int64_t file_size = 0;
+  std::vector<Mp4VideoTrack> video;
+};
+
+// Parse the container from a file path or from memory. "" = ok, else error.
+std::string mp4_parse_file(const char *path, Mp4Info *out);
+std::string mp4_parse_memory(const uint8_t *data, int64_t size, Mp4Info *out);
+
+// libavformat: s->duration = av_rescale(mvhd.duration, AV_TIME_BASE, timescale)
+// (round to nearest, ties away from zero); a timescale <= 0 reads as 1.
+int64_t mvhd_duration_us(const Mp4Info &info);
+
+// Streaming MP4 writer: ftyp, mdat (64-bit size), moov at the end.
+class Mp4Writer {
+ public:
+  ~Mp4Writer();
+  std::string open(const char *path);
+  std::string add_sample(const uint8_t *data, size_t n, bool sync);
+  // track_timescale / sample_delta: constant frame duration; movie timescale
+  // 1000.  sps/pps: NAL units including their header byte.
+  std::string finish(int width, int height, int64_t track_timescale,
+                     int64_t sample_delta, const std::vector<uint8_t> &sps,
+                     const std::vector<uint8_t> &pps);
+  int64_t bytes_written() const { return pos_; }
+
+ private:
+  FILE *f_ = nullptr;
+  int64_t pos_ = 0;
+  int64_t mdat_start_ = 0;
+  std::vector<int64_t> offsets_;
+  std::vector<uint32_t> sizes_;
+  std::vector<uint32_t> sync_;
+};
+
+}  // namespace vts

@@ -1,0 +1,82 @@
+// probe.cpp — container probing (reference utils/video_utils.py:7-38).
+#include <cstring>
+
+#include "common.h"
+#include "h264.h"
+#include "mp4.h"
+
+namespace vts {
+
+// Fill `info` from a parsed container. Returns VTS_OK or an error code.
+int fill_video_info(const Mp4Info &mp4, vts_video_info *info) {
+  std::memset(info, 0, sizeof *info);
+  info->movie_timescale = mp4.movie_timescale;
+  info->movie_duration = mp4.movie_duration;
+  if (mp4.has_mvhd && !mp4.fragmented) {
+    info->duration_us = mvhd_duration_us(mp4);
+    info->duration = static_cast<double>(info->duration_us) / 1e6;
+  }
+  if (mp4.video.empty()) return fail(VTS_E_FORMAT, "no video track");
+  const Mp4VideoTrack &t = mp4.video.front();
+  info->track_timescale = t.timescale;
+  info->n_frames = static_cast<int64_t>(t.size.size());
+  int64_t nsync = 0;
+  if (t.has_stss)
+    for (uint8_t s : t.sync) nsync += s;
+  info->n_sync = nsync;
+  info->width = t.tkhd_width;
+  info->height = t.tkhd_height;
+  info->codec = (t.codec == "avc1" || t.codec == "avc3") ? 1 : 0;
+  if (info->codec && !t.sps.empty()) {
+    Sps sps;
+    if (parse_sps(t.sps[0].data(), t.sps[0].size(), &sps).empty()) {
+      info->width = sps.width();
+      info->height = sps.height();
+      info->coded_width = sps.mb_width * 16;
+      info->coded_height = sps.mb_height * 16;
+      info->profile_idc = sps.profile_idc;
+      info->level_idc = sps.level_idc;
+    }
+  }
+  return VTS_OK;
+}
+
+}  // namespace vts
+
+using namespace vts;
+
+extern "C" int vts_probe_info(const char *path, vts_video_info *info) {
+  clear_error();
+  if (!path || !info) return fail(VTS_E_INVALID, "NULL argument");
+  Mp4Info mp4;
+  const std::string e = mp4_parse_file(path, &mp4);
+  if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
+  return fill_video_info(mp4, info);
+}
+
+extern "C" int vts_probe_duration(const char *path, double *seconds) {
+  clear_error();
+  if (!seconds) return fail(VTS_E_INVALID, "seconds is NULL");
+  *seconds = 0.0;  // reference convention: 0.0 on any failure, never an error
+  if (!path) {
+    fail(VTS_E_INVALID, "path is NULL");
+    return VTS_OK;
+  }
+  Mp4Info mp4;
+  const std::string e = mp4_parse_file(path, &mp4);
+  if (!e.empty()) {
+    fail(VTS_E_FORMAT, "%s", e.c_str());
+    return VTS_OK;
+  }
+  if (!mp4.has_mvhd) {
+    fail(VTS_E_FORMAT, "no mvhd");
+    return VTS_OK;
+  }
+  if (mp4.fragmented) {
+    fail(VTS_E_FORMAT, "fragmented MP4: duration needs the fragment index");
+    return VTS_OK;
+  }
+  // ffprobe prints 0 duration as "N/A" -> the reference's float() fails -> 0.0
+  *seconds = static_cast<double>(mvhd_duration_us(mp4)) / 1e6;
+  return VTS_OK;
+}

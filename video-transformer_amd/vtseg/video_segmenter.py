@@ -1,0 +1,259 @@
+"""Drop-in for the reference ``utils.video_segmenter`` (src/utils/video_segmenter.py).
+
+Same public names, signatures, types and error conventions as the reference
+module; the planning arithmetic runs in libvtseg (C++, bit-exact) through
+``vtseg._lib``.  Manifest persistence stays plain JSON with the reference's
+exact formatting (``indent=2, ensure_ascii=True``) so an existing manifest is
+resumable by either implementation.
+
+Reference map:
+    SegmentInfo / SegmentEntry / SegmentManifest   video_segmenter.py:12-39
+    plan_segments                                  video_segmenter.py:42-83
+    extract_segment                                video_segmenter.py:86-154
+    snap_to_keyframe                               video_segmenter.py:157-159
+    get_segment_dir / get_manifest_path            video_segmenter.py:162-167
+    create_manifest / load_manifest / save_manifest / load_or_create_manifest
+                                                   video_segmenter.py:170-238
+    pending_segments / update_segment_status       video_segmenter.py:241-266
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import logging
+import numbers
+import subprocess
+from dataclasses import dataclass
+from datetime import datetime, timezone
+from pathlib import Path
+from typing import TypedDict, cast
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class SegmentInfo:
+    segment_id: int
+    start: float
+    end: float
+    effective_start: float
+    effective_end: float
+
+
+class SegmentEntry(TypedDict):
+    id: int
+    start: float
+    end: float
+    effective_start: float
+    effective_end: float
+    file_path: str
+    status: str
+    attempts: int
+    error: str | None
+
+
+class SegmentManifest(TypedDict):
+    version: int
+    video_id: str
+    created_at: str
+    segment_seconds: float
+    overlap_seconds: float
+    segments: list[SegmentEntry]
+
+
+def _as_real(name: str, value: object) -> float:
+    """float(value) for the real-number types the reference accepts.
+
+    The reference compares its arguments with ``<=``/``<`` and adds them to
+    floats, so non-numbers raise TypeError there; they do here too.
+    """
+    if isinstance(value, numbers.Real):
+        return float(value)
+    raise TypeError(
+        f"'<=' not supported between instances of '{type(value).__name__}' and 'int'"
+        f" ({name})")
+
+
+def plan_segments(
+    duration: float, segment_seconds: float, overlap_seconds: float
+) -> list[SegmentInfo]:
+    """Fixed windows with overlap on the inner sides (video_segmenter.py:42-83).
+
+    Runs ``vts_plan_segments`` in libvtseg.  Raises ``vtseg.NonTerminatingError``
+    where the reference loop would never end (e.g. duration = +inf).
+    """
+    d = _as_real("duration", duration)
+    s = _as_real("segment_seconds", segment_seconds)
+    o = _as_real("overlap_seconds", overlap_seconds)
+    lib = _lib.lib()
+    n = C.c_int64(0)
+    cap = 64
+    while True:
+        buf = (_lib.Segment * cap)()
+        rc = lib.vts_plan_segments(d, s, o, buf, cap, C.byref(n))
+        if rc == _lib.VTS_E_CAPACITY:
+            cap = int(n.value)
+            continue
+        _lib.check(rc)
+        break
+    # The reference returns the caller's own `duration` object in two places
+    # (min()/ternary picks it); keep that for int durations.
+    keep = isinstance(duration, int)
+    out: list[SegmentInfo] = []
+    for i in range(int(n.value)):
+        g = buf[i]
+        out.append(SegmentInfo(
+            segment_id=int(g.segment_id),
+            start=g.start,
+            end=duration if keep and (g.flags & 1) else g.end,
+            effective_start=g.effective_start,
+            effective_end=duration if keep and (g.flags & 2) else g.effective_end,
+        ))
+    return out
+
+
+def extract_segment(
+    input_path: str | Path,
+    start: float,
+    end: float,
+    output_path: str | Path,
+    stream_copy: bool = True,
+) -> bool:
+    """Cut [start, end] into output_path (video_segmenter.py:86-154).
+
+    Same contract as the reference: ``ffmpeg -ss S -i IN -t D -movflags
+    +faststart -c copy OUT`` with an x264/AAC re-encode fallback, ``%.3f``
+    timestamps, 120 s timeout, never raises, False on any failure, a failed
+    copy's partial output is unlinked.  (A native MP4 stream-copy remuxer is
+    the next item on this path)
+    """
+    duration = end - start
+    if duration <= 0:
+        return False
+
+    input_path = Path(input_path)
+    output_path = Path(output_path)
+    output_path.parent.mkdir(parents=True, exist_ok=True)
+
+    def run(args: list[str]) -> bool:
+        try:
+            proc = subprocess.run(args, capture_output=True, text=True, timeout=120)
+        except (FileNotFoundError, OSError, subprocess.TimeoutExpired):
+            return False
+        return (proc.returncode == 0 and output_path.exists()
+                and output_path.stat().st_size > 0)
+
+    head = ["ffmpeg", "-y", "-hide_banner", "-loglevel", "error",
+            "-ss", f"{start:.3f}", "-i", str(input_path),
+            "-t", f"{duration:.3f}", "-movflags", "+faststart"]
+    if stream_copy:
+        if run(head + ["-c", "copy", str(output_path)]):
+            return True
+        if output_path.exists():
+            output_path.unlink()
+    return run(head + ["-c:v", "libx264", "-preset", "veryfast", "-crf", "23",
+                       "-c:a", "aac", "-b:a", "128k", str(output_path)])
+
+
+def snap_to_keyframe(video_path: str | Path, timestamp: float) -> float:
+    """Identity clamp, exactly as the reference stub (video_segmenter.py:157-159).
+
+    Keyframe/scene-aware snapping is opt-in elsewhere (vtseg.scene); the
+    default must stay the identity so segment lists stay bit-identical.
+    """
+    _ = video_path
+    return max(0.0, float(timestamp))
+
+
+def get_segment_dir(video_id: str, temp_dir: str | Path) -> Path:
+    return Path(temp_dir) / "segments" / video_id
+
+
+def get_manifest_path(video_id: str, temp_dir: str | Path) -> Path:
+    return get_segment_dir(video_id, temp_dir) / "manifest.json"
+
+
+def create_manifest(
+    *,
+    video_id: str,
+    duration: float,
+    segment_seconds: float,
+    overlap_seconds: float,
+    temp_dir: str | Path,
+) -> SegmentManifest:
+    segment_dir = get_segment_dir(video_id, temp_dir)
+    segment_dir.mkdir(parents=True, exist_ok=True)
+    entries: list[SegmentEntry] = []
+    for seg in plan_segments(duration, segment_seconds, overlap_seconds):
+        entries.append({
+            "id": seg.segment_id,
+            "start": seg.start,
+            "end": seg.end,
+            "effective_start": seg.effective_start,
+            "effective_end": seg.effective_end,
+            "file_path": str(segment_dir / f"segment_{seg.segment_id:04d}.mp4"),
+            "status": "pending",
+            "attempts": 0,
+            "error": None,
+        })
+    manifest: SegmentManifest = {
+        "version": 1,
+        "video_id": video_id,
+        "created_at": datetime.now(timezone.utc).isoformat(),
+        "segment_seconds": segment_seconds,
+        "overlap_seconds": overlap_seconds,
+        "segments": entries,
+    }
+    save_manifest(get_manifest_path(video_id, temp_dir), manifest)
+    return manifest
+
+
+def load_manifest(manifest_path: str | Path) -> SegmentManifest:
+    return cast(SegmentManifest,
+                json.loads(Path(manifest_path).read_text(encoding="utf-8")))
+
+
+def save_manifest(manifest_path: str | Path, manifest: SegmentManifest) -> None:
+    path = Path(manifest_path)
+    path.parent.mkdir(parents=True, exist_ok=True)
+    _ = path.write_text(json.dumps(manifest, indent=2, ensure_ascii=True),
+                        encoding="utf-8")
+
+
+def load_or_create_manifest(
+    *,
+    video_id: str,
+    duration: float,
+    segment_seconds: float,
+    overlap_seconds: float,
+    temp_dir: str | Path,
+) -> SegmentManifest:
+    manifest_path = get_manifest_path(video_id, temp_dir)
+    if manifest_path.exists():  # resume: reuse the persisted plan verbatim
+        return load_manifest(manifest_path)
+    return create_manifest(video_id=video_id, duration=duration,
+                           segment_seconds=segment_seconds,
+                           overlap_seconds=overlap_seconds, temp_dir=temp_dir)
+
+
+def pending_segments(manifest: SegmentManifest) -> list[SegmentEntry]:
+    return [seg for seg in manifest["segments"] if seg["status"] != "completed"]
+
+
+def update_segment_status(
+    manifest: SegmentManifest,
+    segment_id: int,
+    status: str,
+    *,
+    error: str | None = None,
+    increment_attempts: bool = False,
+) -> None:
+    for seg in manifest["segments"]:
+        if seg["id"] == segment_id:
+            seg["status"] = status
+            if error is not None:
+                seg["error"] = error
+            if increment_attempts:
+                seg["attempts"] = seg["attempts"] + 1
+            return
+    logging.getLogger(__name__).warning("Segment id %s not found in manifest", segment_id)
