@@ -1,0 +1,240 @@
+"""Benchmark: 720p frames/s decoded+scored per node (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload decode_score|score]
+
+One process per GPU (torch.distributed.run for N > 1; RANK/LOCAL_RANK/
+WORLD_SIZE from the env, rendezvous on 127.0.0.1).  Weak scaling: every rank
+processes its own synthetic 10-min 720p video (BASELINE config [1]; config [3]
+= 32 such videos over 8 GPUs is the same per-GPU load), and after each step
+the ranks all-gather their per-video segment counts over RCCL (the only
+collective on this path; no pixel data crosses GPUs).
+
+A step = one pass of the hot path over one whole video with its input already
+resident in HBM:
+  decode_score : device H.264 subset decode (parse + reconstruct) + scoring
+  score        : scoring kernel only, on pre-decoded NV12 frames
+Rank 0 prints ONE JSON line (contract in the task statement), including
+`roofline` (dominant kernel, HIP-event timed on its own stream) and
+`cpu_baseline` (the C oracle on a bounded sample, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "video-transformer_amd"))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FPS = 30
+METRIC = "720p frames/sec decoded+scored per node; segment-index exact-match vs CPU"
+
+
+def algorithmic_bytes_per_frame(width: int, height: int, k: int) -> int:
+    """NV12 read + RGB thumbnail write + thumbnail luma
+    write/read + histogram + score."""
+    w, h = width // k, height // k
+    return int(1.5 * width * height) + 3 * w * h + 2 * w * h + 1024 + 4
+
+
+def smooth_frames_host(rng, n, width, height):
+    frames = np.empty((n, height * 3 // 2, width), np.uint8)
+    for i in range(n):
+        g = rng.integers(16, 236, size=(height // 32 + 2, width // 32 + 2)).astype(np.float32)
+        y = np.kron(g, np.ones((32, 32), np.float32))[:height, :width]
+        frames[i, :height] = np.clip(y + rng.normal(0, 4, y.shape), 0, 255).astype(np.uint8)
+        c = rng.integers(64, 192, size=(height // 64 + 2, width // 16 + 2)).astype(np.float32)
+        frames[i, height:] = np.kron(c, np.ones((32, 16), np.float32))[:height // 2, :width]
+    return frames
+
+
+def cpu_baseline_score(width, height, k, budget_s=10.0):
+    """Oracle scorer (scalar C, 1 thread) on a bounded sample of frames."""
+    import oracle
+    rng = np.random.default_rng(1)
+    frames = smooth_frames_host(rng, 8, width, height).reshape(-1)
+    stride = width * height * 3 // 2
+    t0 = time.perf_counter()
+    oracle.score_frames(frames, stride, 8, width, height, width, height, k, want_rgb=True)
+    per = (time.perf_counter() - t0) / 8
+    n = max(8, min(4000, int(budget_s / max(per, 1e-6))))
+    reps = (n + 7) // 8
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle.score_frames(frames, stride, 8, width, height, width, height, k, want_rgb=True)
+    dt = time.perf_counter() - t0
+    return {"value": round(reps * 8 / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{reps * 8} frames {width}x{height} scored by oracle/vtseg_oracle.c "
+                      f"or_score_frames (scalar, 1 thread), {dt:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="decode_score", choices=["decode_score", "score"])
+    ap.add_argument("--frames", type=int, default=18000, help="10 min at 30 fps")
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from vtseg import scene
+    from vtseg import budget_planner as bp
+    from vtseg import video_segmenter as vs
+
+    width, height, k = args.width, args.height, 4 if args.height <= 720 else 6
+    F = args.frames
+    w, h = width // k, height // k
+    stride = width * height * 3 // 2
+
+    # ---------------------------------------------------------------- inputs
+    tmpdir = tempfile.mkdtemp(prefix="vtseg_bench_")
+    scorer = None
+    if args.workload == "score":
+        rng = np.random.default_rng(100 + rank)
+        pool = torch.from_numpy(smooth_frames_host(rng, 64, width, height)).to(device)
+        reps = (F + 63) // 64
+        nv12 = pool.reshape(64, -1).repeat(reps, 1)[:F].contiguous().reshape(-1)
+        del pool
+        outs = {}
+
+        def step():
+            outs["r"] = scene.score_nv12(nv12, width=width, height=height, pitch=width,
+                                         uv_row_offset=height, frame_stride=stride,
+                                         n_frames=F, k=k, out=outs.get("r"),
+                                         workspace=outs.get("r", {}).get("_workspace"))
+        duration_s = F / FPS
+    else:
+        path = Path(tmpdir) / f"synth_rank{rank}.mp4"
+        scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
+                          seed=0x5EED + rank)
+        scorer = scene.VideoScorer(path, device=local)
+        duration_s = float(scorer.info.duration)
+
+        def step():
+            scorer.run()
+
+    # per-video segment plan under the reference's default config (config.yaml)
+    cfg = {"analyzer": {"max_continuations": 3, "retry_times": 5,
+                        "long_video": {"enabled": True, "default_segment_seconds": 480,
+                                       "overlap_seconds": 20, "min_segment_seconds": 90,
+                                       "hard_max_api_calls": 50, "consolidate": True,
+                                       "duration_threshold_seconds": None}}}
+    plan = bp.plan_segments_with_budget(duration_s, cfg, 0)
+    n_segments = len(vs.plan_segments(duration_s, plan.segment_duration, plan.overlap))
+    counts_local = torch.tensor([n_segments], dtype=torch.int32, device=device)
+    counts_all = torch.zeros(world, dtype=torch.int32, device=device)
+
+    def gather_counts():
+        if world > 1:
+            dist.all_gather_into_tensor(counts_all, counts_local)
+        else:
+            counts_all.copy_(counts_local)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---------------------------------------------------------------- timing
+    for _ in range(args.warmup):
+        step()
+        gather_counts()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        gather_counts()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_frames = F * world * args.steps
+    value = total_frames / elapsed
+
+    # ------------------------------------------- roofline (dominant kernel)
+    roof = None
+    if args.workload == "score":
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 5
+        ev0.record()
+        for _ in range(reps):
+            step()
+        ev1.record()
+        torch.cuda.synchronize()
+        kern_ms = ev0.elapsed_time(ev1) / reps
+        kname = "score_runs<4>"
+    else:
+        times = []
+        for _ in range(3):
+            scorer.run()
+            times.append(scorer.timings())
+        kern_ms = float(np.mean([t["score_ms"] for t in times]))
+        kname = "score_runs<%d>" % k
+    bytes_per_frame = algorithmic_bytes_per_frame(width, height, k)
+    achieved = bytes_per_frame * F / (kern_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": kname, "kernel_ms": round(kern_ms, 4),
+            "bytes_per_frame": bytes_per_frame, "frames_per_launch": F}
+
+    counts = counts_all.cpu().tolist()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_score(width, height, k)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"{args.workload}: 10-min {width}x{height} @30fps "
+                                   f"({F} frames) per GPU, thumbnails k={k}",
+                       "frames_per_gpu": F, "width": width, "height": height, "k": k,
+                       "parallelism": f"video-per-gpu x{world}",
+                       "segment_counts": counts},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if scorer is not None:
+            line["config"]["stage_ms"] = scorer.timings()
+        print(json.dumps(line), flush=True)
+    if scorer is not None:
+        scorer.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -241,7 +241,10 @@ typedef struct vts_synth_params {
   double cut_min_s, cut_max_s;  /* scene length ~ U[cut_min, cut_max] seconds   */
   double gop_max_s;             /* IDR at least every gop_max seconds           */
   int32_t max_motion;           /* |pan| per frame in luma pixels (even)        */
-  int32_t slices_per_row;       /* 1 = one slice per macroblock row            */
+  int32_t slices_per_row;       /* n > 0: n slices per macroblock row; 0: one
+                                   slice per picture                            */
+  int32_t hash_frames;          /* 1 = compute vts_synth_info.recon_hash        */
+  int32_t _pad;
 } vts_synth_params;
 
 typedef struct vts_synth_info {
@@ -249,6 +252,9 @@ typedef struct vts_synth_info {
   int64_t n_idr;
   int64_t n_cuts;               /* scene cuts (excluding frame 0)               */
   int64_t timescale;            /* track timescale                              */
+  uint64_t recon_hash;          /* sum over frames f, bytes j of the display-size
+                                   NV12 frame: b_j * ((j % 65521) + 1) * (f + 1),
+                                   mod 2^64 (the encoder's own reconstruction)  */
 } vts_synth_info;
 
 /* Write a conforming H.264 (Constrained Baseline, CAVLC, I_PCM intra

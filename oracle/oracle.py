@@ -64,6 +64,10 @@ def lib() -> C.CDLL:
         _lib.or_plan_with_budget.argtypes = [C.c_double, C.POINTER(BudgetCfg), C.c_int64,
                                              C.POINTER(_Plan)]
         u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+        _lib.or_parse_sps_pps.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64,
+                                          C.c_int, C.c_void_p]
+        _lib.or_decode_samples.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_int64, C.c_void_p, C.c_void_p]
         _lib.or_score_frames.argtypes = [
             u8p, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -130,3 +134,162 @@ def score_frames(nv12: np.ndarray, frame_stride: int, n_frames: int, width: int,
         raise RuntimeError(f"oracle score_frames rc={rc}")
     return {"rgb": rgb, "hist": hist.reshape(n_frames, 256), "sad": sad, "score": score,
             "last_luma": last}
+
+
+# ------------------------------------------------------------- MP4 + decode
+class H264Params(C.Structure):
+    _fields_ = [(n, C.c_int) for n in (
+        "mb_width", "mb_height", "crop_right", "crop_bottom", "log2_max_frame_num",
+        "poc_type", "log2_max_poc_lsb", "delta_pic_order_always_zero",
+        "bottom_field_pic_order_in_frame_present", "num_ref_idx_l0_default_active",
+        "redundant_pic_cnt_present", "deblocking_filter_control_present", "pic_init_qp",
+        "pps_id", "nal_length_size")]
+
+
+def _boxes(buf: bytes, start: int, end: int):
+    import struct
+    pos = start
+    while pos + 8 <= end:
+        size, typ = struct.unpack(">I4s", buf[pos:pos + 8])
+        hdr = 8
+        if size == 1:
+            size = struct.unpack(">Q", buf[pos + 8:pos + 16])[0]
+            hdr = 16
+        elif size == 0:
+            size = end - pos
+        if size < hdr or pos + size > end:
+            raise ValueError("bad box")
+        yield typ.decode("latin1"), pos + hdr, pos + size
+        pos += size
+
+
+def read_mp4(path) -> dict:
+    """Minimal independent ISO-BMFF reader (first video track, moov only):
+    sample offsets/sizes/dts, avcC parameter sets, mvhd/mdhd timing."""
+    import struct
+    data = Path(path).read_bytes()
+    top = {t: (a, b) for t, a, b in _boxes(data, 0, len(data))}
+    ma, mb = top["moov"]
+    out = {"data": data}
+
+    def child(a, b, name):
+        for t, ca, cb in _boxes(data, a, b):
+            if t == name:
+                return ca, cb
+        return None
+
+    mv = child(ma, mb, "mvhd")
+    v = data[mv[0]]
+    if v == 1:
+        out["movie_timescale"], out["movie_duration"] = struct.unpack(">IQ", data[mv[0] + 20:mv[0] + 32])
+    else:
+        out["movie_timescale"], out["movie_duration"] = struct.unpack(">II", data[mv[0] + 12:mv[0] + 20])
+    for t, ta, tb in _boxes(data, ma, mb):
+        if t != "trak":
+            continue
+        mdia = child(ta, tb, "mdia")
+        hdlr = child(*mdia, "hdlr")
+        if data[hdlr[0] + 8:hdlr[0] + 12] != b"vide":
+            continue
+        mdhd = child(*mdia, "mdhd")
+        if data[mdhd[0]] == 1:
+            ts, dur = struct.unpack(">IQ", data[mdhd[0] + 20:mdhd[0] + 32])
+        else:
+            ts, dur = struct.unpack(">II", data[mdhd[0] + 12:mdhd[0] + 20])
+        stbl = child(*child(*mdia, "minf"), "stbl")
+        stsd = child(*stbl, "stsd")
+        ea = stsd[0] + 8
+        esz = struct.unpack(">I", data[ea:ea + 4])[0]
+        avcc = child(ea + 8 + 78, ea + esz, "avcC")
+        a = avcc[0]
+        lsize = (data[a + 4] & 3) + 1
+        p = a + 5
+        nsps = data[p] & 31
+        p += 1
+        sps = []
+        for _ in range(nsps):
+            n = struct.unpack(">H", data[p:p + 2])[0]
+            sps.append(data[p + 2:p + 2 + n])
+            p += 2 + n
+        npps = data[p]
+        p += 1
+        pps = []
+        for _ in range(npps):
+            n = struct.unpack(">H", data[p:p + 2])[0]
+            pps.append(data[p + 2:p + 2 + n])
+            p += 2 + n
+        sa, sb = child(*stbl, "stsz")
+        uni, cnt = struct.unpack(">II", data[sa + 4:sa + 12])
+        sizes = [uni] * cnt if uni else list(struct.unpack(f">{cnt}I", data[sa + 12:sa + 12 + 4 * cnt]))
+        co = child(*stbl, "co64")
+        if co:
+            nc = struct.unpack(">I", data[co[0] + 4:co[0] + 8])[0]
+            chunks = list(struct.unpack(f">{nc}Q", data[co[0] + 8:co[0] + 8 + 8 * nc]))
+        else:
+            co = child(*stbl, "stco")
+            nc = struct.unpack(">I", data[co[0] + 4:co[0] + 8])[0]
+            chunks = list(struct.unpack(f">{nc}I", data[co[0] + 8:co[0] + 8 + 4 * nc]))
+        sc = child(*stbl, "stsc")
+        ne = struct.unpack(">I", data[sc[0] + 4:sc[0] + 8])[0]
+        ents = [struct.unpack(">III", data[sc[0] + 8 + 12 * i:sc[0] + 20 + 12 * i]) for i in range(ne)]
+        offsets = []
+        s = 0
+        for i, (first, spc, _) in enumerate(ents):
+            last = ents[i + 1][0] if i + 1 < ne else len(chunks) + 1
+            for c in range(first, last):
+                off = chunks[c - 1]
+                for _ in range(spc):
+                    if s >= cnt:
+                        break
+                    offsets.append(off)
+                    off += sizes[s]
+                    s += 1
+        st = child(*stbl, "stts")
+        ne = struct.unpack(">I", data[st[0] + 4:st[0] + 8])[0]
+        dts, d = [], 0
+        for i in range(ne):
+            c2, delta = struct.unpack(">II", data[st[0] + 8 + 8 * i:st[0] + 16 + 8 * i])
+            for _ in range(c2):
+                dts.append(d)
+                d += delta
+        out.update(timescale=ts, duration=dur, nal_length_size=lsize, sps=sps, pps=pps,
+                   offsets=offsets, sizes=sizes, dts=dts[:cnt])
+        return out
+    raise ValueError("no video track")
+
+
+def decode_file(path):
+    """Decode every frame with the scalar oracle; returns (frames uint8
+    [F, H*3/2, W] display-size NV12, info dict)."""
+    m = read_mp4(path)
+    L = lib()
+    prm = H264Params()
+    sps, pps = m["sps"][0], m["pps"][0]
+    rc = L.or_parse_sps_pps(sps, len(sps), pps, len(pps), m["nal_length_size"], C.byref(prm))
+    if rc != 0:
+        raise RuntimeError(f"oracle SPS/PPS rc={rc}")
+    W = prm.mb_width * 16 - prm.crop_right
+    H = prm.mb_height * 16 - prm.crop_bottom
+    n = len(m["sizes"])
+    out = np.zeros((n, H * 3 // 2, W), np.uint8)
+    offs = np.asarray(m["offsets"], np.int64)
+    sizes = np.asarray(m["sizes"], np.int64)
+    bad = C.c_int64(-1)
+    data = np.frombuffer(m["data"], np.uint8)
+    rc = L.or_decode_samples(C.byref(prm), data.ctypes.data, offs.ctypes.data,
+                             sizes.ctypes.data, n, out.ctypes.data, C.byref(bad))
+    if rc != 0:
+        raise RuntimeError(f"oracle decode rc={rc} at frame {bad.value}")
+    info = {"width": W, "height": H, "timescale": m["timescale"], "pts": m["dts"],
+            "movie_timescale": m["movie_timescale"], "movie_duration": m["movie_duration"]}
+    return out, info
+
+
+def recon_hash(frames: np.ndarray) -> int:
+    """Hash of decoded display-size NV12 frames, same definition as
+    vts_synth_info.recon_hash."""
+    F = frames.shape[0]
+    flat = frames.reshape(F, -1).astype(np.uint64)
+    w = (np.arange(flat.shape[1], dtype=np.uint64) % np.uint64(65521)) + np.uint64(1)
+    per = (flat * w).sum(axis=1, dtype=np.uint64)
+    return int((per * (np.arange(F, dtype=np.uint64) + np.uint64(1))).sum(dtype=np.uint64))

@@ -1,0 +1,115 @@
+"""Device decode + score (vts_open/vts_score, HIP on gfx950) vs the C oracle.
+
+For each synthetic stream: every decoded NV12 frame, every 256-bin histogram
+and SAD, and every fp32 score must equal the scalar oracle's bit for bit
+(north_star allows |d score| <= 1e-4; integer accumulation makes it exact and
+the test asserts exact equality).  Segment boundary frame indices must match
+the exact rational oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+from vtseg import VtsegError, scene
+from vtseg import video_segmenter as vs
+
+pytestmark = pytest.mark.gpu
+
+STREAMS = [
+    ("qvga", dict(width=320, height=240)),
+    ("median", dict(width=320, height=240, slices_per_row=0, max_motion=8)),
+    ("ragged", dict(width=336, height=200, slices_per_row=3, max_motion=6)),
+    ("nhd", dict(width=640, height=360, slices_per_row=2, max_motion=2)),
+    ("static", dict(width=96, height=64, max_motion=0)),
+    ("hd720", dict(width=1280, height=720, max_motion=4)),
+    ("fhd", dict(width=1920, height=1080, max_motion=8)),
+]
+
+
+def _require_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test requires an MI355X")
+
+
+def _oracle_scores(frames, w, h):
+    k = 4 if h <= 720 else 6
+    return oracle.score_frames(frames.reshape(-1), frames[0].size, frames.shape[0], w, h, w, h, k,
+                               want_rgb=False)
+
+
+@pytest.mark.parametrize("name,kw", STREAMS, ids=[s[0] for s in STREAMS])
+def test_decode_and_score_bit_exact(tmp_path, name, kw):
+    _require_gpu()
+    n = 90 if kw["height"] < 720 else 40
+    path = tmp_path / f"{name}.mp4"
+    r = scene.synth_write(path, n_frames=n, cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.8,
+                          hash_frames=True, **kw)
+    frames, info = oracle.decode_file(path)
+    assert oracle.recon_hash(frames) == r["recon_hash"]
+    ref = _oracle_scores(frames, kw["width"], kw["height"])
+    with scene.VideoScorer(path) as vsr:
+        res = vsr.score()
+        for i in range(n):
+            got = vsr.frame_nv12(i).reshape(frames[i].shape)
+            assert np.array_equal(got, frames[i]), f"frame {i} differs"
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+        assert res.pts.tolist() == info["pts"]
+        cuts = vsr.scene_cuts()
+        assert cuts == np.nonzero(ref["score"] > scene.DEFAULT_CUT_THRESHOLD)[0].tolist()
+        assert set(r["cuts"]) <= set(cuts)
+
+
+def test_windowed_two_stream_pipeline_equals_single_window(tmp_path):
+    """Many small windows over two HIP streams / two rings give exactly the
+    single-window results (score continuity across window seams)."""
+    _require_gpu()
+    path = tmp_path / "w.mp4"
+    scene.synth_write(path, width=640, height=360, n_frames=400, cut_min_s=1, cut_max_s=4,
+                      gop_max_s=0.5)
+    with scene.VideoScorer(path) as a:
+        whole = a.score()
+    for n_streams in (1, 2):
+        with scene.VideoScorer(path, window_frames=40, n_streams=n_streams) as b:
+            part = b.score()
+            assert np.array_equal(part.scores, whole.scores)
+            assert np.array_equal(part.hist, whole.hist)
+            assert np.array_equal(part.sad, whole.sad)
+            with pytest.raises(VtsegError):
+                b.frame_nv12(0)  # evicted from the ring
+
+
+def test_repeated_runs_are_deterministic(tmp_path):
+    _require_gpu()
+    path = tmp_path / "d.mp4"
+    scene.synth_write(path, width=320, height=240, n_frames=120)
+    with scene.VideoScorer(path) as v:
+        a = v.score()
+        v.run()
+        b = v.score()
+    assert np.array_equal(a.scores, b.scores) and np.array_equal(a.hist, b.hist)
+
+
+def test_boundary_frames_for_planned_segments(tmp_path):
+    _require_gpu()
+    path = tmp_path / "b.mp4"
+    scene.synth_write(path, width=128, height=96, n_frames=1800, max_motion=2)  # 60 s
+    segs = vs.plan_segments(60.0, 25.0, 2.5)
+    times = [t for s in segs for t in (s.start, s.end, s.effective_start, s.effective_end)]
+    with scene.VideoScorer(path) as v:
+        got = v.boundary_frames(times)
+        pts = v.score().pts.tolist()
+    assert got == oracle.boundary_frames(pts, 30000, times)
+    assert got[:4] == [0, 825, 0, 750]
+
+
+def test_open_rejects_non_mp4(tmp_path):
+    _require_gpu()
+    bad = tmp_path / "x.mp4"
+    bad.write_bytes(b"\x00" * 4096)
+    with pytest.raises(VtsegError):
+        scene.VideoScorer(bad)

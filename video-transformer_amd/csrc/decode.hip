@@ -1,0 +1,494 @@
+// decode.hip — device-side H.264 decode of the supported subset (gfx950).
+//
+// rocDecode/VCN is not available in this image or on the GPU pool (no
+// librocdecode.so, no libva), so the decode that feeds the scorer is done by
+// hand-written HIP kernels on the shader array:
+//
+//   h264_parse      one LANE per slice NAL: slice header + CAVLC macroblock
+//                   layer (mb_skip_run, mb_type, mvd, coded_block_pattern,
+//                   I_PCM alignment), motion-vector prediction (8.4.1.3,
+//                   8.4.1.1).  Slices are independent, so a window of N
+//                   frames x S slices runs N*S lanes at once.  Output: one
+//                   64-bit command per macroblock (see h264.h MB_PCM/MB_INTER).
+//   h264_recon      one WORKGROUP per macroblock row of a frame: turns the
+//                   commands into NV12 samples — I_PCM copy (planar Cb/Cr
+//                   interleaved into NV12 in registers) or motion-compensated
+//                   copy from the reference picture (integer-pel luma, 1/8-pel
+//                   bilinear chroma, edge clamping, 8.4.2.2).  Each lane writes
+//                   one aligned 16-byte chunk; consecutive lanes write
+//                   consecutive chunks of a row.  A launch covers every frame
+//                   at the same distance from its IDR (GOP-parallel).
+//
+// Anything outside the subset sets a bit in a device error word that the
+// host checks after every window (DEC_E_* in h264.h) — never a silent skip.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+#include "decode.h"
+#include "h264.h"
+
+namespace vts {
+namespace {
+
+// ------------------------------------------------------------ bit reader
+// Reads an EBSP (NAL payload after the header byte) from global memory through
+// a 16-byte register cache, removing emulation_prevention_three_byte.
+struct DevBits {
+  const uint8_t *base;   // first payload byte (absolute pointer)
+  int64_t abs0;          // byte offset of `base` inside the ES buffer
+  int32_t size;          // payload bytes
+  int32_t pos;           // next byte index to fetch
+  int32_t bitpos;        // bits left in `cur`
+  int32_t zeros;         // consecutive zero bytes before `pos`
+  uint32_t cur;
+  int32_t cache_at;      // payload index of cache[0], -1 none
+  uint32_t cache[4];
+  bool err;
+
+  __device__ void init(const uint8_t *p, int64_t abs, int32_t n) {
+    base = p;
+    abs0 = abs;
+    size = n;
+    pos = 0;
+    bitpos = 0;
+    zeros = 0;
+    cur = 0;
+    cache_at = -1;
+    err = false;
+  }
+  __device__ uint32_t byte_at(int32_t i) {
+    const int32_t blk = i & ~15;
+    if (blk != cache_at) {
+      // 16-byte aligned within the payload is not 16-byte aligned in memory;
+      // load the enclosing aligned dwords instead.
+      const uintptr_t a = reinterpret_cast<uintptr_t>(base + blk);
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+      const int sh = static_cast<int>(a & 3);
+      uint32_t t[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) t[k] = w[k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        cache[k] = sh ? __builtin_amdgcn_alignbyte(t[k + 1], t[k], sh) : t[k];
+      cache_at = blk;
+    }
+    const int32_t o = i - blk;
+    return (cache[o >> 2] >> (8 * (o & 3))) & 0xffu;
+  }
+  __device__ void next_byte() {
+    if (pos >= size) {
+      err = true;
+      cur = 0;
+      bitpos = 8;
+      return;
+    }
+    uint32_t b = byte_at(pos);
+    if (zeros >= 2 && b == 3) {  // emulation prevention byte
+      ++pos;
+      zeros = 0;
+      if (pos >= size) {
+        err = true;
+        cur = 0;
+        bitpos = 8;
+        return;
+      }
+      b = byte_at(pos);
+    }
+    ++pos;
+    zeros = (b == 0) ? zeros + 1 : 0;
+    cur = b;
+    bitpos = 8;
+  }
+  __device__ uint32_t bit() {
+    if (bitpos == 0) next_byte();
+    --bitpos;
+    return (cur >> bitpos) & 1u;
+  }
+  __device__ uint32_t bits(int n) {
+    uint32_t v = 0;
+    for (int i = 0; i < n; ++i) v = (v << 1) | bit();
+    return v;
+  }
+  __device__ uint32_t ue() {
+    int lz = 0;
+    while (bit() == 0) {
+      if (++lz > 31 || err) {
+        err = true;
+        return 0;
+      }
+    }
+    return lz ? ((1u << lz) - 1u + bits(lz)) : 0u;
+  }
+  __device__ int32_t se() {
+    const uint32_t k = ue();
+    return (k & 1u) ? static_cast<int32_t>((k + 1) >> 1) : -static_cast<int32_t>(k >> 1);
+  }
+  __device__ void align() { bitpos = 0; }  // pcm_alignment_zero_bits
+  // Skip n raw bytes at a byte-aligned position (I_PCM samples).  Assumes no
+  // emulation-prevention byte inside them (checked by h264_recon).
+  __device__ void skip_bytes(int32_t n) {
+    pos += n;
+    if (pos > size) {
+      err = true;
+      return;
+    }
+    const uint32_t b1 = byte_at(pos - 1), b2 = byte_at(pos - 2);
+    zeros = (b1 != 0) ? 0 : ((b2 != 0) ? 1 : 2);
+  }
+  // absolute bit index of the next bit to read (EBSP domain)
+  __device__ int64_t bit_index() const {
+    return bitpos ? (int64_t(pos - 1) * 8 + (8 - bitpos)) : int64_t(pos) * 8;
+  }
+};
+
+__device__ __forceinline__ int median3(int a, int b, int c) {
+  return max(min(a, b), min(max(a, b), c));
+}
+
+struct Nb {
+  bool avail;
+  int ref;
+  int mvx, mvy;
+};
+
+__device__ __forceinline__ Nb nb_from_cmd(uint64_t c) {
+  Nb n{true, -1, 0, 0};
+  if ((c >> 62) == 2) {
+    n.ref = 0;
+    n.mvx = static_cast<int16_t>(c & 0xffff);
+    n.mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+  }
+  return n;
+}
+
+__global__ void __launch_bounds__(64) h264_parse(ParseArgs a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.n_slices) return;
+  const SliceDesc sd = a.slices[s];
+  const H264DevParams &P = a.prm;
+  const int nmb = P.mb_width * P.mb_height;
+  uint64_t *cmd = a.cmd + static_cast<int64_t>(sd.slot) * nmb;
+  uint32_t errs = 0;
+
+  const uint8_t *nal = a.es + sd.nal_offset;
+  const uint32_t hdr = nal[0];
+  const int nal_type = hdr & 0x1f, nal_ref_idc = (hdr >> 5) & 3;
+  DevBits br;
+  br.init(nal + 1, sd.nal_offset + 1, sd.nal_size - 1);
+  // stop bit (rbsp_trailing_bits): last non-zero byte of the NAL
+  int32_t last = sd.nal_size - 1;
+  while (last > 0 && nal[last] == 0) --last;
+  if (last <= 0) {
+    atomicOr(a.err, static_cast<uint32_t>(DEC_E_SYNTAX));
+    return;
+  }
+  const uint32_t lb = nal[last];
+  const int tz = __builtin_ctz(lb);
+  const int64_t stop_bit = int64_t(last - 1) * 8 + (7 - tz);  // payload domain
+
+  // ---- slice_header (7.3.3)
+  const int first_mb = static_cast<int>(br.ue());
+  int slice_type = static_cast<int>(br.ue());
+  if (slice_type > 4) slice_type -= 5;
+  const int pps_id = static_cast<int>(br.ue());
+  if (pps_id != P.pps_id) errs |= DEC_E_PPS;
+  br.bits(P.log2_max_frame_num);  // frame_num
+  if (nal_type == 5) br.ue();      // idr_pic_id
+  if (P.poc_type == 0) {
+    br.bits(P.log2_max_poc_lsb);
+    if (P.bottom_field_pic_order_in_frame_present) br.se();
+  } else if (P.poc_type == 1 && !P.delta_pic_order_always_zero) {
+    br.se();
+    if (P.bottom_field_pic_order_in_frame_present) br.se();
+  }
+  if (P.redundant_pic_cnt_present) {
+    if (br.ue() != 0) errs |= DEC_E_SYNTAX;  // redundant slices are not decoded
+  }
+  const bool is_p = (slice_type == 0);
+  if (!is_p && slice_type != 2) errs |= DEC_E_SLICE_TYPE;
+  int num_ref = P.num_ref_idx_l0_default_active;
+  if (is_p) {
+    if (br.bit()) num_ref = static_cast<int>(br.ue()) + 1;  // override
+    if (br.bit()) errs |= DEC_E_REFLIST;                     // ref_pic_list_modification
+    if (num_ref != 1) errs |= DEC_E_MULTIREF;
+    if (sd.ref_slot < 0) errs |= DEC_E_NO_REF;
+  }
+  if (nal_ref_idc != 0) {  // dec_ref_pic_marking
+    if (nal_type == 5) {
+      br.bit();
+      br.bit();
+    } else if (br.bit()) {
+      errs |= DEC_E_MMCO;
+    }
+  }
+  const int qp = P.pic_init_qp + br.se();
+  int deblock_idc = 0, alpha_off = 0;
+  if (P.deblocking_filter_control_present) {
+    deblock_idc = static_cast<int>(br.ue());
+    if (deblock_idc != 1) {
+      alpha_off = 2 * br.se();
+      br.se();
+    }
+  }
+  // Filtering is a no-op only if disabled or every edge's indexA < 16
+  // (alpha' = 0): max qPav is the slice QP (I_PCM has qP 0).
+  if (deblock_idc != 1 && qp + alpha_off >= 16) errs |= DEC_E_DEBLOCK;
+  if (first_mb < 0 || first_mb >= nmb) errs |= DEC_E_SYNTAX;
+  if (errs || br.err) {
+    atomicOr(a.err, errs | (br.err ? DEC_E_SYNTAX : 0u));
+    return;
+  }
+
+  // ---- slice_data (7.3.4), CAVLC
+  int addr = first_mb;
+  Nb left{false, -1, 0, 0};  // neighbour A of the current MB within the slice
+  bool more = true;
+  const int mbw = P.mb_width;
+  while (more && addr < nmb) {
+    int skip = 0;
+    if (is_p) {
+      skip = static_cast<int>(br.ue());  // mb_skip_run
+      if (br.err || addr + skip > nmb) {
+        errs |= DEC_E_SYNTAX;
+        break;
+      }
+      for (int i = 0; i < skip; ++i, ++addr) {
+        // P_Skip motion (8.4.1.1)
+        const int x = addr % mbw, y = addr / mbw;
+        const bool a_ok = x > 0 && addr - 1 >= first_mb;
+        const bool b_ok = y > 0 && addr - mbw >= first_mb;
+        Nb A = a_ok ? left : Nb{false, -1, 0, 0};
+        Nb B = b_ok ? nb_from_cmd(cmd[addr - mbw]) : Nb{false, -1, 0, 0};
+        int mvx = 0, mvy = 0;
+        if (a_ok && b_ok && !(A.ref == 0 && A.mvx == 0 && A.mvy == 0) &&
+            !(B.ref == 0 && B.mvx == 0 && B.mvy == 0)) {
+          const bool c_ok = y > 0 && x < mbw - 1 && addr - mbw + 1 >= first_mb;
+          const bool d_ok = y > 0 && x > 0 && addr - mbw - 1 >= first_mb;
+          Nb C = c_ok ? nb_from_cmd(cmd[addr - mbw + 1])
+                      : (d_ok ? nb_from_cmd(cmd[addr - mbw - 1]) : Nb{false, -1, 0, 0});
+          const int match = (A.ref == 0) + (B.ref == 0) + (C.ref == 0);
+          if (match == 1) {
+            const Nb &m = (A.ref == 0) ? A : (B.ref == 0) ? B : C;
+            mvx = m.mvx;
+            mvy = m.mvy;
+          } else {
+            mvx = median3(A.mvx, B.mvx, C.mvx);
+            mvy = median3(A.mvy, B.mvy, C.mvy);
+          }
+        }
+        if ((mvx & 3) || (mvy & 3)) errs |= DEC_E_SUBPEL;
+        const uint64_t c = MB_INTER | (uint64_t(uint16_t(mvx))) | (uint64_t(uint16_t(mvy)) << 16);
+        cmd[addr] = c;
+        left = Nb{true, 0, mvx, mvy};
+      }
+      if (skip > 0) more = br.bit_index() < stop_bit;
+      if (!more || addr >= nmb) break;
+    }
+    // ---- macroblock_layer (7.3.5)
+    const int mb_type = static_cast<int>(br.ue());
+    const int x = addr % mbw, y = addr / mbw;
+    if ((!is_p && mb_type == 25) || (is_p && mb_type == 30)) {
+      br.align();
+      const int64_t off = br.abs0 + br.pos;
+      br.skip_bytes(384);
+      cmd[addr] = MB_PCM | static_cast<uint64_t>(off);
+      left = Nb{true, -1, 0, 0};
+    } else if (is_p && mb_type == 0) {
+      // P_L0_16x16: ref_idx_l0 absent (single reference), mvd_l0, cbp
+      const int mvdx = br.se(), mvdy = br.se();
+      const uint32_t cbp_code = br.ue();
+      if (cbp_code != 0) errs |= DEC_E_RESIDUAL;
+      const bool a_ok = x > 0 && addr - 1 >= first_mb;
+      const bool b_ok = y > 0 && addr - mbw >= first_mb;
+      const bool c_ok = y > 0 && x < mbw - 1 && addr - mbw + 1 >= first_mb;
+      const bool d_ok = y > 0 && x > 0 && addr - mbw - 1 >= first_mb;
+      Nb A = a_ok ? left : Nb{false, -1, 0, 0};
+      Nb B = b_ok ? nb_from_cmd(cmd[addr - mbw]) : Nb{false, -1, 0, 0};
+      Nb C = c_ok ? nb_from_cmd(cmd[addr - mbw + 1])
+                  : (d_ok ? nb_from_cmd(cmd[addr - mbw - 1]) : Nb{false, -1, 0, 0});
+      if (!B.avail && !C.avail && A.avail) B = C = A;
+      int px, py;
+      const int match = (A.ref == 0) + (B.ref == 0) + (C.ref == 0);
+      if (match == 1) {
+        const Nb &m = (A.ref == 0) ? A : (B.ref == 0) ? B : C;
+        px = m.mvx;
+        py = m.mvy;
+      } else {
+        px = median3(A.mvx, B.mvx, C.mvx);
+        py = median3(A.mvy, B.mvy, C.mvy);
+      }
+      const int mvx = px + mvdx, mvy = py + mvdy;
+      if ((mvx & 3) || (mvy & 3)) errs |= DEC_E_SUBPEL;
+      if (mvx < -32768 || mvx > 32767 || mvy < -32768 || mvy > 32767) errs |= DEC_E_SYNTAX;
+      cmd[addr] = MB_INTER | (uint64_t(uint16_t(mvx))) | (uint64_t(uint16_t(mvy)) << 16);
+      left = Nb{true, 0, mvx, mvy};
+    } else {
+      errs |= DEC_E_MB_TYPE;
+      break;
+    }
+    ++addr;
+    if (br.err) break;
+    more = br.bit_index() < stop_bit;
+  }
+  if (br.err) errs |= DEC_E_SYNTAX;
+  if (errs) atomicOr(a.err, errs);
+}
+
+// --------------------------------------------------------- reconstruction
+// 16 bytes at an arbitrary byte address, from 5 aligned dwords.
+__device__ __forceinline__ uint4 load16u(const uint8_t *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const int sh = static_cast<int>(a & 3);
+  const uint32_t t0 = w[0], t1 = w[1], t2 = w[2], t3 = w[3];
+  if (sh == 0) return make_uint4(t0, t1, t2, t3);
+  const uint32_t t4 = w[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(t1, t0, sh), __builtin_amdgcn_alignbyte(t2, t1, sh),
+                    __builtin_amdgcn_alignbyte(t3, t2, sh), __builtin_amdgcn_alignbyte(t4, t3, sh));
+}
+
+__device__ __forceinline__ uint2 load8u(const uint8_t *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const int sh = static_cast<int>(a & 3);
+  const uint32_t t0 = w[0], t1 = w[1];
+  if (sh == 0) return make_uint2(t0, t1);
+  const uint32_t t2 = w[2];
+  return make_uint2(__builtin_amdgcn_alignbyte(t1, t0, sh), __builtin_amdgcn_alignbyte(t2, t1, sh));
+}
+
+// true if bytes p[-2 .. n) contain 00 00 03 with the 03 at index >= 0
+__device__ bool has_epb(const uint8_t *p, int n) {
+  uint32_t z = (p[-2] == 0) + 0;
+  z = (p[-1] == 0) ? z + 1 : 0;
+  for (int i = 0; i < n; ++i) {
+    const uint32_t b = p[i];
+    if (z >= 2 && b == 3) return true;
+    z = (b == 0) ? z + 1 : 0;
+  }
+  return false;
+}
+
+// interleave 8 Cb and 8 Cr bytes into 16 NV12 bytes (u0 v0 u1 v1 ...)
+__device__ __forceinline__ uint4 interleave_uv(uint2 u, uint2 v) {
+  // v_perm_b32 selector: bytes of {src0, src1} = {hi word, lo word}
+  const uint32_t x0 = __builtin_amdgcn_perm(v.x, u.x, 0x05010400u);
+  const uint32_t x1 = __builtin_amdgcn_perm(v.x, u.x, 0x07030602u);
+  const uint32_t x2 = __builtin_amdgcn_perm(v.y, u.y, 0x05010400u);
+  const uint32_t x3 = __builtin_amdgcn_perm(v.y, u.y, 0x07030602u);
+  return make_uint4(x0, x1, x2, x3);
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__global__ void __launch_bounds__(256) h264_recon(ReconArgs a) {
+  const int mbw = a.mb_width, mbh = a.mb_height;
+  const int fi = blockIdx.x / mbh;  // frame within this launch
+  const int mby = blockIdx.x - fi * mbh;
+  const int2 fr = a.frames[fi];     // (slot, ref_slot)
+  const int W = mbw * 16, H = mbh * 16, CW = W / 2, CH = H / 2;
+  const int64_t pitch = a.pitch;
+  uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
+  uint8_t *dst_uv = dst + pitch * H;
+  const uint8_t *ref = fr.y >= 0 ? a.surf + static_cast<int64_t>(fr.y) * a.frame_stride : nullptr;
+  const uint8_t *ref_uv = ref ? ref + pitch * H : nullptr;
+  const uint64_t *cmd = a.cmd + static_cast<int64_t>(fr.x) * (mbw * mbh) + mby * mbw;
+  uint32_t errs = 0;
+
+  for (int it = threadIdx.x; it < 24 * mbw; it += blockDim.x) {
+    const int r = it / mbw;       // 0..15 luma rows, 16..23 chroma rows
+    const int m = it - r * mbw;   // macroblock column
+    const uint64_t c = cmd[m];
+    const uint32_t kind = static_cast<uint32_t>(c >> 62);
+    uint4 out = make_uint4(0, 0, 0, 0);
+    if (r < 16) {
+      if (kind == 1) {
+        const uint8_t *src = a.es + static_cast<int64_t>(c & 0xffffffffffffull) + 16 * r;
+        out = load16u(src);
+        if (has_epb(src, 16)) errs |= DEC_E_EPB_IN_PCM;
+      } else if (kind == 2 && ref) {
+        const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+        const int sy = clampi(mby * 16 + r + (mvy >> 2), 0, H - 1);
+        const int sx = m * 16 + (mvx >> 2);
+        const uint8_t *row = ref + sy * pitch;
+        if (sx >= 0 && sx + 15 <= W - 1) {
+          out = load16u(row + sx);
+        } else {
+          uint32_t wv[4] = {0, 0, 0, 0};
+          for (int b = 0; b < 16; ++b)
+            wv[b >> 2] |= uint32_t(row[clampi(sx + b, 0, W - 1)]) << (8 * (b & 3));
+          out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+      } else {
+        errs |= (kind == 0) ? DEC_E_MISSING_MB : DEC_E_NO_REF;
+      }
+      *reinterpret_cast<uint4 *>(dst + (mby * 16 + r) * pitch + m * 16) = out;
+    } else {
+      const int cr = r - 16;
+      if (kind == 1) {
+        const uint8_t *pcm = a.es + static_cast<int64_t>(c & 0xffffffffffffull);
+        const uint8_t *us = pcm + 256 + 8 * cr, *vs = pcm + 320 + 8 * cr;
+        out = interleave_uv(load8u(us), load8u(vs));
+        if (has_epb(us, 8) || has_epb(vs, 8)) errs |= DEC_E_EPB_IN_PCM;
+      } else if (kind == 2 && ref) {
+        const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+        const int fx = mvx & 7, fy = mvy & 7;
+        const int cx = m * 8 + (mvx >> 3), cy = mby * 8 + cr + (mvy >> 3);
+        if (fx == 0 && fy == 0) {
+          const uint8_t *row = ref_uv + clampi(cy, 0, CH - 1) * pitch;
+          if (cx >= 0 && cx + 7 <= CW - 1) {
+            out = load16u(row + 2 * cx);
+          } else {
+            uint32_t wv[4] = {0, 0, 0, 0};
+            for (int b = 0; b < 8; ++b) {
+              const int sx = clampi(cx + b, 0, CW - 1);
+              wv[b >> 1] |= (uint32_t(row[2 * sx]) | (uint32_t(row[2 * sx + 1]) << 8)) << (16 * (b & 1));
+            }
+            out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+          }
+        } else {
+          const uint8_t *ra = ref_uv + clampi(cy, 0, CH - 1) * pitch;
+          const uint8_t *rb = ref_uv + clampi(cy + 1, 0, CH - 1) * pitch;
+          uint32_t wv[4] = {0, 0, 0, 0};
+          for (int b = 0; b < 8; ++b) {
+            const int xa = clampi(cx + b, 0, CW - 1), xb = clampi(cx + b + 1, 0, CW - 1);
+            for (int pl = 0; pl < 2; ++pl) {
+              const int A = ra[2 * xa + pl], B = ra[2 * xb + pl], C = rb[2 * xa + pl], D = rb[2 * xb + pl];
+              const uint32_t v = static_cast<uint32_t>(
+                  ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
+              const int byte = 2 * b + pl;
+              wv[byte >> 2] |= v << (8 * (byte & 3));
+            }
+          }
+          out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+      } else {
+        errs |= (kind == 0) ? DEC_E_MISSING_MB : DEC_E_NO_REF;
+      }
+      *reinterpret_cast<uint4 *>(dst_uv + (mby * 8 + cr) * pitch + m * 16) = out;
+    }
+  }
+  if (errs) atomicOr(a.err, errs);
+}
+
+}  // namespace
+
+int parse_launch(const ParseArgs &a, hipStream_t s) {
+  if (a.n_slices <= 0) return VTS_OK;
+  hipLaunchKernelGGL(h264_parse, dim3((a.n_slices + 63) / 64), dim3(64), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_parse launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
+int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s) {
+  if (n_frames <= 0) return VTS_OK;
+  hipLaunchKernelGGL(h264_recon, dim3(n_frames * a.mb_height), dim3(256), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
+}  // namespace vts

@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(kThreads, 2) score_runs(RunArgs a) {
       }
       // --- thumbnail pixels: round, convert, histogram
       uint32_t yq[G::kG];
-      uint8_t rgbb[3 * G::kG];
+      uint32_t rgb24[G::kG];  // r | g << 8 | b << 16
 #pragma unroll
       for (int p = 0; p < G::kG; ++p) {
         const uint32_t y = (ys[p] + G::kYDiv / 2) / G::kYDiv;
@@ -222,9 +222,7 @@ __global__ void __launch_bounds__(kThreads, 2) score_runs(RunArgs a) {
         yq[p] = y;
         uint32_t r, g, b;
         bt709(y, u, v, &r, &g, &b);
-        rgbb[3 * p + 0] = static_cast<uint8_t>(r);
-        rgbb[3 * p + 1] = static_cast<uint8_t>(g);
-        rgbb[3 * p + 2] = static_cast<uint8_t>(b);
+        rgb24[p] = r | (g << 8) | (b << 16);
         atomicAdd(&lds_hist[y], 1u);
       }
       // --- SAD against the previous frame's thumbnail (thread-private LDS slot)
@@ -253,18 +251,24 @@ __global__ void __launch_bounds__(kThreads, 2) score_runs(RunArgs a) {
       // --- stores: RGB thumbnail, run head / tail thumbnails
       if (a.rgb) {
         uint8_t *dst = a.rgb + f * npx * 3 + tpx * 3;
-        if constexpr ((3 * G::kG) % 4 == 0) {
+        // pack 24-bit pixels into words with shifts only (no byte arrays:
+        // byte-array packing miscompiled on gfx950 in an earlier version)
+        if constexpr (G::kG % 4 == 0) {
+          uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
 #pragma unroll
-          for (int q = 0; q < 3 * G::kG / 4; ++q) {
-            const uint32_t word = rgbb[4 * q] | (rgbb[4 * q + 1] << 8) |
-                                  (rgbb[4 * q + 2] << 16) | (uint32_t(rgbb[4 * q + 3]) << 24);
-            reinterpret_cast<uint32_t *>(dst)[q] = word;
+          for (int q = 0; q < G::kG / 4; ++q) {
+            const uint32_t a0 = rgb24[4 * q], a1 = rgb24[4 * q + 1];
+            const uint32_t a2 = rgb24[4 * q + 2], a3 = rgb24[4 * q + 3];
+            d32[3 * q + 0] = a0 | (a1 << 24);
+            d32[3 * q + 1] = (a1 >> 8) | (a2 << 16);
+            d32[3 * q + 2] = (a2 >> 16) | (a3 << 8);
           }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 3 * G::kG / 2; ++q)
-            reinterpret_cast<uint16_t *>(dst)[q] =
-                static_cast<uint16_t>(rgbb[2 * q] | (rgbb[2 * q + 1] << 8));
+        } else {  // G == 2: 6 bytes, 2-byte aligned
+          uint16_t *d16 = reinterpret_cast<uint16_t *>(dst);
+          const uint32_t a0 = rgb24[0], a1 = rgb24[1];
+          d16[0] = static_cast<uint16_t>(a0 & 0xffffu);
+          d16[1] = static_cast<uint16_t>((a0 >> 16) | ((a1 & 0xffu) << 8));
+          d16[2] = static_cast<uint16_t>(a1 >> 8);
         }
       }
       if (f == f0 && !seeded) {

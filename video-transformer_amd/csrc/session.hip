@@ -1,0 +1,580 @@
+// session.hip — vts_open / vts_score / vts_run / vts_close: one video on one GPU.
+//
+// Host side does only container work (MP4 boxes, NAL length prefixes, the
+// first two Exp-Golomb fields of each slice header to know I vs P) and builds
+// a static schedule once at open:
+//   * windows of whole GOPs (each starts at an intra picture) sized to a
+//     decoded-surface ring; a video that fits in kSingleWindowBytes is one
+//     window (all GOPs decode in parallel);
+//   * per window, "levels": level 0 = intra pictures, level L = pictures L
+//     references after one; one reconstruct launch per level covers that
+//     level of every GOP in the window;
+// and uploads the whole elementary stream to HBM.  A run then is pure device
+// work: memset cmd -> h264_parse (all slices of the window) -> h264_recon
+// per level -> score_runs + score_seams, windows pipelined over two HIP
+// streams (decode of window i+1 overlaps scoring of window i; two rings).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "bitstream.h"
+#include "common.h"
+#include "decode.h"
+#include "h264.h"
+#include "mp4.h"
+
+namespace vts {
+int fill_video_info(const Mp4Info &mp4, vts_video_info *info);
+}
+
+using namespace vts;
+
+namespace {
+
+constexpr int64_t kSingleWindowBytes = 48ll << 30;  // up to 48 GiB decoded: one window
+constexpr int64_t kRingBytes = 8ll << 30;           // else 8 GiB rings (x2)
+constexpr int64_t kPad = 256;
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess)                                                          \
+      return fail(VTS_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));       \
+  } while (0)
+
+struct Window {
+  int64_t f0 = 0, f1 = 0;          // frames [f0, f1)
+  int64_t s0 = 0, s1 = 0;          // slices [s0, s1)
+  std::vector<int64_t> lvl_off;    // into level_frames
+  std::vector<int32_t> lvl_cnt;
+};
+
+}  // namespace
+
+struct vts_ctx {
+  int device = 0;
+  Sps sps;
+  Pps pps;
+  H264DevParams prm{};
+  vts_video_info info{};
+  vts_params params{};
+  int k = 4;
+  int width = 0, height = 0, pitch = 0, coded_w = 0, coded_h = 0;
+  int64_t frame_stride = 0;
+  int64_t n_frames = 0;
+  std::vector<int64_t> pts;
+  std::vector<SliceDesc> slices;
+  std::vector<int2> level_frames;
+  std::vector<Window> windows;
+  int64_t ring_frames = 0;
+  int n_rings = 1;
+  // device
+  uint8_t *d_es = nullptr;
+  int64_t es_bytes = 0;
+  SliceDesc *d_slices = nullptr;
+  int2 *d_levels = nullptr;
+  uint64_t *d_cmd[2] = {nullptr, nullptr};
+  uint8_t *d_surf[2] = {nullptr, nullptr};
+  uint8_t *d_ws[2] = {nullptr, nullptr};
+  int64_t ws_bytes = 0;
+  uint8_t *d_last[2] = {nullptr, nullptr};
+  uint32_t *d_err = nullptr;
+  float *d_score = nullptr;
+  uint64_t *d_sad = nullptr;
+  uint32_t *d_hist = nullptr;
+  hipStream_t s_dec = nullptr, s_score = nullptr;
+  std::vector<hipEvent_t> ev;  // per window: dec0, dec1, sc0, sc1
+  hipEvent_t ev_start = nullptr, ev_end = nullptr;
+  double timings[4] = {0, 0, 0, 0};
+  int64_t last_window_done = -1;
+  bool have_results = false;
+  std::vector<float> host_scores;
+};
+
+namespace {
+
+// Read the sample bytes of the track into one contiguous host buffer.
+int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size, const char *path,
+                   std::vector<uint8_t> *es, std::vector<int64_t> *es_off) {
+  int64_t total = 0;
+  for (uint32_t s : t.size) total += s;
+  es->resize(static_cast<size_t>(total + kPad), 0);
+  es_off->resize(t.size.size());
+  FILE *f = nullptr;
+  if (!mem) {
+    f = std::fopen(path, "rb");
+    if (!f) return fail(VTS_E_IO, "cannot open %s", path);
+  }
+  int64_t pos = 0;
+  for (size_t i = 0; i < t.size.size(); ++i) {
+    (*es_off)[i] = pos;
+    const int64_t off = t.offset[i], n = t.size[i];
+    if (mem) {
+      if (off < 0 || off + n > mem_size) return fail(VTS_E_FORMAT, "sample %zu out of file", i);
+      std::memcpy(es->data() + pos, mem + off, static_cast<size_t>(n));
+    } else {
+      if (fseeko(f, off, SEEK_SET) != 0 ||
+          std::fread(es->data() + pos, 1, static_cast<size_t>(n), f) != static_cast<size_t>(n)) {
+        std::fclose(f);
+        return fail(VTS_E_FORMAT, "cannot read sample %zu", i);
+      }
+    }
+    pos += n;
+  }
+  if (f) std::fclose(f);
+  return VTS_OK;
+}
+
+int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, const char *path) {
+  VTS_TRY(fill_video_info(mp4, &c->info));
+  const Mp4VideoTrack &t = mp4.video.front();
+  if (!(t.codec == "avc1" || t.codec == "avc3"))
+    return fail(VTS_E_UNSUPPORTED, "codec %s: only H.264 (avc1) is decoded", t.codec.c_str());
+  if (t.sps.size() != 1 || t.pps.size() != 1)
+    return fail(VTS_E_UNSUPPORTED, "exactly one SPS and one PPS are supported");
+  std::string e = parse_sps(t.sps[0].data(), t.sps[0].size(), &c->sps);
+  if (!e.empty()) return fail(VTS_E_UNSUPPORTED, "SPS: %s", e.c_str());
+  e = parse_pps(t.pps[0].data(), t.pps[0].size(), &c->pps);
+  if (!e.empty()) return fail(VTS_E_UNSUPPORTED, "PPS: %s", e.c_str());
+  if (c->sps.crop_left || c->sps.crop_top)
+    return fail(VTS_E_UNSUPPORTED, "left/top cropping is not supported");
+  c->prm = make_dev_params(c->sps, c->pps);
+  c->coded_w = c->sps.mb_width * 16;
+  c->coded_h = c->sps.mb_height * 16;
+  c->width = c->sps.width();
+  c->height = c->sps.height();
+  c->pitch = c->coded_w;
+  c->frame_stride = (static_cast<int64_t>(c->pitch) * c->coded_h * 3 / 2 + 4095) & ~int64_t(4095);
+  c->k = c->params.k > 0 ? c->params.k : (c->height <= 720 ? 4 : 6);
+  c->n_frames = static_cast<int64_t>(t.size.size());
+  if (c->n_frames == 0) return fail(VTS_E_FORMAT, "video track has no samples");
+
+  // presentation timestamps; output order must equal decode order
+  c->pts.resize(static_cast<size_t>(c->n_frames));
+  int64_t shift = 0;
+  for (const EditEntry &ed : t.edits)
+    if (ed.media_time >= 0) {
+      shift = ed.media_time;
+      break;
+    }
+  for (int64_t i = 0; i < c->n_frames; ++i) {
+    c->pts[i] = t.dts[i] + t.cts_offset[i] - shift;
+    if (i > 0 && c->pts[i] <= c->pts[i - 1])
+      return fail(VTS_E_UNSUPPORTED, "frame reordering (B-frames / ctts) is not supported");
+  }
+
+  std::vector<uint8_t> es;
+  std::vector<int64_t> es_off;
+  VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off));
+  c->es_bytes = static_cast<int64_t>(es.size());
+
+  // NAL walk: slice table, intra / reference flags per frame
+  const int L = t.nal_length_size;
+  std::vector<int64_t> first_slice(c->n_frames), n_slices(c->n_frames);
+  std::vector<uint8_t> intra(c->n_frames, 1), is_ref(c->n_frames, 0);
+  for (int64_t f = 0; f < c->n_frames; ++f) {
+    int64_t p = es_off[f];
+    const int64_t end = p + t.size[f];
+    first_slice[f] = static_cast<int64_t>(c->slices.size());
+    while (p + L <= end) {
+      uint32_t len = 0;
+      for (int i = 0; i < L; ++i) len = (len << 8) | es[p + i];
+      p += L;
+      if (len == 0 || p + len > end) return fail(VTS_E_FORMAT, "bad NAL length in frame %lld", (long long)f);
+      const uint8_t hdr = es[p];
+      const int type = hdr & 0x1f;
+      if (type == 1 || type == 5) {
+        BitReader br(es.data() + p + 1, len - 1);
+        br.ue();  // first_mb_in_slice
+        uint32_t st = br.ue();
+        if (st > 4) st -= 5;
+        if (st != 2) intra[f] = 0;
+        if ((hdr >> 5) & 3) is_ref[f] = 1;
+        SliceDesc sd{};
+        sd.nal_offset = p;
+        sd.nal_size = static_cast<int32_t>(len);
+        c->slices.push_back(sd);
+      } else if (type == 7 || type == 8) {
+        const std::vector<uint8_t> &ps = (type == 7) ? t.sps[0] : t.pps[0];
+        if (ps.size() != len || std::memcmp(ps.data(), es.data() + p, len) != 0)
+          return fail(VTS_E_UNSUPPORTED, "in-band parameter set differs from avcC");
+      } else if (type >= 2 && type <= 4) {
+        return fail(VTS_E_UNSUPPORTED, "data partitioning is not supported");
+      }
+      p += len;
+    }
+    n_slices[f] = static_cast<int64_t>(c->slices.size()) - first_slice[f];
+    if (n_slices[f] == 0) return fail(VTS_E_FORMAT, "frame %lld has no slices", (long long)f);
+  }
+
+  // references and levels (single reference: the latest reference picture)
+  std::vector<int64_t> ref(c->n_frames, -1), level(c->n_frames, 0);
+  int64_t last_ref = -1;
+  for (int64_t f = 0; f < c->n_frames; ++f) {
+    if (intra[f]) {
+      ref[f] = -1;
+      level[f] = 0;
+    } else {
+      ref[f] = last_ref;  // -1 -> device flags DEC_E_NO_REF
+      level[f] = last_ref >= 0 ? level[last_ref] + 1 : 0;
+    }
+    if (is_ref[f]) last_ref = f;
+  }
+
+  // windows of whole intra-started groups
+  const int64_t total_bytes = c->n_frames * c->frame_stride;
+  int64_t cap;
+  if (c->params.window_frames > 0) cap = c->params.window_frames;
+  else if (total_bytes <= kSingleWindowBytes) cap = c->n_frames;
+  else cap = std::max<int64_t>(1, kRingBytes / c->frame_stride);
+  auto next_intra = [&](int64_t x) {
+    while (x < c->n_frames && !intra[x]) ++x;
+    return x;
+  };
+  for (int64_t f = 0; f < c->n_frames;) {
+    Window w;
+    w.f0 = f;
+    int64_t end = next_intra(f + 1);  // the first group is always taken
+    while (end < c->n_frames) {
+      const int64_t nxt = next_intra(end + 1);
+      if (nxt - f > cap) break;
+      end = nxt;
+    }
+    w.f1 = end;
+    c->windows.push_back(w);
+    f = end;
+  }
+  for (Window &w : c->windows) c->ring_frames = std::max(c->ring_frames, w.f1 - w.f0);
+  c->n_rings = (c->windows.size() > 1 && c->params.n_streams >= 2) ? 2 : 1;
+
+  // slice slots / ref slots and per-level frame lists
+  for (Window &w : c->windows) {
+    w.s0 = first_slice[w.f0];
+    w.s1 = (w.f1 < c->n_frames) ? first_slice[w.f1] : static_cast<int64_t>(c->slices.size());
+    int64_t maxl = 0;
+    for (int64_t x = w.f0; x < w.f1; ++x) {
+      if (ref[x] >= 0 && ref[x] < w.f0)
+        return fail(VTS_E_UNSUPPORTED, "reference crosses a window boundary");
+      maxl = std::max(maxl, level[x]);
+      for (int64_t s = first_slice[x]; s < first_slice[x] + n_slices[x]; ++s) {
+        c->slices[s].slot = static_cast<int32_t>(x - w.f0);
+        c->slices[s].ref_slot = ref[x] >= 0 ? static_cast<int32_t>(ref[x] - w.f0) : -1;
+      }
+    }
+    // levels relative to the window (intra frames restart at 0)
+    std::vector<std::vector<int2>> lv(static_cast<size_t>(maxl + 1));
+    for (int64_t x = w.f0; x < w.f1; ++x)
+      lv[level[x]].push_back(make_int2(static_cast<int>(x - w.f0),
+                                       ref[x] >= 0 ? static_cast<int>(ref[x] - w.f0) : -1));
+    for (auto &l : lv) {
+      if (l.empty()) continue;
+      w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
+      w.lvl_cnt.push_back(static_cast<int32_t>(l.size()));
+      c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
+    }
+  }
+
+  // ---- device allocations and uploads
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
+  HIP_TRY(hipMemcpy(c->d_es, es.data(), static_cast<size_t>(c->es_bytes), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_slices, sizeof(SliceDesc) * c->slices.size()));
+  HIP_TRY(hipMemcpy(c->d_slices, c->slices.data(), sizeof(SliceDesc) * c->slices.size(),
+                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_levels, sizeof(int2) * c->level_frames.size()));
+  HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int2) * c->level_frames.size(),
+                    hipMemcpyHostToDevice));
+  const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
+  c->ws_bytes = score_workspace_bytes(c->width, c->height, c->k, c->ring_frames);
+  const int64_t tw = (c->width / c->k) * (c->height / c->k);
+  for (int r = 0; r < c->n_rings; ++r) {
+    HIP_TRY(hipMalloc(&c->d_cmd[r], static_cast<size_t>(c->ring_frames * nmb * 8)));
+    HIP_TRY(hipMalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
+    HIP_TRY(hipMalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
+  }
+  for (int r = 0; r < 2; ++r) HIP_TRY(hipMalloc(&c->d_last[r], static_cast<size_t>(tw + kPad)));
+  HIP_TRY(hipMalloc(&c->d_err, sizeof(uint32_t)));
+  HIP_TRY(hipMalloc(&c->d_score, sizeof(float) * c->n_frames));
+  HIP_TRY(hipMalloc(&c->d_sad, sizeof(uint64_t) * c->n_frames));
+  HIP_TRY(hipMalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
+  HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
+  c->ev.resize(c->windows.size() * 6);
+  for (auto &e2 : c->ev) HIP_TRY(hipEventCreate(&e2));
+  HIP_TRY(hipEventCreate(&c->ev_start));
+  HIP_TRY(hipEventCreate(&c->ev_end));
+  return VTS_OK;
+}
+
+int open_common(int device, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size,
+                const char *path, const vts_params *params, vts_ctx **out) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(VTS_E_NODEVICE, "no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(VTS_E_NODEVICE, "device %d out of range", device);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return fail(VTS_E_NODEVICE, "hipGetDeviceProperties failed");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(VTS_E_NODEVICE, "device %d is %s, not gfx950", device, prop.gcnArchName);
+  vts_ctx *c = new vts_ctx;
+  c->device = device;
+  if (params) c->params = *params;
+  if (c->params.n_streams <= 0) c->params.n_streams = 2;
+  if (c->params.cut_threshold <= 0) c->params.cut_threshold = 0.08f;
+  const int rc = build(c, mp4, mem, mem_size, path);
+  if (rc != VTS_OK) {
+    const std::string msg = last_error();
+    vts_close(c);
+    last_error() = msg;
+    return rc;
+  }
+  *out = c;
+  return VTS_OK;
+}
+
+int run_all(vts_ctx *c) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
+  HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
+  HIP_TRY(hipStreamWaitEvent(c->s_score, c->ev_start, 0));
+  const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
+  hipStream_t sd = c->s_dec;
+  hipStream_t ss = (c->params.n_streams >= 2) ? c->s_score : c->s_dec;
+  const size_t nw = c->windows.size();
+  for (size_t wi = 0; wi < nw; ++wi) {
+    const Window &w = c->windows[wi];
+    const int r = static_cast<int>(wi % c->n_rings);
+    hipEvent_t *E = &c->ev[wi * 6];  // 0 dec start, 1 parsed, 2 decoded, 3 score start, 4 scored
+    if (wi >= static_cast<size_t>(c->n_rings))
+      HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
+    HIP_TRY(hipEventRecord(E[0], sd));
+    HIP_TRY(hipMemsetAsync(c->d_cmd[r], 0, static_cast<size_t>((w.f1 - w.f0) * nmb * 8), sd));
+    ParseArgs pa{};
+    pa.es = c->d_es;
+    pa.slices = c->d_slices + w.s0;
+    pa.n_slices = static_cast<int32_t>(w.s1 - w.s0);
+    pa.cmd = c->d_cmd[r];
+    pa.err = c->d_err;
+    pa.prm = c->prm;
+    VTS_TRY(parse_launch(pa, sd));
+    HIP_TRY(hipEventRecord(E[1], sd));
+    ReconArgs ra{};
+    ra.es = c->d_es;
+    ra.cmd = c->d_cmd[r];
+    ra.surf = c->d_surf[r];
+    ra.frame_stride = c->frame_stride;
+    ra.pitch = c->pitch;
+    ra.mb_width = c->sps.mb_width;
+    ra.mb_height = c->sps.mb_height;
+    ra.err = c->d_err;
+    for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+      ra.frames = c->d_levels + w.lvl_off[l];
+      VTS_TRY(recon_launch(ra, w.lvl_cnt[l], sd));
+    }
+    HIP_TRY(hipEventRecord(E[2], sd));
+    HIP_TRY(hipStreamWaitEvent(ss, E[2], 0));
+    HIP_TRY(hipEventRecord(E[3], ss));
+    vts_score_desc d{};
+    d.nv12 = c->d_surf[r];
+    d.frame_stride = c->frame_stride;
+    d.n_frames = w.f1 - w.f0;
+    d.width = c->width;
+    d.height = c->height;
+    d.pitch = c->pitch;
+    d.uv_row_offset = c->coded_h;
+    d.k = c->k;
+    d.rgb = nullptr;
+    d.hist = c->d_hist + w.f0 * 256;
+    d.sad = c->d_sad + w.f0;
+    d.score = c->d_score + w.f0;
+    d.prev_luma = wi > 0 ? c->d_last[(wi - 1) & 1] : nullptr;
+    d.last_luma = c->d_last[wi & 1];
+    d.workspace = c->d_ws[r];
+    d.workspace_bytes = c->ws_bytes;
+    VTS_TRY(score_launch(&d, ss));
+    HIP_TRY(hipEventRecord(E[4], ss));
+  }
+  HIP_TRY(hipStreamWaitEvent(sd, c->ev[(nw - 1) * 6 + 4], 0));
+  HIP_TRY(hipEventRecord(c->ev_end, sd));
+  HIP_TRY(hipEventSynchronize(c->ev_end));
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
+  // timings
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, c->ev_start, c->ev_end));
+  c->timings[0] = ms;
+  c->timings[1] = c->timings[2] = c->timings[3] = 0;
+  for (size_t wi = 0; wi < nw; ++wi) {
+    hipEvent_t *E = &c->ev[wi * 6];
+    float a = 0, b = 0, s = 0;
+    HIP_TRY(hipEventElapsedTime(&a, E[0], E[1]));
+    HIP_TRY(hipEventElapsedTime(&b, E[1], E[2]));
+    HIP_TRY(hipEventElapsedTime(&s, E[3], E[4]));
+    c->timings[1] += a;
+    c->timings[2] += b;
+    c->timings[3] += s;
+  }
+  c->last_window_done = static_cast<int64_t>(nw) - 1;
+  if (err) {
+    c->have_results = false;
+    return fail(VTS_E_DECODE, "device decoder: %s", describe_decode_error(err).c_str());
+  }
+  c->have_results = true;
+  c->host_scores.clear();
+  return VTS_OK;
+}
+
+int fetch_scores(vts_ctx *c) {
+  if (!c->host_scores.empty()) return VTS_OK;
+  c->host_scores.resize(static_cast<size_t>(c->n_frames));
+  HIP_TRY(hipMemcpy(c->host_scores.data(), c->d_score, sizeof(float) * c->n_frames,
+                    hipMemcpyDeviceToHost));
+  return VTS_OK;
+}
+
+}  // namespace
+
+extern "C" int vts_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" int vts_open(int device, const char *path, const vts_params *params, vts_ctx **out) {
+  clear_error();
+  if (!path || !out) return fail(VTS_E_INVALID, "NULL argument");
+  *out = nullptr;
+  Mp4Info mp4;
+  const std::string e = mp4_parse_file(path, &mp4);
+  if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
+  if (mp4.fragmented) return fail(VTS_E_UNSUPPORTED, "fragmented MP4 is not supported");
+  return open_common(device, mp4, nullptr, 0, path, params, out);
+}
+
+extern "C" int vts_open_memory(int device, const uint8_t *data, int64_t size, const vts_params *params,
+                               vts_ctx **out) {
+  clear_error();
+  if (!data || size <= 0 || !out) return fail(VTS_E_INVALID, "bad argument");
+  *out = nullptr;
+  Mp4Info mp4;
+  const std::string e = mp4_parse_memory(data, size, &mp4);
+  if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
+  if (mp4.fragmented) return fail(VTS_E_UNSUPPORTED, "fragmented MP4 is not supported");
+  return open_common(device, mp4, data, size, nullptr, params, out);
+}
+
+extern "C" int vts_info(const vts_ctx *c, vts_video_info *info) {
+  clear_error();
+  if (!c || !info) return fail(VTS_E_INVALID, "NULL argument");
+  *info = c->info;
+  return VTS_OK;
+}
+
+extern "C" int vts_run(vts_ctx *c) {
+  clear_error();
+  if (!c) return fail(VTS_E_INVALID, "NULL ctx");
+  return run_all(c);
+}
+
+extern "C" int vts_score(vts_ctx *c, float *scores, uint32_t *hist, uint64_t *sad, int64_t *pts,
+                         int64_t cap, int64_t *n_frames) {
+  clear_error();
+  if (!c || !n_frames) return fail(VTS_E_INVALID, "NULL argument");
+  *n_frames = c->n_frames;
+  if (!scores || cap < c->n_frames)
+    return fail(VTS_E_CAPACITY, "need %lld frames", static_cast<long long>(c->n_frames));
+  VTS_TRY(run_all(c));
+  VTS_TRY(fetch_scores(c));
+  std::memcpy(scores, c->host_scores.data(), sizeof(float) * c->n_frames);
+  if (hist)
+    HIP_TRY(hipMemcpy(hist, c->d_hist, sizeof(uint32_t) * 256 * c->n_frames, hipMemcpyDeviceToHost));
+  if (sad) HIP_TRY(hipMemcpy(sad, c->d_sad, sizeof(uint64_t) * c->n_frames, hipMemcpyDeviceToHost));
+  if (pts) std::memcpy(pts, c->pts.data(), sizeof(int64_t) * c->n_frames);
+  return VTS_OK;
+}
+
+extern "C" int vts_scene_cuts(vts_ctx *c, int64_t *frame_idx, int64_t cap, int64_t *n_out) {
+  clear_error();
+  if (!c || !n_out) return fail(VTS_E_INVALID, "NULL argument");
+  if (!c->have_results) return fail(VTS_E_INVALID, "run vts_score/vts_run first");
+  VTS_TRY(fetch_scores(c));
+  int64_t n = 0;
+  for (int64_t i = 0; i < c->n_frames; ++i)
+    if (c->host_scores[i] > c->params.cut_threshold) {
+      if (frame_idx && n < cap) frame_idx[n] = i;
+      ++n;
+    }
+  *n_out = n;
+  if (n > cap) return fail(VTS_E_CAPACITY, "need %lld", static_cast<long long>(n));
+  return VTS_OK;
+}
+
+extern "C" int vts_boundary_frames(vts_ctx *c, const double *times, int64_t n, int64_t *frame_idx) {
+  clear_error();
+  if (!c) return fail(VTS_E_INVALID, "NULL ctx");
+  return vts_boundary_frames_pts(c->pts.data(), c->n_frames, c->info.track_timescale, times, n,
+                                 frame_idx);
+}
+
+extern "C" int vts_get_frame_nv12(vts_ctx *c, int64_t frame, uint8_t *out, int64_t out_bytes) {
+  clear_error();
+  if (!c || !out) return fail(VTS_E_INVALID, "NULL argument");
+  const int64_t need = static_cast<int64_t>(c->width) * c->height * 3 / 2;
+  if (out_bytes < need) return fail(VTS_E_CAPACITY, "need %lld bytes", static_cast<long long>(need));
+  if (c->last_window_done < 0) return fail(VTS_E_INVALID, "nothing decoded yet");
+  const int64_t first_resident = std::max<int64_t>(0, c->last_window_done - c->n_rings + 1);
+  for (int64_t wi = first_resident; wi <= c->last_window_done; ++wi) {
+    const Window &w = c->windows[static_cast<size_t>(wi)];
+    if (frame < w.f0 || frame >= w.f1) continue;
+    const uint8_t *base = c->d_surf[wi % c->n_rings] + (frame - w.f0) * c->frame_stride;
+    HIP_TRY(hipMemcpy2D(out, c->width, base, c->pitch, c->width, c->height, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy2D(out + static_cast<int64_t>(c->width) * c->height, c->width,
+                        base + static_cast<int64_t>(c->pitch) * c->coded_h, c->pitch, c->width,
+                        c->height / 2, hipMemcpyDeviceToHost));
+    return VTS_OK;
+  }
+  return fail(VTS_E_INVALID, "frame %lld is not resident", static_cast<long long>(frame));
+}
+
+extern "C" int vts_last_timings(const vts_ctx *c, double *ms4) {
+  clear_error();
+  if (!c || !ms4) return fail(VTS_E_INVALID, "NULL argument");
+  for (int i = 0; i < 4; ++i) ms4[i] = c->timings[i];
+  return VTS_OK;
+}
+
+extern "C" int vts_close(vts_ctx *c) {
+  if (!c) return VTS_OK;
+  (void)hipSetDevice(c->device);
+  if (c->s_dec) (void)hipStreamSynchronize(c->s_dec);
+  if (c->s_score) (void)hipStreamSynchronize(c->s_score);
+  auto f = [](void *p) {
+    if (p) (void)hipFree(p);
+  };
+  f(c->d_es);
+  f(c->d_slices);
+  f(c->d_levels);
+  for (int r = 0; r < 2; ++r) {
+    f(c->d_cmd[r]);
+    f(c->d_surf[r]);
+    f(c->d_ws[r]);
+    f(c->d_last[r]);
+  }
+  f(c->d_err);
+  f(c->d_score);
+  f(c->d_sad);
+  f(c->d_hist);
+  for (auto e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+  if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+  if (c->s_dec) (void)hipStreamDestroy(c->s_dec);
+  if (c->s_score) (void)hipStreamDestroy(c->s_score);
+  delete c;
+  return VTS_OK;
+}

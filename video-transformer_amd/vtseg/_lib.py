@@ -97,12 +97,13 @@ class SynthParams(C.Structure):
                 ("fps_den", C.c_int32), ("n_frames", C.c_int64), ("seed", C.c_uint64),
                 ("cut_min_s", C.c_double), ("cut_max_s", C.c_double),
                 ("gop_max_s", C.c_double), ("max_motion", C.c_int32),
-                ("slices_per_row", C.c_int32)]
+                ("slices_per_row", C.c_int32), ("hash_frames", C.c_int32),
+                ("_pad", C.c_int32)]
 
 
 class SynthInfo(C.Structure):
     _fields_ = [("bytes_written", C.c_int64), ("n_idr", C.c_int64), ("n_cuts", C.c_int64),
-                ("timescale", C.c_int64)]
+                ("timescale", C.c_int64), ("recon_hash", C.c_uint64)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/vtseg.h

@@ -1,0 +1,211 @@
+"""GPU scene scoring: decode + NV12 scoring on MI355X through libvtseg.
+
+Two levels:
+
+* ``score_nv12(...)`` — the scoring kernel on NV12 frames already in device
+  memory (torch tensors are used only as device-memory plumbing; the work is
+  ``vts_score_nv12_dev``, hand-written HIP for gfx950, enqueued on torch's
+  current HIP stream).
+* ``VideoScorer`` — a session over one MP4 file: host demux, device H.264
+  subset decode, device scoring (``vts_open`` / ``vts_score`` / ``vts_run``).
+
+There is no CPU fallback: without libvtseg.so or without a GPU these raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib
+
+DEFAULT_CUT_THRESHOLD = 0.08
+
+
+def _torch():
+    import torch  # plumbing only: device allocations and the current stream
+    return torch
+
+
+def _stream_handle(device) -> int:
+    torch = _torch()
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+def thumb_size(width: int, height: int, k: int) -> tuple[int, int]:
+    return width // k, height // k
+
+
+def score_nv12(nv12, *, width: int, height: int, pitch: int, uv_row_offset: int,
+               frame_stride: int, n_frames: int, k: int, prev_luma=None,
+               want_rgb: bool = True, want_hist: bool = True, out: dict | None = None,
+               workspace=None) -> dict:
+    """Score n_frames NV12 frames resident on the GPU (uint8 tensor, any shape,
+    contiguous, 16-byte aligned).  Returns device tensors
+    {rgb [F,h,w,3] u8, hist [F,256] i32(u32 bits), sad [F] i64(u64 bits),
+    score [F] f32, last_luma [h*w] u8}."""
+    torch = _torch()
+    if not nv12.is_cuda:
+        raise ValueError("nv12 must be a device tensor")
+    if nv12.dtype != torch.uint8 or not nv12.is_contiguous():
+        raise ValueError("nv12 must be a contiguous uint8 tensor")
+    dev = nv12.device
+    w, h = thumb_size(width, height, k)
+    if out is None:
+        out = {
+            "rgb": torch.empty((n_frames, h, w, 3), dtype=torch.uint8, device=dev)
+            if want_rgb else None,
+            "hist": torch.empty((n_frames, 256), dtype=torch.int32, device=dev)
+            if want_hist else None,
+            "sad": torch.empty(n_frames, dtype=torch.int64, device=dev),
+            "score": torch.empty(n_frames, dtype=torch.float32, device=dev),
+            "last_luma": torch.empty(h * w, dtype=torch.uint8, device=dev),
+        }
+    ws_bytes = int(_lib.lib().vts_score_workspace_bytes(width, height, k, n_frames))
+    if workspace is None or workspace.numel() < ws_bytes:
+        workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    d = _lib.ScoreDesc()
+    d.nv12 = nv12.data_ptr()
+    d.frame_stride = frame_stride
+    d.n_frames = n_frames
+    d.width, d.height, d.pitch, d.uv_row_offset, d.k = width, height, pitch, uv_row_offset, k
+
+    def p(t):
+        return None if t is None else t.data_ptr()
+
+    d.rgb = p(out["rgb"])
+    d.hist = p(out["hist"])
+    d.sad = p(out["sad"])
+    d.score = p(out["score"])
+    d.prev_luma = p(prev_luma)
+    d.last_luma = p(out["last_luma"])
+    d.workspace = workspace.data_ptr()
+    d.workspace_bytes = workspace.numel()
+    _lib.check(_lib.lib().vts_score_nv12_dev(C.byref(d), C.c_void_p(_stream_handle(dev))))
+    out["_workspace"] = workspace
+    return out
+
+
+@dataclass
+class SceneResult:
+    scores: np.ndarray       # float32 [F]
+    hist: np.ndarray         # uint32 [F, 256]
+    sad: np.ndarray          # uint64 [F]
+    pts: np.ndarray          # int64 [F], track timescale, presentation order
+    timescale: int
+
+    def cuts(self, threshold: float = DEFAULT_CUT_THRESHOLD) -> np.ndarray:
+        return np.nonzero(self.scores > threshold)[0]
+
+
+class VideoScorer:
+    """Decode + score one MP4 file on GPU `device` (vts_open ... vts_close)."""
+
+    def __init__(self, path: str | Path, device: int = 0, *, k: int = 0,
+                 window_frames: int = 0, n_streams: int = 2,
+                 cut_threshold: float = DEFAULT_CUT_THRESHOLD):
+        self._lib = _lib.lib()
+        prm = _lib.Params()
+        prm.k = k
+        prm.window_frames = window_frames
+        prm.keep_rgb = 0
+        prm.n_streams = n_streams
+        prm.cut_threshold = cut_threshold
+        ctx = C.c_void_p()
+        _lib.check(self._lib.vts_open(int(device), str(path).encode(), C.byref(prm),
+                                      C.byref(ctx)))
+        self._ctx = ctx
+        info = _lib.VideoInfo()
+        _lib.check(self._lib.vts_info(self._ctx, C.byref(info)))
+        self.info = info
+
+    @property
+    def n_frames(self) -> int:
+        return int(self.info.n_frames)
+
+    def score(self) -> SceneResult:
+        n = self.n_frames
+        scores = np.zeros(n, np.float32)
+        hist = np.zeros((n, 256), np.uint32)
+        sad = np.zeros(n, np.uint64)
+        pts = np.zeros(n, np.int64)
+        got = C.c_int64(0)
+        f32 = C.POINTER(C.c_float)
+        _lib.check(self._lib.vts_score(
+            self._ctx, scores.ctypes.data_as(f32),
+            hist.ctypes.data_as(C.POINTER(C.c_uint32)),
+            sad.ctypes.data_as(C.POINTER(C.c_uint64)),
+            pts.ctypes.data_as(C.POINTER(C.c_int64)), n, C.byref(got)))
+        return SceneResult(scores, hist, sad, pts, int(self.info.track_timescale))
+
+    def run(self) -> None:
+        """Decode + score with results left on the device (benchmark step)."""
+        _lib.check(self._lib.vts_run(self._ctx))
+
+    def timings(self) -> dict:
+        t = (C.c_double * 4)()
+        _lib.check(self._lib.vts_last_timings(self._ctx, t))
+        return {"total_ms": t[0], "parse_ms": t[1], "reconstruct_ms": t[2],
+                "score_ms": t[3]}
+
+    def boundary_frames(self, times) -> list[int]:
+        arr = (C.c_double * len(times))(*[float(t) for t in times])
+        out = (C.c_int64 * len(times))()
+        _lib.check(self._lib.vts_boundary_frames(self._ctx, arr, len(times), out))
+        return list(out)
+
+    def scene_cuts(self) -> list[int]:
+        n = C.c_int64(0)
+        cap = self.n_frames
+        buf = (C.c_int64 * max(cap, 1))()
+        _lib.check(self._lib.vts_scene_cuts(self._ctx, buf, cap, C.byref(n)))
+        return list(buf[: n.value])
+
+    def frame_nv12(self, i: int) -> np.ndarray:
+        w, h = int(self.info.width), int(self.info.height)
+        out = np.zeros(w * h * 3 // 2, np.uint8)
+        _lib.check(self._lib.vts_get_frame_nv12(
+            self._ctx, i, out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size))
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.vts_close(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
+                fps: int = 30, n_frames: int = 300, seed: int = 0x5EED,
+                cut_min_s: float = 2.0, cut_max_s: float = 20.0, gop_max_s: float = 2.0,
+                max_motion: int = 4, slices_per_row: int = 1,
+                hash_frames: bool = False) -> dict:
+    """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
+    and the ground-truth scene-cut frames."""
+    p = _lib.SynthParams()
+    p.width, p.height, p.fps_num, p.fps_den = width, height, fps, 1
+    p.n_frames, p.seed = n_frames, seed
+    p.cut_min_s, p.cut_max_s, p.gop_max_s = cut_min_s, cut_max_s, gop_max_s
+    p.max_motion, p.slices_per_row = max_motion, slices_per_row
+    p.hash_frames = 1 if hash_frames else 0
+    info = _lib.SynthInfo()
+    cuts = (C.c_int64 * max(n_frames, 1))()
+    _lib.check(_lib.lib().vts_synth_write(str(path).encode(), C.byref(p), C.byref(info),
+                                          cuts, n_frames))
+    return {"bytes": int(info.bytes_written), "n_idr": int(info.n_idr),
+            "n_cuts": int(info.n_cuts), "timescale": int(info.timescale),
+            "recon_hash": int(info.recon_hash),
+            "cuts": list(cuts[: int(info.n_cuts)])}
