@@ -206,6 +206,19 @@ def main() -> None:
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": kname, "kernel_ms": round(kern_ms, 4),
             "bytes_per_frame": bytes_per_frame, "frames_per_launch": F}
+    roof_decode = None
+    if scorer is not None:
+        # h264_recon: one launch per GOP level; bytes per frame = NV12 written +
+        # NV12-sized source read (reference picture or I_PCM samples)
+        n_launch = scorer.recon_launches()
+        rec_ms = float(np.mean([t["reconstruct_ms"] for t in times])) / n_launch
+        rec_bytes = 3 * width * height
+        ach = rec_bytes * (F / n_launch) / (rec_ms * 1e-3) / 1e9
+        roof_decode = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                       "kernel": "h264_recon", "kernel_ms": round(rec_ms, 4),
+                       "launches": n_launch, "bytes_per_frame": rec_bytes,
+                       "frames_per_launch": round(F / n_launch, 1)}
 
     counts = counts_all.cpu().tolist()
     cpu = None
@@ -224,6 +237,7 @@ def main() -> None:
                        "parallelism": f"video-per-gpu x{world}",
                        "segment_counts": counts},
             "roofline": roof,
+            "roofline_decode": roof_decode,
             "cpu_baseline": cpu,
         }
         if scorer is not None:

@@ -190,7 +190,7 @@ typedef struct vts_ctx vts_ctx;
 typedef struct vts_params {
   int32_t k;               /* thumbnail downscale; 0 = auto (4 for <=720p, 6 above) */
   int32_t window_frames;   /* decoded-surface ring size in frames; 0 = auto        */
-  int32_t keep_rgb;        /* 1 = keep the last window's RGB thumbnails            */
+  int32_t keep_rgb;        /* reserved (RGB thumbnails of every frame are kept)    */
   int32_t n_streams;       /* 1 or 2 (2 = decode/score overlap on two HIP streams) */
   float cut_threshold;     /* scene-cut threshold on score (default 0.08 when <=0) */
   int32_t _pad;
@@ -226,9 +226,15 @@ int vts_boundary_frames(vts_ctx *ctx, const double *times, int64_t n,
  * recent window to host; only frames still resident in the ring. */
 int vts_get_frame_nv12(vts_ctx *ctx, int64_t frame, uint8_t *out,
                        int64_t out_bytes);
+/* RGB thumbnail (w x h x 3, see vts_score_desc) of frame i of the last run. */
+int vts_get_thumbnail_rgb(vts_ctx *ctx, int64_t frame, uint8_t *out,
+                          int64_t out_bytes);
 /* Timing of the last vts_run/vts_score, milliseconds, HIP events:
  * [0] whole, [1] parse, [2] reconstruct, [3] score. */
 int vts_last_timings(const vts_ctx *ctx, double *ms4);
+/* Decode schedule facts: what = 0 reconstruct launches per run, 1 windows,
+ * 2 slices, 3 ring frames; < 0 on error. */
+int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);
 int vts_close(vts_ctx *ctx);
 
 /* ------------------------------------------------ synthetic stream writer */

@@ -1,0 +1,59 @@
+"""Multi-process batch path (world_size 2, gloo on CPU): sharding + all-gather.
+
+Each rank plans its own videos (i % 2 == rank); after the all-gather every
+rank holds the same batch plan, equal to a single-process run.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+CONFIG = {"analyzer": {"max_continuations": 3, "retry_times": 5,
+                       "long_video": {"enabled": True, "default_segment_seconds": 20,
+                                      "overlap_seconds": 2, "min_segment_seconds": 5,
+                                      "hard_max_api_calls": 50, "consolidate": True}}}
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, paths, out_dir):
+    sys.path[:0] = [str(ROOT / "video-transformer_amd")]
+    import torch.distributed as dist
+    from vtseg.batch import plan_batch
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    items = plan_batch(paths, CONFIG)
+    (Path(out_dir) / f"r{rank}.txt").write_text(repr([tuple(vars(i).values()) for i in items]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_videos", [5, 2, 1])
+def test_two_rank_batch_equals_serial(tmp_path, n_videos):
+    import torch.multiprocessing as mp
+    from vtseg import scene
+    from vtseg.batch import plan_batch
+    paths = []
+    for i in range(n_videos):
+        p = tmp_path / f"v{i}.mp4"
+        scene.synth_write(p, width=64, height=48, n_frames=300 + 150 * i, seed=i)
+        paths.append(str(p))
+    serial = [tuple(vars(i).values())[:5] for i in plan_batch(paths, CONFIG)]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    mp.start_processes(_worker, args=(2, _free_port(), paths, str(tmp_path)), nprocs=2,
+                       join=True, start_method="spawn")
+    r0 = eval((tmp_path / "r0.txt").read_text())
+    r1 = eval((tmp_path / "r1.txt").read_text())
+    assert r0 == r1
+    assert [t[:5] for t in r0] == serial
+    assert [t[5] for t in r0] == [i % 2 for i in range(n_videos)]
+    assert [t[2] for t in r0] == [(300 + 150 * i) / 30 for i in range(n_videos)]

@@ -37,7 +37,7 @@ def _require_gpu():
 def _oracle_scores(frames, w, h):
     k = 4 if h <= 720 else 6
     return oracle.score_frames(frames.reshape(-1), frames[0].size, frames.shape[0], w, h, w, h, k,
-                               want_rgb=False)
+                               want_rgb=True)
 
 
 @pytest.mark.parametrize("name,kw", STREAMS, ids=[s[0] for s in STREAMS])
@@ -55,6 +55,8 @@ def test_decode_and_score_bit_exact(tmp_path, name, kw):
         for i in range(n):
             got = vsr.frame_nv12(i).reshape(frames[i].shape)
             assert np.array_equal(got, frames[i]), f"frame {i} differs"
+        rgb = np.stack([vsr.thumbnail_rgb(i) for i in range(n)]).reshape(-1)
+        assert np.array_equal(rgb, ref["rgb"])
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])

@@ -78,7 +78,7 @@ def test_score_kernel_prev_luma_continuity():
     from vtseg import scene
     rng = np.random.default_rng(7)
     width, height, k, n = 640, 360, 4, 600
-    host, stride = smooth_nv12(rng, n, width, height, width, height, height)
+    host, stride = smooth_nv12(rng, n, width, height, width, height + height // 2, height)
     dev = torch.from_numpy(host).cuda()
     kw = dict(width=width, height=height, pitch=width, uv_row_offset=height,
               frame_stride=stride, k=k, want_rgb=False)

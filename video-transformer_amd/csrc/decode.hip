@@ -291,6 +291,8 @@ __global__ void __launch_bounds__(64) h264_parse(ParseArgs a) {
     const int x = addr % mbw, y = addr / mbw;
     if ((!is_p && mb_type == 25) || (is_p && mb_type == 30)) {
       br.align();
+      // an emulation-prevention byte right at the PCM start would shift it
+      if (br.zeros >= 2 && br.pos < br.size && br.byte_at(br.pos) == 3) errs |= DEC_E_EPB_IN_PCM;
       const int64_t off = br.abs0 + br.pos;
       br.skip_bytes(384);
       cmd[addr] = MB_PCM | static_cast<uint64_t>(off);
@@ -337,53 +339,54 @@ __global__ void __launch_bounds__(64) h264_parse(ParseArgs a) {
 }
 
 // --------------------------------------------------------- reconstruction
-// 16 bytes at an arbitrary byte address, from 5 aligned dwords.
-__device__ __forceinline__ uint4 load16u(const uint8_t *p) {
+// 16 bytes at any byte address: two aligned 16-byte loads (both coalesced
+// across lanes) and a funnel shift in registers.  Reads up to 15 bytes past
+// the 16 requested (buffers carry >= 32 bytes of padding).
+__device__ __forceinline__ uint4 load16_any(const uint8_t *p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  const int sh = static_cast<int>(a & 3);
-  const uint32_t t0 = w[0], t1 = w[1], t2 = w[2], t3 = w[3];
-  if (sh == 0) return make_uint4(t0, t1, t2, t3);
-  const uint32_t t4 = w[4];
-  return make_uint4(__builtin_amdgcn_alignbyte(t1, t0, sh), __builtin_amdgcn_alignbyte(t2, t1, sh),
-                    __builtin_amdgcn_alignbyte(t3, t2, sh), __builtin_amdgcn_alignbyte(t4, t3, sh));
+  const uint4 *q = reinterpret_cast<const uint4 *>(a & ~uintptr_t(15));
+  const int sh = static_cast<int>(a & 15);
+  const uint4 lo = q[0];
+  if (sh == 0) return lo;
+  const uint4 hi = q[1];
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const int qd = sh >> 2, r = sh & 3;
+  uint32_t s[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+    s[i] = (qd == 0) ? w[i] : (qd == 1) ? w[i + 1] : (qd == 2) ? w[i + 2] : w[i + 3 < 8 ? i + 3 : 7];
+  return make_uint4(__builtin_amdgcn_alignbyte(s[1], s[0], r), __builtin_amdgcn_alignbyte(s[2], s[1], r),
+                    __builtin_amdgcn_alignbyte(s[3], s[2], r), __builtin_amdgcn_alignbyte(s[4], s[3], r));
 }
 
-__device__ __forceinline__ uint2 load8u(const uint8_t *p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  const int sh = static_cast<int>(a & 3);
-  const uint32_t t0 = w[0], t1 = w[1];
-  if (sh == 0) return make_uint2(t0, t1);
-  const uint32_t t2 = w[2];
-  return make_uint2(__builtin_amdgcn_alignbyte(t1, t0, sh), __builtin_amdgcn_alignbyte(t2, t1, sh));
+__device__ __forceinline__ uint32_t has_zero_byte(uint32_t v) {
+  return (v - 0x01010101u) & ~v & 0x80808080u;
 }
 
-// true if bytes p[-2 .. n) contain 00 00 03 with the 03 at index >= 0
-__device__ bool has_epb(const uint8_t *p, int n) {
-  uint32_t z = (p[-2] == 0) + 0;
-  z = (p[-1] == 0) ? z + 1 : 0;
-  for (int i = 0; i < n; ++i) {
-    const uint32_t b = p[i];
-    if (z >= 2 && b == 3) return true;
-    z = (b == 0) ? z + 1 : 0;
+// Emulation-prevention bytes (00 00 03) whose 03 lies inside the I_PCM sample
+// span [pcm, pcm + 384) would make the recorded offsets wrong.  Checked only
+// for chunks that contain a zero byte (a pattern needs two zeros).
+__device__ bool epb_in_pcm(const uint8_t *chunk, int n, const uint8_t *pcm) {
+  for (int j = -2; j < n; ++j) {
+    const uint8_t *t = chunk + j;
+    if (t + 2 < pcm || t + 2 >= pcm + 384) continue;
+    if (t[0] == 0 && t[1] == 0 && t[2] == 3) return true;
   }
   return false;
 }
 
 // interleave 8 Cb and 8 Cr bytes into 16 NV12 bytes (u0 v0 u1 v1 ...)
-__device__ __forceinline__ uint4 interleave_uv(uint2 u, uint2 v) {
+__device__ __forceinline__ uint4 interleave_uv(uint32_t u0, uint32_t u1, uint32_t v0, uint32_t v1) {
   // v_perm_b32 selector: bytes of {src0, src1} = {hi word, lo word}
-  const uint32_t x0 = __builtin_amdgcn_perm(v.x, u.x, 0x05010400u);
-  const uint32_t x1 = __builtin_amdgcn_perm(v.x, u.x, 0x07030602u);
-  const uint32_t x2 = __builtin_amdgcn_perm(v.y, u.y, 0x05010400u);
-  const uint32_t x3 = __builtin_amdgcn_perm(v.y, u.y, 0x07030602u);
-  return make_uint4(x0, x1, x2, x3);
+  return make_uint4(__builtin_amdgcn_perm(v0, u0, 0x05010400u), __builtin_amdgcn_perm(v0, u0, 0x07030602u),
+                    __builtin_amdgcn_perm(v1, u1, 0x05010400u), __builtin_amdgcn_perm(v1, u1, 0x07030602u));
 }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-__global__ void __launch_bounds__(256) h264_recon(ReconArgs a) {
+constexpr int kReconThreads = 256;
+
+__global__ void __launch_bounds__(kReconThreads) h264_recon(ReconArgs a) {
   const int mbw = a.mb_width, mbh = a.mb_height;
   const int fi = blockIdx.x / mbh;  // frame within this launch
   const int mby = blockIdx.x - fi * mbh;
@@ -397,49 +400,56 @@ __global__ void __launch_bounds__(256) h264_recon(ReconArgs a) {
   const uint64_t *cmd = a.cmd + static_cast<int64_t>(fr.x) * (mbw * mbh) + mby * mbw;
   uint32_t errs = 0;
 
-  for (int it = threadIdx.x; it < 24 * mbw; it += blockDim.x) {
-    const int r = it / mbw;       // 0..15 luma rows, 16..23 chroma rows
-    const int m = it - r * mbw;   // macroblock column
+  // items: 24 rows (16 luma + 8 chroma) x mbw 16-byte columns; walk them with
+  // incremental (row, column) instead of a division per item
+  const int n_items = 24 * mbw;
+  const int step_r = kReconThreads / mbw, step_m = kReconThreads - step_r * mbw;
+  int r = threadIdx.x / mbw, m = threadIdx.x - (threadIdx.x / mbw) * mbw;
+  for (int it = threadIdx.x; it < n_items; it += kReconThreads) {
     const uint64_t c = cmd[m];
     const uint32_t kind = static_cast<uint32_t>(c >> 62);
+    const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
     uint4 out = make_uint4(0, 0, 0, 0);
-    if (r < 16) {
+    if (kind == 0 || (kind == 2 && !ref)) {
+      errs |= (kind == 0) ? DEC_E_MISSING_MB : DEC_E_NO_REF;
+    } else if (r < 16) {
       if (kind == 1) {
-        const uint8_t *src = a.es + static_cast<int64_t>(c & 0xffffffffffffull) + 16 * r;
-        out = load16u(src);
-        if (has_epb(src, 16)) errs |= DEC_E_EPB_IN_PCM;
-      } else if (kind == 2 && ref) {
-        const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+        const uint8_t *pcm = a.es + static_cast<int64_t>(c & 0xffffffffffffull);
+        const uint8_t *src = pcm + 16 * r;
+        out = load16_any(src);
+        if ((has_zero_byte(out.x) | has_zero_byte(out.y) | has_zero_byte(out.z) | has_zero_byte(out.w)) &&
+            epb_in_pcm(src, 16, pcm))
+          errs |= DEC_E_EPB_IN_PCM;
+      } else {
         const int sy = clampi(mby * 16 + r + (mvy >> 2), 0, H - 1);
         const int sx = m * 16 + (mvx >> 2);
         const uint8_t *row = ref + sy * pitch;
         if (sx >= 0 && sx + 15 <= W - 1) {
-          out = load16u(row + sx);
+          out = load16_any(row + sx);
         } else {
           uint32_t wv[4] = {0, 0, 0, 0};
           for (int b = 0; b < 16; ++b)
             wv[b >> 2] |= uint32_t(row[clampi(sx + b, 0, W - 1)]) << (8 * (b & 3));
           out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
-      } else {
-        errs |= (kind == 0) ? DEC_E_MISSING_MB : DEC_E_NO_REF;
       }
-      *reinterpret_cast<uint4 *>(dst + (mby * 16 + r) * pitch + m * 16) = out;
     } else {
       const int cr = r - 16;
       if (kind == 1) {
         const uint8_t *pcm = a.es + static_cast<int64_t>(c & 0xffffffffffffull);
-        const uint8_t *us = pcm + 256 + 8 * cr, *vs = pcm + 320 + 8 * cr;
-        out = interleave_uv(load8u(us), load8u(vs));
-        if (has_epb(us, 8) || has_epb(vs, 8)) errs |= DEC_E_EPB_IN_PCM;
-      } else if (kind == 2 && ref) {
-        const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+        const uint4 u = load16_any(pcm + 256 + 8 * cr);  // first 8 bytes used
+        const uint4 v = load16_any(pcm + 320 + 8 * cr);
+        out = interleave_uv(u.x, u.y, v.x, v.y);
+        if ((has_zero_byte(u.x) | has_zero_byte(u.y) | has_zero_byte(v.x) | has_zero_byte(v.y)) &&
+            (epb_in_pcm(pcm + 256 + 8 * cr, 8, pcm) || epb_in_pcm(pcm + 320 + 8 * cr, 8, pcm)))
+          errs |= DEC_E_EPB_IN_PCM;
+      } else {
         const int fx = mvx & 7, fy = mvy & 7;
         const int cx = m * 8 + (mvx >> 3), cy = mby * 8 + cr + (mvy >> 3);
         if (fx == 0 && fy == 0) {
           const uint8_t *row = ref_uv + clampi(cy, 0, CH - 1) * pitch;
           if (cx >= 0 && cx + 7 <= CW - 1) {
-            out = load16u(row + 2 * cx);
+            out = load16_any(row + 2 * cx);
           } else {
             uint32_t wv[4] = {0, 0, 0, 0};
             for (int b = 0; b < 8; ++b) {
@@ -464,10 +474,16 @@ __global__ void __launch_bounds__(256) h264_recon(ReconArgs a) {
           }
           out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
-      } else {
-        errs |= (kind == 0) ? DEC_E_MISSING_MB : DEC_E_NO_REF;
       }
-      *reinterpret_cast<uint4 *>(dst_uv + (mby * 8 + cr) * pitch + m * 16) = out;
+    }
+    uint8_t *o = (r < 16) ? dst + (mby * 16 + r) * pitch + m * 16
+                          : dst_uv + (mby * 8 + (r - 16)) * pitch + m * 16;
+    *reinterpret_cast<uint4 *>(o) = out;
+    m += step_m;
+    r += step_r;
+    if (m >= mbw) {
+      m -= mbw;
+      ++r;
     }
   }
   if (errs) atomicOr(a.err, errs);
@@ -485,7 +501,7 @@ int parse_launch(const ParseArgs &a, hipStream_t s) {
 
 int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
-  hipLaunchKernelGGL(h264_recon, dim3(n_frames * a.mb_height), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(h264_recon, dim3(n_frames * a.mb_height), dim3(kReconThreads), 0, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon launch: %s", hipGetErrorString(e));
   return VTS_OK;

@@ -66,18 +66,24 @@ __device__ __forceinline__ uint32_t byte_sum(const uint32_t *w, uint32_t acc) {
   return acc;
 }
 
-__device__ __forceinline__ uint32_t clamp255(int v) {
-  return static_cast<uint32_t>(v < 0 ? 0 : (v > 255 ? 255 : v));
+// clamp(floor(x / 256), 0, 255).  The shift is an opaque asm statement: for
+// the plain `clamp(x >> 8, 0, 255)` hipcc (ROCm 7.2) selects gfx950's
+// v_ashr_pk_u8_i32 for pairs of such values, and those bytes came out wrong
+// (saturated as if unshifted; caught by the bit-exact tests).
+__device__ __forceinline__ uint32_t shr8_sat(int x) {
+  int t;
+  asm("v_ashrrev_i32 %0, 8, %1" : "=v"(t) : "v"(x));
+  return static_cast<uint32_t>(t < 0 ? 0 : (t > 255 ? 255 : t));
 }
 
-// BT.709 limited range, 8-bit fixed point (x256), arithmetic shift = floor.
+// BT.709 limited range, 8-bit fixed point (x256); floor division by 256.
 __device__ __forceinline__ void bt709(uint32_t y, uint32_t u, uint32_t v, uint32_t *r,
                                       uint32_t *g, uint32_t *b) {
   const int c = static_cast<int>(y) - 16, d = static_cast<int>(u) - 128,
             e = static_cast<int>(v) - 128;
-  *r = clamp255((298 * c + 459 * e + 128) >> 8);
-  *g = clamp255((298 * c - 55 * d - 136 * e + 128) >> 8);
-  *b = clamp255((298 * c + 541 * d + 128) >> 8);
+  *r = shr8_sat(298 * c + 459 * e + 128);
+  *g = shr8_sat(298 * c - 55 * d - 136 * e + 128);
+  *b = shr8_sat(298 * c + 541 * d + 128);
 }
 
 // Load kRowBytes of one row at `p` (16-byte aligned) as words.

@@ -86,6 +86,8 @@ struct vts_ctx {
   float *d_score = nullptr;
   uint64_t *d_sad = nullptr;
   uint32_t *d_hist = nullptr;
+  uint8_t *d_rgb = nullptr;       // RGB thumbnails of every frame
+  int64_t thumb_px = 0;
   hipStream_t s_dec = nullptr, s_score = nullptr;
   std::vector<hipEvent_t> ev;  // per window: dec0, dec1, sc0, sc1
   hipEvent_t ev_start = nullptr, ev_end = nullptr;
@@ -301,6 +303,8 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   HIP_TRY(hipMalloc(&c->d_score, sizeof(float) * c->n_frames));
   HIP_TRY(hipMalloc(&c->d_sad, sizeof(uint64_t) * c->n_frames));
   HIP_TRY(hipMalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
+  c->thumb_px = tw;
+  HIP_TRY(hipMalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
   HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
   c->ev.resize(c->windows.size() * 6);
@@ -344,7 +348,9 @@ int run_all(vts_ctx *c) {
   HIP_TRY(hipStreamWaitEvent(c->s_score, c->ev_start, 0));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
   hipStream_t sd = c->s_dec;
-  hipStream_t ss = (c->params.n_streams >= 2) ? c->s_score : c->s_dec;
+  // one window: one stream (nothing to overlap, and HIP event timing of each
+  // stage stays on a single queue)
+  hipStream_t ss = (c->params.n_streams >= 2 && c->windows.size() > 1) ? c->s_score : c->s_dec;
   const size_t nw = c->windows.size();
   for (size_t wi = 0; wi < nw; ++wi) {
     const Window &w = c->windows[wi];
@@ -388,7 +394,7 @@ int run_all(vts_ctx *c) {
     d.pitch = c->pitch;
     d.uv_row_offset = c->coded_h;
     d.k = c->k;
-    d.rgb = nullptr;
+    d.rgb = c->d_rgb + 3 * c->thumb_px * w.f0;
     d.hist = c->d_hist + w.f0 * 256;
     d.sad = c->d_sad + w.f0;
     d.score = c->d_score + w.f0;
@@ -541,11 +547,38 @@ extern "C" int vts_get_frame_nv12(vts_ctx *c, int64_t frame, uint8_t *out, int64
   return fail(VTS_E_INVALID, "frame %lld is not resident", static_cast<long long>(frame));
 }
 
+extern "C" int vts_get_thumbnail_rgb(vts_ctx *c, int64_t frame, uint8_t *out, int64_t out_bytes) {
+  clear_error();
+  if (!c || !out) return fail(VTS_E_INVALID, "NULL argument");
+  if (!c->have_results) return fail(VTS_E_INVALID, "run vts_score/vts_run first");
+  if (frame < 0 || frame >= c->n_frames) return fail(VTS_E_INVALID, "frame out of range");
+  const int64_t need = 3 * c->thumb_px;
+  if (out_bytes < need) return fail(VTS_E_CAPACITY, "need %lld bytes", static_cast<long long>(need));
+  HIP_TRY(hipMemcpy(out, c->d_rgb + need * frame, static_cast<size_t>(need), hipMemcpyDeviceToHost));
+  return VTS_OK;
+}
+
 extern "C" int vts_last_timings(const vts_ctx *c, double *ms4) {
   clear_error();
   if (!c || !ms4) return fail(VTS_E_INVALID, "NULL argument");
   for (int i = 0; i < 4; ++i) ms4[i] = c->timings[i];
   return VTS_OK;
+}
+
+extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
+  clear_error();
+  if (!c) return fail(VTS_E_INVALID, "NULL ctx");
+  switch (what) {
+    case 0: {
+      int64_t n = 0;
+      for (const Window &w : c->windows) n += static_cast<int64_t>(w.lvl_off.size());
+      return n;
+    }
+    case 1: return static_cast<int64_t>(c->windows.size());
+    case 2: return static_cast<int64_t>(c->slices.size());
+    case 3: return c->ring_frames;
+    default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
+  }
 }
 
 extern "C" int vts_close(vts_ctx *c) {
@@ -569,6 +602,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_score);
   f(c->d_sad);
   f(c->d_hist);
+  f(c->d_rgb);
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);

@@ -129,7 +129,9 @@ SIGNATURES: dict[str, tuple] = {
     "vts_boundary_frames": (C.c_int, [C.c_void_p, _P(C.c_double), C.c_int64,
                                       _P(C.c_int64)]),
     "vts_get_frame_nv12": (C.c_int, [C.c_void_p, C.c_int64, _P(C.c_uint8), C.c_int64]),
+    "vts_get_thumbnail_rgb": (C.c_int, [C.c_void_p, C.c_int64, _P(C.c_uint8), C.c_int64]),
     "vts_last_timings": (C.c_int, [C.c_void_p, _P(C.c_double)]),
+    "vts_schedule_info": (C.c_int64, [C.c_void_p, C.c_int32]),
     "vts_close": (C.c_int, [C.c_void_p]),
     "vts_synth_write": (C.c_int, [C.c_char_p, _P(SynthParams), _P(SynthInfo),
                                   _P(C.c_int64), C.c_int64]),

@@ -150,6 +150,10 @@ class VideoScorer:
         return {"total_ms": t[0], "parse_ms": t[1], "reconstruct_ms": t[2],
                 "score_ms": t[3]}
 
+    def recon_launches(self) -> int:
+        """Reconstruct launches per run (one per GOP level per window)."""
+        return int(self._lib.vts_schedule_info(self._ctx, 0))
+
     def boundary_frames(self, times) -> list[int]:
         arr = (C.c_double * len(times))(*[float(t) for t in times])
         out = (C.c_int64 * len(times))()
@@ -167,6 +171,14 @@ class VideoScorer:
         w, h = int(self.info.width), int(self.info.height)
         out = np.zeros(w * h * 3 // 2, np.uint8)
         _lib.check(self._lib.vts_get_frame_nv12(
+            self._ctx, i, out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size))
+        return out
+
+    def thumbnail_rgb(self, i: int, k: int | None = None) -> np.ndarray:
+        kk = k or (4 if int(self.info.height) <= 720 else 6)
+        w, h = int(self.info.width) // kk, int(self.info.height) // kk
+        out = np.zeros((h, w, 3), np.uint8)
+        _lib.check(self._lib.vts_get_thumbnail_rgb(
             self._ctx, i, out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size))
         return out
 
