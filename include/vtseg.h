@@ -193,7 +193,8 @@ typedef struct vts_params {
   int32_t keep_rgb;        /* reserved (RGB thumbnails of every frame are kept)    */
   int32_t n_streams;       /* 1 or 2 (2 = decode/score overlap on two HIP streams) */
   float cut_threshold;     /* scene-cut threshold on score (default 0.08 when <=0) */
-  int32_t _pad;
+  int32_t fused;           /* 0 auto, 1 require, -1 never: fuse scoring into
+                              reconstruction (k in {2,4,8}, no cropping)       */
 } vts_params;
 
 /* Demux the file's first H.264 video track on the host (MP4 boxes and NAL
@@ -233,7 +234,7 @@ int vts_get_thumbnail_rgb(vts_ctx *ctx, int64_t frame, uint8_t *out,
  * [0] whole, [1] parse, [2] reconstruct, [3] score. */
 int vts_last_timings(const vts_ctx *ctx, double *ms4);
 /* Decode schedule facts: what = 0 reconstruct launches per run, 1 windows,
- * 2 slices, 3 ring frames; < 0 on error. */
+ * 2 slices, 3 ring frames, 4 fused scoring (1/0); < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);
 int vts_close(vts_ctx *ctx);
 

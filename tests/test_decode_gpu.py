@@ -115,3 +115,41 @@ def test_open_rejects_non_mp4(tmp_path):
     bad.write_bytes(b"\x00" * 4096)
     with pytest.raises(VtsegError):
         scene.VideoScorer(bad)
+
+
+@pytest.mark.parametrize("k", [2, 4, 8])
+def test_fused_and_unfused_paths_agree_with_oracle(tmp_path, k):
+    """Scoring fused into reconstruction (one pass) equals the two-kernel path
+    and the oracle, for every k that divides a macroblock."""
+    _require_gpu()
+    path = tmp_path / "f.mp4"
+    n = 75
+    scene.synth_write(path, width=480, height=272, n_frames=n, cut_min_s=0.6, cut_max_s=1.2,
+                      gop_max_s=0.7, max_motion=6, slices_per_row=2)
+    frames, _ = oracle.decode_file(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 480, 272, 480, 272, k)
+    results = []
+    for fused in (1, -1):
+        with scene.VideoScorer(path, k=k, fused=fused) as v:
+            assert v._lib.vts_schedule_info(v._ctx, 4) == (1 if fused == 1 else 0)
+            res = v.score()
+            rgb = np.stack([v.thumbnail_rgb(i, k) for i in range(n)]).reshape(-1)
+            results.append((res, rgb))
+            assert np.array_equal(v.frame_nv12(n - 1).reshape(frames[-1].shape), frames[-1])
+        assert np.array_equal(res.scores, ref["score"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(rgb, ref["rgb"])
+
+
+def test_fused_windowed_pipeline(tmp_path):
+    _require_gpu()
+    path = tmp_path / "fw.mp4"
+    scene.synth_write(path, width=320, height=240, n_frames=300, cut_min_s=1, cut_max_s=3,
+                      gop_max_s=0.5)
+    with scene.VideoScorer(path, fused=-1) as a:
+        whole = a.score()
+    with scene.VideoScorer(path, window_frames=32, n_streams=2, fused=1) as b:
+        part = b.score()
+    assert np.array_equal(part.scores, whole.scores)
+    assert np.array_equal(part.hist, whole.hist)

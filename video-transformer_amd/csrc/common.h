@@ -25,6 +25,10 @@ inline int fail(int code, const char *fmt, ...) {
 
 inline void clear_error() { last_error().clear(); }
 
+// Smallest integer q with q >= t * ts, computed exactly from the double's
+// binary value; *sat = +1 / -1 when that integer is above / below int64.
+int64_t ceil_ticks(double t, int64_t ts, int *sat);
+
 }  // namespace vts
 
 #define VTS_TRY(expr)                 \

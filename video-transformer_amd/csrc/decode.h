@@ -40,7 +40,32 @@ struct ReconArgs {
   uint32_t *err;
 };
 
+// Fused reconstruct + scoring (k in {2,4,8}, display size == coded size).
+struct FusedArgs {
+  ReconArgs r;
+  int64_t frame0;          // global frame index of window slot 0
+  int32_t w, h;            // thumbnail size
+  int32_t wgs_per_frame;   // ceil(MBs / 256)
+  int32_t _pad;
+  uint8_t *thumb;          // [slot][h][w] thumbnail luma
+  uint8_t *rgb;            // [global frame][h][w][3]
+  uint32_t *hist;          // [global frame][256], zeroed before the window
+};
+
+struct ThumbSadArgs {
+  const uint8_t *thumb;    // [slot][h][w]
+  const uint8_t *prev_luma;  // predecessor of slot 0 (nullptr = none)
+  uint8_t *last_luma;      // receives slot n_frames-1 (may be nullptr)
+  int64_t frame0;
+  int64_t n_frames;
+  int32_t w, h;
+  uint64_t *sad;           // [global frame]
+  float *score;
+};
+
 int parse_launch(const ParseArgs &a, hipStream_t s);
+int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s);
+int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s);
 int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s);
 int score_launch(const vts_score_desc *d, hipStream_t stream);
 int64_t score_workspace_bytes(int32_t width, int32_t height, int32_t k, int64_t n_frames);

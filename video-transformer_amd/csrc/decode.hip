@@ -28,6 +28,7 @@
 #include "common.h"
 #include "decode.h"
 #include "h264.h"
+#include "pixel.h"
 
 namespace vts {
 namespace {
@@ -386,107 +387,223 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 constexpr int kReconThreads = 256;
 
-__global__ void __launch_bounds__(kReconThreads) h264_recon(ReconArgs a) {
-  const int mbw = a.mb_width, mbh = a.mb_height;
-  const int fi = blockIdx.x / mbh;  // frame within this launch
-  const int mby = blockIdx.x - fi * mbh;
-  const int2 fr = a.frames[fi];     // (slot, ref_slot)
-  const int W = mbw * 16, H = mbh * 16, CW = W / 2, CH = H / 2;
-  const int64_t pitch = a.pitch;
-  uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
-  uint8_t *dst_uv = dst + pitch * H;
-  const uint8_t *ref = fr.y >= 0 ? a.surf + static_cast<int64_t>(fr.y) * a.frame_stride : nullptr;
-  const uint8_t *ref_uv = ref ? ref + pitch * H : nullptr;
-  const uint64_t *cmd = a.cmd + static_cast<int64_t>(fr.x) * (mbw * mbh) + mby * mbw;
-  uint32_t errs = 0;
+struct FrameRefs {
+  const uint8_t *es;
+  const uint8_t *ref, *ref_uv;  // reference picture (nullptr for none)
+  int W, H, CW, CH;
+  int64_t pitch;
+};
 
-  // items: 24 rows (16 luma + 8 chroma) x mbw 16-byte columns; walk them with
-  // incremental (row, column) instead of a division per item
-  const int n_items = 24 * mbw;
-  const int step_r = kReconThreads / mbw, step_m = kReconThreads - step_r * mbw;
-  int r = threadIdx.x / mbw, m = threadIdx.x - (threadIdx.x / mbw) * mbw;
-  for (int it = threadIdx.x; it < n_items; it += kReconThreads) {
-    const uint64_t c = cmd[m];
-    const uint32_t kind = static_cast<uint32_t>(c >> 62);
-    const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
-    uint4 out = make_uint4(0, 0, 0, 0);
-    if (kind == 0 || (kind == 2 && !ref)) {
-      errs |= (kind == 0) ? DEC_E_MISSING_MB : DEC_E_NO_REF;
-    } else if (r < 16) {
-      if (kind == 1) {
-        const uint8_t *pcm = a.es + static_cast<int64_t>(c & 0xffffffffffffull);
-        const uint8_t *src = pcm + 16 * r;
-        out = load16_any(src);
-        if ((has_zero_byte(out.x) | has_zero_byte(out.y) | has_zero_byte(out.z) | has_zero_byte(out.w)) &&
-            epb_in_pcm(src, 16, pcm))
-          errs |= DEC_E_EPB_IN_PCM;
-      } else {
-        const int sy = clampi(mby * 16 + r + (mvy >> 2), 0, H - 1);
-        const int sx = m * 16 + (mvx >> 2);
-        const uint8_t *row = ref + sy * pitch;
-        if (sx >= 0 && sx + 15 <= W - 1) {
-          out = load16_any(row + sx);
-        } else {
-          uint32_t wv[4] = {0, 0, 0, 0};
-          for (int b = 0; b < 16; ++b)
-            wv[b >> 2] |= uint32_t(row[clampi(sx + b, 0, W - 1)]) << (8 * (b & 3));
-          out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-        }
-      }
+// The 16 output bytes of row r (0..15 luma, 16..23 chroma NV12) of macroblock
+// (m, mby) whose command is c.  errs collects DEC_E_* bits.
+__device__ __forceinline__ uint4 fetch_row(const FrameRefs &F, uint64_t c, int r, int m, int mby,
+                                           uint32_t &errs) {
+  const uint32_t kind = static_cast<uint32_t>(c >> 62);
+  const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+  uint4 out = make_uint4(0, 0, 0, 0);
+  if (kind == 0 || (kind == 2 && !F.ref)) {
+    errs |= (kind == 0) ? DEC_E_MISSING_MB : DEC_E_NO_REF;
+  } else if (r < 16) {
+    if (kind == 1) {
+      const uint8_t *pcm = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
+      const uint8_t *src = pcm + 16 * r;
+      out = load16_any(src);
+      if ((has_zero_byte(out.x) | has_zero_byte(out.y) | has_zero_byte(out.z) | has_zero_byte(out.w)) &&
+          epb_in_pcm(src, 16, pcm))
+        errs |= DEC_E_EPB_IN_PCM;
     } else {
-      const int cr = r - 16;
-      if (kind == 1) {
-        const uint8_t *pcm = a.es + static_cast<int64_t>(c & 0xffffffffffffull);
-        const uint4 u = load16_any(pcm + 256 + 8 * cr);  // first 8 bytes used
-        const uint4 v = load16_any(pcm + 320 + 8 * cr);
-        out = interleave_uv(u.x, u.y, v.x, v.y);
-        if ((has_zero_byte(u.x) | has_zero_byte(u.y) | has_zero_byte(v.x) | has_zero_byte(v.y)) &&
-            (epb_in_pcm(pcm + 256 + 8 * cr, 8, pcm) || epb_in_pcm(pcm + 320 + 8 * cr, 8, pcm)))
-          errs |= DEC_E_EPB_IN_PCM;
+      const int sy = clampi(mby * 16 + r + (mvy >> 2), 0, F.H - 1);
+      const int sx = m * 16 + (mvx >> 2);
+      const uint8_t *row = F.ref + sy * F.pitch;
+      if (sx >= 0 && sx + 15 <= F.W - 1) {
+        out = load16_any(row + sx);
       } else {
-        const int fx = mvx & 7, fy = mvy & 7;
-        const int cx = m * 8 + (mvx >> 3), cy = mby * 8 + cr + (mvy >> 3);
-        if (fx == 0 && fy == 0) {
-          const uint8_t *row = ref_uv + clampi(cy, 0, CH - 1) * pitch;
-          if (cx >= 0 && cx + 7 <= CW - 1) {
-            out = load16_any(row + 2 * cx);
-          } else {
-            uint32_t wv[4] = {0, 0, 0, 0};
-            for (int b = 0; b < 8; ++b) {
-              const int sx = clampi(cx + b, 0, CW - 1);
-              wv[b >> 1] |= (uint32_t(row[2 * sx]) | (uint32_t(row[2 * sx + 1]) << 8)) << (16 * (b & 1));
-            }
-            out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-          }
+        uint32_t wv[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 16; ++b)
+          wv[b >> 2] |= uint32_t(row[clampi(sx + b, 0, F.W - 1)]) << (8 * (b & 3));
+        out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+    }
+  } else {
+    const int cr = r - 16;
+    if (kind == 1) {
+      const uint8_t *pcm = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
+      const uint4 u = load16_any(pcm + 256 + 8 * cr);  // first 8 bytes used
+      const uint4 v = load16_any(pcm + 320 + 8 * cr);
+      out = interleave_uv(u.x, u.y, v.x, v.y);
+      if ((has_zero_byte(u.x) | has_zero_byte(u.y) | has_zero_byte(v.x) | has_zero_byte(v.y)) &&
+          (epb_in_pcm(pcm + 256 + 8 * cr, 8, pcm) || epb_in_pcm(pcm + 320 + 8 * cr, 8, pcm)))
+        errs |= DEC_E_EPB_IN_PCM;
+    } else {
+      const int fx = mvx & 7, fy = mvy & 7;
+      const int cx = m * 8 + (mvx >> 3), cy = mby * 8 + cr + (mvy >> 3);
+      if (fx == 0 && fy == 0) {
+        const uint8_t *row = F.ref_uv + clampi(cy, 0, F.CH - 1) * F.pitch;
+        if (cx >= 0 && cx + 7 <= F.CW - 1) {
+          out = load16_any(row + 2 * cx);
         } else {
-          const uint8_t *ra = ref_uv + clampi(cy, 0, CH - 1) * pitch;
-          const uint8_t *rb = ref_uv + clampi(cy + 1, 0, CH - 1) * pitch;
           uint32_t wv[4] = {0, 0, 0, 0};
           for (int b = 0; b < 8; ++b) {
-            const int xa = clampi(cx + b, 0, CW - 1), xb = clampi(cx + b + 1, 0, CW - 1);
-            for (int pl = 0; pl < 2; ++pl) {
-              const int A = ra[2 * xa + pl], B = ra[2 * xb + pl], C = rb[2 * xa + pl], D = rb[2 * xb + pl];
-              const uint32_t v = static_cast<uint32_t>(
-                  ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
-              const int byte = 2 * b + pl;
-              wv[byte >> 2] |= v << (8 * (byte & 3));
-            }
+            const int sx = clampi(cx + b, 0, F.CW - 1);
+            wv[b >> 1] |= (uint32_t(row[2 * sx]) | (uint32_t(row[2 * sx + 1]) << 8)) << (16 * (b & 1));
           }
           out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
+      } else {
+        const uint8_t *ra = F.ref_uv + clampi(cy, 0, F.CH - 1) * F.pitch;
+        const uint8_t *rb = F.ref_uv + clampi(cy + 1, 0, F.CH - 1) * F.pitch;
+        uint32_t wv[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 8; ++b) {
+          const int xa = clampi(cx + b, 0, F.CW - 1), xb = clampi(cx + b + 1, 0, F.CW - 1);
+          for (int pl = 0; pl < 2; ++pl) {
+            const int A = ra[2 * xa + pl], B = ra[2 * xb + pl], C = rb[2 * xa + pl], D = rb[2 * xb + pl];
+            const uint32_t v = static_cast<uint32_t>(
+                ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
+            const int byte = 2 * b + pl;
+            wv[byte >> 2] |= v << (8 * (byte & 3));
+          }
+        }
+        out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
       }
     }
-    uint8_t *o = (r < 16) ? dst + (mby * 16 + r) * pitch + m * 16
-                          : dst_uv + (mby * 8 + (r - 16)) * pitch + m * 16;
-    *reinterpret_cast<uint4 *>(o) = out;
-    m += step_m;
-    r += step_r;
-    if (m >= mbw) {
-      m -= mbw;
-      ++r;
+  }
+  return out;
+}
+
+__device__ __forceinline__ FrameRefs frame_refs(const ReconArgs &a, int ref_slot) {
+  FrameRefs F;
+  F.es = a.es;
+  F.W = a.mb_width * 16;
+  F.H = a.mb_height * 16;
+  F.CW = F.W / 2;
+  F.CH = F.H / 2;
+  F.pitch = a.pitch;
+  F.ref = ref_slot >= 0 ? a.surf + static_cast<int64_t>(ref_slot) * a.frame_stride : nullptr;
+  F.ref_uv = F.ref ? F.ref + F.pitch * F.H : nullptr;
+  return F;
+}
+
+// ------------------------------------------------ fused decode + scoring
+// h264_recon_score<K>: one LANE per (macroblock, group of rows).  A group is
+// the K luma rows + K/2 chroma rows of one thumbnail row (K = 2, 4, 8; K = 0
+// = plain reconstruction in groups of 4 + 2 rows, nothing scored).  A
+// workgroup of 256 lanes covers 256/Q consecutive macroblocks of one frame
+// for all Q groups; lanes of a wave take consecutive macroblocks of the same
+// group, so every row load and store instruction covers contiguous bytes.
+// Each lane issues all of its row loads before using any (memory-level
+// parallelism instead of a serial walk), stores the reconstructed rows and,
+// while they are in registers, box-sums them into the thumbnail pixels:
+// Y'U'V' -> BT.709 RGB, thumbnail luma for the SAD pass, and an LDS
+// histogram flushed once per workgroup with global atomics.  The decoded
+// frame is never re-read for scoring.
+template <int K>
+__global__ void __launch_bounds__(kReconThreads) h264_recon_score(FusedArgs fa) {
+  constexpr int KK = K ? K : 4;      // rows per group
+  constexpr int Q = 16 / KK;         // groups per macroblock
+  constexpr int G = 16 / KK;         // thumbnail pixels per group row
+  constexpr int HK = KK / 2;         // chroma rows per group
+  constexpr int MB_PER_WG = kReconThreads / Q;
+  __shared__ uint32_t lds_hist[256];
+  const ReconArgs &a = fa.r;
+  const int mbw = a.mb_width, mbh = a.mb_height, nmb = mbw * mbh;
+  const int fi = blockIdx.x / fa.wgs_per_frame;
+  const int q = threadIdx.x / MB_PER_WG;
+  const int mb = (blockIdx.x - fi * fa.wgs_per_frame) * MB_PER_WG + (threadIdx.x % MB_PER_WG);
+  const int2 fr = a.frames[fi];
+  const FrameRefs F = frame_refs(a, fr.y);
+  const int64_t gframe = fa.frame0 + fr.x;
+  if constexpr (K != 0) {
+    lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
+    __syncthreads();
+  }
+  uint32_t errs = 0;
+  if (mb < nmb) {
+    const int mby = mb / mbw, m = mb - mby * mbw;
+    const uint64_t c = a.cmd[static_cast<int64_t>(fr.x) * nmb + mb];
+    uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
+    uint8_t *dst_uv = dst + F.pitch * F.H;
+    uint4 yr[KK], cr[HK];
+#pragma unroll
+    for (int rr = 0; rr < KK; ++rr) yr[rr] = fetch_row(F, c, q * KK + rr, m, mby, errs);
+#pragma unroll
+    for (int rr = 0; rr < HK; ++rr) cr[rr] = fetch_row(F, c, 16 + q * HK + rr, m, mby, errs);
+#pragma unroll
+    for (int rr = 0; rr < KK; ++rr)
+      *reinterpret_cast<uint4 *>(dst + (mby * 16 + q * KK + rr) * F.pitch + m * 16) = yr[rr];
+#pragma unroll
+    for (int rr = 0; rr < HK; ++rr)
+      *reinterpret_cast<uint4 *>(dst_uv + (mby * 8 + q * HK + rr) * F.pitch + m * 16) = cr[rr];
+    if constexpr (K != 0) {
+      uint32_t ys[G], us[G], vs[G];
+#pragma unroll
+      for (int p = 0; p < G; ++p) ys[p] = us[p] = vs[p] = 0;
+#pragma unroll
+      for (int rr = 0; rr < K; ++rr) add_luma16<K>(yr[rr], ys);
+#pragma unroll
+      for (int rr = 0; rr < HK; ++rr) add_chroma16<K>(cr[rr], us, vs);
+      uint32_t rgb24[G], packed[(G + 3) / 4];
+#pragma unroll
+      for (int i = 0; i < (G + 3) / 4; ++i) packed[i] = 0;
+#pragma unroll
+      for (int p = 0; p < G; ++p) {
+        const uint32_t y = (ys[p] + K * K / 2) / (K * K);
+        const uint32_t u = (us[p] + HK * HK / 2) / (HK * HK);
+        const uint32_t v = (vs[p] + HK * HK / 2) / (HK * HK);
+        rgb24[p] = bt709_rgb24(y, u, v);
+        packed[p / 4] |= y << (8 * (p & 3));
+        atomicAdd(&lds_hist[y], 1u);
+      }
+      const int64_t tpx = static_cast<int64_t>(mby * Q + q) * fa.w + m * G;
+      store_rgb<G>(fa.rgb + (gframe * fa.w * fa.h + tpx) * 3, rgb24);
+      uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * fa.w * fa.h + tpx;
+      if constexpr (G >= 4) {
+#pragma unroll
+        for (int i = 0; i < G / 4; ++i) reinterpret_cast<uint32_t *>(thumb)[i] = packed[i];
+      } else {
+        *reinterpret_cast<uint16_t *>(thumb) = static_cast<uint16_t>(packed[0]);
+      }
     }
   }
+  if constexpr (K != 0) {
+    __syncthreads();
+    const uint32_t cnt = lds_hist[threadIdx.x];
+    if (cnt) atomicAdd(&fa.hist[gframe * 256 + threadIdx.x], cnt);
+  }
   if (errs) atomicOr(a.err, errs);
+}
+
+// SAD of each frame's thumbnail luma against its predecessor's (the previous
+// window's last thumbnail for the window's first frame) and the score.
+__global__ void __launch_bounds__(256) thumb_sad(ThumbSadArgs t) {
+  const int64_t f = blockIdx.x;  // window slot
+  const int64_t npx = static_cast<int64_t>(t.w) * t.h;
+  const uint8_t *cur = t.thumb + f * npx;
+  const uint8_t *prev = f > 0 ? t.thumb + (f - 1) * npx : t.prev_luma;
+  const int64_t gf = t.frame0 + f;
+  if (f == t.n_frames - 1 && t.last_luma) {
+    for (int64_t i = threadIdx.x; i < npx / 4; i += blockDim.x)
+      reinterpret_cast<uint32_t *>(t.last_luma)[i] = reinterpret_cast<const uint32_t *>(cur)[i];
+  }
+  if (!prev) {
+    if (threadIdx.x == 0) {
+      t.sad[gf] = 0;
+      t.score[gf] = 0.0f;
+    }
+    return;
+  }
+  uint32_t s = 0;
+  for (int64_t i = threadIdx.x; i < npx / 4; i += blockDim.x)
+    s = sad_u8(reinterpret_cast<const uint32_t *>(cur)[i], reinterpret_cast<const uint32_t *>(prev)[i], s);
+  __shared__ uint32_t red[4];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t total = uint64_t(red[0]) + red[1] + red[2] + red[3];
+    t.sad[gf] = total;
+    t.score[gf] = static_cast<float>(static_cast<double>(total) / (static_cast<double>(npx) * 255.0));
+  }
 }
 
 }  // namespace
@@ -499,12 +616,38 @@ int parse_launch(const ParseArgs &a, hipStream_t s) {
   return VTS_OK;
 }
 
-int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s) {
+int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
-  hipLaunchKernelGGL(h264_recon, dim3(n_frames * a.mb_height), dim3(kReconThreads), 0, s, a);
+  const int q = (k == 0) ? 4 : 16 / k;
+  const int nmb = a.r.mb_width * a.r.mb_height;
+  const int mb_per_wg = kReconThreads / q;
+  FusedArgs b = a;
+  b.wgs_per_frame = (nmb + mb_per_wg - 1) / mb_per_wg;
+  const dim3 grid(n_frames * b.wgs_per_frame), block(kReconThreads);
+  switch (k) {
+    case 0: hipLaunchKernelGGL(h264_recon_score<0>, grid, block, 0, s, b); break;
+    case 2: hipLaunchKernelGGL(h264_recon_score<2>, grid, block, 0, s, b); break;
+    case 4: hipLaunchKernelGGL(h264_recon_score<4>, grid, block, 0, s, b); break;
+    case 8: hipLaunchKernelGGL(h264_recon_score<8>, grid, block, 0, s, b); break;
+    default: return fail(VTS_E_INVALID, "fused path needs k in {0,2,4,8}");
+  }
   const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score launch: %s", hipGetErrorString(e));
   return VTS_OK;
+}
+
+int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s) {
+  if (t.n_frames <= 0) return VTS_OK;
+  hipLaunchKernelGGL(thumb_sad, dim3(static_cast<unsigned>(t.n_frames)), dim3(256), 0, s, t);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "thumb_sad launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
+int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s) {
+  FusedArgs f{};
+  f.r = a;
+  return fused_launch(f, 0, n_frames, s);
 }
 
 }  // namespace vts

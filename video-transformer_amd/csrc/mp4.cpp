@@ -130,6 +130,7 @@ std::string parse_stbl(const Box &stbl, Mp4VideoTrack *t) {
   Box b;
   // stsd -> first sample entry
   if (!find_child(stbl, fourcc("stsd"), &b) || b.n < 16) return "missing stsd";
+  t->stsd.assign(b.p - 8, b.p + b.n);  // 32-bit size header (box < 4 GiB)
   {
     const uint8_t *cur = b.p + 8, *end = b.p + b.n;
     Box entry;
@@ -240,13 +241,15 @@ std::string parse_trak(const Box &trak, Mp4Info *info) {
   Box mdia, hdlr, mdhd, minf, stbl, tkhd;
   if (!find_child(trak, fourcc("mdia"), &mdia)) return "";
   if (!find_child(mdia, fourcc("hdlr"), &hdlr) || hdlr.n < 12) return "";
-  if (rd32(hdlr.p + 8) != fourcc("vide")) return "";  // not a video track
   Mp4VideoTrack t;
+  t.handler = rd32(hdlr.p + 8);
+  t.hdlr.assign(hdlr.p - 8, hdlr.p + hdlr.n);
   if (find_child(trak, fourcc("tkhd"), &tkhd) && tkhd.n >= 84) {
     const int v = tkhd.p[0];
     // version/flags, times, track_ID, reserved, duration
     const size_t base = (v == 1) ? 36 : 24;
     t.track_id = rd32(tkhd.p + (v == 1 ? 20 : 12));
+    t.volume = static_cast<int16_t>(rd16(tkhd.p + base + 8 + 2 + 2));
     // reserved[2], layer, alternate_group, volume, reserved, matrix[9]
     const size_t wpos = base + 8 + 2 + 2 + 2 + 2 + 36;
     if (tkhd.n >= wpos + 8) {
@@ -263,6 +266,7 @@ std::string parse_trak(const Box &trak, Mp4Info *info) {
     t.timescale = rd32(mdhd.p + 12);
     t.duration = rd32(mdhd.p + 16);
   }
+  t.language = rd16(mdhd.p + (mdhd.p[0] == 1 ? 32 : 20));
   Box edts, elst;
   if (find_child(trak, fourcc("edts"), &edts) && find_child(edts, fourcc("elst"), &elst) &&
       elst.n >= 8) {
@@ -285,9 +289,17 @@ std::string parse_trak(const Box &trak, Mp4Info *info) {
   }
   if (!find_child(mdia, fourcc("minf"), &minf) || !find_child(minf, fourcc("stbl"), &stbl))
     return "missing stbl";
+  for (const char *mh : {"vmhd", "smhd", "nmhd", "sthd", "hmhd"}) {
+    Box h;
+    if (find_child(minf, fourcc(mh), &h)) {
+      t.media_header.assign(h.p - 8, h.p + h.n);
+      break;
+    }
+  }
   const std::string e = parse_stbl(stbl, &t);
   if (!e.empty()) return e;
-  info->video.push_back(std::move(t));
+  info->tracks.push_back(t);
+  if (t.handler == fourcc("vide")) info->video.push_back(std::move(t));
   return "";
 }
 

@@ -18,8 +18,14 @@ struct EditEntry {
   int64_t media_time;        // track timescale, -1 = empty edit
 };
 
-struct Mp4VideoTrack {
+struct Mp4VideoTrack {       // any track; `video` holds the 'vide' ones
   uint32_t track_id = 0;
+  uint32_t handler = 0;       // hdlr handler_type fourcc ('vide', 'soun', ...)
+  uint16_t language = 0x55c4; // mdhd packed ISO-639-2 ("und")
+  int16_t volume = 0;         // tkhd volume (8.8)
+  std::vector<uint8_t> stsd;  // the whole stsd box, copied verbatim on remux
+  std::vector<uint8_t> hdlr;  // the whole hdlr box
+  std::vector<uint8_t> media_header;  // vmhd / smhd / nmhd box (whole), if any
   int64_t timescale = 0;
   int64_t duration = 0;       // mdhd, track timescale
   int tkhd_width = 0, tkhd_height = 0;
@@ -43,6 +49,7 @@ struct Mp4Info {
   bool fragmented = false;   // moof/mvex present
   int64_t file_size = 0;
   std::vector<Mp4VideoTrack> video;
+  std::vector<Mp4VideoTrack> tracks;  // every track with a sample table, file order
 };
 
 // Parse the container from a file path or from memory. "" = ok, else error.
@@ -52,6 +59,14 @@ std::string mp4_parse_memory(const uint8_t *data, int64_t size, Mp4Info *out);
 // libavformat: s->duration = av_rescale(mvhd.duration, AV_TIME_BASE, timescale)
 // (round to nearest, ties away from zero); a timescale <= 0 reads as 1.
 int64_t mvhd_duration_us(const Mp4Info &info);
+
+// Stream-copy [start, end) seconds of every track into a new MP4 with moov
+// first (ffmpeg -ss S -i IN -t D -c copy -movflags +faststart):
+// each track starts at the last sync sample with pts <= start (pts/timescale
+// compared exactly), keeps samples with pts < end, and gets an edit list that
+// starts presentation at `start`.  "" = ok, else the reason.
+std::string mp4_remux_segment(const char *in_path, double start, double end,
+                              const char *out_path);
 
 // Streaming MP4 writer: ftyp, mdat (64-bit size), moov at the end.
 class Mp4Writer {

@@ -283,11 +283,11 @@ extern "C" int vts_plan_with_budget(double duration, const vts_budget_cfg *cfg,
 // ---------------------------------------------------------------------------
 // Segment time -> frame index, exact rational comparison pts/timescale >= t.
 // ---------------------------------------------------------------------------
-namespace {
+namespace vts {
 
 // Smallest integer q with q >= t * ts (exact), saturated to int64 bounds.
 // Returns +1/-1 in *sat when the exact value is above/below the int64 range.
-int64_t ceil_scaled(double t, int64_t ts, int *sat) {
+int64_t ceil_ticks(double t, int64_t ts, int *sat) {
   *sat = 0;
   if (t == 0.0) return 0;
   int exp = 0;
@@ -316,7 +316,7 @@ int64_t ceil_scaled(double t, int64_t ts, int *sat) {
   return static_cast<int64_t>(q);
 }
 
-}  // namespace
+}  // namespace vts
 
 extern "C" int vts_boundary_frames_pts(const int64_t *pts, int64_t n_frames,
                                        int64_t timescale, const double *times,
@@ -335,7 +335,7 @@ extern "C" int vts_boundary_frames_pts(const int64_t *pts, int64_t n_frames,
       idx = 0;
     } else {
       int sat = 0;
-      const int64_t thr = ceil_scaled(t, timescale, &sat);
+      const int64_t thr = vts::ceil_ticks(t, timescale, &sat);
       if (sat > 0) {
         idx = n_frames;
       } else if (sat < 0) {

@@ -29,6 +29,7 @@
 #include <cstdint>
 
 #include "common.h"
+#include "pixel.h"
 
 namespace vts {
 namespace {
@@ -46,10 +47,6 @@ struct Geo {
   static constexpr uint32_t kCDiv = kH * kH;
 };
 
-__device__ __forceinline__ uint32_t sad_u8(uint32_t a, uint32_t b, uint32_t acc) {
-  return __builtin_amdgcn_sad_u8(a, b, acc);
-}
-
 // Sum of bytes [b0, b1) of the word array w (compile-time bounds).
 template <int B0, int B1, int MASKSTEP = 1>
 __device__ __forceinline__ uint32_t byte_sum(const uint32_t *w, uint32_t acc) {
@@ -64,26 +61,6 @@ __device__ __forceinline__ uint32_t byte_sum(const uint32_t *w, uint32_t acc) {
     acc = sad_u8(w[wi] & m, 0u, acc);
   }
   return acc;
-}
-
-// clamp(floor(x / 256), 0, 255).  The shift is an opaque asm statement: for
-// the plain `clamp(x >> 8, 0, 255)` hipcc (ROCm 7.2) selects gfx950's
-// v_ashr_pk_u8_i32 for pairs of such values, and those bytes came out wrong
-// (saturated as if unshifted; caught by the bit-exact tests).
-__device__ __forceinline__ uint32_t shr8_sat(int x) {
-  int t;
-  asm("v_ashrrev_i32 %0, 8, %1" : "=v"(t) : "v"(x));
-  return static_cast<uint32_t>(t < 0 ? 0 : (t > 255 ? 255 : t));
-}
-
-// BT.709 limited range, 8-bit fixed point (x256); floor division by 256.
-__device__ __forceinline__ void bt709(uint32_t y, uint32_t u, uint32_t v, uint32_t *r,
-                                      uint32_t *g, uint32_t *b) {
-  const int c = static_cast<int>(y) - 16, d = static_cast<int>(u) - 128,
-            e = static_cast<int>(v) - 128;
-  *r = shr8_sat(298 * c + 459 * e + 128);
-  *g = shr8_sat(298 * c - 55 * d - 136 * e + 128);
-  *b = shr8_sat(298 * c + 541 * d + 128);
 }
 
 // Load kRowBytes of one row at `p` (16-byte aligned) as words.
@@ -226,9 +203,7 @@ __global__ void __launch_bounds__(kThreads, 2) score_runs(RunArgs a) {
         const uint32_t u = (us[p] + G::kCDiv / 2) / G::kCDiv;
         const uint32_t v = (vs[p] + G::kCDiv / 2) / G::kCDiv;
         yq[p] = y;
-        uint32_t r, g, b;
-        bt709(y, u, v, &r, &g, &b);
-        rgb24[p] = r | (g << 8) | (b << 16);
+        rgb24[p] = bt709_rgb24(y, u, v);
         atomicAdd(&lds_hist[y], 1u);
       }
       // --- SAD against the previous frame's thumbnail (thread-private LDS slot)
@@ -257,25 +232,7 @@ __global__ void __launch_bounds__(kThreads, 2) score_runs(RunArgs a) {
       // --- stores: RGB thumbnail, run head / tail thumbnails
       if (a.rgb) {
         uint8_t *dst = a.rgb + f * npx * 3 + tpx * 3;
-        // pack 24-bit pixels into words with shifts only (no byte arrays:
-        // byte-array packing miscompiled on gfx950 in an earlier version)
-        if constexpr (G::kG % 4 == 0) {
-          uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
-#pragma unroll
-          for (int q = 0; q < G::kG / 4; ++q) {
-            const uint32_t a0 = rgb24[4 * q], a1 = rgb24[4 * q + 1];
-            const uint32_t a2 = rgb24[4 * q + 2], a3 = rgb24[4 * q + 3];
-            d32[3 * q + 0] = a0 | (a1 << 24);
-            d32[3 * q + 1] = (a1 >> 8) | (a2 << 16);
-            d32[3 * q + 2] = (a2 >> 16) | (a3 << 8);
-          }
-        } else {  // G == 2: 6 bytes, 2-byte aligned
-          uint16_t *d16 = reinterpret_cast<uint16_t *>(dst);
-          const uint32_t a0 = rgb24[0], a1 = rgb24[1];
-          d16[0] = static_cast<uint16_t>(a0 & 0xffffu);
-          d16[1] = static_cast<uint16_t>((a0 >> 16) | ((a1 & 0xffu) << 8));
-          d16[2] = static_cast<uint16_t>(a1 >> 8);
-        }
+        store_rgb<G::kG>(dst, rgb24);
       }
       if (f == f0 && !seeded) {
         uint8_t *dst = a.head + static_cast<int64_t>(run) * npx + tpx;

@@ -87,6 +87,8 @@ struct vts_ctx {
   uint64_t *d_sad = nullptr;
   uint32_t *d_hist = nullptr;
   uint8_t *d_rgb = nullptr;       // RGB thumbnails of every frame
+  bool fused = false;             // scoring fused into reconstruction
+  uint8_t *d_thumb[2] = {nullptr, nullptr};  // fused: [slot][h][w] thumbnail luma
   int64_t thumb_px = 0;
   hipStream_t s_dec = nullptr, s_score = nullptr;
   std::vector<hipEvent_t> ev;  // per window: dec0, dec1, sc0, sc1
@@ -152,6 +154,13 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   c->pitch = c->coded_w;
   c->frame_stride = (static_cast<int64_t>(c->pitch) * c->coded_h * 3 / 2 + 4095) & ~int64_t(4095);
   c->k = c->params.k > 0 ? c->params.k : (c->height <= 720 ? 4 : 6);
+  {
+    const bool can_fuse = (c->k == 2 || c->k == 4 || c->k == 8) && c->width == c->coded_w &&
+                          c->height == c->coded_h;
+    if (c->params.fused > 0 && !can_fuse)
+      return fail(VTS_E_UNSUPPORTED, "fused scoring needs k in {2,4,8} and no cropping");
+    c->fused = can_fuse && c->params.fused >= 0;
+  }
   c->n_frames = static_cast<int64_t>(t.size.size());
   if (c->n_frames == 0) return fail(VTS_E_FORMAT, "video track has no samples");
 
@@ -297,6 +306,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
     HIP_TRY(hipMalloc(&c->d_cmd[r], static_cast<size_t>(c->ring_frames * nmb * 8)));
     HIP_TRY(hipMalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
     HIP_TRY(hipMalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
+    if (c->fused) HIP_TRY(hipMalloc(&c->d_thumb[r], static_cast<size_t>(c->ring_frames * tw + kPad)));
   }
   for (int r = 0; r < 2; ++r) HIP_TRY(hipMalloc(&c->d_last[r], static_cast<size_t>(tw + kPad)));
   HIP_TRY(hipMalloc(&c->d_err, sizeof(uint32_t)));
@@ -378,31 +388,64 @@ int run_all(vts_ctx *c) {
     ra.mb_width = c->sps.mb_width;
     ra.mb_height = c->sps.mb_height;
     ra.err = c->d_err;
-    for (size_t l = 0; l < w.lvl_off.size(); ++l) {
-      ra.frames = c->d_levels + w.lvl_off[l];
-      VTS_TRY(recon_launch(ra, w.lvl_cnt[l], sd));
+    const int tw = c->width / c->k, th = c->height / c->k;
+    if (c->fused) {
+      HIP_TRY(hipMemsetAsync(c->d_hist + w.f0 * 256, 0,
+                             sizeof(uint32_t) * 256 * static_cast<size_t>(w.f1 - w.f0), sd));
+      FusedArgs fa{};
+      fa.r = ra;
+      fa.frame0 = w.f0;
+      fa.w = tw;
+      fa.h = th;
+      fa.wgs_per_frame = static_cast<int32_t>((nmb + 255) / 256);
+      fa.thumb = c->d_thumb[r];
+      fa.rgb = c->d_rgb;
+      fa.hist = c->d_hist;
+      for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+        fa.r.frames = c->d_levels + w.lvl_off[l];
+        VTS_TRY(fused_launch(fa, c->k, w.lvl_cnt[l], sd));
+      }
+    } else {
+      for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+        ra.frames = c->d_levels + w.lvl_off[l];
+        VTS_TRY(recon_launch(ra, w.lvl_cnt[l], sd));
+      }
     }
     HIP_TRY(hipEventRecord(E[2], sd));
     HIP_TRY(hipStreamWaitEvent(ss, E[2], 0));
     HIP_TRY(hipEventRecord(E[3], ss));
-    vts_score_desc d{};
-    d.nv12 = c->d_surf[r];
-    d.frame_stride = c->frame_stride;
-    d.n_frames = w.f1 - w.f0;
-    d.width = c->width;
-    d.height = c->height;
-    d.pitch = c->pitch;
-    d.uv_row_offset = c->coded_h;
-    d.k = c->k;
-    d.rgb = c->d_rgb + 3 * c->thumb_px * w.f0;
-    d.hist = c->d_hist + w.f0 * 256;
-    d.sad = c->d_sad + w.f0;
-    d.score = c->d_score + w.f0;
-    d.prev_luma = wi > 0 ? c->d_last[(wi - 1) & 1] : nullptr;
-    d.last_luma = c->d_last[wi & 1];
-    d.workspace = c->d_ws[r];
-    d.workspace_bytes = c->ws_bytes;
-    VTS_TRY(score_launch(&d, ss));
+    if (c->fused) {
+      ThumbSadArgs t{};
+      t.thumb = c->d_thumb[r];
+      t.prev_luma = wi > 0 ? c->d_last[(wi - 1) & 1] : nullptr;
+      t.last_luma = c->d_last[wi & 1];
+      t.frame0 = w.f0;
+      t.n_frames = w.f1 - w.f0;
+      t.w = tw;
+      t.h = th;
+      t.sad = c->d_sad;
+      t.score = c->d_score;
+      VTS_TRY(thumb_sad_launch(t, ss));
+    } else {
+      vts_score_desc d{};
+      d.nv12 = c->d_surf[r];
+      d.frame_stride = c->frame_stride;
+      d.n_frames = w.f1 - w.f0;
+      d.width = c->width;
+      d.height = c->height;
+      d.pitch = c->pitch;
+      d.uv_row_offset = c->coded_h;
+      d.k = c->k;
+      d.rgb = c->d_rgb + 3 * c->thumb_px * w.f0;
+      d.hist = c->d_hist + w.f0 * 256;
+      d.sad = c->d_sad + w.f0;
+      d.score = c->d_score + w.f0;
+      d.prev_luma = wi > 0 ? c->d_last[(wi - 1) & 1] : nullptr;
+      d.last_luma = c->d_last[wi & 1];
+      d.workspace = c->d_ws[r];
+      d.workspace_bytes = c->ws_bytes;
+      VTS_TRY(score_launch(&d, ss));
+    }
     HIP_TRY(hipEventRecord(E[4], ss));
   }
   HIP_TRY(hipStreamWaitEvent(sd, c->ev[(nw - 1) * 6 + 4], 0));
@@ -577,6 +620,7 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
     case 1: return static_cast<int64_t>(c->windows.size());
     case 2: return static_cast<int64_t>(c->slices.size());
     case 3: return c->ring_frames;
+    case 4: return c->fused ? 1 : 0;
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
   }
 }
@@ -597,6 +641,7 @@ extern "C" int vts_close(vts_ctx *c) {
     f(c->d_surf[r]);
     f(c->d_ws[r]);
     f(c->d_last[r]);
+    f(c->d_thumb[r]);
   }
   f(c->d_err);
   f(c->d_score);

@@ -105,7 +105,7 @@ class VideoScorer:
 
     def __init__(self, path: str | Path, device: int = 0, *, k: int = 0,
                  window_frames: int = 0, n_streams: int = 2,
-                 cut_threshold: float = DEFAULT_CUT_THRESHOLD):
+                 cut_threshold: float = DEFAULT_CUT_THRESHOLD, fused: int = 0):
         self._lib = _lib.lib()
         prm = _lib.Params()
         prm.k = k
@@ -113,6 +113,7 @@ class VideoScorer:
         prm.keep_rgb = 0
         prm.n_streams = n_streams
         prm.cut_threshold = cut_threshold
+        prm.fused = fused
         ctx = C.c_void_p()
         _lib.check(self._lib.vts_open(int(device), str(path).encode(), C.byref(prm),
                                       C.byref(ctx)))
@@ -153,6 +154,10 @@ class VideoScorer:
     def recon_launches(self) -> int:
         """Reconstruct launches per run (one per GOP level per window)."""
         return int(self._lib.vts_schedule_info(self._ctx, 0))
+
+    def fused(self) -> bool:
+        """Scoring runs fused into reconstruction (k in {2,4,8}, no crop)."""
+        return bool(self._lib.vts_schedule_info(self._ctx, 4))
 
     def boundary_frames(self, times) -> list[int]:
         arr = (C.c_double * len(times))(*[float(t) for t in times])
