@@ -14,6 +14,7 @@
  *   vts_plan_with_budget   utils/budget_planner.py:73-194   plan_segments_with_budget
  *   vts_probe_duration     utils/video_utils.py:7-38        probe_duration (ffprobe format=duration)
  *   vts_probe_info         utils/video_utils.py:7-38        (same probe, all stream facts)
+ *   vts_extract_segment    utils/video_segmenter.py:86-154  extract_segment (ffmpeg -c copy)
  *   vts_boundary_frames*   (no reference code; video_segmenter.py:157-159 snap_to_keyframe
  *                          is the identity stub this feeds)  segment time -> frame index
  *   vts_open/vts_score/... (no reference code; north_star)   decode + NV12 scene scoring
@@ -143,6 +144,13 @@ int vts_probe_duration(const char *path, double *seconds);
 
 /* All container facts of the first video track. Returns < 0 on error. */
 int vts_probe_info(const char *path, vts_video_info *info);
+
+/* extract_segment stream copy (video_segmenter.py:86-154, the `-c copy`
+ * branch) for ISO-BMFF input: every track from the sync sample at or before
+ * `start` to the last sample presented before `end`, an edit list starting
+ * presentation at `start`, moov before mdat (+faststart).  0 = ok. */
+int vts_extract_segment(const char *in_path, double start, double end,
+                        const char *out_path);
 
 /* ------------------------------------------------- device scoring kernel */
 

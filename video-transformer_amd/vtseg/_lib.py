@@ -116,6 +116,7 @@ SIGNATURES: dict[str, tuple] = {
                                           _P(C.c_double), C.c_int64, _P(C.c_int64)]),
     "vts_probe_duration": (C.c_int, [C.c_char_p, _P(C.c_double)]),
     "vts_probe_info": (C.c_int, [C.c_char_p, _P(VideoInfo)]),
+    "vts_extract_segment": (C.c_int, [C.c_char_p, C.c_double, C.c_double, C.c_char_p]),
     "vts_score_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int64]),
     "vts_score_nv12_dev": (C.c_int, [_P(ScoreDesc), C.c_void_p]),
     "vts_open": (C.c_int, [C.c_int, C.c_char_p, _P(Params), _P(C.c_void_p)]),

@@ -29,6 +29,7 @@ from pathlib import Path
 from typing import TypedDict, cast
 
 from . import _lib
+from .video_utils import _is_isobmff
 
 
 @dataclass(frozen=True)
@@ -121,11 +122,13 @@ def extract_segment(
 ) -> bool:
     """Cut [start, end] into output_path (video_segmenter.py:86-154).
 
-    Same contract as the reference: ``ffmpeg -ss S -i IN -t D -movflags
-    +faststart -c copy OUT`` with an x264/AAC re-encode fallback, ``%.3f``
-    timestamps, 120 s timeout, never raises, False on any failure, a failed
-    copy's partial output is unlinked.  (A native MP4 stream-copy remuxer is
-    the next item on this path)
+    Same contract as the reference: never raises, False on any failure, a
+    failed copy's partial output is unlinked, copy first then re-encode.  The
+    stream copy of ISO-BMFF input is native (``vts_extract_segment``: from
+    the keyframe at or before ``start``, moov first, like ``ffmpeg -ss S -i IN
+    -t D -movflags +faststart -c copy``); other containers, a failed native
+    copy and the re-encode fallback run the reference's ffmpeg commands
+    (``%.3f`` timestamps, 120 s timeout).
     """
     duration = end - start
     if duration <= 0:
@@ -142,6 +145,18 @@ def extract_segment(
             return False
         return (proc.returncode == 0 and output_path.exists()
                 and output_path.stat().st_size > 0)
+
+    if stream_copy:
+        if _is_isobmff(input_path):
+            try:
+                rc = _lib.lib().vts_extract_segment(str(input_path).encode(), float(start),
+                                                    float(end), str(output_path).encode())
+            except (TypeError, ValueError):
+                rc = -1
+            if rc == 0 and output_path.exists() and output_path.stat().st_size > 0:
+                return True
+            if output_path.exists():
+                output_path.unlink()
 
     head = ["ffmpeg", "-y", "-hide_banner", "-loglevel", "error",
             "-ss", f"{start:.3f}", "-i", str(input_path),
