@@ -94,6 +94,8 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gops-per-launch", type=int, default=0,
+                    help="0 auto (Infinity-Cache sized), -1 all GOPs per launch")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with several ranks on one GPU")
     args = ap.parse_args()
@@ -147,7 +149,7 @@ def main() -> None:
         path = Path(tmpdir) / f"synth_rank{rank}.mp4"
         scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
                           seed=0x5EED + rank)
-        scorer = scene.VideoScorer(path, device=gpu)
+        scorer = scene.VideoScorer(path, device=gpu, gops_per_launch=args.gops_per_launch)
         duration_s = float(scorer.info.duration)
 
         def step():
@@ -268,6 +270,7 @@ def main() -> None:
         }
         if scorer is not None:
             line["config"]["stage_ms"] = scorer.timings()
+            line["config"]["recon_launches"] = scorer.recon_launches()
         print(json.dumps(line), flush=True)
     if scorer is not None:
         scorer.close()

@@ -153,3 +153,17 @@ def test_fused_windowed_pipeline(tmp_path):
         part = b.score()
     assert np.array_equal(part.scores, whole.scores)
     assert np.array_equal(part.hist, whole.hist)
+
+
+@pytest.mark.parametrize("gops", [1, 3, -1])
+def test_gop_grouped_schedule_equals_all_at_once(tmp_path, gops):
+    _require_gpu()
+    path = tmp_path / "g.mp4"
+    scene.synth_write(path, width=320, height=240, n_frames=240, cut_min_s=0.8, cut_max_s=2,
+                      gop_max_s=0.4)
+    frames, _ = oracle.decode_file(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, 240, 320, 240, 320, 240, 4)
+    with scene.VideoScorer(path, gops_per_launch=gops) as v:
+        res = v.score()
+        assert np.array_equal(v.frame_nv12(239).reshape(frames[-1].shape), frames[-1])
+    assert np.array_equal(res.scores, ref["score"]) and np.array_equal(res.hist, ref["hist"])

@@ -64,9 +64,9 @@ struct DevBits {
     if (blk != cache_at) {
       // 16-byte aligned within the payload is not 16-byte aligned in memory;
       // load the enclosing aligned dwords instead.
-      const uintptr_t a = reinterpret_cast<uintptr_t>(base + blk);
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-      const int sh = static_cast<int>(a & 3);
+      const uint8_t *pb = base + blk;
+      const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pb) & 3);
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(pb - sh);  // global, not flat
       uint32_t t[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) t[k] = w[k];
@@ -344,9 +344,8 @@ __global__ void __launch_bounds__(64) h264_parse(ParseArgs a) {
 // across lanes) and a funnel shift in registers.  Reads up to 15 bytes past
 // the 16 requested (buffers carry >= 32 bytes of padding).
 __device__ __forceinline__ uint4 load16_any(const uint8_t *p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint4 *q = reinterpret_cast<const uint4 *>(a & ~uintptr_t(15));
-  const int sh = static_cast<int>(a & 15);
+  const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+  const uint4 *q = reinterpret_cast<const uint4 *>(p - sh);  // stays a global pointer
   const uint4 lo = q[0];
   if (sh == 0) return lo;
   const uint4 hi = q[1];
@@ -523,10 +522,53 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score(FusedArgs fa) 
     uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
     uint8_t *dst_uv = dst + F.pitch * F.H;
     uint4 yr[KK], cr[HK];
+    const uint32_t kind = static_cast<uint32_t>(c >> 62);
+    const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+    const int sx = m * 16 + (mvx >> 2), cx = m * 8 + (mvx >> 3);
+    // fast path: inter, integer-pel chroma, source rows inside the picture
+    // horizontally (vertical clamping is folded into the row index)
+    const bool fast = kind == 2 && F.ref && ((mvx | mvy) & 7) == 0 && sx >= 0 &&
+                      sx + 15 <= F.W - 1 && cx >= 0 && cx + 7 <= F.CW - 1;
+    if (fast) {
+      // every aligned 16-byte load is issued before any is used
+      uint4 lo[KK + HK], hi[KK + HK];
+      int shf[KK + HK];
 #pragma unroll
-    for (int rr = 0; rr < KK; ++rr) yr[rr] = fetch_row(F, c, q * KK + rr, m, mby, errs);
+      for (int i = 0; i < KK + HK; ++i) {
+        const uint8_t *p;
+        if (i < KK) {
+          const int y = clampi(mby * 16 + q * KK + i + (mvy >> 2), 0, F.H - 1);
+          p = F.ref + y * F.pitch + sx;
+        } else {
+          const int y = clampi(mby * 8 + q * HK + (i - KK) + (mvy >> 3), 0, F.CH - 1);
+          p = F.ref_uv + y * F.pitch + 2 * cx;
+        }
+        // pointer arithmetic (not an integer round trip) keeps the global
+        // address space, so these are global_load_dwordx4, not flat loads
+        const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+        const uint4 *al = reinterpret_cast<const uint4 *>(p - sh);
+        shf[i] = sh;
+        lo[i] = al[0];
+        hi[i] = al[1];
+      }
 #pragma unroll
-    for (int rr = 0; rr < HK; ++rr) cr[rr] = fetch_row(F, c, 16 + q * HK + rr, m, mby, errs);
+      for (int i = 0; i < KK + HK; ++i) {
+        const uint32_t w[8] = {lo[i].x, lo[i].y, lo[i].z, lo[i].w, hi[i].x, hi[i].y, hi[i].z, hi[i].w};
+        const int qd = shf[i] >> 2, r = shf[i] & 3;
+        uint32_t t[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          t[j] = (qd == 0) ? w[j] : (qd == 1) ? w[j + 1] : (qd == 2) ? w[j + 2] : w[j + 3 < 8 ? j + 3 : 7];
+        const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                                   __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+        if (i < KK) yr[i] = v; else cr[i - KK] = v;
+      }
+    } else {
+#pragma unroll
+      for (int rr = 0; rr < KK; ++rr) yr[rr] = fetch_row(F, c, q * KK + rr, m, mby, errs);
+#pragma unroll
+      for (int rr = 0; rr < HK; ++rr) cr[rr] = fetch_row(F, c, 16 + q * HK + rr, m, mby, errs);
+    }
 #pragma unroll
     for (int rr = 0; rr < KK; ++rr)
       *reinterpret_cast<uint4 *>(dst + (mby * 16 + q * KK + rr) * F.pitch + m * 16) = yr[rr];

@@ -38,6 +38,7 @@ namespace {
 constexpr int64_t kSingleWindowBytes = 48ll << 30;  // up to 48 GiB decoded: one window
 constexpr int64_t kRingBytes = 8ll << 30;           // else 8 GiB rings (x2)
 constexpr int64_t kPad = 256;
+constexpr int64_t kLaunchBytes = 96ll << 20;         // decoded bytes per launch (auto)
 
 #define HIP_TRY(expr)                                                              \
   do {                                                                             \
@@ -276,17 +277,38 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
         c->slices[s].ref_slot = ref[x] >= 0 ? static_cast<int32_t>(ref[x] - w.f0) : -1;
       }
     }
-    // levels relative to the window (intra frames restart at 0)
-    std::vector<std::vector<int2>> lv(static_cast<size_t>(maxl + 1));
+    // GOPs (runs starting at an intra frame) of this window, grouped so a
+    // reconstruct launch writes ~kLaunchBytes: the next level of the same group
+    // then reads its references from the Infinity Cache instead of HBM.
+    std::vector<int64_t> gop_start;
     for (int64_t x = w.f0; x < w.f1; ++x)
-      lv[level[x]].push_back(make_int2(static_cast<int>(x - w.f0),
-                                       ref[x] >= 0 ? static_cast<int>(ref[x] - w.f0) : -1));
-    for (auto &l : lv) {
-      if (l.empty()) continue;
-      w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
-      w.lvl_cnt.push_back(static_cast<int32_t>(l.size()));
-      c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
+      if (intra[x] || x == w.f0) gop_start.push_back(x);
+    int64_t per;
+    if (c->params.gops_per_launch < 0) {
+      per = static_cast<int64_t>(gop_start.size());
+    } else if (c->params.gops_per_launch > 0) {
+      per = c->params.gops_per_launch;
+    } else {
+      per = std::max<int64_t>(1, kLaunchBytes / c->frame_stride);
     }
+    for (size_t g0 = 0; g0 < gop_start.size(); g0 += static_cast<size_t>(per)) {
+      const size_t g1 = std::min(gop_start.size(), g0 + static_cast<size_t>(per));
+      const int64_t a = gop_start[g0];
+      const int64_t b = (g1 < gop_start.size()) ? gop_start[g1] : w.f1;
+      int64_t gmax = 0;
+      for (int64_t x = a; x < b; ++x) gmax = std::max(gmax, level[x]);
+      std::vector<std::vector<int2>> lv(static_cast<size_t>(gmax + 1));
+      for (int64_t x = a; x < b; ++x)
+        lv[level[x]].push_back(make_int2(static_cast<int>(x - w.f0),
+                                         ref[x] >= 0 ? static_cast<int>(ref[x] - w.f0) : -1));
+      for (auto &l : lv) {
+        if (l.empty()) continue;
+        w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
+        w.lvl_cnt.push_back(static_cast<int32_t>(l.size()));
+        c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
+      }
+    }
+    (void)maxl;
   }
 
   // ---- device allocations and uploads
