@@ -204,9 +204,7 @@ typedef struct vts_params {
   int32_t fused;           /* 0 auto, 1 require, -1 never: fuse scoring into
                               reconstruction (k in {2,4,8}, no cropping)       */
   int32_t gops_per_launch; /* GOPs decoded together per reconstruct launch;
-                              0 = auto (keep a launch's output near the 256 MiB
-                              Infinity Cache so the next level's reference
-                              reads hit it), < 0 = all GOPs of the window     */
+                              <= 0 = all GOPs of the window (fastest measured) */
   int32_t _pad;
 } vts_params;
 

@@ -287,6 +287,41 @@ __global__ void __launch_bounds__(64) h264_parse(ParseArgs a) {
       if (skip > 0) more = br.bit_index() < stop_bit;
       if (!more || addr >= nmb) break;
     }
+    // ---- I_PCM run speculation: in an I slice, once byte-aligned after an
+    // I_PCM macroblock, the next headers sit at a 386-byte stride (mb_type 25
+    // = 9 bits + 7 alignment zeros = 0x0D 0x00, then 384 samples).  Load up to
+    // 8 predicted headers at once, verify them in order, commit the matching
+    // prefix; anything unexpected falls through to the serial parse below.
+    if (!is_p && br.bitpos == 0 && addr > first_mb) {
+      uint32_t hb0[8], hb1[8];
+      int cand = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t q = static_cast<int64_t>(br.pos) + 386 * j;
+        if ((q + 386) * 8 <= stop_bit && addr + j < nmb) {
+          hb0[j] = nal[1 + q];
+          hb1[j] = nal[2 + q];
+          cand = j + 1;
+        }
+      }
+      int ok = 0;
+      for (int j = 0; j < cand; ++j) {
+        if (hb0[j] != 0x0D || hb1[j] != 0x00) break;
+        ok = j + 1;
+      }
+      if (ok > 0 && br.zeros < 2) {
+        for (int j = 0; j < ok; ++j)
+          cmd[addr + j] = MB_PCM | static_cast<uint64_t>(br.abs0 + br.pos + 386 * j + 2);
+        addr += ok;
+        left = Nb{true, -1, 0, 0};
+        br.pos += 386 * ok;
+        br.zeros = 0;
+        const uint32_t b1 = br.byte_at(br.pos - 1), b2 = br.byte_at(br.pos - 2);
+        br.zeros = (b1 != 0) ? 0 : ((b2 != 0) ? 1 : 2);
+        more = br.bit_index() < stop_bit;
+        continue;
+      }
+    }
     // ---- macroblock_layer (7.3.5)
     const int mb_type = static_cast<int>(br.ue());
     const int x = addr % mbw, y = addr / mbw;

@@ -38,7 +38,6 @@ namespace {
 constexpr int64_t kSingleWindowBytes = 48ll << 30;  // up to 48 GiB decoded: one window
 constexpr int64_t kRingBytes = 8ll << 30;           // else 8 GiB rings (x2)
 constexpr int64_t kPad = 256;
-constexpr int64_t kLaunchBytes = 96ll << 20;         // decoded bytes per launch (auto)
 
 #define HIP_TRY(expr)                                                              \
   do {                                                                             \
@@ -277,9 +276,12 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
         c->slices[s].ref_slot = ref[x] >= 0 ? static_cast<int32_t>(ref[x] - w.f0) : -1;
       }
     }
-    // GOPs (runs starting at an intra frame) of this window, grouped so a
-    // reconstruct launch writes ~kLaunchBytes: the next level of the same group
-    // then reads its references from the Infinity Cache instead of HBM.
+    // GOPs (runs starting at an intra frame) of this window.  Default: every
+    // GOP of the window in each level launch.  Grouping GOPs so a launch's
+    // output fits the 256 MiB Infinity Cache (the next level's reference reads
+    // would hit it) measured slower at every group size on MI355X (the kernel
+    // is latency-bound and needs the full launch width):
+    // profiles/r01_gop_group_sweep.txt.
     std::vector<int64_t> gop_start;
     for (int64_t x = w.f0; x < w.f1; ++x)
       if (intra[x] || x == w.f0) gop_start.push_back(x);
@@ -289,7 +291,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
     } else if (c->params.gops_per_launch > 0) {
       per = c->params.gops_per_launch;
     } else {
-      per = std::max<int64_t>(1, kLaunchBytes / c->frame_stride);
+      per = static_cast<int64_t>(gop_start.size());
     }
     for (size_t g0 = 0; g0 < gop_start.size(); g0 += static_cast<size_t>(per)) {
       const size_t g1 = std::min(gop_start.size(), g0 + static_cast<size_t>(per));
