@@ -57,3 +57,48 @@ def test_two_rank_batch_equals_serial(tmp_path, n_videos):
     assert [t[:5] for t in r0] == serial
     assert [t[5] for t in r0] == [i % 2 for i in range(n_videos)]
     assert [t[2] for t in r0] == [(300 + 150 * i) / 30 for i in range(n_videos)]
+
+
+def _exchange_worker(rank, world, port, out_dir):
+    sys.path[:0] = [str(ROOT / "video-transformer_amd")]
+    import torch
+    import torch.distributed as dist
+    from vtseg.batch import exchange_boundaries
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    # 3 videos per rank; rank r video j has j+1 segments and (r + 2j) % 4 cuts
+    per = 3
+    recs = torch.zeros((world, per, 3), dtype=torch.int64)
+    for r in range(world):
+        for j in range(per):
+            recs[r, j, 0] = j + 1
+            recs[r, j, 1] = (r + 2 * j) % 4
+    seg, cut, tim = [], [], []
+    for j in range(per):
+        ns, nc = j + 1, (rank + 2 * j) % 4
+        seg.append([100 * rank + 10 * j + t for t in range(2 * ns)])
+        cut.append([1000 * rank + 7 * j + t for t in range(nc)])
+        tim.append([0.5 * rank + j + t / 3 for t in range(nc)])
+    out = exchange_boundaries(recs, seg, cut, tim)
+    (Path(out_dir) / f"x{rank}.txt").write_text(repr(out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_boundary_exchange(tmp_path):
+    """Second all-gather: ragged per-video boundary arrays,
+    padded to the batch maximum, arrive intact on every rank."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_exchange_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2,
+                       join=True, start_method="spawn")
+    x0 = eval((tmp_path / "x0.txt").read_text())
+    x1 = eval((tmp_path / "x1.txt").read_text())
+    assert x0 == x1
+    for r in range(2):
+        for j in range(3):
+            ns, nc = j + 1, (r + 2 * j) % 4
+            seg = [100 * r + 10 * j + t for t in range(2 * ns)]
+            sf, cf, ct = x0[r][j]
+            assert sf == tuple((seg[2 * s], seg[2 * s + 1]) for s in range(ns))
+            assert cf == tuple(1000 * r + 7 * j + t for t in range(nc))
+            assert ct == tuple(0.5 * r + j + t / 3 for t in range(nc))

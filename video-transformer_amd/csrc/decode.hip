@@ -410,6 +410,16 @@ __device__ bool epb_in_pcm(const uint8_t *chunk, int n, const uint8_t *pcm) {
   return false;
 }
 
+// DEC_E_EPB_IN_PCM if an emulation-prevention byte falls inside the rows
+// of group q (kk luma rows, hk chroma rows of each plane) of an I_PCM block.
+__device__ __noinline__ uint32_t pcm_rows_epb(const uint8_t *pcm, int q, int kk, int hk) {
+  bool bad = false;
+  for (int i = 0; i < kk; ++i) bad |= epb_in_pcm(pcm + 16 * (q * kk + i), 16, pcm);
+  for (int i = 0; i < hk; ++i)
+    bad |= epb_in_pcm(pcm + 256 + 8 * (q * hk + i), 8, pcm) || epb_in_pcm(pcm + 320 + 8 * (q * hk + i), 8, pcm);
+  return bad ? DEC_E_EPB_IN_PCM : 0u;
+}
+
 // interleave 8 Cb and 8 Cr bytes into 16 NV12 bytes (u0 v0 u1 v1 ...)
 __device__ __forceinline__ uint4 interleave_uv(uint32_t u0, uint32_t u1, uint32_t v0, uint32_t v1) {
   // v_perm_b32 selector: bytes of {src0, src1} = {hi word, lo word}
@@ -421,6 +431,32 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 constexpr int kReconThreads = 256;
 
+#ifndef VTS_NT_LOAD
+#define VTS_NT_LOAD 0
+#endif
+#ifndef VTS_NT_STORE
+#define VTS_NT_STORE 0
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte row load / store of the fused kernel's streams (optionally
+// nontemporal: every reference row is read once, every output row written once)
+__device__ __forceinline__ uint4 ld_row(const uint4 *p) {
+#if VTS_NT_LOAD
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_row(uint8_t *p, const uint4 v) {
+#if VTS_NT_STORE
+  __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(p));
+#else
+  *reinterpret_cast<uint4 *>(p) = v;
+#endif
+}
+
 struct FrameRefs {
   const uint8_t *es;
   const uint8_t *ref, *ref_uv;  // reference picture (nullptr for none)
@@ -430,6 +466,9 @@ struct FrameRefs {
 
 // The 16 output bytes of row r (0..15 luma, 16..23 chroma NV12) of macroblock
 // (m, mby) whose command is c.  errs collects DEC_E_* bits.
+// General (slow) path: sub-pel chroma, edge clamping, error cases.  Inlined:
+// as an out-of-line call it made every wave of the fused kernel set up
+// scratch and the whole decode measured 25% slower.
 __device__ __forceinline__ uint4 fetch_row(const FrameRefs &F, uint64_t c, int r, int m, int mby,
                                            uint32_t &errs) {
   const uint32_t kind = static_cast<uint32_t>(c >> 62);
@@ -530,8 +569,17 @@ __device__ __forceinline__ FrameRefs frame_refs(const ReconArgs &a, int ref_slot
 // Y'U'V' -> BT.709 RGB, thumbnail luma for the SAD pass, and an LDS
 // histogram flushed once per workgroup with global atomics.  The decoded
 // frame is never re-read for scoring.
+#ifndef VTS_WAVES_PER_EU
+#define VTS_WAVES_PER_EU 0
+#endif
+#if VTS_WAVES_PER_EU
+#define VTS_OCCUPANCY __attribute__((amdgpu_waves_per_eu(K == 8 ? 1 : VTS_WAVES_PER_EU)))
+#else
+#define VTS_OCCUPANCY
+#endif
+
 template <int K>
-__global__ void __launch_bounds__(kReconThreads) h264_recon_score(FusedArgs fa) {
+__global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(FusedArgs fa) {
   constexpr int KK = K ? K : 4;      // rows per group
   constexpr int Q = 16 / KK;         // groups per macroblock
   constexpr int G = 16 / KK;         // thumbnail pixels per group row
@@ -546,6 +594,8 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score(FusedArgs fa) 
   const int2 fr = a.frames[fi];
   const FrameRefs F = frame_refs(a, fr.y);
   const int64_t gframe = fa.frame0 + fr.x;
+  // the command load is in flight across the histogram-clearing barrier
+  const uint64_t c = mb < nmb ? a.cmd[static_cast<int64_t>(fr.x) * nmb + mb] : 0;
   if constexpr (K != 0) {
     lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
     __syncthreads();
@@ -553,51 +603,80 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score(FusedArgs fa) 
   uint32_t errs = 0;
   if (mb < nmb) {
     const int mby = mb / mbw, m = mb - mby * mbw;
-    const uint64_t c = a.cmd[static_cast<int64_t>(fr.x) * nmb + mb];
     uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
     uint8_t *dst_uv = dst + F.pitch * F.H;
     uint4 yr[KK], cr[HK];
     const uint32_t kind = static_cast<uint32_t>(c >> 62);
     const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
     const int sx = m * 16 + (mvx >> 2), cx = m * 8 + (mvx >> 3);
-    // fast path: inter, integer-pel chroma, source rows inside the picture
-    // horizontally (vertical clamping is folded into the row index)
-    const bool fast = kind == 2 && F.ref && ((mvx | mvy) & 7) == 0 && sx >= 0 &&
-                      sx + 15 <= F.W - 1 && cx >= 0 && cx + 7 <= F.CW - 1;
+    const bool pcm = kind == 1;
+    // fast paths: I_PCM, and inter with integer-pel chroma whose source rows
+    // lie inside the picture horizontally (vertical clamping is folded into
+    // the row index)
+    const bool fast = pcm || (kind == 2 && F.ref && ((mvx | mvy) & 7) == 0 && sx >= 0 &&
+                              sx + 15 <= F.W - 1 && cx >= 0 && cx + 7 <= F.CW - 1);
     if (fast) {
-      // every aligned 16-byte load is issued before any is used
+      // every aligned load is issued before any is used: 16-byte pairs for
+      // luma / NV12 rows, 8-byte pairs of the planar Cb and Cr rows of I_PCM
+      const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
       uint4 lo[KK + HK], hi[KK + HK];
       int shf[KK + HK];
 #pragma unroll
       for (int i = 0; i < KK + HK; ++i) {
-        const uint8_t *p;
-        if (i < KK) {
-          const int y = clampi(mby * 16 + q * KK + i + (mvy >> 2), 0, F.H - 1);
-          p = F.ref + y * F.pitch + sx;
+        if (pcm && i >= KK) {
+          const uint8_t *pu = pcmb + 256 + 8 * (q * HK + (i - KK));  // Cr row is 64 B on
+          const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pu) & 7);
+          const uint2 *au = reinterpret_cast<const uint2 *>(pu - sh);
+          const uint2 u0 = au[0], u1 = au[1], v0 = au[8], v1 = au[9];
+          shf[i] = sh;
+          lo[i] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+          hi[i] = make_uint4(v0.x, v0.y, v1.x, v1.y);
         } else {
-          const int y = clampi(mby * 8 + q * HK + (i - KK) + (mvy >> 3), 0, F.CH - 1);
-          p = F.ref_uv + y * F.pitch + 2 * cx;
+          const uint8_t *p;
+          if (pcm) {
+            p = pcmb + 16 * (q * KK + i);
+          } else if (i < KK) {
+            const int y = clampi(mby * 16 + q * KK + i + (mvy >> 2), 0, F.H - 1);
+            p = F.ref + y * F.pitch + sx;
+          } else {
+            const int y = clampi(mby * 8 + q * HK + (i - KK) + (mvy >> 3), 0, F.CH - 1);
+            p = F.ref_uv + y * F.pitch + 2 * cx;
+          }
+          // pointer arithmetic (not an integer round trip) keeps the global
+          // address space, so these are global_load_dwordx4, not flat loads
+          const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+          const uint4 *al = reinterpret_cast<const uint4 *>(p - sh);
+          shf[i] = sh;
+          lo[i] = ld_row(al);
+          hi[i] = ld_row(al + 1);
         }
-        // pointer arithmetic (not an integer round trip) keeps the global
-        // address space, so these are global_load_dwordx4, not flat loads
-        const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
-        const uint4 *al = reinterpret_cast<const uint4 *>(p - sh);
-        shf[i] = sh;
-        lo[i] = al[0];
-        hi[i] = al[1];
       }
+      uint32_t zero = 0;
 #pragma unroll
       for (int i = 0; i < KK + HK; ++i) {
-        const uint32_t w[8] = {lo[i].x, lo[i].y, lo[i].z, lo[i].w, hi[i].x, hi[i].y, hi[i].z, hi[i].w};
-        const int qd = shf[i] >> 2, r = shf[i] & 3;
-        uint32_t t[5];
+        uint4 v;
+        if (pcm && i >= KK) {
+          const int qd = shf[i] >> 2, r = shf[i] & 3;
+          const uint32_t a0 = qd ? lo[i].y : lo[i].x, a1 = qd ? lo[i].z : lo[i].y, a2 = qd ? lo[i].w : lo[i].z;
+          const uint32_t b0 = qd ? hi[i].y : hi[i].x, b1 = qd ? hi[i].z : hi[i].y, b2 = qd ? hi[i].w : hi[i].z;
+          const uint32_t ux = __builtin_amdgcn_alignbyte(a1, a0, r), uy = __builtin_amdgcn_alignbyte(a2, a1, r);
+          const uint32_t vx = __builtin_amdgcn_alignbyte(b1, b0, r), vy = __builtin_amdgcn_alignbyte(b2, b1, r);
+          zero |= has_zero_byte(ux) | has_zero_byte(uy) | has_zero_byte(vx) | has_zero_byte(vy);
+          v = interleave_uv(ux, uy, vx, vy);
+        } else {
+          const uint32_t w[8] = {lo[i].x, lo[i].y, lo[i].z, lo[i].w, hi[i].x, hi[i].y, hi[i].z, hi[i].w};
+          const int qd = shf[i] >> 2, r = shf[i] & 3;
+          uint32_t t[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j)
-          t[j] = (qd == 0) ? w[j] : (qd == 1) ? w[j + 1] : (qd == 2) ? w[j + 2] : w[j + 3 < 8 ? j + 3 : 7];
-        const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
-                                   __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+          for (int j = 0; j < 5; ++j)
+            t[j] = (qd == 0) ? w[j] : (qd == 1) ? w[j + 1] : (qd == 2) ? w[j + 2] : w[j + 3 < 8 ? j + 3 : 7];
+          v = make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                         __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+          if (pcm) zero |= has_zero_byte(v.x) | has_zero_byte(v.y) | has_zero_byte(v.z) | has_zero_byte(v.w);
+        }
         if (i < KK) yr[i] = v; else cr[i - KK] = v;
       }
+      if (pcm && zero) errs |= pcm_rows_epb(pcmb, q, KK, HK);
     } else {
 #pragma unroll
       for (int rr = 0; rr < KK; ++rr) yr[rr] = fetch_row(F, c, q * KK + rr, m, mby, errs);
@@ -605,11 +684,9 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score(FusedArgs fa) 
       for (int rr = 0; rr < HK; ++rr) cr[rr] = fetch_row(F, c, 16 + q * HK + rr, m, mby, errs);
     }
 #pragma unroll
-    for (int rr = 0; rr < KK; ++rr)
-      *reinterpret_cast<uint4 *>(dst + (mby * 16 + q * KK + rr) * F.pitch + m * 16) = yr[rr];
+    for (int rr = 0; rr < KK; ++rr) st_row(dst + (mby * 16 + q * KK + rr) * F.pitch + m * 16, yr[rr]);
 #pragma unroll
-    for (int rr = 0; rr < HK; ++rr)
-      *reinterpret_cast<uint4 *>(dst_uv + (mby * 8 + q * HK + rr) * F.pitch + m * 16) = cr[rr];
+    for (int rr = 0; rr < HK; ++rr) st_row(dst_uv + (mby * 8 + q * HK + rr) * F.pitch + m * 16, cr[rr]);
     if constexpr (K != 0) {
       uint32_t ys[G], us[G], vs[G];
 #pragma unroll
@@ -643,8 +720,14 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score(FusedArgs fa) 
   }
   if constexpr (K != 0) {
     __syncthreads();
-    const uint32_t cnt = lds_hist[threadIdx.x];
-    if (cnt) atomicAdd(&fa.hist[gframe * 256 + threadIdx.x], cnt);
+    // two bins per 64-bit atomic (a frame's bin total stays below 2^32, so
+    // the low count never carries into the high one): half the L2 atomics
+    if (threadIdx.x < 128) {
+      const uint64_t lo = lds_hist[2 * threadIdx.x], hi = lds_hist[2 * threadIdx.x + 1];
+      if (lo | hi)
+        atomicAdd(reinterpret_cast<unsigned long long *>(fa.hist + gframe * 256) + threadIdx.x,
+                  static_cast<unsigned long long>(lo | (hi << 32)));
+    }
   }
   if (errs) atomicOr(a.err, errs);
 }

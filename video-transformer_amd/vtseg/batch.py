@@ -5,7 +5,11 @@ The reference processes a batch with a sequential loop
 plans and (optionally) decodes+scores its own videos on its own GPU; the only
 exchange is one all-gather of a small per-video record (segment count, scene
 cut count, duration in microseconds) so every rank ends with the whole batch's
-plan — RCCL over xGMI when the group is NCCL, gloo on CPU.  No pixel data
+plan — RCCL over xGMI when the group is NCCL, gloo on CPU.  When scene
+scoring is requested a second all-gather carries the per-video boundary
+arrays, padded to the batch maximum: the segment windows as
+frame indices [start, end) of every planned segment (int64) and the scene-cut
+frame indices (int64) with their presentation times (f64).  No pixel data
 crosses GPUs.
 """
 from __future__ import annotations
@@ -28,13 +32,18 @@ class BatchItem:
     n_segments: int
     n_cuts: int          # -1 when scene scoring was not requested
     rank: int
+    # with score=True: frame index range [start, end) of every planned
+    # segment's extract window, scene-cut frame indices and their times (s)
+    segment_frames: tuple[tuple[int, int], ...] = ()
+    cut_frames: tuple[int, ...] = ()
+    cut_times: tuple[float, ...] = ()
 
 
-def _segment_count(duration: float, config: dict, current_api_count: int) -> int:
+def _segments(duration: float, config: dict, current_api_count: int):
     plan = plan_segments_with_budget(duration, config, current_api_count)
     if plan.segment_duration <= 0:
-        return 0
-    return len(plan_segments(duration, plan.segment_duration, plan.overlap))
+        return []
+    return plan_segments(duration, plan.segment_duration, plan.overlap)
 
 
 def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int = 0,
@@ -52,28 +61,93 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
 
     local = torch.zeros((per, REC), dtype=torch.int64)
+    seg_frames: list[list[int]] = [[] for _ in range(per)]
+    cut_frames: list[list[int]] = [[] for _ in range(per)]
+    cut_times: list[list[float]] = [[] for _ in range(per)]
     for j, i in enumerate(range(rank, n, world)):
         p = str(paths[i])
         duration = probe_duration(p)
+        segs = _segments(duration, config, current_api_count)
         n_cuts = -1
         if score:
             from .scene import VideoScorer
             with VideoScorer(p, device=torch.cuda.current_device() if device is None else device) as v:
-                v.score()
-                n_cuts = len(v.scene_cuts())
-        local[j, 0] = _segment_count(duration, config, current_api_count)
+                res = v.score()
+                cuts = v.scene_cuts()
+                n_cuts = len(cuts)
+                times = [t for sg in segs for t in (sg.start, sg.end)]
+                seg_frames[j] = v.boundary_frames(times) if times else []
+                cut_frames[j] = list(cuts)
+                cut_times[j] = [float(res.pts[c]) / res.timescale for c in cuts]
+        local[j, 0] = len(segs)
         local[j, 1] = n_cuts
         local[j, 2] = round(duration * 1_000_000)
-    local = local.to(dev)
-    if distributed:
-        gathered = torch.empty((world * per, REC), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(gathered, local, group=group)
-    else:
-        gathered = local
-    g = gathered.cpu().view(world, per, REC)
+    g = _all_gather(local, world, group, dev).view(world, per, REC)
+    arrays = (exchange_boundaries(g, seg_frames, cut_frames, cut_times, group=group, device=dev)
+              if score else None)
     items = []
     for i in range(n):
         r, j = i % world, i // world
+        extra = {}
+        if arrays is not None:
+            sf, cf, ct = arrays[r][j]
+            extra = {"segment_frames": sf, "cut_frames": cf, "cut_times": ct}
         items.append(BatchItem(index=i, path=str(paths[i]), duration=int(g[r, j, 2]) / 1e6,
-                               n_segments=int(g[r, j, 0]), n_cuts=int(g[r, j, 1]), rank=r))
+                               n_segments=int(g[r, j, 0]), n_cuts=int(g[r, j, 1]), rank=r,
+                               **extra))
     return items
+
+
+def exchange_boundaries(records, seg_frames, cut_frames, cut_times, *, group=None,
+                        device=None):
+    """Second all-gather of the batch: per-video boundary arrays.
+
+    records: the gathered [world, per, 3] int64 (n_segments, n_cuts, ...) of
+    the first exchange, identical on every rank, so every rank pads to the
+    same widths.  seg_frames[j] (2 per segment), cut_frames[j], cut_times[j]:
+    this rank's j-th video.  Returns [world][per] of (segment_frames pairs,
+    cut_frames, cut_times) tuples.
+    """
+    import torch
+    import torch.distributed as dist
+
+    distributed = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if distributed else 1
+    dev = device if device is not None else torch.device("cpu")
+    per = records.shape[1]
+    nseg, ncut = records[:, :, 0], records[:, :, 1].clamp(min=0)
+    width_i = max(1, int((2 * nseg + ncut).max()))
+    width_f = max(1, int(ncut.max()))
+    li = torch.full((per, width_i), -1, dtype=torch.int64)
+    lf = torch.zeros((per, width_f), dtype=torch.float64)
+    for j in range(per):
+        row = list(seg_frames[j]) + list(cut_frames[j])
+        if row:
+            li[j, :len(row)] = torch.tensor(row, dtype=torch.int64)
+        if len(cut_times[j]):
+            lf[j, :len(cut_times[j])] = torch.tensor(list(cut_times[j]), dtype=torch.float64)
+    gi = _all_gather(li, world, group, dev).view(world, per, width_i)
+    gf = _all_gather(lf, world, group, dev).view(world, per, width_f)
+    out = []
+    for r in range(world):
+        row_r = []
+        for j in range(per):
+            ns, nc = int(records[r, j, 0]), int(ncut[r, j])
+            vals = gi[r, j].tolist()
+            row_r.append((tuple((vals[2 * s], vals[2 * s + 1]) for s in range(ns)),
+                          tuple(vals[2 * ns:2 * ns + nc]), tuple(gf[r, j, :nc].tolist())))
+        out.append(row_r)
+    return out
+
+
+def _all_gather(local, world: int, group, dev):
+    """[per, ...] on every rank -> [world * per, ...] on the CPU."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return local
+    t = local.to(dev)
+    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return out.cpu()
