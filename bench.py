@@ -1,6 +1,7 @@
 """Benchmark: 720p frames/s decoded+scored per node (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload decode_score|score]
+                    [--config 720p-10min|720p-2h|1080p-2h|480p-60s]
 
 One process per GPU (torch.distributed.run for N > 1; RANK/LOCAL_RANK/
 WORLD_SIZE from the env, rendezvous on 127.0.0.1).  Weak scaling: every rank
@@ -34,6 +35,16 @@ sys.path.insert(0, str(ROOT / "video-transformer_amd"))
 sys.path.insert(0, str(ROOT / "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+# BASELINE.json configs runnable per GPU: name -> (width, height, frames, what)
+CONFIGS = {
+    "720p-10min": (1280, 720, 18000, "BASELINE config [1]: 10-min 720p MP4, one per GPU"),
+    "720p-2h": (1280, 720, 216000, "BASELINE config [2]: 2-h 720p, streamed decode "
+                                   "(two-ring windows)"),
+    "1080p-2h": (1920, 1080, 216000, "BASELINE config [4] per GPU: 2-h 1080p, two-stream "
+                                     "decode/score overlap"),
+    "480p-60s": (640, 480, 1800, "BASELINE config [0] clip (60-s 480p) on the GPU path"),
+}
 FPS = 30
 METRIC = "720p frames/sec decoded+scored per node; segment-index exact-match vs CPU"
 
@@ -140,9 +151,11 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="decode_score", choices=["decode_score", "score"])
-    ap.add_argument("--frames", type=int, default=18000, help="10 min at 30 fps")
-    ap.add_argument("--width", type=int, default=1280)
-    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--config", default="720p-10min", choices=sorted(CONFIGS),
+                    help="BASELINE configuration (per GPU); the N=1 headline is 720p-10min")
+    ap.add_argument("--frames", type=int, default=None, help="override the config's frames")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gops-per-launch", type=int, default=0,
                     help="GOPs per reconstruct launch; <= 0 all GOPs of the window")
@@ -173,8 +186,11 @@ def main() -> None:
     from vtseg import budget_planner as bp
     from vtseg import video_segmenter as vs
 
-    width, height, k = args.width, args.height, 4 if args.height <= 720 else 6
-    F = args.frames
+    cw, ch, cf, cdesc = CONFIGS[args.config]
+    width = args.width or cw
+    height = args.height or ch
+    F = args.frames or cf
+    k = 4 if height <= 720 else 6
     w, h = width // k, height // k
     stride = width * height * 3 // 2
 
@@ -312,8 +328,10 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"{args.workload}: 10-min {width}x{height} @30fps "
-                                   f"({F} frames) per GPU, thumbnails k={k}",
+            "config": {"workload": f"{args.workload}: {cdesc}; synthetic H.264 {width}x{height} "
+                                   f"@30fps, {F} frames ({F / FPS / 60:.1f} min) per GPU, "
+                                   f"thumbnails k={k}",
+                       "config_name": args.config,
                        "frames_per_gpu": F, "width": width, "height": height, "k": k,
                        "parallelism": f"video-per-gpu x{world}",
                        "segment_counts": counts},

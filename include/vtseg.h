@@ -262,7 +262,9 @@ typedef struct vts_synth_params {
   int32_t slices_per_row;       /* n > 0: n slices per macroblock row; 0: one
                                    slice per picture                            */
   int32_t hash_frames;          /* 1 = compute vts_synth_info.recon_hash        */
-  int32_t _pad;
+  int32_t pcm_zero_runs;        /* 1 = plant runs of zero luma samples in each
+                                   scene texture: I_PCM data then holds
+                                   emulation-prevention bytes (edge case)       */
 } vts_synth_params;
 
 typedef struct vts_synth_info {

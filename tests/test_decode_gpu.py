@@ -23,6 +23,8 @@ STREAMS = [
     ("ragged", dict(width=336, height=200, slices_per_row=3, max_motion=6)),
     ("nhd", dict(width=640, height=360, slices_per_row=2, max_motion=2)),
     ("static", dict(width=96, height=64, max_motion=0)),
+    ("bigpan", dict(width=320, height=240, max_motion=24)),    # edge MBs: partial fill
+    ("hugepan", dict(width=256, height=160, max_motion=40)),   # edge MBs: all fill
     ("hd720", dict(width=1280, height=720, max_motion=4)),
     ("fhd", dict(width=1920, height=1080, max_motion=8)),
 ]
@@ -107,6 +109,18 @@ def test_boundary_frames_for_planned_segments(tmp_path):
         pts = v.score().pts.tolist()
     assert got == oracle.boundary_frames(pts, 30000, times)
     assert got[:4] == [0, 825, 0, 750]
+
+
+def test_emulation_prevention_inside_pcm_fails_loudly(tmp_path):
+    """Outside the decoder subset: an EPB inside I_PCM samples.  The device
+    path must refuse with the reason, never return wrong pixels."""
+    _require_gpu()
+    path = tmp_path / "z.mp4"
+    scene.synth_write(path, width=160, height=96, n_frames=30, gop_max_s=0.5,
+                      pcm_zero_runs=True)
+    with scene.VideoScorer(path) as v:
+        with pytest.raises(VtsegError, match="emulation prevention inside I_PCM"):
+            v.score()
 
 
 def test_open_rejects_non_mp4(tmp_path):

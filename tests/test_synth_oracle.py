@@ -37,6 +37,19 @@ def test_generator_reconstruction_equals_oracle_decode(tmp_path, kw):
     assert info["pts"] == [1000 * i for i in range(120)]
 
 
+def test_pcm_with_emulation_prevention_decodes_in_oracle(tmp_path):
+    """Zero runs in I_PCM samples force emulation-prevention bytes inside the
+    PCM span; the oracle's EPB-aware PCM read still matches the generator."""
+    path = tmp_path / "z.mp4"
+    r = scene.synth_write(path, width=160, height=96, n_frames=30, gop_max_s=0.5,
+                          hash_frames=True, pcm_zero_runs=True)
+    m = oracle.read_mp4(path)
+    assert any(b"\x00\x00\x03" in m["data"][o:o + n] for o, n in zip(m["offsets"], m["sizes"]))
+    frames, _ = oracle.decode_file(path)
+    assert oracle.recon_hash(frames) == r["recon_hash"]
+    assert (frames[0, :96, :] == 0).sum() > 0
+
+
 def test_scene_cuts_are_the_top_scores(tmp_path):
     path = tmp_path / "c.mp4"
     r = scene.synth_write(path, width=320, height=240, n_frames=300, cut_min_s=1, cut_max_s=3,

@@ -9,7 +9,7 @@ timeout -k 10 600 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2
 tail -2 gpurun_out/pytest_gpu.log
 LIB=video-transformer_amd/vtseg/libvtseg.so
 cp $LIB gpurun_out/lib_intree.so
-for pass in 1 2; do
+for pass in $(seq ${PASSES:-2}); do
   for v in "$@"; do
     cp tools/exp/lib_$v.so $LIB
     timeout -k 10 300 python bench.py --no-cpu-baseline $ARGS > gpurun_out/var_$v.json 2> gpurun_out/var_$v.err || { tail -20 gpurun_out/var_$v.err; exit 1; }

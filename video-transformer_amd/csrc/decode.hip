@@ -431,16 +431,22 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 constexpr int kReconThreads = 256;
 
+// timing-only experiment switches (tools/exp): 1 no histogram, 2 no RGB
+// store, 4 no thumbnail scoring at all, 8 no BT.709 arithmetic
+#ifndef VTS_EXP_SKIP
+#define VTS_EXP_SKIP 0
+#endif
 #ifndef VTS_NT_LOAD
 #define VTS_NT_LOAD 0
 #endif
 #ifndef VTS_NT_STORE
-#define VTS_NT_STORE 0
+#define VTS_NT_STORE 1
 #endif
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// 16-byte row load / store of the fused kernel's streams (optionally
-// nontemporal: every reference row is read once, every output row written once)
+// 16-byte row load / store of the fused kernel's streams.  Output rows are
+// stored nontemporal (3-5% faster per launch, profiles/r01_variants.txt);
+// nontemporal reference loads measured 8% slower and stay off.
 __device__ __forceinline__ uint4 ld_row(const uint4 *p) {
 #if VTS_NT_LOAD
   const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
@@ -596,7 +602,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
   const int64_t gframe = fa.frame0 + fr.x;
   // the command load is in flight across the histogram-clearing barrier
   const uint64_t c = mb < nmb ? a.cmd[static_cast<int64_t>(fr.x) * nmb + mb] : 0;
-  if constexpr (K != 0) {
+  if constexpr (K != 0 && !(VTS_EXP_SKIP & 1)) {
     lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
     __syncthreads();
   }
@@ -610,17 +616,18 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
     const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
     const int sx = m * 16 + (mvx >> 2), cx = m * 8 + (mvx >> 3);
     const bool pcm = kind == 1;
-    // fast paths: I_PCM, and inter with integer-pel chroma whose source rows
-    // lie inside the picture horizontally (vertical clamping is folded into
-    // the row index)
-    const bool fast = pcm || (kind == 2 && F.ref && ((mvx | mvy) & 7) == 0 && sx >= 0 &&
-                              sx + 15 <= F.W - 1 && cx >= 0 && cx + 7 <= F.CW - 1);
+    // fast paths: I_PCM, and inter with integer-pel chroma.  Vertical
+    // clamping is folded into the row index; horizontal clamping at the
+    // picture edges loads the edge-most aligned chunk and funnels it against
+    // the replicated edge sample, so edge macroblocks (present in almost
+    // every wave) do not fall to the per-byte general path.
+    const bool fast = pcm || (kind == 2 && F.ref && ((mvx | mvy) & 7) == 0);
     if (fast) {
       // every aligned load is issued before any is used: 16-byte pairs for
       // luma / NV12 rows, 8-byte pairs of the planar Cb and Cr rows of I_PCM
       const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
       uint4 lo[KK + HK], hi[KK + HK];
-      int shf[KK + HK];
+      int shf[KK + HK];  // funnel shift | edge mode << 8 (1 left, 2 right)
 #pragma unroll
       for (int i = 0; i < KK + HK; ++i) {
         if (pcm && i >= KK) {
@@ -632,23 +639,51 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
           lo[i] = make_uint4(u0.x, u0.y, u1.x, u1.y);
           hi[i] = make_uint4(v0.x, v0.y, v1.x, v1.y);
         } else {
-          const uint8_t *p;
+          const uint4 *pa;
+          int sh;
           if (pcm) {
-            p = pcmb + 16 * (q * KK + i);
-          } else if (i < KK) {
-            const int y = clampi(mby * 16 + q * KK + i + (mvy >> 2), 0, F.H - 1);
-            p = F.ref + y * F.pitch + sx;
+            const uint8_t *p = pcmb + 16 * (q * KK + i);
+            sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+            pa = reinterpret_cast<const uint4 *>(p - sh);
           } else {
-            const int y = clampi(mby * 8 + q * HK + (i - KK) + (mvy >> 3), 0, F.CH - 1);
-            p = F.ref_uv + y * F.pitch + 2 * cx;
+            // row start (16-byte aligned: pitch and W are multiples of 16)
+            const uint8_t *row = i < KK
+                ? F.ref + clampi(mby * 16 + q * KK + i + (mvy >> 2), 0, F.H - 1) * F.pitch
+                : F.ref_uv + clampi(mby * 8 + q * HK + (i - KK) + (mvy >> 3), 0, F.CH - 1) * F.pitch;
+            const int x0 = i < KK ? sx : 2 * cx;  // first wanted byte (NV12 rows are W bytes)
+            if (x0 < 0) {                         // left edge: [fill x16][row 0..15]
+              pa = reinterpret_cast<const uint4 *>(row);
+              sh = (x0 > -16 ? 16 + x0 : 0) | (1 << 8);
+            } else if (x0 > F.W - 16) {           // right edge: [row W-16..W-1][fill x16]
+              pa = reinterpret_cast<const uint4 *>(row + F.W - 16);
+              sh = min(x0 - (F.W - 16), 16) | (2 << 8);
+            } else {
+              const uint8_t *p = row + x0;
+              // pointer arithmetic (not an integer round trip) keeps the global
+              // address space, so these are global_load_dwordx4, not flat loads
+              sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+              pa = reinterpret_cast<const uint4 *>(p - sh);
+            }
           }
-          // pointer arithmetic (not an integer round trip) keeps the global
-          // address space, so these are global_load_dwordx4, not flat loads
-          const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
-          const uint4 *al = reinterpret_cast<const uint4 *>(p - sh);
           shf[i] = sh;
-          lo[i] = ld_row(al);
-          hi[i] = ld_row(al + 1);
+          lo[i] = ld_row(pa);
+          hi[i] = ld_row(sh >> 8 ? pa : pa + 1);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < KK + HK; ++i) {
+        if (!pcm && (shf[i] >> 8)) {
+          // replicate the edge sample (a byte for luma, a Cb/Cr pair for NV12)
+          const bool luma = i < KK;
+          if ((shf[i] >> 8) == 1) {
+            const uint32_t f = luma ? (hi[i].x & 0xffu) * 0x01010101u : (hi[i].x & 0xffffu) * 0x00010001u;
+            lo[i] = make_uint4(f, f, f, f);
+          } else {
+            const uint32_t g = luma ? (lo[i].w >> 24) * 0x01010101u : (lo[i].w >> 16) * 0x00010001u;
+            hi[i] = make_uint4(g, g, g, g);
+            if ((shf[i] & 0xff) == 16) lo[i] = hi[i];
+          }
+          shf[i] &= 15;
         }
       }
       uint32_t zero = 0;
@@ -687,7 +722,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
     for (int rr = 0; rr < KK; ++rr) st_row(dst + (mby * 16 + q * KK + rr) * F.pitch + m * 16, yr[rr]);
 #pragma unroll
     for (int rr = 0; rr < HK; ++rr) st_row(dst_uv + (mby * 8 + q * HK + rr) * F.pitch + m * 16, cr[rr]);
-    if constexpr (K != 0) {
+    if constexpr (K != 0 && !(VTS_EXP_SKIP & 4)) {
       uint32_t ys[G], us[G], vs[G];
 #pragma unroll
       for (int p = 0; p < G; ++p) ys[p] = us[p] = vs[p] = 0;
@@ -703,12 +738,12 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
         const uint32_t y = (ys[p] + K * K / 2) / (K * K);
         const uint32_t u = (us[p] + HK * HK / 2) / (HK * HK);
         const uint32_t v = (vs[p] + HK * HK / 2) / (HK * HK);
-        rgb24[p] = bt709_rgb24(y, u, v);
+        rgb24[p] = (VTS_EXP_SKIP & 8) ? (y | u << 8 | v << 16) : bt709_rgb24(y, u, v);
         packed[p / 4] |= y << (8 * (p & 3));
-        atomicAdd(&lds_hist[y], 1u);
+        if (!(VTS_EXP_SKIP & 1)) atomicAdd(&lds_hist[y], 1u);
       }
       const int64_t tpx = static_cast<int64_t>(mby * Q + q) * fa.w + m * G;
-      store_rgb<G>(fa.rgb + (gframe * fa.w * fa.h + tpx) * 3, rgb24);
+      if (!(VTS_EXP_SKIP & 2)) store_rgb<G>(fa.rgb + (gframe * fa.w * fa.h + tpx) * 3, rgb24);
       uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * fa.w * fa.h + tpx;
       if constexpr (G >= 4) {
 #pragma unroll
@@ -718,7 +753,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       }
     }
   }
-  if constexpr (K != 0) {
+  if constexpr (K != 0 && !(VTS_EXP_SKIP & 1)) {
     __syncthreads();
     // two bins per 64-bit atomic (a frame's bin total stays below 2^32, so
     // the low count never carries into the high one): half the L2 atomics

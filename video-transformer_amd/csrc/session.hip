@@ -5,14 +5,18 @@
 // a static schedule once at open:
 //   * windows of whole GOPs (each starts at an intra picture) sized to a
 //     decoded-surface ring; a video that fits in kSingleWindowBytes is one
-//     window (all GOPs decode in parallel);
+//     window (all GOPs decode in parallel); longer ones get two rings sized
+//     from the free HBM;
 //   * per window, "levels": level 0 = intra pictures, level L = pictures L
 //     references after one; one reconstruct launch per level covers that
 //     level of every GOP in the window;
 // and uploads the whole elementary stream to HBM.  A run then is pure device
-// work: memset cmd -> h264_parse (all slices of the window) -> h264_recon
-// per level -> score_runs + score_seams, windows pipelined over two HIP
-// streams (decode of window i+1 overlaps scoring of window i; two rings).
+// work per window: memset cmd -> h264_parse (all slices of the window) ->
+// one launch per level of h264_recon_score (reconstruct + thumbnail, RGB,
+// histogram fused; k in {2,4,8}, no crop) -> thumb_sad, or h264_recon per
+// level -> score_runs + score_seams (cropped pictures, k = 6); windows are
+// pipelined over two HIP streams and two rings (decode of window i+1
+// overlaps scoring of window i).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,7 +40,7 @@ using namespace vts;
 namespace {
 
 constexpr int64_t kSingleWindowBytes = 48ll << 30;  // up to 48 GiB decoded: one window
-constexpr int64_t kRingBytes = 8ll << 30;           // else 8 GiB rings (x2)
+constexpr int64_t kMinRingBytes = 1ll << 30;        // else two rings of >= 1 GiB
 constexpr int64_t kPad = 256;
 
 #define HIP_TRY(expr)                                                              \
@@ -236,12 +240,24 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
     if (is_ref[f]) last_ref = f;
   }
 
-  // windows of whole intra-started groups
-  const int64_t total_bytes = c->n_frames * c->frame_stride;
+  // windows of whole intra-started groups.  Device bytes per window frame:
+  // surface + MB commands + thumbnail + scoring workspace share; the rings
+  // get half of the HBM left after the whole-video buffers (ES, RGB
+  // thumbnails, histograms), capped at kSingleWindowBytes each.
+  const int64_t nmb_f = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
+  const int64_t tw_f = static_cast<int64_t>(c->width / c->k) * (c->height / c->k);
+  const int64_t per_frame = c->frame_stride + 8 * nmb_f + tw_f +
+                            score_workspace_bytes(c->width, c->height, c->k, 1);
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const int64_t whole = c->es_bytes + c->n_frames * (3 * tw_f + 1024 + 12) + (1ll << 30);
+  const int64_t avail = std::max<int64_t>(0, static_cast<int64_t>(free_b) - whole);
+  const int64_t ring_budget = std::min(kSingleWindowBytes, std::max(kMinRingBytes, avail / 4));
   int64_t cap;
   if (c->params.window_frames > 0) cap = c->params.window_frames;
-  else if (total_bytes <= kSingleWindowBytes) cap = c->n_frames;
-  else cap = std::max<int64_t>(1, kRingBytes / c->frame_stride);
+  else if (c->n_frames * per_frame <= std::min(kSingleWindowBytes, avail / 2)) cap = c->n_frames;
+  else cap = std::max<int64_t>(1, ring_budget / per_frame);
   auto next_intra = [&](int64_t x) {
     while (x < c->n_frames && !intra[x]) ++x;
     return x;

@@ -60,7 +60,7 @@ struct Picture {
 };
 
 // Smooth value-noise texture: two octaves of bilinear random grids + noise.
-void fill_texture(Picture &p, Pcg32 &rng) {
+void fill_texture(Picture &p, Pcg32 &rng, bool zero_runs) {
   auto plane = [&](uint8_t *dst, int w, int h, int cell, int lo, int hi, int noise) {
     const int gw = w / cell + 2, gh = h / cell + 2;
     std::vector<int> g(size_t(gw) * gh), g2(size_t(gw * 4 + 2) * (gh * 4 + 2));
@@ -89,6 +89,9 @@ void fill_texture(Picture &p, Pcg32 &rng) {
     }
   };
   plane(p.y.data(), p.w, p.h, 64, 24, 232, 3);
+  if (zero_runs)  // 4 zero samples every 97 px on every 16th row: 00 00 00 00
+    for (int yy = 0; yy < p.h; yy += 16)
+      for (int xx = 0; xx + 4 <= p.w; xx += 97) std::memset(&p.y[size_t(yy) * p.w + xx], 0, 4);
   plane(p.u.data(), p.w / 2, p.h / 2, 32, 72, 184, 1);
   plane(p.v.data(), p.w / 2, p.h / 2, 32, 72, 184, 1);
 }
@@ -368,7 +371,7 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
     const bool idr = cut || since_idr >= gop_max;
     std::swap(cur, ref);  // ref = previous reconstruction
     if (cut) {
-      fill_texture(cur, tex_rng);
+      fill_texture(cur, tex_rng, P.pcm_zero_runs != 0);
     } else if (idr) {
       for (int my = 0; my < mbh; ++my)
         for (int mx = 0; mx < mbw; ++mx) mc_mb(ref, cur, mx, my, 4 * vx, 4 * vy);
