@@ -58,10 +58,11 @@ def algorithmic_bytes_per_frame(width: int, height: int, k: int) -> int:
 
 def fused_bytes_per_frame(width: int, height: int, k: int) -> int:
     """h264_recon_score: NV12-sized source read (reference picture or I_PCM
-    samples) + NV12 frame written + RGB thumbnail + thumbnail luma written +
-    histogram; the frame is never re-read for scoring."""
+    samples) + NV12 frame written + RGB thumbnail + thumbnail luma written and
+    the predecessor's read for the fused SAD + histogram + SAD; the frame is
+    never re-read for scoring."""
     w, h = width // k, height // k
-    return 3 * width * height + 3 * w * h + w * h + 1024
+    return 3 * width * height + 3 * w * h + 2 * w * h + 1024 + 8
 
 
 def smooth_frames_host(rng, n, width, height):

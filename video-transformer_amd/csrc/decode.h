@@ -31,7 +31,9 @@ struct ParseArgs {
 struct ReconArgs {
   const uint8_t *es;
   const uint64_t *cmd;
-  const int2 *frames;      // (slot, ref_slot) for every frame of this launch
+  const int4 *frames;      // (slot, ref_slot, sad_prev, 0) per frame of this launch:
+                           // sad_prev = slot of the display predecessor when its
+                           // thumbnail was made by an earlier launch, else -1
   uint8_t *surf;           // ring of decoded NV12 frames
   int64_t frame_stride;
   int32_t pitch;
@@ -50,10 +52,13 @@ struct FusedArgs {
   uint8_t *thumb;          // [slot][h][w] thumbnail luma
   uint8_t *rgb;            // [global frame][h][w][3]
   uint32_t *hist;          // [global frame][256], zeroed before the window
+  uint64_t *sad;           // [global frame], zeroed before the window
 };
 
 struct ThumbSadArgs {
   const uint8_t *thumb;    // [slot][h][w]
+  const int32_t *list;     // slots to compute (nullptr = all n_frames)
+  int64_t n_list;
   const uint8_t *prev_luma;  // predecessor of slot 0 (nullptr = none)
   uint8_t *last_luma;      // receives slot n_frames-1 (may be nullptr)
   int64_t frame0;
@@ -66,6 +71,9 @@ struct ThumbSadArgs {
 int parse_launch(const ParseArgs &a, hipStream_t s);
 int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s);
 int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s);
+// score[frame0 + i] = sad / (w*h*255) for i < n_frames
+int sad_score_launch(const uint64_t *sad, float *score, int64_t frame0, int64_t n_frames,
+                     int64_t npx, hipStream_t s);
 int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s);
 int score_launch(const vts_score_desc *d, hipStream_t stream);
 int64_t score_workspace_bytes(int32_t width, int32_t height, int32_t k, int64_t n_frames);

@@ -597,16 +597,35 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
   const int fi = blockIdx.x / fa.wgs_per_frame;
   const int q = threadIdx.x / MB_PER_WG;
   const int mb = (blockIdx.x - fi * fa.wgs_per_frame) * MB_PER_WG + (threadIdx.x % MB_PER_WG);
-  const int2 fr = a.frames[fi];
+  const int4 fr = a.frames[fi];
   const FrameRefs F = frame_refs(a, fr.y);
   const int64_t gframe = fa.frame0 + fr.x;
   // the command load is in flight across the histogram-clearing barrier
   const uint64_t c = mb < nmb ? a.cmd[static_cast<int64_t>(fr.x) * nmb + mb] : 0;
+  // and so is the display predecessor's thumbnail (fused SAD, see below)
+  constexpr int GW = K ? (16 / K + 3) / 4 : 1;  // thumbnail words per lane
+  uint32_t prevw[GW];
+#pragma unroll
+  for (int i = 0; i < GW; ++i) prevw[i] = 0;
+  if constexpr (K != 0) {
+    if (fr.z >= 0 && mb < nmb) {
+      const int mby = mb / mbw, m = mb - mby * mbw;
+      const uint8_t *pt = fa.thumb + static_cast<int64_t>(fr.z) * fa.w * fa.h +
+                          static_cast<int64_t>(mby * Q + q) * fa.w + m * G;
+      if constexpr (G >= 4) {
+#pragma unroll
+        for (int i = 0; i < G / 4; ++i) prevw[i] = reinterpret_cast<const uint32_t *>(pt)[i];
+      } else {
+        prevw[0] = *reinterpret_cast<const uint16_t *>(pt);
+      }
+    }
+  }
   if constexpr (K != 0 && !(VTS_EXP_SKIP & 1)) {
     lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
     __syncthreads();
   }
   uint32_t errs = 0;
+  uint32_t sad = 0;  // this lane's share of the frame's thumbnail SAD
   if (mb < nmb) {
     const int mby = mb / mbw, m = mb - mby * mbw;
     uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
@@ -744,12 +763,34 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       }
       const int64_t tpx = static_cast<int64_t>(mby * Q + q) * fa.w + m * G;
       if (!(VTS_EXP_SKIP & 2)) store_rgb<G>(fa.rgb + (gframe * fa.w * fa.h + tpx) * 3, rgb24);
-      uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * fa.w * fa.h + tpx;
+      const int64_t npx = static_cast<int64_t>(fa.w) * fa.h;
+      uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx;
       if constexpr (G >= 4) {
 #pragma unroll
         for (int i = 0; i < G / 4; ++i) reinterpret_cast<uint32_t *>(thumb)[i] = packed[i];
       } else {
         *reinterpret_cast<uint16_t *>(thumb) = static_cast<uint16_t>(packed[0]);
+      }
+      // SAD against the display predecessor's thumbnail (made one or more
+      // levels earlier); GOP starts are left to the thumb_sad pass
+      if (fr.z >= 0) {
+#pragma unroll
+        for (int i = 0; i < GW; ++i) sad = sad_u8(packed[i], prevw[i], sad);
+      }
+    }
+  }
+  if constexpr (K != 0) {
+    if (fr.z >= 0) {  // workgroup SAD -> one 64-bit atomic
+      __shared__ uint32_t red[kReconThreads / 64];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) sad += __shfl_xor(sad, off, 64);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sad;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int i = 0; i < kReconThreads / 64; ++i) t += red[i];
+        atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(t));
       }
     }
   }
@@ -768,13 +809,16 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
 }
 
 // SAD of each frame's thumbnail luma against its predecessor's (the previous
-// window's last thumbnail for the window's first frame) and the score.
+// window's last thumbnail for the window's first frame) and the score.  One
+// workgroup per frame; 16-byte loads, all of a thread's loads issued before
+// the SAD (a 320x180 thumbnail is 3 600 uint4 = 14 per thread).
 __global__ void __launch_bounds__(256) thumb_sad(ThumbSadArgs t) {
-  const int64_t f = blockIdx.x;  // window slot
+  const int64_t f = t.list ? t.list[blockIdx.x] : blockIdx.x;  // window slot
   const int64_t npx = static_cast<int64_t>(t.w) * t.h;
   const uint8_t *cur = t.thumb + f * npx;
   const uint8_t *prev = f > 0 ? t.thumb + (f - 1) * npx : t.prev_luma;
   const int64_t gf = t.frame0 + f;
+  const bool vec = (npx & 15) == 0;  // thumbnail rows are 16-byte aligned in the ring
   if (f == t.n_frames - 1 && t.last_luma) {
     for (int64_t i = threadIdx.x; i < npx / 4; i += blockDim.x)
       reinterpret_cast<uint32_t *>(t.last_luma)[i] = reinterpret_cast<const uint32_t *>(cur)[i];
@@ -787,8 +831,30 @@ __global__ void __launch_bounds__(256) thumb_sad(ThumbSadArgs t) {
     return;
   }
   uint32_t s = 0;
-  for (int64_t i = threadIdx.x; i < npx / 4; i += blockDim.x)
-    s = sad_u8(reinterpret_cast<const uint32_t *>(cur)[i], reinterpret_cast<const uint32_t *>(prev)[i], s);
+  if (vec) {
+    const uint4 *c4 = reinterpret_cast<const uint4 *>(cur), *p4 = reinterpret_cast<const uint4 *>(prev);
+    const int64_t n4 = npx / 16;
+    constexpr int U = 8;
+    for (int64_t i0 = threadIdx.x; i0 < n4; i0 += U * blockDim.x) {
+      uint4 a[U], b[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + static_cast<int64_t>(u) * blockDim.x;
+        a[u] = i < n4 ? c4[i] : make_uint4(0, 0, 0, 0);
+        b[u] = i < n4 ? p4[i] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s = sad_u8(a[u].x, b[u].x, s);
+        s = sad_u8(a[u].y, b[u].y, s);
+        s = sad_u8(a[u].z, b[u].z, s);
+        s = sad_u8(a[u].w, b[u].w, s);
+      }
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < npx / 4; i += blockDim.x)
+      s = sad_u8(reinterpret_cast<const uint32_t *>(cur)[i], reinterpret_cast<const uint32_t *>(prev)[i], s);
+  }
   __shared__ uint32_t red[4];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -801,7 +867,23 @@ __global__ void __launch_bounds__(256) thumb_sad(ThumbSadArgs t) {
   }
 }
 
+__global__ void __launch_bounds__(256) sad_score(const uint64_t *sad, float *score, int64_t frame0,
+                                                int64_t n, double denom) {
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i < n) score[frame0 + i] = static_cast<float>(static_cast<double>(sad[frame0 + i]) / denom);
+}
+
 }  // namespace
+
+int sad_score_launch(const uint64_t *sad, float *score, int64_t frame0, int64_t n_frames,
+                     int64_t npx, hipStream_t s) {
+  if (n_frames <= 0) return VTS_OK;
+  hipLaunchKernelGGL(sad_score, dim3(static_cast<unsigned>((n_frames + 255) / 256)), dim3(256), 0, s, sad,
+                     score, frame0, n_frames, static_cast<double>(npx) * 255.0);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "sad_score launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
 
 int parse_launch(const ParseArgs &a, hipStream_t s) {
   if (a.n_slices <= 0) return VTS_OK;
@@ -832,8 +914,9 @@ int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s) {
 }
 
 int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s) {
-  if (t.n_frames <= 0) return VTS_OK;
-  hipLaunchKernelGGL(thumb_sad, dim3(static_cast<unsigned>(t.n_frames)), dim3(256), 0, s, t);
+  const int64_t n = t.list ? t.n_list : t.n_frames;
+  if (n <= 0) return VTS_OK;
+  hipLaunchKernelGGL(thumb_sad, dim3(static_cast<unsigned>(n)), dim3(256), 0, s, t);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "thumb_sad launch: %s", hipGetErrorString(e));
   return VTS_OK;

@@ -55,6 +55,7 @@ struct Window {
   int64_t s0 = 0, s1 = 0;          // slices [s0, s1)
   std::vector<int64_t> lvl_off;    // into level_frames
   std::vector<int32_t> lvl_cnt;
+  int64_t post_off = 0, post_cnt = 0;  // into post_slots
 };
 
 }  // namespace
@@ -72,7 +73,8 @@ struct vts_ctx {
   int64_t n_frames = 0;
   std::vector<int64_t> pts;
   std::vector<SliceDesc> slices;
-  std::vector<int2> level_frames;
+  std::vector<int4> level_frames;
+  std::vector<int32_t> post_slots;  // per window: slots whose SAD the thumb_sad pass makes
   std::vector<Window> windows;
   int64_t ring_frames = 0;
   int n_rings = 1;
@@ -80,7 +82,8 @@ struct vts_ctx {
   uint8_t *d_es = nullptr;
   int64_t es_bytes = 0;
   SliceDesc *d_slices = nullptr;
-  int2 *d_levels = nullptr;
+  int4 *d_levels = nullptr;
+  int32_t *d_post = nullptr;
   uint64_t *d_cmd[2] = {nullptr, nullptr};
   uint8_t *d_surf[2] = {nullptr, nullptr};
   uint8_t *d_ws[2] = {nullptr, nullptr};
@@ -315,10 +318,15 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
       const int64_t b = (g1 < gop_start.size()) ? gop_start[g1] : w.f1;
       int64_t gmax = 0;
       for (int64_t x = a; x < b; ++x) gmax = std::max(gmax, level[x]);
-      std::vector<std::vector<int2>> lv(static_cast<size_t>(gmax + 1));
-      for (int64_t x = a; x < b; ++x)
-        lv[level[x]].push_back(make_int2(static_cast<int>(x - w.f0),
-                                         ref[x] >= 0 ? static_cast<int>(ref[x] - w.f0) : -1));
+      std::vector<std::vector<int4>> lv(static_cast<size_t>(gmax + 1));
+      for (int64_t x = a; x < b; ++x) {
+        // the reconstruct kernel scores SAD against the display predecessor
+        // when that thumbnail comes from an earlier level launch
+        const bool fused_sad = x > w.f0 && level[x - 1] < level[x];
+        lv[level[x]].push_back(make_int4(static_cast<int>(x - w.f0),
+                                         ref[x] >= 0 ? static_cast<int>(ref[x] - w.f0) : -1,
+                                         fused_sad ? static_cast<int>(x - 1 - w.f0) : -1, 0));
+      }
       for (auto &l : lv) {
         if (l.empty()) continue;
         w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
@@ -327,6 +335,13 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
       }
     }
     (void)maxl;
+    // thumb_sad pass: frames without a fused SAD, plus the window's last
+    // frame (its thumbnail seeds the next window)
+    w.post_off = static_cast<int64_t>(c->post_slots.size());
+    for (int64_t x = w.f0; x < w.f1; ++x)
+      if (!(x > w.f0 && level[x - 1] < level[x]) || x == w.f1 - 1)
+        c->post_slots.push_back(static_cast<int32_t>(x - w.f0));
+    w.post_cnt = static_cast<int64_t>(c->post_slots.size()) - w.post_off;
   }
 
   // ---- device allocations and uploads
@@ -336,8 +351,12 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   HIP_TRY(hipMalloc(&c->d_slices, sizeof(SliceDesc) * c->slices.size()));
   HIP_TRY(hipMemcpy(c->d_slices, c->slices.data(), sizeof(SliceDesc) * c->slices.size(),
                     hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&c->d_levels, sizeof(int2) * c->level_frames.size()));
-  HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int2) * c->level_frames.size(),
+  HIP_TRY(hipMalloc(&c->d_post, sizeof(int32_t) * std::max<size_t>(1, c->post_slots.size())));
+  if (!c->post_slots.empty())
+    HIP_TRY(hipMemcpy(c->d_post, c->post_slots.data(), sizeof(int32_t) * c->post_slots.size(),
+                      hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_levels, sizeof(int4) * c->level_frames.size()));
+  HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(),
                     hipMemcpyHostToDevice));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
   c->ws_bytes = score_workspace_bytes(c->width, c->height, c->k, c->ring_frames);
@@ -432,6 +451,7 @@ int run_all(vts_ctx *c) {
     if (c->fused) {
       HIP_TRY(hipMemsetAsync(c->d_hist + w.f0 * 256, 0,
                              sizeof(uint32_t) * 256 * static_cast<size_t>(w.f1 - w.f0), sd));
+      HIP_TRY(hipMemsetAsync(c->d_sad + w.f0, 0, sizeof(uint64_t) * static_cast<size_t>(w.f1 - w.f0), sd));
       FusedArgs fa{};
       fa.r = ra;
       fa.frame0 = w.f0;
@@ -441,6 +461,7 @@ int run_all(vts_ctx *c) {
       fa.thumb = c->d_thumb[r];
       fa.rgb = c->d_rgb;
       fa.hist = c->d_hist;
+      fa.sad = c->d_sad;
       for (size_t l = 0; l < w.lvl_off.size(); ++l) {
         fa.r.frames = c->d_levels + w.lvl_off[l];
         VTS_TRY(fused_launch(fa, c->k, w.lvl_cnt[l], sd));
@@ -465,7 +486,11 @@ int run_all(vts_ctx *c) {
       t.h = th;
       t.sad = c->d_sad;
       t.score = c->d_score;
+      t.list = c->d_post + w.post_off;
+      t.n_list = w.post_cnt;
       VTS_TRY(thumb_sad_launch(t, ss));
+      VTS_TRY(sad_score_launch(c->d_sad, c->d_score, w.f0, w.f1 - w.f0,
+                               static_cast<int64_t>(tw) * th, ss));
     } else {
       vts_score_desc d{};
       d.nv12 = c->d_surf[r];
@@ -676,6 +701,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_es);
   f(c->d_slices);
   f(c->d_levels);
+  f(c->d_post);
   for (int r = 0; r < 2; ++r) {
     f(c->d_cmd[r]);
     f(c->d_surf[r]);
