@@ -262,9 +262,11 @@ typedef struct vts_synth_params {
   int32_t slices_per_row;       /* n > 0: n slices per macroblock row; 0: one
                                    slice per picture                            */
   int32_t hash_frames;          /* 1 = compute vts_synth_info.recon_hash        */
-  int32_t pcm_zero_runs;        /* 1 = plant runs of zero luma samples in each
-                                   scene texture: I_PCM data then holds
-                                   emulation-prevention bytes (edge case)       */
+  int32_t edge_cases;           /* bit 0: plant runs of zero luma samples in
+                                   each scene texture (I_PCM data then holds
+                                   emulation-prevention bytes); bit 1: odd-pixel
+                                   pans (half-pel chroma, 8.4.2.2.2 bilinear);
+                                   max_motion may then be odd                  */
 } vts_synth_params;
 
 typedef struct vts_synth_info {

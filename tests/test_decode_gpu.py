@@ -25,6 +25,7 @@ STREAMS = [
     ("static", dict(width=96, height=64, max_motion=0)),
     ("bigpan", dict(width=320, height=240, max_motion=24)),    # edge MBs: partial fill
     ("hugepan", dict(width=256, height=160, max_motion=40)),   # edge MBs: all fill
+    ("halfpel", dict(width=320, height=240, max_motion=5, odd_motion=True)),   # chroma bilinear
     ("hd720", dict(width=1280, height=720, max_motion=4)),
     ("fhd", dict(width=1920, height=1080, max_motion=8)),
 ]
@@ -153,6 +154,40 @@ def test_fused_and_unfused_paths_agree_with_oracle(tmp_path, k):
         assert np.array_equal(res.scores, ref["score"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(rgb, ref["rgb"])
+
+
+K6_STREAMS = [
+    ("q270", dict(width=480, height=270, max_motion=6, slices_per_row=2)),     # crop 2 rows
+    ("q540", dict(width=960, height=540, max_motion=24, slices_per_row=1)),    # crop 4, edge fills
+    ("nocrop", dict(width=384, height=192, max_motion=4, slices_per_row=0)),   # one slice/picture
+    ("halfpel6", dict(width=480, height=270, max_motion=7, odd_motion=True)),  # general path
+]
+
+
+@pytest.mark.parametrize("name,kw", K6_STREAMS, ids=[s[0] for s in K6_STREAMS])
+def test_k6_band_kernel_agrees_with_unfused_and_oracle(tmp_path, name, kw):
+    """k = 6 (1080p's thumbnail factor) fused into reconstruction: six-row
+    bands across macroblock rows, pixels straddling lanes, cropped rows
+    reconstructed but not scored."""
+    _require_gpu()
+    path = tmp_path / f"{name}.mp4"
+    n = 50
+    scene.synth_write(path, n_frames=n, cut_min_s=0.5, cut_max_s=1.0, gop_max_s=0.6,
+                      hash_frames=True, **kw)
+    frames, _ = oracle.decode_file(path)
+    W, H = kw["width"], kw["height"]
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 6)
+    for fused in (1, -1):
+        with scene.VideoScorer(path, k=6, fused=fused) as v:
+            assert v.fused() == (fused == 1)
+            res = v.score()
+            for i in range(n):
+                assert np.array_equal(v.frame_nv12(i).reshape(frames[i].shape), frames[i]), i
+            rgb = np.stack([v.thumbnail_rgb(i, 6) for i in range(n)]).reshape(-1)
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
         assert np.array_equal(rgb, ref["rgb"])
 
 

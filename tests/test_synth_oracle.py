@@ -23,6 +23,7 @@ STREAMS = [
     dict(width=336, height=200, slices_per_row=3, max_motion=6),   # ragged slices, crop
     dict(width=640, height=360, slices_per_row=2, max_motion=2),   # 360 = 22.5 MB rows: crop 8
     dict(width=96, height=64, max_motion=0),                       # static: P_Skip runs only
+    dict(width=320, height=240, max_motion=5, odd_motion=True),     # half-pel chroma bilinear
 ]
 
 

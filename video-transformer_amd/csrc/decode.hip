@@ -497,10 +497,13 @@ __device__ __forceinline__ uint4 fetch_row(const FrameRefs &F, uint64_t c, int r
       if (sx >= 0 && sx + 15 <= F.W - 1) {
         out = load16_any(row + sx);
       } else {
-        uint32_t wv[4] = {0, 0, 0, 0};
-        for (int b = 0; b < 16; ++b)
-          wv[b >> 2] |= uint32_t(row[clampi(sx + b, 0, F.W - 1)]) << (8 * (b & 3));
-        out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        uint64_t lo8 = 0, hi8 = 0;  // rolled: this path is rare, keep its registers few
+#pragma unroll 1
+        for (int b = 0; b < 16; ++b) {
+          const uint64_t v = row[clampi(sx + b, 0, F.W - 1)];
+          if (b < 8) lo8 |= v << (8 * b); else hi8 |= v << (8 * (b - 8));
+        }
+        out = make_uint4(uint32_t(lo8), uint32_t(lo8 >> 32), uint32_t(hi8), uint32_t(hi8 >> 32));
       }
     }
   } else {
@@ -521,28 +524,33 @@ __device__ __forceinline__ uint4 fetch_row(const FrameRefs &F, uint64_t c, int r
         if (cx >= 0 && cx + 7 <= F.CW - 1) {
           out = load16_any(row + 2 * cx);
         } else {
-          uint32_t wv[4] = {0, 0, 0, 0};
+          uint64_t lo8 = 0, hi8 = 0;
+#pragma unroll 1
           for (int b = 0; b < 8; ++b) {
             const int sx = clampi(cx + b, 0, F.CW - 1);
-            wv[b >> 1] |= (uint32_t(row[2 * sx]) | (uint32_t(row[2 * sx + 1]) << 8)) << (16 * (b & 1));
+            const uint64_t v = uint64_t(row[2 * sx]) | (uint64_t(row[2 * sx + 1]) << 8);
+            if (b < 4) lo8 |= v << (16 * b); else hi8 |= v << (16 * (b - 4));
           }
-          out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+          out = make_uint4(uint32_t(lo8), uint32_t(lo8 >> 32), uint32_t(hi8), uint32_t(hi8 >> 32));
         }
       } else {
         const uint8_t *ra = F.ref_uv + clampi(cy, 0, F.CH - 1) * F.pitch;
         const uint8_t *rb = F.ref_uv + clampi(cy + 1, 0, F.CH - 1) * F.pitch;
-        uint32_t wv[4] = {0, 0, 0, 0};
+        uint64_t lo8 = 0, hi8 = 0;
+#pragma unroll 1
         for (int b = 0; b < 8; ++b) {
           const int xa = clampi(cx + b, 0, F.CW - 1), xb = clampi(cx + b + 1, 0, F.CW - 1);
+          uint64_t pair = 0;
+#pragma unroll
           for (int pl = 0; pl < 2; ++pl) {
             const int A = ra[2 * xa + pl], B = ra[2 * xb + pl], C = rb[2 * xa + pl], D = rb[2 * xb + pl];
-            const uint32_t v = static_cast<uint32_t>(
+            const uint64_t v = static_cast<uint64_t>(
                 ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
-            const int byte = 2 * b + pl;
-            wv[byte >> 2] |= v << (8 * (byte & 3));
+            pair |= v << (8 * pl);
           }
+          if (b < 4) lo8 |= pair << (16 * b); else hi8 |= pair << (16 * (b - 4));
         }
-        out = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        out = make_uint4(uint32_t(lo8), uint32_t(lo8 >> 32), uint32_t(hi8), uint32_t(hi8 >> 32));
       }
     }
   }
@@ -560,6 +568,98 @@ __device__ __forceinline__ FrameRefs frame_refs(const ReconArgs &a, int ref_slot
   F.ref = ref_slot >= 0 ? a.surf + static_cast<int64_t>(ref_slot) * a.frame_stride : nullptr;
   F.ref_uv = F.ref ? F.ref + F.pitch * F.H : nullptr;
   return F;
+}
+
+// ---------------------------------------------- fast-path row source
+// One output row (16 bytes: luma row rin of the macroblock, or NV12 chroma
+// row rin) of an I_PCM or integer-pel-chroma inter macroblock, as a pair of
+// aligned loads issued now (issue_row) and a funnel shift done once they land
+// (finish_row).  shf = byte shift | mode << 8: mode 1/2 = left/right picture
+// edge (the edge-most aligned chunk against the replicated edge sample),
+// I_PCM chroma rows are 8-byte pairs of the planar Cb and Cr rows.
+__device__ __forceinline__ bool fast_cmd(const FrameRefs &F, uint64_t c) {
+  const uint32_t kind = static_cast<uint32_t>(c >> 62);
+  const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+  return kind == 1 || (kind == 2 && F.ref && ((mvx | mvy) & 7) == 0);
+}
+
+__device__ __forceinline__ void issue_row(const FrameRefs &F, const uint8_t *pcmb, bool pcm, bool chroma,
+                                          int rin, int m, int mby, int mvx, int mvy, uint4 &lo, uint4 &hi,
+                                          int &shf) {
+  if (pcm && chroma) {
+    const uint8_t *pu = pcmb + 256 + 8 * rin;  // Cr row is 64 B on
+    const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pu) & 7);
+    const uint2 *au = reinterpret_cast<const uint2 *>(pu - sh);
+    const uint2 u0 = au[0], u1 = au[1], v0 = au[8], v1 = au[9];
+    shf = sh;
+    lo = make_uint4(u0.x, u0.y, u1.x, u1.y);
+    hi = make_uint4(v0.x, v0.y, v1.x, v1.y);
+  } else {
+    const uint4 *pa;
+    int sh;
+    if (pcm) {
+      const uint8_t *p = pcmb + 16 * rin;
+      sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+      pa = reinterpret_cast<const uint4 *>(p - sh);
+    } else {
+      // row start (16-byte aligned: pitch and W are multiples of 16)
+      const uint8_t *row = chroma ? F.ref_uv + clampi(mby * 8 + rin + (mvy >> 3), 0, F.CH - 1) * F.pitch
+                                  : F.ref + clampi(mby * 16 + rin + (mvy >> 2), 0, F.H - 1) * F.pitch;
+      const int x0 = chroma ? 2 * (m * 8 + (mvx >> 3)) : m * 16 + (mvx >> 2);  // NV12 rows are W bytes
+      if (x0 < 0) {                  // left edge: [fill x16][row 0..15]
+        pa = reinterpret_cast<const uint4 *>(row);
+        sh = (x0 > -16 ? 16 + x0 : 0) | (1 << 8);
+      } else if (x0 > F.W - 16) {    // right edge: [row W-16..W-1][fill x16]
+        pa = reinterpret_cast<const uint4 *>(row + F.W - 16);
+        sh = min(x0 - (F.W - 16), 16) | (2 << 8);
+      } else {
+        const uint8_t *p = row + x0;
+        // pointer arithmetic (not an integer round trip) keeps the global
+        // address space, so these are global_load_dwordx4, not flat loads
+        sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+        pa = reinterpret_cast<const uint4 *>(p - sh);
+      }
+    }
+    shf = sh;
+    lo = ld_row(pa);
+    hi = ld_row(sh >> 8 ? pa : pa + 1);
+  }
+}
+
+// zero collects has_zero_byte of I_PCM samples (pcm): any zero byte means a
+// possible emulation-prevention pattern, checked exactly by the caller.
+__device__ __forceinline__ uint4 finish_row(bool chroma, bool pcm, uint4 lo, uint4 hi, int shf, uint32_t &zero) {
+  if (pcm && chroma) {
+    const int sh = shf & 7, qd = sh >> 2, r = sh & 3;
+    const uint32_t a0 = qd ? lo.y : lo.x, a1 = qd ? lo.z : lo.y, a2 = qd ? lo.w : lo.z;
+    const uint32_t b0 = qd ? hi.y : hi.x, b1 = qd ? hi.z : hi.y, b2 = qd ? hi.w : hi.z;
+    const uint32_t ux = __builtin_amdgcn_alignbyte(a1, a0, r), uy = __builtin_amdgcn_alignbyte(a2, a1, r);
+    const uint32_t vx = __builtin_amdgcn_alignbyte(b1, b0, r), vy = __builtin_amdgcn_alignbyte(b2, b1, r);
+    zero |= has_zero_byte(ux) | has_zero_byte(uy) | has_zero_byte(vx) | has_zero_byte(vy);
+    return interleave_uv(ux, uy, vx, vy);
+  }
+  if (!pcm && (shf >> 8)) {
+    // replicate the edge sample (a byte for luma, a Cb/Cr pair for NV12)
+    if ((shf >> 8) == 1) {
+      const uint32_t f = chroma ? (hi.x & 0xffffu) * 0x00010001u : (hi.x & 0xffu) * 0x01010101u;
+      lo = make_uint4(f, f, f, f);
+    } else {
+      const uint32_t g = chroma ? (lo.w >> 16) * 0x00010001u : (lo.w >> 24) * 0x01010101u;
+      hi = make_uint4(g, g, g, g);
+      if ((shf & 0xff) == 16) lo = hi;
+    }
+    shf &= 15;
+  }
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const int qd = (shf >> 2) & 3, r = shf & 3;
+  uint32_t t[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    t[j] = (qd == 0) ? w[j] : (qd == 1) ? w[j + 1] : (qd == 2) ? w[j + 2] : w[j + 3 < 8 ? j + 3 : 7];
+  const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                             __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+  if (pcm) zero |= has_zero_byte(v.x) | has_zero_byte(v.y) | has_zero_byte(v.z) | has_zero_byte(v.w);
+  return v;
 }
 
 // ------------------------------------------------ fused decode + scoring
@@ -808,6 +908,180 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
   if (errs) atomicOr(a.err, errs);
 }
 
+// h264_recon_score6: fused reconstruct + scoring for k = 6 (1080p: coded
+// 1920x1088, display 1920x1080, 320x180 thumbnails).  Six-row thumbnail
+// bands do not tile 16-row macroblocks, but 2-row pairs tile both, so a lane
+// owns two row pairs of one macroblock (luma rows 2p, 2p+1, 2p+8, 2p+9 and
+// chroma rows p, p+4; one command, 6 rows in flight like the k = 4 kernel)
+// and each pair lies in one band.  A workgroup covers 3 macroblock rows (48
+// rows = 8 bands) x 21 macroblock columns (336 pixels = 56 thumbnail
+// pixels); lanes add their partial box sums into LDS (Y, and U | V << 16),
+// then 112 threads turn the 8 x 56 pixel sums into RGB, thumbnail luma,
+// histogram and SAD.  Coded rows past the display height (1080..1087) are
+// reconstructed but not scored.
+constexpr int kK6Cols = 21, kK6Rows = 3;                 // macroblocks per workgroup
+constexpr int kK6Lanes = kK6Cols * kK6Rows * 4;          // 252 of 256 threads
+constexpr int kK6Px = kK6Cols * 16 / 6;                  // 56 thumbnail pixels per band row
+constexpr int kK6Bands = kK6Rows * 16 / 6;               // 8 bands
+
+__device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int w) {
+  // bytes [lo, hi) of a 16-byte chunk that fall in its 32-bit word w
+  const int a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
+  const uint32_t upto_b = b >= 4 ? 0xffffffffu : ((1u << (8 * b)) - 1u);
+  const uint32_t upto_a = a >= 4 ? 0xffffffffu : ((1u << (8 * a)) - 1u);
+  return upto_b & ~upto_a;
+}
+
+__global__ void __launch_bounds__(kReconThreads) h264_recon_score6(FusedArgs fa) {
+  constexpr int K = 6, HK = 3;
+  __shared__ uint32_t lds_y[kK6Bands * kK6Px], lds_uv[kK6Bands * kK6Px];
+  __shared__ uint32_t lds_hist[256];
+  __shared__ uint32_t red[kReconThreads / 64];
+  const ReconArgs &a = fa.r;
+  const int mbw = a.mb_width, mbh = a.mb_height, nmb = mbw * mbh;
+  const int cblocks = (mbw + kK6Cols - 1) / kK6Cols;
+  const int fi = blockIdx.x / fa.wgs_per_frame;
+  const int wb = blockIdx.x - fi * fa.wgs_per_frame;
+  const int rb = wb / cblocks, cb = wb - rb * cblocks;   // 3-MB-row block, 21-MB-column block
+  const int t = threadIdx.x;
+  const int cib = t % kK6Cols, rg = t / kK6Cols;          // column in block, row group 0..11
+  const int m = cb * kK6Cols + cib, mby = rb * kK6Rows + rg / 4, pp = rg % 4;
+  const bool active = t < kK6Lanes && m < mbw && mby < mbh;
+  const int4 fr = a.frames[fi];
+  const FrameRefs F = frame_refs(a, fr.y);
+  const int64_t gframe = fa.frame0 + fr.x;
+  const int64_t npx = static_cast<int64_t>(fa.w) * fa.h;
+  // command, and (finishing threads) the predecessor's thumbnail: in flight
+  // across the barrier that clears the LDS sums
+  const uint64_t c = active ? a.cmd[static_cast<int64_t>(fr.x) * nmb + static_cast<int64_t>(mby) * mbw + m] : 0;
+  constexpr int kFin = kK6Px / 4;                         // finishing threads per band
+  const int fband = rb * kK6Bands + t / kFin, fpx = cb * kK6Px + (t % kFin) * 4;
+  const bool fin = t < kK6Bands * kFin && fband < fa.h && fpx < fa.w;
+  uint32_t prevw = 0;
+  if (fin && fr.z >= 0)
+    prevw = *reinterpret_cast<const uint32_t *>(fa.thumb + static_cast<int64_t>(fr.z) * npx +
+                                                static_cast<int64_t>(fband) * fa.w + fpx);
+  for (int i = t; i < kK6Bands * kK6Px; i += kReconThreads) lds_y[i] = lds_uv[i] = 0;
+  lds_hist[t] = 0;  // kReconThreads == 256
+  __syncthreads();
+  uint32_t errs = 0;
+  if (active) {
+    uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
+    uint8_t *dst_uv = dst + F.pitch * F.H;
+    // rows: 0,1 = luma 2pp, 2pp+1; 2,3 = luma 2pp+8, 2pp+9; 4,5 = chroma pp, pp+4
+    uint4 rows[6];
+    const bool pcm = (c >> 62) == 1;
+    if (fast_cmd(F, c)) {
+      const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
+      const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+      uint4 lo[6], hi[6];
+      int shf[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+        issue_row(F, pcmb, pcm, i >= 4, i < 4 ? 2 * pp + (i & 1) + 8 * (i >> 1) : pp + 4 * (i - 4), m, mby,
+                  mvx, mvy, lo[i], hi[i], shf[i]);
+      uint32_t zero = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) rows[i] = finish_row(i >= 4, pcm, lo[i], hi[i], shf[i], zero);
+      if (pcm && zero) errs |= pcm_rows_epb(pcmb, pp, 2, 1) | pcm_rows_epb(pcmb, pp + 4, 2, 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        st_row(dst + static_cast<int64_t>(mby * 16 + 2 * pp + (i & 1) + 8 * (i >> 1)) * F.pitch + m * 16, rows[i]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        st_row(dst_uv + static_cast<int64_t>(mby * 8 + pp + 4 * i) * F.pitch + m * 16, rows[4 + i]);
+    } else {
+      // general path (sub-pel chroma, errors): rare; one row at a time
+      // (unrolled six times it cost 40 VGPRs and SGPR spills for the whole
+      // kernel), stored, then read back for scoring
+#pragma unroll 1
+      for (int i = 0; i < 6; ++i) {
+        const bool chroma = i >= 4;
+        const int r = chroma ? pp + 4 * (i - 4) : 2 * pp + (i & 1) + 8 * (i >> 1);
+        uint8_t *o = (chroma ? dst_uv + static_cast<int64_t>(mby * 8 + r) * F.pitch
+                             : dst + static_cast<int64_t>(mby * 16 + r) * F.pitch) + m * 16;
+        *reinterpret_cast<uint4 *>(o) = fetch_row(F, c, chroma ? 16 + r : r, m, mby, errs);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const bool chroma = i >= 4;
+        const int r = chroma ? pp + 4 * (i - 4) : 2 * pp + (i & 1) + 8 * (i >> 1);
+        const uint8_t *o = (chroma ? dst_uv + static_cast<int64_t>(mby * 8 + r) * F.pitch
+                                   : dst + static_cast<int64_t>(mby * 16 + r) * F.pitch) + m * 16;
+        rows[i] = *reinterpret_cast<const uint4 *>(o);
+      }
+    }
+    // partial box sums of the (up to 4) thumbnail pixels over this lane's 16
+    // columns, per row pair: pixel p of a 48-column triple covers bytes
+    // [6p, 6p + 6) of it, luma and NV12 chroma alike
+    const int j = m % 3, p0 = j == 0 ? 0 : (j == 1 ? 2 : 5);
+    const int pcol = (cib / 3) * 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int band = (mby * 8 + pp + 4 * h) / 3;       // = its luma rows' band
+      if (band >= fa.h) continue;
+      const int pbase = pcol + (band - rb * kK6Bands) * kK6Px;
+      const uint32_t l0[4] = {rows[2 * h].x, rows[2 * h].y, rows[2 * h].z, rows[2 * h].w};
+      const uint32_t l1[4] = {rows[2 * h + 1].x, rows[2 * h + 1].y, rows[2 * h + 1].z, rows[2 * h + 1].w};
+      const uint32_t ch[4] = {rows[4 + h].x, rows[4 + h].y, rows[4 + h].z, rows[4 + h].w};
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        const int p = p0 + sl;
+        if (p >= 8 || (j != 1 && sl == 3)) continue;
+        const int lo_b = 6 * p - 16 * j, hi_b = lo_b + 6;
+        uint32_t ys = 0, us = 0, vs = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const uint32_t mk = byte_mask(lo_b, hi_b, w);
+          ys = sad_u8(l0[w] & mk, 0u, sad_u8(l1[w] & mk, 0u, ys));
+          us = sad_u8(ch[w] & mk & 0x00ff00ffu, 0u, us);
+          vs = sad_u8(ch[w] & mk & 0xff00ff00u, 0u, vs);
+        }
+        atomicAdd(&lds_y[pbase + p], ys);
+        atomicAdd(&lds_uv[pbase + p], us | (vs << 16));
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t sad = 0;
+  if (fin) {
+    const int li = (fband - rb * kK6Bands) * kK6Px + (t % kFin) * 4;
+    uint32_t rgb24[4], packed = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint32_t uv = lds_uv[li + p];
+      const uint32_t y = (lds_y[li + p] + K * K / 2) / (K * K);
+      const uint32_t u = ((uv & 0xffffu) + HK * HK / 2) / (HK * HK), v = ((uv >> 16) + HK * HK / 2) / (HK * HK);
+      rgb24[p] = bt709_rgb24(y, u, v);
+      packed |= y << (8 * p);
+      atomicAdd(&lds_hist[y], 1u);
+    }
+    const int64_t tpx = static_cast<int64_t>(fband) * fa.w + fpx;
+    store_rgb<4>(fa.rgb + (gframe * npx + tpx) * 3, rgb24);
+    *reinterpret_cast<uint32_t *>(fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx) = packed;
+    if (fr.z >= 0) sad = sad_u8(packed, prevw, 0u);
+  }
+  if (fr.z >= 0) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sad += __shfl_xor(sad, off, 64);
+    if ((t & 63) == 0) red[t >> 6] = sad;
+  }
+  __syncthreads();
+  if (fr.z >= 0 && t == 0) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kReconThreads / 64; ++i) s += red[i];
+    atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(s));
+  }
+  if (t < 128) {
+    const uint64_t lo = lds_hist[2 * t], hi = lds_hist[2 * t + 1];
+    if (lo | hi)
+      atomicAdd(reinterpret_cast<unsigned long long *>(fa.hist + gframe * 256) + t,
+                static_cast<unsigned long long>(lo | (hi << 32)));
+  }
+  if (errs) atomicOr(a.err, errs);
+}
+
 // SAD of each frame's thumbnail luma against its predecessor's (the previous
 // window's last thumbnail for the window's first frame) and the score.  One
 // workgroup per frame; 16-byte loads, all of a thread's loads issued before
@@ -895,6 +1169,14 @@ int parse_launch(const ParseArgs &a, hipStream_t s) {
 
 int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
+  if (k == 6) {
+    FusedArgs b = a;
+    b.wgs_per_frame = ((a.r.mb_width + kK6Cols - 1) / kK6Cols) * ((a.r.mb_height + kK6Rows - 1) / kK6Rows);
+    hipLaunchKernelGGL(h264_recon_score6, dim3(n_frames * b.wgs_per_frame), dim3(kReconThreads), 0, s, b);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score6 launch: %s", hipGetErrorString(e));
+    return VTS_OK;
+  }
   const int q = (k == 0) ? 4 : 16 / k;
   const int nmb = a.r.mb_width * a.r.mb_height;
   const int mb_per_wg = kReconThreads / q;

@@ -162,10 +162,14 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   c->frame_stride = (static_cast<int64_t>(c->pitch) * c->coded_h * 3 / 2 + 4095) & ~int64_t(4095);
   c->k = c->params.k > 0 ? c->params.k : (c->height <= 720 ? 4 : 6);
   {
-    const bool can_fuse = (c->k == 2 || c->k == 4 || c->k == 8) && c->width == c->coded_w &&
-                          c->height == c->coded_h;
+    // h264_recon_score<k>: k in {2,4,8}, display = coded size;
+    // h264_recon_score6: k = 6, any cropping, thumbnail width % 8 == 0
+    const bool can_fuse = ((c->k == 2 || c->k == 4 || c->k == 8) && c->width == c->coded_w &&
+                           c->height == c->coded_h) ||
+                          (c->k == 6 && (c->width / 6) % 8 == 0);
     if (c->params.fused > 0 && !can_fuse)
-      return fail(VTS_E_UNSUPPORTED, "fused scoring needs k in {2,4,8} and no cropping");
+      return fail(VTS_E_UNSUPPORTED,
+                  "fused scoring needs k in {2,4,8} without cropping, or k = 6 with thumbnail width % 8 == 0");
     c->fused = can_fuse && c->params.fused >= 0;
   }
   c->n_frames = static_cast<int64_t>(t.size.size());

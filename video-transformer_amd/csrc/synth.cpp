@@ -322,8 +322,9 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
     return fail(VTS_E_INVALID, "bad size %dx%d", P.width, P.height);
   if (P.fps_num <= 0 || P.fps_den <= 0 || P.n_frames <= 0)
     return fail(VTS_E_INVALID, "bad frame rate or frame count");
-  if (P.max_motion < 0 || (P.max_motion & 1) || P.max_motion > 64)
-    return fail(VTS_E_INVALID, "max_motion must be even, 0..64");
+  const bool odd_pans = (P.edge_cases & 2) != 0;
+  if (P.max_motion < 0 || ((P.max_motion & 1) && !odd_pans) || P.max_motion > 64)
+    return fail(VTS_E_INVALID, "max_motion must be even, 0..64 (odd needs edge_cases bit 1)");
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int cw = mbw * 16, ch = mbh * 16;
   const double fps = double(P.fps_num) / P.fps_den;
@@ -350,7 +351,7 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
   int64_t since_idr = 0, n_idr = 0, n_cuts = 0;
   uint64_t recon_hash = 0;
   int frame_num = 0, idr_pic_id = 0;
-  int vx = 0, vy = 0;  // luma pixels per frame (even)
+  int vx = 0, vy = 0;  // luma pixels per frame (even unless odd_pans)
   const int spr = P.slices_per_row;
   const int slice_mbs = spr > 0 ? (mbw + spr - 1) / spr : mbw * mbh;
   std::vector<uint8_t> sample;
@@ -363,15 +364,21 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
       ++n_cuts;
     }
     if (f % P.fps_num == 0 || cut) {  // new velocity about once a second
-      const int m = P.max_motion / 2;
-      vx = 2 * (static_cast<int>(rng.below(2 * m + 1)) - m);
-      vy = 2 * (static_cast<int>(rng.below(2 * m + 1)) - m);
+      if (odd_pans) {
+        const int m = P.max_motion;
+        vx = static_cast<int>(rng.below(2 * m + 1)) - m;
+        vy = static_cast<int>(rng.below(2 * m + 1)) - m;
+      } else {
+        const int m = P.max_motion / 2;
+        vx = 2 * (static_cast<int>(rng.below(2 * m + 1)) - m);
+        vy = 2 * (static_cast<int>(rng.below(2 * m + 1)) - m);
+      }
       if (rng.below(4) == 0) vx = vy = 0;  // static stretches -> P_Skip runs
     }
     const bool idr = cut || since_idr >= gop_max;
     std::swap(cur, ref);  // ref = previous reconstruction
     if (cut) {
-      fill_texture(cur, tex_rng, P.pcm_zero_runs != 0);
+      fill_texture(cur, tex_rng, (P.edge_cases & 1) != 0);
     } else if (idr) {
       for (int my = 0; my < mbh; ++my)
         for (int mx = 0; mx < mbw; ++mx) mc_mb(ref, cur, mx, my, 4 * vx, 4 * vy);
