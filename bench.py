@@ -21,8 +21,12 @@ Rank 0 prints ONE JSON line (contract in the task statement), including
 from __future__ import annotations
 
 import argparse
+import csv
 import json
 import os
+import re
+import shutil
+import subprocess
 import sys
 import tempfile
 import time
@@ -146,6 +150,54 @@ def cpu_baseline_decode_score(path, k, budget_s=15.0):
                       f"or_score_frames, GOP-parallel on {threads} threads, {dt:.1f} s"}
 
 
+def _kernel_short(name: str) -> str:
+    m = re.search(r"(h264_recon_score6|h264_\w+|thumb_sad|score_\w+)(<\d+>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name.split("(")[0][-60:]
+
+
+def pmc_traffic(argv: list[str], out_dir: Path) -> dict:
+    """HBM bytes per dispatch of every scoring/decode kernel, from two
+    rocprofv3 --pmc passes over a short run of this same benchmark
+    (FETCH_SIZE and WRITE_SIZE cannot share a pass: 3 + 2 TCC slots > 4).
+    Per MI355X_MICROARCH.md (HBM): bytes = 2 x FETCH_SIZE (gfx950 tallies
+    wide coalesced reads at half their bytes) + WRITE_SIZE, both in KiB.
+
+    Runs as child processes BEFORE this process initialises the GPU (no
+    exec from a GPU-initialised process), each under its own time limit."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not Path(prof).exists():
+        return {"error": "rocprofv3 not found"}
+    res: dict = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = out_dir / counter
+        cmd = [prof, "--kernel-trace", "--pmc", counter, "--output-format", "csv", "-d", str(d),
+               "-o", "run", "--", sys.executable, str(Path(__file__).resolve()), *argv,
+               "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-pmc"]
+        try:
+            proc = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True,
+                                  timeout=150)
+        except subprocess.TimeoutExpired:
+            return {"error": f"{counter} pass timed out"}
+        if proc.returncode != 0:
+            return {"error": f"{counter} pass rc={proc.returncode}: {proc.stderr[-300:]}"}
+        acc: dict = {}
+        for f in d.rglob("*counter_collection.csv"):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    if r["Counter_Name"] != counter:
+                        continue
+                    acc.setdefault(_kernel_short(r["Kernel_Name"]), []).append(
+                        float(r["Counter_Value"]))
+        for k, v in acc.items():
+            res.setdefault(k, {})[counter] = sum(v) / len(v)
+            res[k]["dispatches"] = len(v)
+    for k, row in res.items():
+        if "FETCH_SIZE" in row and "WRITE_SIZE" in row:
+            row["hbm_bytes"] = (2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024
+    return res
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -162,12 +214,26 @@ def main() -> None:
                     help="GOPs per reconstruct launch; <= 0 all GOPs of the window")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with several ranks on one GPU")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    pmc = None
+    if world == 1 and not args.no_pmc:
+        # before anything touches the GPU: the passes are child processes
+        child_argv = ["--workload", args.workload, "--config", args.config,
+                      "--gops-per-launch", str(args.gops_per_launch)]
+        for opt in ("frames", "width", "height"):
+            if getattr(args, opt) is not None:
+                child_argv += [f"--{opt}", str(getattr(args, opt))]
+        pmc_dir = Path(tempfile.mkdtemp(prefix="vtseg_pmc_", dir="/tmp"))
+        pmc = pmc_traffic(child_argv, pmc_dir)
+        shutil.rmtree(pmc_dir, ignore_errors=True)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
@@ -289,7 +355,7 @@ def main() -> None:
         if fused:
             # dominant kernel = h264_recon_score (decode + score in one pass)
             kern_ms = rec_ms
-            kname = "h264_recon_score<%d>" % k
+            kname = "h264_recon_score6" if k == 6 else "h264_recon_score<%d>" % k
         else:
             kern_ms = float(np.mean([t["score_ms"] for t in times]))
             kname = "score_runs<%d>" % k
@@ -300,8 +366,19 @@ def main() -> None:
         bytes_per_frame = algorithmic_bytes_per_frame(width, height, k)
         frames_per_launch = F
     achieved = bytes_per_frame * frames_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_note = None, None
+    if pmc is not None:
+        row = pmc.get(kname) if "error" not in pmc else None
+        if row and "hbm_bytes" in row:
+            traffic = round(row["hbm_bytes"])
+            traffic_note = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (2xFETCH+WRITE), "
+                            f"mean of {row['dispatches']} dispatches; "
+                            f"{traffic / (bytes_per_frame * frames_per_launch):.3f}x algorithmic")
+        else:
+            traffic_note = pmc.get("error", f"no counters for {kname}")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_unit": "bytes/launch", "traffic_source": traffic_note,
             "kernel": kname, "kernel_ms": round(kern_ms, 4),
             "bytes_per_frame": bytes_per_frame,
             "frames_per_launch": round(frames_per_launch, 1)}

@@ -293,3 +293,15 @@ def recon_hash(frames: np.ndarray) -> int:
     w = (np.arange(flat.shape[1], dtype=np.uint64) % np.uint64(65521)) + np.uint64(1)
     per = (flat * w).sum(axis=1, dtype=np.uint64)
     return int((per * (np.arange(F, dtype=np.uint64) + np.uint64(1))).sum(dtype=np.uint64))
+
+
+def slice_commands(nal: bytes | np.ndarray, nal_abs: int, prm: "H264Params", have_ref: bool,
+                   cmd_frame: np.ndarray) -> int:
+    """or_slice_commands: the oracle parser's per-macroblock command words for
+    one slice NAL (checker of the device parser).  Returns 0 or a negative code."""
+    L = lib()
+    L.or_slice_commands.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int,
+                                    C.c_void_p]
+    buf = np.frombuffer(bytes(nal), np.uint8)
+    return L.or_slice_commands(C.byref(prm), buf.ctypes.data, len(buf), int(nal_abs),
+                               1 if have_ref else 0, cmd_frame.ctypes.data)

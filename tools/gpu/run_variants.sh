@@ -12,7 +12,7 @@ cp $LIB gpurun_out/lib_intree.so
 for pass in $(seq ${PASSES:-2}); do
   for v in "$@"; do
     cp tools/exp/lib_$v.so $LIB
-    timeout -k 10 300 python bench.py --no-cpu-baseline $ARGS > gpurun_out/var_$v.json 2> gpurun_out/var_$v.err || { tail -20 gpurun_out/var_$v.err; exit 1; }
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-pmc $ARGS > gpurun_out/var_$v.json 2> gpurun_out/var_$v.err || { tail -20 gpurun_out/var_$v.err; exit 1; }
     python - "$v" <<'PY'
 import json,sys
 d=json.load(open(f"gpurun_out/var_{sys.argv[1]}.json"))

@@ -28,349 +28,26 @@
 #include "common.h"
 #include "decode.h"
 #include "h264.h"
+#include "parse_slice.h"
 #include "pixel.h"
 
 namespace vts {
 namespace {
 
-// ------------------------------------------------------------ bit reader
-// Reads an EBSP (NAL payload after the header byte) from global memory through
-// a 16-byte register cache, removing emulation_prevention_three_byte.
-struct DevBits {
-  const uint8_t *base;   // first payload byte (absolute pointer)
-  int64_t abs0;          // byte offset of `base` inside the ES buffer
-  int32_t size;          // payload bytes
-  int32_t pos;           // next byte index to fetch
-  int32_t bitpos;        // bits left in `cur`
-  int32_t zeros;         // consecutive zero bytes before `pos`
-  uint32_t cur;
-  int32_t cache_at;      // payload index of cache[0], -1 none
-  uint32_t cache[4];
-  bool err;
-
-  __device__ void init(const uint8_t *p, int64_t abs, int32_t n) {
-    base = p;
-    abs0 = abs;
-    size = n;
-    pos = 0;
-    bitpos = 0;
-    zeros = 0;
-    cur = 0;
-    cache_at = -1;
-    err = false;
-  }
-  __device__ uint32_t byte_at(int32_t i) {
-    const int32_t blk = i & ~15;
-    if (blk != cache_at) {
-      // 16-byte aligned within the payload is not 16-byte aligned in memory;
-      // load the enclosing aligned dwords instead.
-      const uint8_t *pb = base + blk;
-      const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pb) & 3);
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(pb - sh);  // global, not flat
-      uint32_t t[5];
-#pragma unroll
-      for (int k = 0; k < 5; ++k) t[k] = w[k];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        cache[k] = sh ? __builtin_amdgcn_alignbyte(t[k + 1], t[k], sh) : t[k];
-      cache_at = blk;
-    }
-    const int32_t o = i - blk;
-    return (cache[o >> 2] >> (8 * (o & 3))) & 0xffu;
-  }
-  __device__ void next_byte() {
-    if (pos >= size) {
-      err = true;
-      cur = 0;
-      bitpos = 8;
-      return;
-    }
-    uint32_t b = byte_at(pos);
-    if (zeros >= 2 && b == 3) {  // emulation prevention byte
-      ++pos;
-      zeros = 0;
-      if (pos >= size) {
-        err = true;
-        cur = 0;
-        bitpos = 8;
-        return;
-      }
-      b = byte_at(pos);
-    }
-    ++pos;
-    zeros = (b == 0) ? zeros + 1 : 0;
-    cur = b;
-    bitpos = 8;
-  }
-  __device__ uint32_t bit() {
-    if (bitpos == 0) next_byte();
-    --bitpos;
-    return (cur >> bitpos) & 1u;
-  }
-  __device__ uint32_t bits(int n) {
-    uint32_t v = 0;
-    for (int i = 0; i < n; ++i) v = (v << 1) | bit();
-    return v;
-  }
-  __device__ uint32_t ue() {
-    int lz = 0;
-    while (bit() == 0) {
-      if (++lz > 31 || err) {
-        err = true;
-        return 0;
-      }
-    }
-    return lz ? ((1u << lz) - 1u + bits(lz)) : 0u;
-  }
-  __device__ int32_t se() {
-    const uint32_t k = ue();
-    return (k & 1u) ? static_cast<int32_t>((k + 1) >> 1) : -static_cast<int32_t>(k >> 1);
-  }
-  __device__ void align() { bitpos = 0; }  // pcm_alignment_zero_bits
-  // Skip n raw bytes at a byte-aligned position (I_PCM samples).  Assumes no
-  // emulation-prevention byte inside them (checked by h264_recon).
-  __device__ void skip_bytes(int32_t n) {
-    pos += n;
-    if (pos > size) {
-      err = true;
-      return;
-    }
-    const uint32_t b1 = byte_at(pos - 1), b2 = byte_at(pos - 2);
-    zeros = (b1 != 0) ? 0 : ((b2 != 0) ? 1 : 2);
-  }
-  // absolute bit index of the next bit to read (EBSP domain)
-  __device__ int64_t bit_index() const {
-    return bitpos ? (int64_t(pos - 1) * 8 + (8 - bitpos)) : int64_t(pos) * 8;
-  }
-};
-
-__device__ __forceinline__ int median3(int a, int b, int c) {
-  return max(min(a, b), min(max(a, b), c));
-}
-
-struct Nb {
-  bool avail;
-  int ref;
-  int mvx, mvy;
-};
-
-__device__ __forceinline__ Nb nb_from_cmd(uint64_t c) {
-  Nb n{true, -1, 0, 0};
-  if ((c >> 62) == 2) {
-    n.ref = 0;
-    n.mvx = static_cast<int16_t>(c & 0xffff);
-    n.mvy = static_cast<int16_t>((c >> 16) & 0xffff);
-  }
-  return n;
-}
-
-__global__ void __launch_bounds__(64) h264_parse(ParseArgs a) {
+#ifndef VTS_PARSE_WAVES
+#define VTS_PARSE_WAVES 0
+#endif
+#if VTS_PARSE_WAVES
+#define VTS_PARSE_OCC __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES)))
+#else
+#define VTS_PARSE_OCC
+#endif
+// one lane per slice NAL
+__global__ void __launch_bounds__(64) VTS_PARSE_OCC h264_parse(ParseArgs a) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.n_slices) return;
   const SliceDesc sd = a.slices[s];
-  const H264DevParams &P = a.prm;
-  const int nmb = P.mb_width * P.mb_height;
-  uint64_t *cmd = a.cmd + static_cast<int64_t>(sd.slot) * nmb;
-  uint32_t errs = 0;
-
-  const uint8_t *nal = a.es + sd.nal_offset;
-  const uint32_t hdr = nal[0];
-  const int nal_type = hdr & 0x1f, nal_ref_idc = (hdr >> 5) & 3;
-  DevBits br;
-  br.init(nal + 1, sd.nal_offset + 1, sd.nal_size - 1);
-  // stop bit (rbsp_trailing_bits): last non-zero byte of the NAL
-  int32_t last = sd.nal_size - 1;
-  while (last > 0 && nal[last] == 0) --last;
-  if (last <= 0) {
-    atomicOr(a.err, static_cast<uint32_t>(DEC_E_SYNTAX));
-    return;
-  }
-  const uint32_t lb = nal[last];
-  const int tz = __builtin_ctz(lb);
-  const int64_t stop_bit = int64_t(last - 1) * 8 + (7 - tz);  // payload domain
-
-  // ---- slice_header (7.3.3)
-  const int first_mb = static_cast<int>(br.ue());
-  int slice_type = static_cast<int>(br.ue());
-  if (slice_type > 4) slice_type -= 5;
-  const int pps_id = static_cast<int>(br.ue());
-  if (pps_id != P.pps_id) errs |= DEC_E_PPS;
-  br.bits(P.log2_max_frame_num);  // frame_num
-  if (nal_type == 5) br.ue();      // idr_pic_id
-  if (P.poc_type == 0) {
-    br.bits(P.log2_max_poc_lsb);
-    if (P.bottom_field_pic_order_in_frame_present) br.se();
-  } else if (P.poc_type == 1 && !P.delta_pic_order_always_zero) {
-    br.se();
-    if (P.bottom_field_pic_order_in_frame_present) br.se();
-  }
-  if (P.redundant_pic_cnt_present) {
-    if (br.ue() != 0) errs |= DEC_E_SYNTAX;  // redundant slices are not decoded
-  }
-  const bool is_p = (slice_type == 0);
-  if (!is_p && slice_type != 2) errs |= DEC_E_SLICE_TYPE;
-  int num_ref = P.num_ref_idx_l0_default_active;
-  if (is_p) {
-    if (br.bit()) num_ref = static_cast<int>(br.ue()) + 1;  // override
-    if (br.bit()) errs |= DEC_E_REFLIST;                     // ref_pic_list_modification
-    if (num_ref != 1) errs |= DEC_E_MULTIREF;
-    if (sd.ref_slot < 0) errs |= DEC_E_NO_REF;
-  }
-  if (nal_ref_idc != 0) {  // dec_ref_pic_marking
-    if (nal_type == 5) {
-      br.bit();
-      br.bit();
-    } else if (br.bit()) {
-      errs |= DEC_E_MMCO;
-    }
-  }
-  const int qp = P.pic_init_qp + br.se();
-  int deblock_idc = 0, alpha_off = 0;
-  if (P.deblocking_filter_control_present) {
-    deblock_idc = static_cast<int>(br.ue());
-    if (deblock_idc != 1) {
-      alpha_off = 2 * br.se();
-      br.se();
-    }
-  }
-  // Filtering is a no-op only if disabled or every edge's indexA < 16
-  // (alpha' = 0): max qPav is the slice QP (I_PCM has qP 0).
-  if (deblock_idc != 1 && qp + alpha_off >= 16) errs |= DEC_E_DEBLOCK;
-  if (first_mb < 0 || first_mb >= nmb) errs |= DEC_E_SYNTAX;
-  if (errs || br.err) {
-    atomicOr(a.err, errs | (br.err ? DEC_E_SYNTAX : 0u));
-    return;
-  }
-
-  // ---- slice_data (7.3.4), CAVLC
-  int addr = first_mb;
-  Nb left{false, -1, 0, 0};  // neighbour A of the current MB within the slice
-  bool more = true;
-  const int mbw = P.mb_width;
-  while (more && addr < nmb) {
-    int skip = 0;
-    if (is_p) {
-      skip = static_cast<int>(br.ue());  // mb_skip_run
-      if (br.err || addr + skip > nmb) {
-        errs |= DEC_E_SYNTAX;
-        break;
-      }
-      for (int i = 0; i < skip; ++i, ++addr) {
-        // P_Skip motion (8.4.1.1)
-        const int x = addr % mbw, y = addr / mbw;
-        const bool a_ok = x > 0 && addr - 1 >= first_mb;
-        const bool b_ok = y > 0 && addr - mbw >= first_mb;
-        Nb A = a_ok ? left : Nb{false, -1, 0, 0};
-        Nb B = b_ok ? nb_from_cmd(cmd[addr - mbw]) : Nb{false, -1, 0, 0};
-        int mvx = 0, mvy = 0;
-        if (a_ok && b_ok && !(A.ref == 0 && A.mvx == 0 && A.mvy == 0) &&
-            !(B.ref == 0 && B.mvx == 0 && B.mvy == 0)) {
-          const bool c_ok = y > 0 && x < mbw - 1 && addr - mbw + 1 >= first_mb;
-          const bool d_ok = y > 0 && x > 0 && addr - mbw - 1 >= first_mb;
-          Nb C = c_ok ? nb_from_cmd(cmd[addr - mbw + 1])
-                      : (d_ok ? nb_from_cmd(cmd[addr - mbw - 1]) : Nb{false, -1, 0, 0});
-          const int match = (A.ref == 0) + (B.ref == 0) + (C.ref == 0);
-          if (match == 1) {
-            const Nb &m = (A.ref == 0) ? A : (B.ref == 0) ? B : C;
-            mvx = m.mvx;
-            mvy = m.mvy;
-          } else {
-            mvx = median3(A.mvx, B.mvx, C.mvx);
-            mvy = median3(A.mvy, B.mvy, C.mvy);
-          }
-        }
-        if ((mvx & 3) || (mvy & 3)) errs |= DEC_E_SUBPEL;
-        const uint64_t c = MB_INTER | (uint64_t(uint16_t(mvx))) | (uint64_t(uint16_t(mvy)) << 16);
-        cmd[addr] = c;
-        left = Nb{true, 0, mvx, mvy};
-      }
-      if (skip > 0) more = br.bit_index() < stop_bit;
-      if (!more || addr >= nmb) break;
-    }
-    // ---- I_PCM run speculation: in an I slice, once byte-aligned after an
-    // I_PCM macroblock, the next headers sit at a 386-byte stride (mb_type 25
-    // = 9 bits + 7 alignment zeros = 0x0D 0x00, then 384 samples).  Load up to
-    // 8 predicted headers at once, verify them in order, commit the matching
-    // prefix; anything unexpected falls through to the serial parse below.
-    if (!is_p && br.bitpos == 0 && addr > first_mb) {
-      uint32_t hb0[8], hb1[8];
-      int cand = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int64_t q = static_cast<int64_t>(br.pos) + 386 * j;
-        if ((q + 386) * 8 <= stop_bit && addr + j < nmb) {
-          hb0[j] = nal[1 + q];
-          hb1[j] = nal[2 + q];
-          cand = j + 1;
-        }
-      }
-      int ok = 0;
-      for (int j = 0; j < cand; ++j) {
-        if (hb0[j] != 0x0D || hb1[j] != 0x00) break;
-        ok = j + 1;
-      }
-      if (ok > 0 && br.zeros < 2) {
-        for (int j = 0; j < ok; ++j)
-          cmd[addr + j] = MB_PCM | static_cast<uint64_t>(br.abs0 + br.pos + 386 * j + 2);
-        addr += ok;
-        left = Nb{true, -1, 0, 0};
-        br.pos += 386 * ok;
-        br.zeros = 0;
-        const uint32_t b1 = br.byte_at(br.pos - 1), b2 = br.byte_at(br.pos - 2);
-        br.zeros = (b1 != 0) ? 0 : ((b2 != 0) ? 1 : 2);
-        more = br.bit_index() < stop_bit;
-        continue;
-      }
-    }
-    // ---- macroblock_layer (7.3.5)
-    const int mb_type = static_cast<int>(br.ue());
-    const int x = addr % mbw, y = addr / mbw;
-    if ((!is_p && mb_type == 25) || (is_p && mb_type == 30)) {
-      br.align();
-      // an emulation-prevention byte right at the PCM start would shift it
-      if (br.zeros >= 2 && br.pos < br.size && br.byte_at(br.pos) == 3) errs |= DEC_E_EPB_IN_PCM;
-      const int64_t off = br.abs0 + br.pos;
-      br.skip_bytes(384);
-      cmd[addr] = MB_PCM | static_cast<uint64_t>(off);
-      left = Nb{true, -1, 0, 0};
-    } else if (is_p && mb_type == 0) {
-      // P_L0_16x16: ref_idx_l0 absent (single reference), mvd_l0, cbp
-      const int mvdx = br.se(), mvdy = br.se();
-      const uint32_t cbp_code = br.ue();
-      if (cbp_code != 0) errs |= DEC_E_RESIDUAL;
-      const bool a_ok = x > 0 && addr - 1 >= first_mb;
-      const bool b_ok = y > 0 && addr - mbw >= first_mb;
-      const bool c_ok = y > 0 && x < mbw - 1 && addr - mbw + 1 >= first_mb;
-      const bool d_ok = y > 0 && x > 0 && addr - mbw - 1 >= first_mb;
-      Nb A = a_ok ? left : Nb{false, -1, 0, 0};
-      Nb B = b_ok ? nb_from_cmd(cmd[addr - mbw]) : Nb{false, -1, 0, 0};
-      Nb C = c_ok ? nb_from_cmd(cmd[addr - mbw + 1])
-                  : (d_ok ? nb_from_cmd(cmd[addr - mbw - 1]) : Nb{false, -1, 0, 0});
-      if (!B.avail && !C.avail && A.avail) B = C = A;
-      int px, py;
-      const int match = (A.ref == 0) + (B.ref == 0) + (C.ref == 0);
-      if (match == 1) {
-        const Nb &m = (A.ref == 0) ? A : (B.ref == 0) ? B : C;
-        px = m.mvx;
-        py = m.mvy;
-      } else {
-        px = median3(A.mvx, B.mvx, C.mvx);
-        py = median3(A.mvy, B.mvy, C.mvy);
-      }
-      const int mvx = px + mvdx, mvy = py + mvdy;
-      if ((mvx & 3) || (mvy & 3)) errs |= DEC_E_SUBPEL;
-      if (mvx < -32768 || mvx > 32767 || mvy < -32768 || mvy > 32767) errs |= DEC_E_SYNTAX;
-      cmd[addr] = MB_INTER | (uint64_t(uint16_t(mvx))) | (uint64_t(uint16_t(mvy)) << 16);
-      left = Nb{true, 0, mvx, mvy};
-    } else {
-      errs |= DEC_E_MB_TYPE;
-      break;
-    }
-    ++addr;
-    if (br.err) break;
-    more = br.bit_index() < stop_bit;
-  }
-  if (br.err) errs |= DEC_E_SYNTAX;
+  const uint32_t errs = parse_slice(a.es, sd.nal_offset, sd.nal_size, sd.slot, sd.ref_slot, a.prm, a.cmd);
   if (errs) atomicOr(a.err, errs);
 }
 
