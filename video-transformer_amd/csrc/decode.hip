@@ -361,6 +361,25 @@ __device__ __forceinline__ uint4 finish_row(bool chroma, bool pcm, uint4 lo, uin
 #define VTS_OCCUPANCY
 #endif
 
+// XCD-aware block order (cdna_hip_programming.md T1, bijective form):
+// blocks are dealt round-robin over the 8 XCDs, so remap them so that each
+// XCD walks a contiguous range of tiles.  Horizontally adjacent 64-macroblock
+// tiles share the 128-byte lines at their seams (the misaligned second load of
+// a motion-shifted row); on one XCD the neighbour finds them in its L2.
+// Speed only: any placement is correct.
+#ifndef VTS_XCD_SWZ
+#define VTS_XCD_SWZ 1
+#endif
+__device__ __forceinline__ int xcd_block(int b, int n) {
+#if VTS_XCD_SWZ
+  const int q = n >> 3, r = n & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+#else
+  (void)n;
+  return b;
+#endif
+}
+
 template <int K>
 __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(FusedArgs fa) {
   constexpr int KK = K ? K : 4;      // rows per group
@@ -371,9 +390,10 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
   __shared__ uint32_t lds_hist[256];
   const ReconArgs &a = fa.r;
   const int mbw = a.mb_width, mbh = a.mb_height, nmb = mbw * mbh;
-  const int fi = blockIdx.x / fa.wgs_per_frame;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int fi = bid / fa.wgs_per_frame;
   const int q = threadIdx.x / MB_PER_WG;
-  const int mb = (blockIdx.x - fi * fa.wgs_per_frame) * MB_PER_WG + (threadIdx.x % MB_PER_WG);
+  const int mb = (bid - fi * fa.wgs_per_frame) * MB_PER_WG + (threadIdx.x % MB_PER_WG);
   const int4 fr = a.frames[fi];
   const FrameRefs F = frame_refs(a, fr.y);
   const int64_t gframe = fa.frame0 + fr.x;
@@ -617,8 +637,9 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score6(FusedArgs fa)
   const ReconArgs &a = fa.r;
   const int mbw = a.mb_width, mbh = a.mb_height, nmb = mbw * mbh;
   const int cblocks = (mbw + kK6Cols - 1) / kK6Cols;
-  const int fi = blockIdx.x / fa.wgs_per_frame;
-  const int wb = blockIdx.x - fi * fa.wgs_per_frame;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int fi = bid / fa.wgs_per_frame;
+  const int wb = bid - fi * fa.wgs_per_frame;
   const int rb = wb / cblocks, cb = wb - rb * cblocks;   // 3-MB-row block, 21-MB-column block
   const int t = threadIdx.x;
   const int cib = t % kK6Cols, rg = t / kK6Cols;          // column in block, row group 0..11
