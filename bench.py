@@ -214,6 +214,8 @@ def main() -> None:
                     help="GOPs per reconstruct launch; <= 0 all GOPs of the window")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with several ranks on one GPU")
+    ap.add_argument("--parse-chunks", type=int, default=1,
+                    help="slice-parse chunks overlapped with reconstruction (1 = none, the default)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
     args = ap.parse_args()
@@ -223,7 +225,8 @@ def main() -> None:
     if world == 1 and not args.no_pmc:
         # before anything touches the GPU: the passes are child processes
         child_argv = ["--workload", args.workload, "--config", args.config,
-                      "--gops-per-launch", str(args.gops_per_launch)]
+                      "--gops-per-launch", str(args.gops_per_launch),
+                      "--parse-chunks", str(args.parse_chunks)]
         for opt in ("frames", "width", "height"):
             if getattr(args, opt) is not None:
                 child_argv += [f"--{opt}", str(getattr(args, opt))]
@@ -282,7 +285,8 @@ def main() -> None:
         path = Path(tmpdir) / f"synth_rank{rank}.mp4"
         scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
                           seed=0x5EED + rank)
-        scorer = scene.VideoScorer(path, device=gpu, gops_per_launch=args.gops_per_launch)
+        scorer = scene.VideoScorer(path, device=gpu, gops_per_launch=args.gops_per_launch,
+                                   parse_chunks=args.parse_chunks)
         duration_s = float(scorer.info.duration)
 
         def step():

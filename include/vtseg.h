@@ -205,7 +205,9 @@ typedef struct vts_params {
                               reconstruction (k in {2,4,8}, no cropping)       */
   int32_t gops_per_launch; /* GOPs decoded together per reconstruct launch;
                               <= 0 = all GOPs of the window (fastest measured) */
-  int32_t _pad;
+  int32_t parse_chunks;    /* slice parsing on its own stream in N chunks of
+                              launches, chunk j+1 overlapping reconstruction of
+                              chunk j; <= 1 (default) = one parse launch */
 } vts_params;
 
 /* Demux the file's first H.264 video track on the host (MP4 boxes and NAL

@@ -9,5 +9,6 @@ extern "C" uint32_t ph_parse_slice(const uint8_t *es, int64_t nal_offset, int32_
   vts::H264DevParams P{};
   int32_t *dst = &P.mb_width;  // the POD's int32 fields in declaration order
   for (int i = 0; i < 13; ++i) dst[i] = prm14[i];
-  return vts::parse_slice(es, nal_offset, nal_size, slot, ref_slot, P, cmd_all);
+  vts::ParseScratch scratch{};
+  return vts::parse_slice(es, nal_offset, nal_size, slot, ref_slot, P, cmd_all, &scratch);
 }

@@ -44,10 +44,12 @@ namespace {
 #endif
 // one lane per slice NAL
 __global__ void __launch_bounds__(64) VTS_PARSE_OCC h264_parse(ParseArgs a) {
+  __shared__ ParseScratch scratch[64];
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= a.n_slices) return;
   const SliceDesc sd = a.slices[s];
-  const uint32_t errs = parse_slice(a.es, sd.nal_offset, sd.nal_size, sd.slot, sd.ref_slot, a.prm, a.cmd);
+  const uint32_t errs = parse_slice(a.es, sd.nal_offset, sd.nal_size, sd.slot, sd.ref_slot, a.prm, a.cmd,
+                                    &scratch[threadIdx.x]);
   if (errs) atomicOr(a.err, errs);
 }
 

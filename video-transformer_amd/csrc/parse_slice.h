@@ -51,11 +51,14 @@ struct WinBits {
   int32_t zeros;         // consecutive zero bytes before pos (capped at 2)
   int32_t epb;           // emulation-prevention bytes removed so far
   int32_t epb_next;      // RBSP byte index that followed the last removed EPB
-  int32_t cache_at;      // payload index of c0 (multiple of 16), -1 none
-  uint32_t c0, c1, c2, c3, c4;  // 20 payload bytes from cache_at (no array: stays in VGPRs)
+  int32_t cache_at;      // payload index of cache[0] (multiple of 16), -1 none
+  uint32_t *cache;       // 5 words = 20 payload bytes from cache_at: per-lane
+                         // scratch (LDS on the device), so the copies at every
+                         // control-flow join that register state costs are avoided
   bool err;
 
-  VTS_HD VTS_INLINE void init(const uint8_t *p, int64_t abs, int32_t n) {
+  VTS_HD VTS_INLINE void init(const uint8_t *p, int64_t abs, int32_t n, uint32_t *scratch) {
+    cache = scratch;
     base = p;
     abs0 = abs;
     size = n;
@@ -74,20 +77,15 @@ struct WinBits {
       const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pb) & 3);
       const uint32_t *w = reinterpret_cast<const uint32_t *>(pb - sh);  // global, not flat
       const uint32_t t0 = w[0], t1 = w[1], t2 = w[2], t3 = w[3], t4 = w[4], t5 = w[5];
-      c0 = sh ? vts_alignbyte(t1, t0, sh) : t0;
-      c1 = sh ? vts_alignbyte(t2, t1, sh) : t1;
-      c2 = sh ? vts_alignbyte(t3, t2, sh) : t2;
-      c3 = sh ? vts_alignbyte(t4, t3, sh) : t3;
-      c4 = sh ? vts_alignbyte(t5, t4, sh) : t4;
+      cache[0] = sh ? vts_alignbyte(t1, t0, sh) : t0;
+      cache[1] = sh ? vts_alignbyte(t2, t1, sh) : t1;
+      cache[2] = sh ? vts_alignbyte(t3, t2, sh) : t2;
+      cache[3] = sh ? vts_alignbyte(t4, t3, sh) : t3;
+      cache[4] = sh ? vts_alignbyte(t5, t4, sh) : t4;
       cache_at = blk;
     }
-    // dword select by masks, not ?: on members (which the compiler turns
-    // into a select of addresses and so keeps the whole reader in scratch)
     const int32_t o = i - blk, q = o >> 2, r = o & 3;
-    const uint32_t m0 = 0u - (q == 0), m1 = 0u - (q == 1), m2 = 0u - (q == 2), m3 = 0u - (q == 3);
-    const uint32_t a = (c0 & m0) | (c1 & m1) | (c2 & m2) | (c3 & m3);
-    const uint32_t b = (c1 & m0) | (c2 & m1) | (c3 & m2) | (c4 & m3);
-    return vts_alignbyte(b, a, r);
+    return vts_alignbyte(cache[q + 1], cache[q], r);
   }
   VTS_HD VTS_INLINE void refill() {  // requires nb <= 32
     const uint32_t v = load4(pos);
@@ -221,30 +219,31 @@ VTS_HD VTS_INLINE Nb nb_from_cmd(uint64_t c) {
 // (slice edges) fall back to 8-byte stores.
 struct CmdWriter {
   uint64_t *cmd;      // frame base
+  Cmd2 *e;            // the open group's 4 commands: per-lane scratch (LDS on the device)
   int64_t gbase;      // absolute index (slot * nmb) of cmd[0], for alignment
   int32_t g;          // first frame-relative index of the open group
   uint32_t mask;
-  uint64_t e0, e1, e2, e3;
 
-  VTS_HD VTS_INLINE void init(uint64_t *c, int64_t gb) {
+  VTS_HD VTS_INLINE void init(uint64_t *c, int64_t gb, Cmd2 *scratch) {
     cmd = c;
+    e = scratch;
     gbase = gb;
     g = -1;
     mask = 0;
-    e0 = e1 = e2 = e3 = 0;
   }
   VTS_HD VTS_INLINE void flush() {
     if (!mask) return;
     uint64_t *p = cmd + g;
     if (mask == 0xfu) {
       Cmd2 *q = reinterpret_cast<Cmd2 *>(p);  // two 16-byte stores
-      q[0] = Cmd2{e0, e1};
-      q[1] = Cmd2{e2, e3};
+      q[0] = e[0];
+      q[1] = e[1];
     } else {
-      if (mask & 1u) p[0] = e0;
-      if (mask & 2u) p[1] = e1;
-      if (mask & 4u) p[2] = e2;
-      if (mask & 8u) p[3] = e3;
+      const uint64_t *el = reinterpret_cast<const uint64_t *>(e);
+      if (mask & 1u) p[0] = el[0];
+      if (mask & 2u) p[1] = el[1];
+      if (mask & 4u) p[2] = el[2];
+      if (mask & 8u) p[3] = el[3];
     }
     mask = 0;
   }
@@ -255,40 +254,41 @@ struct CmdWriter {
       flush();
       g = ga;
     }
-    // masked updates, not a branch per entry (kept the entries in scratch)
-    const uint64_t k0 = 0ull - (j == 0), k1 = 0ull - (j == 1), k2 = 0ull - (j == 2), k3 = 0ull - (j == 3);
-    e0 = (c & k0) | (e0 & ~k0);
-    e1 = (c & k1) | (e1 & ~k1);
-    e2 = (c & k2) | (e2 & ~k2);
-    e3 = (c & k3) | (e3 & ~k3);
+    reinterpret_cast<uint64_t *>(e)[j] = c;
     mask |= 1u << j;
     if (j == 3) flush();
   }
   // command of an earlier macroblock of the slice (neighbour B / C / D)
   VTS_HD VTS_INLINE uint64_t get(int32_t addr) const {
-    if (mask && addr >= g && addr < g + 4) {
-      const int32_t j = addr - g;
-      const uint64_t k0 = 0ull - (j == 0), k1 = 0ull - (j == 1), k2 = 0ull - (j == 2), k3 = 0ull - (j == 3);
-      return (e0 & k0) | (e1 & k1) | (e2 & k2) | (e3 & k3);
-    }
-    return cmd[addr];
+    // both loads, then a select of values: a select of the two pointers
+    // would make one flat load (LDS or global)
+    const uint64_t in_group = reinterpret_cast<const uint64_t *>(e)[(addr - g) & 3];
+    const uint64_t in_memory = cmd[addr];
+    return (mask && addr >= g && addr < g + 4) ? in_group : in_memory;
   }
 };
 
 // Parse one slice NAL (header byte at es + nal_offset, nal_size bytes) of the
 // frame in `slot` into cmd_all[slot * nmb + mb].  Returns DEC_E_* bits.
+// `scratch` is the lane's private ParseScratch (LDS in h264_parse).
+struct ParseScratch {
+  Cmd2 cmd[2];         // open command group
+  uint32_t cache[6];   // bit reader's byte cache (5 words used)
+};
+
 VTS_HD VTS_INLINE uint32_t parse_slice(const uint8_t *es, int64_t nal_offset, int32_t nal_size, int32_t slot,
-                                       int32_t ref_slot, const H264DevParams &P, uint64_t *cmd_all) {
+                                       int32_t ref_slot, const H264DevParams &P, uint64_t *cmd_all,
+                                       ParseScratch *scratch) {
   const int nmb = P.mb_width * P.mb_height;
   CmdWriter out;
-  out.init(cmd_all + static_cast<int64_t>(slot) * nmb, static_cast<int64_t>(slot) * nmb);
+  out.init(cmd_all + static_cast<int64_t>(slot) * nmb, static_cast<int64_t>(slot) * nmb, scratch->cmd);
   uint32_t errs = 0;
 
   const uint8_t *nal = es + nal_offset;
   const uint32_t hdr = nal[0];
   const int nal_type = hdr & 0x1f, nal_ref_idc = (hdr >> 5) & 3;
   WinBits br;
-  br.init(nal + 1, nal_offset + 1, nal_size - 1);
+  br.init(nal + 1, nal_offset + 1, nal_size - 1, scratch->cache);
   // stop bit (rbsp_trailing_bits): last non-zero byte of the NAL
   int32_t last = nal_size - 1;
   while (last > 0 && nal[last] == 0) --last;

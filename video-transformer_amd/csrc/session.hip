@@ -52,9 +52,12 @@ constexpr int64_t kPad = 256;
 
 struct Window {
   int64_t f0 = 0, f1 = 0;          // frames [f0, f1)
-  int64_t s0 = 0, s1 = 0;          // slices [s0, s1)
-  std::vector<int64_t> lvl_off;    // into level_frames
+  int64_t s0 = 0, s1 = 0;          // slices [s0, s1), ordered by reconstruct launch
+  std::vector<int64_t> lvl_off;    // into level_frames, one entry per reconstruct launch
   std::vector<int32_t> lvl_cnt;
+  std::vector<int64_t> lvl_s0;     // first slice (absolute) of each launch's frames
+  std::vector<int32_t> chunk_end;  // parse chunk j covers launches [chunk_end[j-1], chunk_end[j])
+  int64_t ev0 = 0;                 // first index of this window's events in vts_ctx::lev
   int64_t post_off = 0, post_cnt = 0;  // into post_slots
 };
 
@@ -97,8 +100,9 @@ struct vts_ctx {
   bool fused = false;             // scoring fused into reconstruction
   uint8_t *d_thumb[2] = {nullptr, nullptr};  // fused: [slot][h][w] thumbnail luma
   int64_t thumb_px = 0;
-  hipStream_t s_dec = nullptr, s_score = nullptr;
-  std::vector<hipEvent_t> ev;  // per window: dec0, dec1, sc0, sc1
+  hipStream_t s_dec = nullptr, s_score = nullptr, s_parse = nullptr;
+  std::vector<hipEvent_t> ev;  // per window: dec start, parsed, decoded, score start, scored, spare
+  std::vector<hipEvent_t> lev;  // per window: (start, end) per reconstruct launch, then one per parse chunk
   hipEvent_t ev_start = nullptr, ev_end = nullptr;
   double timings[4] = {0, 0, 0, 0};
   int64_t last_window_done = -1;
@@ -286,6 +290,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   c->n_rings = (c->windows.size() > 1 && c->params.n_streams >= 2) ? 2 : 1;
 
   // slice slots / ref slots and per-level frame lists
+  std::vector<int32_t> launch_of(static_cast<size_t>(c->n_frames), 0);  // launch index within its window
   for (Window &w : c->windows) {
     w.s0 = first_slice[w.f0];
     w.s1 = (w.f1 < c->n_frames) ? first_slice[w.f1] : static_cast<int64_t>(c->slices.size());
@@ -333,12 +338,52 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
       }
       for (auto &l : lv) {
         if (l.empty()) continue;
+        for (const int4 &e : l) launch_of[static_cast<size_t>(w.f0 + e.x)] = static_cast<int32_t>(w.lvl_off.size());
         w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
         w.lvl_cnt.push_back(static_cast<int32_t>(l.size()));
         c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
       }
     }
     (void)maxl;
+    // Slices in launch order (stable: decode order within a launch), so the
+    // slices of launches [a, b) are one contiguous range that a parse chunk
+    // can cover while reconstruction of earlier launches runs.
+    {
+      const int64_t nl = static_cast<int64_t>(w.lvl_off.size());
+      std::vector<int64_t> cnt(static_cast<size_t>(nl) + 1, 0);
+      for (int64_t x = w.f0; x < w.f1; ++x) cnt[static_cast<size_t>(launch_of[x]) + 1] += n_slices[x];
+      for (int64_t l = 0; l < nl; ++l) cnt[l + 1] += cnt[l];
+      w.lvl_s0.resize(static_cast<size_t>(nl));
+      for (int64_t l = 0; l < nl; ++l) w.lvl_s0[l] = w.s0 + cnt[l];
+      std::vector<SliceDesc> sorted(static_cast<size_t>(w.s1 - w.s0));
+      std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+      for (int64_t x = w.f0; x < w.f1; ++x)
+        for (int64_t sl = first_slice[x]; sl < first_slice[x] + n_slices[x]; ++sl)
+          sorted[static_cast<size_t>(fill[launch_of[x]]++)] = c->slices[sl];
+      std::copy(sorted.begin(), sorted.end(), c->slices.begin() + w.s0);
+      // Parse chunks: the first covers launch 0 alone (reconstruction starts
+      // as soon as the intra pictures are parsed), the rest split the other
+      // launches into runs of about equal slice counts.
+      // Default one chunk: overlapping measured no gain on MI355X (the
+      // parser's VALU work slows the concurrent reconstruction by as much as
+      // it hides, profiles/r01_parse_overlap_ab.txt)
+      const int want = c->params.parse_chunks > 0 ? c->params.parse_chunks : 1;
+      if (want <= 1 || nl <= 1) {
+        w.chunk_end.push_back(static_cast<int32_t>(nl));
+      } else {
+        w.chunk_end.push_back(1);
+        const int64_t rest = cnt[nl] - cnt[1];
+        const int64_t per = std::max<int64_t>(1, (rest + want - 2) / (want - 1));
+        int64_t acc = 0;
+        for (int64_t l = 1; l < nl; ++l) {
+          acc += cnt[l + 1] - cnt[l];
+          if (acc >= per || l == nl - 1) {
+            w.chunk_end.push_back(static_cast<int32_t>(l + 1));
+            acc = 0;
+          }
+        }
+      }
+    }
     // thumb_sad pass: frames without a fused SAD, plus the window's last
     // frame (its thumbnail seeds the next window)
     w.post_off = static_cast<int64_t>(c->post_slots.size());
@@ -380,8 +425,16 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   HIP_TRY(hipMalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
   HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->s_parse, hipStreamNonBlocking));
   c->ev.resize(c->windows.size() * 6);
   for (auto &e2 : c->ev) HIP_TRY(hipEventCreate(&e2));
+  int64_t nlev = 0;
+  for (Window &w : c->windows) {
+    w.ev0 = nlev;
+    nlev += 2 * static_cast<int64_t>(w.lvl_off.size()) + static_cast<int64_t>(w.chunk_end.size());
+  }
+  c->lev.resize(static_cast<size_t>(nlev));
+  for (auto &e2 : c->lev) HIP_TRY(hipEventCreate(&e2));
   HIP_TRY(hipEventCreate(&c->ev_start));
   HIP_TRY(hipEventCreate(&c->ev_end));
   return VTS_OK;
@@ -428,20 +481,41 @@ int run_all(vts_ctx *c) {
   for (size_t wi = 0; wi < nw; ++wi) {
     const Window &w = c->windows[wi];
     const int r = static_cast<int>(wi % c->n_rings);
-    hipEvent_t *E = &c->ev[wi * 6];  // 0 dec start, 1 parsed, 2 decoded, 3 score start, 4 scored
-    if (wi >= static_cast<size_t>(c->n_rings))
+    hipEvent_t *E = &c->ev[wi * 6];  // 0 parse start, 1 parsed, 2 decoded, 3 score start, 4 scored
+    hipEvent_t *LE = &c->lev[static_cast<size_t>(w.ev0)];  // per launch (start, end), then per chunk
+    const size_t nl = w.lvl_off.size();
+    hipStream_t sp = c->s_parse;
+    // the ring's command / surface buffers are free once the window that used
+    // them two steps ago has been scored
+    if (wi >= static_cast<size_t>(c->n_rings)) {
       HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
-    HIP_TRY(hipEventRecord(E[0], sd));
-    HIP_TRY(hipMemsetAsync(c->d_cmd[r], 0, static_cast<size_t>((w.f1 - w.f0) * nmb * 8), sd));
-    ParseArgs pa{};
-    pa.es = c->d_es;
-    pa.slices = c->d_slices + w.s0;
-    pa.n_slices = static_cast<int32_t>(w.s1 - w.s0);
-    pa.cmd = c->d_cmd[r];
-    pa.err = c->d_err;
-    pa.prm = c->prm;
-    VTS_TRY(parse_launch(pa, sd));
-    HIP_TRY(hipEventRecord(E[1], sd));
+      HIP_TRY(hipStreamWaitEvent(sp, c->ev[(wi - c->n_rings) * 6 + 4], 0));
+    }
+    // Slice parsing on its own stream in chunks of launches: the parser is
+    // latency-bound (one lane per slice), reconstruction HBM-bound, so parsing
+    // chunk j+1 overlaps reconstructing the launches of chunk j.
+    HIP_TRY(hipStreamWaitEvent(sp, c->ev_start, 0));
+    HIP_TRY(hipEventRecord(E[0], sp));
+    HIP_TRY(hipMemsetAsync(c->d_cmd[r], 0, static_cast<size_t>((w.f1 - w.f0) * nmb * 8), sp));
+    {
+      ParseArgs pa{};
+      pa.es = c->d_es;
+      pa.cmd = c->d_cmd[r];
+      pa.err = c->d_err;
+      pa.prm = c->prm;
+      int32_t l0 = 0;
+      for (size_t j = 0; j < w.chunk_end.size(); ++j) {
+        const int32_t l1 = w.chunk_end[j];
+        const int64_t a0 = w.lvl_s0[l0];
+        const int64_t a1 = (static_cast<size_t>(l1) < nl) ? w.lvl_s0[l1] : w.s1;
+        pa.slices = c->d_slices + a0;
+        pa.n_slices = static_cast<int32_t>(a1 - a0);
+        VTS_TRY(parse_launch(pa, sp));
+        HIP_TRY(hipEventRecord(LE[2 * nl + j], sp));
+        l0 = l1;
+      }
+    }
+    HIP_TRY(hipEventRecord(E[1], sp));
     ReconArgs ra{};
     ra.es = c->d_es;
     ra.cmd = c->d_cmd[r];
@@ -452,11 +526,11 @@ int run_all(vts_ctx *c) {
     ra.mb_height = c->sps.mb_height;
     ra.err = c->d_err;
     const int tw = c->width / c->k, th = c->height / c->k;
+    FusedArgs fa{};
     if (c->fused) {
       HIP_TRY(hipMemsetAsync(c->d_hist + w.f0 * 256, 0,
                              sizeof(uint32_t) * 256 * static_cast<size_t>(w.f1 - w.f0), sd));
       HIP_TRY(hipMemsetAsync(c->d_sad + w.f0, 0, sizeof(uint64_t) * static_cast<size_t>(w.f1 - w.f0), sd));
-      FusedArgs fa{};
       fa.r = ra;
       fa.frame0 = w.f0;
       fa.w = tw;
@@ -466,15 +540,24 @@ int run_all(vts_ctx *c) {
       fa.rgb = c->d_rgb;
       fa.hist = c->d_hist;
       fa.sad = c->d_sad;
-      for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+    }
+    size_t j = 0;
+    for (size_t l = 0; l < nl; ++l) {
+      if (l == 0 || static_cast<int32_t>(l) == w.chunk_end[j - 1]) {
+        HIP_TRY(hipStreamWaitEvent(sd, LE[2 * nl + j++], 0));  // this launch's slices are parsed
+        // reconstruct span starts once its first launch may run (a timing
+        // event between launches costs ~25 us on ROCm, so only at chunk edges)
+        HIP_TRY(hipEventRecord(LE[2 * l], sd));
+      }
+      if (c->fused) {
         fa.r.frames = c->d_levels + w.lvl_off[l];
         VTS_TRY(fused_launch(fa, c->k, w.lvl_cnt[l], sd));
-      }
-    } else {
-      for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+      } else {
         ra.frames = c->d_levels + w.lvl_off[l];
         VTS_TRY(recon_launch(ra, w.lvl_cnt[l], sd));
       }
+      if (l + 1 == nl || static_cast<int32_t>(l + 1) == w.chunk_end[j - 1])
+        HIP_TRY(hipEventRecord(LE[2 * l + 1], sd));
     }
     HIP_TRY(hipEventRecord(E[2], sd));
     HIP_TRY(hipStreamWaitEvent(ss, E[2], 0));
@@ -529,13 +612,23 @@ int run_all(vts_ctx *c) {
   c->timings[1] = c->timings[2] = c->timings[3] = 0;
   for (size_t wi = 0; wi < nw; ++wi) {
     hipEvent_t *E = &c->ev[wi * 6];
-    float a = 0, b = 0, s = 0;
+    float a = 0, s = 0;
     HIP_TRY(hipEventElapsedTime(&a, E[0], E[1]));
-    HIP_TRY(hipEventElapsedTime(&b, E[1], E[2]));
     HIP_TRY(hipEventElapsedTime(&s, E[3], E[4]));
     c->timings[1] += a;
-    c->timings[2] += b;
     c->timings[3] += s;
+    // reconstruct: the spans of each chunk's launches on the decode stream
+    // (from after the wait for the chunk's parse to its last launch), so
+    // waits for parsing are not counted as kernel time
+    const Window &w = c->windows[wi];
+    const hipEvent_t *LE = &c->lev[static_cast<size_t>(w.ev0)];
+    int32_t l0 = 0;
+    for (int32_t l1 : w.chunk_end) {
+      float b = 0;
+      HIP_TRY(hipEventElapsedTime(&b, LE[2 * l0], LE[2 * (l1 - 1) + 1]));
+      c->timings[2] += b;
+      l0 = l1;
+    }
   }
   c->last_window_done = static_cast<int64_t>(nw) - 1;
   if (err) {
@@ -699,6 +792,7 @@ extern "C" int vts_close(vts_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->s_dec) (void)hipStreamSynchronize(c->s_dec);
   if (c->s_score) (void)hipStreamSynchronize(c->s_score);
+  if (c->s_parse) (void)hipStreamSynchronize(c->s_parse);
   auto f = [](void *p) {
     if (p) (void)hipFree(p);
   };
@@ -720,10 +814,13 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_rgb);
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto e : c->lev)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);
   if (c->s_dec) (void)hipStreamDestroy(c->s_dec);
   if (c->s_score) (void)hipStreamDestroy(c->s_score);
+  if (c->s_parse) (void)hipStreamDestroy(c->s_parse);
   delete c;
   return VTS_OK;
 }

@@ -106,7 +106,7 @@ class VideoScorer:
     def __init__(self, path: str | Path, device: int = 0, *, k: int = 0,
                  window_frames: int = 0, n_streams: int = 2,
                  cut_threshold: float = DEFAULT_CUT_THRESHOLD, fused: int = 0,
-                 gops_per_launch: int = 0):
+                 gops_per_launch: int = 0, parse_chunks: int = 0):
         self._lib = _lib.lib()
         prm = _lib.Params()
         prm.k = k
@@ -116,6 +116,7 @@ class VideoScorer:
         prm.cut_threshold = cut_threshold
         prm.fused = fused
         prm.gops_per_launch = gops_per_launch
+        prm.parse_chunks = parse_chunks
         ctx = C.c_void_p()
         _lib.check(self._lib.vts_open(int(device), str(path).encode(), C.byref(prm),
                                       C.byref(ctx)))
