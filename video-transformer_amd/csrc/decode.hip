@@ -619,8 +619,9 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
 // histogram and SAD.  Coded rows past the display height (1080..1087) are
 // reconstructed but not scored.
 constexpr int kK6Cols = 21, kK6Rows = 3;                 // macroblocks per workgroup
-constexpr int kK6Lanes = kK6Cols * kK6Rows * 4;          // 252 of 256 threads
-constexpr int kK6Px = kK6Cols * 16 / 6;                  // 56 thumbnail pixels per band row
+constexpr int kK6Threads = 256;
+constexpr int kK6Lanes = kK6Cols * kK6Rows * 4;          // 252 lanes used
+constexpr int kK6Px = kK6Cols * 16 / 6;                  // thumbnail pixels per band row
 constexpr int kK6Bands = kK6Rows * 16 / 6;               // 8 bands
 
 __device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int w) {
@@ -631,11 +632,19 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int w) {
   return upto_b & ~upto_a;
 }
 
-__global__ void __launch_bounds__(kReconThreads) h264_recon_score6(FusedArgs fa) {
+#ifndef VTS_K6_WAVES
+#define VTS_K6_WAVES 0
+#endif
+#if VTS_K6_WAVES
+#define VTS_K6_OCC __attribute__((amdgpu_waves_per_eu(VTS_K6_WAVES)))
+#else
+#define VTS_K6_OCC
+#endif
+__global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC h264_recon_score6(FusedArgs fa) {
   constexpr int K = 6, HK = 3;
   __shared__ uint32_t lds_y[kK6Bands * kK6Px], lds_uv[kK6Bands * kK6Px];
   __shared__ uint32_t lds_hist[256];
-  __shared__ uint32_t red[kReconThreads / 64];
+  __shared__ uint32_t red[kK6Threads / 64];
   const ReconArgs &a = fa.r;
   const int mbw = a.mb_width, mbh = a.mb_height, nmb = mbw * mbh;
   const int cblocks = (mbw + kK6Cols - 1) / kK6Cols;
@@ -644,9 +653,12 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score6(FusedArgs fa)
   const int wb = bid - fi * fa.wgs_per_frame;
   const int rb = wb / cblocks, cb = wb - rb * cblocks;   // 3-MB-row block, 21-MB-column block
   const int t = threadIdx.x;
+  // (a 768-thread layout with one wave per row group on 60 consecutive
+  // macroblocks measured 34% slower: one workgroup per CU, profiles/r01_k6_layout_ab.txt)
   const int cib = t % kK6Cols, rg = t / kK6Cols;          // column in block, row group 0..11
+  const bool lane_ok = t < kK6Lanes;
   const int m = cb * kK6Cols + cib, mby = rb * kK6Rows + rg / 4, pp = rg % 4;
-  const bool active = t < kK6Lanes && m < mbw && mby < mbh;
+  const bool active = lane_ok && m < mbw && mby < mbh;
   const int4 fr = a.frames[fi];
   const FrameRefs F = frame_refs(a, fr.y);
   const int64_t gframe = fa.frame0 + fr.x;
@@ -661,8 +673,8 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score6(FusedArgs fa)
   if (fin && fr.z >= 0)
     prevw = *reinterpret_cast<const uint32_t *>(fa.thumb + static_cast<int64_t>(fr.z) * npx +
                                                 static_cast<int64_t>(fband) * fa.w + fpx);
-  for (int i = t; i < kK6Bands * kK6Px; i += kReconThreads) lds_y[i] = lds_uv[i] = 0;
-  lds_hist[t] = 0;  // kReconThreads == 256
+  for (int i = t; i < kK6Bands * kK6Px; i += kK6Threads) lds_y[i] = lds_uv[i] = 0;
+  if (t < 256) lds_hist[t] = 0;
   __syncthreads();
   uint32_t errs = 0;
   if (active) {
@@ -770,7 +782,7 @@ __global__ void __launch_bounds__(kReconThreads) h264_recon_score6(FusedArgs fa)
   if (fr.z >= 0 && t == 0) {
     uint64_t s = 0;
 #pragma unroll
-    for (int i = 0; i < kReconThreads / 64; ++i) s += red[i];
+    for (int i = 0; i < kK6Threads / 64; ++i) s += red[i];
     atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(s));
   }
   if (t < 128) {
@@ -872,7 +884,7 @@ int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s) {
   if (k == 6) {
     FusedArgs b = a;
     b.wgs_per_frame = ((a.r.mb_width + kK6Cols - 1) / kK6Cols) * ((a.r.mb_height + kK6Rows - 1) / kK6Rows);
-    hipLaunchKernelGGL(h264_recon_score6, dim3(n_frames * b.wgs_per_frame), dim3(kReconThreads), 0, s, b);
+    hipLaunchKernelGGL(h264_recon_score6, dim3(n_frames * b.wgs_per_frame), dim3(kK6Threads), 0, s, b);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score6 launch: %s", hipGetErrorString(e));
     return VTS_OK;
