@@ -12,6 +12,7 @@
  * Entry point → reference interface it replaces:
  *   vts_plan_segments      utils/video_segmenter.py:42-83   plan_segments
  *   vts_plan_with_budget   utils/budget_planner.py:73-194   plan_segments_with_budget
+ *   vts_manifest_json      utils/video_segmenter.py:170-218 create_manifest + save_manifest text
  *   vts_probe_duration     utils/video_utils.py:7-38        probe_duration (ffprobe format=duration)
  *   vts_probe_info         utils/video_utils.py:7-38        (same probe, all stream facts)
  *   vts_extract_segment    utils/video_segmenter.py:86-154  extract_segment (ffmpeg -c copy)
@@ -76,6 +77,26 @@ typedef struct vts_segment {
 int vts_plan_segments(double duration, double segment_seconds,
                       double overlap_seconds, vts_segment *out, int64_t cap,
                       int64_t *n_out);
+
+/* Manifest JSON (create_manifest + save_manifest, video_segmenter.py:170-218):
+ * the text json.dumps(manifest, indent=2, ensure_ascii=True) writes, with the
+ * plan from vts_plan_segments.  *_int: the caller's int object's decimal repr
+ * (Python ints print as ints: SegmentPlan fields, an int duration), NULL for a
+ * float.  segment_dir: str(get_segment_dir(...)) (pathlib-normalised).
+ * Two-call size query like vts_plan_segments; VTS_E_INVALID for non-UTF-8. */
+typedef struct vts_manifest_args {
+  const char *video_id;
+  const char *segment_dir;
+  const char *created_at;
+  double duration;
+  const char *duration_int;
+  double segment_seconds;
+  const char *segment_seconds_int;
+  double overlap_seconds;
+  const char *overlap_seconds_int;
+} vts_manifest_args;
+
+int vts_manifest_json(const vts_manifest_args *args, char *out, int64_t cap, int64_t *len);
 
 /* Budget-planner inputs after the reference's _coerce_int/_coerce_bool and
  * float(threshold) (budget_planner.py:20-40, 95-103); the host mirror does the

@@ -107,6 +107,14 @@ class SynthInfo(C.Structure):
                 ("timescale", C.c_int64), ("recon_hash", C.c_uint64)]
 
 
+class ManifestArgs(C.Structure):
+    _fields_ = [("video_id", C.c_char_p), ("segment_dir", C.c_char_p),
+                ("created_at", C.c_char_p), ("duration", C.c_double),
+                ("duration_int", C.c_char_p), ("segment_seconds", C.c_double),
+                ("segment_seconds_int", C.c_char_p), ("overlap_seconds", C.c_double),
+                ("overlap_seconds_int", C.c_char_p)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/vtseg.h
 _P = C.POINTER
 SIGNATURES: dict[str, tuple] = {
@@ -115,6 +123,7 @@ SIGNATURES: dict[str, tuple] = {
     "vts_plan_with_budget": (C.c_int, [C.c_double, _P(BudgetCfg), C.c_int64, _P(Plan)]),
     "vts_boundary_frames_pts": (C.c_int, [_P(C.c_int64), C.c_int64, C.c_int64,
                                           _P(C.c_double), C.c_int64, _P(C.c_int64)]),
+    "vts_manifest_json": (C.c_int, [_P(ManifestArgs), C.c_char_p, C.c_int64, _P(C.c_int64)]),
     "vts_probe_duration": (C.c_int, [C.c_char_p, _P(C.c_double)]),
     "vts_probe_info": (C.c_int, [C.c_char_p, _P(VideoInfo)]),
     "vts_extract_segment": (C.c_int, [C.c_char_p, C.c_double, C.c_double, C.c_char_p]),

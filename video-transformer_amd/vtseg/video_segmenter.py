@@ -219,8 +219,56 @@ def create_manifest(
         "overlap_seconds": overlap_seconds,
         "segments": entries,
     }
-    save_manifest(get_manifest_path(video_id, temp_dir), manifest)
+    path = get_manifest_path(video_id, temp_dir)
+    text = manifest_json(video_id=video_id, duration=duration,
+                         segment_seconds=segment_seconds, overlap_seconds=overlap_seconds,
+                         segment_dir=segment_dir, created_at=manifest["created_at"])
+    if text is None:  # objects only Python's json knows how to print (or refuse)
+        save_manifest(path, manifest)
+    else:
+        path.parent.mkdir(parents=True, exist_ok=True)
+        _ = path.write_text(text, encoding="utf-8")
     return manifest
+
+
+def _num_arg(value: object) -> tuple[float, bytes | None] | None:
+    """(double, int repr) for the number types the native writer prints the
+    way json.dumps does: int (not bool) and float; None for anything else."""
+    if isinstance(value, bool):
+        return None
+    if type(value) is int:
+        return float(value) if abs(value) < 2 ** 1023 else float("inf"), str(value).encode()
+    if isinstance(value, float):
+        return float(value), None
+    return None
+
+
+def manifest_json(*, video_id: str, duration: float, segment_seconds: float,
+                  overlap_seconds: float, segment_dir: str | Path,
+                  created_at: str) -> str | None:
+    """The text create_manifest + save_manifest write
+    (video_segmenter.py:170-218: ``json.dumps(manifest, indent=2,
+    ensure_ascii=True)``), produced natively by ``vts_manifest_json``.
+    None when an argument is not a plain int/float/str the native writer
+    prints exactly like json (the caller then uses Python's json)."""
+    nums = [_num_arg(v) for v in (duration, segment_seconds, overlap_seconds)]
+    if any(n is None for n in nums) or not all(
+            isinstance(x, str) for x in (video_id, created_at)):
+        return None
+    try:
+        sid, sdir, sca = (x.encode("utf-8") for x in (video_id, str(segment_dir), created_at))
+    except UnicodeEncodeError:  # lone surrogates (undecodable file names)
+        return None
+    (d, di), (sg, sgi), (ov, ovi) = nums  # type: ignore[misc]
+    args = _lib.ManifestArgs(sid, sdir, sca, d, di, sg, sgi, ov, ovi)
+    lib = _lib.lib()
+    n = C.c_int64(0)
+    rc = lib.vts_manifest_json(C.byref(args), None, 0, C.byref(n))
+    if rc != _lib.VTS_E_CAPACITY:
+        _lib.check(rc)
+    buf = C.create_string_buffer(int(n.value) + 1)
+    _lib.check(lib.vts_manifest_json(C.byref(args), buf, n.value + 1, C.byref(n)))
+    return buf.raw[: n.value].decode("ascii")
 
 
 def load_manifest(manifest_path: str | Path) -> SegmentManifest:
