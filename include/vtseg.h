@@ -78,6 +78,13 @@ int vts_plan_segments(double duration, double segment_seconds,
                       double overlap_seconds, vts_segment *out, int64_t cap,
                       int64_t *n_out);
 
+/* Sync-sample (keyframe) presentation timestamps of the first video track,
+ * in *timescale units (edit-list shift applied); anchors for the opt-in
+ * keyframe-aware snap_to_keyframe (video_segmenter.py:157-159 stays the
+ * identity by default).  Two-call size query. */
+int vts_keyframe_pts(const char *path, int64_t *pts, int64_t cap, int64_t *n_out,
+                     int64_t *timescale);
+
 /* Manifest JSON (create_manifest + save_manifest, video_segmenter.py:170-218):
  * the text json.dumps(manifest, indent=2, ensure_ascii=True) writes, with the
  * plan from vts_plan_segments.  *_int: the caller's int object's decimal repr

@@ -80,3 +80,34 @@ extern "C" int vts_probe_duration(const char *path, double *seconds) {
   *seconds = static_cast<double>(mvhd_duration_us(mp4)) / 1e6;
   return VTS_OK;
 }
+
+// Presentation timestamps (track timescale, edit-list shift applied as in
+// the device session and the remuxer) of the first video track's sync
+// samples: the anchors of the opt-in keyframe-aware snap_to_keyframe
+// (video_segmenter.py:157-159 is the identity stub).  Two-call size query.
+extern "C" int vts_keyframe_pts(const char *path, int64_t *pts, int64_t cap, int64_t *n_out,
+                                int64_t *timescale) {
+  clear_error();
+  if (!path || !n_out || !timescale) return fail(VTS_E_INVALID, "NULL argument");
+  Mp4Info mp4;
+  const std::string e = mp4_parse_file(path, &mp4);
+  if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
+  if (mp4.video.empty()) return fail(VTS_E_FORMAT, "no video track");
+  const Mp4VideoTrack &t = mp4.video.front();
+  int64_t shift = 0;
+  for (const EditEntry &ed : t.edits)
+    if (ed.media_time >= 0) {
+      shift = ed.media_time;
+      break;
+    }
+  *timescale = t.timescale;
+  int64_t n = 0;
+  for (size_t i = 0; i < t.dts.size(); ++i) {
+    if (!t.sync[i]) continue;
+    if (pts && n < cap) pts[n] = t.dts[i] + t.cts_offset[i] - shift;
+    ++n;
+  }
+  *n_out = n;
+  if (!pts || n > cap) return fail(VTS_E_CAPACITY, "need %lld", static_cast<long long>(n));
+  return VTS_OK;
+}

@@ -125,6 +125,8 @@ SIGNATURES: dict[str, tuple] = {
                                           _P(C.c_double), C.c_int64, _P(C.c_int64)]),
     "vts_manifest_json": (C.c_int, [_P(ManifestArgs), C.c_char_p, C.c_int64, _P(C.c_int64)]),
     "vts_probe_duration": (C.c_int, [C.c_char_p, _P(C.c_double)]),
+    "vts_keyframe_pts": (C.c_int, [C.c_char_p, _P(C.c_int64), C.c_int64, _P(C.c_int64),
+                                   _P(C.c_int64)]),
     "vts_probe_info": (C.c_int, [C.c_char_p, _P(VideoInfo)]),
     "vts_extract_segment": (C.c_int, [C.c_char_p, C.c_double, C.c_double, C.c_char_p]),
     "vts_score_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int64]),

@@ -122,7 +122,9 @@ class SegmentationResult:
 class SegmentationDriver:
     def __init__(self, config: dict, api_counter, analyze: AnalyzeFn, *,
                  probe: Callable = probe_duration, extract: Callable = extract_segment,
-                 limit_exc: type | tuple = APILimitExceeded):
+                 limit_exc: type | tuple = APILimitExceeded,
+                 scene_anchors: Callable[[Path], list[float]] | None = None):
+        self.scene_anchors = scene_anchors  # opt-in `snap: scene` (e.g. scene.scene_cut_times)
         self.config = config
         self.analyzer_config = config.get("analyzer", {})
         self.api_counter = api_counter
@@ -194,6 +196,31 @@ class SegmentationDriver:
                 return left + right
             raise
 
+    def _snap_args(self, video_path: Path, long_video_config: dict,
+                   segment_seconds: float) -> dict:
+        """Opt-in segment boundaries on keyframes / scene cuts (vtseg.snap;
+        SURVEY §8f-3): ``long_video.snap`` = "keyframe" | "scene", moving each
+        boundary by at most ``snap_max_shift_seconds`` (default a tenth of a
+        segment).  Absent (the reference config): no extra arguments, so the
+        manifest call and the segment list are the reference's."""
+        mode = long_video_config.get("snap")
+        if not mode:
+            return {}
+        shift = _coerce_float(long_video_config.get("snap_max_shift_seconds"))
+        if shift is None:
+            shift = 0.1 * float(segment_seconds)
+        if mode == "keyframe":
+            from .snap import keyframe_times
+            anchors = keyframe_times(video_path)
+        elif mode == "scene":
+            if self.scene_anchors is None:
+                raise ValueError("long_video.snap = 'scene' needs a scene_anchors callable "
+                                 "(e.g. vtseg.scene.scene_cut_times)")
+            anchors = self.scene_anchors(video_path)
+        else:
+            raise ValueError(f"long_video.snap must be 'keyframe' or 'scene', not {mode!r}")
+        return {"anchors": anchors, "max_shift": shift}
+
     def _limit(self, msg: str) -> Exception:
         exc = self.limit_exc[0] if isinstance(self.limit_exc, tuple) else self.limit_exc
         return exc(msg)
@@ -219,7 +246,9 @@ class SegmentationDriver:
         video_id = video_path.stem
         manifest = load_or_create_manifest(video_id=video_id, duration=duration,
                                            segment_seconds=segment_seconds,
-                                           overlap_seconds=overlap_seconds, temp_dir=temp_dir)
+                                           overlap_seconds=overlap_seconds, temp_dir=temp_dir,
+                                           **self._snap_args(video_path, long_video_config,
+                                                             segment_seconds))
         segment_dir = Path(temp_dir) / "segments" / video_id
         manifest_path = segment_dir / "manifest.json"
         segments = sorted(manifest["segments"], key=lambda item: item["id"])

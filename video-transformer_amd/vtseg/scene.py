@@ -117,6 +117,7 @@ class VideoScorer:
         prm.fused = fused
         prm.gops_per_launch = gops_per_launch
         prm.parse_chunks = parse_chunks
+        self._threshold = cut_threshold
         ctx = C.c_void_p()
         _lib.check(self._lib.vts_open(int(device), str(path).encode(), C.byref(prm),
                                       C.byref(ctx)))
@@ -175,6 +176,14 @@ class VideoScorer:
         _lib.check(self._lib.vts_scene_cuts(self._ctx, buf, cap, C.byref(n)))
         return list(buf[: n.value])
 
+    def scene_cut_times(self) -> list[float]:
+        """Presentation times (s) of the scene-cut frames (decodes + scores):
+        anchors for the opt-in scene-aware segment boundaries (vtseg.snap)."""
+        from fractions import Fraction
+        res = self.score()
+        return [float(Fraction(int(res.pts[i]), res.timescale))
+                for i in res.cuts(self._threshold)]
+
     def frame_nv12(self, i: int) -> np.ndarray:
         w, h = int(self.info.width), int(self.info.height)
         out = np.zeros(w * h * 3 // 2, np.uint8)
@@ -231,3 +240,9 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
             "n_cuts": int(info.n_cuts), "timescale": int(info.timescale),
             "recon_hash": int(info.recon_hash),
             "cuts": list(cuts[: int(info.n_cuts)])}
+
+
+def scene_cut_times(path: str | Path, device: int = 0) -> list[float]:
+    """Decode + score `path` on the GPU and return its scene-cut times."""
+    with VideoScorer(path, device=device) as v:
+        return v.scene_cut_times()

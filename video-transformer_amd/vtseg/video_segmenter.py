@@ -170,14 +170,26 @@ def extract_segment(
                        "-c:a", "aac", "-b:a", "128k", str(output_path)])
 
 
-def snap_to_keyframe(video_path: str | Path, timestamp: float) -> float:
-    """Identity clamp, exactly as the reference stub (video_segmenter.py:157-159).
+def snap_to_keyframe(video_path: str | Path, timestamp: float, *, mode: str = "identity",
+                     anchors: list[float] | None = None, max_shift: float = float("inf"),
+                     direction: str = "nearest") -> float:
+    """Identity clamp by default, exactly as the reference stub
+    (video_segmenter.py:157-159), so segment lists stay bit-identical.
 
-    Keyframe/scene-aware snapping is opt-in elsewhere (vtseg.scene); the
-    default must stay the identity so segment lists stay bit-identical.
+    Opt-in (vtseg.snap): ``mode="keyframe"`` snaps to the file's keyframes
+    (MP4 sync samples), ``mode="anchors"`` to caller-given times (e.g. scene
+    cuts from ``scene.VideoScorer``), the nearest within ``max_shift``
+    seconds (``direction="floor"``: the latest at or before).
     """
-    _ = video_path
-    return max(0.0, float(timestamp))
+    t = max(0.0, float(timestamp))
+    if mode == "identity":
+        return t
+    from . import snap
+    if mode == "keyframe":
+        anchors = snap.keyframe_times(video_path)
+    elif mode != "anchors" or anchors is None:
+        raise ValueError("mode must be 'identity', 'keyframe' or 'anchors' (with anchors)")
+    return max(0.0, snap.snap_time(t, sorted(anchors), max_shift, direction))
 
 
 def get_segment_dir(video_id: str, temp_dir: str | Path) -> Path:
@@ -195,11 +207,22 @@ def create_manifest(
     segment_seconds: float,
     overlap_seconds: float,
     temp_dir: str | Path,
+    anchors: list[float] | None = None,
+    max_shift: float = 0.0,
 ) -> SegmentManifest:
+    """The reference's create_manifest (video_segmenter.py:170-205).  Opt-in:
+    ``anchors`` (keyframe or scene-cut times) move the inner boundaries by up
+    to ``max_shift`` seconds (vtseg.snap.plan_segments_snapped)."""
     segment_dir = get_segment_dir(video_id, temp_dir)
     segment_dir.mkdir(parents=True, exist_ok=True)
     entries: list[SegmentEntry] = []
-    for seg in plan_segments(duration, segment_seconds, overlap_seconds):
+    if anchors is None:
+        plan = plan_segments(duration, segment_seconds, overlap_seconds)
+    else:
+        from .snap import plan_segments_snapped
+        plan = plan_segments_snapped(duration, segment_seconds, overlap_seconds, anchors,
+                                     max_shift=max_shift)
+    for seg in plan:
         entries.append({
             "id": seg.segment_id,
             "start": seg.start,
@@ -220,9 +243,10 @@ def create_manifest(
         "segments": entries,
     }
     path = get_manifest_path(video_id, temp_dir)
-    text = manifest_json(video_id=video_id, duration=duration,
-                         segment_seconds=segment_seconds, overlap_seconds=overlap_seconds,
-                         segment_dir=segment_dir, created_at=manifest["created_at"])
+    text = None if anchors is not None else manifest_json(
+        video_id=video_id, duration=duration, segment_seconds=segment_seconds,
+        overlap_seconds=overlap_seconds, segment_dir=segment_dir,
+        created_at=manifest["created_at"])
     if text is None:  # objects only Python's json knows how to print (or refuse)
         save_manifest(path, manifest)
     else:
@@ -290,13 +314,16 @@ def load_or_create_manifest(
     segment_seconds: float,
     overlap_seconds: float,
     temp_dir: str | Path,
+    anchors: list[float] | None = None,
+    max_shift: float = 0.0,
 ) -> SegmentManifest:
     manifest_path = get_manifest_path(video_id, temp_dir)
     if manifest_path.exists():  # resume: reuse the persisted plan verbatim
         return load_manifest(manifest_path)
     return create_manifest(video_id=video_id, duration=duration,
                            segment_seconds=segment_seconds,
-                           overlap_seconds=overlap_seconds, temp_dir=temp_dir)
+                           overlap_seconds=overlap_seconds, temp_dir=temp_dir,
+                           anchors=anchors, max_shift=max_shift)
 
 
 def pending_segments(manifest: SegmentManifest) -> list[SegmentEntry]:
