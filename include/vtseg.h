@@ -296,7 +296,9 @@ typedef struct vts_synth_params {
                                    each scene texture (I_PCM data then holds
                                    emulation-prevention bytes); bit 1: odd-pixel
                                    pans (half-pel chroma, 8.4.2.2.2 bilinear);
-                                   max_motion may then be odd                  */
+                                   max_motion may then be odd; bit 2: the last
+                                   picture (if P) loses the slice holding
+                                   macroblock row 1 (missing macroblocks)     */
 } vts_synth_params;
 
 typedef struct vts_synth_info {

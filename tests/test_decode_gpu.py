@@ -216,3 +216,20 @@ def test_gop_grouped_schedule_equals_all_at_once(tmp_path, gops):
         res = v.score()
         assert np.array_equal(v.frame_nv12(239).reshape(frames[-1].shape), frames[-1])
     assert np.array_equal(res.scores, ref["score"]) and np.array_equal(res.hist, ref["hist"])
+
+
+def test_missing_slice_fails_loudly_even_over_stale_commands(tmp_path):
+    """The last picture lacks a slice.  With small windows the two command
+    rings are reused, so the missing macroblocks' slots hold valid commands
+    of an earlier window (another epoch): they must still read as absent and
+    the run must fail with the reason, on every run."""
+    _require_gpu()
+    path = tmp_path / "m.mp4"
+    n = 185  # the last picture is a P picture (IDR every 30)
+    scene.synth_write(path, width=160, height=96, n_frames=n, cut_min_s=20, cut_max_s=30,
+                      gop_max_s=1.0, drop_last_slice=True)
+    for window in (0, 31):
+        with scene.VideoScorer(path, window_frames=window) as v:
+            for _ in range(2):
+                with pytest.raises(VtsegError, match="not covered by any slice"):
+                    v.score()

@@ -22,7 +22,7 @@ struct ParseArgs {
   const uint8_t *es;       // device elementary-stream bytes (+64 B padding)
   const SliceDesc *slices;
   int32_t n_slices;
-  int32_t _pad;
+  uint32_t epoch;          // written into every command (h264.h kCmdEpochMask)
   uint64_t *cmd;           // [slot][mb]
   uint32_t *err;           // DEC_E_* bits
   H264DevParams prm;
@@ -38,7 +38,7 @@ struct ReconArgs {
   int64_t frame_stride;
   int32_t pitch;
   int32_t mb_width, mb_height;
-  int32_t _pad;
+  uint32_t epoch;          // commands of another epoch read as absent
   uint32_t *err;
 };
 

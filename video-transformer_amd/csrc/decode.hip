@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(64) VTS_PARSE_OCC h264_parse(ParseArgs a) {
   if (s >= a.n_slices) return;
   const SliceDesc sd = a.slices[s];
   const uint32_t errs = parse_slice(a.es, sd.nal_offset, sd.nal_size, sd.slot, sd.ref_slot, a.prm, a.cmd,
-                                    &scratch[threadIdx.x]);
+                                    &scratch[threadIdx.x], a.epoch);
   if (errs) atomicOr(a.err, errs);
 }
 
@@ -236,6 +236,12 @@ __device__ __forceinline__ uint4 fetch_row(const FrameRefs &F, uint64_t c, int r
   return out;
 }
 
+// A command of this run (epoch bits stripped), or 0 (= absent) for one left
+// in the ring by an earlier run.
+__device__ __forceinline__ uint64_t current_cmd(uint64_t c, uint32_t epoch) {
+  return ((c & kCmdEpochMask) >> kCmdEpochShift) == epoch ? (c & ~kCmdEpochMask) : 0;
+}
+
 __device__ __forceinline__ FrameRefs frame_refs(const ReconArgs &a, int ref_slot) {
   FrameRefs F;
   F.es = a.es;
@@ -400,7 +406,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
   const FrameRefs F = frame_refs(a, fr.y);
   const int64_t gframe = fa.frame0 + fr.x;
   // the command load is in flight across the histogram-clearing barrier
-  const uint64_t c = mb < nmb ? a.cmd[static_cast<int64_t>(fr.x) * nmb + mb] : 0;
+  const uint64_t c = mb < nmb ? current_cmd(a.cmd[static_cast<int64_t>(fr.x) * nmb + mb], a.epoch) : 0;
   // and so is the display predecessor's thumbnail (fused SAD, see below)
   constexpr int GW = K ? (16 / K + 3) / 4 : 1;  // thumbnail words per lane
   uint32_t prevw[GW];
@@ -419,9 +425,55 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       }
     }
   }
-  if constexpr (K != 0 && !(VTS_EXP_SKIP & 1)) {
-    lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
+  // I pictures (no reference, so every macroblock is I_PCM): a lane reading
+  // its rows straight from the elementary stream touches 64 lines per load
+  // instruction (consecutive macroblocks' samples lie 386 bytes apart), which
+  // made the I-picture launch 1.6x the time of a P level.  Instead the
+  // workgroup copies its macroblocks' 384-byte sample blocks into LDS with
+  // consecutive lanes on consecutive 16-byte chunks; each lane then reads its
+  // rows from LDS.  K = 4 only (24 KB of LDS: 6 workgroups per CU, above the
+  // kernel's register-limited 5).
+#ifndef VTS_PCM_STAGE
+#define VTS_PCM_STAGE 1
+#endif
+  constexpr bool kStage = K == 4 && VTS_PCM_STAGE;
+  constexpr int kPcmChunks = kStage ? MB_PER_WG * 24 : 1;
+  __shared__ uint4 pcm_lds[kPcmChunks];
+  __shared__ uint64_t pcm_src[kStage ? MB_PER_WG : 1];
+  const bool stage = kStage && fr.y < 0;  // uniform over the workgroup
+  if constexpr (kStage) {
+    if (stage && q == 0)
+      pcm_src[threadIdx.x] = (mb < nmb && (c >> 62) == 1) ? (c & 0xffffffffffffull) : ~0ull;
+  }
+  if constexpr (K != 0) {
+    if constexpr (!(VTS_EXP_SKIP & 1)) lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
     __syncthreads();
+  }
+  if constexpr (kStage) {
+    if (stage) {
+      // branch-free: both aligned 16-byte loads of every chunk in flight,
+      // then one funnel shift each (a missing macroblock reads the stream's
+      // first bytes; its command fails in the slow path below)
+      constexpr int PER = kPcmChunks / kReconThreads;  // 6 chunks per thread
+      uint4 lo[PER], hi[PER];
+      int sh[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int i = threadIdx.x + j * kReconThreads;
+        const uint64_t src = pcm_src[i / 24];
+        const uint8_t *p = a.es + (src != ~0ull ? src + 16 * (i % 24) : 0);
+        sh[j] = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 15);
+        const uint4 *pa = reinterpret_cast<const uint4 *>(p - sh[j]);
+        lo[j] = pa[0];
+        hi[j] = pa[1];
+      }
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        uint32_t zero_unused = 0;
+        pcm_lds[threadIdx.x + j * kReconThreads] = finish_row(false, false, lo[j], hi[j], sh[j], zero_unused);
+      }
+      __syncthreads();
+    }
   }
   uint32_t errs = 0;
   uint32_t sad = 0;  // this lane's share of the frame's thumbnail SAD
@@ -446,9 +498,24 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
       uint4 lo[KK + HK], hi[KK + HK];
       int shf[KK + HK];  // funnel shift | edge mode << 8 (1 left, 2 right)
+      // LDS-staged I_PCM block (I pictures): luma row r = chunk r, Cb row r =
+      // bytes 256 + 8r, Cr row r = 320 + 8r; shift 0, so the finish below
+      // passes luma through and interleaves the chroma pairs
+      const uint4 *blk = pcm_lds + (threadIdx.x % MB_PER_WG) * 24;
+      const bool staged = kStage && stage && pcm;
 #pragma unroll
       for (int i = 0; i < KK + HK; ++i) {
-        if (pcm && i >= KK) {
+        if (staged) {
+          shf[i] = 0;
+          if (i < KK) {
+            lo[i] = hi[i] = blk[q * KK + i];
+          } else {
+            const int r = q * HK + (i - KK);
+            const uint4 u = blk[16 + (r >> 1)], v = blk[20 + (r >> 1)];
+            lo[i] = (r & 1) ? make_uint4(u.z, u.w, 0, 0) : make_uint4(u.x, u.y, 0, 0);
+            hi[i] = (r & 1) ? make_uint4(v.z, v.w, 0, 0) : make_uint4(v.x, v.y, 0, 0);
+          }
+        } else if (pcm && i >= KK) {
           const uint8_t *pu = pcmb + 256 + 8 * (q * HK + (i - KK));  // Cr row is 64 B on
           const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pu) & 7);
           const uint2 *au = reinterpret_cast<const uint2 *>(pu - sh);
@@ -665,7 +732,8 @@ __global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC h264_recon_score6(Fused
   const int64_t npx = static_cast<int64_t>(fa.w) * fa.h;
   // command, and (finishing threads) the predecessor's thumbnail: in flight
   // across the barrier that clears the LDS sums
-  const uint64_t c = active ? a.cmd[static_cast<int64_t>(fr.x) * nmb + static_cast<int64_t>(mby) * mbw + m] : 0;
+  const uint64_t c =
+      active ? current_cmd(a.cmd[static_cast<int64_t>(fr.x) * nmb + static_cast<int64_t>(mby) * mbw + m], a.epoch) : 0;
   constexpr int kFin = kK6Px / 4;                         // finishing threads per band
   const int fband = rb * kK6Bands + t / kFin, fpx = cb * kK6Px + (t % kFin) * 4;
   const bool fin = t < kK6Bands * kFin && fband < fa.h && fpx < fa.w;

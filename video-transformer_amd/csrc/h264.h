@@ -83,5 +83,11 @@ std::string describe_decode_error(uint32_t flags);
 //               16-31 mvy, quarter-pel, refIdx 0), 0 = not decoded.
 constexpr uint64_t MB_PCM = 1ull << 62;
 constexpr uint64_t MB_INTER = 2ull << 62;
+// bits 48-61: the run's epoch (1..16383).  The reconstruct kernels treat a
+// command whose epoch is not the current run's as absent (missing
+// macroblock), so the command ring need not be cleared before every parse.
+constexpr int kCmdEpochShift = 48;
+constexpr uint64_t kCmdEpochMask = 0x3fffull << kCmdEpochShift;
+constexpr uint32_t kCmdEpochs = 16383;
 
 }  // namespace vts

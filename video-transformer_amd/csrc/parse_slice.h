@@ -221,12 +221,14 @@ struct CmdWriter {
   uint64_t *cmd;      // frame base
   Cmd2 *e;            // the open group's 4 commands: per-lane scratch (LDS on the device)
   int64_t gbase;      // absolute index (slot * nmb) of cmd[0], for alignment
+  uint64_t tag;       // the run's epoch, in bits 48-61 of every command
   int32_t g;          // first frame-relative index of the open group
   uint32_t mask;
 
-  VTS_HD VTS_INLINE void init(uint64_t *c, int64_t gb, Cmd2 *scratch) {
+  VTS_HD VTS_INLINE void init(uint64_t *c, int64_t gb, Cmd2 *scratch, uint64_t epoch_tag) {
     cmd = c;
     e = scratch;
+    tag = epoch_tag;
     gbase = gb;
     g = -1;
     mask = 0;
@@ -254,7 +256,7 @@ struct CmdWriter {
       flush();
       g = ga;
     }
-    reinterpret_cast<uint64_t *>(e)[j] = c;
+    reinterpret_cast<uint64_t *>(e)[j] = c | tag;
     mask |= 1u << j;
     if (j == 3) flush();
   }
@@ -269,7 +271,8 @@ struct CmdWriter {
 };
 
 // Parse one slice NAL (header byte at es + nal_offset, nal_size bytes) of the
-// frame in `slot` into cmd_all[slot * nmb + mb].  Returns DEC_E_* bits.
+// frame in `slot` into cmd_all[slot * nmb + mb], tagged with `epoch`.
+// Returns DEC_E_* bits.
 // `scratch` is the lane's private ParseScratch (LDS in h264_parse).
 struct ParseScratch {
   Cmd2 cmd[2];         // open command group
@@ -278,10 +281,11 @@ struct ParseScratch {
 
 VTS_HD VTS_INLINE uint32_t parse_slice(const uint8_t *es, int64_t nal_offset, int32_t nal_size, int32_t slot,
                                        int32_t ref_slot, const H264DevParams &P, uint64_t *cmd_all,
-                                       ParseScratch *scratch) {
+                                       ParseScratch *scratch, uint32_t epoch = 0) {
   const int nmb = P.mb_width * P.mb_height;
   CmdWriter out;
-  out.init(cmd_all + static_cast<int64_t>(slot) * nmb, static_cast<int64_t>(slot) * nmb, scratch->cmd);
+  out.init(cmd_all + static_cast<int64_t>(slot) * nmb, static_cast<int64_t>(slot) * nmb, scratch->cmd,
+           static_cast<uint64_t>(epoch) << kCmdEpochShift);
   uint32_t errs = 0;
 
   const uint8_t *nal = es + nal_offset;

@@ -106,6 +106,10 @@ struct vts_ctx {
   hipEvent_t ev_start = nullptr, ev_end = nullptr;
   double timings[4] = {0, 0, 0, 0};
   int64_t last_window_done = -1;
+  // command epochs: run_no counts window runs; a ring is cleared on first use
+  // and again before an epoch value could repeat (h264.h kCmdEpochs)
+  int64_t run_no = 0;
+  int64_t ring_cleared_at[2] = {-1, -1};
   bool have_results = false;
   std::vector<float> host_scores;
 };
@@ -496,9 +500,17 @@ int run_all(vts_ctx *c) {
     // chunk j+1 overlaps reconstructing the launches of chunk j.
     HIP_TRY(hipStreamWaitEvent(sp, c->ev_start, 0));
     HIP_TRY(hipEventRecord(E[0], sp));
-    HIP_TRY(hipMemsetAsync(c->d_cmd[r], 0, static_cast<size_t>((w.f1 - w.f0) * nmb * 8), sp));
+    // commands carry the run's epoch; stale ones read as absent, so the ring
+    // is cleared only on first use and before an epoch could come round again
+    const int64_t run = c->run_no++;
+    const uint32_t epoch = 1u + static_cast<uint32_t>(run % kCmdEpochs);
+    if (c->ring_cleared_at[r] < 0 || run - c->ring_cleared_at[r] >= kCmdEpochs) {
+      HIP_TRY(hipMemsetAsync(c->d_cmd[r], 0, static_cast<size_t>(c->ring_frames * nmb * 8), sp));
+      c->ring_cleared_at[r] = run;
+    }
     {
       ParseArgs pa{};
+      pa.epoch = epoch;
       pa.es = c->d_es;
       pa.cmd = c->d_cmd[r];
       pa.err = c->d_err;
@@ -524,6 +536,7 @@ int run_all(vts_ctx *c) {
     ra.pitch = c->pitch;
     ra.mb_width = c->sps.mb_width;
     ra.mb_height = c->sps.mb_height;
+    ra.epoch = epoch;
     ra.err = c->d_err;
     const int tw = c->width / c->k, th = c->height / c->k;
     FusedArgs fa{};

@@ -461,7 +461,10 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
         }
         if (skip_run) bw.ue(skip_run);
         bw.trailing();
-        append_nal(sample, 0x41, bw.data());  // nal_ref_idc 2, non-IDR
+        // edge case bit 2: the last picture loses the slice holding macroblock
+        // row 1 (a decoder must report the macroblocks as missing)
+        const bool drop = (P.edge_cases & 4) && f == P.n_frames - 1 && first <= mbw && mbw < last;
+        if (!drop) append_nal(sample, 0x41, bw.data());  // nal_ref_idc 2, non-IDR
         first = last;
       }
       ++since_idr;

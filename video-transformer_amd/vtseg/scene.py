@@ -222,7 +222,7 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 cut_min_s: float = 2.0, cut_max_s: float = 20.0, gop_max_s: float = 2.0,
                 max_motion: int = 4, slices_per_row: int = 1,
                 hash_frames: bool = False, pcm_zero_runs: bool = False,
-                odd_motion: bool = False) -> dict:
+                odd_motion: bool = False, drop_last_slice: bool = False) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
     and the ground-truth scene-cut frames."""
     p = _lib.SynthParams()
@@ -231,7 +231,8 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     p.cut_min_s, p.cut_max_s, p.gop_max_s = cut_min_s, cut_max_s, gop_max_s
     p.max_motion, p.slices_per_row = max_motion, slices_per_row
     p.hash_frames = 1 if hash_frames else 0
-    p.edge_cases = (1 if pcm_zero_runs else 0) | (2 if odd_motion else 0)
+    p.edge_cases = (1 if pcm_zero_runs else 0) | (2 if odd_motion else 0) | \
+        (4 if drop_last_slice else 0)
     info = _lib.SynthInfo()
     cuts = (C.c_int64 * max(n_frames, 1))()
     _lib.check(_lib.lib().vts_synth_write(str(path).encode(), C.byref(p), C.byref(info),
