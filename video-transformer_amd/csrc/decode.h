@@ -75,6 +75,8 @@ int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s);
 int sad_score_launch(const uint64_t *sad, float *score, int64_t frame0, int64_t n_frames,
                      int64_t npx, hipStream_t s);
 int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s);
+// hist[0 .. 256 n) = 0, sad[0 .. n) = 0 (hist 16-byte aligned)
+int clear_accum_launch(uint32_t *hist, uint64_t *sad, int64_t n_frames, hipStream_t s);
 int score_launch(const vts_score_desc *d, hipStream_t stream);
 int64_t score_workspace_bytes(int32_t width, int32_t height, int32_t k, int64_t n_frames);
 

@@ -541,9 +541,7 @@ int run_all(vts_ctx *c) {
     const int tw = c->width / c->k, th = c->height / c->k;
     FusedArgs fa{};
     if (c->fused) {
-      HIP_TRY(hipMemsetAsync(c->d_hist + w.f0 * 256, 0,
-                             sizeof(uint32_t) * 256 * static_cast<size_t>(w.f1 - w.f0), sd));
-      HIP_TRY(hipMemsetAsync(c->d_sad + w.f0, 0, sizeof(uint64_t) * static_cast<size_t>(w.f1 - w.f0), sd));
+      VTS_TRY(clear_accum_launch(c->d_hist + w.f0 * 256, c->d_sad + w.f0, w.f1 - w.f0, sd));
       fa.r = ra;
       fa.frame0 = w.f0;
       fa.w = tw;
