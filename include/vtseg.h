@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define VTS_ABI_VERSION 1
+#define VTS_ABI_VERSION 2
 
 enum {
   VTS_OK = 0,
@@ -278,6 +278,41 @@ int vts_last_timings(const vts_ctx *ctx, double *ms4);
  * 2 slices, 3 ring frames, 4 fused scoring (1/0); < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);
 int vts_close(vts_ctx *ctx);
+
+/* ------------------------------- upload transcode (360p)
+ * Replaces the pixel half of ContentAnalyzer._compress_video_for_upload
+ * (src/analyzer/content_analyzer.py:167-236: `ffmpeg -vf scale=-2:360
+ * -c:v libx264 -crf 28`).  The session's device decoder decodes every frame,
+ * an area filter downscales it to (w, height) with w = ffmpeg's scale=-2
+ * width, and a device encoder writes H.264 Constrained Baseline: IDR (all
+ * I_PCM) at scene cuts / every keyint frames, P pictures of full-search
+ * integer motion without residual (P_L0_16x16 / P_Skip) or I_PCM where the
+ * motion prediction misses by more than max_mb_sad; one slice per macroblock
+ * row; MP4 (moov at the end), video only.  DESIGN.md §11. */
+typedef struct vts_transcode_params {
+  int32_t height;          /* output display height, even; 0 = 360            */
+  int32_t search_range;    /* full-search motion range in luma pixels 0..16;
+                              < 0 = 0 (zero motion only); 0 = default 8       */
+  int32_t max_mb_sad;      /* inter if luma+chroma SAD <= this, else I_PCM;
+                              0 = default 768 (2 per sample); < 0 = all I_PCM */
+  int32_t keyint;          /* max frames per GOP; 0 = 250 (x264's default)    */
+  float cut_threshold;     /* IDR where score > this; <= 0 = the session's    */
+  int32_t _pad;
+} vts_transcode_params;
+
+typedef struct vts_transcode_info {
+  int32_t width, height;   /* output display size                              */
+  int64_t n_frames;
+  int64_t n_idr;
+  int64_t pcm_mbs, inter_mbs, skip_mbs;
+  int64_t bytes_written;   /* output file size                                 */
+  double ms[4];            /* device decode+score+downscale, motion search,
+                              slice writing + compaction, host MP4 mux         */
+} vts_transcode_info;
+
+/* Transcode the session's video to `out_path`. */
+int vts_transcode(vts_ctx *ctx, const char *out_path, const vts_transcode_params *p,
+                  vts_transcode_info *info);
 
 /* ------------------------------------------------ synthetic stream writer */
 

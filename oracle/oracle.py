@@ -8,6 +8,8 @@ cpu_baseline leg may import this module.  The product never does.
     boundary_frames                    exact rational pts/timescale >= t (Fraction)
     score_frames                       DESIGN.md §Scoring, scalar C
     decode_file                        DESIGN.md §Decoder subset, scalar C
+    transcode / downscale_nv12         DESIGN.md §11 upload transcode, scalar C
+                                       (transcode_oracle.c)
 """
 from __future__ import annotations
 
@@ -71,6 +73,15 @@ def lib() -> C.CDLL:
         _lib.or_score_frames.argtypes = [
             u8p, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib.or_small_width.argtypes = [C.c_int, C.c_int, C.c_int]
+        _lib.or_downscale_nv12.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        _lib.or_sps_pps.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib.or_pick_level.argtypes = [C.c_int, C.c_double]
+        _lib.or_transcode.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p,
+                                      C.c_float, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_void_p]
     return _lib
 
 
@@ -305,3 +316,90 @@ def slice_commands(nal: bytes | np.ndarray, nal_abs: int, prm: "H264Params", hav
     buf = np.frombuffer(bytes(nal), np.uint8)
     return L.or_slice_commands(C.byref(prm), buf.ctypes.data, len(buf), int(nal_abs),
                                1 if have_ref else 0, cmd_frame.ctypes.data)
+
+
+# ------------------------------------------------------------ upload transcode
+
+def small_width(width: int, height: int, out_height: int = 360) -> int:
+    """ffmpeg scale=-2:H output width (transcode_oracle.c or_small_width)."""
+    return int(lib().or_small_width(width, height, out_height))
+
+
+def downscale_nv12(frame: np.ndarray, width: int, height: int, out_height: int = 360) -> np.ndarray:
+    """Area downscale of one display-size NV12 frame; returns the coded NV12
+    frame [ch*3/2, cw] (16-aligned, edges replicated, samples >= 1)."""
+    sw = small_width(width, height, out_height)
+    cw, ch = (sw + 15) & ~15, (out_height + 15) & ~15
+    src = np.ascontiguousarray(frame, np.uint8).reshape(-1)
+    out = np.zeros((ch * 3 // 2, cw), np.uint8)
+    rc = lib().or_downscale_nv12(src.ctypes.data, width, height, out.ctypes.data, sw, out_height)
+    if rc != 0:
+        raise RuntimeError(f"oracle downscale rc={rc}")
+    return out
+
+
+def sps_pps(mbw: int, mbh: int, crop_r: int, crop_b: int, fps: float) -> tuple[bytes, bytes]:
+    level = lib().or_pick_level(mbw * mbh, mbw * mbh * fps)
+    sps, pps = (C.c_uint8 * 80)(), (C.c_uint8 * 80)()
+    sn, pn = C.c_int64(0), C.c_int64(0)
+    rc = lib().or_sps_pps(mbw, mbh, crop_r, crop_b, level, sps, C.byref(sn), pps, C.byref(pn))
+    if rc != 0:
+        raise RuntimeError(f"oracle sps_pps rc={rc}")
+    return bytes(sps[:sn.value]), bytes(pps[:pn.value])
+
+
+def transcode(frames: np.ndarray, width: int, height: int, scores: np.ndarray, *,
+              threshold: float = 0.08, out_height: int = 360, search_range: int = 8,
+              max_mb_sad: int = 768, keyint: int = 250, want_recon: bool = False) -> dict:
+    """The upload transcode of display-size NV12 frames [F, H*3/2, W] with
+    their scene scores: output samples (bytes), per-frame sizes / sync flags,
+    SPS/PPS, stats and (optionally) the encoder's reconstruction."""
+    F = frames.shape[0]
+    sw = small_width(width, height, out_height)
+    cw, ch = (sw + 15) & ~15, (out_height + 15) & ~15
+    mbw, mbh = cw // 16, ch // 16
+    fr = np.ascontiguousarray(frames, np.uint8)
+    sc = np.ascontiguousarray(scores, np.float32)
+    cap = F * mbh * (64 + mbw * 420 + 8) + 64
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(F, np.int64)
+    size = np.zeros(F, np.int64)
+    sync = np.zeros(F, np.uint8)
+    recon = np.zeros((F, ch * 3 // 2, cw), np.uint8) if want_recon else None
+    stats = np.zeros(4, np.int64)
+    n = C.c_int64(0)
+    rc = lib().or_transcode(fr.ctypes.data, F, width, height, sc.ctypes.data, threshold,
+                            out_height, search_range, max_mb_sad, keyint, out.ctypes.data, cap,
+                            off.ctypes.data, size.ctypes.data, sync.ctypes.data,
+                            recon.ctypes.data if recon is not None else None,
+                            stats.ctypes.data, C.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"oracle transcode rc={rc}")
+    samples = [bytes(out[off[i]:off[i] + size[i]]) for i in range(F)]
+    return {"width": sw, "height": out_height, "coded_width": cw, "coded_height": ch,
+            "samples": samples, "sync": sync.astype(bool), "recon": recon,
+            "pcm_mbs": int(stats[0]), "inter_mbs": int(stats[1]), "skip_mbs": int(stats[2]),
+            "n_idr": int(stats[3])}
+
+
+def decode_samples(sps: bytes, pps: bytes, samples: list[bytes], nal_length_size: int = 4):
+    """or_decode_samples on in-memory AVCC samples; returns display-size NV12
+    frames [F, H*3/2, W]."""
+    L = lib()
+    prm = H264Params()
+    rc = L.or_parse_sps_pps(sps, len(sps), pps, len(pps), nal_length_size, C.byref(prm))
+    if rc != 0:
+        raise RuntimeError(f"oracle SPS/PPS rc={rc}")
+    W = prm.mb_width * 16 - prm.crop_right
+    H = prm.mb_height * 16 - prm.crop_bottom
+    n = len(samples)
+    data = np.frombuffer(b"".join(samples) + bytes(64), np.uint8)
+    sizes = np.array([len(x) for x in samples], np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    out = np.zeros((n, H * 3 // 2, W), np.uint8)
+    bad = C.c_int64(-1)
+    rc = L.or_decode_samples(C.byref(prm), data.ctypes.data, offs.ctypes.data, sizes.ctypes.data,
+                             n, out.ctypes.data, C.byref(bad))
+    if rc != 0:
+        raise RuntimeError(f"oracle decode rc={rc} at frame {bad.value}")
+    return out

@@ -1,0 +1,132 @@
+"""Device upload transcode (vts_transcode) vs the C oracle.
+
+The reference's _compress_video_for_upload (content_analyzer.py:167-236)
+runs x264, which is absent here: byte parity with its output is unpinned.
+Pinned instead: every output sample byte, the SPS/PPS and the macroblock
+statistics of the device encoder equal transcode_oracle.c's on the same
+decoded frames and scene scores, and the device decoder reads the output
+back to exactly the encoder's reconstruction.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+from vtseg import scene
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # name, synth kwargs, transcode kwargs
+    ("qvga_half", dict(width=320, height=192, n_frames=90), dict(height=96)),
+    ("hd720_360", dict(width=1280, height=720, n_frames=75, max_motion=4), dict()),
+    ("vga_4to3", dict(width=640, height=480, n_frames=60, max_motion=6), dict()),
+    ("fhd_360", dict(width=1920, height=1080, n_frames=40, max_motion=8), dict()),
+    ("halfpel", dict(width=320, height=240, n_frames=60, max_motion=5, odd_motion=True),
+     dict(height=120, search_range=4)),
+    ("allpcm", dict(width=320, height=192, n_frames=30), dict(height=96, max_mb_sad=-1)),
+    ("keyint", dict(width=320, height=192, n_frames=70, cut_min_s=30, cut_max_s=40,
+                    gop_max_s=10), dict(height=96, keyint=16, search_range=16)),
+]
+
+
+def _require_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test requires an MI355X")
+
+
+def _oracle_run(path, tk):
+    frames, info = oracle.decode_file(path)
+    F, W, H = frames.shape[0], info["width"], info["height"]
+    k = 4 if H <= 720 else 6
+    sc = oracle.score_frames(frames.reshape(-1), frames[0].size, F, W, H, W, H, k,
+                             want_rgb=False)["score"]
+    kw = dict(out_height=tk.get("height", 360), search_range=tk.get("search_range", 8),
+              max_mb_sad=tk.get("max_mb_sad", 768), keyint=tk.get("keyint", 250))
+    return oracle.transcode(frames, W, H, sc, want_recon=True, **kw), info
+
+
+@pytest.mark.parametrize("name,sk,tk", CASES, ids=[c[0] for c in CASES])
+def test_transcode_bytes_match_oracle(tmp_path, name, sk, tk):
+    _require_gpu()
+    src, out = tmp_path / "in.mp4", tmp_path / "out.mp4"
+    synth = dict(cut_min_s=0.7, cut_max_s=1.5, gop_max_s=0.5)
+    synth.update(sk)
+    scene.synth_write(src, **synth)
+    ref, info = _oracle_run(src, tk)
+    with scene.VideoScorer(src) as v:
+        facts = v.transcode(out, **tk)
+    assert (facts["width"], facts["height"]) == (ref["width"], ref["height"])
+    assert facts["n_idr"] == ref["n_idr"]
+    assert (facts["pcm_mbs"], facts["inter_mbs"], facts["skip_mbs"]) == \
+        (ref["pcm_mbs"], ref["inter_mbs"], ref["skip_mbs"])
+    m = oracle.read_mp4(out)
+    data = m["data"]
+    got = [data[o:o + s] for o, s in zip(m["offsets"], m["sizes"])]
+    assert len(got) == len(ref["samples"])
+    for i, (a, b) in enumerate(zip(got, ref["samples"])):
+        assert a == b, f"sample {i} differs"
+    mbw, mbh = ref["coded_width"] // 16, ref["coded_height"] // 16
+    fps = info["timescale"] / (info["pts"][1] - info["pts"][0])
+    sps, pps = oracle.sps_pps(mbw, mbh, ref["coded_width"] - ref["width"],
+                              ref["coded_height"] - ref["height"], fps)
+    assert m["sps"][0] == sps and m["pps"][0] == pps
+    assert m["dts"] == list(info["pts"])  # same timing as the source
+    # the device decoder reads it back to the encoder's reconstruction
+    sw, sh, ch = ref["width"], ref["height"], ref["coded_height"]
+    rec = ref["recon"]
+    with scene.VideoScorer(out) as d:
+        d.score()
+        last = d.frame_nv12(d.n_frames - 1).reshape(sh * 3 // 2, sw)
+    want = np.concatenate([rec[-1, :sh, :sw], rec[-1, ch:ch + sh // 2, :sw]])
+    assert np.array_equal(last, want)
+
+
+def test_transcode_windowed_equals_one_window(tmp_path):
+    """Streamed decode (two rings of small windows) downscales every window
+    into the same store: identical output file."""
+    _require_gpu()
+    src = tmp_path / "in.mp4"
+    scene.synth_write(src, width=320, height=192, n_frames=150, cut_min_s=0.7, cut_max_s=1.5,
+                      gop_max_s=0.5)
+    outs = []
+    for window in (0, 31):
+        out = tmp_path / f"o{window}.mp4"
+        with scene.VideoScorer(src, window_frames=window) as v:
+            v.transcode(out, height=96)
+        outs.append(out.read_bytes())
+    assert outs[0] == outs[1]
+
+
+def test_transcode_twice_and_after_score(tmp_path):
+    """The session stays usable: scoring, transcoding twice (store reused)."""
+    _require_gpu()
+    src = tmp_path / "in.mp4"
+    scene.synth_write(src, width=320, height=192, n_frames=60, cut_min_s=0.7, cut_max_s=1.5,
+                      gop_max_s=0.5)
+    with scene.VideoScorer(src) as v:
+        r0 = v.score()
+        a = v.transcode(tmp_path / "a.mp4", height=96)
+        b = v.transcode(tmp_path / "b.mp4", height=96)
+        r1 = v.score()
+    assert a["bytes_written"] == b["bytes_written"]
+    assert (tmp_path / "a.mp4").read_bytes() == (tmp_path / "b.mp4").read_bytes()
+    assert np.array_equal(r0.scores, r1.scores)
+
+
+def test_compress_video_for_upload_gpu(tmp_path):
+    """The drop-in method: > max size -> compressed_<name> next to the input,
+    a valid H.264 MP4 at 360 lines; a second call reuses it."""
+    _require_gpu()
+    from vtseg import upload
+    src = tmp_path / "clip.mp4"
+    scene.synth_write(src, width=1280, height=720, n_frames=60, cut_min_s=0.7, cut_max_s=1.5,
+                      gop_max_s=0.5)
+    out = upload.compress_video_for_upload(src, max_size_mb=1)
+    assert out == tmp_path / "compressed_clip.mp4" and out.stat().st_size > 0
+    assert out.stat().st_size < src.stat().st_size
+    m = oracle.read_mp4(out)
+    assert len(m["sizes"]) == 60
+    assert upload.compress_video_for_upload(src, max_size_mb=1) == out

@@ -77,6 +77,14 @@ enum DecodeError : uint32_t {
 };
 std::string describe_decode_error(uint32_t flags);
 
+// Host-side stream writing helpers (synth.cpp), shared with the transcoder:
+// Constrained Baseline SPS/PPS NAL units (pic_order_cnt_type 2, 16-bit
+// frame_num, one reference, CAVLC, deblocking_filter_control_present) for an
+// mbw x mbh macroblock picture cropped by crop_r / crop_b luma samples.
+void make_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level, std::vector<uint8_t> *sps_nal,
+                  std::vector<uint8_t> *pps_nal);
+int h264_pick_level(int mbs, double mbps);
+
 // MB command word written by the parser, read by the reconstruct kernel.
 //   bits 62-63: 1 = I_PCM (bits 0-47 = byte offset of the 384 PCM bytes in the
 //               device elementary-stream buffer), 2 = inter (bits 0-15 mvx,

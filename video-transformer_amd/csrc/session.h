@@ -1,0 +1,111 @@
+// session.h — the per-video device session (vts_ctx) shared by session.hip
+// (open / decode + score) and transcode.hip (360p upload transcode).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "common.h"
+#include "decode.h"
+#include "h264.h"
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess)                                                          \
+      return vts::fail(VTS_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));  \
+  } while (0)
+
+namespace vts {
+
+struct Window {
+  int64_t f0 = 0, f1 = 0;          // frames [f0, f1)
+  int64_t s0 = 0, s1 = 0;          // slices [s0, s1), ordered by reconstruct launch
+  std::vector<int64_t> lvl_off;    // into level_frames, one entry per reconstruct launch
+  std::vector<int32_t> lvl_cnt;
+  std::vector<int64_t> lvl_s0;     // first slice (absolute) of each launch's frames
+  std::vector<int32_t> chunk_end;  // parse chunk j covers launches [chunk_end[j-1], chunk_end[j])
+  int64_t ev0 = 0;                 // first index of this window's events in vts_ctx::lev
+  int64_t post_off = 0, post_cnt = 0;  // into post_slots
+};
+
+// Downscaled copy of every decoded frame (transcode.hip), filled by run_all
+// after each window's reconstruction when `on`.
+struct SmallStore {
+  bool on = false;
+  int w = 0, h = 0;             // display size (even)
+  int cw = 0, ch = 0;           // coded size (16-aligned); NV12, pitch cw, UV at cw * ch
+  int64_t stride = 0;           // bytes per frame
+  uint8_t *d = nullptr;         // [frame]
+  int32_t *d_taps = nullptr;    // area-filter tap tables (transcode.hip area_taps)
+  int64_t off[4] = {0, 0, 0, 0};  // luma x, luma y, chroma x, chroma y tables in d_taps
+  int taps_x = 0, taps_y = 0, taps_cx = 0, taps_cy = 0;  // taps per output sample
+  int32_t tl = 1, tc = 1;       // luma / chroma normalisers
+};
+
+}  // namespace vts
+
+struct vts_ctx {
+  using Sps = vts::Sps;
+  using Pps = vts::Pps;
+  using H264DevParams = vts::H264DevParams;
+  using SliceDesc = vts::SliceDesc;
+  using Window = vts::Window;
+  int device = 0;
+  Sps sps;
+  Pps pps;
+  H264DevParams prm{};
+  vts_video_info info{};
+  vts_params params{};
+  int k = 4;
+  int width = 0, height = 0, pitch = 0, coded_w = 0, coded_h = 0;
+  int64_t frame_stride = 0;
+  int64_t n_frames = 0;
+  std::vector<int64_t> pts;
+  std::vector<SliceDesc> slices;
+  std::vector<int4> level_frames;
+  std::vector<int32_t> post_slots;  // per window: slots whose SAD the thumb_sad pass makes
+  std::vector<Window> windows;
+  int64_t ring_frames = 0;
+  int n_rings = 1;
+  // device
+  uint8_t *d_es = nullptr;
+  int64_t es_bytes = 0;
+  SliceDesc *d_slices = nullptr;
+  int4 *d_levels = nullptr;
+  int32_t *d_post = nullptr;
+  uint64_t *d_cmd[2] = {nullptr, nullptr};
+  uint8_t *d_surf[2] = {nullptr, nullptr};
+  uint8_t *d_ws[2] = {nullptr, nullptr};
+  int64_t ws_bytes = 0;
+  uint8_t *d_last[2] = {nullptr, nullptr};
+  uint32_t *d_err = nullptr;
+  float *d_score = nullptr;
+  uint64_t *d_sad = nullptr;
+  uint32_t *d_hist = nullptr;
+  uint8_t *d_rgb = nullptr;       // RGB thumbnails of every frame
+  bool fused = false;             // scoring fused into reconstruction
+  uint8_t *d_thumb[2] = {nullptr, nullptr};  // fused: [slot][h][w] thumbnail luma
+  int64_t thumb_px = 0;
+  hipStream_t s_dec = nullptr, s_score = nullptr, s_parse = nullptr;
+  std::vector<hipEvent_t> ev;  // per window: dec start, parsed, decoded, score start, scored, spare
+  std::vector<hipEvent_t> lev;  // per window: (start, end) per reconstruct launch, then one per parse chunk
+  hipEvent_t ev_start = nullptr, ev_end = nullptr;
+  double timings[4] = {0, 0, 0, 0};
+  int64_t last_window_done = -1;
+  // command epochs: run_no counts window runs; a ring is cleared on first use
+  // and again before an epoch value could repeat (h264.h kCmdEpochs)
+  int64_t run_no = 0;
+  int64_t ring_cleared_at[2] = {-1, -1};
+  bool have_results = false;
+  std::vector<float> host_scores;
+  vts::SmallStore small;       // transcode: downscaled frames (off unless vts_transcode ran)
+};
+
+namespace vts {
+// Decode + score every window (and downscale when ctx->small.on).
+int run_all(vts_ctx *c);
+int fetch_scores(vts_ctx *c);
+// downscale the window's frames (transcode.hip)
+int small_window(vts_ctx *c, int ring, int64_t f0, int64_t f1, hipStream_t s);
+}  // namespace vts

@@ -30,6 +30,7 @@
 #include "decode.h"
 #include "h264.h"
 #include "mp4.h"
+#include "session.h"
 
 namespace vts {
 int fill_video_info(const Mp4Info &mp4, vts_video_info *info);
@@ -43,76 +44,7 @@ constexpr int64_t kSingleWindowBytes = 48ll << 30;  // up to 48 GiB decoded: one
 constexpr int64_t kMinRingBytes = 1ll << 30;        // else two rings of >= 1 GiB
 constexpr int64_t kPad = 256;
 
-#define HIP_TRY(expr)                                                              \
-  do {                                                                             \
-    hipError_t _e = (expr);                                                        \
-    if (_e != hipSuccess)                                                          \
-      return fail(VTS_E_HIP, "%s failed: %s", #expr, hipGetErrorString(_e));       \
-  } while (0)
-
-struct Window {
-  int64_t f0 = 0, f1 = 0;          // frames [f0, f1)
-  int64_t s0 = 0, s1 = 0;          // slices [s0, s1), ordered by reconstruct launch
-  std::vector<int64_t> lvl_off;    // into level_frames, one entry per reconstruct launch
-  std::vector<int32_t> lvl_cnt;
-  std::vector<int64_t> lvl_s0;     // first slice (absolute) of each launch's frames
-  std::vector<int32_t> chunk_end;  // parse chunk j covers launches [chunk_end[j-1], chunk_end[j])
-  int64_t ev0 = 0;                 // first index of this window's events in vts_ctx::lev
-  int64_t post_off = 0, post_cnt = 0;  // into post_slots
-};
-
 }  // namespace
-
-struct vts_ctx {
-  int device = 0;
-  Sps sps;
-  Pps pps;
-  H264DevParams prm{};
-  vts_video_info info{};
-  vts_params params{};
-  int k = 4;
-  int width = 0, height = 0, pitch = 0, coded_w = 0, coded_h = 0;
-  int64_t frame_stride = 0;
-  int64_t n_frames = 0;
-  std::vector<int64_t> pts;
-  std::vector<SliceDesc> slices;
-  std::vector<int4> level_frames;
-  std::vector<int32_t> post_slots;  // per window: slots whose SAD the thumb_sad pass makes
-  std::vector<Window> windows;
-  int64_t ring_frames = 0;
-  int n_rings = 1;
-  // device
-  uint8_t *d_es = nullptr;
-  int64_t es_bytes = 0;
-  SliceDesc *d_slices = nullptr;
-  int4 *d_levels = nullptr;
-  int32_t *d_post = nullptr;
-  uint64_t *d_cmd[2] = {nullptr, nullptr};
-  uint8_t *d_surf[2] = {nullptr, nullptr};
-  uint8_t *d_ws[2] = {nullptr, nullptr};
-  int64_t ws_bytes = 0;
-  uint8_t *d_last[2] = {nullptr, nullptr};
-  uint32_t *d_err = nullptr;
-  float *d_score = nullptr;
-  uint64_t *d_sad = nullptr;
-  uint32_t *d_hist = nullptr;
-  uint8_t *d_rgb = nullptr;       // RGB thumbnails of every frame
-  bool fused = false;             // scoring fused into reconstruction
-  uint8_t *d_thumb[2] = {nullptr, nullptr};  // fused: [slot][h][w] thumbnail luma
-  int64_t thumb_px = 0;
-  hipStream_t s_dec = nullptr, s_score = nullptr, s_parse = nullptr;
-  std::vector<hipEvent_t> ev;  // per window: dec start, parsed, decoded, score start, scored, spare
-  std::vector<hipEvent_t> lev;  // per window: (start, end) per reconstruct launch, then one per parse chunk
-  hipEvent_t ev_start = nullptr, ev_end = nullptr;
-  double timings[4] = {0, 0, 0, 0};
-  int64_t last_window_done = -1;
-  // command epochs: run_no counts window runs; a ring is cleared on first use
-  // and again before an epoch value could repeat (h264.h kCmdEpochs)
-  int64_t run_no = 0;
-  int64_t ring_cleared_at[2] = {-1, -1};
-  bool have_results = false;
-  std::vector<float> host_scores;
-};
 
 namespace {
 
@@ -471,7 +403,9 @@ int open_common(int device, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_
   return VTS_OK;
 }
 
-int run_all(vts_ctx *c) {
+}  // namespace
+
+int vts::run_all(vts_ctx *c) {
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
   HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
@@ -570,6 +504,8 @@ int run_all(vts_ctx *c) {
       if (l + 1 == nl || static_cast<int32_t>(l + 1) == w.chunk_end[j - 1])
         HIP_TRY(hipEventRecord(LE[2 * l + 1], sd));
     }
+    // transcode: the 360p copy of the window's frames, while they are in the ring
+    if (c->small.on) VTS_TRY(small_window(c, r, w.f0, w.f1, sd));
     HIP_TRY(hipEventRecord(E[2], sd));
     HIP_TRY(hipStreamWaitEvent(ss, E[2], 0));
     HIP_TRY(hipEventRecord(E[3], ss));
@@ -651,15 +587,13 @@ int run_all(vts_ctx *c) {
   return VTS_OK;
 }
 
-int fetch_scores(vts_ctx *c) {
+int vts::fetch_scores(vts_ctx *c) {
   if (!c->host_scores.empty()) return VTS_OK;
   c->host_scores.resize(static_cast<size_t>(c->n_frames));
   HIP_TRY(hipMemcpy(c->host_scores.data(), c->d_score, sizeof(float) * c->n_frames,
                     hipMemcpyDeviceToHost));
   return VTS_OK;
 }
-
-}  // namespace
 
 extern "C" int vts_device_count(void) {
   int n = 0;
@@ -823,6 +757,8 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_sad);
   f(c->d_hist);
   f(c->d_rgb);
+  f(c->small.d);
+  f(c->small.d_taps);
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->lev)

@@ -243,7 +243,11 @@ void append_nal(std::vector<uint8_t> &sample, uint8_t header, std::vector<uint8_
   sample.insert(sample.end(), nal.begin(), nal.end());
 }
 
-int pick_level(int mbs, double mbps) {
+
+}  // namespace
+
+// Smallest level whose MaxFS / MaxMBPS (Table A-1) admit the stream.
+int h264_pick_level(int mbs, double mbps) {
   struct L { int idc, max_fs; double max_mbps; };
   static const L t[] = {{30, 1620, 40500}, {31, 3600, 108000}, {32, 5120, 216000},
                         {40, 8192, 245760}, {42, 8704, 522240}, {50, 22080, 589824},
@@ -253,10 +257,8 @@ int pick_level(int mbs, double mbps) {
   return 52;
 }
 
-}  // namespace
-
 // Build the SPS/PPS RBSPs for the stream (also used by tests via the file).
-static void make_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level,
+void make_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level,
                          std::vector<uint8_t> *sps_nal, std::vector<uint8_t> *pps_nal) {
   BitWriter s;
   s.u(8, 66);        // profile_idc: Baseline
@@ -328,7 +330,7 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int cw = mbw * 16, ch = mbh * 16;
   const double fps = double(P.fps_num) / P.fps_den;
-  const int level = pick_level(mbw * mbh, mbw * mbh * fps);
+  const int level = h264_pick_level(mbw * mbh, mbw * mbh * fps);
   std::vector<uint8_t> sps, pps;
   make_sps_pps(mbw, mbh, cw - P.width, ch - P.height, level, &sps, &pps);
 

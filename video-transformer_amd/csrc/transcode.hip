@@ -1,0 +1,717 @@
+// transcode.hip — vts_transcode: the 360p upload transcode on the device
+// (replaces the pixel work of the reference's
+// ContentAnalyzer._compress_video_for_upload, content_analyzer.py:167-236,
+// `ffmpeg -vf scale=-2:360 -c:v libx264 -crf 28`).  DESIGN.md §11.
+//
+// Pipeline, all device work after the one decode:
+//   1. the session's decode + score run (run_all), with `small_window`
+//      downscaling every window's frames (area filter, NV12 -> NV12 at
+//      (w, 360), coded 16-aligned) into a whole-video store while they sit
+//      in the decode ring;
+//   2. GOP plan on the host from the scene scores: IDR at frame 0, at every
+//      cut and every `keyint` frames;
+//   3. per GOP position j ("level", every GOP at once, as the decoder's
+//      reconstruct levels): `enc_search` — one wave per macroblock, full
+//      integer motion search in LDS against the previous reconstruction,
+//      decision inter / I_PCM, reconstruction written (the next level's
+//      reference); `enc_write` — one lane per slice (macroblock row) writes
+//      the CAVLC slice NAL with emulation prevention into a fixed-capacity
+//      staging slot; `enc_gather` compacts the level's slices for one D2H
+//      copy;
+//   4. host: MP4 mux (Mp4Writer) in display order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "mp4.h"
+#include "session.h"
+
+namespace vts {
+namespace {
+
+constexpr uint32_t kPcmCmd = 0x80008000u;  // (mvx, mvy) = (-32768, -32768): never a motion
+constexpr int kMaxTaps = 16;
+constexpr int kMaxRange = 16;
+constexpr int kWinPitch = 16 + 2 * kMaxRange + 4;  // LDS window row pitch (bytes)
+
+// ----------------------------------------------------------- downscale
+// Area filter, per axis: destination o covers source footprint [o n, (o+1) n)
+// in units of 1/m; source i covers [i m, (i+1) m).  Tap table entry o =
+// [i0, w_0 .. w_{K-1}] (weights / gcd(n, m)); outputs past the display size
+// (coded padding) repeat the last display entry.
+struct DsArgs {
+  const uint8_t *src;      // ring surface of the window's first frame
+  int64_t src_stride;
+  int32_t pitch, uv_rows;  // UV plane at pitch * uv_rows
+  int32_t sw, sh;          // source display size
+  uint8_t *dst;            // small store, the window's first frame
+  int64_t dst_stride;
+  int32_t cw, ch;          // destination coded size
+  const int32_t *tx, *ty, *tcx, *tcy;
+  int32_t kx, ky, kcx, kcy;
+  int32_t tl, tc;          // normalisers (product of the axes' n / gcd)
+  int64_t n_frames;
+};
+
+__device__ __forceinline__ uint32_t area_px(const uint8_t *p, int pitch, int step, const int32_t *ex,
+                                            int kx, const int32_t *ey, int ky, int nx, int ny, int t) {
+  uint32_t sum = 0;
+  const int x0 = ex[0], y0 = ey[0];
+  for (int j = 0; j < ky; ++j) {
+    const uint32_t wy = static_cast<uint32_t>(ey[1 + j]);
+    if (!wy) continue;
+    const uint8_t *row = p + static_cast<int64_t>(min(y0 + j, ny - 1)) * pitch;
+    uint32_t s = 0;
+    for (int i = 0; i < kx; ++i) s += static_cast<uint32_t>(ex[1 + i]) * row[min(x0 + i, nx - 1) * step];
+    sum += wy * s;
+  }
+  const uint32_t v = (sum + static_cast<uint32_t>(t) / 2) / static_cast<uint32_t>(t);
+  return v < 1 ? 1u : v;
+}
+
+__global__ void __launch_bounds__(256) downscale_nv12(DsArgs a) {
+  const int groups = a.cw / 4;
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  const int rows = a.ch + a.ch / 2;
+  if (t >= static_cast<int64_t>(groups) * rows) return;
+  const int64_t f = blockIdx.y;
+  const int g = static_cast<int>(t % groups), row = static_cast<int>(t / groups);
+  const uint8_t *src = a.src + f * a.src_stride;
+  uint8_t *dst = a.dst + f * a.dst_stride;
+  uint32_t out = 0;
+  if (row < a.ch) {
+    const int32_t *ey = a.ty + static_cast<int64_t>(row) * (1 + a.ky);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int32_t *ex = a.tx + static_cast<int64_t>(4 * g + q) * (1 + a.kx);
+      out |= area_px(src, a.pitch, 1, ex, a.kx, ey, a.ky, a.sw, a.sh, a.tl) << (8 * q);
+    }
+    *reinterpret_cast<uint32_t *>(dst + static_cast<int64_t>(row) * a.cw + 4 * g) = out;
+  } else {
+    const int cy = row - a.ch;
+    const uint8_t *uv = src + static_cast<int64_t>(a.pitch) * a.uv_rows;
+    const int32_t *ey = a.tcy + static_cast<int64_t>(cy) * (1 + a.kcy);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // bytes U0 V0 U1 V1 of chroma columns 2g, 2g+1
+      const int32_t *ex = a.tcx + static_cast<int64_t>(2 * g + (q >> 1)) * (1 + a.kcx);
+      out |= area_px(uv + (q & 1), a.pitch, 2, ex, a.kcx, ey, a.kcy, a.sw / 2, a.sh / 2, a.tc) << (8 * q);
+    }
+    *reinterpret_cast<uint32_t *>(dst + static_cast<int64_t>(a.cw) * a.ch + static_cast<int64_t>(cy) * a.cw +
+                                  4 * g) = out;
+  }
+}
+
+// ------------------------------------------------------ motion search
+struct SearchArgs {
+  const int4 *ent;      // per frame of the level: (frame, ref slot or -1 = small[frame-1], dst slot, 0)
+  const uint8_t *small;
+  int64_t stride;
+  uint8_t *recon;       // [slot]
+  uint32_t *cmd;        // [entry][mb]
+  int32_t cw, ch, mbw, nmb;
+  int32_t range, max_sad;
+};
+
+__device__ __forceinline__ uint32_t u32_at(const uint8_t *lds_row, int off) {  // 4 bytes at any offset
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(lds_row + (off & ~3));
+  return __builtin_amdgcn_alignbyte(p[1], p[0], off & 3);  // byte shift
+}
+
+// One wave per macroblock: the reference window (16 + 2R)^2 and the source
+// block go to LDS; each lane takes candidates c = lane, lane + 64, ...;
+// (least luma SAD, candidate index) is a 64-bit min over the wave.
+__global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
+  __shared__ uint8_t win[(16 + 2 * kMaxRange) * kWinPitch];
+  __shared__ uint32_t srcy[64];
+  const int lane = threadIdx.x;
+  const int64_t e = blockIdx.x / a.nmb;
+  const int mb = static_cast<int>(blockIdx.x % a.nmb);
+  const int mx = mb % a.mbw, my = mb / a.mbw;
+  const int4 en = a.ent[e];
+  const uint8_t *src = a.small + static_cast<int64_t>(en.x) * a.stride;
+  const uint8_t *ref = en.y < 0 ? a.small + static_cast<int64_t>(en.x - 1) * a.stride
+                                : a.recon + static_cast<int64_t>(en.y) * a.stride;
+  uint8_t *dst = a.recon + static_cast<int64_t>(en.z) * a.stride;
+  const int R = a.range, side = 2 * R + 1, wsz = 16 + 2 * R;
+  const int x0 = mx * 16 - R, y0 = my * 16 - R;
+  // source luma: lane -> row lane / 4, 4 bytes
+  srcy[lane] = *reinterpret_cast<const uint32_t *>(src + static_cast<int64_t>(my * 16 + (lane >> 2)) * a.cw +
+                                                   mx * 16 + 4 * (lane & 3));
+  for (int i = lane; i < wsz * wsz; i += 64) {
+    const int yy = i / wsz, xx = i % wsz;
+    const int sy = min(max(y0 + yy, 0), a.ch - 1), sx = min(max(x0 + xx, 0), a.cw - 1);
+    win[yy * kWinPitch + xx] = ref[static_cast<int64_t>(sy) * a.cw + sx];
+  }
+  __syncthreads();
+  const int ncand = side * side, center = R * side + R;
+  uint64_t best = ~0ull;
+  for (int c = lane; c < ncand; c += 64) {
+    const int r = c == 0 ? center : (c - 1 < center ? c - 1 : c);
+    const int dy = r / side - R, dx = r % side - R;
+    const int bx = mx * 16 + dx, by = my * 16 + dy;
+    if (bx < 0 || by < 0 || bx + 16 > a.cw || by + 16 > a.ch) continue;
+    uint32_t s = 0;
+    const int ox = dx + R;
+#pragma unroll 4
+    for (int yy = 0; yy < 16; ++yy) {
+      const uint8_t *row = win + (dy + R + yy) * kWinPitch;
+      s = __builtin_amdgcn_sad_u8(u32_at(row, ox), srcy[4 * yy], s);
+      s = __builtin_amdgcn_sad_u8(u32_at(row, ox + 4), srcy[4 * yy + 1], s);
+      s = __builtin_amdgcn_sad_u8(u32_at(row, ox + 8), srcy[4 * yy + 2], s);
+      s = __builtin_amdgcn_sad_u8(u32_at(row, ox + 12), srcy[4 * yy + 3], s);
+    }
+    const uint64_t key = (static_cast<uint64_t>(s) << 32) | static_cast<uint32_t>(c);
+    best = key < best ? key : best;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(best, off);
+    best = o < best ? o : best;
+  }
+  const int c = static_cast<int>(best & 0xffffffffu);  // (0,0) is always valid
+  const int r = c == 0 ? center : (c - 1 < center ? c - 1 : c);
+  const int dy = r / side - R, dx = r % side - R;
+  // prediction and cost: lane -> 4 luma samples (row lane/4) and one chroma pair
+  const int ly = lane >> 2, lx = 4 * (lane & 3);
+  const uint32_t py = u32_at(win + (dy + R + ly) * kWinPitch, dx + R + lx);
+  const uint32_t sy4 = srcy[lane];
+  uint32_t cost = __builtin_amdgcn_sad_u8(py, sy4, 0);
+  const int ci = lane & 7, cj = lane >> 3, ccw = a.cw / 2, cch = a.ch / 2;
+  const int mvx = 4 * dx, mvy = 4 * dy, fx = mvx & 7, fy = mvy & 7;
+  const int xi = mx * 8 + ci + (mvx >> 3), yi = my * 8 + cj + (mvy >> 3);
+  const int xa = min(max(xi, 0), ccw - 1), xb = min(max(xi + 1, 0), ccw - 1);
+  const int ya = min(max(yi, 0), cch - 1), yb = min(max(yi + 1, 0), cch - 1);
+  const uint8_t *ruv = ref + static_cast<int64_t>(a.cw) * a.ch;
+  const uint16_t A = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(ya) * a.cw + 2 * xa);
+  const uint16_t B = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(ya) * a.cw + 2 * xb);
+  const uint16_t Cc = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(yb) * a.cw + 2 * xa);
+  const uint16_t D = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(yb) * a.cw + 2 * xb);
+  const int wa = (8 - fx) * (8 - fy), wb = fx * (8 - fy), wc = (8 - fx) * fy, wd = fx * fy;
+  const int pu = (wa * (A & 255) + wb * (B & 255) + wc * (Cc & 255) + wd * (D & 255) + 32) >> 6;
+  const int pv = (wa * (A >> 8) + wb * (B >> 8) + wc * (Cc >> 8) + wd * (D >> 8) + 32) >> 6;
+  const int64_t co = static_cast<int64_t>(a.cw) * a.ch + static_cast<int64_t>(my * 8 + cj) * a.cw + 2 * (mx * 8 + ci);
+  const uint16_t suv = *reinterpret_cast<const uint16_t *>(src + co);
+  cost += static_cast<uint32_t>(abs(pu - (suv & 255)) + abs(pv - (suv >> 8)));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cost += __shfl_xor(cost, off);
+  const bool inter = a.max_sad >= 0 && cost <= static_cast<uint32_t>(a.max_sad);
+  const int64_t lo = static_cast<int64_t>(my * 16 + ly) * a.cw + mx * 16 + lx;
+  *reinterpret_cast<uint32_t *>(dst + lo) = inter ? py : sy4;
+  *reinterpret_cast<uint16_t *>(dst + co) = inter ? static_cast<uint16_t>(pu | (pv << 8)) : suv;
+  if (lane == 0)
+    a.cmd[e * a.nmb + mb] =
+        inter ? (static_cast<uint32_t>(static_cast<uint16_t>(mvx)) | (static_cast<uint32_t>(static_cast<uint16_t>(mvy)) << 16))
+              : kPcmCmd;
+}
+
+// ------------------------------------------------------ slice writer
+struct WriteArgs {
+  const int4 *ent;      // per frame of the level: (frame, GOP position j, IDR parity, 0)
+  const uint32_t *cmd;  // [entry][mb] (P levels)
+  const uint8_t *small;
+  int64_t stride;
+  int32_t cw, ch, mbw, mbh;
+  uint8_t *staging;     // [slice][cap]
+  int64_t cap;
+  int32_t *sizes;       // [slice] bytes incl. the 4-byte length prefix
+  unsigned long long *stats;  // pcm, inter, skip
+  uint32_t *err;
+  int32_t n_slices;
+  int32_t idr;          // level 0: every picture IDR
+};
+
+// RBSP bits -> EBSP bytes (emulation prevention) into a staging slot.
+struct NalOut {
+  uint8_t *p;
+  int64_t cap, n;
+  uint64_t acc;
+  int nacc, zeros;
+  bool over;
+  __device__ void byte(uint32_t b) {
+    if (zeros >= 2 && b <= 3) {
+      put(3);
+      zeros = 0;
+    }
+    put(b);
+    zeros = b ? 0 : zeros + 1;
+  }
+  __device__ void put(uint32_t b) {
+    if (n < cap) p[n] = static_cast<uint8_t>(b);
+    else over = true;
+    ++n;
+  }
+  __device__ void bits(int k, uint32_t v) {  // k <= 32
+    acc = (acc << k) | v;
+    nacc += k;
+    while (nacc >= 8) {
+      nacc -= 8;
+      byte(static_cast<uint32_t>(acc >> nacc) & 0xffu);
+    }
+  }
+  __device__ void ue(uint32_t v) {
+    const uint32_t x = v + 1;
+    const int len = 31 - __builtin_clz(x);
+    if (len) bits(len, 0);
+    bits(len + 1, x);
+  }
+  __device__ void se(int v) { ue(v > 0 ? static_cast<uint32_t>(2 * v - 1) : static_cast<uint32_t>(-2 * v)); }
+  __device__ void align() {
+    if (nacc) bits(8 - nacc, 0);
+  }
+};
+
+__device__ void put_pcm(NalOut &o, const uint8_t *src, int cw, int ch, int mx, int my) {
+  o.align();
+  for (int j = 0; j < 16; ++j) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(src + static_cast<int64_t>(my * 16 + j) * cw + mx * 16);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int q = 0; q < 16; ++q) o.byte((w[q >> 2] >> (8 * (q & 3))) & 0xffu);
+  }
+  const uint8_t *uv = src + static_cast<int64_t>(cw) * ch;
+  for (int pl = 0; pl < 2; ++pl)
+    for (int j = 0; j < 8; ++j) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(uv + static_cast<int64_t>(my * 8 + j) * cw + mx * 16);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      for (int q = 0; q < 8; ++q) o.byte((w[q >> 1] >> (16 * (q & 1) + 8 * pl)) & 0xffu);
+    }
+}
+
+__global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.n_slices) return;
+  const int e = s / a.mbh, row = s % a.mbh;
+  const int4 en = a.ent[e];
+  const uint8_t *src = a.small + static_cast<int64_t>(en.x) * a.stride;
+  uint8_t *slot = a.staging + static_cast<int64_t>(s) * a.cap;
+  NalOut o{slot + 4, a.cap - 4, 0, 0, 0, 0, false};
+  o.put(a.idr ? 0x65 : 0x41);  // nal_ref_idc 3 IDR / 2 non-IDR; every picture is a reference
+  o.ue(static_cast<uint32_t>(row * a.mbw));  // first_mb_in_slice
+  o.ue(a.idr ? 7 : 5);                       // slice_type I / P (all slices of the picture)
+  o.ue(0);                                   // pic_parameter_set_id
+  o.bits(16, static_cast<uint32_t>(en.y) & 0xffffu);  // frame_num (16 bits)
+  if (a.idr) {
+    o.ue(static_cast<uint32_t>(en.z));       // idr_pic_id
+    o.bits(2, 0);                            // no_output_of_prior_pics, long_term_reference
+  } else {
+    o.bits(3, 0);  // num_ref_idx_active_override, ref_pic_list_modification_l0, adaptive_ref_pic_marking
+  }
+  o.se(0);  // slice_qp_delta
+  o.ue(1);  // disable_deblocking_filter_idc
+  unsigned long long npcm = 0, ninter = 0, nskip = 0;
+  uint32_t skip = 0;
+  bool a_ok = false;
+  int amx = 0, amy = 0;
+  const uint32_t *cmd = a.cmd + static_cast<int64_t>(e) * a.mbw * a.mbh + static_cast<int64_t>(row) * a.mbw;
+  for (int mx = 0; mx < a.mbw; ++mx) {
+    if (a.idr) {
+      o.ue(25);
+      put_pcm(o, src, a.cw, a.ch, mx, row);
+      ++npcm;
+      continue;
+    }
+    const uint32_t c = cmd[mx];
+    if (c == kPcmCmd) {
+      o.ue(skip);
+      skip = 0;
+      o.ue(30);  // I_PCM in a P slice
+      put_pcm(o, src, a.cw, a.ch, mx, row);
+      a_ok = false;
+      ++npcm;
+      continue;
+    }
+    const int mvx = static_cast<int16_t>(c & 0xffffu), mvy = static_cast<int16_t>(c >> 16);
+    if (mvx == 0 && mvy == 0) {  // P_Skip (neighbour B lies in another slice: skip motion is 0)
+      ++skip;
+      ++nskip;
+    } else {
+      const int px = a_ok ? amx : 0, py = a_ok ? amy : 0;  // 8.4.1.3, A the only neighbour
+      o.ue(skip);
+      skip = 0;
+      o.ue(0);  // P_L0_16x16
+      o.se(mvx - px);
+      o.se(mvy - py);
+      o.ue(0);  // coded_block_pattern 0
+      ++ninter;
+    }
+    a_ok = true;
+    amx = mvx;
+    amy = mvy;
+  }
+  if (skip) o.ue(skip);
+  o.bits(1, 1);  // rbsp_stop_one_bit
+  o.align();
+  const int64_t len = o.n;
+  if (o.over) {
+    atomicOr(a.err, 1u);
+    a.sizes[s] = 0;
+    return;
+  }
+  slot[0] = static_cast<uint8_t>(len >> 24);
+  slot[1] = static_cast<uint8_t>(len >> 16);
+  slot[2] = static_cast<uint8_t>(len >> 8);
+  slot[3] = static_cast<uint8_t>(len);
+  a.sizes[s] = static_cast<int32_t>(len + 4);
+  atomicAdd(&a.stats[0], npcm);
+  atomicAdd(&a.stats[1], ninter);
+  atomicAdd(&a.stats[2], nskip);
+}
+
+// one workgroup per slice: staging slot -> packed level output
+__global__ void __launch_bounds__(256) enc_gather(const uint8_t *staging, int64_t cap, const int32_t *sizes,
+                                                  const int64_t *offs, uint8_t *out) {
+  const int s = blockIdx.x;
+  const uint8_t *p = staging + static_cast<int64_t>(s) * cap;
+  uint8_t *q = out + offs[s];
+  const int n = sizes[s];
+  for (int i = threadIdx.x; i < n; i += 256) q[i] = p[i];
+}
+
+// ------------------------------------------------------------ host
+int64_t gcd64(int64_t a, int64_t b) {
+  while (b) {
+    const int64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// tap table for n source -> m destination samples over `coded` outputs
+std::vector<int32_t> area_taps(int64_t n, int64_t m, int coded, int *k_out, int32_t *t_out) {
+  const int64_t g = gcd64(n, m);
+  int k = 1;
+  for (int64_t o = 0; o < m; ++o) {
+    const int64_t i0 = o * n / m, i1 = ((o + 1) * n + m - 1) / m;
+    k = std::max<int>(k, static_cast<int>(i1 - i0));
+  }
+  std::vector<int32_t> t(static_cast<size_t>(coded) * (1 + k), 0);
+  for (int x = 0; x < coded; ++x) {
+    const int64_t o = std::min<int64_t>(x, m - 1);
+    const int64_t i0 = o * n / m;
+    int32_t *e = &t[static_cast<size_t>(x) * (1 + k)];
+    e[0] = static_cast<int32_t>(i0);
+    for (int i = 0; i < k; ++i) {
+      const int64_t si = i0 + i;
+      const int64_t lo = std::max(o * n, si * m), hi = std::min((o + 1) * n, (si + 1) * m);
+      e[1 + i] = (si < n && hi > lo) ? static_cast<int32_t>((hi - lo) / g) : 0;
+    }
+  }
+  *k_out = k;
+  *t_out = static_cast<int32_t>(n / g);
+  return t;
+}
+
+template <class T>
+int dev_alloc(T **p, size_t n) {
+  HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(1, n) * sizeof(T)));
+  return VTS_OK;
+}
+
+struct DevBufs {  // transcode scratch, freed on every exit path
+  std::vector<void *> ptrs;
+  template <class T>
+  int get(T **p, size_t n) {
+    VTS_TRY(dev_alloc(p, n));
+    ptrs.push_back(*p);
+    return VTS_OK;
+  }
+  ~DevBufs() {
+    for (void *p : ptrs) (void)hipFree(p);
+  }
+};
+
+int setup_small(vts_ctx *c, int sh) {
+  SmallStore &S = c->small;
+  const int W = c->width, H = c->height;
+  const int sw = static_cast<int>((static_cast<int64_t>(sh) * W + H) / (2 * static_cast<int64_t>(H))) * 2;
+  if (sw < 2) return fail(VTS_E_INVALID, "output width %d from %dx%d at height %d", sw, W, H, sh);
+  if (S.d && S.w == sw && S.h == sh) return VTS_OK;
+  if (S.d) (void)hipFree(S.d);
+  if (S.d_taps) (void)hipFree(S.d_taps);
+  S = SmallStore{};
+  S.w = sw;
+  S.h = sh;
+  S.cw = (sw + 15) & ~15;
+  S.ch = (sh + 15) & ~15;
+  S.stride = (static_cast<int64_t>(S.cw) * S.ch * 3 / 2 + 255) & ~int64_t(255);
+  int32_t tl_x, tl_y, tc_x, tc_y;
+  const auto tx = area_taps(W, sw, S.cw, &S.taps_x, &tl_x);
+  const auto ty = area_taps(H, sh, S.ch, &S.taps_y, &tl_y);
+  const auto tcx = area_taps(W / 2, sw / 2, S.cw / 2, &S.taps_cx, &tc_x);
+  const auto tcy = area_taps(H / 2, sh / 2, S.ch / 2, &S.taps_cy, &tc_y);
+  if (std::max({S.taps_x, S.taps_y, S.taps_cx, S.taps_cy}) > kMaxTaps)
+    return fail(VTS_E_UNSUPPORTED, "downscale ratio %dx%d -> %dx%d needs more than %d taps", W, H, sw, sh,
+                kMaxTaps);
+  if (static_cast<int64_t>(tl_x) * tl_y * 255 > 0x7fffffffll || static_cast<int64_t>(tc_x) * tc_y * 255 > 0x7fffffffll)
+    return fail(VTS_E_UNSUPPORTED, "downscale ratio %dx%d -> %dx%d overflows 32-bit sums", W, H, sw, sh);
+  S.tl = tl_x * tl_y;
+  S.tc = tc_x * tc_y;
+  std::vector<int32_t> all;
+  S.off[0] = 0;
+  for (const auto *v : {&tx, &ty, &tcx, &tcy}) {
+    all.insert(all.end(), v->begin(), v->end());
+  }
+  S.off[1] = static_cast<int64_t>(tx.size());
+  S.off[2] = S.off[1] + static_cast<int64_t>(ty.size());
+  S.off[3] = S.off[2] + static_cast<int64_t>(tcx.size());
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMalloc(&S.d_taps, all.size() * sizeof(int32_t)));
+  HIP_TRY(hipMemcpy(S.d_taps, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  const size_t bytes = static_cast<size_t>(S.stride * c->n_frames + 256);
+  if (hipMalloc(&S.d, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    S.d = nullptr;
+    return fail(VTS_E_HIP, "cannot allocate %.1f GiB for the %dx%d frames", bytes / 1073741824.0, sw, sh);
+  }
+  return VTS_OK;
+}
+
+}  // namespace
+
+int small_window(vts_ctx *c, int ring, int64_t f0, int64_t f1, hipStream_t s) {
+  const SmallStore &S = c->small;
+  DsArgs a{};
+  a.src = c->d_surf[ring];
+  a.src_stride = c->frame_stride;
+  a.pitch = c->pitch;
+  a.uv_rows = c->coded_h;
+  a.sw = c->width;
+  a.sh = c->height;
+  a.dst = S.d + f0 * S.stride;
+  a.dst_stride = S.stride;
+  a.cw = S.cw;
+  a.ch = S.ch;
+  a.tx = S.d_taps + S.off[0];
+  a.ty = S.d_taps + S.off[1];
+  a.tcx = S.d_taps + S.off[2];
+  a.tcy = S.d_taps + S.off[3];
+  a.kx = S.taps_x;
+  a.ky = S.taps_y;
+  a.kcx = S.taps_cx;
+  a.kcy = S.taps_cy;
+  a.tl = S.tl;
+  a.tc = S.tc;
+  a.n_frames = f1 - f0;
+  const int64_t threads = static_cast<int64_t>(S.cw / 4) * (S.ch + S.ch / 2);
+  hipLaunchKernelGGL(downscale_nv12, dim3(static_cast<unsigned>((threads + 255) / 256), static_cast<unsigned>(f1 - f0)),
+                     dim3(256), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "downscale_nv12 launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
+}  // namespace vts
+
+using namespace vts;
+
+extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transcode_params *pin,
+                             vts_transcode_info *info) {
+  clear_error();
+  if (!c || !out_path) return fail(VTS_E_INVALID, "NULL argument");
+  using clk = std::chrono::steady_clock;
+  vts_transcode_params p{};
+  if (pin) p = *pin;
+  const int sh = p.height > 0 ? p.height : 360;
+  const int R = p.search_range == 0 ? 8 : std::max(0, p.search_range);
+  const int T = p.max_mb_sad == 0 ? 768 : p.max_mb_sad;
+  const int keyint = p.keyint > 0 ? p.keyint : 250;
+  const float thr = p.cut_threshold > 0 ? p.cut_threshold : c->params.cut_threshold;
+  if ((sh & 1) || sh < 16 || sh > c->height)
+    return fail(VTS_E_INVALID, "output height %d: even, 16 .. source height %d", sh, c->height);
+  if (R > kMaxRange) return fail(VTS_E_INVALID, "search_range %d > %d", R, kMaxRange);
+  // constant frame rate (the writer's stts is one entry)
+  const int64_t n = c->n_frames;
+  int64_t delta = n > 1 ? c->pts[1] - c->pts[0] : std::max<int64_t>(1, c->info.track_timescale / 30);
+  for (int64_t i = 1; i < n; ++i)
+    if (c->pts[i] - c->pts[i - 1] != delta)
+      return fail(VTS_E_UNSUPPORTED, "variable frame rate (frame %lld) is not transcoded",
+                  static_cast<long long>(i));
+  HIP_TRY(hipSetDevice(c->device));
+  VTS_TRY(setup_small(c, sh));
+  const SmallStore &S = c->small;
+  const int mbw = S.cw / 16, mbh = S.ch / 16, nmb = mbw * mbh;
+  double ms[4] = {0, 0, 0, 0};
+
+  // 1. decode + score + downscale
+  auto t0 = clk::now();
+  c->small.on = true;
+  const int rc = run_all(c);
+  c->small.on = false;
+  VTS_TRY(rc);
+  VTS_TRY(fetch_scores(c));
+  ms[0] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+
+  // 2. GOPs: IDR at frame 0, at cuts, every keyint frames
+  std::vector<int64_t> gop_start;
+  for (int64_t f = 0; f < n; ++f)
+    if (f == 0 || c->host_scores[f] > thr || f - gop_start.back() >= keyint) gop_start.push_back(f);
+  const int64_t ngop = static_cast<int64_t>(gop_start.size());
+  std::vector<int64_t> gop_len(static_cast<size_t>(ngop));
+  int64_t maxlen = 0;
+  for (int64_t g = 0; g < ngop; ++g) {
+    gop_len[g] = (g + 1 < ngop ? gop_start[g + 1] : n) - gop_start[g];
+    maxlen = std::max(maxlen, gop_len[g]);
+  }
+  // per level j: search entries (frame, ref slot, dst slot) and write entries (frame, j, idr parity)
+  std::vector<int4> sent, went;
+  std::vector<int64_t> lvl_off(static_cast<size_t>(maxlen) + 1, 0);
+  for (int64_t j = 0; j < maxlen; ++j) {
+    lvl_off[j] = static_cast<int64_t>(went.size());
+    for (int64_t g = 0; g < ngop; ++g) {
+      if (gop_len[g] <= j) continue;
+      const int f = static_cast<int>(gop_start[g] + j);
+      sent.push_back(make_int4(f, j == 1 ? -1 : static_cast<int>(2 * g + ((j - 1) & 1)), static_cast<int>(2 * g + (j & 1)), 0));
+      went.push_back(make_int4(f, static_cast<int>(j), static_cast<int>(g & 1), 0));
+    }
+  }
+  lvl_off[maxlen] = static_cast<int64_t>(went.size());
+  int64_t max_ent = 0;
+  for (int64_t j = 0; j < maxlen; ++j) max_ent = std::max(max_ent, lvl_off[j + 1] - lvl_off[j]);
+
+  // 3. device encode, level by level
+  const int64_t cap = ((64 + static_cast<int64_t>(mbw) * 420) + 255) & ~int64_t(255);
+  DevBufs B;
+  int4 *d_sent, *d_went;
+  uint8_t *d_recon, *d_stage, *d_out;
+  uint32_t *d_cmd, *d_err;
+  int32_t *d_sizes;
+  int64_t *d_offs;
+  unsigned long long *d_stats;
+  VTS_TRY(B.get(&d_sent, sent.size()));
+  VTS_TRY(B.get(&d_went, went.size()));
+  VTS_TRY(B.get(&d_recon, static_cast<size_t>(2 * ngop * S.stride + 256)));
+  VTS_TRY(B.get(&d_cmd, static_cast<size_t>(max_ent * nmb)));
+  VTS_TRY(B.get(&d_stage, static_cast<size_t>(max_ent * mbh * cap)));
+  VTS_TRY(B.get(&d_out, static_cast<size_t>(max_ent * mbh * cap)));
+  VTS_TRY(B.get(&d_sizes, static_cast<size_t>(max_ent * mbh)));
+  VTS_TRY(B.get(&d_offs, static_cast<size_t>(max_ent * mbh)));
+  VTS_TRY(B.get(&d_stats, 3));
+  VTS_TRY(B.get(&d_err, 1));
+  hipStream_t s = c->s_dec;
+  HIP_TRY(hipMemcpy(d_sent, sent.data(), sent.size() * sizeof(int4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d_went, went.data(), went.size() * sizeof(int4), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemsetAsync(d_stats, 0, 3 * sizeof(unsigned long long), s));
+  HIP_TRY(hipMemsetAsync(d_err, 0, sizeof(uint32_t), s));
+  hipEvent_t e0, e1, e2;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventCreate(&e2));
+  std::vector<uint8_t> host;           // the output samples, level order
+  std::vector<int64_t> fr_off(static_cast<size_t>(n), 0), fr_size(static_cast<size_t>(n), 0);
+  std::vector<int32_t> sizes(static_cast<size_t>(max_ent * mbh));
+  std::vector<int64_t> offs(sizes.size());
+  int status = VTS_OK;
+  for (int64_t j = 0; j < maxlen && status == VTS_OK; ++j) {
+    const int64_t ne = lvl_off[j + 1] - lvl_off[j];
+    const int ns = static_cast<int>(ne * mbh);
+    (void)hipEventRecord(e0, s);
+    if (j > 0) {
+      SearchArgs sa{};
+      sa.ent = d_sent + lvl_off[j];
+      sa.small = S.d;
+      sa.stride = S.stride;
+      sa.recon = d_recon;
+      sa.cmd = d_cmd;
+      sa.cw = S.cw;
+      sa.ch = S.ch;
+      sa.mbw = mbw;
+      sa.nmb = nmb;
+      sa.range = R;
+      sa.max_sad = T;
+      hipLaunchKernelGGL(enc_search, dim3(static_cast<unsigned>(ne * nmb)), dim3(64), 0, s, sa);
+    }
+    (void)hipEventRecord(e1, s);
+    WriteArgs wa{};
+    wa.ent = d_went + lvl_off[j];
+    wa.cmd = d_cmd;
+    wa.small = S.d;
+    wa.stride = S.stride;
+    wa.cw = S.cw;
+    wa.ch = S.ch;
+    wa.mbw = mbw;
+    wa.mbh = mbh;
+    wa.staging = d_stage;
+    wa.cap = cap;
+    wa.sizes = d_sizes;
+    wa.stats = d_stats;
+    wa.err = d_err;
+    wa.n_slices = ns;
+    wa.idr = j == 0;
+    hipLaunchKernelGGL(enc_write, dim3(static_cast<unsigned>((ns + 63) / 64)), dim3(64), 0, s, wa);
+    (void)hipEventRecord(e2, s);
+    hipError_t he = hipGetLastError();
+    if (he != hipSuccess) {
+      status = fail(VTS_E_HIP, "encoder launch: %s", hipGetErrorString(he));
+      break;
+    }
+    if (hipMemcpyAsync(sizes.data(), d_sizes, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      status = fail(VTS_E_HIP, "encoder level %lld failed", static_cast<long long>(j));
+      break;
+    }
+    float a_ms = 0, b_ms = 0;
+    int64_t tot = 0;
+    for (int i = 0; i < ns; ++i) {
+      offs[i] = tot;
+      tot += sizes[i];
+    }
+    for (int64_t k = 0; k < ne; ++k) {
+      const int64_t f = went[lvl_off[j] + k].x;
+      fr_off[f] = static_cast<int64_t>(host.size()) + offs[k * mbh];
+      fr_size[f] = (k + 1 < ne ? offs[(k + 1) * mbh] : tot) - offs[k * mbh];
+    }
+    HIP_TRY(hipMemcpyAsync(d_offs, offs.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(enc_gather, dim3(static_cast<unsigned>(ns)), dim3(256), 0, s, d_stage, cap, d_sizes, d_offs,
+                       d_out);
+    const size_t h0 = host.size();
+    host.resize(h0 + static_cast<size_t>(tot));
+    HIP_TRY(hipMemcpyAsync(host.data() + h0, d_out, static_cast<size_t>(tot), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    (void)hipEventElapsedTime(&a_ms, e0, e1);
+    (void)hipEventElapsedTime(&b_ms, e1, e2);
+    ms[1] += a_ms;
+    ms[2] += b_ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipEventDestroy(e2);
+  VTS_TRY(status);
+  uint32_t err = 0;
+  unsigned long long st[3] = {0, 0, 0};
+  HIP_TRY(hipMemcpy(&err, d_err, sizeof err, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(st, d_stats, sizeof st, hipMemcpyDeviceToHost));
+  if (err) return fail(VTS_E_CAPACITY, "a slice exceeded its %lld-byte staging slot", static_cast<long long>(cap));
+
+  // 4. MP4 (display order)
+  t0 = clk::now();
+  std::vector<uint8_t> sps, pps;
+  const double fps = static_cast<double>(c->info.track_timescale) / static_cast<double>(delta);
+  make_sps_pps(mbw, mbh, S.cw - S.w, S.ch - S.h, h264_pick_level(nmb, nmb * fps), &sps, &pps);
+  Mp4Writer mw;
+  std::string e = mw.open(out_path);
+  std::vector<uint8_t> is_idr(static_cast<size_t>(n), 0);
+  for (int64_t f : gop_start) is_idr[f] = 1;
+  for (int64_t f = 0; f < n && e.empty(); ++f)
+    e = mw.add_sample(host.data() + fr_off[f], static_cast<size_t>(fr_size[f]), is_idr[f] != 0);
+  if (e.empty()) e = mw.finish(S.w, S.h, c->info.track_timescale, delta, sps, pps);
+  if (!e.empty()) return fail(VTS_E_IO, "%s: %s", out_path, e.c_str());
+  ms[3] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  if (info) {
+    std::memset(info, 0, sizeof *info);
+    info->width = S.w;
+    info->height = S.h;
+    info->n_frames = n;
+    info->n_idr = ngop;
+    info->pcm_mbs = static_cast<int64_t>(st[0]);
+    info->inter_mbs = static_cast<int64_t>(st[1]);
+    info->skip_mbs = static_cast<int64_t>(st[2]);
+    info->bytes_written = mw.bytes_written();
+    for (int i = 0; i < 4; ++i) info->ms[i] = ms[i];
+  }
+  return VTS_OK;
+}

@@ -12,7 +12,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libvtseg.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 VTS_OK = 0
 VTS_E_INVALID = -1
@@ -107,6 +107,17 @@ class SynthInfo(C.Structure):
                 ("timescale", C.c_int64), ("recon_hash", C.c_uint64)]
 
 
+class TranscodeParams(C.Structure):
+    _fields_ = [("height", C.c_int32), ("search_range", C.c_int32), ("max_mb_sad", C.c_int32),
+                ("keyint", C.c_int32), ("cut_threshold", C.c_float), ("_pad", C.c_int32)]
+
+
+class TranscodeInfo(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("n_frames", C.c_int64),
+                ("n_idr", C.c_int64), ("pcm_mbs", C.c_int64), ("inter_mbs", C.c_int64),
+                ("skip_mbs", C.c_int64), ("bytes_written", C.c_int64), ("ms", C.c_double * 4)]
+
+
 class ManifestArgs(C.Structure):
     _fields_ = [("video_id", C.c_char_p), ("segment_dir", C.c_char_p),
                 ("created_at", C.c_char_p), ("duration", C.c_double),
@@ -146,6 +157,8 @@ SIGNATURES: dict[str, tuple] = {
     "vts_last_timings": (C.c_int, [C.c_void_p, _P(C.c_double)]),
     "vts_schedule_info": (C.c_int64, [C.c_void_p, C.c_int32]),
     "vts_close": (C.c_int, [C.c_void_p]),
+    "vts_transcode": (C.c_int, [C.c_void_p, C.c_char_p, _P(TranscodeParams),
+                                _P(TranscodeInfo)]),
     "vts_synth_write": (C.c_int, [C.c_char_p, _P(SynthParams), _P(SynthInfo),
                                   _P(C.c_int64), C.c_int64]),
     "vts_last_error": (C.c_char_p, []),

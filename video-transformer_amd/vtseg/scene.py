@@ -199,6 +199,27 @@ class VideoScorer:
             self._ctx, i, out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size))
         return out
 
+    def transcode(self, out_path: str | Path, *, height: int = 360, search_range: int = 8,
+                  max_mb_sad: int = 768, keyint: int = 250,
+                  cut_threshold: float = 0.0) -> dict:
+        """360p upload transcode of this video into `out_path` (vts_transcode,
+        DESIGN.md §11): decode + score + area downscale + device H.264
+        encode.  Returns the facts and per-stage milliseconds."""
+        prm = _lib.TranscodeParams()
+        prm.height = height
+        prm.search_range = search_range if search_range != 0 else -1
+        prm.max_mb_sad = max_mb_sad
+        prm.keyint = keyint
+        prm.cut_threshold = cut_threshold
+        info = _lib.TranscodeInfo()
+        _lib.check(self._lib.vts_transcode(self._ctx, str(out_path).encode(), C.byref(prm),
+                                           C.byref(info)))
+        return {"width": info.width, "height": info.height, "n_frames": info.n_frames,
+                "n_idr": info.n_idr, "pcm_mbs": info.pcm_mbs, "inter_mbs": info.inter_mbs,
+                "skip_mbs": info.skip_mbs, "bytes_written": info.bytes_written,
+                "decode_ms": info.ms[0], "search_ms": info.ms[1], "write_ms": info.ms[2],
+                "mux_ms": info.ms[3]}
+
     def close(self) -> None:
         if getattr(self, "_ctx", None):
             self._lib.vts_close(self._ctx)
