@@ -285,7 +285,7 @@ int vts_close(vts_ctx *ctx);
  * -c:v libx264 -crf 28`).  The session's device decoder decodes every frame,
  * an area filter downscales it to (w, height) with w = ffmpeg's scale=-2
  * width, and a device encoder writes H.264 Constrained Baseline: IDR (all
- * I_PCM) at scene cuts / every keyint frames, P pictures of full-search
+ * I_PCM) every keyint frames (and at scene cuts if asked), P pictures of full-search
  * integer motion without residual (P_L0_16x16 / P_Skip) or I_PCM where the
  * motion prediction misses by more than max_mb_sad; one slice per macroblock
  * row; MP4 (moov at the end), video only.  DESIGN.md §11. */
@@ -294,10 +294,14 @@ typedef struct vts_transcode_params {
   int32_t search_range;    /* full-search motion range in luma pixels 0..16;
                               < 0 = 0 (zero motion only); 0 = default 8       */
   int32_t max_mb_sad;      /* inter if luma+chroma SAD <= this, else I_PCM;
-                              0 = default 768 (2 per sample); < 0 = all I_PCM */
+                              0 = default 1536 (4 per sample; 36 dB PSNR
+                              on the synthetic 720p clip); < 0 = all I_PCM */
   int32_t keyint;          /* max frames per GOP; 0 = 250 (x264's default)    */
-  float cut_threshold;     /* IDR where score > this; <= 0 = the session's    */
-  int32_t _pad;
+  float cut_threshold;     /* with idr_at_cuts: IDR where score > this;
+                              <= 0 = the session's threshold                  */
+  int32_t idr_at_cuts;     /* 1: also an IDR at every scene cut (an IDR is all
+                              I_PCM, so off by default: a cut P picture falls
+                              back to I_PCM only where motion misses)         */
 } vts_transcode_params;
 
 typedef struct vts_transcode_info {

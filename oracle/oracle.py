@@ -79,7 +79,7 @@ def lib() -> C.CDLL:
                                     C.c_void_p, C.c_void_p, C.c_void_p]
         _lib.or_pick_level.argtypes = [C.c_int, C.c_double]
         _lib.or_transcode.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p,
-                                      C.c_float, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_void_p]
     return _lib
@@ -350,7 +350,8 @@ def sps_pps(mbw: int, mbh: int, crop_r: int, crop_b: int, fps: float) -> tuple[b
 
 def transcode(frames: np.ndarray, width: int, height: int, scores: np.ndarray, *,
               threshold: float = 0.08, out_height: int = 360, search_range: int = 8,
-              max_mb_sad: int = 768, keyint: int = 250, want_recon: bool = False) -> dict:
+              max_mb_sad: int = 1536, keyint: int = 250, idr_at_cuts: bool = False,
+              want_recon: bool = False) -> dict:
     """The upload transcode of display-size NV12 frames [F, H*3/2, W] with
     their scene scores: output samples (bytes), per-frame sizes / sync flags,
     SPS/PPS, stats and (optionally) the encoder's reconstruction."""
@@ -369,7 +370,7 @@ def transcode(frames: np.ndarray, width: int, height: int, scores: np.ndarray, *
     stats = np.zeros(4, np.int64)
     n = C.c_int64(0)
     rc = lib().or_transcode(fr.ctypes.data, F, width, height, sc.ctypes.data, threshold,
-                            out_height, search_range, max_mb_sad, keyint, out.ctypes.data, cap,
+                            int(idr_at_cuts), out_height, search_range, max_mb_sad, keyint, out.ctypes.data, cap,
                             off.ctypes.data, size.ctypes.data, sync.ctypes.data,
                             recon.ctypes.data if recon is not None else None,
                             stats.ctypes.data, C.byref(n))

@@ -23,11 +23,12 @@
  *     reduced), rounded (sum + T/2) / T, then max(1, .) so that I_PCM data
  *     never holds a zero byte; coded size 16-aligned, edge rows/columns
  *     replicated;
- *   - IDR at frame 0, at every scene cut (score > threshold) and when the
- *     GOP reaches `keyint` frames: every macroblock I_PCM;
+ *   - IDR at frame 0, when the GOP reaches `keyint` frames and (opt-in) at
+ *     every scene cut (score > threshold): every macroblock I_PCM;
  *   - P pictures, one slice per macroblock row: per macroblock the integer
- *     luma motion (dx, dy), |dx|,|dy| <= R, block inside the coded picture,
- *     of least luma SAD against the previous reconstructed picture ((0,0)
+ *     luma motion (dx, dy), |dx|,|dy| <= R, of least luma SAD against the
+ *     previous reconstructed picture (samples outside it edge-clamped as the
+ *     decoder's 8.4.2.2.1 reads them; (0,0)
  *     first, then raster order; first minimum wins); inter (P_L0_16x16 or
  *     P_Skip, no residual) if luma+chroma SAD of its prediction (chroma by
  *     8.4.2.2.2) <= T_mb, else I_PCM.
@@ -265,11 +266,10 @@ static void encode_p(const uint8_t *src, const uint8_t *ref, uint8_t *rec, int c
         int r = c == 0 ? center : (c - 1 < center ? c - 1 : c);
         int dy = r / side - R, dx = r % side - R;
         int x0 = mx * 16 + dx, y0 = my * 16 + dy;
-        if (x0 < 0 || y0 < 0 || x0 + 16 > cw || y0 + 16 > ch) continue;
-        int64_t s = 0;
+        int64_t s = 0;  /* reference samples outside the picture: edge clamped (8.4.2.2.1) */
         for (int j = 0; j < 16; j++)
           for (int i = 0; i < 16; i++)
-            s += abs((int)ref[(int64_t)(y0 + j) * cw + x0 + i] -
+            s += abs((int)ref[(int64_t)clampi(y0 + j, 0, ch - 1) * cw + clampi(x0 + i, 0, cw - 1)] -
                      (int)src[(int64_t)(my * 16 + j) * cw + mx * 16 + i]);
         if (best < 0 || s < best) { best = s; bdx = dx; bdy = dy; }
       }
@@ -389,7 +389,7 @@ static int write_picture(const uint8_t *src, int cw, int ch, const or_mb *mbs, i
  * stats: [pcm MBs, P_L0_16x16 MBs, P_Skip MBs, IDR pictures].
  * Returns 0, -1 bad argument, -2 capacity, -3 out of memory. */
 int or_transcode(const uint8_t *frames, int64_t n, int W, int H, const float *scores, float thr,
-                 int sh, int R, int T, int keyint, uint8_t *out, int64_t cap, int64_t *sample_off,
+                 int idr_at_cuts, int sh, int R, int T, int keyint, uint8_t *out, int64_t cap, int64_t *sample_off,
                  int64_t *sample_size, uint8_t *sync, uint8_t *recon, int64_t *stats,
                  int64_t *out_len) {
   if (n <= 0 || sh < 2 || (sh & 1) || R < 0 || R > 16 || keyint < 1) return -1;
@@ -408,7 +408,7 @@ int or_transcode(const uint8_t *frames, int64_t n, int W, int H, const float *sc
   for (int k = 0; k < 4; k++) stats[k] = 0;
   for (int64_t f = 0; f < n && !rc; f++) {
     or_downscale_nv12(frames + f * dsz, W, H, src, sw, sh);
-    int idr = f == 0 || scores[f] > thr || f - last_idr >= keyint;
+    int idr = f == 0 || (idr_at_cuts && scores[f] > thr) || f - last_idr >= keyint;
     if (idr) last_idr = f;
     int j = (int)(f - last_idr);
     sample_off[f] = pos;

@@ -28,6 +28,8 @@ CASES = [
     ("allpcm", dict(width=320, height=192, n_frames=30), dict(height=96, max_mb_sad=-1)),
     ("keyint", dict(width=320, height=192, n_frames=70, cut_min_s=30, cut_max_s=40,
                     gop_max_s=10), dict(height=96, keyint=16, search_range=16)),
+    ("idr_at_cuts", dict(width=320, height=192, n_frames=90), dict(height=96, idr_at_cuts=True)),
+    ("bigpan_edges", dict(width=320, height=192, n_frames=60, max_motion=24), dict(height=96)),
 ]
 
 
@@ -44,7 +46,8 @@ def _oracle_run(path, tk):
     sc = oracle.score_frames(frames.reshape(-1), frames[0].size, F, W, H, W, H, k,
                              want_rgb=False)["score"]
     kw = dict(out_height=tk.get("height", 360), search_range=tk.get("search_range", 8),
-              max_mb_sad=tk.get("max_mb_sad", 768), keyint=tk.get("keyint", 250))
+              max_mb_sad=tk.get("max_mb_sad", 1536), keyint=tk.get("keyint", 250),
+              idr_at_cuts=tk.get("idr_at_cuts", False))
     return oracle.transcode(frames, W, H, sc, want_recon=True, **kw), info
 
 

@@ -109,13 +109,14 @@ def test_oracle_round_trip_and_error_bound(clip, T, R):
         assert r["pcm_mbs"] == n_mb
 
 
-def test_oracle_idr_at_cuts_and_keyint(clip):
+@pytest.mark.parametrize("at_cuts", [False, True])
+def test_oracle_idr_at_keyint_and_optionally_cuts(clip, at_cuts):
     frames, sc, _ = clip
-    r = oracle.transcode(frames, 320, 192, sc, out_height=96, keyint=7)
+    r = oracle.transcode(frames, 320, 192, sc, out_height=96, keyint=7, idr_at_cuts=at_cuts)
     idr = np.nonzero(r["sync"])[0]
     last = 0
     for f in range(len(frames)):
-        is_idr = f == 0 or sc[f] > 0.08 or f - last >= 7
+        is_idr = f == 0 or (at_cuts and sc[f] > 0.08) or f - last >= 7
         last = f if is_idr else last
         assert bool(r["sync"][f]) == is_idr
     assert len(idr) == r["n_idr"]

@@ -440,6 +440,7 @@ Mp4Writer::~Mp4Writer() {
 std::string Mp4Writer::open(const char *path) {
   f_ = std::fopen(path, "wb");
   if (!f_) return std::string("cannot create ") + path + ": " + std::strerror(errno);
+  std::setvbuf(f_, nullptr, _IOFBF, 4 << 20);  // samples are small: 4 MiB writes
   std::vector<uint8_t> v;
   {
     BoxW ftyp(v, "ftyp");

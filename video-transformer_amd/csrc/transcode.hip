@@ -8,8 +8,8 @@
 //      downscaling every window's frames (area filter, NV12 -> NV12 at
 //      (w, 360), coded 16-aligned) into a whole-video store while they sit
 //      in the decode ring;
-//   2. GOP plan on the host from the scene scores: IDR at frame 0, at every
-//      cut and every `keyint` frames;
+//   2. GOP plan on the host: IDR at frame 0 and every `keyint` frames (and,
+//      opt-in, at every scene cut from the scores);
 //   3. per GOP position j ("level", every GOP at once, as the decoder's
 //      reconstruct levels): `enc_search` — one wave per macroblock, full
 //      integer motion search in LDS against the previous reconstruction,
@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -74,6 +75,37 @@ __device__ __forceinline__ uint32_t area_px(const uint8_t *p, int pitch, int ste
   return v < 1 ? 1u : v;
 }
 
+// Integer ratio K on both axes (720p -> 360p: 2, 1080p -> 360p: 3): four
+// outputs from K rows of 4K contiguous bytes, dword loads; luma and NV12
+// chroma (4 bytes U0 V0 U1 V1 from 2K source pairs) share the addressing.
+template <int K>
+__device__ __forceinline__ uint32_t box4(const uint8_t *p, int pitch, bool chroma) {
+  uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t *r = reinterpret_cast<const uint32_t *>(p + static_cast<int64_t>(j) * pitch);
+#pragma unroll
+    for (int w = 0; w < K; ++w) {
+      const uint32_t v = r[w];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int byte = 4 * w + b;  // 0 .. 4K-1
+        // luma: output byte / K; chroma: pair byte / 2 -> output pair (pair / K), plane byte & 1
+        const int q = chroma ? 2 * ((byte >> 1) / K) + (byte & 1) : byte / K;
+        acc[q] += (v >> (8 * b)) & 255u;
+      }
+    }
+  }
+  uint32_t out = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t m = (acc[q] + K * K / 2) / (K * K);
+    out |= (m < 1 ? 1u : m) << (8 * q);
+  }
+  return out;
+}
+
+template <int K>
 __global__ void __launch_bounds__(256) downscale_nv12(DsArgs a) {
   const int groups = a.cw / 4;
   const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
@@ -83,6 +115,21 @@ __global__ void __launch_bounds__(256) downscale_nv12(DsArgs a) {
   const int g = static_cast<int>(t % groups), row = static_cast<int>(t / groups);
   const uint8_t *src = a.src + f * a.src_stride;
   uint8_t *dst = a.dst + f * a.dst_stride;
+  if constexpr (K > 0) {
+    const int dw = a.sw / K, dh = a.sh / K;  // output display size
+    if (row < dh && 4 * g + 3 < dw) {
+      *reinterpret_cast<uint32_t *>(dst + static_cast<int64_t>(row) * a.cw + 4 * g) =
+          box4<K>(src + static_cast<int64_t>(K * row) * a.pitch + 4 * K * g, a.pitch, false);
+      return;
+    }
+    if (row >= a.ch && row - a.ch < dh / 2 && 4 * g + 3 < dw) {
+      const int cy = row - a.ch;
+      const uint8_t *uv = src + static_cast<int64_t>(a.pitch) * a.uv_rows;
+      *reinterpret_cast<uint32_t *>(dst + static_cast<int64_t>(a.cw) * a.ch + static_cast<int64_t>(cy) * a.cw +
+                                    4 * g) = box4<K>(uv + static_cast<int64_t>(K * cy) * a.pitch + 4 * K * g, a.pitch, true);
+      return;
+    }
+  }
   uint32_t out = 0;
   if (row < a.ch) {
     const int32_t *ey = a.ty + static_cast<int64_t>(row) * (1 + a.ky);
@@ -153,9 +200,7 @@ __global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
   for (int c = lane; c < ncand; c += 64) {
     const int r = c == 0 ? center : (c - 1 < center ? c - 1 : c);
     const int dy = r / side - R, dx = r % side - R;
-    const int bx = mx * 16 + dx, by = my * 16 + dy;
-    if (bx < 0 || by < 0 || bx + 16 > a.cw || by + 16 > a.ch) continue;
-    uint32_t s = 0;
+    uint32_t s = 0;  // the window holds edge-clamped samples: every candidate is valid
     const int ox = dx + R;
 #pragma unroll 4
     for (int yy = 0; yy < 16; ++yy) {
@@ -173,7 +218,7 @@ __global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
     const uint64_t o = __shfl_xor(best, off);
     best = o < best ? o : best;
   }
-  const int c = static_cast<int>(best & 0xffffffffu);  // (0,0) is always valid
+  const int c = static_cast<int>(best & 0xffffffffu);
   const int r = c == 0 ? center : (c - 1 < center ? c - 1 : c);
   const int dy = r / side - R, dx = r % side - R;
   // prediction and cost: lane -> 4 luma samples (row lane/4) and one chroma pair
@@ -221,6 +266,8 @@ struct WriteArgs {
   int32_t *sizes;       // [slice] bytes incl. the 4-byte length prefix
   unsigned long long *stats;  // pcm, inter, skip
   uint32_t *err;
+  uint4 *jobs;          // I_PCM payloads left for enc_pcm: (slice, byte offset in the slot, mx, 0)
+  uint32_t *n_jobs;
   int32_t n_slices;
   int32_t idr;          // level 0: every picture IDR
 };
@@ -265,20 +312,16 @@ struct NalOut {
   }
 };
 
-__device__ void put_pcm(NalOut &o, const uint8_t *src, int cw, int ch, int mx, int my) {
+// I_PCM: pcm_alignment_zero_bits, then 384 sample bytes that enc_pcm fills in
+// later.  The samples are >= 1 (downscale clamp), and the byte before them
+// holds mb_type's last 1 bits, so no emulation prevention byte can fall in or
+// next to them and the zero-run state after them is 0.
+__device__ void pcm_gap(NalOut &o, uint4 *job, int s, int mx) {
   o.align();
-  for (int j = 0; j < 16; ++j) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(src + static_cast<int64_t>(my * 16 + j) * cw + mx * 16);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    for (int q = 0; q < 16; ++q) o.byte((w[q >> 2] >> (8 * (q & 3))) & 0xffu);
-  }
-  const uint8_t *uv = src + static_cast<int64_t>(cw) * ch;
-  for (int pl = 0; pl < 2; ++pl)
-    for (int j = 0; j < 8; ++j) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(uv + static_cast<int64_t>(my * 8 + j) * cw + mx * 16);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      for (int q = 0; q < 8; ++q) o.byte((w[q >> 1] >> (16 * (q & 1) + 8 * pl)) & 0xffu);
-    }
+  *job = make_uint4(static_cast<uint32_t>(s), static_cast<uint32_t>(4 + o.n), static_cast<uint32_t>(mx), 0);
+  o.n += 384;
+  if (o.n > o.cap) o.over = true;
+  o.zeros = 0;
 }
 
 __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
@@ -286,7 +329,6 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
   if (s >= a.n_slices) return;
   const int e = s / a.mbh, row = s % a.mbh;
   const int4 en = a.ent[e];
-  const uint8_t *src = a.small + static_cast<int64_t>(en.x) * a.stride;
   uint8_t *slot = a.staging + static_cast<int64_t>(s) * a.cap;
   NalOut o{slot + 4, a.cap - 4, 0, 0, 0, 0, false};
   o.put(a.idr ? 0x65 : 0x41);  // nal_ref_idc 3 IDR / 2 non-IDR; every picture is a reference
@@ -307,10 +349,18 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
   bool a_ok = false;
   int amx = 0, amy = 0;
   const uint32_t *cmd = a.cmd + static_cast<int64_t>(e) * a.mbw * a.mbh + static_cast<int64_t>(row) * a.mbw;
+  // reserve this slice's I_PCM jobs
+  uint32_t njob = 0;
+  if (a.idr) {
+    njob = static_cast<uint32_t>(a.mbw);
+  } else {
+    for (int mx = 0; mx < a.mbw; ++mx) njob += cmd[mx] == kPcmCmd;
+  }
+  uint4 *job = a.jobs + (njob ? atomicAdd(a.n_jobs, njob) : 0u);
   for (int mx = 0; mx < a.mbw; ++mx) {
     if (a.idr) {
       o.ue(25);
-      put_pcm(o, src, a.cw, a.ch, mx, row);
+      pcm_gap(o, job++, s, mx);
       ++npcm;
       continue;
     }
@@ -319,7 +369,7 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
       o.ue(skip);
       skip = 0;
       o.ue(30);  // I_PCM in a P slice
-      put_pcm(o, src, a.cw, a.ch, mx, row);
+      pcm_gap(o, job++, s, mx);
       a_ok = false;
       ++npcm;
       continue;
@@ -369,6 +419,35 @@ __global__ void __launch_bounds__(256) enc_gather(const uint8_t *staging, int64_
   uint8_t *q = out + offs[s];
   const int n = sizes[s];
   for (int i = threadIdx.x; i < n; i += 256) q[i] = p[i];
+}
+
+// I_PCM payloads: one wave per job, 6 bytes per lane, straight into the
+// packed level output (after enc_gather): luma 16x16, then Cb 8x8, Cr 8x8
+// (7.3.5) from the NV12 source.
+__global__ void __launch_bounds__(64) enc_pcm(const uint4 *jobs, const uint32_t *n_jobs, const int4 *ent,
+                                              const uint8_t *small, int64_t stride, int32_t cw, int32_t ch,
+                                              int32_t mbh, const int64_t *offs, uint8_t *out) {
+  const uint32_t n = *n_jobs;
+  for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
+    const uint4 jb = jobs[j];
+    const int s = static_cast<int>(jb.x), mx = static_cast<int>(jb.z);
+    const int e = s / mbh, my = s % mbh;
+    const uint8_t *src = small + static_cast<int64_t>(ent[e].x) * stride;
+    const uint8_t *uv = src + static_cast<int64_t>(cw) * ch;
+    uint8_t *dst = out + offs[s] + jb.y;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int b = 6 * static_cast<int>(threadIdx.x) + q;
+      uint8_t v;
+      if (b < 256) {
+        v = src[static_cast<int64_t>(my * 16 + (b >> 4)) * cw + mx * 16 + (b & 15)];
+      } else {
+        const int i = (b - 256) & 63, pl = (b - 256) >> 6;
+        v = uv[static_cast<int64_t>(my * 8 + (i >> 3)) * cw + 2 * (mx * 8 + (i & 7)) + pl];
+      }
+      dst[b] = v;
+    }
+  }
 }
 
 // ------------------------------------------------------------ host
@@ -498,8 +577,16 @@ int small_window(vts_ctx *c, int ring, int64_t f0, int64_t f1, hipStream_t s) {
   a.tc = S.tc;
   a.n_frames = f1 - f0;
   const int64_t threads = static_cast<int64_t>(S.cw / 4) * (S.ch + S.ch / 2);
-  hipLaunchKernelGGL(downscale_nv12, dim3(static_cast<unsigned>((threads + 255) / 256), static_cast<unsigned>(f1 - f0)),
-                     dim3(256), 0, s, a);
+  const dim3 grid(static_cast<unsigned>((threads + 255) / 256), static_cast<unsigned>(f1 - f0));
+  // integer ratio on both axes (equal): the dword box path; else the tap tables
+  const int W = c->width, H = c->height;
+  const int k = (W % S.w == 0 && H % S.h == 0 && W / S.w == H / S.h) ? W / S.w : 0;
+  switch (k) {
+    case 2: hipLaunchKernelGGL(downscale_nv12<2>, grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(downscale_nv12<3>, grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(downscale_nv12<4>, grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(downscale_nv12<0>, grid, dim3(256), 0, s, a); break;
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "downscale_nv12 launch: %s", hipGetErrorString(e));
   return VTS_OK;
@@ -518,7 +605,7 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   if (pin) p = *pin;
   const int sh = p.height > 0 ? p.height : 360;
   const int R = p.search_range == 0 ? 8 : std::max(0, p.search_range);
-  const int T = p.max_mb_sad == 0 ? 768 : p.max_mb_sad;
+  const int T = p.max_mb_sad == 0 ? 1536 : p.max_mb_sad;
   const int keyint = p.keyint > 0 ? p.keyint : 250;
   const float thr = p.cut_threshold > 0 ? p.cut_threshold : c->params.cut_threshold;
   if ((sh & 1) || sh < 16 || sh > c->height)
@@ -549,7 +636,8 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   // 2. GOPs: IDR at frame 0, at cuts, every keyint frames
   std::vector<int64_t> gop_start;
   for (int64_t f = 0; f < n; ++f)
-    if (f == 0 || c->host_scores[f] > thr || f - gop_start.back() >= keyint) gop_start.push_back(f);
+    if (f == 0 || (p.idr_at_cuts && c->host_scores[f] > thr) || f - gop_start.back() >= keyint)
+      gop_start.push_back(f);
   const int64_t ngop = static_cast<int64_t>(gop_start.size());
   std::vector<int64_t> gop_len(static_cast<size_t>(ngop));
   int64_t maxlen = 0;
@@ -592,6 +680,10 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   VTS_TRY(B.get(&d_offs, static_cast<size_t>(max_ent * mbh)));
   VTS_TRY(B.get(&d_stats, 3));
   VTS_TRY(B.get(&d_err, 1));
+  uint4 *d_jobs;
+  uint32_t *d_njobs;
+  VTS_TRY(B.get(&d_jobs, static_cast<size_t>(max_ent * nmb)));
+  VTS_TRY(B.get(&d_njobs, 1));
   hipStream_t s = c->s_dec;
   HIP_TRY(hipMemcpy(d_sent, sent.data(), sent.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(d_went, went.data(), went.size() * sizeof(int4), hipMemcpyHostToDevice));
@@ -601,8 +693,9 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
   HIP_TRY(hipEventCreate(&e2));
-  std::vector<uint8_t> host;           // the output samples, level order
-  std::vector<int64_t> fr_off(static_cast<size_t>(n), 0), fr_size(static_cast<size_t>(n), 0);
+  std::vector<std::unique_ptr<uint8_t[]>> host;  // the output samples, one buffer per level
+  std::vector<const uint8_t *> fr_ptr(static_cast<size_t>(n), nullptr);
+  std::vector<int64_t> fr_size(static_cast<size_t>(n), 0);
   std::vector<int32_t> sizes(static_cast<size_t>(max_ent * mbh));
   std::vector<int64_t> offs(sizes.size());
   int status = VTS_OK;
@@ -626,6 +719,7 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
       hipLaunchKernelGGL(enc_search, dim3(static_cast<unsigned>(ne * nmb)), dim3(64), 0, s, sa);
     }
     (void)hipEventRecord(e1, s);
+    HIP_TRY(hipMemsetAsync(d_njobs, 0, sizeof(uint32_t), s));
     WriteArgs wa{};
     wa.ent = d_went + lvl_off[j];
     wa.cmd = d_cmd;
@@ -640,6 +734,8 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
     wa.sizes = d_sizes;
     wa.stats = d_stats;
     wa.err = d_err;
+    wa.jobs = d_jobs;
+    wa.n_jobs = d_njobs;
     wa.n_slices = ns;
     wa.idr = j == 0;
     hipLaunchKernelGGL(enc_write, dim3(static_cast<unsigned>((ns + 63) / 64)), dim3(64), 0, s, wa);
@@ -660,17 +756,19 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
       offs[i] = tot;
       tot += sizes[i];
     }
+    host.emplace_back(new uint8_t[static_cast<size_t>(std::max<int64_t>(tot, 1))]);
+    uint8_t *hb = host.back().get();
     for (int64_t k = 0; k < ne; ++k) {
       const int64_t f = went[lvl_off[j] + k].x;
-      fr_off[f] = static_cast<int64_t>(host.size()) + offs[k * mbh];
+      fr_ptr[f] = hb + offs[k * mbh];
       fr_size[f] = (k + 1 < ne ? offs[(k + 1) * mbh] : tot) - offs[k * mbh];
     }
     HIP_TRY(hipMemcpyAsync(d_offs, offs.data(), sizeof(int64_t) * ns, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(enc_gather, dim3(static_cast<unsigned>(ns)), dim3(256), 0, s, d_stage, cap, d_sizes, d_offs,
                        d_out);
-    const size_t h0 = host.size();
-    host.resize(h0 + static_cast<size_t>(tot));
-    HIP_TRY(hipMemcpyAsync(host.data() + h0, d_out, static_cast<size_t>(tot), hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(enc_pcm, dim3(static_cast<unsigned>(std::min<int64_t>(8192, ne * nmb))), dim3(64), 0, s,
+                       d_jobs, d_njobs, d_went + lvl_off[j], S.d, S.stride, S.cw, S.ch, mbh, d_offs, d_out);
+    HIP_TRY(hipMemcpyAsync(hb, d_out, static_cast<size_t>(tot), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     (void)hipEventElapsedTime(&a_ms, e0, e1);
     (void)hipEventElapsedTime(&b_ms, e1, e2);
@@ -697,7 +795,7 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   std::vector<uint8_t> is_idr(static_cast<size_t>(n), 0);
   for (int64_t f : gop_start) is_idr[f] = 1;
   for (int64_t f = 0; f < n && e.empty(); ++f)
-    e = mw.add_sample(host.data() + fr_off[f], static_cast<size_t>(fr_size[f]), is_idr[f] != 0);
+    e = mw.add_sample(fr_ptr[f], static_cast<size_t>(fr_size[f]), is_idr[f] != 0);
   if (e.empty()) e = mw.finish(S.w, S.h, c->info.track_timescale, delta, sps, pps);
   if (!e.empty()) return fail(VTS_E_IO, "%s: %s", out_path, e.c_str());
   ms[3] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();

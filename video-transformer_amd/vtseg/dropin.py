@@ -34,8 +34,12 @@ ANALYZER_NAMES = {
 }
 
 
-def install() -> list[str]:
-    """Bind vtseg under the reference's names; returns what was bound."""
+def install(upload_transcode: bool = False) -> list[str]:
+    """Bind vtseg under the reference's names; returns what was bound.
+
+    upload_transcode: also replace ContentAnalyzer._compress_video_for_upload
+    (content_analyzer.py:167-236) with the GPU transcode (vtseg.upload;
+    opt-in: its bytes differ from x264's)."""
     done = []
     for name, mod in MODULES.items():
         sys.modules[name] = mod
@@ -50,4 +54,12 @@ def install() -> list[str]:
             if hasattr(ca, attr):
                 setattr(ca, attr, obj)
                 done.append(f"analyzer.content_analyzer.{attr}")
+        if upload_transcode and hasattr(ca, "ContentAnalyzer"):
+            from . import upload
+
+            def _compress_video_for_upload(self, video_path):
+                return upload.compress_video_for_upload(video_path, logger=self.logger)
+
+            ca.ContentAnalyzer._compress_video_for_upload = _compress_video_for_upload
+            done.append("analyzer.content_analyzer.ContentAnalyzer._compress_video_for_upload")
     return done

@@ -200,7 +200,7 @@ class VideoScorer:
         return out
 
     def transcode(self, out_path: str | Path, *, height: int = 360, search_range: int = 8,
-                  max_mb_sad: int = 768, keyint: int = 250,
+                  max_mb_sad: int = 1536, keyint: int = 250, idr_at_cuts: bool = False,
                   cut_threshold: float = 0.0) -> dict:
         """360p upload transcode of this video into `out_path` (vts_transcode,
         DESIGN.md §11): decode + score + area downscale + device H.264
@@ -211,6 +211,7 @@ class VideoScorer:
         prm.max_mb_sad = max_mb_sad
         prm.keyint = keyint
         prm.cut_threshold = cut_threshold
+        prm.idr_at_cuts = 1 if idr_at_cuts else 0
         info = _lib.TranscodeInfo()
         _lib.check(self._lib.vts_transcode(self._ctx, str(out_path).encode(), C.byref(prm),
                                            C.byref(info)))
