@@ -310,8 +310,9 @@ typedef struct vts_transcode_info {
   int64_t n_idr;
   int64_t pcm_mbs, inter_mbs, skip_mbs;
   int64_t bytes_written;   /* output file size                                 */
-  double ms[4];            /* device decode+score+downscale, motion search,
-                              slice writing + compaction, host MP4 mux         */
+  double ms[4];            /* decode+score+downscale (host clock), motion
+                              search span (stream 1), slice writing span
+                              (stream 2, overlaps the searches), MP4 mux      */
 } vts_transcode_info;
 
 /* Transcode the session's video to `out_path`. */
