@@ -50,7 +50,9 @@ def test_struct_layouts_match_header(tmp_path):
                "vts_plan": _lib.Plan, "vts_video_info": _lib.VideoInfo,
                "vts_score_desc": _lib.ScoreDesc, "vts_params": _lib.Params,
                "vts_synth_params": _lib.SynthParams, "vts_synth_info": _lib.SynthInfo,
-               "vts_manifest_args": _lib.ManifestArgs}
+               "vts_manifest_args": _lib.ManifestArgs,
+               "vts_transcode_params": _lib.TranscodeParams,
+               "vts_transcode_info": _lib.TranscodeInfo}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"',
              "int main(void) {"]
     for cname, py in structs.items():
