@@ -39,6 +39,7 @@ sys.path.insert(0, str(ROOT / "video-transformer_amd"))
 sys.path.insert(0, str(ROOT / "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+VALU_SAD_PEAK_TOPS = 256 * 4 * 32 * 4 * 2.4e9 / 1e12  # v_sad_u8 byte-SADs/s (MI355X_MICROARCH.md)
 
 # BASELINE.json configs runnable per GPU: name -> (width, height, frames, what)
 CONFIGS = {
@@ -150,6 +151,37 @@ def cpu_baseline_decode_score(path, k, budget_s=15.0):
                       f"or_score_frames, GOP-parallel on {threads} threads, {dt:.1f} s"}
 
 
+def cpu_baseline_transcode(path, k, budget_s=15.0):
+    """The same transcode on the host, 1 thread: the C oracle decodes and
+    scores the first frames of the benchmark video, then or_transcode
+    (transcode_oracle.c: area downscale, scalar full search R = 8, slice
+    writer) encodes them; a bounded sample sized from a 4-frame probe."""
+    import oracle
+    m = oracle.read_mp4(path)
+    n_all = len(m["sizes"])
+
+    def run(n):
+        samples = [m["data"][o:o + z] for o, z in zip(m["offsets"][:n], m["sizes"][:n])]
+        frames = oracle.decode_samples(m["sps"][0], m["pps"][0], samples, m["nal_length_size"])
+        H, W = frames.shape[1] * 2 // 3, frames.shape[2]
+        sc = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, k,
+                                 want_rgb=True)["score"]
+        oracle.transcode(frames, W, H, sc)
+        return W, H
+
+    t0 = time.perf_counter()
+    run(4)
+    per = (time.perf_counter() - t0) / 4
+    n = max(4, min(n_all, int(budget_s / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    W, H = run(n)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} frames ({W}x{H}) of the benchmark video: oracle decode + score + "
+                      f"or_transcode (area downscale, scalar full search R=8, CAVLC writer), "
+                      f"1 thread, {dt:.1f} s"}
+
+
 def _kernel_short(name: str) -> str:
     m = re.search(r"(h264_recon_score6|h264_\w+|thumb_sad|score_\w+)(<\d+>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name.split("(")[0][-60:]
@@ -203,7 +235,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="decode_score", choices=["decode_score", "score"])
+    ap.add_argument("--workload", default="decode_score", choices=["decode_score", "score", "transcode"])
     ap.add_argument("--config", default="720p-10min", choices=sorted(CONFIGS),
                     help="BASELINE configuration (per GPU); the N=1 headline is 720p-10min")
     ap.add_argument("--frames", type=int, default=None, help="override the config's frames")
@@ -222,7 +254,7 @@ def main() -> None:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     pmc = None
-    if world == 1 and not args.no_pmc:
+    if world == 1 and not args.no_pmc and args.workload != "transcode":
         # before anything touches the GPU: the passes are child processes
         child_argv = ["--workload", args.workload, "--config", args.config,
                       "--gops-per-launch", str(args.gops_per_launch),
@@ -289,8 +321,15 @@ def main() -> None:
                                    parse_chunks=args.parse_chunks)
         duration_s = float(scorer.info.duration)
 
-        def step():
-            scorer.run()
+        if args.workload == "transcode":
+            out_path = Path(tmpdir) / f"small_rank{rank}.mp4"
+            outs = {}
+
+            def step():
+                outs["facts"] = scorer.transcode(out_path)
+        else:
+            def step():
+                scorer.run()
 
     # per-video segment plan under the reference's default config (config.yaml)
     cfg = {"analyzer": {"max_continuations": 3, "retry_times": 5,
@@ -348,6 +387,17 @@ def main() -> None:
         torch.cuda.synchronize()
         kern_ms = ev0.elapsed_time(ev1) / reps
         kname = "score_runs<4>"
+    elif args.workload == "transcode":
+        # dominant kernel: enc_search<8> (VALU: v_sad_u8, 4 byte-SADs per lane-instruction)
+        facts = outs["facts"]
+        R = 8
+        sw, sh = facts["width"], facts["height"]
+        nmb = ((sw + 15) // 16) * ((sh + 15) // 16)
+        p_frames = F - facts["n_idr"]
+        n_launch = max(1, min(250, F) - 1)
+        sad_ops = p_frames * nmb * (2 * R + 1) ** 2 * 256
+        kern_ms = facts["search_ms"] / n_launch
+        kname = "enc_search<8>"
     else:
         times = []
         for _ in range(3):
@@ -363,13 +413,19 @@ def main() -> None:
         else:
             kern_ms = float(np.mean([t["score_ms"] for t in times]))
             kname = "score_runs<%d>" % k
-    if scorer is not None and scorer.fused():
+    if args.workload == "transcode":
+        bytes_per_frame = None
+        frames_per_launch = p_frames / n_launch
+    elif scorer is not None and scorer.fused():
         bytes_per_frame = fused_bytes_per_frame(width, height, k)
         frames_per_launch = F / n_launch
     else:
         bytes_per_frame = algorithmic_bytes_per_frame(width, height, k)
         frames_per_launch = F
-    achieved = bytes_per_frame * frames_per_launch / (kern_ms * 1e-3) / 1e9
+    if args.workload == "transcode":
+        achieved = sad_ops / n_launch / (kern_ms * 1e-3) / 1e12
+    else:
+        achieved = bytes_per_frame * frames_per_launch / (kern_ms * 1e-3) / 1e9
     traffic, traffic_note = None, None
     if pmc is not None:
         row = pmc.get(kname) if "error" not in pmc else None
@@ -380,14 +436,23 @@ def main() -> None:
                             f"{traffic / (bytes_per_frame * frames_per_launch):.3f}x algorithmic")
         else:
             traffic_note = pmc.get("error", f"no counters for {kname}")
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_unit": "bytes/launch", "traffic_source": traffic_note,
-            "kernel": kname, "kernel_ms": round(kern_ms, 4),
-            "bytes_per_frame": bytes_per_frame,
-            "frames_per_launch": round(frames_per_launch, 1)}
+    if args.workload == "transcode":
+        roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": VALU_SAD_PEAK_TOPS,
+                "unit": "T byte-SAD/s", "frac": round(achieved / VALU_SAD_PEAK_TOPS, 4),
+                "traffic": None, "kernel": kname, "kernel_ms": round(kern_ms, 4),
+                "sad_ops_per_launch": int(sad_ops / n_launch),
+                "frames_per_launch": round(frames_per_launch, 1),
+                "note": "full-search (2R+1)^2 x 256 byte |a-b| per macroblock, R=8; peak = 256 CUs x "
+                        "4 SIMDs x 32 lanes/clk x 4 B (v_sad_u8) x 2.4 GHz"}
+    else:
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_unit": "bytes/launch", "traffic_source": traffic_note,
+                "kernel": kname, "kernel_ms": round(kern_ms, 4),
+                "bytes_per_frame": bytes_per_frame,
+                "frames_per_launch": round(frames_per_launch, 1)}
     roof_decode = None
-    if scorer is not None and not scorer.fused():
+    if args.workload == "decode_score" and not scorer.fused():
         rec_bytes = 3 * width * height
         ach = rec_bytes * (F / n_launch) / (rec_ms * 1e-3) / 1e9
         roof_decode = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -401,6 +466,8 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if args.workload == "score":
             cpu = cpu_baseline_score(width, height, k)
+        elif args.workload == "transcode":
+            cpu = cpu_baseline_transcode(path, k)
         else:
             cpu = cpu_baseline_decode_score(path, k)
 
@@ -421,7 +488,13 @@ def main() -> None:
             "roofline_decode": roof_decode,
             "cpu_baseline": cpu,
         }
-        if scorer is not None:
+        if args.workload == "transcode":
+            f = outs["facts"]
+            line["metric"] = "720p frames/sec transcoded to 360p (upload compression, SURVEY 8f-2)"
+            line["config"]["transcode"] = {kk: (round(v, 3) if isinstance(v, float) else v)
+                                           for kk, v in f.items()}
+            line["config"]["transcode"]["input_bytes"] = Path(path).stat().st_size
+        elif scorer is not None:
             line["config"]["stage_ms"] = scorer.timings()
             line["config"]["recon_launches"] = scorer.recon_launches()
         print(json.dumps(line), flush=True)

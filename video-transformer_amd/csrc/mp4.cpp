@@ -471,6 +471,24 @@ std::string Mp4Writer::add_sample(const uint8_t *data, size_t n, bool sync) {
   return "";
 }
 
+std::string Mp4Writer::append(const uint8_t *data, size_t n, int64_t *offset) {
+  if (!f_) return "writer not open";
+  if (n && std::fwrite(data, 1, n, f_) != n) return "write error";
+  *offset = pos_;
+  pos_ += static_cast<int64_t>(n);
+  return "";
+}
+
+std::string Mp4Writer::add_sample_at(int64_t offset, size_t n, bool sync) {
+  if (!f_) return "writer not open";
+  if (n > 0xffffffffu) return "sample too large";
+  if (offset < mdat_start_ || offset + static_cast<int64_t>(n) > pos_) return "sample outside mdat";
+  offsets_.push_back(offset);
+  sizes_.push_back(static_cast<uint32_t>(n));
+  if (sync) sync_.push_back(static_cast<uint32_t>(sizes_.size()));
+  return "";
+}
+
 std::string Mp4Writer::finish(int width, int height, int64_t track_timescale,
                               int64_t sample_delta, const std::vector<uint8_t> &sps,
                               const std::vector<uint8_t> &pps) {

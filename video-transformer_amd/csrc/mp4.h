@@ -74,6 +74,11 @@ class Mp4Writer {
   ~Mp4Writer();
   std::string open(const char *path);
   std::string add_sample(const uint8_t *data, size_t n, bool sync);
+  // Raw bytes appended to mdat (samples in any order); *offset = their file
+  // offset, for add_sample_at.
+  std::string append(const uint8_t *data, size_t n, int64_t *offset);
+  // The next sample (decode order) whose n bytes are already in mdat at offset.
+  std::string add_sample_at(int64_t offset, size_t n, bool sync);
   // track_timescale / sample_delta: constant frame duration; movie timescale
   // 1000.  sps/pps: NAL units including their header byte.
   std::string finish(int width, int height, int64_t track_timescale,

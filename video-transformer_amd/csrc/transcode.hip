@@ -14,10 +14,11 @@
 //      reconstruct levels): `enc_search` — one wave per macroblock, full
 //      integer motion search in LDS against the previous reconstruction,
 //      decision inter / I_PCM, reconstruction written (the next level's
-//      reference); `enc_write` — one lane per slice (macroblock row) writes
-//      the CAVLC slice NAL with emulation prevention into a fixed-capacity
-//      staging slot; `enc_gather` compacts the level's slices for one D2H
-//      copy;
+//      reference); then per chunk of 16 levels on a second stream:
+//      `enc_write` — one lane per slice (macroblock row) writes the CAVLC
+//      slice NAL with emulation prevention into a fixed-capacity staging slot,
+//      leaving I_PCM payloads as gaps; `enc_scan` — device offsets;
+//      `enc_gather` + `enc_pcm` — packed output, one D2H copy per chunk;
 //   4. host: MP4 mux (Mp4Writer) in display order.
 #include <hip/hip_runtime.h>
 
@@ -345,16 +346,32 @@ struct WriteArgs {
   uint4 *jobs;          // I_PCM payloads left for enc_pcm: (slice, byte offset in the slot, mx, 0)
   uint32_t *n_jobs;
   int32_t n_slices;
-  int32_t idr;          // level 0: every picture IDR
+  int32_t _pad;
 };
 
-// RBSP bits -> EBSP bytes (emulation prevention) into a staging slot.
+// RBSP bits -> EBSP bytes (emulation prevention) into a staging slot, four
+// bytes per (aligned) dword store.
 struct NalOut {
-  uint8_t *p;
-  int64_t cap, n;
+  uint32_t *w;          // slot payload (slot + 4), 4-byte aligned
+  int64_t cap, n;       // bytes
+  uint32_t cur;         // the bytes of the word being filled
   uint64_t acc;
   int nacc, zeros;
   bool over;
+  __device__ void put(uint32_t b) {
+    cur |= b << (8 * (n & 3));
+    if (!(++n & 3)) {
+      if (n <= cap) w[(n >> 2) - 1] = cur;
+      else over = true;
+      cur = 0;
+    }
+  }
+  __device__ void flush() {  // the partial word (its tail bytes are don't-care)
+    if (n & 3) {
+      if (n <= cap) w[n >> 2] = cur;
+      else over = true;
+    }
+  }
   __device__ void byte(uint32_t b) {
     if (zeros >= 2 && b <= 3) {
       put(3);
@@ -362,11 +379,6 @@ struct NalOut {
     }
     put(b);
     zeros = b ? 0 : zeros + 1;
-  }
-  __device__ void put(uint32_t b) {
-    if (n < cap) p[n] = static_cast<uint8_t>(b);
-    else over = true;
-    ++n;
   }
   __device__ void bits(int k, uint32_t v) {  // k <= 32
     acc = (acc << k) | v;
@@ -389,13 +401,17 @@ struct NalOut {
 };
 
 // I_PCM: pcm_alignment_zero_bits, then 384 sample bytes that enc_pcm fills in
-// later.  The samples are >= 1 (downscale clamp), and the byte before them
-// holds mb_type's last 1 bits, so no emulation prevention byte can fall in or
-// next to them and the zero-run state after them is 0.
+// later (the gap's bytes in the partial words either side are don't-care
+// here: enc_pcm runs after enc_gather).  The samples are >= 1 (downscale
+// clamp), and the byte before them holds mb_type's last 1 bits, so no
+// emulation prevention byte can fall in or next to them and the zero-run
+// state after them is 0.
 __device__ void pcm_gap(NalOut &o, uint4 *job, int s, int mx) {
   o.align();
+  o.flush();
   *job = make_uint4(static_cast<uint32_t>(s), static_cast<uint32_t>(4 + o.n), static_cast<uint32_t>(mx), 0);
-  o.n += 384;
+  o.n += 384;  // a multiple of 4: the word phase is unchanged
+  o.cur = 0;
   if (o.n > o.cap) o.over = true;
   o.zeros = 0;
 }
@@ -405,14 +421,15 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
   if (s >= a.n_slices) return;
   const int e = s / a.mbh, row = s % a.mbh;
   const int4 en = a.ent[e];
+  const bool idr = en.y == 0;  // GOP position 0
   uint8_t *slot = a.staging + static_cast<int64_t>(s) * a.cap;
-  NalOut o{slot + 4, a.cap - 4, 0, 0, 0, 0, false};
-  o.put(a.idr ? 0x65 : 0x41);  // nal_ref_idc 3 IDR / 2 non-IDR; every picture is a reference
+  NalOut o{reinterpret_cast<uint32_t *>(slot + 4), a.cap - 4, 0, 0, 0, 0, 0, false};
+  o.put(idr ? 0x65 : 0x41);  // nal_ref_idc 3 IDR / 2 non-IDR; every picture is a reference
   o.ue(static_cast<uint32_t>(row * a.mbw));  // first_mb_in_slice
-  o.ue(a.idr ? 7 : 5);                       // slice_type I / P (all slices of the picture)
+  o.ue(idr ? 7 : 5);                       // slice_type I / P (all slices of the picture)
   o.ue(0);                                   // pic_parameter_set_id
   o.bits(16, static_cast<uint32_t>(en.y) & 0xffffu);  // frame_num (16 bits)
-  if (a.idr) {
+  if (idr) {
     o.ue(static_cast<uint32_t>(en.z));       // idr_pic_id
     o.bits(2, 0);                            // no_output_of_prior_pics, long_term_reference
   } else {
@@ -427,14 +444,14 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
   const uint32_t *cmd = a.cmd + static_cast<int64_t>(e) * a.mbw * a.mbh + static_cast<int64_t>(row) * a.mbw;
   // reserve this slice's I_PCM jobs
   uint32_t njob = 0;
-  if (a.idr) {
+  if (idr) {
     njob = static_cast<uint32_t>(a.mbw);
   } else {
     for (int mx = 0; mx < a.mbw; ++mx) njob += cmd[mx] == kPcmCmd;
   }
   uint4 *job = a.jobs + (njob ? atomicAdd(a.n_jobs, njob) : 0u);
   for (int mx = 0; mx < a.mbw; ++mx) {
-    if (a.idr) {
+    if (idr) {
       o.ue(25);
       pcm_gap(o, job++, s, mx);
       ++npcm;
@@ -471,16 +488,14 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
   if (skip) o.ue(skip);
   o.bits(1, 1);  // rbsp_stop_one_bit
   o.align();
+  o.flush();
   const int64_t len = o.n;
   if (o.over) {
     atomicOr(a.err, 1u);
     a.sizes[s] = 0;
     return;
   }
-  slot[0] = static_cast<uint8_t>(len >> 24);
-  slot[1] = static_cast<uint8_t>(len >> 16);
-  slot[2] = static_cast<uint8_t>(len >> 8);
-  slot[3] = static_cast<uint8_t>(len);
+  *reinterpret_cast<uint32_t *>(slot) = __builtin_bswap32(static_cast<uint32_t>(len));  // big-endian length
   a.sizes[s] = static_cast<int32_t>(len + 4);
   atomicAdd(&a.stats[0], npcm);
   atomicAdd(&a.stats[1], ninter);
@@ -774,8 +789,6 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
     }
   }
   lvl_off[maxlen] = static_cast<int64_t>(went.size());
-  int64_t max_ent = 0;
-  for (int64_t j = 0; j < maxlen; ++j) max_ent = std::max(max_ent, lvl_off[j + 1] - lvl_off[j]);
 
   // 3. device encode, level by level
   const int64_t cap = ((64 + static_cast<int64_t>(mbw) * 420) + 255) & ~int64_t(255);
@@ -790,32 +803,35 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   VTS_TRY(B.get(&d_went, went.size()));
   VTS_TRY(B.get(&d_recon, static_cast<size_t>(2 * ngop * S.stride + 256)));
   VTS_TRY(B.get(&d_cmd, static_cast<size_t>(went.size()) * nmb));  // every frame: searches run ahead
-  VTS_TRY(B.get(&d_stage, static_cast<size_t>(max_ent * mbh * cap)));
-  constexpr int64_t kChunkLevels = 16;  // levels per device->host drain
-  VTS_TRY(B.get(&d_out, static_cast<size_t>(kChunkLevels * max_ent * mbh * cap)));
+  constexpr int64_t kChunkLevels = 16;  // levels written and drained together
+  int64_t max_chunk = 0;                 // entries of the largest chunk
+  for (int64_t j0 = 0; j0 < maxlen; j0 += kChunkLevels)
+    max_chunk = std::max(max_chunk, lvl_off[std::min(maxlen, j0 + kChunkLevels)] - lvl_off[j0]);
+  VTS_TRY(B.get(&d_stage, static_cast<size_t>(max_chunk * mbh * cap)));
+  VTS_TRY(B.get(&d_out, static_cast<size_t>(max_chunk * mbh * cap)));
   int64_t *d_total, *d_base, *d_fr;
   VTS_TRY(B.get(&d_total, 1));
   VTS_TRY(B.get(&d_base, 1));
   VTS_TRY(B.get(&d_fr, static_cast<size_t>(2 * n)));  // per frame: absolute offset, size
-  VTS_TRY(B.get(&d_sizes, static_cast<size_t>(max_ent * mbh)));
-  VTS_TRY(B.get(&d_offs, static_cast<size_t>(max_ent * mbh)));
+  VTS_TRY(B.get(&d_sizes, static_cast<size_t>(max_chunk * mbh)));
+  VTS_TRY(B.get(&d_offs, static_cast<size_t>(max_chunk * mbh)));
   VTS_TRY(B.get(&d_stats, 3));
   VTS_TRY(B.get(&d_err, 1));
   uint4 *d_jobs;
   uint32_t *d_njobs;
-  VTS_TRY(B.get(&d_jobs, static_cast<size_t>(max_ent * nmb)));
+  VTS_TRY(B.get(&d_jobs, static_cast<size_t>(max_chunk * nmb)));
   VTS_TRY(B.get(&d_njobs, 1));
   // Two streams: every level's motion search is enqueued up front on s1
-  // (level j needs only level j-1's reconstruction); the slice writing of
-  // level j (write, sizes to the host, offsets back, gather, I_PCM payloads,
-  // D2H) runs on s2 behind level j's search event, overlapping the searches
-  // of later levels.
+  // (level j needs only level j-1's reconstruction); the slice writing of a
+  // chunk of 16 levels (write, device offset scan, gather, I_PCM payloads,
+  // drain to the host) runs on s2 behind the chunk's last search event,
+  // overlapping the searches of later chunks.
   hipStream_t s1 = c->s_dec, s2 = c->s_score;
   HIP_TRY(hipMemcpy(d_sent, sent.data(), sent.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(d_went, went.data(), went.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(d_stats, 0, 3 * sizeof(unsigned long long), s2));
   HIP_TRY(hipMemsetAsync(d_err, 0, sizeof(uint32_t), s2));
-  std::vector<hipEvent_t> ev(static_cast<size_t>(maxlen) + 4, nullptr);
+  std::vector<hipEvent_t> ev(static_cast<size_t>(maxlen) + 5, nullptr);
   struct EvGuard {
     std::vector<hipEvent_t> &v;
     ~EvGuard() {
@@ -851,64 +867,92 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   }
   HIP_TRY(hipEventRecord(es1, s1));
   HIP_TRY(hipGetLastError());
-  // output drained to the host every kChunkLevels levels: chunk c holds
-  // absolute bytes [chunk_start[c], chunk_start[c+1])
+  // Output drained to the host every chunk (absolute bytes [chunk_start[c],
+  // chunk_start[c+1])) and appended to the MP4's mdat while the GPU works on
+  // the next chunk; the sample table (display order) points into mdat.
+  Mp4Writer mw;
+  std::string e = mw.open(out_path);
+  if (!e.empty()) return fail(VTS_E_IO, "%s: %s", out_path, e.c_str());
   std::vector<std::unique_ptr<uint8_t[]>> host;
-  std::vector<int64_t> chunk_start{0};
+  std::vector<int64_t> chunk_start{0}, chunk_file;  // chunk c's file offset
+  hipEvent_t ev_d2h = ev[maxlen + 4];              // reused: the last chunk's D2H
+  bool pending = false;                            // a chunk's D2H not yet written out
+  double mux_ms = 0;
+  auto write_pending = [&]() -> int {
+    if (!pending) return VTS_OK;
+    HIP_TRY(hipEventSynchronize(ev_d2h));
+    const auto tw = clk::now();
+    const size_t c = host.size() - 1;
+    int64_t off = 0;
+    const std::string we = mw.append(host[c].get(), static_cast<size_t>(chunk_start[c + 1] - chunk_start[c]), &off);
+    if (!we.empty()) return fail(VTS_E_IO, "%s: %s", out_path, we.c_str());
+    chunk_file.push_back(off);
+    host[c].reset();
+    pending = false;
+    mux_ms += std::chrono::duration<double, std::milli>(clk::now() - tw).count();
+    return VTS_OK;
+  };
   int status = VTS_OK;
   HIP_TRY(hipMemsetAsync(d_total, 0, sizeof(int64_t), s2));
   HIP_TRY(hipEventRecord(ew0, s2));
   for (int64_t j0 = 0; j0 < maxlen && status == VTS_OK; j0 += kChunkLevels) {
+    // one chunk of levels = one contiguous run of entries: written, scanned,
+    // gathered and drained together (wide launches instead of one per level)
+    const int64_t j1 = std::min(maxlen, j0 + kChunkLevels);
+    const int64_t e0 = lvl_off[j0], ne = lvl_off[j1] - e0;
+    const int ns = static_cast<int>(ne * mbh);
+    if (j1 - 1 > 0) HIP_TRY(hipStreamWaitEvent(s2, ev[j1 - 1], 0));  // searches run in level order
     HIP_TRY(hipMemcpyAsync(d_base, d_total, sizeof(int64_t), hipMemcpyDeviceToDevice, s2));
-    for (int64_t j = j0; j < std::min(maxlen, j0 + kChunkLevels); ++j) {
-      const int64_t ne = lvl_off[j + 1] - lvl_off[j];
-      const int ns = static_cast<int>(ne * mbh);
-      if (j > 0) HIP_TRY(hipStreamWaitEvent(s2, ev[j], 0));
-      HIP_TRY(hipMemsetAsync(d_njobs, 0, sizeof(uint32_t), s2));
-      WriteArgs wa{};
-      wa.ent = d_went + lvl_off[j];
-      wa.cmd = d_cmd + lvl_off[j] * nmb;
-      wa.small = S.d;
-      wa.stride = S.stride;
-      wa.cw = S.cw;
-      wa.ch = S.ch;
-      wa.mbw = mbw;
-      wa.mbh = mbh;
-      wa.staging = d_stage;
-      wa.cap = cap;
-      wa.sizes = d_sizes;
-      wa.stats = d_stats;
-      wa.err = d_err;
-      wa.jobs = d_jobs;
-      wa.n_jobs = d_njobs;
-      wa.n_slices = ns;
-      wa.idr = j == 0;
-      hipLaunchKernelGGL(enc_write, dim3(static_cast<unsigned>((ns + 63) / 64)), dim3(64), 0, s2, wa);
-      hipLaunchKernelGGL(enc_scan, dim3(1), dim3(1024), 0, s2, d_sizes, ns, d_went + lvl_off[j], mbh, d_offs,
-                         d_total, d_fr, d_fr + n);
-      hipLaunchKernelGGL(enc_gather, dim3(static_cast<unsigned>(ns)), dim3(256), 0, s2, d_stage, cap, d_sizes, d_offs,
-                         d_base, d_out);
-      hipLaunchKernelGGL(enc_pcm, dim3(static_cast<unsigned>(std::min<int64_t>(8192, ne * nmb))), dim3(64), 0, s2,
-                         d_jobs, d_njobs, d_went + lvl_off[j], S.d, S.stride, S.cw, S.ch, mbh, d_offs, d_base,
-                         d_out);
-      const hipError_t he = hipGetLastError();
-      if (he != hipSuccess) {
-        status = fail(VTS_E_HIP, "encoder launch: %s", hipGetErrorString(he));
-        break;
-      }
+    HIP_TRY(hipMemsetAsync(d_njobs, 0, sizeof(uint32_t), s2));
+    WriteArgs wa{};
+    wa.ent = d_went + e0;
+    wa.cmd = d_cmd + e0 * nmb;
+    wa.small = S.d;
+    wa.stride = S.stride;
+    wa.cw = S.cw;
+    wa.ch = S.ch;
+    wa.mbw = mbw;
+    wa.mbh = mbh;
+    wa.staging = d_stage;
+    wa.cap = cap;
+    wa.sizes = d_sizes;
+    wa.stats = d_stats;
+    wa.err = d_err;
+    wa.jobs = d_jobs;
+    wa.n_jobs = d_njobs;
+    wa.n_slices = ns;
+    hipLaunchKernelGGL(enc_write, dim3(static_cast<unsigned>((ns + 63) / 64)), dim3(64), 0, s2, wa);
+    hipLaunchKernelGGL(enc_scan, dim3(1), dim3(1024), 0, s2, d_sizes, ns, d_went + e0, mbh, d_offs, d_total,
+                       d_fr, d_fr + n);
+    hipLaunchKernelGGL(enc_gather, dim3(static_cast<unsigned>(ns)), dim3(256), 0, s2, d_stage, cap, d_sizes, d_offs,
+                       d_base, d_out);
+    hipLaunchKernelGGL(enc_pcm, dim3(static_cast<unsigned>(std::min<int64_t>(16384, ne * nmb))), dim3(64), 0, s2,
+                       d_jobs, d_njobs, d_went + e0, S.d, S.stride, S.cw, S.ch, mbh, d_offs, d_base, d_out);
+    const hipError_t he = hipGetLastError();
+    if (he != hipSuccess) {
+      status = fail(VTS_E_HIP, "encoder launch: %s", hipGetErrorString(he));
+      break;
     }
     if (status != VTS_OK) break;
     int64_t tot = 0;
-    if (hipMemcpyAsync(&tot, d_total, sizeof tot, hipMemcpyDeviceToHost, s2) != hipSuccess ||
-        hipStreamSynchronize(s2) != hipSuccess) {
+    if (hipMemcpyAsync(&tot, d_total, sizeof tot, hipMemcpyDeviceToHost, s2) != hipSuccess) {
+      status = fail(VTS_E_HIP, "encoder levels %lld.. failed", static_cast<long long>(j0));
+      break;
+    }
+    status = write_pending();  // the previous chunk, while this one runs
+    if (status != VTS_OK) break;
+    if (hipStreamSynchronize(s2) != hipSuccess) {
       status = fail(VTS_E_HIP, "encoder levels %lld.. failed", static_cast<long long>(j0));
       break;
     }
     const int64_t bytes = tot - chunk_start.back();
     host.emplace_back(new uint8_t[static_cast<size_t>(std::max<int64_t>(bytes, 1))]);
     HIP_TRY(hipMemcpyAsync(host.back().get(), d_out, static_cast<size_t>(bytes), hipMemcpyDeviceToHost, s2));
+    HIP_TRY(hipEventRecord(ev_d2h, s2));
+    pending = true;
     chunk_start.push_back(tot);
   }
+  if (status == VTS_OK) status = write_pending();
   std::vector<int64_t> fr(static_cast<size_t>(2 * n), 0);
   if (status == VTS_OK)
     HIP_TRY(hipMemcpyAsync(fr.data(), d_fr, sizeof(int64_t) * 2 * n, hipMemcpyDeviceToHost, s2));
@@ -929,26 +973,24 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   HIP_TRY(hipMemcpy(st, d_stats, sizeof st, hipMemcpyDeviceToHost));
   if (err) return fail(VTS_E_CAPACITY, "a slice exceeded its %lld-byte staging slot", static_cast<long long>(cap));
 
-  // 4. MP4 (display order)
+  // 4. MP4 sample table (display order) over the mdat written above
   t0 = clk::now();
   std::vector<uint8_t> sps, pps;
   const double fps = static_cast<double>(c->info.track_timescale) / static_cast<double>(delta);
   make_sps_pps(mbw, mbh, S.cw - S.w, S.ch - S.h, h264_pick_level(nmb, nmb * fps), &sps, &pps);
-  Mp4Writer mw;
-  std::string e = mw.open(out_path);
   std::vector<uint8_t> is_idr(static_cast<size_t>(n), 0);
   for (int64_t f : gop_start) is_idr[f] = 1;
   for (int64_t f = 0; f < n && e.empty(); ++f) {
     const int64_t off = fr[f], size = fr[n + f];
-    const size_t c = static_cast<size_t>(std::upper_bound(chunk_start.begin(), chunk_start.end(), off) -
-                                         chunk_start.begin()) - 1;
-    if (c >= host.size() || off + size > chunk_start[c + 1])
+    const size_t ci = static_cast<size_t>(std::upper_bound(chunk_start.begin(), chunk_start.end(), off) -
+                                          chunk_start.begin()) - 1;
+    if (ci >= chunk_file.size() || off + size > chunk_start[ci + 1])
       return fail(VTS_E_HIP, "frame %lld: output bookkeeping mismatch", static_cast<long long>(f));
-    e = mw.add_sample(host[c].get() + (off - chunk_start[c]), static_cast<size_t>(size), is_idr[f] != 0);
+    e = mw.add_sample_at(chunk_file[ci] + (off - chunk_start[ci]), static_cast<size_t>(size), is_idr[f] != 0);
   }
   if (e.empty()) e = mw.finish(S.w, S.h, c->info.track_timescale, delta, sps, pps);
   if (!e.empty()) return fail(VTS_E_IO, "%s: %s", out_path, e.c_str());
-  ms[3] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  ms[3] = mux_ms + std::chrono::duration<double, std::milli>(clk::now() - t0).count();
   if (info) {
     std::memset(info, 0, sizeof *info);
     info->width = S.w;
