@@ -708,15 +708,21 @@ int small_window(vts_ctx *c, int ring, int64_t f0, int64_t f1, hipStream_t s) {
   a.tc = S.tc;
   a.n_frames = f1 - f0;
   const int64_t threads = static_cast<int64_t>(S.cw / 4) * (S.ch + S.ch / 2);
-  const dim3 grid(static_cast<unsigned>((threads + 255) / 256), static_cast<unsigned>(f1 - f0));
   // integer ratio on both axes (equal): the dword box path; else the tap tables
   const int W = c->width, H = c->height;
   const int k = (W % S.w == 0 && H % S.h == 0 && W / S.w == H / S.h) ? W / S.w : 0;
-  switch (k) {
-    case 2: hipLaunchKernelGGL(downscale_nv12<2>, grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(downscale_nv12<3>, grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(downscale_nv12<4>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(downscale_nv12<0>, grid, dim3(256), 0, s, a); break;
+  for (int64_t g0 = 0; g0 < f1 - f0; g0 += 65535) {  // grid.y <= 65535 frames per launch
+    DsArgs b = a;
+    b.src = a.src + g0 * a.src_stride;
+    b.dst = a.dst + g0 * a.dst_stride;
+    b.n_frames = std::min<int64_t>(65535, f1 - f0 - g0);
+    const dim3 grid(static_cast<unsigned>((threads + 255) / 256), static_cast<unsigned>(b.n_frames));
+    switch (k) {
+      case 2: hipLaunchKernelGGL(downscale_nv12<2>, grid, dim3(256), 0, s, b); break;
+      case 3: hipLaunchKernelGGL(downscale_nv12<3>, grid, dim3(256), 0, s, b); break;
+      case 4: hipLaunchKernelGGL(downscale_nv12<4>, grid, dim3(256), 0, s, b); break;
+      default: hipLaunchKernelGGL(downscale_nv12<0>, grid, dim3(256), 0, s, b); break;
+    }
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "downscale_nv12 launch: %s", hipGetErrorString(e));
