@@ -173,10 +173,27 @@ __device__ __forceinline__ uint32_t u32_at(const uint8_t *lds_row, int off) {  /
 // One wave per macroblock: the reference window (16 + 2R)^2 and the source
 // block go to LDS; each lane takes candidates c = lane, lane + 64, ...;
 // (least luma SAD, candidate index) is a 64-bit min over the wave.
+#ifndef VTS_SEARCH_WAVES
+#define VTS_SEARCH_WAVES 0
+#endif
+#ifndef VTS_SEARCH_UV_LDS
+#define VTS_SEARCH_UV_LDS 0  // 1: chroma reference window staged in LDS (measured slower: 45 vs 37 ms)
+#endif
+#ifndef VTS_SEARCH_SRC_LDS
+#define VTS_SEARCH_SRC_LDS 1  // source rows read from LDS per use, rolled row loop: 47 VGPRs (vs 163), 33 vs 37 ms
+#endif
+#if VTS_SEARCH_WAVES
+#define VTS_SEARCH_OCC __attribute__((amdgpu_waves_per_eu(VTS_SEARCH_WAVES)))
+#else
+#define VTS_SEARCH_OCC
+#endif
+constexpr int kUvPitch = 8 + 2 * kMaxRange + 2;  // chroma window row pitch (Cb|Cr pairs)
+
 template <int RT>  // compile-time search range (register-blocked path), 0 = any range
-__global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
+__global__ void __launch_bounds__(64) VTS_SEARCH_OCC enc_search(SearchArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t win[(16 + 2 * kMaxRange) * kWinPitch];
   __shared__ __attribute__((aligned(16))) uint32_t srcy[64];
+  __shared__ uint16_t winuv[kUvPitch * kUvPitch];
   const int lane = threadIdx.x;
   const int64_t e = blockIdx.x / a.nmb;
   const int mb = static_cast<int>(blockIdx.x % a.nmb);
@@ -218,6 +235,17 @@ __global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
       }
     }
   }
+  // edge-clamped chroma window (Cb|Cr pairs) covering every candidate's
+  // 8.4.2.2.2 taps: origin (mx 8, my 8) - ceil(R/2), 8 + R + 2 pairs square;
+  // loaded beside the luma window so the epilogue reads LDS, not HBM
+  const int cwn = 8 + R + 2, cox = mx * 8 - ((R + 1) >> 1), coy = my * 8 - ((R + 1) >> 1);
+  const int ccw = a.cw / 2, cch = a.ch / 2;
+  const uint8_t *ruv = ref + static_cast<int64_t>(a.cw) * a.ch;
+  for (int i = lane; VTS_SEARCH_UV_LDS && i < cwn * cwn; i += 64) {
+    const int yy = i / cwn, xx = i - yy * cwn;
+    const int sy = min(max(coy + yy, 0), cch - 1), sx = min(max(cox + xx, 0), ccw - 1);
+    winuv[yy * kUvPitch + xx] = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(sy) * a.cw + 2 * sx);
+  }
   __syncthreads();
   const int ncand = side * side, center = R * side + R;
   uint64_t best = ~0ull;
@@ -230,15 +258,21 @@ __global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
     constexpr int SIDE = 2 * RT + 1, NG = 64 / SIDE, G = (SIDE + NG - 1) / NG;
     const int gx = lane % SIDE, gy = lane / SIDE, dy0 = gy * G;
     if (gy < NG && dy0 < SIDE) {
+#if !VTS_SEARCH_SRC_LDS
       uint32_t sv[64];
 #pragma unroll
       for (int i = 0; i < 64; ++i) sv[i] = srcy[i];
+#endif
       uint32_t acc[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) acc[g] = 0;
       const int sh = gx & 3;
       const uint32_t *wb = reinterpret_cast<const uint32_t *>(win + dy0 * kWinPitch + (gx & ~3));
+#if VTS_SEARCH_SRC_LDS
+#pragma unroll 2
+#else
 #pragma unroll
+#endif
       for (int w = 0; w < 16 + G - 1; ++w) {
         const uint32_t *wr = wb + w * (kWinPitch / 4);
         const uint32_t w0 = wr[0], w1 = wr[1], w2 = wr[2], w3 = wr[3], w4 = wr[4];
@@ -248,10 +282,16 @@ __global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
         for (int g = 0; g < G; ++g) {
           const int yy = w - g;
           if (yy >= 0 && yy < 16) {
-            acc[g] = __builtin_amdgcn_sad_u8(r0, sv[4 * yy], acc[g]);
-            acc[g] = __builtin_amdgcn_sad_u8(r1, sv[4 * yy + 1], acc[g]);
-            acc[g] = __builtin_amdgcn_sad_u8(r2, sv[4 * yy + 2], acc[g]);
-            acc[g] = __builtin_amdgcn_sad_u8(r3, sv[4 * yy + 3], acc[g]);
+#if VTS_SEARCH_SRC_LDS
+            const uint4 q = reinterpret_cast<const uint4 *>(srcy)[yy];  // broadcast read
+            const uint32_t s0 = q.x, s1 = q.y, s2 = q.z, s3 = q.w;
+#else
+            const uint32_t s0 = sv[4 * yy], s1 = sv[4 * yy + 1], s2 = sv[4 * yy + 2], s3 = sv[4 * yy + 3];
+#endif
+            acc[g] = __builtin_amdgcn_sad_u8(r0, s0, acc[g]);
+            acc[g] = __builtin_amdgcn_sad_u8(r1, s1, acc[g]);
+            acc[g] = __builtin_amdgcn_sad_u8(r2, s2, acc[g]);
+            acc[g] = __builtin_amdgcn_sad_u8(r3, s3, acc[g]);
           }
         }
       }
@@ -303,16 +343,23 @@ __global__ void __launch_bounds__(64) enc_search(SearchArgs a) {
   const uint32_t py = u32_at(win + (dy + R + ly) * kWinPitch, dx + R + lx);
   const uint32_t sy4 = srcy[lane];
   uint32_t cost = __builtin_amdgcn_sad_u8(py, sy4, 0);
-  const int ci = lane & 7, cj = lane >> 3, ccw = a.cw / 2, cch = a.ch / 2;
+  const int ci = lane & 7, cj = lane >> 3;
   const int mvx = 4 * dx, mvy = 4 * dy, fx = mvx & 7, fy = mvy & 7;
+  // window coordinates of taps (xi, yi) and (xi + 1, yi + 1); the window holds
+  // the clamped samples, so this equals the decoder's per-tap clamping
+#if VTS_SEARCH_UV_LDS
+  const int wx = ci + (mvx >> 3) + ((R + 1) >> 1), wy = cj + (mvy >> 3) + ((R + 1) >> 1);
+  const uint16_t A = winuv[wy * kUvPitch + wx], B = winuv[wy * kUvPitch + wx + 1];
+  const uint16_t Cc = winuv[(wy + 1) * kUvPitch + wx], D = winuv[(wy + 1) * kUvPitch + wx + 1];
+#else
   const int xi = mx * 8 + ci + (mvx >> 3), yi = my * 8 + cj + (mvy >> 3);
   const int xa = min(max(xi, 0), ccw - 1), xb = min(max(xi + 1, 0), ccw - 1);
   const int ya = min(max(yi, 0), cch - 1), yb = min(max(yi + 1, 0), cch - 1);
-  const uint8_t *ruv = ref + static_cast<int64_t>(a.cw) * a.ch;
   const uint16_t A = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(ya) * a.cw + 2 * xa);
   const uint16_t B = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(ya) * a.cw + 2 * xb);
   const uint16_t Cc = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(yb) * a.cw + 2 * xa);
   const uint16_t D = *reinterpret_cast<const uint16_t *>(ruv + static_cast<int64_t>(yb) * a.cw + 2 * xb);
+#endif
   const int wa = (8 - fx) * (8 - fy), wb = fx * (8 - fy), wc = (8 - fx) * fy, wd = fx * fy;
   const int pu = (wa * (A & 255) + wb * (B & 255) + wc * (Cc & 255) + wd * (D & 255) + 32) >> 6;
   const int pv = (wa * (A >> 8) + wb * (B >> 8) + wc * (Cc >> 8) + wd * (D >> 8) + 32) >> 6;
