@@ -52,3 +52,37 @@ def test_install_rebinds_reference_names(tmp_path, monkeypatch):
         for k in [k for k in sys.modules if k == "utils" or k.startswith(("utils.", "analyzer"))]:
             del sys.modules[k]
         sys.modules.update(saved)
+
+
+def test_install_upload_transcode_is_opt_in(tmp_path, monkeypatch):
+    """install(upload_transcode=True) replaces ContentAnalyzer's
+    _compress_video_for_upload (content_analyzer.py:167-236) with
+    vtseg.upload's; the default leaves it alone."""
+    (tmp_path / "analyzer").mkdir()
+    (tmp_path / "analyzer" / "__init__.py").write_text("")
+    (tmp_path / "analyzer" / "content_analyzer.py").write_text(textwrap.dedent("""
+        class ContentAnalyzer:
+            logger = None
+            def _compress_video_for_upload(self, video_path):
+                return "reference"
+    """))
+    saved = {k: v for k, v in sys.modules.items() if k == "utils" or k.startswith(("utils.", "analyzer"))}
+    for k in list(saved):
+        del sys.modules[k]
+    monkeypatch.syspath_prepend(str(tmp_path))
+    try:
+        ca = importlib.import_module("analyzer.content_analyzer")
+        import vtseg.dropin as dropin
+        from vtseg import upload
+        dropin.install()
+        assert ca.ContentAnalyzer()._compress_video_for_upload("x") == "reference"
+        seen = {}
+        monkeypatch.setattr(upload, "compress_video_for_upload",
+                            lambda p, logger=None: seen.setdefault("p", p))
+        bound = dropin.install(upload_transcode=True)
+        assert "analyzer.content_analyzer.ContentAnalyzer._compress_video_for_upload" in bound
+        assert ca.ContentAnalyzer()._compress_video_for_upload("v.mp4") == "v.mp4"
+    finally:
+        for k in [k for k in sys.modules if k == "utils" or k.startswith(("utils.", "analyzer"))]:
+            del sys.modules[k]
+        sys.modules.update(saved)
