@@ -702,12 +702,15 @@ __device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int w) {
 #ifndef VTS_K6_WAVES
 #define VTS_K6_WAVES 0
 #endif
+#ifndef VTS_K6_BAND
+#define VTS_K6_BAND 1  // h264_recon_score6b (one wave per band); 0: the LDS-sum layout
+#endif
 #if VTS_K6_WAVES
 #define VTS_K6_OCC __attribute__((amdgpu_waves_per_eu(VTS_K6_WAVES)))
 #else
 #define VTS_K6_OCC
 #endif
-__global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC h264_recon_score6(FusedArgs fa) {
+__global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC __attribute__((unused)) h264_recon_score6(FusedArgs fa) {
   constexpr int K = 6, HK = 3;
   __shared__ uint32_t lds_y[kK6Bands * kK6Px], lds_uv[kK6Bands * kK6Px];
   __shared__ uint32_t lds_hist[256];
@@ -862,6 +865,219 @@ __global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC h264_recon_score6(Fused
   if (errs) atomicOr(a.err, errs);
 }
 
+// h264_recon_score6b: the k = 6 kernel with one WAVE per (thumbnail band,
+// 63 consecutive macroblock columns).  A band is 6 luma + 3 chroma rows, so
+// it spans at most two macroblock rows (two commands); lanes of a wave take
+// consecutive macroblocks, so every row load and store instruction covers
+// 63 x 16 contiguous bytes, as in the k = 4 kernel.  A 48-column triple of
+// macroblocks holds 8 thumbnail pixels: the lane of its first macroblock owns
+// pixels 0-2, the second 3-5, the third 6-7; the two pixels that straddle a
+// macroblock edge get the neighbour's partial sum through one shuffle (63 =
+// 21 triples per wave, so no triple crosses a wave).  No LDS partial sums, no
+// LDS atomics except the histogram.  4 waves (4 bands) per workgroup.
+constexpr int kK6bCols = 63;
+
+// DEC_E_EPB_IN_PCM if an emulation-prevention byte falls in row `rin` of an
+// I_PCM block (a luma row, or the Cb and Cr rows of chroma row rin)
+__device__ __noinline__ uint32_t pcm_row_epb(const uint8_t *pcm, bool chroma, int rin) {
+  const bool bad = chroma ? (epb_in_pcm(pcm + 256 + 8 * rin, 8, pcm) || epb_in_pcm(pcm + 320 + 8 * rin, 8, pcm))
+                          : epb_in_pcm(pcm + 16 * rin, 16, pcm);
+  return bad ? DEC_E_EPB_IN_PCM : 0u;
+}
+
+#ifndef VTS_K6B_WAVES
+#define VTS_K6B_WAVES 0
+#endif
+#if VTS_K6B_WAVES
+#define VTS_K6B_OCC __attribute__((amdgpu_waves_per_eu(VTS_K6B_WAVES)))
+#else
+#define VTS_K6B_OCC
+#endif
+__global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs fa) {
+  constexpr int K = 6, HK = 3;
+  __shared__ uint32_t lds_hist[256];
+  __shared__ uint32_t red[4];
+  const ReconArgs &a = fa.r;
+  const int mbw = a.mb_width, nmb = mbw * a.mb_height;
+  const int segs = (mbw + kK6bCols - 1) / kK6bCols;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int fi = bid / fa.wgs_per_frame;
+  const int wb = bid - fi * fa.wgs_per_frame;
+  const int seg = wb % segs, bg = wb / segs;
+  const int lane = threadIdx.x & 63, band = bg * 4 + (threadIdx.x >> 6);
+  const int m = seg * kK6bCols + lane;
+  const int4 fr = a.frames[fi];
+  const FrameRefs F = frame_refs(a, fr.y);
+  const int64_t gframe = fa.frame0 + fr.x;
+  const int64_t npx = static_cast<int64_t>(fa.w) * fa.h;
+  const int r0 = K * band;                                 // first luma row of the band
+  const bool active = lane < kK6bCols && m < mbw && r0 < F.H;
+  const int mby0 = r0 >> 4, mby1 = min(r0 + K - 1, F.H - 1) >> 4;
+  uint64_t c0 = 0, c1 = 0;
+  if (active) {
+    const uint64_t *cm = a.cmd + static_cast<int64_t>(fr.x) * nmb + m;
+    c0 = current_cmd(cm[static_cast<int64_t>(mby0) * mbw], a.epoch);
+    c1 = mby1 == mby0 ? c0 : current_cmd(cm[static_cast<int64_t>(mby1) * mbw], a.epoch);
+  }
+  // owned thumbnail pixels (see above) and the predecessor's bytes, early
+  const int j = lane % 3;
+  const int pix0 = (m / 3) * 8 + (j == 0 ? 0 : (j == 1 ? 3 : 6));
+  const int nown = j == 2 ? 2 : 3;
+  const bool scored = active && band < fa.h;
+  uint32_t prevb[3] = {0, 0, 0};
+  if (scored && fr.z >= 0) {
+    const uint8_t *pt = fa.thumb + static_cast<int64_t>(fr.z) * npx + static_cast<int64_t>(band) * fa.w;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (i < nown && pix0 + i < fa.w) prevb[i] = pt[pix0 + i];
+  }
+  lds_hist[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t errs = 0;
+  uint4 rows[K + HK];  // 6 luma rows, then 3 NV12 chroma rows
+  if (active) {
+    uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
+    uint8_t *dst_uv = dst + F.pitch * F.H;
+    if (fast_cmd(F, c0) && fast_cmd(F, c1)) {
+      uint4 lo[K + HK], hi[K + HK];
+      int shf[K + HK];
+#pragma unroll
+      for (int i = 0; i < K + HK; ++i) {
+        const bool chroma = i >= K;
+        const int r = chroma ? HK * band + (i - K) : r0 + i;  // luma row / chroma row
+        const int mbr = chroma ? r >> 3 : r >> 4;
+        const uint64_t c = mbr == mby0 ? c0 : c1;
+        const bool pcm = (c >> 62) == 1;
+        const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
+        const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+        if (r < (chroma ? F.CH : F.H))
+          issue_row(F, pcmb, pcm, chroma, chroma ? (r & 7) : (r & 15), m, mbr, mvx, mvy, lo[i], hi[i], shf[i]);
+        else
+          lo[i] = hi[i] = make_uint4(0, 0, 0, 0), shf[i] = 0;
+      }
+      uint32_t zero = 0;
+#pragma unroll
+      for (int i = 0; i < K + HK; ++i) {
+        const bool chroma = i >= K;
+        const int r = chroma ? HK * band + (i - K) : r0 + i;
+        const uint64_t c = (chroma ? r >> 3 : r >> 4) == mby0 ? c0 : c1;
+        rows[i] = finish_row(chroma, (c >> 62) == 1, lo[i], hi[i], shf[i], zero);
+      }
+      if (zero) {  // a zero byte in I_PCM samples: check for emulation prevention exactly
+        for (int i = 0; i < K + HK; ++i) {
+          const bool chroma = i >= K;
+          const int r = chroma ? HK * band + (i - K) : r0 + i;
+          const uint64_t c = (chroma ? r >> 3 : r >> 4) == mby0 ? c0 : c1;
+          if ((c >> 62) == 1 && r < (chroma ? F.CH : F.H))
+            errs |= pcm_row_epb(F.es + static_cast<int64_t>(c & 0xffffffffffffull), chroma, chroma ? (r & 7) : (r & 15));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < K + HK; ++i) {
+        const bool chroma = i >= K;
+        const int r = chroma ? HK * band + (i - K) : r0 + i;
+        if (r < (chroma ? F.CH : F.H))
+          st_row((chroma ? dst_uv : dst) + static_cast<int64_t>(r) * F.pitch + m * 16, rows[i]);
+      }
+    } else {
+      // general path (sub-pel chroma, errors): rare; one row at a time,
+      // stored, then read back for scoring (no runtime-indexed register array)
+#pragma unroll 1
+      for (int i = 0; i < K + HK; ++i) {
+        const bool chroma = i >= K;
+        const int r = chroma ? HK * band + (i - K) : r0 + i;
+        const int mbr = chroma ? r >> 3 : r >> 4;
+        if (r < (chroma ? F.CH : F.H))
+          *reinterpret_cast<uint4 *>((chroma ? dst_uv : dst) + static_cast<int64_t>(r) * F.pitch + m * 16) =
+              fetch_row(F, mbr == mby0 ? c0 : c1, chroma ? 16 + (r & 7) : (r & 15), m, mbr, errs);
+      }
+#pragma unroll
+      for (int i = 0; i < K + HK; ++i) {
+        const bool chroma = i >= K;
+        const int r = chroma ? HK * band + (i - K) : r0 + i;
+        rows[i] = r < (chroma ? F.CH : F.H)
+                      ? *reinterpret_cast<const uint4 *>((chroma ? dst_uv : dst) + static_cast<int64_t>(r) * F.pitch + m * 16)
+                      : make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+  // box sums: the left partial (bytes owed to the previous lane's last pixel)
+  // and the owned pixels' segments, luma over 6 rows, Cb / Cr over 3
+  uint32_t ys[4] = {0, 0, 0, 0}, us[4] = {0, 0, 0, 0}, vs[4] = {0, 0, 0, 0};  // [0] = left partial
+  if (scored) {
+    const int b0 = j == 0 ? 0 : (j == 1 ? 2 : 4);  // end of the left partial = start of pixel 1
+#pragma unroll
+    for (int sgm = 0; sgm < 4; ++sgm) {
+      // segment sgm: 0 = [0, b0), 1.. = owned pixels [b0 + 6 (sgm-1), +6) clipped to 16
+      const int lo_b = sgm == 0 ? 0 : b0 + 6 * (sgm - 1);
+      const int hi_b = sgm == 0 ? b0 : min(lo_b + 6, 16);
+      if (hi_b <= lo_b) continue;
+      uint32_t y = 0, u = 0, v = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t mk = byte_mask(lo_b, hi_b, w);
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+          const uint32_t word = w == 0 ? rows[i].x : (w == 1 ? rows[i].y : (w == 2 ? rows[i].z : rows[i].w));
+          y = sad_u8(word & mk, 0u, y);
+        }
+#pragma unroll
+        for (int i = K; i < K + HK; ++i) {
+          const uint32_t word = w == 0 ? rows[i].x : (w == 1 ? rows[i].y : (w == 2 ? rows[i].z : rows[i].w));
+          u = sad_u8(word & mk & 0x00ff00ffu, 0u, u);
+          v = sad_u8(word & mk & 0xff00ff00u, 0u, v);
+        }
+      }
+      ys[sgm] = y;
+      us[sgm] = u;
+      vs[sgm] = v;
+    }
+  }
+  // the next lane's left partial completes this lane's last pixel
+  const uint32_t yn = __shfl_down(ys[0], 1, 64), un = __shfl_down(us[0], 1, 64), vn = __shfl_down(vs[0], 1, 64);
+  uint32_t sad = 0;
+  if (scored) {
+    if (j != 2) {
+      ys[3] += yn;
+      us[3] += un;
+      vs[3] += vn;
+    }
+    const int64_t tpx = static_cast<int64_t>(band) * fa.w + pix0;
+    uint8_t *rgb = fa.rgb + (gframe * npx + tpx) * 3;
+    uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i >= nown || pix0 + i >= fa.w) continue;
+      const uint32_t y = (ys[1 + i] + K * K / 2) / (K * K);
+      const uint32_t u = (us[1 + i] + HK * HK / 2) / (HK * HK), v = (vs[1 + i] + HK * HK / 2) / (HK * HK);
+      const uint32_t c24 = bt709_rgb24(y, u, v);
+      rgb[3 * i] = static_cast<uint8_t>(c24);
+      rgb[3 * i + 1] = static_cast<uint8_t>(c24 >> 8);
+      rgb[3 * i + 2] = static_cast<uint8_t>(c24 >> 16);
+      thumb[i] = static_cast<uint8_t>(y);
+      atomicAdd(&lds_hist[y], 1u);
+      if (fr.z >= 0) sad += y > prevb[i] ? y - prevb[i] : prevb[i] - y;
+    }
+  }
+  if (fr.z >= 0) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sad += __shfl_xor(sad, off, 64);
+    if (lane == 0) red[threadIdx.x >> 6] = sad;
+  }
+  __syncthreads();
+  if (fr.z >= 0 && threadIdx.x == 0) {
+    const uint64_t t = uint64_t(red[0]) + red[1] + red[2] + red[3];
+    if (t) atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(t));
+  }
+  if (threadIdx.x < 128) {
+    const uint64_t lo = lds_hist[2 * threadIdx.x], hi = lds_hist[2 * threadIdx.x + 1];
+    if (lo | hi)
+      atomicAdd(reinterpret_cast<unsigned long long *>(fa.hist + gframe * 256) + threadIdx.x,
+                static_cast<unsigned long long>(lo | (hi << 32)));
+  }
+  if (errs) atomicOr(a.err, errs);
+}
+
 // SAD of each frame's thumbnail luma against its predecessor's (the previous
 // window's last thumbnail for the window's first frame) and the score.  One
 // workgroup per frame; 16-byte loads, all of a thread's loads issued before
@@ -971,8 +1187,15 @@ int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
   if (k == 6) {
     FusedArgs b = a;
+#if VTS_K6_BAND
+    // one wave per (band, 63 macroblock columns), 4 bands per workgroup
+    const int bands = (a.r.mb_height * 16 + 5) / 6;
+    b.wgs_per_frame = ((a.r.mb_width + kK6bCols - 1) / kK6bCols) * ((bands + 3) / 4);
+    hipLaunchKernelGGL(h264_recon_score6b, dim3(n_frames * b.wgs_per_frame), dim3(256), 0, s, b);
+#else
     b.wgs_per_frame = ((a.r.mb_width + kK6Cols - 1) / kK6Cols) * ((a.r.mb_height + kK6Rows - 1) / kK6Rows);
     hipLaunchKernelGGL(h264_recon_score6, dim3(n_frames * b.wgs_per_frame), dim3(kK6Threads), 0, s, b);
+#endif
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score6 launch: %s", hipGetErrorString(e));
     return VTS_OK;
