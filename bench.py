@@ -183,7 +183,7 @@ def cpu_baseline_transcode(path, k, budget_s=15.0):
 
 
 def _kernel_short(name: str) -> str:
-    m = re.search(r"(h264_recon_score6|h264_\w+|thumb_sad|score_\w+)(<\d+>)?", name)
+    m = re.search(r"(h264_recon_score6b?|h264_\w+|thumb_sad|score_\w+)(<\d+>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name.split("(")[0][-60:]
 
 
@@ -409,7 +409,7 @@ def main() -> None:
         if fused:
             # dominant kernel = h264_recon_score (decode + score in one pass)
             kern_ms = rec_ms
-            kname = "h264_recon_score6" if k == 6 else "h264_recon_score<%d>" % k
+            kname = "h264_recon_score6b" if k == 6 else "h264_recon_score<%d>" % k
         else:
             kern_ms = float(np.mean([t["score_ms"] for t in times]))
             kname = "score_runs<%d>" % k
