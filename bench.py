@@ -70,6 +70,21 @@ def fused_bytes_per_frame(width: int, height: int, k: int) -> int:
     return 3 * width * height + 3 * w * h + 2 * w * h + 1024 + 8
 
 
+def tb_bytes_per_launch(width: int, height: int, k: int, frames: int, chains: int,
+                        launches: int, keep: bool = False) -> float:
+    """h264_recon_score_tb (level-blocked): per chain of L levels one
+    NV12-sized source read (reference picture or I_PCM samples), one NV12
+    frame written (the chain's last level; every level with keep) and the
+    predecessor thumbnail read once; per frame the RGB thumbnail, thumbnail
+    luma written, histogram and SAD.  The levels between a chain's first and
+    last stay in LDS and move no HBM bytes."""
+    w, h = width // k, height // k
+    nv12 = 1.5 * width * height
+    per_chain = nv12 + (0 if keep else nv12) + w * h
+    per_frame = 3 * w * h + w * h + 1024 + 8 + (nv12 if keep else 0)
+    return (chains * per_chain + frames * per_frame) / launches
+
+
 def smooth_frames_host(rng, n, width, height):
     frames = np.empty((n, height * 3 // 2, width), np.uint8)
     for i in range(n):
@@ -183,7 +198,7 @@ def cpu_baseline_transcode(path, k, budget_s=15.0):
 
 
 def _kernel_short(name: str) -> str:
-    m = re.search(r"(h264_recon_score6b?|h264_\w+|thumb_sad|score_\w+)(<\d+>)?", name)
+    m = re.search(r"(h264_recon_score_tb|h264_recon_score6b?|h264_\w+|thumb_sad|score_\w+)(<\d+>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name.split("(")[0][-60:]
 
 
@@ -248,6 +263,9 @@ def main() -> None:
                     help="gloo: rehearse the N>1 path with several ranks on one GPU")
     ap.add_argument("--parse-chunks", type=int, default=1,
                     help="slice-parse chunks overlapped with reconstruction (1 = none, the default)")
+    ap.add_argument("--level-block", type=int, default=0,
+                    help="GOP levels per reconstruct launch (0 auto = level-blocked kernel where it "
+                         "applies, 1 = one launch per level)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
     args = ap.parse_args()
@@ -318,7 +336,7 @@ def main() -> None:
         scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
                           seed=0x5EED + rank)
         scorer = scene.VideoScorer(path, device=gpu, gops_per_launch=args.gops_per_launch,
-                                   parse_chunks=args.parse_chunks)
+                                   parse_chunks=args.parse_chunks, level_block=args.level_block)
         duration_s = float(scorer.info.duration)
 
         if args.workload == "transcode":
@@ -377,6 +395,7 @@ def main() -> None:
 
     # ------------------------------------------- roofline (dominant kernel)
     roof = None
+    tb_launches, tb_chains = 0, 0
     if args.workload == "score":
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 5
@@ -403,19 +422,24 @@ def main() -> None:
         for _ in range(3):
             scorer.run()
             times.append(scorer.timings())
-        n_launch = scorer.recon_launches()
+        tb_launches, tb_chains = scorer.level_blocks()
+        n_launch = tb_launches or scorer.recon_launches()
         fused = scorer.fused()
         rec_ms = float(np.mean([t["reconstruct_ms"] for t in times])) / n_launch
         if fused:
             # dominant kernel = h264_recon_score (decode + score in one pass)
             kern_ms = rec_ms
-            kname = "h264_recon_score6b" if k == 6 else "h264_recon_score<%d>" % k
+            kname = ("h264_recon_score_tb" if tb_launches else
+                     "h264_recon_score6b" if k == 6 else "h264_recon_score<%d>" % k)
         else:
             kern_ms = float(np.mean([t["score_ms"] for t in times]))
             kname = "score_runs<%d>" % k
     if args.workload == "transcode":
         bytes_per_frame = None
         frames_per_launch = p_frames / n_launch
+    elif scorer is not None and scorer.fused() and tb_launches:
+        frames_per_launch = F / n_launch
+        bytes_per_frame = tb_bytes_per_launch(width, height, k, F, tb_chains, n_launch) / frames_per_launch
     elif scorer is not None and scorer.fused():
         bytes_per_frame = fused_bytes_per_frame(width, height, k)
         frames_per_launch = F / n_launch

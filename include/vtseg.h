@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define VTS_ABI_VERSION 2
+#define VTS_ABI_VERSION 3
 
 enum {
   VTS_OK = 0,
@@ -236,6 +236,15 @@ typedef struct vts_params {
   int32_t parse_chunks;    /* slice parsing on its own stream in N chunks of
                               launches, chunk j+1 overlapping reconstruction of
                               chunk j; <= 1 (default) = one parse launch */
+  int32_t level_block;     /* GOP levels decoded per reconstruct launch (k = 4,
+                              fused, GOPs that are plain P chains): 0 (auto)
+                              and 1 = one launch per level (fastest measured);
+                              n >= 2 = up to n levels per launch with the
+                              levels between in LDS */
+  int32_t keep_frames;     /* level-blocked launches keep only each block's
+                              last frame in HBM (the next block's reference);
+                              1 = store every decoded frame (vts_get_frame_nv12
+                              of any frame; the transcoder sets it itself)  */
 } vts_params;
 
 /* Demux the file's first H.264 video track on the host (MP4 boxes and NAL

@@ -43,8 +43,12 @@ def _oracle_scores(frames, w, h):
                                want_rgb=True)
 
 
+@pytest.mark.parametrize("level_block", [1, 4], ids=["per_level", "level_blocked"])
 @pytest.mark.parametrize("name,kw", STREAMS, ids=[s[0] for s in STREAMS])
-def test_decode_and_score_bit_exact(tmp_path, name, kw):
+def test_decode_and_score_bit_exact(tmp_path, name, kw, level_block):
+    """level_block 1: one reconstruct launch per GOP level; 4: the
+    level-blocked kernel where it applies (k = 4), storing every frame here
+    (keep_frames) so each one is compared."""
     _require_gpu()
     n = 90 if kw["height"] < 720 else 40
     path = tmp_path / f"{name}.mp4"
@@ -53,7 +57,7 @@ def test_decode_and_score_bit_exact(tmp_path, name, kw):
     frames, info = oracle.decode_file(path)
     assert oracle.recon_hash(frames) == r["recon_hash"]
     ref = _oracle_scores(frames, kw["width"], kw["height"])
-    with scene.VideoScorer(path) as vsr:
+    with scene.VideoScorer(path, level_block=level_block, keep_frames=True) as vsr:
         res = vsr.score()
         for i in range(n):
             got = vsr.frame_nv12(i).reshape(frames[i].shape)

@@ -55,6 +55,15 @@ struct FusedArgs {
   uint64_t *sad;           // [global frame], zeroed before the window
 };
 
+// Level-blocked fused reconstruct + scoring (k = 4, h264_recon_score_tb).
+struct TbArgs {
+  FusedArgs f;             // f.r.frames unused
+  const int4 *chains;      // [chain][L]: (slot, ref_slot, sad_prev, 0) of L consecutive
+                           // GOP levels; slot -1 past the chain's end
+  int32_t L;
+  int32_t keep;            // store every level's frame (else only each chain's last)
+};
+
 struct ThumbSadArgs {
   const uint8_t *thumb;    // [slot][h][w]
   const int32_t *list;     // slots to compute (nullptr = all n_frames)
@@ -75,6 +84,10 @@ int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s);
 int sad_score_launch(const uint64_t *sad, float *score, int64_t frame0, int64_t n_frames,
                      int64_t npx, hipStream_t s);
 int recon_launch(const ReconArgs &a, int n_frames, hipStream_t s);
+// one workgroup per (chain, macroblock row); LDS bytes / tasks per level 0
+int tb_launch(const TbArgs &a, int n_chains, hipStream_t s);
+int tb_lds_bytes(int mb_width, int mb_height, int L);
+int tb_max_tasks(int mb_width, int mb_height, int L);
 // hist[0 .. 256 n) = 0, sad[0 .. n) = 0 (hist 16-byte aligned)
 int clear_accum_launch(uint32_t *hist, uint64_t *sad, int64_t n_frames, hipStream_t s);
 int score_launch(const vts_score_desc *d, hipStream_t stream);

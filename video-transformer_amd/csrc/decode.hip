@@ -1153,6 +1153,331 @@ __global__ void __launch_bounds__(256) clear_accum(uint4 *hist, uint64_t *sad, i
   if (i < n) sad[i] = 0;
 }
 
+// ------------------------------------- level-blocked decode + scoring (k = 4)
+// h264_recon_score_tb: one workgroup per (GOP chain, macroblock row "band")
+// decodes L consecutive GOP levels of that band without sending the levels
+// between the first and the last through HBM.  Every frame at level l >= 1 is
+// predicted from the frame at level l-1 only, with motion of at most one
+// 4-row halo group per level vertically (checked per macroblock; see
+// DEC_W_LEVEL_RANGE), so level j of the band needs level j-1 over the band
+// widened by one group on each side.  The workgroup therefore reconstructs
+// level 0 over the band +- (L-1) groups (full picture width: horizontal
+// motion and edge clamping need no halo), from the HBM reference or the
+// I_PCM samples, into LDS; each following level over one group less on each
+// side, read from and written back to the same LDS rows (all reads of a
+// level land in registers before a barrier, then the writes); the last level
+// covers the band only.  The band rows of every level are scored exactly as
+// h264_recon_score<4> scores them (RGB, thumbnail luma, LDS histogram,
+// SAD against the previous level's thumbnail, which the lane still holds).
+// HBM traffic per L frames: one reference read + one frame write + the
+// scoring outputs, instead of L of each; the halo rows are recomputed
+// (1.75x the reconstruction ALU work at L = 4), not re-read.
+constexpr int kTbThreads = 512;
+constexpr int kTbSlots = 2;  // tasks (macroblock, group) per lane and level
+constexpr int kTbHalo = 1;   // halo groups per level: 4 luma / 2 chroma rows
+
+// 16 bytes of an LDS row at byte x0 (any alignment; horizontal clamping at
+// the picture edges as issue_row / finish_row do it for HBM rows)
+__device__ __forceinline__ uint4 tb_lds_row(const uint8_t *row, int x0, int W, bool chroma) {
+  const uint4 *pa;
+  int sh;
+  if (x0 < 0) {
+    pa = reinterpret_cast<const uint4 *>(row);
+    sh = (x0 > -16 ? 16 + x0 : 0) | (1 << 8);
+  } else if (x0 > W - 16) {
+    pa = reinterpret_cast<const uint4 *>(row + W - 16);
+    sh = min(x0 - (W - 16), 16) | (2 << 8);
+  } else {
+    sh = x0 & 15;
+    pa = reinterpret_cast<const uint4 *>(row + (x0 - sh));
+  }
+  const uint4 lo = pa[0];
+  const uint4 hi = (sh > 0 && sh < 16) ? pa[1] : lo;  // edges (sh >= 256) use lo only
+  uint32_t zero_unused = 0;
+  return finish_row(chroma, false, lo, hi, sh, zero_unused);
+}
+
+// The 6 rows (4 luma, 2 NV12 chroma) of group g of macroblock column m from
+// HBM: the reference picture F or the I_PCM samples (level 0 of a chain),
+// stored straight into the LDS rows (level 0 overwrites nothing it reads).
+__device__ __forceinline__ void tb_group_hbm(const FrameRefs &F, uint64_t c, int m, int g, uint8_t *lds_y,
+                                             uint8_t *lds_uv, int W, uint32_t &errs) {
+  const int mby = g >> 2, q = g & 3;
+  const uint32_t kind = static_cast<uint32_t>(c >> 62);
+  const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+  if (fast_cmd(F, c)) {
+    const bool pcm = kind == 1;
+    const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
+    uint4 lo[6], hi[6];
+    int shf[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      issue_row(F, pcmb, pcm, i >= 4, i < 4 ? 4 * q + i : 2 * q + (i - 4), m, mby, mvx, mvy, lo[i], hi[i], shf[i]);
+    uint32_t zero = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const uint4 v = finish_row(i >= 4, pcm, lo[i], hi[i], shf[i], zero);
+      *reinterpret_cast<uint4 *>((i < 4 ? lds_y + i * W : lds_uv + (i - 4) * W) + m * 16) = v;
+    }
+    if (pcm && zero) errs |= pcm_rows_epb(pcmb, q, 4, 2);
+  } else {
+#pragma unroll 1
+    for (int i = 0; i < 6; ++i) {
+      const uint4 v = fetch_row(F, c, i < 4 ? 4 * q + i : 16 + 2 * q + (i - 4), m, mby, errs);
+      *reinterpret_cast<uint4 *>((i < 4 ? lds_y + i * W : lds_uv + (i - 4) * W) + m * 16) = v;
+    }
+  }
+}
+
+// sub-pel chroma (bilinear eighth-pel) of 8 Cb/Cr pairs from two LDS rows:
+// fetch_row's general path (rolled: rare, kept small).
+__device__ __forceinline__ uint4 tb_subpel(const uint8_t *ra, const uint8_t *rb, int cx, int fx, int fy, int CW) {
+  uint64_t lo8 = 0, hi8 = 0;
+#pragma unroll 1
+  for (int b = 0; b < 8; ++b) {
+    const int xa = clampi(cx + b, 0, CW - 1), xb = clampi(cx + b + 1, 0, CW - 1);
+    uint64_t pair = 0;
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+      const int A = ra[2 * xa + pl], B = ra[2 * xb + pl], C = rb[2 * xa + pl], D = rb[2 * xb + pl];
+      const uint64_t v = static_cast<uint64_t>(
+          ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
+      pair |= v << (8 * pl);
+    }
+    if (b < 4) lo8 |= pair << (16 * b); else hi8 |= pair << (16 * (b - 4));
+  }
+  return make_uint4(uint32_t(lo8), uint32_t(lo8 >> 32), uint32_t(hi8), uint32_t(hi8 >> 32));
+}
+
+// Same from the previous level held in LDS: luma rows [ly0, ly0 + nl) at
+// lds + (y - ly0) W, chroma rows from cy0 at lds + nl W + (cy - cy0) W, of
+// which rows [vy0, vy1) / [vc0, vc1) are valid.  A reference row outside them
+// sets `range` (the launch's halo is too small for this motion).
+__device__ __forceinline__ void tb_group_lds(const uint8_t *lds, int ly0, int cy0, int nl, int W, int H, int vy0,
+                                             int vy1, int vc0, int vc1, const uint8_t *es, uint64_t c, int m,
+                                             int g, uint4 *rows, uint32_t &errs, uint32_t &range) {
+  const int q = g & 3;
+  const uint32_t kind = static_cast<uint32_t>(c >> 62);
+  if (kind == 1) {
+    FrameRefs F{};
+    const uint8_t *pcmb = es + static_cast<int64_t>(c & 0xffffffffffffull);
+    uint4 lo[6], hi[6];
+    int shf[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      issue_row(F, pcmb, true, i >= 4, i < 4 ? 4 * q + i : 2 * q + (i - 4), m, 0, 0, 0, lo[i], hi[i], shf[i]);
+    uint32_t zero = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rows[i] = finish_row(i >= 4, true, lo[i], hi[i], shf[i], zero);
+    if (zero) errs |= pcm_rows_epb(pcmb, q, 4, 2);
+    return;
+  }
+  if (kind != 2) {
+    errs |= DEC_E_MISSING_MB;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rows[i] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+  const int x0 = m * 16 + (mvx >> 2);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int sy = clampi(4 * g + r + (mvy >> 2), 0, H - 1);
+    if (sy < vy0 || sy >= vy1) {
+      range = 1;
+      rows[r] = make_uint4(0, 0, 0, 0);
+    } else {
+      rows[r] = tb_lds_row(lds + (sy - ly0) * W, x0, W, false);
+    }
+  }
+  const int CH = H >> 1, CW = W >> 1;
+  const int fx = mvx & 7, fy = mvy & 7;
+  const uint8_t *uv = lds + nl * W;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int cy = 2 * g + r + (mvy >> 3);
+    const int ya = clampi(cy, 0, CH - 1), yb = fy ? clampi(cy + 1, 0, CH - 1) : ya;
+    if (ya < vc0 || ya >= vc1 || yb < vc0 || yb >= vc1) {
+      range = 1;
+      rows[4 + r] = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    const uint8_t *ra = uv + (ya - cy0) * W, *rb = uv + (yb - cy0) * W;
+    const int cx = m * 8 + (mvx >> 3);
+    if ((fx | fy) == 0) {
+      rows[4 + r] = tb_lds_row(ra, 2 * cx, W, true);
+    } else {
+      rows[4 + r] = tb_subpel(ra, rb, cx, fx, fy, CW);
+    }
+  }
+}
+
+#ifndef VTS_TB_WAVES
+#define VTS_TB_WAVES 2  // 4 spills (336 B/lane) and measured 1.4x slower
+#endif
+__global__ void __launch_bounds__(kTbThreads) __attribute__((amdgpu_waves_per_eu(VTS_TB_WAVES)))
+h264_recon_score_tb(TbArgs ta) {
+  extern __shared__ uint4 tb_dyn[];
+  __shared__ uint32_t lds_hist[256];
+  __shared__ uint32_t red[kTbThreads / 64];
+  const FusedArgs &fa = ta.f;
+  const ReconArgs &a = fa.r;
+  const int mbw = a.mb_width, mbh = a.mb_height, nmb = mbw * mbh;
+  const int W = mbw * 16, H = mbh * 16, NG = 4 * mbh;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int chain = bid / mbh, band = bid - chain * mbh;
+  const int4 *ch = ta.chains + static_cast<int64_t>(chain) * ta.L;
+  int n = 0;
+  for (int j = 0; j < ta.L; ++j) n += ch[j].x >= 0 ? 1 : 0;  // valid prefix (host-built)
+  const int h0 = (n - 1) * kTbHalo;
+  const int r_lo = max(0, 4 * band - h0), r_hi = min(NG, 4 * band + 4 + h0);
+  const int ly0 = 4 * r_lo, cy0 = 2 * r_lo, nl = 4 * (r_hi - r_lo);
+  uint8_t *lds = reinterpret_cast<uint8_t *>(tb_dyn);
+  const int nb = 4 * mbw;  // band tasks: lanes [0, nb), slot 0, the same at every level
+  const int64_t npx = static_cast<int64_t>(fa.w) * fa.h;
+  const bool band_lane = static_cast<int>(threadIdx.x) < nb;
+  const int bg = 4 * band + static_cast<int>(threadIdx.x) / mbw, bm = static_cast<int>(threadIdx.x) % mbw;
+  uint32_t errs = 0, range = 0;
+  uint32_t prevw = 0;  // this lane's 4 thumbnail luma bytes of the previous level
+  {
+    const int4 f0 = ch[0];
+    if (band_lane && f0.z >= 0)
+      prevw = *reinterpret_cast<const uint32_t *>(fa.thumb + f0.z * npx + static_cast<int64_t>(bg) * fa.w + bm * 4);
+  }
+  // the task of slot s at level jj: band groups first (lanes keep their band
+  // task at every level), then the top and bottom halo groups; and its
+  // command, loaded one level ahead so its latency hides behind a level
+  auto task = [&](int jj, int s, int &g, int &m) {
+    const int h = (n - 1 - jj) * kTbHalo;
+    const int g_lo = max(0, 4 * band - h), g_hi = min(NG, 4 * band + 4 + h);
+    const int ntask = (g_hi - g_lo) * mbw, top = (4 * band - g_lo) * mbw;
+    const int t = static_cast<int>(threadIdx.x) + s * kTbThreads;
+    g = -1;
+    m = 0;
+    if (t < ntask) {
+      if (t < nb) {
+        g = 4 * band + t / mbw;
+        m = t - (t / mbw) * mbw;
+      } else {
+        const int u = t - nb;
+        const int base = u < top ? g_lo : 4 * band + 4 - top / mbw;
+        g = base + u / mbw;
+        m = u - (u / mbw) * mbw;
+      }
+    }
+  };
+  auto command = [&](int jj, int g, int m) -> uint64_t {
+    return g >= 0 ? a.cmd[static_cast<int64_t>(ch[jj].x) * nmb + (g >> 2) * mbw + m] : 0ull;
+  };
+  int ga, ma, gb, mb2;
+  task(0, 0, ga, ma);
+  task(0, 1, gb, mb2);
+  uint64_t ca = command(0, ga, ma), cb = command(0, gb, mb2);
+  if (threadIdx.x < 256) lds_hist[threadIdx.x] = 0;
+  __syncthreads();
+  for (int j = 0; j < n; ++j) {
+    const int4 fr = ch[j];
+    const int h = (n - 1 - j) * kTbHalo, hp = h + kTbHalo;
+    const int p_lo = max(0, 4 * band - hp), p_hi = min(NG, 4 * band + 4 + hp);
+    const bool last = j == n - 1;
+    const FrameRefs F = frame_refs(a, fr.y);
+    const int g0 = ga, m0 = ma, g1 = gb, m1 = mb2;
+    const uint64_t c0 = current_cmd(ca, a.epoch), c1 = current_cmd(cb, a.epoch);
+    if (!last) {  // next level's tasks and commands
+      task(j + 1, 0, ga, ma);
+      task(j + 1, 1, gb, mb2);
+      ca = command(j + 1, ga, ma);
+      cb = command(j + 1, gb, mb2);
+    }
+    auto put = [&](int g, int m, const uint4 (&rows)[6]) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) *reinterpret_cast<uint4 *>(lds + (4 * g + r - ly0) * W + m * 16) = rows[r];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        *reinterpret_cast<uint4 *>(lds + nl * W + (2 * g + r - cy0) * W + m * 16) = rows[4 + r];
+    };
+    static_assert(kTbSlots == 2, "two task slots");
+    uint4 ra[6];
+    if (j == 0) {
+      // level 0: HBM reference / I_PCM samples straight into LDS, both slots'
+      // loads in flight together
+      if (g0 >= 0) tb_group_hbm(F, c0, m0, g0, lds + (4 * g0 - ly0) * W, lds + nl * W + (2 * g0 - cy0) * W, W, errs);
+      __builtin_amdgcn_sched_barrier(0);  // one slot's 12 loads in flight at a time (registers)
+      if (g1 >= 0) tb_group_hbm(F, c1, m1, g1, lds + (4 * g1 - ly0) * W, lds + nl * W + (2 * g1 - cy0) * W, W, errs);
+      if (band_lane) {  // this lane's own band rows (slot 0), back from LDS
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ra[r] = *reinterpret_cast<const uint4 *>(lds + (4 * bg + r - ly0) * W + bm * 16);
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          ra[4 + r] = *reinterpret_cast<const uint4 *>(lds + nl * W + (2 * bg + r - cy0) * W + bm * 16);
+      }
+    } else {
+      // level j >= 1 in place: every lane reads level j-1 into registers,
+      // barrier, then writes level j
+      uint4 rb[6];
+      const int vy0 = 4 * p_lo, vy1 = 4 * p_hi, vc0 = 2 * p_lo, vc1 = 2 * p_hi;
+      if (g0 >= 0) tb_group_lds(lds, ly0, cy0, nl, W, H, vy0, vy1, vc0, vc1, a.es, c0, m0, g0, ra, errs, range);
+      __builtin_amdgcn_sched_barrier(0);
+      if (g1 >= 0) tb_group_lds(lds, ly0, cy0, nl, W, H, vy0, vy1, vc0, vc1, a.es, c1, m1, g1, rb, errs, range);
+      __syncthreads();  // level j-1 fully read before level j overwrites it
+      if (!last) {
+        if (g0 >= 0) put(g0, m0, ra);
+        if (g1 >= 0) put(g1, m1, rb);
+      }
+    }
+    uint32_t sad = 0;
+    const int64_t gframe = fa.frame0 + fr.x;
+    if (band_lane) {
+      const uint4 *yr = ra, *cr = ra + 4;
+      if (ta.keep || last) {
+        uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
+        uint8_t *dst_uv = dst + static_cast<int64_t>(a.pitch) * H;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st_row(dst + static_cast<int64_t>(4 * bg + r) * a.pitch + bm * 16, yr[r]);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) st_row(dst_uv + static_cast<int64_t>(2 * bg + r) * a.pitch + bm * 16, cr[r]);
+      }
+      uint32_t ys[4] = {0, 0, 0, 0}, us[4] = {0, 0, 0, 0}, vs[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) add_luma16<4>(yr[r], ys);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) add_chroma16<4>(cr[r], us, vs);
+      uint32_t rgb24[4], packed = 0;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const uint32_t y = (ys[p] + 8) / 16, u = (us[p] + 2) / 4, v = (vs[p] + 2) / 4;
+        rgb24[p] = bt709_rgb24(y, u, v);
+        packed |= y << (8 * p);
+        atomicAdd(&lds_hist[y], 1u);
+      }
+      const int64_t tpx = static_cast<int64_t>(bg) * fa.w + bm * 4;
+      store_rgb<4>(fa.rgb + (gframe * npx + tpx) * 3, rgb24);
+      *reinterpret_cast<uint32_t *>(fa.thumb + fr.x * npx + tpx) = packed;
+      if (fr.z >= 0) sad = sad_u8(packed, prevw, 0u);
+      prevw = packed;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sad += __shfl_xor(sad, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sad;
+    __syncthreads();  // scoring (histogram, SAD shares) and the level's LDS rows are complete
+    if (threadIdx.x == 0 && fr.z >= 0) {
+      uint64_t t = 0;
+#pragma unroll
+      for (int i = 0; i < kTbThreads / 64; ++i) t += red[i];
+      atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(t));
+    }
+    if (threadIdx.x < 128) {
+      const uint64_t lo = lds_hist[2 * threadIdx.x], hi = lds_hist[2 * threadIdx.x + 1];
+      if (lo | hi)
+        atomicAdd(reinterpret_cast<unsigned long long *>(fa.hist + gframe * 256) + threadIdx.x,
+                  static_cast<unsigned long long>(lo | (hi << 32)));
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) lds_hist[threadIdx.x] = 0;
+  }
+  if (errs | range) atomicOr(a.err, errs | (range ? static_cast<uint32_t>(DEC_W_LEVEL_RANGE) : 0u));
+}
+
 }  // namespace
 
 int clear_accum_launch(uint32_t *hist, uint64_t *sad, int64_t n_frames, hipStream_t s) {
@@ -1224,6 +1549,37 @@ int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s) {
   hipLaunchKernelGGL(thumb_sad, dim3(static_cast<unsigned>(n)), dim3(256), 0, s, t);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "thumb_sad launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
+int tb_lds_bytes(int mb_width, int mb_height, int L) {
+  const int groups = std::min(4 * mb_height, 4 + 2 * (L - 1) * kTbHalo);
+  return groups * 6 * mb_width * 16 + 32;  // + the over-read of a row's second chunk
+}
+
+int tb_max_tasks(int mb_width, int mb_height, int L) {
+  return std::min(4 * mb_height, 4 + 2 * (L - 1) * kTbHalo) * mb_width;
+}
+
+int tb_launch(const TbArgs &a, int n_chains, hipStream_t s) {
+  if (n_chains <= 0) return VTS_OK;
+  const int mbw = a.f.r.mb_width, mbh = a.f.r.mb_height;
+  // shapes the kernel assumes: band tasks in slot 0, all tasks in kTbSlots slots
+  if (4 * mbw > kTbThreads || tb_max_tasks(mbw, mbh, a.L) > kTbThreads * kTbSlots || a.L < 1 || a.L > 16)
+    return fail(VTS_E_INVALID, "h264_recon_score_tb: %dx%d macroblocks, L=%d out of range", mbw, mbh, a.L);
+  const int lds = tb_lds_bytes(mbw, mbh, a.L);
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(h264_recon_score_tb),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score_tb attribute: %s", hipGetErrorString(e));
+    attr_set = true;
+  }
+  if (lds > 150 * 1024) return fail(VTS_E_INVALID, "h264_recon_score_tb: %d bytes of LDS", lds);
+  hipLaunchKernelGGL(h264_recon_score_tb, dim3(static_cast<unsigned>(n_chains) * mbh), dim3(kTbThreads),
+                     static_cast<unsigned>(lds), s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score_tb launch: %s", hipGetErrorString(e));
   return VTS_OK;
 }
 

@@ -74,6 +74,9 @@ enum DecodeError : uint32_t {
   DEC_E_REFLIST = 1u << 10,       // ref_pic_list_modification / weighted pred
   DEC_E_NO_REF = 1u << 11,        // P slice without a preceding reference
   DEC_E_MMCO = 1u << 12,          // adaptive reference marking
+  // not an error: a level-blocked reconstruct launch met a motion vector
+  // reaching beyond its halo; the host re-runs with per-level launches
+  DEC_W_LEVEL_RANGE = 1u << 31,
 };
 std::string describe_decode_error(uint32_t flags);
 

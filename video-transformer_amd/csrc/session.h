@@ -27,6 +27,12 @@ struct Window {
   std::vector<int32_t> chunk_end;  // parse chunk j covers launches [chunk_end[j-1], chunk_end[j])
   int64_t ev0 = 0;                 // first index of this window's events in vts_ctx::lev
   int64_t post_off = 0, post_cnt = 0;  // into post_slots
+  // level-blocked schedule (h264_recon_score_tb), when every GOP of the
+  // window is a plain P chain: launch i covers chains [tb_off[i], + tb_cnt[i])
+  // of tb_L[i] levels each in vts_ctx::tb_chains
+  bool tb = false;
+  std::vector<int64_t> tb_off;
+  std::vector<int32_t> tb_cnt, tb_L;
 };
 
 // Downscaled copy of every decoded frame (transcode.hip), filled by run_all
@@ -66,6 +72,11 @@ struct vts_ctx {
   std::vector<int4> level_frames;
   std::vector<int32_t> post_slots;  // per window: slots whose SAD the thumb_sad pass makes
   std::vector<Window> windows;
+  std::vector<int4> tb_chains;      // level-blocked launches: [chain][L] (slot, ref, sad_prev, 0)
+  std::vector<uint8_t> tb_last;     // per frame: last level of its chain (kept in HBM)
+  int4 *d_tb = nullptr;
+  bool tb_off = false;              // a launch met motion beyond its halo: per-level from now on
+  bool tb_ran_sparse = false;       // the last run kept only chain-last frames
   int64_t ring_frames = 0;
   int n_rings = 1;
   // device

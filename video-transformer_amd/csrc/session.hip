@@ -225,6 +225,18 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   for (Window &w : c->windows) c->ring_frames = std::max(c->ring_frames, w.f1 - w.f0);
   c->n_rings = (c->windows.size() > 1 && c->params.n_streams >= 2) ? 2 : 1;
 
+  // level-blocked reconstruction (h264_recon_score_tb): levels per launch
+  int tb_L_max = 0;
+  c->tb_last.assign(static_cast<size_t>(c->n_frames), 0);
+  // Opt-in (level_block >= 2): correct, but measured slower than one launch
+  // per level on MI355X, so auto (0) stays per-level.
+  if (c->fused && c->k == 4 && c->params.level_block >= 2 && 4 * c->sps.mb_width <= 512) {
+    tb_L_max = std::min(c->params.level_block, 16);
+    const int lds_cap = 150 * 1024;
+    while (tb_L_max >= 2 && (tb_lds_bytes(c->sps.mb_width, c->sps.mb_height, tb_L_max) > lds_cap ||
+                             tb_max_tasks(c->sps.mb_width, c->sps.mb_height, tb_L_max) > 1024))
+      --tb_L_max;
+  }
   // slice slots / ref slots and per-level frame lists
   std::vector<int32_t> launch_of(static_cast<size_t>(c->n_frames), 0);  // launch index within its window
   for (Window &w : c->windows) {
@@ -327,6 +339,46 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
       if (!(x > w.f0 && level[x - 1] < level[x]) || x == w.f1 - 1)
         c->post_slots.push_back(static_cast<int32_t>(x - w.f0));
     w.post_cnt = static_cast<int64_t>(c->post_slots.size()) - w.post_off;
+
+    // Level-blocked schedule: every GOP a plain P chain (frame x at level l
+    // predicted from x - 1 at level l - 1), k = 4 fused scoring, one parse
+    // chunk, all GOPs per launch; L levels per launch while the level-0 halo
+    // rows fit the LDS of two workgroups per CU.
+    if (tb_L_max >= 2 && c->params.gops_per_launch <= 0 && w.chunk_end.size() == 1) {
+      bool chain_ok = true;
+      for (int64_t x = w.f0; x < w.f1 && chain_ok; ++x)
+        chain_ok = intra[x] ? (level[x] == 0) : (ref[x] == x - 1 && x > w.f0 && level[x] == level[x - 1] + 1);
+      if (chain_ok) {
+        w.tb = true;
+        int64_t lmax = 0;
+        for (int64_t x = w.f0; x < w.f1; ++x) lmax = std::max(lmax, level[x]);
+        for (int64_t l0 = 0; l0 <= lmax; l0 += tb_L_max) {
+          const int L = static_cast<int>(std::min<int64_t>(tb_L_max, lmax + 1 - l0));
+          const int64_t off = static_cast<int64_t>(c->tb_chains.size());
+          int32_t cnt = 0;
+          for (size_t g = 0; g < gop_start.size(); ++g) {
+            const int64_t gs = gop_start[g], ge = (g + 1 < gop_start.size()) ? gop_start[g + 1] : w.f1;
+            if (ge - gs <= l0) continue;
+            for (int j = 0; j < L; ++j) {
+              const int64_t x = gs + l0 + j;
+              if (x < ge) {
+                const bool fused_sad = x > w.f0 && level[x - 1] < level[x];
+                c->tb_chains.push_back(make_int4(static_cast<int>(x - w.f0),
+                                                 ref[x] >= 0 ? static_cast<int>(ref[x] - w.f0) : -1,
+                                                 fused_sad ? static_cast<int>(x - 1 - w.f0) : -1, 0));
+                if (x + 1 == ge || j + 1 == L) c->tb_last[static_cast<size_t>(x)] = 1;
+              } else {
+                c->tb_chains.push_back(make_int4(-1, -1, -1, 0));
+              }
+            }
+            ++cnt;
+          }
+          w.tb_off.push_back(off);
+          w.tb_cnt.push_back(cnt);
+          w.tb_L.push_back(L);
+        }
+      }
+    }
   }
 
   // ---- device allocations and uploads
@@ -340,6 +392,10 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   if (!c->post_slots.empty())
     HIP_TRY(hipMemcpy(c->d_post, c->post_slots.data(), sizeof(int32_t) * c->post_slots.size(),
                       hipMemcpyHostToDevice));
+  if (!c->tb_chains.empty()) {
+    HIP_TRY(hipMalloc(&c->d_tb, sizeof(int4) * c->tb_chains.size()));
+    HIP_TRY(hipMemcpy(c->d_tb, c->tb_chains.data(), sizeof(int4) * c->tb_chains.size(), hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMalloc(&c->d_levels, sizeof(int4) * c->level_frames.size()));
   HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(),
                     hipMemcpyHostToDevice));
@@ -412,6 +468,10 @@ int vts::run_all(vts_ctx *c) {
   HIP_TRY(hipStreamWaitEvent(c->s_score, c->ev_start, 0));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
   hipStream_t sd = c->s_dec;
+  // level-blocked launches store every frame only on request (or for the
+  // transcoder, which downscales every frame from the ring)
+  const bool keep = c->params.keep_frames > 0 || c->small.on;
+  c->tb_ran_sparse = false;
   // one window: one stream (nothing to overlap, and HIP event timing of each
   // stage stays on a single queue)
   hipStream_t ss = (c->params.n_streams >= 2 && c->windows.size() > 1) ? c->s_score : c->s_dec;
@@ -487,7 +547,22 @@ int vts::run_all(vts_ctx *c) {
       fa.sad = c->d_sad;
     }
     size_t j = 0;
-    for (size_t l = 0; l < nl; ++l) {
+    const bool tb = c->fused && w.tb && !c->tb_off;
+    if (tb) {
+      // level-blocked launches (one parse chunk: wait for all of it)
+      HIP_TRY(hipStreamWaitEvent(sd, LE[2 * nl], 0));
+      HIP_TRY(hipEventRecord(LE[0], sd));
+      TbArgs ta{};
+      ta.f = fa;
+      ta.keep = keep ? 1 : 0;
+      for (size_t i = 0; i < w.tb_off.size(); ++i) {
+        ta.chains = c->d_tb + w.tb_off[i];
+        ta.L = w.tb_L[i];
+        VTS_TRY(tb_launch(ta, w.tb_cnt[i], sd));
+      }
+      HIP_TRY(hipEventRecord(LE[2 * (nl - 1) + 1], sd));
+    }
+    for (size_t l = 0; l < nl && !tb; ++l) {
       if (l == 0 || static_cast<int32_t>(l) == w.chunk_end[j - 1]) {
         HIP_TRY(hipStreamWaitEvent(sd, LE[2 * nl + j++], 0));  // this launch's slices are parsed
         // reconstruct span starts once its first launch may run (a timing
@@ -578,6 +653,12 @@ int vts::run_all(vts_ctx *c) {
     }
   }
   c->last_window_done = static_cast<int64_t>(nw) - 1;
+  if (err & DEC_W_LEVEL_RANGE) {
+    // motion beyond a level-blocked launch's halo: redo with one launch per level
+    c->tb_off = true;
+    return run_all(c);
+  }
+  for (const Window &w : c->windows) c->tb_ran_sparse |= c->fused && w.tb && !c->tb_off && !keep;
   if (err) {
     c->have_results = false;
     return fail(VTS_E_DECODE, "device decoder: %s", describe_decode_error(err).c_str());
@@ -687,6 +768,11 @@ extern "C" int vts_get_frame_nv12(vts_ctx *c, int64_t frame, uint8_t *out, int64
   for (int64_t wi = first_resident; wi <= c->last_window_done; ++wi) {
     const Window &w = c->windows[static_cast<size_t>(wi)];
     if (frame < w.f0 || frame >= w.f1) continue;
+    if (c->tb_ran_sparse && w.tb && !c->tb_last[static_cast<size_t>(frame)])
+      return fail(VTS_E_INVALID,
+                  "frame %lld was decoded in LDS only (level-blocked launches keep each block's last "
+                  "frame; open with vts_params.keep_frames = 1 or level_block = 1)",
+                  static_cast<long long>(frame));
     const uint8_t *base = c->d_surf[wi % c->n_rings] + (frame - w.f0) * c->frame_stride;
     HIP_TRY(hipMemcpy2D(out, c->width, base, c->pitch, c->width, c->height, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy2D(out + static_cast<int64_t>(c->width) * c->height, c->width,
@@ -728,6 +814,21 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
     case 2: return static_cast<int64_t>(c->slices.size());
     case 3: return c->ring_frames;
     case 4: return c->fused ? 1 : 0;
+    case 5: {  // level-blocked launches (0 when the per-level schedule runs)
+      if (c->tb_off || !c->fused) return 0;
+      int64_t n = 0;
+      for (const Window &w : c->windows) n += w.tb ? static_cast<int64_t>(w.tb_off.size()) : 0;
+      return n;
+    }
+    case 6: {  // chains over all level-blocked launches
+      if (c->tb_off || !c->fused) return 0;
+      int64_t n = 0;
+      for (const Window &w : c->windows)
+        if (w.tb)
+          for (int32_t k : w.tb_cnt) n += k;
+      return n;
+    }
+    case 7: return c->tb_off ? 0 : static_cast<int64_t>(c->tb_chains.size());  // chain slots (levels x chains)
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
   }
 }
@@ -744,6 +845,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_es);
   f(c->d_slices);
   f(c->d_levels);
+  f(c->d_tb);
   f(c->d_post);
   for (int r = 0; r < 2; ++r) {
     f(c->d_cmd[r]);

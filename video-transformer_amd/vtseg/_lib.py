@@ -12,7 +12,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libvtseg.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 VTS_OK = 0
 VTS_E_INVALID = -1
@@ -90,7 +90,8 @@ class ScoreDesc(C.Structure):
 class Params(C.Structure):
     _fields_ = [("k", C.c_int32), ("window_frames", C.c_int32), ("keep_rgb", C.c_int32),
                 ("n_streams", C.c_int32), ("cut_threshold", C.c_float), ("fused", C.c_int32),
-                ("gops_per_launch", C.c_int32), ("parse_chunks", C.c_int32)]
+                ("gops_per_launch", C.c_int32), ("parse_chunks", C.c_int32),
+                ("level_block", C.c_int32), ("keep_frames", C.c_int32)]
 
 
 class SynthParams(C.Structure):

@@ -106,7 +106,8 @@ class VideoScorer:
     def __init__(self, path: str | Path, device: int = 0, *, k: int = 0,
                  window_frames: int = 0, n_streams: int = 2,
                  cut_threshold: float = DEFAULT_CUT_THRESHOLD, fused: int = 0,
-                 gops_per_launch: int = 0, parse_chunks: int = 0):
+                 gops_per_launch: int = 0, parse_chunks: int = 0, level_block: int = 0,
+                 keep_frames: bool = False):
         self._lib = _lib.lib()
         prm = _lib.Params()
         prm.k = k
@@ -117,6 +118,8 @@ class VideoScorer:
         prm.fused = fused
         prm.gops_per_launch = gops_per_launch
         prm.parse_chunks = parse_chunks
+        prm.level_block = level_block
+        prm.keep_frames = 1 if keep_frames else 0
         self._threshold = cut_threshold
         ctx = C.c_void_p()
         _lib.check(self._lib.vts_open(int(device), str(path).encode(), C.byref(prm),
@@ -158,6 +161,12 @@ class VideoScorer:
     def recon_launches(self) -> int:
         """Reconstruct launches per run (one per GOP level per window)."""
         return int(self._lib.vts_schedule_info(self._ctx, 0))
+
+    def level_blocks(self) -> tuple[int, int]:
+        """(launches, chains) of the level-blocked schedule per run; (0, 0)
+        when the per-level schedule runs."""
+        return (int(self._lib.vts_schedule_info(self._ctx, 5)),
+                int(self._lib.vts_schedule_info(self._ctx, 6)))
 
     def fused(self) -> bool:
         """Scoring runs fused into reconstruction (k in {2,4,8}, no crop)."""
