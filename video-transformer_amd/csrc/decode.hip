@@ -1197,38 +1197,6 @@ __device__ __forceinline__ uint4 tb_lds_row(const uint8_t *row, int x0, int W, b
   return finish_row(chroma, false, lo, hi, sh, zero_unused);
 }
 
-// The 6 rows (4 luma, 2 NV12 chroma) of group g of macroblock column m from
-// HBM: the reference picture F or the I_PCM samples (level 0 of a chain),
-// stored straight into the LDS rows (level 0 overwrites nothing it reads).
-__device__ __forceinline__ void tb_group_hbm(const FrameRefs &F, uint64_t c, int m, int g, uint8_t *lds_y,
-                                             uint8_t *lds_uv, int W, uint32_t &errs) {
-  const int mby = g >> 2, q = g & 3;
-  const uint32_t kind = static_cast<uint32_t>(c >> 62);
-  const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
-  if (fast_cmd(F, c)) {
-    const bool pcm = kind == 1;
-    const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
-    uint4 lo[6], hi[6];
-    int shf[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-      issue_row(F, pcmb, pcm, i >= 4, i < 4 ? 4 * q + i : 2 * q + (i - 4), m, mby, mvx, mvy, lo[i], hi[i], shf[i]);
-    uint32_t zero = 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const uint4 v = finish_row(i >= 4, pcm, lo[i], hi[i], shf[i], zero);
-      *reinterpret_cast<uint4 *>((i < 4 ? lds_y + i * W : lds_uv + (i - 4) * W) + m * 16) = v;
-    }
-    if (pcm && zero) errs |= pcm_rows_epb(pcmb, q, 4, 2);
-  } else {
-#pragma unroll 1
-    for (int i = 0; i < 6; ++i) {
-      const uint4 v = fetch_row(F, c, i < 4 ? 4 * q + i : 16 + 2 * q + (i - 4), m, mby, errs);
-      *reinterpret_cast<uint4 *>((i < 4 ? lds_y + i * W : lds_uv + (i - 4) * W) + m * 16) = v;
-    }
-  }
-}
-
 // sub-pel chroma (bilinear eighth-pel) of 8 Cb/Cr pairs from two LDS rows:
 // fetch_row's general path (rolled: rare, kept small).
 __device__ __forceinline__ uint4 tb_subpel(const uint8_t *ra, const uint8_t *rb, int cx, int fx, int fy, int CW) {
@@ -1255,7 +1223,7 @@ __device__ __forceinline__ uint4 tb_subpel(const uint8_t *ra, const uint8_t *rb,
 // sets `range` (the launch's halo is too small for this motion).
 __device__ __forceinline__ void tb_group_lds(const uint8_t *lds, int ly0, int cy0, int nl, int W, int H, int vy0,
                                              int vy1, int vc0, int vc1, const uint8_t *es, uint64_t c, int m,
-                                             int g, uint4 *rows, uint32_t &errs, uint32_t &range) {
+                                             int g, bool has_ref, uint4 *rows, uint32_t &errs, uint32_t &range) {
   const int q = g & 3;
   const uint32_t kind = static_cast<uint32_t>(c >> 62);
   if (kind == 1) {
@@ -1272,8 +1240,8 @@ __device__ __forceinline__ void tb_group_lds(const uint8_t *lds, int ly0, int cy
     if (zero) errs |= pcm_rows_epb(pcmb, q, 4, 2);
     return;
   }
-  if (kind != 2) {
-    errs |= DEC_E_MISSING_MB;
+  if (kind != 2 || !has_ref) {
+    errs |= kind != 2 ? DEC_E_MISSING_MB : DEC_E_NO_REF;
 #pragma unroll
     for (int i = 0; i < 6; ++i) rows[i] = make_uint4(0, 0, 0, 0);
     return;
@@ -1315,7 +1283,13 @@ __device__ __forceinline__ void tb_group_lds(const uint8_t *lds, int ly0, int cy
 #ifndef VTS_TB_WAVES
 #define VTS_TB_WAVES 2  // 4 spills (336 B/lane) and measured 1.4x slower
 #endif
-__global__ void __launch_bounds__(kTbThreads) __attribute__((amdgpu_waves_per_eu(VTS_TB_WAVES)))
+#ifndef VTS_TB1_WAVES
+#define VTS_TB1_WAVES 4
+#endif
+// S = task slots per lane (1: every level's tasks fit 512 lanes, e.g. L <= 2
+// at 720p; 2: up to 1024 tasks)
+template <int S>
+__global__ void __launch_bounds__(kTbThreads) __attribute__((amdgpu_waves_per_eu(S == 1 ? VTS_TB1_WAVES : VTS_TB_WAVES)))
 h264_recon_score_tb(TbArgs ta) {
   extern __shared__ uint4 tb_dyn[];
   __shared__ uint32_t lds_hist[256];
@@ -1329,7 +1303,9 @@ h264_recon_score_tb(TbArgs ta) {
   const int4 *ch = ta.chains + static_cast<int64_t>(chain) * ta.L;
   int n = 0;
   for (int j = 0; j < ta.L; ++j) n += ch[j].x >= 0 ? 1 : 0;  // valid prefix (host-built)
-  const int h0 = (n - 1) * kTbHalo;
+  // LDS region: the band +- n halo groups (level 0's reference rows); level
+  // j is rebuilt in place over the band +- (n-1-j) groups
+  const int h0 = n * kTbHalo;
   const int r_lo = max(0, 4 * band - h0), r_hi = min(NG, 4 * band + 4 + h0);
   const int ly0 = 4 * r_lo, cy0 = 2 * r_lo, nl = 4 * (r_hi - r_lo);
   uint8_t *lds = reinterpret_cast<uint8_t *>(tb_dyn);
@@ -1339,11 +1315,9 @@ h264_recon_score_tb(TbArgs ta) {
   const int bg = 4 * band + static_cast<int>(threadIdx.x) / mbw, bm = static_cast<int>(threadIdx.x) % mbw;
   uint32_t errs = 0, range = 0;
   uint32_t prevw = 0;  // this lane's 4 thumbnail luma bytes of the previous level
-  {
-    const int4 f0 = ch[0];
-    if (band_lane && f0.z >= 0)
-      prevw = *reinterpret_cast<const uint32_t *>(fa.thumb + f0.z * npx + static_cast<int64_t>(bg) * fa.w + bm * 4);
-  }
+  const int4 f0 = ch[0];
+  if (band_lane && f0.z >= 0)
+    prevw = *reinterpret_cast<const uint32_t *>(fa.thumb + f0.z * npx + static_cast<int64_t>(bg) * fa.w + bm * 4);
   // the task of slot s at level jj: band groups first (lanes keep their band
   // task at every level), then the top and bottom halo groups; and its
   // command, loaded one level ahead so its latency hides behind a level
@@ -1354,7 +1328,7 @@ h264_recon_score_tb(TbArgs ta) {
     const int t = static_cast<int>(threadIdx.x) + s * kTbThreads;
     g = -1;
     m = 0;
-    if (t < ntask) {
+    if (s < S && t < ntask) {
       if (t < nb) {
         g = 4 * band + t / mbw;
         m = t - (t / mbw) * mbw;
@@ -1373,14 +1347,37 @@ h264_recon_score_tb(TbArgs ta) {
   task(0, 0, ga, ma);
   task(0, 1, gb, mb2);
   uint64_t ca = command(0, ga, ma), cb = command(0, gb, mb2);
+  // level 0's reference rows, HBM -> LDS, 16 bytes a lane, all in flight
+  if (f0.y >= 0) {
+    const uint8_t *ref = a.surf + static_cast<int64_t>(f0.y) * a.frame_stride;
+    const int cpr = W / 16;                     // chunks per row
+    const int nrows = nl + nl / 2, nchunk = nrows * cpr;
+    constexpr int kPer = 8;
+    for (int i0 = 0; i0 < nchunk; i0 += kPer * kTbThreads) {
+      uint4 v[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        // past the end: reload the last chunk (branch-free, every load in flight)
+        const int i = min(i0 + static_cast<int>(threadIdx.x) + k * kTbThreads, nchunk - 1);
+        const int row = i / cpr, col = i - row * cpr;
+        const int64_t src = row < nl ? static_cast<int64_t>(ly0 + row) * a.pitch
+                                     : static_cast<int64_t>(H + cy0 + (row - nl)) * a.pitch;
+        v[k] = *reinterpret_cast<const uint4 *>(ref + src + col * 16);
+      }
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int i = i0 + static_cast<int>(threadIdx.x) + k * kTbThreads;
+        if (i < nchunk) reinterpret_cast<uint4 *>(lds)[i] = v[k];  // row r at r * W: W = cpr * 16
+      }
+    }
+  }
   if (threadIdx.x < 256) lds_hist[threadIdx.x] = 0;
   __syncthreads();
   for (int j = 0; j < n; ++j) {
     const int4 fr = ch[j];
-    const int h = (n - 1 - j) * kTbHalo, hp = h + kTbHalo;
+    const int hp = (n - j) * kTbHalo;
     const int p_lo = max(0, 4 * band - hp), p_hi = min(NG, 4 * band + 4 + hp);
     const bool last = j == n - 1;
-    const FrameRefs F = frame_refs(a, fr.y);
     const int g0 = ga, m0 = ma, g1 = gb, m1 = mb2;
     const uint64_t c0 = current_cmd(ca, a.epoch), c1 = current_cmd(cb, a.epoch);
     if (!last) {  // next level's tasks and commands
@@ -1396,34 +1393,18 @@ h264_recon_score_tb(TbArgs ta) {
       for (int r = 0; r < 2; ++r)
         *reinterpret_cast<uint4 *>(lds + nl * W + (2 * g + r - cy0) * W + m * 16) = rows[4 + r];
     };
-    static_assert(kTbSlots == 2, "two task slots");
-    uint4 ra[6];
-    if (j == 0) {
-      // level 0: HBM reference / I_PCM samples straight into LDS, both slots'
-      // loads in flight together
-      if (g0 >= 0) tb_group_hbm(F, c0, m0, g0, lds + (4 * g0 - ly0) * W, lds + nl * W + (2 * g0 - cy0) * W, W, errs);
-      __builtin_amdgcn_sched_barrier(0);  // one slot's 12 loads in flight at a time (registers)
-      if (g1 >= 0) tb_group_hbm(F, c1, m1, g1, lds + (4 * g1 - ly0) * W, lds + nl * W + (2 * g1 - cy0) * W, W, errs);
-      if (band_lane) {  // this lane's own band rows (slot 0), back from LDS
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ra[r] = *reinterpret_cast<const uint4 *>(lds + (4 * bg + r - ly0) * W + bm * 16);
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-          ra[4 + r] = *reinterpret_cast<const uint4 *>(lds + nl * W + (2 * bg + r - cy0) * W + bm * 16);
-      }
-    } else {
-      // level j >= 1 in place: every lane reads level j-1 into registers,
-      // barrier, then writes level j
-      uint4 rb[6];
-      const int vy0 = 4 * p_lo, vy1 = 4 * p_hi, vc0 = 2 * p_lo, vc1 = 2 * p_hi;
-      if (g0 >= 0) tb_group_lds(lds, ly0, cy0, nl, W, H, vy0, vy1, vc0, vc1, a.es, c0, m0, g0, ra, errs, range);
-      __builtin_amdgcn_sched_barrier(0);
-      if (g1 >= 0) tb_group_lds(lds, ly0, cy0, nl, W, H, vy0, vy1, vc0, vc1, a.es, c1, m1, g1, rb, errs, range);
+    static_assert(S == 1 || S == kTbSlots, "one or two task slots");
+    // in place: every lane reads level j-1 (the reference rows for j = 0)
+    // into registers, barrier, then writes level j
+    uint4 ra[6], rb[6];
+    const bool has_ref = fr.y >= 0;
+    const int vy0 = 4 * p_lo, vy1 = 4 * p_hi, vc0 = 2 * p_lo, vc1 = 2 * p_hi;
+    if (g0 >= 0) tb_group_lds(lds, ly0, cy0, nl, W, H, vy0, vy1, vc0, vc1, a.es, c0, m0, g0, has_ref, ra, errs, range);
+    if (g1 >= 0) tb_group_lds(lds, ly0, cy0, nl, W, H, vy0, vy1, vc0, vc1, a.es, c1, m1, g1, has_ref, rb, errs, range);
+    if (!last) {
       __syncthreads();  // level j-1 fully read before level j overwrites it
-      if (!last) {
-        if (g0 >= 0) put(g0, m0, ra);
-        if (g1 >= 0) put(g1, m1, rb);
-      }
+      if (g0 >= 0) put(g0, m0, ra);
+      if (g1 >= 0) put(g1, m1, rb);
     }
     uint32_t sad = 0;
     const int64_t gframe = fa.frame0 + fr.x;
@@ -1553,7 +1534,7 @@ int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s) {
 }
 
 int tb_lds_bytes(int mb_width, int mb_height, int L) {
-  const int groups = std::min(4 * mb_height, 4 + 2 * (L - 1) * kTbHalo);
+  const int groups = std::min(4 * mb_height, 4 + 2 * L * kTbHalo);  // level 0's reference rows
   return groups * 6 * mb_width * 16 + 32;  // + the over-read of a row's second chunk
 }
 
@@ -1570,14 +1551,19 @@ int tb_launch(const TbArgs &a, int n_chains, hipStream_t s) {
   const int lds = tb_lds_bytes(mbw, mbh, a.L);
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(h264_recon_score_tb),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score_tb attribute: %s", hipGetErrorString(e));
+    for (const void *k : {reinterpret_cast<const void *>(h264_recon_score_tb<1>),
+                          reinterpret_cast<const void *>(h264_recon_score_tb<2>)}) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score_tb attribute: %s", hipGetErrorString(e));
+    }
     attr_set = true;
   }
   if (lds > 150 * 1024) return fail(VTS_E_INVALID, "h264_recon_score_tb: %d bytes of LDS", lds);
-  hipLaunchKernelGGL(h264_recon_score_tb, dim3(static_cast<unsigned>(n_chains) * mbh), dim3(kTbThreads),
-                     static_cast<unsigned>(lds), s, a);
+  const dim3 grid(static_cast<unsigned>(n_chains) * mbh), block(kTbThreads);
+  if (tb_max_tasks(mbw, mbh, a.L) <= kTbThreads)
+    hipLaunchKernelGGL(h264_recon_score_tb<1>, grid, block, static_cast<unsigned>(lds), s, a);
+  else
+    hipLaunchKernelGGL(h264_recon_score_tb<2>, grid, block, static_cast<unsigned>(lds), s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score_tb launch: %s", hipGetErrorString(e));
   return VTS_OK;
