@@ -475,6 +475,11 @@ def main() -> None:
                 "kernel": kname, "kernel_ms": round(kern_ms, 4),
                 "bytes_per_frame": bytes_per_frame,
                 "frames_per_launch": round(frames_per_launch, 1)}
+        if kname.startswith("h264_recon_score"):
+            # two GOP groups reconstruct concurrently: kernel_ms is
+            # the reconstruct span / launches = the union of the dispatch intervals
+            # per dispatch (tools/kernel_busy.py on a rocprofv3 kernel trace)
+            roof["kernel_ms_basis"] = "HIP-event span of all reconstruct launches / launches"
     roof_decode = None
     if args.workload == "decode_score" and not scorer.fused():
         rec_bytes = 3 * width * height

@@ -25,6 +25,7 @@ struct Window {
   std::vector<int32_t> lvl_cnt;
   std::vector<int64_t> lvl_s0;     // first slice (absolute) of each launch's frames
   std::vector<int32_t> chunk_end;  // parse chunk j covers launches [chunk_end[j-1], chunk_end[j])
+  std::vector<int32_t> grp;        // interleaved GOP groups: first launch of each (empty = one group)
   int64_t ev0 = 0;                 // first index of this window's events in vts_ctx::lev
   int64_t post_off = 0, post_cnt = 0;  // into post_slots
   // level-blocked schedule (h264_recon_score_tb), when every GOP of the
@@ -99,6 +100,12 @@ struct vts_ctx {
   uint8_t *d_thumb[2] = {nullptr, nullptr};  // fused: [slot][h][w] thumbnail luma
   int64_t thumb_px = 0;
   hipStream_t s_dec = nullptr, s_score = nullptr, s_parse = nullptr;
+  // interleaved GOP groups: group g >= 1 reconstructs on s_grp[g - 1] and
+  // signals ev_grp[g - 1] when its last launch is done (Window::grp)
+  static constexpr int kMaxGroups = 4;
+  int recon_groups = 2;  // measured best on MI355X; VTS_RECON_GROUPS overrides
+  hipStream_t s_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> ev;  // per window: dec start, parsed, decoded, score start, scored, spare
   std::vector<hipEvent_t> lev;  // per window: (start, end) per reconstruct launch, then one per parse chunk
   hipEvent_t ev_start = nullptr, ev_end = nullptr;

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -81,6 +82,9 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
 }
 
 int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, const char *path) {
+  // interleaved GOP groups per reconstruct level (VTS_RECON_GROUPS, 1..4)
+  if (const char *s = std::getenv("VTS_RECON_GROUPS"))
+    c->recon_groups = std::max(1, std::min(vts_ctx::kMaxGroups, std::atoi(s)));
   VTS_TRY(fill_video_info(mp4, &c->info));
   const Mp4VideoTrack &t = mp4.video.front();
   if (!(t.codec == "avc1" || t.codec == "avc3"))
@@ -267,9 +271,14 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
     } else if (c->params.gops_per_launch > 0) {
       per = c->params.gops_per_launch;
     } else {
-      per = static_cast<int64_t>(gop_start.size());
+      // interleaved groups: each group's level launches on its own stream
+      const int64_t ng = std::min<int64_t>(c->recon_groups, static_cast<int64_t>(gop_start.size()));
+      per = ng > 1 && c->params.parse_chunks <= 1 ? (static_cast<int64_t>(gop_start.size()) + ng - 1) / ng
+                                                   : static_cast<int64_t>(gop_start.size());
     }
+    const bool grouped = c->fused && c->params.gops_per_launch == 0 && per < static_cast<int64_t>(gop_start.size());
     for (size_t g0 = 0; g0 < gop_start.size(); g0 += static_cast<size_t>(per)) {
+      if (grouped) w.grp.push_back(static_cast<int32_t>(w.lvl_off.size()));
       const size_t g1 = std::min(gop_start.size(), g0 + static_cast<size_t>(per));
       const int64_t a = gop_start[g0];
       const int64_t b = (g1 < gop_start.size()) ? gop_start[g1] : w.f1;
@@ -418,6 +427,10 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&c->s_parse, hipStreamNonBlocking));
+  for (int g = 1; g < c->recon_groups; ++g) {
+    HIP_TRY(hipStreamCreateWithFlags(&c->s_grp[g - 1], hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[g - 1], hipEventDisableTiming));
+  }
   c->ev.resize(c->windows.size() * 6);
   for (auto &e2 : c->ev) HIP_TRY(hipEventCreate(&e2));
   int64_t nlev = 0;
@@ -562,7 +575,32 @@ int vts::run_all(vts_ctx *c) {
       }
       HIP_TRY(hipEventRecord(LE[2 * (nl - 1) + 1], sd));
     }
-    for (size_t l = 0; l < nl && !tb; ++l) {
+    if (!tb && w.grp.size() > 1) {
+      // Interleaved GOP groups (one parse chunk): group g's level launches on
+      // its own stream, so one group's launch tail overlaps the others' work.
+      const int ng = static_cast<int>(w.grp.size());
+      HIP_TRY(hipStreamWaitEvent(sd, LE[2 * nl], 0));
+      HIP_TRY(hipEventRecord(LE[0], sd));
+      for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], LE[0], 0));
+      for (size_t i = 0;; ++i) {
+        bool any = false;
+        for (int g = 0; g < ng; ++g) {
+          const size_t l = static_cast<size_t>(w.grp[g]) + i;
+          const size_t end = g + 1 < ng ? static_cast<size_t>(w.grp[g + 1]) : nl;
+          if (l >= end) continue;
+          any = true;
+          fa.r.frames = c->d_levels + w.lvl_off[l];
+          VTS_TRY(fused_launch(fa, c->k, w.lvl_cnt[l], g == 0 ? sd : c->s_grp[g - 1]));
+        }
+        if (!any) break;
+      }
+      for (int g = 1; g < ng; ++g) {
+        HIP_TRY(hipEventRecord(c->ev_grp[g - 1], c->s_grp[g - 1]));
+        HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[g - 1], 0));
+      }
+      HIP_TRY(hipEventRecord(LE[2 * (nl - 1) + 1], sd));
+    }
+    for (size_t l = 0; l < nl && !tb && w.grp.size() <= 1; ++l) {
       if (l == 0 || static_cast<int32_t>(l) == w.chunk_end[j - 1]) {
         HIP_TRY(hipStreamWaitEvent(sd, LE[2 * nl + j++], 0));  // this launch's slices are parsed
         // reconstruct span starts once its first launch may run (a timing
@@ -839,6 +877,8 @@ extern "C" int vts_close(vts_ctx *c) {
   if (c->s_dec) (void)hipStreamSynchronize(c->s_dec);
   if (c->s_score) (void)hipStreamSynchronize(c->s_score);
   if (c->s_parse) (void)hipStreamSynchronize(c->s_parse);
+  for (hipStream_t g : c->s_grp)
+    if (g) (void)hipStreamSynchronize(g);
   auto f = [](void *p) {
     if (p) (void)hipFree(p);
   };
@@ -870,6 +910,10 @@ extern "C" int vts_close(vts_ctx *c) {
   if (c->s_dec) (void)hipStreamDestroy(c->s_dec);
   if (c->s_score) (void)hipStreamDestroy(c->s_score);
   if (c->s_parse) (void)hipStreamDestroy(c->s_parse);
+  for (int g = 0; g < vts_ctx::kMaxGroups - 1; ++g) {
+    if (c->s_grp[g]) (void)hipStreamDestroy(c->s_grp[g]);
+    if (c->ev_grp[g]) (void)hipEventDestroy(c->ev_grp[g]);
+  }
   delete c;
   return VTS_OK;
 }
