@@ -103,6 +103,7 @@ struct vts_ctx {
   // interleaved GOP groups: group g >= 1 reconstructs on s_grp[g - 1] and
   // signals ev_grp[g - 1] when its last launch is done (Window::grp)
   static constexpr int kMaxGroups = 4;
+  bool group_parse = false;  // one parse chunk per group (VTS_GROUP_PARSE)
   int recon_groups = 2;  // measured best on MI355X; VTS_RECON_GROUPS overrides
   hipStream_t s_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};

@@ -85,6 +85,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   // interleaved GOP groups per reconstruct level (VTS_RECON_GROUPS, 1..4)
   if (const char *s = std::getenv("VTS_RECON_GROUPS"))
     c->recon_groups = std::max(1, std::min(vts_ctx::kMaxGroups, std::atoi(s)));
+  if (const char *s = std::getenv("VTS_GROUP_PARSE")) c->group_parse = std::atoi(s) > 0;
   VTS_TRY(fill_video_info(mp4, &c->info));
   const Mp4VideoTrack &t = mp4.video.front();
   if (!(t.codec == "avc1" || t.codec == "avc3"))
@@ -340,6 +341,13 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
           }
         }
       }
+      // interleaved groups: optionally one parse chunk per group, so group
+      // g's reconstruction starts once its own slices are parsed
+      if (w.grp.size() > 1 && c->group_parse && tb_L_max < 2) {
+        w.chunk_end.clear();
+        for (size_t g = 1; g < w.grp.size(); ++g) w.chunk_end.push_back(w.grp[g]);
+        w.chunk_end.push_back(static_cast<int32_t>(nl));
+      }
     }
     // thumb_sad pass: frames without a fused SAD, plus the window's last
     // frame (its thumbnail seeds the next window)
@@ -579,9 +587,12 @@ int vts::run_all(vts_ctx *c) {
       // Interleaved GOP groups (one parse chunk): group g's level launches on
       // its own stream, so one group's launch tail overlaps the others' work.
       const int ng = static_cast<int>(w.grp.size());
+      // group g waits for its own parse chunk (or the single one)
+      const bool per_grp = w.chunk_end.size() == w.grp.size();
       HIP_TRY(hipStreamWaitEvent(sd, LE[2 * nl], 0));
       HIP_TRY(hipEventRecord(LE[0], sd));
-      for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], LE[0], 0));
+      for (int g = 1; g < ng; ++g)
+        HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], per_grp ? LE[2 * nl + g] : LE[0], 0));
       for (size_t i = 0;; ++i) {
         bool any = false;
         for (int g = 0; g < ng; ++g) {
@@ -685,6 +696,10 @@ int vts::run_all(vts_ctx *c) {
     int32_t l0 = 0;
     for (int32_t l1 : w.chunk_end) {
       float b = 0;
+      if (w.grp.size() > 1) {  // interleaved groups: one span over all launches
+        if (l1 != w.chunk_end.back()) continue;
+        l0 = 0;
+      }
       HIP_TRY(hipEventElapsedTime(&b, LE[2 * l0], LE[2 * (l1 - 1) + 1]));
       c->timings[2] += b;
       l0 = l1;
