@@ -876,6 +876,10 @@ __global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC __attribute__((unused))
 // 21 triples per wave, so no triple crosses a wave).  No LDS partial sums, no
 // LDS atomics except the histogram.  4 waves (4 bands) per workgroup.
 constexpr int kK6bCols = 63;
+constexpr int kK6bPx = kK6bCols * 16 / 6;  // thumbnail pixels per wave segment (168)
+#ifndef VTS_K6B_STAGE
+#define VTS_K6B_STAGE 1  // RGB / thumbnail bytes staged in LDS, stored as dwords
+#endif
 
 // DEC_E_EPB_IN_PCM if an emulation-prevention byte falls in row `rin` of an
 // I_PCM block (a luma row, or the Cb and Cr rows of chroma row rin)
@@ -897,6 +901,9 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
   constexpr int K = 6, HK = 3;
   __shared__ uint32_t lds_hist[256];
   __shared__ uint32_t red[4];
+#if VTS_K6B_STAGE
+  __shared__ __attribute__((aligned(16))) uint8_t stage_rgb[4][3 * kK6bPx], stage_th[4][kK6bPx];
+#endif
   const ReconArgs &a = fa.r;
   const int mbw = a.mb_width, nmb = mbw * a.mb_height;
   const int segs = (mbw + kK6bCols - 1) / kK6bCols;
@@ -1042,9 +1049,15 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
       us[3] += un;
       vs[3] += vn;
     }
+#if VTS_K6B_STAGE
+    // the wave's RGB / thumbnail bytes go through LDS and leave as dwords
+    uint8_t *rgb = stage_rgb[threadIdx.x >> 6] + 3 * (pix0 - kK6bPx * seg);
+    uint8_t *thumb = stage_th[threadIdx.x >> 6] + (pix0 - kK6bPx * seg);
+#else
     const int64_t tpx = static_cast<int64_t>(band) * fa.w + pix0;
     uint8_t *rgb = fa.rgb + (gframe * npx + tpx) * 3;
     uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx;
+#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (i >= nown || pix0 + i >= fa.w) continue;
@@ -1065,6 +1078,20 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
     if (lane == 0) red[threadIdx.x >> 6] = sad;
   }
   __syncthreads();
+#if VTS_K6B_STAGE
+  if (band < fa.h && r0 < F.H) {
+    // this wave's segment: pixels [kK6bPx * seg, + np) of thumbnail row `band`
+    // (w % 8 == 0, so every row and segment starts on a dword)
+    const int np = max(0, min(kK6bPx, fa.w - kK6bPx * seg));
+    const int64_t tpx = static_cast<int64_t>(band) * fa.w + kK6bPx * seg;
+    const uint32_t *srgb = reinterpret_cast<const uint32_t *>(stage_rgb[threadIdx.x >> 6]);
+    const uint32_t *sth = reinterpret_cast<const uint32_t *>(stage_th[threadIdx.x >> 6]);
+    uint32_t *grgb = reinterpret_cast<uint32_t *>(fa.rgb + (gframe * npx + tpx) * 3);
+    uint32_t *gth = reinterpret_cast<uint32_t *>(fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx);
+    for (int d = lane; d < 3 * np / 4; d += 64) grgb[d] = srgb[d];
+    if (lane < np / 4) gth[lane] = sth[lane];
+  }
+#endif
   if (fr.z >= 0 && threadIdx.x == 0) {
     const uint64_t t = uint64_t(red[0]) + red[1] + red[2] + red[3];
     if (t) atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(t));
