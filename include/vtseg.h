@@ -16,6 +16,7 @@
  *   vts_probe_duration     utils/video_utils.py:7-38        probe_duration (ffprobe format=duration)
  *   vts_probe_info         utils/video_utils.py:7-38        (same probe, all stream facts)
  *   vts_extract_segment    utils/video_segmenter.py:86-154  extract_segment (ffmpeg -c copy)
+ *   vts_add_tracks         analyzer/content_analyzer.py:206-209 (audio kept in the upload copy)
  *   vts_boundary_frames*   (no reference code; video_segmenter.py:157-159 snap_to_keyframe
  *                          is the identity stub this feeds)  segment time -> frame index
  *   vts_open/vts_score/... (no reference code; north_star)   decode + NV12 scene scoring
@@ -35,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTS_ABI_VERSION 3
+#define VTS_ABI_VERSION 4
 
 enum {
   VTS_OK = 0,
@@ -179,6 +180,12 @@ int vts_probe_info(const char *path, vts_video_info *info);
  * presentation at `start`, moov before mdat (+faststart).  0 = ok. */
 int vts_extract_segment(const char *in_path, double start, double end,
                         const char *out_path);
+
+/* Every track of video_path plus every non-video track (audio, subtitles,
+ * ...) of src_path, whole and stream-copied, into out_path (moov first).  The
+ * upload transcode keeps the source's audio with it, as the reference keeps
+ * audio (content_analyzer.py:206-209, -c:a aac -b:a 64k; here a stream copy). */
+int vts_add_tracks(const char *video_path, const char *src_path, const char *out_path);
 
 /* ------------------------------------------------- device scoring kernel */
 
@@ -347,7 +354,15 @@ typedef struct vts_synth_params {
                                    pans (half-pel chroma, 8.4.2.2.2 bilinear);
                                    max_motion may then be odd; bit 2: the last
                                    picture (if P) loses the slice holding
-                                   macroblock row 1 (missing macroblocks)     */
+                                   macroblock row 1 (missing macroblocks);
+                                   bit 3: refresh pictures (not scene cuts)
+                                   are non-reference non-IDR I pictures, so
+                                   the next P picture predicts across them  */
+  int32_t chunks;               /* the stream is coded as this many runs of
+                                   frames, each starting with an IDR scene cut,
+                                   on parallel host threads; 0 = one run per
+                                   18 000 frames (10 min at 30 fps)             */
+  int32_t _pad;
 } vts_synth_params;
 
 typedef struct vts_synth_info {

@@ -176,9 +176,16 @@ def _boxes(buf: bytes, start: int, end: int):
 
 def read_mp4(path) -> dict:
     """Minimal independent ISO-BMFF reader (first video track, moov only):
-    sample offsets/sizes/dts, avcC parameter sets, mvhd/mdhd timing."""
+    sample offsets/sizes/dts, avcC parameter sets, mvhd/mdhd timing.  Files
+    above 64 MiB are memory-mapped (``data`` is then a read-only mmap)."""
+    import mmap
     import struct
-    data = Path(path).read_bytes()
+    p = Path(path)
+    if p.stat().st_size > (64 << 20):
+        with open(p, "rb") as f:
+            data = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+    else:
+        data = p.read_bytes()
     top = {t: (a, b) for t, a, b in _boxes(data, 0, len(data))}
     ma, mb = top["moov"]
     out = {"data": data}
@@ -404,3 +411,77 @@ def decode_samples(sps: bytes, pps: bytes, samples: list[bytes], nal_length_size
     if rc != 0:
         raise RuntimeError(f"oracle decode rc={rc} at frame {bad.value}")
     return out
+
+
+def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None) -> dict:
+    """Decode + score a whole MP4 with the scalar oracle, GOP-parallel on
+    `threads` host threads (ctypes releases the GIL): every GOP (run of frames
+    from an IDR access unit) is decoded by or_decode_samples and scored by
+    or_score_frames on its own; the SAD / score of each GOP's first frame is
+    then completed against the previous GOP's last thumbnail luma, exactly as
+    or_score_frames would have over the whole sequence.  With max_frames, only
+    the first GOPs covering that many frames.  Returns hist [F, 256] u32,
+    sad [F] u64, score [F] f32, pts, timescale, the frame count and seconds."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+    m = read_mp4(path)
+    L = lib()
+    prm = H264Params()
+    sps, pps = m["sps"][0], m["pps"][0]
+    nls = m["nal_length_size"]
+    if L.or_parse_sps_pps(sps, len(sps), pps, len(pps), nls, C.byref(prm)):
+        raise RuntimeError("oracle SPS/PPS")
+    W = prm.mb_width * 16 - prm.crop_right
+    H = prm.mb_height * 16 - prm.crop_bottom
+    w, h = W // k, H // k
+    data = np.frombuffer(m["data"], np.uint8)
+    offs = np.asarray(m["offsets"], np.int64)
+    sizes = np.asarray(m["sizes"], np.int64)
+    idr = [i for i in range(len(offs)) if data[offs[i] + nls] & 0x1F == 5]
+    if not idr or idr[0] != 0:
+        raise RuntimeError("stream does not start with an IDR access unit")
+    gops = list(zip(idr, idr[1:] + [len(offs)]))
+    if max_frames is not None:
+        keep = []
+        for a, b in gops:
+            if keep and keep[-1][1] >= max_frames:
+                break
+            keep.append((a, b))
+        gops = keep
+    n = gops[-1][1]
+    hist = np.zeros((n, 256), np.uint32)
+    sad = np.zeros(n, np.uint64)
+    score = np.zeros(n, np.float32)
+    first_luma: list = [None] * len(gops)
+    last_luma: list = [None] * len(gops)
+
+    def work(g):
+        a, b = gops[g]
+        cnt = b - a
+        out = np.empty((cnt, H * 3 // 2, W), np.uint8)
+        bad = C.c_int64(-1)
+        if L.or_decode_samples(C.byref(prm), data.ctypes.data, offs[a:b].ctypes.data,
+                               sizes[a:b].ctypes.data, cnt, out.ctypes.data, C.byref(bad)):
+            raise RuntimeError(f"oracle decode failed in GOP at frame {a}")
+        fr = out.reshape(-1)
+        r = score_frames(fr, W * H * 3 // 2, cnt, W, H, W, H, k, want_rgb=False)
+        hist[a:b] = r["hist"]
+        sad[a:b] = r["sad"]
+        score[a:b] = r["score"]
+        last_luma[g] = r["last_luma"]
+        first_luma[g] = score_frames(fr, W * H * 3 // 2, 1, W, H, W, H, k,
+                                     want_rgb=False)["last_luma"]
+        return cnt
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        frames = sum(ex.map(work, range(len(gops))))
+    for g in range(1, len(gops)):
+        a = gops[g][0]
+        s_ = int(np.abs(first_luma[g].astype(np.int32) - last_luma[g - 1].astype(np.int32)).sum())
+        sad[a] = s_
+        score[a] = np.float32(s_ / (w * h * 255.0))
+    dt = time.perf_counter() - t0
+    return {"hist": hist, "sad": sad, "score": score, "frames": frames, "seconds": dt,
+            "pts": [int(x) for x in m["dts"][:n]], "timescale": int(m["timescale"]),
+            "width": W, "height": H, "gops": len(gops)}

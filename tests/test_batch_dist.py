@@ -25,16 +25,72 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, paths, out_dir):
+def _worker(rank, world, port, paths, out_dir, score=False):
     sys.path[:0] = [str(ROOT / "video-transformer_amd")]
     import torch.distributed as dist
     from vtseg.batch import plan_batch
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    items = plan_batch(paths, CONFIG)
-    (Path(out_dir) / f"r{rank}.txt").write_text(repr([tuple(vars(i).values()) for i in items]))
+    items = plan_batch(paths, CONFIG, score=score, device=0 if score else None)
+    # score_error (the message) stays on the rank that owns the video
+    rows = [tuple(vars(i).values())[:-1] for i in items]
+    (Path(out_dir) / f"r{rank}.txt").write_text(repr(rows))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_two_rank_scoring_failure_still_reaches_the_collectives(tmp_path):
+    """score=True where scoring fails on every rank (no GPU in the CPU
+    suite: VideoScorer raises): each rank must still take part in both
+    all-gathers, so the batch completes with every video flagged."""
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.is_available():
+        pytest.skip("scoring succeeds with a GPU; covered by the gpu variant")
+    from vtseg import scene
+    paths = []
+    for i in range(3):
+        p = tmp_path / f"v{i}.mp4"
+        scene.synth_write(p, width=64, height=48, n_frames=300, seed=i)
+        paths.append(str(p))
+    mp.start_processes(_worker, args=(2, _free_port(), paths, str(tmp_path), True), nprocs=2,
+                       join=True, start_method="spawn")
+    r0 = eval((tmp_path / "r0.txt").read_text())
+    r1 = eval((tmp_path / "r1.txt").read_text())
+    assert r0 == r1
+    assert [t[4] for t in r0] == [-1, -1, -1]          # n_cuts
+    assert [t[9] for t in r0] == [True, True, True]    # score_failed
+    assert all(t[6] == () and t[7] == () for t in r0)  # no boundary arrays
+
+
+@pytest.mark.gpu
+def test_two_rank_scored_batch_on_one_gpu_equals_serial(tmp_path):
+    """The scoring + boundary-exchange path with two processes (gloo, both
+    ranks on GPU 0): every rank ends with the serial run's plan, scene cuts,
+    segment frame ranges and cut times."""
+    import torch
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test requires an MI355X")
+    from vtseg import scene
+    from vtseg.batch import plan_batch
+    paths = []
+    for i in range(3):
+        p = tmp_path / f"v{i}.mp4"
+        scene.synth_write(p, width=320, height=240, n_frames=900 + 300 * i, seed=7 + i,
+                          cut_min_s=2, cut_max_s=6)
+        paths.append(str(p))
+    serial = [tuple(vars(i).values())[:-1] for i in plan_batch(paths, CONFIG, score=True,
+                                                                device=0)]
+    assert all(t[4] > 0 and not t[9] for t in serial)
+    mp.start_processes(_worker, args=(2, _free_port(), paths, str(tmp_path), True), nprocs=2,
+                       join=True, start_method="spawn")
+    r0 = eval((tmp_path / "r0.txt").read_text())
+    r1 = eval((tmp_path / "r1.txt").read_text())
+    assert r0 == r1
+    strip = [t[:5] + t[6:] for t in serial]             # rank differs from the serial run
+    assert [t[:5] + t[6:] for t in r0] == strip
+    assert [t[5] for t in r0] == [0, 1, 0]
 
 
 @pytest.mark.parametrize("n_videos", [5, 2, 1])
@@ -48,6 +104,7 @@ def test_two_rank_batch_equals_serial(tmp_path, n_videos):
         scene.synth_write(p, width=64, height=48, n_frames=300 + 150 * i, seed=i)
         paths.append(str(p))
     serial = [tuple(vars(i).values())[:5] for i in plan_batch(paths, CONFIG)]
+    assert all(not i.score_failed for i in plan_batch(paths, CONFIG))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     mp.start_processes(_worker, args=(2, _free_port(), paths, str(tmp_path)), nprocs=2,
                        join=True, start_method="spawn")
@@ -68,7 +125,7 @@ def _exchange_worker(rank, world, port, out_dir):
                             world_size=world)
     # 3 videos per rank; rank r video j has j+1 segments and (r + 2j) % 4 cuts
     per = 3
-    recs = torch.zeros((world, per, 3), dtype=torch.int64)
+    recs = torch.zeros((world, per, 4), dtype=torch.int64)
     for r in range(world):
         for j in range(per):
             recs[r, j, 0] = j + 1

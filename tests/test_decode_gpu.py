@@ -237,3 +237,36 @@ def test_missing_slice_fails_loudly_even_over_stale_commands(tmp_path):
             for _ in range(2):
                 with pytest.raises(VtsegError, match="not covered by any slice"):
                     v.score()
+
+
+@pytest.mark.parametrize("W,H,k", [(1280, 720, 4), (1920, 1080, 6)], ids=["720p", "1080p"])
+def test_streamed_hd_windows_bit_exact(tmp_path, monkeypatch, W, H, k):
+    """BASELINE configs [2] / [4] in miniature: 720p (h264_recon_score<4>) and
+    1080p (h264_recon_score6b, cropped 1088 -> 1080) decoded in the streamed
+    schedule — many whole-GOP windows over two rings and two HIP streams
+    (decode of window i+1 overlapping scoring of window i), two interleaved GOP
+    groups per window — every histogram, SAD, score, scene cut and the frames
+    still in the ring equal the oracle's over 600 frames."""
+    _require_gpu()
+    n = 600
+    path = tmp_path / f"s{H}.mp4"
+    scene.synth_write(path, width=W, height=H, n_frames=n, max_motion=8, cut_min_s=2,
+                      cut_max_s=8, gop_max_s=2.0, seed=0x5EED + H)
+    ref = oracle.decode_score_gops(path, k, threads=8)
+    monkeypatch.setenv("VTS_RECON_GROUPS", "2")
+    with scene.VideoScorer(path, k=k, window_frames=150, n_streams=2) as v:
+        assert v.fused()
+        assert v.windows() >= 4
+        for _ in range(2):
+            res = v.score()
+            assert np.array_equal(res.hist, ref["hist"])
+            assert np.array_equal(res.sad, ref["sad"])
+            assert np.array_equal(res.scores, ref["score"])
+        assert v.scene_cuts() == np.nonzero(ref["score"] > scene.DEFAULT_CUT_THRESHOLD)[0].tolist()
+        m = oracle.read_mp4(path)
+        nls = m["nal_length_size"]
+        last_idr = max(i for i in range(n) if m["data"][m["offsets"][i] + nls] & 0x1F == 5)
+        samples = [m["data"][o:o + z] for o, z in zip(m["offsets"][last_idr:], m["sizes"][last_idr:])]
+        tail = oracle.decode_samples(m["sps"][0], m["pps"][0], samples, nls)[-3:]
+        for j in range(3):
+            assert np.array_equal(v.frame_nv12(n - 3 + j).reshape(tail[j].shape), tail[j])

@@ -24,13 +24,16 @@ STREAMS = [
     dict(width=640, height=360, slices_per_row=2, max_motion=2),   # 360 = 22.5 MB rows: crop 8
     dict(width=96, height=64, max_motion=0),                       # static: P_Skip runs only
     dict(width=320, height=240, max_motion=5, odd_motion=True),     # half-pel chroma bilinear
+    dict(width=160, height=96, max_motion=4, gop_max_s=0.3, nonref_refresh=True),  # non-ref I
 ]
 
 
 @pytest.mark.parametrize("kw", STREAMS)
 def test_generator_reconstruction_equals_oracle_decode(tmp_path, kw):
     path = tmp_path / "s.mp4"
-    r = scene.synth_write(path, n_frames=120, cut_min_s=0.7, cut_max_s=1.6, gop_max_s=1.0,
+    kw = dict(kw)
+    gop = kw.pop("gop_max_s", 1.0)
+    r = scene.synth_write(path, n_frames=120, cut_min_s=0.7, cut_max_s=1.6, gop_max_s=gop,
                           hash_frames=True, **kw)
     frames, info = oracle.decode_file(path)
     assert frames.shape == (120, kw["height"] * 3 // 2, kw["width"])
@@ -77,6 +80,26 @@ def test_probe_duration_never_raises(tmp_path):
     dummy = tmp_path / "dummy.mp4"
     dummy.write_bytes(b"\x00" * 1024)  # reference tests' zero-byte "videos"
     assert video_utils.probe_duration(dummy) == 0.0
+
+
+def test_probe_duration_falls_back_to_ffprobe_without_a_native_answer(tmp_path, monkeypatch):
+    """An ISO-BMFF file the native parser cannot time (no moov / fragmented)
+    gets ffprobe's answer, as in the reference; a timed file never runs it."""
+    calls = []
+
+    def fake(path):
+        calls.append(str(path))
+        return 12.5
+
+    monkeypatch.setattr(video_utils, "_ffprobe_duration", fake)
+    junk = tmp_path / "frag.mp4"
+    junk.write_bytes(b"\x00\x00\x00\x10ftypisom" + b"\x00" * 64)
+    assert video_utils.probe_duration(junk) == 12.5
+    assert calls == [str(junk)]
+    good = tmp_path / "g.mp4"
+    scene.synth_write(good, width=64, height=48, n_frames=30)
+    assert video_utils.probe_duration(good) == 1.0
+    assert calls == [str(junk)]
 
 
 def test_probe_info_fields(tmp_path):
@@ -127,3 +150,26 @@ def test_synth_rejects_bad_parameters(tmp_path):
         scene.synth_write(tmp_path / "x.mp4", width=15, height=16, n_frames=1)
     with pytest.raises(_lib.VtsegError):
         scene.synth_write(tmp_path / "x.mp4", width=64, height=64, n_frames=1, max_motion=3)
+
+
+@pytest.mark.parametrize("k", [4, 6])
+def test_gop_parallel_oracle_equals_sequential(tmp_path, k):
+    """oracle.decode_score_gops (the bench's parity leg): GOP-parallel decode
+    + score with the GOP-start SADs completed afterwards equals one sequential
+    pass over the whole stream."""
+    path = tmp_path / "g.mp4"
+    W, H = (320, 240) if k == 4 else (480, 270)
+    scene.synth_write(path, width=W, height=H, n_frames=200, cut_min_s=0.5, cut_max_s=2.0,
+                      gop_max_s=0.4, max_motion=6)
+    frames, info = oracle.decode_file(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, 200, W, H, W, H, k,
+                              want_rgb=False)
+    got = oracle.decode_score_gops(path, k, threads=4)
+    assert got["frames"] == 200 and got["gops"] > 10
+    assert np.array_equal(got["hist"], ref["hist"])
+    assert np.array_equal(got["sad"], ref["sad"])
+    assert np.array_equal(got["score"], ref["score"])
+    assert got["pts"] == info["pts"]
+    part = oracle.decode_score_gops(path, k, threads=2, max_frames=50)
+    assert 50 <= part["frames"] < 80
+    assert np.array_equal(part["score"], ref["score"][:part["frames"]])

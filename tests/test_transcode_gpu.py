@@ -133,3 +133,27 @@ def test_compress_video_for_upload_gpu(tmp_path):
     m = oracle.read_mp4(out)
     assert len(m["sizes"]) == 60
     assert upload.compress_video_for_upload(src, max_size_mb=1) == out
+
+
+def test_compress_video_for_upload_keeps_audio(tmp_path):
+    """A source with a sound track: the compressed upload copy carries the new
+    360p video and the source's audio samples unchanged (the reference keeps
+    audio with -c:a aac, content_analyzer.py:206-209)."""
+    _require_gpu()
+    from test_remux import _audio_mp4, _tracks
+    from vtseg import _lib, upload
+    video = tmp_path / "v.mp4"
+    scene.synth_write(video, width=1280, height=720, n_frames=60, gop_max_s=0.5)
+    audio = tmp_path / "a.mp4"
+    samples = _audio_mp4(audio, 90)
+    src = tmp_path / "clip.mp4"
+    _lib.check(_lib.lib().vts_add_tracks(str(video).encode(), str(audio).encode(),
+                                         str(src).encode()))
+    out = upload.compress_video_for_upload(src, max_size_mb=1)
+    assert out == tmp_path / "compressed_clip.mp4"
+    got = _tracks(out)
+    assert [h for h, _ in got] == [b"vide", b"soun"]
+    assert got[1][1] == samples
+    m = oracle.read_mp4(out)
+    assert len(m["sizes"]) == 60
+    assert not list(tmp_path.glob("*.tmp"))

@@ -68,6 +68,12 @@ int64_t mvhd_duration_us(const Mp4Info &info);
 std::string mp4_remux_segment(const char *in_path, double start, double end,
                               const char *out_path);
 
+// Every track of video_path plus every non-video track of src_path (audio,
+// subtitles ...), whole and stream-copied, into out_path (moov first).  The
+// upload transcode keeps the source's audio this way (content_analyzer.py:
+// 206-209 keeps it with -c:a aac).  "" = ok, else the reason.
+std::string mp4_add_tracks(const char *video_path, const char *src_path, const char *out_path);
+
 // Streaming MP4 writer: ftyp, mdat (64-bit size), moov at the end.
 class Mp4Writer {
  public:

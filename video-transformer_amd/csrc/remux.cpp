@@ -68,6 +68,7 @@ void put_matrix(std::vector<uint8_t> &v) {
 
 struct Cut {
   const Mp4VideoTrack *t = nullptr;
+  int src = 0;                          // input file the samples come from
   int64_t first = 0, last = -1;         // decode-order sample range [first, last]
   std::vector<int64_t> delta;           // per kept sample
   int64_t media_time = 0;               // edit list, track timescale
@@ -284,25 +285,11 @@ std::vector<uint8_t> build_moov(std::vector<Cut> &cuts) {
 
 }  // namespace
 
-std::string mp4_remux_segment(const char *in_path, double start, double end,
-                              const char *out_path) {
-  if (!(end - start > 0)) return "empty time range";
-  Mp4Info mp4;
-  std::string e = mp4_parse_file(in_path, &mp4);
-  if (!e.empty()) return e;
-  if (mp4.fragmented) return "fragmented MP4 is not supported";
-  if (mp4.video.empty()) return "no video track";
-  std::vector<Cut> cuts;
-  for (const Mp4VideoTrack &t : mp4.tracks) {
-    Cut c;
-    e = plan_cut(t, start, end, &c);
-    if (!e.empty()) {
-      if (t.track_id == mp4.video.front().track_id) return e;  // the video track must cut
-      continue;  // a secondary track with nothing in range is dropped
-    }
-    cuts.push_back(std::move(c));
-  }
-  if (cuts.empty()) return "nothing to copy";
+namespace {
+
+// ftyp, moov, mdat of `cuts` (samples read from srcs[cut.src]) into out_path.
+std::string write_cuts(std::vector<Cut> &cuts, const char *const *srcs, int n_src,
+                       const char *out_path) {
   std::vector<uint8_t> ftyp;
   {
     BoxW b(ftyp, "ftyp");
@@ -328,11 +315,17 @@ std::string mp4_remux_segment(const char *in_path, double start, double end,
   const std::vector<uint8_t> moov = build_moov(cuts);
   if (moov.size() != moov_size) return "internal: moov size changed";
 
-  const int in = ::open(in_path, O_RDONLY | O_CLOEXEC);
-  if (in < 0) return std::string("cannot open ") + in_path;
+  std::vector<int> in(static_cast<size_t>(n_src), -1);
+  for (int k = 0; k < n_src; ++k) {
+    in[k] = ::open(srcs[k], O_RDONLY | O_CLOEXEC);
+    if (in[k] < 0) {
+      for (int j = 0; j < k; ++j) ::close(in[j]);
+      return std::string("cannot open ") + srcs[k];
+    }
+  }
   FILE *out = std::fopen(out_path, "wb");
   if (!out) {
-    ::close(in);
+    for (int fd : in) ::close(fd);
     return std::string("cannot create ") + out_path;
   }
   bool ok = std::fwrite(ftyp.data(), 1, ftyp.size(), out) == ftyp.size() &&
@@ -349,19 +342,71 @@ std::string mp4_remux_segment(const char *in_path, double start, double end,
       buf.resize(n);
       size_t got = 0;
       while (got < n) {
-        const ssize_t r = ::pread(in, buf.data() + got, n - got, c.t->offset[i] + static_cast<int64_t>(got));
+        const ssize_t r = ::pread(in[c.src], buf.data() + got, n - got,
+                                  c.t->offset[i] + static_cast<int64_t>(got));
         if (r <= 0) break;
         got += static_cast<size_t>(r);
       }
       ok = (got == n) && std::fwrite(buf.data(), 1, n, out) == n;
     }
-  ::close(in);
+  for (int fd : in) ::close(fd);
   if (std::fclose(out) != 0) ok = false;
   if (!ok) {
     std::remove(out_path);
     return "I/O error while copying samples";
   }
   return "";
+}
+
+}  // namespace
+
+std::string mp4_add_tracks(const char *video_path, const char *src_path, const char *out_path) {
+  Mp4Info a, b;
+  std::string e = mp4_parse_file(video_path, &a);
+  if (!e.empty()) return e;
+  e = mp4_parse_file(src_path, &b);
+  if (!e.empty()) return e;
+  if (a.fragmented || b.fragmented) return "fragmented MP4 is not supported";
+  const double inf = 1e300;  // finite: ceil_ticks saturates it (frexp of inf is not a number)
+  std::vector<Cut> cuts;
+  for (const Mp4VideoTrack &t : a.tracks) {
+    Cut c;
+    e = plan_cut(t, 0.0, inf, &c);
+    if (!e.empty()) return e;
+    cuts.push_back(std::move(c));
+  }
+  for (const Mp4VideoTrack &t : b.tracks) {
+    if (t.handler == 0x76696465u) continue;  // 'vide': the new video replaces it
+    Cut c;
+    if (!plan_cut(t, 0.0, inf, &c).empty()) continue;  // an empty track is dropped
+    c.src = 1;
+    cuts.push_back(std::move(c));
+  }
+  const char *srcs[2] = {video_path, src_path};
+  return write_cuts(cuts, srcs, 2, out_path);
+}
+
+std::string mp4_remux_segment(const char *in_path, double start, double end,
+                              const char *out_path) {
+  if (!(end - start > 0)) return "empty time range";
+  Mp4Info mp4;
+  std::string e = mp4_parse_file(in_path, &mp4);
+  if (!e.empty()) return e;
+  if (mp4.fragmented) return "fragmented MP4 is not supported";
+  if (mp4.video.empty()) return "no video track";
+  std::vector<Cut> cuts;
+  for (const Mp4VideoTrack &t : mp4.tracks) {
+    Cut c;
+    e = plan_cut(t, start, end, &c);
+    if (!e.empty()) {
+      if (t.track_id == mp4.video.front().track_id) return e;  // the video track must cut
+      continue;  // a secondary track with nothing in range is dropped
+    }
+    cuts.push_back(std::move(c));
+  }
+  if (cuts.empty()) return "nothing to copy";
+  const char *srcs[1] = {in_path};
+  return write_cuts(cuts, srcs, 1, out_path);
 }
 
 }  // namespace vts
@@ -371,6 +416,14 @@ extern "C" int vts_extract_segment(const char *in_path, double start, double end
   vts::clear_error();
   if (!in_path || !out_path) return vts::fail(VTS_E_INVALID, "NULL path");
   const std::string e = vts::mp4_remux_segment(in_path, start, end, out_path);
+  if (!e.empty()) return vts::fail(VTS_E_FORMAT, "%s", e.c_str());
+  return VTS_OK;
+}
+
+extern "C" int vts_add_tracks(const char *video_path, const char *src_path, const char *out_path) {
+  vts::clear_error();
+  if (!video_path || !src_path || !out_path) return vts::fail(VTS_E_INVALID, "NULL path");
+  const std::string e = vts::mp4_add_tracks(video_path, src_path, out_path);
   if (!e.empty()) return vts::fail(VTS_E_FORMAT, "%s", e.c_str());
   return VTS_OK;
 }

@@ -191,6 +191,18 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
     }
     if (is_ref[f]) last_ref = f;
   }
+  // clean[x]: an intra picture no later picture predicts across (a P picture
+  // after a non-reference I picture refers to the reference before it).
+  // Windows and interleaved GOP groups start only at clean pictures, so no
+  // reference crosses a window or a group that reconstructs on another stream.
+  std::vector<uint8_t> clean(c->n_frames, 0);
+  {
+    int64_t min_ref = c->n_frames;  // min ref[y] over y >= x (n_frames: none)
+    for (int64_t x = c->n_frames - 1; x >= 0; --x) {
+      if (ref[x] >= 0) min_ref = std::min(min_ref, ref[x]);
+      clean[x] = intra[x] && min_ref >= x;
+    }
+  }
 
   // windows of whole intra-started groups.  Device bytes per window frame:
   // surface + MB commands + thumbnail + scoring workspace share; the rings
@@ -211,7 +223,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   else if (c->n_frames * per_frame <= std::min(kSingleWindowBytes, avail / 2)) cap = c->n_frames;
   else cap = std::max<int64_t>(1, ring_budget / per_frame);
   auto next_intra = [&](int64_t x) {
-    while (x < c->n_frames && !intra[x]) ++x;
+    while (x < c->n_frames && !clean[x]) ++x;
     return x;
   };
   for (int64_t f = 0; f < c->n_frames;) {
@@ -265,7 +277,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
     // profiles/r01_gop_group_sweep.txt.
     std::vector<int64_t> gop_start;
     for (int64_t x = w.f0; x < w.f1; ++x)
-      if (intra[x] || x == w.f0) gop_start.push_back(x);
+      if (clean[x] || x == w.f0) gop_start.push_back(x);
     int64_t per;
     if (c->params.gops_per_launch < 0) {
       per = static_cast<int64_t>(gop_start.size());
@@ -591,8 +603,13 @@ int vts::run_all(vts_ctx *c) {
       const bool per_grp = w.chunk_end.size() == w.grp.size();
       HIP_TRY(hipStreamWaitEvent(sd, LE[2 * nl], 0));
       HIP_TRY(hipEventRecord(LE[0], sd));
-      for (int g = 1; g < ng; ++g)
-        HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], per_grp ? LE[2 * nl + g] : LE[0], 0));
+      // LE[0] follows clear_accum on sd (this window's histograms / SADs are
+      // zeroed before any group adds to them); with per-group parse chunks a
+      // group also waits for its own chunk
+      for (int g = 1; g < ng; ++g) {
+        HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], LE[0], 0));
+        if (per_grp) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], LE[2 * nl + g], 0));
+      }
       for (size_t i = 0;; ++i) {
         bool any = false;
         for (int g = 0; g < ng; ++g) {

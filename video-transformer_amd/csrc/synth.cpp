@@ -13,9 +13,12 @@
 //     and an IDR refresh at least every gop_max seconds.
 // The encoder keeps its own reconstruction (the exact decoder output), which
 // is what a refresh IDR re-encodes and what `vts_synth_info` hashes.
+#include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bitstream.h"
@@ -162,40 +165,40 @@ struct MvPred {
 
 inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// Motion compensation of one 16x16 MB with an integer-pel luma MV (quarter-pel
-// units, multiple of 4) and 1/8-pel chroma (8.4.2.2.2), edge-clamped.
-void mc_mb(const Picture &ref, Picture &dst, int mbx, int mby, int mvx, int mvy) {
-  const int x0 = mbx * 16, y0 = mby * 16;
+// Motion compensation of the whole picture with one motion vector (quarter-pel
+// units, integer-pel luma: a multiple of 4) and 1/8-pel chroma (8.4.2.2.2),
+// edge-clamped: every macroblock of a P picture predicts with the frame's pan.
+void mc_frame(const Picture &ref, Picture &dst, int mvx, int mvy) {
   const int ix = mvx >> 2, iy = mvy >> 2;
   const int cw = ref.w / 2, ch = ref.h / 2;
-  const int cx0 = mbx * 8, cy0 = mby * 8;
   const int fx = mvx & 7, fy = mvy & 7, cix = mvx >> 3, ciy = mvy >> 3;
-  if (x0 + ix >= 0 && x0 + ix + 16 <= ref.w && y0 + iy >= 0 && y0 + iy + 16 <= ref.h &&
-      fx == 0 && fy == 0) {  // fully inside, integer chroma: plain copies
-    for (int yy = 0; yy < 16; ++yy)
-      std::memcpy(&dst.y[size_t(y0 + yy) * dst.w + x0],
-                  &ref.y[size_t(y0 + yy + iy) * ref.w + x0 + ix], 16);
-    for (int yy = 0; yy < 8; ++yy) {
-      std::memcpy(&dst.u[size_t(cy0 + yy) * cw + cx0], &ref.u[size_t(cy0 + yy + ciy) * cw + cx0 + cix], 8);
-      std::memcpy(&dst.v[size_t(cy0 + yy) * cw + cx0], &ref.v[size_t(cy0 + yy + ciy) * cw + cx0 + cix], 8);
+  auto row = [](const uint8_t *s, uint8_t *d, int w, int dx) {
+    // d[x] = s[clamp(x + dx, 0, w - 1)]
+    const int a = std::min(w, std::max(0, -dx)), b = std::max(a, std::min(w, w - dx));
+    std::memset(d, s[0], static_cast<size_t>(a));
+    if (b > a) std::memcpy(d + a, s + a + dx, static_cast<size_t>(b - a));
+    std::memset(d + b, s[w - 1], static_cast<size_t>(w - b));
+  };
+  for (int y = 0; y < ref.h; ++y)
+    row(&ref.y[size_t(clampi(y + iy, 0, ref.h - 1)) * ref.w], &dst.y[size_t(y) * dst.w], ref.w, ix);
+  if (fx == 0 && fy == 0) {
+    for (int y = 0; y < ch; ++y) {
+      const size_t sr = size_t(clampi(y + ciy, 0, ch - 1)) * cw;
+      row(&ref.u[sr], &dst.u[size_t(y) * cw], cw, cix);
+      row(&ref.v[sr], &dst.v[size_t(y) * cw], cw, cix);
     }
     return;
   }
-  for (int yy = 0; yy < 16; ++yy)
-    for (int xx = 0; xx < 16; ++xx) {
-      const int sx = clampi(x0 + xx + ix, 0, ref.w - 1), sy = clampi(y0 + yy + iy, 0, ref.h - 1);
-      dst.y[size_t(y0 + yy) * dst.w + x0 + xx] = ref.y[size_t(sy) * ref.w + sx];
-    }
-  for (int yy = 0; yy < 8; ++yy)
-    for (int xx = 0; xx < 8; ++xx) {
-      const int xa = clampi(cx0 + xx + cix, 0, cw - 1), xb = clampi(cx0 + xx + cix + 1, 0, cw - 1);
-      const int ya = clampi(cy0 + yy + ciy, 0, ch - 1), yb = clampi(cy0 + yy + ciy + 1, 0, ch - 1);
+  for (int yy = 0; yy < ch; ++yy)
+    for (int xx = 0; xx < cw; ++xx) {
+      const int xa = clampi(xx + cix, 0, cw - 1), xb = clampi(xx + cix + 1, 0, cw - 1);
+      const int ya = clampi(yy + ciy, 0, ch - 1), yb = clampi(yy + ciy + 1, 0, ch - 1);
       for (int pl = 0; pl < 2; ++pl) {
         const std::vector<uint8_t> &s = pl ? ref.v : ref.u;
         std::vector<uint8_t> &d = pl ? dst.v : dst.u;
         const int A = s[size_t(ya) * cw + xa], B = s[size_t(ya) * cw + xb];
         const int C = s[size_t(yb) * cw + xa], D = s[size_t(yb) * cw + xb];
-        d[size_t(cy0 + yy) * cw + cx0 + xx] = static_cast<uint8_t>(
+        d[size_t(yy) * cw + xx] = static_cast<uint8_t>(
             ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6);
       }
     }
@@ -314,32 +317,31 @@ void make_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level,
 
 using namespace vts;
 
-extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
-                               vts_synth_info *info, int64_t *cut_frames, int64_t cap) {
-  clear_error();
-  if (!path || !prm) return fail(VTS_E_INVALID, "NULL argument");
-  const vts_synth_params &P = *prm;
-  if (P.width < 16 || P.height < 16 || (P.width & 1) || (P.height & 1) ||
-      P.width > 8192 || P.height > 8192)
-    return fail(VTS_E_INVALID, "bad size %dx%d", P.width, P.height);
-  if (P.fps_num <= 0 || P.fps_den <= 0 || P.n_frames <= 0)
-    return fail(VTS_E_INVALID, "bad frame rate or frame count");
+namespace vts {
+namespace {
+
+// One independently coded run of frames [f0, f0 + nf) of the stream: it starts
+// with an IDR (a scene cut unless f0 == 0), so chunks concatenate into one
+// valid stream.  Samples stay in memory until the MP4 is written.
+struct Chunk {
+  int64_t f0 = 0, nf = 0;
+  uint64_t seed = 0;
+  int idr_id_base = 0;        // idr_pic_ids 2k, 2k+1: consecutive IDRs across chunks differ
+  std::vector<uint8_t> data;  // samples, back to back
+  std::vector<uint32_t> size;
+  std::vector<uint8_t> sync;
+  std::vector<int64_t> cuts;  // global frame indices
+  int64_t n_idr = 0;
+  uint64_t recon_hash = 0;
+};
+
+void encode_chunk(const vts_synth_params &P, Chunk *ck) {
   const bool odd_pans = (P.edge_cases & 2) != 0;
-  if (P.max_motion < 0 || ((P.max_motion & 1) && !odd_pans) || P.max_motion > 64)
-    return fail(VTS_E_INVALID, "max_motion must be even, 0..64 (odd needs edge_cases bit 1)");
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int cw = mbw * 16, ch = mbh * 16;
   const double fps = double(P.fps_num) / P.fps_den;
-  const int level = h264_pick_level(mbw * mbh, mbw * mbh * fps);
-  std::vector<uint8_t> sps, pps;
-  make_sps_pps(mbw, mbh, cw - P.width, ch - P.height, level, &sps, &pps);
-
-  Mp4Writer mw;
-  std::string e = mw.open(path);
-  if (!e.empty()) return fail(VTS_E_IO, "%s", e.c_str());
-
-  Pcg32 rng(P.seed);
-  Pcg32 tex_rng(P.seed ^ 0x9e3779b97f4a7c15ull, 0x7e47);
+  Pcg32 rng(ck->seed);
+  Pcg32 tex_rng(ck->seed ^ 0x9e3779b97f4a7c15ull, 0x7e47);
   Picture cur, ref;
   cur.alloc(cw, ch);
   ref.alloc(cw, ch);
@@ -350,21 +352,23 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
     return std::max<int64_t>(1, static_cast<int64_t>(std::llround((lo + (hi - lo) * rng.uniform()) * fps)));
   };
   int64_t next_cut = scene_len();
-  int64_t since_idr = 0, n_idr = 0, n_cuts = 0;
-  uint64_t recon_hash = 0;
-  int frame_num = 0, idr_pic_id = 0;
+  int64_t since_idr = 0;
+  int frame_num = 0, idr_pic_id = ck->idr_id_base;
+  // edge case bit 3: refresh pictures (not scene cuts) are written as
+  // non-reference, non-IDR I pictures; the P picture after one predicts from
+  // the reference picture before it
+  const bool nonref_refresh = (P.edge_cases & 8) != 0;
+  bool prev_was_ref = true;
   int vx = 0, vy = 0;  // luma pixels per frame (even unless odd_pans)
   const int spr = P.slices_per_row;
   const int slice_mbs = spr > 0 ? (mbw + spr - 1) / spr : mbw * mbh;
   std::vector<uint8_t> sample;
 
-  for (int64_t f = 0; f < P.n_frames; ++f) {
+  for (int64_t f = 0; f < ck->nf; ++f) {
+    const int64_t gf = ck->f0 + f;  // frame index in the whole stream
     const bool cut = (f == 0) || (f == next_cut);
-    if (f == next_cut) {
-      next_cut = f + scene_len();
-      if (cut_frames && n_cuts < cap) cut_frames[n_cuts] = f;
-      ++n_cuts;
-    }
+    if (f == next_cut) next_cut = f + scene_len();
+    if (cut && gf > 0) ck->cuts.push_back(gf);
     if (f % P.fps_num == 0 || cut) {  // new velocity about once a second
       if (odd_pans) {
         const int m = P.max_motion;
@@ -378,16 +382,19 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
       if (rng.below(4) == 0) vx = vy = 0;  // static stretches -> P_Skip runs
     }
     const bool idr = cut || since_idr >= gop_max;
-    std::swap(cur, ref);  // ref = previous reconstruction
+    const bool nonref_i = idr && !cut && nonref_refresh;
+    if (prev_was_ref) std::swap(cur, ref);  // ref = the latest reference reconstruction
     if (cut) {
       fill_texture(cur, tex_rng, (P.edge_cases & 1) != 0);
-    } else if (idr) {
-      for (int my = 0; my < mbh; ++my)
-        for (int mx = 0; mx < mbw; ++mx) mc_mb(ref, cur, mx, my, 4 * vx, 4 * vy);
+    } else {
+      // refresh IDR: the panned previous picture re-coded as I_PCM; P picture:
+      // every macroblock predicts with the frame's pan (sparkles overwrite
+      // theirs below)
+      mc_frame(ref, cur, 4 * vx, 4 * vy);
     }
     sample.clear();
     if (idr) {
-      frame_num = 0;
+      frame_num = nonref_i ? (frame_num + 1) & 0xffff : 0;
       for (int first = 0; first < mbw * mbh;) {
         const int row_end = (spr > 0) ? ((first / mbw) + 1) * mbw : mbw * mbh;
         const int last = std::min(first + slice_mbs, row_end);
@@ -396,9 +403,11 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
         bw.ue(7);                             // slice_type: I (all slices)
         bw.ue(0);                             // pic_parameter_set_id
         bw.u(16, static_cast<uint32_t>(frame_num));
-        bw.ue(static_cast<uint32_t>(idr_pic_id));
-        bw.u(1, 0);                           // no_output_of_prior_pics_flag
-        bw.u(1, 0);                           // long_term_reference_flag
+        if (!nonref_i) {
+          bw.ue(static_cast<uint32_t>(idr_pic_id));
+          bw.u(1, 0);                         // no_output_of_prior_pics_flag
+          bw.u(1, 0);                         // long_term_reference_flag
+        }                                     // (nal_ref_idc 0: no dec_ref_pic_marking)
         bw.se(0);                             // slice_qp_delta
         bw.ue(1);                             // disable_deblocking_filter_idc
         for (int a = first; a < last; ++a) {
@@ -407,14 +416,17 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
           mbinfo[size_t(a)] = MbInfo{true, 0, 0};
         }
         bw.trailing();
-        append_nal(sample, 0x65, bw.data());  // nal_ref_idc 3, IDR
+        append_nal(sample, nonref_i ? 0x01 : 0x65, bw.data());  // non-ref non-IDR / nal_ref_idc 3 IDR
         first = last;
       }
-      idr_pic_id ^= 1;
+      if (!nonref_i) {
+        idr_pic_id ^= 1;
+        ++ck->n_idr;
+      }
       since_idr = 1;
-      ++n_idr;
     } else {
-      frame_num = (frame_num + 1) & 0xffff;
+      // a non-reference picture does not advance frame_num (7.4.3)
+      if (prev_was_ref) frame_num = (frame_num + 1) & 0xffff;
       // decide macroblocks, reconstruct, then write slices
       for (int first = 0; first < mbw * mbh;) {
         const int row_end = (spr > 0) ? ((first / mbw) + 1) * mbw : mbw * mbh;
@@ -458,14 +470,13 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
             bw.se(mvy - py);
             bw.ue(0);  // coded_block_pattern 0 (inter mapping codeNum 0)
           }
-          mc_mb(ref, cur, mx, my, mvx, mvy);
-          mbinfo[size_t(a)] = MbInfo{false, mvx, mvy};
+          mbinfo[size_t(a)] = MbInfo{false, mvx, mvy};  // samples: mc_frame above
         }
         if (skip_run) bw.ue(skip_run);
         bw.trailing();
         // edge case bit 2: the last picture loses the slice holding macroblock
         // row 1 (a decoder must report the macroblocks as missing)
-        const bool drop = (P.edge_cases & 4) && f == P.n_frames - 1 && first <= mbw && mbw < last;
+        const bool drop = (P.edge_cases & 4) && gf == P.n_frames - 1 && first <= mbw && mbw < last;
         if (!drop) append_nal(sample, 0x41, bw.data());  // nal_ref_idc 2, non-IDR
         first = last;
       }
@@ -483,10 +494,81 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
           h += uint64_t(cur.v[size_t(yy) * (cw / 2) + xx]) * ((j % 65521) + 1);
           ++j;
         }
-      recon_hash += h * uint64_t(f + 1);
+      ck->recon_hash += h * uint64_t(gf + 1);
     }
-    e = mw.add_sample(sample.data(), sample.size(), idr);
-    if (!e.empty()) return fail(VTS_E_IO, "%s", e.c_str());
+    prev_was_ref = !nonref_i;
+    ck->data.insert(ck->data.end(), sample.begin(), sample.end());
+    ck->size.push_back(static_cast<uint32_t>(sample.size()));
+    ck->sync.push_back(idr && !nonref_i ? 1 : 0);
+  }
+}
+
+}  // namespace
+}  // namespace vts
+
+extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
+                               vts_synth_info *info, int64_t *cut_frames, int64_t cap) {
+  clear_error();
+  if (!path || !prm) return fail(VTS_E_INVALID, "NULL argument");
+  const vts_synth_params &P = *prm;
+  if (P.width < 16 || P.height < 16 || (P.width & 1) || (P.height & 1) ||
+      P.width > 8192 || P.height > 8192)
+    return fail(VTS_E_INVALID, "bad size %dx%d", P.width, P.height);
+  if (P.fps_num <= 0 || P.fps_den <= 0 || P.n_frames <= 0)
+    return fail(VTS_E_INVALID, "bad frame rate or frame count");
+  const bool odd_pans = (P.edge_cases & 2) != 0;
+  if (P.max_motion < 0 || ((P.max_motion & 1) && !odd_pans) || P.max_motion > 64)
+    return fail(VTS_E_INVALID, "max_motion must be even, 0..64 (odd needs edge_cases bit 1)");
+  const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
+  const int cw = mbw * 16, ch = mbh * 16;
+  const double fps = double(P.fps_num) / P.fps_den;
+  const int level = h264_pick_level(mbw * mbh, mbw * mbh * fps);
+  std::vector<uint8_t> sps, pps;
+  make_sps_pps(mbw, mbh, cw - P.width, ch - P.height, level, &sps, &pps);
+
+  Mp4Writer mw;
+  std::string e = mw.open(path);
+  if (!e.empty()) return fail(VTS_E_IO, "%s", e.c_str());
+
+  // Chunks of frames coded independently on host threads (auto: one per 18 000
+  // frames, i.e. 10 min at 30 fps), then written in order.
+  int64_t n_chunks = P.chunks > 0 ? P.chunks : (P.n_frames + 17999) / 18000;
+  n_chunks = std::max<int64_t>(1, std::min<int64_t>(n_chunks, std::min<int64_t>(P.n_frames, 16384)));
+  std::vector<Chunk> chunks(static_cast<size_t>(n_chunks));
+  for (int64_t k = 0; k < n_chunks; ++k) {
+    Chunk &c = chunks[static_cast<size_t>(k)];
+    c.f0 = P.n_frames * k / n_chunks;
+    c.nf = P.n_frames * (k + 1) / n_chunks - c.f0;
+    c.seed = P.seed + static_cast<uint64_t>(k) * 0xd1b54a32d192ed03ull;
+    c.idr_id_base = static_cast<int>(2 * k);
+  }
+  {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int64_t nthreads = std::min<int64_t>(n_chunks, std::min<unsigned>(hw, 16u));
+    std::atomic<int64_t> next{0};
+    auto worker = [&]() {
+      for (int64_t k; (k = next.fetch_add(1)) < n_chunks;) encode_chunk(P, &chunks[static_cast<size_t>(k)]);
+    };
+    std::vector<std::thread> pool;
+    for (int64_t t = 1; t < nthreads; ++t) pool.emplace_back(worker);
+    worker();
+    for (std::thread &t : pool) t.join();
+  }
+  int64_t n_idr = 0, n_cuts = 0;
+  uint64_t recon_hash = 0;
+  for (const Chunk &c : chunks) {
+    size_t pos = 0;
+    for (size_t i = 0; i < c.size.size(); ++i) {
+      e = mw.add_sample(c.data.data() + pos, c.size[i], c.sync[i] != 0);
+      if (!e.empty()) return fail(VTS_E_IO, "%s", e.c_str());
+      pos += c.size[i];
+    }
+    for (int64_t cf : c.cuts) {
+      if (cut_frames && n_cuts < cap) cut_frames[n_cuts] = cf;
+      ++n_cuts;
+    }
+    n_idr += c.n_idr;
+    recon_hash += c.recon_hash;
   }
   const int64_t ts = int64_t(P.fps_num) * 1000;
   e = mw.finish(P.width, P.height, ts, int64_t(P.fps_den) * 1000, sps, pps);

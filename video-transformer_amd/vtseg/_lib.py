@@ -12,7 +12,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libvtseg.so"
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 VTS_OK = 0
 VTS_E_INVALID = -1
@@ -100,7 +100,7 @@ class SynthParams(C.Structure):
                 ("cut_min_s", C.c_double), ("cut_max_s", C.c_double),
                 ("gop_max_s", C.c_double), ("max_motion", C.c_int32),
                 ("slices_per_row", C.c_int32), ("hash_frames", C.c_int32),
-                ("edge_cases", C.c_int32)]
+                ("edge_cases", C.c_int32), ("chunks", C.c_int32), ("_pad", C.c_int32)]
 
 
 class SynthInfo(C.Structure):
@@ -141,6 +141,7 @@ SIGNATURES: dict[str, tuple] = {
                                    _P(C.c_int64)]),
     "vts_probe_info": (C.c_int, [C.c_char_p, _P(VideoInfo)]),
     "vts_extract_segment": (C.c_int, [C.c_char_p, C.c_double, C.c_double, C.c_char_p]),
+    "vts_add_tracks": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p]),
     "vts_score_workspace_bytes": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int64]),
     "vts_score_nv12_dev": (C.c_int, [_P(ScoreDesc), C.c_void_p]),
     "vts_open": (C.c_int, [C.c_int, C.c_char_p, _P(Params), _P(C.c_void_p)]),

@@ -21,7 +21,7 @@ from .budget_planner import plan_segments_with_budget
 from .video_segmenter import plan_segments
 from .video_utils import probe_duration
 
-REC = 3  # int64 fields per video: n_segments, n_cuts, duration_us
+REC = 4  # int64 fields per video: n_segments, n_cuts, duration_us, scoring failed (0/1)
 
 
 @dataclass(frozen=True)
@@ -37,6 +37,11 @@ class BatchItem:
     segment_frames: tuple[tuple[int, int], ...] = ()
     cut_frames: tuple[int, ...] = ()
     cut_times: tuple[float, ...] = ()
+    # scene scoring of this video failed on its rank (e.g. a stream outside
+    # the device decoder's subset); n_cuts is -1 and the arrays are empty.
+    # score_error holds the message on the rank that owns the video only.
+    score_failed: bool = False
+    score_error: str | None = None
 
 
 def _segments(duration: float, config: dict, current_api_count: int):
@@ -64,21 +69,31 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
     seg_frames: list[list[int]] = [[] for _ in range(per)]
     cut_frames: list[list[int]] = [[] for _ in range(per)]
     cut_times: list[list[float]] = [[] for _ in range(per)]
+    errors: dict[int, str] = {}
     for j, i in enumerate(range(rank, n, world)):
         p = str(paths[i])
         duration = probe_duration(p)
         segs = _segments(duration, config, current_api_count)
         n_cuts = -1
         if score:
-            from .scene import VideoScorer
-            with VideoScorer(p, device=torch.cuda.current_device() if device is None else device) as v:
-                res = v.score()
-                cuts = v.scene_cuts()
+            # A failure on one video must not keep this rank from the
+            # collectives below (the other ranks would wait forever): record
+            # it in the video's record and carry on.
+            try:
+                from .scene import VideoScorer
+                dev_id = torch.cuda.current_device() if device is None else device
+                with VideoScorer(p, device=dev_id) as v:
+                    res = v.score()
+                    cuts = v.scene_cuts()
+                    times = [t for sg in segs for t in (sg.start, sg.end)]
+                    sf = v.boundary_frames(times) if times else []
                 n_cuts = len(cuts)
-                times = [t for sg in segs for t in (sg.start, sg.end)]
-                seg_frames[j] = v.boundary_frames(times) if times else []
+                seg_frames[j] = sf
                 cut_frames[j] = list(cuts)
                 cut_times[j] = [float(res.pts[c]) / res.timescale for c in cuts]
+            except Exception as exc:  # noqa: BLE001 - reported per video
+                errors[i] = f"{type(exc).__name__}: {exc}"
+                local[j, 3] = 1
         local[j, 0] = len(segs)
         local[j, 1] = n_cuts
         local[j, 2] = round(duration * 1_000_000)
@@ -94,6 +109,7 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
             extra = {"segment_frames": sf, "cut_frames": cf, "cut_times": ct}
         items.append(BatchItem(index=i, path=str(paths[i]), duration=int(g[r, j, 2]) / 1e6,
                                n_segments=int(g[r, j, 0]), n_cuts=int(g[r, j, 1]), rank=r,
+                               score_failed=bool(g[r, j, 3]), score_error=errors.get(i),
                                **extra))
     return items
 
@@ -102,7 +118,7 @@ def exchange_boundaries(records, seg_frames, cut_frames, cut_times, *, group=Non
                         device=None):
     """Second all-gather of the batch: per-video boundary arrays.
 
-    records: the gathered [world, per, 3] int64 (n_segments, n_cuts, ...) of
+    records: the gathered [world, per, REC] int64 (n_segments, n_cuts, ...) of
     the first exchange, identical on every rank, so every rank pads to the
     same widths.  seg_frames[j] (2 per segment), cut_frames[j], cut_times[j]:
     this rank's j-th video.  Returns [world][per] of (segment_frames pairs,
@@ -133,6 +149,9 @@ def exchange_boundaries(records, seg_frames, cut_frames, cut_times, *, group=Non
         row_r = []
         for j in range(per):
             ns, nc = int(records[r, j, 0]), int(ncut[r, j])
+            if records.shape[2] > 3 and int(records[r, j, 3]):
+                row_r.append(((), (), ()))  # scoring failed: no boundary arrays
+                continue
             vals = gi[r, j].tolist()
             row_r.append((tuple((vals[2 * s], vals[2 * s + 1]) for s in range(ns)),
                           tuple(vals[2 * ns:2 * ns + nc]), tuple(gf[r, j, :nc].tolist())))

@@ -162,6 +162,11 @@ class VideoScorer:
         """Reconstruct launches per run (one per GOP level per window)."""
         return int(self._lib.vts_schedule_info(self._ctx, 0))
 
+    def windows(self) -> int:
+        """Decode windows per run (1 = the whole video at once; more = the
+        streamed two-ring schedule)."""
+        return int(self._lib.vts_schedule_info(self._ctx, 1))
+
     def level_blocks(self) -> tuple[int, int]:
         """(launches, chains) of the level-blocked schedule per run; (0, 0)
         when the per-level schedule runs."""
@@ -253,7 +258,8 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 cut_min_s: float = 2.0, cut_max_s: float = 20.0, gop_max_s: float = 2.0,
                 max_motion: int = 4, slices_per_row: int = 1,
                 hash_frames: bool = False, pcm_zero_runs: bool = False,
-                odd_motion: bool = False, drop_last_slice: bool = False) -> dict:
+                odd_motion: bool = False, drop_last_slice: bool = False,
+                nonref_refresh: bool = False, chunks: int = 0) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
     and the ground-truth scene-cut frames."""
     p = _lib.SynthParams()
@@ -263,7 +269,8 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     p.max_motion, p.slices_per_row = max_motion, slices_per_row
     p.hash_frames = 1 if hash_frames else 0
     p.edge_cases = (1 if pcm_zero_runs else 0) | (2 if odd_motion else 0) | \
-        (4 if drop_last_slice else 0)
+        (4 if drop_last_slice else 0) | (8 if nonref_refresh else 0)
+    p.chunks = chunks
     info = _lib.SynthInfo()
     cuts = (C.c_int64 * max(n_frames, 1))()
     _lib.check(_lib.lib().vts_synth_write(str(path).encode(), C.byref(p), C.byref(info),

@@ -9,8 +9,10 @@ is missing, fails or times out.  Here the pixel work runs on the MI355X
 downscale to scale=-2:360, device H.264 encode).  Streams
 outside the device decoder's subset, or a GPU failure, take the reference's
 own ffmpeg command when ffmpeg exists, and otherwise the reference's
-fallback: the original path.  The output carries video only (the synthetic
-inputs have no audio track; with ffmpeg the reference's AAC audio is kept).
+fallback: the original path.  The source's audio (every non-video track)
+is stream-copied into the output (``vts_add_tracks``): the reference
+re-encodes it to AAC 64k, here it keeps its original coding (no AAC encoder in
+the image), so the uploaded file still has the sound track.
 """
 from __future__ import annotations
 
@@ -66,13 +68,21 @@ def compress_video_for_upload(video_path: Path, *, logger: logging.Logger | None
     if out.exists() and out.stat().st_size > 0:
         log.info(f"found existing compressed file {out.name}, skipping compression")
         return out
+    video_only = out.with_name(out.name + ".video.tmp")
     try:
+        from . import _lib
         from .scene import VideoScorer
         with VideoScorer(video_path, device=device) as v:
-            facts = v.transcode(out)
+            facts = v.transcode(video_only)
+        # the source's audio / other tracks, stream-copied beside the new video
+        _lib.check(_lib.lib().vts_add_tracks(str(video_only).encode(),
+                                             str(video_path).encode(), str(out).encode()))
+        video_only.unlink()
+        facts["bytes_written"] = out.stat().st_size
     except (VtsegError, VtsegLibraryError, OSError) as exc:
-        if out.exists():
-            out.unlink()
+        for p in (out, video_only):
+            if p.exists():
+                p.unlink()
         log.warning(f"GPU transcode unavailable ({exc}); using ffmpeg")
         if shutil.which("ffmpeg") is None:
             log.warning("ffmpeg not installed; skipping compression")

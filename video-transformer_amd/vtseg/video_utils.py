@@ -5,8 +5,11 @@
 ``-show_entries format=duration`` on such files:
 ``av_rescale(mvhd.duration, 1_000_000, mvhd.timescale) / 1e6``.  For any other
 container it keeps the reference behaviour exactly: run ffprobe with the
-reference's arguments and 15 s timeout.  Like the reference it never raises
-and returns 0.0 on any failure (video_utils.py:28-38).
+reference's arguments and 15 s timeout.  Where the native parser has no
+answer for an ISO-BMFF file (fragmented MP4, no ``mvhd``, a parse error, a
+zero duration) it also falls back to that ffprobe command, so such files get
+ffprobe's value as in the reference.  Like the reference it never raises and
+returns 0.0 on any failure (video_utils.py:28-38).
 """
 from __future__ import annotations
 
@@ -49,4 +52,7 @@ def probe_duration(video_path: str | Path) -> float:
         return _ffprobe_duration(path)
     seconds = C.c_double(0.0)
     _lib.lib().vts_probe_duration(str(path).encode(), C.byref(seconds))
-    return float(seconds.value)
+    if seconds.value > 0.0:
+        return float(seconds.value)
+    # no native answer (the reason is in vts_last_error()): ffprobe decides
+    return _ffprobe_duration(path)
