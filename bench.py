@@ -383,7 +383,12 @@ def main() -> None:
     w, h = width // k, height // k
     stride = width * height * 3 // 2
 
-    from vtseg import scene  # libvtseg.so: the writer touches no GPU state
+    # torch first: libvtseg.so must bind to the HIP runtime torch loads (loading
+    # libvtseg first hides the device from it); importing torch initialises
+    # no GPU, nor does the stream writer below
+    import torch
+    import torch.distributed as dist
+    from vtseg import scene
 
     # ------------------------------------------------ input video (host only)
     tmpdir = tempfile.mkdtemp(prefix="vtseg_bench_")
@@ -412,9 +417,6 @@ def main() -> None:
         prof = profile_passes(child_argv, pdir,
                               Path(args.profile_dir) if args.profile_dir else None)
         shutil.rmtree(pdir, ignore_errors=True)
-
-    import torch
-    import torch.distributed as dist
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
