@@ -362,7 +362,17 @@ typedef struct vts_synth_params {
                                    frames, each starting with an IDR scene cut,
                                    on parallel host threads; 0 = one run per
                                    18 000 frames (10 min at 30 fps)             */
-  int32_t _pad;
+  int32_t coding;               /* 0: the I_PCM / P_Skip subset above;
+                                   1: full CAVLC syntax, decoded by the general
+                                   device decoder: Intra_4x4 / Intra_16x16 /
+                                   chroma intra modes, I_PCM, residual blocks
+                                   (all coeff_token / level / run codes), P
+                                   partitions 16x16 .. 4x4 with quarter-sample
+                                   motion, up to 3 reference frames (list
+                                   modification, non-reference pictures), QP
+                                   changes, the deblocking filter on (idc 0/2,
+                                   offsets); bit 4 of edge_cases then turns on
+                                   constrained_intra_pred                     */
 } vts_synth_params;
 
 typedef struct vts_synth_info {

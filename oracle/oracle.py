@@ -8,6 +8,8 @@ cpu_baseline leg may import this module.  The product never does.
     boundary_frames                    exact rational pts/timescale >= t (Fraction)
     score_frames                       DESIGN.md §Scoring, scalar C
     decode_file                        DESIGN.md §Decoder subset, scalar C
+    decode_full                        ITU-T H.264 CAVLC I/P decoding, scalar C
+                                       (h264_full_oracle.c)
     transcode / downscale_nv12         DESIGN.md §11 upload transcode, scalar C
                                        (transcode_oracle.c)
 """
@@ -485,3 +487,48 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None)
     return {"hist": hist, "sad": sad, "score": score, "frames": frames, "seconds": dt,
             "pts": [int(x) for x in m["dts"][:n]], "timescale": int(m["timescale"]),
             "width": W, "height": H, "gops": len(gops)}
+
+
+def decode_full(path, flags: int = 0, max_frames: int | None = None):
+    """fo_decode (h264_full_oracle.c) over an MP4's first video track: the
+    general CAVLC I/P decoder (intra, residual, quarter-sample motion,
+    deblocking).  flags bit 0 skips the deblocking filter.  Returns (frames
+    uint8 [F, H*3/2, W] display-size NV12, info dict)."""
+    m = read_mp4(path)
+    L = lib()
+    L.fo_decode.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, C.c_int, C.c_void_p,
+                            C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
+                            C.c_char_p]
+    L.fo_dims.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_void_p]
+    sps, pps = m["sps"][0], m["pps"][0]
+    w, h = C.c_int(0), C.c_int(0)
+    if L.fo_dims(sps, len(sps), C.byref(w), C.byref(h)):
+        raise RuntimeError("oracle SPS")
+    W, H = w.value, h.value
+    n = len(m["sizes"]) if max_frames is None else min(max_frames, len(m["sizes"]))
+    out = np.zeros((n, H * 3 // 2, W), np.uint8)
+    offs = np.asarray(m["offsets"][:n], np.int64)
+    sizes = np.asarray(m["sizes"][:n], np.int64)
+    data = np.frombuffer(m["data"], np.uint8)
+    bad = C.c_int64(-1)
+    err = C.create_string_buffer(256)
+    rc = L.fo_decode(sps, len(sps), pps, len(pps), m["nal_length_size"], data.ctypes.data,
+                     offs.ctypes.data, sizes.ctypes.data, n, flags, out.ctypes.data,
+                     C.byref(bad), err)
+    if rc != 0:
+        raise RuntimeError(f"oracle decode_full rc={rc} at frame {bad.value}: "
+                           f"{err.value.decode(errors='replace')}")
+    info = {"width": W, "height": H, "timescale": m["timescale"], "pts": m["dts"][:n]}
+    return out, info
+
+
+def table_code(table: int, a: int, b: int, c: int = 0) -> str | None:
+    """The standard's VLC bit strings kept by h264_full_oracle.c: table 0
+    coeff_token [column][TotalCoeff][TrailingOnes], 1 total_zeros 4x4
+    [TotalCoeff-1][total_zeros], 2 total_zeros chroma DC, 3 run_before
+    [min(zerosLeft,7)-1][run]."""
+    L = lib()
+    L.fo_table_code.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int]
+    L.fo_table_code.restype = C.c_char_p
+    v = L.fo_table_code(table, a, b, c)
+    return None if v is None else v.decode()

@@ -24,27 +24,10 @@
 #include "bitstream.h"
 #include "common.h"
 #include "mp4.h"
+#include "synth.h"
 
 namespace vts {
 namespace {
-
-struct Pcg32 {  // PCG-XSH-RR 64/32
-  uint64_t state, inc;
-  explicit Pcg32(uint64_t seed, uint64_t seq = 0x5eedull) : state(0), inc((seq << 1) | 1) {
-    next();
-    state += seed;
-    next();
-  }
-  uint32_t next() {
-    const uint64_t old = state;
-    state = old * 6364136223846793005ull + inc;
-    const uint32_t xs = static_cast<uint32_t>(((old >> 18) ^ old) >> 27);
-    const uint32_t rot = static_cast<uint32_t>(old >> 59);
-    return (xs >> rot) | (xs << ((32 - rot) & 31));
-  }
-  uint32_t below(uint32_t n) { return n ? next() % n : 0; }
-  double uniform() { return next() / 4294967296.0; }
-};
 
 inline uint8_t clamp_sample(int v) {  // I_PCM samples kept >= 1 (no 00 00 in PCM data)
   return static_cast<uint8_t>(v < 1 ? 1 : (v > 255 ? 255 : v));
@@ -233,6 +216,8 @@ void fill_sparkle(Picture &p, int mbx, int mby, Pcg32 &rng) {
     }
 }
 
+}  // namespace
+
 void append_nal(std::vector<uint8_t> &sample, uint8_t header, std::vector<uint8_t> &rbsp) {
   std::vector<uint8_t> nal;
   nal.reserve(rbsp.size() + rbsp.size() / 64 + 8);
@@ -245,9 +230,6 @@ void append_nal(std::vector<uint8_t> &sample, uint8_t header, std::vector<uint8_
   sample.push_back(uint8_t(n));
   sample.insert(sample.end(), nal.begin(), nal.end());
 }
-
-
-}  // namespace
 
 // Smallest level whose MaxFS / MaxMBPS (Table A-1) admit the stream.
 int h264_pick_level(int mbs, double mbps) {
@@ -320,22 +302,7 @@ using namespace vts;
 namespace vts {
 namespace {
 
-// One independently coded run of frames [f0, f0 + nf) of the stream: it starts
-// with an IDR (a scene cut unless f0 == 0), so chunks concatenate into one
-// valid stream.  Samples stay in memory until the MP4 is written.
-struct Chunk {
-  int64_t f0 = 0, nf = 0;
-  uint64_t seed = 0;
-  int idr_id_base = 0;        // idr_pic_ids 2k, 2k+1: consecutive IDRs across chunks differ
-  std::vector<uint8_t> data;  // samples, back to back
-  std::vector<uint32_t> size;
-  std::vector<uint8_t> sync;
-  std::vector<int64_t> cuts;  // global frame indices
-  int64_t n_idr = 0;
-  uint64_t recon_hash = 0;
-};
-
-void encode_chunk(const vts_synth_params &P, Chunk *ck) {
+void encode_chunk(const vts_synth_params &P, SynthChunk *ck) {
   const bool odd_pans = (P.edge_cases & 2) != 0;
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int cw = mbw * 16, ch = mbh * 16;
@@ -517,14 +484,16 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
   if (P.fps_num <= 0 || P.fps_den <= 0 || P.n_frames <= 0)
     return fail(VTS_E_INVALID, "bad frame rate or frame count");
   const bool odd_pans = (P.edge_cases & 2) != 0;
-  if (P.max_motion < 0 || ((P.max_motion & 1) && !odd_pans) || P.max_motion > 64)
+  if (P.coding != 0 && P.coding != 1) return fail(VTS_E_INVALID, "coding must be 0 or 1");
+  if (P.max_motion < 0 || ((P.max_motion & 1) && !odd_pans && P.coding == 0) || P.max_motion > 64)
     return fail(VTS_E_INVALID, "max_motion must be even, 0..64 (odd needs edge_cases bit 1)");
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int cw = mbw * 16, ch = mbh * 16;
   const double fps = double(P.fps_num) / P.fps_den;
   const int level = h264_pick_level(mbw * mbh, mbw * mbh * fps);
   std::vector<uint8_t> sps, pps;
-  make_sps_pps(mbw, mbh, cw - P.width, ch - P.height, level, &sps, &pps);
+  if (P.coding == 1) make_sps_pps_full(P, level, &sps, &pps);
+  else make_sps_pps(mbw, mbh, cw - P.width, ch - P.height, level, &sps, &pps);
 
   Mp4Writer mw;
   std::string e = mw.open(path);
@@ -534,9 +503,9 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
   // frames, i.e. 10 min at 30 fps), then written in order.
   int64_t n_chunks = P.chunks > 0 ? P.chunks : (P.n_frames + 17999) / 18000;
   n_chunks = std::max<int64_t>(1, std::min<int64_t>(n_chunks, std::min<int64_t>(P.n_frames, 16384)));
-  std::vector<Chunk> chunks(static_cast<size_t>(n_chunks));
+  std::vector<SynthChunk> chunks(static_cast<size_t>(n_chunks));
   for (int64_t k = 0; k < n_chunks; ++k) {
-    Chunk &c = chunks[static_cast<size_t>(k)];
+    SynthChunk &c = chunks[static_cast<size_t>(k)];
     c.f0 = P.n_frames * k / n_chunks;
     c.nf = P.n_frames * (k + 1) / n_chunks - c.f0;
     c.seed = P.seed + static_cast<uint64_t>(k) * 0xd1b54a32d192ed03ull;
@@ -547,7 +516,11 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
     const int64_t nthreads = std::min<int64_t>(n_chunks, std::min<unsigned>(hw, 16u));
     std::atomic<int64_t> next{0};
     auto worker = [&]() {
-      for (int64_t k; (k = next.fetch_add(1)) < n_chunks;) encode_chunk(P, &chunks[static_cast<size_t>(k)]);
+      for (int64_t k; (k = next.fetch_add(1)) < n_chunks;) {
+        SynthChunk *ck = &chunks[static_cast<size_t>(k)];
+        if (P.coding == 1) encode_chunk_full(P, ck);
+        else encode_chunk(P, ck);
+      }
     };
     std::vector<std::thread> pool;
     for (int64_t t = 1; t < nthreads; ++t) pool.emplace_back(worker);
@@ -556,7 +529,9 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
   }
   int64_t n_idr = 0, n_cuts = 0;
   uint64_t recon_hash = 0;
-  for (const Chunk &c : chunks) {
+  for (const SynthChunk &c : chunks)
+    if (!c.error.empty()) return fail(VTS_E_INVALID, "%s", c.error.c_str());
+  for (const SynthChunk &c : chunks) {
     size_t pos = 0;
     for (size_t i = 0; i < c.size.size(); ++i) {
       e = mw.add_sample(c.data.data() + pos, c.size[i], c.sync[i] != 0);

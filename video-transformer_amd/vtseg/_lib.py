@@ -100,7 +100,7 @@ class SynthParams(C.Structure):
                 ("cut_min_s", C.c_double), ("cut_max_s", C.c_double),
                 ("gop_max_s", C.c_double), ("max_motion", C.c_int32),
                 ("slices_per_row", C.c_int32), ("hash_frames", C.c_int32),
-                ("edge_cases", C.c_int32), ("chunks", C.c_int32), ("_pad", C.c_int32)]
+                ("edge_cases", C.c_int32), ("chunks", C.c_int32), ("coding", C.c_int32)]
 
 
 class SynthInfo(C.Structure):

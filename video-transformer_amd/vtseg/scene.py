@@ -259,7 +259,8 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 max_motion: int = 4, slices_per_row: int = 1,
                 hash_frames: bool = False, pcm_zero_runs: bool = False,
                 odd_motion: bool = False, drop_last_slice: bool = False,
-                nonref_refresh: bool = False, chunks: int = 0) -> dict:
+                nonref_refresh: bool = False, chunks: int = 0, coding: str = "subset",
+                constrained_intra: bool = False) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
     and the ground-truth scene-cut frames."""
     p = _lib.SynthParams()
@@ -271,6 +272,9 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     p.edge_cases = (1 if pcm_zero_runs else 0) | (2 if odd_motion else 0) | \
         (4 if drop_last_slice else 0) | (8 if nonref_refresh else 0)
     p.chunks = chunks
+    p.coding = {"subset": 0, "full": 1}[coding]
+    if constrained_intra:
+        p.edge_cases |= 16
     info = _lib.SynthInfo()
     cuts = (C.c_int64 * max(n_frames, 1))()
     _lib.check(_lib.lib().vts_synth_write(str(path).encode(), C.byref(p), C.byref(info),
