@@ -1231,6 +1231,9 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
     if (d->mb[addr].slice >= 0) return fo_fail(d, FO_E_FORMAT, "macroblock decoded twice");
     d->mb[addr].slice = slice_no;
     int rc = decode_mb(&c, &b, addr, is_p, &qp, &h);
+    if (getenv("FO_TRACE"))
+      fprintf(stderr, "oracle mb %d type %d cbp %d qp %d bits %lld\n", addr, d->mb[addr].type, d->mb[addr].cbp, qp,
+              (long long)fb_index(&b, 0));
     if (rc) return rc;
     if (b.err) return fo_fail(d, FO_E_FORMAT, "bitstream exhausted");
     addr++;
@@ -1430,6 +1433,7 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
   if (cbp >> 4) {
     for (int pl = 0; pl < 2; pl++) {
       int tc = residual_block(b, -1, 0, 3, 4, lvl);
+      if (getenv("FO_TRACE")) fprintf(stderr, "  chroma dc %d tc %d bits %lld\n", pl, tc, (long long)fb_index(b, 0));
       if (tc < 0) return fo_fail(d, FO_E_FORMAT, "ChromaDCLevel");
       for (int k = 0; k < 4; k++) cdc[pl][k] = lvl[k];
     }
@@ -1440,6 +1444,7 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
         int bx = k & 1, by = k >> 1;
         int nC = nc_of(d, addr, bx, by, 1, pl);
         int tc = residual_block(b, nC, 0, 14, 15, lvl);
+        if (getenv("FO_TRACE")) fprintf(stderr, "  chroma ac %d %d nC %d tc %d bits %lld\n", pl, k, nC, tc, (long long)fb_index(b, 0));
         if (tc < 0) return fo_fail(d, FO_E_FORMAT, "ChromaACLevel");
         for (int j = 0; j < 15; j++) cac[pl][k][ZZ4[j + 1]] = lvl[j];
         m->nzc[pl][k] = tc;

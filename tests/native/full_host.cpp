@@ -1,0 +1,163 @@
+// CPU harness of the general device decoder: the product's host scheduler
+// (h264_sched.cpp) and the very per-slice parser / per-macroblock
+// reconstruction and deblocking code the GPU kernels run (parse_full.h,
+// recon_full.h), driven in the kernels' order — inter macroblocks first,
+// intra macroblocks and deblocking along the x + 2y wavefront — on host
+// memory.  TEST INFRASTRUCTURE (tests/test_full_host.py compares it with the
+// oracle); the product never runs the decoder on the CPU.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "h264.h"
+#include "h264_full.h"
+#include "h264_sched.h"
+#include "mp4.h"
+#include "parse_full.h"
+#include "recon_full.h"
+
+using namespace vts;
+
+extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_cap, int64_t *n_out,
+                         int *w_out, int *h_out, char *err, int err_cap) {
+  auto bad = [&](const std::string &m) {
+    std::snprintf(err, static_cast<size_t>(err_cap), "%s", m.c_str());
+    return -1;
+  };
+  Mp4Info mp4;
+  std::string e = mp4_parse_file(path, &mp4);
+  if (!e.empty()) return bad(e);
+  const Mp4VideoTrack &t = mp4.video.front();
+  Sps sps;
+  Pps pps;
+  e = parse_sps(t.sps[0].data(), t.sps[0].size(), &sps);
+  if (!e.empty()) return bad("SPS: " + e);
+  e = parse_pps(t.pps[0].data(), t.pps[0].size(), &pps);
+  if (!e.empty()) return bad("PPS: " + e);
+  SchedStream facts;
+  e = sched_stream_facts(t.sps[0], t.pps[0], sps, pps, &facts);
+  if (!e.empty()) return bad(e);
+  // elementary stream: samples back to back
+  std::vector<uint8_t> es;
+  std::vector<int64_t> off;
+  FILE *f = std::fopen(path, "rb");
+  if (!f) return bad("open");
+  for (size_t i = 0; i < t.size.size(); ++i) {
+    off.push_back(static_cast<int64_t>(es.size()));
+    const size_t n0 = es.size();
+    es.resize(n0 + t.size[i]);
+    if (fseeko(f, t.offset[i], SEEK_SET) != 0 || std::fread(es.data() + n0, 1, t.size[i], f) != t.size[i]) {
+      std::fclose(f);
+      return bad("read");
+    }
+  }
+  std::fclose(f);
+  es.resize(es.size() + 64, 0);
+  std::vector<SchedFrame> frames;
+  std::vector<SchedSlice> slices;
+  e = sched_build(sps, pps, es.data(), off, t.size, t.nal_length_size, &frames, &slices);
+  if (!e.empty()) return bad(e);
+  const int n = static_cast<int>(frames.size());
+  const int mbw = sps.mb_width, mbh = sps.mb_height, nmb = mbw * mbh;
+  const int pitch = mbw * 16, ch = mbh * 16;
+  const int64_t stride = static_cast<int64_t>(pitch) * ch * 3 / 2;
+  const int W = sps.width(), H = sps.height();
+  *w_out = W;
+  *h_out = H;
+  *n_out = n;
+  if (out_cap < static_cast<int64_t>(n) * W * H * 3 / 2) return bad("output too small");
+  std::vector<uint8_t> surf(static_cast<size_t>(stride) * n + 64, 0);
+  std::vector<MbRec> recs(static_cast<size_t>(nmb) * n);
+  std::vector<FullSlice> fs(slices.size());
+  uint32_t arena_blocks = 0;
+  for (size_t i = 0; i < slices.size(); ++i) {
+    const SchedSlice &s = slices[i];
+    FullSlice &d = fs[i];
+    std::memset(&d, 0, sizeof d);
+    d.nal_offset = s.nal_offset;
+    d.nal_size = s.nal_size;
+    d.slot = static_cast<int32_t>(s.frame);
+    d.first_mb = s.first_mb;
+    d.data_byte = s.data_byte;
+    d.data_bit = s.data_bit;
+    d.is_p = s.is_p;
+    d.qp = s.qp;
+    d.num_ref = s.num_ref;
+    d.dbk_idc = s.dbk_idc;
+    d.dbk_a = s.dbk_a;
+    d.dbk_b = s.dbk_b;
+    const int64_t cap = std::min<int64_t>(27ll * s.n_mbs, 3ll * s.nal_size + 27);
+    d.arena = arena_blocks;
+    d.arena_cap = static_cast<uint32_t>(cap);
+    arena_blocks += static_cast<uint32_t>(cap);
+    for (int r = 0; r < 32; ++r) d.ref_slot[r] = static_cast<int8_t>(s.ref[r] >= 0 ? s.ref[r] : -1);
+  }
+  std::vector<int16_t> arena(static_cast<size_t>(arena_blocks) * 16 + 16);
+  FullParams P{};
+  P.mb_width = mbw;
+  P.mb_height = mbh;
+  P.cip = pps.constrained_intra_pred;
+  P.cqp_off = pps.chroma_qp_index_offset;
+  P.cqp_off2 = facts.cqp_off2;
+  const uint32_t epoch = 7;
+  for (int fi = 0; fi < n; ++fi) {
+    const SchedFrame &fr = frames[static_cast<size_t>(fi)];
+    MbRec *fr_recs = recs.data() + static_cast<size_t>(fi) * nmb;
+    uint32_t errs = 0;
+    for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
+      full::FullScratch sc;
+      errs |= full::parse_slice_full(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P, fr_recs,
+                                     arena.data(), epoch, &sc);
+    }
+    if (errs) return bad("frame " + std::to_string(fi) + ": parse: " + describe_decode_error(errs));
+    full::ReconCtx c{};
+    c.recs = fr_recs;
+    c.arena = arena.data();
+    c.slices = fs.data();
+    c.surf = surf.data();
+    c.frame_stride = stride;
+    c.pitch = pitch;
+    c.uv_off = static_cast<int64_t>(pitch) * ch;
+    c.mbw = mbw;
+    c.mbh = mbh;
+    c.cip = P.cip;
+    c.cqp_off = P.cqp_off;
+    c.cqp_off2 = P.cqp_off2;
+    c.epoch = epoch;
+    // kernel order: inter macroblocks, then intra ones along t = x + 2y
+    for (int a = 0; a < nmb; ++a) {
+      const MbRec &m = fr_recs[a];
+      if (m.epoch != epoch) return bad("frame " + std::to_string(fi) + ": missing macroblock");
+      if (m.type == kMbInter || m.type == kMbSkip) {
+        full::MbRecon r(c, fi, a, m);
+        r.run();
+        if (r.err) return bad("recon: " + describe_decode_error(r.err));
+      }
+    }
+    for (int tt = 0; tt < mbw + 2 * mbh; ++tt)
+      for (int y = 0; y < mbh; ++y) {
+        const int x = tt - 2 * y;
+        if (x < 0 || x >= mbw) continue;
+        const MbRec &m = fr_recs[y * mbw + x];
+        if (m.type == kMbInter || m.type == kMbSkip) continue;
+        full::MbRecon r(c, fi, y * mbw + x, m);
+        r.run();
+        if (r.err) return bad("recon: " + describe_decode_error(r.err));
+      }
+    if (!(flags & 1))
+      for (int tt = 0; tt < mbw + 2 * mbh; ++tt)
+        for (int y = 0; y < mbh; ++y) {
+          const int x = tt - 2 * y;
+          if (x >= 0 && x < mbw) full::deblock_mb(c, fi, y * mbw + x);
+        }
+    // display-size NV12 (crop right / bottom)
+    uint8_t *o = out + static_cast<int64_t>(fi) * W * H * 3 / 2;
+    const uint8_t *Y = surf.data() + static_cast<int64_t>(fi) * stride;
+    for (int y = 0; y < H; ++y) std::memcpy(o + static_cast<int64_t>(y) * W, Y + static_cast<int64_t>(y) * pitch, W);
+    for (int y = 0; y < H / 2; ++y)
+      std::memcpy(o + static_cast<int64_t>(W) * H + static_cast<int64_t>(y) * W,
+                  Y + static_cast<int64_t>(pitch) * ch + static_cast<int64_t>(y) * pitch, W);
+  }
+  return 0;
+}

@@ -1,0 +1,80 @@
+"""The general device decoder's own code on the CPU: the host scheduler
+(h264_sched.cpp: slice headers, reference lists, marking) and the exact
+per-slice parser and per-macroblock reconstruction / deblocking routines the
+GPU kernels run (parse_full.h, recon_full.h), driven in the kernels' order
+(inter macroblocks first, then intra ones and the deblocking filter along the
+x + 2y wavefront) by tests/native/full_host.cpp — must decode every stream
+exactly like the independent oracle (h264_full_oracle.c), before and after
+the deblocking filter.  The GPU tests then only have to show that the
+kernels schedule this code faithfully."""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle
+from vtseg import scene
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "video-transformer_amd" / "csrc"
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    so = tmp_path_factory.mktemp("fh") / "libfullhost.so"
+    srcs = [ROOT / "tests" / "native" / "full_host.cpp"] + [CSRC / f for f in
+                                                             ("mp4.cpp", "h264.cpp", "h264_sched.cpp",
+                                                              "plan.cpp")]
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+                    f"-I{CSRC}", f"-I{ROOT / 'include'}", *map(str, srcs), "-o", str(so)], check=True)
+    lib = C.CDLL(str(so))
+    lib.fh_decode.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                              C.c_void_p, C.c_char_p, C.c_int]
+
+    def decode(path, flags=0):
+        m = oracle.read_mp4(path)
+        n = len(m["sizes"])
+        w, h = C.c_int(0), C.c_int(0)
+        cap = n * 1920 * 1088 * 3 // 2
+        out = np.zeros(cap, np.uint8)
+        got = C.c_int64(0)
+        err = C.create_string_buffer(256)
+        rc = lib.fh_decode(str(path).encode(), flags, out.ctypes.data, cap, C.byref(got),
+                           C.byref(w), C.byref(h), err, 256)
+        if rc:
+            raise RuntimeError(err.value.decode())
+        W, H = w.value, h.value
+        return out[:got.value * W * H * 3 // 2].reshape(got.value, H * 3 // 2, W)
+    return decode
+
+
+STREAMS = [
+    ("subset", dict(width=320, height=240)),
+    ("subset_halfpel", dict(width=320, height=240, max_motion=5, odd_motion=True)),
+    ("subset_nonref", dict(width=160, height=96, max_motion=4, gop_max_s=0.3, nonref_refresh=True)),
+    ("full_tiny", dict(width=48, height=32, coding="full", max_motion=2)),
+    ("full_qvga", dict(width=320, height=240, coding="full", max_motion=3)),
+    ("full_ragged", dict(width=336, height=200, slices_per_row=3, max_motion=6, coding="full")),
+    ("full_oneslice", dict(width=320, height=240, slices_per_row=0, max_motion=8, coding="full")),
+    ("full_cip", dict(width=320, height=240, coding="full", constrained_intra=True)),
+    ("full_crop", dict(width=480, height=270, slices_per_row=2, coding="full")),
+]
+
+
+@pytest.mark.parametrize("name,kw", STREAMS, ids=[s[0] for s in STREAMS])
+def test_device_code_on_cpu_equals_oracle(tmp_path, harness, name, kw):
+    kw = dict(kw)
+    gop = kw.pop("gop_max_s", 0.7)
+    path = tmp_path / f"{name}.mp4"
+    scene.synth_write(path, n_frames=60, cut_min_s=0.5, cut_max_s=1.5, gop_max_s=gop, seed=21,
+                      **kw)
+    for flags in (1, 0):   # before and after the deblocking filter
+        want, _ = oracle.decode_full(path, flags=flags)
+        got = harness(path, flags)
+        assert got.shape == want.shape
+        bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
+        assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"

@@ -1,0 +1,80 @@
+// h264_full.h — data shared by the host scheduler (h264_sched.cpp), the
+// general device decoder (decode_full.hip) and its CPU harness
+// (tests/native/full_host.cpp): the per-slice descriptor the host builds from
+// the slice headers, and the per-macroblock record the slice parser writes
+// for the reconstruction and deblocking kernels.
+//
+// The general path decodes progressive CAVLC streams with I and P slices
+// (ITU-T H.264 Baseline without FMO/ASO/redundant pictures, and Main/High
+// streams that use none of CABAC, B slices, interlace, 8x8 transforms,
+// scaling matrices or weighted prediction); DESIGN.md §5b.
+#pragma once
+#include <cstdint>
+
+namespace vts {
+
+// Slice of a window, as scheduled by the host (window-relative indices).
+struct FullSlice {
+  int64_t nal_offset;   // NAL header byte inside the device ES buffer
+  int32_t nal_size;     // bytes including the header byte
+  int32_t slot;         // ring slot of the picture
+  int32_t first_mb;
+  int32_t data_byte;    // slice_data(): EBSP byte of the payload (after the header byte)
+  int32_t data_bit;     // ... and its RBSP bit index
+  int32_t is_p;
+  int32_t qp;           // SliceQPY
+  int32_t num_ref;      // num_ref_idx_l0_active (P)
+  int32_t dbk_idc;      // disable_deblocking_filter_idc
+  int32_t dbk_a, dbk_b; // FilterOffsetA / FilterOffsetB
+  uint32_t arena;       // first coefficient block reserved for the slice
+  uint32_t arena_cap;   // blocks reserved: min(27 x MBs, 3 x NAL bytes + 27) bounds
+                        // what CAVLC can code (a stored block costs >= 3 bits)
+  int32_t _pad;
+  int8_t ref_slot[32];  // RefPicList0[i] -> ring slot (-1: no reference picture)
+};
+
+struct FullParams {
+  int32_t mb_width, mb_height;
+  int32_t cip;          // constrained_intra_pred_flag
+  int32_t cqp_off;      // chroma_qp_index_offset (Cb)
+  int32_t cqp_off2;     // second_chroma_qp_index_offset (Cr)
+  int32_t _pad;
+};
+
+// Stored coefficient blocks of a macroblock, in parse order = bit order.
+enum : uint32_t {
+  kBlkI16Dc = 0,        // Intra16x16DCLevel (raster 4x4 of the 16 DC levels)
+  kBlkLuma0 = 1,        // + luma4x4BlkIdx (Intra16x16ACLevel / LumaLevel4x4)
+  kBlkChromaDc0 = 17,   // + iCbCr (4 levels in entries 0..3)
+  kBlkChromaAc0 = 19,   // + 4 * iCbCr + chroma4x4BlkIdx
+  kPcmBlocks = 12,      // I_PCM: 384 samples in 12 blocks (256 luma, 64 Cb, 64 Cr)
+};
+
+enum : uint8_t {
+  kMbInter = 0,
+  kMbI4x4 = 1,
+  kMbI16 = 2,
+  kMbPcm = 3,
+  kMbSkip = 4,
+};
+
+// One decoded macroblock's syntax (128 bytes).
+struct alignas(16) MbRec {
+  uint32_t epoch;       // the run's epoch; another value = macroblock absent
+  uint32_t slice;       // window slice index (availability: same slice)
+  uint32_t coef;        // arena index of the first stored block
+  uint32_t blocks;      // stored blocks (kBlk* bits)
+  uint8_t type;         // kMb*
+  uint8_t qp;           // QPY
+  uint8_t cbp;          // coded_block_pattern
+  uint8_t modes;        // bits 0-1 Intra16x16PredMode, bits 2-3 intra_chroma_pred_mode
+  int8_t ref[4];        // RefPicList0 index per 8x8 (-1: intra)
+  int8_t ref_slot[4];   // its ring slot (the picture identity the deblocking bS compares)
+  uint8_t i4[8];        // Intra4x4PredMode of raster 4x4 block b: nibble (b & 1) of byte b >> 1
+  uint8_t nz[16];       // total_coeff of raster luma 4x4 blocks (16 for I_PCM)
+  uint8_t nzc[8];       // chroma AC total_coeff: Cb raster 0-3, Cr raster 0-3
+  int16_t mv[16][2];    // quarter-sample motion of raster 4x4 blocks
+};
+static_assert(sizeof(MbRec) == 128, "MbRec layout");
+
+}  // namespace vts

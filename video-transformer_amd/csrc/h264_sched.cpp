@@ -1,0 +1,422 @@
+// h264_sched.cpp — slice headers and reference lists for the general decoder
+// (see h264_sched.h).  ITU-T H.264 7.3.3 slice_header(), 7.3.3.1
+// ref_pic_list_modification(), 7.3.3.3 dec_ref_pic_marking(), 8.2.4
+// (reference picture list initialisation for P slices in frames, and
+// modification), 8.2.5 (IDR, sliding window, MMCO 1-6).
+#include "h264_sched.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+
+namespace vts {
+namespace {
+
+// RBSP reader over a NAL payload that also reports where it is in EBSP bytes
+struct HdrReader {
+  const uint8_t *p;
+  int64_t n;
+  int64_t pos = 0;   // next EBSP byte
+  int zeros = 0;
+  int bitpos = 0;    // bits left in cur
+  uint32_t cur = 0;
+  int64_t rbits = 0; // RBSP bits consumed
+  bool err = false;
+  HdrReader(const uint8_t *b, int64_t len) : p(b), n(len) {}
+  uint32_t bit() {
+    if (bitpos == 0) {
+      if (pos >= n) {
+        err = true;
+        return 0;
+      }
+      uint32_t v = p[pos];
+      if (zeros >= 2 && v == 3) {
+        ++pos;
+        zeros = 0;
+        if (pos >= n) {
+          err = true;
+          return 0;
+        }
+        v = p[pos];
+      }
+      ++pos;
+      zeros = v == 0 ? zeros + 1 : 0;
+      cur = v;
+      bitpos = 8;
+    }
+    --bitpos;
+    ++rbits;
+    return (cur >> bitpos) & 1u;
+  }
+  uint32_t u(int k) {
+    uint32_t v = 0;
+    for (int i = 0; i < k; ++i) v = (v << 1) | bit();
+    return v;
+  }
+  uint32_t ue() {
+    int lz = 0;
+    while (!bit()) {
+      if (++lz > 31 || err) {
+        err = true;
+        return 0;
+      }
+    }
+    return lz ? ((1u << lz) - 1u + u(lz)) : 0u;
+  }
+  int32_t se() {
+    const uint32_t k = ue();
+    return (k & 1u) ? static_cast<int32_t>((k + 1) / 2) : -static_cast<int32_t>(k / 2);
+  }
+  // EBSP byte holding the next bit (for a mid-byte position: the current byte)
+  int64_t ebsp_byte() const { return bitpos ? pos - 1 : pos; }
+};
+
+struct RefPic {
+  int64_t frame;
+  int frame_num;
+  int lt_idx;
+  int kind;  // 1 short-term, 2 long-term
+};
+
+bool more_rbsp(const std::vector<uint8_t> &nal, const HdrReader &r) {
+  int64_t last = static_cast<int64_t>(nal.size()) - 1;
+  while (last > 0 && nal[last] == 0) --last;
+  if (last <= 0) return false;
+  const int tz = __builtin_ctz(static_cast<uint32_t>(nal[last]));
+  const int64_t stop = (last - 1) * 8 + (7 - tz);  // EBSP bit index in the payload
+  const int64_t at = r.bitpos ? (r.pos - 1) * 8 + (8 - r.bitpos) : r.pos * 8;
+  return at < stop;
+}
+
+}  // namespace
+
+std::string sched_stream_facts(const std::vector<uint8_t> &sps_nal, const std::vector<uint8_t> &pps_nal,
+                               const Sps &sps, const Pps &pps, SchedStream *out) {
+  *out = SchedStream{};
+  out->cqp_off2 = pps.chroma_qp_index_offset;
+  {  // SPS: seq_scaling_matrix_present_flag (High profiles only)
+    HdrReader r(sps_nal.data() + 1, static_cast<int64_t>(sps_nal.size()) - 1);
+    const int prof = static_cast<int>(r.u(8));
+    r.u(16);
+    r.ue();
+    const bool high = prof == 100 || prof == 110 || prof == 122 || prof == 244 || prof == 44 ||
+                      prof == 83 || prof == 86 || prof == 118 || prof == 128 || prof == 138 ||
+                      prof == 139 || prof == 134 || prof == 135;
+    if (high) {
+      const uint32_t cf = r.ue();
+      if (cf == 3) r.u(1);
+      r.ue();
+      r.ue();
+      r.u(1);
+      out->seq_scaling = static_cast<int>(r.u(1));
+    }
+  }
+  {  // PPS: skip to the optional tail (7.3.2.2)
+    HdrReader r(pps_nal.data() + 1, static_cast<int64_t>(pps_nal.size()) - 1);
+    r.ue();
+    r.ue();
+    r.u(1);
+    r.u(1);
+    if (r.ue() != 0) return "slice groups (FMO)";
+    r.ue();
+    r.ue();
+    r.u(1);
+    r.u(2);
+    r.se();
+    r.se();
+    r.se();
+    r.u(3);
+    if (more_rbsp(pps_nal, r)) {
+      out->transform_8x8 = static_cast<int>(r.u(1));
+      out->pic_scaling = static_cast<int>(r.u(1));
+      if (out->pic_scaling) return "PPS scaling matrices";
+      out->cqp_off2 = r.se();
+    }
+    if (r.err) return "truncated PPS";
+  }
+  if (out->seq_scaling) return "SPS scaling matrices";
+  if (out->transform_8x8) return "8x8 transform (transform_8x8_mode_flag)";
+  if (pps.redundant_pic_cnt_present) return "redundant pictures";
+  return "";
+}
+
+std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const std::vector<int64_t> &off,
+                        const std::vector<uint32_t> &size, int nal_len, std::vector<SchedFrame> *frames,
+                        std::vector<SchedSlice> *slices) {
+  const int nmb = sps.mb_width * sps.mb_height;
+  const int max_fn = 1 << sps.log2_max_frame_num;
+  const int max_refs = std::max(1, sps.max_num_ref_frames);
+  std::vector<RefPic> dpb;
+  int prev_ref_fn = 0;
+  int max_lt_idx = -1;
+  bool have_prev = false;
+  frames->assign(off.size(), SchedFrame{});
+  slices->clear();
+  char msg[160];
+  for (size_t f = 0; f < off.size(); ++f) {
+    SchedFrame &fr = (*frames)[f];
+    fr.s0 = static_cast<int64_t>(slices->size());
+    int64_t p = off[f];
+    const int64_t end = p + size[f];
+    bool first = true, idr = false, adaptive = false, lt_ref_flag = false;
+    int fn = 0;
+    std::vector<std::pair<int, int>> mmco;  // (op, arg) ; op 3/6 carry lt idx in arg2 below
+    std::vector<int> mmco_arg2;
+    while (p + nal_len <= end) {
+      uint32_t len = 0;
+      for (int i = 0; i < nal_len; ++i) len = (len << 8) | es[p + i];
+      p += nal_len;
+      if (len == 0 || p + len > end) return "bad NAL length";
+      const uint8_t hdr = es[p];
+      const int type = hdr & 31, ref_idc = (hdr >> 5) & 3;
+      if (type != 1 && type != 5) {
+        if (type >= 2 && type <= 4) return "data partitioning";
+        p += len;
+        continue;
+      }
+      HdrReader r(es + p + 1, len - 1);
+      SchedSlice s{};
+      s.frame = static_cast<int64_t>(f);
+      s.nal_offset = p;
+      s.nal_size = static_cast<int32_t>(len);
+      s.first_mb = static_cast<int32_t>(r.ue());
+      int st = static_cast<int>(r.ue());
+      if (st > 4) st -= 5;
+      if (st != 0 && st != 2) return "B / SP / SI slices";
+      s.is_p = st == 0;
+      if (static_cast<int>(r.ue()) != pps.pps_id) return "slice refers to another PPS";
+      const int frame_num = static_cast<int>(r.u(sps.log2_max_frame_num));
+      if (type == 5) r.ue();  // idr_pic_id
+      if (sps.poc_type == 0) {
+        r.u(sps.log2_max_poc_lsb);
+        if (pps.bottom_field_pic_order_in_frame_present) r.se();
+      } else if (sps.poc_type == 1 && !sps.delta_pic_order_always_zero) {
+        r.se();
+        if (pps.bottom_field_pic_order_in_frame_present) r.se();
+      }
+      if (pps.redundant_pic_cnt_present) r.ue();
+      s.num_ref = pps.num_ref_idx_l0_default_active;
+      std::vector<std::pair<int, int>> mods;
+      if (s.is_p) {
+        if (r.u(1)) s.num_ref = static_cast<int>(r.ue()) + 1;
+        if (s.num_ref > 32) return "num_ref_idx_l0_active > 32";
+        if (r.u(1)) {
+          for (;;) {
+            const int idc = static_cast<int>(r.ue());
+            if (idc == 3 || r.err) break;
+            if (idc > 2) return "bad modification_of_pic_nums_idc";
+            mods.emplace_back(idc, static_cast<int>(r.ue()));
+            if (mods.size() > 64) return "too many list modifications";
+          }
+        }
+      }
+      bool this_adaptive = false, this_lt = false;
+      std::vector<std::pair<int, int>> this_mmco;
+      std::vector<int> this_arg2;
+      if (ref_idc) {
+        if (type == 5) {
+          r.u(1);
+          this_lt = r.u(1) != 0;
+        } else if ((this_adaptive = r.u(1) != 0)) {
+          for (;;) {
+            const int op = static_cast<int>(r.ue());
+            if (op == 0 || r.err) break;
+            if (op > 6) return "bad MMCO";
+            int a1 = 0, a2 = 0;
+            if (op == 1 || op == 3) a1 = static_cast<int>(r.ue());
+            if (op == 2) a1 = static_cast<int>(r.ue());
+            if (op == 3 || op == 6) a2 = static_cast<int>(r.ue());
+            if (op == 4) a1 = static_cast<int>(r.ue());
+            this_mmco.emplace_back(op, a1);
+            this_arg2.push_back(a2);
+            if (this_mmco.size() > 66) return "too many MMCOs";
+          }
+        }
+      }
+      s.qp = pps.pic_init_qp + r.se();
+      s.dbk_idc = 0;
+      if (pps.deblocking_filter_control_present) {
+        s.dbk_idc = static_cast<int>(r.ue());
+        if (s.dbk_idc != 1) {
+          s.dbk_a = 2 * r.se();
+          s.dbk_b = 2 * r.se();
+        }
+      }
+      if (r.err || s.first_mb < 0 || s.first_mb >= nmb || s.qp < 0 || s.qp > 51 || s.dbk_idc > 2 ||
+          s.dbk_a < -12 || s.dbk_a > 12 || s.dbk_b < -12 || s.dbk_b > 12)
+        return "malformed slice header";
+      s.data_byte = static_cast<int32_t>(r.ebsp_byte());
+      s.data_bit = static_cast<int32_t>(r.rbits);
+      if (first) {
+        idr = type == 5;
+        fn = frame_num;
+        fr.is_ref = ref_idc != 0;
+        adaptive = this_adaptive;
+        lt_ref_flag = this_lt;
+        mmco = this_mmco;
+        mmco_arg2 = this_arg2;
+        // frame_num continuity (gaps_in_frame_num_value_allowed_flag = 0)
+        if (!idr && have_prev) {
+          const int want = (prev_ref_fn + 1) % max_fn;
+          if (frame_num != want) {
+            std::snprintf(msg, sizeof msg, "frame_num gap at frame %zu (%d after %d)", f, frame_num, prev_ref_fn);
+            return msg;
+          }
+        }
+        if (!idr && !have_prev) return "stream does not start with an IDR picture";
+        if (idr) dpb.clear();
+      } else if (frame_num != fn || (type == 5) != idr) {
+        return "slices of one picture disagree";
+      }
+      first = false;
+      if (s.is_p) fr.intra = false;
+      // RefPicList0 (8.2.4.2.1 + 8.2.4.3)
+      for (int i = 0; i < 32; ++i) s.ref[i] = -1;
+      if (s.is_p) {
+        std::vector<RefPic> st_refs, lt_refs;
+        for (const RefPic &rp : dpb) (rp.kind == 1 ? st_refs : lt_refs).push_back(rp);
+        auto wrap = [&](const RefPic &rp) { return rp.frame_num > fn ? rp.frame_num - max_fn : rp.frame_num; };
+        std::stable_sort(st_refs.begin(), st_refs.end(),
+                         [&](const RefPic &a, const RefPic &b) { return wrap(a) > wrap(b); });
+        std::stable_sort(lt_refs.begin(), lt_refs.end(),
+                         [](const RefPic &a, const RefPic &b) { return a.lt_idx < b.lt_idx; });
+        std::vector<const RefPic *> list;
+        for (const RefPic &rp : st_refs) list.push_back(&rp);
+        for (const RefPic &rp : lt_refs) list.push_back(&rp);
+        const int n = s.num_ref;
+        list.resize(static_cast<size_t>(n) + 1, nullptr);
+        int pred = fn, ridx = 0;
+        for (const auto &md : mods) {
+          const RefPic *pic = nullptr;
+          if (md.first < 2) {
+            const int d = md.second + 1;
+            int nowrap = md.first == 0 ? pred - d : pred + d;
+            if (nowrap < 0) nowrap += max_fn;
+            if (nowrap >= max_fn) nowrap -= max_fn;
+            pred = nowrap;
+            const int num = nowrap > fn ? nowrap - max_fn : nowrap;
+            for (const RefPic &rp : st_refs)
+              if (wrap(rp) == num) pic = &rp;
+          } else {
+            for (const RefPic &rp : lt_refs)
+              if (rp.lt_idx == md.second) pic = &rp;
+          }
+          if (!pic) return "list modification names no reference picture";
+          for (int c = n; c > ridx; --c) list[c] = list[c - 1];
+          list[ridx++] = pic;
+          int ni = ridx;
+          for (int c = ridx; c <= n; ++c)
+            if (list[c] != pic) list[ni++] = list[c];
+        }
+        // the pointers refer to st_refs / lt_refs, alive until here
+        for (int i = 0; i < n; ++i) {
+          s.ref[i] = list[i] ? list[i]->frame : -1;
+          if (s.ref[i] >= 0 && std::find(fr.refs.begin(), fr.refs.end(), s.ref[i]) == fr.refs.end())
+            fr.refs.push_back(s.ref[i]);
+        }
+      }
+      slices->push_back(s);
+      p += len;
+    }
+    fr.ns = static_cast<int64_t>(slices->size()) - fr.s0;
+    if (fr.ns == 0) {
+      std::snprintf(msg, sizeof msg, "frame %zu has no slices", f);
+      return msg;
+    }
+    // macroblock counts per slice (slices of a picture in increasing first_mb)
+    for (int64_t k = fr.s0; k < fr.s0 + fr.ns; ++k) {
+      SchedSlice &s = (*slices)[static_cast<size_t>(k)];
+      const int next = (k + 1 < fr.s0 + fr.ns) ? (*slices)[static_cast<size_t>(k + 1)].first_mb : nmb;
+      if (next <= s.first_mb) return "slices out of order (ASO) or overlapping";
+      s.n_mbs = next - s.first_mb;
+    }
+    // reference marking (8.2.5) after the picture
+    if (fr.is_ref) {
+      RefPic cur{static_cast<int64_t>(f), fn, 0, 1};
+      if (idr) {
+        dpb.clear();
+        if (lt_ref_flag) {
+          cur.kind = 2;
+          cur.lt_idx = 0;
+          max_lt_idx = 0;
+        } else {
+          max_lt_idx = -1;
+        }
+        dpb.push_back(cur);
+        prev_ref_fn = fn;
+      } else {
+        bool cur_long = false, reset = false;
+        if (adaptive) {
+          for (size_t k = 0; k < mmco.size(); ++k) {
+            const int op = mmco[k].first, a1 = mmco[k].second, a2 = mmco_arg2[k];
+            auto wrap = [&](const RefPic &rp) { return rp.frame_num > fn ? rp.frame_num - max_fn : rp.frame_num; };
+            if (op == 1 || op == 3) {
+              const int pn = fn - (a1 + 1);
+              for (size_t i = 0; i < dpb.size(); ++i)
+                if (dpb[i].kind == 1 && wrap(dpb[i]) == pn) {
+                  if (op == 1) {
+                    dpb.erase(dpb.begin() + static_cast<int64_t>(i));
+                  } else {
+                    dpb.erase(std::remove_if(dpb.begin(), dpb.end(),
+                                             [&](const RefPic &x) { return x.kind == 2 && x.lt_idx == a2; }),
+                              dpb.end());
+                    for (RefPic &x : dpb)
+                      if (x.kind == 1 && wrap(x) == pn) {
+                        x.kind = 2;
+                        x.lt_idx = a2;
+                      }
+                  }
+                  break;
+                }
+            } else if (op == 2) {
+              dpb.erase(std::remove_if(dpb.begin(), dpb.end(),
+                                       [&](const RefPic &x) { return x.kind == 2 && x.lt_idx == a1; }),
+                        dpb.end());
+            } else if (op == 4) {
+              max_lt_idx = a1 - 1;
+              dpb.erase(std::remove_if(dpb.begin(), dpb.end(),
+                                       [&](const RefPic &x) { return x.kind == 2 && x.lt_idx > max_lt_idx; }),
+                        dpb.end());
+            } else if (op == 5) {
+              dpb.clear();
+              max_lt_idx = -1;
+              reset = true;
+            } else if (op == 6) {
+              dpb.erase(std::remove_if(dpb.begin(), dpb.end(),
+                                       [&](const RefPic &x) { return x.kind == 2 && x.lt_idx == a2; }),
+                        dpb.end());
+              cur.kind = 2;
+              cur.lt_idx = a2;
+              cur_long = true;
+            }
+          }
+        } else {
+          int ns = 0;
+          for (const RefPic &x : dpb) ns += x.kind == 1;
+          if (static_cast<int>(dpb.size()) >= max_refs && ns > 0) {
+            size_t o = dpb.size();
+            int ow = 0;
+            for (size_t i = 0; i < dpb.size(); ++i) {
+              if (dpb[i].kind != 1) continue;
+              const int w = dpb[i].frame_num > fn ? dpb[i].frame_num - max_fn : dpb[i].frame_num;
+              if (o == dpb.size() || w < ow) {
+                o = i;
+                ow = w;
+              }
+            }
+            dpb.erase(dpb.begin() + static_cast<int64_t>(o));
+          }
+        }
+        if (reset) cur.frame_num = 0;
+        (void)cur_long;
+        dpb.push_back(cur);
+        prev_ref_fn = reset ? 0 : fn;
+        if (static_cast<int>(dpb.size()) > 16) return "more than 16 reference frames";
+      }
+    }
+    have_prev = true;
+  }
+  return "";
+}
+
+}  // namespace vts

@@ -85,6 +85,15 @@ namespace h264 {
   {{1, 0}, {1, 1, 0}, {3, 2, 1, 0}, {3, 2, 1, 1, 0}, {3, 2, 3, 2, 1, 0}, {3, 0, 1, 3, 2, 5, 4},    \
    {7, 6, 5, 4, 3, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1}}
 
+#define VTS_ZZ_DATA {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15}
+#define VTS_CBPI_DATA {47, 31, 15, 0, 23, 27, 29, 30, 7, 11, 13, 14, 39, 43, 45, 46, 16, 3, 5, 10, 12, 19, 21, 26, 28, 35, 37, 42, 44, 1, 2, 4, 8, 17, 18, 20, 24, 6, 9, 22, 25, 32, 33, 34, 36, 40, 38, 41}
+#define VTS_CBPP_DATA {0, 16, 1, 2, 4, 8, 32, 3, 5, 10, 12, 15, 47, 7, 11, 13, 14, 6, 9, 31, 35, 37, 42, 44, 33, 34, 36, 40, 39, 43, 45, 46, 17, 18, 20, 24, 19, 21, 26, 28, 23, 27, 29, 30, 22, 25, 38, 41}
+#define VTS_NORMV_DATA {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}}
+#define VTS_QPC_DATA {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 32, 33, 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39}
+#define VTS_ALPHA_DATA {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 4, 5, 6, 7, 8, 9, 10, 12, 13, 15, 17, 20, 22, 25, 28, 32, 36, 40, 45, 50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255}
+#define VTS_BETA_DATA {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18}
+#define VTS_TC0_DATA { {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4}, {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11}, {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}}
+
 VTS_TAB_HOST uint8_t kCoeffTokenLen[4][17][4] = VTS_CT_LEN_DATA;
 VTS_TAB_HOST uint8_t kCoeffTokenCode[4][17][4] = VTS_CT_CODE_DATA;
 VTS_TAB_HOST uint8_t kTotalZerosLen[15][16] = VTS_TZ_LEN_DATA;
@@ -95,41 +104,34 @@ VTS_TAB_HOST uint8_t kRunBeforeLen[7][15] = VTS_RB_LEN_DATA;
 VTS_TAB_HOST uint8_t kRunBeforeCode[7][15] = VTS_RB_CODE_DATA;
 
 // 8.5.6 frame zig-zag: scan index -> raster index (row * 4 + column)
-VTS_TAB_HOST uint8_t kZigzag4x4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+VTS_TAB_HOST uint8_t kZigzag4x4[16] = VTS_ZZ_DATA;
 // Table 9-4 (chroma_format_idc 1): codeNum -> coded_block_pattern
-VTS_TAB_HOST uint8_t kCbpIntra[48] = {47, 31, 15, 0,  23, 27, 29, 30, 7,  11, 13, 14, 39, 43, 45, 46,
-                                      16, 3,  5,  10, 12, 19, 21, 26, 28, 35, 37, 42, 44, 1,  2,  4,
-                                      8,  17, 18, 20, 24, 6,  9,  22, 25, 32, 33, 34, 36, 40, 38, 41};
-VTS_TAB_HOST uint8_t kCbpInter[48] = {0,  16, 1,  2,  4,  8,  32, 3,  5,  10, 12, 15, 47, 7,  11, 13,
-                                      14, 6,  9,  31, 35, 37, 42, 44, 33, 34, 36, 40, 39, 43, 45, 46,
-                                      17, 18, 20, 24, 19, 21, 26, 28, 23, 27, 29, 30, 22, 25, 38, 41};
+VTS_TAB_HOST uint8_t kCbpIntra[48] = VTS_CBPI_DATA;
+VTS_TAB_HOST uint8_t kCbpInter[48] = VTS_CBPP_DATA;
 // luma4x4BlkIdx -> position in 4x4-block units (6.4.3)
 VTS_TAB_HOST uint8_t kBlkX[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
 VTS_TAB_HOST uint8_t kBlkY[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
 // 8.5.9 normAdjust4x4 v[m][0..2]
-VTS_TAB_HOST uint8_t kNormV[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16},
-                                     {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+VTS_TAB_HOST uint8_t kNormV[6][3] = VTS_NORMV_DATA;
 // Table 8-15: QPc = f(qPI), qPI in 0..51
-VTS_TAB_HOST uint8_t kQpc[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
-                                 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 32, 33,
-                                 34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+VTS_TAB_HOST uint8_t kQpc[52] = VTS_QPC_DATA;
 // Tables 8-16 / 8-17: alpha'(indexA), beta'(indexB), tC0'(indexA, bS 1..3)
-VTS_TAB_HOST uint8_t kAlpha[52] = {0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   0,   0,
-                                   0,  0,  0,  4,  4,  5,  6,  7,   8,   9,   10,  12,  13,
-                                   15, 17, 20, 22, 25, 28, 32, 36,  40,  45,  50,  56,  63,
-                                   71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
-VTS_TAB_HOST uint8_t kBeta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  2,  2,
-                                  2,  3,  3,  3,  3,  4,  4,  4,  6,  6,  7,  7,  8,  8,  9,  9,  10, 10,
-                                  11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
-VTS_TAB_HOST uint8_t kTc0[52][3] = {
-    {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},
-    {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},
-    {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 1},   {0, 0, 1},   {0, 0, 1},   {0, 0, 1},
-    {0, 1, 1},   {0, 1, 1},   {1, 1, 1},   {1, 1, 1},   {1, 1, 1},   {1, 1, 1},   {1, 1, 2},
-    {1, 1, 2},   {1, 1, 2},   {1, 1, 2},   {1, 2, 3},   {1, 2, 3},   {2, 2, 3},   {2, 2, 4},
-    {2, 3, 4},   {2, 3, 4},   {3, 3, 5},   {3, 4, 6},   {3, 4, 6},   {4, 5, 7},   {4, 5, 8},
-    {4, 6, 9},   {5, 7, 10},  {6, 8, 11},  {6, 8, 13},  {7, 10, 14}, {8, 11, 16}, {9, 12, 18},
-    {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+VTS_TAB_HOST uint8_t kAlpha[52] = VTS_ALPHA_DATA;
+VTS_TAB_HOST uint8_t kBeta[52] = VTS_BETA_DATA;
+VTS_TAB_HOST uint8_t kTc0[52][3] = VTS_TC0_DATA;
+
+// Device copies (constant memory) of the tables the kernels index at run time,
+// from the same data macros.
+#if defined(__HIPCC__)
+__device__ __constant__ static const uint8_t kdZigzag4x4[16] = VTS_ZZ_DATA;
+__device__ __constant__ static const uint8_t kdCbpIntra[48] = VTS_CBPI_DATA;
+__device__ __constant__ static const uint8_t kdCbpInter[48] = VTS_CBPP_DATA;
+__device__ __constant__ static const uint8_t kdNormV[6][3] = VTS_NORMV_DATA;
+__device__ __constant__ static const uint8_t kdQpc[52] = VTS_QPC_DATA;
+__device__ __constant__ static const uint8_t kdAlpha[52] = VTS_ALPHA_DATA;
+__device__ __constant__ static const uint8_t kdBeta[52] = VTS_BETA_DATA;
+__device__ __constant__ static const uint8_t kdTc0[52][3] = VTS_TC0_DATA;
+#endif
 
 }  // namespace h264
 }  // namespace vts

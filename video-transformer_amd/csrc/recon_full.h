@@ -1,0 +1,604 @@
+// recon_full.h — per-macroblock reconstruction and deblocking of the general
+// device decoder, written once for the device kernels (decode_full.hip: one
+// lane per macroblock, intra macroblocks and deblocking in wavefront order)
+// and the CPU harness (tests/native/full_host.cpp).
+//
+// Pictures are NV12 in the decode ring: luma rows of `pitch` bytes, the
+// interleaved Cb/Cr plane at + uv_off.  Clauses: 8.3 intra prediction, 8.4.2
+// inter prediction (6-tap / bilinear interpolation on clamped reference
+// windows), 8.5 scaling and transforms, 8.7 deblocking.
+#pragma once
+#include <cstdint>
+
+#include "h264.h"
+#include "h264_full.h"
+#include "h264_tables.h"
+#include "parse_full.h"
+
+namespace vts {
+namespace full {
+
+#if defined(__HIPCC__)
+#define kNv h264::kdNormV
+#define kQpcT h264::kdQpc
+#define kAl h264::kdAlpha
+#define kBe h264::kdBeta
+#define kTc h264::kdTc0
+#else
+static const uint8_t (*const kNv)[3] = h264::kNormV;
+static const uint8_t *const kQpcT = h264::kQpc;
+static const uint8_t *const kAl = h264::kAlpha;
+static const uint8_t *const kBe = h264::kBeta;
+static const uint8_t (*const kTc)[3] = h264::kTc0;
+#endif
+
+VTS_HD VTS_INLINE int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+VTS_HD VTS_INLINE int clip1(int v) { return clip3(0, 255, v); }
+VTS_HD VTS_INLINE int iabs(int v) { return v < 0 ? -v : v; }
+VTS_HD VTS_INLINE int qpc_of(int qpy, int off) { return kQpcT[clip3(0, 51, qpy + off)]; }
+VTS_HD VTS_INLINE int level_scale(int m, int i, int j) {
+  const int k = (!(i & 1) && !(j & 1)) ? 0 : (((i & 1) && (j & 1)) ? 1 : 2);
+  return 16 * kNv[m][k];
+}
+
+struct ReconCtx {
+  const MbRec *recs;        // this frame's records
+  const int16_t *arena;
+  const FullSlice *slices;  // window slices
+  uint8_t *surf;            // ring base
+  int64_t frame_stride;
+  int32_t pitch;            // luma and UV row bytes
+  int64_t uv_off;           // UV plane offset in a frame
+  int32_t mbw, mbh;
+  int32_t cip, cqp_off, cqp_off2;
+  uint32_t epoch;
+};
+
+// 8.5.12: scaling (flat) + 4x4 inverse transform; c raster (row i, col j);
+// dc_done: c[0] is an already scaled DC; r receives the residual
+VTS_HD inline void scale_idct4(const int *c, int qp, bool dc_done, int *r) {
+  int d[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      const int k = i * 4 + j;
+      if (k == 0 && dc_done) {
+        d[0] = c[0];
+        continue;
+      }
+      const int ls = level_scale(qp % 6, i, j);
+      d[k] = qp >= 24 ? (c[k] * ls) << (qp / 6 - 4) : (c[k] * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+    }
+  int f[16];
+  for (int i = 0; i < 4; ++i) {
+    const int e0 = d[i * 4] + d[i * 4 + 2], e1 = d[i * 4] - d[i * 4 + 2];
+    const int e2 = (d[i * 4 + 1] >> 1) - d[i * 4 + 3], e3 = d[i * 4 + 1] + (d[i * 4 + 3] >> 1);
+    f[i * 4] = e0 + e3;
+    f[i * 4 + 1] = e1 + e2;
+    f[i * 4 + 2] = e1 - e2;
+    f[i * 4 + 3] = e0 - e3;
+  }
+  for (int j = 0; j < 4; ++j) {
+    const int g0 = f[j] + f[8 + j], g1 = f[j] - f[8 + j];
+    const int g2 = (f[4 + j] >> 1) - f[12 + j], g3 = f[4 + j] + (f[12 + j] >> 1);
+    r[j] = (g0 + g3 + 32) >> 6;
+    r[4 + j] = (g1 + g2 + 32) >> 6;
+    r[8 + j] = (g1 - g2 + 32) >> 6;
+    r[12 + j] = (g0 - g3 + 32) >> 6;
+  }
+}
+
+VTS_HD VTS_INLINE int tap6(int a, int b, int c, int d, int e, int f) {
+  return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
+}
+
+struct MbRecon {
+  const ReconCtx &c;
+  int slot, mb, mx, my;
+  const MbRec &m;
+  uint8_t *Y;   // frame luma
+  uint8_t *UV;  // frame interleaved chroma
+  uint32_t err = 0;
+
+  VTS_HD MbRecon(const ReconCtx &ctx, int s, int a, const MbRec &rec)
+      : c(ctx), slot(s), mb(a), mx(a % ctx.mbw), my(a / ctx.mbw), m(rec) {
+    Y = c.surf + static_cast<int64_t>(slot) * c.frame_stride;
+    UV = Y + c.uv_off;
+  }
+
+  // block index in the arena of stored-block bit `bit`, -1 if not stored
+  VTS_HD VTS_INLINE int64_t block_of(uint32_t bit) const {
+    if (!((m.blocks >> bit) & 1u)) return -1;
+    return static_cast<int64_t>(m.coef) + __builtin_popcount(m.blocks & ((1u << bit) - 1u));
+  }
+  VTS_HD VTS_INLINE void load_block(uint32_t bit, int *cf) const {
+    const int64_t b = block_of(bit);
+    for (int i = 0; i < 16; ++i) cf[i] = b < 0 ? 0 : c.arena[16 * b + i];
+  }
+
+  // neighbour macroblock available for intra prediction (6.4.8, CIP)
+  VTS_HD VTS_INLINE bool intra_nb(int n) const {
+    if (n < 0) return false;
+    const MbRec &r = c.recs[n];
+    if (r.epoch != c.epoch || r.slice != m.slice) return false;
+    if (c.cip && (r.type == kMbInter || r.type == kMbSkip)) return false;
+    return true;
+  }
+  VTS_HD VTS_INLINE int nb_addr(int dx, int dy) const {  // dx, dy in {-1, 0, 1} macroblocks
+    const int x = mx + dx, y = my + dy;
+    if (x < 0 || x >= c.mbw || y < 0) return -1;
+    return y * c.mbw + x;
+  }
+
+  VTS_HD VTS_INLINE int ly(int x, int y) const { return Y[static_cast<int64_t>(y) * c.pitch + x]; }
+  VTS_HD VTS_INLINE int lc(int pl, int x, int y) const { return UV[static_cast<int64_t>(y) * c.pitch + 2 * x + pl]; }
+
+  // ---- inter (8.4.2.2)
+  VTS_HD void inter_block(int b) {
+    const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+    const int rs = m.ref_slot[p8];
+    const uint8_t *R = c.surf + static_cast<int64_t>(rs) * c.frame_stride;
+    const uint8_t *RUV = R + c.uv_off;
+    const int W = c.mbw * 16, H = c.mbh * 16;
+    const int mvx = m.mv[b][0], mvy = m.mv[b][1];
+    const int bx = mx * 16 + (b & 3) * 4, by = my * 16 + (b >> 2) * 4;
+    const int xi = bx + (mvx >> 2), yi = by + (mvy >> 2), xf = mvx & 3, yf = mvy & 3;
+    uint8_t w[9][9];
+    for (int r = 0; r < 9; ++r) {
+      const int yy = clip3(0, H - 1, yi - 2 + r);
+      for (int q = 0; q < 9; ++q) w[r][q] = R[static_cast<int64_t>(yy) * c.pitch + clip3(0, W - 1, xi - 2 + q)];
+    }
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) {
+        const int G = w[y + 2][x + 2];
+        int v;
+        if (!xf && !yf) {
+          v = G;
+        } else {
+          const int b1 = tap6(w[y + 2][x], w[y + 2][x + 1], w[y + 2][x + 2], w[y + 2][x + 3], w[y + 2][x + 4], w[y + 2][x + 5]);
+          const int h1 = tap6(w[y][x + 2], w[y + 1][x + 2], w[y + 2][x + 2], w[y + 3][x + 2], w[y + 4][x + 2], w[y + 5][x + 2]);
+          const int s1 = tap6(w[y + 3][x], w[y + 3][x + 1], w[y + 3][x + 2], w[y + 3][x + 3], w[y + 3][x + 4], w[y + 3][x + 5]);
+          const int m1 = tap6(w[y][x + 3], w[y + 1][x + 3], w[y + 2][x + 3], w[y + 3][x + 3], w[y + 4][x + 3], w[y + 5][x + 3]);
+          const int bb = clip1((b1 + 16) >> 5), hh = clip1((h1 + 16) >> 5);
+          const int ss = clip1((s1 + 16) >> 5), mm = clip1((m1 + 16) >> 5);
+          int jj = 0;
+          if ((xf | yf) & 1 ? (xf == 2 || yf == 2) : (xf == 2 && yf == 2)) {
+            int hr[6];
+            for (int k = 0; k < 6; ++k)
+              hr[k] = tap6(w[y + k][x], w[y + k][x + 1], w[y + k][x + 2], w[y + k][x + 3], w[y + k][x + 4], w[y + k][x + 5]);
+            jj = clip1((tap6(hr[0], hr[1], hr[2], hr[3], hr[4], hr[5]) + 512) >> 10);
+          }
+          const int Hs = w[y + 2][x + 3], Ms = w[y + 3][x + 2];
+          switch (yf * 4 + xf) {
+            case 1: v = (G + bb + 1) >> 1; break;
+            case 2: v = bb; break;
+            case 3: v = (Hs + bb + 1) >> 1; break;
+            case 4: v = (G + hh + 1) >> 1; break;
+            case 5: v = (bb + hh + 1) >> 1; break;
+            case 6: v = (bb + jj + 1) >> 1; break;
+            case 7: v = (bb + mm + 1) >> 1; break;
+            case 8: v = hh; break;
+            case 9: v = (hh + jj + 1) >> 1; break;
+            case 10: v = jj; break;
+            case 11: v = (jj + mm + 1) >> 1; break;
+            case 12: v = (Ms + hh + 1) >> 1; break;
+            case 13: v = (hh + ss + 1) >> 1; break;
+            case 14: v = (jj + ss + 1) >> 1; break;
+            default: v = (mm + ss + 1) >> 1; break;
+          }
+        }
+        pred_y[((b >> 2) * 4 + y) * 16 + (b & 3) * 4 + x] = static_cast<uint8_t>(v);
+      }
+    // chroma 2x2 (8.4.2.2.2)
+    const int cw = W / 2, ch = H / 2;
+    const int cfx = mvx & 7, cfy = mvy & 7;
+    const int cx0 = bx / 2 + (mvx >> 3), cy0 = by / 2 + (mvy >> 3);
+    for (int y = 0; y < 2; ++y)
+      for (int x = 0; x < 2; ++x) {
+        const int xa = clip3(0, cw - 1, cx0 + x), xb = clip3(0, cw - 1, cx0 + x + 1);
+        const int ya = clip3(0, ch - 1, cy0 + y), yb = clip3(0, ch - 1, cy0 + y + 1);
+        for (int pl = 0; pl < 2; ++pl) {
+          const int A = RUV[static_cast<int64_t>(ya) * c.pitch + 2 * xa + pl];
+          const int B = RUV[static_cast<int64_t>(ya) * c.pitch + 2 * xb + pl];
+          const int C = RUV[static_cast<int64_t>(yb) * c.pitch + 2 * xa + pl];
+          const int D = RUV[static_cast<int64_t>(yb) * c.pitch + 2 * xb + pl];
+          const int v = ((8 - cfx) * (8 - cfy) * A + cfx * (8 - cfy) * B + (8 - cfx) * cfy * C + cfx * cfy * D + 32) >> 6;
+          pred_c[pl][((b >> 2) * 2 + y) * 8 + (b & 3) * 2 + x] = static_cast<uint8_t>(v);
+        }
+      }
+  }
+
+  uint8_t pred_y[256];
+  uint8_t pred_c[2][64];
+
+  // ---- Intra_4x4 (8.3.1.2) for luma4x4BlkIdx k, reading the picture
+  VTS_HD void intra4x4(int k, int mode, uint32_t done) {
+    const int bx = blk_x(k), by = blk_y(k);
+    const int x0 = mx * 16 + bx * 4, y0 = my * 16 + by * 4;
+    // availability of p[x,-1] (x=0..3 and 4..7), p[-1,y], p[-1,-1]
+    auto avail = [&](int xN, int yN) -> bool {  // MB-relative luma location
+      int dx = xN < 0 ? -1 : (xN > 15 ? 1 : 0), dy = yN < 0 ? -1 : 0;
+      if (yN > 15 || (xN > 15 && yN >= 0)) return false;
+      if (dx == 0 && dy == 0) {
+        const int r = (yN / 4) * 4 + xN / 4;
+        return (done >> r) & 1u;
+      }
+      return intra_nb(nb_addr(dx, dy));
+    };
+    const bool top = avail(bx * 4, by * 4 - 1);
+    const bool tr = avail(bx * 4 + 4, by * 4 - 1);
+    const bool left = avail(bx * 4 - 1, by * 4);
+    const bool tl = avail(bx * 4 - 1, by * 4 - 1);
+    int T[9], L[5];  // T[0] = L[0] = p[-1,-1]; T[1+x], L[1+y]
+    T[0] = L[0] = tl ? ly(x0 - 1, y0 - 1) : 0;
+    for (int x = 0; x < 4; ++x) T[1 + x] = top ? ly(x0 + x, y0 - 1) : 0;
+    for (int x = 4; x < 8; ++x) T[1 + x] = tr ? ly(x0 + x, y0 - 1) : T[4];
+    for (int y = 0; y < 4; ++y) L[1 + y] = left ? ly(x0 - 1, y0 + y) : 0;
+#define PT(x) T[1 + (x)]
+#define PL(y) L[1 + (y)]
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) {
+        int v;
+        switch (mode) {
+          case 0: v = PT(x); break;
+          case 1: v = PL(y); break;
+          case 2:
+            if (top && left) v = (PT(0) + PT(1) + PT(2) + PT(3) + PL(0) + PL(1) + PL(2) + PL(3) + 4) >> 3;
+            else if (left) v = (PL(0) + PL(1) + PL(2) + PL(3) + 2) >> 2;
+            else if (top) v = (PT(0) + PT(1) + PT(2) + PT(3) + 2) >> 2;
+            else v = 128;
+            break;
+          case 3:
+            v = (x == 3 && y == 3) ? (PT(6) + 3 * PT(7) + 2) >> 2
+                                   : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
+            break;
+          case 4:
+            if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
+            else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
+            else v = (PT(0) + 2 * PT(-1) + PL(0) + 2) >> 2;
+            break;
+          case 5: {
+            const int z = 2 * x - y;
+            if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+            else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+            else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+            else v = (PL(y - 1) + 2 * PL(y - 2) + PL(y - 3) + 2) >> 2;
+            break;
+          }
+          case 6: {
+            const int z = 2 * y - x;
+            if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+            else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+            else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+            else v = (PT(x - 1) + 2 * PT(x - 2) + PT(x - 3) + 2) >> 2;
+            break;
+          }
+          case 7:
+            v = (y & 1) ? (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2
+                        : (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1;
+            break;
+          default: {
+            const int z = x + 2 * y;
+            if (z == 0 || z == 2 || z == 4) v = (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
+            else if (z == 1 || z == 3) v = (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
+            else if (z == 5) v = (PL(2) + 3 * PL(3) + 2) >> 2;
+            else v = PL(3);
+            break;
+          }
+        }
+        pred_y[(by * 4 + y) * 16 + bx * 4 + x] = static_cast<uint8_t>(v);
+      }
+#undef PT
+#undef PL
+  }
+
+  // ---- Intra_16x16 (8.3.3) and chroma (8.3.4) predictions
+  VTS_HD void intra16(int mode) {
+    const bool la = intra_nb(nb_addr(-1, 0)), ta = intra_nb(nb_addr(0, -1)), ca = intra_nb(nb_addr(-1, -1));
+    const int x0 = mx * 16, y0 = my * 16;
+    int T[17], L[17];
+    T[0] = L[0] = ca ? ly(x0 - 1, y0 - 1) : 0;
+    for (int i = 0; i < 16; ++i) {
+      T[1 + i] = ta ? ly(x0 + i, y0 - 1) : 0;
+      L[1 + i] = la ? ly(x0 - 1, y0 + i) : 0;
+    }
+    int dc = 128, a = 0, b = 0, cc = 0;
+    if (mode == 2) {
+      int st = 0, sl = 0;
+      for (int i = 0; i < 16; ++i) {
+        st += T[1 + i];
+        sl += L[1 + i];
+      }
+      dc = (ta && la) ? (st + sl + 16) >> 5 : (la ? (sl + 8) >> 4 : (ta ? (st + 8) >> 4 : 128));
+    } else if (mode == 3) {
+      int Hh = 0, Vv = 0;
+      for (int i = 0; i < 8; ++i) {
+        Hh += (i + 1) * (T[1 + 8 + i] - T[1 + 6 - i]);
+        Vv += (i + 1) * (L[1 + 8 + i] - L[1 + 6 - i]);
+      }
+      a = 16 * (L[16] + T[16]);
+      b = (5 * Hh + 32) >> 6;
+      cc = (5 * Vv + 32) >> 6;
+    }
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) {
+        int v;
+        if (mode == 0) v = T[1 + x];
+        else if (mode == 1) v = L[1 + y];
+        else if (mode == 2) v = dc;
+        else v = clip1((a + b * (x - 7) + cc * (y - 7) + 16) >> 5);
+        pred_y[y * 16 + x] = static_cast<uint8_t>(v);
+      }
+  }
+  VTS_HD void intra_chroma(int mode) {
+    const bool la = intra_nb(nb_addr(-1, 0)), ta = intra_nb(nb_addr(0, -1)), ca = intra_nb(nb_addr(-1, -1));
+    const int x0 = mx * 8, y0 = my * 8;
+    for (int pl = 0; pl < 2; ++pl) {
+      int T[9], L[9];
+      T[0] = L[0] = ca ? lc(pl, x0 - 1, y0 - 1) : 0;
+      for (int i = 0; i < 8; ++i) {
+        T[1 + i] = ta ? lc(pl, x0 + i, y0 - 1) : 0;
+        L[1 + i] = la ? lc(pl, x0 - 1, y0 + i) : 0;
+      }
+      int a = 0, b = 0, cc = 0;
+      if (mode == 3) {
+        int Hh = 0, Vv = 0;
+        for (int i = 0; i < 4; ++i) {
+          Hh += (i + 1) * (T[1 + 4 + i] - T[1 + 2 - i]);
+          Vv += (i + 1) * (L[1 + 4 + i] - L[1 + 2 - i]);
+        }
+        a = 16 * (L[8] + T[8]);
+        b = (34 * Hh + 32) >> 6;
+        cc = (34 * Vv + 32) >> 6;
+      }
+      for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) {
+          int v = 128;
+          if (mode == 0) {
+            const int xo = x & 4, yo = y & 4;
+            int st = 0, sl = 0;
+            for (int i = 0; i < 4; ++i) {
+              st += T[1 + xo + i];
+              sl += L[1 + yo + i];
+            }
+            if ((xo == 0 && yo == 0) || (xo && yo)) {
+              if (ta && la) v = (st + sl + 4) >> 3;
+              else if (la) v = (sl + 2) >> 2;
+              else if (ta) v = (st + 2) >> 2;
+            } else if (xo) {
+              if (ta) v = (st + 2) >> 2;
+              else if (la) v = (sl + 2) >> 2;
+            } else {
+              if (la) v = (sl + 2) >> 2;
+              else if (ta) v = (st + 2) >> 2;
+            }
+          } else if (mode == 1) {
+            v = L[1 + y];
+          } else if (mode == 2) {
+            v = T[1 + x];
+          } else {
+            v = clip1((a + b * (x - 3) + cc * (y - 3) + 16) >> 5);
+          }
+          pred_c[pl][y * 8 + x] = static_cast<uint8_t>(v);
+        }
+    }
+  }
+
+  // write luma 4x4 block (raster b) = clip(pred + residual)
+  VTS_HD VTS_INLINE void put_luma(int b, const int *res) {
+    const int bx = (b & 3) * 4, by = (b >> 2) * 4;
+    uint8_t *d = Y + static_cast<int64_t>(my * 16 + by) * c.pitch + mx * 16 + bx;
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) d[static_cast<int64_t>(y) * c.pitch + x] = static_cast<uint8_t>(clip1(pred_y[(by + y) * 16 + bx + x] + res[y * 4 + x]));
+  }
+
+  VTS_HD void luma_residual_block(int b, int qp, bool i16, const int *dcy, int *res) {
+    int cf[16];
+    const int k = ((b >> 3) << 3) | (((b & 3) >> 1) << 2) | (((b >> 2) & 1) << 1) | (b & 1);  // luma4x4BlkIdx
+    load_block(kBlkLuma0 + k, cf);
+    if (i16) cf[0] = dcy[b];
+    scale_idct4(cf, qp, i16, res);
+  }
+
+  VTS_HD void chroma_residual(int qpy) {
+    for (int pl = 0; pl < 2; ++pl) {
+      const int qpc = qpc_of(qpy, pl ? c.cqp_off2 : c.cqp_off);
+      int dcl[16];
+      load_block(kBlkChromaDc0 + pl, dcl);
+      const int c0 = dcl[0], c1 = dcl[1], c2 = dcl[2], c3 = dcl[3];
+      const int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+      const int ls = level_scale(qpc % 6, 0, 0);
+      for (int k = 0; k < 4; ++k) {
+        int cf[16], r[16];
+        load_block(kBlkChromaAc0 + 4 * pl + k, cf);
+        cf[0] = ((f[k] * ls) << (qpc / 6)) >> 5;
+        scale_idct4(cf, qpc, true, r);
+        const int bx = (k & 1) * 4, by = (k >> 1) * 4;
+        for (int y = 0; y < 4; ++y)
+          for (int x = 0; x < 4; ++x)
+            UV[static_cast<int64_t>(my * 8 + by + y) * c.pitch + 2 * (mx * 8 + bx + x) + pl] =
+                static_cast<uint8_t>(clip1(pred_c[pl][(by + y) * 8 + bx + x] + r[y * 4 + x]));
+      }
+    }
+  }
+
+  VTS_HD void run() {
+    if (m.epoch != c.epoch) {
+      err |= DEC_E_MISSING_MB;
+      return;
+    }
+    const int qp = m.qp;
+    if (m.type == kMbPcm) {
+      const int16_t *s = c.arena + 16 * static_cast<int64_t>(m.coef);
+      const uint8_t *b = reinterpret_cast<const uint8_t *>(s);
+      for (int y = 0; y < 16; ++y)
+        for (int x = 0; x < 16; ++x) Y[static_cast<int64_t>(my * 16 + y) * c.pitch + mx * 16 + x] = b[y * 16 + x];
+      for (int pl = 0; pl < 2; ++pl)
+        for (int y = 0; y < 8; ++y)
+          for (int x = 0; x < 8; ++x)
+            UV[static_cast<int64_t>(my * 8 + y) * c.pitch + 2 * (mx * 8 + x) + pl] = b[256 + 64 * pl + y * 8 + x];
+      return;
+    }
+    int res[16];
+    const int dummy_dc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (m.type == kMbInter || m.type == kMbSkip) {
+      for (int b = 0; b < 16; ++b) {
+        const int rs = m.ref_slot[(b >> 3) * 2 + ((b & 3) >> 1)];
+        if (rs < 0) {
+          err |= DEC_E_NO_REF;
+          return;
+        }
+        inter_block(b);
+      }
+      for (int b = 0; b < 16; ++b) {
+        luma_residual_block(b, qp, false, dummy_dc, res);
+        put_luma(b, res);
+      }
+    } else if (m.type == kMbI4x4) {
+      uint32_t done = 0;
+      for (int k = 0; k < 16; ++k) {
+        const int b = blk_y(k) * 4 + blk_x(k);
+        intra4x4(k, (m.i4[b >> 1] >> ((b & 1) * 4)) & 15, done);
+        luma_residual_block(b, qp, false, dummy_dc, res);
+        put_luma(b, res);
+        done |= 1u << b;
+      }
+    } else {
+      intra16(m.modes & 3);
+      // 8.5.10: Intra16x16 DC, Hadamard + scaling
+      int dcl[16], t[16], dcy[16];
+      load_block(kBlkI16Dc, dcl);
+      for (int i = 0; i < 4; ++i) {
+        const int a0 = dcl[i * 4], a1 = dcl[i * 4 + 1], a2 = dcl[i * 4 + 2], a3 = dcl[i * 4 + 3];
+        t[i * 4] = a0 + a1 + a2 + a3;
+        t[i * 4 + 1] = a0 + a1 - a2 - a3;
+        t[i * 4 + 2] = a0 - a1 - a2 + a3;
+        t[i * 4 + 3] = a0 - a1 + a2 - a3;
+      }
+      const int ls = level_scale(qp % 6, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        const int a0 = t[j], a1 = t[4 + j], a2 = t[8 + j], a3 = t[12 + j];
+        const int f[4] = {a0 + a1 + a2 + a3, a0 + a1 - a2 - a3, a0 - a1 - a2 + a3, a0 - a1 + a2 - a3};
+        for (int i = 0; i < 4; ++i)
+          dcy[i * 4 + j] = qp >= 36 ? (f[i] * ls) << (qp / 6 - 6) : (f[i] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+      }
+      for (int b = 0; b < 16; ++b) {
+        luma_residual_block(b, qp, true, dcy, res);
+        put_luma(b, res);
+      }
+    }
+    if (m.type != kMbInter && m.type != kMbSkip) intra_chroma((m.modes >> 2) & 3);
+    chroma_residual(qp);
+  }
+};
+
+// ---------------------------------------------------------- deblocking (8.7)
+VTS_HD VTS_INLINE bool mb_is_intra(const MbRec &r) { return r.type == kMbI4x4 || r.type == kMbI16 || r.type == kMbPcm; }
+
+VTS_HD VTS_INLINE int bs_of(const MbRec &p, int bp, const MbRec &q, int bq, bool mb_edge) {
+  if (mb_is_intra(p) || mb_is_intra(q)) return mb_edge ? 4 : 3;
+  if (p.nz[bp] || q.nz[bq]) return 2;
+  const int p8 = (bp >> 3) * 2 + ((bp & 3) >> 1), q8 = (bq >> 3) * 2 + ((bq & 3) >> 1);
+  if (p.ref_slot[p8] != q.ref_slot[q8]) return 1;
+  if (iabs(p.mv[bp][0] - q.mv[bq][0]) >= 4 || iabs(p.mv[bp][1] - q.mv[bq][1]) >= 4) return 1;
+  return 0;
+}
+
+// one line across an edge: s[k * step], k = -4..3 (p3..q3)
+VTS_HD VTS_INLINE void filter_line(uint8_t *s, int64_t step, int bS, bool chroma, int iA, int alpha, int beta) {
+  const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
+  if (!(bS > 0 && iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
+  if (bS < 4) {
+    const int tc0 = kTc[iA][bS - 1];
+    if (chroma) {
+      const int tc = tc0 + 1;
+      const int delta = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+      s[-step] = static_cast<uint8_t>(clip1(p0 + delta));
+      s[0] = static_cast<uint8_t>(clip1(q0 - delta));
+      return;
+    }
+    const int p2 = s[-3 * step], q2 = s[2 * step];
+    const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
+    const int tc = tc0 + (ap < beta) + (aq < beta);
+    const int delta = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+    s[-step] = static_cast<uint8_t>(clip1(p0 + delta));
+    s[0] = static_cast<uint8_t>(clip1(q0 - delta));
+    if (ap < beta) s[-2 * step] = static_cast<uint8_t>(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
+    if (aq < beta) s[step] = static_cast<uint8_t>(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+    return;
+  }
+  if (chroma) {
+    s[-step] = static_cast<uint8_t>((2 * p1 + p0 + q1 + 2) >> 2);
+    s[0] = static_cast<uint8_t>((2 * q1 + q0 + p1 + 2) >> 2);
+    return;
+  }
+  const int p2 = s[-3 * step], q2 = s[2 * step], p3 = s[-4 * step], q3 = s[3 * step];
+  const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
+  const bool small = iabs(p0 - q0) < ((alpha >> 2) + 2);
+  if (ap < beta && small) {
+    s[-step] = static_cast<uint8_t>((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+    s[-2 * step] = static_cast<uint8_t>((p2 + p1 + p0 + q0 + 2) >> 2);
+    s[-3 * step] = static_cast<uint8_t>((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+  } else {
+    s[-step] = static_cast<uint8_t>((2 * p1 + p0 + q1 + 2) >> 2);
+  }
+  if (aq < beta && small) {
+    s[0] = static_cast<uint8_t>((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+    s[step] = static_cast<uint8_t>((p0 + q0 + q1 + q2 + 2) >> 2);
+    s[2 * step] = static_cast<uint8_t>((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+  } else {
+    s[0] = static_cast<uint8_t>((2 * q1 + q0 + p1 + 2) >> 2);
+  }
+}
+
+// Deblock macroblock `a` of the frame in `slot` (all of its edges, 8.7)
+VTS_HD inline void deblock_mb(const ReconCtx &c, int slot, int a) {
+  const MbRec &q = c.recs[a];
+  const FullSlice &sd = c.slices[q.slice];
+  if (sd.dbk_idc == 1) return;
+  const int mx = a % c.mbw, my = a / c.mbw;
+  bool left = mx > 0, top = my > 0;
+  if (sd.dbk_idc == 2) {
+    if (left && c.recs[a - 1].slice != q.slice) left = false;
+    if (top && c.recs[a - c.mbw].slice != q.slice) top = false;
+  }
+  uint8_t *Y = c.surf + static_cast<int64_t>(slot) * c.frame_stride;
+  uint8_t *UV = Y + c.uv_off;
+  for (int dir = 0; dir < 2; ++dir)
+    for (int e = 0; e < 4; ++e) {
+      if (e == 0 && !(dir ? top : left)) continue;
+      const MbRec &p = e == 0 ? c.recs[dir ? a - c.mbw : a - 1] : q;
+      const int qpp = p.type == kMbPcm ? 0 : p.qp, qpq = q.type == kMbPcm ? 0 : q.qp;
+      {
+        const int qpav = (qpp + qpq + 1) >> 1;
+        const int iA = clip3(0, 51, qpav + sd.dbk_a), iB = clip3(0, 51, qpav + sd.dbk_b);
+        const int alpha = kAl[iA], beta = kBe[iB];
+        if (alpha && beta)
+          for (int k = 0; k < 16; ++k) {
+            const int xq = dir ? k : 4 * e, yq = dir ? 4 * e : k;
+            const int xp = dir ? xq : (xq + 15) & 15, yp = dir ? (yq + 15) & 15 : yq;
+            const int bS = bs_of(p, (yp >> 2) * 4 + (xp >> 2), q, (yq >> 2) * 4 + (xq >> 2), e == 0);
+            uint8_t *s = Y + static_cast<int64_t>(my * 16 + yq) * c.pitch + mx * 16 + xq;
+            filter_line(s, dir ? c.pitch : 1, bS, false, iA, alpha, beta);
+          }
+      }
+      if (e == 0 || e == 2)
+        for (int pl = 0; pl < 2; ++pl) {
+          const int off = pl ? c.cqp_off2 : c.cqp_off;
+          const int qpav = (qpc_of(qpp, off) + qpc_of(qpq, off) + 1) >> 1;
+          const int iA = clip3(0, 51, qpav + sd.dbk_a), iB = clip3(0, 51, qpav + sd.dbk_b);
+          const int alpha = kAl[iA], beta = kBe[iB];
+          if (!alpha || !beta) continue;
+          for (int k = 0; k < 8; ++k) {
+            const int xq = dir ? 2 * k : 4 * e, yq = dir ? 4 * e : 2 * k;
+            const int xp = dir ? xq : (xq + 15) & 15, yp = dir ? (yq + 15) & 15 : yq;
+            const int bS = bs_of(p, (yp >> 2) * 4 + (xp >> 2), q, (yq >> 2) * 4 + (xq >> 2), e == 0);
+            const int cx = dir ? k : 2 * e, cy = dir ? 2 * e : k;
+            uint8_t *s = UV + static_cast<int64_t>(my * 8 + cy) * c.pitch + 2 * (mx * 8 + cx) + pl;
+            filter_line(s, dir ? c.pitch : 2, bS, true, iA, alpha, beta);
+          }
+        }
+    }
+}
+
+}  // namespace full
+}  // namespace vts
