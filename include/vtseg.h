@@ -252,6 +252,12 @@ typedef struct vts_params {
                               last frame in HBM (the next block's reference);
                               1 = store every decoded frame (vts_get_frame_nv12
                               of any frame; the transcoder sets it itself)  */
+  int32_t decoder;         /* 0 auto: the I_PCM / integer-motion subset kernels
+                              when the stream's headers allow, else (or when
+                              the device parser meets syntax outside the
+                              subset) the general CAVLC decoder; 1 subset
+                              only; 2 general              */
+  int32_t _pad;
 } vts_params;
 
 /* Demux the file's first H.264 video track on the host (MP4 boxes and NAL
@@ -292,7 +298,7 @@ int vts_get_thumbnail_rgb(vts_ctx *ctx, int64_t frame, uint8_t *out,
 int vts_last_timings(const vts_ctx *ctx, double *ms4);
 /* Decode schedule facts: what = 0 reconstruct launches per run, 1 windows,
  * 2 slices, 3 ring frames, 4 fused scoring (1/0); < 0 on error. */
-int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);
+int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);  /* 8: general decoder in use (1/0) */
 int vts_close(vts_ctx *ctx);
 
 /* ------------------------------- upload transcode (360p)

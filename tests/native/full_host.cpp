@@ -91,7 +91,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     d.arena = arena_blocks;
     d.arena_cap = static_cast<uint32_t>(cap);
     arena_blocks += static_cast<uint32_t>(cap);
-    for (int r = 0; r < 32; ++r) d.ref_slot[r] = static_cast<int8_t>(s.ref[r] >= 0 ? s.ref[r] : -1);
+    for (int r = 0; r < 32; ++r) d.ref_slot[r] = static_cast<int16_t>(s.ref[r] >= 0 ? s.ref[r] : -1);
   }
   std::vector<int16_t> arena(static_cast<size_t>(arena_blocks) * 16 + 16);
   FullParams P{};

@@ -1,0 +1,119 @@
+"""General device decoder (decode_full.hip) vs the oracle (h264_full_oracle.c).
+
+Full-syntax streams (coding="full": intra 4x4 / 16x16 / chroma modes,
+residual blocks, quarter-sample partitions over up to 3 references, list
+modification, non-reference pictures, QP changes, the deblocking filter with
+idc 0/1/2 and offsets): every decoded frame, histogram, SAD, score and RGB
+thumbnail must equal the oracle's bit for bit.  The subset streams must also
+decode identically on the general path (decoder="general").  Parity of the
+pictures themselves against a third-party decoder is unpinned (none in the
+image); the product's decoding code is the same as the CPU harness checked in
+tests/test_full_host.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+from vtseg import VtsegError, scene
+
+pytestmark = pytest.mark.gpu
+
+
+def _require_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test requires an MI355X")
+
+
+def _first_diff(a, b):
+    bad = np.nonzero((a != b).reshape(a.shape[0], -1).any(1))[0]
+    return bad[:8].tolist()
+
+
+FULL = [
+    ("tiny", dict(width=48, height=32, max_motion=2)),
+    ("qvga", dict(width=320, height=240, max_motion=3)),
+    ("ragged", dict(width=336, height=200, slices_per_row=3, max_motion=6)),
+    ("oneslice", dict(width=320, height=240, slices_per_row=0, max_motion=8)),
+    ("cip", dict(width=320, height=240, max_motion=3, constrained_intra=True)),
+    ("crop", dict(width=480, height=270, slices_per_row=2, max_motion=4)),
+    ("hd720", dict(width=1280, height=720, slices_per_row=0, max_motion=6)),
+]
+
+
+@pytest.mark.parametrize("name,kw", FULL, ids=[f[0] for f in FULL])
+def test_general_decoder_bit_exact(tmp_path, name, kw):
+    _require_gpu()
+    n = 24 if kw["height"] >= 720 else 48
+    path = tmp_path / f"{name}.mp4"
+    scene.synth_write(path, n_frames=n, cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.7,
+                      coding="full", seed=31, **kw)
+    frames, _ = oracle.decode_full(path)
+    W, H = kw["width"], kw["height"]
+    k = 4 if H <= 720 else 6
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, k)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+        assert _first_diff(got, frames) == []
+        rgb = np.stack([v.thumbnail_rgb(i) for i in range(n)]).reshape(-1)
+        assert np.array_equal(rgb, ref["rgb"])
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+        res2 = v.score()   # a second run over the same rings (record epochs)
+        assert np.array_equal(res2.scores, res.scores)
+
+
+def test_general_decoder_windows_and_rings(tmp_path):
+    """Many small windows on two rings / two streams equal one window."""
+    _require_gpu()
+    n = 150
+    path = tmp_path / "w.mp4"
+    scene.synth_write(path, width=320, height=240, n_frames=n, cut_min_s=0.5, cut_max_s=1.5,
+                      gop_max_s=0.5, coding="full", seed=5)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 320, 240, 320, 240, 4)
+    with scene.VideoScorer(path, window_frames=30, n_streams=2) as v:
+        assert v.general() and v.windows() >= 4
+        res = v.score()
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+        assert np.array_equal(v.frame_nv12(n - 1).reshape(frames[-1].shape), frames[-1])
+
+
+@pytest.mark.parametrize("kw", [dict(width=320, height=240, max_motion=4),
+                                dict(width=336, height=200, slices_per_row=3, max_motion=6,
+                                     odd_motion=True),
+                                dict(width=160, height=96, max_motion=4, gop_max_s=0.3,
+                                     nonref_refresh=True)])
+def test_subset_streams_on_the_general_path(tmp_path, kw):
+    _require_gpu()
+    kw = dict(kw)
+    gop = kw.pop("gop_max_s", 0.8)
+    path = tmp_path / "s.mp4"
+    scene.synth_write(path, n_frames=60, cut_min_s=0.5, cut_max_s=1.5, gop_max_s=gop, **kw)
+    with scene.VideoScorer(path) as a:
+        assert not a.general()
+        want = a.score()
+    with scene.VideoScorer(path, decoder="general", keep_frames=True) as b:
+        assert b.general()
+        got = b.score()
+        frames, _ = oracle.decode_full(path)
+        assert np.array_equal(b.frame_nv12(59).reshape(frames[-1].shape), frames[-1])
+    assert np.array_equal(got.hist, want.hist)
+    assert np.array_equal(got.sad, want.sad)
+    assert np.array_equal(got.scores, want.scores)
+
+
+def test_subset_only_decoder_refuses_full_syntax(tmp_path):
+    _require_gpu()
+    path = tmp_path / "f.mp4"
+    scene.synth_write(path, width=64, height=48, n_frames=10, coding="full")
+    with scene.VideoScorer(path, decoder="subset") as v:
+        with pytest.raises(VtsegError):
+            v.score()

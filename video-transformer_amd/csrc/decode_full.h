@@ -1,0 +1,45 @@
+// decode_full.h — host <-> device interface of the general decoder kernels
+// (decode_full.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "h264_full.h"
+
+namespace vts {
+
+struct FullParseArgs {
+  const uint8_t *es;         // device elementary stream (+ padding)
+  const FullSlice *slices;   // this launch's slices
+  int32_t n_slices;
+  int32_t slice0;            // window index of slices[0] (MbRec.slice)
+  uint32_t epoch;
+  int32_t _pad;
+  MbRec *recs;               // ring: [slot][mb]
+  int16_t *arena;            // ring's coefficient arena
+  uint32_t *err;
+  FullParams P;
+};
+
+struct FullReconArgs {
+  const int4 *frames;        // (slot, -, -, -) per picture of the launch
+  const MbRec *recs;
+  const int16_t *arena;
+  const FullSlice *slices;   // the window's slices (MbRec.slice indexes them)
+  uint8_t *surf;             // ring of NV12 pictures
+  int64_t frame_stride;
+  int64_t uv_off;            // UV plane offset in a picture (pitch * coded height)
+  int32_t pitch;
+  uint32_t epoch;
+  int32_t deblock;           // 1: run the deblocking kernel after reconstruction
+  int32_t _pad;
+  uint32_t *err;
+  FullParams P;
+};
+
+int parse_full_launch(const FullParseArgs &a, hipStream_t s);
+// reconstruction (+ deblocking) of n_frames pictures of one level
+int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);
+
+}  // namespace vts

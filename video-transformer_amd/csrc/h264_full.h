@@ -30,7 +30,7 @@ struct FullSlice {
   uint32_t arena_cap;   // blocks reserved: min(27 x MBs, 3 x NAL bytes + 27) bounds
                         // what CAVLC can code (a stored block costs >= 3 bits)
   int32_t _pad;
-  int8_t ref_slot[32];  // RefPicList0[i] -> ring slot (-1: no reference picture)
+  int16_t ref_slot[32]; // RefPicList0[i] -> ring slot (-1: no reference picture)
 };
 
 struct FullParams {
@@ -69,7 +69,7 @@ struct alignas(16) MbRec {
   uint8_t cbp;          // coded_block_pattern
   uint8_t modes;        // bits 0-1 Intra16x16PredMode, bits 2-3 intra_chroma_pred_mode
   int8_t ref[4];        // RefPicList0 index per 8x8 (-1: intra)
-  int8_t ref_slot[4];   // its ring slot (the picture identity the deblocking bS compares)
+  int16_t ref_slot[4];  // its ring slot (the picture identity the deblocking bS compares)
   uint8_t i4[8];        // Intra4x4PredMode of raster 4x4 block b: nibble (b & 1) of byte b >> 1
   uint8_t nz[16];       // total_coeff of raster luma 4x4 blocks (16 for I_PCM)
   uint8_t nzc[8];       // chroma AC total_coeff: Cb raster 0-3, Cr raster 0-3

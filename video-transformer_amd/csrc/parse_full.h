@@ -387,7 +387,7 @@ struct Parser {
     sc->cur.mv[b][1] = static_cast<int16_t>(mvy);
     const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
     sc->cur.ref[p8] = static_cast<int8_t>(ref);
-    sc->cur.ref_slot[p8] = s->ref_slot[ref];
+    sc->cur.ref_slot[p8] = s->ref_slot[ref & 31];
   }
 
   VTS_HD void skip_mb(int addr, int qp) {

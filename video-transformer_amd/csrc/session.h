@@ -8,6 +8,7 @@
 #include "common.h"
 #include "decode.h"
 #include "h264.h"
+#include "h264_full.h"
 
 #define HIP_TRY(expr)                                                              \
   do {                                                                             \
@@ -34,6 +35,7 @@ struct Window {
   bool tb = false;
   std::vector<int64_t> tb_off;
   std::vector<int32_t> tb_cnt, tb_L;
+  int64_t fs0 = 0, fs1 = 0;        // general decoder: slices [fs0, fs1) of vts_ctx::fslices
 };
 
 // Downscaled copy of every decoded frame (transcode.hip), filled by run_all
@@ -119,12 +121,34 @@ struct vts_ctx {
   bool have_results = false;
   std::vector<float> host_scores;
   vts::SmallStore small;       // transcode: downscaled frames (off unless vts_transcode ran)
+  // ---- general decoder (decode_full.hip, session_full.hip)
+  bool general = false;
+  vts::FullParams fprm{};
+  std::vector<vts::FullSlice> fslices;  // every window's slices (window-relative slots, arena)
+  vts::FullSlice *d_fslices = nullptr;
+  vts::MbRec *d_recs[2] = {nullptr, nullptr};
+  int16_t *d_arena[2] = {nullptr, nullptr};
+  int64_t arena_blocks = 0;             // per ring
+  // kept from open for a later switch to the general decoder (decoder = auto)
+  std::vector<int64_t> es_off;          // sample offsets in the ES buffer
+  std::vector<uint32_t> sample_size;
+  int nal_length_size = 4;
+  std::vector<uint8_t> sps_nal, pps_nal;
 };
 
 namespace vts {
 // Decode + score every window (and downscale when ctx->small.on).
 int run_all(vts_ctx *c);
 int fetch_scores(vts_ctx *c);
+// general decoder: schedule + buffers from the host ES (session_full.hip);
+// `sps_nal` / `pps_nal` are the avcC parameter sets
+int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+                  const std::vector<uint32_t> &sizes, int nal_length_size, const std::vector<uint8_t> &sps_nal,
+                  const std::vector<uint8_t> &pps_nal);
+int run_general(vts_ctx *c);
+// cheap look at the stream's first pictures: does it need the general decoder?
+bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+                   const std::vector<uint32_t> &sizes, int nal_length_size);
 // downscale the window's frames (transcode.hip)
 int small_window(vts_ctx *c, int ring, int64_t f0, int64_t f1, hipStream_t s);
 }  // namespace vts

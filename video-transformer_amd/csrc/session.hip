@@ -81,6 +81,89 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
   return VTS_OK;
 }
 
+// Device buffers of the general decoder (the ES is uploaded when host_es is
+// given, else already resident).
+int alloc_general(vts_ctx *c, const uint8_t *host_es) {
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->d_es) {
+    HIP_TRY(hipMalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
+    HIP_TRY(hipMemcpy(c->d_es, host_es, static_cast<size_t>(c->es_bytes), hipMemcpyHostToDevice));
+  }
+  HIP_TRY(hipMalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
+  if (!c->fslices.empty())
+    HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_levels, sizeof(int4) * std::max<size_t>(1, c->level_frames.size())));
+  HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(), hipMemcpyHostToDevice));
+  const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
+  c->ws_bytes = score_workspace_bytes(c->width, c->height, c->k, c->ring_frames);
+  const int64_t tw = (c->width / c->k) * (c->height / c->k);
+  for (int r = 0; r < c->n_rings; ++r) {
+    HIP_TRY(hipMalloc(&c->d_recs[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec)));
+    HIP_TRY(hipMalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
+    HIP_TRY(hipMalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
+    HIP_TRY(hipMalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
+    c->ring_cleared_at[r] = -1;
+  }
+  if (!c->d_last[0])
+    for (int r = 0; r < 2; ++r) HIP_TRY(hipMalloc(&c->d_last[r], static_cast<size_t>(tw + kPad)));
+  if (!c->d_err) HIP_TRY(hipMalloc(&c->d_err, sizeof(uint32_t)));
+  if (!c->d_score) HIP_TRY(hipMalloc(&c->d_score, sizeof(float) * c->n_frames));
+  if (!c->d_sad) HIP_TRY(hipMalloc(&c->d_sad, sizeof(uint64_t) * c->n_frames));
+  if (!c->d_hist) HIP_TRY(hipMalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
+  c->thumb_px = tw;
+  if (!c->d_rgb) HIP_TRY(hipMalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
+  if (!c->s_dec) HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
+  if (!c->s_score) HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
+  if (!c->s_parse) HIP_TRY(hipStreamCreateWithFlags(&c->s_parse, hipStreamNonBlocking));
+  for (auto e2 : c->ev)
+    if (e2) (void)hipEventDestroy(e2);
+  c->ev.assign(c->windows.size() * 6, nullptr);
+  for (auto &e2 : c->ev) HIP_TRY(hipEventCreate(&e2));
+  if (!c->ev_start) HIP_TRY(hipEventCreate(&c->ev_start));
+  if (!c->ev_end) HIP_TRY(hipEventCreate(&c->ev_end));
+  return VTS_OK;
+}
+
+// decoder = auto: the subset kernels met syntax outside their subset; rebuild
+// the schedule for the general decoder from the resident ES.
+int switch_to_general(vts_ctx *c) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<uint8_t> es(static_cast<size_t>(c->es_bytes));
+  HIP_TRY(hipMemcpy(es.data(), c->d_es, es.size(), hipMemcpyDeviceToHost));
+  auto f = [](void *p) {
+    if (p) (void)hipFree(p);
+  };
+  for (int r = 0; r < 2; ++r) {
+    f(c->d_cmd[r]);
+    f(c->d_thumb[r]);
+    f(c->d_surf[r]);
+    f(c->d_ws[r]);
+    c->d_cmd[r] = nullptr;
+    c->d_thumb[r] = nullptr;
+    c->d_surf[r] = nullptr;
+    c->d_ws[r] = nullptr;
+  }
+  f(c->d_tb);
+  f(c->d_post);
+  f(c->d_slices);
+  f(c->d_levels);
+  c->d_tb = nullptr;
+  c->d_post = nullptr;
+  c->d_slices = nullptr;
+  c->d_levels = nullptr;
+  for (auto e2 : c->lev)
+    if (e2) (void)hipEventDestroy(e2);
+  c->lev.clear();
+  c->windows.clear();
+  c->level_frames.clear();
+  c->slices.clear();
+  c->post_slots.clear();
+  c->tb_chains.clear();
+  VTS_TRY(build_general(c, es, c->es_off, c->sample_size, c->nal_length_size, c->sps_nal, c->pps_nal));
+  return alloc_general(c, nullptr);
+}
+
 int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, const char *path) {
   // interleaved GOP groups per reconstruct level (VTS_RECON_GROUPS, 1..4)
   if (const char *s = std::getenv("VTS_RECON_GROUPS"))
@@ -138,6 +221,19 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   std::vector<int64_t> es_off;
   VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off));
   c->es_bytes = static_cast<int64_t>(es.size());
+  c->es_off = es_off;
+  c->sample_size = t.size;
+  c->nal_length_size = t.nal_length_size;
+  c->sps_nal = t.sps[0];
+  c->pps_nal = t.pps[0];
+
+  // General CAVLC decoder (decode_full.hip) when asked, or when the headers
+  // show features outside the subset kernels (deblocking, several references)
+  if (c->params.decoder == 2 ||
+      (c->params.decoder == 0 && wants_general(c, es, es_off, t.size, t.nal_length_size))) {
+    VTS_TRY(build_general(c, es, es_off, t.size, t.nal_length_size, t.sps[0], t.pps[0]));
+    return alloc_general(c, es.data());
+  }
 
   // NAL walk: slice table, intra / reference flags per frame
   const int L = t.nal_length_size;
@@ -495,6 +591,7 @@ int open_common(int device, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_
 }  // namespace
 
 int vts::run_all(vts_ctx *c) {
+  if (c->general) return run_general(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
   HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
@@ -729,6 +826,13 @@ int vts::run_all(vts_ctx *c) {
     return run_all(c);
   }
   for (const Window &w : c->windows) c->tb_ran_sparse |= c->fused && w.tb && !c->tb_off && !keep;
+  // decoder = auto: syntax outside the subset kernels -> the general decoder
+  constexpr uint32_t kSubsetMiss = DEC_E_MB_TYPE | DEC_E_RESIDUAL | DEC_E_SUBPEL | DEC_E_MULTIREF |
+                                   DEC_E_DEBLOCK | DEC_E_REFLIST | DEC_E_MMCO | DEC_E_EPB_IN_PCM;
+  if ((err & kSubsetMiss) && c->params.decoder == 0 && !c->small.on) {
+    VTS_TRY(switch_to_general(c));
+    return run_general(c);
+  }
   if (err) {
     c->have_results = false;
     return fail(VTS_E_DECODE, "device decoder: %s", describe_decode_error(err).c_str());
@@ -899,6 +1003,7 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
       return n;
     }
     case 7: return c->tb_off ? 0 : static_cast<int64_t>(c->tb_chains.size());  // chain slots (levels x chains)
+    case 8: return c->general ? 1 : 0;
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
   }
 }
@@ -933,6 +1038,11 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_rgb);
   f(c->small.d);
   f(c->small.d_taps);
+  f(c->d_fslices);
+  for (int r = 0; r < 2; ++r) {
+    f(c->d_recs[r]);
+    f(c->d_arena[r]);
+  }
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->lev)

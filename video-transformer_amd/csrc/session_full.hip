@@ -1,0 +1,293 @@
+// session_full.hip — the general decoder's schedule and run loop (vts_ctx with
+// general = true).  DESIGN.md §5b.
+//
+// Open: every slice header is parsed on the host (h264_sched.cpp), which also
+// keeps the reference picture bookkeeping, so each slice reaches the device
+// with its RefPicList0 as ring slots.  A picture's level is one more than the
+// highest level among the pictures its lists may name; windows hold whole
+// runs of pictures that start at an intra picture no later picture predicts
+// across (as in the subset path), sized to a ring budget of decoded surfaces,
+// macroblock records and coefficient arena.
+// Run, per window (two rings, decode of window i+1 overlapping scoring of
+// window i): h264_parse_full over the window's slices, then per level
+// h264_recon_full + h264_deblock_full over that level's pictures, then the
+// scoring kernels on the finished pictures (score.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "decode.h"
+#include "decode_full.h"
+#include "h264_sched.h"
+#include "session.h"
+
+namespace vts {
+namespace {
+
+constexpr int64_t kWindowBytes = 48ll << 30;  // per ring, as the subset path
+constexpr int64_t kMinRingBytes = 1ll << 30;
+
+}  // namespace
+
+bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+                   const std::vector<uint32_t> &sizes, int nal_length_size) {
+  if (c->sps.max_num_ref_frames > 1 || c->pps.num_ref_idx_l0_default_active > 1) return true;
+  if (!c->pps.deblocking_filter_control_present) return true;  // deblocking on, offsets 0
+  // the first pictures' slice headers: an active deblocking filter or several references
+  const size_t n = std::min<size_t>(sizes.size(), 3);
+  std::vector<int64_t> off(es_off.begin(), es_off.begin() + static_cast<int64_t>(n));
+  std::vector<uint32_t> sz(sizes.begin(), sizes.begin() + static_cast<int64_t>(n));
+  std::vector<SchedFrame> frames;
+  std::vector<SchedSlice> slices;
+  if (!sched_build(c->sps, c->pps, es.data(), off, sz, nal_length_size, &frames, &slices).empty()) return true;
+  for (const SchedSlice &s : slices)
+    if ((s.dbk_idc != 1 && s.qp + s.dbk_a >= 16) || (s.is_p && s.num_ref > 1)) return true;
+  return false;
+}
+
+int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+                  const std::vector<uint32_t> &sizes, int nal_length_size, const std::vector<uint8_t> &sps_nal,
+                  const std::vector<uint8_t> &pps_nal) {
+  SchedStream facts;
+  std::string e = sched_stream_facts(sps_nal, pps_nal, c->sps, c->pps, &facts);
+  if (!e.empty()) return fail(VTS_E_UNSUPPORTED, "%s", e.c_str());
+  if (c->sps.crop_left || c->sps.crop_top) return fail(VTS_E_UNSUPPORTED, "left/top cropping is not supported");
+  std::vector<SchedFrame> frames;
+  std::vector<SchedSlice> slices;
+  e = sched_build(c->sps, c->pps, es.data(), es_off, sizes, nal_length_size, &frames, &slices);
+  if (!e.empty()) return fail(VTS_E_UNSUPPORTED, "%s", e.c_str());
+  c->general = true;
+  c->fused = false;
+  c->fprm = FullParams{};
+  c->fprm.mb_width = c->sps.mb_width;
+  c->fprm.mb_height = c->sps.mb_height;
+  c->fprm.cip = c->pps.constrained_intra_pred;
+  c->fprm.cqp_off = c->pps.chroma_qp_index_offset;
+  c->fprm.cqp_off2 = facts.cqp_off2;
+  const int64_t n = c->n_frames;
+  const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
+
+  // levels and clean window starts
+  std::vector<int64_t> level(static_cast<size_t>(n), 0), minref(static_cast<size_t>(n), n);
+  for (int64_t f = 0; f < n; ++f) {
+    const SchedFrame &fr = frames[static_cast<size_t>(f)];
+    int64_t l = 0;
+    for (int64_t r : fr.refs) {
+      l = std::max(l, level[static_cast<size_t>(r)] + 1);
+      minref[static_cast<size_t>(f)] = std::min(minref[static_cast<size_t>(f)], r);
+    }
+    level[static_cast<size_t>(f)] = l;
+  }
+  std::vector<uint8_t> clean(static_cast<size_t>(n), 0);
+  {
+    int64_t m = n;
+    for (int64_t x = n - 1; x >= 0; --x) {
+      m = std::min(m, minref[static_cast<size_t>(x)]);
+      clean[static_cast<size_t>(x)] = frames[static_cast<size_t>(x)].intra && m >= x;
+    }
+  }
+  // coefficient blocks each slice may need (CAVLC bound, h264_full.h)
+  std::vector<int64_t> cap(slices.size());
+  int64_t cap_total = 0;
+  for (size_t i = 0; i < slices.size(); ++i) {
+    cap[i] = std::min<int64_t>(27ll * slices[i].n_mbs, 3ll * slices[i].nal_size + 27);
+    cap_total += cap[i];
+  }
+  // windows
+  const int64_t tw_f = static_cast<int64_t>(c->width / c->k) * (c->height / c->k);
+  const int64_t per_frame = c->frame_stride + nmb * static_cast<int64_t>(sizeof(MbRec)) +
+                            score_workspace_bytes(c->width, c->height, c->k, 1) +
+                            32 * ((cap_total + n - 1) / std::max<int64_t>(1, n));
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const int64_t whole = c->es_bytes + n * (3 * tw_f + 1024 + 12) +
+                        static_cast<int64_t>(slices.size()) * static_cast<int64_t>(sizeof(FullSlice)) + (1ll << 30);
+  const int64_t avail = std::max<int64_t>(0, static_cast<int64_t>(free_b) - whole);
+  const int64_t ring_budget = std::min(kWindowBytes, std::max(kMinRingBytes, avail / 4));
+  int64_t wcap;
+  if (c->params.window_frames > 0) wcap = c->params.window_frames;
+  else if (n * per_frame <= std::min(kWindowBytes, avail / 2)) wcap = n;
+  else wcap = std::max<int64_t>(1, ring_budget / per_frame);
+  wcap = std::min<int64_t>(wcap, 32767);  // ring slots are int16 (FullSlice / MbRec ref_slot)
+  auto next_clean = [&](int64_t x) {
+    while (x < n && !clean[static_cast<size_t>(x)]) ++x;
+    return x;
+  };
+  c->windows.clear();
+  for (int64_t f = 0; f < n;) {
+    Window w;
+    w.f0 = f;
+    int64_t end = next_clean(f + 1);
+    while (end < n) {
+      const int64_t nxt = next_clean(end + 1);
+      if (nxt - f > wcap) break;
+      end = nxt;
+    }
+    w.f1 = end;
+    c->windows.push_back(w);
+    f = end;
+  }
+  c->ring_frames = 0;
+  for (const Window &w : c->windows) c->ring_frames = std::max(c->ring_frames, w.f1 - w.f0);
+  c->n_rings = (c->windows.size() > 1 && c->params.n_streams >= 2) ? 2 : 1;
+
+  // per window: device slices (window-relative slots and arena), level lists
+  c->fslices.clear();
+  c->level_frames.clear();
+  c->arena_blocks = 0;
+  for (Window &w : c->windows) {
+    w.fs0 = static_cast<int64_t>(c->fslices.size());
+    int64_t arena = 0, maxl = 0;
+    for (int64_t f = w.f0; f < w.f1; ++f) {
+      const SchedFrame &fr = frames[static_cast<size_t>(f)];
+      maxl = std::max(maxl, level[static_cast<size_t>(f)]);
+      for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
+        const SchedSlice &s = slices[static_cast<size_t>(si)];
+        FullSlice d{};
+        d.nal_offset = s.nal_offset;
+        d.nal_size = s.nal_size;
+        d.slot = static_cast<int32_t>(f - w.f0);
+        d.first_mb = s.first_mb;
+        d.data_byte = s.data_byte;
+        d.data_bit = s.data_bit;
+        d.is_p = s.is_p;
+        d.qp = s.qp;
+        d.num_ref = s.num_ref;
+        d.dbk_idc = s.dbk_idc;
+        d.dbk_a = s.dbk_a;
+        d.dbk_b = s.dbk_b;
+        d.arena = static_cast<uint32_t>(arena);
+        d.arena_cap = static_cast<uint32_t>(cap[static_cast<size_t>(si)]);
+        arena += cap[static_cast<size_t>(si)];
+        for (int i = 0; i < 32; ++i) {
+          const int64_t r = s.ref[i];
+          if (r >= 0 && (r < w.f0 || r >= f)) return fail(VTS_E_UNSUPPORTED, "reference crosses a window boundary");
+          d.ref_slot[i] = static_cast<int16_t>(r >= 0 ? r - w.f0 : -1);
+        }
+        c->fslices.push_back(d);
+      }
+    }
+    if (arena > 0xffffffffll) return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
+    w.fs1 = static_cast<int64_t>(c->fslices.size());
+    c->arena_blocks = std::max(c->arena_blocks, arena);
+    std::vector<std::vector<int4>> lv(static_cast<size_t>(maxl + 1));
+    for (int64_t f = w.f0; f < w.f1; ++f)
+      lv[static_cast<size_t>(level[static_cast<size_t>(f)])].push_back(make_int4(static_cast<int>(f - w.f0), 0, 0, 0));
+    for (auto &l : lv) {
+      if (l.empty()) continue;
+      w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
+      w.lvl_cnt.push_back(static_cast<int32_t>(l.size()));
+      c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
+    }
+  }
+  return VTS_OK;
+}
+
+int run_general(vts_ctx *c) {
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
+  HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
+  HIP_TRY(hipStreamWaitEvent(c->s_score, c->ev_start, 0));
+  hipStream_t sd = c->s_dec;
+  hipStream_t ss = (c->params.n_streams >= 2 && c->windows.size() > 1) ? c->s_score : c->s_dec;
+  const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
+  const size_t nw = c->windows.size();
+  for (size_t wi = 0; wi < nw; ++wi) {
+    const Window &w = c->windows[wi];
+    const int r = static_cast<int>(wi % c->n_rings);
+    hipEvent_t *E = &c->ev[wi * 6];
+    if (wi >= static_cast<size_t>(c->n_rings)) HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
+    const int64_t run = c->run_no++;
+    const uint32_t epoch = 1u + static_cast<uint32_t>(run % 0x7fffffff);
+    if (c->ring_cleared_at[r] < 0) {  // records of another run read as absent (their epoch)
+      HIP_TRY(hipMemsetAsync(c->d_recs[r], 0, static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec), sd));
+      c->ring_cleared_at[r] = run;
+    }
+    HIP_TRY(hipEventRecord(E[0], sd));
+    FullParseArgs pa{};
+    pa.es = c->d_es;
+    pa.slices = c->d_fslices + w.fs0;
+    pa.n_slices = static_cast<int32_t>(w.fs1 - w.fs0);
+    pa.slice0 = 0;
+    pa.epoch = epoch;
+    pa.recs = c->d_recs[r];
+    pa.arena = c->d_arena[r];
+    pa.err = c->d_err;
+    pa.P = c->fprm;
+    VTS_TRY(parse_full_launch(pa, sd));
+    HIP_TRY(hipEventRecord(E[1], sd));
+    FullReconArgs ra{};
+    ra.recs = c->d_recs[r];
+    ra.arena = c->d_arena[r];
+    ra.slices = c->d_fslices + w.fs0;
+    ra.surf = c->d_surf[r];
+    ra.frame_stride = c->frame_stride;
+    ra.uv_off = static_cast<int64_t>(c->pitch) * c->coded_h;
+    ra.pitch = c->pitch;
+    ra.epoch = epoch;
+    ra.deblock = 1;
+    ra.err = c->d_err;
+    ra.P = c->fprm;
+    for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+      ra.frames = c->d_levels + w.lvl_off[l];
+      VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], sd));
+    }
+    if (c->small.on) VTS_TRY(small_window(c, r, w.f0, w.f1, sd));
+    HIP_TRY(hipEventRecord(E[2], sd));
+    HIP_TRY(hipStreamWaitEvent(ss, E[2], 0));
+    HIP_TRY(hipEventRecord(E[3], ss));
+    vts_score_desc d{};
+    d.nv12 = c->d_surf[r];
+    d.frame_stride = c->frame_stride;
+    d.n_frames = w.f1 - w.f0;
+    d.width = c->width;
+    d.height = c->height;
+    d.pitch = c->pitch;
+    d.uv_row_offset = c->coded_h;
+    d.k = c->k;
+    d.rgb = c->d_rgb + 3 * c->thumb_px * w.f0;
+    d.hist = c->d_hist + w.f0 * 256;
+    d.sad = c->d_sad + w.f0;
+    d.score = c->d_score + w.f0;
+    d.prev_luma = wi > 0 ? c->d_last[(wi - 1) & 1] : nullptr;
+    d.last_luma = c->d_last[wi & 1];
+    d.workspace = c->d_ws[r];
+    d.workspace_bytes = c->ws_bytes;
+    VTS_TRY(score_launch(&d, ss));
+    HIP_TRY(hipEventRecord(E[4], ss));
+  }
+  HIP_TRY(hipStreamWaitEvent(sd, c->ev[(nw - 1) * 6 + 4], 0));
+  HIP_TRY(hipEventRecord(c->ev_end, sd));
+  HIP_TRY(hipEventSynchronize(c->ev_end));
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, c->ev_start, c->ev_end));
+  c->timings[0] = ms;
+  c->timings[1] = c->timings[2] = c->timings[3] = 0;
+  for (size_t wi = 0; wi < nw; ++wi) {
+    hipEvent_t *E = &c->ev[wi * 6];
+    float a = 0, b = 0, s = 0;
+    HIP_TRY(hipEventElapsedTime(&a, E[0], E[1]));
+    HIP_TRY(hipEventElapsedTime(&b, E[1], E[2]));
+    HIP_TRY(hipEventElapsedTime(&s, E[3], E[4]));
+    c->timings[1] += a;
+    c->timings[2] += b;
+    c->timings[3] += s;
+  }
+  c->last_window_done = static_cast<int64_t>(nw) - 1;
+  if (err) {
+    c->have_results = false;
+    return fail(VTS_E_DECODE, "device decoder: %s", describe_decode_error(err).c_str());
+  }
+  c->have_results = true;
+  c->host_scores.clear();
+  return VTS_OK;
+}
+
+}  // namespace vts

@@ -91,7 +91,8 @@ class Params(C.Structure):
     _fields_ = [("k", C.c_int32), ("window_frames", C.c_int32), ("keep_rgb", C.c_int32),
                 ("n_streams", C.c_int32), ("cut_threshold", C.c_float), ("fused", C.c_int32),
                 ("gops_per_launch", C.c_int32), ("parse_chunks", C.c_int32),
-                ("level_block", C.c_int32), ("keep_frames", C.c_int32)]
+                ("level_block", C.c_int32), ("keep_frames", C.c_int32), ("decoder", C.c_int32),
+                ("_pad", C.c_int32)]
 
 
 class SynthParams(C.Structure):

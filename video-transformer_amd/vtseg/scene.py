@@ -107,7 +107,7 @@ class VideoScorer:
                  window_frames: int = 0, n_streams: int = 2,
                  cut_threshold: float = DEFAULT_CUT_THRESHOLD, fused: int = 0,
                  gops_per_launch: int = 0, parse_chunks: int = 0, level_block: int = 0,
-                 keep_frames: bool = False):
+                 keep_frames: bool = False, decoder: str = "auto"):
         self._lib = _lib.lib()
         prm = _lib.Params()
         prm.k = k
@@ -120,6 +120,7 @@ class VideoScorer:
         prm.parse_chunks = parse_chunks
         prm.level_block = level_block
         prm.keep_frames = 1 if keep_frames else 0
+        prm.decoder = {"auto": 0, "subset": 1, "general": 2}[decoder]
         self._threshold = cut_threshold
         ctx = C.c_void_p()
         _lib.check(self._lib.vts_open(int(device), str(path).encode(), C.byref(prm),
@@ -161,6 +162,11 @@ class VideoScorer:
     def recon_launches(self) -> int:
         """Reconstruct launches per run (one per GOP level per window)."""
         return int(self._lib.vts_schedule_info(self._ctx, 0))
+
+    def general(self) -> bool:
+        """The general CAVLC decoder runs (not the I_PCM / integer-motion
+        subset kernels)."""
+        return bool(self._lib.vts_schedule_info(self._ctx, 8))
 
     def windows(self) -> int:
         """Decode windows per run (1 = the whole video at once; more = the
