@@ -303,7 +303,7 @@ def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None) -> dic
 
 
 def parity_check(scorer, path, k: int, duration_s: float, segs, threads: int,
-                 max_frames: int | None) -> tuple[dict, dict]:
+                 max_frames: int | None, decoder: str = "subset") -> tuple[dict, dict]:
     """This run's device results against the C oracle (oracle.decode_score_gops,
     GOP-parallel on `threads` host threads): every frame's fp32 score (exact;
     north_star allows |d| <= 1e-4), 256-bin histogram and SAD, the scene cuts,
@@ -314,7 +314,7 @@ def parity_check(scorer, path, k: int, duration_s: float, segs, threads: int,
     import oracle
     res = scorer.score()                     # a full decode + score, results to the host
     cuts = scorer.scene_cuts()
-    ref = oracle.decode_score_gops(path, k, threads, max_frames=max_frames)
+    ref = oracle.decode_score_gops(path, k, threads, max_frames=max_frames, decoder=decoder)
     n = ref["frames"]
     times = [t for sg in segs for t in (sg.start, sg.end, sg.effective_start, sg.effective_end)]
     times = [t for t in times if max_frames is None or t * FPS < n]
@@ -332,8 +332,9 @@ def parity_check(scorer, path, k: int, duration_s: float, segs, threads: int,
               "segment_times": len(times),
               "boundary_frames_equal": list(got_idx) == list(want_idx),
               "pts_equal": res.pts[:n].tolist() == ref["pts"],
-              "oracle": "oracle/vtseg_oracle.c or_decode_samples + or_score_frames "
-                        f"(GOP-parallel, {threads} threads)"}
+              "oracle": ("oracle/h264_full_oracle.c fo_decode" if decoder == "full" else
+                         "oracle/vtseg_oracle.c or_decode_samples") +
+                        f" + or_score_frames (GOP-parallel, {threads} threads)"}
     parity["all_equal"] = all(parity[x] for x in ("scores_equal", "hist_equal", "sad_equal",
                                                   "scene_cuts_equal", "boundary_frames_equal",
                                                   "pts_equal"))
@@ -350,6 +351,11 @@ def main() -> None:
     ap.add_argument("--config", default="720p-2h", choices=sorted(CONFIGS),
                     help="BASELINE configuration (per GPU); the N=1 headline is 720p-2h, the "
                          "largest single-GPU config")
+    ap.add_argument("--coding", default="subset", choices=["subset", "full"],
+                    help="synthetic stream syntax: subset = I_PCM + integer-motion P_Skip/P16x16 "
+                         "(no residual, deblocking off: the subset kernels); full = intra 4x4/16x16, "
+                         "residuals, quarter-sample partitions, 3 references, deblocking on (the "
+                         "general decoder)")
     ap.add_argument("--video", default=None,
                     help="use this MP4 instead of synthesizing one (the rocprofv3 child passes)")
     ap.add_argument("--no-parity", action="store_true",
@@ -398,13 +404,18 @@ def main() -> None:
             path = Path(args.video)
         else:
             path = Path(tmpdir) / f"synth_rank{rank}.mp4"
-            scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
-                              seed=0x5EED + rank)
+            if args.coding == "full":
+                scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
+                                  seed=0x5EED + rank, coding="full", slices_per_row=0,
+                                  max_motion=4)
+            else:
+                scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
+                                  seed=0x5EED + rank)
 
     prof = None
     if world == 1 and not args.no_pmc and args.workload != "transcode":
         # before anything touches the GPU: the passes are child processes
-        child_argv = ["--workload", args.workload, "--config", args.config,
+        child_argv = ["--workload", args.workload, "--config", args.config, "--coding", args.coding,
                       "--gops-per-launch", str(args.gops_per_launch),
                       "--parse-chunks", str(args.parse_chunks),
                       "--level-block", str(args.level_block)]
@@ -636,14 +647,19 @@ def main() -> None:
         threads = max(1, min(16, aff // max(1, world)))
         # N > 1: every rank checks a bounded GOP-aligned prefix of its video
         maxf = None if world == 1 else min(F, 3000)
-        parity, ct = parity_check(scorer, path, k, duration_s, segs, threads, maxf)
+        dec = "full" if scorer.general() else "subset"
+        if dec == "full" and world == 1:
+            maxf = min(F, 18000)  # the general oracle decodes ~350 720p frames/s on 16 threads
+        parity, ct = parity_check(scorer, path, k, duration_s, segs, threads, maxf, dec)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = {"value": round(ct["frames"] / ct["seconds"], 2), "unit": "frames/s",
                    "cores": ct["threads"], "kind": "port",
-                   "sample": f"the parity pass: all {ct['frames']} frames ({ct['width']}x"
+                   "sample": f"the parity pass: {ct['frames']} frames ({ct['width']}x"
                              f"{ct['height']}, {ct['gops']} GOPs) of the benchmark video decoded by "
-                             f"oracle/vtseg_oracle.c or_decode_samples + scored by or_score_frames, "
-                             f"GOP-parallel on {ct['threads']} threads, {ct['seconds']:.1f} s"}
+                             + ("oracle/h264_full_oracle.c fo_decode" if dec == "full" else
+                                "oracle/vtseg_oracle.c or_decode_samples") +
+                             f" + scored by or_score_frames, GOP-parallel on {ct['threads']} "
+                             f"threads, {ct['seconds']:.1f} s"}
         if world > 1:
             ok = torch.tensor([1 if parity["all_equal"] else 0], dtype=torch.int32, device=coll_dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)

@@ -367,7 +367,8 @@ typedef struct vts_synth_params {
   int32_t chunks;               /* the stream is coded as this many runs of
                                    frames, each starting with an IDR scene cut,
                                    on parallel host threads; 0 = one run per
-                                   18 000 frames (10 min at 30 fps)             */
+                                   18 000 frames (10 min at 30 fps; 1 800 for
+                                   coding 1)                                    */
   int32_t coding;               /* 0: the I_PCM / P_Skip subset above;
                                    1: full CAVLC syntax, decoded by the general
                                    device decoder: Intra_4x4 / Intra_16x16 /

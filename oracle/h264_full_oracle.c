@@ -208,16 +208,48 @@ static const char *const RB[7][15] = {
    "00000001", "000000001", "0000000001", "00000000001"},
 };
 
-/* Read a code of `table` (n entries of strings, NULL = absent): returns the
- * entry index or -1 (no match within 16 bits). */
-static int fb_vlc(fb_t *b, const char *const *table, int n) {
-  char s[24];
-  for (int len = 0; len < 16;) {
-    s[len++] = (char)('0' + fb_bit(b));
-    s[len] = 0;
-    for (int i = 0; i < n; i++)
-      if (table[i] && strcmp(table[i], s) == 0) return i;
+/* The strings as (length, value) pairs, converted once when the library
+ * loads (matching stays exact: a code is its length and its bits). */
+typedef struct {
+  int n;
+  uint8_t len[68];
+  uint32_t val[68];
+} fo_vlc;
+static fo_vlc VLC_CT[4], VLC_TZ[15], VLC_TZC[3], VLC_RB[7];
+
+static void vlc_make(fo_vlc *t, const char *const *table, int n) {
+  t->n = n;
+  for (int i = 0; i < n; i++) {
+    t->len[i] = 0;
+    t->val[i] = 0;
+    if (!table[i]) continue;
+    for (const char *c = table[i]; *c; c++) {
+      t->val[i] = (t->val[i] << 1) | (uint32_t)(*c - '0');
+      t->len[i]++;
+    }
+  }
+}
+
+__attribute__((constructor)) static void vlc_init(void) {
+  for (int c = 0; c < 4; c++) {
+    const char *flat[68];
+    for (int r = 0; r < 17; r++)
+      for (int k = 0; k < 4; k++) flat[r * 4 + k] = CT[c][r][k];
+    vlc_make(&VLC_CT[c], flat, c == 3 ? 20 : 68);
+  }
+  for (int t = 0; t < 15; t++) vlc_make(&VLC_TZ[t], TZ[t], 16);
+  for (int t = 0; t < 3; t++) vlc_make(&VLC_TZC[t], TZC[t], 4);
+  for (int r = 0; r < 7; r++) vlc_make(&VLC_RB[r], RB[r], 15);
+}
+
+/* Read one code of table t: the entry index, or -1 (no code within 16 bits). */
+static int fb_vlc(fb_t *b, const fo_vlc *t) {
+  uint32_t v = 0;
+  for (int len = 1; len <= 16; len++) {
+    v = (v << 1) | fb_bit(b);
     if (b->err) return -1;
+    for (int i = 0; i < t->n; i++)
+      if (t->len[i] == len && t->val[i] == v) return i;
   }
   return -1;
 }
@@ -499,11 +531,7 @@ static int residual_block(fb_t *b, int nC, int start, int end, int maxNum, int *
     }
   } else {
     int col = nC == -1 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
-    int rows = col == 3 ? 5 : 17;
-    const char *flat[17 * 4];
-    for (int r = 0; r < rows; r++)
-      for (int c = 0; c < 4; c++) flat[r * 4 + c] = CT[col][r][c];
-    int idx = fb_vlc(b, flat, rows * 4);
+    int idx = fb_vlc(b, &VLC_CT[col]);
     if (idx < 0) return -1;
     tc = idx / 4;
     t1 = idx % 4;
@@ -532,18 +560,13 @@ static int residual_block(fb_t *b, int nC, int start, int end, int maxNum, int *
   int zerosLeft = 0;
   if (tc < end - start + 1) {
     int tz;
-    if (maxNum == 4) {
-      const char *row[4] = {TZC[tc - 1][0], TZC[tc - 1][1], TZC[tc - 1][2], TZC[tc - 1][3]};
-      tz = fb_vlc(b, row, 4);
-    } else {
-      tz = fb_vlc(b, TZ[tc - 1], 16);
-    }
+    tz = fb_vlc(b, maxNum == 4 ? &VLC_TZC[tc - 1] : &VLC_TZ[tc - 1]);
     if (tz < 0) return -1;
     zerosLeft = tz;
   }
   for (int i = 0; i < tc - 1; i++) {
     if (zerosLeft > 0) {
-      int rb = fb_vlc(b, RB[imin(zerosLeft, 7) - 1], 15);
+      int rb = fb_vlc(b, &VLC_RB[imin(zerosLeft, 7) - 1]);
       if (rb < 0 || rb > zerosLeft) return -1;
       run[i] = rb;
     } else {
@@ -797,23 +820,28 @@ static int ref_luma(const fo_dec *d, const fo_pic *r, int x, int y) {
 }
 static int tap6(int a, int b, int c, int dd, int e, int f) { return a - 5 * b + 20 * c + 20 * dd - 5 * e + f; }
 
-/* luma sample at integer (xi, yi) + fraction (xf, yf) (Table 8-12) */
+/* luma sample at integer (xi, yi) + fraction (xf, yf) (Table 8-12); only the
+ * intermediate values the position needs are formed */
 static int luma_sample(const fo_dec *d, const fo_pic *r, int xi, int yi, int xf, int yf) {
 #define G(dx, dy) ref_luma(d, r, xi + (dx), yi + (dy))
+#define HTAP(dy) tap6(G(-2, dy), G(-1, dy), G(0, dy), G(1, dy), G(2, dy), G(3, dy))
+#define VTAP(dx) tap6(G(dx, -2), G(dx, -1), G(dx, 0), G(dx, 1), G(dx, 2), G(dx, 3))
   int Gv = G(0, 0);
   if (!xf && !yf) return Gv;
-  /* intermediate (unrounded) half-sample values */
-  int b1 = tap6(G(-2, 0), G(-1, 0), G(0, 0), G(1, 0), G(2, 0), G(3, 0));
-  int h1 = tap6(G(0, -2), G(0, -1), G(0, 0), G(0, 1), G(0, 2), G(0, 3));
-  int s1 = tap6(G(-2, 1), G(-1, 1), G(0, 1), G(1, 1), G(2, 1), G(3, 1));
-  int m1 = tap6(G(1, -2), G(1, -1), G(1, 0), G(1, 1), G(1, 2), G(1, 3));
-  int hr[6];
-  for (int k = 0; k < 6; k++) /* horizontal intermediates at rows -2..3 */
-    hr[k] = tap6(G(-2, k - 2), G(-1, k - 2), G(0, k - 2), G(1, k - 2), G(2, k - 2), G(3, k - 2));
-  int j1 = tap6(hr[0], hr[1], hr[2], hr[3], hr[4], hr[5]);
-  int b = clip1((b1 + 16) >> 5), h = clip1((h1 + 16) >> 5), s = clip1((s1 + 16) >> 5);
-  int m = clip1((m1 + 16) >> 5), j = clip1((j1 + 512) >> 10);
-  int H = G(1, 0), M = G(0, 1);
+  int b = 0, h = 0, s = 0, m = 0, j = 0;
+  int need_b = (yf == 0 && xf) || (yf == 1 && xf) || (xf == 2);
+  int need_h = (xf == 0 && yf) || (xf == 1 && yf) || (yf == 2);
+  int need_s = yf == 3 && xf;
+  int need_m = xf == 3 && yf;
+  int need_j = (xf == 2 && yf) || (yf == 2 && xf);
+  if (need_b) b = clip1((HTAP(0) + 16) >> 5);
+  if (need_h) h = clip1((VTAP(0) + 16) >> 5);
+  if (need_s) s = clip1((HTAP(1) + 16) >> 5);
+  if (need_m) m = clip1((VTAP(1) + 16) >> 5);
+  if (need_j) j = clip1((tap6(HTAP(-2), HTAP(-1), HTAP(0), HTAP(1), HTAP(2), HTAP(3)) + 512) >> 10);
+  int H = xf == 3 && yf == 0 ? G(1, 0) : 0, M = xf == 0 && yf == 3 ? G(0, 1) : 0;
+#undef HTAP
+#undef VTAP
 #undef G
   switch (yf * 4 + xf) {
     case 0 * 4 + 1: return (Gv + b + 1) >> 1;   /* a */

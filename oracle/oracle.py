@@ -415,14 +415,17 @@ def decode_samples(sps: bytes, pps: bytes, samples: list[bytes], nal_length_size
     return out
 
 
-def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None) -> dict:
+def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None,
+                      decoder: str = "subset") -> dict:
     """Decode + score a whole MP4 with the scalar oracle, GOP-parallel on
     `threads` host threads (ctypes releases the GIL): every GOP (run of frames
     from an IDR access unit) is decoded by or_decode_samples and scored by
     or_score_frames on its own; the SAD / score of each GOP's first frame is
     then completed against the previous GOP's last thumbnail luma, exactly as
     or_score_frames would have over the whole sequence.  With max_frames, only
-    the first GOPs covering that many frames.  Returns hist [F, 256] u32,
+    the first GOPs covering that many frames.  decoder "full" decodes with
+    the general oracle (h264_full_oracle.c fo_decode; an IDR starts every GOP,
+    so GOPs are independent).  Returns hist [F, 256] u32,
     sad [F] u64, score [F] f32, pts, timescale, the frame count and seconds."""
     import time
     from concurrent.futures import ThreadPoolExecutor
@@ -431,10 +434,20 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None)
     prm = H264Params()
     sps, pps = m["sps"][0], m["pps"][0]
     nls = m["nal_length_size"]
-    if L.or_parse_sps_pps(sps, len(sps), pps, len(pps), nls, C.byref(prm)):
-        raise RuntimeError("oracle SPS/PPS")
-    W = prm.mb_width * 16 - prm.crop_right
-    H = prm.mb_height * 16 - prm.crop_bottom
+    if decoder == "full":
+        L.fo_decode.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, C.c_int, C.c_void_p,
+                                C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
+                                C.c_void_p, C.c_char_p]
+        L.fo_dims.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_void_p]
+        w_, h_ = C.c_int(0), C.c_int(0)
+        if L.fo_dims(sps, len(sps), C.byref(w_), C.byref(h_)):
+            raise RuntimeError("oracle SPS")
+        W, H = w_.value, h_.value
+    else:
+        if L.or_parse_sps_pps(sps, len(sps), pps, len(pps), nls, C.byref(prm)):
+            raise RuntimeError("oracle SPS/PPS")
+        W = prm.mb_width * 16 - prm.crop_right
+        H = prm.mb_height * 16 - prm.crop_bottom
     w, h = W // k, H // k
     data = np.frombuffer(m["data"], np.uint8)
     offs = np.asarray(m["offsets"], np.int64)
@@ -462,8 +475,15 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None)
         cnt = b - a
         out = np.empty((cnt, H * 3 // 2, W), np.uint8)
         bad = C.c_int64(-1)
-        if L.or_decode_samples(C.byref(prm), data.ctypes.data, offs[a:b].ctypes.data,
-                               sizes[a:b].ctypes.data, cnt, out.ctypes.data, C.byref(bad)):
+        if decoder == "full":
+            err = C.create_string_buffer(256)
+            o, z = np.ascontiguousarray(offs[a:b]), np.ascontiguousarray(sizes[a:b])
+            if L.fo_decode(sps, len(sps), pps, len(pps), nls, data.ctypes.data, o.ctypes.data,
+                           z.ctypes.data, cnt, 0, out.ctypes.data, C.byref(bad), err):
+                raise RuntimeError(f"oracle decode_full failed in GOP at frame {a}: "
+                                   f"{err.value.decode(errors='replace')}")
+        elif L.or_decode_samples(C.byref(prm), data.ctypes.data, offs[a:b].ctypes.data,
+                                 sizes[a:b].ctypes.data, cnt, out.ctypes.data, C.byref(bad)):
             raise RuntimeError(f"oracle decode failed in GOP at frame {a}")
         fr = out.reshape(-1)
         r = score_frames(fr, W * H * 3 // 2, cnt, W, H, W, H, k, want_rgb=False)

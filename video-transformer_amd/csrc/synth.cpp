@@ -501,7 +501,9 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
 
   // Chunks of frames coded independently on host threads (auto: one per 18 000
   // frames, i.e. 10 min at 30 fps), then written in order.
-  int64_t n_chunks = P.chunks > 0 ? P.chunks : (P.n_frames + 17999) / 18000;
+  // (full syntax: one run per 1 800 frames; its writer is ~10x slower per frame)
+  const int64_t per_chunk = P.coding == 1 ? 1800 : 18000;
+  int64_t n_chunks = P.chunks > 0 ? P.chunks : (P.n_frames + per_chunk - 1) / per_chunk;
   n_chunks = std::max<int64_t>(1, std::min<int64_t>(n_chunks, std::min<int64_t>(P.n_frames, 16384)));
   std::vector<SynthChunk> chunks(static_cast<size_t>(n_chunks));
   for (int64_t k = 0; k < n_chunks; ++k) {
