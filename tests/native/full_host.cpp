@@ -69,6 +69,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   if (out_cap < static_cast<int64_t>(n) * W * H * 3 / 2) return bad("output too small");
   std::vector<uint8_t> surf(static_cast<size_t>(stride) * n + 64, 0);
   std::vector<MbRec> recs(static_cast<size_t>(nmb) * n);
+  std::vector<uint16_t> ilvl(static_cast<size_t>(nmb) * n);
   std::vector<FullSlice> fs(slices.size());
   uint32_t arena_blocks = 0;
   for (size_t i = 0; i < slices.size(); ++i) {
@@ -108,7 +109,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
       full::FullScratch sc;
       errs |= full::parse_slice_full(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P, fr_recs,
-                                     arena.data(), epoch, &sc);
+                                     ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(), epoch, &sc);
     }
     if (errs) return bad("frame " + std::to_string(fi) + ": parse: " + describe_decode_error(errs));
     full::ReconCtx c{};

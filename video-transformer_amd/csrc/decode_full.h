@@ -17,6 +17,7 @@ struct FullParseArgs {
   uint32_t epoch;
   int32_t _pad;
   MbRec *recs;               // ring: [slot][mb]
+  uint16_t *ilvl;            // ring: [slot][mb] intra dependency levels
   int16_t *arena;            // ring's coefficient arena
   uint32_t *err;
   FullParams P;
@@ -25,6 +26,7 @@ struct FullParseArgs {
 struct FullReconArgs {
   const int4 *frames;        // (slot, -, -, -) per picture of the launch
   const MbRec *recs;
+  const uint16_t *ilvl;
   const int16_t *arena;
   const FullSlice *slices;   // the window's slices (MbRec.slice indexes them)
   uint8_t *surf;             // ring of NV12 pictures

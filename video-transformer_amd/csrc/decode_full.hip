@@ -3,17 +3,26 @@
 // 16 references, the deblocking filter).  DESIGN.md §5b.
 //
 //   h264_parse_full   one lane per slice: slice_data() -> MbRec + coefficient
-//                     blocks (parse_full.h)
-//   h264_recon_full   one workgroup per picture of a level launch: every inter
-//                     macroblock in parallel (one lane each), then the intra
-//                     macroblocks along the t = x + 2y wavefront (left, top,
-//                     top-right neighbours are done one step earlier), a
-//                     workgroup barrier per step (recon_full.h MbRecon)
-//   h264_deblock_full one workgroup per picture: macroblocks along the same
-//                     wavefront, which orders every pair of overlapping edge
-//                     filters as the standard's raster order does (8.7)
-// The per-macroblock code is shared with the CPU harness that is checked
-// against the oracle (tests/test_full_host.py).
+//                     blocks + intra dependency level (parse_full.h)
+//   h264_inter_full   one lane per 4x4 luma block (+ its 2x2 Cb/Cr) of every
+//                     inter / skip / I_PCM macroblock of every picture of the
+//                     level: 6-tap / bilinear prediction from dword windows,
+//                     residual, one dword store per row
+//   h264_intra_full   one workgroup per picture: the intra-predicted
+//                     macroblocks by dependency level (the parser's level =
+//                     1 + the highest level among the intra neighbours it
+//                     reads; an all-intra picture gives the x + 2y wavefront),
+//                     16 lanes per macroblock, its borders and 4x4 blocks in LDS
+//   h264_deblock_full one workgroup per picture, one wave per pair of
+//                     macroblock rows (the lower row two macroblocks behind the
+//                     upper, the pair behind the pair above through LDS
+//                     progress counters): the standard's raster order (8.7) as
+//                     a wavefront; a lane filters one row across the vertical
+//                     edges in registers, then one column across the
+//                     horizontal edges out of an LDS tile
+// Per-macroblock arithmetic (transforms, interpolation, intra modes, edge
+// filters) follows the same clauses as recon_full.h, which the CPU harness
+// runs against the oracle.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -25,8 +34,11 @@ namespace vts {
 namespace {
 
 constexpr int kParseLanes = 64;
-constexpr int kReconThreads = 256;
-constexpr int kDeblockThreads = 64;
+constexpr int kInterThreads = 256;   // 16 macroblocks x 16 blocks
+constexpr int kIntraThreads = 1024;  // 64 macroblocks in flight
+constexpr int kIntraSlots = kIntraThreads / 16;
+constexpr int kDbkThreads = 1024;    // 16 waves = 16 row pairs in flight
+constexpr int kDbkWaves = kDbkThreads / 64;
 
 __global__ void __launch_bounds__(kParseLanes) h264_parse_full(FullParseArgs a) {
   __shared__ full::FullScratch scratch[kParseLanes];
@@ -35,76 +47,893 @@ __global__ void __launch_bounds__(kParseLanes) h264_parse_full(FullParseArgs a) 
   const FullSlice s = a.slices[i];
   const int64_t nmb = static_cast<int64_t>(a.P.mb_width) * a.P.mb_height;
   const uint32_t e = full::parse_slice_full(a.es, s, static_cast<uint32_t>(a.slice0 + i), a.P,
-                                            a.recs + s.slot * nmb, a.arena, a.epoch, &scratch[threadIdx.x]);
+                                            a.recs + s.slot * nmb, a.ilvl + s.slot * nmb, a.arena, a.epoch,
+                                            &scratch[threadIdx.x]);
   if (e) atomicOr(a.err, e);
 }
 
-__device__ full::ReconCtx make_ctx(const FullReconArgs &a, int slot) {
-  full::ReconCtx c{};
-  const int64_t nmb = static_cast<int64_t>(a.P.mb_width) * a.P.mb_height;
-  c.recs = a.recs + slot * nmb;
-  c.arena = a.arena;
-  c.slices = a.slices;
-  c.surf = a.surf;
-  c.frame_stride = a.frame_stride;
-  c.pitch = a.pitch;
-  c.uv_off = a.uv_off;
-  c.mbw = a.P.mb_width;
-  c.mbh = a.P.mb_height;
-  c.cip = a.P.cip;
-  c.cqp_off = a.P.cqp_off;
-  c.cqp_off2 = a.P.cqp_off2;
-  c.epoch = a.epoch;
-  return c;
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ int c255(int v) { return min(max(v, 0), 255); }
+__device__ __forceinline__ int t6(int a, int b, int c, int d, int e, int f) {
+  return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
+}
+template <int N>
+__device__ __forceinline__ int px(const uint32_t (&w)[9][N], int r, int c) {
+  return (w[r][c >> 2] >> ((c & 3) * 8)) & 255;
+}
+__device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
+  return static_cast<uint32_t>(a) | (static_cast<uint32_t>(b) << 8) | (static_cast<uint32_t>(c) << 16) |
+         (static_cast<uint32_t>(d) << 24);
+}
+// luma4x4BlkIdx of raster 4x4 block b
+__device__ __forceinline__ int blkidx(int b) {
+  return ((b >> 3) << 3) | (((b & 3) >> 1) << 2) | (((b >> 2) & 1) << 1) | (b & 1);
+}
+// arena block of stored-block bit `bit` of a macroblock, -1 if absent
+__device__ __forceinline__ int64_t stored(uint32_t blocks, uint32_t coef, uint32_t bit) {
+  if (!((blocks >> bit) & 1u)) return -1;
+  return static_cast<int64_t>(coef) + __builtin_popcount(blocks & ((1u << bit) - 1u));
+}
+__device__ __forceinline__ void load_coefs(const int16_t *arena, int64_t blk, int *cf) {
+  if (blk < 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cf[i] = 0;
+    return;
+  }
+  const uint4 *p = reinterpret_cast<const uint4 *>(arena + 16 * blk);
+  const uint4 u0 = p[0], u1 = p[1];
+  const uint32_t w[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    cf[2 * i] = static_cast<int16_t>(w[i] & 0xffff);
+    cf[2 * i + 1] = static_cast<int16_t>(w[i] >> 16);
+  }
 }
 
-__global__ void __launch_bounds__(kReconThreads) h264_recon_full(FullReconArgs a) {
-  const int slot = a.frames[blockIdx.x].x;
-  const full::ReconCtx c = make_ctx(a, slot);
-  const int mbw = c.mbw, mbh = c.mbh, nmb = mbw * mbh;
-  uint32_t err = 0;
-  // inter macroblocks: independent of each other
-  for (int mb = threadIdx.x; mb < nmb; mb += kReconThreads) {
-    const MbRec &m = c.recs[mb];
-    if (m.epoch != c.epoch) {
-      err |= DEC_E_MISSING_MB;
-      continue;
+// 9x9 luma window w[r][c] = R[clampY(ys + r)][clampX(xs + c)], 3 packed dwords per row
+__device__ __forceinline__ void load_win9(const uint8_t *R, int pitch, int W, int H, int xs, int ys,
+                                          uint32_t (&w)[9][3]) {
+  if (xs >= 0 && xs + 8 < W && ys >= 0 && ys + 8 < H) {
+    const int sh = xs & 3;
+    const uint8_t *p = R + static_cast<int64_t>(ys) * pitch + (xs & ~3);
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const uint32_t *q = reinterpret_cast<const uint32_t *>(p + static_cast<int64_t>(r) * pitch);
+      const uint32_t d0 = q[0], d1 = q[1], d2 = q[2];
+      w[r][0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+      w[r][1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      w[r][2] = d2 >> (8 * sh);
     }
-    if (m.type == kMbInter || m.type == kMbSkip) {
-      full::MbRecon r(c, slot, mb, m);
-      r.run();
-      err |= r.err;
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    const uint8_t *row = R + static_cast<int64_t>(min(max(ys + r, 0), H - 1)) * pitch;
+    uint32_t v[3] = {0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 9; ++c) v[c >> 2] |= static_cast<uint32_t>(row[min(max(xs + c, 0), W - 1)]) << ((c & 3) * 8);
+    w[r][0] = v[0];
+    w[r][1] = v[1];
+    w[r][2] = v[2];
+  }
+}
+
+#define HT(r, x) t6(px(w, r, x), px(w, r, x + 1), px(w, r, x + 2), px(w, r, x + 3), px(w, r, x + 4), px(w, r, x + 5))
+#define VT(c, y) t6(px(w, y, c), px(w, y + 1, c), px(w, y + 2, c), px(w, y + 3, c), px(w, y + 4, c), px(w, y + 5, c))
+
+// 8.4.2.2.1: the 4x4 luma prediction at fractional offset (xf, yf), packed rows
+__device__ __forceinline__ void luma_pred4(const uint32_t (&w)[9][3], int xf, int yf, int (&v)[16]) {
+  if (!(xf | yf)) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) v[y * 4 + x] = px(w, y + 2, x + 2);
+  } else if (!yf) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int b = c255((HT(y + 2, x) + 16) >> 5);
+        const int o = xf == 1 ? px(w, y + 2, x + 2) : px(w, y + 2, x + 3);
+        v[y * 4 + x] = xf == 2 ? b : (b + o + 1) >> 1;
+      }
+  } else if (!xf) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int h = c255((VT(x + 2, y) + 16) >> 5);
+        const int o = yf == 1 ? px(w, y + 2, x + 2) : px(w, y + 3, x + 2);
+        v[y * 4 + x] = yf == 2 ? h : (h + o + 1) >> 1;
+      }
+  } else if (xf == 2 || yf == 2) {
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        int hb[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) hb[k] = HT(y + k, x);
+        const int j = c255((t6(hb[0], hb[1], hb[2], hb[3], hb[4], hb[5]) + 512) >> 10);
+        int o;
+        if (xf == 2) o = c255(((yf == 1 ? hb[2] : hb[3]) + 16) >> 5);  // b or s
+        else o = c255(((xf == 1 ? VT(x + 2, y) : VT(x + 3, y)) + 16) >> 5);  // h or m
+        v[y * 4 + x] = (xf == 2 && yf == 2) ? j : (j + o + 1) >> 1;
+      }
+  } else {
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int bs = c255(((yf == 1 ? HT(y + 2, x) : HT(y + 3, x)) + 16) >> 5);
+        const int hm = c255(((xf == 1 ? VT(x + 2, y) : VT(x + 3, y)) + 16) >> 5);
+        v[y * 4 + x] = (bs + hm + 1) >> 1;
+      }
+  }
+}
+#undef HT
+#undef VT
+
+// 8.5.12.1 chroma DC of chroma block ck: 2x2 Hadamard of the plane's DC levels, scaled
+__device__ __forceinline__ int chroma_dc(const int16_t *arena, uint32_t blocks, uint32_t coef, int pl, int ck,
+                                         int qpc) {
+  const int64_t blk = stored(blocks, coef, kBlkChromaDc0 + pl);
+  if (blk < 0) return 0;
+  const uint2 u = *reinterpret_cast<const uint2 *>(arena + 16 * blk);
+  const int c0 = static_cast<int16_t>(u.x & 0xffff), c1 = static_cast<int16_t>(u.x >> 16);
+  const int c2 = static_cast<int16_t>(u.y & 0xffff), c3 = static_cast<int16_t>(u.y >> 16);
+  const int f = ck == 0 ? c0 + c1 + c2 + c3 : ck == 1 ? c0 - c1 + c2 - c3 : ck == 2 ? c0 + c1 - c2 - c3 : c0 - c1 - c2 + c3;
+  return ((f * full::level_scale(qpc % 6, 0, 0)) << (qpc / 6)) >> 5;
+}
+// chroma residual of one 4x4 chroma block of plane pl
+__device__ __forceinline__ void chroma_res(const int16_t *arena, uint32_t blocks, uint32_t coef, int pl, int ck,
+                                           int qpc, int (&r)[16]) {
+  int cf[16];
+  load_coefs(arena, stored(blocks, coef, kBlkChromaAc0 + 4 * pl + ck), cf);
+  cf[0] = chroma_dc(arena, blocks, coef, pl, ck, qpc);
+  full::scale_idct4(cf, qpc, true, r);
+}
+
+// MbRec header words (the first 32 bytes)
+struct MbHdr {
+  uint32_t epoch, slice, coef, blocks;
+  int type, qp, cbp, modes;
+  uint32_t refs;            // ref[4] bytes
+  int16_t ref_slot[4];
+};
+__device__ __forceinline__ MbHdr load_hdr(const MbRec *m) {
+  const uint4 *p = reinterpret_cast<const uint4 *>(m);
+  const uint4 a = p[0], b = p[1];
+  MbHdr h;
+  h.epoch = a.x;
+  h.slice = a.y;
+  h.coef = a.z;
+  h.blocks = a.w;
+  h.type = b.x & 255;
+  h.qp = (b.x >> 8) & 255;
+  h.cbp = (b.x >> 16) & 255;
+  h.modes = b.x >> 24;
+  h.refs = b.y;
+  h.ref_slot[0] = static_cast<int16_t>(b.z & 0xffff);
+  h.ref_slot[1] = static_cast<int16_t>(b.z >> 16);
+  h.ref_slot[2] = static_cast<int16_t>(b.w & 0xffff);
+  h.ref_slot[3] = static_cast<int16_t>(b.w >> 16);
+  return h;
+}
+
+// ------------------------------------------------------- inter / I_PCM blocks
+// grid (ceil(nmb / 16), pictures of the level); lane = (macroblock, raster 4x4 block b)
+__global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a) {
+  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
+  const int slot = a.frames[blockIdx.y].x;
+  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int b = threadIdx.x & 15;
+  if (mb >= nmb) return;
+  const MbRec *rec = a.recs + static_cast<int64_t>(slot) * nmb + mb;
+  const MbHdr h = load_hdr(rec);
+  if (h.epoch != a.epoch) {
+    if (b == 0) atomicOr(a.err, static_cast<uint32_t>(DEC_E_MISSING_MB));
+    return;
+  }
+  if (h.type == kMbI4x4 || h.type == kMbI16) return;  // h264_intra_full
+  const int mx = mb % mbw, my = mb / mbw, bx = b & 3, by = b >> 2;
+  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
+  uint8_t *UV = Y + a.uv_off;
+  const int x0 = mx * 16 + bx * 4, y0 = my * 16 + by * 4;
+  const int cx = mx * 8 + bx * 2, cy = my * 8 + by * 2;
+  const int pitch = a.pitch;
+  if (h.type == kMbPcm) {
+    const uint8_t *pcm = reinterpret_cast<const uint8_t *>(a.arena + 16 * static_cast<int64_t>(h.coef));
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<uint32_t *>(Y + static_cast<int64_t>(y0 + r) * pitch + x0) =
+          *reinterpret_cast<const uint32_t *>(pcm + (by * 4 + r) * 16 + bx * 4);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int o = (by * 2 + r) * 8 + bx * 2;
+      *reinterpret_cast<uint32_t *>(UV + static_cast<int64_t>(cy + r) * pitch + 2 * cx) =
+          pack4(pcm[256 + o], pcm[320 + o], pcm[256 + o + 1], pcm[320 + o + 1]);
+    }
+    return;
+  }
+  const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+  const int rs = h.ref_slot[p8];
+  if (rs < 0) {
+    atomicOr(a.err, static_cast<uint32_t>(DEC_E_NO_REF));
+    return;
+  }
+  const uint32_t mvw = reinterpret_cast<const uint32_t *>(rec)[16 + b];
+  const int mvx = static_cast<int16_t>(mvw & 0xffff), mvy = static_cast<int16_t>(mvw >> 16);
+  const uint8_t *R = a.surf + static_cast<int64_t>(rs) * a.frame_stride;
+  const int W = mbw * 16, H = mbh * 16;
+  // luma
+  uint32_t w[9][3];
+  load_win9(R, pitch, W, H, x0 + (mvx >> 2) - 2, y0 + (mvy >> 2) - 2, w);
+  // chroma window: 3 rows x (Cb, Cr) x 3 samples at (cx0, cy0)
+  const int CW = W / 2, CH = H / 2;
+  const int cx0 = cx + (mvx >> 3), cy0 = cy + (mvy >> 3);
+  const uint8_t *RUV = R + a.uv_off;
+  uint32_t cwn[3][2];
+  if (cx0 >= 0 && cx0 + 2 < CW && cy0 >= 0 && cy0 + 2 < CH) {
+    const int o = 2 * cx0, sh = o & 3;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const uint32_t *q = reinterpret_cast<const uint32_t *>(RUV + static_cast<int64_t>(cy0 + r) * pitch + (o & ~3));
+      const uint32_t d0 = q[0], d1 = q[1];
+      cwn[r][0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+      cwn[r][1] = d1 >> (8 * sh);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const uint8_t *row = RUV + static_cast<int64_t>(min(max(cy0 + r, 0), CH - 1)) * pitch;
+      uint32_t v[2] = {0, 0};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int xx = 2 * min(max(cx0 + c, 0), CW - 1);
+        v[(2 * c) >> 2] |= static_cast<uint32_t>(row[xx]) << (((2 * c) & 3) * 8);
+        v[(2 * c + 1) >> 2] |= static_cast<uint32_t>(row[xx + 1]) << (((2 * c + 1) & 3) * 8);
+      }
+      cwn[r][0] = v[0];
+      cwn[r][1] = v[1];
     }
   }
+  int pv[16];
+  luma_pred4(w, mvx & 3, mvy & 3, pv);
+  // luma residual
+  int res[16];
+  const int64_t lb = stored(h.blocks, h.coef, kBlkLuma0 + blkidx(b));
+  if (lb >= 0) {
+    int cf[16];
+    load_coefs(a.arena, lb, cf);
+    full::scale_idct4(cf, h.qp, false, res);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) res[i] = 0;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    *reinterpret_cast<uint32_t *>(Y + static_cast<int64_t>(y0 + r) * pitch + x0) =
+        pack4(c255(pv[r * 4] + res[r * 4]), c255(pv[r * 4 + 1] + res[r * 4 + 1]), c255(pv[r * 4 + 2] + res[r * 4 + 2]),
+              c255(pv[r * 4 + 3] + res[r * 4 + 3]));
+  // chroma 2x2 per plane (8.4.2.2.2)
+  const int fx = mvx & 7, fy = mvy & 7;
+  auto cpx = [&](int r, int i) { return static_cast<int>((cwn[r][i >> 2] >> ((i & 3) * 8)) & 255); };
+  int cpred[2][4];
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int A = cpx(y, 2 * x + pl), B = cpx(y, 2 * x + 2 + pl);
+        const int C = cpx(y + 1, 2 * x + pl), D = cpx(y + 1, 2 * x + 2 + pl);
+        cpred[pl][y * 2 + x] = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
+      }
+  if (h.cbp >> 4) {
+    const int ck = ((by >> 1) << 1) | (bx >> 1), sx = (bx & 1) * 2, sy = (by & 1) * 2;
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+      int r[16];
+      chroma_res(a.arena, h.blocks, h.coef, pl, ck, full::qpc_of(h.qp, pl ? a.P.cqp_off2 : a.P.cqp_off), r);
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int x = 0; x < 2; ++x) cpred[pl][y * 2 + x] = c255(cpred[pl][y * 2 + x] + r[(sy + y) * 4 + sx + x]);
+    }
+  }
+#pragma unroll
+  for (int y = 0; y < 2; ++y)
+    *reinterpret_cast<uint32_t *>(UV + static_cast<int64_t>(cy + y) * pitch + 2 * cx) =
+        pack4(cpred[0][y * 2], cpred[1][y * 2], cpred[0][y * 2 + 1], cpred[1][y * 2 + 1]);
+}
+
+// ------------------------------------------------------------ intra blocks
+struct IntraTile {
+  uint8_t y[17][28];   // luma rows -1..15 (index + 1) x cols -4..23 (index + 4)
+  uint8_t ct[2][9];    // chroma row -1, cols -1..7 (index + 1), per plane
+  uint8_t cl[2][8];    // chroma col -1, rows 0..7
+  uint8_t cout[8][16]; // reconstructed chroma rows, interleaved
+};
+
+__device__ __forceinline__ void lane_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one intra-predicted macroblock with 16 lanes (lane = raster 4x4 block b)
+__device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraTile &t) {
+  const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
+  const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
+  const MbRec *rec = frecs + mb;
+  const MbHdr h = load_hdr(rec);
+  const int mx = mb % mbw, my = mb / mbw, bx = b & 3, by = b >> 2;
+  const int pitch = a.pitch;
+  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
+  uint8_t *UV = Y + a.uv_off;
+  auto nb_ok = [&](int n) -> bool {
+    if (n < 0) return false;
+    const uint4 u = reinterpret_cast<const uint4 *>(frecs + n)[0];
+    if (u.x != a.epoch || u.y != h.slice) return false;
+    if (a.P.cip) {
+      const int ty = reinterpret_cast<const uint32_t *>(frecs + n)[4] & 255;
+      if (ty == kMbInter || ty == kMbSkip) return false;
+    }
+    return true;
+  };
+  const bool A = nb_ok(mx > 0 ? mb - 1 : -1);
+  const bool B = nb_ok(my > 0 ? mb - mbw : -1);
+  const bool C = nb_ok(my > 0 && mx < mbw - 1 ? mb - mbw + 1 : -1);
+  const bool D = nb_ok(mx > 0 && my > 0 ? mb - mbw - 1 : -1);
+  // borders into the tile
+  const int64_t yrow0 = static_cast<int64_t>(my * 16) * pitch + mx * 16;
+  if (b < 7 && my > 0) {
+    const bool need = b == 0 ? D : (b < 5 ? B : C);
+    uint32_t v = 0;
+    if (need) v = *reinterpret_cast<const uint32_t *>(Y + yrow0 - pitch - 4 + 4 * b);
+    *reinterpret_cast<uint32_t *>(&t.y[0][4 * b]) = v;
+  }
+  if (A) t.y[1 + b][3] = Y[yrow0 + static_cast<int64_t>(b) * pitch - 1];
+  const int64_t crow0 = static_cast<int64_t>(my * 8) * pitch + mx * 16;
+  if (b < 8 && A) {
+    const uint32_t v = *reinterpret_cast<const uint32_t *>(UV + crow0 + static_cast<int64_t>(b) * pitch - 4);
+    t.cl[0][b] = (v >> 16) & 255;
+    t.cl[1][b] = v >> 24;
+  }
+  if (b >= 8 && b < 13 && my > 0) {
+    const int i = b - 8;  // dword i of chroma row -1, interleaved bytes -4 + 4i
+    if (i == 0 ? D : B) {
+      const uint32_t v = *reinterpret_cast<const uint32_t *>(UV + crow0 - pitch - 4 + 4 * i);
+      if (i == 0) {
+        t.ct[0][0] = (v >> 16) & 255;
+        t.ct[1][0] = v >> 24;
+      } else {
+        const int c0 = 2 * (i - 1);
+        t.ct[0][1 + c0] = v & 255;
+        t.ct[1][1 + c0] = (v >> 8) & 255;
+        t.ct[0][2 + c0] = (v >> 16) & 255;
+        t.ct[1][2 + c0] = v >> 24;
+      }
+    }
+  }
+  lane_sync();
+  const int qp = h.qp;
+  if (h.type == kMbI16) {
+    const int mode = h.modes & 3;
+    int v[16];
+    if (mode == 0) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v[y * 4 + x] = t.y[0][4 + bx * 4 + x];
+    } else if (mode == 1) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v[y * 4 + x] = t.y[1 + by * 4 + y][3];
+    } else if (mode == 2) {
+      int st = 0, sl = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        st += t.y[0][4 + i];
+        sl += t.y[1 + i][3];
+      }
+      const int dc = (A && B) ? (st + sl + 16) >> 5 : (A ? (sl + 8) >> 4 : (B ? (st + 8) >> 4 : 128));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = dc;
+    } else {
+      int Hh = 0, Vv = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        Hh += (i + 1) * (t.y[0][4 + 8 + i] - t.y[0][4 + 6 - i]);
+        Vv += (i + 1) * (t.y[1 + 8 + i][3] - t.y[1 + 6 - i][3]);  // row -1 is t.y[0][3]
+      }
+      const int aa = 16 * (t.y[16][3] + t.y[0][19]);
+      const int bb = (5 * Hh + 32) >> 6, cc = (5 * Vv + 32) >> 6;
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v[y * 4 + x] = c255((aa + bb * (bx * 4 + x - 7) + cc * (by * 4 + y - 7) + 16) >> 5);
+    }
+    // 8.5.10 DC: Hadamard of the 16 DC levels (raster), scaled; this block's entry
+    int dcl[16];
+    load_coefs(a.arena, stored(h.blocks, h.coef, kBlkI16Dc), dcl);
+    int tr[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a0 = dcl[i * 4], a1 = dcl[i * 4 + 1], a2 = dcl[i * 4 + 2], a3 = dcl[i * 4 + 3];
+      tr[i * 4] = a0 + a1 + a2 + a3;
+      tr[i * 4 + 1] = a0 + a1 - a2 - a3;
+      tr[i * 4 + 2] = a0 - a1 - a2 + a3;
+      tr[i * 4 + 3] = a0 - a1 + a2 - a3;
+    }
+    const int a0 = tr[bx], a1 = tr[4 + bx], a2 = tr[8 + bx], a3 = tr[12 + bx];
+    const int f = by == 0 ? a0 + a1 + a2 + a3 : by == 1 ? a0 + a1 - a2 - a3 : by == 2 ? a0 - a1 - a2 + a3 : a0 - a1 + a2 - a3;
+    const int ls = full::level_scale(qp % 6, 0, 0);
+    int cf[16], res[16];
+    load_coefs(a.arena, stored(h.blocks, h.coef, kBlkLuma0 + blkidx(b)), cf);
+    cf[0] = qp >= 36 ? (f * ls) << (qp / 6 - 6) : (f * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    full::scale_idct4(cf, qp, true, res);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<uint32_t *>(Y + yrow0 + static_cast<int64_t>(by * 4 + r) * pitch + bx * 4) =
+          pack4(c255(v[r * 4] + res[r * 4]), c255(v[r * 4 + 1] + res[r * 4 + 1]), c255(v[r * 4 + 2] + res[r * 4 + 2]),
+                c255(v[r * 4 + 3] + res[r * 4 + 3]));
+  } else {
+    // Intra_4x4: block (bx, by) at step bx + 2 by; its left / top / top-left /
+    // top-right blocks (earlier in luma4x4BlkIdx order) are done one or more steps before
+    const int k = blkidx(b);
+    const uint32_t i4w = reinterpret_cast<const uint32_t *>(rec)[8 + (b >> 3)];
+    const int m4 = (i4w >> (((b >> 1) & 3) * 8 + (b & 1) * 4)) & 15;
+    const bool top = by > 0 || B;
+    const bool left = bx > 0 || A;
+    const bool tl = (bx > 0 && by > 0) || (by == 0 && bx > 0 ? B : (bx == 0 && by > 0 ? A : D));
+    bool tr;
+    if (by == 0) tr = bx < 3 ? B : C;
+    else tr = bx < 3 && blkidx((by - 1) * 4 + bx + 1) < k;
+    int cf[16], res[16];
+    load_coefs(a.arena, stored(h.blocks, h.coef, kBlkLuma0 + k), cf);
+    full::scale_idct4(cf, qp, false, res);
+    const int step = bx + 2 * by;
+    for (int s = 0; s <= 9; ++s) {
+      if (s == step) {
+        const int ty = by * 4, tx = 4 + bx * 4;  // tile row of p[., -1] and col of p[0, .]
+        int T[9], L[5];
+        T[0] = L[0] = tl ? t.y[ty][tx - 1] : 0;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) T[1 + x] = top ? t.y[ty][tx + x] : 0;
+#pragma unroll
+        for (int x = 4; x < 8; ++x) T[1 + x] = tr ? t.y[ty][tx + x] : T[4];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) L[1 + y] = left ? t.y[ty + 1 + y][tx - 1] : 0;
+#define PT(x) T[1 + (x)]
+#define PL(y) L[1 + (y)]
+        int o[16];
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            int v;
+            switch (m4) {
+              case 0: v = PT(x); break;
+              case 1: v = PL(y); break;
+              case 2:
+                if (top && left) v = (PT(0) + PT(1) + PT(2) + PT(3) + PL(0) + PL(1) + PL(2) + PL(3) + 4) >> 3;
+                else if (left) v = (PL(0) + PL(1) + PL(2) + PL(3) + 2) >> 2;
+                else if (top) v = (PT(0) + PT(1) + PT(2) + PT(3) + 2) >> 2;
+                else v = 128;
+                break;
+              case 3:
+                v = (x == 3 && y == 3) ? (PT(6) + 3 * PT(7) + 2) >> 2
+                                       : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
+                break;
+              case 4:
+                if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
+                else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
+                else v = (PT(0) + 2 * PT(-1) + PL(0) + 2) >> 2;
+                break;
+              case 5: {
+                const int z = 2 * x - y;
+                if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+                else v = (PL(y - 1) + 2 * PL(y - 2) + PL(y - 3) + 2) >> 2;
+                break;
+              }
+              case 6: {
+                const int z = 2 * y - x;
+                if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+                else v = (PT(x - 1) + 2 * PT(x - 2) + PT(x - 3) + 2) >> 2;
+                break;
+              }
+              case 7:
+                v = (y & 1) ? (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2
+                            : (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1;
+                break;
+              default: {
+                const int z = x + 2 * y;
+                if (z == 0 || z == 2 || z == 4) v = (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
+                else if (z == 1 || z == 3) v = (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
+                else if (z == 5) v = (PL(2) + 3 * PL(3) + 2) >> 2;
+                else v = PL(3);
+                break;
+              }
+            }
+            o[y * 4 + x] = c255(v + res[y * 4 + x]);
+          }
+#undef PT
+#undef PL
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t w4 = pack4(o[r * 4], o[r * 4 + 1], o[r * 4 + 2], o[r * 4 + 3]);
+          *reinterpret_cast<uint32_t *>(&t.y[ty + 1 + r][tx]) = w4;
+          *reinterpret_cast<uint32_t *>(Y + yrow0 + static_cast<int64_t>(by * 4 + r) * pitch + bx * 4) = w4;
+        }
+      }
+      lane_sync();
+    }
+  }
+  // chroma (8.3.4): lanes 0..7 = (plane, 4x4 block)
+  if (b < 8) {
+    const int pl = b >> 2, ck = b & 3, ox = (ck & 1) * 4, oy = (ck >> 1) * 4;
+    const int cm = (h.modes >> 2) & 3;
+    const uint8_t *T = t.ct[pl];  // T[0] = p[-1,-1], T[1 + x]
+    const uint8_t *L = t.cl[pl];  // L[y]
+    int v[16];
+    if (cm == 0) {
+      int st = 0, sl = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        st += T[1 + ox + i];
+        sl += L[oy + i];
+      }
+      int dc = 128;
+      if ((ox == 0 && oy == 0) || (ox && oy)) {
+        if (B && A) dc = (st + sl + 4) >> 3;
+        else if (A) dc = (sl + 2) >> 2;
+        else if (B) dc = (st + 2) >> 2;
+      } else if (ox) {
+        if (B) dc = (st + 2) >> 2;
+        else if (A) dc = (sl + 2) >> 2;
+      } else {
+        if (A) dc = (sl + 2) >> 2;
+        else if (B) dc = (st + 2) >> 2;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = dc;
+    } else if (cm == 1) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v[y * 4 + x] = L[oy + y];
+    } else if (cm == 2) {
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v[y * 4 + x] = T[1 + ox + x];
+    } else {
+      int Hh = 0, Vv = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        Hh += (i + 1) * (T[1 + 4 + i] - T[1 + 2 - i]);
+        Vv += (i + 1) * ((4 + i < 8 ? L[4 + i] : 0) - (2 - i >= 0 ? L[2 - i] : T[0]));
+      }
+      const int aa = 16 * (L[7] + T[8]);
+      const int bb = (34 * Hh + 32) >> 6, cc = (34 * Vv + 32) >> 6;
+#pragma unroll
+      for (int y = 0; y < 4; ++y)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v[y * 4 + x] = c255((aa + bb * (ox + x - 3) + cc * (oy + y - 3) + 16) >> 5);
+    }
+    int r[16];
+    chroma_res(a.arena, h.blocks, h.coef, pl, ck, full::qpc_of(qp, pl ? a.P.cqp_off2 : a.P.cqp_off), r);
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) t.cout[oy + y][2 * (ox + x) + pl] = static_cast<uint8_t>(c255(v[y * 4 + x] + r[y * 4 + x]));
+  }
+  lane_sync();
+  if (b < 8) {
+    const uint4 row = *reinterpret_cast<const uint4 *>(&t.cout[b][0]);
+    *reinterpret_cast<uint4 *>(UV + crow0 + static_cast<int64_t>(b) * pitch) = row;
+  }
+  lane_sync();
+}
+
+// grid: pictures of the level; the intra-predicted macroblocks by dependency level
+__global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a) {
+  extern __shared__ uint16_t s_list[];  // nmb entries
+  __shared__ IntraTile tiles[kIntraSlots];
+  __shared__ int s_max, s_cnt;
+  const int nmb = a.P.mb_width * a.P.mb_height;
+  const int slot = a.frames[blockIdx.x].x;
+  const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_max = -1;
   __syncthreads();
-  // intra macroblocks along the wavefront t = x + 2y
-  const int steps = mbw + 2 * (mbh - 1);
-  for (int t = 0; t < steps; ++t) {
-    for (int y = threadIdx.x; y < mbh; y += kReconThreads) {
-      const int x = t - 2 * y;
-      if (x < 0 || x >= mbw) continue;
-      const MbRec &m = c.recs[y * mbw + x];
-      if (m.epoch != c.epoch || m.type == kMbInter || m.type == kMbSkip) continue;
-      full::MbRecon r(c, slot, y * mbw + x, m);
-      r.run();
-      err |= r.err;
-    }
+  int m = -1;
+  for (int i = tid; i < nmb; i += kIntraThreads) {
+    const int v = lv[i];
+    if (v != kNoLevel) m = max(m, v);
+  }
+  if (m >= 0) atomicMax(&s_max, m);
+  __syncthreads();
+  const int maxl = s_max;
+  const int ms = tid >> 4, b = tid & 15;
+  for (int l = 0; l <= maxl; ++l) {
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    for (int i = tid; i < nmb; i += kIntraThreads)
+      if (lv[i] == l) s_list[atomicAdd(&s_cnt, 1)] = static_cast<uint16_t>(i);
+    __syncthreads();
+    const int n = s_cnt;
+    for (int j = ms; j < n; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms]);
     __syncthreads();
   }
-  if (err) atomicOr(a.err, err);
 }
 
-__global__ void __launch_bounds__(kDeblockThreads) h264_deblock_full(FullReconArgs a) {
+// --------------------------------------------------------------- deblocking
+__device__ __forceinline__ bool is_intra_t(int ty) { return ty == kMbI4x4 || ty == kMbI16 || ty == kMbPcm; }
+
+// bS between 4x4 blocks bp of P and bq of Q (8.7.2.1, frames, P slices)
+__device__ __forceinline__ int bs_dev(const MbRec *P, int bp, const MbRec *Q, int bq, int tp, int tq, bool mbe) {
+  if (is_intra_t(tp) || is_intra_t(tq)) return mbe ? 4 : 3;
+  if (P->nz[bp] || Q->nz[bq]) return 2;
+  const int p8 = (bp >> 3) * 2 + ((bp & 3) >> 1), q8 = (bq >> 3) * 2 + ((bq & 3) >> 1);
+  if (P->ref_slot[p8] != Q->ref_slot[q8]) return 1;
+  const uint32_t mp = reinterpret_cast<const uint32_t *>(P)[16 + bp], mq = reinterpret_cast<const uint32_t *>(Q)[16 + bq];
+  const int dx = static_cast<int16_t>(mp & 0xffff) - static_cast<int16_t>(mq & 0xffff);
+  const int dy = static_cast<int16_t>(mp >> 16) - static_cast<int16_t>(mq >> 16);
+  return (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
+}
+
+// one line of samples s[0..7] = p3 p2 p1 p0 q0 q1 q2 q3 (8.7.2.3 / 8.7.2.4)
+__device__ __forceinline__ void filt_luma(int (&s)[8], int bS, int iA, int alpha, int beta) {
+  const int p0 = s[3], p1 = s[2], q0 = s[4], q1 = s[5];
+  if (!(bS > 0 && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+  const int p2 = s[1], q2 = s[6];
+  const int ap = abs(p2 - p0), aq = abs(q2 - q0);
+  if (bS < 4) {
+    const int tc0 = kTc[iA][bS - 1];
+    const int tc = tc0 + (ap < beta) + (aq < beta);
+    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
+    s[3] = c255(p0 + delta);
+    s[4] = c255(q0 - delta);
+    if (ap < beta) s[2] = p1 + min(max((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0), tc0);
+    if (aq < beta) s[5] = q1 + min(max((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0), tc0);
+    return;
+  }
+  const int p3 = s[0], q3 = s[7];
+  const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
+  if (ap < beta && small) {
+    s[3] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+    s[2] = (p2 + p1 + p0 + q0 + 2) >> 2;
+    s[1] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+  } else {
+    s[3] = (2 * p1 + p0 + q1 + 2) >> 2;
+  }
+  if (aq < beta && small) {
+    s[4] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+    s[5] = (p0 + q0 + q1 + q2 + 2) >> 2;
+    s[6] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+  } else {
+    s[4] = (2 * q1 + q0 + p1 + 2) >> 2;
+  }
+}
+// chroma line p1 p0 q0 q1
+__device__ __forceinline__ void filt_chroma(int &p1, int &p0, int &q0, int &q1, int bS, int iA, int alpha, int beta) {
+  if (!(bS > 0 && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+  if (bS < 4) {
+    const int tc = kTc[iA][bS - 1] + 1;
+    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
+    const int np0 = c255(p0 + delta), nq0 = c255(q0 - delta);
+    p0 = np0;
+    q0 = nq0;
+    return;
+  }
+  const int np0 = (2 * p1 + p0 + q1 + 2) >> 2, nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
+  p0 = np0;
+  q0 = nq0;
+}
+
+struct DbkTile {
+  uint8_t y[20][20];  // luma rows -4..15 x cols -4..15
+  uint8_t c[10][20];  // chroma rows -2..7 x interleaved bytes -4..15
+};
+
+struct EdgeQ {  // alpha/beta/indexA for an edge between macroblocks of qp qpp, qpq
+  int iA, alpha, beta;
+};
+__device__ __forceinline__ EdgeQ edge_q(int qpav, int fa, int fb) {
+  EdgeQ e;
+  e.iA = min(max(qpav + fa, 0), 51);
+  const int iB = min(max(qpav + fb, 0), 51);
+  e.alpha = kAl[e.iA];
+  e.beta = kBe[iB];
+  return e;
+}
+
+// grid: pictures of the level
+__global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a) {
+  __shared__ DbkTile tiles[kDbkWaves * 2];
+  __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
+  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
   const int slot = a.frames[blockIdx.x].x;
-  const full::ReconCtx c = make_ctx(a, slot);
-  const int mbw = c.mbw, mbh = c.mbh;
-  const int steps = mbw + 2 * (mbh - 1);
-  for (int t = 0; t < steps; ++t) {
-    for (int y = threadIdx.x; y < mbh; y += kDeblockThreads) {
-      const int x = t - 2 * y;
-      if (x >= 0 && x < mbw) full::deblock_mb(c, slot, y * mbw + x);
+  const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
+  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
+  uint8_t *UV = Y + a.uv_off;
+  const int pitch = a.pitch;
+  for (int i = threadIdx.x; i < mbh; i += kDbkThreads) prog[i] = 0;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int half = lane >> 5, l = lane & 31;
+  DbkTile &t = tiles[wave * 2 + half];
+  const int npairs = (mbh + 1) >> 1;
+  for (int p = wave; p < npairs; p += kDbkWaves) {
+    const int y = 2 * p + half;
+    const bool row_ok = y < mbh;
+    uint32_t left = 0;  // carried cols 12..15 (luma row l / chroma row l - 16) of the previous macroblock
+    for (int it = 0; it < mbw + 2; ++it) {
+      const int x = it - 2 * half;
+      const bool act = row_ok && x >= 0 && x < mbw;
+      // the upper row of the pair waits for the row above (another wave)
+      if (half == 0 && act && y > 0) {
+        const int need = x + 1 < mbw ? x + 2 : mbw + 1;
+        while (__hip_atomic_load(&prog[y - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const int mb = y * mbw + x;
+      const MbRec *Q = frecs + (act ? mb : 0);
+      const FullSlice *sd = a.slices + (act ? Q->slice : 0);
+      const int idc = act ? sd->dbk_idc : 1;
+      const int tq = act ? (reinterpret_cast<const uint32_t *>(Q)[4] & 255) : 0;
+      const int qpq = tq == kMbPcm ? 0 : (act ? Q->qp : 0);
+      const int fa = act ? sd->dbk_a : 0, fb = act ? sd->dbk_b : 0;
+      const MbRec *PL = Q - 1, *PT = Q - mbw;
+      bool fl = act && idc != 1 && x > 0, ft = act && idc != 1 && y > 0;
+      if (fl && idc == 2 && PL->slice != Q->slice) fl = false;
+      if (ft && idc == 2 && PT->slice != Q->slice) ft = false;
+      const int tl = fl ? (reinterpret_cast<const uint32_t *>(PL)[4] & 255) : 0;
+      const int tt = ft ? (reinterpret_cast<const uint32_t *>(PT)[4] & 255) : 0;
+      const int qpl = fl ? (tl == kMbPcm ? 0 : PL->qp) : 0, qpt = ft ? (tt == kMbPcm ? 0 : PT->qp) : 0;
+      const int64_t ybase = static_cast<int64_t>(y * 16) * pitch + x * 16;
+      const int64_t cbase = static_cast<int64_t>(y * 8) * pitch + x * 16;
+      // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
+      if (act && l < 24) {
+        const bool luma = l < 16;
+        const int row = luma ? l : l - 16;
+        const uint4 q4 = *reinterpret_cast<const uint4 *>((luma ? Y + ybase : UV + cbase) + static_cast<int64_t>(row) * pitch);
+        const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
+        int r[20];
+#pragma unroll
+        for (int i = 0; i < 20; ++i) r[i] = (wv[i >> 2] >> ((i & 3) * 8)) & 255;
+        if (idc != 1) {
+          if (luma) {
+            const int br = (row >> 2) * 4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (e == 0 && !fl) continue;
+              const MbRec *Pm = e ? Q : PL;
+              const int tp = e ? tq : tl, qpp = e ? qpq : qpl;
+              const int bS = bs_dev(Pm, e ? br + e - 1 : br + 3, Q, br + e, tp, tq, e == 0);
+              if (!bS) continue;
+              const EdgeQ eq = edge_q((qpp + qpq + 1) >> 1, fa, fb);
+              if (!eq.alpha || !eq.beta) continue;
+              int s[8];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) s[i] = r[4 * e + i];
+              filt_luma(s, bS, eq.iA, eq.alpha, eq.beta);
+#pragma unroll
+              for (int i = 0; i < 8; ++i) r[4 * e + i] = s[i];
+            }
+          } else {
+            const int br = ((2 * row) >> 2) * 4;
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+              if (e == 0 && !fl) continue;
+              const MbRec *Pm = e ? Q : PL;
+              const int tp = e ? tq : tl, qpp = e ? qpq : qpl;
+              const int bS = bs_dev(Pm, e ? br + e - 1 : br + 3, Q, br + e, tp, tq, e == 0);
+              if (!bS) continue;
+#pragma unroll
+              for (int pl = 0; pl < 2; ++pl) {
+                const int off = pl ? a.P.cqp_off2 : a.P.cqp_off;
+                const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, fa, fb);
+                if (!eq.alpha || !eq.beta) continue;
+                const int c0 = 4 + 2 * (2 * e) + pl;  // q0 of chroma col 2e (luma edge e)
+                filt_chroma(r[c0 - 4], r[c0 - 2], r[c0], r[c0 + 2], bS, eq.iA, eq.alpha, eq.beta);
+              }
+            }
+          }
+        }
+        uint8_t *dst = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+          *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+      }
+      // rows above (final: the row above is two macroblocks ahead)
+      if (act && l >= 24 && l < 30 && y > 0) {
+        const int i = l - 24;
+        if (i < 4) *reinterpret_cast<uint4 *>(&t.y[i][4]) = *reinterpret_cast<const uint4 *>(Y + ybase + static_cast<int64_t>(i - 4) * pitch);
+        else *reinterpret_cast<uint4 *>(&t.c[i - 4][4]) = *reinterpret_cast<const uint4 *>(UV + cbase + static_cast<int64_t>(i - 6) * pitch);
+      }
+      lane_sync();
+      // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved chroma column l - 16
+      if (act && idc != 1) {
+        if (l < 16) {
+          const int col = l, bc = col >> 2;
+          int r[20];
+#pragma unroll
+          for (int i = 0; i < 20; ++i) r[i] = t.y[i][4 + col];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (e == 0 && !ft) continue;
+            const MbRec *Pm = e ? Q : PT;
+            const int tp = e ? tq : tt, qpp = e ? qpq : qpt;
+            const int bS = bs_dev(Pm, e ? (e - 1) * 4 + bc : 12 + bc, Q, e * 4 + bc, tp, tq, e == 0);
+            if (!bS) continue;
+            const EdgeQ eq = edge_q((qpp + qpq + 1) >> 1, fa, fb);
+            if (!eq.alpha || !eq.beta) continue;
+            int s[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s[i] = r[4 * e + i];
+            filt_luma(s, bS, eq.iA, eq.alpha, eq.beta);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[4 * e + i] = s[i];
+          }
+#pragma unroll
+          for (int i = 1; i < 20; ++i) t.y[i][4 + col] = static_cast<uint8_t>(r[i]);
+        } else {
+          const int j = l - 16, pl = j & 1, cc = j >> 1, bc = (2 * cc) >> 2;
+          const int off = pl ? a.P.cqp_off2 : a.P.cqp_off;
+          int r[10];
+#pragma unroll
+          for (int i = 0; i < 10; ++i) r[i] = t.c[i][4 + j];
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            if (e == 0 && !ft) continue;
+            const MbRec *Pm = e ? Q : PT;
+            const int tp = e ? tq : tt, qpp = e ? qpq : qpt;
+            const int bS = bs_dev(Pm, e ? (e - 1) * 4 + bc : 12 + bc, Q, e * 4 + bc, tp, tq, e == 0);
+            if (!bS) continue;
+            const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, fa, fb);
+            if (!eq.alpha || !eq.beta) continue;
+            const int q0 = 2 + 2 * e;  // chroma row 2e
+            filt_chroma(r[q0 - 2], r[q0 - 1], r[q0], r[q0 + 1], bS, eq.iA, eq.alpha, eq.beta);
+          }
+#pragma unroll
+          for (int i = 1; i < 10; ++i) t.c[i][4 + j] = static_cast<uint8_t>(r[i]);
+        }
+      }
+      lane_sync();
+      // ---- write back: rows of this macroblock shifted 4 bytes left (the left
+      // neighbour's last columns are final now), rows above, the row's tail
+      if (act) {
+        if (l < 24) {
+          const bool luma = l < 16;
+          const int row = luma ? l : l - 16;
+          const uint8_t *src = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
+          uint8_t *dst = (luma ? Y + ybase : UV + cbase) + static_cast<int64_t>(row) * pitch;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (x > 0 || i > 0) *reinterpret_cast<uint32_t *>(dst - 4 + 4 * i) = *reinterpret_cast<const uint32_t *>(src + 4 * i);
+          left = *reinterpret_cast<const uint32_t *>(src + 16);
+          if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
+        } else if (l < 28 && y > 0 && ft) {
+          const int i = l - 24;  // luma rows -3..-1, chroma row -1
+          if (i < 3) *reinterpret_cast<uint4 *>(Y + ybase + static_cast<int64_t>(i - 3) * pitch) = *reinterpret_cast<const uint4 *>(&t.y[1 + i][4]);
+          else *reinterpret_cast<uint4 *>(UV + cbase - pitch) = *reinterpret_cast<const uint4 *>(&t.c[1][4]);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      if (act && l == 0)
+        __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __syncthreads();
   }
 }
 
@@ -120,11 +949,17 @@ int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
 
 int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
-  hipLaunchKernelGGL(h264_recon_full, dim3(n_frames), dim3(kReconThreads), 0, s, a);
+  const int nmb = a.P.mb_width * a.P.mb_height;
+  if (a.P.mb_height > 1024) return fail(VTS_E_UNSUPPORTED, "picture taller than 1024 macroblock rows");
+  if (n_frames > 65535) return fail(VTS_E_UNSUPPORTED, "more than 65535 pictures in one level launch");
+  hipLaunchKernelGGL(h264_inter_full, dim3((nmb + 15) / 16, n_frames), dim3(kInterThreads), 0, s, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_full launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_inter_full launch: %s", hipGetErrorString(e));
+  hipLaunchKernelGGL(h264_intra_full, dim3(n_frames), dim3(kIntraThreads), sizeof(uint16_t) * nmb, s, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_intra_full launch: %s", hipGetErrorString(e));
   if (a.deblock) {
-    hipLaunchKernelGGL(h264_deblock_full, dim3(n_frames), dim3(kDeblockThreads), 0, s, a);
+    hipLaunchKernelGGL(h264_deblock_full, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));
   }

@@ -50,6 +50,9 @@ enum : uint32_t {
   kPcmBlocks = 12,      // I_PCM: 384 samples in 12 blocks (256 luma, 64 Cb, 64 Cr)
 };
 
+// MbRec-parallel intra dependency level of a macroblock that is not intra-predicted
+constexpr uint16_t kNoLevel = 0xffff;
+
 enum : uint8_t {
   kMbInter = 0,
   kMbI4x4 = 1,

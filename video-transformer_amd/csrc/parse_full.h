@@ -130,6 +130,7 @@ struct Parser {
   const FullSlice *s;
   const FullParams *P;
   MbRec *recs;            // the frame's records (global)
+  uint16_t *ilvl;         // the frame's intra dependency levels (kNoLevel: not intra-predicted)
   int16_t *arena;         // window coefficient arena, 16 int16 per block
   FullScratch *sc;
   uint32_t used;          // blocks stored so far in the slice
@@ -372,6 +373,20 @@ struct Parser {
     (void)addr;
   }
   VTS_HD VTS_INLINE void end_mb(int addr) {
+    // intra dependency level: 1 + the highest level among the intra-predicted
+    // neighbours A, B, C, D the prediction may read (same slice), else 0; the
+    // reconstruction runs the levels in order (h264_intra_full)
+    uint16_t lv = kNoLevel;
+    if (sc->cur.type == kMbI4x4 || sc->cur.type == kMbI16) {
+      int l = 0, xw, yw;
+      const int nbx[4] = {-1, 0, 16, -1}, nby[4] = {0, -1, -1, -1};
+      for (int i = 0; i < 4; ++i) {
+        const int n = nb_mb(addr, nbx[i], nby[i], 16, &xw, &yw);
+        if (n >= 0 && ilvl[n] != kNoLevel) l = vts_max(l, ilvl[n] + 1);
+      }
+      lv = static_cast<uint16_t>(l);
+    }
+    ilvl[addr] = lv;
 #if defined(__HIPCC__)
     uint4 *d = reinterpret_cast<uint4 *>(&recs[addr]);
     const uint4 *s4 = reinterpret_cast<const uint4 *>(&sc->cur);
@@ -606,12 +621,14 @@ struct Parser {
 // Parse slice `s` (window slice index si) into recs (the frame's records) and
 // the arena.  Returns DEC_E_* bits.
 VTS_HD inline uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams &P,
-                                        MbRec *frame_recs, int16_t *arena, uint32_t epoch, FullScratch *sc) {
+                                        MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena, uint32_t epoch,
+                                        FullScratch *sc) {
   const uint8_t *nal = es + s.nal_offset;
   Parser p;
   p.s = &s;
   p.P = &P;
   p.recs = frame_recs;
+  p.ilvl = frame_ilvl;
   p.arena = arena;
   p.sc = sc;
   p.used = 0;

@@ -127,6 +127,7 @@ struct vts_ctx {
   std::vector<vts::FullSlice> fslices;  // every window's slices (window-relative slots, arena)
   vts::FullSlice *d_fslices = nullptr;
   vts::MbRec *d_recs[2] = {nullptr, nullptr};
+  uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   int16_t *d_arena[2] = {nullptr, nullptr};
   int64_t arena_blocks = 0;             // per ring
   // kept from open for a later switch to the general decoder (decoder = auto)

@@ -99,7 +99,7 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   }
   // windows
   const int64_t tw_f = static_cast<int64_t>(c->width / c->k) * (c->height / c->k);
-  const int64_t per_frame = c->frame_stride + nmb * static_cast<int64_t>(sizeof(MbRec)) +
+  const int64_t per_frame = c->frame_stride + nmb * static_cast<int64_t>(sizeof(MbRec) + sizeof(uint16_t)) +
                             score_workspace_bytes(c->width, c->height, c->k, 1) +
                             32 * ((cap_total + n - 1) / std::max<int64_t>(1, n));
   size_t free_b = 0, total_b = 0;
@@ -216,6 +216,7 @@ int run_general(vts_ctx *c) {
     pa.slice0 = 0;
     pa.epoch = epoch;
     pa.recs = c->d_recs[r];
+    pa.ilvl = c->d_ilvl[r];
     pa.arena = c->d_arena[r];
     pa.err = c->d_err;
     pa.P = c->fprm;
@@ -223,6 +224,7 @@ int run_general(vts_ctx *c) {
     HIP_TRY(hipEventRecord(E[1], sd));
     FullReconArgs ra{};
     ra.recs = c->d_recs[r];
+    ra.ilvl = c->d_ilvl[r];
     ra.arena = c->d_arena[r];
     ra.slices = c->d_fslices + w.fs0;
     ra.surf = c->d_surf[r];
