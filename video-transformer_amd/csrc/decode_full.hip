@@ -33,22 +33,24 @@
 namespace vts {
 namespace {
 
-constexpr int kParseLanes = 64;
 constexpr int kInterThreads = 256;   // 16 macroblocks x 16 blocks
 constexpr int kIntraThreads = 1024;  // 64 macroblocks in flight
 constexpr int kIntraSlots = kIntraThreads / 16;
 constexpr int kDbkThreads = 1024;    // 16 waves = 16 row pairs in flight
 constexpr int kDbkWaves = kDbkThreads / 64;
 
-__global__ void __launch_bounds__(kParseLanes) h264_parse_full(FullParseArgs a) {
-  __shared__ full::FullScratch scratch[kParseLanes];
-  const int i = blockIdx.x * kParseLanes + threadIdx.x;
-  if (i >= a.n_slices) return;
-  const FullSlice s = a.slices[i];
-  const int64_t nmb = static_cast<int64_t>(a.P.mb_width) * a.P.mb_height;
-  const uint32_t e = full::parse_slice_full(a.es, s, static_cast<uint32_t>(a.slice0 + i), a.P,
+// One slice per wave and the wave's one lane: every value of the parse is
+// wave-uniform, so control flow never diverges and the integer work can go to
+// the scalar unit; the parallelism is the window's slices (thousands of waves).
+__global__ void __launch_bounds__(1) h264_parse_full(FullParseArgs a) {
+  __shared__ full::FullScratch scratch;
+  const int i = blockIdx.x;
+  const FullSlice &s = a.slices[i];
+  const FullParams P = a.P;
+  const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
+  const uint32_t e = full::parse_slice_full(a.es, s, static_cast<uint32_t>(a.slice0 + i), P,
                                             a.recs + s.slot * nmb, a.ilvl + s.slot * nmb, a.arena, a.epoch,
-                                            &scratch[threadIdx.x]);
+                                            &scratch);
   if (e) atomicOr(a.err, e);
 }
 
@@ -941,7 +943,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
 
 int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
   if (a.n_slices <= 0) return VTS_OK;
-  hipLaunchKernelGGL(h264_parse_full, dim3((a.n_slices + kParseLanes - 1) / kParseLanes), dim3(kParseLanes), 0, s, a);
+  hipLaunchKernelGGL(h264_parse_full, dim3(a.n_slices), dim3(1), 0, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_parse_full launch: %s", hipGetErrorString(e));
   return VTS_OK;

@@ -118,17 +118,33 @@ static const uint8_t *const kCbpP = h264::kCbpInter;
 VTS_HD VTS_INLINE int blk_x(int k) { return ((k >> 2) & 1) * 2 + (k & 1); }
 VTS_HD VTS_INLINE int blk_y(int k) { return ((k >> 3) & 1) * 2 + ((k >> 1) & 1); }
 
-// Per-lane scratch (LDS on the device).
+// Per-lane scratch (LDS on the device): everything the parser indexes at run
+// time lives here, so nothing spills to scratch memory, and the neighbours a
+// macroblock reads are LDS copies instead of global records.
+constexpr int kCacheWords = 17;  // bit reader: 64-byte blocks
 struct FullScratch {
-  MbRec cur;              // the macroblock being parsed
+  MbRec mb[2];            // the macroblock being parsed and the previous one (left neighbour)
+  MbRec top[3];           // row above, columns x-1, x, x+1 at slot column % 3: bytes 16..63 and
+                          // 112..127 of the record (type, refs, modes, nz, bottom motion),
+                          // word 0 = its intra dependency level
   int16_t blk[16];        // coefficient block being decoded (raster)
-  uint32_t cache[6];      // WinBits byte cache
+  int32_t lev[16];        // its levels in decoding order
+  uint32_t cache[kCacheWords];
+  uint8_t prev[16], rem[16];  // Intra4x4 prev_intra4x4_pred_mode_flag / rem_intra4x4_pred_mode
+  int8_t sub[4], refs[4];     // sub_mb_type / ref_idx_l0 of the partitions
+};
+
+typedef uint32_t u32x4 __attribute__((vector_size(16)));  // SROA-friendly (uint4 copies are memmoves)
+// the parts of a row-above record the parser reads (record bytes 16..63, 112..127)
+struct TopCtx {
+  u32x4 v0, v1, v2, v3;
+  uint32_t lvl;
 };
 
 struct Parser {
-  WinBits br;
-  const FullSlice *s;
-  const FullParams *P;
+  WinBitsT<kCacheWords> br;
+  const FullSlice *s;     // global (the ref_slot table is indexed at run time)
+  int cip;                // constrained_intra_pred_flag
   MbRec *recs;            // the frame's records (global)
   uint16_t *ilvl;         // the frame's intra dependency levels (kNoLevel: not intra-predicted)
   int16_t *arena;         // window coefficient arena, 16 int16 per block
@@ -139,6 +155,16 @@ struct Parser {
   int mbw;
   int first_mb;
   uint32_t err;
+  int cur_addr;           // macroblock being parsed
+  int cs;                 // sc->mb[cs] = current, sc->mb[cs ^ 1] = previous
+  int tslots;             // sc->top slots of D, B, C in bits 0-1, 2-3, 4-5 (one field: a ?:
+                          // between three fields becomes a select of their addresses)
+  uint16_t lvl_prev;      // intra dependency level of the previous macroblock
+  // row above, column pf_col: prefetched during the previous macroblock
+  int pf_col;
+  TopCtx pf;
+  uint32_t todo;          // residual blocks of the current macroblock still to decode (kBlk* bits)
+  bool cur_i16;           // the current macroblock is Intra_16x16
 
   // --- neighbour access (6.4.12): mb -1 unavailable, -2 the current MB
   VTS_HD VTS_INLINE int nb_mb(int cur, int xN, int yN, int maxW, int *xw, int *yw) const {
@@ -157,10 +183,67 @@ struct Parser {
     *yw = (yN + maxW) % maxW;
     return n;
   }
-  VTS_HD VTS_INLINE const MbRec &rec(int n) const { return n == -2 ? sc->cur : recs[n]; }
+  VTS_HD VTS_INLINE MbRec &cur() const { return sc->mb[cs]; }
+  VTS_HD VTS_INLINE const MbRec &rec(int n) const {
+    if (n == -2) return sc->mb[cs];
+    if (n == cur_addr - 1) return sc->mb[cs ^ 1];
+    const int d = n - (cur_addr - mbw);  // -1, 0, 1: D, B, C
+    return sc->top[(tslots >> (2 * (d + 1))) & 3];
+  }
+  VTS_HD VTS_INLINE int level_of(int n) const {
+    if (n == cur_addr - 1) return lvl_prev;
+    return static_cast<int>(rec(n).epoch);
+  }
+
+  // --- row-above contexts (global record -> LDS slot)
+  VTS_HD VTS_INLINE TopCtx top_load(int col) const {
+    const int n = cur_addr - mbw + (col - cur_addr % mbw);
+    const u32x4 *g = reinterpret_cast<const u32x4 *>(recs + n);
+    TopCtx t;
+    t.v0 = g[1];
+    t.v1 = g[2];
+    t.v2 = g[3];
+    t.v3 = g[7];
+    t.lvl = ilvl[n];
+    return t;
+  }
+  VTS_HD VTS_INLINE void top_store(int col, TopCtx t) const {
+    u32x4 *d = reinterpret_cast<u32x4 *>(&sc->top[col % 3]);
+    d[1] = t.v0;
+    d[2] = t.v1;
+    d[3] = t.v2;
+    d[7] = t.v3;
+    sc->top[col % 3].epoch = t.lvl;
+  }
+  VTS_HD VTS_INLINE void top_sync(int col) const { top_store(col, top_load(col)); }
+  // a new macroblock: the previous one becomes the left neighbour; the row
+  // above rotates through the three slots, its next column loading one
+  // macroblock ahead
+  VTS_HD VTS_INLINE void advance(int addr) {
+    const bool cont = addr > first_mb && addr == cur_addr + 1 && addr % mbw != 0;
+    cs ^= 1;
+    cur_addr = addr;
+    const int x = addr % mbw, y = addr / mbw;
+    tslots = ((x + 2) % 3) | ((x % 3) << 2) | (((x + 1) % 3) << 4);
+    if (y > 0) {
+      if (!cont) {
+        if (x > 0) top_sync(x - 1);
+        top_sync(x);
+      }
+      if (x + 1 < mbw) {
+        if (pf_col != x + 1) pf = top_load(x + 1);
+        top_store(x + 1, pf);
+      }
+      pf_col = -1;
+      if (x + 2 < mbw) {
+        pf = top_load(x + 2);
+        pf_col = x + 2;
+      }
+    }
+  }
 
   // 9.2.1 nC
-  VTS_HD int nc_of(int cur, int bx, int by, bool chroma, int plane) const {
+  VTS_HD VTS_INLINE int nc_of(int cur, int bx, int by, bool chroma, int plane) const {
     const int maxW = chroma ? 8 : 16;
     int xa, ya, xb, yb;
     const int a = nb_mb(cur, bx * 4 - 1, by * 4, maxW, &xa, &ya);
@@ -184,7 +267,7 @@ struct Parser {
 
   // residual_block_cavlc into sc->blk (raster, coefficient list index k ->
   // zig-zag position k + start_pos); returns TotalCoeff or -1
-  VTS_HD int residual_block(int nC, int maxNum, int start_pos) {
+  VTS_HD VTS_INLINE int residual_block(int nC, int maxNum, int start_pos) {
     for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
     int tc, t1;
     br.ensure(32);
@@ -219,7 +302,7 @@ struct Parser {
     }
     if (tc > maxNum) return -1;
     if (tc == 0) return 0;
-    int level[16];
+    int32_t *level = sc->lev;
     int suffix_len = (tc > 10 && t1 < 3) ? 1 : 0;
     for (int i = 0; i < tc; ++i) {
       if (i < t1) {
@@ -291,15 +374,15 @@ struct Parser {
     if (used >= s->arena_cap) return false;
     int16_t *dst = arena + 16 * static_cast<int64_t>(s->arena + used);
 #if defined(__HIPCC__)
-    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(sc->blk);
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(dst);
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(sc->blk);
     d4[0] = s4[0];
     d4[1] = s4[1];
 #else
     for (int i = 0; i < 16; ++i) dst[i] = sc->blk[i];
 #endif
-    if (sc->cur.blocks == 0) sc->cur.coef = s->arena + used;
-    sc->cur.blocks |= 1u << bit;
+    if (cur().blocks == 0) cur().coef = s->arena + used;
+    cur().blocks |= 1u << bit;
     ++used;
     return true;
   }
@@ -309,7 +392,7 @@ struct Parser {
     bool avail;
     int ref, x, y;
   };
-  VTS_HD Mv nb_mv(int cur, int xN, int yN, uint32_t done) const {
+  VTS_HD VTS_INLINE Mv nb_mv(int cur, int xN, int yN, uint32_t done) const {
     Mv r{false, -1, 0, 0};
     int xw, yw;
     const int n = nb_mb(cur, xN, yN, 16, &xw, &yw);
@@ -324,7 +407,7 @@ struct Parser {
     r.y = m.mv[b][1];
     return r;
   }
-  VTS_HD void mv_pred(int cur, int x0, int y0, int w, int h, int ref, uint32_t done, int *px, int *py) const {
+  VTS_HD VTS_INLINE void mv_pred(int cur, int x0, int y0, int w, int h, int ref, uint32_t done, int *px, int *py) const {
     const Mv A = nb_mv(cur, x0 - 1, y0, done);
     Mv B = nb_mv(cur, x0, y0 - 1, done);
     Mv C = nb_mv(cur, x0 + w, y0 - 1, done);
@@ -352,7 +435,8 @@ struct Parser {
   }
 
   VTS_HD VTS_INLINE void begin_mb(int addr) {
-    MbRec &m = sc->cur;
+    advance(addr);
+    MbRec &m = cur();
     m.epoch = epoch;
     m.slice = slice_index;
     m.coef = 0;
@@ -370,44 +454,48 @@ struct Parser {
       m.mv[i][0] = m.mv[i][1] = 0;
     }
     for (int i = 0; i < 8; ++i) m.nzc[i] = 0;
-    (void)addr;
   }
   VTS_HD VTS_INLINE void end_mb(int addr) {
     // intra dependency level: 1 + the highest level among the intra-predicted
     // neighbours A, B, C, D the prediction may read (same slice), else 0; the
     // reconstruction runs the levels in order (h264_intra_full)
     uint16_t lv = kNoLevel;
-    if (sc->cur.type == kMbI4x4 || sc->cur.type == kMbI16) {
+    const MbRec &c = cur();
+    if (c.type == kMbI4x4 || c.type == kMbI16) {
       int l = 0, xw, yw;
-      const int nbx[4] = {-1, 0, 16, -1}, nby[4] = {0, -1, -1, -1};
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int n = nb_mb(addr, nbx[i], nby[i], 16, &xw, &yw);
-        if (n >= 0 && ilvl[n] != kNoLevel) l = vts_max(l, ilvl[n] + 1);
+        const int n = nb_mb(addr, i == 2 ? 16 : (i == 1 ? 0 : -1), i == 0 ? 0 : -1, 16, &xw, &yw);
+        if (n >= 0) {
+          const int ln = level_of(n);
+          if (ln != kNoLevel) l = vts_max(l, ln + 1);
+        }
       }
       lv = static_cast<uint16_t>(l);
     }
     ilvl[addr] = lv;
+    lvl_prev = lv;
 #if defined(__HIPCC__)
-    uint4 *d = reinterpret_cast<uint4 *>(&recs[addr]);
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(&sc->cur);
+    u32x4 *d = reinterpret_cast<u32x4 *>(&recs[addr]);
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(&cur());
 #pragma unroll
     for (int i = 0; i < 8; ++i) d[i] = s4[i];
 #else
-    recs[addr] = sc->cur;
+    recs[addr] = cur();
 #endif
   }
 
   VTS_HD VTS_INLINE void set_motion(int b, int ref, int mvx, int mvy) {
-    sc->cur.mv[b][0] = static_cast<int16_t>(mvx);
-    sc->cur.mv[b][1] = static_cast<int16_t>(mvy);
+    cur().mv[b][0] = static_cast<int16_t>(mvx);
+    cur().mv[b][1] = static_cast<int16_t>(mvy);
     const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
-    sc->cur.ref[p8] = static_cast<int8_t>(ref);
-    sc->cur.ref_slot[p8] = s->ref_slot[ref & 31];
+    cur().ref[p8] = static_cast<int8_t>(ref);
+    cur().ref_slot[p8] = s->ref_slot[ref & 31];
   }
 
-  VTS_HD void skip_mb(int addr, int qp) {
+  VTS_HD VTS_INLINE void skip_mb(int addr, int qp) {
     begin_mb(addr);
-    MbRec &m = sc->cur;
+    MbRec &m = cur();
     m.type = kMbSkip;
     m.qp = static_cast<uint8_t>(qp);
     int xw, yw;
@@ -418,13 +506,12 @@ struct Parser {
       mv_pred(addr, 0, 0, 16, 16, 0, 0, &px, &py);
     if (s->ref_slot[0] < 0) err |= DEC_E_NO_REF;
     for (int i = 0; i < 16; ++i) set_motion(i, 0, px, py);
-    end_mb(addr);
   }
 
   // macroblock_layer(); returns false to stop the slice
-  VTS_HD bool mb_layer(int addr, int *qp) {
+  VTS_HD VTS_INLINE bool mb_layer(int addr, int *qp) {
     begin_mb(addr);
-    MbRec &m = sc->cur;
+    MbRec &m = cur();
     const int mb_type = static_cast<int>(br.ue());
     const int itype = s->is_p ? mb_type - 5 : mb_type;  // < 0: inter
     if (mb_type > (s->is_p ? 30 : 25)) {
@@ -448,17 +535,17 @@ struct Parser {
         }
       }
       m.blocks = 0;  // PCM samples: kPcmBlocks from coef, not a kBlk mask
-      end_mb(addr);
+      todo = 0;
       return true;
     }
     int cbp = 0;
     bool i16 = false;
     if (itype == 0) {  // I_NxN
       m.type = kMbI4x4;
-      int prev[16], rem[16];
+      uint8_t *prev = sc->prev, *rem = sc->rem;
       for (int k = 0; k < 16; ++k) {
-        prev[k] = static_cast<int>(br.bit());
-        rem[k] = prev[k] ? 0 : static_cast<int>(br.bits(3));
+        prev[k] = static_cast<uint8_t>(br.bit());
+        rem[k] = prev[k] ? 0 : static_cast<uint8_t>(br.bits(3));
       }
       for (int k = 0; k < 16; ++k) {
         const int bx = blk_x(k), by = blk_y(k);
@@ -467,7 +554,7 @@ struct Parser {
         const int b = nb_mb(addr, bx * 4, by * 4 - 1, 16, &xb, &yb);
         int pred = 2;
         bool dcf = a == -1 || b == -1;
-        if (!dcf && P->cip) {
+        if (!dcf && cip) {
           const int ta = rec(a).type, tb = rec(b).type;
           dcf = ta == kMbInter || ta == kMbSkip || tb == kMbInter || tb == kMbSkip;
         }
@@ -496,18 +583,23 @@ struct Parser {
     } else {  // inter
       m.type = kMbInter;
       const int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
-      int sub[4] = {0, 0, 0, 0}, refs[4] = {0, 0, 0, 0};
+      int8_t *sub = sc->sub, *refs = sc->refs;
+      for (int k = 0; k < 4; ++k) sub[k] = refs[k] = 0;
       if (mb_type >= 3)
         for (int k = 0; k < 4; ++k) {
-          sub[k] = static_cast<int>(br.ue());
-          if (sub[k] > 3) {
+          const uint32_t sv = br.ue();
+          sub[k] = static_cast<int8_t>(sv & 7);
+          if (sv > 3) {
             err |= DEC_E_SYNTAX;
             return false;
           }
         }
       const int nref = s->num_ref;
       if (mb_type != 4 && nref > 1)
-        for (int k = 0; k < nparts; ++k) refs[k] = nref == 2 ? static_cast<int>(!br.bit()) : static_cast<int>(br.ue());
+        for (int k = 0; k < nparts; ++k) {
+          const uint32_t rv = nref == 2 ? static_cast<uint32_t>(!br.bit()) : br.ue();
+          refs[k] = static_cast<int8_t>(rv > 127 ? 127 : rv);
+        }
       for (int k = 0; k < nparts; ++k)
         if (refs[k] >= nref || s->ref_slot[refs[k] & 31] < 0) {
           err |= DEC_E_NO_REF;
@@ -567,53 +659,63 @@ struct Parser {
       *qp = (*qp + dq + 52) % 52;
     }
     m.qp = static_cast<uint8_t>(*qp);
-    // ---- residual (7.3.5.3)
-    if (i16) {
-      const int tc = residual_block(nc_of(addr, 0, 0, false, 0), 16, 0);
-      VTS_PARSE_TRACE("  i16 dc tc %d bits %d\n", tc, br.consumed());
-      if (tc < 0) { err |= DEC_E_SYNTAX; return false; }
-      if (tc > 0 && !store_block(kBlkI16Dc)) { err |= DEC_E_SYNTAX; return false; }
-    }
-    for (int k = 0; k < 16; ++k) {
-      if (!((cbp >> (k >> 2)) & 1)) continue;
-      const int bx = blk_x(k), by = blk_y(k);
-      const int n = nc_of(addr, bx, by, false, 0);
-      const int tc = i16 ? residual_block(n, 15, 1) : residual_block(n, 16, 0);
-      VTS_PARSE_TRACE("  luma blk %d nC %d tc %d bits %d\n", k, n, tc, br.consumed());
-      if (tc < 0) { err |= DEC_E_SYNTAX; return false; }
-      m.nz[by * 4 + bx] = static_cast<uint8_t>(tc);
-      if (tc > 0 && !store_block(kBlkLuma0 + k)) { err |= DEC_E_SYNTAX; return false; }
-    }
-    if (cbp >> 4) {
-      for (int pl = 0; pl < 2; ++pl) {
-        const int tc = residual_block(-1, 4, 0);
-        VTS_PARSE_TRACE("  chroma dc %d tc %d bits %d\n", pl, tc, br.consumed());
-        if (tc < 0) { err |= DEC_E_SYNTAX; return false; }
-        if (tc > 0) {
-          // chroma DC levels in list order (not zig-zag): undo the scan
-          int16_t lv[4];
-          for (int i = 0; i < 4; ++i) lv[i] = sc->blk[kZz[i]];
-          for (int i = 0; i < 16; ++i) sc->blk[i] = i < 4 ? lv[i] : 0;
-          if (!store_block(kBlkChromaDc0 + pl)) { err |= DEC_E_SYNTAX; return false; }
-        }
-      }
-    }
-    if ((cbp >> 4) & 2) {
-      for (int pl = 0; pl < 2; ++pl)
-        for (int k = 0; k < 4; ++k) {
-          const int n = nc_of(addr, k & 1, k >> 1, true, pl);
-          const int tc = residual_block(n, 15, 1);
-          VTS_PARSE_TRACE("  chroma ac %d %d nC %d tc %d bits %d\n", pl, k, n, tc, br.consumed());
-          if (tc < 0) { err |= DEC_E_SYNTAX; return false; }
-          m.nzc[pl * 4 + k] = static_cast<uint8_t>(tc);
-          if (tc > 0 && !store_block(kBlkChromaAc0 + 4 * pl + k)) { err |= DEC_E_SYNTAX; return false; }
-        }
-    }
+    // residual blocks (7.3.5.3), in bitstream order = kBlk* bit order; they are
+    // decoded one per step of the slice loop (block_step)
+    uint32_t t = 0;
+    if (i16) t |= 1u << kBlkI16Dc;
+    for (int q = 0; q < 4; ++q)
+      if ((cbp >> q) & 1) t |= 15u << (kBlkLuma0 + 4 * q);
+    if (cbp >> 4) t |= 3u << kBlkChromaDc0;
+    if ((cbp >> 4) & 2) t |= 255u << kBlkChromaAc0;
+    todo = t;
+    cur_i16 = i16;
     if (br.err || br.overrun()) {
       err |= DEC_E_SYNTAX;
       return false;
     }
-    end_mb(addr);
+    return true;
+  }
+
+  // one residual block of the current macroblock (the lowest bit of todo);
+  // returns false to stop the slice
+  VTS_HD VTS_INLINE bool block_step(int addr) {
+    const uint32_t bt = static_cast<uint32_t>(__builtin_ctz(todo));
+    todo &= todo - 1u;
+    MbRec &m = cur();
+    int nC = -1, maxNum = 15, start = 1;
+    const bool luma = bt < kBlkChromaDc0, chroma_ac = bt >= kBlkChromaAc0;
+    const int k = bt >= kBlkLuma0 && luma ? static_cast<int>(bt) - kBlkLuma0 : 0;
+    const int j = chroma_ac ? static_cast<int>(bt) - kBlkChromaAc0 : 0;
+    if (luma) {
+      nC = nc_of(addr, blk_x(k), blk_y(k), false, 0);
+      if (bt == kBlkI16Dc || !cur_i16) {
+        maxNum = 16;
+        start = 0;
+      }
+    } else if (chroma_ac) {
+      nC = nc_of(addr, j & 3 & 1, (j & 3) >> 1, true, j >> 2);
+    } else {
+      maxNum = 4;
+      start = 0;
+    }
+    const int tc = residual_block(nC, maxNum, start);
+    if (tc < 0 || br.err) {
+      err |= DEC_E_SYNTAX;
+      return false;
+    }
+    if (bt >= kBlkLuma0 && luma) m.nz[blk_y(k) * 4 + blk_x(k)] = static_cast<uint8_t>(tc);
+    if (chroma_ac) m.nzc[j] = static_cast<uint8_t>(tc);
+    if (tc > 0) {
+      if (!luma && !chroma_ac) {  // chroma DC levels in list order (not zig-zag): undo the scan
+        int16_t lv[4];
+        for (int i = 0; i < 4; ++i) lv[i] = sc->blk[kZz[i]];
+        for (int i = 0; i < 16; ++i) sc->blk[i] = i < 4 ? lv[i] : 0;
+      }
+      if (!store_block(bt)) {
+        err |= DEC_E_SYNTAX;
+        return false;
+      }
+    }
     return true;
   }
 };
@@ -626,7 +728,7 @@ VTS_HD inline uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, u
   const uint8_t *nal = es + s.nal_offset;
   Parser p;
   p.s = &s;
-  p.P = &P;
+  p.cip = P.cip;
   p.recs = frame_recs;
   p.ilvl = frame_ilvl;
   p.arena = arena;
@@ -637,6 +739,11 @@ VTS_HD inline uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, u
   p.mbw = P.mb_width;
   p.first_mb = s.first_mb;
   p.err = 0;
+  p.cur_addr = -2;
+  p.cs = 0;
+  p.tslots = 0;
+  p.lvl_prev = kNoLevel;
+  p.pf_col = -1;
   const int nmb = P.mb_width * P.mb_height;
   int32_t last = s.nal_size - 1;
   while (last > 0 && nal[last] == 0) --last;
@@ -648,35 +755,59 @@ VTS_HD inline uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, u
   p.br.reset_at(s.data_byte, s.data_bit & ~7);
   p.br.ensure(8);
   p.br.skip(s.data_bit & 7);
-  int addr = s.first_mb, qp = s.qp;
-  bool more = true;
-  while (more) {
-    if (addr >= nmb) {
-      p.err |= DEC_E_SYNTAX;
-      break;
-    }
-    if (s.is_p) {
-      const int run = static_cast<int>(p.br.ue());
+  p.todo = 0;
+  p.cur_i16 = false;
+  // slice_data() as a state machine whose every iteration does one small step
+  // (a skipped macroblock, a macroblock header, or one residual block), so the
+  // lanes of a wave - each parsing its own slice - meet again in the same
+  // code at every iteration instead of serialising whole macroblocks
+  enum { kRun, kSkip, kHeader, kBlock };
+  int addr = s.first_mb, qp = s.qp, run = 0;
+  int state = s.is_p ? kRun : kHeader;
+  if (addr >= nmb) p.err |= DEC_E_SYNTAX;
+  while (!p.err) {
+    bool finish = false;  // the current macroblock is complete
+    if (state == kBlock) {
+      if (!p.block_step(addr)) break;
+      finish = p.todo == 0;
+    } else if (state == kRun) {
+      run = static_cast<int>(p.br.ue());
       if (p.br.err || addr + run > nmb) {
         p.err |= DEC_E_SYNTAX;
         break;
       }
-      for (int i = 0; i < run; ++i, ++addr) p.skip_mb(addr, qp);
-      if (run > 0) {
-        more = p.br.more(stop_byte, stop_bit);
-        if (!more) break;
+      state = run > 0 ? kSkip : kHeader;
+      if (state == kHeader && addr >= nmb) {
+        p.err |= DEC_E_SYNTAX;
+        break;
       }
+    } else if (state == kSkip) {
+      p.skip_mb(addr, qp);
+      p.end_mb(addr);
+      ++addr;
+      if (--run == 0) {
+        if (!p.br.more(stop_byte, stop_bit)) break;
+        if (addr >= nmb) {
+          p.err |= DEC_E_SYNTAX;
+          break;
+        }
+        state = kHeader;
+      }
+    } else {
+      if (!p.mb_layer(addr, &qp)) break;
+      state = kBlock;
+      finish = p.todo == 0;
+    }
+    if (finish) {
+      p.end_mb(addr);
+      ++addr;
+      if (!p.br.more(stop_byte, stop_bit)) break;
       if (addr >= nmb) {
         p.err |= DEC_E_SYNTAX;
         break;
       }
+      state = s.is_p ? kRun : kHeader;
     }
-    const bool ok = p.mb_layer(addr, &qp);
-    VTS_PARSE_TRACE("mb %d type %d cbp %d qp %d bits %d err %u\n", addr, p.sc->cur.type, p.sc->cur.cbp, qp,
-                    p.br.consumed(), p.err);
-    if (!ok) break;
-    ++addr;
-    more = p.br.more(stop_byte, stop_bit);
   }
   if (!p.err && (p.br.err || p.br.overrun() || p.br.consumed() != stop_bit - 8ll * p.br.epb)) p.err |= DEC_E_SYNTAX;
   return p.err;

@@ -39,7 +39,8 @@ struct alignas(16) Cmd2 {
 // and is appended whole, otherwise it goes byte by byte and the EPBs are
 // dropped.  ue()/se() decode with one count-leading-zeros instead of a loop
 // per bit.  Positions: `fill - nb` is the RBSP bit index of the next bit.
-struct WinBits {
+template <int kW>
+struct WinBitsT {
   const uint8_t *base;   // first payload byte (absolute pointer)
   int64_t abs0;          // byte offset of `base` inside the ES buffer
   uint64_t win;          // next bits, MSB first
@@ -52,7 +53,7 @@ struct WinBits {
   int32_t epb;           // emulation-prevention bytes removed so far
   int32_t epb_next;      // RBSP byte index that followed the last removed EPB
   int32_t cache_at;      // payload index of cache[0] (multiple of 16), -1 none
-  uint32_t *cache;       // 5 words = 20 payload bytes from cache_at: per-lane
+  uint32_t *cache;       // kW words = 4 (kW - 1) payload bytes + 4 from cache_at: per-lane
                          // scratch (LDS on the device), so the copies at every
                          // control-flow join that register state costs are avoided
   bool err;
@@ -71,17 +72,26 @@ struct WinBits {
   // 4 payload bytes at i (little endian: byte i in bits 0..7); reads up to 24
   // bytes past the payload (the ES buffer is padded)
   VTS_HD VTS_INLINE uint32_t load4(int32_t i) {
-    const int32_t blk = i & ~15;
+    constexpr int32_t kBlk = 4 * (kW - 1);  // bytes per cache block (16 or 64)
+    const int32_t blk = i - (i % kBlk);
     if (blk != cache_at) {
       const uint8_t *pb = base + blk;
       const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pb) & 3);
       const uint32_t *w = reinterpret_cast<const uint32_t *>(pb - sh);  // global, not flat
-      const uint32_t t0 = w[0], t1 = w[1], t2 = w[2], t3 = w[3], t4 = w[4], t5 = w[5];
-      cache[0] = sh ? vts_alignbyte(t1, t0, sh) : t0;
-      cache[1] = sh ? vts_alignbyte(t2, t1, sh) : t1;
-      cache[2] = sh ? vts_alignbyte(t3, t2, sh) : t2;
-      cache[3] = sh ? vts_alignbyte(t4, t3, sh) : t3;
-      cache[4] = sh ? vts_alignbyte(t5, t4, sh) : t4;
+      uint32_t t[kW + 1];
+      if constexpr (kW > 5) {
+        // wave-uniform parse (h264_parse_full): keep these vector loads; as
+        // scalar loads the compiler folded the alignment into an SMEM base of
+        // (aligned - 1) + offset 1, which reads the wrong dword
+        const volatile uint32_t *vw = w;
+#pragma unroll
+        for (int k = 0; k <= kW; ++k) t[k] = vw[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k <= kW; ++k) t[k] = w[k];
+      }
+#pragma unroll
+      for (int k = 0; k < kW; ++k) cache[k] = sh ? vts_alignbyte(t[k + 1], t[k], sh) : t[k];
       cache_at = blk;
     }
     const int32_t o = i - blk, q = o >> 2, r = o & 3;
@@ -191,6 +201,7 @@ struct WinBits {
     zeros = (b1 != 0) ? 0 : ((b2 != 0) ? 1 : 2);
   }
 };
+using WinBits = WinBitsT<5>;
 
 VTS_HD VTS_INLINE int median3(int a, int b, int c) {
   return vts_max(vts_min(a, b), vts_min(vts_max(a, b), c));
