@@ -23,6 +23,16 @@ struct FullParseArgs {
   FullParams P;
 };
 
+// per macroblock deblocking descriptor (h264_bs_full -> h264_deblock_full)
+struct DbkInfo {
+  uint32_t bs[4];   // bS of edge e (0 = the macroblock edge; 0 when it is not filtered) of direction
+                    // dir (0 vertical), 4-sample segment seg: nibble (e & 1) * 4 + seg of word dir * 2 + e / 2
+  uint32_t qp;      // QPq | QPleft << 8 | QPtop << 16 (I_PCM: 0) | (disable_deblocking_filter_idc == 1) << 24
+  int32_t fa, fb;   // FilterOffsetA / B of the macroblock's slice
+  uint32_t _pad;
+};
+static_assert(sizeof(DbkInfo) == 32, "DbkInfo layout");
+
 struct FullReconArgs {
   const int4 *frames;        // (slot, -, -, -) per picture of the launch
   const MbRec *recs;
@@ -36,6 +46,7 @@ struct FullReconArgs {
   uint32_t epoch;
   int32_t deblock;           // 1: run the deblocking kernel after reconstruction
   int32_t _pad;
+  DbkInfo *dbk;              // ring: [slot][mb] deblocking descriptors
   uint32_t *err;
   FullParams P;
 };

@@ -42,7 +42,7 @@ constexpr int kDbkWaves = kDbkThreads / 64;
 // One slice per wave and the wave's one lane: every value of the parse is
 // wave-uniform, so control flow never diverges and the integer work can go to
 // the scalar unit; the parallelism is the window's slices (thousands of waves).
-__global__ void __launch_bounds__(1) h264_parse_full(FullParseArgs a) {
+__global__ void __launch_bounds__(1) __attribute__((amdgpu_waves_per_eu(4, 4))) h264_parse_full(FullParseArgs a) {
   __shared__ full::FullScratch scratch;
   const int i = blockIdx.x;
   const FullSlice &s = a.slices[i];
@@ -758,13 +758,90 @@ __device__ __forceinline__ EdgeQ edge_q(int qpav, int fa, int fb) {
   return e;
 }
 
+// bS of edge e (0 = the macroblock edge) of direction dir, 4-sample segment seg
+__device__ __forceinline__ int dbk_bs(const DbkInfo &d, int dir, int e, int seg) {
+  return (d.bs[dir * 2 + (e >> 1)] >> (((e & 1) * 4 + seg) * 4)) & 15;
+}
+
+// grid (ceil(nmb / 256), pictures of the level): one lane per macroblock
+// derives every boundary strength of its edges (8.7.2.1) and the QPs, so the
+// wavefront below reads one 32-byte descriptor per macroblock
+__global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
+  const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
+  const int slot = a.frames[blockIdx.y].x;
+  const int mb = blockIdx.x * 256 + threadIdx.x;
+  if (mb >= nmb) return;
+  const MbRec *Q = a.recs + static_cast<int64_t>(slot) * nmb + mb;
+  const MbHdr hq = load_hdr(Q);
+  const FullSlice &sd = a.slices[hq.slice];
+  const int x = mb % mbw, y = mb / mbw;
+  const int idc = sd.dbk_idc, tq = hq.type;
+  DbkInfo d;
+  d.bs[0] = d.bs[1] = d.bs[2] = d.bs[3] = 0;
+  int qpl = 0, qpt = 0;
+  if (idc != 1) {
+    const MbRec *PL = Q - 1, *PT = Q - mbw;
+    bool fl = x > 0, ft = y > 0;
+    int tl = 0, tt = 0;
+    if (fl) {
+      const MbHdr h = load_hdr(PL);
+      if (idc == 2 && h.slice != hq.slice) fl = false;
+      tl = h.type;
+      qpl = tl == kMbPcm ? 0 : h.qp;
+    }
+    if (ft) {
+      const MbHdr h = load_hdr(PT);
+      if (idc == 2 && h.slice != hq.slice) ft = false;
+      tt = h.type;
+      qpt = tt == kMbPcm ? 0 : h.qp;
+    }
+#pragma unroll
+    for (int dir = 0; dir < 2; ++dir)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (e == 0 && !(dir ? ft : fl)) continue;
+        const MbRec *Pm = e ? Q : (dir ? PT : PL);
+        const int tp = e ? tq : (dir ? tt : tl);
+#pragma unroll
+        for (int seg = 0; seg < 4; ++seg) {
+          const int bq = dir ? e * 4 + seg : seg * 4 + e;
+          const int bp = dir ? (e ? bq - 4 : 12 + seg) : (e ? bq - 1 : seg * 4 + 3);
+          const int bS = bs_dev(Pm, bp, Q, bq, tp, tq, e == 0);
+          d.bs[dir * 2 + (e >> 1)] |= static_cast<uint32_t>(bS) << (((e & 1) * 4 + seg) * 4);
+        }
+      }
+  }
+  d.qp = static_cast<uint32_t>(tq == kMbPcm ? 0 : hq.qp) | (static_cast<uint32_t>(qpl) << 8) |
+         (static_cast<uint32_t>(qpt) << 16) | (idc == 1 ? 1u << 24 : 0u);
+  d.fa = sd.dbk_a;
+  d.fb = sd.dbk_b;
+  d._pad = 0;
+  DbkInfo *o = a.dbk + static_cast<int64_t>(slot) * nmb + mb;
+  reinterpret_cast<uint4 *>(o)[0] = make_uint4(d.bs[0], d.bs[1], d.bs[2], d.bs[3]);
+  reinterpret_cast<uint4 *>(o)[1] = make_uint4(d.qp, static_cast<uint32_t>(d.fa), static_cast<uint32_t>(d.fb), 0u);
+}
+
+__device__ __forceinline__ DbkInfo dbk_load(const DbkInfo *p) {
+  const uint4 u0 = reinterpret_cast<const uint4 *>(p)[0], u1 = reinterpret_cast<const uint4 *>(p)[1];
+  DbkInfo d;
+  d.bs[0] = u0.x;
+  d.bs[1] = u0.y;
+  d.bs[2] = u0.z;
+  d.bs[3] = u0.w;
+  d.qp = u1.x;
+  d.fa = static_cast<int32_t>(u1.y);
+  d.fb = static_cast<int32_t>(u1.z);
+  d._pad = 0;
+  return d;
+}
+
 // grid: pictures of the level
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a) {
   __shared__ DbkTile tiles[kDbkWaves * 2];
   __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
   const int slot = a.frames[blockIdx.x].x;
-  const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
+  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
   uint8_t *UV = Y + a.uv_off;
   const int pitch = a.pitch;
@@ -772,15 +849,32 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int half = lane >> 5, l = lane & 31;
+  const bool lrow = l < 24, luma = l < 16;
+  const int row = luma ? l : l - 16;  // V phase: luma row l / chroma row l - 16
   DbkTile &t = tiles[wave * 2 + half];
   const int npairs = (mbh + 1) >> 1;
   for (int p = wave; p < npairs; p += kDbkWaves) {
     const int y = 2 * p + half;
     const bool row_ok = y < mbh;
-    uint32_t left = 0;  // carried cols 12..15 (luma row l / chroma row l - 16) of the previous macroblock
+    const int64_t yrow = static_cast<int64_t>(y * 16) * pitch, crow = static_cast<int64_t>(y * 8) * pitch;
+    uint8_t *const rowp = (luma ? Y + yrow : UV + crow) + static_cast<int64_t>(row) * pitch;
+    uint32_t left = 0;  // carried cols 12..15 of the previous macroblock (this lane's row)
+    // the macroblock of the next iteration: descriptor and this lane's row, loaded one iteration ahead
+    uint4 npx = make_uint4(0, 0, 0, 0);
+    DbkInfo nd{};
+    if (row_ok && half == 0) {
+      nd = dbk_load(fdbk + y * mbw);
+      if (lrow) npx = *reinterpret_cast<const uint4 *>(rowp);
+    }
     for (int it = 0; it < mbw + 2; ++it) {
       const int x = it - 2 * half;
       const bool act = row_ok && x >= 0 && x < mbw;
+      const DbkInfo D = nd;
+      const uint4 q4 = npx;
+      if (row_ok && x + 1 >= 0 && x + 1 < mbw) {
+        nd = dbk_load(fdbk + y * mbw + x + 1);
+        if (lrow) npx = *reinterpret_cast<const uint4 *>(rowp + (x + 1) * 16);
+      }
       // the upper row of the pair waits for the row above (another wave)
       if (half == 0 && act && y > 0) {
         const int need = x + 1 < mbw ? x + 2 : mbw + 1;
@@ -788,42 +882,29 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
           __builtin_amdgcn_s_sleep(1);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      const int mb = y * mbw + x;
-      const MbRec *Q = frecs + (act ? mb : 0);
-      const FullSlice *sd = a.slices + (act ? Q->slice : 0);
-      const int idc = act ? sd->dbk_idc : 1;
-      const int tq = act ? (reinterpret_cast<const uint32_t *>(Q)[4] & 255) : 0;
-      const int qpq = tq == kMbPcm ? 0 : (act ? Q->qp : 0);
-      const int fa = act ? sd->dbk_a : 0, fb = act ? sd->dbk_b : 0;
-      const MbRec *PL = Q - 1, *PT = Q - mbw;
-      bool fl = act && idc != 1 && x > 0, ft = act && idc != 1 && y > 0;
-      if (fl && idc == 2 && PL->slice != Q->slice) fl = false;
-      if (ft && idc == 2 && PT->slice != Q->slice) ft = false;
-      const int tl = fl ? (reinterpret_cast<const uint32_t *>(PL)[4] & 255) : 0;
-      const int tt = ft ? (reinterpret_cast<const uint32_t *>(PT)[4] & 255) : 0;
-      const int qpl = fl ? (tl == kMbPcm ? 0 : PL->qp) : 0, qpt = ft ? (tt == kMbPcm ? 0 : PT->qp) : 0;
-      const int64_t ybase = static_cast<int64_t>(y * 16) * pitch + x * 16;
-      const int64_t cbase = static_cast<int64_t>(y * 8) * pitch + x * 16;
+      const bool on = act && !((D.qp >> 24) & 1);  // disable_deblocking_filter_idc != 1
+      const int qpq = D.qp & 255, qpl = (D.qp >> 8) & 255, qpt = (D.qp >> 16) & 255;
+      const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
+      // rows above (final: the row above is two macroblocks ahead)
+      if (act && l >= 24 && l < 30 && y > 0) {
+        const int i = l - 24;
+        if (i < 4) *reinterpret_cast<uint4 *>(&t.y[i][4]) = *reinterpret_cast<const uint4 *>(Y + ybase + static_cast<int64_t>(i - 4) * pitch);
+        else *reinterpret_cast<uint4 *>(&t.c[i - 4][4]) = *reinterpret_cast<const uint4 *>(UV + cbase + static_cast<int64_t>(i - 6) * pitch);
+      }
       // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
-      if (act && l < 24) {
-        const bool luma = l < 16;
-        const int row = luma ? l : l - 16;
-        const uint4 q4 = *reinterpret_cast<const uint4 *>((luma ? Y + ybase : UV + cbase) + static_cast<int64_t>(row) * pitch);
+      if (act && lrow) {
         const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
         int r[20];
 #pragma unroll
         for (int i = 0; i < 20; ++i) r[i] = (wv[i >> 2] >> ((i & 3) * 8)) & 255;
-        if (idc != 1) {
+        if (on) {
           if (luma) {
-            const int br = (row >> 2) * 4;
+            const int seg = row >> 2;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              if (e == 0 && !fl) continue;
-              const MbRec *Pm = e ? Q : PL;
-              const int tp = e ? tq : tl, qpp = e ? qpq : qpl;
-              const int bS = bs_dev(Pm, e ? br + e - 1 : br + 3, Q, br + e, tp, tq, e == 0);
+              const int bS = dbk_bs(D, 0, e, seg);
               if (!bS) continue;
-              const EdgeQ eq = edge_q((qpp + qpq + 1) >> 1, fa, fb);
+              const EdgeQ eq = edge_q(e ? qpq : (qpl + qpq + 1) >> 1, D.fa, D.fb);
               if (!eq.alpha || !eq.beta) continue;
               int s[8];
 #pragma unroll
@@ -833,18 +914,16 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
               for (int i = 0; i < 8; ++i) r[4 * e + i] = s[i];
             }
           } else {
-            const int br = ((2 * row) >> 2) * 4;
+            const int seg = row >> 1;
 #pragma unroll
             for (int e = 0; e < 4; e += 2) {
-              if (e == 0 && !fl) continue;
-              const MbRec *Pm = e ? Q : PL;
-              const int tp = e ? tq : tl, qpp = e ? qpq : qpl;
-              const int bS = bs_dev(Pm, e ? br + e - 1 : br + 3, Q, br + e, tp, tq, e == 0);
+              const int bS = dbk_bs(D, 0, e, seg);
               if (!bS) continue;
+              const int qpp = e ? qpq : qpl;
 #pragma unroll
               for (int pl = 0; pl < 2; ++pl) {
                 const int off = pl ? a.P.cqp_off2 : a.P.cqp_off;
-                const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, fa, fb);
+                const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, D.fa, D.fb);
                 if (!eq.alpha || !eq.beta) continue;
                 const int c0 = 4 + 2 * (2 * e) + pl;  // q0 of chroma col 2e (luma edge e)
                 filt_chroma(r[c0 - 4], r[c0 - 2], r[c0], r[c0 + 2], bS, eq.iA, eq.alpha, eq.beta);
@@ -857,28 +936,19 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
         for (int i = 0; i < 5; ++i)
           *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
       }
-      // rows above (final: the row above is two macroblocks ahead)
-      if (act && l >= 24 && l < 30 && y > 0) {
-        const int i = l - 24;
-        if (i < 4) *reinterpret_cast<uint4 *>(&t.y[i][4]) = *reinterpret_cast<const uint4 *>(Y + ybase + static_cast<int64_t>(i - 4) * pitch);
-        else *reinterpret_cast<uint4 *>(&t.c[i - 4][4]) = *reinterpret_cast<const uint4 *>(UV + cbase + static_cast<int64_t>(i - 6) * pitch);
-      }
       lane_sync();
       // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved chroma column l - 16
-      if (act && idc != 1) {
+      if (on) {
         if (l < 16) {
-          const int col = l, bc = col >> 2;
+          const int col = l, seg = col >> 2;
           int r[20];
 #pragma unroll
           for (int i = 0; i < 20; ++i) r[i] = t.y[i][4 + col];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            if (e == 0 && !ft) continue;
-            const MbRec *Pm = e ? Q : PT;
-            const int tp = e ? tq : tt, qpp = e ? qpq : qpt;
-            const int bS = bs_dev(Pm, e ? (e - 1) * 4 + bc : 12 + bc, Q, e * 4 + bc, tp, tq, e == 0);
+            const int bS = dbk_bs(D, 1, e, seg);
             if (!bS) continue;
-            const EdgeQ eq = edge_q((qpp + qpq + 1) >> 1, fa, fb);
+            const EdgeQ eq = edge_q(e ? qpq : (qpt + qpq + 1) >> 1, D.fa, D.fb);
             if (!eq.alpha || !eq.beta) continue;
             int s[8];
 #pragma unroll
@@ -890,19 +960,17 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
 #pragma unroll
           for (int i = 1; i < 20; ++i) t.y[i][4 + col] = static_cast<uint8_t>(r[i]);
         } else {
-          const int j = l - 16, pl = j & 1, cc = j >> 1, bc = (2 * cc) >> 2;
+          const int j = l - 16, pl = j & 1, cc = j >> 1, seg = cc >> 1;
           const int off = pl ? a.P.cqp_off2 : a.P.cqp_off;
           int r[10];
 #pragma unroll
           for (int i = 0; i < 10; ++i) r[i] = t.c[i][4 + j];
 #pragma unroll
           for (int e = 0; e < 4; e += 2) {
-            if (e == 0 && !ft) continue;
-            const MbRec *Pm = e ? Q : PT;
-            const int tp = e ? tq : tt, qpp = e ? qpq : qpt;
-            const int bS = bs_dev(Pm, e ? (e - 1) * 4 + bc : 12 + bc, Q, e * 4 + bc, tp, tq, e == 0);
+            const int bS = dbk_bs(D, 1, e, seg);
             if (!bS) continue;
-            const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, fa, fb);
+            const int qpp = e ? qpq : qpt;
+            const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, D.fa, D.fb);
             if (!eq.alpha || !eq.beta) continue;
             const int q0 = 2 + 2 * e;  // chroma row 2e
             filt_chroma(r[q0 - 2], r[q0 - 1], r[q0], r[q0 + 1], bS, eq.iA, eq.alpha, eq.beta);
@@ -915,17 +983,15 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
       // ---- write back: rows of this macroblock shifted 4 bytes left (the left
       // neighbour's last columns are final now), rows above, the row's tail
       if (act) {
-        if (l < 24) {
-          const bool luma = l < 16;
-          const int row = luma ? l : l - 16;
+        if (lrow) {
           const uint8_t *src = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
-          uint8_t *dst = (luma ? Y + ybase : UV + cbase) + static_cast<int64_t>(row) * pitch;
+          uint8_t *dst = rowp + x * 16;
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if (x > 0 || i > 0) *reinterpret_cast<uint32_t *>(dst - 4 + 4 * i) = *reinterpret_cast<const uint32_t *>(src + 4 * i);
           left = *reinterpret_cast<const uint32_t *>(src + 16);
           if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
-        } else if (l < 28 && y > 0 && ft) {
+        } else if (l < 28 && y > 0 && on && dbk_bs(D, 1, 0, 0) + dbk_bs(D, 1, 0, 1) + dbk_bs(D, 1, 0, 2) + dbk_bs(D, 1, 0, 3)) {
           const int i = l - 24;  // luma rows -3..-1, chroma row -1
           if (i < 3) *reinterpret_cast<uint4 *>(Y + ybase + static_cast<int64_t>(i - 3) * pitch) = *reinterpret_cast<const uint4 *>(&t.y[1 + i][4]);
           else *reinterpret_cast<uint4 *>(UV + cbase - pitch) = *reinterpret_cast<const uint4 *>(&t.c[1][4]);
@@ -961,6 +1027,9 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_intra_full launch: %s", hipGetErrorString(e));
   if (a.deblock) {
+    hipLaunchKernelGGL(h264_bs_full, dim3((nmb + 255) / 256, n_frames), dim3(256), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_bs_full launch: %s", hipGetErrorString(e));
     hipLaunchKernelGGL(h264_deblock_full, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));

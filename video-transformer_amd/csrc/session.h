@@ -7,6 +7,7 @@
 
 #include "common.h"
 #include "decode.h"
+#include "decode_full.h"
 #include "h264.h"
 #include "h264_full.h"
 
@@ -128,6 +129,7 @@ struct vts_ctx {
   vts::FullSlice *d_fslices = nullptr;
   vts::MbRec *d_recs[2] = {nullptr, nullptr};
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
+  vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock
   int16_t *d_arena[2] = {nullptr, nullptr};
   int64_t arena_blocks = 0;             // per ring
   // kept from open for a later switch to the general decoder (decoder = auto)

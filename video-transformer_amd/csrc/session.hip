@@ -100,6 +100,7 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   for (int r = 0; r < c->n_rings; ++r) {
     HIP_TRY(hipMalloc(&c->d_recs[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec)));
     HIP_TRY(hipMalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
+    HIP_TRY(hipMalloc(&c->d_dbk[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(DbkInfo)));
     HIP_TRY(hipMalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
     HIP_TRY(hipMalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
     HIP_TRY(hipMalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
@@ -1043,6 +1044,7 @@ extern "C" int vts_close(vts_ctx *c) {
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_ilvl[r]);
+    f(c->d_dbk[r]);
     f(c->d_arena[r]);
   }
   for (auto e : c->ev)

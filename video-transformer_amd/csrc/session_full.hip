@@ -99,7 +99,7 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   }
   // windows
   const int64_t tw_f = static_cast<int64_t>(c->width / c->k) * (c->height / c->k);
-  const int64_t per_frame = c->frame_stride + nmb * static_cast<int64_t>(sizeof(MbRec) + sizeof(uint16_t)) +
+  const int64_t per_frame = c->frame_stride + nmb * static_cast<int64_t>(sizeof(MbRec) + sizeof(uint16_t) + sizeof(DbkInfo)) +
                             score_workspace_bytes(c->width, c->height, c->k, 1) +
                             32 * ((cap_total + n - 1) / std::max<int64_t>(1, n));
   size_t free_b = 0, total_b = 0;
@@ -193,7 +193,12 @@ int run_general(vts_ctx *c) {
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
   HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
   HIP_TRY(hipStreamWaitEvent(c->s_score, c->ev_start, 0));
+  HIP_TRY(hipStreamWaitEvent(c->s_parse, c->ev_start, 0));
   hipStream_t sd = c->s_dec;
+  // slice parsing runs on its own stream one window ahead: window i + 1 parses
+  // (thousands of one-lane waves) while window i reconstructs (one workgroup per
+  // picture of a level, which leaves most compute units idle)
+  hipStream_t sp = c->s_parse;
   hipStream_t ss = (c->params.n_streams >= 2 && c->windows.size() > 1) ? c->s_score : c->s_dec;
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
   const size_t nw = c->windows.size();
@@ -201,14 +206,17 @@ int run_general(vts_ctx *c) {
     const Window &w = c->windows[wi];
     const int r = static_cast<int>(wi % c->n_rings);
     hipEvent_t *E = &c->ev[wi * 6];
-    if (wi >= static_cast<size_t>(c->n_rings)) HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
+    if (wi >= static_cast<size_t>(c->n_rings)) {  // ring r: the window before has been scored
+      HIP_TRY(hipStreamWaitEvent(sp, c->ev[(wi - c->n_rings) * 6 + 4], 0));
+      HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
+    }
     const int64_t run = c->run_no++;
     const uint32_t epoch = 1u + static_cast<uint32_t>(run % 0x7fffffff);
     if (c->ring_cleared_at[r] < 0) {  // records of another run read as absent (their epoch)
-      HIP_TRY(hipMemsetAsync(c->d_recs[r], 0, static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec), sd));
+      HIP_TRY(hipMemsetAsync(c->d_recs[r], 0, static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec), sp));
       c->ring_cleared_at[r] = run;
     }
-    HIP_TRY(hipEventRecord(E[0], sd));
+    HIP_TRY(hipEventRecord(E[0], sp));
     FullParseArgs pa{};
     pa.es = c->d_es;
     pa.slices = c->d_fslices + w.fs0;
@@ -220,11 +228,14 @@ int run_general(vts_ctx *c) {
     pa.arena = c->d_arena[r];
     pa.err = c->d_err;
     pa.P = c->fprm;
-    VTS_TRY(parse_full_launch(pa, sd));
-    HIP_TRY(hipEventRecord(E[1], sd));
+    VTS_TRY(parse_full_launch(pa, sp));
+    HIP_TRY(hipEventRecord(E[1], sp));
+    HIP_TRY(hipStreamWaitEvent(sd, E[1], 0));
+    HIP_TRY(hipEventRecord(E[5], sd));
     FullReconArgs ra{};
     ra.recs = c->d_recs[r];
     ra.ilvl = c->d_ilvl[r];
+    ra.dbk = c->d_dbk[r];
     ra.arena = c->d_arena[r];
     ra.slices = c->d_fslices + w.fs0;
     ra.surf = c->d_surf[r];
@@ -276,7 +287,7 @@ int run_general(vts_ctx *c) {
     hipEvent_t *E = &c->ev[wi * 6];
     float a = 0, b = 0, s = 0;
     HIP_TRY(hipEventElapsedTime(&a, E[0], E[1]));
-    HIP_TRY(hipEventElapsedTime(&b, E[1], E[2]));
+    HIP_TRY(hipEventElapsedTime(&b, E[5], E[2]));
     HIP_TRY(hipEventElapsedTime(&s, E[3], E[4]));
     c->timings[1] += a;
     c->timings[2] += b;
