@@ -35,6 +35,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* CABAC / 8x8-transform constant tables (Tables 9-12..9-33, 9-43, 9-44,
+ * 8.5.6, 8.5.9): the standard's numbers as one C header shared with the
+ * device parser (data only; no product code is linked) */
+#include "../video-transformer_amd/csrc/h264_cabac_tables.h"
+
 #define FO_E_FORMAT -8
 #define FO_E_UNSUPPORTED -9
 #define FO_E_DECODE -12
@@ -319,6 +324,7 @@ typedef struct {
 typedef struct {
   int valid, sps_id, bfpo, num_ref_l0, weighted_pred, weighted_bipred, pic_init_qp;
   int cqp_off, cqp_off2, deblock_ctrl, cip, redundant;
+  int cabac, t8mode;   /* entropy_coding_mode_flag, transform_8x8_mode_flag */
 } fo_pps;
 
 static int is_high(int p) {
@@ -379,7 +385,7 @@ static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, char *err) {
   uint32_t id = fb_ue(&b);
   if (id > 255) return FO_E_FORMAT;
   p.sps_id = (int)fb_ue(&b);
-  if (fb_bit(&b)) { strcpy(err, "CABAC"); return FO_E_UNSUPPORTED; }
+  p.cabac = (int)fb_bit(&b);
   p.bfpo = (int)fb_bit(&b);
   if (fb_ue(&b)) { strcpy(err, "slice groups (FMO)"); return FO_E_UNSUPPORTED; }
   p.num_ref_l0 = (int)fb_ue(&b) + 1;
@@ -404,7 +410,7 @@ static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, char *err) {
     while (!((nal[last] >> tz) & 1)) tz++;
     int64_t stop = (last - 1) * 8 + (7 - tz);
     if (pos_bits < stop) {
-      if (fb_bit(&b)) { strcpy(err, "8x8 transform"); return FO_E_UNSUPPORTED; }
+      p.t8mode = (int)fb_bit(&b);
       if (fb_bit(&b)) { strcpy(err, "scaling matrices"); return FO_E_UNSUPPORTED; }
       p.cqp_off2 = fb_se(&b);
     }
@@ -434,8 +440,14 @@ typedef struct {
   int refidx[16];   /* per raster 4x4 block, -1 intra */
   int refpic[16];   /* picture id per raster 4x4 block */
   int mv[16][2];
-  int nz[16];       /* total_coeff per raster luma 4x4 block */
+  int nz[16];       /* total_coeff per raster luma 4x4 block (8x8 transform: the 8x8's count) */
   int nzc[2][4];    /* chroma AC total_coeff, raster 2x2 */
+  int t8;           /* transform_size_8x8_flag (I_NxN with it = I_8x8) */
+  int cmode;        /* intra_chroma_pred_mode */
+  int mvd[16][2];   /* CABAC: mvd_l0 per raster 4x4 block (context of later mvds) */
+  uint32_t cbf;     /* CABAC coded_block_flag: bit 0 Intra16x16 DC, 1 + raster luma 4x4,
+                       17 + iCbCr chroma DC, 19 + 4 iCbCr + raster chroma AC */
+  int qpd;          /* mb_qp_delta */
 } fo_mb;
 
 typedef struct {
@@ -1004,10 +1016,11 @@ static void deblock_picture(fo_dec *d, fo_pic *pic) {
     for (int dir = 0; dir < 2; dir++) {       /* 0: vertical edges, 1: horizontal */
       for (int e = 0; e < 4; e++) {          /* luma edges at 0, 4, 8, 12 */
         if (e == 0 && !(dir ? top : left)) continue;
+        int luma_edge = !(q->t8 && (e & 1)); /* 8.7: 8x8 transform: no 4-sample internal luma edges */
         const fo_mb *p = e == 0 ? &d->mb[dir ? a - d->mbw : a - 1] : q;
         int qpp = p->type == 3 ? 0 : p->qp, qpq = q->type == 3 ? 0 : q->qp;
         /* luma */
-        {
+        if (luma_edge) {
           int qpav = (qpp + qpq + 1) >> 1;
           int iA = clip3(0, 51, qpav + sd->off_a), iB = clip3(0, 51, qpav + sd->off_b);
           for (int k = 0; k < 16; k++) {
@@ -1087,11 +1100,246 @@ typedef struct {
 
 static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_hdr *h);
 
+/* 8.5.13: scaling (flat) + 8x8 inverse transform of raster coefficients c */
+static const int NORM8[6][6] = VTS_NORM8_DATA;
+static void scale_idct8(const int *c, int qp, int *r) {
+  int d[64], g[64];
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) {
+      int ls = 16 * NORM8[qp % 6][vts_norm8_class(i, j)];
+      int k = i * 8 + j;
+      d[k] = qp >= 36 ? (c[k] * ls) << (qp / 6 - 6) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    }
+  for (int pass = 0; pass < 2; pass++) {
+    for (int u = 0; u < 8; u++) {
+      int v[8], o[8];
+      for (int k = 0; k < 8; k++) v[k] = pass == 0 ? d[u * 8 + k] : g[k * 8 + u];
+      int a0 = v[0] + v[4], a4 = v[0] - v[4], a2 = (v[2] >> 1) - v[6], a6 = v[2] + (v[6] >> 1);
+      int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+      int a1 = -v[3] + v[5] - v[7] - (v[7] >> 1), a3 = v[1] + v[7] - v[3] - (v[3] >> 1);
+      int a5 = -v[1] + v[7] + v[5] + (v[5] >> 1), a7 = v[3] + v[5] + v[1] + (v[1] >> 1);
+      int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+      o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1;
+      o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
+      for (int k = 0; k < 8; k++) {
+        if (pass == 0) g[u * 8 + k] = o[k];
+        else r[k * 8 + u] = (o[k] + 32) >> 6;
+      }
+    }
+  }
+}
+
+/* 8.3.2: Intra_8x8 prediction of 8x8 block b8 (raster 0..3) with the
+ * reference sample filtering of 8.3.2.2.1 */
+static void intra8x8(const fo_dec *d, fo_pic *pic, int cur, int b8, int mode, int done_mask, int pred[64]) {
+  int xo = (b8 & 1) * 8, yo = (b8 >> 1) * 8;
+  int P_[25], av[25]; /* index 0 = p[-1,-1], 1..16 = p[0..15,-1], 17..24 = p[-1,0..7] */
+  fo_s s = luma_nb(d, pic, cur, xo, yo, -1, -1, done_mask);
+  av[0] = s.avail; P_[0] = s.v;
+  for (int x = 0; x < 16; x++) { s = luma_nb(d, pic, cur, xo, yo, x, -1, done_mask); av[1 + x] = s.avail; P_[1 + x] = s.v; }
+  for (int y = 0; y < 8; y++) { s = luma_nb(d, pic, cur, xo, yo, -1, y, done_mask); av[17 + y] = s.avail; P_[17 + y] = s.v; }
+  if (!av[9] && av[8]) for (int x = 8; x < 16; x++) { P_[1 + x] = P_[8]; av[1 + x] = 1; }
+  int top = av[1], left = av[17], tl = av[0];
+  /* filtered samples pt[-1..15] (pt[0] = p'[-1,-1]) and pl[0..7] */
+  int T[17] = {0}, L[8] = {0};
+  if (top) {
+    T[1] = tl ? (P_[0] + 2 * P_[1] + P_[2] + 2) >> 2 : (3 * P_[1] + P_[2] + 2) >> 2;
+    for (int x = 1; x < 15; x++) T[1 + x] = (P_[x] + 2 * P_[1 + x] + P_[2 + x] + 2) >> 2;
+    T[16] = (P_[15] + 3 * P_[16] + 2) >> 2;
+  }
+  if (tl) {
+    if (top && left) T[0] = (P_[1] + 2 * P_[0] + P_[17] + 2) >> 2;
+    else if (top) T[0] = (3 * P_[0] + P_[1] + 2) >> 2;
+    else if (left) T[0] = (3 * P_[0] + P_[17] + 2) >> 2;
+    else T[0] = P_[0];
+  }
+  if (left) {
+    L[0] = tl ? (P_[0] + 2 * P_[17] + P_[18] + 2) >> 2 : (3 * P_[17] + P_[18] + 2) >> 2;
+    for (int y = 1; y < 7; y++) L[y] = (P_[16 + y] + 2 * P_[17 + y] + P_[18 + y] + 2) >> 2;
+    L[7] = (P_[23] + 3 * P_[24] + 2) >> 2;
+  }
+#define PT(x) T[1 + (x)]
+#define PL(y) ((y) < 0 ? T[0] : L[(y)])
+  for (int y = 0; y < 8; y++)
+    for (int x = 0; x < 8; x++) {
+      int v = 128;
+      switch (mode) {
+        case 0: v = PT(x); break;
+        case 1: v = PL(y); break;
+        case 2: {
+          int st = 0, sl = 0;
+          for (int i = 0; i < 8; i++) { st += top ? PT(i) : 0; sl += left ? L[i] : 0; }
+          if (top && left) v = (st + sl + 8) >> 4;
+          else if (left) v = (sl + 4) >> 3;
+          else if (top) v = (st + 4) >> 3;
+          break;
+        }
+        case 3:
+          if (x == 7 && y == 7) v = (PT(14) + 3 * PT(15) + 2) >> 2;
+          else v = (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
+          break;
+        case 4:
+          if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
+          else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
+          else v = (PT(0) + 2 * PT(-1) + PL(0) + 2) >> 2;
+          break;
+        case 5: {
+          int z = 2 * x - y;
+          if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+          else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+          else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+          else v = (PL(y - 2 * x - 1) + 2 * PL(y - 2 * x - 2) + PL(y - 2 * x - 3) + 2) >> 2;
+          break;
+        }
+        case 6: {
+          int z = 2 * y - x;
+          if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+          else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+          else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+          else v = (PT(x - 2 * y - 1) + 2 * PT(x - 2 * y - 2) + PT(x - 2 * y - 3) + 2) >> 2;
+          break;
+        }
+        case 7:
+          if (!(y & 1)) v = (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1;
+          else v = (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2;
+          break;
+        default: {
+          int z = x + 2 * y;
+          if (z < 13 && !(z & 1)) v = (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
+          else if (z < 13) v = (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
+          else if (z == 13) v = (PL(6) + 3 * PL(7) + 2) >> 2;
+          else v = PL(7);
+          break;
+        }
+      }
+      pred[y * 8 + x] = v;
+    }
+#undef PT
+#undef PL
+}
+
+/* reconstruction of a parsed (non-skip, non-PCM) macroblock: prediction +
+ * residual (8.3, 8.4, 8.5); coef8 != NULL holds the 8x8 blocks when
+ * transform_size_8x8_flag is set */
+static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*cdc)[4], int (*cac)[4][16],
+                    int (*coef8)[64], int i16mode, int cmode) {
+  fo_dec *d = c->d;
+  fo_mb *m = &d->mb[addr];
+  fo_pic *pic = c->cur;
+  int mx = addr % d->mbw, my = addr / d->mbw;
+  int pred_y[256], pred_u[64], pred_v[64];
+  int qpy = m->qp;
+  uint8_t *Y = pic->y + (int64_t)(my * 16) * d->W + mx * 16;
+  if (m->type == 0) {
+    /* predict each 4x4 block with its motion (partitions share them;
+       interpolation is per sample, so the block size does not matter) */
+    for (int blk = 0; blk < 16; blk++)
+      mc_part(d, c->list[m->refidx[blk]], addr, (blk % 4) * 4, (blk / 4) * 4, 4, 4, m->mv[blk][0],
+              m->mv[blk][1], pred_y, pred_u, pred_v);
+    if (m->t8) {
+      for (int b8 = 0; b8 < 4; b8++) {
+        int r[64], bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
+        scale_idct8(coef8[b8], qpy, r);
+        for (int y = 0; y < 8; y++)
+          for (int x = 0; x < 8; x++)
+            Y[(int64_t)(by + y) * d->W + bx + x] = (uint8_t)clip1(pred_y[(by + y) * 16 + bx + x] + r[y * 8 + x]);
+      }
+    } else {
+      for (int blk = 0; blk < 16; blk++) {
+        int r[16], bx = blk % 4, by = blk / 4;
+        scale_idct4(coef[blk], qpy, 0, r);
+        for (int y = 0; y < 4; y++)
+          for (int x = 0; x < 4; x++)
+            Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred_y[(by * 4 + y) * 16 + bx * 4 + x] + r[y * 4 + x]);
+      }
+    }
+  } else if (m->type == 1 && m->t8) {
+    int done = 0;
+    for (int b8 = 0; b8 < 4; b8++) {
+      int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8, pred[64], r[64];
+      intra8x8(d, pic, addr, b8, m->i4[(by / 4) * 4 + bx / 4], done, pred);
+      scale_idct8(coef8[b8], qpy, r);
+      for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) Y[(int64_t)(by + y) * d->W + bx + x] = (uint8_t)clip1(pred[y * 8 + x] + r[y * 8 + x]);
+      int r4 = (by / 4) * 4 + bx / 4;
+      done |= (1 << r4) | (1 << (r4 + 1)) | (1 << (r4 + 4)) | (1 << (r4 + 5));
+    }
+  } else if (m->type == 1) {
+    int done = 0;
+    for (int k = 0; k < 16; k++) {
+      int bx = BLK_X[k], by = BLK_Y[k], blk = by * 4 + bx, pred[16], r[16];
+      intra4x4(d, pic, addr, k, m->i4[blk], done, pred);
+      scale_idct4(coef[blk], qpy, 0, r);
+      for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++)
+          Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred[y * 4 + x] + r[y * 4 + x]);
+      done |= 1 << blk;
+    }
+  } else {
+    intra_big(d, pic, addr, 0, i16mode, pred_y);
+    /* 8.5.10: Intra16x16 DC Hadamard + scaling */
+    int f[16], t[16];
+    for (int i = 0; i < 4; i++) {
+      int a0 = dcl[i * 4 + 0], a1 = dcl[i * 4 + 1], a2 = dcl[i * 4 + 2], a3 = dcl[i * 4 + 3];
+      t[i * 4 + 0] = a0 + a1 + a2 + a3;
+      t[i * 4 + 1] = a0 + a1 - a2 - a3;
+      t[i * 4 + 2] = a0 - a1 - a2 + a3;
+      t[i * 4 + 3] = a0 - a1 + a2 - a3;
+    }
+    for (int j = 0; j < 4; j++) {
+      int a0 = t[0 * 4 + j], a1 = t[1 * 4 + j], a2 = t[2 * 4 + j], a3 = t[3 * 4 + j];
+      f[0 * 4 + j] = a0 + a1 + a2 + a3;
+      f[1 * 4 + j] = a0 + a1 - a2 - a3;
+      f[2 * 4 + j] = a0 - a1 - a2 + a3;
+      f[3 * 4 + j] = a0 - a1 + a2 - a3;
+    }
+    int ls = level_scale(qpy % 6, 0, 0);
+    for (int k = 0; k < 16; k++) {
+      int dc = qpy >= 36 ? (f[k] * ls) << (qpy / 6 - 6) : (f[k] * ls + (1 << (5 - qpy / 6))) >> (6 - qpy / 6);
+      coef[k][0] = dc; /* dcY row i col j -> block (x = j, y = i) */
+    }
+    for (int blk = 0; blk < 16; blk++) {
+      int r[16], bx = blk % 4, by = blk / 4;
+      scale_idct4(coef[blk], qpy, 1, r);
+      for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++)
+          Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred_y[(by * 4 + y) * 16 + bx * 4 + x] + r[y * 4 + x]);
+    }
+  }
+  /* chroma */
+  if (m->type != 0) {
+    intra_big(d, pic, addr, 1, cmode, pred_u);
+    intra_big(d, pic, addr, 2, cmode, pred_v);
+  }
+  for (int pl = 0; pl < 2; pl++) {
+    int qpc = qpc_of(qpy, pl ? d->P->cqp_off2 : d->P->cqp_off);
+    int c0 = cdc[pl][0], c1 = cdc[pl][1], c2 = cdc[pl][2], c3 = cdc[pl][3];
+    int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+    int ls = level_scale(qpc % 6, 0, 0);
+    uint8_t *U = (pl ? pic->v : pic->u) + (int64_t)(my * 8) * (d->W / 2) + mx * 8;
+    int *pr = pl ? pred_v : pred_u;
+    for (int k = 0; k < 4; k++) {
+      int bx = k & 1, by = k >> 1, r[16];
+      cac[pl][k][0] = ((f[k] * ls) << (qpc / 6)) >> 5;
+      scale_idct4(cac[pl][k], qpc, 1, r);
+      for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++)
+          U[(int64_t)(by * 4 + y) * (d->W / 2) + bx * 4 + x] = (uint8_t)clip1(pr[(by * 4 + y) * 8 + bx * 4 + x] + r[y * 4 + x]);
+    }
+  }
+  return 0;
+}
+
+
+static int slice_data_cabac(fo_ctx *c, fb_t *b, const fo_hdr *h, int is_p, int64_t stop);
+
 static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len, int slice_no,
                         int *is_idr_out, fo_hdr *hdr_out) {
   int nal_type = nal[0] & 31, nal_ref_idc = (nal[0] >> 5) & 3;
   int64_t last = len - 1;
-  while (last > 0 && nal[last] == 0) last--;
+  /* trailing cabac_zero_words (0x0000, escaped as 00 00 03) are not RBSP data */
+  while (last > 0 && (nal[last] == 0 || (nal[last] == 3 && last >= 2 && nal[last - 1] == 0 && nal[last - 2] == 0)))
+    last--;
   if (last <= 0) return fo_fail(d, FO_E_FORMAT, "empty slice NAL");
   int tz = 0;
   while (!((nal[last] >> tz) & 1)) tz++;
@@ -1158,6 +1406,10 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
         if (op == 4) m[1] = (int)fb_ue(&b);
       }
     }
+  }
+  if (P->cabac && is_p) {
+    int idc = (int)fb_ue(&b);
+    if (idc != 0) return fo_fail(d, FO_E_UNSUPPORTED, "cabac_init_idc 1/2 (only the idc 0 tables are restated)");
   }
   h.qp = P->pic_init_qp + fb_se(&b);
   if (P->deblock_ctrl) {
@@ -1237,6 +1489,7 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
     c.nlist = n;
   }
 
+  if (P->cabac) return slice_data_cabac(&c, &b, &h, is_p, stop);
   /* 7.3.4 slice_data */
   int addr = h.first_mb, more = 1, qp = h.qp;
   while (more) {
@@ -1480,85 +1733,513 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
   }
   if (b->err) return fo_fail(d, FO_E_FORMAT, "bitstream exhausted in residual");
 
-  /* ---- reconstruction */
-  int qpy = m->qp;
-  uint8_t *Y = pic->y + (int64_t)(my * 16) * d->W + mx * 16;
-  if (m->type == 0) {
-    /* predict each 4x4 block with its motion (partitions share them;
-       interpolation is per sample, so the block size does not matter) */
-    for (int blk = 0; blk < 16; blk++)
-      mc_part(d, c->list[m->refidx[blk]], addr, (blk % 4) * 4, (blk / 4) * 4, 4, 4, m->mv[blk][0],
-              m->mv[blk][1], pred_y, pred_u, pred_v);
-    for (int blk = 0; blk < 16; blk++) {
-      int r[16], bx = blk % 4, by = blk / 4;
-      scale_idct4(coef[blk], qpy, 0, r);
-      for (int y = 0; y < 4; y++)
-        for (int x = 0; x < 4; x++)
-          Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred_y[(by * 4 + y) * 16 + bx * 4 + x] + r[y * 4 + x]);
+  return recon_mb(c, addr, coef, dcl, cdc, cac, NULL, i16mode, cmode);
+}
+
+/* ------------------------------------------------------------ CABAC (9.3) */
+static const int8_t CAB_INIT_I[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_I_DATA;
+static const int8_t CAB_INIT_P0[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_P0_DATA;
+static const uint8_t RANGE_LPS[64][4] = VTS_CABAC_RANGE_LPS_DATA;
+static const uint8_t TRANS_LPS[64] = VTS_CABAC_TRANS_LPS_DATA;
+static const uint8_t SIG8[63] = VTS_SIG8x8_DATA;
+static const uint8_t LAST8[63] = VTS_LAST8x8_DATA;
+static const int ZZ8[64] = VTS_ZZ8_DATA;
+
+typedef struct {
+  fb_t *b;
+  uint32_t range, offset;
+  uint8_t state[VTS_CABAC_NCTX], mps[VTS_CABAC_NCTX];
+} fo_cab;
+
+static void cab_start(fo_cab *k) { /* 9.3.1.2 */
+  k->range = 510;
+  k->offset = fb_bits(k->b, 9);
+}
+static void cab_init(fo_cab *k, int is_i, int qp) { /* 9.3.1.1 */
+  const int8_t(*t)[2] = is_i ? CAB_INIT_I : CAB_INIT_P0;
+  for (int i = 0; i < VTS_CABAC_NCTX; i++) {
+    int pre = clip3(1, 126, ((t[i][0] * clip3(0, 51, qp)) >> 4) + t[i][1]);
+    if (pre <= 63) { k->state[i] = (uint8_t)(63 - pre); k->mps[i] = 0; }
+    else { k->state[i] = (uint8_t)(pre - 64); k->mps[i] = 1; }
+  }
+}
+static int cab_dec(fo_cab *k, int ctx) { /* 9.3.3.2.1 DecodeDecision */
+  int s = k->state[ctx], bin;
+  uint32_t lps = RANGE_LPS[s][(k->range >> 6) & 3];
+  k->range -= lps;
+  if (k->offset >= k->range) {
+    bin = !k->mps[ctx];
+    k->offset -= k->range;
+    k->range = lps;
+    if (s == 0) k->mps[ctx] = (uint8_t)(1 - k->mps[ctx]);
+    k->state[ctx] = TRANS_LPS[s];
+  } else {
+    bin = k->mps[ctx];
+    if (s < 62) k->state[ctx] = (uint8_t)(s + 1);
+  }
+  while (k->range < 256) { /* RenormD */
+    k->range <<= 1;
+    k->offset = (k->offset << 1) | fb_bit(k->b);
+  }
+  return bin;
+}
+static int cab_bypass(fo_cab *k) { /* 9.3.3.2.3 */
+  k->offset = (k->offset << 1) | fb_bit(k->b);
+  if (k->offset >= k->range) { k->offset -= k->range; return 1; }
+  return 0;
+}
+static int cab_term(fo_cab *k) { /* 9.3.3.2.2.3: binVal 1 ends parsing without renormalisation */
+  k->range -= 2;
+  if (k->offset >= k->range) return 1;
+  while (k->range < 256) {
+    k->range <<= 1;
+    k->offset = (k->offset << 1) | fb_bit(k->b);
+  }
+  return 0;
+}
+static int cab_fl3(fo_cab *k, int ctx) { /* FL, cMax 7: bins least significant first */
+  int v = cab_dec(k, ctx);
+  v |= cab_dec(k, ctx) << 1;
+  v |= cab_dec(k, ctx) << 2;
+  return v;
+}
+
+/* mb_type of an I macroblock (Table 9-36): prefix ctxIdx 3 (I slice, inc from
+ * the neighbours) or the P-slice suffix at ctxIdx 17; returns 0..25 */
+static int cab_i_type(fo_cab *k, int suffix, int inc0) {
+  if (!cab_dec(k, suffix ? 17 : 3 + inc0)) return 0; /* I_NxN */
+  if (cab_term(k)) return 25;                       /* I_PCM */
+  int luma = cab_dec(k, suffix ? 18 : 6);
+  int chroma = cab_dec(k, suffix ? 19 : 7);
+  if (chroma) chroma += cab_dec(k, suffix ? 19 : 8);
+  int pm = cab_dec(k, suffix ? 20 : 9) << 1;
+  pm |= cab_dec(k, suffix ? 20 : 10);
+  return 1 + pm + 4 * chroma + 12 * luma;
+}
+/* mvd_lX component (U prefix cMax 9 + UEG3 suffix + sign, 9.3.2.3), sum =
+ * absMvdComp(A) + absMvdComp(B) */
+static int cab_mvd(fo_cab *k, int base, int sum) {
+  if (!cab_dec(k, base + (sum < 3 ? 0 : (sum > 32 ? 2 : 1)))) return 0;
+  static const int inc[8] = {3, 4, 5, 6, 6, 6, 6, 6};
+  int v = 1;
+  while (v < 9 && cab_dec(k, base + inc[v - 1])) v++;
+  if (v >= 9) {
+    int kk = 3;
+    while (cab_bypass(k)) { v += 1 << kk; if (++kk > 30) return 0; }
+    while (kk--) v += cab_bypass(k) << kk;
+  }
+  return cab_bypass(k) ? -v : v;
+}
+
+static const int CBF_OFF[5] = {0, 4, 8, 12, 16};
+static const int SIG_OFF[5] = {0, 15, 29, 44, 47};
+static const int ABS_OFF[5] = {0, 10, 20, 30, 39};
+/* residual_block_cabac (7.3.5.3.3, 9.3.3.1.3) of ctxBlockCat cat: levels in
+ * coefficient-list order into lvl; returns the count of non-zero levels
+ * (0: coded_block_flag 0) or -1 */
+static int cab_residual(fo_cab *k, int cat, int cbf_inc, int maxNum, int *lvl) {
+  for (int i = 0; i < maxNum; i++) lvl[i] = 0;
+  if (cat != 5 && !cab_dec(k, 85 + CBF_OFF[cat] + cbf_inc)) return 0;
+  int sig[64] = {0}, numCoeff = maxNum;
+  for (int i = 0; i < numCoeff - 1; i++) {
+    int inc = cat == 3 ? imin(i, 2) : i;
+    if (cab_dec(k, cat == 5 ? 402 + SIG8[i] : 105 + SIG_OFF[cat] + inc)) {
+      sig[i] = 1;
+      if (cab_dec(k, cat == 5 ? 417 + LAST8[i] : 166 + SIG_OFF[cat] + inc)) { numCoeff = i + 1; break; }
     }
-  } else if (m->type == 1) {
-    int done = 0;
-    for (int k = 0; k < 16; k++) {
-      int bx = BLK_X[k], by = BLK_Y[k], blk = by * 4 + bx, pred[16], r[16];
-      intra4x4(d, pic, addr, k, m->i4[blk], done, pred);
-      scale_idct4(coef[blk], qpy, 0, r);
-      for (int y = 0; y < 4; y++)
-        for (int x = 0; x < 4; x++)
-          Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred[y * 4 + x] + r[y * 4 + x]);
-      done |= 1 << blk;
+  }
+  sig[numCoeff - 1] = 1;
+  int eq1 = 0, gt1 = 0, n = 0, base = cat == 5 ? 426 : 227 + ABS_OFF[cat];
+  for (int i = numCoeff - 1; i >= 0; i--) {
+    if (!sig[i]) continue;
+    int v = 0;
+    if (cab_dec(k, base + (gt1 ? 0 : imin(4, 1 + eq1)))) {
+      v = 1;
+      int inc = 5 + imin(4 - (cat == 3), gt1);
+      while (v < 14 && cab_dec(k, base + inc)) v++;
+      if (v >= 14) { /* UEG0 suffix */
+        int kk = 0;
+        while (cab_bypass(k)) { v += 1 << kk; if (++kk > 30) return -1; }
+        while (kk--) v += cab_bypass(k) << kk;
+      }
+    }
+    int lv = v + 1;
+    if (cab_bypass(k)) lv = -lv;
+    lvl[i] = lv;
+    if (v == 0) eq1++;
+    else gt1++;
+    n++;
+  }
+  return n;
+}
+
+/* condTermFlagN of coded_block_flag (9.3.3.1.1.9): neighbour macroblock n
+ * (-1 unavailable), transBlockN available (tb), its flag bit */
+static int cbf_cond(const fo_dec *d, int cur_intra, int n, int tb, int bit) {
+  if (n < 0) return cur_intra;
+  const fo_mb *m = &d->mb[n];
+  if (m->type == 3) return 1;
+  if (!tb || m->type == 4) return 0;
+  return (int)((m->cbf >> bit) & 1u);
+}
+/* coded_block_flag ctxIdxInc of a luma 4x4 block at (x, y) (4x4 units) */
+static int cbf_luma_inc(const fo_dec *d, int addr, int x, int y, int intra) {
+  int inc = 0;
+  for (int nb = 0; nb < 2; nb++) {
+    fo_loc L = nb_loc(d, addr, nb ? x * 4 : x * 4 - 1, nb ? y * 4 - 1 : y * 4, 16, 16);
+    int tb = 0, bit = 0;
+    if (L.mb >= 0) {
+      const fo_mb *m = &d->mb[L.mb];
+      int b8 = (L.yw / 8) * 2 + L.xw / 8;
+      tb = (m->cbp >> b8) & 1;
+      bit = 1 + (L.yw / 4) * 4 + L.xw / 4;
+    }
+    inc += cbf_cond(d, intra, L.mb, tb, bit) << nb;
+  }
+  return inc;
+}
+static int cbf_chroma_inc(const fo_dec *d, int addr, int pl, int blk, int dc, int intra) {
+  int inc = 0;
+  for (int nb = 0; nb < 2; nb++) {
+    int x = dc ? 0 : (blk & 1) * 4, y = dc ? 0 : (blk >> 1) * 4;
+    fo_loc L = nb_loc(d, addr, nb ? x : x - 1, nb ? y - 1 : y, 8, 8);
+    int tb = 0, bit = 0;
+    if (L.mb >= 0) {
+      const fo_mb *m = &d->mb[L.mb];
+      tb = dc ? (m->cbp >> 4) != 0 : (m->cbp >> 4) == 2;
+      bit = dc ? 17 + pl : 19 + 4 * pl + (L.yw / 4) * 2 + L.xw / 4;
+    }
+    inc += cbf_cond(d, intra, L.mb, tb, bit) << nb;
+  }
+  return inc;
+}
+static int abs_mvd_at(const fo_dec *d, int addr, int xN, int yN, int comp) {
+  fo_loc L = nb_loc(d, addr, xN, yN, 16, 16);
+  if (L.mb < 0) return 0;
+  const fo_mb *m = &d->mb[L.mb];
+  if (m->type != 0) return 0; /* skip, intra */
+  return iabs(m->mvd[(L.yw / 4) * 4 + L.xw / 4][comp]);
+}
+static int ref_gt0_at(const fo_dec *d, int addr, int xN, int yN) {
+  fo_loc L = nb_loc(d, addr, xN, yN, 16, 16);
+  if (L.mb < 0) return 0;
+  const fo_mb *m = &d->mb[L.mb];
+  if (m->type != 0) return 0;
+  return m->refidx[(L.yw / 4) * 4 + L.xw / 4] > 0;
+}
+/* Intra NxN mode predictor (8.3.1.1 / 8.3.2.1) of the block whose top-left
+ * luma sample is (x0, y0); is8: the current block is 8x8 */
+static int intra_pred_mode_pred(const fo_dec *d, int addr, int x0, int y0, int is8) {
+  fo_loc LA = nb_loc(d, addr, x0 - 1, y0, 16, 16), LB = nb_loc(d, addr, x0, y0 - 1, 16, 16);
+  if (LA.mb < 0 || LB.mb < 0) return 2;
+  const fo_mb *ma = &d->mb[LA.mb], *mb2 = &d->mb[LB.mb];
+  if (d->P->cip && (!mb_intra(ma) || !mb_intra(mb2))) return 2;
+  int modes[2];
+  const fo_loc *L[2] = {&LA, &LB};
+  const fo_mb *M[2] = {ma, mb2};
+  for (int i = 0; i < 2; i++) {
+    const fo_mb *m = M[i];
+    if (m->type != 1) { modes[i] = 2; continue; }
+    if (m->t8 || !is8) { modes[i] = m->i4[(L[i]->yw / 4) * 4 + L[i]->xw / 4]; continue; }
+    /* 4x4 neighbour of an 8x8 block: Intra4x4PredMode[luma8x8BlkIdxN * 4 + n], n = 1 (A), 2 (B) */
+    int b8 = (L[i]->yw / 8) * 2 + L[i]->xw / 8, idx = b8 * 4 + (i == 0 ? 1 : 2);
+    modes[i] = m->i4[BLK_Y[idx] * 4 + BLK_X[idx]];
+  }
+  return imin(modes[0], modes[1]);
+}
+
+/* macroblock_layer (7.3.5) with CABAC (not P_Skip) + reconstruction */
+static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, int prev) {
+  fo_dec *d = c->d;
+  fo_mb *m = &d->mb[addr];
+  fo_pic *pic = c->cur;
+  int slice = m->slice;
+  memset(m, 0, sizeof *m);
+  m->slice = slice;
+  for (int i = 0; i < 16; i++) { m->refidx[i] = -1; m->refpic[i] = -1; m->i4[i] = 2; }
+  int mx = addr % d->mbw, my = addr / d->mbw;
+  int A = nb_loc(d, addr, -1, 0, 16, 16).mb, B = nb_loc(d, addr, 0, -1, 16, 16).mb;
+  const fo_mb *ma = A >= 0 ? &d->mb[A] : NULL, *mbb = B >= 0 ? &d->mb[B] : NULL;
+  int mb_type, itype;
+  if (is_p) {
+    if (cab_dec(k, 14)) {
+      itype = cab_i_type(k, 1, 0);
+      mb_type = 5 + itype;
+    } else {
+      itype = -1;
+      if (!cab_dec(k, 15)) mb_type = cab_dec(k, 16) ? 3 : 0;
+      else mb_type = cab_dec(k, 17) ? 1 : 2;
     }
   } else {
-    intra_big(d, pic, addr, 0, i16mode, pred_y);
-    /* 8.5.10: Intra16x16 DC Hadamard + scaling */
-    int f[16], t[16];
-    for (int i = 0; i < 4; i++) {
-      int a0 = dcl[i * 4 + 0], a1 = dcl[i * 4 + 1], a2 = dcl[i * 4 + 2], a3 = dcl[i * 4 + 3];
-      t[i * 4 + 0] = a0 + a1 + a2 + a3;
-      t[i * 4 + 1] = a0 + a1 - a2 - a3;
-      t[i * 4 + 2] = a0 - a1 - a2 + a3;
-      t[i * 4 + 3] = a0 - a1 + a2 - a3;
+    itype = cab_i_type(k, 0, (ma && ma->type != 1) + (mbb && mbb->type != 1));
+    mb_type = itype;
+  }
+  (void)mb_type;
+  if (itype == 25) { /* I_PCM: pcm_alignment_zero_bit, samples, engine restart (9.3.1.2) */
+    m->type = 3;
+    m->qp = *qp;
+    k->b->bitpos = 0;
+    for (int y = 0; y < 16; y++)
+      for (int x = 0; x < 16; x++) pic->y[(int64_t)(my * 16 + y) * d->W + mx * 16 + x] = (uint8_t)fb_byte(k->b);
+    for (int pl = 0; pl < 2; pl++)
+      for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++)
+          (pl ? pic->v : pic->u)[(int64_t)(my * 8 + y) * (d->W / 2) + mx * 8 + x] = (uint8_t)fb_byte(k->b);
+    for (int i = 0; i < 16; i++) m->nz[i] = 16;
+    for (int i = 0; i < 4; i++) m->nzc[0][i] = m->nzc[1][i] = 16;
+    m->cbp = 0x2f;
+    cab_start(k);
+    return k->b->err ? fo_fail(d, FO_E_FORMAT, "I_PCM") : 0;
+  }
+  int cbp = 0, i16mode = 0, cmode = 0, sub[4] = {0, 0, 0, 0}, small = 0;
+  if (itype == 0) { /* I_NxN */
+    m->type = 1;
+    if (d->P->t8mode) m->t8 = cab_dec(k, 399 + (ma && ma->t8) + (mbb && mbb->t8));
+    int nb = m->t8 ? 4 : 16, prev_f[16], rem[16];
+    for (int i = 0; i < nb; i++) {
+      prev_f[i] = cab_dec(k, 68);
+      rem[i] = prev_f[i] ? 0 : cab_fl3(k, 69);
     }
-    for (int j = 0; j < 4; j++) {
-      int a0 = t[0 * 4 + j], a1 = t[1 * 4 + j], a2 = t[2 * 4 + j], a3 = t[3 * 4 + j];
-      f[0 * 4 + j] = a0 + a1 + a2 + a3;
-      f[1 * 4 + j] = a0 + a1 - a2 - a3;
-      f[2 * 4 + j] = a0 - a1 - a2 + a3;
-      f[3 * 4 + j] = a0 - a1 + a2 - a3;
+    for (int i = 0; i < nb; i++) {
+      int x0 = m->t8 ? (i & 1) * 8 : BLK_X[i] * 4, y0 = m->t8 ? (i >> 1) * 8 : BLK_Y[i] * 4;
+      int pm = intra_pred_mode_pred(d, addr, x0, y0, m->t8);
+      int mode = prev_f[i] ? pm : (rem[i] < pm ? rem[i] : rem[i] + 1);
+      if (m->t8) {
+        int r = (y0 / 4) * 4 + x0 / 4;
+        m->i4[r] = m->i4[r + 1] = m->i4[r + 4] = m->i4[r + 5] = mode;
+      } else {
+        m->i4[(y0 / 4) * 4 + x0 / 4] = mode;
+      }
     }
-    int ls = level_scale(qpy % 6, 0, 0);
-    for (int k = 0; k < 16; k++) {
-      int dc = qpy >= 36 ? (f[k] * ls) << (qpy / 6 - 6) : (f[k] * ls + (1 << (5 - qpy / 6))) >> (6 - qpy / 6);
-      coef[k][0] = dc; /* dcY row i col j -> block (x = j, y = i) */
+  } else if (itype >= 1) { /* I_16x16 */
+    m->type = 2;
+    i16mode = (itype - 1) % 4;
+    cbp = (((itype - 1) / 4) % 3) << 4 | (itype >= 13 ? 15 : 0);
+  } else { /* inter, Table 7-13 */
+    m->type = 0;
+    int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4), refs[4] = {0, 0, 0, 0};
+    if (mb_type == 3) {
+      for (int i = 0; i < 4; i++) {
+        if (cab_dec(k, 21)) sub[i] = 0;
+        else if (!cab_dec(k, 22)) sub[i] = 1;
+        else sub[i] = cab_dec(k, 23) ? 2 : 3;
+        if (sub[i]) small = 1;
+      }
     }
-    for (int blk = 0; blk < 16; blk++) {
-      int r[16], bx = blk % 4, by = blk / 4;
-      scale_idct4(coef[blk], qpy, 1, r);
-      for (int y = 0; y < 4; y++)
-        for (int x = 0; x < 4; x++)
-          Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred_y[(by * 4 + y) * 16 + bx * 4 + x] + r[y * 4 + x]);
+    int nref = c->nlist;
+    /* ref_idx_l0 of every partition, then every mvd (7.3.5.1 / 7.3.5.2) */
+    for (int i = 0; i < nparts; i++) {
+      int x0 = (mb_type == 2 || mb_type == 3) ? 8 * (i & 1) : 0;
+      int y0 = mb_type == 1 ? 8 * i : (mb_type == 3 ? 8 * (i >> 1) : 0);
+      int pw = mb_type == 0 || mb_type == 1 ? 16 : 8, ph = mb_type == 0 || mb_type == 2 ? 16 : 8;
+      if (nref > 1) {
+        int v = 0;
+        if (cab_dec(k, 54 + ref_gt0_at(d, addr, x0 - 1, y0) + 2 * ref_gt0_at(d, addr, x0, y0 - 1))) {
+          v = 1;
+          if (cab_dec(k, 58)) {
+            v = 2;
+            while (cab_dec(k, 59)) { if (++v > 32) return fo_fail(d, FO_E_FORMAT, "ref_idx"); }
+          }
+        }
+        refs[i] = v;
+      }
+      if (refs[i] >= nref || !c->list[refs[i]]) return fo_fail(d, FO_E_DECODE, "ref_idx names no reference picture");
+      for (int yy = y0 / 4; yy < (y0 + ph) / 4; yy++)
+        for (int xx = x0 / 4; xx < (x0 + pw) / 4; xx++) {
+          m->refidx[yy * 4 + xx] = refs[i];
+          m->refpic[yy * 4 + xx] = c->list[refs[i]]->id;
+        }
+    }
+    int done = 0;
+    for (int i = 0; i < nparts; i++) {
+      int nsub = 1, pw, ph, x0, y0;
+      if (mb_type == 0) { pw = 16; ph = 16; x0 = y0 = 0; }
+      else if (mb_type == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * i; }
+      else if (mb_type == 2) { pw = 8; ph = 16; x0 = 8 * i; y0 = 0; }
+      else {
+        x0 = 8 * (i & 1);
+        y0 = 8 * (i >> 1);
+        nsub = sub[i] == 0 ? 1 : (sub[i] == 3 ? 4 : 2);
+        pw = sub[i] == 0 || sub[i] == 1 ? 8 : 4;
+        ph = sub[i] == 0 || sub[i] == 2 ? 8 : 4;
+      }
+      for (int s = 0; s < nsub; s++) {
+        int sx = x0, sy = y0;
+        if (mb_type == 3) {
+          if (sub[i] == 1) sy += 4 * s;
+          else if (sub[i] == 2) sx += 4 * s;
+          else if (sub[i] == 3) { sx += 4 * (s & 1); sy += 4 * (s >> 1); }
+        }
+        int dmv[2];
+        for (int comp = 0; comp < 2; comp++)
+          dmv[comp] = cab_mvd(k, comp ? 47 : 40, abs_mvd_at(d, addr, sx - 1, sy, comp) + abs_mvd_at(d, addr, sx, sy - 1, comp));
+        int px, py;
+        mv_pred(d, addr, sx, sy, pw, ph, refs[i], done, &px, &py);
+        int vx = px + dmv[0], vy = py + dmv[1];
+        if (vx < -32768 || vx > 32767 || vy < -32768 || vy > 32767) return fo_fail(d, FO_E_FORMAT, "mv range");
+        for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
+          for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) {
+            int blk = yy * 4 + xx;
+            m->mv[blk][0] = vx;
+            m->mv[blk][1] = vy;
+            m->mvd[blk][0] = dmv[0];
+            m->mvd[blk][1] = dmv[1];
+            done |= 1 << blk;
+          }
+      }
     }
   }
-  /* chroma */
-  if (m->type != 0) {
-    intra_big(d, pic, addr, 1, cmode, pred_u);
-    intra_big(d, pic, addr, 2, cmode, pred_v);
+  if (m->type == 1 || m->type == 2) { /* intra_chroma_pred_mode: TU cMax 3 */
+    int inc = 0;
+    for (int nb = 0; nb < 2; nb++) {
+      const fo_mb *n = nb ? mbb : ma;
+      inc += n && (n->type == 1 || n->type == 2) && n->cmode != 0;
+    }
+    if (cab_dec(k, 64 + inc)) {
+      cmode = 1;
+      if (cab_dec(k, 67)) {
+        cmode = 2;
+        if (cab_dec(k, 67)) cmode = 3;
+      }
+    }
+    m->cmode = cmode;
   }
-  for (int pl = 0; pl < 2; pl++) {
-    int qpc = qpc_of(qpy, pl ? d->P->cqp_off2 : d->P->cqp_off);
-    int c0 = cdc[pl][0], c1 = cdc[pl][1], c2 = cdc[pl][2], c3 = cdc[pl][3];
-    int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
-    int ls = level_scale(qpc % 6, 0, 0);
-    uint8_t *U = (pl ? pic->v : pic->u) + (int64_t)(my * 8) * (d->W / 2) + mx * 8;
-    int *pr = pl ? pred_v : pred_u;
-    for (int k = 0; k < 4; k++) {
-      int bx = k & 1, by = k >> 1, r[16];
-      cac[pl][k][0] = ((f[k] * ls) << (qpc / 6)) >> 5;
-      scale_idct4(cac[pl][k], qpc, 1, r);
-      for (int y = 0; y < 4; y++)
-        for (int x = 0; x < 4; x++)
-          U[(int64_t)(by * 4 + y) * (d->W / 2) + bx * 4 + x] = (uint8_t)clip1(pr[(by * 4 + y) * 8 + bx * 4 + x] + r[y * 4 + x]);
+  if (m->type != 2) { /* coded_block_pattern: 4 luma bins (FL), chroma TU (9.3.3.1.1.4) */
+    for (int b8 = 0; b8 < 4; b8++) {
+      int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8, cond[2];
+      for (int nb = 0; nb < 2; nb++) {
+        fo_loc L = nb_loc(d, addr, nb ? bx : bx - 1, nb ? by - 1 : by, 16, 16);
+        int b8n = (L.yw / 8) * 2 + L.xw / 8;
+        if (L.mb < 0) cond[nb] = 0;
+        else if (L.mb == addr) cond[nb] = !((cbp >> b8n) & 1);
+        else {
+          const fo_mb *n = &d->mb[L.mb];
+          cond[nb] = n->type == 3 ? 0 : (n->type == 4 ? 1 : !((n->cbp >> b8n) & 1));
+        }
+      }
+      cbp |= cab_dec(k, 73 + cond[0] + 2 * cond[1]) << b8;
+    }
+    int ca[2], cb2[2];
+    for (int nb = 0; nb < 2; nb++) {
+      const fo_mb *n = nb ? mbb : ma;
+      int cc = !n ? 0 : (n->type == 3 ? 2 : (n->type == 4 ? 0 : n->cbp >> 4));
+      ca[nb] = cc != 0;
+      cb2[nb] = cc == 2;
+    }
+    if (cab_dec(k, 77 + ca[0] + 2 * ca[1])) cbp |= (1 + cab_dec(k, 77 + 4 + cb2[0] + 2 * cb2[1])) << 4;
+  }
+  m->cbp = cbp;
+  if (m->type == 0 && (cbp & 15) && d->P->t8mode && !small)
+    m->t8 = cab_dec(k, 399 + (ma && ma->t8) + (mbb && mbb->t8));
+  if ((cbp & 15) || (cbp >> 4) || m->type == 2) { /* mb_qp_delta: U of the se mapping */
+    const fo_mb *pm = prev >= 0 ? &d->mb[prev] : NULL;
+    int inc = pm && pm->type != 4 && pm->type != 3 && (pm->type == 2 || pm->cbp != 0) && pm->qpd != 0;
+    int kk = 0;
+    if (cab_dec(k, 60 + inc)) {
+      kk = 1;
+      if (cab_dec(k, 62)) {
+        kk = 2;
+        while (cab_dec(k, 63)) { if (++kk > 104) return fo_fail(d, FO_E_FORMAT, "mb_qp_delta"); }
+      }
+    }
+    int dq = (kk & 1) ? (kk + 1) / 2 : -(kk / 2);
+    if (dq < -26 || dq > 25) return fo_fail(d, FO_E_FORMAT, "mb_qp_delta");
+    m->qpd = dq;
+    *qp = (*qp + dq + 52) % 52;
+  }
+  m->qp = *qp;
+  /* residual (7.3.5.3): coefficients in raster per block */
+  int coef[16][16], dcl[16], cdc[2][4], cac[2][4][16], coef8[4][64], lvl[64];
+  memset(coef, 0, sizeof coef);
+  memset(dcl, 0, sizeof dcl);
+  memset(cdc, 0, sizeof cdc);
+  memset(cac, 0, sizeof cac);
+  memset(coef8, 0, sizeof coef8);
+  int intra = m->type == 1 || m->type == 2;
+  if (m->type == 2) {
+    int inc = 0;
+    for (int nb = 0; nb < 2; nb++) {
+      const fo_mb *n = nb ? mbb : ma;
+      inc += cbf_cond(d, intra, nb ? B : A, n && n->type == 2, 0) << nb;
+    }
+    int n = cab_residual(k, 0, inc, 16, lvl);
+    if (n < 0) return fo_fail(d, FO_E_FORMAT, "Intra16x16DCLevel");
+    for (int i = 0; i < 16; i++) dcl[ZZ4[i]] = lvl[i];
+    if (n) m->cbf |= 1u;
+  }
+  for (int b8 = 0; b8 < 4; b8++) {
+    if (!((cbp >> b8) & 1)) continue;
+    int r0 = (b8 >> 1) * 8 + (b8 & 1) * 2; /* raster 4x4 index of the 8x8's top-left */
+    if (m->t8) {
+      int n = cab_residual(k, 5, 0, 64, lvl);
+      if (n < 0) return fo_fail(d, FO_E_FORMAT, "LumaLevel8x8");
+      for (int i = 0; i < 64; i++) coef8[b8][ZZ8[i]] = lvl[i];
+      int rs[4] = {r0, r0 + 1, r0 + 4, r0 + 5};
+      for (int j = 0; j < 4; j++) { m->nz[rs[j]] = n; m->cbf |= 1u << (1 + rs[j]); }
+      continue;
+    }
+    for (int i4 = 0; i4 < 4; i4++) {
+      int blk = b8 * 4 + i4, bx = BLK_X[blk], by = BLK_Y[blk], r = by * 4 + bx;
+      int inc = cbf_luma_inc(d, addr, bx, by, intra);
+      int n = m->type == 2 ? cab_residual(k, 1, inc, 15, lvl) : cab_residual(k, 2, inc, 16, lvl);
+      if (n < 0) return fo_fail(d, FO_E_FORMAT, "LumaLevel4x4");
+      if (m->type == 2) for (int i = 0; i < 15; i++) coef[r][ZZ4[i + 1]] = lvl[i];
+      else for (int i = 0; i < 16; i++) coef[r][ZZ4[i]] = lvl[i];
+      m->nz[r] = n;
+      if (n) m->cbf |= 1u << (1 + r);
     }
   }
+  if (cbp >> 4) {
+    for (int pl = 0; pl < 2; pl++) {
+      int n = cab_residual(k, 3, cbf_chroma_inc(d, addr, pl, 0, 1, intra), 4, lvl);
+      if (n < 0) return fo_fail(d, FO_E_FORMAT, "ChromaDCLevel");
+      for (int i = 0; i < 4; i++) cdc[pl][i] = lvl[i];
+      if (n) m->cbf |= 1u << (17 + pl);
+    }
+  }
+  if ((cbp >> 4) == 2) {
+    for (int pl = 0; pl < 2; pl++)
+      for (int b = 0; b < 4; b++) {
+        int n = cab_residual(k, 4, cbf_chroma_inc(d, addr, pl, b, 0, intra), 15, lvl);
+        if (n < 0) return fo_fail(d, FO_E_FORMAT, "ChromaACLevel");
+        for (int i = 0; i < 15; i++) cac[pl][b][ZZ4[i + 1]] = lvl[i];
+        m->nzc[pl][b] = n;
+        if (n) m->cbf |= 1u << (19 + 4 * pl + b);
+      }
+  }
+  if (k->b->err) return fo_fail(d, FO_E_FORMAT, "bitstream exhausted in residual");
+  return recon_mb(c, addr, coef, dcl, cdc, cac, coef8, i16mode, cmode);
+}
+
+/* 7.3.4 slice_data() with CABAC; stop = the RBSP stop bit (EBSP bit index) */
+static int slice_data_cabac(fo_ctx *c, fb_t *b, const fo_hdr *h, int is_p, int64_t stop) {
+  fo_dec *d = c->d;
+  while (b->bitpos)
+    if (!fb_bit(b)) return fo_fail(d, FO_E_FORMAT, "cabac_alignment_one_bit");
+  fo_cab k;
+  k.b = b;
+  cab_init(&k, !is_p, h->qp);
+  cab_start(&k);
+  int addr = h->first_mb, qp = h->qp, prev = -1;
+  for (;;) {
+    if (addr >= d->nmb) return fo_fail(d, FO_E_FORMAT, "macroblock address past the picture");
+    if (d->mb[addr].slice >= 0) return fo_fail(d, FO_E_FORMAT, "macroblock decoded twice");
+    d->mb[addr].slice = c->slice_no;
+    int skip = 0;
+    if (is_p) {
+      int A = nb_loc(d, addr, -1, 0, 16, 16).mb, B = nb_loc(d, addr, 0, -1, 16, 16).mb;
+      skip = cab_dec(&k, 11 + (A >= 0 && d->mb[A].type != 4) + (B >= 0 && d->mb[B].type != 4));
+    }
+    int rc = skip ? decode_mb(c, NULL, addr, 1, &qp, h) : decode_mb_cabac(c, &k, addr, is_p, &qp, prev);
+    if (getenv("FO_TRACE"))
+      fprintf(stderr, "oracle cabac mb %d type %d cbp %d qp %d t8 %d bits %lld\n", addr, d->mb[addr].type,
+              d->mb[addr].cbp, qp, d->mb[addr].t8, (long long)fb_index(b, 0));
+    if (rc) return rc;
+    if (b->err) return fo_fail(d, FO_E_FORMAT, "bitstream exhausted");
+    prev = addr++;
+    if (cab_term(&k)) break; /* end_of_slice_flag */
+  }
+  if (fb_index(b, 0) != stop + 1) return fo_fail(d, FO_E_FORMAT, "CABAC slice data does not end at the stop bit");
   return 0;
 }
 
