@@ -14,6 +14,7 @@
 #include "h264_full.h"
 #include "h264_sched.h"
 #include "mp4.h"
+#include "parse_cabac.h"
 #include "parse_full.h"
 #include "recon_full.h"
 
@@ -88,7 +89,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     d.dbk_idc = s.dbk_idc;
     d.dbk_a = s.dbk_a;
     d.dbk_b = s.dbk_b;
-    const int64_t cap = std::min<int64_t>(27ll * s.n_mbs, 3ll * s.nal_size + 27);
+    const int64_t cap = pps.entropy_coding_mode ? 27ll * s.n_mbs : std::min<int64_t>(27ll * s.n_mbs, 3ll * s.nal_size + 27);
     d.arena = arena_blocks;
     d.arena_cap = static_cast<uint32_t>(cap);
     arena_blocks += static_cast<uint32_t>(cap);
@@ -101,6 +102,8 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   P.cip = pps.constrained_intra_pred;
   P.cqp_off = pps.chroma_qp_index_offset;
   P.cqp_off2 = facts.cqp_off2;
+  P.cabac = pps.entropy_coding_mode;
+  P.t8mode = facts.transform_8x8;
   const uint32_t epoch = 7;
   for (int fi = 0; fi < n; ++fi) {
     const SchedFrame &fr = frames[static_cast<size_t>(fi)];
@@ -108,8 +111,12 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     uint32_t errs = 0;
     for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
       full::FullScratch sc;
-      errs |= full::parse_slice_full(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P, fr_recs,
-                                     ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(), epoch, &sc);
+      errs |= P.cabac ? full::parse_slice_cabac(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P,
+                                                fr_recs, ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(),
+                                                epoch, &sc)
+                      : full::parse_slice_full(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P,
+                                               fr_recs, ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(),
+                                               epoch, &sc);
     }
     if (errs) return bad("frame " + std::to_string(fi) + ": parse: " + describe_decode_error(errs));
     full::ReconCtx c{};

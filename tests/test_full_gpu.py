@@ -117,3 +117,33 @@ def test_subset_only_decoder_refuses_full_syntax(tmp_path):
     with scene.VideoScorer(path, decoder="subset") as v:
         with pytest.raises(VtsegError):
             v.score()
+
+
+def test_real_cabac_high_profile_stream():
+    """A real High-profile CABAC clip (tests/golden/real/realshort.mp4: CABAC
+    I/P slices, 8x8 transform, Intra 8x8/4x4/16x16, deblocking) decodes and
+    scores on the device bit for bit like the oracle (auto-selected general
+    decoder)."""
+    _require_gpu()
+    from pathlib import Path
+    path = Path(__file__).resolve().parent / "golden" / "real" / "realshort.mp4"
+    frames, _ = oracle.decode_full(path)
+    n = frames.shape[0]
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 320, 240, 320, 240, 4)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+        assert _first_diff(got, frames) == []
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+
+
+def test_real_cabac_subset_decoder_refuses():
+    _require_gpu()
+    from pathlib import Path
+    path = Path(__file__).resolve().parent / "golden" / "real" / "realshort.mp4"
+    with pytest.raises(VtsegError):
+        with scene.VideoScorer(path, decoder="subset") as v:
+            v.score()

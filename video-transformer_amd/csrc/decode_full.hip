@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "decode_full.h"
+#include "parse_cabac.h"
 #include "parse_full.h"
 #include "recon_full.h"
 
@@ -34,7 +35,7 @@ namespace vts {
 namespace {
 
 constexpr int kInterThreads = 256;   // 16 macroblocks x 16 blocks
-constexpr int kIntraThreads = 1024;  // 64 macroblocks in flight
+constexpr int kIntraThreads = 512;   // 32 macroblocks in flight (256 VGPRs for the Intra_8x8 path)
 constexpr int kIntraSlots = kIntraThreads / 16;
 constexpr int kDbkThreads = 1024;    // 16 waves = 16 row pairs in flight
 constexpr int kDbkWaves = kDbkThreads / 64;
@@ -48,9 +49,11 @@ __global__ void __launch_bounds__(1) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
   const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
-  const uint32_t e = full::parse_slice_full(a.es, s, static_cast<uint32_t>(a.slice0 + i), P,
-                                            a.recs + s.slot * nmb, a.ilvl + s.slot * nmb, a.arena, a.epoch,
-                                            &scratch);
+  const uint32_t e =
+      P.cabac ? full::parse_slice_cabac(a.es, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
+                                        a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch)
+              : full::parse_slice_full(a.es, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
+                                       a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch);
   if (e) atomicOr(a.err, e);
 }
 
@@ -196,6 +199,48 @@ __device__ __forceinline__ void chroma_res(const int16_t *arena, uint32_t blocks
   full::scale_idct4(cf, qpc, true, r);
 }
 
+// 8.5.13 for one 4x4 quarter (qx, qy) of an 8x8 block stored as raster rows
+// in the arena (4 consecutive blocks): all 8 rows transformed, then this
+// quarter's 4 columns
+__device__ __forceinline__ void idct8_quarter(const int16_t *arena, int64_t blk, int qp, int qx, int qy, int (&res)[16]) {
+  int n8[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) n8[c] = 16 * full::kNorm8[qp % 6][c];
+  const int sh = qp / 6;
+  int t[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 u = *reinterpret_cast<const uint4 *>(arena + 16 * blk + 8 * i);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    int v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = static_cast<int16_t>((w[j >> 1] >> ((j & 1) * 16)) & 0xffff);
+      const int ls = n8[vts_norm8_class(i, j)];
+      v[j] = qp >= 36 ? (c * ls) << (sh - 6) : (c * ls + (1 << (5 - sh))) >> (6 - sh);
+    }
+    const int a0 = v[0] + v[4], a4 = v[0] - v[4], a2 = (v[2] >> 1) - v[6], a6 = v[2] + (v[6] >> 1);
+    const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+    const int a1 = -v[3] + v[5] - v[7] - (v[7] >> 1), a3 = v[1] + v[7] - v[3] - (v[3] >> 1);
+    const int a5 = -v[1] + v[7] + v[5] + (v[5] >> 1), a7 = v[3] + v[5] + v[1] + (v[1] >> 1);
+    const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+    const int o[8] = {b0 + b7, b2 + b5, b4 + b3, b6 + b1, b6 - b1, b4 - b3, b2 - b5, b0 - b7};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[i][k] = qx ? o[4 + k] : o[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int a0 = t[0][k] + t[4][k], a4 = t[0][k] - t[4][k], a2 = (t[2][k] >> 1) - t[6][k], a6 = t[2][k] + (t[6][k] >> 1);
+    const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+    const int a1 = -t[3][k] + t[5][k] - t[7][k] - (t[7][k] >> 1), a3 = t[1][k] + t[7][k] - t[3][k] - (t[3][k] >> 1);
+    const int a5 = -t[1][k] + t[7][k] + t[5][k] + (t[5][k] >> 1), a7 = t[3][k] + t[5][k] + t[1][k] + (t[1][k] >> 1);
+    const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+    const int o[8] = {b0 + b7, b2 + b5, b4 + b3, b6 + b1, b6 - b1, b4 - b3, b2 - b5, b0 - b7};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) res[r * 4 + k] = ((qy ? o[4 + r] : o[r]) + 32) >> 6;
+  }
+}
+
 // MbRec header words (the first 32 bytes)
 struct MbHdr {
   uint32_t epoch, slice, coef, blocks;
@@ -304,8 +349,11 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
   luma_pred4(w, mvx & 3, mvy & 3, pv);
   // luma residual
   int res[16];
-  const int64_t lb = stored(h.blocks, h.coef, kBlkLuma0 + blkidx(b));
-  if (lb >= 0) {
+  const bool t8 = (h.modes & kModeT8) != 0;
+  const int64_t lb = stored(h.blocks, h.coef, t8 ? kBlkLuma0 + 4 * ((by >> 1) * 2 + (bx >> 1)) : kBlkLuma0 + blkidx(b));
+  if (lb >= 0 && t8) {
+    idct8_quarter(a.arena, lb, h.qp, bx & 1, by & 1, res);
+  } else if (lb >= 0) {
     int cf[16];
     load_coefs(a.arena, lb, cf);
     full::scale_idct4(cf, h.qp, false, res);
@@ -356,6 +404,7 @@ struct IntraTile {
   uint8_t ct[2][9];    // chroma row -1, cols -1..7 (index + 1), per plane
   uint8_t cl[2][8];    // chroma col -1, rows 0..7
   uint8_t cout[8][16]; // reconstructed chroma rows, interleaved
+  int16_t f8[25];      // Intra_8x8: filtered p'[-1,-1], p'[0..15,-1] (1..16), p'[-1,0..7] (17..24)
 };
 
 __device__ __forceinline__ void lane_sync() {
@@ -482,6 +531,137 @@ __device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraT
       *reinterpret_cast<uint32_t *>(Y + yrow0 + static_cast<int64_t>(by * 4 + r) * pitch + bx * 4) =
           pack4(c255(v[r * 4] + res[r * 4]), c255(v[r * 4 + 1] + res[r * 4 + 1]), c255(v[r * 4 + 2] + res[r * 4 + 2]),
                 c255(v[r * 4 + 3] + res[r * 4 + 3]));
+  } else if (h.modes & kModeT8) {
+    // Intra_8x8 (8.3.2): the 8x8 blocks in order, one step each; the 4 lanes
+    // of a block each predict and reconstruct one 4x4 quarter from the
+    // filtered reference samples (every lane filters them itself)
+    const int b8 = (by >> 1) * 2 + (bx >> 1), qx = bx & 1, qy = by & 1;
+    const int xo = (b8 & 1) * 8, yo = (b8 >> 1) * 8;
+    const int r8 = (b8 >> 1) * 8 + (b8 & 1) * 2;
+    const uint32_t i4w = reinterpret_cast<const uint32_t *>(rec)[8 + (r8 >> 3)];
+    const int m8 = (i4w >> (((r8 >> 1) & 3) * 8 + (r8 & 1) * 4)) & 15;
+    const bool top = yo > 0 || B, left = xo > 0 || A;
+    const bool tl = (xo > 0 && yo > 0) || (yo == 0 && xo > 0 ? B : (xo == 0 && yo > 0 ? A : D));
+    const bool tr = b8 == 0 ? B : (b8 == 1 ? C : b8 == 2);
+    const int64_t lb = stored(h.blocks, h.coef, kBlkLuma0 + 4 * b8);
+    for (int s = 0; s < 4; ++s) {
+      if (s == b8 && qx == 0 && qy == 0) {  // the block's first lane filters the reference samples
+        const int ty = yo, tx = 4 + xo;  // tile row of p[., -1], col of p[0, .]
+        int P_[25];  // 0 = p[-1,-1], 1 + x = p[x,-1], 17 + y = p[-1,y]
+        P_[0] = tl ? t.y[ty][tx - 1] : 0;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) P_[1 + x] = top ? t.y[ty][tx + x] : 0;
+#pragma unroll
+        for (int x = 8; x < 16; ++x) P_[1 + x] = tr ? t.y[ty][tx + x] : P_[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) P_[17 + y] = left ? t.y[ty + 1 + y][tx - 1] : 0;
+        int T[17], L[8];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) T[i] = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) L[i] = 0;
+        if (top) {
+          T[1] = tl ? (P_[0] + 2 * P_[1] + P_[2] + 2) >> 2 : (3 * P_[1] + P_[2] + 2) >> 2;
+#pragma unroll
+          for (int x = 1; x < 15; ++x) T[1 + x] = (P_[x] + 2 * P_[1 + x] + P_[2 + x] + 2) >> 2;
+          T[16] = (P_[15] + 3 * P_[16] + 2) >> 2;
+        }
+        if (tl) {
+          if (top && left) T[0] = (P_[1] + 2 * P_[0] + P_[17] + 2) >> 2;
+          else if (top) T[0] = (3 * P_[0] + P_[1] + 2) >> 2;
+          else if (left) T[0] = (3 * P_[0] + P_[17] + 2) >> 2;
+          else T[0] = P_[0];
+        }
+        if (left) {
+          L[0] = tl ? (P_[0] + 2 * P_[17] + P_[18] + 2) >> 2 : (3 * P_[17] + P_[18] + 2) >> 2;
+#pragma unroll
+          for (int y = 1; y < 7; ++y) L[y] = (P_[16 + y] + 2 * P_[17 + y] + P_[18 + y] + 2) >> 2;
+          L[7] = (P_[23] + 3 * P_[24] + 2) >> 2;
+        }
+#pragma unroll
+        for (int i = 0; i < 17; ++i) t.f8[i] = static_cast<int16_t>(T[i]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t.f8[17 + i] = static_cast<int16_t>(L[i]);
+      }
+      lane_sync();
+      if (s == b8) {
+        const int16_t *T = t.f8, *L = t.f8 + 17;
+        int res[16];
+        if (lb >= 0) idct8_quarter(a.arena, lb, qp, qx, qy, res);
+        else
+#pragma unroll
+          for (int i = 0; i < 16; ++i) res[i] = 0;
+#define PT(x) static_cast<int>(T[1 + (x)])
+#define PL(y) static_cast<int>((y) < 0 ? T[0] : L[(y)])
+        int dc = 128;
+        if (m8 == 2) {
+          int st = 0, sl = 0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            st += PT(i);
+            sl += PL(i);
+          }
+          dc = (top && left) ? (st + sl + 8) >> 4 : (left ? (sl + 4) >> 3 : (top ? (st + 4) >> 3 : 128));
+        }
+#pragma unroll
+        for (int yy = 0; yy < 4; ++yy) {
+          int o[4];
+#pragma unroll
+          for (int xx = 0; xx < 4; ++xx) {
+            const int x = qx * 4 + xx, y = qy * 4 + yy;
+            int v;
+            switch (m8) {
+              case 0: v = PT(x); break;
+              case 1: v = PL(y); break;
+              case 2: v = dc; break;
+              case 3:
+                v = (x == 7 && y == 7) ? (PT(14) + 3 * PT(15) + 2) >> 2 : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
+                break;
+              case 4:
+                if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
+                else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
+                else v = (PT(0) + 2 * PT(-1) + PL(0) + 2) >> 2;
+                break;
+              case 5: {
+                const int z = 2 * x - y;
+                if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+                else v = (PL(y - 2 * x - 1) + 2 * PL(y - 2 * x - 2) + PL(y - 2 * x - 3) + 2) >> 2;
+                break;
+              }
+              case 6: {
+                const int z = 2 * y - x;
+                if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+                else v = (PT(x - 2 * y - 1) + 2 * PT(x - 2 * y - 2) + PT(x - 2 * y - 3) + 2) >> 2;
+                break;
+              }
+              case 7:
+                v = !(y & 1) ? (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1
+                             : (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2;
+                break;
+              default: {
+                const int z = x + 2 * y;
+                if (z < 13 && !(z & 1)) v = (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
+                else if (z < 13) v = (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
+                else if (z == 13) v = (PL(6) + 3 * PL(7) + 2) >> 2;
+                else v = PL(7);
+                break;
+              }
+            }
+            o[xx] = c255(v + res[yy * 4 + xx]);
+          }
+          const uint32_t w4 = pack4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<uint32_t *>(&t.y[1 + by * 4 + yy][4 + bx * 4]) = w4;
+          *reinterpret_cast<uint32_t *>(Y + yrow0 + static_cast<int64_t>(by * 4 + yy) * pitch + bx * 4) = w4;
+        }
+#undef PT
+#undef PL
+      }
+      lane_sync();
+    }
   } else {
     // Intra_4x4: block (bx, by) at step bx + 2 by; its left / top / top-left /
     // top-right blocks (earlier in luma4x4BlkIdx order) are done one or more steps before
@@ -795,11 +975,13 @@ __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
       tt = h.type;
       qpt = tt == kMbPcm ? 0 : h.qp;
     }
+    const bool t8 = (hq.modes & kModeT8) != 0;
 #pragma unroll
     for (int dir = 0; dir < 2; ++dir)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if (e == 0 && !(dir ? ft : fl)) continue;
+        if (t8 && (e & 1)) continue;  // 8x8 transform: no 4-sample internal luma edges (chroma uses e = 0, 2)
         const MbRec *Pm = e ? Q : (dir ? PT : PL);
         const int tp = e ? tq : (dir ? tt : tl);
 #pragma unroll

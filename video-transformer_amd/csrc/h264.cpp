@@ -91,8 +91,7 @@ std::string parse_pps(const uint8_t *nal, size_t n, Pps *p) {
   BitReader br(nal + 1, n - 1);
   p->pps_id = static_cast<int>(br.ue());
   p->sps_id = static_cast<int>(br.ue());
-  p->entropy_coding_mode = static_cast<int>(br.u(1));
-  if (p->entropy_coding_mode) return "CABAC entropy coding is not supported";
+  p->entropy_coding_mode = static_cast<int>(br.u(1));  // CABAC: the general decoder only
   p->bottom_field_pic_order_in_frame_present = static_cast<int>(br.u(1));
   p->num_slice_groups = 1 + static_cast<int>(br.ue());
   if (p->num_slice_groups != 1) return "slice groups (FMO) are not supported";

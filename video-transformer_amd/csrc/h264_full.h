@@ -38,6 +38,8 @@ struct FullParams {
   int32_t cip;          // constrained_intra_pred_flag
   int32_t cqp_off;      // chroma_qp_index_offset (Cb)
   int32_t cqp_off2;     // second_chroma_qp_index_offset (Cr)
+  int32_t cabac;        // entropy_coding_mode_flag (parse_cabac.h)
+  int32_t t8mode;       // transform_8x8_mode_flag
   int32_t _pad;
 };
 
@@ -52,6 +54,7 @@ enum : uint32_t {
 
 // MbRec-parallel intra dependency level of a macroblock that is not intra-predicted
 constexpr uint16_t kNoLevel = 0xffff;
+constexpr uint8_t kModeT8 = 0x10;  // MbRec.modes: transform_size_8x8_flag
 
 enum : uint8_t {
   kMbInter = 0,
@@ -70,12 +73,18 @@ struct alignas(16) MbRec {
   uint8_t type;         // kMb*
   uint8_t qp;           // QPY
   uint8_t cbp;          // coded_block_pattern
-  uint8_t modes;        // bits 0-1 Intra16x16PredMode, bits 2-3 intra_chroma_pred_mode
+  uint8_t modes;        // bits 0-1 Intra16x16PredMode, bits 2-3 intra_chroma_pred_mode,
+                        // bit 4 transform_size_8x8_flag (8x8 blocks: 4 consecutive arena
+                        // blocks = raster 8x8, kBlkLuma0 + 4 b8 + 0..3 all set)
   int8_t ref[4];        // RefPicList0 index per 8x8 (-1: intra)
   int16_t ref_slot[4];  // its ring slot (the picture identity the deblocking bS compares)
   uint8_t i4[8];        // Intra4x4PredMode of raster 4x4 block b: nibble (b & 1) of byte b >> 1
+                        // (Intra_8x8: the 8x8 mode in its four blocks); CABAC inter macroblocks:
+                        // Min(|mvd|, 33) of bottom-row block x, component c at byte 2 x + c
   uint8_t nz[16];       // total_coeff of raster luma 4x4 blocks (16 for I_PCM)
-  uint8_t nzc[8];       // chroma AC total_coeff: Cb raster 0-3, Cr raster 0-3
+  uint8_t nzc[8];       // CAVLC: chroma AC total_coeff, Cb raster 0-3, Cr raster 0-3;
+                        // CABAC: bytes 0-3 the coded_block_flag bits (kBlk* numbering,
+                        // luma 4x4 by raster index: bit 1 + raster)
   int16_t mv[16][2];    // quarter-sample motion of raster 4x4 blocks
 };
 static_assert(sizeof(MbRec) == 128, "MbRec layout");

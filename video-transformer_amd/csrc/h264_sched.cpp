@@ -135,7 +135,7 @@ std::string sched_stream_facts(const std::vector<uint8_t> &sps_nal, const std::v
     if (r.err) return "truncated PPS";
   }
   if (out->seq_scaling) return "SPS scaling matrices";
-  if (out->transform_8x8) return "8x8 transform (transform_8x8_mode_flag)";
+  if (out->transform_8x8 && !pps.entropy_coding_mode) return "8x8 transform with CAVLC (CABAC only)";
   if (pps.redundant_pic_cnt_present) return "redundant pictures";
   return "";
 }
@@ -232,6 +232,10 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
             if (this_mmco.size() > 66) return "too many MMCOs";
           }
         }
+      }
+      if (pps.entropy_coding_mode && s.is_p) {
+        // only the cabac_init_idc 0 context tables are restated (x264 writes 0)
+        if (r.ue() != 0) return "cabac_init_idc 1 or 2 (only the idc 0 context tables are supported)";
       }
       s.qp = pps.pic_init_qp + r.se();
       s.dbk_idc = 0;

@@ -1,0 +1,693 @@
+// parse_cabac.h — CABAC slice_data() parser of the general device decoder
+// (ITU-T H.264 9.3): High-profile I and P slices with 8x8 transforms.  The
+// kernel (h264_parse_full) runs one slice per single-lane wave, so the whole
+// arithmetic decoder is wave-uniform scalar code; the CPU harness compiles the
+// same header.  It produces exactly what the CAVLC parser produces (MbRec,
+// coefficient blocks, intra dependency level) plus, for the reconstruction,
+// transform_size_8x8_flag (MbRec.modes bit 4) and 8x8 coefficient blocks.
+//
+// Context state lives in LDS (FullScratch.cst, one byte per ctxIdx).  The
+// neighbour facts CABAC's context selection needs come through the CAVLC
+// parser's LDS neighbour copies: coded_block_flag bits in the (CAVLC-only)
+// nzc bytes, clamped |mvd| of inter macroblocks' bottom rows in their i4
+// bytes, the previous macroblock's right-column |mvd| in FullScratch.mvdl.
+#pragma once
+#include <cstdint>
+
+#include "h264_cabac_tables.h"
+#include "parse_full.h"
+
+namespace vts {
+namespace full {
+
+#if defined(__HIPCC__)
+#define VTS_CTAB __device__ __constant__ static const
+#else
+#define VTS_CTAB static const
+#endif
+VTS_CTAB int8_t kCabInitI[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_I_DATA;
+VTS_CTAB int8_t kCabInitP[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_P0_DATA;
+VTS_CTAB uint8_t kRangeLps[64][4] = VTS_CABAC_RANGE_LPS_DATA;
+VTS_CTAB uint8_t kTransLps[64] = VTS_CABAC_TRANS_LPS_DATA;
+VTS_CTAB uint8_t kSig8[63] = VTS_SIG8x8_DATA;
+VTS_CTAB uint8_t kLast8[63] = VTS_LAST8x8_DATA;
+VTS_CTAB uint8_t kZz8[64] = VTS_ZZ8_DATA;
+VTS_CTAB uint8_t kCbfOff[5] = {0, 4, 8, 12, 16};
+VTS_CTAB uint8_t kSigOff[5] = {0, 15, 29, 44, 47};
+VTS_CTAB uint8_t kAbsOff[5] = {0, 10, 20, 30, 39};
+VTS_CTAB uint8_t kMvdInc[8] = {3, 4, 5, 6, 6, 6, 6, 6};
+#undef VTS_CTAB
+
+struct CabacParser : Parser {
+  uint32_t range, offset;
+  bool prev_qpd;  // the previous macroblock of the slice has mb_qp_delta != 0
+
+  // ---------------------------------------------- arithmetic decoder (9.3.3.2)
+  VTS_HD VTS_INLINE void cab_start() {  // 9.3.1.2
+    range = 510;
+    offset = br.bits(9);
+  }
+  VTS_HD VTS_INLINE void cab_init(bool is_i, int qp) {  // 9.3.1.1
+    const int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
+    for (int i = 0; i < VTS_CABAC_NCTX; ++i) {
+      const int m = is_i ? kCabInitI[i][0] : kCabInitP[i][0], n = is_i ? kCabInitI[i][1] : kCabInitP[i][1];
+      int pre = ((m * q) >> 4) + n;
+      pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
+      sc->cst[i] = static_cast<uint8_t>(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1);
+    }
+  }
+  VTS_HD VTS_INLINE uint32_t dec(int ctx) {  // DecodeDecision
+    const uint32_t s = sc->cst[ctx], ps = s >> 1, mps = s & 1u;
+    const uint32_t lps = kRangeLps[ps][(range >> 6) & 3u];
+    range -= lps;
+    uint32_t bin;
+    if (offset >= range) {
+      bin = mps ^ 1u;
+      offset -= range;
+      range = lps;
+      sc->cst[ctx] = static_cast<uint8_t>((kTransLps[ps] << 1) | (ps == 0 ? (mps ^ 1u) : mps));
+    } else {
+      bin = mps;
+      sc->cst[ctx] = static_cast<uint8_t>(((ps < 62 ? ps + 1 : 62) << 1) | mps);
+    }
+    if (range < 256) {  // RenormD as one shift
+      const int n = __builtin_clz(range) - 23;
+      range <<= n;
+      offset = (offset << n) | br.bits(n);
+    }
+    return bin;
+  }
+  VTS_HD VTS_INLINE uint32_t bypass() {  // DecodeBypass
+    offset = (offset << 1) | br.bit();
+    if (offset >= range) {
+      offset -= range;
+      return 1;
+    }
+    return 0;
+  }
+  VTS_HD VTS_INLINE uint32_t term() {  // DecodeTerminate: 1 ends parsing, no renormalisation
+    range -= 2;
+    if (offset >= range) return 1;
+    if (range < 256) {
+      range <<= 1;
+      offset = (offset << 1) | br.bit();
+    }
+    return 0;
+  }
+
+  // ------------------------------------------------------ neighbour facts
+  VTS_HD VTS_INLINE uint32_t cbf_of(const MbRec &m) const {
+    return static_cast<uint32_t>(m.nzc[0]) | (static_cast<uint32_t>(m.nzc[1]) << 8) |
+           (static_cast<uint32_t>(m.nzc[2]) << 16) | (static_cast<uint32_t>(m.nzc[3]) << 24);
+  }
+  VTS_HD VTS_INLINE void set_cbf(uint32_t bit) {
+    MbRec &m = cur();
+    m.nzc[bit >> 3] = static_cast<uint8_t>(m.nzc[bit >> 3] | (1u << (bit & 7)));
+  }
+  VTS_HD VTS_INLINE bool avail_not(int n, int type) const { return n != -1 && rec(n).type != type; }
+  // condTermFlagN of coded_block_flag (9.3.3.1.1.9)
+  VTS_HD VTS_INLINE int cbf_cond(int n, bool cur_intra, bool tb, uint32_t bit) const {
+    if (n == -1) return cur_intra ? 1 : 0;
+    const MbRec &m = rec(n);
+    if (m.type == kMbPcm) return 1;
+    if (!tb || m.type == kMbSkip) return 0;
+    return static_cast<int>((cbf_of(m) >> bit) & 1u);
+  }
+  VTS_HD VTS_INLINE int cbf_luma_inc(int addr, int bx, int by, bool intra) const {
+    int inc = 0;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      int xw = 0, yw = 0;
+      const int n = nb_mb(addr, nb ? bx * 4 : bx * 4 - 1, nb ? by * 4 - 1 : by * 4, 16, &xw, &yw);
+      bool tb = false;
+      uint32_t bit = 0;
+      if (n != -1) {
+        tb = (rec(n).cbp >> ((yw / 8) * 2 + xw / 8)) & 1;
+        bit = 1u + static_cast<uint32_t>((yw / 4) * 4 + xw / 4);
+      }
+      inc += cbf_cond(n, intra, tb, bit) << nb;
+    }
+    return inc;
+  }
+  VTS_HD VTS_INLINE int cbf_chroma_inc(int addr, int pl, int blk, bool dc, bool intra) const {
+    int inc = 0;
+    const int x = dc ? 0 : (blk & 1) * 4, y = dc ? 0 : (blk >> 1) * 4;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      int xw = 0, yw = 0;
+      const int n = nb_mb(addr, nb ? x : x - 1, nb ? y - 1 : y, 8, &xw, &yw);
+      bool tb = false;
+      uint32_t bit = 0;
+      if (n != -1) {
+        const int cc = rec(n).cbp >> 4;
+        tb = dc ? cc != 0 : cc == 2;
+        bit = dc ? 17u + static_cast<uint32_t>(pl) : 19u + static_cast<uint32_t>(4 * pl + (yw / 4) * 2 + xw / 4);
+      }
+      inc += cbf_cond(n, intra, tb, bit) << nb;
+    }
+    return inc;
+  }
+  // Min(|mvd|, 33) at luma (xN, yN) of the current macroblock's neighbourhood
+  VTS_HD VTS_INLINE int mvd_at(int addr, int xN, int yN, int comp) const {
+    int xw = 0, yw = 0;
+    const int n = nb_mb(addr, xN, yN, 16, &xw, &yw);
+    if (n == -1) return 0;
+    if (n == -2) return sc->mvdc[(yw / 4) * 4 + xw / 4][comp];
+    const MbRec &m = rec(n);
+    if (m.type != kMbInter) return 0;
+    if (n == cur_addr - 1) return sc->mvdl[yw / 4][comp];
+    return m.i4[(xw / 4) * 2 + comp];  // the row above: bottom-row values
+  }
+  VTS_HD VTS_INLINE int ref_gt0_at(int addr, int xN, int yN) const {
+    int xw = 0, yw = 0;
+    const int n = nb_mb(addr, xN, yN, 16, &xw, &yw);
+    if (n == -1) return 0;
+    const MbRec &m = rec(n);
+    if (m.type != kMbInter) return 0;
+    return m.ref[(yw / 8) * 2 + xw / 8] > 0 ? 1 : 0;
+  }
+  // Intra NxN mode predictor (8.3.1.1 / 8.3.2.1) of the block at (x0, y0)
+  VTS_HD VTS_INLINE int mode_pred(int addr, int x0, int y0, bool is8) const {
+    int xa = 0, ya = 0, xb = 0, yb = 0;
+    const int a = nb_mb(addr, x0 - 1, y0, 16, &xa, &ya), b = nb_mb(addr, x0, y0 - 1, 16, &xb, &yb);
+    if (a == -1 || b == -1) return 2;
+    const MbRec &ma = rec(a), &mb = rec(b);
+    if (cip && (ma.type == kMbInter || ma.type == kMbSkip || mb.type == kMbInter || mb.type == kMbSkip)) return 2;
+    int md[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const MbRec &m = i ? mb : ma;
+      const int xw = i ? xb : xa, yw = i ? yb : ya;
+      if (m.type != kMbI4x4) {
+        md[i] = 2;
+        continue;
+      }
+      int r = (yw / 4) * 4 + xw / 4;
+      if (is8 && !(m.modes & kModeT8)) {  // Intra4x4PredMode[luma8x8BlkIdxN * 4 + (A ? 1 : 2)]
+        const int k = ((yw / 8) * 2 + xw / 8) * 4 + (i ? 2 : 1);
+        r = blk_y(k) * 4 + blk_x(k);
+      }
+      md[i] = (m.i4[r >> 1] >> ((r & 1) * 4)) & 15;
+    }
+    return vts_min(md[0], md[1]);
+  }
+  VTS_HD VTS_INLINE void set_i4(int r, int mode) {
+    MbRec &m = cur();
+    m.i4[r >> 1] = static_cast<uint8_t>((m.i4[r >> 1] & (0xf0 >> ((r & 1) * 4))) | (mode << ((r & 1) * 4)));
+  }
+
+  // ------------------------------------------------------- syntax elements
+  // mb_type of an I macroblock (Table 9-36): I slice prefix at ctxIdx 3 or the
+  // P-slice suffix at 17; 0..25
+  VTS_HD VTS_INLINE int i_type(bool suffix, int inc0) {
+    if (!dec(suffix ? 17 : 3 + inc0)) return 0;
+    if (term()) return 25;
+    const int luma = static_cast<int>(dec(suffix ? 18 : 6));
+    int chroma = static_cast<int>(dec(suffix ? 19 : 7));
+    if (chroma) chroma += static_cast<int>(dec(suffix ? 19 : 8));
+    int pm = static_cast<int>(dec(suffix ? 20 : 9)) << 1;
+    pm |= static_cast<int>(dec(suffix ? 20 : 10));
+    return 1 + pm + 4 * chroma + 12 * luma;
+  }
+  VTS_HD VTS_INLINE int mvd(int base, int sum) {  // U prefix cMax 9 + UEG3 + sign
+    if (!dec(base + (sum < 3 ? 0 : (sum > 32 ? 2 : 1)))) return 0;
+    int v = 1;
+    while (v < 9 && dec(base + kMvdInc[v - 1])) ++v;
+    if (v >= 9) {
+      int k = 3;
+      while (bypass()) {
+        v += 1 << k;
+        if (++k > 24) {
+          err |= DEC_E_SYNTAX;
+          return 0;
+        }
+      }
+      while (k--) v += static_cast<int>(bypass()) << k;
+    }
+    return bypass() ? -v : v;
+  }
+  // residual_block_cabac (7.3.5.3.3): levels in list order into sc->lv;
+  // count of non-zero levels (0: coded_block_flag 0), -1 on error
+  VTS_HD VTS_INLINE int residual(int cat, int cbf_inc, int maxNum) {
+    int16_t *lv = sc->lv;
+    for (int i = 0; i < maxNum; ++i) lv[i] = 0;
+    if (cat != 5 && !dec(85 + kCbfOff[cat] + cbf_inc)) return 0;
+    uint64_t sig = 0;
+    int numc = maxNum;
+    for (int i = 0; i < numc - 1; ++i) {
+      const int inc = cat == 3 ? vts_min(i, 2) : i;
+      if (dec(cat == 5 ? 402 + kSig8[i] : 105 + kSigOff[cat] + inc)) {
+        sig |= 1ull << i;
+        if (dec(cat == 5 ? 417 + kLast8[i] : 166 + kSigOff[cat] + inc)) {
+          numc = i + 1;
+          break;
+        }
+      }
+    }
+    sig |= 1ull << (numc - 1);
+    int eq1 = 0, gt1 = 0, n = 0;
+    const int base = cat == 5 ? 426 : 227 + kAbsOff[cat];
+    for (int i = numc - 1; i >= 0; --i) {
+      if (!((sig >> i) & 1ull)) continue;
+      int v = 0;
+      if (dec(base + (gt1 ? 0 : vts_min(4, 1 + eq1)))) {
+        v = 1;
+        const int inc = 5 + vts_min(4 - (cat == 3 ? 1 : 0), gt1);
+        while (v < 14 && dec(base + inc)) ++v;
+        if (v >= 14) {  // UEG0 suffix
+          int k = 0;
+          while (bypass()) {
+            v += 1 << k;
+            if (++k > 24) return -1;
+          }
+          while (k--) v += static_cast<int>(bypass()) << k;
+        }
+      }
+      int lvl = v + 1;
+      if (bypass()) lvl = -lvl;
+      if (lvl > 32767 || lvl < -32768) return -1;
+      lv[i] = static_cast<int16_t>(lvl);
+      if (v == 0) ++eq1;
+      else ++gt1;
+      ++n;
+    }
+    return n;
+  }
+
+  // ------------------------------------------------------ macroblock_layer
+  // (begin_mb done by the caller); returns false to stop the slice
+  VTS_HD VTS_INLINE bool mb_cabac(int addr, int *qp) {
+    MbRec &m = cur();
+    int xw, yw;
+    const int A = nb_mb(addr, -1, 0, 16, &xw, &yw), B = nb_mb(addr, 0, -1, 16, &xw, &yw);
+    int itype, mb_type = 0;
+    if (s->is_p) {
+      if (dec(14)) {
+        itype = i_type(true, 0);
+      } else {
+        itype = -1;
+        if (!dec(15)) mb_type = dec(16) ? 3 : 0;
+        else mb_type = dec(17) ? 1 : 2;
+      }
+    } else {
+      itype = i_type(false, (avail_not(A, kMbI4x4) ? 1 : 0) + (avail_not(B, kMbI4x4) ? 1 : 0));
+    }
+    for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
+    if (itype == 25) {  // I_PCM: alignment, 384 samples through the RBSP reader, engine restart
+      m.type = kMbPcm;
+      m.qp = static_cast<uint8_t>(*qp);
+      br.align();
+      for (int j = 0; j < 16; ++j) m.nz[j] = 16;
+      for (int k = 0; k < 12; ++k) {
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t lo = br.bits(8), hi = br.bits(8);
+          sc->blk[i] = static_cast<int16_t>(lo | (hi << 8));
+        }
+        if (!store_block(k)) {
+          err |= DEC_E_SYNTAX;
+          return false;
+        }
+      }
+      m.blocks = 0;
+      prev_qpd = false;
+      cab_start();
+      return !br.err;
+    }
+    int cbp = 0;
+    bool small = false;
+    if (itype == 0) {  // I_NxN
+      m.type = kMbI4x4;
+      bool t8 = false;
+      if (P_t8mode) {
+        const int inc = (A != -1 && (rec(A).modes & kModeT8) ? 1 : 0) + (B != -1 && (rec(B).modes & kModeT8) ? 1 : 0);
+        t8 = dec(399 + inc) != 0;
+      }
+      const int nb = t8 ? 4 : 16;
+      if (t8) m.modes = kModeT8;
+      uint8_t *pflag = sc->prev, *rem = sc->rem;
+      for (int i = 0; i < nb; ++i) {
+        pflag[i] = static_cast<uint8_t>(dec(68));
+        if (!pflag[i]) {
+          uint32_t r = dec(69);
+          r |= dec(69) << 1;
+          r |= dec(69) << 2;
+          rem[i] = static_cast<uint8_t>(r);
+        }
+      }
+      for (int i = 0; i < nb; ++i) {
+        const int x0 = t8 ? (i & 1) * 8 : blk_x(i) * 4, y0 = t8 ? (i >> 1) * 8 : blk_y(i) * 4;
+        const int pm = mode_pred(addr, x0, y0, t8);
+        const int mode = pflag[i] ? pm : (rem[i] < pm ? rem[i] : rem[i] + 1);
+        const int r = (y0 / 4) * 4 + x0 / 4;
+        set_i4(r, mode);
+        if (t8) {
+          set_i4(r + 1, mode);
+          set_i4(r + 4, mode);
+          set_i4(r + 5, mode);
+        }
+      }
+    } else if (itype > 0) {  // I_16x16
+      m.type = kMbI16;
+      cbp = ((((itype - 1) / 4) % 3) << 4) | (itype >= 13 ? 15 : 0);
+      m.modes = static_cast<uint8_t>((itype - 1) % 4);
+    } else {  // inter (Table 7-13)
+      m.type = kMbInter;
+      const int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
+      int8_t *sub = sc->sub, *refs = sc->refs;
+      for (int k = 0; k < 4; ++k) sub[k] = refs[k] = 0;
+      if (mb_type == 3)
+        for (int k = 0; k < 4; ++k) {
+          int v;
+          if (dec(21)) v = 0;
+          else if (!dec(22)) v = 1;
+          else v = dec(23) ? 2 : 3;
+          sub[k] = static_cast<int8_t>(v);
+          if (v) small = true;
+        }
+      const int nref = s->num_ref;
+      for (int k = 0; k < nparts; ++k) {
+        const int x0 = (mb_type == 2 || mb_type == 3) ? 8 * (k & 1) : 0;
+        const int y0 = mb_type == 1 ? 8 * k : (mb_type == 3 ? 8 * (k >> 1) : 0);
+        int v = 0;
+        if (nref > 1 && dec(54 + ref_gt0_at(addr, x0 - 1, y0) + 2 * ref_gt0_at(addr, x0, y0 - 1))) {
+          v = 1;
+          if (dec(58)) {
+            v = 2;
+            while (dec(59))
+              if (++v > 32) break;
+          }
+        }
+        if (v >= nref || s->ref_slot[v & 31] < 0) {
+          err |= DEC_E_NO_REF;
+          return false;
+        }
+        refs[k] = static_cast<int8_t>(v);
+        // the partition's 8x8 quarters carry the index for later contexts
+        const int pw = (mb_type == 0 || mb_type == 1) ? 2 : 1, ph = (mb_type == 0 || mb_type == 2) ? 2 : 1;
+        for (int qy = 0; qy < ph; ++qy)
+          for (int qx = 0; qx < pw; ++qx) m.ref[(y0 / 8 + qy) * 2 + x0 / 8 + qx] = static_cast<int8_t>(v);
+      }
+      uint32_t done = 0;
+      for (int k = 0; k < nparts; ++k) {
+        int nsub = 1, pw, ph, x0, y0;
+        if (mb_type == 0) { pw = ph = 16; x0 = y0 = 0; }
+        else if (mb_type == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * k; }
+        else if (mb_type == 2) { pw = 8; ph = 16; x0 = 8 * k; y0 = 0; }
+        else {
+          x0 = 8 * (k & 1);
+          y0 = 8 * (k >> 1);
+          nsub = sub[k] == 0 ? 1 : (sub[k] == 3 ? 4 : 2);
+          pw = (sub[k] == 0 || sub[k] == 1) ? 8 : 4;
+          ph = (sub[k] == 0 || sub[k] == 2) ? 8 : 4;
+        }
+        for (int q = 0; q < nsub; ++q) {
+          int sx = x0, sy = y0;
+          if (mb_type == 3) {
+            if (sub[k] == 1) sy += 4 * q;
+            else if (sub[k] == 2) sx += 4 * q;
+            else if (sub[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+          }
+          const int dx = mvd(40, mvd_at(addr, sx - 1, sy, 0) + mvd_at(addr, sx, sy - 1, 0));
+          const int dy = mvd(47, mvd_at(addr, sx - 1, sy, 1) + mvd_at(addr, sx, sy - 1, 1));
+          int px, py;
+          mv_pred(addr, sx, sy, pw, ph, refs[k], done, &px, &py);
+          const int vx = px + dx, vy = py + dy;
+          if (vx < -32768 || vx > 32767 || vy < -32768 || vy > 32767) {
+            err |= DEC_E_SYNTAX;
+            return false;
+          }
+          const uint8_t ax = static_cast<uint8_t>(vts_min(dx < 0 ? -dx : dx, 33));
+          const uint8_t ay = static_cast<uint8_t>(vts_min(dy < 0 ? -dy : dy, 33));
+          for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
+            for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
+              set_motion(yy * 4 + xx, refs[k], vx, vy);
+              sc->mvdc[yy * 4 + xx][0] = ax;
+              sc->mvdc[yy * 4 + xx][1] = ay;
+              done |= 1u << (yy * 4 + xx);
+            }
+        }
+      }
+    }
+    if (m.type == kMbI4x4 || m.type == kMbI16) {  // intra_chroma_pred_mode, TU cMax 3
+      int inc = 0;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int n = nb ? B : A;
+        if (n == -1) continue;
+        const MbRec &r = rec(n);
+        inc += ((r.type == kMbI4x4 || r.type == kMbI16) && ((r.modes >> 2) & 3)) ? 1 : 0;
+      }
+      int cm = 0;
+      if (dec(64 + inc)) {
+        cm = 1;
+        if (dec(67)) {
+          cm = 2;
+          if (dec(67)) cm = 3;
+        }
+      }
+      m.modes = static_cast<uint8_t>(m.modes | (cm << 2));
+    }
+    if (m.type != kMbI16) {  // coded_block_pattern (9.3.3.1.1.4)
+      for (int b8 = 0; b8 < 4; ++b8) {
+        const int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
+        int cond[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          int x2 = 0, y2 = 0;
+          const int n = nb_mb(addr, nb ? bx : bx - 1, nb ? by - 1 : by, 16, &x2, &y2);
+          const int b8n = (y2 / 8) * 2 + x2 / 8;
+          if (n == -1) cond[nb] = 0;
+          else if (n == -2) cond[nb] = ((cbp >> b8n) & 1) ? 0 : 1;
+          else {
+            const MbRec &r = rec(n);
+            cond[nb] = r.type == kMbPcm ? 0 : (r.type == kMbSkip ? 1 : (((r.cbp >> b8n) & 1) ? 0 : 1));
+          }
+        }
+        cbp |= static_cast<int>(dec(73 + cond[0] + 2 * cond[1])) << b8;
+      }
+      int ca[2] = {0, 0}, c2[2] = {0, 0};
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int n = nb ? B : A;
+        if (n == -1) continue;
+        const MbRec &r = rec(n);
+        const int cc = r.type == kMbPcm ? 2 : (r.type == kMbSkip ? 0 : r.cbp >> 4);
+        ca[nb] = cc != 0;
+        c2[nb] = cc == 2;
+      }
+      if (dec(77 + ca[0] + 2 * ca[1])) cbp |= (1 + static_cast<int>(dec(81 + c2[0] + 2 * c2[1]))) << 4;
+    }
+    m.cbp = static_cast<uint8_t>(cbp);
+    if (m.type == kMbInter && (cbp & 15) && P_t8mode && !small) {
+      const int inc = (A != -1 && (rec(A).modes & kModeT8) ? 1 : 0) + (B != -1 && (rec(B).modes & kModeT8) ? 1 : 0);
+      if (dec(399 + inc)) m.modes = static_cast<uint8_t>(m.modes | kModeT8);
+    }
+    bool qpd = false;
+    if (cbp || m.type == kMbI16) {  // mb_qp_delta: U of the se() mapping
+      int k = 0;
+      if (dec(60 + (prev_qpd ? 1 : 0))) {
+        k = 1;
+        if (dec(62)) {
+          k = 2;
+          while (dec(63))
+            if (++k > 104) {
+              err |= DEC_E_SYNTAX;
+              return false;
+            }
+        }
+      }
+      const int dq = (k & 1) ? (k + 1) / 2 : -(k / 2);
+      if (dq < -26 || dq > 25) {
+        err |= DEC_E_SYNTAX;
+        return false;
+      }
+      *qp = (*qp + dq + 52) % 52;
+      qpd = dq != 0;
+    }
+    prev_qpd = qpd;
+    m.qp = static_cast<uint8_t>(*qp);
+    // ---- residual (7.3.5.3), blocks in bitstream order
+    const bool intra = m.type == kMbI4x4 || m.type == kMbI16;
+    const bool t8 = (m.modes & kModeT8) != 0;
+    if (m.type == kMbI16) {
+      int inc = 0;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int n = nb ? B : A;
+        inc += cbf_cond(n, true, n != -1 && rec(n).type == kMbI16, 0) << nb;
+      }
+      const int nc = residual(0, inc, 16);
+      if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
+      if (nc) {
+        for (int i = 0; i < 16; ++i) sc->blk[kZz[i]] = sc->lv[i];
+        set_cbf(0);
+        if (!store_block(kBlkI16Dc)) { err |= DEC_E_SYNTAX; return false; }
+      }
+    }
+    for (int b8 = 0; b8 < 4; ++b8) {
+      if (!((cbp >> b8) & 1)) continue;
+      const int r0 = (b8 >> 1) * 8 + (b8 & 1) * 2;
+      if (t8) {
+        const int nc = residual(5, 0, 64);
+        if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
+        const int rs[4] = {r0, r0 + 1, r0 + 4, r0 + 5};
+        for (int j = 0; j < 4; ++j) {
+          m.nz[rs[j]] = static_cast<uint8_t>(nc > 255 ? 255 : nc);
+          set_cbf(1u + static_cast<uint32_t>(rs[j]));
+        }
+        if (nc) {  // raster 8x8 over the quarter's 4 blocks: block j = rows 2j, 2j + 1
+          for (int j = 0; j < 4; ++j) {
+            for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
+            for (int i = 0; i < 64; ++i) {
+              const int pos = kZz8[i];
+              if ((pos >> 4) == j) sc->blk[pos & 15] = sc->lv[i];
+            }
+            if (!store_block(kBlkLuma0 + 4 * b8 + j)) { err |= DEC_E_SYNTAX; return false; }
+          }
+        }
+        continue;
+      }
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const int k = b8 * 4 + i4, bx = blk_x(k), by = blk_y(k), r = by * 4 + bx;
+        const int inc = cbf_luma_inc(addr, bx, by, intra);
+        const int nc = m.type == kMbI16 ? residual(1, inc, 15) : residual(2, inc, 16);
+        if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
+        m.nz[r] = static_cast<uint8_t>(nc);
+        if (nc) {
+          for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
+          if (m.type == kMbI16)
+            for (int i = 0; i < 15; ++i) sc->blk[kZz[i + 1]] = sc->lv[i];
+          else
+            for (int i = 0; i < 16; ++i) sc->blk[kZz[i]] = sc->lv[i];
+          set_cbf(1u + static_cast<uint32_t>(r));
+          if (!store_block(kBlkLuma0 + k)) { err |= DEC_E_SYNTAX; return false; }
+        }
+      }
+    }
+    if (cbp >> 4) {
+      for (int pl = 0; pl < 2; ++pl) {
+        const int nc = residual(3, cbf_chroma_inc(addr, pl, 0, true, intra), 4);
+        if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
+        if (nc) {
+          for (int i = 0; i < 16; ++i) sc->blk[i] = i < 4 ? sc->lv[i] : 0;
+          set_cbf(17u + static_cast<uint32_t>(pl));
+          if (!store_block(kBlkChromaDc0 + pl)) { err |= DEC_E_SYNTAX; return false; }
+        }
+      }
+    }
+    if ((cbp >> 4) == 2) {
+      for (int pl = 0; pl < 2; ++pl)
+        for (int b = 0; b < 4; ++b) {
+          const int nc = residual(4, cbf_chroma_inc(addr, pl, b, false, intra), 15);
+          if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
+          if (nc) {
+            for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
+            for (int i = 0; i < 15; ++i) sc->blk[kZz[i + 1]] = sc->lv[i];
+            set_cbf(19u + static_cast<uint32_t>(4 * pl + b));
+            if (!store_block(kBlkChromaAc0 + 4 * pl + b)) { err |= DEC_E_SYNTAX; return false; }
+          }
+        }
+    }
+    if (br.err || br.overrun()) {
+      err |= DEC_E_SYNTAX;
+      return false;
+    }
+    return true;
+  }
+
+  // after a macroblock: its clamped |mvd| for the neighbours below / right
+  VTS_HD VTS_INLINE void finish_mvd() {
+    MbRec &m = cur();
+    if (m.type == kMbInter)
+      for (int x = 0; x < 4; ++x) {
+        m.i4[2 * x] = sc->mvdc[12 + x][0];
+        m.i4[2 * x + 1] = sc->mvdc[12 + x][1];
+      }
+    for (int y = 0; y < 4; ++y) {
+      sc->mvdl[y][0] = sc->mvdc[y * 4 + 3][0];
+      sc->mvdl[y][1] = sc->mvdc[y * 4 + 3][1];
+    }
+  }
+
+  bool P_t8mode;
+};
+
+// Parse CABAC slice `s` (window slice index si).  Returns DEC_E_* bits.
+VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams P,
+                                         MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena, uint32_t epoch,
+                                         FullScratch *sc) {
+  const uint8_t *nal = es + s.nal_offset;
+  CabacParser p;
+  p.s = &s;
+  p.cip = P.cip;
+  p.P_t8mode = P.t8mode != 0;
+  p.recs = frame_recs;
+  p.ilvl = frame_ilvl;
+  p.arena = arena;
+  p.sc = sc;
+  p.used = 0;
+  p.slice_index = si;
+  p.epoch = epoch;
+  p.mbw = P.mb_width;
+  p.first_mb = s.first_mb;
+  p.err = 0;
+  p.cur_addr = -2;
+  p.cs = 0;
+  p.tslots = 0;
+  p.lvl_prev = kNoLevel;
+  p.pf_col = -1;
+  p.todo = 0;
+  p.cur_i16 = false;
+  p.prev_qpd = false;
+  const int nmb = P.mb_width * P.mb_height;
+  // the RBSP stop bit, past any trailing cabac_zero_words (00 00 03 in the EBSP)
+  int32_t last = s.nal_size - 1;
+  while (last > 0 && (nal[last] == 0 || (nal[last] == 3 && last >= 2 && nal[last - 1] == 0 && nal[last - 2] == 0)))
+    --last;
+  if (last <= 0) return DEC_E_SYNTAX;
+  const int tz = __builtin_ctz(static_cast<uint32_t>(nal[last]));
+  const int64_t stop_bit = int64_t(last - 1) * 8 + (7 - tz);
+  p.br.init(nal + 1, s.nal_offset + 1, s.nal_size - 1, sc->cache);
+  p.br.reset_at(s.data_byte, s.data_bit & ~7);
+  p.br.ensure(8);
+  p.br.skip(s.data_bit & 7);
+  // cabac_alignment_one_bit
+  while (p.br.consumed() & 7)
+    if (!p.br.bit()) return DEC_E_SYNTAX;
+  p.cab_init(!s.is_p, s.qp);
+  p.cab_start();
+  for (int i = 0; i < 4; ++i) sc->mvdl[i][0] = sc->mvdl[i][1] = 0;
+  int addr = s.first_mb, qp = s.qp;
+  for (;;) {
+    if (addr >= nmb) {
+      p.err |= DEC_E_SYNTAX;
+      break;
+    }
+    p.begin_mb(addr);
+    bool ok = true;
+    if (s.is_p) {
+      int xw, yw;
+      const int A = p.nb_mb(addr, -1, 0, 16, &xw, &yw), B = p.nb_mb(addr, 0, -1, 16, &xw, &yw);
+      if (p.dec(11 + (p.avail_not(A, kMbSkip) ? 1 : 0) + (p.avail_not(B, kMbSkip) ? 1 : 0))) {
+        p.skip_body(addr, qp);
+        for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
+        p.prev_qpd = false;
+      } else {
+        ok = p.mb_cabac(addr, &qp);
+      }
+    } else {
+      ok = p.mb_cabac(addr, &qp);
+    }
+    if (!ok || p.err) break;
+    p.finish_mvd();
+    p.end_mb(addr);
+    ++addr;
+    if (p.term()) break;  // end_of_slice_flag
+  }
+  // the arithmetic decoder has read through the stop bit
+  if (!p.err && (p.br.err || p.br.overrun() || p.br.consumed() != stop_bit - 8ll * p.br.epb + 1)) p.err |= DEC_E_SYNTAX;
+  return p.err;
+}
+
+}  // namespace full
+}  // namespace vts

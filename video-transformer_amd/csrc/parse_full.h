@@ -15,6 +15,7 @@
 #include "h264.h"
 #include "h264_full.h"
 #include "h264_tables.h"
+#include "h264_cabac_tables.h"
 #include "parse_slice.h"  // WinBits, VTS_HD, VTS_INLINE
 
 #ifndef VTS_PARSE_TRACE
@@ -132,6 +133,11 @@ struct FullScratch {
   uint32_t cache[kCacheWords];
   uint8_t prev[16], rem[16];  // Intra4x4 prev_intra4x4_pred_mode_flag / rem_intra4x4_pred_mode
   int8_t sub[4], refs[4];     // sub_mb_type / ref_idx_l0 of the partitions
+  // CABAC (parse_cabac.h)
+  uint8_t cst[VTS_CABAC_NCTX];  // context states: pStateIdx << 1 | valMPS
+  int16_t lv[64];               // levels of the block being decoded, coefficient-list order
+  uint8_t mvdc[16][2];          // Min(|mvd|, 33) of the current macroblock's 4x4 blocks
+  uint8_t mvdl[4][2];           // ... of the previous macroblock's right column
 };
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));  // SROA-friendly (uint4 copies are memmoves)
@@ -495,6 +501,10 @@ struct Parser {
 
   VTS_HD VTS_INLINE void skip_mb(int addr, int qp) {
     begin_mb(addr);
+    skip_body(addr, qp);
+  }
+  // P_Skip (8.4.1.1) of the macroblock begin_mb has started
+  VTS_HD VTS_INLINE void skip_body(int addr, int qp) {
     MbRec &m = cur();
     m.type = kMbSkip;
     m.qp = static_cast<uint8_t>(qp);
@@ -722,7 +732,7 @@ struct Parser {
 
 // Parse slice `s` (window slice index si) into recs (the frame's records) and
 // the arena.  Returns DEC_E_* bits.
-VTS_HD inline uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams &P,
+VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams P,
                                         MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena, uint32_t epoch,
                                         FullScratch *sc) {
   const uint8_t *nal = es + s.nal_offset;

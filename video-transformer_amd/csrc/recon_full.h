@@ -13,6 +13,7 @@
 #include "h264.h"
 #include "h264_full.h"
 #include "h264_tables.h"
+#include "h264_cabac_tables.h"
 #include "parse_full.h"
 
 namespace vts {
@@ -87,6 +88,37 @@ VTS_HD inline void scale_idct4(const int *c, int qp, bool dc_done, int *r) {
   }
 }
 
+// 8.5.13: scaling (flat) + 8x8 inverse transform; c raster 8x8; r receives the residual
+#if defined(__HIPCC__)
+__device__ __constant__ static const uint8_t kNorm8[6][6] = VTS_NORM8_DATA;
+#else
+static const uint8_t kNorm8[6][6] = VTS_NORM8_DATA;
+#endif
+VTS_HD inline void scale_idct8(const int *c, int qp, int *r) {
+  int d[64], g[64];
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) {
+      const int ls = 16 * kNorm8[qp % 6][vts_norm8_class(i, j)], k = i * 8 + j;
+      d[k] = qp >= 36 ? (c[k] * ls) << (qp / 6 - 6) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    }
+  for (int pass = 0; pass < 2; ++pass)
+    for (int u = 0; u < 8; ++u) {
+      int v[8], o[8];
+      for (int k = 0; k < 8; ++k) v[k] = pass == 0 ? d[u * 8 + k] : g[k * 8 + u];
+      const int a0 = v[0] + v[4], a4 = v[0] - v[4], a2 = (v[2] >> 1) - v[6], a6 = v[2] + (v[6] >> 1);
+      const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+      const int a1 = -v[3] + v[5] - v[7] - (v[7] >> 1), a3 = v[1] + v[7] - v[3] - (v[3] >> 1);
+      const int a5 = -v[1] + v[7] + v[5] + (v[5] >> 1), a7 = v[3] + v[5] + v[1] + (v[1] >> 1);
+      const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+      o[0] = b0 + b7; o[1] = b2 + b5; o[2] = b4 + b3; o[3] = b6 + b1;
+      o[4] = b6 - b1; o[5] = b4 - b3; o[6] = b2 - b5; o[7] = b0 - b7;
+      for (int k = 0; k < 8; ++k) {
+        if (pass == 0) g[u * 8 + k] = o[k];
+        else r[k * 8 + u] = (o[k] + 32) >> 6;
+      }
+    }
+}
+
 VTS_HD VTS_INLINE int tap6(int a, int b, int c, int d, int e, int f) {
   return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
 }
@@ -109,6 +141,10 @@ struct MbRecon {
   VTS_HD VTS_INLINE int64_t block_of(uint32_t bit) const {
     if (!((m.blocks >> bit) & 1u)) return -1;
     return static_cast<int64_t>(m.coef) + __builtin_popcount(m.blocks & ((1u << bit) - 1u));
+  }
+  VTS_HD VTS_INLINE void load_block8(int b8, int *cf) const {  // 4 consecutive blocks = raster 8x8
+    const int64_t b = block_of(kBlkLuma0 + 4 * b8);
+    for (int i = 0; i < 64; ++i) cf[i] = b < 0 ? 0 : c.arena[16 * b + i];
   }
   VTS_HD VTS_INLINE void load_block(uint32_t bit, int *cf) const {
     const int64_t b = block_of(bit);
@@ -291,6 +327,109 @@ struct MbRecon {
 #undef PL
   }
 
+  // ---- Intra_8x8 (8.3.2) of raster 8x8 block b8, reference samples filtered
+  VTS_HD void intra8x8(int b8, int mode, uint32_t done) {
+    const int xo = (b8 & 1) * 8, yo = (b8 >> 1) * 8, x0 = mx * 16 + xo, y0 = my * 16 + yo;
+    auto avail = [&](int xN, int yN) -> bool {  // MB-relative luma location
+      const int dx = xN < 0 ? -1 : (xN > 15 ? 1 : 0), dy = yN < 0 ? -1 : 0;
+      if (yN > 15 || (xN > 15 && yN >= 0)) return false;
+      if (dx == 0 && dy == 0) return (done >> ((yN / 4) * 4 + xN / 4)) & 1u;
+      return intra_nb(nb_addr(dx, dy));
+    };
+    int P_[25];  // 0 = p[-1,-1], 1 + x = p[x,-1] (x 0..15), 17 + y = p[-1,y]
+    const bool tl = avail(xo - 1, yo - 1), top = avail(xo, yo - 1), left = avail(xo - 1, yo);
+    bool tr = avail(xo + 8, yo - 1);
+    P_[0] = tl ? ly(x0 - 1, y0 - 1) : 0;
+    for (int x = 0; x < 16; ++x) P_[1 + x] = (x < 8 ? top : tr) ? ly(x0 + x, y0 - 1) : 0;
+    if (!tr && top)
+      for (int x = 8; x < 16; ++x) P_[1 + x] = P_[8];
+    for (int y = 0; y < 8; ++y) P_[17 + y] = left ? ly(x0 - 1, y0 + y) : 0;
+    int T[17] = {0}, L[8] = {0};
+    if (top) {
+      T[1] = tl ? (P_[0] + 2 * P_[1] + P_[2] + 2) >> 2 : (3 * P_[1] + P_[2] + 2) >> 2;
+      for (int x = 1; x < 15; ++x) T[1 + x] = (P_[x] + 2 * P_[1 + x] + P_[2 + x] + 2) >> 2;
+      T[16] = (P_[15] + 3 * P_[16] + 2) >> 2;
+    }
+    if (tl) {
+      if (top && left) T[0] = (P_[1] + 2 * P_[0] + P_[17] + 2) >> 2;
+      else if (top) T[0] = (3 * P_[0] + P_[1] + 2) >> 2;
+      else if (left) T[0] = (3 * P_[0] + P_[17] + 2) >> 2;
+      else T[0] = P_[0];
+    }
+    if (left) {
+      L[0] = tl ? (P_[0] + 2 * P_[17] + P_[18] + 2) >> 2 : (3 * P_[17] + P_[18] + 2) >> 2;
+      for (int y = 1; y < 7; ++y) L[y] = (P_[16 + y] + 2 * P_[17 + y] + P_[18 + y] + 2) >> 2;
+      L[7] = (P_[23] + 3 * P_[24] + 2) >> 2;
+    }
+#define PT(x) T[1 + (x)]
+#define PL(y) ((y) < 0 ? T[0] : L[(y)])
+    for (int y = 0; y < 8; ++y)
+      for (int x = 0; x < 8; ++x) {
+        int v = 128;
+        switch (mode) {
+          case 0: v = PT(x); break;
+          case 1: v = PL(y); break;
+          case 2: {
+            int st = 0, sl = 0;
+            for (int i = 0; i < 8; ++i) {
+              st += PT(i);
+              sl += L[i];
+            }
+            if (top && left) v = (st + sl + 8) >> 4;
+            else if (left) v = (sl + 4) >> 3;
+            else if (top) v = (st + 4) >> 3;
+            break;
+          }
+          case 3:
+            v = (x == 7 && y == 7) ? (PT(14) + 3 * PT(15) + 2) >> 2 : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
+            break;
+          case 4:
+            if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
+            else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
+            else v = (PT(0) + 2 * PT(-1) + PL(0) + 2) >> 2;
+            break;
+          case 5: {
+            const int z = 2 * x - y;
+            if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
+            else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
+            else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+            else v = (PL(y - 2 * x - 1) + 2 * PL(y - 2 * x - 2) + PL(y - 2 * x - 3) + 2) >> 2;
+            break;
+          }
+          case 6: {
+            const int z = 2 * y - x;
+            if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
+            else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
+            else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
+            else v = (PT(x - 2 * y - 1) + 2 * PT(x - 2 * y - 2) + PT(x - 2 * y - 3) + 2) >> 2;
+            break;
+          }
+          case 7:
+            v = !(y & 1) ? (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1
+                         : (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2;
+            break;
+          default: {
+            const int z = x + 2 * y;
+            if (z < 13 && !(z & 1)) v = (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
+            else if (z < 13) v = (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
+            else if (z == 13) v = (PL(6) + 3 * PL(7) + 2) >> 2;
+            else v = PL(7);
+            break;
+          }
+        }
+        pred_y[(yo + y) * 16 + xo + x] = static_cast<uint8_t>(v);
+      }
+#undef PT
+#undef PL
+  }
+  VTS_HD void put_luma8(int b8, const int *res) {
+    const int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
+    uint8_t *d = Y + static_cast<int64_t>(my * 16 + by) * c.pitch + mx * 16 + bx;
+    for (int y = 0; y < 8; ++y)
+      for (int x = 0; x < 8; ++x)
+        d[static_cast<int64_t>(y) * c.pitch + x] = static_cast<uint8_t>(clip1(pred_y[(by + y) * 16 + bx + x] + res[y * 8 + x]));
+  }
+
   // ---- Intra_16x16 (8.3.3) and chroma (8.3.4) predictions
   VTS_HD void intra16(int mode) {
     const bool la = intra_nb(nb_addr(-1, 0)), ta = intra_nb(nb_addr(0, -1)), ca = intra_nb(nb_addr(-1, -1));
@@ -449,9 +588,29 @@ struct MbRecon {
         }
         inter_block(b);
       }
-      for (int b = 0; b < 16; ++b) {
-        luma_residual_block(b, qp, false, dummy_dc, res);
-        put_luma(b, res);
+      if (m.modes & kModeT8) {
+        for (int b8 = 0; b8 < 4; ++b8) {
+          int cf[64], r8[64];
+          load_block8(b8, cf);
+          scale_idct8(cf, qp, r8);
+          put_luma8(b8, r8);
+        }
+      } else {
+        for (int b = 0; b < 16; ++b) {
+          luma_residual_block(b, qp, false, dummy_dc, res);
+          put_luma(b, res);
+        }
+      }
+    } else if (m.type == kMbI4x4 && (m.modes & kModeT8)) {
+      uint32_t done = 0;
+      for (int b8 = 0; b8 < 4; ++b8) {
+        const int r = (b8 >> 1) * 8 + (b8 & 1) * 2;
+        intra8x8(b8, (m.i4[r >> 1] >> ((r & 1) * 4)) & 15, done);
+        int cf[64], r8[64];
+        load_block8(b8, cf);
+        scale_idct8(cf, qp, r8);
+        put_luma8(b8, r8);
+        done |= (1u << r) | (1u << (r + 1)) | (1u << (r + 4)) | (1u << (r + 5));
       }
     } else if (m.type == kMbI4x4) {
       uint32_t done = 0;
@@ -563,6 +722,7 @@ VTS_HD inline void deblock_mb(const ReconCtx &c, int slot, int a) {
   }
   uint8_t *Y = c.surf + static_cast<int64_t>(slot) * c.frame_stride;
   uint8_t *UV = Y + c.uv_off;
+  const bool t8 = (q.modes & kModeT8) != 0;
   for (int dir = 0; dir < 2; ++dir)
     for (int e = 0; e < 4; ++e) {
       if (e == 0 && !(dir ? top : left)) continue;
@@ -572,7 +732,7 @@ VTS_HD inline void deblock_mb(const ReconCtx &c, int slot, int a) {
         const int qpav = (qpp + qpq + 1) >> 1;
         const int iA = clip3(0, 51, qpav + sd.dbk_a), iB = clip3(0, 51, qpav + sd.dbk_b);
         const int alpha = kAl[iA], beta = kBe[iB];
-        if (alpha && beta)
+        if (alpha && beta && !(t8 && (e & 1)))  // 8x8 transform: no 4-sample internal luma edges
           for (int k = 0; k < 16; ++k) {
             const int xq = dir ? k : 4 * e, yq = dir ? 4 * e : k;
             const int xp = dir ? xq : (xq + 15) & 15, yp = dir ? (yq + 15) & 15 : yq;

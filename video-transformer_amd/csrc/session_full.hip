@@ -35,6 +35,7 @@ constexpr int64_t kMinRingBytes = 1ll << 30;
 
 bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
                    const std::vector<uint32_t> &sizes, int nal_length_size) {
+  if (c->pps.entropy_coding_mode) return true;  // CABAC
   if (c->sps.max_num_ref_frames > 1 || c->pps.num_ref_idx_l0_default_active > 1) return true;
   if (!c->pps.deblocking_filter_control_present) return true;  // deblocking on, offsets 0
   // the first pictures' slice headers: an active deblocking filter or several references
@@ -68,6 +69,8 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   c->fprm.cip = c->pps.constrained_intra_pred;
   c->fprm.cqp_off = c->pps.chroma_qp_index_offset;
   c->fprm.cqp_off2 = facts.cqp_off2;
+  c->fprm.cabac = c->pps.entropy_coding_mode;
+  c->fprm.t8mode = facts.transform_8x8;
   const int64_t n = c->n_frames;
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
 
@@ -94,7 +97,9 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   std::vector<int64_t> cap(slices.size());
   int64_t cap_total = 0;
   for (size_t i = 0; i < slices.size(); ++i) {
-    cap[i] = std::min<int64_t>(27ll * slices[i].n_mbs, 3ll * slices[i].nal_size + 27);
+    // CAVLC stores a block for >= 3 bits; CABAC can code one in less, so it gets the per-macroblock bound
+    cap[i] = c->pps.entropy_coding_mode ? 27ll * slices[i].n_mbs
+                                        : std::min<int64_t>(27ll * slices[i].n_mbs, 3ll * slices[i].nal_size + 27);
     cap_total += cap[i];
   }
   // windows
