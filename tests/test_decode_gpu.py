@@ -117,15 +117,23 @@ def test_boundary_frames_for_planned_segments(tmp_path):
 
 
 def test_emulation_prevention_inside_pcm_fails_loudly(tmp_path):
-    """Outside the decoder subset: an EPB inside I_PCM samples.  The device
-    path must refuse with the reason, never return wrong pixels."""
+    """Outside the subset kernels: an EPB inside I_PCM samples.  The subset-only
+    decoder must refuse with the reason, never return wrong pixels; the default
+    (auto) decoder hands the stream to the general decoder, which reads the
+    samples through the RBSP and equals the general oracle."""
     _require_gpu()
     path = tmp_path / "z.mp4"
     scene.synth_write(path, width=160, height=96, n_frames=30, gop_max_s=0.5,
                       pcm_zero_runs=True)
-    with scene.VideoScorer(path) as v:
+    with scene.VideoScorer(path, decoder="subset") as v:
         with pytest.raises(VtsegError, match="emulation prevention inside I_PCM"):
             v.score()
+    frames, _ = oracle.decode_full(path)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        v.score()
+        assert v.general()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(30)])
+    assert np.array_equal(got, frames)
 
 
 def test_open_rejects_non_mp4(tmp_path):
