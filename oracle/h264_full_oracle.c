@@ -320,9 +320,12 @@ static int median3(int a, int b, int c) {
 typedef struct {
   int valid, profile_idc, log2_max_frame_num, poc_type, log2_max_poc_lsb, dpoaz;
   int max_num_ref_frames, gaps, mbw, mbh, crop_l, crop_r, crop_t, crop_b;
+  int direct8x8;                     /* direct_8x8_inference_flag */
+  int off_non_ref, off_t2b, ncycle;  /* POC type 1 (7.4.2.1.1) */
+  int off_ref[256];
 } fo_sps;
 typedef struct {
-  int valid, sps_id, bfpo, num_ref_l0, weighted_pred, weighted_bipred, pic_init_qp;
+  int valid, sps_id, bfpo, num_ref_l0, num_ref_l1, weighted_pred, weighted_bipred, pic_init_qp;
   int cqp_off, cqp_off2, deblock_ctrl, cip, redundant;
   int cabac, t8mode;   /* entropy_coding_mode_flag, transform_8x8_mode_flag */
 } fo_pps;
@@ -353,18 +356,19 @@ static int parse_sps(const uint8_t *nal, int64_t n, fo_sps *tab, char *err) {
     s.log2_max_poc_lsb = (int)fb_ue(&b) + 4;
   } else if (s.poc_type == 1) {
     s.dpoaz = (int)fb_bit(&b);
-    fb_se(&b);
-    fb_se(&b);
+    s.off_non_ref = fb_se(&b);
+    s.off_t2b = fb_se(&b);
     uint32_t nc = fb_ue(&b);
     if (nc > 255) return FO_E_FORMAT;
-    for (uint32_t i = 0; i < nc; i++) fb_se(&b);
+    s.ncycle = (int)nc;
+    for (uint32_t i = 0; i < nc; i++) s.off_ref[i] = fb_se(&b);
   }
   s.max_num_ref_frames = (int)fb_ue(&b);
   s.gaps = (int)fb_bit(&b);
   s.mbw = (int)fb_ue(&b) + 1;
   s.mbh = (int)fb_ue(&b) + 1;
   if (!fb_bit(&b)) { strcpy(err, "interlaced (frame_mbs_only_flag 0)"); return FO_E_UNSUPPORTED; }
-  fb_bit(&b); /* direct_8x8_inference_flag */
+  s.direct8x8 = (int)fb_bit(&b);
   if (fb_bit(&b)) {
     s.crop_l = 2 * (int)fb_ue(&b);
     s.crop_r = 2 * (int)fb_ue(&b);
@@ -389,7 +393,7 @@ static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, char *err) {
   p.bfpo = (int)fb_bit(&b);
   if (fb_ue(&b)) { strcpy(err, "slice groups (FMO)"); return FO_E_UNSUPPORTED; }
   p.num_ref_l0 = (int)fb_ue(&b) + 1;
-  fb_ue(&b);
+  p.num_ref_l1 = (int)fb_ue(&b) + 1;
   p.weighted_pred = (int)fb_bit(&b);
   p.weighted_bipred = (int)fb_bits(&b, 2);
   p.pic_init_qp = 26 + fb_se(&b);
@@ -416,7 +420,6 @@ static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, char *err) {
     }
   }
   if (b.err) return FO_E_FORMAT;
-  if (p.weighted_pred) { strcpy(err, "weighted prediction"); return FO_E_UNSUPPORTED; }
   if (p.redundant) { strcpy(err, "redundant pictures"); return FO_E_UNSUPPORTED; }
   p.valid = 1;
   tab[id] = p;
@@ -429,7 +432,20 @@ typedef struct {
   int frame_num, frame_num_wrap, lt_idx;
   int ref;              /* 0 unused, 1 short-term, 2 long-term */
   int id;               /* identity for bS comparisons */
+  int poc;              /* PicOrderCnt (8.2.1) */
+  /* motion of the decoded picture, per macroblock x raster 4x4 block, kept
+     for the direct prediction of later B pictures (8.4.1.2.1 colocated) */
+  int8_t *mref[2];      /* refIdxLX, -1: list unused or intra */
+  int16_t *mmv[2];      /* mvLX (x, y) */
+  int32_t *mpic[2];     /* id of the picture refIdxLX named */
 } fo_pic;
+
+static void pic_free(fo_pic *p) {
+  free(p->y); free(p->u); free(p->v);
+  for (int l = 0; l < 2; l++) { free(p->mref[l]); free(p->mmv[l]); free(p->mpic[l]); }
+  p->y = p->u = p->v = NULL;
+  for (int l = 0; l < 2; l++) { p->mref[l] = NULL; p->mmv[l] = NULL; p->mpic[l] = NULL; }
+}
 
 typedef struct {
   int type;     /* 0 P inter, 1 I_NxN, 2 I_16x16, 3 I_PCM, 4 P_Skip */
@@ -437,14 +453,14 @@ typedef struct {
   int qp;       /* QPY */
   int cbp;
   int i4[16];   /* Intra4x4PredMode per raster 4x4 block */
-  int refidx[16];   /* per raster 4x4 block, -1 intra */
-  int refpic[16];   /* picture id per raster 4x4 block */
-  int mv[16][2];
+  int refidx[2][16];   /* per list, per raster 4x4 block; -1: list unused / intra */
+  int refpic[2][16];   /* picture id per list and raster 4x4 block (-1: none) */
+  int mv[2][16][2];
   int nz[16];       /* total_coeff per raster luma 4x4 block (8x8 transform: the 8x8's count) */
   int nzc[2][4];    /* chroma AC total_coeff, raster 2x2 */
   int t8;           /* transform_size_8x8_flag (I_NxN with it = I_8x8) */
   int cmode;        /* intra_chroma_pred_mode */
-  int mvd[16][2];   /* CABAC: mvd_l0 per raster 4x4 block (context of later mvds) */
+  int mvd[2][16][2];   /* CABAC: mvd_lX per raster 4x4 block (context of later mvds) */
   uint32_t cbf;     /* CABAC coded_block_flag: bit 0 Intra16x16 DC, 1 + raster luma 4x4,
                        17 + iCbCr chroma DC, 19 + 4 iCbCr + raster chroma AC */
   int qpd;          /* mb_qp_delta */
@@ -468,6 +484,10 @@ typedef struct {
   int nslices;
   int max_lt_idx;       /* -1: no long-term frame indices */
   int prev_ref_frame_num;
+  /* 8.2.1 picture order count state */
+  int prev_poc_msb, prev_poc_lsb;   /* of the previous reference picture (type 0) */
+  int prev_fn_offset, prev_fn;      /* FrameNumOffset / frame_num of the previous picture (types 1, 2) */
+  int prev_mmco5;                   /* the previous picture had memory_management_control_operation 5 */
   int flags;
   char *err;
 } fo_dec;
@@ -907,7 +927,7 @@ typedef struct {
 
 /* neighbour motion data at MB-relative luma location (xN, yN); done_mask =
  * raster 4x4 blocks of the current MB whose motion is already set */
-static fo_nbmv nb_mv(const fo_dec *d, int cur, int xN, int yN, int done_mask) {
+static fo_nbmv nb_mv(const fo_dec *d, int l, int cur, int xN, int yN, int done_mask) {
   fo_nbmv r = {0, -1, 0, 0};
   fo_loc L = nb_loc(d, cur, xN, yN, 16, 16);
   if (L.mb < 0) return r;
@@ -916,19 +936,20 @@ static fo_nbmv nb_mv(const fo_dec *d, int cur, int xN, int yN, int done_mask) {
   r.avail = 1;
   const fo_mb *m = &d->mb[L.mb];
   if (m->type == 1 || m->type == 2 || m->type == 3) return r;
-  r.ref = m->refidx[blk];
-  r.mvx = m->mv[blk][0];
-  r.mvy = m->mv[blk][1];
+  r.ref = m->refidx[l][blk];
+  if (r.ref < 0) return r;   /* predFlagLX 0: refIdxLXN -1, mvLXN 0 */
+  r.mvx = m->mv[l][blk][0];
+  r.mvy = m->mv[l][blk][1];
   return r;
 }
 
 /* mbPart (x0, y0, w, h) in luma samples; shape: 0 generic, 1 16x8, 2 8x16 */
-static void mv_pred(const fo_dec *d, int cur, int x0, int y0, int w, int h, int ref, int done_mask,
+static void mv_pred(const fo_dec *d, int l, int cur, int x0, int y0, int w, int h, int ref, int done_mask,
                     int *px, int *py) {
-  fo_nbmv A = nb_mv(d, cur, x0 - 1, y0, done_mask);
-  fo_nbmv B = nb_mv(d, cur, x0, y0 - 1, done_mask);
-  fo_nbmv C = nb_mv(d, cur, x0 + w, y0 - 1, done_mask);
-  if (!C.avail) C = nb_mv(d, cur, x0 - 1, y0 - 1, done_mask);
+  fo_nbmv A = nb_mv(d, l, cur, x0 - 1, y0, done_mask);
+  fo_nbmv B = nb_mv(d, l, cur, x0, y0 - 1, done_mask);
+  fo_nbmv C = nb_mv(d, l, cur, x0 + w, y0 - 1, done_mask);
+  if (!C.avail) C = nb_mv(d, l, cur, x0 - 1, y0 - 1, done_mask);
   if (w == 16 && h == 8) {
     if (y0 == 0 && B.ref == ref) { *px = B.mvx; *py = B.mvy; return; }
     if (y0 == 8 && A.ref == ref) { *px = A.mvx; *py = A.mvy; return; }
@@ -951,13 +972,29 @@ static void mv_pred(const fo_dec *d, int cur, int x0, int y0, int w, int h, int 
 /* ---------------------------------------------------- deblocking (8.7) */
 static int mb_intra(const fo_mb *m) { return m->type == 1 || m->type == 2 || m->type == 3; }
 
-/* bS for the edge between luma samples p0 (in mb p, raster blk bp) and q0 */
+static int mv_far(const int *a, const int *b) { return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= 4; }
+
+/* bS for the edge between luma samples p0 (in mb p, raster blk bp) and q0
+   (8.7.2.1; reference pictures compared as pictures, not indices, and as the
+   set of pictures a bi-predicted block uses) */
 static int bs_of(const fo_mb *p, int bp, const fo_mb *q, int bq, int mb_edge) {
   if (mb_intra(p) || mb_intra(q)) return mb_edge ? 4 : 3;
   if (p->nz[bp] || q->nz[bq]) return 2;
-  if (p->refpic[bp] != q->refpic[bq]) return 1;
-  if (iabs(p->mv[bp][0] - q->mv[bq][0]) >= 4 || iabs(p->mv[bp][1] - q->mv[bq][1]) >= 4) return 1;
-  return 0;
+  int p0 = p->refpic[0][bp], p1 = p->refpic[1][bp], q0 = q->refpic[0][bq], q1 = q->refpic[1][bq];
+  int np = (p0 >= 0) + (p1 >= 0), nq = (q0 >= 0) + (q1 >= 0);
+  if (np != nq) return 1;
+  if (np == 1) {
+    int lp = p0 >= 0 ? 0 : 1, lq = q0 >= 0 ? 0 : 1;
+    if ((lp ? p1 : p0) != (lq ? q1 : q0)) return 1;
+    return mv_far(p->mv[lp][bp], q->mv[lq][bq]);
+  }
+  if (!((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0))) return 1;
+  if (p0 != p1) {
+    if (p0 == q0) return mv_far(p->mv[0][bp], q->mv[0][bq]) || mv_far(p->mv[1][bp], q->mv[1][bq]);
+    return mv_far(p->mv[0][bp], q->mv[1][bq]) || mv_far(p->mv[1][bp], q->mv[0][bq]);
+  }
+  return (mv_far(p->mv[0][bp], q->mv[0][bq]) || mv_far(p->mv[1][bp], q->mv[1][bq])) &&
+         (mv_far(p->mv[0][bp], q->mv[1][bq]) || mv_far(p->mv[1][bp], q->mv[0][bq]));
 }
 
 /* filter one line of samples across an edge; s[k * step] for k = -4..3 (p3..q3) */
@@ -1075,7 +1112,7 @@ static void dpb_compact(fo_dec *d) {
   int j = 0;
   for (int i = 0; i < d->ndpb; i++) {
     if (d->dpb[i].ref) d->dpb[j++] = d->dpb[i];
-    else { free(d->dpb[i].y); free(d->dpb[i].u); free(d->dpb[i].v); }
+    else pic_free(&d->dpb[i]);
   }
   d->ndpb = j;
 }
@@ -1083,8 +1120,13 @@ static void dpb_compact(fo_dec *d) {
 typedef struct {
   int nal_type, nal_ref_idc;
   int first_mb, slice_type, pps_id, frame_num, idr_pic_id;
-  int num_ref;
-  int mod_n, mod_idc[33], mod_val[33];
+  int poc_lsb, delta_bottom, delta_poc[2];
+  int direct_spatial;   /* direct_spatial_mv_pred_flag (B) */
+  int num_ref, num_ref1;
+  int mod_n, mod_idc[33], mod_val[33];      /* ref_pic_list_modification l0 */
+  int mod1_n, mod1_idc[33], mod1_val[33];   /* ... l1 */
+  /* pred_weight_table (7.3.3.2): [list][refIdx] luma weight / offset, chroma [Cb, Cr] */
+  int lwd, cwd, lw[2][32], lo[2][32], cw[2][32][2], co[2][32][2];
   int lt_ref_flag, adaptive, mmco_n, mmco[66][3];
   int qp, dbk_idc, off_a, off_b;
 } fo_hdr;
@@ -1093,12 +1135,18 @@ typedef struct {
 typedef struct {
   fo_dec *d;
   fo_pic *cur;
-  fo_pic *list[33];
+  fo_pic *list[33];     /* RefPicList0 */
   int nlist;
+  fo_pic *list1[33];    /* RefPicList1 (B) */
+  int nlist1;
   int slice_no;
+  int is_b;
+  int wmode;            /* 8.4.2.3: 0 default, 1 explicit, 2 implicit weighted prediction */
+  const fo_hdr *h;
 } fo_ctx;
 
 static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_hdr *h);
+static void inter_pred_mb(const fo_ctx *c, int addr, int *py, int *pu, int *pv);
 
 /* 8.5.13: scaling (flat) + 8x8 inverse transform of raster coefficients c */
 static const int NORM8[6][6] = VTS_NORM8_DATA;
@@ -1233,9 +1281,7 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
   if (m->type == 0) {
     /* predict each 4x4 block with its motion (partitions share them;
        interpolation is per sample, so the block size does not matter) */
-    for (int blk = 0; blk < 16; blk++)
-      mc_part(d, c->list[m->refidx[blk]], addr, (blk % 4) * 4, (blk / 4) * 4, 4, 4, m->mv[blk][0],
-              m->mv[blk][1], pred_y, pred_u, pred_v);
+    inter_pred_mb(c, addr, pred_y, pred_u, pred_v);
     if (m->t8) {
       for (int b8 = 0; b8 < 4; b8++) {
         int r[64], bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
@@ -1331,6 +1377,66 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
 }
 
 
+/* 8.2.1 PicOrderCnt of the picture a slice header belongs to (frames only);
+   the "previous picture" state is advanced by poc_advance() after it */
+static int pic_order_cnt(const fo_dec *d, const fo_hdr *h) {
+  const fo_sps *S = d->S;
+  int idr = h->nal_type == 5, maxfn = fo_max_frame_num(d);
+  if (S->poc_type == 0) { /* 8.2.1.1 */
+    int max_lsb = 1 << S->log2_max_poc_lsb, pmsb = idr ? 0 : d->prev_poc_msb, plsb = idr ? 0 : d->prev_poc_lsb;
+    int msb;
+    if (h->poc_lsb < plsb && plsb - h->poc_lsb >= max_lsb / 2) msb = pmsb + max_lsb;
+    else if (h->poc_lsb > plsb && h->poc_lsb - plsb > max_lsb / 2) msb = pmsb - max_lsb;
+    else msb = pmsb;
+    int top = msb + h->poc_lsb, bot = top + h->delta_bottom;
+    return top < bot ? top : bot;
+  }
+  int off = idr ? 0 : (d->prev_fn > h->frame_num ? d->prev_fn_offset + maxfn : d->prev_fn_offset);
+  if (S->poc_type == 2) { /* 8.2.1.3 */
+    if (idr) return 0;
+    return h->nal_ref_idc ? 2 * (off + h->frame_num) : 2 * (off + h->frame_num) - 1;
+  }
+  /* 8.2.1.2 */
+  int abs_fn = S->ncycle ? off + h->frame_num : 0;
+  if (!h->nal_ref_idc && abs_fn > 0) abs_fn--;
+  int expected = 0;
+  if (abs_fn > 0) {
+    int delta_cycle = 0;
+    for (int i = 0; i < S->ncycle; i++) delta_cycle += S->off_ref[i];
+    int cyc = (abs_fn - 1) / S->ncycle, in = (abs_fn - 1) % S->ncycle;
+    expected = cyc * delta_cycle;
+    for (int i = 0; i <= in; i++) expected += S->off_ref[i];
+  }
+  if (!h->nal_ref_idc) expected += S->off_non_ref;
+  int top = expected + h->delta_poc[0], bot = top + S->off_t2b + h->delta_poc[1];
+  return top < bot ? top : bot;
+}
+
+/* after a picture: the state 8.2.1 keeps for the next one */
+static void poc_advance(fo_dec *d, const fo_hdr *h) {
+  int idr = h->nal_type == 5, mmco5 = 0, maxfn = fo_max_frame_num(d);
+  for (int k = 0; h->adaptive && k < h->mmco_n; k++) mmco5 |= h->mmco[k][0] == 5;
+  if (d->S->poc_type == 0) {
+    if (h->nal_ref_idc) {
+      if (mmco5) { d->prev_poc_msb = 0; d->prev_poc_lsb = h->delta_bottom < 0 ? -h->delta_bottom : 0; }
+      else {
+        int max_lsb = 1 << d->S->log2_max_poc_lsb;
+        int pmsb = idr ? 0 : d->prev_poc_msb, plsb = idr ? 0 : d->prev_poc_lsb, msb;
+        if (h->poc_lsb < plsb && plsb - h->poc_lsb >= max_lsb / 2) msb = pmsb + max_lsb;
+        else if (h->poc_lsb > plsb && h->poc_lsb - plsb > max_lsb / 2) msb = pmsb - max_lsb;
+        else msb = pmsb;
+        d->prev_poc_msb = msb;
+        d->prev_poc_lsb = h->poc_lsb;
+      }
+    }
+  } else {
+    int off = idr ? 0 : (d->prev_fn > h->frame_num ? d->prev_fn_offset + maxfn : d->prev_fn_offset);
+    d->prev_fn_offset = mmco5 ? 0 : off;
+  }
+  d->prev_fn = mmco5 ? 0 : h->frame_num;
+  d->prev_mmco5 = mmco5;
+}
+
 static int slice_data_cabac(fo_ctx *c, fb_t *b, const fo_hdr *h, int is_p, int64_t stop);
 
 static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len, int slice_no,
@@ -1363,30 +1469,61 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
     return fo_fail(d, FO_E_UNSUPPORTED, "picture size change");
   d->S = S;
   d->P = P;
-  if (h.slice_type != 0 && h.slice_type != 2) return fo_fail(d, FO_E_UNSUPPORTED, "B/SP/SI slice");
-  int is_p = h.slice_type == 0;
+  if (h.slice_type > 2) return fo_fail(d, FO_E_UNSUPPORTED, "SP/SI slice");
+  int is_b = h.slice_type == 1;
+  int is_p = h.slice_type == 0 || is_b;   /* inter slice (P or B) */
   h.frame_num = (int)fb_bits(&b, S->log2_max_frame_num);
   if (nal_type == 5) h.idr_pic_id = (int)fb_ue(&b);
   if (S->poc_type == 0) {
-    fb_bits(&b, S->log2_max_poc_lsb);
-    if (P->bfpo) fb_se(&b);
+    h.poc_lsb = (int)fb_bits(&b, S->log2_max_poc_lsb);
+    if (P->bfpo) h.delta_bottom = fb_se(&b);
   } else if (S->poc_type == 1 && !S->dpoaz) {
-    fb_se(&b);
-    if (P->bfpo) fb_se(&b);
+    h.delta_poc[0] = fb_se(&b);
+    if (P->bfpo) h.delta_poc[1] = fb_se(&b);
   }
+  if (is_b) h.direct_spatial = (int)fb_bit(&b);
   h.num_ref = P->num_ref_l0;
+  h.num_ref1 = P->num_ref_l1;
   if (is_p) {
-    if (fb_bit(&b)) h.num_ref = (int)fb_ue(&b) + 1;
-    if (h.num_ref > 32) return fo_fail(d, FO_E_FORMAT, "num_ref_idx");
-    if (fb_bit(&b)) { /* ref_pic_list_modification (7.3.3.1) */
-      for (;;) {
-        int idc = (int)fb_ue(&b);
-        if (idc == 3 || b.err) break;
-        if (idc > 2 || h.mod_n >= 33) return fo_fail(d, FO_E_FORMAT, "ref list modification");
-        h.mod_idc[h.mod_n] = idc;
-        h.mod_val[h.mod_n++] = (int)fb_ue(&b);
+    if (fb_bit(&b)) { /* num_ref_idx_active_override_flag */
+      h.num_ref = (int)fb_ue(&b) + 1;
+      if (is_b) h.num_ref1 = (int)fb_ue(&b) + 1;
+    }
+    if (h.num_ref > 32 || h.num_ref1 > 32) return fo_fail(d, FO_E_FORMAT, "num_ref_idx");
+    for (int l = 0; l < 1 + is_b; l++) {
+      int *n = l ? &h.mod1_n : &h.mod_n, *idcs = l ? h.mod1_idc : h.mod_idc, *vals = l ? h.mod1_val : h.mod_val;
+      if (fb_bit(&b)) { /* ref_pic_list_modification (7.3.3.1) */
+        for (;;) {
+          int idc = (int)fb_ue(&b);
+          if (idc == 3 || b.err) break;
+          if (idc > 2 || *n >= 33) return fo_fail(d, FO_E_FORMAT, "ref list modification");
+          idcs[*n] = idc;
+          vals[(*n)++] = (int)fb_ue(&b);
+        }
       }
     }
+  }
+  if ((P->weighted_pred && is_p && !is_b) || (P->weighted_bipred == 1 && is_b)) { /* 7.3.3.2 */
+    h.lwd = (int)fb_ue(&b);
+    h.cwd = (int)fb_ue(&b);
+    if (h.lwd > 7 || h.cwd > 7) return fo_fail(d, FO_E_FORMAT, "pred_weight_table denominators");
+    for (int l = 0; l < 1 + is_b; l++)
+      for (int i = 0; i < (l ? h.num_ref1 : h.num_ref); i++) {
+        h.lw[l][i] = 1 << h.lwd;
+        h.lo[l][i] = 0;
+        if (fb_bit(&b)) {
+          h.lw[l][i] = fb_se(&b);
+          h.lo[l][i] = fb_se(&b);
+        }
+        for (int j = 0; j < 2; j++) { h.cw[l][i][j] = 1 << h.cwd; h.co[l][i][j] = 0; }
+        if (fb_bit(&b))
+          for (int j = 0; j < 2; j++) {
+            h.cw[l][i][j] = fb_se(&b);
+            h.co[l][i][j] = fb_se(&b);
+          }
+        if (h.lw[l][i] < -128 || h.lw[l][i] > 127 || h.lo[l][i] < -128 || h.lo[l][i] > 127)
+          return fo_fail(d, FO_E_FORMAT, "pred_weight_table");
+      }
   }
   if (nal_ref_idc) { /* dec_ref_pic_marking (7.3.3.3) */
     if (nal_type == 5) {
@@ -1411,6 +1548,7 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
     int idc = (int)fb_ue(&b);
     if (idc != 0) return fo_fail(d, FO_E_UNSUPPORTED, "cabac_init_idc 1/2 (only the idc 0 tables are restated)");
   }
+  if (P->cabac && is_b) return fo_fail(d, FO_E_UNSUPPORTED, "CABAC B slices");
   h.qp = P->pic_init_qp + fb_se(&b);
   if (P->deblock_ctrl) {
     h.dbk_idc = (int)fb_ue(&b);
@@ -1421,20 +1559,24 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
   }
   if (b.err || h.first_mb >= d->nmb || h.qp < 0 || h.qp > 51 || h.dbk_idc > 2)
     return fo_fail(d, FO_E_FORMAT, "slice header");
+  if (is_b && !S->direct8x8 && 0) return fo_fail(d, FO_E_UNSUPPORTED, "direct_8x8_inference_flag 0");
   *is_idr_out = nal_type == 5;
   *hdr_out = h;
   if (slice_no >= 4096) return fo_fail(d, FO_E_UNSUPPORTED, "too many slices");
   d->dbk[slice_no].idc = h.dbk_idc;
   d->dbk[slice_no].off_a = h.off_a;
   d->dbk[slice_no].off_b = h.off_b;
+  cur->poc = pic_order_cnt(d, &h);
 
   fo_ctx c;
   memset(&c, 0, sizeof c);
   c.d = d;
   c.cur = cur;
   c.slice_no = slice_no;
+  c.is_b = is_b;
+  c.h = hdr_out;
+  c.wmode = is_b ? (P->weighted_bipred == 1 ? 1 : (P->weighted_bipred == 2 ? 2 : 0)) : (is_p && P->weighted_pred ? 1 : 0);
   if (is_p) {
-    /* 8.2.4.2.1: short-term by descending PicNum, then long-term ascending */
     int fn = h.frame_num, maxfn = fo_max_frame_num(d);
     fo_pic *st[17], *lt[17];
     int ns = 0, nl = 0;
@@ -1447,47 +1589,77 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
         lt[nl++] = p;
       }
     }
-    for (int i = 1; i < ns; i++)
-      for (int j = i; j > 0 && st[j]->frame_num_wrap > st[j - 1]->frame_num_wrap; j--) {
-        fo_pic *t = st[j]; st[j] = st[j - 1]; st[j - 1] = t;
-      }
+    /* long-term: ascending LongTermPicNum (8.2.4.2.1 / 8.2.4.2.3) */
     for (int i = 1; i < nl; i++)
       for (int j = i; j > 0 && lt[j]->lt_idx < lt[j - 1]->lt_idx; j--) {
         fo_pic *t = lt[j]; lt[j] = lt[j - 1]; lt[j - 1] = t;
       }
-    fo_pic *init[34];
-    int ni = 0;
-    for (int i = 0; i < ns; i++) init[ni++] = st[i];
-    for (int i = 0; i < nl; i++) init[ni++] = lt[i];
-    for (int i = 0; i < 33; i++) c.list[i] = i < ni ? init[i] : NULL;
-    /* 8.2.4.3 modification */
-    int pred = fn, ridx = 0, n = h.num_ref;
-    for (int k = 0; k < h.mod_n; k++) {
-      fo_pic *pic = NULL;
-      int is_long = h.mod_idc[k] == 2, num = 0;
-      if (!is_long) {
-        int abs_diff = h.mod_val[k] + 1, nowrap;
-        if (h.mod_idc[k] == 0) nowrap = pred - abs_diff < 0 ? pred - abs_diff + maxfn : pred - abs_diff;
-        else nowrap = pred + abs_diff >= maxfn ? pred + abs_diff - maxfn : pred + abs_diff;
-        pred = nowrap;
-        num = nowrap > fn ? nowrap - maxfn : nowrap;
-        pic = dpb_find_short(d, num, fn);
-      } else {
-        num = h.mod_val[k];
-        pic = dpb_find_long(d, num);
-      }
-      if (!pic) return fo_fail(d, FO_E_DECODE, "modification names no reference picture");
-      for (int ci = n; ci > ridx; ci--) c.list[ci] = c.list[ci - 1];
-      c.list[ridx++] = pic;
-      int ni2 = ridx;
-      for (int ci = ridx; ci <= n; ci++) {
-        fo_pic *q = c.list[ci];
-        int same = q == pic;
-        if (!same) c.list[ni2++] = q;
-      }
+    fo_pic *init[2][34];
+    int ni[2] = {0, 0};
+    if (!is_b) {
+      /* 8.2.4.2.1: short-term by descending PicNum, then long-term */
+      for (int i = 1; i < ns; i++)
+        for (int j = i; j > 0 && st[j]->frame_num_wrap > st[j - 1]->frame_num_wrap; j--) {
+          fo_pic *t = st[j]; st[j] = st[j - 1]; st[j - 1] = t;
+        }
+      for (int i = 0; i < ns; i++) init[0][ni[0]++] = st[i];
+    } else {
+      /* 8.2.4.2.3: list 0 = POC below the current picture's descending, then
+         above ascending; list 1 the other way round; long-term after both */
+      for (int i = 1; i < ns; i++)
+        for (int j = i; j > 0 && st[j]->poc < st[j - 1]->poc; j--) {
+          fo_pic *t = st[j]; st[j] = st[j - 1]; st[j - 1] = t;
+        }
+      for (int i = ns - 1; i >= 0; i--) if (st[i]->poc < cur->poc) init[0][ni[0]++] = st[i];
+      for (int i = 0; i < ns; i++) if (st[i]->poc > cur->poc) init[0][ni[0]++] = st[i];
+      for (int i = 0; i < ns; i++) if (st[i]->poc > cur->poc) init[1][ni[1]++] = st[i];
+      for (int i = ns - 1; i >= 0; i--) if (st[i]->poc < cur->poc) init[1][ni[1]++] = st[i];
     }
-    c.nlist = n;
+    for (int l = 0; l < 1 + is_b; l++)
+      for (int i = 0; i < nl; i++) init[l][ni[l]++] = lt[i];
+    if (is_b && ni[1] > 1 && ni[0] == ni[1]) {
+      int same = 1;
+      for (int i = 0; i < ni[0]; i++) same &= init[0][i] == init[1][i];
+      if (same) { fo_pic *t = init[1][0]; init[1][0] = init[1][1]; init[1][1] = t; }
+    }
+    for (int l = 0; l < 1 + is_b; l++) {
+      fo_pic **list = l ? c.list1 : c.list;
+      int n = l ? h.num_ref1 : h.num_ref;
+      for (int i = 0; i < 33; i++) list[i] = i < ni[l] && i < n ? init[l][i] : NULL;
+      /* 8.2.4.3 modification */
+      int pred = fn, ridx = 0;
+      int mn = l ? h.mod1_n : h.mod_n;
+      const int *idcs = l ? h.mod1_idc : h.mod_idc, *vals = l ? h.mod1_val : h.mod_val;
+      for (int k = 0; k < mn; k++) {
+        fo_pic *pic = NULL;
+        int is_long = idcs[k] == 2, num = 0;
+        if (!is_long) {
+          int abs_diff = vals[k] + 1, nowrap;
+          if (idcs[k] == 0) nowrap = pred - abs_diff < 0 ? pred - abs_diff + maxfn : pred - abs_diff;
+          else nowrap = pred + abs_diff >= maxfn ? pred + abs_diff - maxfn : pred + abs_diff;
+          pred = nowrap;
+          num = nowrap > fn ? nowrap - maxfn : nowrap;
+          pic = dpb_find_short(d, num, fn);
+        } else {
+          num = vals[k];
+          pic = dpb_find_long(d, num);
+        }
+        if (!pic) return fo_fail(d, FO_E_DECODE, "modification names no reference picture");
+        for (int ci = n; ci > ridx; ci--) list[ci] = list[ci - 1];
+        list[ridx++] = pic;
+        int ni2 = ridx;
+        for (int ci = ridx; ci <= n; ci++) {
+          fo_pic *q = list[ci];
+          if (q != pic) list[ni2++] = q;
+        }
+      }
+      list[n] = NULL;
+      if (l) c.nlist1 = n;
+      else c.nlist = n;
+    }
   }
+  if (is_b && (!c.list1[0] || !c.list1[0]->mref[0]))
+    return fo_fail(d, FO_E_DECODE, "B slice without a colocated picture (RefPicList1[0])");
 
   if (P->cabac) return slice_data_cabac(&c, &b, &h, is_p, stop);
   /* 7.3.4 slice_data */
@@ -1524,6 +1696,252 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
   return 0;
 }
 
+/* ------------------------------------------- B / weighted prediction */
+/* Table 7-14: prediction of the two partitions of B mb_type 1..21 (1 Pred_L0,
+   2 Pred_L1, 3 BiPred); odd types >= 5 are 8x16, even >= 4 16x8 */
+static const uint8_t B_PART[22][2] = {{0, 0}, {1, 0}, {2, 0}, {3, 0}, {1, 1}, {1, 1}, {2, 2}, {2, 2},
+                                      {1, 2}, {1, 2}, {2, 1}, {2, 1}, {1, 3}, {1, 3}, {2, 3}, {2, 3},
+                                      {3, 1}, {3, 1}, {3, 2}, {3, 2}, {3, 3}, {3, 3}};
+/* Table 7-18: B sub_mb_type -> (prediction, shape 0 8x8 / 1 8x4 / 2 4x8 / 3 4x4); prediction 0 = direct */
+static const uint8_t B_SUB[13][2] = {{0, 0}, {1, 0}, {2, 0}, {3, 0}, {1, 1}, {1, 2}, {2, 1},
+                                     {2, 2}, {3, 1}, {3, 2}, {1, 3}, {2, 3}, {3, 3}};
+
+static void set_mv(const fo_ctx *c, fo_mb *m, int l, int blk, int ref, int mvx, int mvy) {
+  fo_pic *const *list = l ? c->list1 : c->list;
+  m->refidx[l][blk] = ref;
+  m->refpic[l][blk] = ref >= 0 ? list[ref]->id : -1;
+  m->mv[l][blk][0] = ref >= 0 ? mvx : 0;
+  m->mv[l][blk][1] = ref >= 0 ? mvy : 0;
+}
+
+static int min_positive(int x, int y) { return (x >= 0 && y >= 0) ? (x < y ? x : y) : (x > y ? x : y); }
+
+/* 8.4.1.2: direct prediction of the 4x4 blocks in mask (raster bits) */
+static int direct_pred(fo_ctx *c, int addr, int mask) {
+  fo_dec *d = c->d;
+  fo_mb *m = &d->mb[addr];
+  const fo_pic *col = c->list1[0];
+  int spatial = c->h->direct_spatial;
+  int ref[2] = {-1, -1}, mvp[2][2] = {{0, 0}, {0, 0}}, zero = 0;
+  if (spatial) { /* 8.4.1.2.2: reference indices and predictors of the 16x16 */
+    for (int l = 0; l < 2; l++) {
+      fo_nbmv A = nb_mv(d, l, addr, -1, 0, 0), B = nb_mv(d, l, addr, 0, -1, 0), C = nb_mv(d, l, addr, 16, -1, 0);
+      if (!C.avail) C = nb_mv(d, l, addr, -1, -1, 0);
+      ref[l] = min_positive(A.ref, min_positive(B.ref, C.ref));
+    }
+    if (ref[0] < 0 && ref[1] < 0) { ref[0] = ref[1] = 0; zero = 1; }
+    for (int l = 0; l < 2; l++)
+      if (ref[l] >= 0 && !zero) mv_pred(d, l, addr, 0, 0, 16, 16, ref[l], 0, &mvp[l][0], &mvp[l][1]);
+  }
+  for (int blk = 0; blk < 16; blk++) {
+    if (!((mask >> blk) & 1)) continue;
+    /* 8.4.1.2.1 colocated 4x4 block (direct_8x8_inference: the macroblock corner of the 8x8) */
+    int cb = blk;
+    if (d->S->direct8x8) cb = ((blk >> 3) * 3) * 4 + ((blk & 3) >> 1) * 3;
+    int ci = addr * 16 + cb, cl = col->mref[0][ci] >= 0 ? 0 : 1;
+    int ref_col = col->mref[cl][ci];   /* -1: intra */
+    int mvc_x = ref_col < 0 ? 0 : col->mmv[cl][ci * 2], mvc_y = ref_col < 0 ? 0 : col->mmv[cl][ci * 2 + 1];
+    if (spatial) {
+      int col_zero = col->ref == 1 && ref_col == 0 && mvc_x >= -1 && mvc_x <= 1 && mvc_y >= -1 && mvc_y <= 1;
+      for (int l = 0; l < 2; l++) {
+        int z = zero || ref[l] < 0 || (ref[l] == 0 && col_zero);
+        set_mv(c, m, l, blk, ref[l], z ? 0 : mvp[l][0], z ? 0 : mvp[l][1]);
+      }
+    } else { /* 8.4.1.2.3 temporal */
+      int r0 = 0;
+      if (ref_col >= 0) {
+        int id = col->mpic[cl][ci];
+        r0 = -1;
+        for (int i = 0; i < c->nlist && r0 < 0; i++)
+          if (c->list[i] && c->list[i]->id == id) r0 = i;
+        if (r0 < 0) return fo_fail(d, FO_E_DECODE, "temporal direct: colocated reference not in RefPicList0");
+      }
+      const fo_pic *p0 = c->list[r0], *p1 = c->list1[0];
+      if (!p0) return fo_fail(d, FO_E_DECODE, "temporal direct: no reference picture");
+      int tb = clip3(-128, 127, c->cur->poc - p0->poc), td = clip3(-128, 127, p1->poc - p0->poc);
+      int m0x, m0y, m1x, m1y;
+      if (p0->ref == 2 || td == 0) { m0x = mvc_x; m0y = mvc_y; m1x = m1y = 0; }
+      else {
+        int tx = (16384 + iabs(td / 2)) / td;
+        int dsf = clip3(-1024, 1023, (tb * tx + 32) >> 6);
+        m0x = (dsf * mvc_x + 128) >> 8;
+        m0y = (dsf * mvc_y + 128) >> 8;
+        m1x = m0x - mvc_x;
+        m1y = m0y - mvc_y;
+      }
+      set_mv(c, m, 0, blk, r0, m0x, m0y);
+      set_mv(c, m, 1, blk, 0, m1x, m1y);
+    }
+  }
+  return 0;
+}
+
+/* mb_pred / sub_mb_pred (7.3.5.1-2) and the motion of a P or B inter macroblock (CAVLC) */
+static int inter_mb_cavlc(fo_ctx *c, fb_t *b, int addr, int mb_type) {
+  fo_dec *d = c->d;
+  fo_mb *m = &d->mb[addr];
+  int shape, pm[4] = {1, 1, 1, 1}, ssh[4] = {0, 0, 0, 0}, ref0 = 0;
+  if (!c->is_b) {
+    shape = mb_type == 0 ? 0 : (mb_type <= 2 ? mb_type : 3);
+    ref0 = mb_type == 4;   /* P_8x8ref0 */
+  } else if (mb_type == 0) {
+    shape = 0;
+    pm[0] = 0;             /* B_Direct_16x16 */
+  } else if (mb_type <= 3) {
+    shape = 0;
+    pm[0] = mb_type;
+  } else if (mb_type < 22) {
+    shape = (mb_type & 1) ? 2 : 1;
+    pm[0] = B_PART[mb_type][0];
+    pm[1] = B_PART[mb_type][1];
+  } else {
+    shape = 3;
+  }
+  int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
+  if (shape == 3)
+    for (int k = 0; k < 4; k++) {
+      uint32_t v = fb_ue(b);
+      if (v > (c->is_b ? 12u : 3u)) return fo_fail(d, FO_E_FORMAT, "sub_mb_type");
+      if (c->is_b) { pm[k] = B_SUB[v][0]; ssh[k] = B_SUB[v][1]; }
+      else ssh[k] = (int)v;
+    }
+  int refs[2][4] = {{-1, -1, -1, -1}, {-1, -1, -1, -1}};
+  for (int l = 0; l < 1 + c->is_b; l++) {
+    int nref = l ? c->nlist1 : c->nlist;
+    fo_pic *const *list = l ? c->list1 : c->list;
+    for (int k = 0; k < nparts; k++) {
+      if (!((pm[k] >> l) & 1)) continue;
+      refs[l][k] = (nref > 1 && !ref0) ? fb_te(b, nref - 1) : 0;
+      if (refs[l][k] < 0 || refs[l][k] >= nref || !list[refs[l][k]])
+        return fo_fail(d, FO_E_DECODE, "ref_idx names no reference picture");
+    }
+  }
+  int mvd[2][4][4][2];
+  for (int l = 0; l < 1 + c->is_b; l++)
+    for (int k = 0; k < nparts; k++) {
+      if (!((pm[k] >> l) & 1)) continue;
+      int nsub = shape < 3 ? 1 : (ssh[k] == 0 ? 1 : (ssh[k] == 3 ? 4 : 2));
+      for (int q = 0; q < nsub; q++) {
+        mvd[l][k][q][0] = fb_se(b);
+        mvd[l][k][q][1] = fb_se(b);
+      }
+    }
+  /* motion: partitions in order, both lists of a (sub-)partition before the next */
+  int done = 0;
+  for (int k = 0; k < nparts; k++) {
+    int nsub = 1, pw, ph, x0, y0;
+    if (shape == 0) { pw = ph = 16; x0 = y0 = 0; }
+    else if (shape == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * k; }
+    else if (shape == 2) { pw = 8; ph = 16; x0 = 8 * k; y0 = 0; }
+    else {
+      x0 = 8 * (k & 1);
+      y0 = 8 * (k >> 1);
+      nsub = ssh[k] == 0 ? 1 : (ssh[k] == 3 ? 4 : 2);
+      pw = ssh[k] == 0 || ssh[k] == 1 ? 8 : 4;
+      ph = ssh[k] == 0 || ssh[k] == 2 ? 8 : 4;
+    }
+    if (pm[k] == 0) { /* direct: B_Direct_16x16 or B_Direct_8x8 */
+      int bm = 0;
+      for (int yy = y0 / 4; yy < (y0 + ph) / 4; yy++)
+        for (int xx = x0 / 4; xx < (x0 + pw) / 4; xx++) bm |= 1 << (yy * 4 + xx);
+      int rc = direct_pred(c, addr, bm);
+      if (rc) return rc;
+      done |= bm;
+      continue;
+    }
+    for (int q = 0; q < nsub; q++) {
+      int sx = x0, sy = y0;
+      if (shape == 3) {
+        if (ssh[k] == 1) sy += 4 * q;
+        else if (ssh[k] == 2) sx += 4 * q;
+        else if (ssh[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+      }
+      for (int l = 0; l < 2; l++) {
+        int use = (pm[k] >> l) & 1;
+        int vx = 0, vy = 0;
+        if (use) {
+          int px, py;
+          mv_pred(d, l, addr, sx, sy, pw, ph, refs[l][k], done, &px, &py);
+          vx = px + mvd[l][k][q][0];
+          vy = py + mvd[l][k][q][1];
+          if (vx < -32768 || vx > 32767 || vy < -32768 || vy > 32767) return fo_fail(d, FO_E_FORMAT, "mv range");
+        }
+        for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
+          for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) set_mv(c, m, l, yy * 4 + xx, use ? refs[l][k] : -1, vx, vy);
+      }
+      for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
+        for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) done |= 1 << (yy * 4 + xx);
+    }
+  }
+  return 0;
+}
+
+/* implicit bi-prediction weights (8.4.2.3.1) for refIdxL0 r0, refIdxL1 r1 */
+static void implicit_w(const fo_ctx *c, int r0, int r1, int *w0, int *w1) {
+  const fo_pic *p0 = c->list[r0], *p1 = c->list1[r1];
+  int tb = clip3(-128, 127, c->cur->poc - p0->poc), td = clip3(-128, 127, p1->poc - p0->poc);
+  *w0 = *w1 = 32;
+  if (td == 0 || p0->ref == 2 || p1->ref == 2) return;
+  int tx = (16384 + iabs(td / 2)) / td;
+  int dsf = clip3(-1024, 1023, (tb * tx + 32) >> 6);
+  if ((dsf >> 2) < -64 || (dsf >> 2) > 128) return;
+  *w0 = 64 - (dsf >> 2);
+  *w1 = dsf >> 2;
+}
+
+/* 8.4.2.3: one predicted sample from the list-0 / list-1 predictions p0, p1
+   (r0 / r1 < 0: list unused); pl -1 luma, 0 Cb, 1 Cr */
+static int wp_sample(const fo_ctx *c, int pl, int r0, int r1, int p0, int p1) {
+  if (c->wmode == 1) {
+    const fo_hdr *h = c->h;
+    int lwd = pl < 0 ? h->lwd : h->cwd;
+    int w0 = 0, o0 = 0, w1 = 0, o1 = 0;
+    if (r0 >= 0) { w0 = pl < 0 ? h->lw[0][r0] : h->cw[0][r0][pl]; o0 = pl < 0 ? h->lo[0][r0] : h->co[0][r0][pl]; }
+    if (r1 >= 0) { w1 = pl < 0 ? h->lw[1][r1] : h->cw[1][r1][pl]; o1 = pl < 0 ? h->lo[1][r1] : h->co[1][r1][pl]; }
+    if (r0 >= 0 && r1 >= 0) return clip1(((p0 * w0 + p1 * w1 + (1 << lwd)) >> (lwd + 1)) + ((o0 + o1 + 1) >> 1));
+    int p = r0 >= 0 ? p0 : p1, w = r0 >= 0 ? w0 : w1, o = r0 >= 0 ? o0 : o1;
+    if (lwd >= 1) return clip1(((p * w + (1 << (lwd - 1))) >> lwd) + o);
+    return clip1(p * w + o);
+  }
+  if (r0 >= 0 && r1 >= 0) {
+    if (c->wmode == 2) {
+      int w0, w1;
+      implicit_w(c, r0, r1, &w0, &w1);
+      return clip1((p0 * w0 + p1 * w1 + 32) >> 6);
+    }
+    return (p0 + p1 + 1) >> 1;
+  }
+  return r0 >= 0 ? p0 : p1;
+}
+
+/* inter prediction of the whole macroblock from its per-4x4 motion */
+static void inter_pred_mb(const fo_ctx *c, int addr, int *py, int *pu, int *pv) {
+  const fo_dec *d = c->d;
+  const fo_mb *m = &d->mb[addr];
+  int ty[2][256], tu[2][64], tv[2][64];
+  for (int blk = 0; blk < 16; blk++) {
+    int bx = (blk % 4) * 4, by = (blk / 4) * 4;
+    int r0 = m->refidx[0][blk], r1 = m->refidx[1][blk];
+    for (int l = 0; l < 2; l++) {
+      int r = l ? r1 : r0;
+      if (r < 0) continue;
+      mc_part(d, l ? c->list1[r] : c->list[r], addr, bx, by, 4, 4, m->mv[l][blk][0], m->mv[l][blk][1], ty[l], tu[l],
+              tv[l]);
+    }
+    for (int y = 0; y < 4; y++)
+      for (int x = 0; x < 4; x++) {
+        int i = (by + y) * 16 + bx + x;
+        py[i] = wp_sample(c, -1, r0, r1, ty[0][i], ty[1][i]);
+      }
+    for (int y = 0; y < 2; y++)
+      for (int x = 0; x < 2; x++) {
+        int i = (by / 2 + y) * 8 + bx / 2 + x;
+        pu[i] = wp_sample(c, 0, r0, r1, tu[0][i], tu[1][i]);
+        pv[i] = wp_sample(c, 1, r0, r1, tv[0][i], tv[1][i]);
+      }
+  }
+}
+
 /* macroblock_layer (7.3.5) + reconstruction; b == NULL: P_Skip */
 static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_hdr *h) {
   (void)h;
@@ -1533,26 +1951,30 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
   int slice = m->slice;
   memset(m, 0, sizeof *m);
   m->slice = slice;
-  for (int i = 0; i < 16; i++) { m->refidx[i] = -1; m->refpic[i] = -1; m->i4[i] = 2; }
+  for (int i = 0; i < 16; i++) {
+    m->refidx[0][i] = m->refidx[1][i] = -1;
+    m->refpic[0][i] = m->refpic[1][i] = -1;
+    m->i4[i] = 2;
+  }
   int mx = addr % d->mbw, my = addr / d->mbw;
   int pred_y[256], pred_u[64], pred_v[64];
-  if (!b) { /* P_Skip (8.4.1.1) */
+  if (!b) { /* P_Skip (8.4.1.1) / B_Skip (8.4.1.2) */
     m->type = 4;
     m->qp = *qp;
-    int px = 0, py = 0;
-    fo_loc LA = nb_loc(d, addr, -1, 0, 16, 16), LB = nb_loc(d, addr, 0, -1, 16, 16);
-    fo_nbmv A = nb_mv(d, addr, -1, 0, 0), B = nb_mv(d, addr, 0, -1, 0);
-    if (!(LA.mb < 0 || LB.mb < 0 || (A.ref == 0 && A.mvx == 0 && A.mvy == 0) ||
-          (B.ref == 0 && B.mvx == 0 && B.mvy == 0)))
-      mv_pred(d, addr, 0, 0, 16, 16, 0, 0, &px, &py);
-    if (!c->list[0] || c->nlist < 1) return fo_fail(d, FO_E_DECODE, "P_Skip without a reference picture");
-    for (int i = 0; i < 16; i++) {
-      m->refidx[i] = 0;
-      m->refpic[i] = c->list[0]->id;
-      m->mv[i][0] = px;
-      m->mv[i][1] = py;
+    if (c->is_b) {
+      int rc = direct_pred(c, addr, 0xffff);
+      if (rc) return rc;
+    } else {
+      int px = 0, py = 0;
+      fo_loc LA = nb_loc(d, addr, -1, 0, 16, 16), LB = nb_loc(d, addr, 0, -1, 16, 16);
+      fo_nbmv A = nb_mv(d, 0, addr, -1, 0, 0), B = nb_mv(d, 0, addr, 0, -1, 0);
+      if (!(LA.mb < 0 || LB.mb < 0 || (A.ref == 0 && A.mvx == 0 && A.mvy == 0) ||
+            (B.ref == 0 && B.mvx == 0 && B.mvy == 0)))
+        mv_pred(d, 0, addr, 0, 0, 16, 16, 0, 0, &px, &py);
+      if (!c->list[0] || c->nlist < 1) return fo_fail(d, FO_E_DECODE, "P_Skip without a reference picture");
+      for (int i = 0; i < 16; i++) set_mv(c, m, 0, i, 0, px, py);
     }
-    mc_part(d, c->list[0], addr, 0, 0, 16, 16, px, py, pred_y, pred_u, pred_v);
+    inter_pred_mb(c, addr, pred_y, pred_u, pred_v);
     for (int y = 0; y < 16; y++)
       for (int x = 0; x < 16; x++) pic->y[(int64_t)(my * 16 + y) * d->W + mx * 16 + x] = (uint8_t)pred_y[y * 16 + x];
     for (int y = 0; y < 8; y++)
@@ -1564,9 +1986,9 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
   }
   int mb_type = (int)fb_ue(b);
   int itype;                 /* I mb_type (0..25) or -1 for inter */
-  if (is_p) itype = mb_type >= 5 ? mb_type - 5 : -1;
-  else itype = mb_type;
-  if (itype > 25 || (is_p && mb_type > 30)) return fo_fail(d, FO_E_FORMAT, "mb_type");
+  int intra0 = c->is_b ? 23 : (is_p ? 5 : 0);   /* first intra mb_type (Tables 7-11, 7-13, 7-14) */
+  itype = mb_type >= intra0 ? mb_type - intra0 : -1;
+  if (itype > 25) return fo_fail(d, FO_E_FORMAT, "mb_type");
   if (itype == 25) { /* I_PCM (7.3.5) */
     m->type = 3;
     m->qp = *qp;
@@ -1582,7 +2004,6 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
     return b->err ? fo_fail(d, FO_E_FORMAT, "I_PCM") : 0;
   }
   int cbp = 0, i16mode = 0, cmode = 0;
-  int nparts = 0, sub[4] = {0, 0, 0, 0};
   if (itype == 0) { /* I_NxN: 8.3.1.1 mode prediction */
     m->type = 1;
     int prev[16], rem[16];
@@ -1613,59 +2034,10 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
     i16mode = (itype - 1) % 4;
     cbp = (((itype - 1) / 4) % 3) << 4 | (itype >= 13 ? 15 : 0);
     cmode = (int)fb_ue(b);
-  } else { /* inter (Table 7-13, 7-17) */
+  } else { /* inter (Tables 7-13, 7-14, 7-17, 7-18) */
     m->type = 0;
-    nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
-    int refs[4] = {0, 0, 0, 0};
-    if (mb_type >= 3) {
-      for (int k = 0; k < 4; k++) {
-        sub[k] = (int)fb_ue(b);
-        if (sub[k] > 3) return fo_fail(d, FO_E_FORMAT, "sub_mb_type");
-      }
-    }
-    int nref = c->nlist;
-    if (mb_type != 4 && nref > 1)
-      for (int k = 0; k < nparts; k++) refs[k] = fb_te(b, nref - 1);
-    for (int k = 0; k < nparts; k++)
-      if (refs[k] < 0 || refs[k] >= nref || !c->list[refs[k]])
-        return fo_fail(d, FO_E_DECODE, "ref_idx names no reference picture");
-    /* motion vectors: partitions in order, prediction as each is decoded */
-    int done = 0;
-    for (int k = 0; k < nparts; k++) {
-      int nsub = 1, pw, ph, x0, y0;
-      if (mb_type == 0) { pw = 16; ph = 16; x0 = y0 = 0; }
-      else if (mb_type == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * k; }
-      else if (mb_type == 2) { pw = 8; ph = 16; x0 = 8 * k; y0 = 0; }
-      else {
-        x0 = 8 * (k & 1);
-        y0 = 8 * (k >> 1);
-        nsub = sub[k] == 0 ? 1 : (sub[k] == 3 ? 4 : 2);
-        pw = sub[k] == 0 || sub[k] == 1 ? 8 : 4;
-        ph = sub[k] == 0 || sub[k] == 2 ? 8 : 4;
-      }
-      for (int s = 0; s < nsub; s++) {
-        int sx = x0, sy = y0;
-        if (mb_type >= 3) {
-          if (sub[k] == 1) sy += 4 * s;
-          else if (sub[k] == 2) sx += 4 * s;
-          else if (sub[k] == 3) { sx += 4 * (s & 1); sy += 4 * (s >> 1); }
-        }
-        int dx = fb_se(b), dy = fb_se(b);
-        int px, py;
-        mv_pred(d, addr, sx, sy, pw, ph, refs[k], done, &px, &py);
-        int vx = px + dx, vy = py + dy;
-        if (vx < -32768 || vx > 32767 || vy < -32768 || vy > 32767) return fo_fail(d, FO_E_FORMAT, "mv range");
-        for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
-          for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) {
-            int blk = yy * 4 + xx;
-            m->refidx[blk] = refs[k];
-            m->refpic[blk] = c->list[refs[k]]->id;
-            m->mv[blk][0] = vx;
-            m->mv[blk][1] = vy;
-            done |= 1 << blk;
-          }
-      }
-    }
+    int rc = inter_mb_cavlc(c, b, addr, mb_type);
+    if (rc) return rc;
   }
   if (m->type != 2) {
     uint32_t code = fb_ue(b);
@@ -1918,14 +2290,14 @@ static int abs_mvd_at(const fo_dec *d, int addr, int xN, int yN, int comp) {
   if (L.mb < 0) return 0;
   const fo_mb *m = &d->mb[L.mb];
   if (m->type != 0) return 0; /* skip, intra */
-  return iabs(m->mvd[(L.yw / 4) * 4 + L.xw / 4][comp]);
+  return iabs(m->mvd[0][(L.yw / 4) * 4 + L.xw / 4][comp]);
 }
 static int ref_gt0_at(const fo_dec *d, int addr, int xN, int yN) {
   fo_loc L = nb_loc(d, addr, xN, yN, 16, 16);
   if (L.mb < 0) return 0;
   const fo_mb *m = &d->mb[L.mb];
   if (m->type != 0) return 0;
-  return m->refidx[(L.yw / 4) * 4 + L.xw / 4] > 0;
+  return m->refidx[0][(L.yw / 4) * 4 + L.xw / 4] > 0;
 }
 /* Intra NxN mode predictor (8.3.1.1 / 8.3.2.1) of the block whose top-left
  * luma sample is (x0, y0); is8: the current block is 8x8 */
@@ -1956,7 +2328,11 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
   int slice = m->slice;
   memset(m, 0, sizeof *m);
   m->slice = slice;
-  for (int i = 0; i < 16; i++) { m->refidx[i] = -1; m->refpic[i] = -1; m->i4[i] = 2; }
+  for (int i = 0; i < 16; i++) {
+    m->refidx[0][i] = m->refidx[1][i] = -1;
+    m->refpic[0][i] = m->refpic[1][i] = -1;
+    m->i4[i] = 2;
+  }
   int mx = addr % d->mbw, my = addr / d->mbw;
   int A = nb_loc(d, addr, -1, 0, 16, 16).mb, B = nb_loc(d, addr, 0, -1, 16, 16).mb;
   const fo_mb *ma = A >= 0 ? &d->mb[A] : NULL, *mbb = B >= 0 ? &d->mb[B] : NULL;
@@ -2046,8 +2422,8 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
       if (refs[i] >= nref || !c->list[refs[i]]) return fo_fail(d, FO_E_DECODE, "ref_idx names no reference picture");
       for (int yy = y0 / 4; yy < (y0 + ph) / 4; yy++)
         for (int xx = x0 / 4; xx < (x0 + pw) / 4; xx++) {
-          m->refidx[yy * 4 + xx] = refs[i];
-          m->refpic[yy * 4 + xx] = c->list[refs[i]]->id;
+          m->refidx[0][yy * 4 + xx] = refs[i];
+          m->refpic[0][yy * 4 + xx] = c->list[refs[i]]->id;
         }
     }
     int done = 0;
@@ -2074,16 +2450,16 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
         for (int comp = 0; comp < 2; comp++)
           dmv[comp] = cab_mvd(k, comp ? 47 : 40, abs_mvd_at(d, addr, sx - 1, sy, comp) + abs_mvd_at(d, addr, sx, sy - 1, comp));
         int px, py;
-        mv_pred(d, addr, sx, sy, pw, ph, refs[i], done, &px, &py);
+        mv_pred(d, 0, addr, sx, sy, pw, ph, refs[i], done, &px, &py);
         int vx = px + dmv[0], vy = py + dmv[1];
         if (vx < -32768 || vx > 32767 || vy < -32768 || vy > 32767) return fo_fail(d, FO_E_FORMAT, "mv range");
         for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
           for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) {
             int blk = yy * 4 + xx;
-            m->mv[blk][0] = vx;
-            m->mv[blk][1] = vy;
-            m->mvd[blk][0] = dmv[0];
-            m->mvd[blk][1] = dmv[1];
+            m->mv[0][blk][0] = vx;
+            m->mv[0][blk][1] = vy;
+            m->mvd[0][blk][0] = dmv[0];
+            m->mvd[0][blk][1] = dmv[1];
             done |= 1 << blk;
           }
       }
@@ -2415,6 +2791,34 @@ int fo_decode(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, in
     if (rc) break;
     d->nslices = nslice;
     if (!(flags & 1)) deblock_picture(d, &cur);
+    /* the picture's motion, for the direct prediction of later B pictures */
+    for (int l = 0; l < 2; l++) {
+      cur.mref[l] = (int8_t *)malloc((size_t)d->nmb * 16);
+      cur.mmv[l] = (int16_t *)malloc((size_t)d->nmb * 32 * sizeof(int16_t));
+      cur.mpic[l] = (int32_t *)malloc((size_t)d->nmb * 16 * sizeof(int32_t));
+      if (!cur.mref[l] || !cur.mmv[l] || !cur.mpic[l]) { rc = fo_fail(d, FO_E_DECODE, "out of memory"); break; }
+      for (int a = 0; a < d->nmb; a++)
+        for (int k = 0; k < 16; k++) {
+          const fo_mb *m = &d->mb[a];
+          int intra = mb_intra(m);
+          cur.mref[l][a * 16 + k] = (int8_t)(intra ? -1 : m->refidx[l][k]);
+          cur.mpic[l][a * 16 + k] = intra ? -1 : m->refpic[l][k];
+          cur.mmv[l][(a * 16 + k) * 2] = (int16_t)m->mv[l][k][0];
+          cur.mmv[l][(a * 16 + k) * 2 + 1] = (int16_t)m->mv[l][k][1];
+        }
+    }
+    if (rc) break;
+    if (getenv("FO_MVDUMP")) { /* debugging aid: per-block motion, for cross-checks with the writer */
+      FILE *df = fopen(getenv("FO_MVDUMP"), "a");
+      for (int a = 0; df && a < d->nmb; a++)
+        for (int k = 0; k < 16; k++)
+          for (int l = 0; l < 2; l++)
+            fprintf(df, "%lld %d %d %d %d %d %d\n", (long long)f, a, k, l, d->mb[a].refidx[l][k],
+                    d->mb[a].refidx[l][k] >= 0 ? d->mb[a].mv[l][k][0] : 0, d->mb[a].refidx[l][k] >= 0 ? d->mb[a].mv[l][k][1] : 0);
+      if (df) fclose(df);
+    }
+    poc_advance(d, &h0);
+    if (d->prev_mmco5) cur.poc = 0; /* 8.2.1: tempPicOrderCnt subtracted */
     int dw = d->W - d->S->crop_l - d->S->crop_r, dh = d->H - d->S->crop_t - d->S->crop_b;
     out_size = (int64_t)dw * dh * 3 / 2;
     out_frame(d, &cur, out + f * out_size);
@@ -2425,15 +2829,15 @@ int fo_decode(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, in
       mark_refs(d, &d->dpb[d->ndpb++], &h0, is_idr);
       /* mark_refs compacts: the current picture is kept (ref != 0) */
     } else {
-      free(cur.y); free(cur.u); free(cur.v);
+      pic_free(&cur);
     }
     memset(&cur, 0, sizeof cur);
   }
   if (rc) {
     *bad_frame = f < n ? f : n - 1;
-    free(cur.y); free(cur.u); free(cur.v);
+    pic_free(&cur);
   }
-  for (int i = 0; i < d->ndpb; i++) { free(d->dpb[i].y); free(d->dpb[i].u); free(d->dpb[i].v); }
+  for (int i = 0; i < d->ndpb; i++) pic_free(&d->dpb[i]);
   free(d->mb);
   free(d);
   return rc;

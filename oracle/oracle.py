@@ -272,8 +272,20 @@ def read_mp4(path) -> dict:
             for _ in range(c2):
                 dts.append(d)
                 d += delta
+        cts = [0] * cnt
+        ct = child(*stbl, "ctts")
+        if ct:  # composition offsets (B-frame reordering): pts = dts + offset
+            ne = struct.unpack(">I", data[ct[0] + 4:ct[0] + 8])[0]
+            i = 0
+            for e in range(ne):
+                c2, off = struct.unpack(">Ii", data[ct[0] + 8 + 8 * e:ct[0] + 16 + 8 * e])
+                for _ in range(c2):
+                    if i < cnt:
+                        cts[i] = off
+                        i += 1
         out.update(timescale=ts, duration=dur, nal_length_size=lsize, sps=sps, pps=pps,
-                   offsets=offsets, sizes=sizes, dts=dts[:cnt])
+                   offsets=offsets, sizes=sizes, dts=dts[:cnt], cts=cts,
+                   pts=[a + b for a, b in zip(dts[:cnt], cts)])
         return out
     raise ValueError("no video track")
 
@@ -511,9 +523,10 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None,
 
 def decode_full(path, flags: int = 0, max_frames: int | None = None):
     """fo_decode (h264_full_oracle.c) over an MP4's first video track: the
-    general CAVLC I/P decoder (intra, residual, quarter-sample motion,
-    deblocking).  flags bit 0 skips the deblocking filter.  Returns (frames
-    uint8 [F, H*3/2, W] display-size NV12, info dict)."""
+    general decoder (CAVLC I/P/B, CABAC I/P; intra, residual, quarter-sample
+    motion, direct and weighted prediction, deblocking).  flags bit 0 skips the
+    deblocking filter.  Returns (frames uint8 [F, H*3/2, W] display-size NV12
+    in presentation order, info dict)."""
     m = read_mp4(path)
     L = lib()
     L.fo_decode.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, C.c_int, C.c_void_p,
@@ -538,7 +551,13 @@ def decode_full(path, flags: int = 0, max_frames: int | None = None):
     if rc != 0:
         raise RuntimeError(f"oracle decode_full rc={rc} at frame {bad.value}: "
                            f"{err.value.decode(errors='replace')}")
-    info = {"width": W, "height": H, "timescale": m["timescale"], "pts": m["dts"][:n]}
+    # display order: frames sorted by presentation time (dts + ctts offset);
+    # without B pictures this is the decoding order
+    pts = m["pts"][:n]
+    order = sorted(range(n), key=lambda i: pts[i])
+    if order != list(range(n)):
+        out = out[order]
+    info = {"width": W, "height": H, "timescale": m["timescale"], "pts": [pts[i] for i in order]}
     return out, info
 
 

@@ -460,10 +460,12 @@ std::string Mp4Writer::open(const char *path) {
   return "";
 }
 
-std::string Mp4Writer::add_sample(const uint8_t *data, size_t n, bool sync) {
+std::string Mp4Writer::add_sample(const uint8_t *data, size_t n, bool sync, uint32_t cts_frames) {
   if (!f_) return "writer not open";
   if (n > 0xffffffffu) return "sample too large";
   if (std::fwrite(data, 1, n, f_) != n) return "write error";
+  cts_.push_back(cts_frames);
+  any_cts_ |= cts_frames != 0;
   offsets_.push_back(pos_);
   sizes_.push_back(static_cast<uint32_t>(n));
   if (sync) sync_.push_back(static_cast<uint32_t>(sizes_.size()));
@@ -483,6 +485,7 @@ std::string Mp4Writer::add_sample_at(int64_t offset, size_t n, bool sync) {
   if (!f_) return "writer not open";
   if (n > 0xffffffffu) return "sample too large";
   if (offset < mdat_start_ || offset + static_cast<int64_t>(n) > pos_) return "sample outside mdat";
+  cts_.push_back(0);
   offsets_.push_back(offset);
   sizes_.push_back(static_cast<uint32_t>(n));
   if (sync) sync_.push_back(static_cast<uint32_t>(sizes_.size()));
@@ -609,6 +612,21 @@ std::string Mp4Writer::finish(int width, int height, int64_t track_timescale,
               put32(v, 1);
               put32(v, static_cast<uint32_t>(nsamp));
               put32(v, static_cast<uint32_t>(sample_delta));
+            }
+            if (any_cts_) {  // composition offsets, run-length coded (version 0)
+              std::vector<std::pair<uint32_t, uint32_t>> runs;
+              for (uint32_t c : cts_) {
+                const uint32_t o = c * static_cast<uint32_t>(sample_delta);
+                if (!runs.empty() && runs.back().second == o) ++runs.back().first;
+                else runs.emplace_back(1u, o);
+              }
+              BoxW ctts(v, "ctts");
+              put32(v, 0);
+              put32(v, static_cast<uint32_t>(runs.size()));
+              for (const auto &r : runs) {
+                put32(v, r.first);
+                put32(v, r.second);
+              }
             }
             if (sync_.size() != nsamp) {
               BoxW stss(v, "stss");

@@ -79,7 +79,9 @@ class Mp4Writer {
  public:
   ~Mp4Writer();
   std::string open(const char *path);
-  std::string add_sample(const uint8_t *data, size_t n, bool sync);
+  // cts_frames: composition offset (ctts) in sample durations; any non-zero
+  // value makes finish() write a ctts box (B-frame reordering)
+  std::string add_sample(const uint8_t *data, size_t n, bool sync, uint32_t cts_frames = 0);
   // Raw bytes appended to mdat (samples in any order); *offset = their file
   // offset, for add_sample_at.
   std::string append(const uint8_t *data, size_t n, int64_t *offset);
@@ -99,6 +101,8 @@ class Mp4Writer {
   std::vector<int64_t> offsets_;
   std::vector<uint32_t> sizes_;
   std::vector<uint32_t> sync_;
+  std::vector<uint32_t> cts_;
+  bool any_cts_ = false;
 };
 
 }  // namespace vts

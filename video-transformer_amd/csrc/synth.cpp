@@ -536,7 +536,7 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
   for (const SynthChunk &c : chunks) {
     size_t pos = 0;
     for (size_t i = 0; i < c.size.size(); ++i) {
-      e = mw.add_sample(c.data.data() + pos, c.size[i], c.sync[i] != 0);
+      e = mw.add_sample(c.data.data() + pos, c.size[i], c.sync[i] != 0, c.cts.empty() ? 0u : c.cts[i]);
       if (!e.empty()) return fail(VTS_E_IO, "%s", e.c_str());
       pos += c.size[i];
     }

@@ -39,6 +39,7 @@ struct SynthChunk {
   std::vector<uint8_t> data;  // samples, back to back
   std::vector<uint32_t> size;
   std::vector<uint8_t> sync;
+  std::vector<uint32_t> cts;  // composition offsets in frames (B pictures); empty = none
   std::vector<int64_t> cuts;  // global frame indices
   int64_t n_idr = 0;
   uint64_t recon_hash = 0;

@@ -21,6 +21,8 @@
 // I_PCM ~1%.  Residuals: random coded_block_pattern, mb_qp_delta, 4x4 blocks
 // of 0..16 coefficients mostly +-1 with escapes up to |2000|.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -46,8 +48,9 @@ struct GMb {
   int i4[16];     // Intra4x4PredMode, raster 4x4 blocks
   int nz[16];     // total_coeff, raster luma 4x4 blocks
   int nzc[2][4];  // chroma AC total_coeff
-  int ref[16];
-  int mv[16][2];
+  int ref[2][16];  // refIdxLX per raster 4x4 block (-1: list unused)
+  int mv[2][16][2];
+  int refd[2][16]; // display index of the picture refIdxLX names (B mode)
 };
 
 struct Loc {
@@ -66,6 +69,7 @@ class FullWriter {
     cip_ = (P.edge_cases & 16) != 0;
   }
   void run();
+  void run_b();
 
  private:
   const vts_synth_params &P_;
@@ -77,6 +81,24 @@ class FullWriter {
   BitWriter *bw_ = nullptr;
   int nref_ = 0;      // active references of the current P slice
   int qp_ = 26;       // QPY of the previous macroblock (mb_qp_delta base)
+  // B mode (edge_cases bit 5): display index of each RefPicListX entry, the
+  // current picture's display index / POC, and the pictures' motion fields
+  bool bmode_ = false;
+  int lst_[2][33] = {};
+  int nlst_[2] = {0, 0};
+  int cur_d_ = 0, cur_poc_ = 0;
+  bool spatial_ = true;
+  struct RefPic {
+    int d, poc, fn;
+    std::vector<GMb> mbs;
+  };
+  std::vector<RefPic> dpb_;
+  const RefPic *col_ = nullptr;   // RefPicList1[0]
+  const RefPic *pic_of(int d) const {
+    for (const RefPic &r : dpb_)
+      if (r.d == d) return &r;
+    return nullptr;
+  }
 
   bool intra(int n) const { return mb_[n].type >= 1 && mb_[n].type <= 3; }
   // 6.4.12 with 6.4.8 availability (same slice, lower address)
@@ -120,7 +142,7 @@ class FullWriter {
     bool avail = false;
     int ref = -1, mvx = 0, mvy = 0;
   };
-  Nb nbmv(int cur, int xN, int yN, int done) const {
+  Nb nbmv(int cur, int xN, int yN, int done, int lx = 0) const {
     Nb r;
     const Loc l = loc(cur, xN, yN, 16);
     if (l.mb < 0) return r;
@@ -129,14 +151,15 @@ class FullWriter {
     r.avail = true;
     const GMb &m = mb_[l.mb];
     if (m.type >= 1 && m.type <= 3) return r;
-    r.ref = m.ref[blk];
-    r.mvx = m.mv[blk][0];
-    r.mvy = m.mv[blk][1];
+    r.ref = m.ref[lx][blk];
+    if (r.ref < 0) return r;
+    r.mvx = m.mv[lx][blk][0];
+    r.mvy = m.mv[lx][blk][1];
     return r;
   }
-  void mvpred(int cur, int x0, int y0, int w, int h, int ref, int done, int *px, int *py) const {
-    Nb a = nbmv(cur, x0 - 1, y0, done), b = nbmv(cur, x0, y0 - 1, done), c = nbmv(cur, x0 + w, y0 - 1, done);
-    if (!c.avail) c = nbmv(cur, x0 - 1, y0 - 1, done);
+  void mvpred(int cur, int x0, int y0, int w, int h, int ref, int done, int *px, int *py, int l = 0) const {
+    Nb a = nbmv(cur, x0 - 1, y0, done, l), b = nbmv(cur, x0, y0 - 1, done, l), c = nbmv(cur, x0 + w, y0 - 1, done, l);
+    if (!c.avail) c = nbmv(cur, x0 - 1, y0 - 1, done, l);
     if (w == 16 && h == 8) {
       if (y0 == 0 && b.ref == ref) { *px = b.mvx; *py = b.mvy; return; }
       if (y0 == 8 && a.ref == ref) { *px = a.mvx; *py = a.mvy; return; }
@@ -294,7 +317,8 @@ class FullWriter {
   }
 
   // valid intra modes
-  void write_intra(int cur, bool in_p) {
+  void write_intra(int cur, bool in_p, int base_b = -1) {
+    const int base = base_b >= 0 ? base_b : (in_p ? 5 : 0);
     GMb &m = mb_[cur];
     const uint32_t r = rng_.below(1000);
     const Loc A = loc(cur, -1, 0, 16), B = loc(cur, 0, -1, 16), D = loc(cur, -1, -1, 16);
@@ -309,7 +333,7 @@ class FullWriter {
     };
     if (r < 10) {  // I_PCM
       m.type = 3;
-      bw_->ue(in_p ? 30 : 25);
+      bw_->ue(static_cast<uint32_t>(base + 25));
       bw_->align_zero();
       uint8_t buf[384];
       for (uint8_t &x : buf) x = static_cast<uint8_t>(rng_.below(256));
@@ -320,7 +344,7 @@ class FullWriter {
     }
     if (r < 600) {  // I_NxN
       m.type = 1;
-      bw_->ue(in_p ? 5 : 0);
+      bw_->ue(static_cast<uint32_t>(base));
       for (int k = 0; k < 16; ++k) {
         const int bx = kBlkX[k], by = kBlkY[k];
         // availability of top / left / top-left samples of this block
@@ -374,7 +398,7 @@ class FullWriter {
     if (la && ta && ca) modes[n++] = 3;
     const int pm = modes[rng_.below(static_cast<uint32_t>(n))];
     const int cc = static_cast<int>(rng_.below(3)), lum = rng_.below(2) ? 15 : 0;
-    bw_->ue(static_cast<uint32_t>((in_p ? 5 : 0) + 1 + pm + 4 * cc + (lum ? 12 : 0)));
+    bw_->ue(static_cast<uint32_t>(base + 1 + pm + 4 * cc + (lum ? 12 : 0)));
     bw_->ue(static_cast<uint32_t>(chroma_mode()));
     write_qp_delta();
     write_residual(cur, (cc << 4) | lum, true);
@@ -422,16 +446,18 @@ class FullWriter {
         }
         int px, py;
         mvpred(cur, sx, sy, pw, ph, refs[k], done, &px, &py);
-        const int tx = (refs[k] + 1) * pan_x + static_cast<int>(rng_.below(13)) - 6;
-        const int ty = (refs[k] + 1) * pan_y + static_cast<int>(rng_.below(13)) - 6;
+        const int dist = bmode_ ? cur_d_ - lst_[0][refs[k]] : refs[k] + 1;
+        const int tx = dist * pan_x + static_cast<int>(rng_.below(13)) - 6;
+        const int ty = dist * pan_y + static_cast<int>(rng_.below(13)) - 6;
         bw_->se(tx - px);
         bw_->se(ty - py);
         for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
           for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
             const int blk = yy * 4 + xx;
-            m.ref[blk] = refs[k];
-            m.mv[blk][0] = tx;
-            m.mv[blk][1] = ty;
+            m.ref[0][blk] = refs[k];
+            m.mv[0][blk][0] = tx;
+            m.mv[0][blk][1] = ty;
+            m.refd[0][blk] = lst_[0][refs[k]];
             done |= 1 << blk;
           }
       }
@@ -455,8 +481,11 @@ class FullWriter {
     for (int i = 0; i < 16; ++i) {
       m.i4[i] = 2;
       m.nz[i] = 0;
-      m.ref[i] = -1;
-      m.mv[i][0] = m.mv[i][1] = 0;
+      for (int l = 0; l < 2; ++l) {
+        m.ref[l][i] = -1;
+        m.refd[l][i] = -1;
+        m.mv[l][i][0] = m.mv[l][i][1] = 0;
+      }
     }
     for (int i = 0; i < 4; ++i) m.nzc[0][i] = m.nzc[1][i] = 0;
   }
@@ -473,9 +502,10 @@ class FullWriter {
           int px, py;
           skipmv(a, &px, &py);
           for (int i = 0; i < 16; ++i) {
-            m.ref[i] = 0;
-            m.mv[i][0] = px;
-            m.mv[i][1] = py;
+            m.ref[0][i] = 0;
+            m.mv[0][i][0] = px;
+            m.mv[0][i][1] = py;
+            m.refd[0][i] = lst_[0][0];
           }
           ++skip_run;
           continue;
@@ -491,6 +521,219 @@ class FullWriter {
     if (is_p && skip_run) bw_->ue(skip_run);
   }
 
+
+  // ---------------------------------------------------------------- B mode
+  static int min_pos(int x, int y) { return (x >= 0 && y >= 0) ? std::min(x, y) : std::max(x, y); }
+  void set_b(GMb &m, int l, int blk, int ref, int mvx, int mvy) {
+    m.ref[l][blk] = ref;
+    m.refd[l][blk] = ref >= 0 ? lst_[l][ref] : -1;
+    m.mv[l][blk][0] = ref >= 0 ? mvx : 0;
+    m.mv[l][blk][1] = ref >= 0 ? mvy : 0;
+  }
+  // 8.4.1.2 direct prediction of the blocks in mask (as the decoder derives it)
+  void direct(int cur, int mask) {
+    GMb &m = mb_[static_cast<size_t>(cur)];
+    int ref[2] = {-1, -1}, mvp[2][2] = {{0, 0}, {0, 0}};
+    bool zero = false;
+    if (spatial_) {
+      for (int l = 0; l < 2; ++l) {
+        Nb a = nbmv(cur, -1, 0, 0, l), b = nbmv(cur, 0, -1, 0, l), c = nbmv(cur, 16, -1, 0, l);
+        if (!c.avail) c = nbmv(cur, -1, -1, 0, l);
+        ref[l] = min_pos(a.ref, min_pos(b.ref, c.ref));
+      }
+      if (ref[0] < 0 && ref[1] < 0) {
+        ref[0] = ref[1] = 0;
+        zero = true;
+      }
+      for (int l = 0; l < 2; ++l)
+        if (ref[l] >= 0 && !zero) mvpred(cur, 0, 0, 16, 16, ref[l], 0, &mvp[l][0], &mvp[l][1], l);
+    }
+    for (int blk = 0; blk < 16; ++blk) {
+      if (!((mask >> blk) & 1)) continue;
+      const int cb = ((blk >> 3) * 3) * 4 + ((blk & 3) >> 1) * 3;  // direct_8x8_inference
+      const GMb &cm = col_->mbs[static_cast<size_t>(cur)];
+      const bool cintra = cm.type >= 1 && cm.type <= 3;
+      const int cl = cm.ref[0][cb] >= 0 ? 0 : 1;
+      const int rcol = cintra ? -1 : cm.ref[cl][cb];
+      const int mcx = rcol < 0 ? 0 : cm.mv[cl][cb][0], mcy = rcol < 0 ? 0 : cm.mv[cl][cb][1];
+      if (spatial_) {
+        const bool cz = rcol == 0 && mcx >= -1 && mcx <= 1 && mcy >= -1 && mcy <= 1;
+        for (int l = 0; l < 2; ++l) {
+          const bool z = zero || ref[l] < 0 || (ref[l] == 0 && cz);
+          set_b(m, l, blk, ref[l], z ? 0 : mvp[l][0], z ? 0 : mvp[l][1]);
+        }
+      } else {
+        int r0 = 0;
+        if (rcol >= 0) {
+          const int dref = cm.refd[cl][cb];
+          r0 = -1;
+          for (int i = 0; i < nlst_[0] && r0 < 0; ++i)
+            if (lst_[0][i] == dref) r0 = i;
+          if (r0 < 0) r0 = 0;  // run_b only picks temporal when every colocated reference is listed
+        }
+        const RefPic *p0 = pic_of(lst_[0][r0]), *p1 = col_;
+        const int tb = std::clamp(cur_poc_ - p0->poc, -128, 127), td = std::clamp(p1->poc - p0->poc, -128, 127);
+        int m0x = mcx, m0y = mcy, m1x = 0, m1y = 0;
+        if (td != 0) {
+          const int tx = (16384 + std::abs(td / 2)) / td;
+          const int dsf = std::clamp((tb * tx + 32) >> 6, -1024, 1023);
+          m0x = (dsf * mcx + 128) >> 8;
+          m0y = (dsf * mcy + 128) >> 8;
+          m1x = m0x - mcx;
+          m1y = m0y - mcy;
+        }
+        set_b(m, 0, blk, r0, m0x, m0y);
+        set_b(m, 1, blk, 0, m1x, m1y);
+      }
+    }
+  }
+
+  // B macroblock (inter): mb_type, sub types, ref_idx_l0/l1, mvd_l0/l1, cbp, residual
+  void write_b_inter(int cur, int pan_x, int pan_y) {
+    GMb &m = mb_[static_cast<size_t>(cur)];
+    m.type = 0;
+    static const uint8_t kPart[22][2] = {{0, 0}, {1, 0}, {2, 0}, {3, 0}, {1, 1}, {1, 1}, {2, 2}, {2, 2},
+                                         {1, 2}, {1, 2}, {2, 1}, {2, 1}, {1, 3}, {1, 3}, {2, 3}, {2, 3},
+                                         {3, 1}, {3, 1}, {3, 2}, {3, 2}, {3, 3}, {3, 3}};
+    static const uint8_t kSub[13][2] = {{0, 0}, {1, 0}, {2, 0}, {3, 0}, {1, 1}, {1, 2}, {2, 1},
+                                        {2, 2}, {3, 1}, {3, 2}, {1, 3}, {2, 3}, {3, 3}};
+    const uint32_t r = rng_.below(100);
+    int mb_type;
+    if (r < 5) mb_type = 0;
+    else if (r < 60) mb_type = 1 + static_cast<int>(rng_.below(3));
+    else if (r < 85) mb_type = 4 + static_cast<int>(rng_.below(18));
+    else mb_type = 22;
+    bw_->ue(static_cast<uint32_t>(mb_type));
+    int shape, pm[4] = {1, 1, 1, 1}, ssh[4] = {0, 0, 0, 0}, subv[4] = {0, 0, 0, 0};
+    if (mb_type == 0) { shape = 0; pm[0] = 0; }
+    else if (mb_type <= 3) { shape = 0; pm[0] = mb_type; }
+    else if (mb_type < 22) { shape = (mb_type & 1) ? 2 : 1; pm[0] = kPart[mb_type][0]; pm[1] = kPart[mb_type][1]; }
+    else shape = 3;
+    const int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
+    if (shape == 3)
+      for (int k = 0; k < 4; ++k) {
+        subv[k] = static_cast<int>(rng_.below(13));
+        pm[k] = kSub[subv[k]][0];
+        ssh[k] = kSub[subv[k]][1];
+      }
+    int refs[2][4];
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < 4; ++k)
+        refs[l][k] = ((pm[k] >> l) & 1) ? (rng_.below(4) ? 0 : static_cast<int>(rng_.below(static_cast<uint32_t>(nlst_[l])))) : -1;
+    // motion in derivation order; mvds kept for the syntax order
+    int mvd[2][4][4][2] = {};
+    int done = 0;
+    for (int k = 0; k < nparts; ++k) {
+      int nsub = 1, pw, ph, x0, y0;
+      if (shape == 0) { pw = ph = 16; x0 = y0 = 0; }
+      else if (shape == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * k; }
+      else if (shape == 2) { pw = 8; ph = 16; x0 = 8 * k; y0 = 0; }
+      else {
+        x0 = 8 * (k & 1);
+        y0 = 8 * (k >> 1);
+        nsub = ssh[k] == 0 ? 1 : (ssh[k] == 3 ? 4 : 2);
+        pw = (ssh[k] == 0 || ssh[k] == 1) ? 8 : 4;
+        ph = (ssh[k] == 0 || ssh[k] == 2) ? 8 : 4;
+      }
+      if (pm[k] == 0) {
+        int bm = 0;
+        for (int yy = y0 / 4; yy < (y0 + ph) / 4; ++yy)
+          for (int xx = x0 / 4; xx < (x0 + pw) / 4; ++xx) bm |= 1 << (yy * 4 + xx);
+        direct(cur, bm);
+        done |= bm;
+        continue;
+      }
+      for (int q = 0; q < nsub; ++q) {
+        int sx = x0, sy = y0;
+        if (shape == 3) {
+          if (ssh[k] == 1) sy += 4 * q;
+          else if (ssh[k] == 2) sx += 4 * q;
+          else if (ssh[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+        }
+        for (int l = 0; l < 2; ++l) {
+          int tx = 0, ty = 0;
+          if (refs[l][k] >= 0) {
+            int px, py;
+            mvpred(cur, sx, sy, pw, ph, refs[l][k], done, &px, &py, l);
+            const int dist = cur_d_ - lst_[l][refs[l][k]];
+            tx = dist * pan_x + static_cast<int>(rng_.below(13)) - 6;
+            ty = dist * pan_y + static_cast<int>(rng_.below(13)) - 6;
+            mvd[l][k][q][0] = tx - px;
+            mvd[l][k][q][1] = ty - py;
+          }
+          for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
+            for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) set_b(m, l, yy * 4 + xx, refs[l][k], tx, ty);
+        }
+        for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
+          for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) done |= 1 << (yy * 4 + xx);
+      }
+    }
+    // syntax order (7.3.5.1 / 7.3.5.2)
+    if (shape == 3)
+      for (int k = 0; k < 4; ++k) bw_->ue(static_cast<uint32_t>(subv[k]));
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < nparts; ++k) {
+        if (refs[l][k] < 0 || nlst_[l] < 2) continue;
+        if (nlst_[l] == 2) bw_->bit(refs[l][k] ? 0 : 1);
+        else bw_->ue(static_cast<uint32_t>(refs[l][k]));
+      }
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < nparts; ++k) {
+        if (refs[l][k] < 0) continue;
+        const int nsub = shape < 3 ? 1 : (ssh[k] == 0 ? 1 : (ssh[k] == 3 ? 4 : 2));
+        for (int q = 0; q < nsub; ++q) {
+          bw_->se(mvd[l][k][q][0]);
+          bw_->se(mvd[l][k][q][1]);
+        }
+      }
+    int cbp = 0;
+    for (int k8 = 0; k8 < 4; ++k8)
+      if (rng_.below(100) < 30) cbp |= 1 << k8;
+    const uint32_t cr = rng_.below(100);
+    cbp |= (cr < 60 ? 0 : (cr < 85 ? 1 : 2)) << 4;
+    int code = 0;
+    while (kCbpInter[code] != cbp) ++code;
+    bw_->ue(static_cast<uint32_t>(code));
+    if (cbp) write_qp_delta();
+    write_residual(cur, cbp, false);
+  }
+
+  void write_slice_data_b(int first, int last, int slice, int pan_x, int pan_y) {
+    uint32_t skip_run = 0;
+    for (int a = first; a < last; ++a) {
+      reset_mb(a, slice);
+      const uint32_t r = rng_.below(1000);
+      if (r < 350) {  // B_Skip
+        mb_[static_cast<size_t>(a)].type = 4;
+        direct(a, 0xffff);
+        ++skip_run;
+        continue;
+      }
+      bw_->ue(skip_run);
+      skip_run = 0;
+      if (r < 950) write_b_inter(a, pan_x, pan_y);
+      else write_intra_b(a);
+    }
+    if (skip_run) bw_->ue(skip_run);
+  }
+  void write_intra_b(int a) { write_intra(a, true, 23); }
+
+  // 8.2.4.2.3 list initialisation (no modification) from the writer's DPB
+  void b_lists() {
+    std::vector<const RefPic *> st;
+    for (const RefPic &r : dpb_) st.push_back(&r);
+    std::sort(st.begin(), st.end(), [](const RefPic *a, const RefPic *b) { return a->poc < b->poc; });
+    std::vector<int> l0, l1;
+    for (int i = static_cast<int>(st.size()) - 1; i >= 0; --i) if (st[i]->poc < cur_poc_) l0.push_back(st[i]->d);
+    for (const RefPic *r : st) if (r->poc > cur_poc_) l0.push_back(r->d);
+    for (const RefPic *r : st) if (r->poc > cur_poc_) l1.push_back(r->d);
+    for (int i = static_cast<int>(st.size()) - 1; i >= 0; --i) if (st[i]->poc < cur_poc_) l1.push_back(st[i]->d);
+    if (l1.size() > 1 && l0 == l1) std::swap(l1[0], l1[1]);
+    for (size_t i = 0; i < l0.size(); ++i) lst_[0][i] = l0[i];
+    for (size_t i = 0; i < l1.size(); ++i) lst_[1][i] = l1[i];
+    nlst_[0] = static_cast<int>(l0.size());
+    nlst_[1] = static_cast<int>(l1.size());
+  }
 };
 
 void FullWriter::run() {
@@ -598,11 +841,236 @@ void FullWriter::run() {
   }
 }
 
+
+// B mode (edge_cases bit 5): mini-GOPs of 1..4 display frames coded anchor
+// first (P, reference), then the B pictures between (the middle one of three a
+// reference picture half the time: a B-picture colocated for the others), POC
+// type 0 (2 x display distance from the IDR, 6-bit lsb so it wraps), list
+// initialisation by POC, spatial or (bit 8) temporal direct prediction,
+// explicit (bit 6) or implicit (bit 7) weighted prediction.  The MP4 carries
+// composition offsets (display = decode position + 2 - reorder).
+void FullWriter::run_b() {
+  bmode_ = true;
+  const int ec = P_.edge_cases;
+  const double fps = double(P_.fps_num) / P_.fps_den;
+  const int gop_max = std::max(1, static_cast<int>(P_.gop_max_s * fps));
+  auto scene_len = [&]() {
+    const double lo = std::max(P_.cut_min_s, 1.0 / fps), hi = std::max(P_.cut_max_s, lo);
+    return std::max<int64_t>(1, static_cast<int64_t>((lo + (hi - lo) * rng_.uniform()) * fps + 0.5));
+  };
+  const int64_t nf = ck_->nf;
+  std::vector<uint8_t> cut(static_cast<size_t>(nf), 0);
+  std::vector<int> pxs(static_cast<size_t>(nf)), pys(static_cast<size_t>(nf));
+  {
+    int64_t next_cut = scene_len();
+    int pan_x = 0, pan_y = 0;
+    for (int64_t f = 0; f < nf; ++f) {
+      const bool c = f == 0 || f == next_cut;
+      if (f == next_cut) next_cut = f + scene_len();
+      cut[static_cast<size_t>(f)] = c;
+      if (c && ck_->f0 + f > 0) ck_->cuts.push_back(ck_->f0 + f);
+      if (f % P_.fps_num == 0 || c) {
+        const int m = 4 * P_.max_motion;
+        pan_x = static_cast<int>(rng_.below(static_cast<uint32_t>(2 * m + 1))) - m;
+        pan_y = static_cast<int>(rng_.below(static_cast<uint32_t>(2 * m + 1))) - m;
+        if (rng_.below(4) == 0) pan_x = pan_y = 0;
+      }
+      pxs[static_cast<size_t>(f)] = pan_x;
+      pys[static_cast<size_t>(f)] = pan_y;
+    }
+  }
+  struct Pic {
+    int64_t d;
+    int kind;  // 0 IDR, 1 P, 2 B
+    bool ref;
+  };
+  std::vector<Pic> order;
+  {
+    int64_t d = 0, since_idr = 0;
+    while (d < nf) {
+      if (cut[static_cast<size_t>(d)] || since_idr >= gop_max) {
+        order.push_back({d, 0, true});
+        since_idr = 1;
+        ++d;
+        continue;
+      }
+      int64_t lim = d;
+      while (lim < nf && !cut[static_cast<size_t>(lim)] && since_idr + (lim - d) < gop_max) ++lim;
+      const int64_t g = std::min<int64_t>(1 + rng_.below(4), lim - d);
+      const int64_t a = d + g - 1;
+      order.push_back({a, 1, true});
+      if (g >= 4 && rng_.below(2)) {
+        const int64_t mid = d + (g - 1) / 2;
+        order.push_back({mid, 2, true});
+        for (int64_t x = d; x < a; ++x)
+          if (x != mid) order.push_back({x, 2, false});
+      } else {
+        for (int64_t x = d; x < a; ++x) order.push_back({x, 2, rng_.below(8) == 0});
+      }
+      since_idr += g;
+      d = a + 1;
+    }
+  }
+  const int spr = P_.slices_per_row;
+  const int slice_mbs = spr > 0 ? (mbw_ + spr - 1) / spr : nmb_;
+  int frame_num = 0, prev_ref_fn = 0, idr_id = ck_->idr_id_base;
+  int64_t d_idr = 0;
+  std::vector<uint8_t> sample;
+  for (size_t p = 0; p < order.size(); ++p) {
+    const Pic &pc = order[p];
+    const bool idr = pc.kind == 0, is_b = pc.kind == 2;
+    cur_d_ = static_cast<int>(pc.d);
+    if (idr) {
+      frame_num = 0;
+      dpb_.clear();
+      d_idr = pc.d;
+    } else {
+      frame_num = (prev_ref_fn + 1) & ((1 << kLog2MaxFrameNum) - 1);
+    }
+    cur_poc_ = static_cast<int>(2 * (pc.d - d_idr));
+    // reference lists (no modification in B mode)
+    if (is_b) {
+      b_lists();
+    } else {
+      std::vector<const RefPic *> st;
+      for (const RefPic &r : dpb_) st.push_back(&r);
+      auto wrap = [&](const RefPic *r) { return r->fn > frame_num ? r->fn - (1 << kLog2MaxFrameNum) : r->fn; };
+      std::stable_sort(st.begin(), st.end(), [&](const RefPic *a, const RefPic *b) { return wrap(a) > wrap(b); });
+      for (size_t i = 0; i < st.size(); ++i) lst_[0][i] = st[i]->d;
+      nlst_[0] = static_cast<int>(st.size());
+      nlst_[1] = 0;
+    }
+    if (!idr) {
+      nlst_[0] = 1 + static_cast<int>(rng_.below(static_cast<uint32_t>(nlst_[0])));
+      if (is_b) nlst_[1] = 1 + static_cast<int>(rng_.below(static_cast<uint32_t>(nlst_[1])));
+    }
+    col_ = is_b ? pic_of(lst_[1][0]) : nullptr;
+    spatial_ = true;
+    if (is_b && (ec & 256) && rng_.below(2)) {
+      // temporal direct only when every colocated reference is in RefPicList0
+      bool ok = true;
+      for (const GMb &cm : col_->mbs)
+        for (int b = 0; b < 16 && ok; ++b)
+          for (int l = 0; l < 2; ++l) {
+            if (cm.ref[l][b] < 0 || (cm.type >= 1 && cm.type <= 3)) continue;
+            bool found = false;
+            for (int i = 0; i < nlst_[0]; ++i) found |= lst_[0][i] == cm.refd[l][b];
+            ok &= found;
+          }
+      spatial_ = !ok;
+    }
+    const int slice_type = idr ? (rng_.below(2) ? 7 : 2) : (is_b ? (rng_.below(2) ? 6 : 1) : (rng_.below(2) ? 5 : 0));
+    const int pic_qp = 20 + static_cast<int>(rng_.below(17));
+    const bool wp = !idr && (ec & 64) != 0;   // explicit weights (weighted_pred_flag / weighted_bipred_idc 1)
+    sample.clear();
+    int slice = 0;
+    for (int first = 0; first < nmb_; ++slice) {
+      const int row_end = spr > 0 ? ((first / mbw_) + 1) * mbw_ : nmb_;
+      const int last = std::min(first + slice_mbs, row_end);
+      BitWriter bw;
+      bw_ = &bw;
+      bw.ue(static_cast<uint32_t>(first));
+      bw.ue(static_cast<uint32_t>(slice_type));
+      bw.ue(0);
+      bw.u(kLog2MaxFrameNum, static_cast<uint32_t>(frame_num));
+      if (idr) bw.ue(static_cast<uint32_t>(idr_id));
+      bw.u(6, static_cast<uint32_t>(cur_poc_ & 63));  // pic_order_cnt_lsb
+      if (is_b) bw.u(1, spatial_ ? 1 : 0);
+      if (!idr) {
+        nref_ = nlst_[0];
+        bw.u(1, 1);  // num_ref_idx_active_override_flag
+        bw.ue(static_cast<uint32_t>(nlst_[0] - 1));
+        if (is_b) bw.ue(static_cast<uint32_t>(nlst_[1] - 1));
+        bw.u(1, 0);  // ref_pic_list_modification_flag_l0
+        if (is_b) bw.u(1, 0);
+      }
+      if (wp) {  // pred_weight_table (7.3.3.2)
+        const int lwd = static_cast<int>(rng_.below(7)), cwd = static_cast<int>(rng_.below(7));
+        bw.ue(static_cast<uint32_t>(lwd));
+        bw.ue(static_cast<uint32_t>(cwd));
+        for (int l = 0; l < 1 + is_b; ++l)
+          for (int i = 0; i < nlst_[l]; ++i) {
+            if (rng_.below(3)) {
+              bw.u(1, 1);
+              bw.se((1 << lwd) + static_cast<int>(rng_.below(17)) - 8);
+              bw.se(static_cast<int>(rng_.below(21)) - 10);
+            } else {
+              bw.u(1, 0);
+            }
+            if (rng_.below(2)) {
+              bw.u(1, 1);
+              for (int j = 0; j < 2; ++j) {
+                bw.se((1 << cwd) + static_cast<int>(rng_.below(9)) - 4);
+                bw.se(static_cast<int>(rng_.below(11)) - 5);
+              }
+            } else {
+              bw.u(1, 0);
+            }
+          }
+      }
+      if (pc.ref) {  // dec_ref_pic_marking
+        if (idr) { bw.u(1, 0); bw.u(1, 0); }
+        else bw.u(1, 0);
+      }
+      qp_ = pic_qp;
+      bw.se(pic_qp - 26);
+      const uint32_t dr = rng_.below(20);
+      const int didc = dr < 16 ? 0 : (dr < 18 ? 2 : 1);
+      bw.ue(static_cast<uint32_t>(didc));
+      if (didc != 1) {
+        bw.se(static_cast<int>(rng_.below(7)) - 3);
+        bw.se(static_cast<int>(rng_.below(7)) - 3);
+      }
+      const int pxn = pxs[static_cast<size_t>(pc.d)], pyn = pys[static_cast<size_t>(pc.d)];
+      if (is_b) write_slice_data_b(first, last, slice, pxn, pyn);
+      else write_slice_data(first, last, slice, !idr, pxn, pyn);
+      bw.trailing();
+      append_nal(sample, idr ? 0x65 : (pc.ref ? 0x41 : 0x01), bw.data());
+      first = last;
+    }
+    bw_ = nullptr;
+    if (idr) {
+      idr_id ^= 1;
+      ++ck_->n_idr;
+    }
+    if (pc.ref) {
+      if (static_cast<int>(dpb_.size()) >= kMaxRefs) {  // sliding window (8.2.5.3)
+        size_t o = 0;
+        auto wrap = [&](const RefPic &r) { return r.fn > frame_num ? r.fn - (1 << kLog2MaxFrameNum) : r.fn; };
+        for (size_t i = 1; i < dpb_.size(); ++i)
+          if (wrap(dpb_[i]) < wrap(dpb_[o])) o = i;
+        dpb_.erase(dpb_.begin() + static_cast<int64_t>(o));
+      }
+      dpb_.push_back(RefPic{cur_d_, cur_poc_, frame_num, mb_});
+      prev_ref_fn = frame_num;
+    }
+    ck_->data.insert(ck_->data.end(), sample.begin(), sample.end());
+    ck_->size.push_back(static_cast<uint32_t>(sample.size()));
+    ck_->sync.push_back(idr ? 1 : 0);
+    ck_->cts.push_back(static_cast<uint32_t>(pc.d - static_cast<int64_t>(p) + 2));
+    if (const char *dump = std::getenv("VTS_SYNTH_MVDUMP")) {  // debugging aid (see the oracle's FO_MVDUMP)
+      if (FILE *df = std::fopen(dump, "a")) {
+        for (int a = 0; a < nmb_; ++a)
+          for (int k = 0; k < 16; ++k)
+            for (int l = 0; l < 2; ++l) {
+              const GMb &m = mb_[static_cast<size_t>(a)];
+              const bool in = m.type >= 1 && m.type <= 3;
+              const int r = in ? -1 : m.ref[l][k];
+              std::fprintf(df, "%lld %d %d %d %d %d %d\n", static_cast<long long>(ck_->f0 + static_cast<int64_t>(p)), a,
+                           k, l, r, r >= 0 ? m.mv[l][k][0] : 0, r >= 0 ? m.mv[l][k][1] : 0);
+            }
+        std::fclose(df);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 void encode_chunk_full(const vts_synth_params &P, SynthChunk *ck) {
   FullWriter w(P, ck);
-  w.run();
+  if (P.edge_cases & 32) w.run_b();
+  else w.run();
 }
 
 // Constrained Baseline SPS / PPS of the full-syntax streams: 3 reference
@@ -612,13 +1080,19 @@ void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t
                        std::vector<uint8_t> *pps_nal) {
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int crop_r = mbw * 16 - P.width, crop_b = mbh * 16 - P.height;
+  const bool bm = (P.edge_cases & 32) != 0;
   BitWriter s;
-  s.u(8, 66);
-  s.u(8, 0xC0);
+  s.u(8, bm ? 77 : 66);  // B pictures: Main profile
+  s.u(8, bm ? 0x00 : 0xC0);
   s.u(8, static_cast<uint32_t>(level));
   s.ue(0);
   s.ue(kLog2MaxFrameNum - 4);
-  s.ue(2);
+  if (bm) {
+    s.ue(0);  // pic_order_cnt_type 0
+    s.ue(2);  // log2_max_pic_order_cnt_lsb_minus4: 6-bit lsb
+  } else {
+    s.ue(2);
+  }
   s.ue(kMaxRefs);
   s.u(1, 0);
   s.ue(static_cast<uint32_t>(mbw - 1));
@@ -647,8 +1121,8 @@ void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t
   p.ue(0);
   p.ue(kPpsRefDefault - 1);
   p.ue(0);
-  p.u(1, 0);
-  p.u(2, 0);
+  p.u(1, (bm && (P.edge_cases & 64)) ? 1 : 0);                           // weighted_pred_flag
+  p.u(2, !bm ? 0u : ((P.edge_cases & 64) ? 1u : ((P.edge_cases & 128) ? 2u : 0u)));  // weighted_bipred_idc
   p.se(0);                                     // pic_init_qp 26
   p.se(0);
   p.se(static_cast<int>(P.seed % 5) - 2);      // chroma_qp_index_offset

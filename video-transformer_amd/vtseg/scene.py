@@ -266,9 +266,14 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 hash_frames: bool = False, pcm_zero_runs: bool = False,
                 odd_motion: bool = False, drop_last_slice: bool = False,
                 nonref_refresh: bool = False, chunks: int = 0, coding: str = "subset",
-                constrained_intra: bool = False) -> dict:
+                constrained_intra: bool = False, bframes: bool = False,
+                weighted: str | None = None, temporal_direct: bool = False) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
-    and the ground-truth scene-cut frames."""
+    and the ground-truth scene-cut frames.  coding="full" only: ``bframes`` codes
+    B pictures (Main profile, POC type 0, composition offsets in the MP4),
+    ``weighted`` = "explicit" (pred_weight_table in P and B slices) or
+    "implicit" (weighted_bipred_idc 2), ``temporal_direct`` mixes temporal with
+    spatial direct prediction."""
     p = _lib.SynthParams()
     p.width, p.height, p.fps_num, p.fps_den = width, height, fps, 1
     p.n_frames, p.seed = n_frames, seed
@@ -281,6 +286,11 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     p.coding = {"subset": 0, "full": 1}[coding]
     if constrained_intra:
         p.edge_cases |= 16
+    if bframes or weighted or temporal_direct:
+        if coding != "full":
+            raise ValueError("B pictures / weighted prediction need coding='full'")
+        p.edge_cases |= 32 | {None: 0, "explicit": 64, "implicit": 128}[weighted] | \
+            (256 if temporal_direct else 0)
     info = _lib.SynthInfo()
     cuts = (C.c_int64 * max(n_frames, 1))()
     _lib.check(_lib.lib().vts_synth_write(str(path).encode(), C.byref(p), C.byref(info),
