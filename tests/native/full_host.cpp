@@ -5,6 +5,7 @@
 // intra macroblocks and deblocking along the x + 2y wavefront — on host
 // memory.  TEST INFRASTRUCTURE (tests/test_full_host.py compares it with the
 // oracle); the product never runs the decoder on the CPU.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -60,6 +61,17 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   e = sched_build(sps, pps, es.data(), off, t.size, t.nal_length_size, &frames, &slices);
   if (!e.empty()) return bad(e);
   const int n = static_cast<int>(frames.size());
+  // presentation order: rank of dts + composition offset
+  std::vector<int> disp(static_cast<size_t>(n));
+  {
+    std::vector<int> ord(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) ord[static_cast<size_t>(i)] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+      return t.dts[static_cast<size_t>(a)] + t.cts_offset[static_cast<size_t>(a)] <
+             t.dts[static_cast<size_t>(b)] + t.cts_offset[static_cast<size_t>(b)];
+    });
+    for (int i = 0; i < n; ++i) disp[static_cast<size_t>(ord[static_cast<size_t>(i)])] = i;
+  }
   const int mbw = sps.mb_width, mbh = sps.mb_height, nmb = mbw * mbh;
   const int pitch = mbw * 16, ch = mbh * 16;
   const int64_t stride = static_cast<int64_t>(pitch) * ch * 3 / 2;
@@ -72,6 +84,10 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   std::vector<MbRec> recs(static_cast<size_t>(nmb) * n);
   std::vector<uint16_t> ilvl(static_cast<size_t>(nmb) * n);
   std::vector<FullSlice> fs(slices.size());
+  std::vector<SliceExt> exts;
+  bool bframes = false;
+  for (const SchedFrame &fr : frames) bframes |= fr.has_b;
+  std::vector<MbRecB> recs1(bframes ? static_cast<size_t>(nmb) * n : 0);
   uint32_t arena_blocks = 0;
   for (size_t i = 0; i < slices.size(); ++i) {
     const SchedSlice &s = slices[i];
@@ -94,6 +110,28 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     d.arena_cap = static_cast<uint32_t>(cap);
     arena_blocks += static_cast<uint32_t>(cap);
     for (int r = 0; r < 32; ++r) d.ref_slot[r] = static_cast<int16_t>(s.ref[r] >= 0 ? s.ref[r] : -1);
+    d.ext = -1;
+    if (s.needs_ext()) {
+      SliceExt x;
+      std::memset(&x, 0, sizeof x);
+      x.num_ref1 = s.num_ref1;
+      x.direct_spatial = s.direct_spatial;
+      x.wmode = s.wmode;
+      x.lwd = s.lwd;
+      x.cwd = s.cwd;
+      x.col_short = s.col_short;
+      x.poc = s.poc;
+      x.lt0 = s.lt0;
+      x.lt1 = s.lt1;
+      for (int r = 0; r < 32; ++r) {
+        x.ref_slot1[r] = static_cast<int16_t>(s.ref1[r] >= 0 ? s.ref1[r] : -1);
+        x.poc0[r] = s.poc0[r];
+        x.poc1[r] = s.poc1[r];
+      }
+      std::memcpy(x.w, s.w, sizeof x.w);
+      d.ext = static_cast<int32_t>(exts.size());
+      exts.push_back(x);
+    }
   }
   std::vector<int16_t> arena(static_cast<size_t>(arena_blocks) * 16 + 16);
   FullParams P{};
@@ -104,6 +142,8 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   P.cqp_off2 = facts.cqp_off2;
   P.cabac = pps.entropy_coding_mode;
   P.t8mode = facts.transform_8x8;
+  P.bframes = bframes;
+  P.direct8x8 = sps.direct_8x8_inference;
   const uint32_t epoch = 7;
   for (int fi = 0; fi < n; ++fi) {
     const SchedFrame &fr = frames[static_cast<size_t>(fi)];
@@ -111,16 +151,27 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     uint32_t errs = 0;
     for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
       full::FullScratch sc;
+      const FullSlice &fsl = fs[static_cast<size_t>(si)];
+      full::BCtx bc{};
+      bc.recs1 = bframes ? recs1.data() + static_cast<size_t>(fi) * nmb : nullptr;
+      bc.x = fsl.ext >= 0 ? &exts[static_cast<size_t>(fsl.ext)] : nullptr;
+      if (fsl.is_p == kSliceB) {
+        const int col = exts[static_cast<size_t>(fsl.ext)].ref_slot1[0];
+        bc.col = recs.data() + static_cast<size_t>(col) * nmb;
+        bc.col1 = recs1.data() + static_cast<size_t>(col) * nmb;
+      }
       errs |= P.cabac ? full::parse_slice_cabac(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P,
                                                 fr_recs, ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(),
-                                                epoch, &sc)
+                                                epoch, &sc, bc)
                       : full::parse_slice_full(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P,
                                                fr_recs, ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(),
-                                               epoch, &sc);
+                                               epoch, &sc, bc);
     }
     if (errs) return bad("frame " + std::to_string(fi) + ": parse: " + describe_decode_error(errs));
     full::ReconCtx c{};
     c.recs = fr_recs;
+    c.recs1 = bframes ? recs1.data() + static_cast<size_t>(fi) * nmb : nullptr;
+    c.exts = exts.data();
     c.arena = arena.data();
     c.slices = fs.data();
     c.surf = surf.data();
@@ -159,8 +210,8 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
           const int x = tt - 2 * y;
           if (x >= 0 && x < mbw) full::deblock_mb(c, fi, y * mbw + x);
         }
-    // display-size NV12 (crop right / bottom)
-    uint8_t *o = out + static_cast<int64_t>(fi) * W * H * 3 / 2;
+    // display-size NV12 (crop right / bottom), in presentation order
+    uint8_t *o = out + static_cast<int64_t>(disp[static_cast<size_t>(fi)]) * W * H * 3 / 2;
     const uint8_t *Y = surf.data() + static_cast<int64_t>(fi) * stride;
     for (int y = 0; y < H; ++y) std::memcpy(o + static_cast<int64_t>(y) * W, Y + static_cast<int64_t>(y) * pitch, W);
     for (int y = 0; y < H / 2; ++y)

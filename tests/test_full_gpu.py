@@ -147,3 +147,68 @@ def test_real_cabac_subset_decoder_refuses():
     with pytest.raises(VtsegError):
         with scene.VideoScorer(path, decoder="subset") as v:
             v.score()
+
+
+B_STREAMS = [
+    ("spatial", dict(width=176, height=144)),
+    ("explicit", dict(width=176, height=144, weighted="explicit")),
+    ("implicit", dict(width=176, height=144, weighted="implicit")),
+    ("temporal", dict(width=176, height=144, temporal_direct=True)),
+    ("slices", dict(width=176, height=144, slices_per_row=2, weighted="implicit", temporal_direct=True)),
+    ("hd720", dict(width=1280, height=720, slices_per_row=0, weighted="explicit", temporal_direct=True)),
+]
+
+
+@pytest.mark.parametrize("name,kw", B_STREAMS, ids=[b[0] for b in B_STREAMS])
+def test_b_pictures_bit_exact(tmp_path, name, kw):
+    """Main-profile B streams (reordered mini-GOPs with B reference pictures,
+    spatial / temporal direct, every B partition shape, explicit / implicit
+    weighted prediction, explicitly weighted P slices): frames in presentation
+    order, thumbnails, histograms, SADs and scores equal the oracle; the
+    parse runs B pictures one launch after their colocated pictures."""
+    _require_gpu()
+    n = 30 if kw["height"] >= 720 else 45
+    path = tmp_path / f"b_{name}.mp4"
+    scene.synth_write(path, n_frames=n, coding="full", bframes=True, cut_min_s=0.5, cut_max_s=1.2,
+                      gop_max_s=0.8, seed=11, chunks=1, **kw)
+    frames, _ = oracle.decode_full(path)
+    W, H = kw["width"], kw["height"]
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 4)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+        assert _first_diff(got, frames) == []
+        rgb = np.stack([v.thumbnail_rgb(i, 4) for i in range(n)]).reshape(-1)
+        assert np.array_equal(rgb, ref["rgb"])
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+
+
+def test_b_pictures_windows_and_rings(tmp_path):
+    """A B stream in many windows (closed mini-GOP runs: the same frames in
+    decode and presentation order) on two rings equals the oracle."""
+    _require_gpu()
+    n = 120
+    path = tmp_path / "bw.mp4"
+    scene.synth_write(path, width=160, height=96, n_frames=n, coding="full", bframes=True,
+                      weighted="explicit", chunks=4, cut_min_s=0.5, cut_max_s=1.5, gop_max_s=0.6, seed=9)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 160, 96, 160, 96, 4)
+    with scene.VideoScorer(path, window_frames=30, n_streams=2) as v:
+        assert v.general() and v.windows() >= 3
+        res = v.score()
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+        assert np.array_equal(v.frame_nv12(n - 1).reshape(frames[-1].shape), frames[-1])
+
+
+def test_b_stream_refused_by_the_subset_decoder(tmp_path):
+    _require_gpu()
+    path = tmp_path / "b.mp4"
+    scene.synth_write(path, width=64, height=48, n_frames=20, coding="full", bframes=True)
+    with pytest.raises(VtsegError):
+        with scene.VideoScorer(path, decoder="subset") as v:
+            v.score()

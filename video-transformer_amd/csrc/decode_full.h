@@ -17,6 +17,8 @@ struct FullParseArgs {
   uint32_t epoch;
   int32_t _pad;
   MbRec *recs;               // ring: [slot][mb]
+  MbRecB *recs1;             // ring: [slot][mb] list-1 halves (P.bframes), else null
+  const SliceExt *exts;      // the window's SliceExt records
   uint16_t *ilvl;            // ring: [slot][mb] intra dependency levels
   int16_t *arena;            // ring's coefficient arena
   uint32_t *err;
@@ -36,6 +38,8 @@ static_assert(sizeof(DbkInfo) == 32, "DbkInfo layout");
 struct FullReconArgs {
   const int4 *frames;        // (slot, -, -, -) per picture of the launch
   const MbRec *recs;
+  const MbRecB *recs1;       // list-1 halves (P.bframes), else null
+  const SliceExt *exts;      // the window's SliceExt records (FullSlice.ext)
   const uint16_t *ilvl;
   const int16_t *arena;
   const FullSlice *slices;   // the window's slices (MbRec.slice indexes them)

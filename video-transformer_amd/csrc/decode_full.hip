@@ -49,11 +49,19 @@ __global__ void __launch_bounds__(1) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
   const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
+  full::BCtx bc{};
+  if (P.bframes) bc.recs1 = a.recs1 + s.slot * nmb;
+  if (s.ext >= 0) bc.x = a.exts + s.ext;
+  if (s.is_p == kSliceB && bc.x) {  // colocated picture: RefPicList1[0], parsed by an earlier launch
+    const int col = bc.x->ref_slot1[0];
+    bc.col = a.recs + col * nmb;
+    bc.col1 = a.recs1 + col * nmb;
+  }
   const uint32_t e =
       P.cabac ? full::parse_slice_cabac(a.es, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
-                                        a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch)
+                                        a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch, bc)
               : full::parse_slice_full(a.es, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
-                                       a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch);
+                                       a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch, bc);
   if (e) atomicOr(a.err, e);
 }
 
@@ -268,6 +276,61 @@ __device__ __forceinline__ MbHdr load_hdr(const MbRec *m) {
   return h;
 }
 
+// one list's prediction of a 4x4 luma block at (x0, y0) and its 2x2 Cb / Cr at
+// (cx, cy) from the picture in ring slot rs, motion mvw = mvx | mvy << 16
+// (8.4.2.2.1 luma 6-tap, 8.4.2.2.2 chroma bilinear; windows edge-clamped)
+__device__ __forceinline__ void pred_ref(const FullReconArgs &a, int rs, uint32_t mvw, int x0, int y0, int cx, int cy,
+                                         int W, int H, int (&pv)[16], int (&cpred)[2][4]) {
+  const int mvx = static_cast<int16_t>(mvw & 0xffff), mvy = static_cast<int16_t>(mvw >> 16);
+  const int pitch = a.pitch;
+  const uint8_t *R = a.surf + static_cast<int64_t>(rs) * a.frame_stride;
+  // luma
+  uint32_t w[9][3];
+  load_win9(R, pitch, W, H, x0 + (mvx >> 2) - 2, y0 + (mvy >> 2) - 2, w);
+  // chroma window: 3 rows x (Cb, Cr) x 3 samples at (cx0, cy0)
+  const int CW = W / 2, CH = H / 2;
+  const int cx0 = cx + (mvx >> 3), cy0 = cy + (mvy >> 3);
+  const uint8_t *RUV = R + a.uv_off;
+  uint32_t cwn[3][2];
+  if (cx0 >= 0 && cx0 + 2 < CW && cy0 >= 0 && cy0 + 2 < CH) {
+    const int o = 2 * cx0, sh = o & 3;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const uint32_t *q = reinterpret_cast<const uint32_t *>(RUV + static_cast<int64_t>(cy0 + r) * pitch + (o & ~3));
+      const uint32_t d0 = q[0], d1 = q[1];
+      cwn[r][0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+      cwn[r][1] = d1 >> (8 * sh);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const uint8_t *row = RUV + static_cast<int64_t>(min(max(cy0 + r, 0), CH - 1)) * pitch;
+      uint32_t v[2] = {0, 0};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int xx = 2 * min(max(cx0 + c, 0), CW - 1);
+        v[(2 * c) >> 2] |= static_cast<uint32_t>(row[xx]) << (((2 * c) & 3) * 8);
+        v[(2 * c + 1) >> 2] |= static_cast<uint32_t>(row[xx + 1]) << (((2 * c + 1) & 3) * 8);
+      }
+      cwn[r][0] = v[0];
+      cwn[r][1] = v[1];
+    }
+  }
+  luma_pred4(w, mvx & 3, mvy & 3, pv);
+  const int fx = mvx & 7, fy = mvy & 7;
+  auto cpx = [&](int r, int i) { return static_cast<int>((cwn[r][i >> 2] >> ((i & 3) * 8)) & 255); };
+#pragma unroll
+  for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int A = cpx(y, 2 * x + pl), B = cpx(y, 2 * x + 2 + pl);
+        const int C = cpx(y + 1, 2 * x + pl), D = cpx(y + 1, 2 * x + 2 + pl);
+        cpred[pl][y * 2 + x] = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
+      }
+}
+
 // ------------------------------------------------------- inter / I_PCM blocks
 // grid (ceil(nmb / 16), pictures of the level); lane = (macroblock, raster 4x4 block b)
 __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a) {
@@ -304,49 +367,38 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
     return;
   }
   const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
-  const int rs = h.ref_slot[p8];
-  if (rs < 0) {
+  const int rs0 = h.ref_slot[p8];
+  const uint32_t mvw = reinterpret_cast<const uint32_t *>(rec)[16 + b];
+  int rs1 = -1, r1 = -1;
+  uint32_t mvw1 = 0;
+  if (a.P.bframes) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a.recs1 + static_cast<int64_t>(slot) * nmb + mb);
+    const uint32_t w0 = q[0], wsl = q[1 + (p8 >> 1)];
+    mvw1 = q[16 + b];
+    r1 = static_cast<int8_t>((w0 >> (8 * p8)) & 255);
+    rs1 = static_cast<int16_t>((wsl >> (16 * (p8 & 1))) & 0xffff);
+    if (rs1 < 0) r1 = -1;
+  }
+  const int r0 = rs0 >= 0 ? static_cast<int8_t>((h.refs >> (8 * p8)) & 255) : -1;
+  if (rs0 < 0 && rs1 < 0) {
     atomicOr(a.err, static_cast<uint32_t>(DEC_E_NO_REF));
     return;
   }
-  const uint32_t mvw = reinterpret_cast<const uint32_t *>(rec)[16 + b];
-  const int mvx = static_cast<int16_t>(mvw & 0xffff), mvy = static_cast<int16_t>(mvw >> 16);
-  const uint8_t *R = a.surf + static_cast<int64_t>(rs) * a.frame_stride;
   const int W = mbw * 16, H = mbh * 16;
-  // luma
-  uint32_t w[9][3];
-  load_win9(R, pitch, W, H, x0 + (mvx >> 2) - 2, y0 + (mvy >> 2) - 2, w);
-  // chroma window: 3 rows x (Cb, Cr) x 3 samples at (cx0, cy0)
-  const int CW = W / 2, CH = H / 2;
-  const int cx0 = cx + (mvx >> 3), cy0 = cy + (mvy >> 3);
-  const uint8_t *RUV = R + a.uv_off;
-  uint32_t cwn[3][2];
-  if (cx0 >= 0 && cx0 + 2 < CW && cy0 >= 0 && cy0 + 2 < CH) {
-    const int o = 2 * cx0, sh = o & 3;
+  int pv[16], cpred[2][4];
+  pred_ref(a, rs0 >= 0 ? rs0 : rs1, rs0 >= 0 ? mvw : mvw1, x0, y0, cx, cy, W, H, pv, cpred);
+  const int ext = a.slices[h.slice].ext;
+  if (rs1 >= 0 || ext >= 0) {  // bi-prediction / weighted prediction (8.4.2.3)
+    const full::Wp Wt = full::wp_make(ext >= 0 ? a.exts + ext : nullptr, r0, r1);
+    int pv1[16], cp1[2][4];
+    if (rs0 >= 0 && rs1 >= 0) pred_ref(a, rs1, mvw1, x0, y0, cx, cy, W, H, pv1, cp1);
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const uint32_t *q = reinterpret_cast<const uint32_t *>(RUV + static_cast<int64_t>(cy0 + r) * pitch + (o & ~3));
-      const uint32_t d0 = q[0], d1 = q[1];
-      cwn[r][0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
-      cwn[r][1] = d1 >> (8 * sh);
-    }
-  } else {
+    for (int i = 0; i < 16; ++i) pv[i] = full::wp_apply(Wt, 0, pv[i], Wt.both ? pv1[i] : 0);
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const uint8_t *row = RUV + static_cast<int64_t>(min(max(cy0 + r, 0), CH - 1)) * pitch;
-      uint32_t v[2] = {0, 0};
+    for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int xx = 2 * min(max(cx0 + c, 0), CW - 1);
-        v[(2 * c) >> 2] |= static_cast<uint32_t>(row[xx]) << (((2 * c) & 3) * 8);
-        v[(2 * c + 1) >> 2] |= static_cast<uint32_t>(row[xx + 1]) << (((2 * c + 1) & 3) * 8);
-      }
-      cwn[r][0] = v[0];
-      cwn[r][1] = v[1];
-    }
+      for (int i = 0; i < 4; ++i) cpred[pl][i] = full::wp_apply(Wt, 1 + pl, cpred[pl][i], Wt.both ? cp1[pl][i] : 0);
   }
-  int pv[16];
-  luma_pred4(w, mvx & 3, mvy & 3, pv);
   // luma residual
   int res[16];
   const bool t8 = (h.modes & kModeT8) != 0;
@@ -366,20 +418,7 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
     *reinterpret_cast<uint32_t *>(Y + static_cast<int64_t>(y0 + r) * pitch + x0) =
         pack4(c255(pv[r * 4] + res[r * 4]), c255(pv[r * 4 + 1] + res[r * 4 + 1]), c255(pv[r * 4 + 2] + res[r * 4 + 2]),
               c255(pv[r * 4 + 3] + res[r * 4 + 3]));
-  // chroma 2x2 per plane (8.4.2.2.2)
-  const int fx = mvx & 7, fy = mvy & 7;
-  auto cpx = [&](int r, int i) { return static_cast<int>((cwn[r][i >> 2] >> ((i & 3) * 8)) & 255); };
-  int cpred[2][4];
-#pragma unroll
-  for (int pl = 0; pl < 2; ++pl)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        const int A = cpx(y, 2 * x + pl), B = cpx(y, 2 * x + 2 + pl);
-        const int C = cpx(y + 1, 2 * x + pl), D = cpx(y + 1, 2 * x + 2 + pl);
-        cpred[pl][y * 2 + x] = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
-      }
+  // chroma residual
   if (h.cbp >> 4) {
     const int ck = ((by >> 1) << 1) | (bx >> 1), sx = (bx & 1) * 2, sy = (by & 1) * 2;
 #pragma unroll
@@ -860,13 +899,22 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
 // --------------------------------------------------------------- deblocking
 __device__ __forceinline__ bool is_intra_t(int ty) { return ty == kMbI4x4 || ty == kMbI16 || ty == kMbPcm; }
 
-// bS between 4x4 blocks bp of P and bq of Q (8.7.2.1, frames, P slices)
-__device__ __forceinline__ int bs_dev(const MbRec *P, int bp, const MbRec *Q, int bq, int tp, int tq, bool mbe) {
+// bS between 4x4 blocks bp of P and bq of Q (8.7.2.1, frames); P1 / Q1: their
+// list-1 halves in streams with B slices, else null
+__device__ __forceinline__ int bs_dev(const MbRec *P, const MbRecB *P1, int bp, const MbRec *Q, const MbRecB *Q1, int bq,
+                                      int tp, int tq, bool mbe) {
   if (is_intra_t(tp) || is_intra_t(tq)) return mbe ? 4 : 3;
   if (P->nz[bp] || Q->nz[bq]) return 2;
   const int p8 = (bp >> 3) * 2 + ((bp & 3) >> 1), q8 = (bq >> 3) * 2 + ((bq & 3) >> 1);
-  if (P->ref_slot[p8] != Q->ref_slot[q8]) return 1;
   const uint32_t mp = reinterpret_cast<const uint32_t *>(P)[16 + bp], mq = reinterpret_cast<const uint32_t *>(Q)[16 + bq];
+  if (P1) {
+    const uint32_t mp1 = reinterpret_cast<const uint32_t *>(P1)[16 + bp], mq1 = reinterpret_cast<const uint32_t *>(Q1)[16 + bq];
+    return full::bs_motion(P->ref_slot[p8], P1->ref_slot1[p8], static_cast<int16_t>(mp & 0xffff), static_cast<int16_t>(mp >> 16),
+                           static_cast<int16_t>(mp1 & 0xffff), static_cast<int16_t>(mp1 >> 16), Q->ref_slot[q8],
+                           Q1->ref_slot1[q8], static_cast<int16_t>(mq & 0xffff), static_cast<int16_t>(mq >> 16),
+                           static_cast<int16_t>(mq1 & 0xffff), static_cast<int16_t>(mq1 >> 16));
+  }
+  if (P->ref_slot[p8] != Q->ref_slot[q8]) return 1;
   const int dx = static_cast<int16_t>(mp & 0xffff) - static_cast<int16_t>(mq & 0xffff);
   const int dy = static_cast<int16_t>(mp >> 16) - static_cast<int16_t>(mq >> 16);
   return (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
@@ -952,6 +1000,7 @@ __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
   const int mb = blockIdx.x * 256 + threadIdx.x;
   if (mb >= nmb) return;
   const MbRec *Q = a.recs + static_cast<int64_t>(slot) * nmb + mb;
+  const MbRecB *Q1 = a.P.bframes ? a.recs1 + static_cast<int64_t>(slot) * nmb + mb : nullptr;
   const MbHdr hq = load_hdr(Q);
   const FullSlice &sd = a.slices[hq.slice];
   const int x = mb % mbw, y = mb / mbw;
@@ -983,12 +1032,13 @@ __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
         if (e == 0 && !(dir ? ft : fl)) continue;
         if (t8 && (e & 1)) continue;  // 8x8 transform: no 4-sample internal luma edges (chroma uses e = 0, 2)
         const MbRec *Pm = e ? Q : (dir ? PT : PL);
+        const MbRecB *Pm1 = Q1 ? Q1 - (e ? 0 : (dir ? mbw : 1)) : nullptr;
         const int tp = e ? tq : (dir ? tt : tl);
 #pragma unroll
         for (int seg = 0; seg < 4; ++seg) {
           const int bq = dir ? e * 4 + seg : seg * 4 + e;
           const int bp = dir ? (e ? bq - 4 : 12 + seg) : (e ? bq - 1 : seg * 4 + 3);
-          const int bS = bs_dev(Pm, bp, Q, bq, tp, tq, e == 0);
+          const int bS = bs_dev(Pm, Pm1, bp, Q, Q1, bq, tp, tq, e == 0);
           d.bs[dir * 2 + (e >> 1)] |= static_cast<uint32_t>(bS) << (((e & 1) * 4 + seg) * 4);
         }
       }

@@ -57,11 +57,12 @@ std::string parse_sps(const uint8_t *nal, size_t n, Sps *s) {
     s->log2_max_poc_lsb = 4 + static_cast<int>(br.ue());
   } else if (s->poc_type == 1) {
     s->delta_pic_order_always_zero = static_cast<int>(br.u(1));
-    br.se();
-    br.se();
+    s->offset_for_non_ref_pic = br.se();
+    s->offset_for_top_to_bottom_field = br.se();
     const uint32_t cyc = br.ue();
     if (cyc > 255) return "bad num_ref_frames_in_pic_order_cnt_cycle";
-    for (uint32_t i = 0; i < cyc; ++i) br.se();
+    s->offset_for_ref_frame.clear();
+    for (uint32_t i = 0; i < cyc; ++i) s->offset_for_ref_frame.push_back(br.se());
   } else if (s->poc_type != 2) {
     return "bad pic_order_cnt_type";
   }
@@ -72,7 +73,7 @@ std::string parse_sps(const uint8_t *nal, size_t n, Sps *s) {
   s->frame_mbs_only = static_cast<int>(br.u(1));
   if (!s->frame_mbs_only) return "interlaced (field) coding is not supported";
   s->mb_height = map_units;
-  br.u(1);  // direct_8x8_inference_flag
+  s->direct_8x8_inference = static_cast<int>(br.u(1));
   if (br.u(1)) {  // frame_cropping_flag; 4:2:0 crop units are 2 samples
     s->crop_left = 2 * static_cast<int>(br.ue());
     s->crop_right = 2 * static_cast<int>(br.ue());
@@ -106,7 +107,7 @@ std::string parse_pps(const uint8_t *nal, size_t n, Pps *p) {
   p->constrained_intra_pred = static_cast<int>(br.u(1));
   p->redundant_pic_cnt_present = static_cast<int>(br.u(1));
   if (!br.ok()) return "truncated PPS";
-  if (p->weighted_pred) return "weighted prediction is not supported";
+  if (p->weighted_bipred_idc > 2) return "bad weighted_bipred_idc";
   return "";
 }
 

@@ -12,6 +12,9 @@ struct Sps {
   int chroma_format_idc = 1, bit_depth_luma = 8, bit_depth_chroma = 8;
   int log2_max_frame_num = 4, poc_type = 0, log2_max_poc_lsb = 4;
   int delta_pic_order_always_zero = 0;
+  int offset_for_non_ref_pic = 0, offset_for_top_to_bottom_field = 0;  // POC type 1 (7.4.2.1.1)
+  std::vector<int> offset_for_ref_frame;
+  int direct_8x8_inference = 1;
   int max_num_ref_frames = 0, gaps_allowed = 0;
   int mb_width = 0, mb_height = 0, frame_mbs_only = 1;
   int crop_left = 0, crop_right = 0, crop_top = 0, crop_bottom = 0;  // luma samples

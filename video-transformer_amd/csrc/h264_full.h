@@ -4,10 +4,11 @@
 // the slice headers, and the per-macroblock record the slice parser writes
 // for the reconstruction and deblocking kernels.
 //
-// The general path decodes progressive CAVLC streams with I and P slices
-// (ITU-T H.264 Baseline without FMO/ASO/redundant pictures, and Main/High
-// streams that use none of CABAC, B slices, interlace, 8x8 transforms,
-// scaling matrices or weighted prediction); DESIGN.md §5b.
+// The general path decodes progressive 4:2:0 8-bit streams: CAVLC I / P / B
+// slices, CABAC I / P slices, 8x8 transforms, explicit and implicit weighted
+// prediction, spatial and temporal direct prediction (Baseline without
+// FMO/ASO/redundant pictures, Main, High without scaling matrices or
+// interlace); DESIGN.md §5b.
 #pragma once
 #include <cstdint>
 
@@ -21,17 +22,36 @@ struct FullSlice {
   int32_t first_mb;
   int32_t data_byte;    // slice_data(): EBSP byte of the payload (after the header byte)
   int32_t data_bit;     // ... and its RBSP bit index
-  int32_t is_p;
+  int32_t is_p;         // 0 I slice, 1 P slice, 2 B slice (kSliceB)
   int32_t qp;           // SliceQPY
-  int32_t num_ref;      // num_ref_idx_l0_active (P)
+  int32_t num_ref;      // num_ref_idx_l0_active (P, B)
   int32_t dbk_idc;      // disable_deblocking_filter_idc
   int32_t dbk_a, dbk_b; // FilterOffsetA / FilterOffsetB
   uint32_t arena;       // first coefficient block reserved for the slice
   uint32_t arena_cap;   // blocks reserved: min(27 x MBs, 3 x NAL bytes + 27) bounds
                         // what CAVLC can code (a stored block costs >= 3 bits)
-  int32_t _pad;
+  int32_t ext;          // SliceExt of a B slice or a weighted P slice, -1: none
   int16_t ref_slot[32]; // RefPicList0[i] -> ring slot (-1: no reference picture)
 };
+static_assert(sizeof(FullSlice) == 128, "FullSlice layout");
+constexpr int32_t kSliceB = 2;
+
+// What a B slice or an explicitly weighted P slice adds to FullSlice (the
+// slices of one picture usually share one record: the host de-duplicates).
+struct SliceExt {
+  int32_t num_ref1;       // num_ref_idx_l1_active (B)
+  int32_t direct_spatial; // direct_spatial_mv_pred_flag
+  int32_t wmode;          // 0 default, 1 explicit (pred_weight_table), 2 implicit (8.4.2.3.1)
+  int32_t lwd, cwd;       // luma / chroma_log2_weight_denom
+  int32_t col_short;      // RefPicList1[0] is a short-term reference picture (colZeroFlag)
+  int32_t poc;            // PicOrderCnt(CurrPic)
+  uint32_t lt0, lt1;      // bit i: RefPicList0 / 1 [i] is a long-term reference picture
+  int32_t _pad[3];
+  int16_t ref_slot1[32];  // RefPicList1[i] -> ring slot
+  int32_t poc0[32], poc1[32];  // PicOrderCnt of RefPicList0 / 1 [i]
+  int16_t w[2][32][6];    // list, index: luma weight, luma offset, Cb weight, Cb offset, Cr weight, Cr offset
+};
+static_assert(sizeof(SliceExt) == 1136, "SliceExt layout");
 
 struct FullParams {
   int32_t mb_width, mb_height;
@@ -40,7 +60,9 @@ struct FullParams {
   int32_t cqp_off2;     // second_chroma_qp_index_offset (Cr)
   int32_t cabac;        // entropy_coding_mode_flag (parse_cabac.h)
   int32_t t8mode;       // transform_8x8_mode_flag
-  int32_t _pad;
+  int32_t bframes;      // the stream has B slices: every macroblock also writes an MbRecB
+  int32_t direct8x8;    // direct_8x8_inference_flag
+  int32_t _pad[3];
 };
 
 // Stored coefficient blocks of a macroblock, in parse order = bit order.
@@ -88,5 +110,19 @@ struct alignas(16) MbRec {
   int16_t mv[16][2];    // quarter-sample motion of raster 4x4 blocks
 };
 static_assert(sizeof(MbRec) == 128, "MbRec layout");
+
+// List-1 half of a macroblock's motion (streams with B slices; same indexing
+// as MbRec).  I / P macroblocks: ref1 -1.
+constexpr uint8_t kDirect16 = 0x10;  // MbRecB.direct: B_Skip / B_Direct_16x16
+struct alignas(16) MbRecB {
+  int8_t ref1[4];        // RefPicList1 index per 8x8 (-1: list 1 unused)
+  int16_t ref_slot1[4];  // its ring slot
+  uint8_t direct;        // bits 0-3: 8x8 quadrants predicted in direct mode; kDirect16
+  uint8_t _p[3];
+  uint8_t mvd1[8];       // CABAC: Min(|mvdL1|, 33) of bottom-row block x, component c at byte 2 x + c
+  uint8_t _q[40];
+  int16_t mv1[16][2];    // quarter-sample list-1 motion of raster 4x4 blocks
+};
+static_assert(sizeof(MbRecB) == 128, "MbRecB layout");
 
 }  // namespace vts

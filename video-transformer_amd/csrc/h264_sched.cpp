@@ -1,7 +1,8 @@
 // h264_sched.cpp — slice headers and reference lists for the general decoder
 // (see h264_sched.h).  ITU-T H.264 7.3.3 slice_header(), 7.3.3.1
-// ref_pic_list_modification(), 7.3.3.3 dec_ref_pic_marking(), 8.2.4
-// (reference picture list initialisation for P slices in frames, and
+// ref_pic_list_modification(), 7.3.3.2 pred_weight_table(), 7.3.3.3
+// dec_ref_pic_marking(), 8.2.1 picture order count (types 0, 1, 2), 8.2.4
+// (reference picture list initialisation for P and B slices in frames, and
 // modification), 8.2.5 (IDR, sliding window, MMCO 1-6).
 #include "h264_sched.h"
 
@@ -76,6 +77,7 @@ struct RefPic {
   int frame_num;
   int lt_idx;
   int kind;  // 1 short-term, 2 long-term
+  int poc;   // PicOrderCnt
 };
 
 bool more_rbsp(const std::vector<uint8_t> &nal, const HdrReader &r) {
@@ -150,6 +152,8 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
   int prev_ref_fn = 0;
   int max_lt_idx = -1;
   bool have_prev = false;
+  // 8.2.1 state carried from the previous picture(s)
+  int prev_poc_msb = 0, prev_poc_lsb = 0, prev_fn = 0, prev_fn_offset = 0;
   frames->assign(off.size(), SchedFrame{});
   slices->clear();
   char msg[160];
@@ -159,7 +163,7 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
     int64_t p = off[f];
     const int64_t end = p + size[f];
     bool first = true, idr = false, adaptive = false, lt_ref_flag = false;
-    int fn = 0;
+    int fn = 0, cur_poc = 0, h_poc_lsb = 0, h_dbot = 0;
     std::vector<std::pair<int, int>> mmco;  // (op, arg) ; op 3/6 carry lt idx in arg2 below
     std::vector<int> mmco_arg2;
     while (p + nal_len <= end) {
@@ -182,34 +186,71 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
       s.first_mb = static_cast<int32_t>(r.ue());
       int st = static_cast<int>(r.ue());
       if (st > 4) st -= 5;
-      if (st != 0 && st != 2) return "B / SP / SI slices";
-      s.is_p = st == 0;
+      if (st > 2) return "SP / SI slices";
+      s.is_p = st == 0 ? 1 : (st == 1 ? 2 : 0);
+      const bool is_b = s.is_p == 2, inter = s.is_p != 0;
       if (static_cast<int>(r.ue()) != pps.pps_id) return "slice refers to another PPS";
       const int frame_num = static_cast<int>(r.u(sps.log2_max_frame_num));
       if (type == 5) r.ue();  // idr_pic_id
+      int poc_lsb = 0, dbot = 0, dpoc0 = 0, dpoc1 = 0;
       if (sps.poc_type == 0) {
-        r.u(sps.log2_max_poc_lsb);
-        if (pps.bottom_field_pic_order_in_frame_present) r.se();
+        poc_lsb = static_cast<int>(r.u(sps.log2_max_poc_lsb));
+        if (pps.bottom_field_pic_order_in_frame_present) dbot = r.se();
       } else if (sps.poc_type == 1 && !sps.delta_pic_order_always_zero) {
-        r.se();
-        if (pps.bottom_field_pic_order_in_frame_present) r.se();
+        dpoc0 = r.se();
+        if (pps.bottom_field_pic_order_in_frame_present) dpoc1 = r.se();
       }
       if (pps.redundant_pic_cnt_present) r.ue();
+      if (is_b) s.direct_spatial = static_cast<int>(r.u(1));
       s.num_ref = pps.num_ref_idx_l0_default_active;
-      std::vector<std::pair<int, int>> mods;
-      if (s.is_p) {
-        if (r.u(1)) s.num_ref = static_cast<int>(r.ue()) + 1;
-        if (s.num_ref > 32) return "num_ref_idx_l0_active > 32";
+      s.num_ref1 = is_b ? pps.num_ref_idx_l1_default_active : 0;
+      std::vector<std::pair<int, int>> mods[2];
+      if (inter) {
         if (r.u(1)) {
-          for (;;) {
-            const int idc = static_cast<int>(r.ue());
-            if (idc == 3 || r.err) break;
-            if (idc > 2) return "bad modification_of_pic_nums_idc";
-            mods.emplace_back(idc, static_cast<int>(r.ue()));
-            if (mods.size() > 64) return "too many list modifications";
-          }
+          s.num_ref = static_cast<int>(r.ue()) + 1;
+          if (is_b) s.num_ref1 = static_cast<int>(r.ue()) + 1;
         }
+        if (s.num_ref > 32 || s.num_ref1 > 32) return "num_ref_idx_active > 32";
+        for (int l = 0; l < (is_b ? 2 : 1); ++l)
+          if (r.u(1)) {
+            for (;;) {
+              const int idc = static_cast<int>(r.ue());
+              if (idc == 3 || r.err) break;
+              if (idc > 2) return "bad modification_of_pic_nums_idc";
+              mods[l].emplace_back(idc, static_cast<int>(r.ue()));
+              if (mods[l].size() > 64) return "too many list modifications";
+            }
+          }
       }
+      // pred_weight_table (7.3.3.2); absent entries keep the default weights
+      s.wmode = is_b ? (pps.weighted_bipred_idc == 1 ? 1 : (pps.weighted_bipred_idc == 2 ? 2 : 0))
+                     : (s.is_p == 1 && pps.weighted_pred ? 1 : 0);
+      if (s.wmode == 1) {
+        s.lwd = static_cast<int>(r.ue());
+        s.cwd = static_cast<int>(r.ue());
+        if (s.lwd > 7 || s.cwd > 7) return "bad pred_weight_table denominators";
+      }
+      for (int l = 0; l < 2; ++l)
+        for (int i = 0; i < 32; ++i) {
+          int16_t *w = s.w[l][i];
+          w[0] = static_cast<int16_t>(1 << s.lwd);
+          w[2] = w[4] = static_cast<int16_t>(1 << s.cwd);
+          w[1] = w[3] = w[5] = 0;
+          if (s.wmode != 1 || i >= (l ? s.num_ref1 : s.num_ref)) continue;
+          if (r.u(1)) {
+            const int lw = r.se(), lo = r.se();
+            if (lw < -128 || lw > 127 || lo < -128 || lo > 127) return "pred_weight_table out of range";
+            w[0] = static_cast<int16_t>(lw);
+            w[1] = static_cast<int16_t>(lo);
+          }
+          if (r.u(1))
+            for (int j = 0; j < 2; ++j) {
+              const int cw = r.se(), co = r.se();
+              if (cw < -128 || cw > 127 || co < -128 || co > 127) return "pred_weight_table out of range";
+              w[2 + 2 * j] = static_cast<int16_t>(cw);
+              w[3 + 2 * j] = static_cast<int16_t>(co);
+            }
+        }
       bool this_adaptive = false, this_lt = false;
       std::vector<std::pair<int, int>> this_mmco;
       std::vector<int> this_arg2;
@@ -233,9 +274,10 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
           }
         }
       }
-      if (pps.entropy_coding_mode && s.is_p) {
+      if (pps.entropy_coding_mode && inter) {
         // only the cabac_init_idc 0 context tables are restated (x264 writes 0)
         if (r.ue() != 0) return "cabac_init_idc 1 or 2 (only the idc 0 context tables are supported)";
+        if (is_b) return "CABAC B slices";
       }
       s.qp = pps.pic_init_qp + r.se();
       s.dbk_idc = 0;
@@ -259,6 +301,8 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
         lt_ref_flag = this_lt;
         mmco = this_mmco;
         mmco_arg2 = this_arg2;
+        h_poc_lsb = poc_lsb;
+        h_dbot = dbot;
         // frame_num continuity (gaps_in_frame_num_value_allowed_flag = 0)
         if (!idr && have_prev) {
           const int want = (prev_ref_fn + 1) % max_fn;
@@ -269,54 +313,118 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
         }
         if (!idr && !have_prev) return "stream does not start with an IDR picture";
         if (idr) dpb.clear();
+        // PicOrderCnt (8.2.1), frames
+        if (sps.poc_type == 0) {
+          const int max_lsb = 1 << sps.log2_max_poc_lsb;
+          const int pmsb = idr ? 0 : prev_poc_msb, plsb = idr ? 0 : prev_poc_lsb;
+          int msb = pmsb;
+          if (poc_lsb < plsb && plsb - poc_lsb >= max_lsb / 2) msb = pmsb + max_lsb;
+          else if (poc_lsb > plsb && poc_lsb - plsb > max_lsb / 2) msb = pmsb - max_lsb;
+          const int top = msb + poc_lsb, bot = top + dbot;
+          cur_poc = std::min(top, bot);
+        } else {
+          const int fno = idr ? 0 : (prev_fn > frame_num ? prev_fn_offset + max_fn : prev_fn_offset);
+          if (sps.poc_type == 2) {
+            cur_poc = idr ? 0 : (ref_idc ? 2 * (fno + frame_num) : 2 * (fno + frame_num) - 1);
+          } else {
+            const int ncyc = static_cast<int>(sps.offset_for_ref_frame.size());
+            int abs_fn = ncyc ? fno + frame_num : 0;
+            if (!ref_idc && abs_fn > 0) --abs_fn;
+            int expected = 0;
+            if (abs_fn > 0) {
+              int delta_cycle = 0;
+              for (int v : sps.offset_for_ref_frame) delta_cycle += v;
+              const int cyc = (abs_fn - 1) / ncyc, in = (abs_fn - 1) % ncyc;
+              expected = cyc * delta_cycle;
+              for (int i = 0; i <= in; ++i) expected += sps.offset_for_ref_frame[static_cast<size_t>(i)];
+            }
+            if (!ref_idc) expected += sps.offset_for_non_ref_pic;
+            const int top = expected + dpoc0, bot = top + sps.offset_for_top_to_bottom_field + dpoc1;
+            cur_poc = std::min(top, bot);
+          }
+        }
       } else if (frame_num != fn || (type == 5) != idr) {
         return "slices of one picture disagree";
       }
       first = false;
-      if (s.is_p) fr.intra = false;
-      // RefPicList0 (8.2.4.2.1 + 8.2.4.3)
-      for (int i = 0; i < 32; ++i) s.ref[i] = -1;
-      if (s.is_p) {
-        std::vector<RefPic> st_refs, lt_refs;
-        for (const RefPic &rp : dpb) (rp.kind == 1 ? st_refs : lt_refs).push_back(rp);
+      s.poc = cur_poc;
+      if (inter) fr.intra = false;
+      if (is_b) fr.has_b = true;
+      // RefPicList0 / 1 (8.2.4.2.1, 8.2.4.2.3 + 8.2.4.3)
+      for (int i = 0; i < 32; ++i) {
+        s.ref[i] = s.ref1[i] = -1;
+        s.poc0[i] = s.poc1[i] = 0;
+      }
+      if (inter) {
+        std::vector<const RefPic *> st_refs, lt_refs;
+        for (const RefPic &rp : dpb) (rp.kind == 1 ? st_refs : lt_refs).push_back(&rp);
         auto wrap = [&](const RefPic &rp) { return rp.frame_num > fn ? rp.frame_num - max_fn : rp.frame_num; };
-        std::stable_sort(st_refs.begin(), st_refs.end(),
-                         [&](const RefPic &a, const RefPic &b) { return wrap(a) > wrap(b); });
         std::stable_sort(lt_refs.begin(), lt_refs.end(),
-                         [](const RefPic &a, const RefPic &b) { return a.lt_idx < b.lt_idx; });
-        std::vector<const RefPic *> list;
-        for (const RefPic &rp : st_refs) list.push_back(&rp);
-        for (const RefPic &rp : lt_refs) list.push_back(&rp);
-        const int n = s.num_ref;
-        list.resize(static_cast<size_t>(n) + 1, nullptr);
-        int pred = fn, ridx = 0;
-        for (const auto &md : mods) {
-          const RefPic *pic = nullptr;
-          if (md.first < 2) {
-            const int d = md.second + 1;
-            int nowrap = md.first == 0 ? pred - d : pred + d;
-            if (nowrap < 0) nowrap += max_fn;
-            if (nowrap >= max_fn) nowrap -= max_fn;
-            pred = nowrap;
-            const int num = nowrap > fn ? nowrap - max_fn : nowrap;
-            for (const RefPic &rp : st_refs)
-              if (wrap(rp) == num) pic = &rp;
-          } else {
-            for (const RefPic &rp : lt_refs)
-              if (rp.lt_idx == md.second) pic = &rp;
-          }
-          if (!pic) return "list modification names no reference picture";
-          for (int c = n; c > ridx; --c) list[c] = list[c - 1];
-          list[ridx++] = pic;
-          int ni = ridx;
-          for (int c = ridx; c <= n; ++c)
-            if (list[c] != pic) list[ni++] = list[c];
+                         [](const RefPic *a, const RefPic *b) { return a->lt_idx < b->lt_idx; });
+        std::vector<const RefPic *> init[2];
+        if (!is_b) {
+          std::stable_sort(st_refs.begin(), st_refs.end(),
+                           [&](const RefPic *a, const RefPic *b) { return wrap(*a) > wrap(*b); });
+          init[0] = st_refs;
+        } else {
+          std::stable_sort(st_refs.begin(), st_refs.end(),
+                           [](const RefPic *a, const RefPic *b) { return a->poc < b->poc; });
+          for (auto it = st_refs.rbegin(); it != st_refs.rend(); ++it)
+            if ((*it)->poc < cur_poc) init[0].push_back(*it);
+          for (const RefPic *rp : st_refs)
+            if (rp->poc > cur_poc) init[0].push_back(rp);
+          for (const RefPic *rp : st_refs)
+            if (rp->poc > cur_poc) init[1].push_back(rp);
+          for (auto it = st_refs.rbegin(); it != st_refs.rend(); ++it)
+            if ((*it)->poc < cur_poc) init[1].push_back(*it);
         }
-        // the pointers refer to st_refs / lt_refs, alive until here
-        for (int i = 0; i < n; ++i) {
-          s.ref[i] = list[i] ? list[i]->frame : -1;
-          if (s.ref[i] >= 0 && std::find(fr.refs.begin(), fr.refs.end(), s.ref[i]) == fr.refs.end())
-            fr.refs.push_back(s.ref[i]);
+        for (int l = 0; l < (is_b ? 2 : 1); ++l) init[l].insert(init[l].end(), lt_refs.begin(), lt_refs.end());
+        if (is_b && init[1].size() > 1 && init[0] == init[1]) std::swap(init[1][0], init[1][1]);
+        for (int l = 0; l < (is_b ? 2 : 1); ++l) {
+          const int n = l ? s.num_ref1 : s.num_ref;
+          std::vector<const RefPic *> list(static_cast<size_t>(n) + 1, nullptr);
+          for (int i = 0; i < n && i < static_cast<int>(init[l].size()); ++i) list[static_cast<size_t>(i)] = init[l][static_cast<size_t>(i)];
+          int pred = fn, ridx = 0;
+          for (const auto &md : mods[l]) {
+            const RefPic *pic = nullptr;
+            if (md.first < 2) {
+              const int d = md.second + 1;
+              int nowrap = md.first == 0 ? pred - d : pred + d;
+              if (nowrap < 0) nowrap += max_fn;
+              if (nowrap >= max_fn) nowrap -= max_fn;
+              pred = nowrap;
+              const int num = nowrap > fn ? nowrap - max_fn : nowrap;
+              for (const RefPic *rp : st_refs)
+                if (wrap(*rp) == num) pic = rp;
+            } else {
+              for (const RefPic *rp : lt_refs)
+                if (rp->lt_idx == md.second) pic = rp;
+            }
+            if (!pic) return "list modification names no reference picture";
+            for (int c = n; c > ridx; --c) list[static_cast<size_t>(c)] = list[static_cast<size_t>(c - 1)];
+            list[static_cast<size_t>(ridx++)] = pic;
+            int ni = ridx;
+            for (int c = ridx; c <= n; ++c)
+              if (list[static_cast<size_t>(c)] != pic) list[static_cast<size_t>(ni++)] = list[static_cast<size_t>(c)];
+          }
+          // the pointers refer to dpb entries, alive until the marking below
+          int64_t *ref = l ? s.ref1 : s.ref;
+          int32_t *pocs = l ? s.poc1 : s.poc0;
+          uint32_t &lt = l ? s.lt1 : s.lt0;
+          for (int i = 0; i < n; ++i) {
+            const RefPic *rp = list[static_cast<size_t>(i)];
+            ref[i] = rp ? rp->frame : -1;
+            pocs[i] = rp ? rp->poc : 0;
+            if (rp && rp->kind == 2) lt |= 1u << i;
+            if (ref[i] >= 0 && std::find(fr.refs.begin(), fr.refs.end(), ref[i]) == fr.refs.end())
+              fr.refs.push_back(ref[i]);
+          }
+          if (l == 1) {
+            if (!list[0]) return "B slice without a colocated picture (RefPicList1[0])";
+            s.col_short = list[0]->kind == 1;
+            if (std::find(fr.cols.begin(), fr.cols.end(), list[0]->frame) == fr.cols.end())
+              fr.cols.push_back(list[0]->frame);
+          }
         }
       }
       slices->push_back(s);
@@ -334,9 +442,33 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
       if (next <= s.first_mb) return "slices out of order (ASO) or overlapping";
       s.n_mbs = next - s.first_mb;
     }
+    // 8.2.1 state after the picture
+    bool mmco5 = false;
+    for (const auto &m : mmco) mmco5 |= adaptive && m.first == 5;
+    if (sps.poc_type == 0) {
+      if (fr.is_ref) {
+        if (mmco5) {
+          prev_poc_msb = 0;
+          prev_poc_lsb = h_dbot < 0 ? -h_dbot : 0;
+        } else {
+          const int max_lsb = 1 << sps.log2_max_poc_lsb;
+          const int pmsb = idr ? 0 : prev_poc_msb, plsb = idr ? 0 : prev_poc_lsb;
+          int msb = pmsb;
+          if (h_poc_lsb < plsb && plsb - h_poc_lsb >= max_lsb / 2) msb = pmsb + max_lsb;
+          else if (h_poc_lsb > plsb && h_poc_lsb - plsb > max_lsb / 2) msb = pmsb - max_lsb;
+          prev_poc_msb = msb;
+          prev_poc_lsb = h_poc_lsb;
+        }
+      }
+    } else {
+      const int fno = idr ? 0 : (prev_fn > fn ? prev_fn_offset + max_fn : prev_fn_offset);
+      prev_fn_offset = mmco5 ? 0 : fno;
+    }
+    prev_fn = mmco5 ? 0 : fn;
+    fr.poc = mmco5 ? 0 : cur_poc;
     // reference marking (8.2.5) after the picture
     if (fr.is_ref) {
-      RefPic cur{static_cast<int64_t>(f), fn, 0, 1};
+      RefPic cur{static_cast<int64_t>(f), fn, 0, 1, fr.poc};
       if (idr) {
         dpb.clear();
         if (lt_ref_flag) {

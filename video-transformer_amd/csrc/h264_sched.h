@@ -20,19 +20,35 @@ struct SchedSlice {
   int32_t first_mb, n_mbs;
   int32_t data_byte;    // slice_data(): EBSP byte of the payload (after the header byte)
   int32_t data_bit;     // ... RBSP bit index
-  int32_t is_p, qp, num_ref;
+  int32_t is_p, qp, num_ref;  // is_p: 0 I, 1 P, 2 B
   int32_t dbk_idc, dbk_a, dbk_b;
   int64_t ref[32];      // RefPicList0[i] as a frame index, -1 = no reference picture
+  // B slices and weighted prediction (h264_full.h SliceExt)
+  int32_t num_ref1 = 0, direct_spatial = 0;
+  int32_t wmode = 0;    // 0 default, 1 explicit, 2 implicit
+  int32_t lwd = 0, cwd = 0;
+  int32_t poc = 0;      // PicOrderCnt of the picture
+  int32_t col_short = 0;
+  uint32_t lt0 = 0, lt1 = 0;
+  int64_t ref1[32];     // RefPicList1
+  int32_t poc0[32], poc1[32];
+  int16_t w[2][32][6];  // pred_weight_table (defaults where absent)
+  bool needs_ext() const { return is_p == 2 || wmode != 0; }
 };
 
 struct SchedFrame {
   int64_t s0 = 0, ns = 0;   // slices [s0, s0 + ns)
   bool intra = true;        // every slice is an I slice
   bool is_ref = false;      // nal_ref_idc != 0
-  std::vector<int64_t> refs;  // distinct frames in any slice's active RefPicList0
+  bool has_b = false;       // a B slice (direct prediction reads the colocated picture's motion)
+  int32_t poc = 0;          // PicOrderCnt after the picture (0 after memory_management_control_operation 5)
+  std::vector<int64_t> refs;  // distinct frames in any slice's active RefPicList0 / 1
+  std::vector<int64_t> cols;  // distinct RefPicList1[0] of its B slices
 };
 
 // Stream facts the general path needs beyond h264.h's Sps / Pps.
+// (B slices come with PicOrderCnt 8.2.1, list initialisation 8.2.4.2.3 and
+// pred_weight_table 7.3.3.2.)
 struct SchedStream {
   int seq_scaling = 0;       // seq_scaling_matrix_present_flag
   int transform_8x8 = 0;     // PPS transform_8x8_mode_flag

@@ -615,9 +615,13 @@ struct CabacParser : Parser {
 // Parse CABAC slice `s` (window slice index si).  Returns DEC_E_* bits.
 VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams P,
                                          MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena, uint32_t epoch,
-                                         FullScratch *sc) {
+                                         FullScratch *sc, const BCtx &bc) {
   const uint8_t *nal = es + s.nal_offset;
   CabacParser p;
+  p.bc = bc;
+  p.bframes = P.bframes;
+  p.direct8x8 = P.direct8x8;
+  if (s.is_p == kSliceB) return DEC_E_SLICE_TYPE;  // CABAC B slices: not restated
   p.s = &s;
   p.cip = P.cip;
   p.P_t8mode = P.t8mode != 0;

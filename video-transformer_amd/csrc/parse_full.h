@@ -3,12 +3,14 @@
 // harness tests/native/full_host.cpp compiles the same code for the host).
 //
 // The host has already parsed the slice header (h264_sched.cpp) and hands
-// over where slice_data() starts, the slice QP and RefPicList0 as ring slots.
-// Per macroblock the lane derives everything later stages need and the
+// over where slice_data() starts, the slice QP and RefPicList0 / 1 as ring
+// slots.  Per macroblock the lane derives everything later stages need and the
 // standard derives from syntax alone — Intra_4x4 modes (8.3.1.1), motion
-// vectors (8.4.1.3, P_Skip 8.4.1.1), QPY, total_coeff — and writes one MbRec
-// plus its non-zero coefficient blocks (raster order, int16) into the slice's
-// reserved arena range.  Errors come back as DEC_E_* bits.
+// vectors (8.4.1.3, P_Skip 8.4.1.1, B direct prediction 8.4.1.2 from the
+// colocated picture's records), QPY, total_coeff — and writes one MbRec (+ an
+// MbRecB with the list-1 motion in streams with B slices) plus its non-zero
+// coefficient blocks (raster order, int16) into the slice's reserved arena
+// range.  Errors come back as DEC_E_* bits.
 #pragma once
 #include <cstdint>
 
@@ -115,6 +117,34 @@ static const uint8_t *const kCbpI = h264::kCbpIntra;
 static const uint8_t *const kCbpP = h264::kCbpInter;
 #endif
 
+// Table 7-14: prediction of the two partitions of B mb_type 1..21 (1 Pred_L0,
+// 2 Pred_L1, 3 BiPred), as pm0 | pm1 << 2; Table 7-18: B sub_mb_type ->
+// prediction (0 direct) | shape << 2 (0 8x8, 1 8x4, 2 4x8, 3 4x4)
+#if defined(__HIPCC__)
+__device__ __constant__ static const uint8_t kBPart[22] = {
+#else
+static const uint8_t kBPart[22] = {
+#endif
+    0, 1, 2, 3, 5, 5, 10, 10, 9, 9, 6, 6, 13, 13, 14, 14, 7, 7, 11, 11, 15, 15};
+#if defined(__HIPCC__)
+__device__ __constant__ static const uint8_t kBSub[13] = {
+#else
+static const uint8_t kBSub[13] = {
+#endif
+    0, 1, 2, 3, 5, 9, 6, 10, 7, 11, 13, 14, 15};
+
+// What a B slice adds to the parse (null / zero otherwise)
+struct BCtx {
+  MbRecB *recs1;          // the frame's list-1 records (streams with B slices)
+  const MbRec *col;       // the colocated picture's records (RefPicList1[0], B slices)
+  const MbRecB *col1;
+  const SliceExt *x;      // the slice's SliceExt (B slices, weighted P slices)
+};
+
+VTS_HD VTS_INLINE int clip3i(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+// MinPositive (8.4.1.2.2)
+VTS_HD VTS_INLINE int min_positive(int x, int y) { return (x >= 0 && y >= 0) ? (x < y ? x : y) : (x > y ? x : y); }
+
 // luma4x4BlkIdx <-> raster 4x4 block
 VTS_HD VTS_INLINE int blk_x(int k) { return ((k >> 2) & 1) * 2 + (k & 1); }
 VTS_HD VTS_INLINE int blk_y(int k) { return ((k >> 3) & 1) * 2 + ((k >> 1) & 1); }
@@ -133,6 +163,11 @@ struct FullScratch {
   uint32_t cache[kCacheWords];
   uint8_t prev[16], rem[16];  // Intra4x4 prev_intra4x4_pred_mode_flag / rem_intra4x4_pred_mode
   int8_t sub[4], refs[4];     // sub_mb_type / ref_idx_l0 of the partitions
+  int8_t refs1[4];            // B: ref_idx_l1 of the partitions
+  uint8_t pm[4];              // B: prediction of the partitions (0 direct, 1 L0, 2 L1, 3 Bi)
+  int32_t mvd[2][16][2];      // B: mvd_lX of partition k, sub-partition q at [X][4 k + q]
+  MbRecB mb1[2];              // list-1 halves of mb[2] (streams with B slices)
+  MbRecB top1[3];             // ... of top[3]: bytes 0..31 and 112..127
   // CABAC (parse_cabac.h)
   uint8_t cst[VTS_CABAC_NCTX];  // context states: pStateIdx << 1 | valMPS
   int16_t lv[64];               // levels of the block being decoded, coefficient-list order
@@ -169,6 +204,10 @@ struct Parser {
   // row above, column pf_col: prefetched during the previous macroblock
   int pf_col;
   TopCtx pf;
+  u32x4 pf1[3];           // the prefetched column's list-1 context (bframes)
+  BCtx bc;
+  int bframes;            // write / read the list-1 records
+  int direct8x8;          // direct_8x8_inference_flag
   uint32_t todo;          // residual blocks of the current macroblock still to decode (kBlk* bits)
   bool cur_i16;           // the current macroblock is Intra_16x16
 
@@ -196,6 +235,13 @@ struct Parser {
     const int d = n - (cur_addr - mbw);  // -1, 0, 1: D, B, C
     return sc->top[(tslots >> (2 * (d + 1))) & 3];
   }
+  VTS_HD VTS_INLINE MbRecB &cur1() const { return sc->mb1[cs]; }
+  VTS_HD VTS_INLINE const MbRecB &rec1(int n) const {
+    if (n == -2) return sc->mb1[cs];
+    if (n == cur_addr - 1) return sc->mb1[cs ^ 1];
+    const int d = n - (cur_addr - mbw);
+    return sc->top1[(tslots >> (2 * (d + 1))) & 3];
+  }
   VTS_HD VTS_INLINE int level_of(int n) const {
     if (n == cur_addr - 1) return lvl_prev;
     return static_cast<int>(rec(n).epoch);
@@ -221,7 +267,27 @@ struct Parser {
     d[7] = t.v3;
     sc->top[col % 3].epoch = t.lvl;
   }
-  VTS_HD VTS_INLINE void top_sync(int col) const { top_store(col, top_load(col)); }
+  VTS_HD VTS_INLINE void top_load1(int col, u32x4 (&v)[3]) const {
+    const int n = cur_addr - mbw + (col - cur_addr % mbw);
+    const u32x4 *g = reinterpret_cast<const u32x4 *>(bc.recs1 + n);
+    v[0] = g[0];
+    v[1] = g[1];
+    v[2] = g[7];
+  }
+  VTS_HD VTS_INLINE void top_store1(int col, const u32x4 (&v)[3]) const {
+    u32x4 *d = reinterpret_cast<u32x4 *>(&sc->top1[col % 3]);
+    d[0] = v[0];
+    d[1] = v[1];
+    d[7] = v[2];
+  }
+  VTS_HD VTS_INLINE void top_sync(int col) const {
+    top_store(col, top_load(col));
+    if (bframes) {
+      u32x4 v[3];
+      top_load1(col, v);
+      top_store1(col, v);
+    }
+  }
   // a new macroblock: the previous one becomes the left neighbour; the row
   // above rotates through the three slots, its next column loading one
   // macroblock ahead
@@ -237,12 +303,17 @@ struct Parser {
         top_sync(x);
       }
       if (x + 1 < mbw) {
-        if (pf_col != x + 1) pf = top_load(x + 1);
+        if (pf_col != x + 1) {
+          pf = top_load(x + 1);
+          if (bframes) top_load1(x + 1, pf1);
+        }
         top_store(x + 1, pf);
+        if (bframes) top_store1(x + 1, pf1);
       }
       pf_col = -1;
       if (x + 2 < mbw) {
         pf = top_load(x + 2);
+        if (bframes) top_load1(x + 2, pf1);
         pf_col = x + 2;
       }
     }
@@ -398,7 +469,9 @@ struct Parser {
     bool avail;
     int ref, x, y;
   };
-  VTS_HD VTS_INLINE Mv nb_mv(int cur, int xN, int yN, uint32_t done) const {
+  // list l's motion of the neighbouring 4x4 block (ref -1: unavailable, intra
+  // or list l unused, with a zero vector)
+  VTS_HD VTS_INLINE Mv nb_mv(int cur, int xN, int yN, uint32_t done, int l = 0) const {
     Mv r{false, -1, 0, 0};
     int xw, yw;
     const int n = nb_mb(cur, xN, yN, 16, &xw, &yw);
@@ -408,16 +481,25 @@ struct Parser {
     r.avail = true;
     const MbRec &m = rec(n);
     if (m.type != kMbInter && m.type != kMbSkip) return r;
-    r.ref = m.ref[(b >> 3) * 2 + ((b & 3) >> 1)];
-    r.x = m.mv[b][0];
-    r.y = m.mv[b][1];
+    const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+    if (l) {
+      const MbRecB &m1 = rec1(n);
+      r.ref = m1.ref1[p8];
+      r.x = m1.mv1[b][0];
+      r.y = m1.mv1[b][1];
+    } else {
+      r.ref = m.ref[p8];
+      r.x = m.mv[b][0];
+      r.y = m.mv[b][1];
+    }
     return r;
   }
-  VTS_HD VTS_INLINE void mv_pred(int cur, int x0, int y0, int w, int h, int ref, uint32_t done, int *px, int *py) const {
-    const Mv A = nb_mv(cur, x0 - 1, y0, done);
-    Mv B = nb_mv(cur, x0, y0 - 1, done);
-    Mv C = nb_mv(cur, x0 + w, y0 - 1, done);
-    if (!C.avail) C = nb_mv(cur, x0 - 1, y0 - 1, done);
+  VTS_HD VTS_INLINE void mv_pred(int cur, int x0, int y0, int w, int h, int ref, uint32_t done, int *px, int *py,
+                                 int l = 0) const {
+    const Mv A = nb_mv(cur, x0 - 1, y0, done, l);
+    Mv B = nb_mv(cur, x0, y0 - 1, done, l);
+    Mv C = nb_mv(cur, x0 + w, y0 - 1, done, l);
+    if (!C.avail) C = nb_mv(cur, x0 - 1, y0 - 1, done, l);
     if (w == 16 && h == 8) {
       if (y0 == 0 && B.ref == ref) { *px = B.x; *py = B.y; return; }
       if (y0 == 8 && A.ref == ref) { *px = A.x; *py = A.y; return; }
@@ -460,6 +542,16 @@ struct Parser {
       m.mv[i][0] = m.mv[i][1] = 0;
     }
     for (int i = 0; i < 8; ++i) m.nzc[i] = 0;
+    if (bframes) {
+      MbRecB &m1 = cur1();
+      for (int i = 0; i < 4; ++i) {
+        m1.ref1[i] = -1;
+        m1.ref_slot1[i] = -1;
+      }
+      m1.direct = 0;
+      for (int i = 0; i < 8; ++i) m1.mvd1[i] = 0;
+      for (int i = 0; i < 16; ++i) m1.mv1[i][0] = m1.mv1[i][1] = 0;
+    }
   }
   VTS_HD VTS_INLINE void end_mb(int addr) {
     // intra dependency level: 1 + the highest level among the intra-predicted
@@ -489,18 +581,116 @@ struct Parser {
 #else
     recs[addr] = cur();
 #endif
+    if (bframes) {
+#if defined(__HIPCC__)
+      u32x4 *d1 = reinterpret_cast<u32x4 *>(&bc.recs1[addr]);
+      const u32x4 *s1 = reinterpret_cast<const u32x4 *>(&cur1());
+      d1[0] = s1[0];
+      d1[1] = s1[1];
+#pragma unroll
+      for (int i = 4; i < 8; ++i) d1[i] = s1[i];
+#else
+      bc.recs1[addr] = cur1();
+#endif
+    }
   }
 
   VTS_HD VTS_INLINE void set_motion(int b, int ref, int mvx, int mvy) {
-    cur().mv[b][0] = static_cast<int16_t>(mvx);
-    cur().mv[b][1] = static_cast<int16_t>(mvy);
+    cur().mv[b][0] = static_cast<int16_t>(ref >= 0 ? mvx : 0);
+    cur().mv[b][1] = static_cast<int16_t>(ref >= 0 ? mvy : 0);
     const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
     cur().ref[p8] = static_cast<int8_t>(ref);
-    cur().ref_slot[p8] = s->ref_slot[ref & 31];
+    cur().ref_slot[p8] = ref >= 0 ? s->ref_slot[ref & 31] : static_cast<int16_t>(-1);
+  }
+  VTS_HD VTS_INLINE void set_motion1(int b, int ref, int mvx, int mvy) {
+    MbRecB &m1 = cur1();
+    m1.mv1[b][0] = static_cast<int16_t>(ref >= 0 ? mvx : 0);
+    m1.mv1[b][1] = static_cast<int16_t>(ref >= 0 ? mvy : 0);
+    const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+    m1.ref1[p8] = static_cast<int8_t>(ref);
+    m1.ref_slot1[p8] = ref >= 0 ? bc.x->ref_slot1[ref & 31] : static_cast<int16_t>(-1);
+  }
+
+  // 8.4.1.2: direct prediction of the raster 4x4 blocks in `mask` from the
+  // colocated picture's records (8.4.1.2.1) — spatial (8.4.1.2.2) or temporal
+  // (8.4.1.2.3)
+  VTS_HD void direct_pred(int addr, uint32_t mask) {
+    const SliceExt &x = *bc.x;
+    int ref0 = -1, ref1 = -1, mp[2][2] = {{0, 0}, {0, 0}};
+    bool zero = false;
+    if (x.direct_spatial) {
+      int rf[2];
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        const Mv A = nb_mv(addr, -1, 0, 0, l), B = nb_mv(addr, 0, -1, 0, l);
+        Mv C = nb_mv(addr, 16, -1, 0, l);
+        if (!C.avail) C = nb_mv(addr, -1, -1, 0, l);
+        rf[l] = min_positive(A.ref, min_positive(B.ref, C.ref));
+      }
+      ref0 = rf[0];
+      ref1 = rf[1];
+      if (ref0 < 0 && ref1 < 0) {
+        ref0 = ref1 = 0;
+        zero = true;
+      }
+      if (!zero) {
+        if (ref0 >= 0) mv_pred(addr, 0, 0, 16, 16, ref0, 0, &mp[0][0], &mp[0][1], 0);
+        if (ref1 >= 0) mv_pred(addr, 0, 0, 16, 16, ref1, 0, &mp[1][0], &mp[1][1], 1);
+      }
+    }
+    const MbRec &cm = bc.col[addr];
+    const MbRecB &cm1 = bc.col1[addr];
+    for (int blk = 0; blk < 16; ++blk) {
+      if (!((mask >> blk) & 1u)) continue;
+      const int cb = direct8x8 ? ((blk >> 3) * 3) * 4 + ((blk & 3) >> 1) * 3 : blk;
+      const int c8 = (cb >> 3) * 2 + ((cb & 3) >> 1);
+      const bool use0 = cm.ref[c8] >= 0;
+      const int ref_col = use0 ? cm.ref[c8] : cm1.ref1[c8];  // -1: intra
+      const int mcx = ref_col < 0 ? 0 : (use0 ? cm.mv[cb][0] : cm1.mv1[cb][0]);
+      const int mcy = ref_col < 0 ? 0 : (use0 ? cm.mv[cb][1] : cm1.mv1[cb][1]);
+      if (x.direct_spatial) {
+        const bool col_zero = x.col_short && ref_col == 0 && mcx >= -1 && mcx <= 1 && mcy >= -1 && mcy <= 1;
+        const bool z0 = zero || ref0 < 0 || (ref0 == 0 && col_zero);
+        const bool z1 = zero || ref1 < 0 || (ref1 == 0 && col_zero);
+        set_motion(blk, ref0, z0 ? 0 : mp[0][0], z0 ? 0 : mp[0][1]);
+        set_motion1(blk, ref1, z1 ? 0 : mp[1][0], z1 ? 0 : mp[1][1]);
+      } else {
+        int r0 = 0;
+        if (ref_col >= 0) {  // the lowest list-0 index naming the colocated block's reference picture
+          const int slot = use0 ? cm.ref_slot[c8] : cm1.ref_slot1[c8];
+          r0 = -1;
+          for (int i = s->num_ref - 1; i >= 0; --i)
+            if (s->ref_slot[i] == slot) r0 = i;
+          if (r0 < 0) {
+            err |= DEC_E_NO_REF;
+            return;
+          }
+        }
+        int m0x = mcx, m0y = mcy, m1x = 0, m1y = 0;
+        const int tb = clip3i(-128, 127, x.poc - x.poc0[r0]), td = clip3i(-128, 127, x.poc1[0] - x.poc0[r0]);
+        if (!((x.lt0 >> r0) & 1u) && td != 0) {
+          const int tx = (16384 + (td < 0 ? -td : td) / 2) / td;
+          const int dsf = clip3i(-1024, 1023, (tb * tx + 32) >> 6);
+          m0x = (dsf * mcx + 128) >> 8;
+          m0y = (dsf * mcy + 128) >> 8;
+          m1x = m0x - mcx;
+          m1y = m0y - mcy;
+        }
+        set_motion(blk, r0, m0x, m0y);
+        set_motion1(blk, 0, m1x, m1y);
+      }
+    }
   }
 
   VTS_HD VTS_INLINE void skip_mb(int addr, int qp) {
     begin_mb(addr);
+    if (s->is_p == kSliceB) {  // B_Skip (8.4.1.2)
+      cur().type = kMbSkip;
+      cur().qp = static_cast<uint8_t>(qp);
+      cur1().direct = 0x0f | kDirect16;
+      direct_pred(addr, 0xffffu);
+      return;
+    }
     skip_body(addr, qp);
   }
   // P_Skip (8.4.1.1) of the macroblock begin_mb has started
@@ -518,13 +708,124 @@ struct Parser {
     for (int i = 0; i < 16; ++i) set_motion(i, 0, px, py);
   }
 
+  // mb_pred / sub_mb_pred of a B macroblock (7.3.5.1-2, Tables 7-14, 7-18)
+  // and its motion: partitions in order, list 0 before list 1 of each
+  // (sub-)partition, direct partitions by 8.4.1.2 in place
+  VTS_HD bool b_inter(int addr, int mb_type) {
+    uint8_t *pm = sc->pm;
+    int8_t *sub = sc->sub, *r0 = sc->refs, *r1 = sc->refs1;
+    int shape;
+    for (int k = 0; k < 4; ++k) {
+      pm[k] = 0;
+      sub[k] = 0;
+      r0[k] = r1[k] = -1;
+    }
+    if (mb_type == 0) {  // B_Direct_16x16
+      cur1().direct = 0x0f | kDirect16;
+      direct_pred(addr, 0xffffu);
+      return true;
+    }
+    if (mb_type <= 3) {
+      shape = 0;
+      pm[0] = static_cast<uint8_t>(mb_type);
+    } else if (mb_type < 22) {
+      shape = (mb_type & 1) ? 2 : 1;
+      pm[0] = kBPart[mb_type] & 3;
+      pm[1] = kBPart[mb_type] >> 2;
+    } else {
+      shape = 3;
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = br.ue();
+        if (v > 12) {
+          err |= DEC_E_SYNTAX;
+          return false;
+        }
+        pm[k] = kBSub[v] & 3;
+        sub[k] = static_cast<int8_t>(kBSub[v] >> 2);
+      }
+    }
+    const int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
+    for (int l = 0; l < 2; ++l) {
+      const int nref = l ? bc.x->num_ref1 : s->num_ref;
+      int8_t *rr = l ? r1 : r0;
+      for (int k = 0; k < nparts; ++k) {
+        if (!((pm[k] >> l) & 1)) continue;
+        const uint32_t rv = nref > 1 ? (nref == 2 ? static_cast<uint32_t>(!br.bit()) : br.ue()) : 0u;
+        if (rv >= static_cast<uint32_t>(nref) || (l ? bc.x->ref_slot1[rv & 31] : s->ref_slot[rv & 31]) < 0) {
+          err |= DEC_E_NO_REF;
+          return false;
+        }
+        rr[k] = static_cast<int8_t>(rv);
+      }
+    }
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < nparts; ++k) {
+        if (!((pm[k] >> l) & 1)) continue;
+        const int nsub = shape < 3 ? 1 : (sub[k] == 0 ? 1 : (sub[k] == 3 ? 4 : 2));
+        for (int q = 0; q < nsub; ++q) {
+          sc->mvd[l][4 * k + q][0] = br.se();
+          sc->mvd[l][4 * k + q][1] = br.se();
+        }
+      }
+    uint32_t done = 0;
+    for (int k = 0; k < nparts; ++k) {
+      int nsub = 1, pw, ph, x0, y0;
+      if (shape == 0) { pw = ph = 16; x0 = y0 = 0; }
+      else if (shape == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * k; }
+      else if (shape == 2) { pw = 8; ph = 16; x0 = 8 * k; y0 = 0; }
+      else {
+        x0 = 8 * (k & 1);
+        y0 = 8 * (k >> 1);
+        nsub = sub[k] == 0 ? 1 : (sub[k] == 3 ? 4 : 2);
+        pw = (sub[k] == 0 || sub[k] == 1) ? 8 : 4;
+        ph = (sub[k] == 0 || sub[k] == 2) ? 8 : 4;
+      }
+      if (pm[k] == 0) {  // B_Direct_8x8
+        const uint32_t bm = 0x33u << ((y0 / 4) * 4 + x0 / 4);
+        cur1().direct |= static_cast<uint8_t>(1u << k);
+        direct_pred(addr, bm);
+        if (err) return false;
+        done |= bm;
+        continue;
+      }
+      for (int q = 0; q < nsub; ++q) {
+        int sx = x0, sy = y0;
+        if (shape == 3) {
+          if (sub[k] == 1) sy += 4 * q;
+          else if (sub[k] == 2) sx += 4 * q;
+          else if (sub[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+        }
+        int v[2][2] = {{0, 0}, {0, 0}};
+        for (int l = 0; l < 2; ++l) {
+          if (!((pm[k] >> l) & 1)) continue;
+          int px, py;
+          mv_pred(addr, sx, sy, pw, ph, l ? r1[k] : r0[k], done, &px, &py, l);
+          v[l][0] = px + sc->mvd[l][4 * k + q][0];
+          v[l][1] = py + sc->mvd[l][4 * k + q][1];
+          if (v[l][0] < -32768 || v[l][0] > 32767 || v[l][1] < -32768 || v[l][1] > 32767) {
+            err |= DEC_E_SYNTAX;
+            return false;
+          }
+        }
+        for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
+          for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
+            set_motion(yy * 4 + xx, (pm[k] & 1) ? r0[k] : -1, v[0][0], v[0][1]);
+            set_motion1(yy * 4 + xx, (pm[k] & 2) ? r1[k] : -1, v[1][0], v[1][1]);
+            done |= 1u << (yy * 4 + xx);
+          }
+      }
+    }
+    return true;
+  }
+
   // macroblock_layer(); returns false to stop the slice
   VTS_HD VTS_INLINE bool mb_layer(int addr, int *qp) {
     begin_mb(addr);
     MbRec &m = cur();
     const int mb_type = static_cast<int>(br.ue());
-    const int itype = s->is_p ? mb_type - 5 : mb_type;  // < 0: inter
-    if (mb_type > (s->is_p ? 30 : 25)) {
+    const int intra0 = s->is_p == kSliceB ? 23 : (s->is_p ? 5 : 0);  // Tables 7-11, 7-13, 7-14
+    const int itype = mb_type - intra0;  // < 0: inter
+    if (mb_type > intra0 + 25) {
       err |= DEC_E_SYNTAX;
       return false;
     }
@@ -590,6 +891,9 @@ struct Parser {
       const uint32_t cm = br.ue();
       if (cm > 3) err |= DEC_E_SYNTAX;
       m.modes = static_cast<uint8_t>(pm | ((cm & 3) << 2));
+    } else if (s->is_p == kSliceB) {
+      m.type = kMbInter;
+      if (!b_inter(addr, mb_type)) return false;
     } else {  // inter
       m.type = kMbInter;
       const int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
@@ -734,7 +1038,7 @@ struct Parser {
 // the arena.  Returns DEC_E_* bits.
 VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams P,
                                         MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena, uint32_t epoch,
-                                        FullScratch *sc) {
+                                        FullScratch *sc, const BCtx &bc) {
   const uint8_t *nal = es + s.nal_offset;
   Parser p;
   p.s = &s;
@@ -754,7 +1058,11 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &
   p.tslots = 0;
   p.lvl_prev = kNoLevel;
   p.pf_col = -1;
+  p.bc = bc;
+  p.bframes = P.bframes;
+  p.direct8x8 = P.direct8x8;
   const int nmb = P.mb_width * P.mb_height;
+  if (s.is_p == kSliceB && (!bc.x || !bc.col || !P.bframes)) return DEC_E_NO_REF;
   int32_t last = s.nal_size - 1;
   while (last > 0 && nal[last] == 0) --last;
   if (last <= 0) return DEC_E_SYNTAX;

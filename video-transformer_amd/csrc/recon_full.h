@@ -42,8 +42,62 @@ VTS_HD VTS_INLINE int level_scale(int m, int i, int j) {
   return 16 * kNv[m][k];
 }
 
+// 8.4.2.3 weighted sample prediction of one block, reduced to one form per
+// colour component c (0 Y, 1 Cb, 2 Cr): bi-predicted
+//   Clip1(((p0 w0 + p1 w1 + 2^lwd) >> (lwd + 1)) + o)
+// (explicit: the table's weights, o = (o0 + o1 + 1) >> 1; implicit 8.4.2.3.1:
+// lwd 5, o 0; default: w 1, lwd 0), single list
+//   Clip1(((p w0 + round) >> lwd) + o), round = 2^(lwd - 1) for lwd >= 1
+// (default: w 1, lwd 0, o 0).
+struct Wp {
+  bool both;
+  int lwd[3], w0[3], w1[3], o[3];
+};
+// r0 / r1: refIdxL0 / L1 (< 0: list unused); x null: default prediction
+VTS_HD VTS_INLINE Wp wp_make(const SliceExt *x, int r0, int r1) {
+  Wp W;
+  W.both = r0 >= 0 && r1 >= 0;
+  const int mode = x ? x->wmode : 0;
+  int iw0 = 32, iw1 = 32;
+  if (mode == 2 && W.both) {
+    const int tb = clip3(-128, 127, x->poc - x->poc0[r0 & 31]), td = clip3(-128, 127, x->poc1[r1 & 31] - x->poc0[r0 & 31]);
+    if (td != 0 && !((x->lt0 >> (r0 & 31)) & 1u) && !((x->lt1 >> (r1 & 31)) & 1u)) {
+      const int tx = (16384 + iabs(td / 2)) / td;
+      const int dsf = clip3(-1024, 1023, (tb * tx + 32) >> 6);
+      if ((dsf >> 2) >= -64 && (dsf >> 2) <= 128) {
+        iw0 = 64 - (dsf >> 2);
+        iw1 = dsf >> 2;
+      }
+    }
+  }
+  for (int c = 0; c < 3; ++c) {
+    if (mode == 1) {
+      W.lwd[c] = c ? x->cwd : x->lwd;
+      const int wa = r0 >= 0 ? x->w[0][r0 & 31][2 * c] : 0, oa = r0 >= 0 ? x->w[0][r0 & 31][2 * c + 1] : 0;
+      const int wb = r1 >= 0 ? x->w[1][r1 & 31][2 * c] : 0, ob = r1 >= 0 ? x->w[1][r1 & 31][2 * c + 1] : 0;
+      W.w0[c] = W.both || r0 >= 0 ? wa : wb;
+      W.w1[c] = wb;
+      W.o[c] = W.both ? (oa + ob + 1) >> 1 : (r0 >= 0 ? oa : ob);
+    } else {
+      W.lwd[c] = mode == 2 && W.both ? 5 : 0;
+      W.w0[c] = mode == 2 && W.both ? iw0 : 1;
+      W.w1[c] = mode == 2 && W.both ? iw1 : 1;
+      W.o[c] = 0;
+    }
+  }
+  return W;
+}
+// p: the used list's prediction when only one list is used
+VTS_HD VTS_INLINE int wp_apply(const Wp &W, int c, int p0, int p1) {
+  const int l = W.lwd[c];
+  if (W.both) return clip1(((p0 * W.w0[c] + p1 * W.w1[c] + (1 << l)) >> (l + 1)) + W.o[c]);
+  return clip1(((p0 * W.w0[c] + (l ? 1 << (l - 1) : 0)) >> l) + W.o[c]);
+}
+
 struct ReconCtx {
   const MbRec *recs;        // this frame's records
+  const MbRecB *recs1;      // ... their list-1 halves (streams with B slices), else null
+  const SliceExt *exts;     // the window's SliceExt records
   const int16_t *arena;
   const FullSlice *slices;  // window slices
   uint8_t *surf;            // ring base
@@ -168,14 +222,32 @@ struct MbRecon {
   VTS_HD VTS_INLINE int ly(int x, int y) const { return Y[static_cast<int64_t>(y) * c.pitch + x]; }
   VTS_HD VTS_INLINE int lc(int pl, int x, int y) const { return UV[static_cast<int64_t>(y) * c.pitch + 2 * x + pl]; }
 
-  // ---- inter (8.4.2.2)
+  // ---- inter (8.4.2.2, weighted 8.4.2.3): both lists' predictions of the
+  // block, combined into pred_y / pred_c
   VTS_HD void inter_block(int b) {
     const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
-    const int rs = m.ref_slot[p8];
+    const int r0 = m.ref_slot[p8] >= 0 ? m.ref[p8] : -1;
+    const MbRecB *m1 = c.recs1 ? &c.recs1[mb] : nullptr;
+    const int r1 = m1 && m1->ref_slot1[p8] >= 0 ? m1->ref1[p8] : -1;
+    uint8_t ty[2][16] = {}, tc[2][2][4] = {};
+    if (r0 >= 0) pred_list(b, m.ref_slot[p8], m.mv[b][0], m.mv[b][1], ty[0], tc[0]);
+    if (r1 >= 0) pred_list(b, m1->ref_slot1[p8], m1->mv1[b][0], m1->mv1[b][1], ty[1], tc[1]);
+    const FullSlice &sl = c.slices[m.slice];
+    const Wp W = wp_make(sl.ext >= 0 ? &c.exts[sl.ext] : nullptr, r0, r1);
+    const int u = r0 >= 0 ? 0 : 1;  // the list a single-list block uses
+    const int bx = (b & 3) * 4, by = (b >> 2) * 4;
+    for (int i = 0; i < 16; ++i)
+      pred_y[(by + i / 4) * 16 + bx + i % 4] = static_cast<uint8_t>(wp_apply(W, 0, ty[u][i], ty[1][i]));
+    for (int pl = 0; pl < 2; ++pl)
+      for (int i = 0; i < 4; ++i)
+        pred_c[pl][(by / 2 + i / 2) * 8 + bx / 2 + i % 2] =
+            static_cast<uint8_t>(wp_apply(W, 1 + pl, tc[u][pl][i], tc[1][pl][i]));
+  }
+  // one list's 4x4 luma + 2x2 Cb / Cr prediction of raster block b from the picture in ring slot rs
+  VTS_HD void pred_list(int b, int rs, int mvx, int mvy, uint8_t *oy, uint8_t (*oc)[4]) {
     const uint8_t *R = c.surf + static_cast<int64_t>(rs) * c.frame_stride;
     const uint8_t *RUV = R + c.uv_off;
     const int W = c.mbw * 16, H = c.mbh * 16;
-    const int mvx = m.mv[b][0], mvy = m.mv[b][1];
     const int bx = mx * 16 + (b & 3) * 4, by = my * 16 + (b >> 2) * 4;
     const int xi = bx + (mvx >> 2), yi = by + (mvy >> 2), xf = mvx & 3, yf = mvy & 3;
     uint8_t w[9][9];
@@ -222,7 +294,7 @@ struct MbRecon {
             default: v = (mm + ss + 1) >> 1; break;
           }
         }
-        pred_y[((b >> 2) * 4 + y) * 16 + (b & 3) * 4 + x] = static_cast<uint8_t>(v);
+        oy[y * 4 + x] = static_cast<uint8_t>(v);
       }
     // chroma 2x2 (8.4.2.2.2)
     const int cw = W / 2, ch = H / 2;
@@ -238,7 +310,7 @@ struct MbRecon {
           const int C = RUV[static_cast<int64_t>(yb) * c.pitch + 2 * xa + pl];
           const int D = RUV[static_cast<int64_t>(yb) * c.pitch + 2 * xb + pl];
           const int v = ((8 - cfx) * (8 - cfy) * A + cfx * (8 - cfy) * B + (8 - cfx) * cfy * C + cfx * cfy * D + 32) >> 6;
-          pred_c[pl][((b >> 2) * 2 + y) * 8 + (b & 3) * 2 + x] = static_cast<uint8_t>(v);
+          oc[pl][y * 2 + x] = static_cast<uint8_t>(v);
         }
       }
   }
@@ -581,7 +653,8 @@ struct MbRecon {
     const int dummy_dc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (m.type == kMbInter || m.type == kMbSkip) {
       for (int b = 0; b < 16; ++b) {
-        const int rs = m.ref_slot[(b >> 3) * 2 + ((b & 3) >> 1)];
+        const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+        const int rs = m.ref_slot[p8] >= 0 ? m.ref_slot[p8] : (c.recs1 ? c.recs1[mb].ref_slot1[p8] : -1);
         if (rs < 0) {
           err |= DEC_E_NO_REF;
           return;
@@ -653,13 +726,38 @@ struct MbRecon {
 // ---------------------------------------------------------- deblocking (8.7)
 VTS_HD VTS_INLINE bool mb_is_intra(const MbRec &r) { return r.type == kMbI4x4 || r.type == kMbI16 || r.type == kMbPcm; }
 
-VTS_HD VTS_INLINE int bs_of(const MbRec &p, int bp, const MbRec &q, int bq, bool mb_edge) {
+VTS_HD VTS_INLINE bool mv_far(int ax, int ay, int bx, int by) { return iabs(ax - bx) >= 4 || iabs(ay - by) >= 4; }
+
+// bS 1 / 0 from the motion of two inter blocks (8.7.2.1, mixedModeEdgeFlag 0):
+// reference pictures compared as pictures (ring slots, -1 = list unused) and
+// as the set a bi-predicted block uses; mv X = (x, y) of list X
+VTS_HD VTS_INLINE int bs_motion(int p0, int p1, int pm0x, int pm0y, int pm1x, int pm1y, int q0, int q1, int qm0x,
+                                int qm0y, int qm1x, int qm1y) {
+  const int np = (p0 >= 0) + (p1 >= 0), nq = (q0 >= 0) + (q1 >= 0);
+  if (np != nq) return 1;
+  if (np == 1) {
+    const bool lp = p0 < 0, lq = q0 < 0;
+    if ((lp ? p1 : p0) != (lq ? q1 : q0)) return 1;
+    return mv_far(lp ? pm1x : pm0x, lp ? pm1y : pm0y, lq ? qm1x : qm0x, lq ? qm1y : qm0y);
+  }
+  if (!((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0))) return 1;
+  const bool same = mv_far(pm0x, pm0y, qm0x, qm0y) || mv_far(pm1x, pm1y, qm1x, qm1y);
+  const bool cross = mv_far(pm0x, pm0y, qm1x, qm1y) || mv_far(pm1x, pm1y, qm0x, qm0y);
+  if (p0 != p1) return p0 == q0 ? same : cross;
+  return same && cross;
+}
+
+VTS_HD VTS_INLINE int bs_of(const MbRec &p, const MbRecB *p1, int bp, const MbRec &q, const MbRecB *q1, int bq,
+                            bool mb_edge) {
   if (mb_is_intra(p) || mb_is_intra(q)) return mb_edge ? 4 : 3;
   if (p.nz[bp] || q.nz[bq]) return 2;
   const int p8 = (bp >> 3) * 2 + ((bp & 3) >> 1), q8 = (bq >> 3) * 2 + ((bq & 3) >> 1);
-  if (p.ref_slot[p8] != q.ref_slot[q8]) return 1;
-  if (iabs(p.mv[bp][0] - q.mv[bq][0]) >= 4 || iabs(p.mv[bp][1] - q.mv[bq][1]) >= 4) return 1;
-  return 0;
+  if (!p1) {  // P pictures: one list
+    if (p.ref_slot[p8] != q.ref_slot[q8]) return 1;
+    return mv_far(p.mv[bp][0], p.mv[bp][1], q.mv[bq][0], q.mv[bq][1]);
+  }
+  return bs_motion(p.ref_slot[p8], p1->ref_slot1[p8], p.mv[bp][0], p.mv[bp][1], p1->mv1[bp][0], p1->mv1[bp][1],
+                   q.ref_slot[q8], q1->ref_slot1[q8], q.mv[bq][0], q.mv[bq][1], q1->mv1[bq][0], q1->mv1[bq][1]);
 }
 
 // one line across an edge: s[k * step], k = -4..3 (p3..q3)
@@ -726,7 +824,9 @@ VTS_HD inline void deblock_mb(const ReconCtx &c, int slot, int a) {
   for (int dir = 0; dir < 2; ++dir)
     for (int e = 0; e < 4; ++e) {
       if (e == 0 && !(dir ? top : left)) continue;
-      const MbRec &p = e == 0 ? c.recs[dir ? a - c.mbw : a - 1] : q;
+      const int pa = e == 0 ? (dir ? a - c.mbw : a - 1) : a;
+      const MbRec &p = c.recs[pa];
+      const MbRecB *p1 = c.recs1 ? &c.recs1[pa] : nullptr, *q1 = c.recs1 ? &c.recs1[a] : nullptr;
       const int qpp = p.type == kMbPcm ? 0 : p.qp, qpq = q.type == kMbPcm ? 0 : q.qp;
       {
         const int qpav = (qpp + qpq + 1) >> 1;
@@ -736,7 +836,7 @@ VTS_HD inline void deblock_mb(const ReconCtx &c, int slot, int a) {
           for (int k = 0; k < 16; ++k) {
             const int xq = dir ? k : 4 * e, yq = dir ? 4 * e : k;
             const int xp = dir ? xq : (xq + 15) & 15, yp = dir ? (yq + 15) & 15 : yq;
-            const int bS = bs_of(p, (yp >> 2) * 4 + (xp >> 2), q, (yq >> 2) * 4 + (xq >> 2), e == 0);
+            const int bS = bs_of(p, p1, (yp >> 2) * 4 + (xp >> 2), q, q1, (yq >> 2) * 4 + (xq >> 2), e == 0);
             uint8_t *s = Y + static_cast<int64_t>(my * 16 + yq) * c.pitch + mx * 16 + xq;
             filter_line(s, dir ? c.pitch : 1, bS, false, iA, alpha, beta);
           }
@@ -751,7 +851,7 @@ VTS_HD inline void deblock_mb(const ReconCtx &c, int slot, int a) {
           for (int k = 0; k < 8; ++k) {
             const int xq = dir ? 2 * k : 4 * e, yq = dir ? 4 * e : 2 * k;
             const int xp = dir ? xq : (xq + 15) & 15, yp = dir ? (yq + 15) & 15 : yq;
-            const int bS = bs_of(p, (yp >> 2) * 4 + (xp >> 2), q, (yq >> 2) * 4 + (xq >> 2), e == 0);
+            const int bS = bs_of(p, p1, (yp >> 2) * 4 + (xp >> 2), q, q1, (yq >> 2) * 4 + (xq >> 2), e == 0);
             const int cx = dir ? k : 2 * e, cy = dir ? 2 * e : k;
             uint8_t *s = UV + static_cast<int64_t>(my * 8 + cy) * c.pitch + 2 * (mx * 8 + cx) + pl;
             filter_line(s, dir ? c.pitch : 2, bS, true, iA, alpha, beta);

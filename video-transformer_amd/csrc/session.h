@@ -37,6 +37,8 @@ struct Window {
   std::vector<int64_t> tb_off;
   std::vector<int32_t> tb_cnt, tb_L;
   int64_t fs0 = 0, fs1 = 0;        // general decoder: slices [fs0, fs1) of vts_ctx::fslices
+  std::vector<int32_t> plv_end;    // general decoder: parse launch j covers window slices
+                                   // [plv_end[j-1], plv_end[j]) (B pictures after their colocated picture)
 };
 
 // Downscaled copy of every decoded frame (transcode.hip), filled by run_all
@@ -128,6 +130,10 @@ struct vts_ctx {
   std::vector<vts::FullSlice> fslices;  // every window's slices (window-relative slots, arena)
   vts::FullSlice *d_fslices = nullptr;
   vts::MbRec *d_recs[2] = {nullptr, nullptr};
+  vts::MbRecB *d_recs1[2] = {nullptr, nullptr};  // list-1 halves (streams with B slices)
+  std::vector<vts::SliceExt> exts;      // B / weighted slices' SliceExt records (all windows)
+  vts::SliceExt *d_exts = nullptr;
+  std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock
   int16_t *d_arena[2] = {nullptr, nullptr};

@@ -92,6 +92,9 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   HIP_TRY(hipMalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
   if (!c->fslices.empty())
     HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
+  if (!c->exts.empty())
+    HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_levels, sizeof(int4) * std::max<size_t>(1, c->level_frames.size())));
   HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(), hipMemcpyHostToDevice));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
@@ -99,6 +102,8 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   const int64_t tw = (c->width / c->k) * (c->height / c->k);
   for (int r = 0; r < c->n_rings; ++r) {
     HIP_TRY(hipMalloc(&c->d_recs[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec)));
+    if (c->fprm.bframes)
+      HIP_TRY(hipMalloc(&c->d_recs1[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRecB)));
     HIP_TRY(hipMalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
     HIP_TRY(hipMalloc(&c->d_dbk[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(DbkInfo)));
     HIP_TRY(hipMalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
@@ -207,19 +212,40 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   c->n_frames = static_cast<int64_t>(t.size.size());
   if (c->n_frames == 0) return fail(VTS_E_FORMAT, "video track has no samples");
 
-  // presentation timestamps; output order must equal decode order
+  // presentation timestamps (sorted: frame i of every result is the i-th in
+  // presentation order); with B pictures the decode order differs and only the
+  // general decoder reorders (disp = presentation rank of each sample)
   c->pts.resize(static_cast<size_t>(c->n_frames));
+  c->disp.resize(static_cast<size_t>(c->n_frames));
   int64_t shift = 0;
   for (const EditEntry &ed : t.edits)
     if (ed.media_time >= 0) {
       shift = ed.media_time;
       break;
     }
+  bool reorder = false;
   for (int64_t i = 0; i < c->n_frames; ++i) {
     c->pts[i] = t.dts[i] + t.cts_offset[i] - shift;
-    if (i > 0 && c->pts[i] <= c->pts[i - 1])
-      return fail(VTS_E_UNSUPPORTED, "frame reordering (B-frames / ctts) is not supported");
+    reorder |= i > 0 && c->pts[i] <= c->pts[i - 1];
   }
+  {
+    std::vector<int64_t> ord(static_cast<size_t>(c->n_frames));
+    for (int64_t i = 0; i < c->n_frames; ++i) ord[static_cast<size_t>(i)] = i;
+    if (reorder)
+      std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return c->pts[a] < c->pts[b]; });
+    std::vector<int64_t> sorted(static_cast<size_t>(c->n_frames));
+    for (int64_t i = 0; i < c->n_frames; ++i) {
+      c->disp[static_cast<size_t>(ord[static_cast<size_t>(i)])] = i;
+      sorted[static_cast<size_t>(i)] = c->pts[ord[static_cast<size_t>(i)]];
+      if (i > 0 && sorted[static_cast<size_t>(i)] == sorted[static_cast<size_t>(i - 1)])
+        return fail(VTS_E_FORMAT, "two samples share a presentation time");
+    }
+    c->pts = sorted;
+  }
+  if (reorder && c->params.decoder == 1)
+    return fail(VTS_E_UNSUPPORTED, "frame reordering (B-frames / ctts) needs the general decoder");
+  if ((c->pps.weighted_pred || c->pps.weighted_bipred_idc) && c->params.decoder == 1)
+    return fail(VTS_E_UNSUPPORTED, "weighted prediction needs the general decoder");
 
   std::vector<uint8_t> es;
   std::vector<int64_t> es_off;
@@ -233,7 +259,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
 
   // General CAVLC decoder (decode_full.hip) when asked, or when the headers
   // show features outside the subset kernels (deblocking, several references)
-  if (c->params.decoder == 2 ||
+  if (c->params.decoder == 2 || reorder ||
       (c->params.decoder == 0 && wants_general(c, es, es_off, t.size, t.nal_length_size))) {
     VTS_TRY(build_general(c, es, es_off, t.size, t.nal_length_size, t.sps[0], t.pps[0]));
     return alloc_general(c, es.data());
@@ -1043,8 +1069,10 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->small.d);
   f(c->small.d_taps);
   f(c->d_fslices);
+  f(c->d_exts);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
+    f(c->d_recs1[r]);
     f(c->d_ilvl[r]);
     f(c->d_dbk[r]);
     f(c->d_arena[r]);

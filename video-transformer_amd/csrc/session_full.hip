@@ -36,6 +36,7 @@ constexpr int64_t kMinRingBytes = 1ll << 30;
 bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
                    const std::vector<uint32_t> &sizes, int nal_length_size) {
   if (c->pps.entropy_coding_mode) return true;  // CABAC
+  if (c->pps.weighted_pred || c->pps.weighted_bipred_idc) return true;
   if (c->sps.max_num_ref_frames > 1 || c->pps.num_ref_idx_l0_default_active > 1) return true;
   if (!c->pps.deblocking_filter_control_present) return true;  // deblocking on, offsets 0
   // the first pictures' slice headers: an active deblocking filter or several references
@@ -71,7 +72,10 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   c->fprm.cqp_off2 = facts.cqp_off2;
   c->fprm.cabac = c->pps.entropy_coding_mode;
   c->fprm.t8mode = facts.transform_8x8;
+  for (const SchedFrame &fr : frames) c->fprm.bframes |= fr.has_b ? 1 : 0;
+  c->fprm.direct8x8 = c->sps.direct_8x8_inference;
   const int64_t n = c->n_frames;
+  const std::vector<int64_t> &disp = c->disp;  // presentation rank per sample
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
 
   // levels and clean window starts
@@ -85,6 +89,9 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
     }
     level[static_cast<size_t>(f)] = l;
   }
+  // clean[x]: an intra picture no later picture predicts across, before which
+  // exactly the pictures [0, x) of the presentation order are decoded (so a
+  // window is the same range of frames in decode and presentation order)
   std::vector<uint8_t> clean(static_cast<size_t>(n), 0);
   {
     int64_t m = n;
@@ -92,7 +99,18 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
       m = std::min(m, minref[static_cast<size_t>(x)]);
       clean[static_cast<size_t>(x)] = frames[static_cast<size_t>(x)].intra && m >= x;
     }
+    int64_t mx = -1;
+    for (int64_t x = 0; x < n; ++x) {
+      if (mx != x - 1) clean[static_cast<size_t>(x)] = 0;
+      mx = std::max(mx, disp[static_cast<size_t>(x)]);
+    }
   }
+  // parse order: a B picture's direct prediction reads its colocated
+  // picture's records, so it parses one launch after that picture's
+  std::vector<int32_t> plevel(static_cast<size_t>(n), 0);
+  for (int64_t f = 0; f < n; ++f)
+    for (int64_t col : frames[static_cast<size_t>(f)].cols)
+      plevel[static_cast<size_t>(f)] = std::max(plevel[static_cast<size_t>(f)], plevel[static_cast<size_t>(col)] + 1);
   // coefficient blocks each slice may need (CAVLC bound, h264_full.h)
   std::vector<int64_t> cap(slices.size());
   int64_t cap_total = 0;
@@ -143,12 +161,19 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
 
   // per window: device slices (window-relative slots and arena), level lists
   c->fslices.clear();
+  c->exts.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
   for (Window &w : c->windows) {
     w.fs0 = static_cast<int64_t>(c->fslices.size());
     int64_t arena = 0, maxl = 0;
+    int32_t maxp = 0;
+    for (int64_t f = w.f0; f < w.f1; ++f) maxp = std::max(maxp, plevel[static_cast<size_t>(f)]);
+    w.plv_end.clear();
+    auto slot_of = [&](int64_t f) { return static_cast<int16_t>(disp[static_cast<size_t>(f)] - w.f0); };
+    for (int32_t pl = 0; pl <= maxp; ++pl) {
     for (int64_t f = w.f0; f < w.f1; ++f) {
+      if (plevel[static_cast<size_t>(f)] != pl) continue;
       const SchedFrame &fr = frames[static_cast<size_t>(f)];
       maxl = std::max(maxl, level[static_cast<size_t>(f)]);
       for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
@@ -156,7 +181,7 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
         FullSlice d{};
         d.nal_offset = s.nal_offset;
         d.nal_size = s.nal_size;
-        d.slot = static_cast<int32_t>(f - w.f0);
+        d.slot = slot_of(f);
         d.first_mb = s.first_mb;
         d.data_byte = s.data_byte;
         d.data_bit = s.data_bit;
@@ -169,20 +194,47 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
         d.arena = static_cast<uint32_t>(arena);
         d.arena_cap = static_cast<uint32_t>(cap[static_cast<size_t>(si)]);
         arena += cap[static_cast<size_t>(si)];
+        d.ext = -1;
         for (int i = 0; i < 32; ++i) {
           const int64_t r = s.ref[i];
           if (r >= 0 && (r < w.f0 || r >= f)) return fail(VTS_E_UNSUPPORTED, "reference crosses a window boundary");
-          d.ref_slot[i] = static_cast<int16_t>(r >= 0 ? r - w.f0 : -1);
+          d.ref_slot[i] = r >= 0 ? slot_of(r) : static_cast<int16_t>(-1);
+        }
+        if (s.needs_ext()) {
+          SliceExt x;
+          std::memset(&x, 0, sizeof x);
+          x.num_ref1 = s.num_ref1;
+          x.direct_spatial = s.direct_spatial;
+          x.wmode = s.wmode;
+          x.lwd = s.lwd;
+          x.cwd = s.cwd;
+          x.col_short = s.col_short;
+          x.poc = s.poc;
+          x.lt0 = s.lt0;
+          x.lt1 = s.lt1;
+          for (int i = 0; i < 32; ++i) {
+            const int64_t r = s.ref1[i];
+            if (r >= 0 && (r < w.f0 || r >= f)) return fail(VTS_E_UNSUPPORTED, "reference crosses a window boundary");
+            x.ref_slot1[i] = r >= 0 ? slot_of(r) : static_cast<int16_t>(-1);
+            x.poc0[i] = s.poc0[i];
+            x.poc1[i] = s.poc1[i];
+          }
+          std::memcpy(x.w, s.w, sizeof x.w);
+          // the slices of a picture share one record
+          if (c->exts.empty() || std::memcmp(&c->exts.back(), &x, sizeof x) != 0) c->exts.push_back(x);
+          d.ext = static_cast<int32_t>(c->exts.size()) - 1;
         }
         c->fslices.push_back(d);
       }
+    }
+    w.plv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->fslices.size()) - w.fs0));
     }
     if (arena > 0xffffffffll) return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
     w.fs1 = static_cast<int64_t>(c->fslices.size());
     c->arena_blocks = std::max(c->arena_blocks, arena);
     std::vector<std::vector<int4>> lv(static_cast<size_t>(maxl + 1));
     for (int64_t f = w.f0; f < w.f1; ++f)
-      lv[static_cast<size_t>(level[static_cast<size_t>(f)])].push_back(make_int4(static_cast<int>(f - w.f0), 0, 0, 0));
+      lv[static_cast<size_t>(level[static_cast<size_t>(f)])].push_back(make_int4(slot_of(f), 0, 0, 0));
     for (auto &l : lv) {
       if (l.empty()) continue;
       w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
@@ -224,21 +276,28 @@ int run_general(vts_ctx *c) {
     HIP_TRY(hipEventRecord(E[0], sp));
     FullParseArgs pa{};
     pa.es = c->d_es;
-    pa.slices = c->d_fslices + w.fs0;
-    pa.n_slices = static_cast<int32_t>(w.fs1 - w.fs0);
-    pa.slice0 = 0;
     pa.epoch = epoch;
     pa.recs = c->d_recs[r];
+    pa.recs1 = c->d_recs1[r];
+    pa.exts = c->d_exts;
     pa.ilvl = c->d_ilvl[r];
     pa.arena = c->d_arena[r];
     pa.err = c->d_err;
     pa.P = c->fprm;
-    VTS_TRY(parse_full_launch(pa, sp));
+    for (size_t j = 0; j < w.plv_end.size(); ++j) {  // B pictures after their colocated pictures
+      const int32_t b0 = j ? w.plv_end[j - 1] : 0;
+      pa.slices = c->d_fslices + w.fs0 + b0;
+      pa.n_slices = w.plv_end[j] - b0;
+      pa.slice0 = b0;
+      VTS_TRY(parse_full_launch(pa, sp));
+    }
     HIP_TRY(hipEventRecord(E[1], sp));
     HIP_TRY(hipStreamWaitEvent(sd, E[1], 0));
     HIP_TRY(hipEventRecord(E[5], sd));
     FullReconArgs ra{};
     ra.recs = c->d_recs[r];
+    ra.recs1 = c->d_recs1[r];
+    ra.exts = c->d_exts;
     ra.ilvl = c->d_ilvl[r];
     ra.dbk = c->d_dbk[r];
     ra.arena = c->d_arena[r];
