@@ -40,6 +40,9 @@
  * device parser (data only; no product code is linked) */
 #include "../video-transformer_amd/csrc/h264_cabac_tables.h"
 
+/* CABAC synthesis mode (fo_cabac_convert, test infrastructure) */
+typedef struct fo_enc_s fo_enc;
+static fo_enc *g_enc;      /* non-null: synthesis mode */
 #define FO_E_FORMAT -8
 #define FO_E_UNSUPPORTED -9
 #define FO_E_DECODE -12
@@ -464,6 +467,8 @@ typedef struct {
   uint32_t cbf;     /* CABAC coded_block_flag: bit 0 Intra16x16 DC, 1 + raster luma 4x4,
                        17 + iCbCr chroma DC, 19 + 4 iCbCr + raster chroma AC */
   int qpd;          /* mb_qp_delta */
+  int direct8;      /* B: 8x8 quadrants predicted in direct mode (B_Skip / B_Direct_16x16: 15 and d16) */
+  int d16;          /* B_Skip or B_Direct_16x16 */
 } fo_mb;
 
 typedef struct {
@@ -490,6 +495,7 @@ typedef struct {
   int prev_mmco5;                   /* the previous picture had memory_management_control_operation 5 */
   int flags;
   char *err;
+  int64_t enc_pos_qp, enc_pos_data;  /* synthesis: RBSP bit positions in the source slice header */
 } fo_dec;
 
 static int fo_fail(fo_dec *d, int rc, const char *msg) {
@@ -1544,11 +1550,11 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
       }
     }
   }
-  if (P->cabac && is_p) {
+  if (g_enc) d->enc_pos_qp = fb_index(&b, 0);
+  if (P->cabac && is_p && !g_enc) {
     int idc = (int)fb_ue(&b);
     if (idc != 0) return fo_fail(d, FO_E_UNSUPPORTED, "cabac_init_idc 1/2 (only the idc 0 tables are restated)");
   }
-  if (P->cabac && is_b) return fo_fail(d, FO_E_UNSUPPORTED, "CABAC B slices");
   h.qp = P->pic_init_qp + fb_se(&b);
   if (P->deblock_ctrl) {
     h.dbk_idc = (int)fb_ue(&b);
@@ -1661,6 +1667,7 @@ static int decode_slice(fo_dec *d, fo_pic *cur, const uint8_t *nal, int64_t len,
   if (is_b && (!c.list1[0] || !c.list1[0]->mref[0]))
     return fo_fail(d, FO_E_DECODE, "B slice without a colocated picture (RefPicList1[0])");
 
+  if (g_enc) d->enc_pos_data = fb_index(&b, 0);
   if (P->cabac) return slice_data_cabac(&c, &b, &h, is_p, stop);
   /* 7.3.4 slice_data */
   int addr = h.first_mb, more = 1, qp = h.qp;
@@ -1962,6 +1969,8 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
     m->type = 4;
     m->qp = *qp;
     if (c->is_b) {
+      m->direct8 = 15;
+      m->d16 = 1;
       int rc = direct_pred(c, addr, 0xffff);
       if (rc) return rc;
     } else {
@@ -2117,6 +2126,56 @@ static const uint8_t SIG8[63] = VTS_SIG8x8_DATA;
 static const uint8_t LAST8[63] = VTS_LAST8x8_DATA;
 static const int ZZ8[64] = VTS_ZZ8_DATA;
 
+/* CABAC stream synthesis (TEST INFRASTRUCTURE, fo_cabac_convert below): the
+ * decoder below runs unchanged, but every bin it asks for is chosen by a
+ * seeded random policy and arithmetic-coded (9.3.4) instead of being read, so
+ * the bitstream written is exactly what the decoder would have parsed. */
+struct fo_enc_s {
+  uint8_t *out;            /* bit writer */
+  int64_t cap, nbits;
+  uint32_t low, range;
+  int first, outstanding;
+  uint64_t rng;
+  int last_mb;             /* end_of_slice_flag is 1 after this macroblock */
+  int nref, ref_ones;      /* ref_idx being chosen: entries of the list, ones so far */
+  int overflow;
+};
+
+static void enc_write(fo_enc *e, int b) {
+  if (e->nbits >= e->cap * 8) { e->overflow = 1; return; }
+  if (b) e->out[e->nbits >> 3] |= (uint8_t)(0x80 >> (e->nbits & 7));
+  e->nbits++;
+}
+static void enc_put(fo_enc *e, int b) { /* PutBit (9.3.4.2) */
+  if (e->first) e->first = 0;
+  else enc_write(e, b);
+  for (; e->outstanding > 0; e->outstanding--) enc_write(e, !b);
+}
+static void enc_renorm(fo_enc *e) { /* RenormE */
+  while (e->range < 256) {
+    if (e->low < 256) enc_put(e, 0);
+    else if (e->low >= 512) { e->low -= 512; enc_put(e, 1); }
+    else { e->low -= 256; e->outstanding++; }
+    e->range <<= 1;
+    e->low <<= 1;
+  }
+}
+static uint32_t enc_rand(fo_enc *e) {
+  e->rng = e->rng * 6364136223846793005ull + 1442695040888963407ull;
+  return (uint32_t)(e->rng >> 33);
+}
+/* probability (per 1024) of a 1 bin for ctxIdx, by syntax element (Table 9-34) */
+static int enc_p1(int ctx) {
+  if (ctx >= 11 && ctx <= 13) return 300;   /* mb_skip_flag P */
+  if (ctx >= 24 && ctx <= 26) return 300;   /* mb_skip_flag B */
+  if (ctx >= 40 && ctx <= 53) return 380;   /* mvd prefix */
+  if (ctx >= 60 && ctx <= 63) return 250;   /* mb_qp_delta */
+  if (ctx >= 105 && ctx <= 226) return 330; /* significant / last */
+  if (ctx >= 227 && ctx <= 275) return 300; /* coeff_abs_level_minus1 */
+  if (ctx >= 402 && ctx <= 459) return 330; /* 8x8 significant / last / levels */
+  return 512;
+}
+
 typedef struct {
   fb_t *b;
   uint32_t range, offset;
@@ -2125,6 +2184,14 @@ typedef struct {
 
 static void cab_start(fo_cab *k) { /* 9.3.1.2 */
   k->range = 510;
+  if (g_enc) { /* 9.3.4.1 */
+    g_enc->low = 0;
+    g_enc->range = 510;
+    g_enc->first = 1;
+    g_enc->outstanding = 0;
+    k->offset = 0;
+    return;
+  }
   k->offset = fb_bits(k->b, 9);
 }
 static void cab_init(fo_cab *k, int is_i, int qp) { /* 9.3.1.1 */
@@ -2137,6 +2204,28 @@ static void cab_init(fo_cab *k, int is_i, int qp) { /* 9.3.1.1 */
 }
 static int cab_dec(fo_cab *k, int ctx) { /* 9.3.3.2.1 DecodeDecision */
   int s = k->state[ctx], bin;
+  if (g_enc) { /* synthesis: choose the bin, EncodeDecision (9.3.4.2) */
+    fo_enc *e = g_enc;
+    if (ctx >= 54 && ctx <= 59) { /* ref_idx: unary, stays inside the list */
+      if (ctx <= 57) e->ref_ones = 0;
+      bin = e->ref_ones + 1 < e->nref && (int)(enc_rand(e) & 1023) < 300;
+      e->ref_ones += bin;
+    } else {
+      bin = (int)(enc_rand(e) & 1023) < enc_p1(ctx);
+    }
+    uint32_t lps = RANGE_LPS[s][(e->range >> 6) & 3];
+    e->range -= lps;
+    if (bin != k->mps[ctx]) {
+      e->low += e->range;
+      e->range = lps;
+      if (s == 0) k->mps[ctx] = (uint8_t)(1 - k->mps[ctx]);
+      k->state[ctx] = TRANS_LPS[s];
+    } else if (s < 62) {
+      k->state[ctx] = (uint8_t)(s + 1);
+    }
+    enc_renorm(e);
+    return bin;
+  }
   uint32_t lps = RANGE_LPS[s][(k->range >> 6) & 3];
   k->range -= lps;
   if (k->offset >= k->range) {
@@ -2156,11 +2245,37 @@ static int cab_dec(fo_cab *k, int ctx) { /* 9.3.3.2.1 DecodeDecision */
   return bin;
 }
 static int cab_bypass(fo_cab *k) { /* 9.3.3.2.3 */
+  if (g_enc) { /* EncodeBypass (9.3.4.4); suffixes stay short */
+    fo_enc *e = g_enc;
+    int bin = (int)(enc_rand(e) & 1023) < 350;
+    e->low <<= 1;
+    if (bin) e->low += e->range;
+    if (e->low >= 1024) { enc_put(e, 1); e->low -= 1024; }
+    else if (e->low < 512) enc_put(e, 0);
+    else { e->low -= 512; e->outstanding++; }
+    return bin;
+  }
   k->offset = (k->offset << 1) | fb_bit(k->b);
   if (k->offset >= k->range) { k->offset -= k->range; return 1; }
   return 0;
 }
 static int cab_term(fo_cab *k) { /* 9.3.3.2.2.3: binVal 1 ends parsing without renormalisation */
+  if (g_enc) { /* EncodeTerminate (9.3.4.5): 1 only for end_of_slice_flag after the slice's last macroblock */
+    fo_enc *e = g_enc;
+    int bin = e->last_mb < 0;
+    e->range -= 2;
+    if (bin) {
+      e->low += e->range;
+      e->range = 2; /* EncodeFlush */
+      enc_renorm(e);
+      enc_put(e, (e->low >> 9) & 1);
+      enc_write(e, (e->low >> 8) & 1);
+      enc_write(e, 1); /* rbsp_stop_one_bit */
+    } else {
+      enc_renorm(e);
+    }
+    return bin;
+  }
   k->range -= 2;
   if (k->offset >= k->range) return 1;
   while (k->range < 256) {
@@ -2177,16 +2292,46 @@ static int cab_fl3(fo_cab *k, int ctx) { /* FL, cMax 7: bins least significant f
 }
 
 /* mb_type of an I macroblock (Table 9-36): prefix ctxIdx 3 (I slice, inc from
- * the neighbours) or the P-slice suffix at ctxIdx 17; returns 0..25 */
+ * the neighbours) or the suffix of a P (ctxIdxOffset 17) or B (32) slice's
+ * intra mb_type (suffix = its offset); returns 0..25 */
 static int cab_i_type(fo_cab *k, int suffix, int inc0) {
-  if (!cab_dec(k, suffix ? 17 : 3 + inc0)) return 0; /* I_NxN */
+  if (!cab_dec(k, suffix ? suffix : 3 + inc0)) return 0; /* I_NxN */
   if (cab_term(k)) return 25;                       /* I_PCM */
-  int luma = cab_dec(k, suffix ? 18 : 6);
-  int chroma = cab_dec(k, suffix ? 19 : 7);
-  if (chroma) chroma += cab_dec(k, suffix ? 19 : 8);
-  int pm = cab_dec(k, suffix ? 20 : 9) << 1;
-  pm |= cab_dec(k, suffix ? 20 : 10);
+  int luma = cab_dec(k, suffix ? suffix + 1 : 6);
+  int chroma = cab_dec(k, suffix ? suffix + 2 : 7);
+  if (chroma) chroma += cab_dec(k, suffix ? suffix + 2 : 8);
+  int pm = cab_dec(k, suffix ? suffix + 3 : 9) << 1;
+  pm |= cab_dec(k, suffix ? suffix + 3 : 10);
   return 1 + pm + 4 * chroma + 12 * luma;
+}
+/* B-slice mb_type (Table 9-37 binarization, ctxIdx 27..35 by Table 9-39):
+ * 0 .. 22, or 23 + the intra suffix's mb_type */
+static int cab_b_type(fo_cab *k, int inc0) {
+  if (!cab_dec(k, 27 + inc0)) return 0;                  /* 0: B_Direct_16x16 */
+  if (!cab_dec(k, 27 + 3)) return 1 + cab_dec(k, 27 + 5);  /* 1 0 b: B_L0 / B_L1_16x16 */
+  int bits = cab_dec(k, 27 + 4) << 3;
+  bits |= cab_dec(k, 27 + 5) << 2;
+  bits |= cab_dec(k, 27 + 5) << 1;
+  bits |= cab_dec(k, 27 + 5);
+  if (bits < 8) return bits + 3;                          /* 1 1 0 x x x: 3 .. 10 */
+  if (bits == 13) return 23 + cab_i_type(k, 32, 0);       /* 1 1 1 1 0 1: intra prefix */
+  if (bits == 14) return 11;                              /* 1 1 1 1 1 0 */
+  if (bits == 15) return 22;                              /* 1 1 1 1 1 1: B_8x8 */
+  bits = (bits << 1) | cab_dec(k, 27 + 5);                /* 1 1 1 x x x x: 12 .. 21 */
+  return bits - 4;
+}
+/* B sub_mb_type (Table 9-38 binarization, ctxIdx 36..39): 0 .. 12 */
+static int cab_b_sub(fo_cab *k) {
+  if (!cab_dec(k, 36)) return 0;                          /* B_Direct_8x8 */
+  if (!cab_dec(k, 37)) return 1 + cab_dec(k, 39);         /* B_L0_8x8, B_L1_8x8 */
+  int t = 3;
+  if (cab_dec(k, 38)) {
+    if (cab_dec(k, 39)) return 11 + cab_dec(k, 39);       /* B_L1_4x4, B_Bi_4x4 */
+    t += 4;
+  }
+  t += 2 * cab_dec(k, 39);
+  t += cab_dec(k, 39);
+  return t;
 }
 /* mvd_lX component (U prefix cMax 9 + UEG3 suffix + sign, 9.3.2.3), sum =
  * absMvdComp(A) + absMvdComp(B) */
@@ -2285,19 +2430,25 @@ static int cbf_chroma_inc(const fo_dec *d, int addr, int pl, int blk, int dc, in
   }
   return inc;
 }
-static int abs_mvd_at(const fo_dec *d, int addr, int xN, int yN, int comp) {
+/* absMvdComp of list l's neighbouring block (0: unavailable, skip, intra,
+   direct or list unused: their mvd is 0) */
+static int abs_mvd_at(const fo_dec *d, int l, int addr, int xN, int yN, int comp) {
   fo_loc L = nb_loc(d, addr, xN, yN, 16, 16);
   if (L.mb < 0) return 0;
   const fo_mb *m = &d->mb[L.mb];
   if (m->type != 0) return 0; /* skip, intra */
-  return iabs(m->mvd[0][(L.yw / 4) * 4 + L.xw / 4][comp]);
+  return iabs(m->mvd[l][(L.yw / 4) * 4 + L.xw / 4][comp]);
 }
-static int ref_gt0_at(const fo_dec *d, int addr, int xN, int yN) {
+/* condTermFlagN of ref_idx_lX (9.3.3.1.1.6): refIdxLX > 0 of an inter
+   neighbour block that is not skipped and not predicted in direct mode */
+static int ref_gt0_at(const fo_dec *d, int l, int addr, int xN, int yN) {
   fo_loc L = nb_loc(d, addr, xN, yN, 16, 16);
   if (L.mb < 0) return 0;
   const fo_mb *m = &d->mb[L.mb];
   if (m->type != 0) return 0;
-  return m->refidx[0][(L.yw / 4) * 4 + L.xw / 4] > 0;
+  int blk = (L.yw / 4) * 4 + L.xw / 4;
+  if ((m->direct8 >> ((blk >> 3) * 2 + ((blk & 3) >> 1))) & 1) return 0;
+  return m->refidx[l][blk] > 0;
 }
 /* Intra NxN mode predictor (8.3.1.1 / 8.3.2.1) of the block whose top-left
  * luma sample is (x0, y0); is8: the current block is 8x8 */
@@ -2320,6 +2471,131 @@ static int intra_pred_mode_pred(const fo_dec *d, int addr, int x0, int y0, int i
   return imin(modes[0], modes[1]);
 }
 
+/* mb_pred / sub_mb_pred of a B macroblock with CABAC (7.3.5.1-2) and its
+   motion; *small: a sub-macroblock partition below 8x8 (or a direct one
+   without direct_8x8_inference), which rules out transform_size_8x8_flag */
+static int inter_mb_cabac_b(fo_ctx *c, fo_cab *k, int addr, int mb_type, int *small) {
+  fo_dec *d = c->d;
+  fo_mb *m = &d->mb[addr];
+  int shape, pm[4] = {0, 0, 0, 0}, ssh[4] = {0, 0, 0, 0};
+  if (mb_type == 0) { /* B_Direct_16x16 */
+    m->direct8 = 15;
+    m->d16 = 1;
+    return direct_pred(c, addr, 0xffff);
+  }
+  if (mb_type <= 3) { shape = 0; pm[0] = mb_type; }
+  else if (mb_type < 22) { shape = (mb_type & 1) ? 2 : 1; pm[0] = B_PART[mb_type][0]; pm[1] = B_PART[mb_type][1]; }
+  else {
+    shape = 3;
+    for (int i = 0; i < 4; i++) {
+      int v = cab_b_sub(k);
+      pm[i] = B_SUB[v][0];
+      ssh[i] = B_SUB[v][1];
+      if (pm[i] == 0) {
+        m->direct8 |= 1 << i;
+        if (!d->S->direct8x8) *small = 1;
+      } else if (ssh[i]) {
+        *small = 1;
+      }
+    }
+  }
+  int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
+  int refs[2][4] = {{-1, -1, -1, -1}, {-1, -1, -1, -1}};
+  /* ref_idx_l0 of the partitions, ref_idx_l1, then mvd_l0, mvd_l1 (7.3.5.1 / 7.3.5.2) */
+  for (int l = 0; l < 2; l++) {
+    int nref = l ? c->nlist1 : c->nlist;
+    fo_pic *const *list = l ? c->list1 : c->list;
+    for (int i = 0; i < nparts; i++) {
+      if (!((pm[i] >> l) & 1)) continue;
+      int x0 = shape == 2 || shape == 3 ? 8 * (i & 1) : 0, y0 = shape == 1 ? 8 * i : (shape == 3 ? 8 * (i >> 1) : 0);
+      int pw = shape == 0 || shape == 1 ? 16 : 8, ph = shape == 0 || shape == 2 ? 16 : 8;
+      int v = 0;
+      if (g_enc) { g_enc->nref = 0; while (g_enc->nref < nref && list[g_enc->nref]) g_enc->nref++; }
+      if (nref > 1 && cab_dec(k, 54 + ref_gt0_at(d, l, addr, x0 - 1, y0) + 2 * ref_gt0_at(d, l, addr, x0, y0 - 1))) {
+        v = 1;
+        if (cab_dec(k, 58)) {
+          v = 2;
+          while (cab_dec(k, 59)) { if (++v > 32) return fo_fail(d, FO_E_FORMAT, "ref_idx"); }
+        }
+      }
+      if (v >= nref || !list[v]) return fo_fail(d, FO_E_DECODE, "ref_idx names no reference picture");
+      refs[l][i] = v;
+      for (int yy = y0 / 4; yy < (y0 + ph) / 4; yy++)
+        for (int xx = x0 / 4; xx < (x0 + pw) / 4; xx++) m->refidx[l][yy * 4 + xx] = v;
+    }
+  }
+  int mvd[2][4][4][2];
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < nparts; i++) {
+      if (!((pm[i] >> l) & 1)) continue;
+      int nsub = shape < 3 ? 1 : (ssh[i] == 0 ? 1 : (ssh[i] == 3 ? 4 : 2));
+      int x0 = shape == 2 || shape == 3 ? 8 * (i & 1) : 0, y0 = shape == 1 ? 8 * i : (shape == 3 ? 8 * (i >> 1) : 0);
+      int pw = shape == 0 || shape == 1 ? 16 : 8, ph = shape == 0 || shape == 2 ? 16 : 8;
+      if (shape == 3) { pw = ssh[i] == 0 || ssh[i] == 1 ? 8 : 4; ph = ssh[i] == 0 || ssh[i] == 2 ? 8 : 4; }
+      for (int q = 0; q < nsub; q++) {
+        int sx = x0, sy = y0;
+        if (shape == 3) {
+          if (ssh[i] == 1) sy += 4 * q;
+          else if (ssh[i] == 2) sx += 4 * q;
+          else if (ssh[i] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+        }
+        for (int comp = 0; comp < 2; comp++)
+          mvd[l][i][q][comp] = cab_mvd(k, comp ? 47 : 40,
+                                       abs_mvd_at(d, l, addr, sx - 1, sy, comp) + abs_mvd_at(d, l, addr, sx, sy - 1, comp));
+        for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
+          for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) {
+            m->mvd[l][yy * 4 + xx][0] = mvd[l][i][q][0];
+            m->mvd[l][yy * 4 + xx][1] = mvd[l][i][q][1];
+          }
+      }
+    }
+  /* motion: partitions in order, both lists of a (sub-)partition before the next */
+  int done = 0;
+  for (int i = 0; i < nparts; i++) {
+    int nsub = 1, pw, ph, x0, y0;
+    if (shape == 0) { pw = ph = 16; x0 = y0 = 0; }
+    else if (shape == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * i; }
+    else if (shape == 2) { pw = 8; ph = 16; x0 = 8 * i; y0 = 0; }
+    else {
+      x0 = 8 * (i & 1);
+      y0 = 8 * (i >> 1);
+      nsub = ssh[i] == 0 ? 1 : (ssh[i] == 3 ? 4 : 2);
+      pw = ssh[i] == 0 || ssh[i] == 1 ? 8 : 4;
+      ph = ssh[i] == 0 || ssh[i] == 2 ? 8 : 4;
+    }
+    if (pm[i] == 0) { /* B_Direct_8x8 */
+      int bm = 0x33 << ((y0 / 4) * 4 + x0 / 4);
+      int rc = direct_pred(c, addr, bm);
+      if (rc) return rc;
+      done |= bm;
+      continue;
+    }
+    for (int q = 0; q < nsub; q++) {
+      int sx = x0, sy = y0;
+      if (shape == 3) {
+        if (ssh[i] == 1) sy += 4 * q;
+        else if (ssh[i] == 2) sx += 4 * q;
+        else if (ssh[i] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+      }
+      for (int l = 0; l < 2; l++) {
+        int use = (pm[i] >> l) & 1, vx = 0, vy = 0;
+        if (use) {
+          int px, py;
+          mv_pred(d, l, addr, sx, sy, pw, ph, refs[l][i], done, &px, &py);
+          vx = px + mvd[l][i][q][0];
+          vy = py + mvd[l][i][q][1];
+          if (vx < -32768 || vx > 32767 || vy < -32768 || vy > 32767) return fo_fail(d, FO_E_FORMAT, "mv range");
+        }
+        for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
+          for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) set_mv(c, m, l, yy * 4 + xx, use ? refs[l][i] : -1, vx, vy);
+      }
+      for (int yy = sy / 4; yy < (sy + ph) / 4; yy++)
+        for (int xx = sx / 4; xx < (sx + pw) / 4; xx++) done |= 1 << (yy * 4 + xx);
+    }
+  }
+  return 0;
+}
+
 /* macroblock_layer (7.3.5) with CABAC (not P_Skip) + reconstruction */
 static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, int prev) {
   fo_dec *d = c->d;
@@ -2337,9 +2613,12 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
   int A = nb_loc(d, addr, -1, 0, 16, 16).mb, B = nb_loc(d, addr, 0, -1, 16, 16).mb;
   const fo_mb *ma = A >= 0 ? &d->mb[A] : NULL, *mbb = B >= 0 ? &d->mb[B] : NULL;
   int mb_type, itype;
-  if (is_p) {
+  if (c->is_b) {
+    mb_type = cab_b_type(k, (ma && !ma->d16) + (mbb && !mbb->d16));
+    itype = mb_type >= 23 ? mb_type - 23 : -1;
+  } else if (is_p) {
     if (cab_dec(k, 14)) {
-      itype = cab_i_type(k, 1, 0);
+      itype = cab_i_type(k, 17, 0);
       mb_type = 5 + itype;
     } else {
       itype = -1;
@@ -2391,6 +2670,10 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
     m->type = 2;
     i16mode = (itype - 1) % 4;
     cbp = (((itype - 1) / 4) % 3) << 4 | (itype >= 13 ? 15 : 0);
+  } else if (c->is_b) { /* Table 7-14 */
+    m->type = 0;
+    int rc = inter_mb_cabac_b(c, k, addr, mb_type, &small);
+    if (rc) return rc;
   } else { /* inter, Table 7-13 */
     m->type = 0;
     int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4), refs[4] = {0, 0, 0, 0};
@@ -2410,7 +2693,8 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
       int pw = mb_type == 0 || mb_type == 1 ? 16 : 8, ph = mb_type == 0 || mb_type == 2 ? 16 : 8;
       if (nref > 1) {
         int v = 0;
-        if (cab_dec(k, 54 + ref_gt0_at(d, addr, x0 - 1, y0) + 2 * ref_gt0_at(d, addr, x0, y0 - 1))) {
+        if (g_enc) { g_enc->nref = 0; while (g_enc->nref < nref && c->list[g_enc->nref]) g_enc->nref++; }
+        if (cab_dec(k, 54 + ref_gt0_at(d, 0, addr, x0 - 1, y0) + 2 * ref_gt0_at(d, 0, addr, x0, y0 - 1))) {
           v = 1;
           if (cab_dec(k, 58)) {
             v = 2;
@@ -2448,7 +2732,7 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
         }
         int dmv[2];
         for (int comp = 0; comp < 2; comp++)
-          dmv[comp] = cab_mvd(k, comp ? 47 : 40, abs_mvd_at(d, addr, sx - 1, sy, comp) + abs_mvd_at(d, addr, sx, sy - 1, comp));
+          dmv[comp] = cab_mvd(k, comp ? 47 : 40, abs_mvd_at(d, 0, addr, sx - 1, sy, comp) + abs_mvd_at(d, 0, addr, sx, sy - 1, comp));
         int px, py;
         mv_pred(d, 0, addr, sx, sy, pw, ph, refs[i], done, &px, &py);
         int vx = px + dmv[0], vy = py + dmv[1];
@@ -2505,7 +2789,7 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
     if (cab_dec(k, 77 + ca[0] + 2 * ca[1])) cbp |= (1 + cab_dec(k, 77 + 4 + cb2[0] + 2 * cb2[1])) << 4;
   }
   m->cbp = cbp;
-  if (m->type == 0 && (cbp & 15) && d->P->t8mode && !small)
+  if (m->type == 0 && (cbp & 15) && d->P->t8mode && !small && !(m->d16 && !d->S->direct8x8))
     m->t8 = cab_dec(k, 399 + (ma && ma->t8) + (mbb && mbb->t8));
   if ((cbp & 15) || (cbp >> 4) || m->type == 2) { /* mb_qp_delta: U of the se mapping */
     const fo_mb *pm = prev >= 0 ? &d->mb[prev] : NULL;
@@ -2590,7 +2874,7 @@ static int decode_mb_cabac(fo_ctx *c, fo_cab *k, int addr, int is_p, int *qp, in
 /* 7.3.4 slice_data() with CABAC; stop = the RBSP stop bit (EBSP bit index) */
 static int slice_data_cabac(fo_ctx *c, fb_t *b, const fo_hdr *h, int is_p, int64_t stop) {
   fo_dec *d = c->d;
-  while (b->bitpos)
+  while (b->bitpos && !g_enc)
     if (!fb_bit(b)) return fo_fail(d, FO_E_FORMAT, "cabac_alignment_one_bit");
   fo_cab k;
   k.b = b;
@@ -2604,17 +2888,19 @@ static int slice_data_cabac(fo_ctx *c, fb_t *b, const fo_hdr *h, int is_p, int64
     int skip = 0;
     if (is_p) {
       int A = nb_loc(d, addr, -1, 0, 16, 16).mb, B = nb_loc(d, addr, 0, -1, 16, 16).mb;
-      skip = cab_dec(&k, 11 + (A >= 0 && d->mb[A].type != 4) + (B >= 0 && d->mb[B].type != 4));
+      skip = cab_dec(&k, (c->is_b ? 24 : 11) + (A >= 0 && d->mb[A].type != 4) + (B >= 0 && d->mb[B].type != 4));
     }
     int rc = skip ? decode_mb(c, NULL, addr, 1, &qp, h) : decode_mb_cabac(c, &k, addr, is_p, &qp, prev);
     if (getenv("FO_TRACE"))
       fprintf(stderr, "oracle cabac mb %d type %d cbp %d qp %d t8 %d bits %lld\n", addr, d->mb[addr].type,
               d->mb[addr].cbp, qp, d->mb[addr].t8, (long long)fb_index(b, 0));
     if (rc) return rc;
-    if (b->err) return fo_fail(d, FO_E_FORMAT, "bitstream exhausted");
+    if (b->err && !g_enc) return fo_fail(d, FO_E_FORMAT, "bitstream exhausted");
+    if (g_enc && addr == g_enc->last_mb) g_enc->last_mb = -1;
     prev = addr++;
     if (cab_term(&k)) break; /* end_of_slice_flag */
   }
+  if (g_enc) return 0;
   if (fb_index(b, 0) != stop + 1) return fo_fail(d, FO_E_FORMAT, "CABAC slice data does not end at the stop bit");
   return 0;
 }
@@ -2720,9 +3006,91 @@ int fo_dims(const uint8_t *sps, int64_t sn, int *w, int *h) {
  * avcC SPS / PPS; write every frame as display-size NV12 (pitch = width) into
  * out.  flags bit 0: skip the deblocking filter (pre-filter pictures, for
  * staged device bring-up).  Returns 0 or < 0 with *bad_frame and err set. */
+/* CABAC synthesis output (fo_cabac_convert) */
+typedef struct {
+  uint64_t seed;
+  int t8;                  /* also switch transform_8x8_mode_flag on */
+  uint8_t *out;            /* samples, AVCC (nls-byte lengths) */
+  int64_t cap, used;
+  int64_t *sizes;          /* per sample */
+  uint8_t *pps_out;        /* the converted PPS NAL */
+  int64_t pps_len;
+} fo_conv;
+
+/* bit writer for the converted headers */
+typedef struct { uint8_t *p; int64_t n; } fo_bw;
+static void bw_bit(fo_bw *w, int b) {
+  if (b) w->p[w->n >> 3] |= (uint8_t)(0x80 >> (w->n & 7));
+  w->n++;
+}
+static void bw_ue(fo_bw *w, uint32_t v) {
+  int len = 0;
+  while ((v + 1) >> (len + 1)) len++;
+  for (int i = 0; i < len; i++) bw_bit(w, 0);
+  for (int i = len; i >= 0; i--) bw_bit(w, ((v + 1) >> i) & 1);
+}
+static void bw_se(fo_bw *w, int v) { bw_ue(w, v > 0 ? (uint32_t)(2 * v - 1) : (uint32_t)(-2 * v)); }
+/* RBSP bytes -> NAL payload with emulation_prevention_three_bytes */
+static int64_t escape_rbsp(const uint8_t *r, int64_t n, uint8_t *o) {
+  int64_t m = 0;
+  int zeros = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (zeros >= 2 && r[i] <= 3) { o[m++] = 3; zeros = 0; }
+    o[m++] = r[i];
+    zeros = r[i] == 0 ? zeros + 1 : 0;
+  }
+  return m;
+}
+static int64_t unescape_nal(const uint8_t *p, int64_t n, uint8_t *o) {
+  int64_t m = 0;
+  int zeros = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (zeros >= 2 && p[i] == 3) { zeros = 0; continue; }
+    o[m++] = p[i];
+    zeros = p[i] == 0 ? zeros + 1 : 0;
+  }
+  return m;
+}
+
+static int fo_run(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, int nls,
+                  const uint8_t *data, const int64_t *offsets, const int64_t *sizes, int64_t n,
+                  int flags, uint8_t *out, int64_t *bad_frame, char *err, fo_conv *cv);
+
 int fo_decode(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, int nls,
               const uint8_t *data, const int64_t *offsets, const int64_t *sizes, int64_t n,
               int flags, uint8_t *out, int64_t *bad_frame, char *err) {
+  return fo_run(sps, sn, pps, pn, nls, data, offsets, sizes, n, flags, out, bad_frame, err, NULL);
+}
+
+/* TEST INFRASTRUCTURE: re-code a CAVLC stream's slice data as CABAC.  Every
+ * slice keeps its header (cabac_init_idc 0 inserted for P / B slices) and
+ * its macroblock range; the macroblock layer is generated by the decoder
+ * itself in synthesis mode (g_enc: seeded random syntax, arithmetic-coded as
+ * 9.3.4 prescribes), so the stream exercises every CABAC syntax element the
+ * decoder parses.  The PPS gets entropy_coding_mode_flag 1 (and, with t8,
+ * transform_8x8_mode_flag 1).  out receives the samples (AVCC, nls-byte
+ * lengths), out_sizes their sizes, pps_out the PPS NAL; frames (may be
+ * null-sized: flags bit 1) the pictures the synthesis decoded.  0 or < 0. */
+int fo_cabac_convert(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, int nls,
+                     const uint8_t *data, const int64_t *offsets, const int64_t *sizes, int64_t n,
+                     uint64_t seed, int t8, uint8_t *out, int64_t out_cap, int64_t *out_sizes,
+                     uint8_t *pps_out, int64_t *pps_len, uint8_t *frames, int64_t *bad_frame, char *err) {
+  fo_conv cv;
+  memset(&cv, 0, sizeof cv);
+  cv.seed = seed;
+  cv.t8 = t8;
+  cv.out = out;
+  cv.cap = out_cap;
+  cv.sizes = out_sizes;
+  cv.pps_out = pps_out;
+  int rc = fo_run(sps, sn, pps, pn, nls, data, offsets, sizes, n, 0, frames, bad_frame, err, &cv);
+  *pps_len = cv.pps_len;
+  return rc;
+}
+
+static int fo_run(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, int nls,
+                  const uint8_t *data, const int64_t *offsets, const int64_t *sizes, int64_t n,
+                  int flags, uint8_t *out, int64_t *bad_frame, char *err, fo_conv *cv) {
   fo_dec *d = (fo_dec *)calloc(1, sizeof *d);
   if (!d) return FO_E_FORMAT;
   char ebuf[256] = {0};
@@ -2733,6 +3101,42 @@ int fo_decode(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, in
   *bad_frame = -1;
   int rc = parse_sps(sps, sn, d->sps, d->err);
   if (!rc) rc = parse_pps(pps, pn, d->pps, d->err);
+  if (!rc && cv) { /* the converted PPS, written from the parsed fields */
+    for (int id = 0; id < 256; id++) {
+      fo_pps *P = &d->pps[id];
+      if (!P->valid) continue;
+      P->cabac = 1;
+      if (cv->t8) P->t8mode = 1;
+      uint8_t rb[64];
+      memset(rb, 0, sizeof rb);
+      fo_bw w = {rb, 0};
+      bw_ue(&w, (uint32_t)id);
+      bw_ue(&w, (uint32_t)P->sps_id);
+      bw_bit(&w, 1);
+      bw_bit(&w, P->bfpo);
+      bw_ue(&w, 0);
+      bw_ue(&w, (uint32_t)(P->num_ref_l0 - 1));
+      bw_ue(&w, (uint32_t)(P->num_ref_l1 - 1));
+      bw_bit(&w, P->weighted_pred);
+      bw_bit(&w, (P->weighted_bipred >> 1) & 1);
+      bw_bit(&w, P->weighted_bipred & 1);
+      bw_se(&w, P->pic_init_qp - 26);
+      bw_se(&w, 0);
+      bw_se(&w, P->cqp_off);
+      bw_bit(&w, P->deblock_ctrl);
+      bw_bit(&w, P->cip);
+      bw_bit(&w, 0);
+      if (P->t8mode || P->cqp_off2 != P->cqp_off) {
+        bw_bit(&w, P->t8mode);
+        bw_bit(&w, 0);
+        bw_se(&w, P->cqp_off2);
+      }
+      bw_bit(&w, 1);
+      cv->pps_out[0] = pps[0];
+      cv->pps_len = 1 + escape_rbsp(rb, (w.n + 7) >> 3, cv->pps_out + 1);
+      break;
+    }
+  }
   int64_t f = 0;
   fo_pic cur;
   memset(&cur, 0, sizeof cur);
@@ -2768,7 +3172,67 @@ int fo_decode(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, in
       pos += nls;
       if (L == 0 || pos + L > end) { rc = fo_fail(d, FO_E_FORMAT, "bad NAL length"); break; }
       int t = s[pos] & 31;
-      if (t == 1 || t == 5) {
+      if ((t == 1 || t == 5) && cv) {
+        /* synthesis: source slice as RBSP, its macroblock range from the next slice's first_mb */
+        uint8_t *rb = (uint8_t *)malloc((size_t)L + 64), *nb = (uint8_t *)calloc((size_t)L * 4 + 4096, 1);
+        uint8_t *eb = (uint8_t *)malloc((size_t)L * 8 + 8192);
+        int64_t rn = unescape_nal(s + pos, L, rb);
+        memset(rb + rn, 0, 64);
+        int last = d->nmb - 1;
+        for (int64_t q = pos + L; q + nls <= end; ) {
+          uint32_t L2 = 0;
+          for (int i = 0; i < nls; i++) L2 = (L2 << 8) | s[q + i];
+          q += nls;
+          int t2 = s[q] & 31;
+          if (t2 == 1 || t2 == 5) {
+            fb_t hb;
+            fb_init(&hb, s + q + 1, L2 - 1);
+            last = (int)fb_ue(&hb) - 1;
+            break;
+          }
+          q += L2;
+        }
+        fo_enc e;
+        memset(&e, 0, sizeof e);
+        e.out = (uint8_t *)calloc((size_t)L * 4 + 65536 + (size_t)d->nmb * 1024, 1);
+        e.cap = (int64_t)L * 4 + 65536 + (int64_t)d->nmb * 1024;
+        e.rng = cv->seed * 0x9E3779B97F4A7C15ull + (uint64_t)f * 1000003u + (uint64_t)nslice * 7919u + 1;
+        e.last_mb = last;
+        g_enc = &e;
+        int idr = 0;
+        rc = decode_slice(d, &cur, rb, rn, nslice, &idr, &h);
+        g_enc = NULL;
+        if (!rc && (e.overflow || e.last_mb != -1)) rc = fo_fail(d, FO_E_DECODE, "synthesis overflow / slice end");
+        if (!rc) {
+          /* header bits [0, pos_qp) + cabac_init_idc + [pos_qp, pos_data) + alignment ones + CABAC data */
+          fo_bw w = {nb, 0};
+          const uint8_t *hdr = rb + 1;
+          for (int64_t i = 0; i < d->enc_pos_qp; i++) bw_bit(&w, (hdr[i >> 3] >> (7 - (i & 7))) & 1);
+          if (h.slice_type != 2) bw_ue(&w, 0);
+          for (int64_t i = d->enc_pos_qp; i < d->enc_pos_data; i++) bw_bit(&w, (hdr[i >> 3] >> (7 - (i & 7))) & 1);
+          while (w.n & 7) bw_bit(&w, 1);
+          for (int64_t i = 0; i < e.nbits; i++) bw_bit(&w, (e.out[i >> 3] >> (7 - (i & 7))) & 1);
+          int64_t nbytes = (w.n + 7) >> 3;
+          eb[0] = s[pos];
+          int64_t en = 1 + escape_rbsp(nb, nbytes, eb + 1);
+          if (cv->used + nls + en > cv->cap) rc = fo_fail(d, FO_E_DECODE, "synthesis output full");
+          else {
+            for (int i = 0; i < nls; i++) cv->out[cv->used++] = (uint8_t)(en >> (8 * (nls - 1 - i)));
+            memcpy(cv->out + cv->used, eb, (size_t)en);
+            cv->used += en;
+            cv->sizes[f] += nls + en;
+          }
+        }
+        free(e.out);
+        free(rb);
+        free(nb);
+        free(eb);
+        if (!rc) {
+          if (nslice == 0) { h0 = h; is_idr = idr; }
+          any_ref |= h.nal_ref_idc != 0;
+          nslice++;
+        }
+      } else if (t == 1 || t == 5) {
         int idr = 0;
         rc = decode_slice(d, &cur, s + pos, L, nslice, &idr, &h);
         if (!rc) {
@@ -2779,7 +3243,8 @@ int fo_decode(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn, in
       } else if (t == 7) {
         rc = parse_sps(s + pos, L, d->sps, d->err);
       } else if (t == 8) {
-        rc = parse_pps(s + pos, L, d->pps, d->err);
+        if (cv) rc = fo_fail(d, FO_E_UNSUPPORTED, "synthesis: in-band PPS");
+        else rc = parse_pps(s + pos, L, d->pps, d->err);
       } else if (t >= 2 && t <= 4) {
         rc = fo_fail(d, FO_E_UNSUPPORTED, "data partitioning");
       }

@@ -571,3 +571,119 @@ def table_code(table: int, a: int, b: int, c: int = 0) -> str | None:
     L.fo_table_code.restype = C.c_char_p
     v = L.fo_table_code(table, a, b, c)
     return None if v is None else v.decode()
+
+
+def write_mp4(path, sps: bytes, pps: bytes, samples: list[bytes], dts: list[int], cts: list[int],
+              timescale: int, width: int, height: int, nal_length_size: int = 4) -> None:
+    """Minimal ISO-BMFF writer (one avc1 track, one chunk; ctts when any
+    composition offset is non-zero; stss from the IDR samples).  TEST
+    INFRASTRUCTURE for streams the oracle synthesises (cabac_convert)."""
+    import struct
+
+    def box(t, p):
+        return struct.pack(">I4s", 8 + len(p), t) + p
+
+    def full(t, v, f, p):
+        return box(t, struct.pack(">I", (v << 24) | f) + p)
+    n = len(samples)
+    dur = (dts[-1] - dts[0] + (dts[-1] - dts[-2] if n > 1 else 1)) if n else 0
+    matrix = struct.pack(">9I", 0x10000, 0, 0, 0, 0x10000, 0, 0, 0, 0x40000000)
+    ms = dur * 1000 // max(1, timescale)
+    mvhd = full(b"mvhd", 0, 0, struct.pack(">IIII", 0, 0, 1000, ms) + struct.pack(">IH", 0x10000, 0x100) +
+                b"\0" * 10 + matrix + b"\0" * 24 + struct.pack(">I", 2))
+    tkhd = full(b"tkhd", 0, 3, struct.pack(">IIIII", 0, 0, 1, 0, ms) + b"\0" * 8 +
+                struct.pack(">HHHH", 0, 0, 0, 0) + matrix + struct.pack(">II", width << 16, height << 16))
+    mdhd = full(b"mdhd", 0, 0, struct.pack(">IIIIHH", 0, 0, timescale, dur, 0x55c4, 0))
+    hdlr = full(b"hdlr", 0, 0, struct.pack(">I4s", 0, b"vide") + b"\0" * 12 + b"VideoHandler\0")
+    avcc = box(b"avcC", bytes([1, sps[1], sps[2], sps[3], 0xFC | (nal_length_size - 1), 0xE1]) +
+               struct.pack(">H", len(sps)) + sps + bytes([1]) + struct.pack(">H", len(pps)) + pps)
+    avc1 = box(b"avc1", b"\0" * 6 + struct.pack(">H", 1) + b"\0" * 16 + struct.pack(">HH", width, height) +
+               struct.pack(">II", 0x480000, 0x480000) + b"\0" * 4 + struct.pack(">H", 1) + b"\0" * 32 +
+               struct.pack(">Hh", 0x18, -1) + avcc)
+    stsd = full(b"stsd", 0, 0, struct.pack(">I", 1) + avc1)
+    deltas = [dts[i + 1] - dts[i] for i in range(n - 1)] + ([dts[-1] - dts[-2]] if n > 1 else [1])
+    runs = []
+    for dl in deltas:
+        if runs and runs[-1][1] == dl:
+            runs[-1][0] += 1
+        else:
+            runs.append([1, dl])
+    stts = full(b"stts", 0, 0, struct.pack(">I", len(runs)) + b"".join(struct.pack(">II", c, dl) for c, dl in runs))
+    extra = b""
+    if any(cts):
+        extra += full(b"ctts", 0, 0, struct.pack(">I", n) + b"".join(struct.pack(">Ii", 1, c) for c in cts))
+    sync = []
+    for i, smp in enumerate(samples):
+        p = 0
+        while p + nal_length_size <= len(smp):
+            ln = int.from_bytes(smp[p:p + nal_length_size], "big")
+            if smp[p + nal_length_size] & 31 == 5:
+                sync.append(i + 1)
+                break
+            p += nal_length_size + ln
+    extra += full(b"stss", 0, 0, struct.pack(">I", len(sync)) + b"".join(struct.pack(">I", x) for x in sync))
+    stsc = full(b"stsc", 0, 0, struct.pack(">IIII", 1, 1, n, 1))
+    stsz = full(b"stsz", 0, 0, struct.pack(">II", 0, n) + b"".join(struct.pack(">I", len(x)) for x in samples))
+    ftyp = box(b"ftyp", b"isom" + struct.pack(">I", 512) + b"isomiso2avc1mp41")
+
+    def build(off):
+        co64 = full(b"co64", 0, 0, struct.pack(">IQ", 1, off))
+        stbl = box(b"stbl", stsd + stts + extra + stsc + stsz + co64)
+        dinf = box(b"dinf", full(b"dref", 0, 0, struct.pack(">I", 1) + full(b"url ", 0, 1, b"")))
+        minf = box(b"minf", full(b"vmhd", 0, 1, b"\0" * 8) + dinf + stbl)
+        return box(b"moov", mvhd + box(b"trak", tkhd + box(b"mdia", mdhd + hdlr + minf)))
+    moov = build(0)
+    payload = b"".join(samples)
+    off = len(ftyp) + len(moov) + 8
+    moov = build(off)
+    with open(path, "wb") as f:
+        f.write(ftyp + moov + struct.pack(">I4s", 8 + len(payload), b"mdat") + payload)
+
+
+def cabac_convert(src, dst, seed: int = 1, t8: bool = False):
+    """Re-code a CAVLC MP4 (the synthetic writer's) as CABAC with
+    h264_full_oracle.c fo_cabac_convert: every slice header is kept (plus
+    cabac_init_idc 0), the macroblock layer is random syntax generated by the
+    oracle's own CABAC parser in synthesis mode and arithmetic-coded (9.3.4).
+    Returns the frames the synthesis decoded (decode order, display size).
+    TEST INFRASTRUCTURE: the resulting stream pins nothing against the
+    standard beyond the parser's own restatement; it gives the device
+    decoder's CABAC paths a stream with every syntax element to match."""
+    m = read_mp4(src)
+    L = lib()
+    L.fo_cabac_convert.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64, C.c_int, C.c_void_p,
+                                   C.c_void_p, C.c_void_p, C.c_int64, C.c_uint64, C.c_int, C.c_void_p,
+                                   C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_char_p]
+    L.fo_dims.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_void_p]
+    sps, pps = m["sps"][0], m["pps"][0]
+    w, h = C.c_int(0), C.c_int(0)
+    if L.fo_dims(sps, len(sps), C.byref(w), C.byref(h)):
+        raise RuntimeError("oracle SPS")
+    W, H = w.value, h.value
+    n = len(m["sizes"])
+    data = np.frombuffer(m["data"], np.uint8)
+    offs = np.asarray(m["offsets"], np.int64)
+    sizes = np.asarray(m["sizes"], np.int64)
+    nmb = ((W + 15) // 16) * ((H + 15) // 16)
+    cap = int(sizes.sum()) * 4 + n * (nmb * 512 + 4096)
+    out = np.zeros(cap, np.uint8)
+    osz = np.zeros(n, np.int64)
+    pps_out = np.zeros(256, np.uint8)
+    pps_len = C.c_int64(0)
+    frames = np.zeros((n, H * 3 // 2, W), np.uint8)
+    bad = C.c_int64(-1)
+    err = C.create_string_buffer(256)
+    rc = L.fo_cabac_convert(sps, len(sps), pps, len(pps), m["nal_length_size"], data.ctypes.data,
+                            offs.ctypes.data, sizes.ctypes.data, n, seed, int(t8), out.ctypes.data, cap,
+                            osz.ctypes.data, pps_out.ctypes.data, C.byref(pps_len), frames.ctypes.data,
+                            C.byref(bad), err)
+    if rc != 0:
+        raise RuntimeError(f"fo_cabac_convert rc={rc} at frame {bad.value}: {err.value.decode(errors='replace')}")
+    samples, p = [], 0
+    for s in osz:
+        samples.append(out[p:p + int(s)].tobytes())
+        p += int(s)
+    write_mp4(dst, bytes(sps), pps_out[:pps_len.value].tobytes(), samples, m["dts"], m["cts"],
+              m["timescale"], W, H, m["nal_length_size"])
+    return frames

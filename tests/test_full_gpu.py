@@ -212,3 +212,38 @@ def test_b_stream_refused_by_the_subset_decoder(tmp_path):
     with pytest.raises(VtsegError):
         with scene.VideoScorer(path, decoder="subset") as v:
             v.score()
+
+
+CABAC_B = [
+    ("p_t8", dict(width=176, height=144), True),
+    ("b_spatial", dict(width=176, height=144, bframes=True), False),
+    ("b_explicit_t8", dict(width=176, height=144, bframes=True, weighted="explicit"), True),
+    ("b_temporal_implicit", dict(width=176, height=144, bframes=True, temporal_direct=True, weighted="implicit"), False),
+    ("b_slices_t8", dict(width=176, height=144, bframes=True, slices_per_row=2), True),
+    ("b_hd720_t8", dict(width=1280, height=720, bframes=True, slices_per_row=0, weighted="explicit"), True),
+]
+
+
+@pytest.mark.parametrize("name,kw,t8", CABAC_B, ids=[c[0] for c in CABAC_B])
+def test_cabac_b_streams_bit_exact(tmp_path, name, kw, t8):
+    """CABAC P / B streams (oracle.cabac_convert: the writer's headers with a
+    synthesised CABAC macroblock layer covering every B mb_type /
+    sub_mb_type, both lists' contexts, direct quadrants and 8x8 transforms)
+    decode and score on the device exactly like the oracle."""
+    _require_gpu()
+    n = 16 if kw["height"] >= 720 else 30
+    src, path = tmp_path / "src.mp4", tmp_path / f"{name}.mp4"
+    scene.synth_write(src, n_frames=n, coding="full", cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.8, seed=3,
+                      chunks=1, **kw)
+    oracle.cabac_convert(src, path, seed=5, t8=t8)
+    frames, _ = oracle.decode_full(path)
+    W, H = kw["width"], kw["height"]
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 4)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+        assert _first_diff(got, frames) == []
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])

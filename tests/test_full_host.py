@@ -108,6 +108,35 @@ def test_b_pictures_on_cpu_equal_oracle(tmp_path, harness, name, kw):
         assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"
 
 
+CABAC_STREAMS = [
+    ("p", {}, False),
+    ("b_spatial", {"bframes": True}, False),
+    ("b_spatial_t8", {"bframes": True}, True),
+    ("b_explicit_t8", {"bframes": True, "weighted": "explicit"}, True),
+    ("b_temporal_implicit", {"bframes": True, "temporal_direct": True, "weighted": "implicit"}, False),
+    ("b_slices_t8", {"bframes": True, "slices_per_row": 2}, True),
+]
+
+
+@pytest.mark.parametrize("name,kw,t8", CABAC_STREAMS, ids=[s[0] for s in CABAC_STREAMS])
+def test_cabac_b_streams_on_cpu_equal_oracle(tmp_path, harness, name, kw, t8):
+    """CABAC P / B streams (oracle.cabac_convert: the writer's slice headers,
+    CABAC macroblock layers synthesised by the oracle's parser — every B
+    mb_type / sub_mb_type, both lists' ref_idx / mvd contexts, direct
+    quadrants, transform_size_8x8_flag): the product's CABAC parser and
+    reconstruction equal the oracle, before and after deblocking."""
+    src, dst = tmp_path / "src.mp4", tmp_path / f"{name}.mp4"
+    scene.synth_write(src, width=176, height=144, n_frames=30, coding="full", cut_min_s=0.5, cut_max_s=1.2,
+                      gop_max_s=0.8, seed=3, chunks=1, **kw)
+    oracle.cabac_convert(src, dst, seed=5, t8=t8)
+    for flags in (1, 0):
+        want, _ = oracle.decode_full(dst, flags=flags)
+        got = harness(dst, flags)
+        assert got.shape == want.shape
+        bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
+        assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"
+
+
 def test_real_cabac_high_profile_stream(harness):
     """A real High-profile CABAC clip (tests/golden/real/realshort.mp4:
     CABAC I/P slices, 8x8 transform, Intra 8x8) through the product's CABAC

@@ -277,7 +277,6 @@ std::string sched_build(const Sps &sps, const Pps &pps, const uint8_t *es, const
       if (pps.entropy_coding_mode && inter) {
         // only the cabac_init_idc 0 context tables are restated (x264 writes 0)
         if (r.ue() != 0) return "cabac_init_idc 1 or 2 (only the idc 0 context tables are supported)";
-        if (is_b) return "CABAC B slices";
       }
       s.qp = pps.pic_init_qp + r.se();
       s.dbk_idc = 0;

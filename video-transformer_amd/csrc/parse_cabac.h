@@ -1,5 +1,5 @@
 // parse_cabac.h — CABAC slice_data() parser of the general device decoder
-// (ITU-T H.264 9.3): High-profile I and P slices with 8x8 transforms.  The
+// (ITU-T H.264 9.3): High-profile I, P and B slices with 8x8 transforms.  The
 // kernel (h264_parse_full) runs one slice per single-lane wave, so the whole
 // arithmetic decoder is wave-uniform scalar code; the CPU harness compiles the
 // same header.  It produces exactly what the CAVLC parser produces (MbRec,
@@ -147,24 +147,29 @@ struct CabacParser : Parser {
     }
     return inc;
   }
-  // Min(|mvd|, 33) at luma (xN, yN) of the current macroblock's neighbourhood
-  VTS_HD VTS_INLINE int mvd_at(int addr, int xN, int yN, int comp) const {
+  // Min(|mvd_lX|, 33) at luma (xN, yN) of the current macroblock's
+  // neighbourhood (skipped, intra and direct blocks carry 0)
+  VTS_HD VTS_INLINE int mvd_at(int addr, int xN, int yN, int comp, int l = 0) const {
     int xw = 0, yw = 0;
     const int n = nb_mb(addr, xN, yN, 16, &xw, &yw);
     if (n == -1) return 0;
-    if (n == -2) return sc->mvdc[(yw / 4) * 4 + xw / 4][comp];
+    if (n == -2) return l ? sc->mvdc1[(yw / 4) * 4 + xw / 4][comp] : sc->mvdc[(yw / 4) * 4 + xw / 4][comp];
     const MbRec &m = rec(n);
     if (m.type != kMbInter) return 0;
-    if (n == cur_addr - 1) return sc->mvdl[yw / 4][comp];
-    return m.i4[(xw / 4) * 2 + comp];  // the row above: bottom-row values
+    if (n == cur_addr - 1) return l ? sc->mvdl1[yw / 4][comp] : sc->mvdl[yw / 4][comp];
+    return l ? rec1(n).mvd1[(xw / 4) * 2 + comp] : m.i4[(xw / 4) * 2 + comp];  // the row above: bottom-row values
   }
-  VTS_HD VTS_INLINE int ref_gt0_at(int addr, int xN, int yN) const {
+  // condTermFlagN of ref_idx_lX (9.3.3.1.1.6): refIdxLX > 0 of an inter
+  // neighbour that is neither skipped nor predicted in direct mode
+  VTS_HD VTS_INLINE int ref_gt0_at(int addr, int xN, int yN, int l = 0) const {
     int xw = 0, yw = 0;
     const int n = nb_mb(addr, xN, yN, 16, &xw, &yw);
     if (n == -1) return 0;
     const MbRec &m = rec(n);
     if (m.type != kMbInter) return 0;
-    return m.ref[(yw / 8) * 2 + xw / 8] > 0 ? 1 : 0;
+    const int p8 = (yw / 8) * 2 + xw / 8;
+    if (bframes && ((rec1(n).direct >> p8) & 1)) return 0;
+    return (l ? rec1(n).ref1[p8] : m.ref[p8]) > 0 ? 1 : 0;
   }
   // Intra NxN mode predictor (8.3.1.1 / 8.3.2.1) of the block at (x0, y0)
   VTS_HD VTS_INLINE int mode_pred(int addr, int x0, int y0, bool is8) const {
@@ -197,17 +202,166 @@ struct CabacParser : Parser {
   }
 
   // ------------------------------------------------------- syntax elements
-  // mb_type of an I macroblock (Table 9-36): I slice prefix at ctxIdx 3 or the
-  // P-slice suffix at 17; 0..25
-  VTS_HD VTS_INLINE int i_type(bool suffix, int inc0) {
-    if (!dec(suffix ? 17 : 3 + inc0)) return 0;
+  // mb_type of an I macroblock (Table 9-36): I slice prefix at ctxIdx 3, or
+  // the suffix of a P (ctxIdxOffset sfx 17) or B (32) slice's intra mb_type; 0..25
+  VTS_HD VTS_INLINE int i_type(int sfx, int inc0) {
+    if (!dec(sfx ? sfx : 3 + inc0)) return 0;
     if (term()) return 25;
-    const int luma = static_cast<int>(dec(suffix ? 18 : 6));
-    int chroma = static_cast<int>(dec(suffix ? 19 : 7));
-    if (chroma) chroma += static_cast<int>(dec(suffix ? 19 : 8));
-    int pm = static_cast<int>(dec(suffix ? 20 : 9)) << 1;
-    pm |= static_cast<int>(dec(suffix ? 20 : 10));
+    const int luma = static_cast<int>(dec(sfx ? sfx + 1 : 6));
+    int chroma = static_cast<int>(dec(sfx ? sfx + 2 : 7));
+    if (chroma) chroma += static_cast<int>(dec(sfx ? sfx + 2 : 8));
+    int pm = static_cast<int>(dec(sfx ? sfx + 3 : 9)) << 1;
+    pm |= static_cast<int>(dec(sfx ? sfx + 3 : 10));
     return 1 + pm + 4 * chroma + 12 * luma;
+  }
+  // B mb_type (Table 9-37 binarization, ctxIdx 27..35 per Table 9-39): 0..22,
+  // or 23 + the intra suffix's mb_type
+  VTS_HD VTS_INLINE int b_type(int inc0) {
+    if (!dec(27 + inc0)) return 0;                                       // B_Direct_16x16
+    if (!dec(27 + 3)) return 1 + static_cast<int>(dec(27 + 5));           // B_L0 / B_L1_16x16
+    int bits = static_cast<int>(dec(27 + 4)) << 3;
+    bits |= static_cast<int>(dec(27 + 5)) << 2;
+    bits |= static_cast<int>(dec(27 + 5)) << 1;
+    bits |= static_cast<int>(dec(27 + 5));
+    if (bits < 8) return bits + 3;
+    if (bits == 13) return 23 + i_type(32, 0);
+    if (bits == 14) return 11;
+    if (bits == 15) return 22;                                           // B_8x8
+    bits = (bits << 1) | static_cast<int>(dec(27 + 5));
+    return bits - 4;
+  }
+  // B sub_mb_type (Table 9-38, ctxIdx 36..39): 0..12
+  VTS_HD VTS_INLINE int b_sub() {
+    if (!dec(36)) return 0;
+    if (!dec(37)) return 1 + static_cast<int>(dec(39));
+    int t = 3;
+    if (dec(38)) {
+      if (dec(39)) return 11 + static_cast<int>(dec(39));
+      t += 4;
+    }
+    t += 2 * static_cast<int>(dec(39));
+    t += static_cast<int>(dec(39));
+    return t;
+  }
+  // ref_idx_lX (U binarization, ctxIdx 54..59)
+  VTS_HD VTS_INLINE int ref_idx(int addr, int x0, int y0, int l) {
+    int v = 0;
+    if (dec(54 + ref_gt0_at(addr, x0 - 1, y0, l) + 2 * ref_gt0_at(addr, x0, y0 - 1, l))) {
+      v = 1;
+      if (dec(58)) {
+        v = 2;
+        while (dec(59))
+          if (++v > 32) break;
+      }
+    }
+    return v;
+  }
+  // mb_pred / sub_mb_pred of a B macroblock (7.3.5.1-2): mb_type 0..22;
+  // *small: a partition below 8x8 (or a direct one without
+  // direct_8x8_inference) rules out transform_size_8x8_flag
+  VTS_HD bool b_inter_cabac(int addr, int mb_type, bool *small) {
+    uint8_t *pm = sc->pm;
+    int8_t *sub = sc->sub, *r0 = sc->refs, *r1 = sc->refs1;
+    for (int k = 0; k < 4; ++k) {
+      pm[k] = 0;
+      sub[k] = 0;
+      r0[k] = r1[k] = -1;
+    }
+    if (mb_type == 0) {  // B_Direct_16x16
+      cur1().direct = 0x0f | kDirect16;
+      if (!direct8x8) *small = true;
+      direct_pred(addr, 0xffffu);
+      return !err;
+    }
+    int shape;
+    if (mb_type <= 3) {
+      shape = 0;
+      pm[0] = static_cast<uint8_t>(mb_type);
+    } else if (mb_type < 22) {
+      shape = (mb_type & 1) ? 2 : 1;
+      pm[0] = kBPart[mb_type] & 3;
+      pm[1] = kBPart[mb_type] >> 2;
+    } else {
+      shape = 3;
+      for (int k = 0; k < 4; ++k) {
+        const int v = b_sub();
+        pm[k] = kBSub[v] & 3;
+        sub[k] = static_cast<int8_t>(kBSub[v] >> 2);
+        if (pm[k] == 0) {
+          cur1().direct |= static_cast<uint8_t>(1u << k);
+          if (!direct8x8) *small = true;
+        } else if (sub[k]) {
+          *small = true;
+        }
+      }
+    }
+    const int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
+    MbRec &m = cur();
+    MbRecB &m1 = cur1();
+    for (int l = 0; l < 2; ++l) {
+      const int nref = l ? bc.x->num_ref1 : s->num_ref;
+      int8_t *rr = l ? r1 : r0;
+      for (int k = 0; k < nparts; ++k) {
+        if (!((pm[k] >> l) & 1)) continue;
+        const int x0 = (shape == 2 || shape == 3) ? 8 * (k & 1) : 0;
+        const int y0 = shape == 1 ? 8 * k : (shape == 3 ? 8 * (k >> 1) : 0);
+        const int v = nref > 1 ? ref_idx(addr, x0, y0, l) : 0;
+        if (v >= nref || (l ? bc.x->ref_slot1[v & 31] : s->ref_slot[v & 31]) < 0) {
+          err |= DEC_E_NO_REF;
+          return false;
+        }
+        rr[k] = static_cast<int8_t>(v);
+        // the partition's 8x8 quarters carry the index for later contexts
+        const int pw = (shape == 0 || shape == 1) ? 2 : 1, ph = (shape == 0 || shape == 2) ? 2 : 1;
+        for (int qy = 0; qy < ph; ++qy)
+          for (int qx = 0; qx < pw; ++qx) {
+            const int q8 = (y0 / 8 + qy) * 2 + x0 / 8 + qx;
+            if (l) m1.ref1[q8] = static_cast<int8_t>(v);
+            else m.ref[q8] = static_cast<int8_t>(v);
+          }
+      }
+    }
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < nparts; ++k) {
+        if (!((pm[k] >> l) & 1)) continue;
+        int nsub = 1, pw, ph, x0, y0;
+        if (shape == 0) { pw = ph = 16; x0 = y0 = 0; }
+        else if (shape == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * k; }
+        else if (shape == 2) { pw = 8; ph = 16; x0 = 8 * k; y0 = 0; }
+        else {
+          x0 = 8 * (k & 1);
+          y0 = 8 * (k >> 1);
+          nsub = sub[k] == 0 ? 1 : (sub[k] == 3 ? 4 : 2);
+          pw = (sub[k] == 0 || sub[k] == 1) ? 8 : 4;
+          ph = (sub[k] == 0 || sub[k] == 2) ? 8 : 4;
+        }
+        for (int q = 0; q < nsub; ++q) {
+          int sx = x0, sy = y0;
+          if (shape == 3) {
+            if (sub[k] == 1) sy += 4 * q;
+            else if (sub[k] == 2) sx += 4 * q;
+            else if (sub[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+          }
+          const int dx = mvd(40, mvd_at(addr, sx - 1, sy, 0, l) + mvd_at(addr, sx, sy - 1, 0, l));
+          const int dy = mvd(47, mvd_at(addr, sx - 1, sy, 1, l) + mvd_at(addr, sx, sy - 1, 1, l));
+          sc->mvd[l][4 * k + q][0] = dx;
+          sc->mvd[l][4 * k + q][1] = dy;
+          const uint8_t ax = static_cast<uint8_t>(vts_min(dx < 0 ? -dx : dx, 33));
+          const uint8_t ay = static_cast<uint8_t>(vts_min(dy < 0 ? -dy : dy, 33));
+          uint8_t(*mc)[2] = l ? sc->mvdc1 : sc->mvdc;
+          for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
+            for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
+              mc[yy * 4 + xx][0] = ax;
+              mc[yy * 4 + xx][1] = ay;
+            }
+        }
+      }
+    // the references the parse recorded are set again by the motion below
+    for (int k = 0; k < 4; ++k) {
+      m.ref[k] = -1;
+      m1.ref1[k] = -1;
+    }
+    return b_motion(addr, shape);
   }
   VTS_HD VTS_INLINE int mvd(int base, int sum) {  // U prefix cMax 9 + UEG3 + sign
     if (!dec(base + (sum < 3 ? 0 : (sum > 32 ? 2 : 1)))) return 0;
@@ -281,18 +435,25 @@ struct CabacParser : Parser {
     int xw, yw;
     const int A = nb_mb(addr, -1, 0, 16, &xw, &yw), B = nb_mb(addr, 0, -1, 16, &xw, &yw);
     int itype, mb_type = 0;
-    if (s->is_p) {
+    for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
+    if (bframes)
+      for (int i = 0; i < 16; ++i) sc->mvdc1[i][0] = sc->mvdc1[i][1] = 0;
+    if (s->is_p == kSliceB) {
+      const int t = b_type((A != -1 && !(rec1(A).direct & kDirect16) ? 1 : 0) +
+                           (B != -1 && !(rec1(B).direct & kDirect16) ? 1 : 0));
+      itype = t >= 23 ? t - 23 : -1;
+      mb_type = t;
+    } else if (s->is_p) {
       if (dec(14)) {
-        itype = i_type(true, 0);
+        itype = i_type(17, 0);
       } else {
         itype = -1;
         if (!dec(15)) mb_type = dec(16) ? 3 : 0;
         else mb_type = dec(17) ? 1 : 2;
       }
     } else {
-      itype = i_type(false, (avail_not(A, kMbI4x4) ? 1 : 0) + (avail_not(B, kMbI4x4) ? 1 : 0));
+      itype = i_type(0, (avail_not(A, kMbI4x4) ? 1 : 0) + (avail_not(B, kMbI4x4) ? 1 : 0));
     }
-    for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
     if (itype == 25) {  // I_PCM: alignment, 384 samples through the RBSP reader, engine restart
       m.type = kMbPcm;
       m.qp = static_cast<uint8_t>(*qp);
@@ -350,6 +511,9 @@ struct CabacParser : Parser {
       m.type = kMbI16;
       cbp = ((((itype - 1) / 4) % 3) << 4) | (itype >= 13 ? 15 : 0);
       m.modes = static_cast<uint8_t>((itype - 1) % 4);
+    } else if (s->is_p == kSliceB) {  // Table 7-14
+      m.type = kMbInter;
+      if (!b_inter_cabac(addr, mb_type, &small)) return false;
     } else {  // inter (Table 7-13)
       m.type = kMbInter;
       const int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
@@ -369,14 +533,7 @@ struct CabacParser : Parser {
         const int x0 = (mb_type == 2 || mb_type == 3) ? 8 * (k & 1) : 0;
         const int y0 = mb_type == 1 ? 8 * k : (mb_type == 3 ? 8 * (k >> 1) : 0);
         int v = 0;
-        if (nref > 1 && dec(54 + ref_gt0_at(addr, x0 - 1, y0) + 2 * ref_gt0_at(addr, x0, y0 - 1))) {
-          v = 1;
-          if (dec(58)) {
-            v = 2;
-            while (dec(59))
-              if (++v > 32) break;
-          }
-        }
+        if (nref > 1) v = ref_idx(addr, x0, y0, 0);
         if (v >= nref || s->ref_slot[v & 31] < 0) {
           err |= DEC_E_NO_REF;
           return false;
@@ -607,6 +764,17 @@ struct CabacParser : Parser {
       sc->mvdl[y][0] = sc->mvdc[y * 4 + 3][0];
       sc->mvdl[y][1] = sc->mvdc[y * 4 + 3][1];
     }
+    if (bframes) {
+      MbRecB &m1 = cur1();
+      for (int x = 0; x < 4; ++x) {
+        m1.mvd1[2 * x] = sc->mvdc1[12 + x][0];
+        m1.mvd1[2 * x + 1] = sc->mvdc1[12 + x][1];
+      }
+      for (int y = 0; y < 4; ++y) {
+        sc->mvdl1[y][0] = sc->mvdc1[y * 4 + 3][0];
+        sc->mvdl1[y][1] = sc->mvdc1[y * 4 + 3][1];
+      }
+    }
   }
 
   bool P_t8mode;
@@ -621,7 +789,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice 
   p.bc = bc;
   p.bframes = P.bframes;
   p.direct8x8 = P.direct8x8;
-  if (s.is_p == kSliceB) return DEC_E_SLICE_TYPE;  // CABAC B slices: not restated
+  if (s.is_p == kSliceB && (!bc.x || !bc.col || !P.bframes)) return DEC_E_NO_REF;
   p.s = &s;
   p.cip = P.cip;
   p.P_t8mode = P.t8mode != 0;
@@ -660,7 +828,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice 
     if (!p.br.bit()) return DEC_E_SYNTAX;
   p.cab_init(!s.is_p, s.qp);
   p.cab_start();
-  for (int i = 0; i < 4; ++i) sc->mvdl[i][0] = sc->mvdl[i][1] = 0;
+  for (int i = 0; i < 4; ++i) sc->mvdl[i][0] = sc->mvdl[i][1] = sc->mvdl1[i][0] = sc->mvdl1[i][1] = 0;
   int addr = s.first_mb, qp = s.qp;
   for (;;) {
     if (addr >= nmb) {
@@ -672,9 +840,10 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice 
     if (s.is_p) {
       int xw, yw;
       const int A = p.nb_mb(addr, -1, 0, 16, &xw, &yw), B = p.nb_mb(addr, 0, -1, 16, &xw, &yw);
-      if (p.dec(11 + (p.avail_not(A, kMbSkip) ? 1 : 0) + (p.avail_not(B, kMbSkip) ? 1 : 0))) {
-        p.skip_body(addr, qp);
-        for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
+      if (p.dec((s.is_p == kSliceB ? 24 : 11) + (p.avail_not(A, kMbSkip) ? 1 : 0) + (p.avail_not(B, kMbSkip) ? 1 : 0))) {
+        if (s.is_p == kSliceB) p.b_skip_body(addr, qp);
+        else p.skip_body(addr, qp);
+        for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = sc->mvdc1[i][0] = sc->mvdc1[i][1] = 0;
         p.prev_qpd = false;
       } else {
         ok = p.mb_cabac(addr, &qp);

@@ -173,6 +173,7 @@ struct FullScratch {
   int16_t lv[64];               // levels of the block being decoded, coefficient-list order
   uint8_t mvdc[16][2];          // Min(|mvd|, 33) of the current macroblock's 4x4 blocks
   uint8_t mvdl[4][2];           // ... of the previous macroblock's right column
+  uint8_t mvdc1[16][2], mvdl1[4][2];  // the same for list 1 (B slices)
 };
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));  // SROA-friendly (uint4 copies are memmoves)
@@ -684,14 +685,15 @@ struct Parser {
 
   VTS_HD VTS_INLINE void skip_mb(int addr, int qp) {
     begin_mb(addr);
-    if (s->is_p == kSliceB) {  // B_Skip (8.4.1.2)
-      cur().type = kMbSkip;
-      cur().qp = static_cast<uint8_t>(qp);
-      cur1().direct = 0x0f | kDirect16;
-      direct_pred(addr, 0xffffu);
-      return;
-    }
-    skip_body(addr, qp);
+    if (s->is_p == kSliceB) b_skip_body(addr, qp);
+    else skip_body(addr, qp);
+  }
+  // B_Skip (8.4.1.2) of the macroblock begin_mb has started
+  VTS_HD VTS_INLINE void b_skip_body(int addr, int qp) {
+    cur().type = kMbSkip;
+    cur().qp = static_cast<uint8_t>(qp);
+    cur1().direct = 0x0f | kDirect16;
+    direct_pred(addr, 0xffffu);
   }
   // P_Skip (8.4.1.1) of the macroblock begin_mb has started
   VTS_HD VTS_INLINE void skip_body(int addr, int qp) {
@@ -767,6 +769,18 @@ struct Parser {
           sc->mvd[l][4 * k + q][1] = br.se();
         }
       }
+    for (int k = 0; k < 4; ++k)
+      if (shape == 3 && pm[k] == 0) cur1().direct |= static_cast<uint8_t>(1u << k);
+    return b_motion(addr, shape);
+  }
+
+  // the motion of a B macroblock from sc->pm / sub / refs / refs1 / mvd:
+  // partitions in order, list 0 before list 1 of each (sub-)partition, direct
+  // quadrants by 8.4.1.2 in place
+  VTS_HD bool b_motion(int addr, int shape) {
+    const uint8_t *pm = sc->pm;
+    const int8_t *sub = sc->sub, *r0 = sc->refs, *r1 = sc->refs1;
+    const int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
     uint32_t done = 0;
     for (int k = 0; k < nparts; ++k) {
       int nsub = 1, pw, ph, x0, y0;
@@ -782,7 +796,6 @@ struct Parser {
       }
       if (pm[k] == 0) {  // B_Direct_8x8
         const uint32_t bm = 0x33u << ((y0 / 4) * 4 + x0 / 4);
-        cur1().direct |= static_cast<uint8_t>(1u << k);
         direct_pred(addr, bm);
         if (err) return false;
         done |= bm;
