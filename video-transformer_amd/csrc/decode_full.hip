@@ -478,23 +478,24 @@ __device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraT
   const bool D = nb_ok(mx > 0 && my > 0 ? mb - mbw - 1 : -1);
   // borders into the tile
   const int64_t yrow0 = static_cast<int64_t>(my * 16) * pitch + mx * 16;
-  if (b < 7 && my > 0) {
+  // unavailable neighbours read as 0 (as the oracle; conforming streams never use them)
+  if (b < 7) {
     const bool need = b == 0 ? D : (b < 5 ? B : C);
     uint32_t v = 0;
     if (need) v = *reinterpret_cast<const uint32_t *>(Y + yrow0 - pitch - 4 + 4 * b);
     *reinterpret_cast<uint32_t *>(&t.y[0][4 * b]) = v;
   }
-  if (A) t.y[1 + b][3] = Y[yrow0 + static_cast<int64_t>(b) * pitch - 1];
+  t.y[1 + b][3] = A ? Y[yrow0 + static_cast<int64_t>(b) * pitch - 1] : 0;
   const int64_t crow0 = static_cast<int64_t>(my * 8) * pitch + mx * 16;
-  if (b < 8 && A) {
-    const uint32_t v = *reinterpret_cast<const uint32_t *>(UV + crow0 + static_cast<int64_t>(b) * pitch - 4);
+  if (b < 8) {
+    const uint32_t v = A ? *reinterpret_cast<const uint32_t *>(UV + crow0 + static_cast<int64_t>(b) * pitch - 4) : 0u;
     t.cl[0][b] = (v >> 16) & 255;
     t.cl[1][b] = v >> 24;
   }
-  if (b >= 8 && b < 13 && my > 0) {
+  if (b >= 8 && b < 13) {
     const int i = b - 8;  // dword i of chroma row -1, interleaved bytes -4 + 4i
-    if (i == 0 ? D : B) {
-      const uint32_t v = *reinterpret_cast<const uint32_t *>(UV + crow0 - pitch - 4 + 4 * i);
+    {
+      const uint32_t v = (i == 0 ? D : B) ? *reinterpret_cast<const uint32_t *>(UV + crow0 - pitch - 4 + 4 * i) : 0u;
       if (i == 0) {
         t.ct[0][0] = (v >> 16) & 255;
         t.ct[1][0] = v >> 24;
