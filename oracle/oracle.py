@@ -437,7 +437,8 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None,
     or_score_frames would have over the whole sequence.  With max_frames, only
     the first GOPs covering that many frames.  decoder "full" decodes with
     the general oracle (h264_full_oracle.c fo_decode; an IDR starts every GOP,
-    so GOPs are independent).  Returns hist [F, 256] u32,
+    so GOPs are independent; with B pictures each GOP's frames are put in
+    presentation order, which an IDR keeps inside the GOP).  Returns hist [F, 256] u32,
     sad [F] u64, score [F] f32, pts, timescale, the frame count and seconds."""
     import time
     from concurrent.futures import ThreadPoolExecutor
@@ -464,6 +465,7 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None,
     data = np.frombuffer(m["data"], np.uint8)
     offs = np.asarray(m["offsets"], np.int64)
     sizes = np.asarray(m["sizes"], np.int64)
+    pts_all = list(m["pts"])
     idr = [i for i in range(len(offs)) if data[offs[i] + nls] & 0x1F == 5]
     if not idr or idr[0] != 0:
         raise RuntimeError("stream does not start with an IDR access unit")
@@ -497,6 +499,9 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None,
         elif L.or_decode_samples(C.byref(prm), data.ctypes.data, offs[a:b].ctypes.data,
                                  sizes[a:b].ctypes.data, cnt, out.ctypes.data, C.byref(bad)):
             raise RuntimeError(f"oracle decode failed in GOP at frame {a}")
+        order = sorted(range(cnt), key=lambda i: pts_all[a + i])
+        if order != list(range(cnt)):
+            out = out[order]
         fr = out.reshape(-1)
         r = score_frames(fr, W * H * 3 // 2, cnt, W, H, W, H, k, want_rgb=False)
         hist[a:b] = r["hist"]
@@ -516,8 +521,11 @@ def decode_score_gops(path, k: int, threads: int, max_frames: int | None = None,
         sad[a] = s_
         score[a] = np.float32(s_ / (w * h * 255.0))
     dt = time.perf_counter() - t0
+    pts_sorted = sorted(pts_all[:n])
+    if n < len(pts_all) and pts_sorted[-1] > min(pts_all[n:]):
+        raise RuntimeError("a GOP's frames are presented after the next GOP's")
     return {"hist": hist, "sad": sad, "score": score, "frames": frames, "seconds": dt,
-            "pts": [int(x) for x in m["dts"][:n]], "timescale": int(m["timescale"]),
+            "pts": [int(x) for x in pts_sorted], "timescale": int(m["timescale"]),
             "width": W, "height": H, "gops": len(gops)}
 
 
