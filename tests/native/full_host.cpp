@@ -143,6 +143,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   P.cabac = pps.entropy_coding_mode;
   P.t8mode = facts.transform_8x8;
   P.bframes = bframes;
+  P.has_ext = exts.empty() ? 0 : 1;
   P.direct8x8 = sps.direct_8x8_inference;
   const uint32_t epoch = 7;
   for (int fi = 0; fi < n; ++fi) {

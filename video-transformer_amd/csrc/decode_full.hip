@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
   const int W = mbw * 16, H = mbh * 16;
   int pv[16], cpred[2][4];
   pred_ref(a, rs0 >= 0 ? rs0 : rs1, rs0 >= 0 ? mvw : mvw1, x0, y0, cx, cy, W, H, pv, cpred);
-  const int ext = a.slices[h.slice].ext;
+  const int ext = a.P.has_ext ? a.slices[h.slice].ext : -1;
   if (rs1 >= 0 || ext >= 0) {  // bi-prediction / weighted prediction (8.4.2.3)
     const full::Wp Wt = full::wp_make(ext >= 0 ? a.exts + ext : nullptr, r0, r1);
     int pv1[16], cp1[2][4];

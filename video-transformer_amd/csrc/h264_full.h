@@ -62,7 +62,8 @@ struct FullParams {
   int32_t t8mode;       // transform_8x8_mode_flag
   int32_t bframes;      // the stream has B slices: every macroblock also writes an MbRecB
   int32_t direct8x8;    // direct_8x8_inference_flag
-  int32_t _pad[3];
+  int32_t has_ext;      // some slice has a SliceExt (B or weighted prediction)
+  int32_t _pad[2];
 };
 
 // Stored coefficient blocks of a macroblock, in parse order = bit order.

@@ -259,7 +259,7 @@ struct CabacParser : Parser {
   // mb_pred / sub_mb_pred of a B macroblock (7.3.5.1-2): mb_type 0..22;
   // *small: a partition below 8x8 (or a direct one without
   // direct_8x8_inference) rules out transform_size_8x8_flag
-  VTS_HD bool b_inter_cabac(int addr, int mb_type, bool *small) {
+  VTS_HD VTS_INLINE bool b_inter_cabac(int addr, int mb_type, bool *small) {
     uint8_t *pm = sc->pm;
     int8_t *sub = sc->sub, *r0 = sc->refs, *r1 = sc->refs1;
     for (int k = 0; k < 4; ++k) {

@@ -615,7 +615,7 @@ struct Parser {
   // 8.4.1.2: direct prediction of the raster 4x4 blocks in `mask` from the
   // colocated picture's records (8.4.1.2.1) — spatial (8.4.1.2.2) or temporal
   // (8.4.1.2.3)
-  VTS_HD void direct_pred(int addr, uint32_t mask) {
+  VTS_HD VTS_INLINE void direct_pred(int addr, uint32_t mask) {
     const SliceExt &x = *bc.x;
     int ref0 = -1, ref1 = -1, mp[2][2] = {{0, 0}, {0, 0}};
     bool zero = false;
@@ -713,7 +713,7 @@ struct Parser {
   // mb_pred / sub_mb_pred of a B macroblock (7.3.5.1-2, Tables 7-14, 7-18)
   // and its motion: partitions in order, list 0 before list 1 of each
   // (sub-)partition, direct partitions by 8.4.1.2 in place
-  VTS_HD bool b_inter(int addr, int mb_type) {
+  VTS_HD VTS_INLINE bool b_inter(int addr, int mb_type) {
     uint8_t *pm = sc->pm;
     int8_t *sub = sc->sub, *r0 = sc->refs, *r1 = sc->refs1;
     int shape;
@@ -777,7 +777,7 @@ struct Parser {
   // the motion of a B macroblock from sc->pm / sub / refs / refs1 / mvd:
   // partitions in order, list 0 before list 1 of each (sub-)partition, direct
   // quadrants by 8.4.1.2 in place
-  VTS_HD bool b_motion(int addr, int shape) {
+  VTS_HD VTS_INLINE bool b_motion(int addr, int shape) {
     const uint8_t *pm = sc->pm;
     const int8_t *sub = sc->sub, *r0 = sc->refs, *r1 = sc->refs1;
     const int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
@@ -809,6 +809,7 @@ struct Parser {
           else if (sub[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
         }
         int v[2][2] = {{0, 0}, {0, 0}};
+#pragma unroll
         for (int l = 0; l < 2; ++l) {
           if (!((pm[k] >> l) & 1)) continue;
           int px, py;

@@ -230,6 +230,7 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
     w.plv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->fslices.size()) - w.fs0));
     }
     if (arena > 0xffffffffll) return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
+    c->fprm.has_ext = c->exts.empty() ? 0 : 1;
     w.fs1 = static_cast<int64_t>(c->fslices.size());
     c->arena_blocks = std::max(c->arena_blocks, arena);
     std::vector<std::vector<int4>> lv(static_cast<size_t>(maxl + 1));
