@@ -157,3 +157,69 @@ def test_compress_video_for_upload_keeps_audio(tmp_path):
     m = oracle.read_mp4(out)
     assert len(m["sizes"]) == 60
     assert not list(tmp_path.glob("*.tmp"))
+
+
+def _oracle_run_full(path, tk):
+    """The oracle side for any stream the general decoder takes: frames in
+    presentation order from h264_full_oracle.c, then the same transcode."""
+    frames, info = oracle.decode_full(path)
+    F, W, H = frames.shape[0], info["width"], info["height"]
+    k = 4 if H <= 720 else 6
+    sc = oracle.score_frames(frames.reshape(-1), frames[0].size, F, W, H, W, H, k,
+                             want_rgb=False)["score"]
+    kw = dict(out_height=tk.get("height", 360), search_range=tk.get("search_range", 8),
+              max_mb_sad=tk.get("max_mb_sad", 1536), keyint=tk.get("keyint", 250),
+              idr_at_cuts=tk.get("idr_at_cuts", False))
+    return oracle.transcode(frames, W, H, sc, want_recon=True, **kw), info
+
+
+FULL_CASES = [
+    ("full_ip", dict(width=320, height=240, n_frames=60, coding="full"), None),
+    ("b_frames", dict(width=320, height=240, n_frames=60, coding="full", bframes=True, weighted="implicit"),
+     None),
+    ("cabac_b", dict(width=320, height=240, n_frames=45, coding="full", bframes=True, chunks=1), "cabac"),
+    ("real_cabac_clip", None, "real"),
+]
+
+
+@pytest.mark.parametrize("name,sk,mode", FULL_CASES, ids=[c[0] for c in FULL_CASES])
+def test_transcode_of_general_decoder_inputs(tmp_path, name, sk, mode):
+    """The upload transcode on inputs only the general decoder takes
+    (residuals + deblocking, B pictures reordered to presentation order,
+    CABAC B, the real High-profile CABAC clip): every output byte equals the
+    oracle's transcode of the oracle's decode, timing follows the source's
+    presentation times, and the device decoder reads the output back to the
+    encoder's reconstruction."""
+    _require_gpu()
+    from pathlib import Path
+    src, out = tmp_path / "in.mp4", tmp_path / "out.mp4"
+    if mode == "real":
+        src = Path(__file__).resolve().parent / "golden" / "real" / "realshort.mp4"
+    elif mode == "cabac":
+        cav = tmp_path / "cavlc.mp4"
+        scene.synth_write(cav, cut_min_s=0.7, cut_max_s=1.5, gop_max_s=0.8, seed=3, **sk)
+        oracle.cabac_convert(cav, src, seed=5, t8=True)
+    else:
+        scene.synth_write(src, cut_min_s=0.7, cut_max_s=1.5, gop_max_s=0.8, seed=3, **sk)
+    tk = dict(height=120)
+    ref, info = _oracle_run_full(src, tk)
+    with scene.VideoScorer(src) as v:
+        assert v.general()
+        facts = v.transcode(out, **tk)
+    assert (facts["width"], facts["height"]) == (ref["width"], ref["height"])
+    assert (facts["pcm_mbs"], facts["inter_mbs"], facts["skip_mbs"]) == \
+        (ref["pcm_mbs"], ref["inter_mbs"], ref["skip_mbs"])
+    m = oracle.read_mp4(out)
+    data = m["data"]
+    got = [data[o:o + s] for o, s in zip(m["offsets"], m["sizes"])]
+    assert len(got) == len(ref["samples"])
+    for i, (a, b) in enumerate(zip(got, ref["samples"])):
+        assert a == b, f"sample {i} differs"
+    assert m["dts"] == [p - info["pts"][0] for p in info["pts"]] or m["dts"] == list(info["pts"])
+    sw, sh, ch = ref["width"], ref["height"], ref["coded_height"]
+    rec = ref["recon"]
+    with scene.VideoScorer(out) as d:
+        d.score()
+        last = d.frame_nv12(d.n_frames - 1).reshape(sh * 3 // 2, sw)
+    want = np.concatenate([rec[-1, :sh, :sw], rec[-1, ch:ch + sh // 2, :sw]])
+    assert np.array_equal(last, want)
