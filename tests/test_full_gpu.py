@@ -156,6 +156,7 @@ B_STREAMS = [
     ("temporal", dict(width=176, height=144, temporal_direct=True)),
     ("slices", dict(width=176, height=144, slices_per_row=2, weighted="implicit", temporal_direct=True)),
     ("hd720", dict(width=1280, height=720, slices_per_row=0, weighted="explicit", temporal_direct=True)),
+    ("fhd_crop", dict(width=1920, height=1080, slices_per_row=0, weighted="implicit")),
 ]
 
 
@@ -167,19 +168,20 @@ def test_b_pictures_bit_exact(tmp_path, name, kw):
     order, thumbnails, histograms, SADs and scores equal the oracle; the
     parse runs B pictures one launch after their colocated pictures."""
     _require_gpu()
-    n = 30 if kw["height"] >= 720 else 45
+    n = 16 if kw["height"] > 720 else (30 if kw["height"] >= 720 else 45)
     path = tmp_path / f"b_{name}.mp4"
     scene.synth_write(path, n_frames=n, coding="full", bframes=True, cut_min_s=0.5, cut_max_s=1.2,
                       gop_max_s=0.8, seed=11, chunks=1, **kw)
     frames, _ = oracle.decode_full(path)
     W, H = kw["width"], kw["height"]
-    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 4)
-    with scene.VideoScorer(path, keep_frames=True) as v:
+    k = 4 if H <= 720 else 6
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, k)
+    with scene.VideoScorer(path, keep_frames=True, k=k) as v:
         assert v.general()
         res = v.score()
         got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
         assert _first_diff(got, frames) == []
-        rgb = np.stack([v.thumbnail_rgb(i, 4) for i in range(n)]).reshape(-1)
+        rgb = np.stack([v.thumbnail_rgb(i, k) for i in range(n)]).reshape(-1)
         assert np.array_equal(rgb, ref["rgb"])
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
