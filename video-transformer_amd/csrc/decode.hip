@@ -347,6 +347,101 @@ __device__ __forceinline__ uint4 finish_row(bool chroma, bool pcm, uint4 lo, uin
   return v;
 }
 
+// Row source in at most 6 dwords (h264_recon_score6b, whose 9 rows are all
+// in flight at once): a 16-byte load at 4-byte alignment plus the dword after
+// it (interior and I_PCM luma rows: 5 dwords instead of two aligned 16-byte
+// loads' 8), the aligned 16 bytes at a picture edge (4 dwords; the fill comes
+// from them), or the Cb and Cr 8-byte runs of an I_PCM chroma row (3 + 3).
+// shf = byte shift | mode << 8: 0 funnel, 1 / 2 left / right edge, 3 I_PCM
+// chroma.
+#ifndef VTS_K4_ROW6
+#define VTS_K4_ROW6 0  // 1: h264_recon_score<K> rows in flight as <= 6 dwords (measured -1 %)
+#endif
+typedef uint4 uint4_a4 __attribute__((aligned(4)));
+typedef uint32_t u32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
+struct Row6 {
+  uint32_t w0, w1, w2, w3, w4, w5;
+  int shf;
+};
+__device__ __forceinline__ void issue_row6(const FrameRefs &F, const uint8_t *pcmb, bool pcm, bool chroma, int rin,
+                                           int m, int mby, int mvx, int mvy, Row6 &o) {
+  if (pcm && chroma) {
+    const uint8_t *pu = pcmb + 256 + 8 * rin;  // Cr row is 64 B on
+    const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pu) & 3);
+    const u32x3_a4 a = *reinterpret_cast<const u32x3_a4 *>(pu - sh);
+    const u32x3_a4 b = *reinterpret_cast<const u32x3_a4 *>(pu + 64 - sh);
+    o.w0 = a.x, o.w1 = a.y, o.w2 = a.z, o.w3 = b.x, o.w4 = b.y, o.w5 = b.z;
+    o.shf = sh | (3 << 8);
+    return;
+  }
+  const uint8_t *p;
+  int mode = 0, esh = 0;
+  if (pcm) {
+    p = pcmb + 16 * rin;
+  } else {
+    const uint8_t *row = chroma ? F.ref_uv + clampi(mby * 8 + rin + (mvy >> 3), 0, F.CH - 1) * F.pitch
+                                : F.ref + clampi(mby * 16 + rin + (mvy >> 2), 0, F.H - 1) * F.pitch;
+    const int x0 = chroma ? 2 * (m * 8 + (mvx >> 3)) : m * 16 + (mvx >> 2);
+    if (x0 < 0) {
+      p = row;
+      mode = 1;
+      esh = x0 > -16 ? 16 + x0 : 0;
+    } else if (x0 > F.W - 16) {
+      p = row + F.W - 16;
+      mode = 2;
+      esh = min(x0 - (F.W - 16), 16);
+    } else {
+      p = row + x0;
+    }
+  }
+  if (mode == 0) {
+    const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(p) & 3);
+    const uint4 v = *reinterpret_cast<const uint4_a4 *>(p - sh);
+    o.w0 = v.x, o.w1 = v.y, o.w2 = v.z, o.w3 = v.w;
+    o.w4 = *reinterpret_cast<const uint32_t *>(p - sh + 16);
+    o.shf = sh;
+  } else {
+    const uint4 v = *reinterpret_cast<const uint4 *>(p);
+    o.w0 = v.x, o.w1 = v.y, o.w2 = v.z, o.w3 = v.w, o.w4 = 0;
+    o.shf = esh | (mode << 8);
+  }
+}
+__device__ __forceinline__ uint4 finish_row6(bool chroma, bool pcm, const Row6 &o, uint32_t &zero) {
+  const int mode = o.shf >> 8, sh = o.shf & 255;
+  if (mode == 3) {
+    const uint32_t u0 = __builtin_amdgcn_alignbyte(o.w1, o.w0, sh), u1 = __builtin_amdgcn_alignbyte(o.w2, o.w1, sh);
+    const uint32_t v0 = __builtin_amdgcn_alignbyte(o.w4, o.w3, sh), v1 = __builtin_amdgcn_alignbyte(o.w5, o.w4, sh);
+    zero |= has_zero_byte(u0) | has_zero_byte(u1) | has_zero_byte(v0) | has_zero_byte(v1);
+    return interleave_uv(u0, u1, v0, v1);
+  }
+  if (mode == 0) {
+    const uint4 v = make_uint4(__builtin_amdgcn_alignbyte(o.w1, o.w0, sh), __builtin_amdgcn_alignbyte(o.w2, o.w1, sh),
+                               __builtin_amdgcn_alignbyte(o.w3, o.w2, sh), __builtin_amdgcn_alignbyte(o.w4, o.w3, sh));
+    if (pcm) zero |= has_zero_byte(v.x) | has_zero_byte(v.y) | has_zero_byte(v.z) | has_zero_byte(v.w);
+    return v;
+  }
+  // picture edge: the 16 bytes at the edge against the replicated edge sample
+  // (a byte for luma, a Cb/Cr pair for NV12), bytes [sh, sh + 16) of the pair
+  uint32_t w[8];
+  if (mode == 1) {
+    const uint32_t f = chroma ? (o.w0 & 0xffffu) * 0x00010001u : (o.w0 & 0xffu) * 0x01010101u;
+    w[0] = w[1] = w[2] = w[3] = f;
+    w[4] = o.w0, w[5] = o.w1, w[6] = o.w2, w[7] = o.w3;
+  } else {
+    const uint32_t g = chroma ? (o.w3 >> 16) * 0x00010001u : (o.w3 >> 24) * 0x01010101u;
+    if (sh >= 16) return make_uint4(g, g, g, g);
+    w[0] = o.w0, w[1] = o.w1, w[2] = o.w2, w[3] = o.w3;
+    w[4] = w[5] = w[6] = w[7] = g;
+  }
+  const int qd = (sh >> 2) & 3, r = sh & 3;
+  uint32_t t[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+    t[j] = (qd == 0) ? w[j] : (qd == 1) ? w[j + 1] : (qd == 2) ? w[j + 2] : w[j + 3 < 8 ? j + 3 : 7];
+  return make_uint4(__builtin_amdgcn_alignbyte(t[1], t[0], r), __builtin_amdgcn_alignbyte(t[2], t[1], r),
+                    __builtin_amdgcn_alignbyte(t[3], t[2], r), __builtin_amdgcn_alignbyte(t[4], t[3], r));
+}
+
 // ------------------------------------------------ fused decode + scoring
 // h264_recon_score<K>: one LANE per (macroblock, group of rows).  A group is
 // the K luma rows + K/2 chroma rows of one thumbnail row (K = 2, 4, 8; K = 0
@@ -496,6 +591,38 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       // every aligned load is issued before any is used: 16-byte pairs for
       // luma / NV12 rows, 8-byte pairs of the planar Cb and Cr rows of I_PCM
       const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
+#if VTS_K4_ROW6
+      // rows in flight as <= 6 dwords (issue_row6: a 4-byte-aligned 16-byte
+      // load + one dword; LDS-staged I_PCM rows pass through with shift 0)
+      Row6 src[KK + HK];
+      const uint4 *blk = pcm_lds + (threadIdx.x % MB_PER_WG) * 24;
+      const bool staged = kStage && stage && pcm;
+#pragma unroll
+      for (int i = 0; i < KK + HK; ++i) {
+        if (staged) {
+          if (i < KK) {
+            const uint4 v = blk[q * KK + i];
+            src[i].w0 = v.x, src[i].w1 = v.y, src[i].w2 = v.z, src[i].w3 = v.w, src[i].w4 = 0, src[i].w5 = 0;
+            src[i].shf = 0;
+          } else {
+            const int r = q * HK + (i - KK);
+            const uint4 u = blk[16 + (r >> 1)], v = blk[20 + (r >> 1)];
+            src[i].w0 = (r & 1) ? u.z : u.x, src[i].w1 = (r & 1) ? u.w : u.y, src[i].w2 = 0;
+            src[i].w3 = (r & 1) ? v.z : v.x, src[i].w4 = (r & 1) ? v.w : v.y, src[i].w5 = 0;
+            src[i].shf = 3 << 8;
+          }
+        } else {
+          const bool ch = i >= KK;
+          issue_row6(F, pcmb, pcm, ch, ch ? q * HK + (i - KK) : q * KK + i, m, mby, mvx, mvy, src[i]);
+        }
+      }
+      uint32_t zero = 0;
+#pragma unroll
+      for (int i = 0; i < KK + HK; ++i) {
+        const uint4 v = finish_row6(i >= KK, pcm, src[i], zero);
+        if (i < KK) yr[i] = v; else cr[i - KK] = v;
+      }
+#else
       uint4 lo[KK + HK], hi[KK + HK];
       int shf[KK + HK];  // funnel shift | edge mode << 8 (1 left, 2 right)
       // LDS-staged I_PCM block (I pictures): luma row r = chunk r, Cb row r =
@@ -596,6 +723,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
         }
         if (i < KK) yr[i] = v; else cr[i - KK] = v;
       }
+#endif
       if (pcm && zero) errs |= pcm_rows_epb(pcmb, q, KK, HK);
     } else {
 #pragma unroll
@@ -892,6 +1020,33 @@ __device__ __noinline__ uint32_t pcm_row_epb(const uint8_t *pcm, bool chroma, in
 #ifndef VTS_K6B_WAVES
 #define VTS_K6B_WAVES 0
 #endif
+#ifndef VTS_K6B_ROW6
+#define VTS_K6B_ROW6 1  // rows in flight as <= 6 dwords (issue_row6), each finished,
+                        // stored and box-summed as it lands (no 9-row array)
+#endif
+
+// add row i of a band (0..5 luma, 6..8 NV12 chroma) into the lane's segment
+// box sums: [0] = the left partial [0, b0), [1..3] = the owned pixels
+__device__ __forceinline__ void k6_acc_row(int i, int b0, const uint4 row, uint32_t (&ys)[4], uint32_t (&us)[4],
+                                           uint32_t (&vs)[4]) {
+#pragma unroll
+  for (int sgm = 0; sgm < 4; ++sgm) {
+    const int lo_b = sgm == 0 ? 0 : b0 + 6 * (sgm - 1);
+    const int hi_b = sgm == 0 ? b0 : min(lo_b + 6, 16);
+    if (hi_b <= lo_b) continue;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t mk = byte_mask(lo_b, hi_b, w);
+      const uint32_t word = w == 0 ? row.x : (w == 1 ? row.y : (w == 2 ? row.z : row.w));
+      if (i < 6) {
+        ys[sgm] = sad_u8(word & mk, 0u, ys[sgm]);
+      } else {
+        us[sgm] = sad_u8(word & mk & 0x00ff00ffu, 0u, us[sgm]);
+        vs[sgm] = sad_u8(word & mk & 0xff00ff00u, 0u, vs[sgm]);
+      }
+    }
+  }
+}
 #if VTS_K6B_WAVES
 #define VTS_K6B_OCC __attribute__((amdgpu_waves_per_eu(VTS_K6B_WAVES)))
 #else
@@ -942,10 +1097,43 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
   __syncthreads();
   uint32_t errs = 0;
   uint4 rows[K + HK];  // 6 luma rows, then 3 NV12 chroma rows
+  uint32_t ys[4] = {0, 0, 0, 0}, us[4] = {0, 0, 0, 0}, vs[4] = {0, 0, 0, 0};  // box sums, [0] = left partial
+  const int b0 = j == 0 ? 0 : (j == 1 ? 2 : 4);  // end of the left partial = start of pixel 1
+  bool summed = false;
   if (active) {
     uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
     uint8_t *dst_uv = dst + F.pitch * F.H;
     if (fast_cmd(F, c0) && fast_cmd(F, c1)) {
+#if VTS_K6B_ROW6
+      Row6 src[K + HK];  // <= 6 dwords per row in flight (48 VGPRs for the 9 rows, not 72)
+#pragma unroll
+      for (int i = 0; i < K + HK; ++i) {
+        const bool chroma = i >= K;
+        const int r = chroma ? HK * band + (i - K) : r0 + i;  // luma row / chroma row
+        const int mbr = chroma ? r >> 3 : r >> 4;
+        const uint64_t c = mbr == mby0 ? c0 : c1;
+        const bool pcm = (c >> 62) == 1;
+        const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
+        const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
+        if (r < (chroma ? F.CH : F.H)) {
+          issue_row6(F, pcmb, pcm, chroma, chroma ? (r & 7) : (r & 15), m, mbr, mvx, mvy, src[i]);
+        } else {
+          src[i].w0 = src[i].w1 = src[i].w2 = src[i].w3 = src[i].w4 = src[i].w5 = 0;
+          src[i].shf = 0;
+        }
+      }
+      uint32_t zero = 0;
+#pragma unroll
+      for (int i = 0; i < K + HK; ++i) {
+        const bool chroma = i >= K;
+        const int r = chroma ? HK * band + (i - K) : r0 + i;
+        const uint64_t c = (chroma ? r >> 3 : r >> 4) == mby0 ? c0 : c1;
+        const uint4 row = finish_row6(chroma, (c >> 62) == 1, src[i], zero);
+        if (r < (chroma ? F.CH : F.H)) st_row((chroma ? dst_uv : dst) + static_cast<int64_t>(r) * F.pitch + m * 16, row);
+        if (scored) k6_acc_row(i, b0, row, ys, us, vs);
+      }
+      summed = true;
+#else
       uint4 lo[K + HK], hi[K + HK];
       int shf[K + HK];
 #pragma unroll
@@ -970,6 +1158,7 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
         const uint64_t c = (chroma ? r >> 3 : r >> 4) == mby0 ? c0 : c1;
         rows[i] = finish_row(chroma, (c >> 62) == 1, lo[i], hi[i], shf[i], zero);
       }
+#endif
       if (zero) {  // a zero byte in I_PCM samples: check for emulation prevention exactly
         for (int i = 0; i < K + HK; ++i) {
           const bool chroma = i >= K;
@@ -979,6 +1168,7 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
             errs |= pcm_row_epb(F.es + static_cast<int64_t>(c & 0xffffffffffffull), chroma, chroma ? (r & 7) : (r & 15));
         }
       }
+#if !VTS_K6B_ROW6
 #pragma unroll
       for (int i = 0; i < K + HK; ++i) {
         const bool chroma = i >= K;
@@ -986,6 +1176,7 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
         if (r < (chroma ? F.CH : F.H))
           st_row((chroma ? dst_uv : dst) + static_cast<int64_t>(r) * F.pitch + m * 16, rows[i]);
       }
+#endif
     } else {
       // general path (sub-pel chroma, errors): rare; one row at a time,
       // stored, then read back for scoring (no runtime-indexed register array)
@@ -1010,9 +1201,7 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
   }
   // box sums: the left partial (bytes owed to the previous lane's last pixel)
   // and the owned pixels' segments, luma over 6 rows, Cb / Cr over 3
-  uint32_t ys[4] = {0, 0, 0, 0}, us[4] = {0, 0, 0, 0}, vs[4] = {0, 0, 0, 0};  // [0] = left partial
-  if (scored) {
-    const int b0 = j == 0 ? 0 : (j == 1 ? 2 : 4);  // end of the left partial = start of pixel 1
+  if (scored && !summed) {
 #pragma unroll
     for (int sgm = 0; sgm < 4; ++sgm) {
       // segment sgm: 0 = [0, b0), 1.. = owned pixels [b0 + 6 (sgm-1), +6) clipped to 16
