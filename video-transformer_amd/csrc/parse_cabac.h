@@ -384,7 +384,7 @@ struct CabacParser : Parser {
   // count of non-zero levels (0: coded_block_flag 0), -1 on error
   VTS_HD VTS_INLINE int residual(int cat, int cbf_inc, int maxNum) {
     int16_t *lv = sc->lv;
-    for (int i = 0; i < maxNum; ++i) lv[i] = 0;
+    zero16x(lv, maxNum == 15 ? 16 : maxNum < 8 ? 8 : maxNum);
     if (cat != 5 && !dec(85 + kCbfOff[cat] + cbf_inc)) return 0;
     uint64_t sig = 0;
     int numc = maxNum;
@@ -694,7 +694,7 @@ struct CabacParser : Parser {
         }
         if (nc) {  // raster 8x8 over the quarter's 4 blocks: block j = rows 2j, 2j + 1
           for (int j = 0; j < 4; ++j) {
-            for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
+            zero16x(sc->blk, 16);
             for (int i = 0; i < 64; ++i) {
               const int pos = kZz8[i];
               if ((pos >> 4) == j) sc->blk[pos & 15] = sc->lv[i];
@@ -711,7 +711,7 @@ struct CabacParser : Parser {
         if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
         m.nz[r] = static_cast<uint8_t>(nc);
         if (nc) {
-          for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
+          zero16x(sc->blk, 16);
           if (m.type == kMbI16)
             for (int i = 0; i < 15; ++i) sc->blk[kZz[i + 1]] = sc->lv[i];
           else
@@ -738,7 +738,7 @@ struct CabacParser : Parser {
           const int nc = residual(4, cbf_chroma_inc(addr, pl, b, false, intra), 15);
           if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
           if (nc) {
-            for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
+            zero16x(sc->blk, 16);
             for (int i = 0; i < 15; ++i) sc->blk[kZz[i + 1]] = sc->lv[i];
             set_cbf(19u + static_cast<uint32_t>(4 * pl + b));
             if (!store_block(kBlkChromaAc0 + 4 * pl + b)) { err |= DEC_E_SYNTAX; return false; }

@@ -145,6 +145,19 @@ VTS_HD VTS_INLINE int clip3i(int lo, int hi, int v) { return v < lo ? lo : (v > 
 // MinPositive (8.4.1.2.2)
 VTS_HD VTS_INLINE int min_positive(int x, int y) { return (x >= 0 && y >= 0) ? (x < y ? x : y) : (x > y ? x : y); }
 
+// zero n (a multiple of 8) int16 in 16-byte stores (LDS on the device)
+VTS_HD VTS_INLINE void zero16x(int16_t *p, int n) {
+  for (int i = 0; i < n; i += 8) {
+    int16_t *q = p + i;
+#if defined(__HIPCC__)
+    typedef uint32_t z4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<z4 *>(q) = z4{0, 0, 0, 0};
+#else
+    for (int k = 0; k < 8; ++k) q[k] = 0;
+#endif
+  }
+}
+
 // luma4x4BlkIdx <-> raster 4x4 block
 VTS_HD VTS_INLINE int blk_x(int k) { return ((k >> 2) & 1) * 2 + (k & 1); }
 VTS_HD VTS_INLINE int blk_y(int k) { return ((k >> 3) & 1) * 2 + ((k >> 1) & 1); }
@@ -158,7 +171,7 @@ struct FullScratch {
   MbRec top[3];           // row above, columns x-1, x, x+1 at slot column % 3: bytes 16..63 and
                           // 112..127 of the record (type, refs, modes, nz, bottom motion),
                           // word 0 = its intra dependency level
-  int16_t blk[16];        // coefficient block being decoded (raster)
+  alignas(16) int16_t blk[16];  // coefficient block being decoded (raster)
   int32_t lev[16];        // its levels in decoding order
   uint32_t cache[kCacheWords];
   uint8_t prev[16], rem[16];  // Intra4x4 prev_intra4x4_pred_mode_flag / rem_intra4x4_pred_mode
@@ -170,7 +183,7 @@ struct FullScratch {
   MbRecB top1[3];             // ... of top[3]: bytes 0..31 and 112..127
   // CABAC (parse_cabac.h)
   uint8_t cst[VTS_CABAC_NCTX];  // context states: pStateIdx << 1 | valMPS
-  int16_t lv[64];               // levels of the block being decoded, coefficient-list order
+  alignas(16) int16_t lv[64];   // levels of the block being decoded, coefficient-list order
   uint8_t mvdc[16][2];          // Min(|mvd|, 33) of the current macroblock's 4x4 blocks
   uint8_t mvdl[4][2];           // ... of the previous macroblock's right column
   uint8_t mvdc1[16][2], mvdl1[4][2];  // the same for list 1 (B slices)
@@ -346,7 +359,6 @@ struct Parser {
   // residual_block_cavlc into sc->blk (raster, coefficient list index k ->
   // zig-zag position k + start_pos); returns TotalCoeff or -1
   VTS_HD VTS_INLINE int residual_block(int nC, int maxNum, int start_pos) {
-    for (int i = 0; i < 16; ++i) sc->blk[i] = 0;
     int tc, t1;
     br.ensure(32);
     const uint32_t peek = static_cast<uint32_t>(br.win >> 32);
@@ -380,6 +392,7 @@ struct Parser {
     }
     if (tc > maxNum) return -1;
     if (tc == 0) return 0;
+    zero16x(sc->blk, 16);
     int32_t *level = sc->lev;
     int suffix_len = (tc > 10 && t1 < 3) ? 1 : 0;
     for (int i = 0; i < tc; ++i) {
