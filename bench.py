@@ -369,6 +369,8 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--window-frames", type=int, default=0,
+                    help="decoded-surface window in frames (vts_params.window_frames); 0 = sized from HBM")
     ap.add_argument("--gops-per-launch", type=int, default=0,
                     help="GOPs per reconstruct launch; <= 0 all GOPs of the window")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -471,7 +473,8 @@ def main() -> None:
         duration_s = F / FPS
     else:
         scorer = scene.VideoScorer(path, device=gpu, gops_per_launch=args.gops_per_launch,
-                                   parse_chunks=args.parse_chunks, level_block=args.level_block)
+                                   parse_chunks=args.parse_chunks, level_block=args.level_block,
+                                   window_frames=args.window_frames)
         duration_s = float(scorer.info.duration)
         F = scorer.n_frames
 

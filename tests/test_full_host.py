@@ -29,7 +29,7 @@ def harness(tmp_path_factory):
     srcs = [ROOT / "tests" / "native" / "full_host.cpp"] + [CSRC / f for f in
                                                              ("mp4.cpp", "h264.cpp", "h264_sched.cpp",
                                                               "plan.cpp")]
-    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+    subprocess.run(["g++", "-Og", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
                     f"-I{CSRC}", f"-I{ROOT / 'include'}", *map(str, srcs), "-o", str(so)], check=True)
     lib = C.CDLL(str(so))
     lib.fh_decode.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
