@@ -22,6 +22,7 @@ struct FullParseArgs {
   uint16_t *ilvl;            // ring: [slot][mb] intra dependency levels
   int16_t *arena;            // ring's coefficient arena
   uint32_t *err;
+  const int32_t *order;      // launch-relative slice of workgroup i (longest first), null = i
   FullParams P;
 };
 

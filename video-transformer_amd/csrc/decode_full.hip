@@ -43,9 +43,13 @@ constexpr int kDbkWaves = kDbkThreads / 64;
 // One slice per wave and the wave's one lane: every value of the parse is
 // wave-uniform, so control flow never diverges and the integer work can go to
 // the scalar unit; the parallelism is the window's slices (thousands of waves).
-__global__ void __launch_bounds__(1) __attribute__((amdgpu_waves_per_eu(4, 4))) h264_parse_full(FullParseArgs a) {
+#ifndef VTS_PARSE_WAVES
+#define VTS_PARSE_WAVES 4
+#endif
+__global__ void __launch_bounds__(1)
+__attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full(FullParseArgs a) {
   __shared__ full::FullScratch scratch;
-  const int i = blockIdx.x;
+  const int i = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
   const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;

@@ -133,6 +133,8 @@ struct vts_ctx {
   vts::MbRecB *d_recs1[2] = {nullptr, nullptr};  // list-1 halves (streams with B slices)
   std::vector<vts::SliceExt> exts;      // B / weighted slices' SliceExt records (all windows)
   vts::SliceExt *d_exts = nullptr;
+  std::vector<int32_t> porder;          // per fslice: parse order inside its launch (longest slice first)
+  int32_t *d_porder = nullptr;
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock

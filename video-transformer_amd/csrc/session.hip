@@ -92,6 +92,9 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   HIP_TRY(hipMalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
   if (!c->fslices.empty())
     HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_porder, sizeof(int32_t) * std::max<size_t>(1, c->porder.size())));
+  if (!c->porder.empty())
+    HIP_TRY(hipMemcpy(c->d_porder, c->porder.data(), sizeof(int32_t) * c->porder.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
@@ -1070,6 +1073,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->small.d_taps);
   f(c->d_fslices);
   f(c->d_exts);
+  f(c->d_porder);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);

@@ -28,7 +28,7 @@
 namespace vts {
 namespace {
 
-constexpr int64_t kWindowBytes = 48ll << 30;  // per ring, as the subset path
+constexpr int64_t kWindowBytes = 96ll << 30;  // per ring: parse throughput grows with the slices per launch
 constexpr int64_t kMinRingBytes = 1ll << 30;
 
 }  // namespace
@@ -162,6 +162,7 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   // per window: device slices (window-relative slots and arena), level lists
   c->fslices.clear();
   c->exts.clear();
+  c->porder.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
   for (Window &w : c->windows) {
@@ -228,6 +229,14 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
       }
     }
     w.plv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->fslices.size()) - w.fs0));
+    // workgroups are dispatched in index order and a slice's wave runs for
+    // time ~ its size: the largest slices first, so the launch does not end
+    // on a few long waves running alone
+    const int64_t l0 = static_cast<int64_t>(c->porder.size()), b = w.fs0 + (pl ? w.plv_end[pl - 1] : 0);
+    for (int64_t k = b; k < static_cast<int64_t>(c->fslices.size()); ++k) c->porder.push_back(static_cast<int32_t>(k - b));
+    std::stable_sort(c->porder.begin() + l0, c->porder.end(), [&](int32_t x, int32_t y) {
+      return c->fslices[static_cast<size_t>(b + x)].nal_size > c->fslices[static_cast<size_t>(b + y)].nal_size;
+    });
     }
     if (arena > 0xffffffffll) return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
     c->fprm.has_ext = c->exts.empty() ? 0 : 1;
@@ -290,6 +299,7 @@ int run_general(vts_ctx *c) {
       pa.slices = c->d_fslices + w.fs0 + b0;
       pa.n_slices = w.plv_end[j] - b0;
       pa.slice0 = b0;
+      pa.order = c->d_porder + w.fs0 + b0;
       VTS_TRY(parse_full_launch(pa, sp));
     }
     HIP_TRY(hipEventRecord(E[1], sp));
