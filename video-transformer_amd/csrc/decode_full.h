@@ -57,7 +57,11 @@ struct FullReconArgs {
 };
 
 int parse_full_launch(const FullParseArgs &a, hipStream_t s);
-// reconstruction (+ deblocking) of n_frames pictures of one level
+// deblocking descriptors (bS, QPs) of n_frames pictures: reads only the
+// parse's records, so one launch covers a whole window
+int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);
+// reconstruction (+ deblocking from bs_full_launch's descriptors when
+// a.deblock) of n_frames pictures of one level
 int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);
 
 }  // namespace vts

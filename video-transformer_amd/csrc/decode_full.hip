@@ -1252,6 +1252,16 @@ int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
   return VTS_OK;
 }
 
+int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
+  if (n_frames <= 0) return VTS_OK;
+  if (n_frames > 65535) return fail(VTS_E_UNSUPPORTED, "more than 65535 pictures in one bS launch");
+  const int nmb = a.P.mb_width * a.P.mb_height;
+  hipLaunchKernelGGL(h264_bs_full, dim3((nmb + 255) / 256, n_frames), dim3(256), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_bs_full launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
 int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
   const int nmb = a.P.mb_width * a.P.mb_height;
@@ -1264,9 +1274,6 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_intra_full launch: %s", hipGetErrorString(e));
   if (a.deblock) {
-    hipLaunchKernelGGL(h264_bs_full, dim3((nmb + 255) / 256, n_frames), dim3(256), 0, s, a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_bs_full launch: %s", hipGetErrorString(e));
     hipLaunchKernelGGL(h264_deblock_full, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));

@@ -321,6 +321,10 @@ int run_general(vts_ctx *c) {
     ra.deblock = 1;
     ra.err = c->d_err;
     ra.P = c->fprm;
+    if (!w.lvl_off.empty()) {  // every picture's bS at once: it needs only the parse's records
+      ra.frames = c->d_levels + w.lvl_off[0];
+      VTS_TRY(bs_full_launch(ra, static_cast<int>(w.lvl_off.back() + w.lvl_cnt.back() - w.lvl_off[0]), sd));
+    }
     for (size_t l = 0; l < w.lvl_off.size(); ++l) {
       ra.frames = c->d_levels + w.lvl_off[l];
       VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], sd));
