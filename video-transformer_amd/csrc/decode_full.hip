@@ -35,9 +35,15 @@ namespace vts {
 namespace {
 
 constexpr int kInterThreads = 256;   // 16 macroblocks x 16 blocks
-constexpr int kIntraThreads = 512;   // 32 macroblocks in flight (256 VGPRs for the Intra_8x8 path)
+#ifndef VTS_INTRA_THREADS
+#define VTS_INTRA_THREADS 512
+#endif
+#ifndef VTS_DBK_THREADS
+#define VTS_DBK_THREADS 1024
+#endif
+constexpr int kIntraThreads = VTS_INTRA_THREADS;  // 512: 32 macroblocks in flight (256 VGPRs for the Intra_8x8 path)
 constexpr int kIntraSlots = kIntraThreads / 16;
-constexpr int kDbkThreads = 1024;    // 16 waves = 16 row pairs in flight
+constexpr int kDbkThreads = VTS_DBK_THREADS;      // 1024: 16 waves = 16 row pairs in flight
 constexpr int kDbkWaves = kDbkThreads / 64;
 
 // One slice per wave and the wave's one lane: every value of the parse is
