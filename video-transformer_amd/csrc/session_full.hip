@@ -242,14 +242,41 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
     c->fprm.has_ext = c->exts.empty() ? 0 : 1;
     w.fs1 = static_cast<int64_t>(c->fslices.size());
     c->arena_blocks = std::max(c->arena_blocks, arena);
-    std::vector<std::vector<int4>> lv(static_cast<size_t>(maxl + 1));
-    for (int64_t f = w.f0; f < w.f1; ++f)
-      lv[static_cast<size_t>(level[static_cast<size_t>(f)])].push_back(make_int4(slot_of(f), 0, 0, 0));
-    for (auto &l : lv) {
-      if (l.empty()) continue;
-      w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
-      w.lvl_cnt.push_back(static_cast<int32_t>(l.size()));
-      c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
+    // two interleaved groups of GOPs reconstruct on two streams: a level's
+    // pictures are one workgroup each, and two unsynchronised level sequences
+    // pack the compute units better than one whose every level is a whole
+    // number of rounds.  A GOP here is a run of pictures that no later picture
+    // of the window predicts across, so a group never reads the other's pictures.
+    const int64_t wn = w.f1 - w.f0;
+    std::vector<uint8_t> fg(static_cast<size_t>(wn), 0);
+    int ngrp = 1;
+    if (c->general_groups > 1) {
+      std::vector<uint8_t> split(static_cast<size_t>(wn), 0);
+      int64_t m = w.f1;
+      for (int64_t x = w.f1 - 1; x >= w.f0; --x) {
+        m = std::min(m, minref[static_cast<size_t>(x)]);
+        split[static_cast<size_t>(x - w.f0)] = m >= x;
+      }
+      int64_t seg = -1;
+      for (int64_t x = 0; x < wn; ++x) {
+        if (split[static_cast<size_t>(x)]) ++seg;
+        fg[static_cast<size_t>(x)] = static_cast<uint8_t>(seg & 1);
+      }
+      if (seg >= 1) ngrp = 2;
+    }
+    w.grp.clear();
+    for (int g = 0; g < ngrp; ++g) {
+      if (g) w.grp.push_back(static_cast<int32_t>(w.lvl_off.size()));
+      std::vector<std::vector<int4>> lv(static_cast<size_t>(maxl + 1));
+      for (int64_t f = w.f0; f < w.f1; ++f)
+        if (fg[static_cast<size_t>(f - w.f0)] == g)
+          lv[static_cast<size_t>(level[static_cast<size_t>(f)])].push_back(make_int4(slot_of(f), 0, 0, 0));
+      for (auto &l : lv) {
+        if (l.empty()) continue;
+        w.lvl_off.push_back(static_cast<int64_t>(c->level_frames.size()));
+        w.lvl_cnt.push_back(static_cast<int32_t>(l.size()));
+        c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
+      }
     }
   }
   return VTS_OK;
@@ -277,6 +304,7 @@ int run_general(vts_ctx *c) {
       HIP_TRY(hipStreamWaitEvent(sp, c->ev[(wi - c->n_rings) * 6 + 4], 0));
       HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
     }
+    const size_t g1 = w.grp.empty() ? w.lvl_off.size() : static_cast<size_t>(w.grp[0]);  // group 1's first launch
     const int64_t run = c->run_no++;
     const uint32_t epoch = 1u + static_cast<uint32_t>(run % 0x7fffffff);
     if (c->ring_cleared_at[r] < 0) {  // records of another run read as absent (their epoch)
@@ -325,9 +353,17 @@ int run_general(vts_ctx *c) {
       ra.frames = c->d_levels + w.lvl_off[0];
       VTS_TRY(bs_full_launch(ra, static_cast<int>(w.lvl_off.back() + w.lvl_cnt.back() - w.lvl_off[0]), sd));
     }
+    if (g1 < w.lvl_off.size()) {  // group 1 on its own stream, after the bS launch
+      HIP_TRY(hipEventRecord(c->ev_grp[0], sd));
+      HIP_TRY(hipStreamWaitEvent(c->s_grp[0], c->ev_grp[0], 0));
+    }
     for (size_t l = 0; l < w.lvl_off.size(); ++l) {
       ra.frames = c->d_levels + w.lvl_off[l];
-      VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], sd));
+      VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], l < g1 ? sd : c->s_grp[0]));
+    }
+    if (g1 < w.lvl_off.size()) {
+      HIP_TRY(hipEventRecord(c->ev_grp[0], c->s_grp[0]));
+      HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[0], 0));
     }
     if (c->small.on) VTS_TRY(small_window(c, r, w.f0, w.f1, sd));
     HIP_TRY(hipEventRecord(E[2], sd));
