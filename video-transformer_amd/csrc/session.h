@@ -110,8 +110,8 @@ struct vts_ctx {
   static constexpr int kMaxGroups = 4;
   bool group_parse = false;  // one parse chunk per group (VTS_GROUP_PARSE)
   int recon_groups = 2;  // measured best on MI355X; VTS_RECON_GROUPS overrides
-  int general_groups = 2;  // general decoder: GOP groups reconstructing on s_dec / s_grp[0]
-                           // (DESIGN.md §5b); VTS_GENERAL_GROUPS=1 turns it off
+  int general_groups = 2;  // general decoder: GOP groups reconstructing on s_dec / s_grp[g - 1]
+                           // (DESIGN.md §5b); VTS_GENERAL_GROUPS (1..4) overrides
   hipStream_t s_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> ev;  // per window: dec start, parsed, decoded, score start, scored, spare

@@ -125,8 +125,10 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   if (!c->s_dec) HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
   if (!c->s_score) HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
   if (!c->s_parse) HIP_TRY(hipStreamCreateWithFlags(&c->s_parse, hipStreamNonBlocking));
-  if (!c->s_grp[0]) HIP_TRY(hipStreamCreateWithFlags(&c->s_grp[0], hipStreamNonBlocking));
-  if (!c->ev_grp[0]) HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[0], hipEventDisableTiming));
+  for (int g = 0; g + 1 < vts_ctx::kMaxGroups; ++g) {
+    if (!c->s_grp[g]) HIP_TRY(hipStreamCreateWithFlags(&c->s_grp[g], hipStreamNonBlocking));
+    if (!c->ev_grp[g]) HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[g], hipEventDisableTiming));
+  }
   for (auto e2 : c->ev)
     if (e2) (void)hipEventDestroy(e2);
   c->ev.assign(c->windows.size() * 6, nullptr);
@@ -181,7 +183,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   if (const char *s = std::getenv("VTS_RECON_GROUPS"))
     c->recon_groups = std::max(1, std::min(vts_ctx::kMaxGroups, std::atoi(s)));
   if (const char *s = std::getenv("VTS_GROUP_PARSE")) c->group_parse = std::atoi(s) > 0;
-  if (const char *s = std::getenv("VTS_GENERAL_GROUPS")) c->general_groups = std::max(1, std::min(2, std::atoi(s)));
+  if (const char *s = std::getenv("VTS_GENERAL_GROUPS")) c->general_groups = std::max(1, std::min(vts_ctx::kMaxGroups, std::atoi(s)));
   VTS_TRY(fill_video_info(mp4, &c->info));
   const Mp4VideoTrack &t = mp4.video.front();
   if (!(t.codec == "avc1" || t.codec == "avc3"))

@@ -260,9 +260,9 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
       int64_t seg = -1;
       for (int64_t x = 0; x < wn; ++x) {
         if (split[static_cast<size_t>(x)]) ++seg;
-        fg[static_cast<size_t>(x)] = static_cast<uint8_t>(seg & 1);
+        fg[static_cast<size_t>(x)] = static_cast<uint8_t>(seg % c->general_groups);
       }
-      if (seg >= 1) ngrp = 2;
+      ngrp = static_cast<int>(std::min<int64_t>(c->general_groups, seg + 1));
     }
     w.grp.clear();
     for (int g = 0; g < ngrp; ++g) {
@@ -304,7 +304,12 @@ int run_general(vts_ctx *c) {
       HIP_TRY(hipStreamWaitEvent(sp, c->ev[(wi - c->n_rings) * 6 + 4], 0));
       HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
     }
-    const size_t g1 = w.grp.empty() ? w.lvl_off.size() : static_cast<size_t>(w.grp[0]);  // group 1's first launch
+    const int ng = 1 + static_cast<int>(w.grp.size());
+    auto grp_of = [&](size_t l) {  // group of reconstruct launch l
+      int g = 0;
+      while (g + 1 < ng && l >= static_cast<size_t>(w.grp[static_cast<size_t>(g)])) ++g;
+      return g;
+    };
     const int64_t run = c->run_no++;
     const uint32_t epoch = 1u + static_cast<uint32_t>(run % 0x7fffffff);
     if (c->ring_cleared_at[r] < 0) {  // records of another run read as absent (their epoch)
@@ -353,17 +358,18 @@ int run_general(vts_ctx *c) {
       ra.frames = c->d_levels + w.lvl_off[0];
       VTS_TRY(bs_full_launch(ra, static_cast<int>(w.lvl_off.back() + w.lvl_cnt.back() - w.lvl_off[0]), sd));
     }
-    if (g1 < w.lvl_off.size()) {  // group 1 on its own stream, after the bS launch
+    if (ng > 1) {  // groups >= 1 on their own streams, after the bS launch
       HIP_TRY(hipEventRecord(c->ev_grp[0], sd));
-      HIP_TRY(hipStreamWaitEvent(c->s_grp[0], c->ev_grp[0], 0));
+      for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], c->ev_grp[0], 0));
     }
     for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+      const int g = grp_of(l);
       ra.frames = c->d_levels + w.lvl_off[l];
-      VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], l < g1 ? sd : c->s_grp[0]));
+      VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], g ? c->s_grp[g - 1] : sd));
     }
-    if (g1 < w.lvl_off.size()) {
-      HIP_TRY(hipEventRecord(c->ev_grp[0], c->s_grp[0]));
-      HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[0], 0));
+    for (int g = 1; g < ng; ++g) {
+      HIP_TRY(hipEventRecord(c->ev_grp[g - 1], c->s_grp[g - 1]));
+      HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[g - 1], 0));
     }
     if (c->small.on) VTS_TRY(small_window(c, r, w.f0, w.f1, sd));
     HIP_TRY(hipEventRecord(E[2], sd));
