@@ -249,3 +249,30 @@ def test_cabac_b_streams_bit_exact(tmp_path, name, kw, t8):
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
+
+
+@pytest.mark.parametrize("groups", [1, 2, 3, 4])
+@pytest.mark.parametrize("bframes", [False, True], ids=["ip", "b"])
+def test_gop_groups_on_streams_equal_the_oracle(tmp_path, monkeypatch, groups, bframes):
+    """The window's GOPs dealt to 1-4 groups that reconstruct on their own
+    streams (VTS_GENERAL_GROUPS): every frame, histogram, SAD and score still
+    equals the oracle, in one window and in several windows on two rings."""
+    _require_gpu()
+    monkeypatch.setenv("VTS_GENERAL_GROUPS", str(groups))
+    n = 120
+    path = tmp_path / "g.mp4"
+    scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=bframes,
+                      weighted="implicit" if bframes else None, cut_min_s=0.5, cut_max_s=1.5,
+                      gop_max_s=0.4, seed=17)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
+    for wf in (0, 60):
+        with scene.VideoScorer(path, keep_frames=wf == 0, window_frames=wf, n_streams=2) as v:
+            assert v.general()
+            res = v.score()
+            if wf == 0:
+                got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+                assert _first_diff(got, frames) == []
+            assert np.array_equal(res.hist, ref["hist"])
+            assert np.array_equal(res.sad, ref["sad"])
+            assert np.array_equal(res.scores, ref["score"])
