@@ -156,7 +156,7 @@ class H264Params(C.Structure):
         "poc_type", "log2_max_poc_lsb", "delta_pic_order_always_zero",
         "bottom_field_pic_order_in_frame_present", "num_ref_idx_l0_default_active",
         "redundant_pic_cnt_present", "deblocking_filter_control_present", "pic_init_qp",
-        "pps_id", "nal_length_size")]
+        "pps_id", "nal_length_size", "chroma_qp_index_offset")]
 
 
 def _boxes(buf: bytes, start: int, end: int):

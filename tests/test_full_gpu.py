@@ -276,3 +276,51 @@ def test_gop_groups_on_streams_equal_the_oracle(tmp_path, monkeypatch, groups, b
             assert np.array_equal(res.hist, ref["hist"])
             assert np.array_equal(res.sad, ref["sad"])
             assert np.array_equal(res.scores, ref["score"])
+
+
+def test_chroma_only_deblocking_goes_to_the_general_decoder(tmp_path):
+    """A subset-syntax stream whose deblocking filter is active on chroma
+    edges only (QPY 3, chroma_qp_index_offset 12, filter offsets +12: luma
+    indexA <= 15, chroma indexA 24 on I_PCM edges) must not run on the subset kernels, which do not filter: auto mode
+    picks the general decoder and matches the general oracle; subset-only
+    mode refuses it (8.7.2.2: an edge filters where indexA >= 16)."""
+    _require_gpu()
+    path = tmp_path / "cdbk.mp4"
+    scene.synth_write(path, width=320, height=240, n_frames=40, cut_min_s=0.5, cut_max_s=1.2,
+                      gop_max_s=0.6, seed=77, chroma_deblock=True)
+    frames, _ = oracle.decode_full(path)
+    unfiltered, _ = oracle.decode_full(path, flags=1)
+    assert not np.array_equal(frames, unfiltered)   # the filter changes chroma
+    H = 240
+    assert np.array_equal(frames[:, :H], unfiltered[:, :H])  # and only chroma
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, 40, 320, 240, 320, 240, 4)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(40)])
+        assert _first_diff(got, frames) == []
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.scores, ref["score"])
+    with scene.VideoScorer(path, decoder="subset") as v:
+        with pytest.raises(VtsegError):
+            v.score()
+
+
+def test_window_without_clean_picture_in_slot_range_is_refused(tmp_path, monkeypatch):
+    """ADVICE r02: a window always extends to the next clean intra picture;
+    when clean pictures are further apart than the int16 ring-slot range the
+    open must fail cleanly (VTS_E_UNSUPPORTED) instead of wrapping slots.  The
+    cap is lowered with VTS_WINDOW_SLOT_CAP so the stream stays small: one
+    IDR, then 39 P pictures."""
+    _require_gpu()
+    path = tmp_path / "onegop.mp4"
+    scene.synth_write(path, width=64, height=48, n_frames=40, cut_min_s=100, cut_max_s=100,
+                      gop_max_s=100, coding="full", seed=3)
+    monkeypatch.setenv("VTS_WINDOW_SLOT_CAP", "16")
+    with pytest.raises(VtsegError, match="clean intra picture"):
+        scene.VideoScorer(path, decoder="general")
+    monkeypatch.setenv("VTS_WINDOW_SLOT_CAP", "40")
+    frames, _ = oracle.decode_full(path)
+    with scene.VideoScorer(path, decoder="general", keep_frames=True) as v:
+        v.score()
+        assert np.array_equal(v.frame_nv12(39).reshape(frames[-1].shape), frames[-1])

@@ -82,3 +82,21 @@ def test_full_syntax_chunks_concatenate(tmp_path):
                       cut_min_s=5, cut_max_s=9, gop_max_s=2.0)
     frames, _ = oracle.decode_full(p)
     assert frames.shape[0] == 90
+
+
+def test_chroma_only_deblocking_is_outside_the_subset(tmp_path):
+    """deblocking active on chroma edges only (luma indexA < 16,
+    chroma QPc(QPY + chroma_qp_index_offset) pushing indexA to 24).  The
+    subset oracle refuses the stream like the subset device parser, and the
+    general oracle's filter changes chroma samples only."""
+    path = tmp_path / "cdbk.mp4"
+    scene.synth_write(path, width=160, height=96, n_frames=12, cut_min_s=0.2, cut_max_s=0.4,
+                      gop_max_s=0.2, seed=77, chroma_deblock=True)
+    m = oracle.read_mp4(path)
+    samples = [m["data"][o:o + z] for o, z in zip(m["offsets"], m["sizes"])]
+    with pytest.raises(RuntimeError, match="rc=-9"):
+        oracle.decode_samples(m["sps"][0], m["pps"][0], samples, m["nal_length_size"])
+    frames, _ = oracle.decode_full(path)
+    unfiltered, _ = oracle.decode_full(path, flags=1)
+    assert np.array_equal(frames[:, :96], unfiltered[:, :96])
+    assert not np.array_equal(frames[:, 96:], unfiltered[:, 96:])

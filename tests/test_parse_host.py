@@ -35,7 +35,7 @@ SHAPES = [
 DEV_FIELDS = ["mb_width", "mb_height", "log2_max_frame_num", "poc_type", "log2_max_poc_lsb",
               "delta_pic_order_always_zero", "bottom_field_pic_order_in_frame_present",
               "num_ref_idx_l0_default_active", "redundant_pic_cnt_present",
-              "deblocking_filter_control_present", "pic_init_qp", None, "pps_id"]
+              "deblocking_filter_control_present", "pic_init_qp", "chroma_qp_index_offset", "pps_id"]
 
 
 @pytest.fixture(scope="module")

@@ -88,7 +88,7 @@ std::string describe_decode_error(uint32_t flags);
 // frame_num, one reference, CAVLC, deblocking_filter_control_present) for an
 // mbw x mbh macroblock picture cropped by crop_r / crop_b luma samples.
 void make_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level, std::vector<uint8_t> *sps_nal,
-                  std::vector<uint8_t> *pps_nal);
+                  std::vector<uint8_t> *pps_nal, int chroma_qp_index_offset = 0);
 int h264_pick_level(int mbs, double mbps);
 
 // MB command word written by the parser, read by the reconstruct kernel.

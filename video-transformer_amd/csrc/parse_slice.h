@@ -358,8 +358,11 @@ VTS_HD VTS_INLINE uint32_t parse_slice(const uint8_t *es, int64_t nal_offset, in
     }
   }
   // Filtering is a no-op only if disabled or every edge's indexA < 16
-  // (alpha' = 0): max qPav is the slice QP (I_PCM has qP 0).
-  if (deblock_idc != 1 && qp + alpha_off >= 16) errs |= DEC_E_DEBLOCK;
+  // (alpha' = 0): max qPav is the slice QP (I_PCM has qP 0); chroma edges use
+  // QPc(QP + chroma_qp_index_offset), which is >= 16 exactly when
+  // QP + offset is (QPc(x) = x below 30, >= 29 above).
+  const int cqp_up = P.chroma_qp_index_offset > 0 ? P.chroma_qp_index_offset : 0;
+  if (deblock_idc != 1 && qp + cqp_up + alpha_off >= 16) errs |= DEC_E_DEBLOCK;
   if (first_mb < 0 || first_mb >= nmb) errs |= DEC_E_SYNTAX;
   if (errs || br.err || br.overrun()) return errs | ((br.err || br.overrun()) ? DEC_E_SYNTAX : 0u);
 

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -46,8 +47,13 @@ bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::
   std::vector<SchedFrame> frames;
   std::vector<SchedSlice> slices;
   if (!sched_build(c->sps, c->pps, es.data(), off, sz, nal_length_size, &frames, &slices).empty()) return true;
+  // 8.7.2.2: an edge is filtered only where indexA = qPav + filterOffsetA >= 16
+  // (alpha is 0 below).  Chroma edges use QPc of QPY + chroma_qp_index_offset;
+  // QPc(x) = x below 30 and >= 29 from there, so x + offset >= 16 is exact
+  // for the slice's QPY (I_PCM's QPY 0 only lowers qPav).
+  const int cqp = std::max(0, c->pps.chroma_qp_index_offset);
   for (const SchedSlice &s : slices)
-    if ((s.dbk_idc != 1 && s.qp + s.dbk_a >= 16) || (s.is_p && s.num_ref > 1)) return true;
+    if ((s.dbk_idc != 1 && s.qp + cqp + s.dbk_a >= 16) || (s.is_p && s.num_ref > 1)) return true;
   return false;
 }
 
@@ -122,7 +128,9 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   }
   // windows
   const int64_t tw_f = static_cast<int64_t>(c->width / c->k) * (c->height / c->k);
-  const int64_t per_frame = c->frame_stride + nmb * static_cast<int64_t>(sizeof(MbRec) + sizeof(uint16_t) + sizeof(DbkInfo)) +
+  const int64_t per_frame = c->frame_stride +
+                            nmb * static_cast<int64_t>(sizeof(MbRec) + sizeof(uint16_t) + sizeof(DbkInfo) +
+                                                       (c->fprm.bframes ? sizeof(MbRecB) : 0)) +
                             score_workspace_bytes(c->width, c->height, c->k, 1) +
                             32 * ((cap_total + n - 1) / std::max<int64_t>(1, n));
   size_t free_b = 0, total_b = 0;
@@ -136,7 +144,11 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   if (c->params.window_frames > 0) wcap = c->params.window_frames;
   else if (n * per_frame <= std::min(kWindowBytes, avail / 2)) wcap = n;
   else wcap = std::max<int64_t>(1, ring_budget / per_frame);
-  wcap = std::min<int64_t>(wcap, 32767);  // ring slots are int16 (FullSlice / MbRec ref_slot)
+  // ring slots are int16 (FullSlice.slot / ref_slot, MbRec ref slots, level
+  // lists); VTS_WINDOW_SLOT_CAP lowers the cap (tests of the refusal below)
+  int64_t slot_cap = 32767;
+  if (const char *sc = std::getenv("VTS_WINDOW_SLOT_CAP")) slot_cap = std::max<int64_t>(1, std::min<int64_t>(32767, std::atoll(sc)));
+  wcap = std::min<int64_t>(wcap, slot_cap);
   auto next_clean = [&](int64_t x) {
     while (x < n && !clean[static_cast<size_t>(x)]) ++x;
     return x;
@@ -152,6 +164,13 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
       end = nxt;
     }
     w.f1 = end;
+    // a window always reaches the next clean picture, so clean pictures
+    // further apart than the slot range (one IDR then an endless GOP, intra
+    // refresh, long open GOPs) cannot be windowed: refuse, never wrap a slot
+    if (w.f1 - w.f0 > slot_cap)
+      return fail(VTS_E_UNSUPPORTED,
+                  "frames %lld..%lld hold no clean intra picture to start a window at (%lld frames > %lld ring slots)",
+                  (long long)w.f0, (long long)w.f1 - 1, (long long)(w.f1 - w.f0), (long long)slot_cap);
     c->windows.push_back(w);
     f = end;
   }

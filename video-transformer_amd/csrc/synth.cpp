@@ -244,7 +244,8 @@ int h264_pick_level(int mbs, double mbps) {
 
 // Build the SPS/PPS RBSPs for the stream (also used by tests via the file).
 void make_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level,
-                         std::vector<uint8_t> *sps_nal, std::vector<uint8_t> *pps_nal) {
+                         std::vector<uint8_t> *sps_nal, std::vector<uint8_t> *pps_nal,
+                         int chroma_qp_index_offset) {
   BitWriter s;
   s.u(8, 66);        // profile_idc: Baseline
   s.u(8, 0xC0);      // constraint_set0 + set1: Constrained Baseline
@@ -285,7 +286,7 @@ void make_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level,
   p.u(2, 0);         // weighted_bipred_idc
   p.se(0);           // pic_init_qp_minus26
   p.se(0);           // pic_init_qs_minus26
-  p.se(0);           // chroma_qp_index_offset
+  p.se(chroma_qp_index_offset);
   p.u(1, 1);         // deblocking_filter_control_present_flag
   p.u(1, 0);         // constrained_intra_pred_flag
   p.u(1, 0);         // redundant_pic_cnt_present_flag
@@ -325,6 +326,23 @@ void encode_chunk(const vts_synth_params &P, SynthChunk *ck) {
   // non-reference, non-IDR I pictures; the P picture after one predicts from
   // the reference picture before it
   const bool nonref_refresh = (P.edge_cases & 8) != 0;
+  // edge case bit 9: deblocking on, active on chroma edges only: QPY 3,
+  // chroma_qp_index_offset 12, filter offsets +12.  Luma indexA <= 3 + 12 <
+  // 16 everywhere; chroma qPav reaches QPc(0 + 12) = 12 on I_PCM edges (bS 3 /
+  // 4), indexA 24.  A subset decoder must refuse it; the writer's own
+  // pictures are unfiltered.
+  const bool chroma_dbk = (P.edge_cases & 512) != 0;
+  auto qp_dbk = [&](BitWriter &bw) {
+    if (chroma_dbk) {
+      bw.se(-23);  // slice_qp_delta: QPY 3
+      bw.ue(0);    // disable_deblocking_filter_idc
+      bw.se(6);    // slice_alpha_c0_offset_div2
+      bw.se(6);    // slice_beta_offset_div2
+    } else {
+      bw.se(0);    // slice_qp_delta
+      bw.ue(1);    // disable_deblocking_filter_idc
+    }
+  };
   bool prev_was_ref = true;
   int vx = 0, vy = 0;  // luma pixels per frame (even unless odd_pans)
   const int spr = P.slices_per_row;
@@ -375,8 +393,7 @@ void encode_chunk(const vts_synth_params &P, SynthChunk *ck) {
           bw.u(1, 0);                         // no_output_of_prior_pics_flag
           bw.u(1, 0);                         // long_term_reference_flag
         }                                     // (nal_ref_idc 0: no dec_ref_pic_marking)
-        bw.se(0);                             // slice_qp_delta
-        bw.ue(1);                             // disable_deblocking_filter_idc
+        qp_dbk(bw);
         for (int a = first; a < last; ++a) {
           bw.ue(25);  // mb_type I_PCM
           put_pcm(bw, cur, a % mbw, a / mbw);
@@ -407,8 +424,7 @@ void encode_chunk(const vts_synth_params &P, SynthChunk *ck) {
         bw.u(1, 0);                           // num_ref_idx_active_override_flag
         bw.u(1, 0);                           // ref_pic_list_modification_flag_l0
         bw.u(1, 0);                           // adaptive_ref_pic_marking_mode_flag
-        bw.se(0);                             // slice_qp_delta
-        bw.ue(1);                             // disable_deblocking_filter_idc
+        qp_dbk(bw);
         uint32_t skip_run = 0;
         for (int a = first; a < last; ++a) {
           const int mx = a % mbw, my = a / mbw;
@@ -493,7 +509,7 @@ extern "C" int vts_synth_write(const char *path, const vts_synth_params *prm,
   const int level = h264_pick_level(mbw * mbh, mbw * mbh * fps);
   std::vector<uint8_t> sps, pps;
   if (P.coding == 1) make_sps_pps_full(P, level, &sps, &pps);
-  else make_sps_pps(mbw, mbh, cw - P.width, ch - P.height, level, &sps, &pps);
+  else make_sps_pps(mbw, mbh, cw - P.width, ch - P.height, level, &sps, &pps, (P.edge_cases & 512) ? 12 : 0);
 
   Mp4Writer mw;
   std::string e = mw.open(path);

@@ -267,13 +267,17 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 odd_motion: bool = False, drop_last_slice: bool = False,
                 nonref_refresh: bool = False, chunks: int = 0, coding: str = "subset",
                 constrained_intra: bool = False, bframes: bool = False,
-                weighted: str | None = None, temporal_direct: bool = False) -> dict:
+                weighted: str | None = None, temporal_direct: bool = False,
+                chroma_deblock: bool = False) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
     and the ground-truth scene-cut frames.  coding="full" only: ``bframes`` codes
     B pictures (Main profile, POC type 0, composition offsets in the MP4),
     ``weighted`` = "explicit" (pred_weight_table in P and B slices) or
     "implicit" (weighted_bipred_idc 2), ``temporal_direct`` mixes temporal with
-    spatial direct prediction."""
+    spatial direct prediction.  coding="subset" only: ``chroma_deblock``
+    turns the deblocking filter on at QPY 3 with chroma_qp_index_offset 12 and
+    filter offsets +12, so only chroma edges filter (a stream the subset
+    kernels must refuse)."""
     p = _lib.SynthParams()
     p.width, p.height, p.fps_num, p.fps_den = width, height, fps, 1
     p.n_frames, p.seed = n_frames, seed
@@ -286,6 +290,10 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     p.coding = {"subset": 0, "full": 1}[coding]
     if constrained_intra:
         p.edge_cases |= 16
+    if chroma_deblock:
+        if coding != "subset":
+            raise ValueError("chroma_deblock is a subset-stream edge case")
+        p.edge_cases |= 512
     if bframes or weighted or temporal_direct:
         if coding != "full":
             raise ValueError("B pictures / weighted prediction need coding='full'")
