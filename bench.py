@@ -1,32 +1,50 @@
 """Benchmark: 720p frames/s decoded+scored per node (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload decode_score|score|transcode]
-                    [--config 720p-2h|720p-10min|1080p-2h|480p-60s] [--profile-dir DIR]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--config 720p-batch|720p-10min|720p-2h|1080p-2h|480p-60s]
+                    [--workload decode_score|score|transcode] [--extras all|none]
 
 One process per GPU (torch.distributed.run for N > 1; RANK/LOCAL_RANK/
 WORLD_SIZE from the env, rendezvous on 127.0.0.1).  Weak scaling: every rank
-processes its own synthetic video; after each step the ranks all-gather their
-per-video segment counts over RCCL (the only collective on this path; no pixel
-data crosses GPUs).  The default (N=1) workload is BASELINE config [2], the
-largest single-GPU configuration: a 2-h 720p video (216 000 frames at 30 fps),
-decoded in streamed two-ring windows.
+owns `videos_per_gpu` synthetic videos (video i on rank i mod N, BASELINE
+config [3]'s partition) and a step is one call of vtseg.batch.plan_batch over
+the whole batch: per local video probe + plan + device decode + score + scene
+cuts + boundary frames, then the two all-gathers of the batch (segment / cut
+counts and the padded boundary arrays; RCCL over xGMI with NCCL, gloo in the
+rehearsal), so every rank ends with the whole batch's segmentation.  No pixel
+data crosses GPUs.  The default workload at every N is config [3]'s per-GPU
+share, 4 x 10-min 720p (BASELINE config [1]) videos per GPU: N = 8 is exactly
+config [3] (32 videos), N = 1 is four config-[1] videos.  `--config 1080p-2h`
+is config [4] per GPU (one 2-h 1080p video per rank).
 
-A step = one pass of the hot path over one whole video with its input already
-resident in HBM:
-  decode_score : device H.264 subset decode (parse + reconstruct) + scoring
-  score        : scoring kernel only, on pre-decoded NV12 frames
-  transcode    : the 360p upload transcode
+A step's inputs are resident in HBM when the timed region starts: every local
+video's session (vts_open: demux, elementary-stream upload, schedule) is open
+before the warm-up, and only the per-frame work runs inside it.
+  decode_score : device H.264 decode (subset kernels for the synthetic streams)
+                 + scoring, through plan_batch
+  score        : scoring kernel only, on pre-decoded NV12 frames (one video)
+  transcode    : the 360p upload transcode (one video)
 Rank 0 prints ONE JSON line (contract in the task statement), including
   roofline     : the dominant kernel; `achieved`/`frac` on SURVEY 8(d)'s
                  algorithmic bytes per frame, kernel time = busy time (union of
                  dispatch intervals) per dispatch from a rocprofv3 kernel trace
                  of this same command (HIP-event value beside it), `traffic`
                  from rocprofv3 PMC passes; the decode-inclusive figure beside;
-  parity       : this run's scores / histograms / SADs, scene cuts and the
-                 planned segments' boundary frame indices against the C oracle
-                 over the whole video (bounded prefix per rank for N > 1);
+  parity       : every local video's scores / histograms / SADs, scene cuts,
+                 boundary frame indices and the gathered batch records against
+                 the C oracle (whole videos at N = 1; a bounded prefix per
+                 video for N > 1 unless --parity-frames all), and
+                 all_ranks_equal over the ranks;
   cpu_baseline : the oracle's decode + score on the host's cores (the parity
-                 pass, timed), N = 1 only.
+                 pass, timed), N = 1 only;
+  extras       : (N = 1, --extras all) `e2e`: file -> segment list through
+                 plan_batch with nothing resident (demux, upload, decode,
+                 score, results to the host); `long_video`: BASELINE config
+                 [2], one 2-h 720p video in streamed two-ring windows;
+                 `general`: the general decoder on a 10-min 720p full-syntax
+                 stream (B pictures, weighted prediction, deblocking) with
+                 per-kernel rooflines, the parse's issue rate and the
+                 stream's bits per frame.
 The rocprofv3 passes are child processes started before this process touches
 the GPU; --profile-dir keeps their summaries.
 """
@@ -42,6 +60,7 @@ import subprocess
 import sys
 import tempfile
 import time
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 import numpy as np
@@ -52,18 +71,34 @@ sys.path.insert(0, str(ROOT / "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 VALU_SAD_PEAK_TOPS = 256 * 4 * 32 * 4 * 2.4e9 / 1e12  # v_sad_u8 byte-SADs/s (MI355X_MICROARCH.md)
+CU_ISSUE_PEAK = 256 * 2.4e9  # instructions/s if every CU issued one per cycle
 
-# BASELINE.json configs runnable per GPU: name -> (width, height, frames, what)
+# BASELINE.json configs, per GPU: name -> (width, height, frames per video,
+# videos per GPU, what)
 CONFIGS = {
-    "720p-10min": (1280, 720, 18000, "BASELINE config [1]: 10-min 720p MP4, one per GPU"),
-    "720p-2h": (1280, 720, 216000, "BASELINE config [2]: 2-h 720p, streamed decode "
-                                   "(two-ring windows)"),
-    "1080p-2h": (1920, 1080, 216000, "BASELINE config [4] per GPU: 2-h 1080p, two-stream "
-                                     "decode/score overlap"),
-    "480p-60s": (640, 480, 1800, "BASELINE config [0] clip (60-s 480p) on the GPU path"),
+    "720p-batch": (1280, 720, 18000, 4,
+                   "BASELINE config [3] per-GPU share: 4 x 10-min 720p MP4 per GPU (config [3] = "
+                   "32 videos over 8 GPUs; at N GPUs 4N videos, video i on rank i mod N) through "
+                   "vtseg.batch.plan_batch"),
+    "720p-10min": (1280, 720, 18000, 1, "BASELINE config [1]: 10-min 720p MP4, one per GPU"),
+    "720p-2h": (1280, 720, 216000, 1, "BASELINE config [2]: 2-h 720p, streamed decode "
+                                      "(two-ring windows)"),
+    "1080p-2h": (1920, 1080, 216000, 1, "BASELINE config [4] per GPU: 2-h 1080p, one per GPU (8 "
+                                        "over 8 GPUs), two-stream decode/score overlap"),
+    "480p-60s": (640, 480, 1800, 1, "BASELINE config [0] clip (60-s 480p) on the GPU path"),
 }
 FPS = 30
 METRIC = "720p frames/sec decoded+scored per node; segment-index exact-match vs CPU"
+# the reference's default analyzer config (config/config.yaml:84-96)
+REF_CONFIG = {"analyzer": {"max_continuations": 3, "retry_times": 5,
+                           "long_video": {"enabled": True, "default_segment_seconds": 480,
+                                          "overlap_seconds": 20, "min_segment_seconds": 90,
+                                          "hard_max_api_calls": 50, "consolidate": True,
+                                          "duration_threshold_seconds": None}}}
+
+
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def algorithmic_bytes_per_frame(width: int, height: int, k: int) -> int:
@@ -129,55 +164,6 @@ def cpu_baseline_score(width, height, k, budget_s=10.0):
                       f"or_score_frames (scalar, 1 thread), {dt:.1f} s"}
 
 
-def cpu_baseline_decode_score(path, k, budget_s=15.0):
-    """The same decode + score on the host: the C oracle's H.264 subset
-    decoder (or_decode_samples) and scorer (or_score_frames), GOP-parallel on
-    a thread pool (ctypes releases the GIL), over a bounded GOP-aligned sample
-    of the benchmark video itself."""
-    import ctypes as C
-    from concurrent.futures import ThreadPoolExecutor
-
-    import oracle
-    m = oracle.read_mp4(path)
-    L = oracle.lib()
-    prm = oracle.H264Params()
-    sps, pps = m["sps"][0], m["pps"][0]
-    if L.or_parse_sps_pps(sps, len(sps), pps, len(pps), m["nal_length_size"], C.byref(prm)):
-        raise RuntimeError("oracle SPS/PPS")
-    W = prm.mb_width * 16 - prm.crop_right
-    H = prm.mb_height * 16 - prm.crop_bottom
-    data = np.frombuffer(m["data"], np.uint8)
-    offs = np.asarray(m["offsets"], np.int64)
-    sizes = np.asarray(m["sizes"], np.int64)
-    nls = m["nal_length_size"]
-    idr = [i for i in range(len(offs)) if data[offs[i] + nls] & 0x1F == 5]
-    gops = [(a, b) for a, b in zip(idr, idr[1:] + [len(offs)])]
-
-    def work(g):
-        a, b = g
-        n = b - a
-        out = np.empty((n, H * 3 // 2, W), np.uint8)
-        bad = C.c_int64(-1)
-        if L.or_decode_samples(C.byref(prm), data.ctypes.data, offs[a:b].ctypes.data,
-                               sizes[a:b].ctypes.data, n, out.ctypes.data, C.byref(bad)):
-            raise RuntimeError("oracle decode")
-        oracle.score_frames(out.reshape(-1), W * H * 3 // 2, n, W, H, W, H, k, want_rgb=True)
-        return n
-
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    t0 = time.perf_counter()
-    per_gop = work(gops[0]) and (time.perf_counter() - t0)
-    n_gops = max(1, min(len(gops), int(budget_s * threads / max(per_gop, 1e-6))))
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        frames = sum(ex.map(work, gops[:n_gops]))
-    dt = time.perf_counter() - t0
-    return {"value": round(frames / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"first {n_gops} GOPs ({frames} frames {W}x{H}) of the benchmark video, "
-                      f"decoded by oracle/vtseg_oracle.c or_decode_samples + scored by "
-                      f"or_score_frames, GOP-parallel on {threads} threads, {dt:.1f} s"}
-
-
 def cpu_baseline_transcode(path, k, budget_s=15.0):
     """The same transcode on the host, 1 thread: the C oracle decodes and
     scores the first frames of the benchmark video, then or_transcode
@@ -226,16 +212,18 @@ def _busy(intervals: list[tuple[int, int]]) -> tuple[float, float]:
     return tot + ce - cs, sum(e - b for b, e in iv)
 
 
-def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None) -> dict:
+def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None,
+                   passes=("trace", "FETCH_SIZE", "WRITE_SIZE"), timeout: int = 240) -> dict:
     """rocprofv3 child runs of this same benchmark (1 timed step each):
-      * --kernel-trace --stats: per kernel, dispatches, mean dispatch duration
-        and busy time (union of the dispatch intervals) per dispatch; with two
-        GOP groups two reconstruct dispatches overlap, so the mean duration
-        overstates each one's share of the wall time and the busy time is the
-        kernel time per launch;
-      * --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes: 3 + 2 TCC
-        slots > 4): HBM bytes per dispatch = 2 x FETCH_SIZE (gfx950 tallies
-        wide coalesced reads at half their bytes) + WRITE_SIZE, both KiB
+      * "trace" = --kernel-trace --stats: per kernel, dispatches, mean dispatch
+        duration and busy time (union of the dispatch intervals) per dispatch;
+        with two GOP groups two reconstruct dispatches overlap, so the mean
+        duration overstates each one's share of the wall time and the busy
+        time is the kernel time per launch;
+      * a counter name (or a space-separated group of SQ counters) = --pmc
+        pass; FETCH_SIZE and WRITE_SIZE need separate passes (3 + 2 TCC slots
+        > 4): HBM bytes per dispatch = 2 x FETCH_SIZE (gfx950 tallies wide
+        coalesced reads at half their bytes) + WRITE_SIZE, both KiB
         (MI355X_MICROARCH.md, HBM section).
     Started before this process initialises the GPU (no exec from a
     GPU-initialised process), each under its own time limit."""
@@ -245,18 +233,21 @@ def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None) -> dic
     res: dict = {}
     env = dict(os.environ, TMPDIR="/tmp")
     child = [sys.executable, str(Path(__file__).resolve()), *argv, "--steps", "1", "--warmup", "1",
-             "--no-cpu-baseline", "--no-pmc", "--no-parity"]
-    for what in ("trace", "FETCH_SIZE", "WRITE_SIZE"):
-        d = out_dir / what
+             "--no-cpu-baseline", "--no-pmc", "--no-parity", "--extras", "none"]
+    for pi, what in enumerate(passes):
+        d = out_dir / f"p{pi}"
+        counters = what.split()
         opts = (["--kernel-trace", "--stats"] if what == "trace" else
-                ["--kernel-trace", "--pmc", what])
+                ["--kernel-trace", "--pmc", *counters])
         cmd = [prof, *opts, "--output-format", "csv", "-d", str(d), "-o", "run", "--", *child]
+        t0 = time.perf_counter()
         try:
             proc = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True,
-                                  timeout=240)
+                                  timeout=timeout)
         except subprocess.TimeoutExpired:
             res["error"] = f"{what} pass timed out"
             continue
+        log(f"profile pass {what!r}: rc={proc.returncode}, {time.perf_counter() - t0:.1f} s")
         if proc.returncode != 0:
             res["error"] = f"{what} pass rc={proc.returncode}: {proc.stderr[-300:]}"
             continue
@@ -271,13 +262,15 @@ def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None) -> dic
                 union, total = _busy(v)
                 res.setdefault(k, {}).update(dispatches_traced=len(v),
                                              busy_ns_per_dispatch=union / len(v),
+                                             busy_ns_total=union,
                                              mean_dispatch_ns=total / len(v))
             if keep_dir is not None:
                 keep_dir.mkdir(parents=True, exist_ok=True)
                 for f in d.rglob("*kernel_stats.csv"):
                     shutil.copy(f, keep_dir / "kernel_stats.csv")
-                rows = sorted(((k, v) for k, v in res.items() if "busy_ns_per_dispatch" in v),
-                              key=lambda kv: -kv[1]["busy_ns_per_dispatch"] * kv[1]["dispatches_traced"])
+                rows = sorted(((k, v) for k, v in res.items()
+                               if isinstance(v, dict) and "busy_ns_per_dispatch" in v),
+                              key=lambda kv: -kv[1]["busy_ns_total"])
                 (keep_dir / "kernel_busy.txt").write_text("".join(
                     f"{k}: {v['dispatches_traced']} dispatches, busy (union of intervals) "
                     f"{v['busy_ns_per_dispatch'] / 1e3:.2f} us per dispatch, mean dispatch "
@@ -287,30 +280,55 @@ def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None) -> dic
         for f in d.rglob("*counter_collection.csv"):
             with open(f) as fh:
                 for r in csv.DictReader(fh):
-                    if r["Counter_Name"] != what:
+                    if r["Counter_Name"] not in counters:
                         continue
-                    acc.setdefault(_kernel_short(r["Kernel_Name"]), []).append(
-                        float(r["Counter_Value"]))
-        for k, v in acc.items():
-            res.setdefault(k, {})[what] = sum(v) / len(v)
-            res[k]["dispatches"] = len(v)
+                    acc.setdefault((_kernel_short(r["Kernel_Name"]), r["Counter_Name"]),
+                                   []).append(float(r["Counter_Value"]))
+        for (k, cn), v in acc.items():
+            row = res.setdefault(k, {})
+            row[cn] = sum(v) / len(v)
+            row[cn + "_total"] = sum(v)
+            row["dispatches"] = len(v)
     for k, row in res.items():
         if isinstance(row, dict) and "FETCH_SIZE" in row and "WRITE_SIZE" in row:
             row["hbm_bytes"] = (2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024
     if keep_dir is not None:
+        keep_dir.mkdir(parents=True, exist_ok=True)
         (keep_dir / "profile_passes.json").write_text(json.dumps(res, indent=1))
     return res
 
 
-def parity_check(scorer, path, k: int, duration_s: float, segs, threads: int,
-                 max_frames: int | None, decoder: str = "subset") -> tuple[dict, dict]:
+def synth_videos(jobs: list[tuple[Path, int]], width: int, height: int, frames: int,
+                 coding: str = "subset", bframes: bool = False) -> list[dict]:
+    """Write the synthetic H.264/MP4 inputs (vts_synth_write; ctypes releases
+    the GIL, so the videos are written in parallel)."""
+    from vtseg import scene
+
+    def one(job):
+        path, seed = job
+        if coding == "full":
+            # x264-like structure: one slice per picture; with bframes B
+            # reference pictures, spatial direct, implicit weighted bi-prediction
+            extra = dict(bframes=True, weighted="implicit") if bframes else {}
+            return scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=frames,
+                                     seed=seed, coding="full", slices_per_row=0, max_motion=4,
+                                     **extra)
+        return scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=frames,
+                                 seed=seed)
+
+    with ThreadPoolExecutor(max(1, len(jobs))) as ex:
+        return list(ex.map(one, jobs))
+
+
+def parity_check(scorer, path, k: int, segs, threads: int, max_frames: int | None,
+                 decoder: str = "subset") -> tuple[dict, dict]:
     """This run's device results against the C oracle (oracle.decode_score_gops,
     GOP-parallel on `threads` host threads): every frame's fp32 score (exact;
     north_star allows |d| <= 1e-4), 256-bin histogram and SAD, the scene cuts,
     and the boundary frame index of every planned segment time (start, end,
     effective start/end of each segment of the reference's plan,
     src/utils/video_segmenter.py:42-83) in exact rationals.  Returns (parity,
-    cpu timing of the oracle pass)."""
+    the oracle pass: timing + its pts / cuts for the batch-record check)."""
     import oracle
     res = scorer.score()                     # a full decode + score, results to the host
     cuts = scorer.scene_cuts()
@@ -331,15 +349,264 @@ def parity_check(scorer, path, k: int, duration_s: float, segs, threads: int,
               "scene_cuts_equal": [c for c in cuts if c < n] == ref_cuts,
               "segment_times": len(times),
               "boundary_frames_equal": list(got_idx) == list(want_idx),
-              "pts_equal": res.pts[:n].tolist() == ref["pts"],
-              "oracle": ("oracle/h264_full_oracle.c fo_decode" if decoder == "full" else
-                         "oracle/vtseg_oracle.c or_decode_samples") +
-                        f" + or_score_frames (GOP-parallel, {threads} threads)"}
+              "pts_equal": res.pts[:n].tolist() == ref["pts"]}
     parity["all_equal"] = all(parity[x] for x in ("scores_equal", "hist_equal", "sad_equal",
                                                   "scene_cuts_equal", "boundary_frames_equal",
                                                   "pts_equal"))
     return parity, {"frames": n, "seconds": ref["seconds"], "threads": threads,
-                    "gops": ref["gops"], "width": ref["width"], "height": ref["height"]}
+                    "gops": ref["gops"], "width": ref["width"], "height": ref["height"],
+                    "pts": ref["pts"], "timescale": ref["timescale"], "cuts": ref_cuts}
+
+
+def batch_record_check(item, segs, ref: dict, full: bool) -> bool:
+    """The gathered BatchItem of a local video against the oracle: segment
+    count, every planned segment's [start, end) frame window, the scene-cut
+    frames and their times (prefix-restricted when only a prefix was checked)."""
+    import oracle
+    n = len(ref["pts"])
+    if item.n_segments != len(segs) or item.score_failed:
+        return False
+    times = [t for sg in segs for t in (sg.start, sg.end)]
+    want = oracle.boundary_frames(ref["pts"], ref["timescale"], times) if times else []
+    got = [x for pair in item.segment_frames for x in pair]
+    cut_t = [float(ref["pts"][c]) / ref["timescale"] for c in ref["cuts"]]
+    if full:
+        return got == want and list(item.cut_frames) == ref["cuts"] and \
+            list(item.cut_times) == cut_t and item.n_cuts == len(ref["cuts"])
+    keep = [i for i, t in enumerate(times) if t * FPS < n]
+    return [got[i] for i in keep] == [want[i] for i in keep] and \
+        [c for c in item.cut_frames if c < n] == ref["cuts"]
+
+
+def kernel_stats_from(prof: dict | None, name: str) -> dict | None:
+    row = (prof or {}).get(name)
+    return row if isinstance(row, dict) else None
+
+
+def recon_kernel_name(scorer, k: int) -> str:
+    tb = scorer.level_blocks()[0]
+    if scorer.fused():
+        return ("h264_recon_score_tb" if tb else
+                "h264_recon_score6b" if k == 6 else "h264_recon_score<%d>" % k)
+    return "score_runs<%d>" % k
+
+
+def roofline_decode_score(scorers, prof: dict | None, width: int, height: int, k: int,
+                          frames_per_video: int) -> dict:
+    """Roofline of the dominant kernel over the local videos' sessions: the
+    reconstruct+score kernel's time per launch from HIP events on its stream
+    (mean of 3 runs per session), replaced by the rocprofv3 trace's busy time
+    per dispatch when the trace pass ran."""
+    s0 = scorers[0]
+    rec, sco, launches = [], [], []
+    for v in scorers:
+        for _ in range(3):
+            v.run()
+            t = v.timings()
+            rec.append(t["reconstruct_ms"])
+            sco.append(t["score_ms"])
+        launches.append(v.level_blocks()[0] or v.recon_launches())
+    tb_launches, tb_chains = s0.level_blocks()
+    n_launch = int(np.mean(launches))
+    kname = recon_kernel_name(s0, k)
+    F = frames_per_video
+    if s0.fused():
+        kern_ms = float(np.mean(rec)) / n_launch
+        frames_per_launch = F / n_launch
+    else:
+        n_score = max(1, s0.windows())
+        kern_ms = float(np.mean(sco)) / n_score
+        frames_per_launch = F / n_score
+    kern_ms_events = kern_ms
+    kern_basis = "HIP events on the kernel's stream"
+    prow = kernel_stats_from(prof, kname)
+    if prow and "busy_ns_per_dispatch" in prow:
+        kern_ms = prow["busy_ns_per_dispatch"] / 1e6
+        kern_basis = (f"rocprofv3 --kernel-trace of this command: busy time (union of "
+                      f"{prow['dispatches_traced']} dispatch intervals) per dispatch; mean "
+                      f"dispatch duration {prow['mean_dispatch_ns'] / 1e3:.2f} us")
+    alg_bpf = algorithmic_bytes_per_frame(width, height, k)
+    if s0.fused() and tb_launches:
+        bytes_per_frame = tb_bytes_per_launch(width, height, k, F, tb_chains, n_launch) / frames_per_launch
+    elif s0.fused():
+        bytes_per_frame = fused_bytes_per_frame(width, height, k)
+    else:
+        bytes_per_frame = alg_bpf
+    achieved = alg_bpf * frames_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_note = None, None
+    if prof is not None:
+        if prow and "hbm_bytes" in prow:
+            traffic = round(prow["hbm_bytes"])
+            traffic_note = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (2xFETCH+WRITE), "
+                            f"mean of {prow['dispatches']} dispatches; "
+                            f"{traffic / (alg_bpf * frames_per_launch):.3f}x SURVEY 8(d) bytes, "
+                            f"{traffic / (bytes_per_frame * frames_per_launch):.3f}x the "
+                            f"decode-inclusive bytes")
+        else:
+            traffic_note = prof.get("error", f"no counters for {kname}")
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_unit": "bytes/launch", "traffic_source": traffic_note,
+            "kernel": kname, "kernel_ms": round(kern_ms, 5), "kernel_ms_basis": kern_basis,
+            "kernel_ms_hip_events": round(kern_ms_events, 5),
+            "bytes_per_frame": alg_bpf,
+            "bytes_basis": "SURVEY 8(d): 1.5*W*H NV12 read + 3*w*h RGB + 2*w*h thumbnail "
+                           "luma write/read + 1024 histogram + 4 score",
+            "frames_per_launch": round(frames_per_launch, 1)}
+    if bytes_per_frame != alg_bpf:
+        ach_d = bytes_per_frame * frames_per_launch / (kern_ms * 1e-3) / 1e9
+        roof["decode_inclusive"] = {
+            "bytes_per_frame": round(bytes_per_frame, 1), "achieved": round(ach_d, 1),
+            "frac": round(ach_d / HBM_PEAK_GBS, 4),
+            "basis": "the fused decode+score kernel's own bytes: NV12-sized reference/I_PCM "
+                     "read + NV12 frame write + RGB + thumbnail luma write + predecessor "
+                     "read + histogram + SAD"}
+    return roof
+
+
+# --------------------------------------------------------------- extras (N = 1)
+
+GENERAL_PMC = ("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM "
+               "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH")
+
+
+def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames: int,
+                             mbs_per_frame: int) -> dict:
+    """Per-kernel rooflines of the general decoder from a rocprofv3 kernel
+    trace (busy time = union of each kernel's dispatch intervals) and an SQ
+    instruction-count pass.  Algorithmic bytes per picture (display-size NV12
+    = 1.5*W*H):
+      h264_inter_full   reference read + NV12 write          3.0*W*H
+      h264_intra_full   NV12 write (intra pictures' share)   1.5*W*H
+      h264_deblock_full NV12 read + write                    3.0*W*H
+      score_runs        SURVEY 8(d) bytes                     1.5*W*H + 5*w*h + 1028
+    (intra and inter both count the whole picture's write; their sum
+    overstates a picture that mixes them, so the sum is not reported).
+    h264_parse_full is serial bit parsing: its bound is instruction issue,
+    reported as instructions / (256 CUs x 2.4 GHz x busy time)."""
+    nv12 = 1.5 * width * height
+    w, h = width // k, height // k
+    per_pic = {"h264_inter_full": 2 * nv12, "h264_intra_full": nv12,
+               "h264_deblock_full": 2 * nv12, f"score_runs<{k}>": nv12 + 5 * w * h + 1028}
+    out = {}
+    for name, b in per_pic.items():
+        row = prof.get(name)
+        if not isinstance(row, dict) or "busy_ns_total" not in row:
+            continue
+        t = row["busy_ns_total"] * 1e-9
+        ach = b * frames / t / 1e9
+        out[name] = {"bound": "hbm", "busy_ms": round(t * 1e3, 2),
+                     "dispatches": row["dispatches_traced"], "bytes_per_picture": round(b),
+                     "achieved": round(ach, 1), "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4)}
+    row = prof.get("h264_parse_full")
+    if isinstance(row, dict) and "busy_ns_total" in row:
+        t = row["busy_ns_total"] * 1e-9
+        rec = {"bound": "issue", "busy_ms": round(t * 1e3, 2),
+               "dispatches": row["dispatches_traced"]}
+        kinds = ["SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM",
+                 "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_BRANCH"]
+        if all(kk + "_total" in row for kk in kinds):
+            insts = sum(row[kk + "_total"] for kk in kinds)
+            mbs = frames * mbs_per_frame
+            rec.update({"instructions": insts, "instructions_per_mb": round(insts / mbs, 1),
+                        "salu_per_mb": round(row["SQ_INSTS_SALU_total"] / mbs, 1),
+                        "valu_per_mb": round(row["SQ_INSTS_VALU_total"] / mbs, 1),
+                        "achieved": round(insts / t / 1e9, 2), "unit": "G instructions/s",
+                        "peak": CU_ISSUE_PEAK / 1e9,
+                        "frac": round(insts / t / CU_ISSUE_PEAK, 4),
+                        "peak_basis": "one instruction per CU per cycle: 256 CUs x 2.4 GHz "
+                                      "(the scalar unit a CU's waves share issues at most one "
+                                      "SALU instruction per cycle)"})
+        out["h264_parse_full"] = rec
+    return out
+
+
+def run_single(path: Path, *, gpu: int, k: int, steps: int, threads: int, label: str,
+               decoder: str = "auto", prof: dict | None = None, parity: bool = True) -> dict:
+    """One video through its session: `steps` timed vts_run calls (inputs
+    resident), stage times, the dominant kernel's roofline and parity over
+    every frame against the oracle."""
+    import torch
+    from vtseg import budget_planner as bp
+    from vtseg import scene
+    from vtseg import video_segmenter as vs
+    t0 = time.perf_counter()
+    v = scene.VideoScorer(path, device=gpu, decoder=decoder)
+    open_s = time.perf_counter() - t0
+    try:
+        F = v.n_frames
+        W, H = int(v.info.width), int(v.info.height)
+        v.run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            v.run()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        rec = {"label": label, "frames": F, "width": W, "height": H, "steps": steps,
+               "value": round(F * steps / el, 1), "unit": "frames/s",
+               "ms_per_step": round(el / steps * 1e3, 3), "open_s": round(open_s, 3),
+               "decoder": "general" if v.general() else "subset",
+               "stage_ms": v.timings(), "recon_launches": v.recon_launches(),
+               "windows": v.windows(),
+               "bits_per_frame": round(Path(path).stat().st_size * 8 / F, 1)}
+        if not v.general():
+            rec["roofline"] = roofline_decode_score([v], prof, W, H, k, F)
+        if parity:
+            duration = float(v.info.duration)
+            plan = bp.plan_segments_with_budget(duration, REF_CONFIG, 0)
+            segs = vs.plan_segments(duration, plan.segment_duration, plan.overlap)
+            par, ct = parity_check(v, path, k, segs, threads, None,
+                                   "full" if v.general() else "subset")
+            par["oracle"] = ("oracle/h264_full_oracle.c fo_decode" if v.general() else
+                             "oracle/vtseg_oracle.c or_decode_samples") + \
+                f" + or_score_frames (GOP-parallel, {threads} threads)"
+            rec["parity"] = par
+            rec["cpu_oracle_frames_per_s"] = round(ct["frames"] / ct["seconds"], 2)
+        return rec
+    finally:
+        v.close()
+
+
+def e2e_record(paths: list[Path], gpu: int) -> dict:
+    """File -> segment list with nothing resident: plan_batch over the batch's
+    files (per video: native moov probe, plan, vts_open = MP4 demux +
+    elementary-stream upload over PCIe + schedule, device decode + score,
+    scores to the host, scene cuts, boundary frames, close), then the same
+    stages timed one by one on the first video."""
+    import torch
+    from vtseg import batch, scene
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    items = batch.plan_batch([str(p) for p in paths], REF_CONFIG, score=True, device=gpu)
+    dt = time.perf_counter() - t0
+    frames = 0
+    stages = {}
+    for p in paths[:1]:
+        t0 = time.perf_counter()
+        v = scene.VideoScorer(p, device=gpu)
+        t1 = time.perf_counter()
+        v.run()
+        t2 = time.perf_counter()
+        cuts = v.scene_cuts()
+        v.frame_pts()
+        v.boundary_frames([0.0, float(v.info.duration)])
+        t3 = time.perf_counter()
+        v.close()
+        stages = {"open_ms": round((t1 - t0) * 1e3, 1), "decode_score_ms": round((t2 - t1) * 1e3, 1),
+                  "results_ms": round((t3 - t2) * 1e3, 2), "scene_cuts": len(cuts),
+                  "input_bytes": Path(p).stat().st_size,
+                  "upload_inclusive_GBps": round(Path(p).stat().st_size / (t1 - t0) / 1e9, 2)}
+    for it in items:
+        frames += int(round(it.duration * FPS))
+    return {"videos": len(paths), "frames": frames, "seconds": round(dt, 3),
+            "value": round(frames / dt, 1), "unit": "frames/s",
+            "segments": [it.n_segments for it in items], "cuts": [it.n_cuts for it in items],
+            "first_video_stages": stages,
+            "includes": "per video: moov probe, plan, vts_open (host MP4 demux, elementary-stream "
+                        "upload H2D, decode schedule), decode + score, scores D2H, scene cuts, "
+                        "boundary frames, close; files in the page cache (just written)"}
 
 
 def main() -> None:
@@ -348,9 +615,10 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="decode_score", choices=["decode_score", "score", "transcode"])
-    ap.add_argument("--config", default="720p-2h", choices=sorted(CONFIGS),
-                    help="BASELINE configuration (per GPU); the N=1 headline is 720p-2h, the "
-                         "largest single-GPU config")
+    ap.add_argument("--config", default="720p-batch", choices=sorted(CONFIGS),
+                    help="BASELINE configuration per GPU; default = config [3]'s per-GPU share "
+                         "(4 x 10-min 720p) at every N")
+    ap.add_argument("--videos-per-gpu", type=int, default=0, help="override the config's")
     ap.add_argument("--bframes", action="store_true",
                     help="with --coding full: B pictures (x264-like: B references, spatial direct, "
                          "implicit weighted bi-prediction, reordered presentation)")
@@ -360,9 +628,15 @@ def main() -> None:
                          "residuals, quarter-sample partitions, 3 references, deblocking on (the "
                          "general decoder)")
     ap.add_argument("--video", default=None,
-                    help="use this MP4 instead of synthesizing one (the rocprofv3 child passes)")
+                    help="comma-separated MP4s (this rank's videos) instead of synthesizing them "
+                         "(the rocprofv3 child passes)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle parity check of the run's results")
+    ap.add_argument("--parity-frames", default="auto",
+                    help="frames per video the parity pass checks: auto (all at N=1, a 3000-frame "
+                         "prefix at N>1), all, or a number")
+    ap.add_argument("--extras", default="all", choices=["all", "none"],
+                    help="N=1: the e2e / long_video / general sub-records")
     ap.add_argument("--profile-dir", default=None,
                     help="keep the rocprofv3 kernel stats / busy-time summary here")
     ap.add_argument("--frames", type=int, default=None, help="override the config's frames")
@@ -381,18 +655,27 @@ def main() -> None:
                     help="GOP levels per reconstruct launch (0 auto = level-blocked kernel where it "
                          "applies, 1 = one launch per level)")
     ap.add_argument("--no-pmc", action="store_true",
-                    help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
+                    help="skip the rocprofv3 passes (kernel trace and --pmc) of the headline")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    cw, ch, cf, cdesc = CONFIGS[args.config]
+    cw, ch, cf, cvpg, cdesc = CONFIGS[args.config]
     width = args.width or cw
     height = args.height or ch
     F = args.frames or cf
+    vpg = args.videos_per_gpu or cvpg
+    if args.workload != "decode_score":
+        vpg = 1
+    n_videos = vpg * world
+    local_idx = list(range(rank, n_videos, world))
     k = 4 if height <= 720 else 6
     w, h = width // k, height // k
     stride = width * height * 3 // 2
+    aff = len(os.sched_getaffinity(0))
+    threads = max(1, min(16, aff // max(1, world)))
+    extras = args.extras == "all" and world == 1 and args.workload == "decode_score" and \
+        not args.no_parity
 
     # torch first: libvtseg.so must bind to the HIP runtime torch loads (loading
     # libvtseg first hides the device from it); importing torch initialises
@@ -401,41 +684,59 @@ def main() -> None:
     import torch.distributed as dist
     from vtseg import scene
 
-    # ------------------------------------------------ input video (host only)
-    tmpdir = tempfile.mkdtemp(prefix="vtseg_bench_")
-    path = None
+    # ------------------------------------------------ input videos (host only)
+    tmpdir = Path(tempfile.mkdtemp(prefix="vtseg_bench_"))
+    all_paths = [tmpdir / f"synth_v{i}.mp4" for i in range(n_videos)]
     if args.workload != "score":
         if args.video:
-            path = Path(args.video)
+            given = [Path(p) for p in args.video.split(",")]
+            if len(given) != len(local_idx):
+                raise SystemExit(f"--video: {len(given)} files for {len(local_idx)} local videos")
+            for i, p in zip(local_idx, given):
+                all_paths[i] = p
         else:
-            path = Path(tmpdir) / f"synth_rank{rank}.mp4"
-            if args.coding == "full":
-                # --bframes: x264-like structure (B reference pictures, spatial
-                # direct, implicit weighted bi-prediction, composition offsets)
-                extra = dict(bframes=True, weighted="implicit") if args.bframes else {}
-                scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
-                                  seed=0x5EED + rank, coding="full", slices_per_row=0,
-                                  max_motion=4, **extra)
-            else:
-                scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=F,
-                                  seed=0x5EED + rank)
+            t0 = time.perf_counter()
+            synth_videos([(all_paths[i], 0x5EED + i) for i in local_idx], width, height, F,
+                         args.coding, args.bframes)
+            log(f"rank {rank}: wrote {len(local_idx)} synthetic videos in {time.perf_counter() - t0:.1f} s")
+    local_paths = [all_paths[i] for i in local_idx]
 
-    prof = None
+    # extras' inputs, written before the profile passes (which read them)
+    gen_path = long_path = None
+    if extras:
+        t0 = time.perf_counter()
+        gen_path = tmpdir / "general_720p_10min.mp4"
+        long_path = tmpdir / "long_720p_2h.mp4"
+        with ThreadPoolExecutor(2) as ex:
+            fa = ex.submit(synth_videos, [(gen_path, 0x5EED)], 1280, 720, 18000, "full", True)
+            fb = ex.submit(synth_videos, [(long_path, 0x5EED)], 1280, 720, 216000)
+            fa.result()
+            fb.result()
+        log(f"extras inputs written in {time.perf_counter() - t0:.1f} s")
+
+    prof = gprof = None
     if world == 1 and not args.no_pmc and args.workload != "transcode":
         # before anything touches the GPU: the passes are child processes
         child_argv = ["--workload", args.workload, "--config", args.config, "--coding", args.coding,
                       *(["--bframes"] if args.bframes else []),
+                      "--videos-per-gpu", str(vpg),
                       "--gops-per-launch", str(args.gops_per_launch),
                       "--parse-chunks", str(args.parse_chunks),
                       "--level-block", str(args.level_block)]
-        if path is not None:
-            child_argv += ["--video", str(path)]
+        if args.workload != "score":
+            child_argv += ["--video", ",".join(str(p) for p in local_paths)]
         for opt in ("frames", "width", "height"):
             if getattr(args, opt) is not None:
                 child_argv += [f"--{opt}", str(getattr(args, opt))]
         pdir = Path(tempfile.mkdtemp(prefix="vtseg_prof_", dir="/tmp"))
         prof = profile_passes(child_argv, pdir,
                               Path(args.profile_dir) if args.profile_dir else None)
+        if extras:
+            gargv = ["--config", "720p-10min", "--coding", "full", "--bframes",
+                     "--video", str(gen_path)]
+            gprof = profile_passes(gargv, pdir / "general",
+                                   Path(args.profile_dir) / "general" if args.profile_dir else None,
+                                   passes=("trace", GENERAL_PMC))
         shutil.rmtree(pdir, ignore_errors=True)
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -452,59 +753,50 @@ def main() -> None:
     torch.cuda.set_device(device)
     coll_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
 
+    from vtseg import batch
     from vtseg import budget_planner as bp
     from vtseg import video_segmenter as vs
 
     # ---------------------------------------------------------------- inputs
-    scorer = None
+    scorers: dict = {}
+    outs: dict = {}
     if args.workload == "score":
         rng = np.random.default_rng(100 + rank)
         pool = torch.from_numpy(smooth_frames_host(rng, 64, width, height)).to(device)
         reps = (F + 63) // 64
         nv12 = pool.reshape(64, -1).repeat(reps, 1)[:F].contiguous().reshape(-1)
         del pool
-        outs = {}
 
         def step():
             outs["r"] = scene.score_nv12(nv12, width=width, height=height, pitch=width,
                                          uv_row_offset=height, frame_stride=stride,
                                          n_frames=F, k=k, out=outs.get("r"),
                                          workspace=outs.get("r", {}).get("_workspace"))
-        duration_s = F / FPS
+        durations = [F / FPS]
     else:
-        scorer = scene.VideoScorer(path, device=gpu, gops_per_launch=args.gops_per_launch,
-                                   parse_chunks=args.parse_chunks, level_block=args.level_block,
-                                   window_frames=args.window_frames)
-        duration_s = float(scorer.info.duration)
-        F = scorer.n_frames
+        t0 = time.perf_counter()
+        for i in local_idx:
+            scorers[i] = scene.VideoScorer(all_paths[i], device=gpu,
+                                           gops_per_launch=args.gops_per_launch,
+                                           parse_chunks=args.parse_chunks,
+                                           level_block=args.level_block,
+                                           window_frames=args.window_frames)
+        log(f"rank {rank}: opened {len(scorers)} sessions in {time.perf_counter() - t0:.1f} s")
+        F = scorers[local_idx[0]].n_frames
+        durations = [float(scorers[i].info.duration) for i in local_idx]
 
         if args.workload == "transcode":
-            out_path = Path(tmpdir) / f"small_rank{rank}.mp4"
-            outs = {}
+            out_path = tmpdir / f"small_rank{rank}.mp4"
+            v0 = scorers[local_idx[0]]
 
             def step():
-                outs["facts"] = scorer.transcode(out_path)
+                outs["facts"] = v0.transcode(out_path)
         else:
+            str_paths = [str(p) for p in all_paths]
+
             def step():
-                scorer.run()
-
-    # per-video segment plan under the reference's default config (config.yaml)
-    cfg = {"analyzer": {"max_continuations": 3, "retry_times": 5,
-                        "long_video": {"enabled": True, "default_segment_seconds": 480,
-                                       "overlap_seconds": 20, "min_segment_seconds": 90,
-                                       "hard_max_api_calls": 50, "consolidate": True,
-                                       "duration_threshold_seconds": None}}}
-    plan = bp.plan_segments_with_budget(duration_s, cfg, 0)
-    segs = vs.plan_segments(duration_s, plan.segment_duration, plan.overlap)
-    n_segments = len(segs)
-    counts_local = torch.tensor([n_segments], dtype=torch.int32, device=coll_dev)
-    counts_all = torch.zeros(world, dtype=torch.int32, device=coll_dev)
-
-    def gather_counts():
-        if world > 1:
-            dist.all_gather_into_tensor(counts_all, counts_local)
-        else:
-            counts_all.copy_(counts_local)
+                outs["items"] = batch.plan_batch(str_paths, REF_CONFIG, score=True,
+                                                 sessions=scorers)
 
     def barrier():
         if world > 1:
@@ -513,14 +805,12 @@ def main() -> None:
     # ---------------------------------------------------------------- timing
     for _ in range(args.warmup):
         step()
-        gather_counts()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        gather_counts()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -530,12 +820,13 @@ def main() -> None:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     ms_per_step = elapsed / args.steps * 1e3
-    total_frames = F * world * args.steps
+    total_frames = F * n_videos * args.steps
     value = total_frames / elapsed
+    log(f"rank {rank}: {args.steps} steps in {elapsed:.3f} s -> {value:.0f} frames/s")
 
     # ------------------------------------------- roofline (dominant kernel)
     roof = None
-    tb_launches, tb_chains = 0, 0
+    sl = [scorers[i] for i in local_idx] if scorers else []
     if args.workload == "score":
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 5
@@ -545,7 +836,13 @@ def main() -> None:
         ev1.record()
         torch.cuda.synchronize()
         kern_ms = ev0.elapsed_time(ev1) / reps
-        kname = "score_runs<4>"
+        alg_bpf = algorithmic_bytes_per_frame(width, height, k)
+        achieved = alg_bpf * F / (kern_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "score_runs<%d>" % k, "kernel_ms": round(kern_ms, 5),
+                "kernel_ms_basis": "torch events on the current stream (score_nv12 enqueues there)",
+                "bytes_per_frame": alg_bpf, "frames_per_launch": F}
     elif args.workload == "transcode":
         # dominant kernel: enc_search<8> (VALU: v_sad_u8, 4 byte-SADs per lane-instruction)
         facts = outs["facts"]
@@ -556,138 +853,125 @@ def main() -> None:
         n_launch = max(1, min(250, F) - 1)
         sad_ops = p_frames * nmb * (2 * R + 1) ** 2 * 256
         kern_ms = facts["search_ms"] / n_launch
-        kname = "enc_search<8>"
-    else:
-        times = []
-        for _ in range(3):
-            scorer.run()
-            times.append(scorer.timings())
-        tb_launches, tb_chains = scorer.level_blocks()
-        n_launch = tb_launches or scorer.recon_launches()
-        fused = scorer.fused()
-        rec_ms = float(np.mean([t["reconstruct_ms"] for t in times])) / n_launch
-        if fused:
-            # dominant kernel = h264_recon_score (decode + score in one pass)
-            kern_ms = rec_ms
-            kname = ("h264_recon_score_tb" if tb_launches else
-                     "h264_recon_score6b" if k == 6 else "h264_recon_score<%d>" % k)
-        else:
-            # one score_runs launch per window: per-launch time and frames
-            n_score = max(1, scorer.windows())
-            kern_ms = float(np.mean([t["score_ms"] for t in times])) / n_score
-            kname = "score_runs<%d>" % k
-    kern_ms_events = kern_ms
-    kern_basis = "HIP events on the kernel's stream"
-    prow = (prof or {}).get(kname) if isinstance((prof or {}).get(kname), dict) else None
-    if args.workload == "decode_score" and prow and "busy_ns_per_dispatch" in prow:
-        # the rocprofv3 kernel trace of this same command: union of the
-        # dispatch intervals per dispatch (two GOP groups overlap)
-        kern_ms = prow["busy_ns_per_dispatch"] / 1e6
-        kern_basis = (f"rocprofv3 --kernel-trace of this command: busy time (union of "
-                      f"{prow['dispatches_traced']} dispatch intervals) per dispatch; mean "
-                      f"dispatch duration {prow['mean_dispatch_ns'] / 1e3:.2f} us")
-    alg_bpf = algorithmic_bytes_per_frame(width, height, k)  # SURVEY 8(d)
-    if args.workload == "transcode":
-        bytes_per_frame = None
-        frames_per_launch = p_frames / n_launch
-    elif scorer is not None and scorer.fused() and tb_launches:
-        frames_per_launch = F / n_launch
-        bytes_per_frame = tb_bytes_per_launch(width, height, k, F, tb_chains, n_launch) / frames_per_launch
-    elif scorer is not None and scorer.fused():
-        bytes_per_frame = fused_bytes_per_frame(width, height, k)
-        frames_per_launch = F / n_launch
-    elif scorer is not None:
-        bytes_per_frame = alg_bpf
-        frames_per_launch = F / max(1, scorer.windows())
-    else:
-        bytes_per_frame = alg_bpf
-        frames_per_launch = F
-    if args.workload == "transcode":
         achieved = sad_ops / n_launch / (kern_ms * 1e-3) / 1e12
-    else:
-        achieved = alg_bpf * frames_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_note = None, None
-    if prof is not None:
-        if prow and "hbm_bytes" in prow:
-            traffic = round(prow["hbm_bytes"])
-            traffic_note = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (2xFETCH+WRITE), "
-                            f"mean of {prow['dispatches']} dispatches; "
-                            f"{traffic / (alg_bpf * frames_per_launch):.3f}x SURVEY 8(d) bytes, "
-                            f"{traffic / (bytes_per_frame * frames_per_launch):.3f}x the "
-                            f"decode-inclusive bytes")
-        else:
-            traffic_note = prof.get("error", f"no counters for {kname}")
-    if args.workload == "transcode":
         roof = {"bound": "valu", "achieved": round(achieved, 2), "peak": VALU_SAD_PEAK_TOPS,
                 "unit": "T byte-SAD/s", "frac": round(achieved / VALU_SAD_PEAK_TOPS, 4),
-                "traffic": None, "kernel": kname, "kernel_ms": round(kern_ms, 4),
+                "traffic": None, "kernel": "enc_search<8>", "kernel_ms": round(kern_ms, 4),
                 "sad_ops_per_launch": int(sad_ops / n_launch),
-                "frames_per_launch": round(frames_per_launch, 1),
+                "frames_per_launch": round(p_frames / n_launch, 1),
                 "note": "full-search (2R+1)^2 x 256 byte |a-b| per macroblock, R=8; peak = 256 CUs x "
                         "4 SIMDs x 32 lanes/clk x 4 B (v_sad_u8) x 2.4 GHz"}
     else:
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_unit": "bytes/launch", "traffic_source": traffic_note,
-                "kernel": kname, "kernel_ms": round(kern_ms, 5), "kernel_ms_basis": kern_basis,
-                "kernel_ms_hip_events": round(kern_ms_events, 5),
-                "bytes_per_frame": alg_bpf,
-                "bytes_basis": "SURVEY 8(d): 1.5*W*H NV12 read + 3*w*h RGB + 2*w*h thumbnail "
-                               "luma write/read + 1024 histogram + 4 score",
-                "frames_per_launch": round(frames_per_launch, 1)}
-        if bytes_per_frame != alg_bpf:
-            ach_d = bytes_per_frame * frames_per_launch / (kern_ms * 1e-3) / 1e9
-            roof["decode_inclusive"] = {
-                "bytes_per_frame": round(bytes_per_frame, 1), "achieved": round(ach_d, 1),
-                "frac": round(ach_d / HBM_PEAK_GBS, 4),
-                "basis": "the fused decode+score kernel's own bytes: NV12-sized reference/I_PCM "
-                         "read + NV12 frame write + RGB + thumbnail luma write + predecessor "
-                         "read + histogram + SAD"}
+        roof = roofline_decode_score(sl, prof, width, height, k, F)
     roof_decode = None
-    if args.workload == "decode_score" and not scorer.fused():
+    if args.workload == "decode_score" and not sl[0].fused():
+        t = sl[0].timings()
+        n_launch = sl[0].recon_launches()
+        rec_ms = t["reconstruct_ms"] / n_launch
         rec_bytes = 3 * width * height
         ach = rec_bytes * (F / n_launch) / (rec_ms * 1e-3) / 1e9
         roof_decode = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                        "kernel": ("reconstruct level: h264_inter_full + h264_intra_full + h264_bs_full + "
-                                  "h264_deblock_full" if scorer.general() else "h264_recon"),
+                                  "h264_deblock_full" if sl[0].general() else "h264_recon"),
                        "kernel_ms": round(rec_ms, 4),
                        "launches": n_launch, "bytes_per_frame": rec_bytes,
                        "frames_per_launch": round(F / n_launch, 1)}
 
-    counts = counts_all.cpu().tolist()
+    items = outs.get("items")
+    counts = [it.n_segments for it in items] if items else None
+    stage_info = ({"stage_ms": sl[0].timings(), "recon_launches": sl[0].recon_launches(),
+                   "windows": sl[0].windows()} if sl else {})
 
     # ------------------------------------- parity vs the CPU oracle (+ baseline)
     parity, cpu = None, None
     if args.workload == "decode_score" and not args.no_parity:
-        aff = len(os.sched_getaffinity(0))
-        threads = max(1, min(16, aff // max(1, world)))
-        # N > 1: every rank checks a bounded GOP-aligned prefix of its video
-        maxf = None if world == 1 else min(F, 3000)
-        dec = "full" if scorer.general() else "subset"
-        if dec == "full" and world == 1:
-            maxf = min(F, 18000)  # the general oracle decodes ~350 720p frames/s on 16 threads
-        parity, ct = parity_check(scorer, path, k, duration_s, segs, threads, maxf, dec)
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            cpu = {"value": round(ct["frames"] / ct["seconds"], 2), "unit": "frames/s",
-                   "cores": ct["threads"], "kind": "port",
-                   "sample": f"the parity pass: {ct['frames']} frames ({ct['width']}x"
-                             f"{ct['height']}, {ct['gops']} GOPs) of the benchmark video decoded by "
-                             + ("oracle/h264_full_oracle.c fo_decode" if dec == "full" else
-                                "oracle/vtseg_oracle.c or_decode_samples") +
-                             f" + scored by or_score_frames, GOP-parallel on {ct['threads']} "
-                             f"threads, {ct['seconds']:.1f} s"}
+        if args.parity_frames == "all":
+            maxf = None
+        elif args.parity_frames == "auto":
+            maxf = None if world == 1 else min(F, 3000)
+        else:
+            maxf = min(F, int(args.parity_frames))
+        dec = "full" if sl[0].general() else "subset"
+        per_video, secs, nfr = [], 0.0, 0
+        records_ok = True
+        for i in local_idx:
+            v = scorers[i]
+            duration = float(v.info.duration)
+            plan = bp.plan_segments_with_budget(duration, REF_CONFIG, 0)
+            segs = vs.plan_segments(duration, plan.segment_duration, plan.overlap)
+            par, ct = parity_check(v, all_paths[i], k, segs, threads, maxf, dec)
+            par["video"] = i
+            per_video.append(par)
+            secs += ct["seconds"]
+            nfr += ct["frames"]
+            if items is not None:
+                ok = batch_record_check(items[i], segs, ct, maxf is None or ct["frames"] >= F)
+                par["batch_record_equal"] = ok
+                records_ok &= ok
+        parity = {"videos": len(per_video), "frames": nfr, "of_frames": F * len(per_video),
+                  "scores_equal": all(p["scores_equal"] for p in per_video),
+                  "max_abs_score_diff": max(p["max_abs_score_diff"] for p in per_video),
+                  "score_tolerance": 1e-4,
+                  "hist_equal": all(p["hist_equal"] for p in per_video),
+                  "sad_equal": all(p["sad_equal"] for p in per_video),
+                  "scene_cuts": sum(p["scene_cuts"] for p in per_video),
+                  "scene_cuts_equal": all(p["scene_cuts_equal"] for p in per_video),
+                  "segment_times": sum(p["segment_times"] for p in per_video),
+                  "boundary_frames_equal": all(p["boundary_frames_equal"] for p in per_video),
+                  "pts_equal": all(p["pts_equal"] for p in per_video),
+                  "batch_records_equal": records_ok if items is not None else None,
+                  "oracle": ("oracle/h264_full_oracle.c fo_decode" if dec == "full" else
+                             "oracle/vtseg_oracle.c or_decode_samples") +
+                            f" + or_score_frames (GOP-parallel, {threads} threads)"}
+        parity["all_equal"] = all(p["all_equal"] for p in per_video) and \
+            (records_ok if items is not None else True)
         if world > 1:
             ok = torch.tensor([1 if parity["all_equal"] else 0], dtype=torch.int32, device=coll_dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             parity["all_ranks_equal"] = bool(ok.item())
+            parity["checked_on_each_rank"] = f"{len(per_video)} videos x {nfr // max(1, len(per_video))} frames"
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = {"value": round(nfr / secs, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+                   "sample": f"the parity pass: {nfr} frames ({width}x{height}, {len(per_video)} "
+                             f"videos) of the benchmark batch decoded by " +
+                             ("oracle/h264_full_oracle.c fo_decode" if dec == "full" else
+                              "oracle/vtseg_oracle.c or_decode_samples") +
+                             f" + scored by or_score_frames, GOP-parallel on {threads} "
+                             f"threads, {secs:.1f} s"}
+        log(f"rank {rank}: parity all_equal={parity['all_equal']}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu is None:
         if args.workload == "score":
             cpu = cpu_baseline_score(width, height, k)
         elif args.workload == "transcode":
-            cpu = cpu_baseline_transcode(path, k)
-        else:
-            cpu = cpu_baseline_decode_score(path, k)
+            cpu = cpu_baseline_transcode(all_paths[0], k)
+
+    # -------------------------------------------------- extras (N = 1 only)
+    extra = {}
+    if extras:
+        try:
+            extra["e2e"] = e2e_record(local_paths, gpu)
+            log(f"e2e: {extra['e2e']['value']} frames/s")
+        except Exception as exc:  # noqa: BLE001 - reported in the line
+            extra["e2e"] = {"error": f"{type(exc).__name__}: {exc}"}
+        # the batch's sessions give their HBM back before the 2-h video's rings
+        for v in sl:
+            v.close()
+        for key, p, label in (("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
+                                                        "(216 000 frames), streamed two-ring decode"),
+                              ("general", gen_path, "general decoder: 10-min 720p full-syntax "
+                                                    "stream (CAVLC, B pictures with B references, "
+                                                    "spatial direct, implicit weighted "
+                                                    "bi-prediction, 3 references, deblocking)")):
+            try:
+                r = run_single(p, gpu=gpu, k=4, steps=3, threads=threads, label=label)
+                if key == "general" and gprof:
+                    r["kernels"] = general_kernel_rooflines(gprof, 1280, 720, 4, r["frames"],
+                                                            80 * 45)
+                extra[key] = r
+                log(f"{key}: {r['value']} frames/s, parity {r.get('parity', {}).get('all_equal')}")
+            except Exception as exc:  # noqa: BLE001 - reported in the line
+                extra[key] = {"error": f"{type(exc).__name__}: {exc}"}
 
     if rank == 0:
         line = {
@@ -698,11 +982,16 @@ def main() -> None:
             "config": {"workload": f"{args.workload}: {cdesc}; synthetic H.264 {width}x{height} "
                                    + ("(full syntax" + (", B pictures" if args.bframes else "") + ") "
                                       if args.coding == "full" else "")
-                                   + f"@30fps, {F} frames ({F / FPS / 60:.1f} min) per GPU, "
+                                   + f"@30fps, {vpg} x {F} frames ({F / FPS / 60:.1f} min) per GPU, "
                                    f"thumbnails k={k}",
                        "config_name": args.config,
-                       "frames_per_gpu": F, "width": width, "height": height, "k": k,
-                       "parallelism": f"video-per-gpu x{world}",
+                       "videos": n_videos, "videos_per_gpu": vpg,
+                       "frames_per_video": F, "frames_per_gpu": F * vpg,
+                       "width": width, "height": height, "k": k,
+                       "parallelism": f"video-per-gpu x{world} (video i on rank i mod {world})",
+                       "collectives": ("plan_batch: all_gather of per-video records + padded "
+                                       "boundary arrays, " + (args.dist_backend if world > 1
+                                                              else "none at N=1")),
                        "segment_counts": counts},
             "roofline": roof,
             "roofline_decode": roof_decode,
@@ -714,16 +1003,21 @@ def main() -> None:
             line["metric"] = "720p frames/sec transcoded to 360p (upload compression, SURVEY 8f-2)"
             line["config"]["transcode"] = {kk: (round(v, 3) if isinstance(v, float) else v)
                                            for kk, v in f.items()}
-            line["config"]["transcode"]["input_bytes"] = Path(path).stat().st_size
-        elif scorer is not None:
-            line["config"]["stage_ms"] = scorer.timings()
-            line["config"]["recon_launches"] = scorer.recon_launches()
-            line["config"]["windows"] = scorer.windows()
+            line["config"]["transcode"]["input_bytes"] = Path(all_paths[0]).stat().st_size
+        elif sl:
+            line["config"].update(stage_info)
+            line["config"]["bits_per_frame"] = round(
+                sum(Path(p).stat().st_size for p in local_paths) * 8 / (F * len(local_paths)), 1)
+        line.update(extra)
         print(json.dumps(line), flush=True)
-    if scorer is not None:
-        scorer.close()
+    for v in sl:
+        v.close()
     if not args.video:
         shutil.rmtree(tmpdir, ignore_errors=True)
+    else:
+        for p in (gen_path, long_path):
+            if p is not None:
+                Path(p).unlink(missing_ok=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

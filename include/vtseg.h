@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTS_ABI_VERSION 4
+#define VTS_ABI_VERSION 5
 
 enum {
   VTS_OK = 0,
@@ -283,6 +283,12 @@ int vts_run(vts_ctx *ctx);
 /* Scene cut frame indices (score > threshold) of the last vts_score/vts_run. */
 int vts_scene_cuts(vts_ctx *ctx, int64_t *frame_idx, int64_t cap,
                    int64_t *n_out);
+/* Presentation timestamps of every frame (track timescale, presentation
+ * order, the order of every result); host data, no device work.  Two-call
+ * size query: with pts == NULL or cap < n_frames returns VTS_E_CAPACITY and
+ * sets *n_out.  The batch driver (vtseg.batch.plan_batch) turns scene-cut
+ * indices into times with it without copying the per-frame results. */
+int vts_frame_pts(const vts_ctx *ctx, int64_t *pts, int64_t cap, int64_t *n_out);
 /* Frame index of each segment time (see vts_boundary_frames_pts). */
 int vts_boundary_frames(vts_ctx *ctx, const double *times, int64_t n,
                         int64_t *frame_idx);

@@ -970,6 +970,15 @@ extern "C" int vts_boundary_frames(vts_ctx *c, const double *times, int64_t n, i
                                  frame_idx);
 }
 
+extern "C" int vts_frame_pts(const vts_ctx *c, int64_t *pts, int64_t cap, int64_t *n_out) {
+  clear_error();
+  if (!c || !n_out) return fail(VTS_E_INVALID, "NULL argument");
+  *n_out = c->n_frames;
+  if (!pts || cap < c->n_frames) return fail(VTS_E_CAPACITY, "need %lld", static_cast<long long>(c->n_frames));
+  std::memcpy(pts, c->pts.data(), sizeof(int64_t) * static_cast<size_t>(c->n_frames));
+  return VTS_OK;
+}
+
 extern "C" int vts_get_frame_nv12(vts_ctx *c, int64_t frame, uint8_t *out, int64_t out_bytes) {
   clear_error();
   if (!c || !out) return fail(VTS_E_INVALID, "NULL argument");

@@ -12,7 +12,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libvtseg.so"
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 VTS_OK = 0
 VTS_E_INVALID = -1
@@ -153,6 +153,7 @@ SIGNATURES: dict[str, tuple] = {
                             _P(C.c_int64), C.c_int64, _P(C.c_int64)]),
     "vts_run": (C.c_int, [C.c_void_p]),
     "vts_scene_cuts": (C.c_int, [C.c_void_p, _P(C.c_int64), C.c_int64, _P(C.c_int64)]),
+    "vts_frame_pts": (C.c_int, [C.c_void_p, _P(C.c_int64), C.c_int64, _P(C.c_int64)]),
     "vts_boundary_frames": (C.c_int, [C.c_void_p, _P(C.c_double), C.c_int64,
                                       _P(C.c_int64)]),
     "vts_get_frame_nv12": (C.c_int, [C.c_void_p, C.c_int64, _P(C.c_uint8), C.c_int64]),

@@ -52,7 +52,15 @@ def _segments(duration: float, config: dict, current_api_count: int):
 
 
 def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int = 0,
-               score: bool = False, device: int | None = None, group=None) -> list[BatchItem]:
+               score: bool = False, device: int | None = None, group=None,
+               sessions: dict | None = None) -> list[BatchItem]:
+    """Plan (and with score=True decode + score) a batch of videos, video i on
+    rank i % world, and all-gather the results (module docstring).
+
+    sessions: optional {video index: open scene.VideoScorer} for this rank's
+    videos, kept open by the caller (their elementary streams stay resident in
+    HBM across calls; the benchmark's timed step).  Videos without one are
+    opened from their file and closed again (demux + upload included)."""
     import torch
     import torch.distributed as dist
 
@@ -81,16 +89,25 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
             # it in the video's record and carry on.
             try:
                 from .scene import VideoScorer
-                dev_id = torch.cuda.current_device() if device is None else device
-                with VideoScorer(p, device=dev_id) as v:
-                    res = v.score()
-                    cuts = v.scene_cuts()
+                v = (sessions or {}).get(i)
+                own = v is None
+                if own:
+                    dev_id = torch.cuda.current_device() if device is None else device
+                    v = VideoScorer(p, device=dev_id)
+                try:
+                    v.run()                  # decode + score; per-frame results stay on the device
+                    cuts = v.scene_cuts()    # only the scores come back to find the cuts
+                    pts = v.frame_pts()
                     times = [t for sg in segs for t in (sg.start, sg.end)]
                     sf = v.boundary_frames(times) if times else []
+                    ts = int(v.info.track_timescale)
+                finally:
+                    if own:
+                        v.close()
                 n_cuts = len(cuts)
                 seg_frames[j] = sf
                 cut_frames[j] = list(cuts)
-                cut_times[j] = [float(res.pts[c]) / res.timescale for c in cuts]
+                cut_times[j] = [float(pts[c]) / ts for c in cuts]
             except Exception as exc:  # noqa: BLE001 - reported per video
                 errors[i] = f"{type(exc).__name__}: {exc}"
                 local[j, 3] = 1

@@ -196,6 +196,16 @@ class VideoScorer:
         _lib.check(self._lib.vts_scene_cuts(self._ctx, buf, cap, C.byref(n)))
         return list(buf[: n.value])
 
+    def frame_pts(self) -> np.ndarray:
+        """Presentation timestamps of every frame (int64, track timescale,
+        presentation order; host data, no device work)."""
+        n = self.n_frames
+        pts = np.zeros(max(n, 1), np.int64)
+        got = C.c_int64(0)
+        _lib.check(self._lib.vts_frame_pts(self._ctx, pts.ctypes.data_as(C.POINTER(C.c_int64)),
+                                           n, C.byref(got)))
+        return pts[:n]
+
     def scene_cut_times(self) -> list[float]:
         """Presentation times (s) of the scene-cut frames (decodes + scores):
         anchors for the opt-in scene-aware segment boundaries (vtseg.snap)."""
