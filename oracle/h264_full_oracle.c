@@ -1,7 +1,7 @@
 /*
  * h264_full_oracle.c — scalar CPU restatement of ITU-T H.264 decoding for
  * progressive CAVLC streams with I and P slices, used ONLY as the checker of
- * the device decoder (video-transformer_amd/csrc/decode_full.hip).
+ * the device decoder (decode_full.hip in the product package).
  *
  * TEST INFRASTRUCTURE.  Only tests/, __graft_entry__.smoke() and bench.py's
  * parity / cpu_baseline legs may load this code; the product never links it.
@@ -35,10 +35,12 @@
 #include <stdlib.h>
 #include <string.h>
 
-/* CABAC / 8x8-transform constant tables (Tables 9-12..9-33, 9-43, 9-44,
- * 8.5.6, 8.5.9): the standard's numbers as one C header shared with the
- * device parser (data only; no product code is linked) */
-#include "../video-transformer_amd/csrc/h264_cabac_tables.h"
+/* CABAC / 8x8-transform constants (Tables 9-12..9-33, 9-43, 9-44, 8-16):
+ * the oracle's own transcription in the standard's layout, independent of
+ * the product's header (tests/test_cabac_tables.py diffs the two) */
+#include "h264_std_tables.h"
+
+#define FO_NCTX 460
 
 /* CABAC synthesis mode (fo_cabac_convert, test infrastructure) */
 typedef struct fo_enc_s fo_enc;
@@ -1154,13 +1156,22 @@ typedef struct {
 static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_hdr *h);
 static void inter_pred_mb(const fo_ctx *c, int addr, int *py, int *pu, int *pv);
 
+/* 8.5.9: the position class of (i, j) that selects v8x8's column */
+static int norm8_class(int i, int j) {
+  if (i % 4 == 0 && j % 4 == 0) return 0;
+  if (i % 2 == 1 && j % 2 == 1) return 1;
+  if (i % 4 == 2 && j % 4 == 2) return 2;
+  if ((i % 4 == 0 && j % 2 == 1) || (i % 2 == 1 && j % 4 == 0)) return 3;
+  if ((i % 4 == 0 && j % 4 == 2) || (i % 4 == 2 && j % 4 == 0)) return 4;
+  return 5;
+}
+
 /* 8.5.13: scaling (flat) + 8x8 inverse transform of raster coefficients c */
-static const int NORM8[6][6] = VTS_NORM8_DATA;
 static void scale_idct8(const int *c, int qp, int *r) {
   int d[64], g[64];
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 8; j++) {
-      int ls = 16 * NORM8[qp % 6][vts_norm8_class(i, j)];
+      int ls = 16 * FO_V8[qp % 6][norm8_class(i, j)];
       int k = i * 8 + j;
       d[k] = qp >= 36 ? (c[k] * ls) << (qp / 6 - 6) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     }
@@ -2118,13 +2129,64 @@ static int decode_mb(fo_ctx *c, fb_t *b, int addr, int is_p, int *qp, const fo_h
 }
 
 /* ------------------------------------------------------------ CABAC (9.3) */
-static const int8_t CAB_INIT_I[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_I_DATA;
-static const int8_t CAB_INIT_P0[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_P0_DATA;
-static const uint8_t RANGE_LPS[64][4] = VTS_CABAC_RANGE_LPS_DATA;
-static const uint8_t TRANS_LPS[64] = VTS_CABAC_TRANS_LPS_DATA;
-static const uint8_t SIG8[63] = VTS_SIG8x8_DATA;
-static const uint8_t LAST8[63] = VTS_LAST8x8_DATA;
-static const int ZZ8[64] = VTS_ZZ8_DATA;
+#define RANGE_LPS FO_RANGE_LPS
+#define TRANS_LPS FO_TRANS_LPS
+#define SIG8 FO_SIG8_FRAME
+#define LAST8 FO_LAST8_FRAME
+/* (m, n) by ctxIdx for the I column and cabac_init_idc 0, spread from the
+ * standard's per-range listing (h264_std_tables.h); entries the standard
+ * leaves undefined for a column stay (0, 0) and are never used by it */
+static int8_t CAB_INIT_I[FO_NCTX][2], CAB_INIT_P0[FO_NCTX][2];
+/* 8.5.6 / Figure 8-9: frame zig-zag of an 8x8 block, coefficient list index
+ * -> raster position, by walking the anti-diagonals alternately */
+static int ZZ8[64];
+static void fo_tables_init(void) {
+  static int done;
+  if (done) return;
+  for (size_t i = 0; i < sizeof FO_CTX_INIT / sizeof FO_CTX_INIT[0]; i++) {
+    const fo_ctx_init *e = &FO_CTX_INIT[i];
+    if (e->mi != FO_NA) { CAB_INIT_I[e->ctx][0] = e->mi; CAB_INIT_I[e->ctx][1] = e->ni; }
+    CAB_INIT_P0[e->ctx][0] = e->mp;
+    CAB_INIT_P0[e->ctx][1] = e->np;
+  }
+  int k = 0;
+  for (int d = 0; d < 15; d++) {        /* d = row + column */
+    for (int t = 0; t <= d; t++) {
+      int row = (d % 2 == 0) ? d - t : t; /* even diagonals run up-right, odd down-left */
+      int col = d - row;
+      if (row < 8 && col < 8) ZZ8[k++] = row * 8 + col;
+    }
+  }
+  done = 1;
+}
+
+/* the oracle's tables, for tests/test_cabac_tables.py:
+ * which 0: CAB_INIT_I (i = ctxIdx, j = 0 m / 1 n; defined[i] in *ok),
+ * 1: CAB_INIT_P0, 2: rangeTabLPS[i][j], 3: transIdxLPS[i], 4: Table 9-43
+ * significant ctxIdxInc [i], 5: last ctxIdxInc [i], 6: zig-zag [i],
+ * 7: normAdjust8x8 v8x8[i][j] (m, class) */
+int fo_std_table(int which, int i, int j, int *ok) {
+  fo_tables_init();
+  *ok = 1;
+  switch (which) {
+    case 0: case 1:
+      for (size_t x = 0; x < sizeof FO_CTX_INIT / sizeof FO_CTX_INIT[0]; x++)
+        if (FO_CTX_INIT[x].ctx == i) {
+          if (which == 0 && FO_CTX_INIT[x].mi == FO_NA) break;
+          return which == 0 ? (j ? FO_CTX_INIT[x].ni : FO_CTX_INIT[x].mi)
+                            : (j ? FO_CTX_INIT[x].np : FO_CTX_INIT[x].mp);
+        }
+      *ok = 0;
+      return 0;
+    case 2: return FO_RANGE_LPS[i][j];
+    case 3: return FO_TRANS_LPS[i];
+    case 4: return FO_SIG8_FRAME[i];
+    case 5: return FO_LAST8_FRAME[i];
+    case 6: return ZZ8[i];
+    case 7: return FO_V8[i][j];
+    default: *ok = 0; return 0;
+  }
+}
 
 /* CABAC stream synthesis (TEST INFRASTRUCTURE, fo_cabac_convert below): the
  * decoder below runs unchanged, but every bin it asks for is chosen by a
@@ -2179,7 +2241,7 @@ static int enc_p1(int ctx) {
 typedef struct {
   fb_t *b;
   uint32_t range, offset;
-  uint8_t state[VTS_CABAC_NCTX], mps[VTS_CABAC_NCTX];
+  uint8_t state[FO_NCTX], mps[FO_NCTX];
 } fo_cab;
 
 static void cab_start(fo_cab *k) { /* 9.3.1.2 */
@@ -2195,8 +2257,9 @@ static void cab_start(fo_cab *k) { /* 9.3.1.2 */
   k->offset = fb_bits(k->b, 9);
 }
 static void cab_init(fo_cab *k, int is_i, int qp) { /* 9.3.1.1 */
+  fo_tables_init();
   const int8_t(*t)[2] = is_i ? CAB_INIT_I : CAB_INIT_P0;
-  for (int i = 0; i < VTS_CABAC_NCTX; i++) {
+  for (int i = 0; i < FO_NCTX; i++) {
     int pre = clip3(1, 126, ((t[i][0] * clip3(0, 51, qp)) >> 4) + t[i][1]);
     if (pre <= 63) { k->state[i] = (uint8_t)(63 - pre); k->mps[i] = 0; }
     else { k->state[i] = (uint8_t)(pre - 64); k->mps[i] = 1; }

@@ -5,7 +5,7 @@
  * -c:v libx264 -crf 28`).  Used ONLY as a checker.
  *
  * TEST INFRASTRUCTURE.  Only tests/ may load this (through liboracle.so);
- * the product (libvtseg.so, csrc/transcode.hip) never links or calls it.
+ * the product (libvtseg.so, its transcode.hip) never links or calls it.
  * Plain scalar C, written from the definition in DESIGN.md §11, not from the
  * device code.
  *
