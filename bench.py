@@ -299,7 +299,7 @@ def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None,
 
 
 def synth_videos(jobs: list[tuple[Path, int]], width: int, height: int, frames: int,
-                 coding: str = "subset", bframes: bool = False) -> list[dict]:
+                 coding: str = "subset", bframes: bool = False, cabac: bool = False) -> list[dict]:
     """Write the synthetic H.264/MP4 inputs (vts_synth_write; ctypes releases
     the GIL, so the videos are written in parallel)."""
     from vtseg import scene
@@ -308,8 +308,12 @@ def synth_videos(jobs: list[tuple[Path, int]], width: int, height: int, frames: 
         path, seed = job
         if coding == "full":
             # x264-like structure: one slice per picture; with bframes B
-            # reference pictures, spatial direct, implicit weighted bi-prediction
+            # reference pictures, spatial direct, implicit weighted
+            # bi-prediction; with cabac CABAC and the High profile's 8x8
+            # transform (x264's defaults: cabac, 8x8dct, b-pyramid, weightb)
             extra = dict(bframes=True, weighted="implicit") if bframes else {}
+            if cabac:
+                extra.update(cabac=True, transform_8x8=True)
             return scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=frames,
                                      seed=seed, coding="full", slices_per_row=0, max_motion=4,
                                      **extra)
@@ -708,7 +712,7 @@ def main() -> None:
         gen_path = tmpdir / "general_720p_10min.mp4"
         long_path = tmpdir / "long_720p_2h.mp4"
         with ThreadPoolExecutor(2) as ex:
-            fa = ex.submit(synth_videos, [(gen_path, 0x5EED)], 1280, 720, 18000, "full", True)
+            fa = ex.submit(synth_videos, [(gen_path, 0x5EED)], 1280, 720, 18000, "full", True, True)
             fb = ex.submit(synth_videos, [(long_path, 0x5EED)], 1280, 720, 216000)
             fa.result()
             fb.result()
@@ -959,10 +963,12 @@ def main() -> None:
             v.close()
         for key, p, label in (("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
                                                         "(216 000 frames), streamed two-ring decode"),
-                              ("general", gen_path, "general decoder: 10-min 720p full-syntax "
-                                                    "stream (CAVLC, B pictures with B references, "
-                                                    "spatial direct, implicit weighted "
-                                                    "bi-prediction, 3 references, deblocking)")):
+                              ("general", gen_path, "general decoder: 10-min 720p x264-like "
+                                                    "full-syntax stream (High profile: CABAC, 8x8 "
+                                                    "transform and Intra_8x8, B pyramid with B "
+                                                    "references, spatial direct, implicit weighted "
+                                                    "bi-prediction, 3 references, deblocking, one "
+                                                    "slice per picture)")):
             try:
                 r = run_single(p, gpu=gpu, k=4, steps=3, threads=threads, label=label)
                 if key == "general" and gprof:

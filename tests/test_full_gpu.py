@@ -324,3 +324,38 @@ def test_window_without_clean_picture_in_slot_range_is_refused(tmp_path, monkeyp
     with scene.VideoScorer(path, decoder="general", keep_frames=True) as v:
         v.score()
         assert np.array_equal(v.frame_nv12(39).reshape(frames[-1].shape), frames[-1])
+
+
+WRITER_CABAC = [
+    ("ip_t8", dict(width=320, height=240, transform_8x8=True)),
+    ("b_t8_implicit", dict(width=320, height=240, bframes=True, transform_8x8=True, weighted="implicit")),
+    ("b_t8_explicit_temporal_rows", dict(width=336, height=200, bframes=True, transform_8x8=True,
+                                         weighted="explicit", temporal_direct=True, slices_per_row=1)),
+    ("hd720_x264like", dict(width=1280, height=720, bframes=True, transform_8x8=True, weighted="implicit")),
+]
+
+
+@pytest.mark.parametrize("name,kw", WRITER_CABAC, ids=[c[0] for c in WRITER_CABAC])
+def test_writer_cabac_streams_bit_exact(tmp_path, name, kw):
+    """The writer's own CABAC streams (synth_full.cpp, cabac=True; High
+    profile with transform_8x8): x264's structure (CABAC, B pyramid, 8x8
+    transform, weighted bi-prediction, one slice per picture) decoded and
+    scored on the device equal the oracle frame for frame."""
+    _require_gpu()
+    kw = dict(kw)
+    spr = kw.pop("slices_per_row", 0)
+    n = 24 if kw["height"] >= 720 else 45
+    path = tmp_path / f"{name}.mp4"
+    scene.synth_write(path, n_frames=n, coding="full", cabac=True, slices_per_row=spr, cut_min_s=0.4,
+                      cut_max_s=1.0, gop_max_s=0.6, seed=29, max_motion=4, **kw)
+    frames, _ = oracle.decode_full(path)
+    W, H = kw["width"], kw["height"]
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 4)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+        assert _first_diff(got, frames) == []
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])

@@ -147,3 +147,37 @@ def test_real_cabac_high_profile_stream(harness):
     assert got.shape == want.shape
     bad = [i for i in range(len(want)) if not np.array_equal(got[i], want[i])]
     assert bad == []
+
+
+WRITER_CABAC = [
+    ("ip", {}),
+    ("ip_t8", {"transform_8x8": True}),
+    ("ip_t8_rows", {"transform_8x8": True, "slices_per_row": 1}),
+    ("ip_cip_t8", {"transform_8x8": True, "constrained_intra": True}),
+    ("b", {"bframes": True}),
+    ("b_t8_implicit", {"bframes": True, "transform_8x8": True, "weighted": "implicit"}),
+    ("b_t8_explicit_temporal", {"bframes": True, "transform_8x8": True, "weighted": "explicit",
+                                "temporal_direct": True}),
+]
+
+
+@pytest.mark.parametrize("name,kw", WRITER_CABAC, ids=[s[0] for s in WRITER_CABAC])
+def test_writer_cabac_streams_on_cpu_equal_oracle(tmp_path, harness, name, kw):
+    """The stream writer's own CABAC output (synth_full.cpp, cabac=True:
+    Main / High profile, the writer's syntax decisions arithmetic-coded with
+    its own binarizations and context selection; Intra_8x8 and 8x8-transform
+    inter macroblocks with transform_8x8): every slice must parse to its stop
+    bit in the oracle, and the product's CABAC parser and reconstruction must
+    equal the oracle before and after deblocking."""
+    kw = dict(kw)
+    spr = kw.pop("slices_per_row", 0)
+    path = tmp_path / f"wc_{name}.mp4"
+    scene.synth_write(path, width=176, height=144, n_frames=36, coding="full", cabac=True,
+                      slices_per_row=spr, cut_min_s=0.4, cut_max_s=1.0, gop_max_s=0.6, seed=13,
+                      chunks=1, **kw)
+    for flags in (1, 0):
+        want, _ = oracle.decode_full(path, flags=flags)
+        got = harness(path, flags)
+        assert got.shape == want.shape
+        bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
+        assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"

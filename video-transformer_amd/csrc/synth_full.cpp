@@ -20,6 +20,17 @@
 // intra ~8%; (I): Intra_4x4 ~60% with random valid modes, Intra_16x16 ~38%,
 // I_PCM ~1%.  Residuals: random coded_block_pattern, mb_qp_delta, 4x4 blocks
 // of 0..16 coefficients mostly +-1 with escapes up to |2000|.
+//
+// CABAC (edge_cases bit 10, Main / High profile): the same decisions written
+// through the arithmetic coder of 9.3.4 with cabac_init_idc 0: every syntax
+// element's binarization (9.3.2) and context selection (9.3.3.1), which the
+// writer derives from its own neighbour records the way a decoder does
+// (mb_skip_flag, mb_type, sub_mb_type, ref_idx, mvd, coded_block_pattern,
+// mb_qp_delta, intra modes, coded_block_flag, significance maps, levels,
+// end_of_slice_flag, I_PCM with the engine flushed and restarted).  With
+// bit 11 (High profile, transform_8x8_mode_flag) Intra_NxN macroblocks are
+// Intra_8x8 half the time and inter macroblocks without sub-8x8 partitions
+// use the 8x8 transform half the time (8x8 blocks of up to 64 levels).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +41,7 @@
 #include "bitstream.h"
 #include "common.h"
 #include "h264.h"
+#include "h264_cabac_tables.h"
 #include "h264_tables.h"
 #include "synth.h"
 
@@ -43,14 +55,127 @@ constexpr int kMaxRefs = 3;
 constexpr int kPpsRefDefault = 2;    // num_ref_idx_l0_default_active
 
 struct GMb {
-  int type = 0;   // 0 inter, 1 I_NxN, 2 I_16x16, 3 I_PCM, 4 P_Skip
+  int type = 0;   // 0 inter, 1 I_NxN, 2 I_16x16, 3 I_PCM, 4 P_Skip / B_Skip
   int slice = -1;
-  int i4[16];     // Intra4x4PredMode, raster 4x4 blocks
+  int i4[16];     // Intra4x4PredMode, raster 4x4 blocks (Intra8x8PredMode repeated over its 4)
   int nz[16];     // total_coeff, raster luma 4x4 blocks
   int nzc[2][4];  // chroma AC total_coeff
   int ref[2][16];  // refIdxLX per raster 4x4 block (-1: list unused)
   int mv[2][16][2];
   int refd[2][16]; // display index of the picture refIdxLX names (B mode)
+  // CABAC context facts (9.3.3.1.1)
+  int cbp = 0;        // coded_block_pattern (I_16x16: the one its mb_type implies)
+  int cmode = 0;      // intra_chroma_pred_mode
+  bool t8 = false;    // transform_size_8x8_flag
+  bool d16 = false;   // B_Skip / B_Direct_16x16
+  int dmask = 0;      // 8x8 quarters predicted in direct mode
+  uint32_t cbf = 0;   // coded_block_flag: bit 0 Intra16x16 DC, 1 + raster luma 4x4,
+                      // 17 + plane chroma DC, 19 + 4 * plane + raster chroma AC
+  int mvda[2][16][2]; // |mvd_lX| per raster 4x4 block (0: none written)
+};
+
+// CABAC arithmetic encoder (9.3.4) writing into a BitWriter; context
+// variables initialised per 9.3.1.1 from the I column or cabac_init_idc 0.
+const int8_t kInitI[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_I_DATA;
+const int8_t kInitP[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_P0_DATA;
+const uint8_t kRangeLps[64][4] = VTS_CABAC_RANGE_LPS_DATA;
+const uint8_t kTransLps[64] = VTS_CABAC_TRANS_LPS_DATA;
+const uint8_t kSig8[63] = VTS_SIG8x8_DATA;
+const uint8_t kLast8[63] = VTS_LAST8x8_DATA;
+
+class CabacEnc {
+ public:
+  void init(BitWriter *bw, bool is_i, int qp) {  // 9.3.1.1 + 9.3.4.1
+    bw_ = bw;
+    const int q = std::clamp(qp, 0, 51);
+    for (int i = 0; i < VTS_CABAC_NCTX; ++i) {
+      const int m = is_i ? kInitI[i][0] : kInitP[i][0], n = is_i ? kInitI[i][1] : kInitP[i][1];
+      const int pre = std::clamp(((m * q) >> 4) + n, 1, 126);
+      st_[i] = static_cast<uint8_t>(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1);
+    }
+    start();
+  }
+  void start() {  // InitEncoder
+    low_ = 0;
+    range_ = 510;
+    first_ = true;
+    outstanding_ = 0;
+  }
+  void enc(int ctx, int bin) {  // EncodeDecision
+    const int s = st_[ctx], ps = s >> 1, mps = s & 1;
+    const uint32_t lps = kRangeLps[ps][(range_ >> 6) & 3];
+    range_ -= lps;
+    if (bin != mps) {
+      low_ += range_;
+      range_ = lps;
+      st_[ctx] = static_cast<uint8_t>((kTransLps[ps] << 1) | (ps == 0 ? 1 - mps : mps));
+    } else {
+      st_[ctx] = static_cast<uint8_t>((std::min(ps + 1, 62) << 1) | mps);
+    }
+    renorm();
+  }
+  void bypass(int bin) {  // EncodeBypass
+    low_ <<= 1;
+    if (bin) low_ += range_;
+    if (low_ >= 1024) {
+      put(1);
+      low_ -= 1024;
+    } else if (low_ < 512) {
+      put(0);
+    } else {
+      low_ -= 512;
+      ++outstanding_;
+    }
+  }
+  void term(int bin) {  // EncodeTerminate; 1 flushes (the last bit written is the stop / final bit)
+    range_ -= 2;
+    if (bin) {
+      low_ += range_;
+      range_ = 2;  // EncodeFlush
+      renorm();
+      put((low_ >> 9) & 1);
+      bw_->bit((low_ >> 8) & 1);
+      bw_->bit(1);
+    } else {
+      renorm();
+    }
+  }
+  void ueg(int v, int k) {  // k-th order Exp-Golomb suffix, bypass (9.3.2.3)
+    while (v >= (1 << k)) {
+      bypass(1);
+      v -= 1 << k;
+      ++k;
+    }
+    bypass(0);
+    while (k--) bypass((v >> k) & 1);
+  }
+
+ private:
+  void put(int b) {
+    if (first_) first_ = false;
+    else bw_->bit(static_cast<uint32_t>(b));
+    for (; outstanding_ > 0; --outstanding_) bw_->bit(static_cast<uint32_t>(1 - b));
+  }
+  void renorm() {
+    while (range_ < 256) {
+      if (low_ < 256) {
+        put(0);
+      } else if (low_ >= 512) {
+        low_ -= 512;
+        put(1);
+      } else {
+        low_ -= 256;
+        ++outstanding_;
+      }
+      range_ <<= 1;
+      low_ <<= 1;
+    }
+  }
+  BitWriter *bw_ = nullptr;
+  uint32_t low_ = 0, range_ = 510;
+  bool first_ = true;
+  int outstanding_ = 0;
+  uint8_t st_[VTS_CABAC_NCTX];
 };
 
 struct Loc {
@@ -67,6 +192,8 @@ class FullWriter {
     nmb_ = mbw_ * mbh_;
     mb_.resize(static_cast<size_t>(nmb_));
     cip_ = (P.edge_cases & 16) != 0;
+    cabac_ = (P.edge_cases & 1024) != 0;
+    t8mode_ = cabac_ && (P.edge_cases & 2048) != 0;
   }
   void run();
   void run_b();
@@ -77,6 +204,11 @@ class FullWriter {
   Pcg32 rng_;
   int mbw_, mbh_, nmb_;
   bool cip_;
+  bool cabac_ = false, t8mode_ = false;
+  CabacEnc cab_;
+  bool qpd_prev_ = false, qpd_cur_ = false;  // mb_qp_delta != 0 of the previous / current macroblock
+  int cref_[2][4];                          // ref_idx_lX of the current macroblock's quarters written so far
+  int cmvd_[2][16][2];                      // |mvd_lX| of the current macroblock written so far
   std::vector<GMb> mb_;
   BitWriter *bw_ = nullptr;
   int nref_ = 0;      // active references of the current P slice
@@ -272,39 +404,182 @@ class FullWriter {
     }
   }
 
+  // CABAC residual_block (7.3.5.3.3, 9.3.2.3 / 9.3.3.1.3): coef[0, maxNum) in
+  // scan order; cat = ctxBlockCat (5: an 8x8 block, which has no
+  // coded_block_flag and at least one non-zero level).  Returns the count of
+  // non-zero levels.
+  int cab_block(const int *coef, int maxNum, int cat, int cbf_inc) {
+    static const int kCbfOff[5] = {0, 4, 8, 12, 16}, kSigOff[5] = {0, 15, 29, 44, 47};
+    static const int kAbsOff[5] = {0, 10, 20, 30, 39};
+    int last = -1, n = 0;
+    for (int i = 0; i < maxNum; ++i)
+      if (coef[i]) {
+        last = i;
+        ++n;
+      }
+    if (cat != 5) {
+      cab_.enc(85 + kCbfOff[cat] + cbf_inc, last >= 0);
+      if (last < 0) return 0;
+    }
+    for (int i = 0; i < maxNum - 1; ++i) {
+      const int inc = cat == 3 ? std::min(i, 2) : i;
+      const int sig = coef[i] != 0;
+      cab_.enc(cat == 5 ? 402 + kSig8[i] : 105 + kSigOff[cat] + inc, sig);
+      if (sig) {
+        cab_.enc(cat == 5 ? 417 + kLast8[i] : 166 + kSigOff[cat] + inc, i == last);
+        if (i == last) break;
+      }
+    }
+    int eq1 = 0, gt1 = 0;
+    const int base = cat == 5 ? 426 : 227 + kAbsOff[cat];
+    for (int i = last; i >= 0; --i) {
+      if (!coef[i]) continue;
+      const int a = std::abs(coef[i]) - 1;  // coeff_abs_level_minus1: TU prefix cMax 14 + UEG0
+      cab_.enc(base + (gt1 ? 0 : std::min(4, 1 + eq1)), a > 0);
+      if (a > 0) {
+        const int inc = 5 + std::min(4 - (cat == 3 ? 1 : 0), gt1);
+        for (int k = 1; k < 14; ++k) {
+          cab_.enc(base + inc, k < a);
+          if (k >= a) break;
+        }
+        if (a >= 14) cab_.ueg(a - 14, 0);
+      }
+      cab_.bypass(coef[i] < 0);
+      if (a == 0) ++eq1;
+      else ++gt1;
+    }
+    return n;
+  }
+  // condTermFlagN of coded_block_flag (9.3.3.1.1.9); n: the neighbour
+  // macroblock (-1 unavailable), tb: transBlockN is available
+  int cbf_cond(int n, bool intra, bool tb, int bit) const {
+    if (n < 0) return intra ? 1 : 0;
+    const GMb &m = mb_[static_cast<size_t>(n)];
+    if (m.type == 3) return 1;
+    if (!tb || m.type == 4) return 0;
+    return static_cast<int>((m.cbf >> bit) & 1u);
+  }
+  int cbf_inc_dc(int cur) const {
+    const int a = nb_a(cur), b = nb_b(cur);
+    return cbf_cond(a, true, a >= 0 && mb_[static_cast<size_t>(a)].type == 2, 0) +
+           2 * cbf_cond(b, true, b >= 0 && mb_[static_cast<size_t>(b)].type == 2, 0);
+  }
+  int cbf_inc_luma(int cur, int bx, int by, bool intra) const {
+    int inc = 0;
+    for (int nb = 0; nb < 2; ++nb) {
+      const Loc l = loc(cur, nb ? bx * 4 : bx * 4 - 1, nb ? by * 4 - 1 : by * 4, 16);
+      bool tb = false;
+      int bit = 0;
+      if (l.mb >= 0) {
+        tb = (mb_[static_cast<size_t>(l.mb)].cbp >> ((l.yw / 8) * 2 + l.xw / 8)) & 1;
+        bit = 1 + (l.yw / 4) * 4 + l.xw / 4;
+      }
+      inc += cbf_cond(l.mb, intra, tb, bit) << nb;
+    }
+    return inc;
+  }
+  int cbf_inc_chroma(int cur, int pl, int blk, bool dc, bool intra) const {
+    const int x = dc ? 0 : (blk & 1) * 4, y = dc ? 0 : (blk >> 1) * 4;
+    int inc = 0;
+    for (int nb = 0; nb < 2; ++nb) {
+      const Loc l = loc(cur, nb ? x : x - 1, nb ? y - 1 : y, 8);
+      bool tb = false;
+      int bit = 0;
+      if (l.mb >= 0) {
+        const int cc = mb_[static_cast<size_t>(l.mb)].cbp >> 4;
+        tb = dc ? cc != 0 : cc == 2;
+        bit = dc ? 17 + pl : 19 + 4 * pl + (l.yw / 4) * 2 + l.xw / 4;
+      }
+      inc += cbf_cond(l.mb, intra, tb, bit) << nb;
+    }
+    return inc;
+  }
+  // 64 levels of an 8x8 block in scan order, at least one non-zero
+  void rand_block8(int *coef) {
+    for (int i = 0; i < 64; ++i) coef[i] = 0;
+    int tc = 1;
+    while (tc < 64 && rng_.below(100) < 70) ++tc;
+    for (int k = 0; k < tc; ++k) {
+      int p = 0;
+      while (p < 63 && rng_.below(100) < 80) ++p;
+      while (p < 63 && coef[p]) ++p;
+      if (coef[p]) {
+        p = 0;
+        while (p < 64 && coef[p]) ++p;
+        if (p >= 64) break;
+      }
+      coef[p] = rand_level();
+    }
+  }
+
   void write_residual(int cur, int cbp, bool i16) {
-    GMb &m = mb_[cur];
-    int coef[16];
+    GMb &m = mb_[static_cast<size_t>(cur)];
+    const bool intra = m.type == 1 || m.type == 2;
+    int coef[64];
     if (i16) {
       rand_block(coef, 0, 15, 30);
-      write_block(coef, 0, 15, 16, nc(cur, 0, 0, false, 0));
-    }
-    for (int k8 = 0; k8 < 4; ++k8)
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const int blk = k8 * 4 + k4, bx = kBlkX[blk], by = kBlkY[blk];
-        if (!((cbp >> k8) & 1)) continue;
-        const int n = nc(cur, bx, by, false, 0);
-        int tc;
-        if (i16) {
-          rand_block(coef, 0, 14, 35);
-          tc = write_block(coef, 0, 14, 15, n);
-        } else {
-          rand_block(coef, 0, 15, 30);
-          tc = write_block(coef, 0, 15, 16, n);
-        }
-        m.nz[by * 4 + bx] = tc;
+      if (cabac_) {
+        if (cab_block(coef, 16, 0, cbf_inc_dc(cur))) m.cbf |= 1u;
+      } else {
+        write_block(coef, 0, 15, 16, nc(cur, 0, 0, false, 0));
       }
+    }
+    for (int k8 = 0; k8 < 4; ++k8) {
+      if (!((cbp >> k8) & 1)) continue;
+      if (m.t8) {  // CABAC only (the decoders refuse CAVLC 8x8 streams)
+        rand_block8(coef);
+        const int tc = cab_block(coef, 64, 5, 0);
+        for (int j = 0; j < 4; ++j) {
+          const int blk = k8 * 4 + j, r = kBlkY[blk] * 4 + kBlkX[blk];
+          m.nz[r] = tc;
+          m.cbf |= 1u << (1 + r);
+        }
+        continue;
+      }
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int blk = k8 * 4 + k4, bx = kBlkX[blk], by = kBlkY[blk], r = by * 4 + bx;
+        int tc;
+        if (cabac_) {
+          if (i16) rand_block(coef, 0, 14, 35);
+          else rand_block(coef, 0, 15, 30);
+          tc = cab_block(coef, i16 ? 15 : 16, i16 ? 1 : 2, cbf_inc_luma(cur, bx, by, intra));
+        } else {
+          const int n = nc(cur, bx, by, false, 0);
+          if (i16) {
+            rand_block(coef, 0, 14, 35);
+            tc = write_block(coef, 0, 14, 15, n);
+          } else {
+            rand_block(coef, 0, 15, 30);
+            tc = write_block(coef, 0, 15, 16, n);
+          }
+        }
+        m.nz[r] = tc;
+        if (tc) m.cbf |= 1u << (1 + r);
+      }
+    }
     if (cbp >> 4)
       for (int pl = 0; pl < 2; ++pl) {
         rand_block(coef, 0, 3, 20);
-        write_block(coef, 0, 3, 4, -1);
+        if (cabac_) {
+          if (cab_block(coef, 4, 3, cbf_inc_chroma(cur, pl, 0, true, intra))) m.cbf |= 1u << (17 + pl);
+        } else {
+          write_block(coef, 0, 3, 4, -1);
+        }
       }
     if ((cbp >> 4) & 2)
       for (int pl = 0; pl < 2; ++pl)
         for (int k = 0; k < 4; ++k) {
-          const int n = nc(cur, k & 1, k >> 1, true, pl);
-          rand_block(coef, 0, 14, 40);
-          m.nzc[pl][k] = write_block(coef, 0, 14, 15, n);
+          int tc;
+          if (cabac_) {
+            rand_block(coef, 0, 14, 40);
+            tc = cab_block(coef, 15, 4, cbf_inc_chroma(cur, pl, k, false, intra));
+          } else {
+            const int n = nc(cur, k & 1, k >> 1, true, pl);
+            rand_block(coef, 0, 14, 40);
+            tc = write_block(coef, 0, 14, 15, n);
+          }
+          m.nzc[pl][k] = tc;
+          if (tc) m.cbf |= 1u << (19 + 4 * pl + k);
         }
   }
 
@@ -312,8 +587,298 @@ class FullWriter {
     int dq = 0;
     if (rng_.below(5) == 0) dq = static_cast<int>(rng_.below(9)) - 4;
     if (qp_ + dq < 12 || qp_ + dq > 44) dq = -dq;
-    bw_->se(dq);
+    if (cabac_) {  // U binarization of the se() mapping; bin 0's context: the previous macroblock's delta
+      const int k = dq > 0 ? 2 * dq - 1 : -2 * dq;
+      cab_.enc(60 + (qpd_prev_ ? 1 : 0), k > 0);
+      if (k > 0) {
+        cab_.enc(62, k > 1);
+        if (k > 1) {
+          for (int i = 2; i < k; ++i) cab_.enc(63, 1);
+          cab_.enc(63, 0);
+        }
+      }
+      qpd_cur_ = dq != 0;
+    } else {
+      bw_->se(dq);
+    }
     qp_ += dq;
+  }
+
+  // ------------------------------------------- syntax elements (CAVLC / CABAC)
+  int nb_a(int cur) const { return loc(cur, -1, 0, 16).mb; }
+  int nb_b(int cur) const { return loc(cur, 0, -1, 16).mb; }
+  // mb_type of an intra macroblock: v 0 I_NxN, 1..24 I_16x16, 25 I_PCM;
+  // base 0 (I slice), 5 (P), 23 (B): Table 9-36 after the slice's prefix
+  void put_i_type(int cur, int v, int base) {
+    if (!cabac_) {
+      bw_->ue(static_cast<uint32_t>(base + v));
+      return;
+    }
+    int sfx = 0, inc0 = 0;
+    if (base == 0) {
+      const int a = nb_a(cur), b = nb_b(cur);
+      inc0 = (a >= 0 && mb_[static_cast<size_t>(a)].type != 1) + (b >= 0 && mb_[static_cast<size_t>(b)].type != 1);
+    } else if (base == 5) {
+      cab_.enc(14, 1);
+      sfx = 17;
+    } else {
+      put_b_type(cur, 23);
+      sfx = 32;
+    }
+    cab_.enc(sfx ? sfx : 3 + inc0, v != 0);
+    if (v == 0) return;
+    cab_.term(v == 25);
+    if (v == 25) return;  // I_PCM: the caller aligns, writes the samples, restarts the engine
+    const int cc = ((v - 1) / 4) % 3, pm = (v - 1) % 4;
+    cab_.enc(sfx ? sfx + 1 : 6, v >= 13);
+    cab_.enc(sfx ? sfx + 2 : 7, cc != 0);
+    if (cc) cab_.enc(sfx ? sfx + 2 : 8, cc == 2);
+    cab_.enc(sfx ? sfx + 3 : 9, pm >> 1);
+    cab_.enc(sfx ? sfx + 3 : 10, pm & 1);
+  }
+  // P inter mb_type 0..3 (Table 9-37 P rows; P_8x8ref0 does not exist in CABAC)
+  void put_p_type(int t) {
+    if (!cabac_) {
+      bw_->ue(static_cast<uint32_t>(t));
+      return;
+    }
+    cab_.enc(14, 0);
+    if (t == 0 || t == 3) {
+      cab_.enc(15, 0);
+      cab_.enc(16, t == 3);
+    } else {
+      cab_.enc(15, 1);
+      cab_.enc(17, t == 1);
+    }
+  }
+  void put_p_sub(int v) {
+    if (!cabac_) {
+      bw_->ue(static_cast<uint32_t>(v));
+      return;
+    }
+    cab_.enc(21, v == 0);
+    if (v == 0) return;
+    cab_.enc(22, v >= 2);
+    if (v >= 2) cab_.enc(23, v == 2);
+  }
+  // B mb_type t 0..22, 23 = the intra prefix (Table 9-37 B rows, ctxIdx 27..35)
+  void put_b_type(int cur, int t) {
+    if (!cabac_) {
+      bw_->ue(static_cast<uint32_t>(t));
+      return;
+    }
+    const int a = nb_a(cur), b = nb_b(cur);
+    cab_.enc(27 + (a >= 0 && !mb_[static_cast<size_t>(a)].d16) + (b >= 0 && !mb_[static_cast<size_t>(b)].d16), t != 0);
+    if (t == 0) return;
+    if (t <= 2) {
+      cab_.enc(30, 0);
+      cab_.enc(32, t - 1);
+      return;
+    }
+    cab_.enc(30, 1);
+    int bits, extra = -1;
+    if (t <= 10) bits = t - 3;
+    else if (t == 11) bits = 14;
+    else if (t == 22) bits = 15;
+    else if (t == 23) bits = 13;
+    else {
+      bits = (t + 4) >> 1;
+      extra = (t + 4) & 1;
+    }
+    cab_.enc(31, (bits >> 3) & 1);
+    cab_.enc(32, (bits >> 2) & 1);
+    cab_.enc(32, (bits >> 1) & 1);
+    cab_.enc(32, bits & 1);
+    if (extra >= 0) cab_.enc(32, extra);
+  }
+  void put_b_sub(int v) {
+    if (!cabac_) {
+      bw_->ue(static_cast<uint32_t>(v));
+      return;
+    }
+    cab_.enc(36, v != 0);
+    if (v == 0) return;
+    if (v <= 2) {
+      cab_.enc(37, 0);
+      cab_.enc(39, v - 1);
+      return;
+    }
+    cab_.enc(37, 1);
+    if (v <= 6) {
+      cab_.enc(38, 0);
+      cab_.enc(39, (v - 3) >> 1);
+      cab_.enc(39, (v - 3) & 1);
+    } else if (v <= 10) {
+      cab_.enc(38, 1);
+      cab_.enc(39, 0);
+      cab_.enc(39, (v - 7) >> 1);
+      cab_.enc(39, (v - 7) & 1);
+    } else {
+      cab_.enc(38, 1);
+      cab_.enc(39, 1);
+      cab_.enc(39, v - 11);
+    }
+  }
+  // condTermFlagN of ref_idx_lX (9.3.3.1.1.6)
+  int ref_cond(int cur, int xN, int yN, int l) const {
+    const Loc L = loc(cur, xN, yN, 16);
+    if (L.mb < 0) return 0;
+    const int p8 = (L.yw / 8) * 2 + L.xw / 8;
+    const GMb &m = mb_[static_cast<size_t>(L.mb)];
+    if ((m.dmask >> p8) & 1) return 0;
+    if (L.mb == cur) return cref_[l][p8] > 0;
+    if (m.type != 0) return 0;
+    return m.ref[l][(L.yw / 4) * 4 + L.xw / 4] > 0;
+  }
+  // ref_idx_lX of the partition at (x0, y0), w8 x h8 quarters
+  void put_ref(int cur, int x0, int y0, int w8, int h8, int l, int v, int nref) {
+    if (!cabac_) {
+      if (nref == 2) bw_->bit(v ? 0 : 1);  // te(v), range 1
+      else bw_->ue(static_cast<uint32_t>(v));
+    } else {
+      cab_.enc(54 + ref_cond(cur, x0 - 1, y0, l) + 2 * ref_cond(cur, x0, y0 - 1, l), v > 0);
+      if (v > 0) {
+        cab_.enc(58, v > 1);
+        if (v > 1) {
+          for (int i = 2; i < v; ++i) cab_.enc(59, 1);
+          cab_.enc(59, 0);
+        }
+      }
+    }
+    for (int qy = 0; qy < h8; ++qy)
+      for (int qx = 0; qx < w8; ++qx) cref_[l][(y0 / 8 + qy) * 2 + x0 / 8 + qx] = v;
+  }
+  int mvd_abs_at(int cur, int xN, int yN, int comp, int l) const {
+    const Loc L = loc(cur, xN, yN, 16);
+    if (L.mb < 0) return 0;
+    const int blk = (L.yw / 4) * 4 + L.xw / 4;
+    if (L.mb == cur) return cmvd_[l][blk][comp];
+    const GMb &m = mb_[static_cast<size_t>(L.mb)];
+    return m.type == 0 ? m.mvda[l][blk][comp] : 0;
+  }
+  void cab_mvd(int base, int sum, int v) {  // UEG3, signedValFlag 1, uCoff 9 (9.3.2.3)
+    static const int kInc[8] = {3, 4, 5, 6, 6, 6, 6, 6};
+    const int a = std::abs(v);
+    cab_.enc(base + (sum < 3 ? 0 : (sum > 32 ? 2 : 1)), a > 0);
+    if (a == 0) return;
+    for (int k = 1; k < 9; ++k) {
+      cab_.enc(base + kInc[k - 1], k < a);
+      if (k >= a) break;
+    }
+    if (a >= 9) cab_.ueg(a - 9, 3);
+    cab_.bypass(v < 0);
+  }
+  // mvd_lX of the (sub-)partition at (sx, sy), pw x ph
+  void put_mvd(int cur, int sx, int sy, int pw, int ph, int l, int dx, int dy) {
+    if (!cabac_) {
+      bw_->se(dx);
+      bw_->se(dy);
+    } else {
+      cab_mvd(40, mvd_abs_at(cur, sx - 1, sy, 0, l) + mvd_abs_at(cur, sx, sy - 1, 0, l), dx);
+      cab_mvd(47, mvd_abs_at(cur, sx - 1, sy, 1, l) + mvd_abs_at(cur, sx, sy - 1, 1, l), dy);
+    }
+    for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
+      for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
+        cmvd_[l][yy * 4 + xx][0] = std::abs(dx);
+        cmvd_[l][yy * 4 + xx][1] = std::abs(dy);
+      }
+  }
+  void put_pred_mode(bool use_pred, int rem) {  // prev_intraNxN_pred_mode_flag / rem_intraNxN_pred_mode
+    if (!cabac_) {
+      bw_->bit(use_pred ? 1 : 0);
+      if (!use_pred) bw_->u(3, static_cast<uint32_t>(rem));
+      return;
+    }
+    cab_.enc(68, use_pred);
+    if (!use_pred)
+      for (int i = 0; i < 3; ++i) cab_.enc(69, (rem >> i) & 1);
+  }
+  void put_chroma_mode(int cur, int cm) {
+    mb_[static_cast<size_t>(cur)].cmode = cm;
+    if (!cabac_) {
+      bw_->ue(static_cast<uint32_t>(cm));
+      return;
+    }
+    int inc = 0;
+    for (const int n : {nb_a(cur), nb_b(cur)})
+      if (n >= 0) {
+        const GMb &m = mb_[static_cast<size_t>(n)];
+        inc += (m.type == 1 || m.type == 2) && m.cmode != 0;
+      }
+    cab_.enc(64 + inc, cm > 0);
+    if (cm > 0) {
+      cab_.enc(67, cm > 1);
+      if (cm > 1) cab_.enc(67, cm > 2);
+    }
+  }
+  void put_cbp(int cur, int cbp, bool intra) {
+    GMb &m = mb_[static_cast<size_t>(cur)];
+    if (!cabac_) {
+      const uint8_t *t = intra ? kCbpIntra : kCbpInter;
+      int code = 0;
+      while (t[code] != cbp) ++code;
+      bw_->ue(static_cast<uint32_t>(code));
+      m.cbp = cbp;
+      return;
+    }
+    int sofar = 0;  // 9.3.3.1.1.4: the current macroblock's bins already coded
+    for (int b8 = 0; b8 < 4; ++b8) {
+      const int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
+      int cond[2];
+      for (int nb = 0; nb < 2; ++nb) {
+        const Loc l = loc(cur, nb ? bx : bx - 1, nb ? by - 1 : by, 16);
+        const int b8n = (l.yw / 8) * 2 + l.xw / 8;
+        if (l.mb < 0) {
+          cond[nb] = 0;
+        } else if (l.mb == cur) {
+          cond[nb] = ((sofar >> b8n) & 1) ? 0 : 1;
+        } else {
+          const GMb &n = mb_[static_cast<size_t>(l.mb)];
+          cond[nb] = n.type == 3 ? 0 : (n.type == 4 ? 1 : (((n.cbp >> b8n) & 1) ? 0 : 1));
+        }
+      }
+      const int bit = (cbp >> b8) & 1;
+      cab_.enc(73 + cond[0] + 2 * cond[1], bit);
+      sofar |= bit << b8;
+    }
+    int ca[2] = {0, 0}, c2[2] = {0, 0};
+    const int nbs[2] = {nb_a(cur), nb_b(cur)};
+    for (int i = 0; i < 2; ++i) {
+      if (nbs[i] < 0) continue;
+      const GMb &n = mb_[static_cast<size_t>(nbs[i])];
+      const int cc = n.type == 3 ? 2 : (n.type == 4 ? 0 : n.cbp >> 4);
+      ca[i] = cc != 0;
+      c2[i] = cc == 2;
+    }
+    const int cc = cbp >> 4;
+    cab_.enc(77 + ca[0] + 2 * ca[1], cc != 0);
+    if (cc) cab_.enc(81 + c2[0] + 2 * c2[1], cc == 2);
+    m.cbp = cbp;
+  }
+  void put_t8(int cur, bool t8) {  // transform_size_8x8_flag (CABAC streams only)
+    mb_[static_cast<size_t>(cur)].t8 = t8;
+    const int a = nb_a(cur), b = nb_b(cur);
+    cab_.enc(399 + (a >= 0 && mb_[static_cast<size_t>(a)].t8) + (b >= 0 && mb_[static_cast<size_t>(b)].t8), t8);
+  }
+  void put_skip(int cur, bool skip, bool b_slice) {  // mb_skip_flag
+    const int a = nb_a(cur), b = nb_b(cur);
+    cab_.enc((b_slice ? 24 : 11) + (a >= 0 && mb_[static_cast<size_t>(a)].type != 4) +
+                 (b >= 0 && mb_[static_cast<size_t>(b)].type != 4),
+             skip);
+  }
+  void begin_mb(int a, int slice) {
+    reset_mb(a, slice);
+    qpd_prev_ = qpd_cur_;
+    qpd_cur_ = false;
+    for (int l = 0; l < 2; ++l) {
+      for (int k = 0; k < 4; ++k) cref_[l][k] = -1;
+      for (int k = 0; k < 16; ++k) cmvd_[l][k][0] = cmvd_[l][k][1] = 0;
+    }
+  }
+  void end_mb(int a, int last) {
+    GMb &m = mb_[static_cast<size_t>(a)];
+    if (m.type == 0) std::memcpy(m.mvda, cmvd_, sizeof m.mvda);
+    if (cabac_) cab_.term(a == last - 1);  // end_of_slice_flag
   }
 
   // valid intra modes
@@ -333,20 +898,25 @@ class FullWriter {
     };
     if (r < 10) {  // I_PCM
       m.type = 3;
-      bw_->ue(static_cast<uint32_t>(base + 25));
+      m.cbp = 0x2f;
+      put_i_type(cur, 25, base);  // CABAC: the terminate bin 1 flushed the engine
       bw_->align_zero();
       uint8_t buf[384];
       for (uint8_t &x : buf) x = static_cast<uint8_t>(rng_.below(256));
       bw_->bytes(buf, 384);
       for (int i = 0; i < 16; ++i) m.nz[i] = 16;
       for (int i = 0; i < 4; ++i) m.nzc[0][i] = m.nzc[1][i] = 16;
+      if (cabac_) cab_.start();   // 9.3.1.2 after pcm_sample data
       return;
     }
-    if (r < 600) {  // I_NxN
+    if (r < 600) {  // I_NxN (Intra_8x8 with transform_size_8x8_flag)
       m.type = 1;
-      bw_->ue(static_cast<uint32_t>(base));
-      for (int k = 0; k < 16; ++k) {
-        const int bx = kBlkX[k], by = kBlkY[k];
+      put_i_type(cur, 0, base);
+      const bool t8 = t8mode_ && rng_.below(2) != 0;
+      if (t8mode_) put_t8(cur, t8);
+      const int nblk = t8 ? 4 : 16, bs = t8 ? 8 : 4;
+      for (int k = 0; k < nblk; ++k) {
+        const int bx = t8 ? (k & 1) * 2 : kBlkX[k], by = t8 ? (k >> 1) * 2 : kBlkY[k];
         // availability of top / left / top-left samples of this block
         auto av = [&](int xN, int yN) {
           const Loc l = loc(cur, xN, yN, 16);
@@ -372,19 +942,15 @@ class FullWriter {
         bool pred_ok = false;
         for (int i = 0; i < n; ++i) pred_ok |= modes[i] == pred;
         const int mode = (pred_ok && rng_.below(2)) ? pred : modes[rng_.below(static_cast<uint32_t>(n))];
-        if (mode == pred) {
-          bw_->bit(1);
-        } else {
-          bw_->bit(0);
-          bw_->u(3, static_cast<uint32_t>(mode < pred ? mode : mode - 1));
-        }
-        m.i4[by * 4 + bx] = mode;
+        put_pred_mode(mode == pred, mode < pred ? mode : mode - 1);
+        // Intra8x8PredMode is kept on each of its 4x4 blocks: the 8.3.1.1 /
+        // 8.3.2.1 neighbour lookups then read the block at the sample position
+        for (int yy = 0; yy < bs / 4; ++yy)
+          for (int xx = 0; xx < bs / 4; ++xx) m.i4[(by + yy) * 4 + bx + xx] = mode;
       }
-      bw_->ue(static_cast<uint32_t>(chroma_mode()));
+      put_chroma_mode(cur, chroma_mode());
       const int cbp = static_cast<int>(rng_.below(16)) | (static_cast<int>(rng_.below(3)) << 4);
-      int code = 0;
-      while (kCbpIntra[code] != cbp) ++code;
-      bw_->ue(static_cast<uint32_t>(code));
+      put_cbp(cur, cbp, true);
       if (cbp) write_qp_delta();
       write_residual(cur, cbp, false);
       return;
@@ -398,8 +964,9 @@ class FullWriter {
     if (la && ta && ca) modes[n++] = 3;
     const int pm = modes[rng_.below(static_cast<uint32_t>(n))];
     const int cc = static_cast<int>(rng_.below(3)), lum = rng_.below(2) ? 15 : 0;
-    bw_->ue(static_cast<uint32_t>(base + 1 + pm + 4 * cc + (lum ? 12 : 0)));
-    bw_->ue(static_cast<uint32_t>(chroma_mode()));
+    m.cbp = (cc << 4) | lum;
+    put_i_type(cur, 1 + pm + 4 * cc + (lum ? 12 : 0), base);
+    put_chroma_mode(cur, chroma_mode());
     write_qp_delta();
     write_residual(cur, (cc << 4) | lum, true);
   }
@@ -409,20 +976,24 @@ class FullWriter {
     m.type = 0;
     const uint32_t r = rng_.below(1000);
     int mb_type = r < 640 ? 0 : (r < 760 ? 1 : (r < 880 ? 2 : (r < 980 ? 3 : 4)));
-    if (mb_type == 4 && nref_ < 1) mb_type = 3;
-    bw_->ue(static_cast<uint32_t>(mb_type));
+    if (mb_type == 4 && (nref_ < 1 || cabac_)) mb_type = 3;  // no P_8x8ref0 in CABAC
+    put_p_type(mb_type);
     const int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
     int sub[4] = {0, 0, 0, 0}, refs[4] = {0, 0, 0, 0};
+    bool small = false;
     if (mb_type >= 3)
       for (int k = 0; k < 4; ++k) {
         sub[k] = static_cast<int>(rng_.below(4));
-        bw_->ue(static_cast<uint32_t>(sub[k]));
+        small |= sub[k] != 0;
+        put_p_sub(sub[k]);
       }
     if (mb_type != 4 && nref_ > 1)
       for (int k = 0; k < nparts; ++k) {
         refs[k] = rng_.below(4) ? 0 : static_cast<int>(rng_.below(static_cast<uint32_t>(nref_)));
-        if (nref_ == 2) bw_->bit(refs[k] ? 0 : 1);  // te(v), range 1
-        else bw_->ue(static_cast<uint32_t>(refs[k]));
+        const int x0 = (mb_type == 2 || mb_type == 3) ? 8 * (k & 1) : 0;
+        const int y0 = mb_type == 1 ? 8 * k : (mb_type == 3 ? 8 * (k >> 1) : 0);
+        put_ref(cur, x0, y0, (mb_type == 0 || mb_type == 1) ? 2 : 1, (mb_type == 0 || mb_type == 2) ? 2 : 1, 0,
+                refs[k], nref_);
       }
     int done = 0;
     for (int k = 0; k < nparts; ++k) {
@@ -449,8 +1020,7 @@ class FullWriter {
         const int dist = bmode_ ? cur_d_ - lst_[0][refs[k]] : refs[k] + 1;
         const int tx = dist * pan_x + static_cast<int>(rng_.below(13)) - 6;
         const int ty = dist * pan_y + static_cast<int>(rng_.below(13)) - 6;
-        bw_->se(tx - px);
-        bw_->se(ty - py);
+        put_mvd(cur, sx, sy, pw, ph, 0, tx - px, ty - py);
         for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
           for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
             const int blk = yy * 4 + xx;
@@ -467,9 +1037,8 @@ class FullWriter {
       if (rng_.below(100) < 35) cbp |= 1 << k8;
     const uint32_t cr = rng_.below(100);
     cbp |= (cr < 60 ? 0 : (cr < 85 ? 1 : 2)) << 4;
-    int code = 0;
-    while (kCbpInter[code] != cbp) ++code;
-    bw_->ue(static_cast<uint32_t>(code));
+    put_cbp(cur, cbp, false);
+    if (t8mode_ && (cbp & 15) && !small) put_t8(cur, rng_.below(2) != 0);
     if (cbp) write_qp_delta();
     write_residual(cur, cbp, false);
   }
@@ -485,15 +1054,18 @@ class FullWriter {
         m.ref[l][i] = -1;
         m.refd[l][i] = -1;
         m.mv[l][i][0] = m.mv[l][i][1] = 0;
+        m.mvda[l][i][0] = m.mvda[l][i][1] = 0;
       }
     }
     for (int i = 0; i < 4; ++i) m.nzc[0][i] = m.nzc[1][i] = 0;
   }
 
+  // slice_data(): CAVLC mb_skip_run, or CABAC mb_skip_flag + end_of_slice_flag
   void write_slice_data(int first, int last, int slice, bool is_p, int pan_x, int pan_y) {
     uint32_t skip_run = 0;
+    qpd_cur_ = false;
     for (int a = first; a < last; ++a) {
-      reset_mb(a, slice);
+      begin_mb(a, slice);
       if (is_p) {
         const uint32_t r = rng_.below(1000);
         if (r < 450) {  // P_Skip
@@ -507,18 +1079,25 @@ class FullWriter {
             m.mv[0][i][1] = py;
             m.refd[0][i] = lst_[0][0];
           }
-          ++skip_run;
+          if (cabac_) put_skip(a, true, false);
+          else ++skip_run;
+          end_mb(a, last);
           continue;
         }
-        bw_->ue(skip_run);
-        skip_run = 0;
+        if (cabac_) {
+          put_skip(a, false, false);
+        } else {
+          bw_->ue(skip_run);
+          skip_run = 0;
+        }
         if (r < 920) write_inter(a, pan_x, pan_y);
         else write_intra(a, true);
       } else {
         write_intra(a, false);
       }
+      end_mb(a, last);
     }
-    if (is_p && skip_run) bw_->ue(skip_run);
+    if (!cabac_ && is_p && skip_run) bw_->ue(skip_run);
   }
 
 
@@ -603,9 +1182,9 @@ class FullWriter {
     else if (r < 60) mb_type = 1 + static_cast<int>(rng_.below(3));
     else if (r < 85) mb_type = 4 + static_cast<int>(rng_.below(18));
     else mb_type = 22;
-    bw_->ue(static_cast<uint32_t>(mb_type));
+    put_b_type(cur, mb_type);
     int shape, pm[4] = {1, 1, 1, 1}, ssh[4] = {0, 0, 0, 0}, subv[4] = {0, 0, 0, 0};
-    if (mb_type == 0) { shape = 0; pm[0] = 0; }
+    if (mb_type == 0) { shape = 0; pm[0] = 0; m.d16 = true; }
     else if (mb_type <= 3) { shape = 0; pm[0] = mb_type; }
     else if (mb_type < 22) { shape = (mb_type & 1) ? 2 : 1; pm[0] = kPart[mb_type][0]; pm[1] = kPart[mb_type][1]; }
     else shape = 3;
@@ -616,6 +1195,15 @@ class FullWriter {
         pm[k] = kSub[subv[k]][0];
         ssh[k] = kSub[subv[k]][1];
       }
+    // direct-predicted quarters (ref_idx contexts treat them as refIdx 0);
+    // sub-8x8 partitions rule out the 8x8 transform (direct ones do not:
+    // direct_8x8_inference_flag is 1)
+    bool small = false;
+    for (int k = 0; k < (shape == 3 ? 4 : 0); ++k) {
+      if (pm[k] == 0) m.dmask |= 1 << k;
+      else small |= ssh[k] != 0;
+    }
+    if (mb_type == 0) m.dmask = 0xf;
     int refs[2][4];
     for (int l = 0; l < 2; ++l)
       for (int k = 0; k < 4; ++k)
@@ -670,20 +1258,38 @@ class FullWriter {
     }
     // syntax order (7.3.5.1 / 7.3.5.2)
     if (shape == 3)
-      for (int k = 0; k < 4; ++k) bw_->ue(static_cast<uint32_t>(subv[k]));
+      for (int k = 0; k < 4; ++k) put_b_sub(subv[k]);
+    auto part = [&](int k, int *x0, int *y0, int *pw, int *ph) {
+      if (shape == 0) { *pw = *ph = 16; *x0 = *y0 = 0; }
+      else if (shape == 1) { *pw = 16; *ph = 8; *x0 = 0; *y0 = 8 * k; }
+      else if (shape == 2) { *pw = 8; *ph = 16; *x0 = 8 * k; *y0 = 0; }
+      else { *pw = *ph = 8; *x0 = 8 * (k & 1); *y0 = 8 * (k >> 1); }
+    };
     for (int l = 0; l < 2; ++l)
       for (int k = 0; k < nparts; ++k) {
         if (refs[l][k] < 0 || nlst_[l] < 2) continue;
-        if (nlst_[l] == 2) bw_->bit(refs[l][k] ? 0 : 1);
-        else bw_->ue(static_cast<uint32_t>(refs[l][k]));
+        int x0, y0, pw, ph;
+        part(k, &x0, &y0, &pw, &ph);
+        put_ref(cur, x0, y0, pw / 8, ph / 8, l, refs[l][k], nlst_[l]);
       }
     for (int l = 0; l < 2; ++l)
       for (int k = 0; k < nparts; ++k) {
         if (refs[l][k] < 0) continue;
+        int x0, y0, pw, ph;
+        part(k, &x0, &y0, &pw, &ph);
         const int nsub = shape < 3 ? 1 : (ssh[k] == 0 ? 1 : (ssh[k] == 3 ? 4 : 2));
+        if (shape == 3) {
+          pw = (ssh[k] == 0 || ssh[k] == 1) ? 8 : 4;
+          ph = (ssh[k] == 0 || ssh[k] == 2) ? 8 : 4;
+        }
         for (int q = 0; q < nsub; ++q) {
-          bw_->se(mvd[l][k][q][0]);
-          bw_->se(mvd[l][k][q][1]);
+          int sx = x0, sy = y0;
+          if (shape == 3) {
+            if (ssh[k] == 1) sy += 4 * q;
+            else if (ssh[k] == 2) sx += 4 * q;
+            else if (ssh[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
+          }
+          put_mvd(cur, sx, sy, pw, ph, l, mvd[l][k][q][0], mvd[l][k][q][1]);
         }
       }
     int cbp = 0;
@@ -691,30 +1297,40 @@ class FullWriter {
       if (rng_.below(100) < 30) cbp |= 1 << k8;
     const uint32_t cr = rng_.below(100);
     cbp |= (cr < 60 ? 0 : (cr < 85 ? 1 : 2)) << 4;
-    int code = 0;
-    while (kCbpInter[code] != cbp) ++code;
-    bw_->ue(static_cast<uint32_t>(code));
+    put_cbp(cur, cbp, false);
+    if (t8mode_ && (cbp & 15) && !small) put_t8(cur, rng_.below(2) != 0);
     if (cbp) write_qp_delta();
     write_residual(cur, cbp, false);
   }
 
   void write_slice_data_b(int first, int last, int slice, int pan_x, int pan_y) {
     uint32_t skip_run = 0;
+    qpd_cur_ = false;
     for (int a = first; a < last; ++a) {
-      reset_mb(a, slice);
+      begin_mb(a, slice);
       const uint32_t r = rng_.below(1000);
       if (r < 350) {  // B_Skip
-        mb_[static_cast<size_t>(a)].type = 4;
+        GMb &m = mb_[static_cast<size_t>(a)];
+        m.type = 4;
+        m.d16 = true;
+        m.dmask = 0xf;
         direct(a, 0xffff);
-        ++skip_run;
+        if (cabac_) put_skip(a, true, true);
+        else ++skip_run;
+        end_mb(a, last);
         continue;
       }
-      bw_->ue(skip_run);
-      skip_run = 0;
+      if (cabac_) {
+        put_skip(a, false, true);
+      } else {
+        bw_->ue(skip_run);
+        skip_run = 0;
+      }
       if (r < 950) write_b_inter(a, pan_x, pan_y);
       else write_intra_b(a);
+      end_mb(a, last);
     }
-    if (skip_run) bw_->ue(skip_run);
+    if (!cabac_ && skip_run) bw_->ue(skip_run);
   }
   void write_intra_b(int a) { write_intra(a, true, 23); }
 
@@ -808,6 +1424,7 @@ void FullWriter::run() {
         if (idr) { bw.u(1, 0); bw.u(1, 0); }
         else bw.u(1, 0);
       }
+      if (cabac_ && !idr) bw.ue(0);  // cabac_init_idc
       qp_ = pic_qp;
       bw.se(pic_qp - 26);
       const uint32_t dr = rng_.below(20);
@@ -817,8 +1434,13 @@ void FullWriter::run() {
         bw.se(static_cast<int>(rng_.below(7)) - 3);
         bw.se(static_cast<int>(rng_.below(7)) - 3);
       }
+      if (cabac_) {  // cabac_alignment_one_bit, then 9.3.1 initialisation
+        while (!bw.aligned()) bw.bit(1);
+        cab_.init(&bw, idr, pic_qp);
+      }
       write_slice_data(first, last, slice, !idr, pan_x, pan_y);
-      bw.trailing();
+      if (cabac_) bw.align_zero();  // the flush wrote the rbsp_stop_one_bit
+      else bw.trailing();
       append_nal(sample, idr ? 0x65 : (nonref ? 0x01 : 0x41), bw.data());
       first = last;
     }
@@ -1012,6 +1634,7 @@ void FullWriter::run_b() {
         if (idr) { bw.u(1, 0); bw.u(1, 0); }
         else bw.u(1, 0);
       }
+      if (cabac_ && !idr) bw.ue(0);  // cabac_init_idc
       qp_ = pic_qp;
       bw.se(pic_qp - 26);
       const uint32_t dr = rng_.below(20);
@@ -1021,10 +1644,15 @@ void FullWriter::run_b() {
         bw.se(static_cast<int>(rng_.below(7)) - 3);
         bw.se(static_cast<int>(rng_.below(7)) - 3);
       }
+      if (cabac_) {
+        while (!bw.aligned()) bw.bit(1);
+        cab_.init(&bw, idr, pic_qp);
+      }
       const int pxn = pxs[static_cast<size_t>(pc.d)], pyn = pys[static_cast<size_t>(pc.d)];
       if (is_b) write_slice_data_b(first, last, slice, pxn, pyn);
       else write_slice_data(first, last, slice, !idr, pxn, pyn);
-      bw.trailing();
+      if (cabac_) bw.align_zero();
+      else bw.trailing();
       append_nal(sample, idr ? 0x65 : (pc.ref ? 0x41 : 0x01), bw.data());
       first = last;
     }
@@ -1081,11 +1709,20 @@ void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int crop_r = mbw * 16 - P.width, crop_b = mbh * 16 - P.height;
   const bool bm = (P.edge_cases & 32) != 0;
+  const bool cabac = (P.edge_cases & 1024) != 0, t8 = cabac && (P.edge_cases & 2048) != 0;
+  const int profile = t8 ? 100 : ((bm || cabac) ? 77 : 66);  // High / Main / Constrained Baseline
   BitWriter s;
-  s.u(8, bm ? 77 : 66);  // B pictures: Main profile
-  s.u(8, bm ? 0x00 : 0xC0);
+  s.u(8, static_cast<uint32_t>(profile));
+  s.u(8, profile == 66 ? 0xC0 : 0x00);
   s.u(8, static_cast<uint32_t>(level));
   s.ue(0);
+  if (profile == 100) {
+    s.ue(1);    // chroma_format_idc 4:2:0
+    s.ue(0);    // bit_depth_luma_minus8
+    s.ue(0);    // bit_depth_chroma_minus8
+    s.u(1, 0);  // qpprime_y_zero_transform_bypass_flag
+    s.u(1, 0);  // seq_scaling_matrix_present_flag
+  }
   s.ue(kLog2MaxFrameNum - 4);
   if (bm) {
     s.ue(0);  // pic_order_cnt_type 0
@@ -1116,7 +1753,7 @@ void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t
   BitWriter p;
   p.ue(0);
   p.ue(0);
-  p.u(1, 0);                                   // CAVLC
+  p.u(1, cabac ? 1 : 0);                       // entropy_coding_mode_flag
   p.u(1, 0);
   p.ue(0);
   p.ue(kPpsRefDefault - 1);
@@ -1129,6 +1766,11 @@ void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t
   p.u(1, 1);                                   // deblocking_filter_control_present_flag
   p.u(1, (P.edge_cases & 16) ? 1 : 0);         // constrained_intra_pred_flag
   p.u(1, 0);
+  if (t8) {
+    p.u(1, 1);                                 // transform_8x8_mode_flag
+    p.u(1, 0);                                 // pic_scaling_matrix_present_flag
+    p.se(static_cast<int>(P.seed % 3) - 1);    // second_chroma_qp_index_offset
+  }
   p.trailing();
   pps_nal->clear();
   pps_nal->push_back(0x68);

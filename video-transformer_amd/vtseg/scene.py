@@ -278,7 +278,8 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 nonref_refresh: bool = False, chunks: int = 0, coding: str = "subset",
                 constrained_intra: bool = False, bframes: bool = False,
                 weighted: str | None = None, temporal_direct: bool = False,
-                chroma_deblock: bool = False) -> dict:
+                chroma_deblock: bool = False, cabac: bool = False,
+                transform_8x8: bool = False) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
     and the ground-truth scene-cut frames.  coding="full" only: ``bframes`` codes
     B pictures (Main profile, POC type 0, composition offsets in the MP4),
@@ -287,7 +288,10 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     spatial direct prediction.  coding="subset" only: ``chroma_deblock``
     turns the deblocking filter on at QPY 3 with chroma_qp_index_offset 12 and
     filter offsets +12, so only chroma edges filter (a stream the subset
-    kernels must refuse)."""
+    kernels must refuse).  coding="full" only: ``cabac`` writes the same syntax
+    decisions with CABAC (cabac_init_idc 0, Main profile; x264's default entropy
+    coder) and ``transform_8x8`` (with cabac, High profile) adds Intra_8x8 and
+    8x8-transform inter macroblocks."""
     p = _lib.SynthParams()
     p.width, p.height, p.fps_num, p.fps_den = width, height, fps, 1
     p.n_frames, p.seed = n_frames, seed
@@ -300,6 +304,12 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     p.coding = {"subset": 0, "full": 1}[coding]
     if constrained_intra:
         p.edge_cases |= 16
+    if cabac or transform_8x8:
+        if coding != "full":
+            raise ValueError("cabac / transform_8x8 need coding='full'")
+        if transform_8x8 and not cabac:
+            raise ValueError("transform_8x8 needs cabac (8x8 CAVLC streams are refused)")
+        p.edge_cases |= 1024 | (2048 if transform_8x8 else 0)
     if chroma_deblock:
         if coding != "subset":
             raise ValueError("chroma_deblock is a subset-stream edge case")
