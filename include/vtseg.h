@@ -314,9 +314,9 @@ int vts_close(vts_ctx *ctx);
  * an area filter downscales it to (w, height) with w = ffmpeg's scale=-2
  * width, and a device encoder writes H.264 Constrained Baseline: IDR (all
  * I_PCM) every keyint frames (and at scene cuts if asked), P pictures of full-search
- * integer motion without residual (P_L0_16x16 / P_Skip) or I_PCM where the
- * motion prediction misses by more than max_mb_sad; one slice per macroblock
- * row; MP4 (moov at the end), video only.  DESIGN.md §11. */
+ * integer motion (P_L0_16x16 / P_Skip) with a quantised residual (qp), I_PCM
+ * where that residual would cost more; one slice per macroblock row; MP4
+ * (moov at the end), video only.  DESIGN.md §11. */
 typedef struct vts_transcode_params {
   int32_t height;          /* output display height, even; 0 = 360            */
   int32_t search_range;    /* full-search motion range in luma pixels 0..16;
@@ -330,6 +330,12 @@ typedef struct vts_transcode_params {
   int32_t idr_at_cuts;     /* 1: also an IDR at every scene cut (an IDR is all
                               I_PCM, so off by default: a cut P picture falls
                               back to I_PCM only where motion misses)         */
+  int32_t qp;              /* residual coding of P macroblocks at this QP (flat
+                              scaling): P_L0_16x16 + quantised 4x4 residual,
+                              I_PCM only where the residual's CAVLC bits would
+                              exceed the I_PCM payload; 0 = default 28 (the
+                              reference's CRF); < 0 = no residual (inter within
+                              max_mb_sad, else I_PCM)                        */
 } vts_transcode_params;
 
 typedef struct vts_transcode_info {

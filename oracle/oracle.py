@@ -81,7 +81,7 @@ def lib() -> C.CDLL:
                                     C.c_void_p, C.c_void_p, C.c_void_p]
         _lib.or_pick_level.argtypes = [C.c_int, C.c_double]
         _lib.or_transcode.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p,
-                                      C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_void_p]
     return _lib
@@ -372,17 +372,20 @@ def sps_pps(mbw: int, mbh: int, crop_r: int, crop_b: int, fps: float) -> tuple[b
 def transcode(frames: np.ndarray, width: int, height: int, scores: np.ndarray, *,
               threshold: float = 0.08, out_height: int = 360, search_range: int = 8,
               max_mb_sad: int = 1536, keyint: int = 250, idr_at_cuts: bool = False,
-              want_recon: bool = False) -> dict:
+              want_recon: bool = False, qp: int = 28) -> dict:
     """The upload transcode of display-size NV12 frames [F, H*3/2, W] with
     their scene scores: output samples (bytes), per-frame sizes / sync flags,
-    SPS/PPS, stats and (optionally) the encoder's reconstruction."""
+    SPS/PPS, stats and (optionally) the encoder's reconstruction.  qp >= 1:
+    P macroblocks carry a quantised residual at that QP (I_PCM only where the
+    residual would cost more); qp <= 0: the round-2 encoder (no residual,
+    I_PCM where the prediction misses by more than max_mb_sad)."""
     F = frames.shape[0]
     sw = small_width(width, height, out_height)
     cw, ch = (sw + 15) & ~15, (out_height + 15) & ~15
     mbw, mbh = cw // 16, ch // 16
     fr = np.ascontiguousarray(frames, np.uint8)
     sc = np.ascontiguousarray(scores, np.float32)
-    cap = F * mbh * (64 + mbw * 420 + 8) + 64
+    cap = F * mbh * (64 + mbw * 600 + 8) + 64
     out = np.zeros(cap, np.uint8)
     off = np.zeros(F, np.int64)
     size = np.zeros(F, np.int64)
@@ -391,7 +394,8 @@ def transcode(frames: np.ndarray, width: int, height: int, scores: np.ndarray, *
     stats = np.zeros(4, np.int64)
     n = C.c_int64(0)
     rc = lib().or_transcode(fr.ctypes.data, F, width, height, sc.ctypes.data, threshold,
-                            int(idr_at_cuts), out_height, search_range, max_mb_sad, keyint, out.ctypes.data, cap,
+                            int(idr_at_cuts), out_height, search_range, max_mb_sad, keyint, int(qp),
+                            out.ctypes.data, cap,
                             off.ctypes.data, size.ctypes.data, sync.ctypes.data,
                             recon.ctypes.data if recon is not None else None,
                             stats.ctypes.data, C.byref(n))

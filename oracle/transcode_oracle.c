@@ -32,6 +32,19 @@
  *     first, then raster order; first minimum wins); inter (P_L0_16x16 or
  *     P_Skip, no residual) if luma+chroma SAD of its prediction (chroma by
  *     8.4.2.2.2) <= T_mb, else I_PCM.
+ *   - residual coding (qp >= 1, the default since round 3): the best motion
+ *     is always tried with a quantised residual at QP qp (flat scaling,
+ *     chroma_qp_index_offset 0): per 4x4 block the forward core transform
+ *     W = Cf X Cf^T, levels sign(W) min(2047, (|W| MF + f) >> qbits),
+ *     qbits = 15 + qp / 6, f = 2^qbits / 6, MF by position class; chroma DC
+ *     through the 2x2 Hadamard at (qbits + 1, 2f); the reconstruction is the
+ *     decoder's (8.5.12 scaling + inverse transform, chroma DC 8.5.11).  A
+ *     macroblock stays inter when an upper bound of its residual's CAVLC bits
+ *     (every code exact but coeff_token, taken as the longest over the nC
+ *     classes) is <= 3072 (the I_PCM payload), else it is I_PCM; P_Skip when
+ *     its motion is (0, 0) and nothing is coded.  cbp, mb_qp_delta 0 and
+ *     residual_block_cavlc with nC from the left macroblock (the one above is
+ *     another slice) as 7.3.5.3 / 9.2.1 write them.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -223,8 +236,246 @@ int or_sps_pps(int mbw, int mbh, int crop_r, int crop_b, int level, uint8_t *sps
 /* ------------------------------------------------------- encoder */
 
 static int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+/* Table 9-4 (chroma_format_idc 1), inter column: codeNum -> coded_block_pattern */
+static const int CBP_P[48] = {0,  16, 1,  2,  4,  8,  32, 3,  5,  10, 12, 15, 47, 7,  11, 13,
+                              14, 6,  9,  31, 35, 37, 42, 44, 33, 34, 36, 40, 39, 43, 45, 46,
+                              17, 18, 20, 24, 19, 21, 26, 28, 23, 27, 29, 30, 22, 25, 38, 41};
 
-typedef struct { int pcm, mvx, mvy; } or_mb;  /* mv in quarter-pel */
+typedef struct {
+  int pcm, mvx, mvy;  /* mv in quarter-pel */
+  int cbp;            /* coded_block_pattern of an inter macroblock */
+  int16_t lv[384];    /* levels in scan order: luma by luma4x4BlkIdx (16 x 16), Cb / Cr DC (2 x 4),
+                         Cb / Cr AC by chroma4x4BlkIdx (8 x 15) */
+} or_mb;
+
+/* ------------------------------------------------------ residual coding */
+
+const char *fo_table_code(int table, int a, int b, int c);  /* h264_full_oracle.c: the standard's strings */
+static int code_len(int table, int a, int b, int c) {
+  const char *s = fo_table_code(table, a, b, c);
+  return s ? (int)strlen(s) : -1;
+}
+static void put_code(or_bw *b, int table, int a, int bb, int c) {
+  const char *s = fo_table_code(table, a, bb, c);
+  for (; s && *s; s++) bw_bit(b, (uint32_t)(*s - '0'));
+}
+
+static const int ZZ[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15}; /* 8.5.6 */
+/* luma4x4BlkIdx -> raster 4x4 position (6.4.3) */
+static const int BLK_X[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
+static const int BLK_Y[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
+/* quantisation multipliers by qP % 6 and position class (0: both coordinates
+ * even, 1: both odd, 2: mixed); the encoder's choice, the inverse of 8.5.9's
+ * v = {10, 16, 13} ... so that (v MF) ~ 2^17 */
+static const int MF[6][3] = {{13107, 5243, 8066}, {11916, 4660, 7490}, {10082, 4194, 6554},
+                             {9362, 3647, 5825},  {8192, 3355, 5243},  {7282, 2893, 4559}};
+static const int NV[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+static const int QPC[52] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
+                            18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 32, 33,
+                            34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+static int pos_class(int i, int j) { return (!(i & 1) && !(j & 1)) ? 0 : ((i & 1) && (j & 1) ? 1 : 2); }
+
+/* W = Cf X Cf^T, Cf = [1 1 1 1; 2 1 -1 -2; 1 -1 -1 1; 1 -2 2 -1]; raster */
+static void fwd4(const int *x, int *w) {
+  static const int Cf[4][4] = {{1, 1, 1, 1}, {2, 1, -1, -2}, {1, -1, -1, 1}, {1, -2, 2, -1}};
+  int t[16];
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 4; k++) {
+      int a = 0;
+      for (int j = 0; j < 4; j++) a += x[i * 4 + j] * Cf[k][j];
+      t[i * 4 + k] = a;
+    }
+  for (int k = 0; k < 4; k++)
+    for (int c = 0; c < 4; c++) {
+      int a = 0;
+      for (int i = 0; i < 4; i++) a += Cf[k][i] * t[i * 4 + c];
+      w[k * 4 + c] = a;
+    }
+}
+static int quant1(int w, int mf, int qbits, int64_t f) {
+  int64_t z = ((int64_t)abs(w) * mf + f) >> qbits;
+  if (z > 2047) z = 2047;
+  return w < 0 ? -(int)z : (int)z;
+}
+/* 8.5.12.1 scaling (flat) + 8.5.12.2 inverse transform; dc_done: c[0] already scaled */
+static void idct4(const int *c, int qp, int dc_done, int *r) {
+  int d[16], f[16];
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      int k = i * 4 + j;
+      if (k == 0 && dc_done) { d[0] = c[0]; continue; }
+      int ls = 16 * NV[qp % 6][pos_class(i, j)];
+      d[k] = qp >= 24 ? (c[k] * ls) << (qp / 6 - 4) : (c[k] * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+    }
+  for (int i = 0; i < 4; i++) {
+    int e0 = d[i * 4] + d[i * 4 + 2], e1 = d[i * 4] - d[i * 4 + 2];
+    int e2 = (d[i * 4 + 1] >> 1) - d[i * 4 + 3], e3 = d[i * 4 + 1] + (d[i * 4 + 3] >> 1);
+    f[i * 4] = e0 + e3; f[i * 4 + 1] = e1 + e2; f[i * 4 + 2] = e1 - e2; f[i * 4 + 3] = e0 - e3;
+  }
+  for (int j = 0; j < 4; j++) {
+    int g0 = f[j] + f[8 + j], g1 = f[j] - f[8 + j];
+    int g2 = (f[4 + j] >> 1) - f[12 + j], g3 = f[4 + j] + (f[12 + j] >> 1);
+    r[j] = (g0 + g3 + 32) >> 6; r[4 + j] = (g1 + g2 + 32) >> 6;
+    r[8 + j] = (g1 - g2 + 32) >> 6; r[12 + j] = (g0 - g3 + 32) >> 6;
+  }
+}
+
+/* residual_block_cavlc of levels lv[0, maxNum) (scan order) with nC (-1:
+ * chroma DC); bits to b, or (b == NULL) only counted; coeff_token counted as
+ * the longest code over the nC classes when nC < -1 (the bound) */
+static int block_bits(or_bw *b, const int16_t *lv, int maxNum, int nC) {
+  int pos[16], lev[16], tc = 0, bits = 0;
+  for (int i = maxNum - 1; i >= 0; i--)
+    if (lv[i]) { pos[tc] = i; lev[tc++] = lv[i]; }
+  int t1 = 0;
+  while (t1 < tc && t1 < 3 && (lev[t1] == 1 || lev[t1] == -1)) t1++;
+  if (nC < -1) {  /* upper bound over every nC class: Table 9-5 columns and the 6-bit FLC */
+    int m = 6;
+    for (int c = 0; c < 3; c++) { int l = code_len(0, c, tc, t1); if (l > m) m = l; }
+    bits += m;
+  } else if (nC >= 8) {
+    bits += 6;
+    if (b) bw_u(b, 6, tc == 0 ? 3u : (uint32_t)(((tc - 1) << 2) | t1));
+  } else {
+    int col = nC == -1 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+    bits += code_len(0, col, tc, t1);
+    if (b) put_code(b, 0, col, tc, t1);
+  }
+  if (tc == 0) return bits;
+  for (int i = 0; i < t1; i++) { bits++; if (b) bw_bit(b, lev[i] < 0); }
+  int sl = (tc > 10 && t1 < 3) ? 1 : 0;
+  for (int i = t1; i < tc; i++) {  /* 9.2.2.1 inverted */
+    int level = lev[i];
+    int code = level > 0 ? 2 * level - 2 : -2 * level - 1;
+    if (i == t1 && t1 < 3) code -= 2;
+    int prefix, suffix = 0, ssize = 0;
+    if (sl == 0) {
+      if (code < 14) prefix = code;
+      else if (code < 30) { prefix = 14; suffix = code - 14; ssize = 4; }
+      else { prefix = 15; suffix = code - 30; ssize = 12; }
+    } else {
+      if (code < (15 << sl)) { prefix = code >> sl; suffix = code & ((1 << sl) - 1); ssize = sl; }
+      else { prefix = 15; suffix = code - (15 << sl); ssize = 12; }
+    }
+    bits += prefix + 1 + ssize;
+    if (b) {
+      for (int z = 0; z < prefix; z++) bw_bit(b, 0);
+      bw_bit(b, 1);
+      if (ssize) bw_u(b, ssize, (uint32_t)suffix);
+    }
+    if (sl == 0) sl = 1;
+    if (abs(level) > (3 << (sl - 1)) && sl < 6) sl++;
+  }
+  int zeros = pos[0] + 1 - tc;
+  if (tc < maxNum) {
+    int t = maxNum == 4 ? 2 : 1;
+    bits += code_len(t, tc - 1, zeros, 0);
+    if (b) put_code(b, t, tc - 1, zeros, 0);
+  }
+  for (int i = 0; i < tc - 1 && zeros > 0; i++) {
+    int run = pos[i] - pos[i + 1] - 1, row = (zeros < 7 ? zeros : 7) - 1;
+    bits += code_len(3, row, run, 0);
+    if (b) put_code(b, 3, row, run, 0);
+    zeros -= run;
+  }
+  return bits;
+}
+
+/* Quantise the macroblock's residual (src - prediction) at qp, reconstruct
+ * into ry / ru / rv (16x16, 8x8, 8x8 samples) and return the residual's
+ * CAVLC bit bound; levels and cbp into m. */
+static int residual_mb(const uint8_t *sy, const uint8_t *su, const uint8_t *sv, const uint8_t *py,
+                       const uint8_t *pu, const uint8_t *pv, int qp, or_mb *m, uint8_t *ry, uint8_t *ru,
+                       uint8_t *rv) {
+  int qbits = 15 + qp / 6;
+  int64_t f = ((int64_t)1 << qbits) / 6;
+  int cbp = 0, bound = 0, nz[16];
+  memset(m->lv, 0, sizeof m->lv);
+  for (int k = 0; k < 16; k++) {  /* luma, luma4x4BlkIdx order */
+    int bx = BLK_X[k] * 4, by = BLK_Y[k] * 4, x[16], w[16], z[16], r[16];
+    for (int i = 0; i < 4; i++)
+      for (int j = 0; j < 4; j++) x[i * 4 + j] = sy[(by + i) * 16 + bx + j] - py[(by + i) * 16 + bx + j];
+    fwd4(x, w);
+    nz[k] = 0;
+    for (int i = 0; i < 4; i++)
+      for (int j = 0; j < 4; j++) {
+        z[i * 4 + j] = quant1(w[i * 4 + j], MF[qp % 6][pos_class(i, j)], qbits, f);
+        nz[k] |= z[i * 4 + j] != 0;
+      }
+    for (int s = 0; s < 16; s++) m->lv[16 * k + s] = (int16_t)z[ZZ[s]];
+    idct4(z, qp, 0, r);
+    for (int i = 0; i < 4; i++)
+      for (int j = 0; j < 4; j++) {
+        int v = py[(by + i) * 16 + bx + j] + r[i * 4 + j];
+        ry[(by + i) * 16 + bx + j] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+      }
+    if (nz[k]) cbp |= 1 << (k >> 2);
+  }
+  for (int k8 = 0; k8 < 4; k8++)
+    if ((cbp >> k8) & 1)
+      for (int k = 4 * k8; k < 4 * k8 + 4; k++) bound += block_bits(NULL, m->lv + 16 * k, 16, -2);
+  int qpc = QPC[qp], cqb = 15 + qpc / 6;
+  int64_t cf = ((int64_t)1 << cqb) / 6;
+  int dcnz = 0, acnz = 0, acz[2][4][16], dcl[2][4];
+  for (int pl = 0; pl < 2; pl++) {
+    const uint8_t *s = pl ? sv : su, *p = pl ? pv : pu;
+    int wdc[4];
+    for (int k = 0; k < 4; k++) {
+      int bx = (k & 1) * 4, by = (k >> 1) * 4, x[16], w[16];
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) x[i * 4 + j] = s[(by + i) * 8 + bx + j] - p[(by + i) * 8 + bx + j];
+      fwd4(x, w);
+      wdc[k] = w[0];
+      acz[pl][k][0] = 0;
+      for (int q = 1; q < 16; q++) {
+        int i = q >> 2, j = q & 3;
+        acz[pl][k][q] = quant1(w[q], MF[qpc % 6][pos_class(i, j)], cqb, cf);
+        acnz |= acz[pl][k][q] != 0;
+      }
+      for (int sidx = 1; sidx < 16; sidx++) m->lv[264 + pl * 60 + k * 15 + sidx - 1] = (int16_t)acz[pl][k][ZZ[sidx]];
+    }
+    int fd[4] = {wdc[0] + wdc[1] + wdc[2] + wdc[3], wdc[0] - wdc[1] + wdc[2] - wdc[3],
+                 wdc[0] + wdc[1] - wdc[2] - wdc[3], wdc[0] - wdc[1] - wdc[2] + wdc[3]};
+    for (int k = 0; k < 4; k++) {
+      dcl[pl][k] = quant1(fd[k], MF[qpc % 6][0], cqb + 1, 2 * cf);
+      dcnz |= dcl[pl][k] != 0;
+      m->lv[256 + 4 * pl + k] = (int16_t)dcl[pl][k];
+    }
+  }
+  int cc = acnz ? 2 : (dcnz ? 1 : 0);
+  cbp |= cc << 4;
+  if (cc) for (int pl = 0; pl < 2; pl++) bound += block_bits(NULL, m->lv + 256 + 4 * pl, 4, -1);
+  if (cc == 2) for (int b = 0; b < 8; b++) bound += block_bits(NULL, m->lv + 264 + 15 * b, 15, -2);
+  /* chroma reconstruction (8.5.11: DC through the 2x2 transform, then 8.5.12) */
+  for (int pl = 0; pl < 2; pl++) {
+    const int *c = dcl[pl];
+    int F[4] = {c[0] + c[1] + c[2] + c[3], c[0] - c[1] + c[2] - c[3], c[0] + c[1] - c[2] - c[3],
+                c[0] - c[1] - c[2] + c[3]};
+    const uint8_t *p = pl ? pv : pu;
+    uint8_t *rr = pl ? rv : ru;
+    for (int k = 0; k < 4; k++) {
+      int co[16], r[16], bx = (k & 1) * 4, by = (k >> 1) * 4;
+      for (int q = 0; q < 16; q++) co[q] = cc == 2 ? acz[pl][k][q] : 0;
+      co[0] = ((F[k] * 16 * NV[qpc % 6][0]) << (qpc / 6)) >> 5;
+      idct4(co, qpc, 1, r);
+      for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+          int v = p[(by + i) * 8 + bx + j] + r[i * 4 + j];
+          rr[(by + i) * 8 + bx + j] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+        }
+    }
+  }
+  /* without a luma 8x8 bit its levels are not coded: the decoder sees zeros */
+  for (int k8 = 0; k8 < 4; k8++)
+    if (!((cbp >> k8) & 1))
+      for (int k = 4 * k8; k < 4 * k8 + 4; k++) {
+        int bx = BLK_X[k] * 4, by = BLK_Y[k] * 4;
+        for (int i = 0; i < 4; i++)
+          for (int j = 0; j < 4; j++) ry[(by + i) * 16 + bx + j] = py[(by + i) * 16 + bx + j];
+      }
+  m->cbp = cbp;
+  return bound;
+}
 
 /* prediction of one macroblock from ref (coded NV12 cw x ch), integer luma
  * motion (dx, dy); chroma 8.4.2.2.2 with edge clamping */
@@ -251,9 +502,9 @@ static void predict_mb(const uint8_t *ref, int cw, int ch, int mx, int my, int d
     }
 }
 
-/* encode one P picture's decisions and reconstruction */
+/* encode one P picture's decisions and reconstruction (qp >= 1: residual coding) */
 static void encode_p(const uint8_t *src, const uint8_t *ref, uint8_t *rec, int cw, int ch, int R,
-                     int T, or_mb *mbs) {
+                     int T, int qp, or_mb *mbs) {
   int mbw = cw / 16, mbh = ch / 16;
   const uint8_t *suv = src + (int64_t)cw * ch;
   uint8_t *ruv = rec + (int64_t)cw * ch;
@@ -285,7 +536,31 @@ static void encode_p(const uint8_t *src, const uint8_t *ref, uint8_t *rec, int c
           cost += abs((int)pu[j * 8 + i] - (int)suv[o]) + abs((int)pv[j * 8 + i] - (int)suv[o + 1]);
         }
       or_mb *m = &mbs[my * mbw + mx];
-      int inter = T >= 0 && cost <= T;
+      m->cbp = 0;
+      int inter;
+      if (qp >= 1) {  /* residual coding: inter unless the residual costs more than I_PCM */
+        uint8_t sy[256], su[64], sv[64];
+        for (int j = 0; j < 16; j++)
+          for (int i = 0; i < 16; i++) sy[j * 16 + i] = src[(int64_t)(my * 16 + j) * cw + mx * 16 + i];
+        for (int j = 0; j < 8; j++)
+          for (int i = 0; i < 8; i++) {
+            int64_t o = (int64_t)(my * 8 + j) * cw + 2 * (mx * 8 + i);
+            su[j * 8 + i] = suv[o];
+            sv[j * 8 + i] = suv[o + 1];
+          }
+        uint8_t ry[256], ru[64], rv[64];
+        int bound = residual_mb(sy, su, sv, py, pu, pv, qp, m, ry, ru, rv);
+        inter = T >= 0 && bound <= 3072;
+        if (inter) {
+          memcpy(py, ry, 256);
+          memcpy(pu, ru, 64);
+          memcpy(pv, rv, 64);
+        } else {
+          m->cbp = 0;
+        }
+      } else {
+        inter = T >= 0 && cost <= T;
+      }
       m->pcm = !inter;
       m->mvx = inter ? 4 * bdx : 0;
       m->mvy = inter ? 4 * bdy : 0;
@@ -303,6 +578,42 @@ static void encode_p(const uint8_t *src, const uint8_t *ref, uint8_t *rec, int c
     }
 }
 
+/* residual() of an inter macroblock (7.3.5.3) with nC from the left
+ * macroblock (lnz / lnzc: its right-column total_coeff, -1 unavailable) and
+ * the blocks above inside this one; cnz / cnzc receive this macroblock's */
+static void put_residual(or_bw *b, const or_mb *m, const int *lnz, const int (*lnzc)[2], int *cnz,
+                         int (*cnzc)[4]) {
+  int cbp = m->cbp;
+  for (int i = 0; i < 16; i++) cnz[i] = 0;
+  for (int pl = 0; pl < 2; pl++)
+    for (int i = 0; i < 4; i++) cnzc[pl][i] = 0;
+  for (int k = 0; k < 16; k++) {
+    if (!((cbp >> (k >> 2)) & 1)) continue;
+    int bx = BLK_X[k], by = BLK_Y[k];
+    int na = bx ? cnz[by * 4 + bx - 1] : lnz[by], nb = by ? cnz[(by - 1) * 4 + bx] : -1;
+    int nC = (na >= 0 && nb >= 0) ? (na + nb + 1) >> 1 : (na >= 0 ? na : (nb >= 0 ? nb : 0));
+    const int16_t *lv = m->lv + 16 * k;
+    block_bits(b, lv, 16, nC);
+    int tc = 0;
+    for (int i = 0; i < 16; i++) tc += lv[i] != 0;
+    cnz[by * 4 + bx] = tc;
+  }
+  if (cbp >> 4)
+    for (int pl = 0; pl < 2; pl++) block_bits(b, m->lv + 256 + 4 * pl, 4, -1);
+  if ((cbp >> 4) == 2)
+    for (int pl = 0; pl < 2; pl++)
+      for (int k = 0; k < 4; k++) {
+        int bx = k & 1, by = k >> 1;
+        int na = bx ? cnzc[pl][by * 2] : lnzc[pl][by], nb = by ? cnzc[pl][bx] : -1;
+        int nC = (na >= 0 && nb >= 0) ? (na + nb + 1) >> 1 : (na >= 0 ? na : (nb >= 0 ? nb : 0));
+        const int16_t *lv = m->lv + 264 + 60 * pl + 15 * k;
+        block_bits(b, lv, 15, nC);
+        int tc = 0;
+        for (int i = 0; i < 15; i++) tc += lv[i] != 0;
+        cnzc[pl][k] = tc;
+      }
+}
+
 static void put_pcm(or_bw *b, const uint8_t *src, int cw, int ch, int mx, int my) {
   bw_align(b);
   for (int j = 0; j < 16; j++)
@@ -315,7 +626,7 @@ static void put_pcm(or_bw *b, const uint8_t *src, int cw, int ch, int mx, int my
 
 /* one picture, one slice per macroblock row, appended to out */
 static int write_picture(const uint8_t *src, int cw, int ch, const or_mb *mbs, int idr, int idr_id,
-                         int frame_num, uint8_t *out, int64_t cap, int64_t *pos, uint8_t *rbsp,
+                         int frame_num, int qp, uint8_t *out, int64_t cap, int64_t *pos, uint8_t *rbsp,
                          int64_t rcap, int64_t *stats) {
   int mbw = cw / 16, mbh = ch / 16;
   for (int row = 0; row < mbh; row++) {
@@ -336,10 +647,12 @@ static int write_picture(const uint8_t *src, int cw, int ch, const or_mb *mbs, i
     } else {
       bw_u(&b, 1, 0);                  /* adaptive_ref_pic_marking_mode_flag */
     }
-    bw_se(&b, 0);                      /* slice_qp_delta */
+    bw_se(&b, qp >= 1 ? qp - 26 : 0);  /* slice_qp_delta: SliceQPY = the residual's QP (pic_init_qp 26) */
     bw_ue(&b, 1);                      /* disable_deblocking_filter_idc */
     uint32_t skip = 0;
     int amv_ok = 0, amvx = 0, amvy = 0;  /* left neighbour A: inter with this mv */
+    /* total_coeff of the left macroblock's right column (nC, 9.2.1): -1 none */
+    int lnz[4] = {-1, -1, -1, -1}, lnzc[2][2] = {{-1, -1}, {-1, -1}}, cnz[16], cnzc[2][4];
     for (int mx = 0; mx < mbw; mx++) {
       const or_mb *m = &mbs[row * mbw + mx];
       if (idr) {
@@ -355,11 +668,15 @@ static int write_picture(const uint8_t *src, int cw, int ch, const or_mb *mbs, i
         put_pcm(&b, src, cw, ch, mx, row);
         amv_ok = 0;
         stats[0]++;
+        for (int i = 0; i < 4; i++) lnz[i] = 16;
+        for (int pl = 0; pl < 2; pl++) lnzc[pl][0] = lnzc[pl][1] = 16;
         continue;
       }
-      if (m->mvx == 0 && m->mvy == 0) {  /* P_Skip: B unavailable -> mv 0 */
+      if (m->mvx == 0 && m->mvy == 0 && m->cbp == 0) {  /* P_Skip: B unavailable -> mv 0 */
         skip++;
         stats[2]++;
+        for (int i = 0; i < 4; i++) lnz[i] = 0;
+        for (int pl = 0; pl < 2; pl++) lnzc[pl][0] = lnzc[pl][1] = 0;
       } else {
         int px = amv_ok ? amvx : 0, py = amv_ok ? amvy : 0;  /* 8.4.1.3, only A available */
         bw_ue(&b, skip);
@@ -367,7 +684,22 @@ static int write_picture(const uint8_t *src, int cw, int ch, const or_mb *mbs, i
         bw_ue(&b, 0);                  /* P_L0_16x16 */
         bw_se(&b, m->mvx - px);
         bw_se(&b, m->mvy - py);
-        bw_ue(&b, 0);                  /* coded_block_pattern 0 */
+        int code = 0;
+        while (CBP_P[code] != m->cbp) code++;
+        bw_ue(&b, (uint32_t)code);     /* coded_block_pattern me(v) */
+        if (m->cbp) {
+          bw_se(&b, 0);                /* mb_qp_delta */
+          put_residual(&b, m, lnz, (const int(*)[2])lnzc, cnz, cnzc);
+        } else {
+          for (int i = 0; i < 16; i++) cnz[i] = 0;
+          for (int pl = 0; pl < 2; pl++)
+            for (int i = 0; i < 4; i++) cnzc[pl][i] = 0;
+        }
+        for (int i = 0; i < 4; i++) lnz[i] = cnz[i * 4 + 3];
+        for (int pl = 0; pl < 2; pl++) {
+          lnzc[pl][0] = cnzc[pl][1];
+          lnzc[pl][1] = cnzc[pl][3];
+        }
         stats[1]++;
       }
       amv_ok = 1;
@@ -389,10 +721,10 @@ static int write_picture(const uint8_t *src, int cw, int ch, const or_mb *mbs, i
  * stats: [pcm MBs, P_L0_16x16 MBs, P_Skip MBs, IDR pictures].
  * Returns 0, -1 bad argument, -2 capacity, -3 out of memory. */
 int or_transcode(const uint8_t *frames, int64_t n, int W, int H, const float *scores, float thr,
-                 int idr_at_cuts, int sh, int R, int T, int keyint, uint8_t *out, int64_t cap, int64_t *sample_off,
+                 int idr_at_cuts, int sh, int R, int T, int keyint, int qp, uint8_t *out, int64_t cap, int64_t *sample_off,
                  int64_t *sample_size, uint8_t *sync, uint8_t *recon, int64_t *stats,
                  int64_t *out_len) {
-  if (n <= 0 || sh < 2 || (sh & 1) || R < 0 || R > 16 || keyint < 1) return -1;
+  if (n <= 0 || sh < 2 || (sh & 1) || R < 0 || R > 16 || keyint < 1 || qp > 51) return -1;
   int sw = or_small_width(W, H, sh);
   int cw = (sw + 15) & ~15, ch = (sh + 15) & ~15, mbw = cw / 16, mbh = ch / 16;
   int64_t fsz = (int64_t)cw * ch * 3 / 2, dsz = (int64_t)W * H * 3 / 2;
@@ -415,11 +747,11 @@ int or_transcode(const uint8_t *frames, int64_t n, int W, int H, const float *sc
     sync[f] = (uint8_t)idr;
     if (idr) {
       memcpy(rec[cur], src, (size_t)fsz);
-      rc = write_picture(src, cw, ch, mbs, 1, (int)(n_idr & 1), 0, out, cap, &pos, rbsp, rcap, stats);
+      rc = write_picture(src, cw, ch, mbs, 1, (int)(n_idr & 1), 0, qp, out, cap, &pos, rbsp, rcap, stats);
       n_idr++;
     } else {
-      encode_p(src, rec[cur ^ 1], rec[cur], cw, ch, R, T, mbs);
-      rc = write_picture(src, cw, ch, mbs, 0, 0, j & 0xffff, out, cap, &pos, rbsp, rcap, stats);
+      encode_p(src, rec[cur ^ 1], rec[cur], cw, ch, R, T, qp, mbs);
+      rc = write_picture(src, cw, ch, mbs, 0, 0, j & 0xffff, qp, out, cap, &pos, rbsp, rcap, stats);
     }
     sample_size[f] = pos - sample_off[f];
     if (recon) memcpy(recon + f * fsz, rec[cur], (size_t)fsz);

@@ -30,6 +30,9 @@ CASES = [
                     gop_max_s=10), dict(height=96, keyint=16, search_range=16)),
     ("idr_at_cuts", dict(width=320, height=192, n_frames=90), dict(height=96, idr_at_cuts=True)),
     ("bigpan_edges", dict(width=320, height=192, n_frames=60, max_motion=24), dict(height=96)),
+    ("qp36", dict(width=640, height=480, n_frames=45, max_motion=6), dict(qp=36)),
+    ("qp20_sparkle", dict(width=320, height=192, n_frames=60, pcm_zero_runs=True), dict(height=96, qp=20)),
+    ("no_residual", dict(width=320, height=192, n_frames=60), dict(height=96, qp=0)),
 ]
 
 
@@ -47,7 +50,7 @@ def _oracle_run(path, tk):
                              want_rgb=False)["score"]
     kw = dict(out_height=tk.get("height", 360), search_range=tk.get("search_range", 8),
               max_mb_sad=tk.get("max_mb_sad", 1536), keyint=tk.get("keyint", 250),
-              idr_at_cuts=tk.get("idr_at_cuts", False))
+              idr_at_cuts=tk.get("idr_at_cuts", False), qp=tk.get("qp", 28))
     return oracle.transcode(frames, W, H, sc, want_recon=True, **kw), info
 
 
@@ -85,6 +88,30 @@ def test_transcode_bytes_match_oracle(tmp_path, name, sk, tk):
         last = d.frame_nv12(d.n_frames - 1).reshape(sh * 3 // 2, sw)
     want = np.concatenate([rec[-1, :sh, :sw], rec[-1, ch:ch + sh // 2, :sw]])
     assert np.array_equal(last, want)
+
+
+def test_transcode_residual_coding_compresses(tmp_path):
+    """Residual coding (qp 28, the reference's CRF) against the round-2
+    encoder on a 720p synthetic: the output is below 0.3x the input (the
+    reference expects 1/5 .. 1/10 from x264, content_analyzer.py:170), smaller
+    than without a residual, and byte-equal to the oracle's."""
+    _require_gpu()
+    src = tmp_path / "in.mp4"
+    scene.synth_write(src, width=1280, height=720, n_frames=120, max_motion=4, cut_min_s=2, cut_max_s=4,
+                      gop_max_s=2)
+    sizes = {}
+    for qp in (28, 0):
+        out = tmp_path / f"o{qp}.mp4"
+        with scene.VideoScorer(src) as v:
+            facts = v.transcode(out, qp=qp)
+        ref, _ = _oracle_run(src, dict(qp=qp))
+        m = oracle.read_mp4(out)
+        got = [m["data"][o:o + z] for o, z in zip(m["offsets"], m["sizes"])]
+        assert got == ref["samples"]
+        sizes[qp] = sum(map(len, got))
+        assert facts["pcm_mbs"] == ref["pcm_mbs"]
+    assert sizes[28] < sizes[0]
+    assert sizes[28] < 0.3 * src.stat().st_size
 
 
 def test_transcode_windowed_equals_one_window(tmp_path):
@@ -169,7 +196,7 @@ def _oracle_run_full(path, tk):
                              want_rgb=False)["score"]
     kw = dict(out_height=tk.get("height", 360), search_range=tk.get("search_range", 8),
               max_mb_sad=tk.get("max_mb_sad", 1536), keyint=tk.get("keyint", 250),
-              idr_at_cuts=tk.get("idr_at_cuts", False))
+              idr_at_cuts=tk.get("idr_at_cuts", False), qp=tk.get("qp", 28))
     return oracle.transcode(frames, W, H, sc, want_recon=True, **kw), info
 
 

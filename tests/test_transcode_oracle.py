@@ -85,9 +85,12 @@ def clip(tmp_path_factory):
 
 @pytest.mark.parametrize("T,R", [(768, 8), (0, 8), (768, 0), (-1, 8), (5000, 16)])
 def test_oracle_round_trip_and_error_bound(clip, T, R):
+    """The round-2 encoder (qp 0: no residual): I_PCM where the motion
+    misses by more than T, every output decodes (subset decoder) to the
+    encoder's reconstruction."""
     frames, sc, info = clip
     r = oracle.transcode(frames, 320, 192, sc, out_height=96, search_range=R, max_mb_sad=T,
-                         want_recon=True)
+                         want_recon=True, qp=0)
     cw, ch, sw, sh = r["coded_width"], r["coded_height"], r["width"], r["height"]
     sps, pps = oracle.sps_pps(cw // 16, ch // 16, cw - sw, ch - sh, 30.0)
     dec = oracle.decode_samples(sps, pps, r["samples"])
@@ -107,6 +110,44 @@ def test_oracle_round_trip_and_error_bound(clip, T, R):
     assert r["sync"][0] and r["sync"].sum() == r["n_idr"]
     if T < 0:
         assert r["pcm_mbs"] == n_mb
+
+
+def _decode_full_samples(tmp_path, r, name="o.mp4"):
+    cw, ch, sw, sh = r["coded_width"], r["coded_height"], r["width"], r["height"]
+    sps, pps = oracle.sps_pps(cw // 16, ch // 16, cw - sw, ch - sh, 30.0)
+    n = len(r["samples"])
+    path = tmp_path / name
+    oracle.write_mp4(path, sps, pps, r["samples"], [i * 1000 for i in range(n)], [0] * n, 30000, sw, sh)
+    dec, _ = oracle.decode_full(path)
+    return dec
+
+
+@pytest.mark.parametrize("qp,R,T", [(28, 8, 1536), (20, 8, 1536), (36, 4, 1536), (28, 0, 1536),
+                                    (28, 8, -1)])
+def test_oracle_residual_coding_round_trip(tmp_path, clip, qp, R, T):
+    """Residual coding (P_L0_16x16 + quantised 4x4 residual, CAVLC
+    residual_block with nC from the left macroblock): the general oracle
+    decoder reads the output back to exactly the encoder's reconstruction,
+    every inter macroblock's residual bound stays within the I_PCM payload,
+    and the result is smaller than the residual-free encoder's."""
+    frames, sc, _ = clip
+    r = oracle.transcode(frames, 320, 192, sc, out_height=96, search_range=R, max_mb_sad=T,
+                         want_recon=True, qp=qp)
+    cw, ch, sw, sh = r["coded_width"], r["coded_height"], r["width"], r["height"]
+    rec = r["recon"]
+    dec = _decode_full_samples(tmp_path, r)
+    assert np.array_equal(dec, np.concatenate([rec[:, :sh, :sw], rec[:, ch:ch + sh // 2, :sw]], 1))
+    n_mb = len(frames) * (cw // 16) * (ch // 16)
+    assert r["pcm_mbs"] + r["inter_mbs"] + r["skip_mbs"] == n_mb
+    if T < 0:
+        assert r["pcm_mbs"] == n_mb
+        return
+    old = oracle.transcode(frames, 320, 192, sc, out_height=96, search_range=R, max_mb_sad=T, qp=0)
+    assert sum(map(len, r["samples"])) < sum(map(len, old["samples"]))
+    assert r["pcm_mbs"] <= old["pcm_mbs"]
+    ds = np.stack([oracle.downscale_nv12(f, 320, 192, 96) for f in frames]).astype(np.float64)
+    mse = np.mean((ds[:, :sh, :sw] - rec[:, :sh, :sw].astype(np.float64)) ** 2)
+    assert 10 * np.log10(255.0 ** 2 / max(mse, 1e-9)) > 30.0
 
 
 @pytest.mark.parametrize("at_cuts", [False, True])

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "mp4.h"
+#include "recon_full.h"
 #include "session.h"
 
 namespace vts {
@@ -154,6 +155,64 @@ __global__ void __launch_bounds__(256) downscale_nv12(DsArgs a) {
   }
 }
 
+// ------------------------------------------------------ residual coding
+// Quantised residual of P_L0_16x16 macroblocks: the forward
+// core transform W = Cf X Cf^T, levels sign(W) min(2047, (|W| MF + f) >>
+// qbits) with qbits = 15 + qp / 6 and f = 2^qbits / 6 (chroma DC through the
+// 2x2 Hadamard at qbits + 1 and 2f), the decoder's own scaling + inverse
+// transform (full::scale_idct4) for the reconstruction, and CAVLC
+// residual_block (9.2) for the bits.  Restated in oracle/transcode_oracle.c.
+constexpr int kCoefPerMb = 384;  // luma 16 x 16 by luma4x4BlkIdx, Cb / Cr DC 2 x 4, Cb / Cr AC 8 x 15 (scan order)
+constexpr int kPcmBits = 3072;   // I_PCM payload: a residual bounded above it is not worth coding
+__device__ __constant__ static const uint8_t kCtLen[4][17][4] = VTS_CT_LEN_DATA;
+__device__ __constant__ static const uint8_t kCtCode[4][17][4] = VTS_CT_CODE_DATA;
+__device__ __constant__ static const uint8_t kTzLen[15][16] = VTS_TZ_LEN_DATA;
+__device__ __constant__ static const uint8_t kTzCode[15][16] = VTS_TZ_CODE_DATA;
+__device__ __constant__ static const uint8_t kTzcLen[3][4] = VTS_TZC_LEN_DATA;
+__device__ __constant__ static const uint8_t kTzcCode[3][4] = VTS_TZC_CODE_DATA;
+__device__ __constant__ static const uint8_t kRbLen[7][15] = VTS_RB_LEN_DATA;
+__device__ __constant__ static const uint8_t kRbCode[7][15] = VTS_RB_CODE_DATA;
+__device__ __constant__ static const uint8_t kZz4[16] = VTS_ZZ_DATA;
+__device__ __constant__ static const uint8_t kCbpInterTab[48] = VTS_CBPP_DATA;
+__device__ __constant__ static const uint8_t kQpcTab[52] = VTS_QPC_DATA;
+__device__ __constant__ static const uint8_t kBlkXd[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
+__device__ __constant__ static const uint8_t kBlkYd[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
+__device__ __constant__ static const int kMf[6][3] = {{13107, 5243, 8066}, {11916, 4660, 7490}, {10082, 4194, 6554},
+                                                      {9362, 3647, 5825},  {8192, 3355, 5243},  {7282, 2893, 4559}};
+
+__device__ __forceinline__ int pos_class(int i, int j) { return (!(i & 1) && !(j & 1)) ? 0 : ((i & 1) && (j & 1) ? 1 : 2); }
+__device__ __forceinline__ void fwd4(const int *x, int *w) {  // W = Cf X Cf^T, raster
+  int t[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int a = x[i * 4], b = x[i * 4 + 1], c = x[i * 4 + 2], d = x[i * 4 + 3];
+    t[i * 4] = a + b + c + d;
+    t[i * 4 + 1] = 2 * a + b - c - 2 * d;
+    t[i * 4 + 2] = a - b - c + d;
+    t[i * 4 + 3] = a - 2 * b + 2 * c - d;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int a = t[j], b = t[4 + j], c = t[8 + j], d = t[12 + j];
+    w[j] = a + b + c + d;
+    w[4 + j] = 2 * a + b - c - 2 * d;
+    w[8 + j] = a - b - c + d;
+    w[12 + j] = a - 2 * b + 2 * c - d;
+  }
+}
+__device__ __forceinline__ int quant1(int w, int mf, int qbits, int64_t f) {
+  const int64_t z = min(static_cast<int64_t>(2047), (static_cast<int64_t>(abs(w)) * mf + f) >> qbits);
+  return w < 0 ? -static_cast<int>(z) : static_cast<int>(z);
+}
+
+// bits of residual_block_cavlc (7.3.5.3.2, 9.2) of levels lv[0, maxNum) in
+// scan order with nC (-1: chroma DC); nC < -1: an upper bound (coeff_token
+// taken as the longest code over the nC classes and the 6-bit FLC).  With o,
+// the block is also written.
+struct NalOut;
+template <bool kWrite>
+__device__ int cavlc_block(NalOut *o, const int *lv, int maxNum, int nC);
+
 // ------------------------------------------------------ motion search
 struct SearchArgs {
   const int4 *ent;      // per frame of the level: (frame, ref slot or -1 = small[frame-1], dst slot, 0)
@@ -161,8 +220,11 @@ struct SearchArgs {
   int64_t stride;
   uint8_t *recon;       // [slot]
   uint32_t *cmd;        // [entry][mb]
+  uint8_t *cbp;         // [entry][mb] coded_block_pattern (residual coding)
+  int16_t *coef;        // [entry][mb][kCoefPerMb] levels (this level's ring slot)
   int32_t cw, ch, mbw, nmb;
   int32_t range, max_sad;
+  int32_t qp, _pad;     // qp >= 1: residual coding at that QP
 };
 
 __device__ __forceinline__ uint32_t u32_at(const uint8_t *lds_row, int off) {  // 4 bytes at any offset
@@ -368,20 +430,164 @@ __global__ void __launch_bounds__(64) VTS_SEARCH_OCC enc_search(SearchArgs a) {
   cost += static_cast<uint32_t>(abs(pu - (suv & 255)) + abs(pv - (suv >> 8)));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) cost += __shfl_xor(cost, off);
-  const bool inter = a.max_sad >= 0 && cost <= static_cast<uint32_t>(a.max_sad);
   const int64_t lo = static_cast<int64_t>(my * 16 + ly) * a.cw + mx * 16 + lx;
-  *reinterpret_cast<uint32_t *>(dst + lo) = inter ? py : sy4;
-  *reinterpret_cast<uint16_t *>(dst + co) = inter ? static_cast<uint16_t>(pu | (pv << 8)) : suv;
-  if (lane == 0)
-    a.cmd[e * a.nmb + mb] =
-        inter ? (static_cast<uint32_t>(static_cast<uint16_t>(mvx)) | (static_cast<uint32_t>(static_cast<uint16_t>(mvy)) << 16))
-              : kPcmCmd;
+  const uint32_t mvw =
+      static_cast<uint32_t>(static_cast<uint16_t>(mvx)) | (static_cast<uint32_t>(static_cast<uint16_t>(mvy)) << 16);
+  if (a.qp < 1 || a.max_sad < 0) {  // no residual: inter within max_sad, else I_PCM
+    const bool inter = a.max_sad >= 0 && cost <= static_cast<uint32_t>(a.max_sad);
+    *reinterpret_cast<uint32_t *>(dst + lo) = inter ? py : sy4;
+    *reinterpret_cast<uint16_t *>(dst + co) = inter ? static_cast<uint16_t>(pu | (pv << 8)) : suv;
+    if (lane == 0) {
+      a.cmd[e * a.nmb + mb] = inter ? mvw : kPcmCmd;
+      if (a.cbp) a.cbp[e * a.nmb + mb] = 0;
+    }
+    return;
+  }
+  // ---- residual coding: lanes 0..15 the luma blocks (luma4x4BlkIdx), 16..23
+  // the chroma blocks (Cb 0..3, Cr 0..3), 24 / 25 the chroma DC blocks
+  __shared__ uint32_t predy[64], recy[64];
+  __shared__ uint16_t predc[64], srcc[64];
+  __shared__ uint8_t recc[2][64];
+  __shared__ int dcw[2][4], dcl[2][4];
+  predy[lane] = py;
+  predc[lane] = static_cast<uint16_t>(pu | (pv << 8));
+  srcc[lane] = suv;
+  __syncthreads();
+  const int qp = a.qp, qpc = kQpcTab[qp];
+  const int qbits = 15 + qp / 6, cqb = 15 + qpc / 6;
+  const int64_t f = (int64_t(1) << qbits) / 6, cf = (int64_t(1) << cqb) / 6;
+  int lv[16], z[16], nzb = 0, bits = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) lv[i] = z[i] = 0;
+  if (lane < 16) {
+    const int bx = kBlkXd[lane], by = kBlkYd[lane];
+    int x[16], w[16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t sv = srcy[(by * 4 + r) * 4 + bx], pv4 = predy[(by * 4 + r) * 4 + bx];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[r * 4 + c] = static_cast<int>((sv >> (8 * c)) & 255) - static_cast<int>((pv4 >> (8 * c)) & 255);
+    }
+    fwd4(x, w);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      z[q] = quant1(w[q], kMf[qp % 6][pos_class(q >> 2, q & 3)], qbits, f);
+      nzb |= z[q] != 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) lv[q] = z[kZz4[q]];
+    int res[16];
+    full::scale_idct4(z, qp, false, res);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t pv4 = predy[(by * 4 + r) * 4 + bx];
+      uint32_t o = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        o |= static_cast<uint32_t>(min(max(static_cast<int>((pv4 >> (8 * c)) & 255) + res[r * 4 + c], 0), 255)) << (8 * c);
+      recy[(by * 4 + r) * 4 + bx] = o;
+    }
+    bits = cavlc_block<false>(nullptr, lv, 16, -2);
+  } else if (lane < 24) {
+    const int pl = (lane - 16) >> 2, k = (lane - 16) & 3, bx = (k & 1) * 4, by = (k >> 1) * 4;
+    int x[16], w[16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int i = (by + r) * 8 + bx + c;
+        x[r * 4 + c] = static_cast<int>((srcc[i] >> (8 * pl)) & 255) - static_cast<int>((predc[i] >> (8 * pl)) & 255);
+      }
+    fwd4(x, w);
+    dcw[pl][k] = w[0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+      z[q] = quant1(w[q], kMf[qpc % 6][pos_class(q >> 2, q & 3)], cqb, cf);
+      nzb |= z[q] != 0;
+    }
+#pragma unroll
+    for (int q = 1; q < 16; ++q) lv[q - 1] = z[kZz4[q]];
+  }
+  __syncthreads();
+  if (lane == 16 || lane == 17) {  // chroma DC: 2x2 Hadamard, quantised at (qbits + 1, 2f)
+    const int pl = lane - 16;
+    const int c0 = dcw[pl][0], c1 = dcw[pl][1], c2 = dcw[pl][2], c3 = dcw[pl][3];
+    const int fd[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dcl[pl][k] = quant1(fd[k], kMf[qpc % 6][0], cqb + 1, 2 * cf);
+  }
+  __syncthreads();
+  const uint64_t nzm = __ballot(nzb);
+  int cbp = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if ((nzm >> (4 * q)) & 15u) cbp |= 1 << q;
+  bool dcnz = false;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dcnz |= dcl[k >> 2][k & 3] != 0;
+  const int cc = ((nzm >> 16) & 0xffu) ? 2 : (dcnz ? 1 : 0);
+  cbp |= cc << 4;
+  int contrib = 0;  // this lane's share of the residual's CAVLC bound
+  if (lane < 16) {
+    contrib = ((cbp >> (lane >> 2)) & 1) ? bits : 0;
+  } else if (lane < 24) {
+    contrib = cc == 2 ? cavlc_block<false>(nullptr, lv, 15, -2) : 0;
+  } else if (lane < 26 && cc) {
+    const int d4[4] = {dcl[lane - 24][0], dcl[lane - 24][1], dcl[lane - 24][2], dcl[lane - 24][3]};
+    contrib = cavlc_block<false>(nullptr, d4, 4, -1);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) contrib += __shfl_xor(contrib, off);
+  const bool inter = contrib <= kPcmBits;
+  if (lane >= 16 && lane < 24) {  // chroma reconstruction (8.5.11 DC, then 8.5.12)
+    const int pl = (lane - 16) >> 2, k = (lane - 16) & 3, bx = (k & 1) * 4, by = (k >> 1) * 4;
+    const int *c = dcl[pl];
+    const int F = k == 0 ? c[0] + c[1] + c[2] + c[3]
+                         : (k == 1 ? c[0] - c[1] + c[2] - c[3] : (k == 2 ? c[0] + c[1] - c[2] - c[3] : c[0] - c[1] - c[2] + c[3]));
+    int co[16], res[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) co[q] = cc == 2 ? z[q] : 0;
+    co[0] = ((F * full::level_scale(qpc % 6, 0, 0)) << (qpc / 6)) >> 5;
+    full::scale_idct4(co, qpc, true, res);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int cx = 0; cx < 4; ++cx) {
+        const int i = (by + r) * 8 + bx + cx;
+        recc[pl][i] = static_cast<uint8_t>(min(max(static_cast<int>((predc[i] >> (8 * pl)) & 255) + res[r * 4 + cx], 0), 255));
+      }
+  }
+  __syncthreads();
+  *reinterpret_cast<uint32_t *>(dst + lo) = inter ? recy[lane] : sy4;
+  *reinterpret_cast<uint16_t *>(dst + co) =
+      inter ? static_cast<uint16_t>(recc[0][lane] | (recc[1][lane] << 8)) : suv;
+  if (inter && cbp) {  // the levels the slice writer codes
+    int16_t *cp = a.coef + (e * a.nmb + mb) * kCoefPerMb;
+    if (lane < 16) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) cp[16 * lane + q] = static_cast<int16_t>(lv[q]);
+    } else if (lane < 24) {
+#pragma unroll
+      for (int q = 0; q < 15; ++q) cp[264 + 15 * (lane - 16) + q] = static_cast<int16_t>(lv[q]);
+    } else if (lane < 26) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cp[256 + 4 * (lane - 24) + q] = static_cast<int16_t>(dcl[lane - 24][q]);
+    }
+  }
+  if (lane == 0) {
+    a.cmd[e * a.nmb + mb] = inter ? mvw : kPcmCmd;
+    a.cbp[e * a.nmb + mb] = static_cast<uint8_t>(inter ? cbp : 0);
+  }
 }
 
 // ------------------------------------------------------ slice writer
 struct WriteArgs {
-  const int4 *ent;      // per frame of the level: (frame, GOP position j, IDR parity, 0)
+  const int4 *ent;      // per frame of the level: (frame, GOP position j, IDR parity, index within its level)
   const uint32_t *cmd;  // [entry][mb] (P levels)
+  const uint8_t *cbp;   // [entry][mb] coded_block_pattern
+  const int16_t *coef;  // level ring: [ring slot][index within level][mb][kCoefPerMb]
+  int64_t coef_per_level;  // entries a ring slot holds
+  int32_t ring, qp;     // ring slots (levels); qp >= 1: residual coding (slice_qp_delta = qp - 26)
   const uint8_t *small;
   int64_t stride;
   int32_t cw, ch, mbw, mbh;
@@ -447,6 +653,131 @@ struct NalOut {
   }
 };
 
+template <bool kWrite>
+__device__ int cavlc_block(NalOut *o, const int *lv, int maxNum, int nC) {
+  int tc = 0, t1 = 0, top = -1;
+  bool open = true;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {
+    const int v = i < maxNum ? lv[i] : 0;
+    if (!v) continue;
+    if (top < 0) top = i;
+    ++tc;
+    if (open && t1 < 3 && (v == 1 || v == -1)) ++t1;
+    else open = false;
+  }
+  int bits;
+  if (nC < -1) {  // the bound: the longest coeff_token over nC classes 0..2 and the FLC
+    bits = max(6, max(static_cast<int>(kCtLen[0][tc][t1]), max(static_cast<int>(kCtLen[1][tc][t1]),
+                                                              static_cast<int>(kCtLen[2][tc][t1]))));
+  } else if (nC >= 8) {
+    bits = 6;
+    if (kWrite) o->bits(6, tc == 0 ? 3u : static_cast<uint32_t>(((tc - 1) << 2) | t1));
+  } else {
+    const int col = nC == -1 ? 3 : (nC < 2 ? 0 : (nC < 4 ? 1 : 2));
+    bits = kCtLen[col][tc][t1];
+    if (kWrite) o->bits(bits, kCtCode[col][tc][t1]);
+  }
+  if (tc == 0) return bits;
+  int k = 0, sl = (tc > 10 && t1 < 3) ? 1 : 0;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {  // trailing ones' signs, then levels (9.2.2.1 inverted)
+    const int v = i < maxNum ? lv[i] : 0;
+    if (!v) continue;
+    if (k < t1) {
+      ++bits;
+      if (kWrite) o->bits(1, v < 0 ? 1u : 0u);
+    } else {
+      int code = v > 0 ? 2 * v - 2 : -2 * v - 1;
+      if (k == t1 && t1 < 3) code -= 2;
+      int prefix, suffix = 0, ssize = 0;
+      if (sl == 0) {
+        if (code < 14) prefix = code;
+        else if (code < 30) { prefix = 14; suffix = code - 14; ssize = 4; }
+        else { prefix = 15; suffix = code - 30; ssize = 12; }
+      } else if (code < (15 << sl)) {
+        prefix = code >> sl;
+        suffix = code & ((1 << sl) - 1);
+        ssize = sl;
+      } else {
+        prefix = 15;
+        suffix = code - (15 << sl);
+        ssize = 12;
+      }
+      bits += prefix + 1 + ssize;
+      if (kWrite) {
+        o->bits(prefix + 1, 1u);
+        if (ssize) o->bits(ssize, static_cast<uint32_t>(suffix));
+      }
+      if (sl == 0) sl = 1;
+      if (abs(v) > (3 << (sl - 1)) && sl < 6) ++sl;
+    }
+    ++k;
+  }
+  int zl = top + 1 - tc;  // total_zeros
+  if (tc < maxNum) {
+    const int len = maxNum == 4 ? kTzcLen[tc - 1][zl] : kTzLen[tc - 1][zl];
+    bits += len;
+    if (kWrite) o->bits(len, maxNum == 4 ? kTzcCode[tc - 1][zl] : kTzCode[tc - 1][zl]);
+  }
+  int prev = -1;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {  // run_before of every coefficient but the lowest
+    const int v = i < maxNum ? lv[i] : 0;
+    if (!v) continue;
+    if (prev >= 0 && zl > 0) {
+      const int run = prev - i - 1, row = min(zl, 7) - 1;
+      bits += kRbLen[row][run];
+      if (kWrite) o->bits(kRbLen[row][run], kRbCode[row][run]);
+      zl -= run;
+    }
+    prev = i;
+  }
+  return bits;
+}
+
+// residual() of an inter macroblock (7.3.5.3): cp the levels, cnz / cnzc
+// receive the blocks' total_coeff; lnz / lnzc the left macroblock's right
+// column (-1: unavailable; the macroblock above is another slice)
+__device__ void put_residual(NalOut &o, const int16_t *cp, int cbp, const int *lnz, const int (*lnzc)[2], int *cnz,
+                             int (*cnzc)[4]) {
+  for (int i = 0; i < 16; ++i) cnz[i] = 0;
+  for (int i = 0; i < 4; ++i) cnzc[0][i] = cnzc[1][i] = 0;
+  int lv[16];
+  for (int k = 0; k < 16; ++k) {
+    if (!((cbp >> (k >> 2)) & 1)) continue;
+    const int bx = kBlkXd[k], by = kBlkYd[k];
+    const int na = bx ? cnz[by * 4 + bx - 1] : lnz[by], nb = by ? cnz[(by - 1) * 4 + bx] : -1;
+    const int nC = (na >= 0 && nb >= 0) ? (na + nb + 1) >> 1 : (na >= 0 ? na : (nb >= 0 ? nb : 0));
+    int tc = 0;
+    for (int q = 0; q < 16; ++q) {
+      lv[q] = cp[16 * k + q];
+      tc += lv[q] != 0;
+    }
+    cavlc_block<true>(&o, lv, 16, nC);
+    cnz[by * 4 + bx] = tc;
+  }
+  if (cbp >> 4)
+    for (int pl = 0; pl < 2; ++pl) {
+      for (int q = 0; q < 4; ++q) lv[q] = cp[256 + 4 * pl + q];
+      cavlc_block<true>(&o, lv, 4, -1);
+    }
+  if ((cbp >> 4) == 2)
+    for (int pl = 0; pl < 2; ++pl)
+      for (int k = 0; k < 4; ++k) {
+        const int bx = k & 1, by = k >> 1;
+        const int na = bx ? cnzc[pl][by * 2] : lnzc[pl][by], nb = by ? cnzc[pl][bx] : -1;
+        const int nC = (na >= 0 && nb >= 0) ? (na + nb + 1) >> 1 : (na >= 0 ? na : (nb >= 0 ? nb : 0));
+        int tc = 0;
+        for (int q = 0; q < 15; ++q) {
+          lv[q] = cp[264 + 60 * pl + 15 * k + q];
+          tc += lv[q] != 0;
+        }
+        cavlc_block<true>(&o, lv, 15, nC);
+        cnzc[pl][k] = tc;
+      }
+}
+
 // I_PCM: pcm_alignment_zero_bits, then 384 sample bytes that enc_pcm fills in
 // later (the gap's bytes in the partial words either side are don't-care
 // here: enc_pcm runs after enc_gather).  The samples are >= 1 (downscale
@@ -482,13 +813,18 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
   } else {
     o.bits(3, 0);  // num_ref_idx_active_override, ref_pic_list_modification_l0, adaptive_ref_pic_marking
   }
-  o.se(0);  // slice_qp_delta
+  o.se(a.qp >= 1 ? a.qp - 26 : 0);  // slice_qp_delta: SliceQPY = the residual's QP (pic_init_qp 26)
   o.ue(1);  // disable_deblocking_filter_idc
   unsigned long long npcm = 0, ninter = 0, nskip = 0;
   uint32_t skip = 0;
   bool a_ok = false;
   int amx = 0, amy = 0;
   const uint32_t *cmd = a.cmd + static_cast<int64_t>(e) * a.mbw * a.mbh + static_cast<int64_t>(row) * a.mbw;
+  const uint8_t *cbpr = a.cbp + static_cast<int64_t>(e) * a.mbw * a.mbh + static_cast<int64_t>(row) * a.mbw;
+  const int16_t *coef_row =
+      a.coef + ((static_cast<int64_t>(en.y % a.ring) * a.coef_per_level + en.w) * a.mbh + row) * a.mbw * kCoefPerMb;
+  // total_coeff of the left macroblock's right column for nC (9.2.1); -1 none
+  int lnz[4] = {-1, -1, -1, -1}, lnzc[2][2] = {{-1, -1}, {-1, -1}}, cnz[16], cnzc[2][4];
   // reserve this slice's I_PCM jobs
   uint32_t njob = 0;
   if (idr) {
@@ -512,12 +848,17 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
       pcm_gap(o, job++, s, mx);
       a_ok = false;
       ++npcm;
+      for (int i = 0; i < 4; ++i) lnz[i] = 16;
+      lnzc[0][0] = lnzc[0][1] = lnzc[1][0] = lnzc[1][1] = 16;
       continue;
     }
     const int mvx = static_cast<int16_t>(c & 0xffffu), mvy = static_cast<int16_t>(c >> 16);
-    if (mvx == 0 && mvy == 0) {  // P_Skip (neighbour B lies in another slice: skip motion is 0)
+    const int cbp = cbpr[mx];
+    if (mvx == 0 && mvy == 0 && cbp == 0) {  // P_Skip (neighbour B lies in another slice: skip motion is 0)
       ++skip;
       ++nskip;
+      for (int i = 0; i < 4; ++i) lnz[i] = 0;
+      lnzc[0][0] = lnzc[0][1] = lnzc[1][0] = lnzc[1][1] = 0;
     } else {
       const int px = a_ok ? amx : 0, py = a_ok ? amy : 0;  // 8.4.1.3, A the only neighbour
       o.ue(skip);
@@ -525,7 +866,21 @@ __global__ void __launch_bounds__(64) enc_write(WriteArgs a) {
       o.ue(0);  // P_L0_16x16
       o.se(mvx - px);
       o.se(mvy - py);
-      o.ue(0);  // coded_block_pattern 0
+      int code = 0;
+      while (kCbpInterTab[code] != cbp) ++code;
+      o.ue(static_cast<uint32_t>(code));  // coded_block_pattern me(v)
+      if (cbp) {
+        o.se(0);  // mb_qp_delta
+        put_residual(o, coef_row + static_cast<int64_t>(mx) * kCoefPerMb, cbp, lnz, lnzc, cnz, cnzc);
+      } else {
+        for (int i = 0; i < 16; ++i) cnz[i] = 0;
+        for (int i = 0; i < 4; ++i) cnzc[0][i] = cnzc[1][i] = 0;
+      }
+      for (int i = 0; i < 4; ++i) lnz[i] = cnz[i * 4 + 3];
+      for (int pl = 0; pl < 2; ++pl) {
+        lnzc[pl][0] = cnzc[pl][1];
+        lnzc[pl][1] = cnzc[pl][3];
+      }
       ++ninter;
     }
     a_ok = true;
@@ -790,6 +1145,8 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   const int sh = p.height > 0 ? p.height : 360;
   const int R = p.search_range == 0 ? 8 : std::max(0, p.search_range);
   const int T = p.max_mb_sad == 0 ? 1536 : p.max_mb_sad;
+  const int qp = p.qp == 0 ? 28 : (p.qp < 0 ? 0 : p.qp);  // 0: no residual coding (the round-2 encoder)
+  if (qp > 51) return fail(VTS_E_INVALID, "qp %d > 51", qp);
   const int keyint = p.keyint > 0 ? p.keyint : 250;
   const float thr = p.cut_threshold > 0 ? p.cut_threshold : c->params.cut_threshold;
   if ((sh & 1) || sh < 16 || sh > c->height)
@@ -838,13 +1195,17 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
       if (gop_len[g] <= j) continue;
       const int f = static_cast<int>(gop_start[g] + j);
       sent.push_back(make_int4(f, j == 1 ? -1 : static_cast<int>(2 * g + ((j - 1) & 1)), static_cast<int>(2 * g + (j & 1)), 0));
-      went.push_back(make_int4(f, static_cast<int>(j), static_cast<int>(g & 1), 0));
+      went.push_back(make_int4(f, static_cast<int>(j), static_cast<int>(g & 1),
+                               static_cast<int>(static_cast<int64_t>(went.size()) - lvl_off[j])));
     }
   }
   lvl_off[maxlen] = static_cast<int64_t>(went.size());
 
   // 3. device encode, level by level
-  const int64_t cap = ((64 + static_cast<int64_t>(mbw) * 420) + 255) & ~int64_t(255);
+  // staging slot per slice: an I_PCM macroblock is < 400 bytes, and so is an
+  // inter one (its residual is coded only under a 3072-bit bound); the rest
+  // is headroom for emulation prevention bytes in residual data
+  const int64_t cap = ((64 + static_cast<int64_t>(mbw) * 600) + 255) & ~int64_t(255);
   DevBufs B;
   int4 *d_sent, *d_went;
   uint8_t *d_recon, *d_stage, *d_out;
@@ -856,6 +1217,13 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   VTS_TRY(B.get(&d_went, went.size()));
   VTS_TRY(B.get(&d_recon, static_cast<size_t>(2 * ngop * S.stride + 256)));
   VTS_TRY(B.get(&d_cmd, static_cast<size_t>(went.size()) * nmb));  // every frame: searches run ahead
+  uint8_t *d_cbp;
+  VTS_TRY(B.get(&d_cbp, static_cast<size_t>(went.size()) * nmb));
+  // residual levels: a ring of kRing levels (the searches run at most kRing
+  // levels ahead of the slice writing that reads them)
+  constexpr int64_t kRing = 32;
+  int16_t *d_coef = nullptr;
+  if (qp >= 1) VTS_TRY(B.get(&d_coef, static_cast<size_t>(kRing * ngop * nmb * kCoefPerMb)));
   constexpr int64_t kChunkLevels = 16;  // levels written and drained together
   int64_t max_chunk = 0;                 // entries of the largest chunk
   for (int64_t j0 = 0; j0 < maxlen; j0 += kChunkLevels)
@@ -884,7 +1252,8 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   HIP_TRY(hipMemcpy(d_went, went.data(), went.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(d_stats, 0, 3 * sizeof(unsigned long long), s2));
   HIP_TRY(hipMemsetAsync(d_err, 0, sizeof(uint32_t), s2));
-  std::vector<hipEvent_t> ev(static_cast<size_t>(maxlen) + 5, nullptr);
+  const int64_t nchunks = (maxlen + kChunkLevels - 1) / kChunkLevels;
+  std::vector<hipEvent_t> ev(static_cast<size_t>(maxlen + 5 + nchunks), nullptr);
   struct EvGuard {
     std::vector<hipEvent_t> &v;
     ~EvGuard() {
@@ -894,31 +1263,48 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   } ev_guard{ev};
   for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
   hipEvent_t es0 = ev[maxlen], es1 = ev[maxlen + 1], ew0 = ev[maxlen + 2], ew1 = ev[maxlen + 3];
+  hipEvent_t *wev = &ev[maxlen + 5];  // per chunk: its slices written (its ring slots free again)
   HIP_TRY(hipEventRecord(es0, s1));
-  for (int64_t j = 1; j < maxlen; ++j) {
-    const int64_t ne = lvl_off[j + 1] - lvl_off[j];
-    SearchArgs sa{};
-    sa.ent = d_sent + lvl_off[j];
-    sa.small = S.d;
-    sa.stride = S.stride;
-    sa.recon = d_recon;
-    sa.cmd = d_cmd + lvl_off[j] * nmb;
-    sa.cw = S.cw;
-    sa.ch = S.ch;
-    sa.mbw = mbw;
-    sa.nmb = nmb;
-    sa.range = R;
-    sa.max_sad = T;
-    const dim3 grid(static_cast<unsigned>(ne * nmb));
-    switch (R) {
-      case 4: hipLaunchKernelGGL(enc_search<4>, grid, dim3(64), 0, s1, sa); break;
-      case 8: hipLaunchKernelGGL(enc_search<8>, grid, dim3(64), 0, s1, sa); break;
-      case 16: hipLaunchKernelGGL(enc_search<16>, grid, dim3(64), 0, s1, sa); break;
-      default: hipLaunchKernelGGL(enc_search<0>, grid, dim3(64), 0, s1, sa); break;
+  int64_t next_search = 1;
+  bool searches_done = false;
+  // enqueue the searches of levels < upto; level j reuses the ring slot of
+  // level j - kRing, whose chunk's slice writing must have finished
+  auto enqueue_searches = [&](int64_t upto) -> int {
+    for (; next_search < std::min(maxlen, upto); ++next_search) {
+      const int64_t j = next_search;
+      if (qp >= 1 && j >= kRing) HIP_TRY(hipStreamWaitEvent(s1, wev[(j - kRing) / kChunkLevels], 0));
+      const int64_t ne = lvl_off[j + 1] - lvl_off[j];
+      SearchArgs sa{};
+      sa.ent = d_sent + lvl_off[j];
+      sa.small = S.d;
+      sa.stride = S.stride;
+      sa.recon = d_recon;
+      sa.cmd = d_cmd + lvl_off[j] * nmb;
+      sa.cbp = d_cbp + lvl_off[j] * nmb;
+      sa.coef = d_coef ? d_coef + (j % kRing) * ngop * nmb * kCoefPerMb : nullptr;
+      sa.cw = S.cw;
+      sa.ch = S.ch;
+      sa.mbw = mbw;
+      sa.nmb = nmb;
+      sa.range = R;
+      sa.max_sad = T;
+      sa.qp = qp;
+      const dim3 grid(static_cast<unsigned>(ne * nmb));
+      switch (R) {
+        case 4: hipLaunchKernelGGL(enc_search<4>, grid, dim3(64), 0, s1, sa); break;
+        case 8: hipLaunchKernelGGL(enc_search<8>, grid, dim3(64), 0, s1, sa); break;
+        case 16: hipLaunchKernelGGL(enc_search<16>, grid, dim3(64), 0, s1, sa); break;
+        default: hipLaunchKernelGGL(enc_search<0>, grid, dim3(64), 0, s1, sa); break;
+      }
+      HIP_TRY(hipEventRecord(ev[j], s1));
     }
-    HIP_TRY(hipEventRecord(ev[j], s1));
-  }
-  HIP_TRY(hipEventRecord(es1, s1));
+    if (next_search >= maxlen && !searches_done) {
+      HIP_TRY(hipEventRecord(es1, s1));
+      searches_done = true;
+    }
+    return VTS_OK;
+  };
+  VTS_TRY(enqueue_searches(qp >= 1 ? kRing : maxlen));
   HIP_TRY(hipGetLastError());
   // Output drained to the host every chunk (absolute bytes [chunk_start[c],
   // chunk_start[c+1])) and appended to the MP4's mdat while the GPU works on
@@ -960,6 +1346,11 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
     WriteArgs wa{};
     wa.ent = d_went + e0;
     wa.cmd = d_cmd + e0 * nmb;
+    wa.cbp = d_cbp + e0 * nmb;
+    wa.coef = d_coef;
+    wa.coef_per_level = ngop;
+    wa.ring = static_cast<int32_t>(kRing);
+    wa.qp = qp;
     wa.small = S.d;
     wa.stride = S.stride;
     wa.cw = S.cw;
@@ -975,6 +1366,8 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
     wa.n_jobs = d_njobs;
     wa.n_slices = ns;
     hipLaunchKernelGGL(enc_write, dim3(static_cast<unsigned>((ns + 63) / 64)), dim3(64), 0, s2, wa);
+    HIP_TRY(hipEventRecord(wev[j0 / kChunkLevels], s2));
+    VTS_TRY(enqueue_searches(j1 + kRing));  // the ring slots of this chunk's levels are free once it is written
     hipLaunchKernelGGL(enc_scan, dim3(1), dim3(1024), 0, s2, d_sizes, ns, d_went + e0, mbh, d_offs, d_total,
                        d_fr, d_fr + n);
     hipLaunchKernelGGL(enc_gather, dim3(static_cast<unsigned>(ns)), dim3(256), 0, s2, d_stage, cap, d_sizes, d_offs,

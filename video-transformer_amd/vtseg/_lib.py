@@ -111,7 +111,8 @@ class SynthInfo(C.Structure):
 
 class TranscodeParams(C.Structure):
     _fields_ = [("height", C.c_int32), ("search_range", C.c_int32), ("max_mb_sad", C.c_int32),
-                ("keyint", C.c_int32), ("cut_threshold", C.c_float), ("idr_at_cuts", C.c_int32)]
+                ("keyint", C.c_int32), ("cut_threshold", C.c_float), ("idr_at_cuts", C.c_int32),
+                ("qp", C.c_int32)]
 
 
 class TranscodeInfo(C.Structure):

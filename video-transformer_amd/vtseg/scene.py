@@ -231,10 +231,11 @@ class VideoScorer:
 
     def transcode(self, out_path: str | Path, *, height: int = 360, search_range: int = 8,
                   max_mb_sad: int = 1536, keyint: int = 250, idr_at_cuts: bool = False,
-                  cut_threshold: float = 0.0) -> dict:
+                  cut_threshold: float = 0.0, qp: int = 28) -> dict:
         """360p upload transcode of this video into `out_path` (vts_transcode,
         DESIGN.md §11): decode + score + area downscale + device H.264
-        encode.  Returns the facts and per-stage milliseconds."""
+        encode with a quantised residual at `qp` (<= 0: none, the round-2
+        encoder).  Returns the facts and per-stage milliseconds."""
         prm = _lib.TranscodeParams()
         prm.height = height
         prm.search_range = search_range if search_range != 0 else -1
@@ -242,6 +243,7 @@ class VideoScorer:
         prm.keyint = keyint
         prm.cut_threshold = cut_threshold
         prm.idr_at_cuts = 1 if idr_at_cuts else 0
+        prm.qp = qp if qp > 0 else -1
         info = _lib.TranscodeInfo()
         _lib.check(self._lib.vts_transcode(self._ctx, str(out_path).encode(), C.byref(prm),
                                            C.byref(info)))
