@@ -31,7 +31,10 @@ CASES = [
     ("idr_at_cuts", dict(width=320, height=192, n_frames=90), dict(height=96, idr_at_cuts=True)),
     ("bigpan_edges", dict(width=320, height=192, n_frames=60, max_motion=24), dict(height=96)),
     ("qp36", dict(width=640, height=480, n_frames=45, max_motion=6), dict(qp=36)),
-    ("qp20_sparkle", dict(width=320, height=192, n_frames=60, pcm_zero_runs=True), dict(height=96, qp=20)),
+    ("qp20_pan", dict(width=320, height=192, n_frames=60, max_motion=8), dict(height=96, qp=20)),
+    # EPB inside I_PCM: the subset kernels refuse mid-transcode and auto mode
+    # reruns the decode + downscale on the general decoder
+    ("auto_switch", dict(width=320, height=192, n_frames=60, pcm_zero_runs=True), dict(height=96, qp=20)),
     ("no_residual", dict(width=320, height=192, n_frames=60), dict(height=96, qp=0)),
 ]
 

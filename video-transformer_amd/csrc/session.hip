@@ -867,7 +867,7 @@ int vts::run_all(vts_ctx *c) {
   // decoder = auto: syntax outside the subset kernels -> the general decoder
   constexpr uint32_t kSubsetMiss = DEC_E_MB_TYPE | DEC_E_RESIDUAL | DEC_E_SUBPEL | DEC_E_MULTIREF |
                                    DEC_E_DEBLOCK | DEC_E_REFLIST | DEC_E_MMCO | DEC_E_EPB_IN_PCM;
-  if ((err & kSubsetMiss) && c->params.decoder == 0 && !c->small.on) {
+  if ((err & kSubsetMiss) && c->params.decoder == 0) {  // small.on too: run_general downscales
     VTS_TRY(switch_to_general(c));
     return run_general(c);
   }
