@@ -404,7 +404,7 @@ def roofline_decode_score(scorers, prof: dict | None, width: int, height: int, k
     s0 = scorers[0]
     rec, sco, launches = [], [], []
     for v in scorers:
-        for _ in range(3):
+        for _ in range(ROOF_RUNS):
             v.run()
             t = v.timings()
             rec.append(t["reconstruct_ms"])
@@ -470,6 +470,8 @@ def roofline_decode_score(scorers, prof: dict | None, width: int, height: int, k
 
 # --------------------------------------------------------------- extras (N = 1)
 
+ROOF_RUNS = 3             # roofline_decode_score's vts_run calls per session
+CHILD_RUNS = 2 + ROOF_RUNS  # a profile child's vts_run calls: warmup 1 + step 1 + the roofline's
 GENERAL_PMC = ("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM "
                "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH")
 
@@ -487,7 +489,9 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
     (intra and inter both count the whole picture's write; their sum
     overstates a picture that mixes them, so the sum is not reported).
     h264_parse_full is serial bit parsing: its bound is instruction issue,
-    reported as instructions / (256 CUs x 2.4 GHz x busy time)."""
+    reported as instructions / (256 CUs x 2.4 GHz x busy time).  The child
+    ran the whole decode CHILD_RUNS times: busy times and counter totals are
+    divided by it (per run)."""
     nv12 = 1.5 * width * height
     w, h = width // k, height // k
     per_pic = {"h264_inter_full": 2 * nv12, "h264_intra_full": nv12,
@@ -497,25 +501,29 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
         row = prof.get(name)
         if not isinstance(row, dict) or "busy_ns_total" not in row:
             continue
-        t = row["busy_ns_total"] * 1e-9
+        t = row["busy_ns_total"] * 1e-9 / CHILD_RUNS
         ach = b * frames / t / 1e9
         out[name] = {"bound": "hbm", "busy_ms": round(t * 1e3, 2),
-                     "dispatches": row["dispatches_traced"], "bytes_per_picture": round(b),
+                     "dispatches": row["dispatches_traced"] // CHILD_RUNS, "bytes_per_picture": round(b),
                      "achieved": round(ach, 1), "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4)}
     row = prof.get("h264_parse_full")
     if isinstance(row, dict) and "busy_ns_total" in row:
-        t = row["busy_ns_total"] * 1e-9
+        t = row["busy_ns_total"] * 1e-9 / CHILD_RUNS
         rec = {"bound": "issue", "busy_ms": round(t * 1e3, 2),
-               "dispatches": row["dispatches_traced"]}
+               "dispatches": row["dispatches_traced"] // CHILD_RUNS}
         kinds = ["SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM",
                  "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_BRANCH"]
         if all(kk + "_total" in row for kk in kinds):
-            insts = sum(row[kk + "_total"] for kk in kinds)
-            mbs = frames * mbs_per_frame
-            rec.update({"instructions": insts, "instructions_per_mb": round(insts / mbs, 1),
+            insts = sum(row[kk + "_total"] for kk in kinds) / CHILD_RUNS
+            mbs = frames * mbs_per_frame * CHILD_RUNS  # per-kind totals below span every run
+            rec.update({"instructions": insts, "instructions_per_mb": round(insts * CHILD_RUNS / mbs, 1),
                         "salu_per_mb": round(row["SQ_INSTS_SALU_total"] / mbs, 1),
                         "valu_per_mb": round(row["SQ_INSTS_VALU_total"] / mbs, 1),
+                        "lds_per_mb": round(row["SQ_INSTS_LDS_total"] / mbs, 1),
+                        "smem_per_mb": round(row["SQ_INSTS_SMEM_total"] / mbs, 1),
+                        "vmem_per_mb": round((row["SQ_INSTS_VMEM_RD_total"] + row["SQ_INSTS_VMEM_WR_total"]) / mbs, 1),
+                        "branch_per_mb": round(row["SQ_INSTS_BRANCH_total"] / mbs, 1),
                         "achieved": round(insts / t / 1e9, 2), "unit": "G instructions/s",
                         "peak": CU_ISSUE_PEAK / 1e9,
                         "frac": round(insts / t / CU_ISSUE_PEAK, 4),
