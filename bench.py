@@ -507,7 +507,8 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
                      "dispatches": row["dispatches_traced"] // CHILD_RUNS, "bytes_per_picture": round(b),
                      "achieved": round(ach, 1), "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4)}
-    row = prof.get("h264_parse_full")
+    pname = "h264_parse_full_cabac" if "h264_parse_full_cabac" in prof else "h264_parse_full"
+    row = prof.get(pname)
     if isinstance(row, dict) and "busy_ns_total" in row:
         t = row["busy_ns_total"] * 1e-9 / CHILD_RUNS
         rec = {"bound": "issue", "busy_ms": round(t * 1e3, 2),
@@ -530,7 +531,7 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
                         "peak_basis": "one instruction per CU per cycle: 256 CUs x 2.4 GHz "
                                       "(the scalar unit a CU's waves share issues at most one "
                                       "SALU instruction per cycle)"})
-        out["h264_parse_full"] = rec
+        out[pname] = rec
     return out
 
 

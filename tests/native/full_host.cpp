@@ -11,6 +11,15 @@
 #include <string>
 #include <vector>
 
+// -DVTS_STATS: count the parser's trace points (VTS_PARSE_TRACE: 0 macroblock,
+// 1 context-coded bin, 2 bypass bin, 3 terminate bin) for fh_stats()
+#ifdef VTS_STATS
+static unsigned long long g_trace[8];
+#define VTS_PARSE_TRACE(k) (++g_trace[(k)])
+extern "C" void fh_stats(unsigned long long *out) {
+  for (int i = 0; i < 8; ++i) out[i] = g_trace[i];
+}
+#endif
 #include "h264.h"
 #include "h264_full.h"
 #include "h264_sched.h"
@@ -161,12 +170,15 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
         bc.col = recs.data() + static_cast<size_t>(col) * nmb;
         bc.col1 = recs1.data() + static_cast<size_t>(col) * nmb;
       }
-      errs |= P.cabac ? full::parse_slice_cabac(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P,
-                                                fr_recs, ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(),
-                                                epoch, &sc, bc)
-                      : full::parse_slice_full(es.data(), fs[static_cast<size_t>(si)], static_cast<uint32_t>(si), P,
-                                               fr_recs, ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(),
-                                               epoch, &sc, bc);
+      // the device's nal_unescape, serially: the payload's RBSP (+ zero padding)
+      std::vector<uint8_t> rbsp(static_cast<size_t>(fsl.nal_size) + 128, 0);
+      const int32_t rlen = full::unescape_nal(es.data() + fsl.nal_offset + 1, fsl.nal_size - 1, rbsp.data());
+      errs |= P.cabac ? full::parse_slice_cabac(rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, fr_recs,
+                                                ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(), epoch, &sc,
+                                                bc)
+                      : full::parse_slice_full(rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, fr_recs,
+                                               ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(), epoch, &sc,
+                                               bc);
     }
     if (errs) return bad("frame " + std::to_string(fi) + ": parse: " + describe_decode_error(errs));
     full::ReconCtx c{};

@@ -10,7 +10,8 @@
 namespace vts {
 
 struct FullParseArgs {
-  const uint8_t *es;         // device elementary stream (+ padding)
+  const uint8_t *rbsp;       // the slice NALs' RBSPs at their ES offsets (nal_unescape_launch)
+  const int32_t *rbsp_len;   // RBSP bytes of this launch's slices (parallel to slices)
   const FullSlice *slices;   // this launch's slices
   int32_t n_slices;
   int32_t slice0;            // window index of slices[0] (MbRec.slice)
@@ -56,6 +57,11 @@ struct FullReconArgs {
   FullParams P;
 };
 
+// 7.4.1 per slice NAL: the payload (after the header byte) without its
+// emulation-prevention bytes, at the same offset of rbsp; rbsp_len[i] = its
+// length.  Once per session: the parsers then read plain RBSP bits.
+int nal_unescape_launch(const uint8_t *es, uint8_t *rbsp, const FullSlice *slices, int32_t n_slices,
+                        int32_t *rbsp_len, hipStream_t s);
 int parse_full_launch(const FullParseArgs &a, hipStream_t s);
 // deblocking descriptors (bS, QPs) of n_frames pictures: reads only the
 // parse's records, so one launch covers a whole window

@@ -3,7 +3,8 @@
 // 16 references, the deblocking filter).  DESIGN.md §5b.
 //
 //   h264_parse_full   one lane per slice: slice_data() -> MbRec + coefficient
-//                     blocks + intra dependency level (parse_full.h)
+//   h264_parse_full_cabac  blocks + intra dependency level (parse_full.h,
+//                     parse_cabac.h), one kernel per entropy mode
 //   h264_inter_full   one lane per 4x4 luma block (+ its 2x2 Cb/Cr) of every
 //                     inter / skip / I_PCM macroblock of every picture of the
 //                     level: 6-tap / bilinear prediction from dword windows,
@@ -27,6 +28,21 @@
 
 #include "common.h"
 #include "decode_full.h"
+#ifdef VTS_EXP_PROF
+// parse section timing (experiment builds): s_memtime deltas per section,
+// summed over all slices; read with vts_debug_parse_prof
+__device__ unsigned long long vts_prof_acc[8];
+#define VTS_PROF(k) prof_mark(k)
+#define VTS_PROF_P(p, k) (p).prof_mark(k)
+#define VTS_PROF_FLUSH(p)                                               \
+  for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&vts_prof_acc[k_], (p).sc->pacc[k_])
+#define VTS_PROF_START(p)                                               \
+  do {                                                                  \
+    for (int k_ = 0; k_ < 8; ++k_) (p).sc->pacc[k_] = 0;                \
+    (p).sc->pt = __builtin_amdgcn_s_memtime();                          \
+    (p).sc->psec = 0;                                                   \
+  } while (0)
+#endif
 #include "parse_cabac.h"
 #include "parse_full.h"
 #include "recon_full.h"
@@ -46,15 +62,16 @@ constexpr int kIntraSlots = kIntraThreads / 16;
 constexpr int kDbkThreads = VTS_DBK_THREADS;      // 1024: 16 waves = 16 row pairs in flight
 constexpr int kDbkWaves = kDbkThreads / 64;
 
-// One slice per wave and the wave's one lane: every value of the parse is
+// One slice per wave: every value of the parse is
 // wave-uniform, so control flow never diverges and the integer work can go to
 // the scalar unit; the parallelism is the window's slices (thousands of waves).
 #ifndef VTS_PARSE_WAVES
 #define VTS_PARSE_WAVES 4
 #endif
-__global__ void __launch_bounds__(1)
-__attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full(FullParseArgs a) {
-  __shared__ full::FullScratch scratch;
+// The entropy mode is per stream, so each mode is its own kernel: a wave only
+// ever runs one parser's code, and each fits the instruction cache better.
+template <bool kCabac>
+__device__ __forceinline__ void parse_one(const FullParseArgs &a, full::FullScratch *scratch) {
   const int i = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
@@ -67,12 +84,65 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
     bc.col = a.recs + col * nmb;
     bc.col1 = a.recs1 + col * nmb;
   }
-  const uint32_t e =
-      P.cabac ? full::parse_slice_cabac(a.es, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
-                                        a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch, bc)
-              : full::parse_slice_full(a.es, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
-                                       a.ilvl + s.slot * nmb, a.arena, a.epoch, &scratch, bc);
+  const uint8_t *rbsp = a.rbsp + s.nal_offset + 1;
+  const int32_t len = a.rbsp_len[i];
+  uint32_t e;
+  if constexpr (kCabac)
+    e = full::parse_slice_cabac(rbsp, len, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
+                                a.ilvl + s.slot * nmb, a.arena, a.epoch, scratch, bc);
+  else
+    e = full::parse_slice_full(rbsp, len, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
+                               a.ilvl + s.slot * nmb, a.arena, a.epoch, scratch, bc);
   if (e) atomicOr(a.err, e);
+}
+// A wave of 64 lanes that all run the same (uniform) parse: the parser's state
+// is scalar, and full EXEC keeps the lane tables (LaneTab, parse_full.h) whole
+// through every VGPR copy the compiler makes (a copy under a one-lane EXEC
+// would move lane 0 only).  Stores of the same value to the same address from
+// every lane coalesce into one.
+__global__ void __launch_bounds__(64)
+__attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full(FullParseArgs a) {
+  __shared__ full::FullScratch scratch;
+  parse_one<false>(a, &scratch);
+}
+__global__ void __launch_bounds__(64)
+__attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full_cabac(FullParseArgs a) {
+  __shared__ full::FullScratch scratch;
+  parse_one<true>(a, &scratch);
+}
+
+// 7.4.1: one workgroup per slice NAL, 256 payload bytes per step; a byte is
+// an emulation-prevention byte by full::is_epb (a local rule), its output
+// index is its own minus the EPBs before it (wave ballots + a 4-entry scan)
+constexpr int kUnescThreads = 256;
+__global__ void __launch_bounds__(kUnescThreads) nal_unescape(const uint8_t *es, uint8_t *rbsp, const FullSlice *sl,
+                                                              int32_t *lens) {
+  __shared__ int wcnt[kUnescThreads / 64];
+  const FullSlice &s = sl[blockIdx.x];
+  const uint8_t *in = es + s.nal_offset + 1;
+  uint8_t *out = rbsp + s.nal_offset + 1;
+  const int32_t n = s.nal_size - 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t removed = 0;
+  for (int32_t c0 = 0; c0 < n; c0 += kUnescThreads) {
+    const int32_t j = c0 + static_cast<int32_t>(threadIdx.x);
+    const bool in_range = j < n;
+    const uint8_t b = in_range ? in[j] : 0;
+    const bool epb = in_range && full::is_epb(in, j);
+    const uint64_t m = __ballot(epb);
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    int before = removed + __popcll(m & ((1ull << lane) - 1ull)), total = 0;
+#pragma unroll
+    for (int k = 0; k < kUnescThreads / 64; ++k) {
+      before += k < w ? wcnt[k] : 0;
+      total += wcnt[k];
+    }
+    if (in_range && !epb) out[j - before] = b;
+    __syncthreads();
+    removed += total;
+  }
+  if (threadIdx.x == 0) lens[blockIdx.x] = n - removed;
 }
 
 // ------------------------------------------------------------------ helpers
@@ -1250,9 +1320,27 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
 
 }  // namespace
 
+#ifdef VTS_EXP_PROF
+extern "C" int vts_debug_parse_prof(unsigned long long *out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_prof_acc), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  unsigned long long z[8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(vts_prof_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
+int nal_unescape_launch(const uint8_t *es, uint8_t *rbsp, const FullSlice *slices, int32_t n_slices,
+                        int32_t *rbsp_len, hipStream_t s) {
+  if (n_slices <= 0) return VTS_OK;
+  hipLaunchKernelGGL(nal_unescape, dim3(n_slices), dim3(kUnescThreads), 0, s, es, rbsp, slices, rbsp_len);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "nal_unescape launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
 int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
   if (a.n_slices <= 0) return VTS_OK;
-  hipLaunchKernelGGL(h264_parse_full, dim3(a.n_slices), dim3(1), 0, s, a);
+  if (a.P.cabac) hipLaunchKernelGGL(h264_parse_full_cabac, dim3(a.n_slices), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(h264_parse_full, dim3(a.n_slices), dim3(64), 0, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_parse_full launch: %s", hipGetErrorString(e));
   return VTS_OK;

@@ -6,7 +6,9 @@
 // coefficient blocks, intra dependency level) plus, for the reconstruction,
 // transform_size_8x8_flag (MbRec.modes bit 4) and 8x8 coefficient blocks.
 //
-// Context state lives in LDS (FullScratch.cst, one byte per ctxIdx).  The
+// Context states and the engine's tables live in lane tables (LaneTab: the
+// idle lanes of a few VGPRs, read and written with v_readlane / v_writelane),
+// so a bin costs no memory access.  The
 // neighbour facts CABAC's context selection needs come through the CAVLC
 // parser's LDS neighbour copies: coded_block_flag bits in the (CAVLC-only)
 // nzc bytes, clamped |mvd| of inter macroblocks' bottom rows in their i4
@@ -27,70 +29,148 @@ namespace full {
 #endif
 VTS_CTAB int8_t kCabInitI[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_I_DATA;
 VTS_CTAB int8_t kCabInitP[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_P0_DATA;
-VTS_CTAB uint8_t kRangeLps[64][4] = VTS_CABAC_RANGE_LPS_DATA;
-VTS_CTAB uint8_t kTransLps[64] = VTS_CABAC_TRANS_LPS_DATA;
-VTS_CTAB uint8_t kSig8[63] = VTS_SIG8x8_DATA;
-VTS_CTAB uint8_t kLast8[63] = VTS_LAST8x8_DATA;
-VTS_CTAB uint8_t kZz8[64] = VTS_ZZ8_DATA;
-VTS_CTAB uint8_t kCbfOff[5] = {0, 4, 8, 12, 16};
-VTS_CTAB uint8_t kSigOff[5] = {0, 15, 29, 44, 47};
-VTS_CTAB uint8_t kAbsOff[5] = {0, 10, 20, 30, 39};
-VTS_CTAB uint8_t kMvdInc[8] = {3, 4, 5, 6, 6, 6, 6, 6};
 #undef VTS_CTAB
 
+// The engine's tables as 64 dwords each, loaded into lane tables (LaneTab) at
+// slice start: rangeTabLPS[pStateIdx][0..3] in bytes 0..3; transIdxLPS; the
+// 8x8 block's significant / last ctxIdxInc (Table 9-43, frame) and zig-zag
+// position of coefficient i in bytes 0 / 1 / 2
+struct CabLanes {
+  uint32_t lps[64], trans[64], s8[64];
+};
+constexpr CabLanes make_cab_lanes() {
+  CabLanes t{};
+  const uint8_t r[64][4] = VTS_CABAC_RANGE_LPS_DATA;
+  const uint8_t tr[64] = VTS_CABAC_TRANS_LPS_DATA;
+  const uint8_t sig[63] = VTS_SIG8x8_DATA;
+  const uint8_t last[63] = VTS_LAST8x8_DATA;
+  const uint8_t zz[64] = VTS_ZZ8_DATA;
+  for (int i = 0; i < 64; ++i) {
+    t.lps[i] = r[i][0] | (uint32_t(r[i][1]) << 8) | (uint32_t(r[i][2]) << 16) | (uint32_t(r[i][3]) << 24);
+    t.trans[i] = tr[i];
+    t.s8[i] = (i < 63 ? sig[i] | (uint32_t(last[i]) << 8) : 0u) | (uint32_t(zz[i]) << 16);
+  }
+  return t;
+}
+#if defined(__HIPCC__)
+__device__ __constant__ static const CabLanes kCabLanes = make_cab_lanes();
+#else
+static const CabLanes kCabLanes = make_cab_lanes();
+#endif
+// per-category ctxIdxOffset parts (ctxBlockCat 0..4) as byte fields of one constant
+VTS_HD VTS_INLINE int cbf_off(int cat) { return static_cast<int>((0x100C080400ull >> (8 * cat)) & 255u); }
+VTS_HD VTS_INLINE int sig_off(int cat) { return static_cast<int>((0x2F2C1D0F00ull >> (8 * cat)) & 255u); }
+VTS_HD VTS_INLINE int abs_off(int cat) { return static_cast<int>((0x271E140A00ull >> (8 * cat)) & 255u); }
+
 struct CabacParser : Parser {
-  uint32_t range, offset;
+  // The engine (9.3.1.2, 9.3.3.2) with codIOffset scaled: val holds the 9-bit
+  // codIOffset in bits 31..23 and the next `la` bitstream bits below it, so
+  // renormalisation is a shift of val and the bit reader is touched once per
+  // 16 bits (la < 8 -> 16 more), not per bin.  codIOffset >= codIRange is
+  // val >= codIRange << 23.
+  uint32_t range, val;
+  int32_t la;
   bool prev_qpd;  // the previous macroblock of the slice has mb_qp_delta != 0
+  // context states (pStateIdx << 1 | valMPS), four per dword: ctxIdx c in
+  // st[c >> 8], lane (c >> 2) & 63, byte c & 3
+  LaneTab st[2];
+  LaneTab lps, trn, s8;  // kCabLanes
 
   // ---------------------------------------------- arithmetic decoder (9.3.3.2)
-  VTS_HD VTS_INLINE void cab_start() {  // 9.3.1.2
+  VTS_HD VTS_INLINE void cab_start() {  // 9.3.1.2: codIOffset = read_bits(9)
     range = 510;
-    offset = br.bits(9);
+    val = br.bits(32);
+    la = 23;
+  }
+  // bits the engine has consumed (9.3.1.2's 9 + every renormalisation shift)
+  VTS_HD VTS_INLINE int32_t cab_consumed() const { return br.consumed() - la; }
+  VTS_HD VTS_INLINE void cab_fill() {
+    if (la < 8) {
+      val |= br.bits(16) << (7 - la);
+      la += 16;
+    }
+  }
+  VTS_HD VTS_INLINE void cab_tables() {
+    for (int i = 0; i < 64; ++i) {
+      lps.set(i, kCabLanes.lps[i]);
+      trn.set(i, kCabLanes.trans[i]);
+      s8.set(i, kCabLanes.s8[i]);
+    }
   }
   VTS_HD VTS_INLINE void cab_init(bool is_i, int qp) {  // 9.3.1.1
     const int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
-    for (int i = 0; i < VTS_CABAC_NCTX; ++i) {
-      const int m = is_i ? kCabInitI[i][0] : kCabInitP[i][0], n = is_i ? kCabInitI[i][1] : kCabInitP[i][1];
-      int pre = ((m * q) >> 4) + n;
-      pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
-      sc->cst[i] = static_cast<uint8_t>(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1);
+    for (int w = 0; w < 128; ++w) {
+      uint32_t word = 0;
+      for (int b = 0; b < 4; ++b) {
+        const int i = 4 * w + b;
+        if (i >= VTS_CABAC_NCTX) break;
+        const int m = is_i ? kCabInitI[i][0] : kCabInitP[i][0], n = is_i ? kCabInitI[i][1] : kCabInitP[i][1];
+        int pre = ((m * q) >> 4) + n;
+        pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
+        word |= static_cast<uint32_t>(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1) << (8 * b);
+      }
+      if (w < 64) st[0].set(w, word);
+      else st[1].set(w - 64, word);
     }
   }
   VTS_HD VTS_INLINE uint32_t dec(int ctx) {  // DecodeDecision
-    const uint32_t s = sc->cst[ctx], ps = s >> 1, mps = s & 1u;
-    const uint32_t lps = kRangeLps[ps][(range >> 6) & 3u];
-    range -= lps;
-    uint32_t bin;
-    if (offset >= range) {
-      bin = mps ^ 1u;
-      offset -= range;
-      range = lps;
-      sc->cst[ctx] = static_cast<uint8_t>((kTransLps[ps] << 1) | (ps == 0 ? (mps ^ 1u) : mps));
+    VTS_PARSE_TRACE(1);
+    const uint32_t ln = static_cast<uint32_t>(ctx >> 2) & 63u, sh = static_cast<uint32_t>(ctx & 3) * 8u;
+    // which of the two lane tables: folded where ctx is a constant, else both
+    // are read and written with selects (no branch)
+    const bool fixed = __builtin_constant_p(ctx < 256), hi = ctx >= 256;
+    const uint32_t wa = fixed && hi ? 0u : st[0].get(ln), wb = fixed && !hi ? 0u : st[1].get(ln);
+    const uint32_t word = hi ? wb : wa;
+    const uint32_t s = (word >> sh) & 127u, ps = s >> 1, mps = s & 1u;
+    const uint32_t lpsr = (lps.get(ps) >> ((range >> 3) & 24u)) & 255u;
+    range -= lpsr;
+    const uint32_t rs = range << 23;
+    const bool lpsb = val >= rs;
+    const uint32_t bin = mps ^ (lpsb ? 1u : 0u);
+    const uint32_t ns = lpsb ? (trn.get(ps) << 1) | (ps == 0 ? (mps ^ 1u) : mps)
+                             : ((ps < 62 ? ps + 1 : 62) << 1) | mps;
+    val -= lpsb ? rs : 0u;
+    range = lpsb ? lpsr : range;
+    const uint32_t nw = (word & ~(255u << sh)) | (ns << sh);
+    if (fixed) {
+      if (hi) st[1].set(ln, nw);
+      else st[0].set(ln, nw);
     } else {
-      bin = mps;
-      sc->cst[ctx] = static_cast<uint8_t>(((ps < 62 ? ps + 1 : 62) << 1) | mps);
+      st[0].set(ln, hi ? wa : nw);
+      st[1].set(ln, hi ? nw : wb);
     }
-    if (range < 256) {  // RenormD as one shift
-      const int n = __builtin_clz(range) - 23;
-      range <<= n;
-      offset = (offset << n) | br.bits(n);
-    }
+    const int n = __builtin_clz(range) - 23;  // RenormD as one shift (0..6)
+    range <<= n;
+    val <<= n;
+    la -= n;
+    cab_fill();
     return bin;
   }
   VTS_HD VTS_INLINE uint32_t bypass() {  // DecodeBypass
-    offset = (offset << 1) | br.bit();
-    if (offset >= range) {
-      offset -= range;
+    VTS_PARSE_TRACE(2);
+    // the doubled codIOffset needs 10 bits: its top bit leaves val, and then
+    // the offset is >= codIRange whatever val holds (val - rs wraps to the
+    // right difference)
+    const uint32_t top = val >> 31;
+    val <<= 1;
+    --la;
+    cab_fill();
+    const uint32_t rs = range << 23;
+    if (top || val >= rs) {
+      val -= rs;
       return 1;
     }
     return 0;
   }
   VTS_HD VTS_INLINE uint32_t term() {  // DecodeTerminate: 1 ends parsing, no renormalisation
+    VTS_PARSE_TRACE(3);
     range -= 2;
-    if (offset >= range) return 1;
+    if (val >= (range << 23)) return 1;
     if (range < 256) {
       range <<= 1;
-      offset = (offset << 1) | br.bit();
+      val <<= 1;
+      --la;
+      cab_fill();
     }
     return 0;
   }
@@ -268,6 +348,7 @@ struct CabacParser : Parser {
       r0[k] = r1[k] = -1;
     }
     if (mb_type == 0) {  // B_Direct_16x16
+      VTS_PARSE_TRACE(6);
       cur1().direct = 0x0f | kDirect16;
       if (!direct8x8) *small = true;
       direct_pred(addr, 0xffffu);
@@ -349,11 +430,11 @@ struct CabacParser : Parser {
           const uint8_t ax = static_cast<uint8_t>(vts_min(dx < 0 ? -dx : dx, 33));
           const uint8_t ay = static_cast<uint8_t>(vts_min(dy < 0 ? -dy : dy, 33));
           uint8_t(*mc)[2] = l ? sc->mvdc1 : sc->mvdc;
-          for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
-            for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
-              mc[yy * 4 + xx][0] = ax;
-              mc[yy * 4 + xx][1] = ay;
-            }
+          const uint32_t bm = blk_mask(sx, sy, pw, ph);
+          VTS_LANES(16, b) if ((bm >> b) & 1u) {
+            mc[b][0] = ax;
+            mc[b][1] = ay;
+          }
         }
       }
     // the references the parse recorded are set again by the motion below
@@ -366,7 +447,7 @@ struct CabacParser : Parser {
   VTS_HD VTS_INLINE int mvd(int base, int sum) {  // U prefix cMax 9 + UEG3 + sign
     if (!dec(base + (sum < 3 ? 0 : (sum > 32 ? 2 : 1)))) return 0;
     int v = 1;
-    while (v < 9 && dec(base + kMvdInc[v - 1])) ++v;
+    while (v < 9 && dec(base + vts_min(v + 2, 6))) ++v;  // ctxIdxInc 3, 4, 5, 6, 6, ...
     if (v >= 9) {
       int k = 3;
       while (bypass()) {
@@ -380,19 +461,27 @@ struct CabacParser : Parser {
     }
     return bypass() ? -v : v;
   }
-  // residual_block_cabac (7.3.5.3.3): levels in list order into sc->lv;
+  // residual_block_cabac (7.3.5.3.3): each level goes straight to its raster
+  // position in dst, which the caller has zeroed (4x4 blocks: zig-zag position
+  // of coefficient start + i; 8x8: the 8x8 zig-zag; chroma DC: list order);
   // count of non-zero levels (0: coded_block_flag 0), -1 on error
-  VTS_HD VTS_INLINE int residual(int cat, int cbf_inc, int maxNum) {
-    int16_t *lv = sc->lv;
-    zero16x(lv, maxNum == 15 ? 16 : maxNum < 8 ? 8 : maxNum);
-    if (cat != 5 && !dec(85 + kCbfOff[cat] + cbf_inc)) return 0;
+  VTS_HD VTS_INLINE int residual(int cat, int cbf_inc, int maxNum, int16_t *dst, int start) {
+    if (cat != 5 && !dec(85 + cbf_off(cat) + cbf_inc)) return 0;
     uint64_t sig = 0;
     int numc = maxNum;
+    const int sig_base = cat == 5 ? 402 : 105 + sig_off(cat), last_base = cat == 5 ? 417 : 166 + sig_off(cat);
     for (int i = 0; i < numc - 1; ++i) {
-      const int inc = cat == 3 ? vts_min(i, 2) : i;
-      if (dec(cat == 5 ? 402 + kSig8[i] : 105 + kSigOff[cat] + inc)) {
+      int inc_s, inc_l;
+      if (cat == 5) {
+        const uint32_t e = s8.get(static_cast<uint32_t>(i));
+        inc_s = static_cast<int>(e & 255u);
+        inc_l = static_cast<int>((e >> 8) & 255u);
+      } else {
+        inc_s = inc_l = cat == 3 ? vts_min(i, 2) : i;
+      }
+      if (dec(sig_base + inc_s)) {
         sig |= 1ull << i;
-        if (dec(cat == 5 ? 417 + kLast8[i] : 166 + kSigOff[cat] + inc)) {
+        if (dec(last_base + inc_l)) {
           numc = i + 1;
           break;
         }
@@ -400,7 +489,7 @@ struct CabacParser : Parser {
     }
     sig |= 1ull << (numc - 1);
     int eq1 = 0, gt1 = 0, n = 0;
-    const int base = cat == 5 ? 426 : 227 + kAbsOff[cat];
+    const int base = cat == 5 ? 426 : 227 + abs_off(cat);
     for (int i = numc - 1; i >= 0; --i) {
       if (!((sig >> i) & 1ull)) continue;
       int v = 0;
@@ -420,7 +509,9 @@ struct CabacParser : Parser {
       int lvl = v + 1;
       if (bypass()) lvl = -lvl;
       if (lvl > 32767 || lvl < -32768) return -1;
-      lv[i] = static_cast<int16_t>(lvl);
+      const int pos = cat == 5 ? static_cast<int>((s8.get(static_cast<uint32_t>(i)) >> 16) & 63u)
+                               : (cat == 3 ? i : zz4(i + start));
+      dst[pos] = static_cast<int16_t>(lvl);
       if (v == 0) ++eq1;
       else ++gt1;
       ++n;
@@ -431,13 +522,15 @@ struct CabacParser : Parser {
   // ------------------------------------------------------ macroblock_layer
   // (begin_mb done by the caller); returns false to stop the slice
   VTS_HD VTS_INLINE bool mb_cabac(int addr, int *qp) {
+    VTS_PROF(2);
     MbRec &m = cur();
     int xw, yw;
     const int A = nb_mb(addr, -1, 0, 16, &xw, &yw), B = nb_mb(addr, 0, -1, 16, &xw, &yw);
     int itype, mb_type = 0;
-    for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
-    if (bframes)
-      for (int i = 0; i < 16; ++i) sc->mvdc1[i][0] = sc->mvdc1[i][1] = 0;
+    VTS_LANES(32, i) {
+      if (i < 16) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
+      else if (bframes) sc->mvdc1[i - 16][0] = sc->mvdc1[i - 16][1] = 0;
+    }
     if (s->is_p == kSliceB) {
       const int t = b_type((A != -1 && !(rec1(A).direct & kDirect16) ? 1 : 0) +
                            (B != -1 && !(rec1(B).direct & kDirect16) ? 1 : 0));
@@ -457,6 +550,7 @@ struct CabacParser : Parser {
     if (itype == 25) {  // I_PCM: alignment, 384 samples through the RBSP reader, engine restart
       m.type = kMbPcm;
       m.qp = static_cast<uint8_t>(*qp);
+      br.reset_at(cab_consumed());  // the engine's lookahead goes back to the bit reader
       br.align();
       for (int j = 0; j < 16; ++j) m.nz[j] = 16;
       for (int k = 0; k < 12; ++k) {
@@ -513,8 +607,10 @@ struct CabacParser : Parser {
       m.modes = static_cast<uint8_t>((itype - 1) % 4);
     } else if (s->is_p == kSliceB) {  // Table 7-14
       m.type = kMbInter;
+      VTS_PROF(3);
       if (!b_inter_cabac(addr, mb_type, &small)) return false;
     } else {  // inter (Table 7-13)
+      VTS_PROF(3);
       m.type = kMbInter;
       const int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
       int8_t *sub = sc->sub, *refs = sc->refs;
@@ -575,16 +671,18 @@ struct CabacParser : Parser {
           }
           const uint8_t ax = static_cast<uint8_t>(vts_min(dx < 0 ? -dx : dx, 33));
           const uint8_t ay = static_cast<uint8_t>(vts_min(dy < 0 ? -dy : dy, 33));
-          for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
-            for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
-              set_motion(yy * 4 + xx, refs[k], vx, vy);
-              sc->mvdc[yy * 4 + xx][0] = ax;
-              sc->mvdc[yy * 4 + xx][1] = ay;
-              done |= 1u << (yy * 4 + xx);
-            }
+          const uint32_t bm = blk_mask(sx, sy, pw, ph);
+          const int rk = refs[k];
+          VTS_LANES(16, b) if ((bm >> b) & 1u) {
+            set_motion(b, rk, vx, vy);
+            sc->mvdc[b][0] = ax;
+            sc->mvdc[b][1] = ay;
+          }
+          done |= bm;
         }
       }
     }
+    VTS_PROF(2);
     if (m.type == kMbI4x4 || m.type == kMbI16) {  // intra_chroma_pred_mode, TU cMax 3
       int inc = 0;
 #pragma unroll
@@ -604,6 +702,7 @@ struct CabacParser : Parser {
       }
       m.modes = static_cast<uint8_t>(m.modes | (cm << 2));
     }
+    VTS_PROF(4);
     if (m.type != kMbI16) {  // coded_block_pattern (9.3.3.1.1.4)
       for (int b8 = 0; b8 < 4; ++b8) {
         const int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
@@ -666,86 +765,74 @@ struct CabacParser : Parser {
     // ---- residual (7.3.5.3), blocks in bitstream order
     const bool intra = m.type == kMbI4x4 || m.type == kMbI16;
     const bool t8 = (m.modes & kModeT8) != 0;
-    if (m.type == kMbI16) {
-      int inc = 0;
+    // the blocks present, in bitstream order = kBlk* bit order; an 8x8 block
+    // is its quarter's first 4x4 bit.  One residual() site for all of them.
+    uint32_t todo = m.type == kMbI16 ? 1u << kBlkI16Dc : 0u;
+    for (int q = 0; q < 4; ++q)
+      if ((cbp >> q) & 1) todo |= (t8 ? 1u : 15u) << (kBlkLuma0 + 4 * q);
+    if (cbp >> 4) todo |= 3u << kBlkChromaDc0;
+    if ((cbp >> 4) == 2) todo |= 255u << kBlkChromaAc0;
+    VTS_PROF(5);
+    while (todo) {
+      const uint32_t bt = static_cast<uint32_t>(__builtin_ctz(todo));
+      todo &= todo - 1u;
+      int cat, inc = 0, maxNum = 16, start = 0, r = 0;
+      int16_t *dst = sc->blk;
+      if (bt == kBlkI16Dc) {
+        cat = 0;
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const int n = nb ? B : A;
-        inc += cbf_cond(n, true, n != -1 && rec(n).type == kMbI16, 0) << nb;
+        for (int nb = 0; nb < 2; ++nb) {
+          const int n = nb ? B : A;
+          inc += cbf_cond(n, true, n != -1 && rec(n).type == kMbI16, 0) << nb;
+        }
+      } else if (bt < kBlkChromaDc0) {
+        const int k = static_cast<int>(bt) - kBlkLuma0, bx = blk_x(k), by = blk_y(k);
+        r = by * 4 + bx;
+        if (t8) {
+          cat = 5;
+          maxNum = 64;
+          dst = sc->blk8;
+        } else {
+          cat = m.type == kMbI16 ? 1 : 2;
+          if (cat == 1) {
+            maxNum = 15;
+            start = 1;
+          }
+          inc = cbf_luma_inc(addr, bx, by, intra);
+        }
+      } else if (bt < kBlkChromaAc0) {
+        cat = 3;
+        maxNum = 4;
+        inc = cbf_chroma_inc(addr, static_cast<int>(bt) - kBlkChromaDc0, 0, true, intra);
+      } else {
+        const int j = static_cast<int>(bt) - kBlkChromaAc0;
+        cat = 4;
+        maxNum = 15;
+        start = 1;
+        inc = cbf_chroma_inc(addr, j >> 2, j & 3, false, intra);
       }
-      const int nc = residual(0, inc, 16);
+      zero16x(dst, cat == 5 ? 64 : 16);
+      const int nc = residual(cat, inc, maxNum, dst, start);
       if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
-      if (nc) {
-        for (int i = 0; i < 16; ++i) sc->blk[kZz[i]] = sc->lv[i];
-        set_cbf(0);
-        if (!store_block(kBlkI16Dc)) { err |= DEC_E_SYNTAX; return false; }
-      }
-    }
-    for (int b8 = 0; b8 < 4; ++b8) {
-      if (!((cbp >> b8) & 1)) continue;
-      const int r0 = (b8 >> 1) * 8 + (b8 & 1) * 2;
-      if (t8) {
-        const int nc = residual(5, 0, 64);
-        if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
-        const int rs[4] = {r0, r0 + 1, r0 + 4, r0 + 5};
+      if (cat == 5) {  // the quarter's 4 blocks: raster 8x8 rows 2j, 2j + 1
+        const int rs[4] = {r, r + 1, r + 4, r + 5};
         for (int j = 0; j < 4; ++j) {
           m.nz[rs[j]] = static_cast<uint8_t>(nc > 255 ? 255 : nc);
           set_cbf(1u + static_cast<uint32_t>(rs[j]));
         }
-        if (nc) {  // raster 8x8 over the quarter's 4 blocks: block j = rows 2j, 2j + 1
-          for (int j = 0; j < 4; ++j) {
-            zero16x(sc->blk, 16);
-            for (int i = 0; i < 64; ++i) {
-              const int pos = kZz8[i];
-              if ((pos >> 4) == j) sc->blk[pos & 15] = sc->lv[i];
-            }
-            if (!store_block(kBlkLuma0 + 4 * b8 + j)) { err |= DEC_E_SYNTAX; return false; }
-          }
-        }
+        if (nc)
+          for (int j = 0; j < 4; ++j)
+            if (!store_block(bt + j, sc->blk8 + 16 * j)) { err |= DEC_E_SYNTAX; return false; }
         continue;
       }
-      for (int i4 = 0; i4 < 4; ++i4) {
-        const int k = b8 * 4 + i4, bx = blk_x(k), by = blk_y(k), r = by * 4 + bx;
-        const int inc = cbf_luma_inc(addr, bx, by, intra);
-        const int nc = m.type == kMbI16 ? residual(1, inc, 15) : residual(2, inc, 16);
-        if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
-        m.nz[r] = static_cast<uint8_t>(nc);
-        if (nc) {
-          zero16x(sc->blk, 16);
-          if (m.type == kMbI16)
-            for (int i = 0; i < 15; ++i) sc->blk[kZz[i + 1]] = sc->lv[i];
-          else
-            for (int i = 0; i < 16; ++i) sc->blk[kZz[i]] = sc->lv[i];
-          set_cbf(1u + static_cast<uint32_t>(r));
-          if (!store_block(kBlkLuma0 + k)) { err |= DEC_E_SYNTAX; return false; }
-        }
+      if (cat == 1 || cat == 2) m.nz[r] = static_cast<uint8_t>(nc);
+      if (nc) {
+        set_cbf(bt == kBlkI16Dc ? 0u : (cat <= 2 ? 1u + static_cast<uint32_t>(r) : bt));
+        if (!store_block(bt)) { err |= DEC_E_SYNTAX; return false; }
       }
     }
-    if (cbp >> 4) {
-      for (int pl = 0; pl < 2; ++pl) {
-        const int nc = residual(3, cbf_chroma_inc(addr, pl, 0, true, intra), 4);
-        if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
-        if (nc) {
-          for (int i = 0; i < 16; ++i) sc->blk[i] = i < 4 ? sc->lv[i] : 0;
-          set_cbf(17u + static_cast<uint32_t>(pl));
-          if (!store_block(kBlkChromaDc0 + pl)) { err |= DEC_E_SYNTAX; return false; }
-        }
-      }
-    }
-    if ((cbp >> 4) == 2) {
-      for (int pl = 0; pl < 2; ++pl)
-        for (int b = 0; b < 4; ++b) {
-          const int nc = residual(4, cbf_chroma_inc(addr, pl, b, false, intra), 15);
-          if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
-          if (nc) {
-            zero16x(sc->blk, 16);
-            for (int i = 0; i < 15; ++i) sc->blk[kZz[i + 1]] = sc->lv[i];
-            set_cbf(19u + static_cast<uint32_t>(4 * pl + b));
-            if (!store_block(kBlkChromaAc0 + 4 * pl + b)) { err |= DEC_E_SYNTAX; return false; }
-          }
-        }
-    }
-    if (br.err || br.overrun()) {
+    VTS_PROF(6);
+    if (br.err || cab_consumed() > 8 * br.size) {
       err |= DEC_E_SYNTAX;
       return false;
     }
@@ -780,11 +867,11 @@ struct CabacParser : Parser {
   bool P_t8mode;
 };
 
-// Parse CABAC slice `s` (window slice index si).  Returns DEC_E_* bits.
-VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams P,
-                                         MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena, uint32_t epoch,
-                                         FullScratch *sc, const BCtx &bc) {
-  const uint8_t *nal = es + s.nal_offset;
+// Parse CABAC slice `s` (window slice index si) from its RBSP (rbsp_len
+// bytes, emulation-prevention bytes removed).  Returns DEC_E_* bits.
+VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_len, const FullSlice &s, uint32_t si,
+                                         const FullParams P, MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena,
+                                         uint32_t epoch, FullScratch *sc, const BCtx &bc) {
   CabacParser p;
   p.bc = bc;
   p.bframes = P.bframes;
@@ -812,20 +899,19 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice 
   p.cur_i16 = false;
   p.prev_qpd = false;
   const int nmb = P.mb_width * P.mb_height;
-  // the RBSP stop bit, past any trailing cabac_zero_words (00 00 03 in the EBSP)
-  int32_t last = s.nal_size - 1;
-  while (last > 0 && (nal[last] == 0 || (nal[last] == 3 && last >= 2 && nal[last - 1] == 0 && nal[last - 2] == 0)))
-    --last;
-  if (last <= 0) return DEC_E_SYNTAX;
-  const int tz = __builtin_ctz(static_cast<uint32_t>(nal[last]));
-  const int64_t stop_bit = int64_t(last - 1) * 8 + (7 - tz);
-  p.br.init(nal + 1, s.nal_offset + 1, s.nal_size - 1, sc->cache);
-  p.br.reset_at(s.data_byte, s.data_bit & ~7);
-  p.br.ensure(8);
-  p.br.skip(s.data_bit & 7);
+  // the RBSP stop bit, past any trailing cabac_zero_words (zero bytes once
+  // their emulation-prevention bytes are gone)
+  int32_t last = rbsp_len - 1;
+  while (last >= 0 && rbsp[last] == 0) --last;
+  if (last < 0) return DEC_E_SYNTAX;
+  const int64_t stop_bit = int64_t(last) * 8 + (7 - __builtin_ctz(static_cast<uint32_t>(rbsp[last])));
+  p.br.init(rbsp, rbsp_len, sc->cache);
+  p.br.reset_at(s.data_bit);
   // cabac_alignment_one_bit
   while (p.br.consumed() & 7)
     if (!p.br.bit()) return DEC_E_SYNTAX;
+  VTS_PROF_START(p);
+  p.cab_tables();
   p.cab_init(!s.is_p, s.qp);
   p.cab_start();
   for (int i = 0; i < 4; ++i) sc->mvdl[i][0] = sc->mvdl[i][1] = sc->mvdl1[i][0] = sc->mvdl1[i][1] = 0;
@@ -835,30 +921,37 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *es, const FullSlice 
       p.err |= DEC_E_SYNTAX;
       break;
     }
+    VTS_PROF_P(p, 1);
     p.begin_mb(addr);
-    bool ok = true;
+    VTS_PROF_P(p, 2);
+    bool ok = true, skip = false;
     if (s.is_p) {
       int xw, yw;
       const int A = p.nb_mb(addr, -1, 0, 16, &xw, &yw), B = p.nb_mb(addr, 0, -1, 16, &xw, &yw);
-      if (p.dec((s.is_p == kSliceB ? 24 : 11) + (p.avail_not(A, kMbSkip) ? 1 : 0) + (p.avail_not(B, kMbSkip) ? 1 : 0))) {
-        if (s.is_p == kSliceB) p.b_skip_body(addr, qp);
-        else p.skip_body(addr, qp);
-        for (int i = 0; i < 16; ++i) sc->mvdc[i][0] = sc->mvdc[i][1] = sc->mvdc1[i][0] = sc->mvdc1[i][1] = 0;
-        p.prev_qpd = false;
-      } else {
-        ok = p.mb_cabac(addr, &qp);
-      }
+      skip = p.dec((s.is_p == kSliceB ? 24 : 11) + (p.avail_not(A, kMbSkip) ? 1 : 0) +
+                   (p.avail_not(B, kMbSkip) ? 1 : 0)) != 0;
+    }
+    if (skip) {
+      VTS_PARSE_TRACE(s.is_p == kSliceB ? 4 : 5);
+      VTS_PROF_P(p, 3);
+      if (s.is_p == kSliceB) p.b_skip_body(addr, qp);
+      else p.skip_body(addr, qp);
+      VTS_LANES(16, i) sc->mvdc[i][0] = sc->mvdc[i][1] = sc->mvdc1[i][0] = sc->mvdc1[i][1] = 0;
+      p.prev_qpd = false;
     } else {
-      ok = p.mb_cabac(addr, &qp);
+      ok = p.mb_cabac(addr, &qp);  // one inlined copy for every slice type
     }
     if (!ok || p.err) break;
+    VTS_PROF_P(p, 6);
     p.finish_mvd();
     p.end_mb(addr);
     ++addr;
     if (p.term()) break;  // end_of_slice_flag
   }
+  VTS_PROF_P(p, 7);
+  VTS_PROF_FLUSH(p);
   // the arithmetic decoder has read through the stop bit
-  if (!p.err && (p.br.err || p.br.overrun() || p.br.consumed() != stop_bit - 8ll * p.br.epb + 1)) p.err |= DEC_E_SYNTAX;
+  if (!p.err && (p.br.err || p.cab_consumed() != stop_bit + 1)) p.err |= DEC_E_SYNTAX;
   return p.err;
 }
 

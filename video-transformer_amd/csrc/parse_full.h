@@ -23,6 +23,13 @@
 #ifndef VTS_PARSE_TRACE
 #define VTS_PARSE_TRACE(...)
 #endif
+// section markers of the parse (VTS_EXP_PROF builds time them: decode_full.hip)
+#ifndef VTS_PROF
+#define VTS_PROF(k)
+#define VTS_PROF_P(p, k)
+#define VTS_PROF_FLUSH(p)
+#define VTS_PROF_START(p)
+#endif
 
 namespace vts {
 namespace full {
@@ -158,9 +165,181 @@ VTS_HD VTS_INLINE void zero16x(int16_t *p, int n) {
   }
 }
 
+// 64 dwords the single parse lane indexes at run time without a memory access:
+// on the device the lanes of one VGPR (v_readlane / v_writelane with the lane
+// in an SGPR; the kernel runs one lane per wave, so the other 63 lanes of every
+// VGPR are free storage), on the host an array.  A byte table read this way
+// costs one VALU instruction instead of a dependent global load (the __constant__
+// byte tables compile to global_load_ubyte through the GOT).
+#if defined(__HIP_DEVICE_COMPILE__)
+// the intrinsic behind v_writelane_b32 (this compiler has no builtin for it)
+extern "C" __device__ int vts_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane");
+#endif
+struct LaneTab {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // seeded with the lane id: the value must be divergent (a VGPR), or the
+  // compiler treats the all-uniform writelane chain as one uniform value and
+  // folds every readlane of it to that value
+  uint32_t v = __builtin_amdgcn_mbcnt_lo(~0u, 0u);
+  __device__ VTS_INLINE uint32_t get(uint32_t i) const {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(i)));
+  }
+  __device__ VTS_INLINE void set(uint32_t i, uint32_t x) {
+    v = static_cast<uint32_t>(vts_writelane(static_cast<int>(x), static_cast<int>(i), static_cast<int>(v)));
+  }
+#else
+  uint32_t v[64];
+  uint32_t get(uint32_t i) const { return v[i & 63]; }
+  void set(uint32_t i, uint32_t x) { v[i & 63] = x; }
+#endif
+};
+
+// ------------------------------------------------------------ RBSP bits
+// 7.4.1: byte j of a NAL payload (after the header byte) is an
+// emulation_prevention_three_byte iff it is 0x03 after two zero payload bytes
+// (00 00 03 00 00 03 holds two: an EPB resets the zero count, and the two
+// zeros before the second one are bytes 3 and 4).  The device removes them
+// once per session (nal_unescape in decode_full.hip, one workgroup per slice
+// NAL); this is the same rule, serially (the CPU harness).
+VTS_HD VTS_INLINE bool is_epb(const uint8_t *p, int32_t j) { return j >= 2 && p[j] == 3 && p[j - 1] == 0 && p[j - 2] == 0; }
+VTS_HD VTS_INLINE int32_t unescape_nal(const uint8_t *in, int32_t n, uint8_t *out) {
+  int32_t o = 0;
+  for (int32_t j = 0; j < n; ++j)
+    if (!is_epb(in, j)) out[o++] = in[j];
+  return o;
+}
+
+// The general parsers' bit reader: a left-aligned 64-bit window over an
+// RBSP (no emulation-prevention bytes left, so a refill is one 4-byte append)
+// filled from kW - 1 cached payload dwords in per-lane scratch (LDS on the
+// device).  Bits past the RBSP read as zeros and make overrun() true.
+template <int kW>
+struct RbspBitsT {
+  const uint8_t *base;   // first RBSP byte of the payload
+  uint64_t win;          // next bits, MSB first
+  int32_t nb;            // valid bits in win
+  int32_t fill;          // bits appended to the window so far (incl. zero padding)
+  int32_t size;          // RBSP bytes
+  int32_t pos;           // next byte to append
+  int32_t cache_at;      // payload index of cache[0] (multiple of 4 (kW - 1)), -1 none
+  uint32_t *cache;       // kW dwords from cache_at (per-lane scratch)
+  bool err;
+
+  VTS_HD VTS_INLINE void init(const uint8_t *p, int32_t n, uint32_t *scratch) {
+    cache = scratch;
+    base = p;
+    size = n;
+    win = 0;
+    nb = fill = pos = 0;
+    cache_at = -1;
+    err = false;
+  }
+  // 4 payload bytes at i, little endian (reads past the payload stay inside
+  // the padded buffer)
+  VTS_HD VTS_INLINE uint32_t load4(int32_t i) {
+    constexpr int32_t kBlk = 4 * (kW - 1);
+    const int32_t blk = i - (i % kBlk);
+    if (blk != cache_at) {
+      const uint8_t *pb = base + blk;
+      const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pb) & 3);
+      // plain loads from a base the compiler can see is dword aligned, all in
+      // flight together
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(pb) & ~uintptr_t(3));
+      uint32_t t[kW + 1];
+#pragma unroll
+      for (int k = 0; k <= kW; ++k) t[k] = w[k];
+#pragma unroll
+      for (int k = 0; k < kW; ++k) cache[k] = sh ? vts_alignbyte(t[k + 1], t[k], sh) : t[k];
+      cache_at = blk;
+    }
+    const int32_t o = i - blk, q = o >> 2, r = o & 3;
+    return vts_alignbyte(cache[q + 1], cache[q], r);
+  }
+  VTS_HD VTS_INLINE void refill() {  // requires nb <= 32
+    uint32_t v = load4(pos);
+    const int32_t left = size - pos;
+    if (left < 4) v = left <= 0 ? 0u : v & (0xffffffffu >> (8 * (4 - left)));
+    win |= static_cast<uint64_t>(__builtin_bswap32(v)) << (32 - nb);
+    nb += 32;
+    fill += 32;
+    pos += 4;
+  }
+  VTS_HD VTS_INLINE void ensure(int n) {  // n <= 32
+    if (nb < n) refill();
+  }
+  VTS_HD VTS_INLINE void skip(int n) {  // n < 64, n <= nb
+    win <<= n;
+    nb -= n;
+  }
+  VTS_HD VTS_INLINE uint32_t bits(int n) {  // n <= 32
+    if (n == 0) return 0;
+    ensure(n);
+    const uint32_t v = static_cast<uint32_t>(win >> (64 - n));
+    skip(n);
+    return v;
+  }
+  VTS_HD VTS_INLINE uint32_t bit() { return bits(1); }
+  VTS_HD VTS_INLINE uint32_t ue() {
+    ensure(32);
+    const uint32_t p = static_cast<uint32_t>(win >> 32);
+    if (p == 0) {  // more than 31 leading zeros
+      err = true;
+      return 0;
+    }
+    const int lz = __builtin_clz(p);
+    if (lz < 16) {
+      const int len = 2 * lz + 1;
+      skip(len);
+      return (p >> (32 - len)) - 1u;
+    }
+    skip(lz + 1);
+    return ((1u << lz) - 1u) + bits(lz);
+  }
+  VTS_HD VTS_INLINE int32_t se() {
+    const uint32_t k = ue();
+    return (k & 1u) ? static_cast<int32_t>((k + 1) >> 1) : -static_cast<int32_t>(k >> 1);
+  }
+  VTS_HD VTS_INLINE int32_t consumed() const { return fill - nb; }  // RBSP bit index
+  VTS_HD VTS_INLINE void align() { skip(nb & 7); }                  // fill is a multiple of 8
+  VTS_HD VTS_INLINE bool overrun() const { return consumed() > 8 * size; }
+  // more_rbsp_data(): the next bit lies before the stop bit (RBSP bit index)
+  VTS_HD VTS_INLINE bool more(int64_t stop_bit) const { return consumed() < stop_bit; }
+  // drop the window and continue at RBSP bit rb
+  VTS_HD VTS_INLINE void reset_at(int32_t rb) {
+    pos = rb >> 3;
+    if (pos > size) err = true;
+    win = 0;
+    nb = 0;
+    fill = pos * 8;
+    ensure(8);
+    skip(rb & 7);
+  }
+};
+
+// Per-element work of a macroblock (its 16 blocks, its record's 32 dwords) on
+// the wave's lanes: on the device the lanes l < n run the body once each (the
+// parse waves have 64 lanes, all running the same uniform parse), on the host
+// a loop.  Bodies are independent per l (no continue / break, no state carried
+// between elements); a per-lane condition comes back uniform through vts_any.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define VTS_LANES(n, l) if (const int l = static_cast<int>(threadIdx.x); l < (n))
+__device__ VTS_INLINE bool vts_any(bool b) { return __ballot(b) != 0; }
+#else
+#define VTS_LANES(n, l) for (int l = 0; l < (n); ++l)
+inline bool vts_any(bool b) { return b; }
+#endif
+
+// zig-zag position of coefficient i of a 4x4 block (8.5.6): 4-bit fields of one constant
+VTS_HD VTS_INLINE int zz4(int i) { return static_cast<int>((0xFEB7ADC963258410ull >> (4 * i)) & 15u); }
+
 // luma4x4BlkIdx <-> raster 4x4 block
 VTS_HD VTS_INLINE int blk_x(int k) { return ((k >> 2) & 1) * 2 + (k & 1); }
 VTS_HD VTS_INLINE int blk_y(int k) { return ((k >> 3) & 1) * 2 + ((k >> 1) & 1); }
+// raster 4x4 blocks (bit y * 4 + x) of the luma rectangle (x0, y0, w, h)
+VTS_HD VTS_INLINE uint32_t blk_mask(int x0, int y0, int w, int h) {
+  const uint32_t cols = ((1u << (w >> 2)) - 1u) << (x0 >> 2), rows = 0x1111u & ((1u << (4 * (h >> 2))) - 1u);
+  return (cols * rows) << (4 * (y0 >> 2));
+}
 
 // Per-lane scratch (LDS on the device): everything the parser indexes at run
 // time lives here, so nothing spills to scratch memory, and the neighbours a
@@ -182,11 +361,14 @@ struct FullScratch {
   MbRecB mb1[2];              // list-1 halves of mb[2] (streams with B slices)
   MbRecB top1[3];             // ... of top[3]: bytes 0..31 and 112..127
   // CABAC (parse_cabac.h)
-  uint8_t cst[VTS_CABAC_NCTX];  // context states: pStateIdx << 1 | valMPS
-  alignas(16) int16_t lv[64];   // levels of the block being decoded, coefficient-list order
+  alignas(16) int16_t blk8[64]; // 8x8 block being decoded (raster)
   uint8_t mvdc[16][2];          // Min(|mvd|, 33) of the current macroblock's 4x4 blocks
   uint8_t mvdl[4][2];           // ... of the previous macroblock's right column
   uint8_t mvdc1[16][2], mvdl1[4][2];  // the same for list 1 (B slices)
+#ifdef VTS_EXP_PROF
+  uint64_t pacc[8], pt;
+  int32_t psec;
+#endif
 };
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));  // SROA-friendly (uint4 copies are memmoves)
@@ -197,7 +379,7 @@ struct TopCtx {
 };
 
 struct Parser {
-  WinBitsT<kCacheWords> br;
+  RbspBitsT<kCacheWords> br;
   const FullSlice *s;     // global (the ref_slot table is indexed at run time)
   int cip;                // constrained_intra_pred_flag
   MbRec *recs;            // the frame's records (global)
@@ -217,13 +399,25 @@ struct Parser {
   uint16_t lvl_prev;      // intra dependency level of the previous macroblock
   // row above, column pf_col: prefetched during the previous macroblock
   int pf_col;
+#if defined(__HIP_DEVICE_COMPILE__)
+  u32x4 pfl;              // lane p < 8: piece p of the prefetched column (piece_load)
+#else
   TopCtx pf;
   u32x4 pf1[3];           // the prefetched column's list-1 context (bframes)
+#endif
   BCtx bc;
   int bframes;            // write / read the list-1 records
   int direct8x8;          // direct_8x8_inference_flag
   uint32_t todo;          // residual blocks of the current macroblock still to decode (kBlk* bits)
   bool cur_i16;           // the current macroblock is Intra_16x16
+#if defined(__HIP_DEVICE_COMPILE__) && defined(VTS_EXP_PROF)
+  __device__ VTS_INLINE void prof_mark(int k) const {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    sc->pacc[sc->psec] += t - sc->pt;
+    sc->pt = t;
+    sc->psec = k;
+  }
+#endif
 
   // --- neighbour access (6.4.12): mb -1 unavailable, -2 the current MB
   VTS_HD VTS_INLINE int nb_mb(int cur, int xN, int yN, int maxW, int *xw, int *yw) const {
@@ -302,6 +496,26 @@ struct Parser {
       top_store1(col, v);
     }
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the same context on the lanes: lane p < 8 moves piece p (record u32x4 1,
+  // 2, 3, 7; the intra level; list-1 record u32x4 0, 1, 7), so the prefetch
+  // lives in one VGPR quad per lane instead of 29 scalar registers
+  __device__ VTS_INLINE u32x4 piece_load(int col) const {
+    const int l = static_cast<int>(threadIdx.x);
+    const int n = cur_addr - mbw + (col - cur_addr % mbw);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (l < 4) v = reinterpret_cast<const u32x4 *>(recs + n)[l == 3 ? 7 : l + 1];
+    else if (l == 4) v[0] = ilvl[n];
+    else if (l < 8 && bframes) v = reinterpret_cast<const u32x4 *>(bc.recs1 + n)[l == 7 ? 7 : l - 5];
+    return v;
+  }
+  __device__ VTS_INLINE void piece_store(int col, u32x4 v) const {
+    const int l = static_cast<int>(threadIdx.x);
+    if (l < 4) reinterpret_cast<u32x4 *>(&sc->top[col % 3])[l == 3 ? 7 : l + 1] = v;
+    else if (l == 4) sc->top[col % 3].epoch = v[0];
+    else if (l < 8 && bframes) reinterpret_cast<u32x4 *>(&sc->top1[col % 3])[l == 7 ? 7 : l - 5] = v;
+  }
+#endif
   // a new macroblock: the previous one becomes the left neighbour; the row
   // above rotates through the three slots, its next column loading one
   // macroblock ahead
@@ -311,6 +525,23 @@ struct Parser {
     cur_addr = addr;
     const int x = addr % mbw, y = addr / mbw;
     tslots = ((x + 2) % 3) | ((x % 3) << 2) | (((x + 1) % 3) << 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (y > 0) {
+      if (!cont) {
+        if (x > 0) piece_store(x - 1, piece_load(x - 1));
+        piece_store(x, piece_load(x));
+      }
+      if (x + 1 < mbw) {
+        if (pf_col != x + 1) pfl = piece_load(x + 1);
+        piece_store(x + 1, pfl);
+      }
+      pf_col = -1;
+      if (x + 2 < mbw) {
+        pfl = piece_load(x + 2);
+        pf_col = x + 2;
+      }
+    }
+#else
     if (y > 0) {
       if (!cont) {
         if (x > 0) top_sync(x - 1);
@@ -331,6 +562,7 @@ struct Parser {
         pf_col = x + 2;
       }
     }
+#endif
   }
 
   // 9.2.1 nC
@@ -461,16 +693,18 @@ struct Parser {
   }
 
   // store sc->blk as the next arena block; bit = kBlk* index
-  VTS_HD VTS_INLINE bool store_block(uint32_t bit) {
+  VTS_HD VTS_INLINE bool store_block(uint32_t bit) { return store_block(bit, sc->blk); }
+  VTS_HD VTS_INLINE bool store_block(uint32_t bit, const int16_t *src) {
+    VTS_PARSE_TRACE(7);
     if (used >= s->arena_cap) return false;
     int16_t *dst = arena + 16 * static_cast<int64_t>(s->arena + used);
 #if defined(__HIPCC__)
     u32x4 *d4 = reinterpret_cast<u32x4 *>(dst);
-    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(sc->blk);
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src);
     d4[0] = s4[0];
     d4[1] = s4[1];
 #else
-    for (int i = 0; i < 16; ++i) dst[i] = sc->blk[i];
+    for (int i = 0; i < 16; ++i) dst[i] = src[i];
 #endif
     if (cur().blocks == 0) cur().coef = s->arena + used;
     cur().blocks |= 1u << bit;
@@ -537,13 +771,28 @@ struct Parser {
   }
 
   VTS_HD VTS_INLINE void begin_mb(int addr) {
+    VTS_PARSE_TRACE(0);
     advance(addr);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the records' initial dwords, one per lane: epoch, slice, 0 coef / blocks /
+    // type..modes, ref -1, ref_slot -1, i4 DC (2), then zeros; list 1: ref1 -1,
+    // ref_slot1 -1, then zeros
+    VTS_LANES(64, l) {
+      if (l < 32) {
+        const uint32_t v = l == 0 ? epoch : (l == 1 ? slice_index : ((l >= 5 && l <= 7) ? ~0u : ((l == 8 || l == 9) ? 0x22222222u : 0u)));
+        reinterpret_cast<uint32_t *>(&cur())[l] = v;
+      } else if (bframes) {
+        reinterpret_cast<uint32_t *>(&cur1())[l - 32] = l - 32 < 3 ? ~0u : 0u;
+      }
+    }
+#else
     MbRec &m = cur();
     m.epoch = epoch;
     m.slice = slice_index;
     m.coef = 0;
     m.blocks = 0;
     m.type = 0;
+    m.qp = 0;
     m.cbp = 0;
     m.modes = 0;
     for (int i = 0; i < 4; ++i) {
@@ -563,9 +812,12 @@ struct Parser {
         m1.ref_slot1[i] = -1;
       }
       m1.direct = 0;
+      for (int i = 0; i < 3; ++i) m1._p[i] = 0;
       for (int i = 0; i < 8; ++i) m1.mvd1[i] = 0;
+      for (int i = 0; i < 40; ++i) m1._q[i] = 0;
       for (int i = 0; i < 16; ++i) m1.mv1[i][0] = m1.mv1[i][1] = 0;
     }
+#endif
   }
   VTS_HD VTS_INLINE void end_mb(int addr) {
     // intra dependency level: 1 + the highest level among the intra-predicted
@@ -587,26 +839,17 @@ struct Parser {
     }
     ilvl[addr] = lv;
     lvl_prev = lv;
-#if defined(__HIPCC__)
-    u32x4 *d = reinterpret_cast<u32x4 *>(&recs[addr]);
-    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(&cur());
-#pragma unroll
-    for (int i = 0; i < 8; ++i) d[i] = s4[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the records to global memory, 16 bytes per lane (list 1: its u32x4 2, 3 are padding)
+    VTS_LANES(16, l) {
+      if (l < 8) reinterpret_cast<u32x4 *>(&recs[addr])[l] = reinterpret_cast<const u32x4 *>(&cur())[l];
+      else if (bframes && (l < 10 || l >= 12))
+        reinterpret_cast<u32x4 *>(&bc.recs1[addr])[l - 8] = reinterpret_cast<const u32x4 *>(&cur1())[l - 8];
+    }
 #else
     recs[addr] = cur();
+    if (bframes) bc.recs1[addr] = cur1();
 #endif
-    if (bframes) {
-#if defined(__HIPCC__)
-      u32x4 *d1 = reinterpret_cast<u32x4 *>(&bc.recs1[addr]);
-      const u32x4 *s1 = reinterpret_cast<const u32x4 *>(&cur1());
-      d1[0] = s1[0];
-      d1[1] = s1[1];
-#pragma unroll
-      for (int i = 4; i < 8; ++i) d1[i] = s1[i];
-#else
-      bc.recs1[addr] = cur1();
-#endif
-    }
   }
 
   VTS_HD VTS_INLINE void set_motion(int b, int ref, int mvx, int mvy) {
@@ -654,8 +897,8 @@ struct Parser {
     }
     const MbRec &cm = bc.col[addr];
     const MbRecB &cm1 = bc.col1[addr];
-    for (int blk = 0; blk < 16; ++blk) {
-      if (!((mask >> blk) & 1u)) continue;
+    bool bad = false;  // temporal: the colocated reference is not in RefPicList0
+    VTS_LANES(16, blk) if ((mask >> blk) & 1u) {
       const int cb = direct8x8 ? ((blk >> 3) * 3) * 4 + ((blk & 3) >> 1) * 3 : blk;
       const int c8 = (cb >> 3) * 2 + ((cb & 3) >> 1);
       const bool use0 = cm.ref[c8] >= 0;
@@ -676,8 +919,8 @@ struct Parser {
           for (int i = s->num_ref - 1; i >= 0; --i)
             if (s->ref_slot[i] == slot) r0 = i;
           if (r0 < 0) {
-            err |= DEC_E_NO_REF;
-            return;
+            bad = true;
+            r0 = 0;
           }
         }
         int m0x = mcx, m0y = mcy, m1x = 0, m1y = 0;
@@ -694,6 +937,7 @@ struct Parser {
         set_motion1(blk, 0, m1x, m1y);
       }
     }
+    if (vts_any(bad)) err |= DEC_E_NO_REF;
   }
 
   VTS_HD VTS_INLINE void skip_mb(int addr, int qp) {
@@ -720,7 +964,7 @@ struct Parser {
     if (!(a == -1 || b == -1 || (A.ref == 0 && A.x == 0 && A.y == 0) || (B.ref == 0 && B.x == 0 && B.y == 0)))
       mv_pred(addr, 0, 0, 16, 16, 0, 0, &px, &py);
     if (s->ref_slot[0] < 0) err |= DEC_E_NO_REF;
-    for (int i = 0; i < 16; ++i) set_motion(i, 0, px, py);
+    VTS_LANES(16, i) set_motion(i, 0, px, py);
   }
 
   // mb_pred / sub_mb_pred of a B macroblock (7.3.5.1-2, Tables 7-14, 7-18)
@@ -834,12 +1078,13 @@ struct Parser {
             return false;
           }
         }
-        for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
-          for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
-            set_motion(yy * 4 + xx, (pm[k] & 1) ? r0[k] : -1, v[0][0], v[0][1]);
-            set_motion1(yy * 4 + xx, (pm[k] & 2) ? r1[k] : -1, v[1][0], v[1][1]);
-            done |= 1u << (yy * 4 + xx);
-          }
+        const uint32_t bm = blk_mask(sx, sy, pw, ph);
+        const int ra = (pm[k] & 1) ? r0[k] : -1, rb = (pm[k] & 2) ? r1[k] : -1;
+        VTS_LANES(16, b) if ((bm >> b) & 1u) {
+          set_motion(b, ra, v[0][0], v[0][1]);
+          set_motion1(b, rb, v[1][0], v[1][1]);
+        }
+        done |= bm;
       }
     }
     return true;
@@ -974,11 +1219,10 @@ struct Parser {
             err |= DEC_E_SYNTAX;
             return false;
           }
-          for (int yy = sy / 4; yy < (sy + ph) / 4; ++yy)
-            for (int xx = sx / 4; xx < (sx + pw) / 4; ++xx) {
-              set_motion(yy * 4 + xx, refs[k], vx, vy);
-              done |= 1u << (yy * 4 + xx);
-            }
+          const uint32_t bm = blk_mask(sx, sy, pw, ph);
+          const int rk = refs[k];
+          VTS_LANES(16, b) if ((bm >> b) & 1u) set_motion(b, rk, vx, vy);
+          done |= bm;
         }
       }
     }
@@ -1062,11 +1306,11 @@ struct Parser {
 };
 
 // Parse slice `s` (window slice index si) into recs (the frame's records) and
-// the arena.  Returns DEC_E_* bits.
-VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &s, uint32_t si, const FullParams P,
-                                        MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena, uint32_t epoch,
-                                        FullScratch *sc, const BCtx &bc) {
-  const uint8_t *nal = es + s.nal_offset;
+// the arena.  rbsp = the slice NAL's payload with its emulation-prevention
+// bytes removed (rbsp_len bytes).  Returns DEC_E_* bits.
+VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *rbsp, int32_t rbsp_len, const FullSlice &s, uint32_t si,
+                                        const FullParams P, MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena,
+                                        uint32_t epoch, FullScratch *sc, const BCtx &bc) {
   Parser p;
   p.s = &s;
   p.cip = P.cip;
@@ -1090,16 +1334,12 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &
   p.direct8x8 = P.direct8x8;
   const int nmb = P.mb_width * P.mb_height;
   if (s.is_p == kSliceB && (!bc.x || !bc.col || !P.bframes)) return DEC_E_NO_REF;
-  int32_t last = s.nal_size - 1;
-  while (last > 0 && nal[last] == 0) --last;
-  if (last <= 0) return DEC_E_SYNTAX;
-  const int tz = __builtin_ctz(static_cast<uint32_t>(nal[last]));
-  const int32_t stop_byte = last - 1;
-  const int64_t stop_bit = int64_t(stop_byte) * 8 + (7 - tz);
-  p.br.init(nal + 1, s.nal_offset + 1, s.nal_size - 1, sc->cache);
-  p.br.reset_at(s.data_byte, s.data_bit & ~7);
-  p.br.ensure(8);
-  p.br.skip(s.data_bit & 7);
+  int32_t last = rbsp_len - 1;  // the stop bit's byte
+  while (last >= 0 && rbsp[last] == 0) --last;
+  if (last < 0) return DEC_E_SYNTAX;
+  const int64_t stop_bit = int64_t(last) * 8 + (7 - __builtin_ctz(static_cast<uint32_t>(rbsp[last])));
+  p.br.init(rbsp, rbsp_len, sc->cache);
+  p.br.reset_at(s.data_bit);
   p.todo = 0;
   p.cur_i16 = false;
   // slice_data() as a state machine whose every iteration does one small step
@@ -1131,7 +1371,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &
       p.end_mb(addr);
       ++addr;
       if (--run == 0) {
-        if (!p.br.more(stop_byte, stop_bit)) break;
+        if (!p.br.more(stop_bit)) break;
         if (addr >= nmb) {
           p.err |= DEC_E_SYNTAX;
           break;
@@ -1146,7 +1386,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &
     if (finish) {
       p.end_mb(addr);
       ++addr;
-      if (!p.br.more(stop_byte, stop_bit)) break;
+      if (!p.br.more(stop_bit)) break;
       if (addr >= nmb) {
         p.err |= DEC_E_SYNTAX;
         break;
@@ -1154,7 +1394,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *es, const FullSlice &
       state = s.is_p ? kRun : kHeader;
     }
   }
-  if (!p.err && (p.br.err || p.br.overrun() || p.br.consumed() != stop_bit - 8ll * p.br.epb)) p.err |= DEC_E_SYNTAX;
+  if (!p.err && (p.br.err || p.br.overrun() || p.br.consumed() != stop_bit)) p.err |= DEC_E_SYNTAX;
   return p.err;
 }
 

@@ -77,16 +77,23 @@ struct WinBitsT {
     if (blk != cache_at) {
       const uint8_t *pb = base + blk;
       const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pb) & 3);
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(pb - sh);  // global, not flat
       uint32_t t[kW + 1];
       if constexpr (kW > 5) {
-        // wave-uniform parse (h264_parse_full): keep these vector loads; as
-        // scalar loads the compiler folded the alignment into an SMEM base of
-        // (aligned - 1) + offset 1, which reads the wrong dword
-        const volatile uint32_t *vw = w;
+        // wave-uniform parse (h264_parse_full): plain loads from a base the
+        // compiler can see is dword aligned, all in flight together (as
+        // scalar loads from `pb - sh` the compiler once formed an SMEM base of
+        // (aligned - 1) + offset 1, which reads the wrong dword; volatile
+        // loads, the earlier cure, waited for memory one dword at a time)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(VTS_EXP_BITS_GLOBAL)
+        typedef const __attribute__((address_space(1))) uint32_t gu32;  // global, not flat
+#else
+        typedef const uint32_t gu32;
+#endif
+        gu32 *w = reinterpret_cast<gu32 *>(reinterpret_cast<uintptr_t>(pb) & ~uintptr_t(3));
 #pragma unroll
-        for (int k = 0; k <= kW; ++k) t[k] = vw[k];
+        for (int k = 0; k <= kW; ++k) t[k] = w[k];
       } else {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(pb - sh);  // global, not flat
 #pragma unroll
         for (int k = 0; k <= kW; ++k) t[k] = w[k];
       }

@@ -87,6 +87,8 @@ struct vts_ctx {
   int n_rings = 1;
   // device
   uint8_t *d_es = nullptr;
+  uint8_t *d_rbsp = nullptr;      // general decoder: slice NAL payloads without EPBs (at ES offsets)
+  int32_t *d_rbsp_len = nullptr;  // ... their lengths, per fslice
   int64_t es_bytes = 0;
   SliceDesc *d_slices = nullptr;
   int4 *d_levels = nullptr;

@@ -92,6 +92,12 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   HIP_TRY(hipMalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
   if (!c->fslices.empty())
     HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
+  // the slice NALs' RBSPs, made once: the parsers read plain bits
+  HIP_TRY(hipMalloc(&c->d_rbsp, static_cast<size_t>(c->es_bytes)));
+  HIP_TRY(hipMalloc(&c->d_rbsp_len, sizeof(int32_t) * std::max<size_t>(1, c->fslices.size())));
+  VTS_TRY(nal_unescape_launch(c->d_es, c->d_rbsp, c->d_fslices, static_cast<int32_t>(c->fslices.size()),
+                              c->d_rbsp_len, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMalloc(&c->d_porder, sizeof(int32_t) * std::max<size_t>(1, c->porder.size())));
   if (!c->porder.empty())
     HIP_TRY(hipMemcpy(c->d_porder, c->porder.data(), sizeof(int32_t) * c->porder.size(), hipMemcpyHostToDevice));
@@ -1086,6 +1092,8 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->small.d);
   f(c->small.d_taps);
   f(c->d_fslices);
+  f(c->d_rbsp);
+  f(c->d_rbsp_len);
   f(c->d_exts);
   f(c->d_porder);
   for (int r = 0; r < 2; ++r) {

@@ -337,7 +337,7 @@ int run_general(vts_ctx *c) {
     }
     HIP_TRY(hipEventRecord(E[0], sp));
     FullParseArgs pa{};
-    pa.es = c->d_es;
+    pa.rbsp = c->d_rbsp;
     pa.epoch = epoch;
     pa.recs = c->d_recs[r];
     pa.recs1 = c->d_recs1[r];
@@ -349,6 +349,7 @@ int run_general(vts_ctx *c) {
     for (size_t j = 0; j < w.plv_end.size(); ++j) {  // B pictures after their colocated pictures
       const int32_t b0 = j ? w.plv_end[j - 1] : 0;
       pa.slices = c->d_fslices + w.fs0 + b0;
+      pa.rbsp_len = c->d_rbsp_len + w.fs0 + b0;
       pa.n_slices = w.plv_end[j] - b0;
       pa.slice0 = b0;
       pa.order = c->d_porder + w.fs0 + b0;
