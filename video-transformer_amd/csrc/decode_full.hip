@@ -32,6 +32,12 @@
 // parse section timing (experiment builds): s_memtime deltas per section,
 // summed over all slices; read with vts_debug_parse_prof
 __device__ unsigned long long vts_prof_acc[8];
+#if !defined(__HIP_DEVICE_COMPILE__)
+#define VTS_PROF(k)
+#define VTS_PROF_P(p, k)
+#define VTS_PROF_FLUSH(p)
+#define VTS_PROF_START(p)
+#else
 #define VTS_PROF(k) prof_mark(k)
 #define VTS_PROF_P(p, k) (p).prof_mark(k)
 #define VTS_PROF_FLUSH(p)                                               \
@@ -42,6 +48,7 @@ __device__ unsigned long long vts_prof_acc[8];
     (p).sc->pt = __builtin_amdgcn_s_memtime();                          \
     (p).sc->psec = 0;                                                   \
   } while (0)
+#endif
 #endif
 #include "parse_cabac.h"
 #include "parse_full.h"

@@ -15,6 +15,7 @@
 // bytes, the previous macroblock's right-column |mvd| in FullScratch.mvdl.
 #pragma once
 #include <cstdint>
+#include <type_traits>
 
 #include "h264_cabac_tables.h"
 #include "parse_full.h"
@@ -71,9 +72,13 @@ struct CabacParser : Parser {
   uint32_t range, val;
   int32_t la;
   bool prev_qpd;  // the previous macroblock of the slice has mb_qp_delta != 0
-  // context states (pStateIdx << 1 | valMPS), four per dword: ctxIdx c in
-  // st[c >> 8], lane (c >> 2) & 63, byte c & 3
+  // context states (pStateIdx << 1 | valMPS), four per dword.  The residual
+  // contexts of 4x4 blocks (ctxIdx 85..275) fill st[0] (slot c - 85); all
+  // others (0..84, and 399..459 at 85..145) st[1], so every decode's table is
+  // known at compile time (slot q: lane q >> 2, byte q & 3)
   LaneTab st[2];
+  static VTS_HD VTS_INLINE int ctx_tab(int c) { return (c >= 85 && c <= 275) ? 0 : 1; }
+  static VTS_HD VTS_INLINE int ctx_slot(int c) { return c >= 399 ? c - 314 : (c >= 85 ? c - 85 : c); }
   LaneTab lps, trn, s8;  // kCabLanes
 
   // ---------------------------------------------- arithmetic decoder (9.3.3.2)
@@ -99,26 +104,29 @@ struct CabacParser : Parser {
   }
   VTS_HD VTS_INLINE void cab_init(bool is_i, int qp) {  // 9.3.1.1
     const int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
-    for (int w = 0; w < 128; ++w) {
-      uint32_t word = 0;
-      for (int b = 0; b < 4; ++b) {
-        const int i = 4 * w + b;
-        if (i >= VTS_CABAC_NCTX) break;
-        const int m = is_i ? kCabInitI[i][0] : kCabInitP[i][0], n = is_i ? kCabInitI[i][1] : kCabInitP[i][1];
-        int pre = ((m * q) >> 4) + n;
-        pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
-        word |= static_cast<uint32_t>(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1) << (8 * b);
+    for (int t = 0; t < 2; ++t)
+      for (int w = 0; w < 64; ++w) {
+        uint32_t word = 0;
+        for (int b = 0; b < 4; ++b) {
+          const int slot = 4 * w + b;
+          // the ctxIdx of this slot (the inverse of ctx_slot); unused slots stay 0
+          const int i = t == 0 ? (slot <= 190 ? slot + 85 : -1) : (slot < 85 ? slot : (slot <= 145 ? slot + 314 : -1));
+          if (i < 0) continue;
+          const int m = is_i ? kCabInitI[i][0] : kCabInitP[i][0], n = is_i ? kCabInitI[i][1] : kCabInitP[i][1];
+          int pre = ((m * q) >> 4) + n;
+          pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
+          word |= static_cast<uint32_t>(pre <= 63 ? (63 - pre) << 1 : ((pre - 64) << 1) | 1) << (8 * b);
+        }
+        st[t].set(w, word);
       }
-      if (w < 64) st[0].set(w, word);
-      else st[1].set(w - 64, word);
-    }
   }
   VTS_HD VTS_INLINE uint32_t dec(int ctx) {  // DecodeDecision
     VTS_PARSE_TRACE(1);
-    const uint32_t ln = static_cast<uint32_t>(ctx >> 2) & 63u, sh = static_cast<uint32_t>(ctx & 3) * 8u;
-    // which of the two lane tables: folded where ctx is a constant, else both
-    // are read and written with selects (no branch)
-    const bool fixed = __builtin_constant_p(ctx < 256), hi = ctx >= 256;
+    const int q = ctx_slot(ctx);
+    const uint32_t ln = static_cast<uint32_t>(q >> 2) & 63u, sh = static_cast<uint32_t>(q & 3) * 8u;
+    // which of the two lane tables: folded where it is a constant (every call
+    // site), else both are read and written with selects (no branch)
+    const bool fixed = __builtin_constant_p(ctx_tab(ctx)), hi = ctx_tab(ctx) != 0;
     const uint32_t wa = fixed && hi ? 0u : st[0].get(ln), wb = fixed && !hi ? 0u : st[1].get(ln);
     const uint32_t word = hi ? wb : wa;
     const uint32_t s = (word >> sh) & 127u, ps = s >> 1, mps = s & 1u;
@@ -464,34 +472,41 @@ struct CabacParser : Parser {
   // residual_block_cabac (7.3.5.3.3): each level goes straight to its raster
   // position in dst, which the caller has zeroed (4x4 blocks: zig-zag position
   // of coefficient start + i; 8x8: the 8x8 zig-zag; chroma DC: list order);
-  // count of non-zero levels (0: coded_block_flag 0), -1 on error
-  VTS_HD VTS_INLINE int residual(int cat, int cbf_inc, int maxNum, int16_t *dst, int start) {
-    if (cat != 5 && !dec(85 + cbf_off(cat) + cbf_inc)) return 0;
-    uint64_t sig = 0;
+  // count of non-zero levels (0: coded_block_flag 0), -1 on error.  kT8: an
+  // 8x8 block (ctxBlockCat 5, contexts 402..459); else cat 0..4 (85..275)
+  template <bool kT8>
+  VTS_HD VTS_INLINE int residual_t(int cat, int cbf_inc, int maxNum, int16_t *dst, int start) {
+    typedef typename std::conditional<kT8, uint64_t, uint32_t>::type Mask;
+    if (!kT8 && !dec(85 + cbf_off(cat) + cbf_inc)) return 0;
+    Mask sig = 0;
     int numc = maxNum;
-    const int sig_base = cat == 5 ? 402 : 105 + sig_off(cat), last_base = cat == 5 ? 417 : 166 + sig_off(cat);
+    const int sig_base = kT8 ? 402 : 105 + sig_off(cat), last_base = kT8 ? 417 : 166 + sig_off(cat);
     for (int i = 0; i < numc - 1; ++i) {
       int inc_s, inc_l;
-      if (cat == 5) {
+      if (kT8) {
         const uint32_t e = s8.get(static_cast<uint32_t>(i));
         inc_s = static_cast<int>(e & 255u);
         inc_l = static_cast<int>((e >> 8) & 255u);
       } else {
         inc_s = inc_l = cat == 3 ? vts_min(i, 2) : i;
       }
-      if (dec(sig_base + inc_s)) {
-        sig |= 1ull << i;
-        if (dec(last_base + inc_l)) {
+      if (dec(kT8 ? 402 + (inc_s & 15) : vts_min(sig_base + inc_s, 165))) {
+        sig |= Mask(1) << i;
+        if (dec(kT8 ? 417 + (inc_l & 15) : vts_min(last_base + inc_l, 226))) {
           numc = i + 1;
           break;
         }
       }
     }
-    sig |= 1ull << (numc - 1);
+    (void)sig_base;
+    (void)last_base;
+    sig |= Mask(1) << (numc - 1);
     int eq1 = 0, gt1 = 0, n = 0;
-    const int base = cat == 5 ? 426 : 227 + abs_off(cat);
-    for (int i = numc - 1; i >= 0; --i) {
-      if (!((sig >> i) & 1ull)) continue;
+    const int base = kT8 ? 426 : 227 + abs_off(cat);
+    while (sig) {  // the significant coefficients, highest first
+      const int i = kT8 ? 63 - static_cast<int>(__builtin_clzll(static_cast<uint64_t>(sig)))
+                        : 31 - static_cast<int>(__builtin_clz(static_cast<uint32_t>(sig)));
+      sig &= ~(Mask(1) << i);
       int v = 0;
       if (dec(base + (gt1 ? 0 : vts_min(4, 1 + eq1)))) {
         v = 1;
@@ -509,8 +524,8 @@ struct CabacParser : Parser {
       int lvl = v + 1;
       if (bypass()) lvl = -lvl;
       if (lvl > 32767 || lvl < -32768) return -1;
-      const int pos = cat == 5 ? static_cast<int>((s8.get(static_cast<uint32_t>(i)) >> 16) & 63u)
-                               : (cat == 3 ? i : zz4(i + start));
+      const int pos = kT8 ? static_cast<int>((s8.get(static_cast<uint32_t>(i)) >> 16) & 63u)
+                          : (cat == 3 ? i : zz4(i + start));
       dst[pos] = static_cast<int16_t>(lvl);
       if (v == 0) ++eq1;
       else ++gt1;
@@ -767,6 +782,36 @@ struct CabacParser : Parser {
     const bool t8 = (m.modes & kModeT8) != 0;
     // the blocks present, in bitstream order = kBlk* bit order; an 8x8 block
     // is its quarter's first 4x4 bit.  One residual() site for all of them.
+    // condTermFlagN (9.3.3.1.1.9) of the luma 4x4 blocks on the macroblock's
+    // left / top edge, from the neighbours' records once: bits 0-3 = A of
+    // rows 0-3, bits 4-7 = B of columns 0-3; inside the macroblock the
+    // neighbour's flag is its coded_block_flag (cbfc)
+    uint32_t nbl = 0, cbfc = 0;
+    if ((cbp & 15) && !t8) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int n = nb ? B : A;
+        uint32_t f = 0;
+        if (n == -1) {
+          f = intra ? 15u : 0u;
+        } else {
+          const MbRec &r = rec(n);
+          if (r.type == kMbPcm) {
+            f = 15u;
+          } else if (r.type != kMbSkip) {
+            const uint32_t cb = cbf_of(r);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              // A: row k, right column (raster 4k + 3) in 8x8 (k / 2) * 2 + 1;
+              // B: column k, bottom row (raster 12 + k) in 8x8 2 + k / 2
+              const int b8 = nb ? 2 + (k >> 1) : (k >> 1) * 2 + 1, rr = nb ? 12 + k : 4 * k + 3;
+              f |= (((r.cbp >> b8) & 1) ? (cb >> (1 + rr)) & 1u : 0u) << k;
+            }
+          }
+        }
+        nbl |= f << (4 * nb);
+      }
+    }
     uint32_t todo = m.type == kMbI16 ? 1u << kBlkI16Dc : 0u;
     for (int q = 0; q < 4; ++q)
       if ((cbp >> q) & 1) todo |= (t8 ? 1u : 15u) << (kBlkLuma0 + 4 * q);
@@ -798,7 +843,9 @@ struct CabacParser : Parser {
             maxNum = 15;
             start = 1;
           }
-          inc = cbf_luma_inc(addr, bx, by, intra);
+          const uint32_t ca = bx ? (cbfc >> (r - 1)) & 1u : (nbl >> by) & 1u;
+          const uint32_t cb = by ? (cbfc >> (r - 4)) & 1u : (nbl >> (4 + bx)) & 1u;
+          inc = static_cast<int>(ca + 2 * cb);
         }
       } else if (bt < kBlkChromaAc0) {
         cat = 3;
@@ -812,7 +859,7 @@ struct CabacParser : Parser {
         inc = cbf_chroma_inc(addr, j >> 2, j & 3, false, intra);
       }
       zero16x(dst, cat == 5 ? 64 : 16);
-      const int nc = residual(cat, inc, maxNum, dst, start);
+      const int nc = cat == 5 ? residual_t<true>(5, 0, 64, dst, 0) : residual_t<false>(cat, inc, maxNum, dst, start);
       if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
       if (cat == 5) {  // the quarter's 4 blocks: raster 8x8 rows 2j, 2j + 1
         const int rs[4] = {r, r + 1, r + 4, r + 5};
@@ -825,7 +872,10 @@ struct CabacParser : Parser {
             if (!store_block(bt + j, sc->blk8 + 16 * j)) { err |= DEC_E_SYNTAX; return false; }
         continue;
       }
-      if (cat == 1 || cat == 2) m.nz[r] = static_cast<uint8_t>(nc);
+      if (cat == 1 || cat == 2) {
+        m.nz[r] = static_cast<uint8_t>(nc);
+        cbfc |= (nc ? 1u : 0u) << r;
+      }
       if (nc) {
         set_cbf(bt == kBlkI16Dc ? 0u : (cat <= 2 ? 1u + static_cast<uint32_t>(r) : bt));
         if (!store_block(bt)) { err |= DEC_E_SYNTAX; return false; }
