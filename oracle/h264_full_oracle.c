@@ -322,18 +322,59 @@ static int median3(int a, int b, int c) {
 }
 
 /* ------------------------------------------------- parameter sets (7.3.2) */
+static int ZZ8[64]; /* 8.5.7 8x8 zig-zag (fo_tables_init) */
+static void fo_tables_init(void);
 typedef struct {
   int valid, profile_idc, log2_max_frame_num, poc_type, log2_max_poc_lsb, dpoaz;
   int max_num_ref_frames, gaps, mbw, mbh, crop_l, crop_r, crop_t, crop_b;
   int direct8x8;                     /* direct_8x8_inference_flag */
   int off_non_ref, off_t2b, ncycle;  /* POC type 1 (7.4.2.1.1) */
   int off_ref[256];
+  uint8_t sl4[6][16], sl8[2][64];    /* sequence-level scaling lists (scan order; 16s when absent) */
 } fo_sps;
 typedef struct {
   int valid, sps_id, bfpo, num_ref_l0, num_ref_l1, weighted_pred, weighted_bipred, pic_init_qp;
   int cqp_off, cqp_off2, deblock_ctrl, cip, redundant;
   int cabac, t8mode;   /* entropy_coding_mode_flag, transform_8x8_mode_flag */
+  int pic_scaling;     /* pic_scaling_matrix_present_flag */
+  /* weightScale4x4 / 8x8 in raster order (8.5.6 / 8.5.7 inverse scans of the
+     picture's scaling lists): lists Intra Y, Cb, Cr, Inter Y, Cb, Cr / Intra Y, Inter Y */
+  uint8_t w4[6][16], w8[2][64];
 } fo_pps;
+
+/* 7.3.2.1.1.1 scaling_list(): returns useDefaultScalingMatrixFlag */
+static int fo_scaling_list(fb_t *b, int size, uint8_t *list) {
+  int last_scale = 8, next_scale = 8, use_default = 0;
+  for (int j = 0; j < size; j++) {
+    if (next_scale != 0) {
+      int delta_scale = fb_se(b);
+      next_scale = (last_scale + delta_scale + 256) % 256;
+      use_default = (j == 0 && next_scale == 0);
+    }
+    list[j] = (uint8_t)(next_scale == 0 ? last_scale : next_scale);
+    last_scale = list[j];
+  }
+  return use_default;
+}
+/* the 8 (4:2:0) scaling lists of an SPS (fall-back rule A) or a PPS (rule
+ * B: lists 0, 3, 6, 7 fall back to the SPS's own), Table 7-2; n_sent =
+ * how many list flags the parameter set carries */
+static void fo_scaling_matrix(fb_t *b, int n_sent, const fo_sps *seq, uint8_t (*l4)[16], uint8_t (*l8)[64]) {
+  for (int i = 0; i < 8; i++) {
+    int sent = i < n_sent ? (int)fb_bit(b) : 0;
+    int size = i < 6 ? 16 : 64, cls = (i < 3 || i == 6) ? 0 : 1; /* 0 intra, 1 inter */
+    uint8_t *dst = i < 6 ? l4[i] : l8[i - 6];
+    const uint8_t *dflt = i < 6 ? FO_DEFAULT_4x4[cls] : FO_DEFAULT_8x8[cls];
+    if (sent) {
+      if (fo_scaling_list(b, size, dst)) memcpy(dst, dflt, (size_t)size);
+    } else if (i == 0 || i == 3 || i >= 6) { /* rule A: the default; rule B: the SPS's list */
+      const uint8_t *src = !seq ? dflt : (i < 6 ? seq->sl4[i] : seq->sl8[i - 6]);
+      memcpy(dst, src, (size_t)size);
+    } else {                                  /* both rules: the previous list */
+      memcpy(dst, l4[i - 1], 16);
+    }
+  }
+}
 
 static int is_high(int p) {
   return p == 100 || p == 110 || p == 122 || p == 244 || p == 44 || p == 83 || p == 86 ||
@@ -353,8 +394,10 @@ static int parse_sps(const uint8_t *nal, int64_t n, fo_sps *tab, char *err) {
     if (fb_ue(&b) != 1) { strcpy(err, "chroma_format_idc != 1"); return FO_E_UNSUPPORTED; }
     if (fb_ue(&b) || fb_ue(&b)) { strcpy(err, "bit depth > 8"); return FO_E_UNSUPPORTED; }
     fb_bit(&b);
-    if (fb_bit(&b)) { strcpy(err, "scaling matrices"); return FO_E_UNSUPPORTED; }
   }
+  memset(s.sl4, 16, sizeof s.sl4); /* Flat_4x4_16 / Flat_8x8_16 */
+  memset(s.sl8, 16, sizeof s.sl8);
+  if (is_high(s.profile_idc) && fb_bit(&b)) fo_scaling_matrix(&b, 8, NULL, s.sl4, s.sl8);
   s.log2_max_frame_num = (int)fb_ue(&b) + 4;
   s.poc_type = (int)fb_ue(&b);
   if (s.poc_type == 0) {
@@ -386,7 +429,7 @@ static int parse_sps(const uint8_t *nal, int64_t n, fo_sps *tab, char *err) {
   return 0;
 }
 
-static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, char *err) {
+static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, const fo_sps *sps_tab, char *err) {
   fb_t b;
   fb_init(&b, nal + 1, n - 1);
   fo_pps p;
@@ -418,11 +461,21 @@ static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, char *err) {
     int tz = 0;
     while (!((nal[last] >> tz) & 1)) tz++;
     int64_t stop = (last - 1) * 8 + (7 - tz);
+    const fo_sps *S = &sps_tab[p.sps_id & 31];
+    uint8_t l4[6][16], l8[2][64];
+    memcpy(l4, S->sl4, sizeof l4); /* no picture-level matrix: the sequence's */
+    memcpy(l8, S->sl8, sizeof l8);
     if (pos_bits < stop) {
       p.t8mode = (int)fb_bit(&b);
-      if (fb_bit(&b)) { strcpy(err, "scaling matrices"); return FO_E_UNSUPPORTED; }
+      p.pic_scaling = (int)fb_bit(&b);
+      if (p.pic_scaling) fo_scaling_matrix(&b, 6 + 2 * p.t8mode, S, l4, l8);
       p.cqp_off2 = fb_se(&b);
     }
+    fo_tables_init(); /* ZZ8 */
+    for (int l = 0; l < 6; l++)
+      for (int k = 0; k < 16; k++) p.w4[l][ZZ4[k]] = l4[l][k];
+    for (int l = 0; l < 2; l++)
+      for (int k = 0; k < 64; k++) p.w8[l][ZZ8[k]] = l8[l][k];
   }
   if (b.err) return FO_E_FORMAT;
   if (p.redundant) { strcpy(err, "redundant pictures"); return FO_E_UNSUPPORTED; }
@@ -629,19 +682,21 @@ static int qpc_of(int qpy, int off) {
   int qpi = clip3(0, 51, qpy + off);
   return qpi < 30 ? qpi : QPC_TAB[qpi - 30];
 }
-static int level_scale(int m, int i, int j) {
+/* 8.5.9: LevelScale4x4(m, i, j) = weightScale4x4(i, j) * normAdjust4x4(m, i, j);
+ * w = the block's weightScale4x4 in raster order */
+static int level_scale(const uint8_t *w, int m, int i, int j) {
   int k = ((i & 1) == 0 && (j & 1) == 0) ? 0 : (((i & 1) == 1 && (j & 1) == 1) ? 1 : 2);
-  return 16 * NORM_V[m][k];
+  return w[i * 4 + j] * NORM_V[m][k];
 }
 /* c: 4x4 coefficients in raster (row i, column j); dc_done: c[0] is an
  * already-scaled DC (Intra16x16 / chroma); out r: residual samples */
-static void scale_idct4(const int *c, int qp, int dc_done, int *r) {
+static void scale_idct4(const int *c, int qp, const uint8_t *w, int dc_done, int *r) {
   int d[16];
   for (int i = 0; i < 4; i++)
     for (int j = 0; j < 4; j++) {
       int k = i * 4 + j;
       if (k == 0 && dc_done) { d[0] = c[0]; continue; }
-      int ls = level_scale(qp % 6, i, j);
+      int ls = level_scale(w, qp % 6, i, j);
       if (qp >= 24) d[k] = (c[k] * ls) << (qp / 6 - 4);
       else d[k] = (c[k] * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
     }
@@ -1166,12 +1221,13 @@ static int norm8_class(int i, int j) {
   return 5;
 }
 
-/* 8.5.13: scaling (flat) + 8x8 inverse transform of raster coefficients c */
-static void scale_idct8(const int *c, int qp, int *r) {
+/* 8.5.13: scaling + 8x8 inverse transform of raster coefficients c; w8 =
+ * weightScale8x8 (raster), LevelScale8x8 = w8 * normAdjust8x8 (8.5.9) */
+static void scale_idct8(const int *c, int qp, const uint8_t *w8, int *r) {
   int d[64], g[64];
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 8; j++) {
-      int ls = 16 * FO_V8[qp % 6][norm8_class(i, j)];
+      int ls = w8[i * 8 + j] * FO_V8[qp % 6][norm8_class(i, j)];
       int k = i * 8 + j;
       d[k] = qp >= 36 ? (c[k] * ls) << (qp / 6 - 6) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     }
@@ -1302,7 +1358,7 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
     if (m->t8) {
       for (int b8 = 0; b8 < 4; b8++) {
         int r[64], bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
-        scale_idct8(coef8[b8], qpy, r);
+        scale_idct8(coef8[b8], qpy, d->P->w8[1], r);
         for (int y = 0; y < 8; y++)
           for (int x = 0; x < 8; x++)
             Y[(int64_t)(by + y) * d->W + bx + x] = (uint8_t)clip1(pred_y[(by + y) * 16 + bx + x] + r[y * 8 + x]);
@@ -1310,7 +1366,7 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
     } else {
       for (int blk = 0; blk < 16; blk++) {
         int r[16], bx = blk % 4, by = blk / 4;
-        scale_idct4(coef[blk], qpy, 0, r);
+        scale_idct4(coef[blk], qpy, d->P->w4[3], 0, r);
         for (int y = 0; y < 4; y++)
           for (int x = 0; x < 4; x++)
             Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred_y[(by * 4 + y) * 16 + bx * 4 + x] + r[y * 4 + x]);
@@ -1321,7 +1377,7 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
     for (int b8 = 0; b8 < 4; b8++) {
       int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8, pred[64], r[64];
       intra8x8(d, pic, addr, b8, m->i4[(by / 4) * 4 + bx / 4], done, pred);
-      scale_idct8(coef8[b8], qpy, r);
+      scale_idct8(coef8[b8], qpy, d->P->w8[0], r);
       for (int y = 0; y < 8; y++)
         for (int x = 0; x < 8; x++) Y[(int64_t)(by + y) * d->W + bx + x] = (uint8_t)clip1(pred[y * 8 + x] + r[y * 8 + x]);
       int r4 = (by / 4) * 4 + bx / 4;
@@ -1332,7 +1388,7 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
     for (int k = 0; k < 16; k++) {
       int bx = BLK_X[k], by = BLK_Y[k], blk = by * 4 + bx, pred[16], r[16];
       intra4x4(d, pic, addr, k, m->i4[blk], done, pred);
-      scale_idct4(coef[blk], qpy, 0, r);
+      scale_idct4(coef[blk], qpy, d->P->w4[0], 0, r);
       for (int y = 0; y < 4; y++)
         for (int x = 0; x < 4; x++)
           Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred[y * 4 + x] + r[y * 4 + x]);
@@ -1356,14 +1412,14 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
       f[2 * 4 + j] = a0 - a1 - a2 + a3;
       f[3 * 4 + j] = a0 - a1 + a2 - a3;
     }
-    int ls = level_scale(qpy % 6, 0, 0);
+    int ls = level_scale(d->P->w4[0], qpy % 6, 0, 0);
     for (int k = 0; k < 16; k++) {
       int dc = qpy >= 36 ? (f[k] * ls) << (qpy / 6 - 6) : (f[k] * ls + (1 << (5 - qpy / 6))) >> (6 - qpy / 6);
       coef[k][0] = dc; /* dcY row i col j -> block (x = j, y = i) */
     }
     for (int blk = 0; blk < 16; blk++) {
       int r[16], bx = blk % 4, by = blk / 4;
-      scale_idct4(coef[blk], qpy, 1, r);
+      scale_idct4(coef[blk], qpy, d->P->w4[0], 1, r);
       for (int y = 0; y < 4; y++)
         for (int x = 0; x < 4; x++)
           Y[(int64_t)(by * 4 + y) * d->W + bx * 4 + x] = (uint8_t)clip1(pred_y[(by * 4 + y) * 16 + bx * 4 + x] + r[y * 4 + x]);
@@ -1378,13 +1434,14 @@ static int recon_mb(fo_ctx *c, int addr, int (*coef)[16], const int *dcl, int (*
     int qpc = qpc_of(qpy, pl ? d->P->cqp_off2 : d->P->cqp_off);
     int c0 = cdc[pl][0], c1 = cdc[pl][1], c2 = cdc[pl][2], c3 = cdc[pl][3];
     int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
-    int ls = level_scale(qpc % 6, 0, 0);
+    const uint8_t *wc = d->P->w4[(m->type == 0 ? 3 : 0) + 1 + pl]; /* Cb / Cr, intra or inter */
+    int ls = level_scale(wc, qpc % 6, 0, 0);
     uint8_t *U = (pl ? pic->v : pic->u) + (int64_t)(my * 8) * (d->W / 2) + mx * 8;
     int *pr = pl ? pred_v : pred_u;
     for (int k = 0; k < 4; k++) {
       int bx = k & 1, by = k >> 1, r[16];
       cac[pl][k][0] = ((f[k] * ls) << (qpc / 6)) >> 5;
-      scale_idct4(cac[pl][k], qpc, 1, r);
+      scale_idct4(cac[pl][k], qpc, wc, 1, r);
       for (int y = 0; y < 4; y++)
         for (int x = 0; x < 4; x++)
           U[(int64_t)(by * 4 + y) * (d->W / 2) + bx * 4 + x] = (uint8_t)clip1(pr[(by * 4 + y) * 8 + bx * 4 + x] + r[y * 4 + x]);
@@ -2184,6 +2241,8 @@ int fo_std_table(int which, int i, int j, int *ok) {
     case 5: return FO_LAST8_FRAME[i];
     case 6: return ZZ8[i];
     case 7: return FO_V8[i][j];
+    case 8: return FO_DEFAULT_4x4[i][j];   /* Table 7-3: [intra / inter][scan index] */
+    case 9: return FO_DEFAULT_8x8[i][j];   /* Table 7-4 */
     default: *ok = 0; return 0;
   }
 }
@@ -3163,11 +3222,12 @@ static int fo_run(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn
   d->max_lt_idx = -1;
   *bad_frame = -1;
   int rc = parse_sps(sps, sn, d->sps, d->err);
-  if (!rc) rc = parse_pps(pps, pn, d->pps, d->err);
+  if (!rc) rc = parse_pps(pps, pn, d->pps, d->sps, d->err);
   if (!rc && cv) { /* the converted PPS, written from the parsed fields */
     for (int id = 0; id < 256; id++) {
       fo_pps *P = &d->pps[id];
       if (!P->valid) continue;
+      if (P->pic_scaling) { rc = fo_fail(d, FO_E_UNSUPPORTED, "synthesis: PPS scaling matrices"); break; }
       P->cabac = 1;
       if (cv->t8) P->t8mode = 1;
       uint8_t rb[64];
@@ -3307,7 +3367,7 @@ static int fo_run(const uint8_t *sps, int64_t sn, const uint8_t *pps, int64_t pn
         rc = parse_sps(s + pos, L, d->sps, d->err);
       } else if (t == 8) {
         if (cv) rc = fo_fail(d, FO_E_UNSUPPORTED, "synthesis: in-band PPS");
-        else rc = parse_pps(s + pos, L, d->pps, d->err);
+        else rc = parse_pps(s + pos, L, d->pps, d->sps, d->err);
       } else if (t >= 2 && t <= 4) {
         rc = fo_fail(d, FO_E_UNSUPPORTED, "data partitioning");
       }

@@ -15,6 +15,8 @@ static const uint8_t kSig8[63] = VTS_SIG8x8_DATA;
 static const uint8_t kLast8[63] = VTS_LAST8x8_DATA;
 static const int kZz8[64] = VTS_ZZ8_DATA;
 static const int kNorm8[6][6] = VTS_NORM8_DATA;
+static const uint8_t kDef4[2][16] = VTS_DEFAULT_4x4_DATA;
+static const uint8_t kDef8[2][64] = VTS_DEFAULT_8x8_DATA;
 
 int main() {
   for (int i = 0; i < VTS_CABAC_NCTX; ++i)
@@ -32,5 +34,9 @@ int main() {
     for (int c = 0; c < 6; ++c) std::printf("norm8 %d %d %d\n", m, c, kNorm8[m][c]);
   for (int i = 0; i < 8; ++i)
     for (int j = 0; j < 8; ++j) std::printf("norm8_class %d %d %d\n", i, j, vts_norm8_class(i, j));
+  for (int l = 0; l < 2; ++l) {
+    for (int k = 0; k < 16; ++k) std::printf("default4 %d %d %d\n", l, k, kDef4[l][k]);
+    for (int k = 0; k < 64; ++k) std::printf("default8 %d %d %d\n", l, k, kDef8[l][k]);
+  }
   return 0;
 }

@@ -151,6 +151,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   P.cqp_off2 = facts.cqp_off2;
   P.cabac = pps.entropy_coding_mode;
   P.t8mode = facts.transform_8x8;
+  P.scaled = facts.seq_scaling || facts.pic_scaling;
   P.bframes = bframes;
   P.has_ext = exts.empty() ? 0 : 1;
   P.direct8x8 = sps.direct_8x8_inference;
@@ -197,6 +198,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     c.cqp_off = P.cqp_off;
     c.cqp_off2 = P.cqp_off2;
     c.epoch = epoch;
+    c.sct = &facts.scale;
     // kernel order: inter macroblocks, then intra ones along t = x + 2y
     for (int a = 0; a < nmb; ++a) {
       const MbRec &m = fr_recs[a];

@@ -87,6 +87,32 @@ def test_8x8_tables_agree(product):
             assert product[("norm8", m, c)] == std(7, m, c), (m, c)
 
 
+def test_default_scaling_lists_agree(product):
+    """Tables 7-3 / 7-4 (scaling matrices, 8.5.9): both transcriptions, and
+    the structure the standard gives them -- constant along each anti-diagonal
+    of the scan except the 8x8 lists' third diagonal (13 11 13 / 15 13 15),
+    non-decreasing from one diagonal to the next."""
+    for l in range(2):
+        for k in range(16):
+            assert product[("default4", l, k)] == std(8, l, k), (l, k)
+        for k in range(64):
+            assert product[("default8", l, k)] == std(9, l, k), (l, k)
+    for size, which, diag in ((16, 8, [1, 2, 3, 4, 3, 2, 1]), (64, 9, [1, 2, 3, 4, 5, 6, 7, 8, 7, 6, 5, 4, 3, 2, 1])):
+        for l in range(2):
+            vals = [std(which, l, k) for k in range(size)]
+            runs, k = [], 0
+            for n in diag:
+                runs.append(vals[k:k + n])
+                k += n
+            for d, r in enumerate(runs):
+                if size == 64 and d == 2:
+                    assert r[0] == r[2] and r[1] < r[0], (l, r)
+                else:
+                    assert len(set(r)) == 1, (size, l, d, r)
+            heads = [max(r) for r in runs]
+            assert heads == sorted(heads), (size, l, heads)
+
+
 def test_norm8_position_classes_follow_8_5_9(product):
     """8.5.9's six position classes, from their definition."""
     for i in range(8):

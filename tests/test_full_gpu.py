@@ -359,3 +359,36 @@ def test_writer_cabac_streams_bit_exact(tmp_path, name, kw):
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
+
+
+SCALING = [
+    ("cavlc_sps", dict(scaling="sps")),
+    ("cavlc_both_b", dict(scaling="both", bframes=True)),
+    ("cabac_pps_t8", dict(scaling="pps", cabac=True, transform_8x8=True)),
+    ("cabac_both_t8_b", dict(scaling="both", cabac=True, transform_8x8=True, bframes=True, weighted="implicit")),
+    ("cabac_pps_no_t8", dict(scaling="pps", cabac=True)),
+]
+
+
+@pytest.mark.parametrize("name,kw", SCALING, ids=[s[0] for s in SCALING])
+def test_scaling_matrix_streams_bit_exact(tmp_path, name, kw):
+    """Scaling matrices (8.5.9, the writer's seeded SPS / PPS lists with the
+    fall-back rules, defaults, early-ended and full lists): the device's
+    LevelScale dequantisation (4x4 / 8x8, intra / inter, luma / chroma, the
+    DC transforms) equals the oracle's on every frame, thumbnail, histogram,
+    SAD and score."""
+    _require_gpu()
+    n, W, H = 30, 320, 240
+    path = tmp_path / f"sc_{name}.mp4"
+    scene.synth_write(path, width=W, height=H, n_frames=n, cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.7,
+                      coding="full", slices_per_row=0, max_motion=4, seed=7, **kw)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 4)
+    with scene.VideoScorer(path, keep_frames=True, k=4) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+        assert _first_diff(got, frames) == []
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])

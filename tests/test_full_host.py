@@ -181,3 +181,35 @@ def test_writer_cabac_streams_on_cpu_equal_oracle(tmp_path, harness, name, kw):
         assert got.shape == want.shape
         bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
         assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"
+
+
+SCALING = [
+    ("cavlc_sps", {"scaling": "sps"}),
+    ("cavlc_pps", {"scaling": "pps"}),
+    ("cavlc_both_b", {"scaling": "both", "bframes": True}),
+    ("cabac_sps_t8", {"scaling": "sps", "cabac": True, "transform_8x8": True}),
+    ("cabac_pps_t8", {"scaling": "pps", "cabac": True, "transform_8x8": True}),
+    ("cabac_both_t8_b", {"scaling": "both", "cabac": True, "transform_8x8": True, "bframes": True,
+                         "weighted": "implicit"}),
+    ("cabac_pps_no_t8", {"scaling": "pps", "cabac": True}),
+]
+
+
+@pytest.mark.parametrize("name,kw", SCALING, ids=[s[0] for s in SCALING])
+@pytest.mark.parametrize("seed", [5, 6])
+def test_scaling_matrix_streams_on_cpu_equal_oracle(tmp_path, harness, name, kw, seed):
+    """Streams with scaling matrices (8.5.9; the writer's seeded lists in the
+    SPS, the PPS or both: absent lists under fall-back rules A / B,
+    useDefaultScalingMatrixFlag, lists that end early, full lists; 4x4 and
+    8x8, intra and inter, luma and chroma, Intra16x16 and chroma DC): the
+    product's LevelScale tables (h264_sched.cpp) and dequantisation must
+    equal the oracle's own restatement frame for frame."""
+    path = tmp_path / f"sc_{name}_{seed}.mp4"
+    scene.synth_write(path, width=176, height=144, n_frames=24, coding="full", slices_per_row=0,
+                      cut_min_s=0.4, cut_max_s=1.0, gop_max_s=0.6, seed=seed, **kw)
+    for flags in (1, 0):
+        want, _ = oracle.decode_full(path, flags=flags)
+        got = harness(path, flags)
+        assert got.shape == want.shape
+        bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
+        assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"

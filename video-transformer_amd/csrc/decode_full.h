@@ -54,6 +54,7 @@ struct FullReconArgs {
   int32_t _pad;
   DbkInfo *dbk;              // ring: [slot][mb] deblocking descriptors
   uint32_t *err;
+  const ScaleTab *sct;       // LevelScale4x4 / 8x8 (read when P.scaled)
   FullParams P;
 };
 

@@ -276,28 +276,37 @@ __device__ __forceinline__ void luma_pred4(const uint32_t (&w)[9][3], int xf, in
 
 // 8.5.12.1 chroma DC of chroma block ck: 2x2 Hadamard of the plane's DC levels, scaled
 __device__ __forceinline__ int chroma_dc(const int16_t *arena, uint32_t blocks, uint32_t coef, int pl, int ck,
-                                         int qpc) {
+                                         int qpc, const int32_t *ls) {
   const int64_t blk = stored(blocks, coef, kBlkChromaDc0 + pl);
   if (blk < 0) return 0;
   const uint2 u = *reinterpret_cast<const uint2 *>(arena + 16 * blk);
   const int c0 = static_cast<int16_t>(u.x & 0xffff), c1 = static_cast<int16_t>(u.x >> 16);
   const int c2 = static_cast<int16_t>(u.y & 0xffff), c3 = static_cast<int16_t>(u.y >> 16);
   const int f = ck == 0 ? c0 + c1 + c2 + c3 : ck == 1 ? c0 - c1 + c2 - c3 : ck == 2 ? c0 + c1 - c2 - c3 : c0 - c1 - c2 + c3;
-  return ((f * full::level_scale(qpc % 6, 0, 0)) << (qpc / 6)) >> 5;
+  return ((f * ls[0]) << (qpc / 6)) >> 5;
 }
 // chroma residual of one 4x4 chroma block of plane pl
+// (ls: LevelScale4x4(qPc % 6, .) of the plane's list, 8.5.9)
 __device__ __forceinline__ void chroma_res(const int16_t *arena, uint32_t blocks, uint32_t coef, int pl, int ck,
-                                           int qpc, int (&r)[16]) {
+                                           int qpc, const int32_t *ls, int (&r)[16]) {
   int cf[16];
   load_coefs(arena, stored(blocks, coef, kBlkChromaAc0 + 4 * pl + ck), cf);
-  cf[0] = chroma_dc(arena, blocks, coef, pl, ck, qpc);
-  full::scale_idct4(cf, qpc, true, r);
+  cf[0] = chroma_dc(arena, blocks, coef, pl, ck, qpc, ls);
+  full::scale_idct4(cf, qpc, ls, true, r);
+}
+// LevelScale4x4(qP % 6, .) of a 4x4 block of plane pl (0 Y) in an intra or
+// inter macroblock: the stream's table (flat values without scaling matrices)
+__device__ __forceinline__ const int32_t *ls4_of(const FullReconArgs &a, bool intra, int pl, int qp) {
+  return a.sct->ls4[scale_list4(intra, pl)][qp % 6];
 }
 
 // 8.5.13 for one 4x4 quarter (qx, qy) of an 8x8 block stored as raster rows
 // in the arena (4 consecutive blocks): all 8 rows transformed, then this
 // quarter's 4 columns
-__device__ __forceinline__ void idct8_quarter(const int16_t *arena, int64_t blk, int qp, int qx, int qy, int (&res)[16]) {
+// (ls8: LevelScale8x8(qP % 6, .) of the list when the stream has scaling
+// matrices, else null: Flat_16 from normAdjust8x8's six values)
+__device__ __forceinline__ void idct8_quarter(const int16_t *arena, int64_t blk, int qp, int qx, int qy,
+                                              const int32_t *ls8, int (&res)[16]) {
   int n8[6];
 #pragma unroll
   for (int c = 0; c < 6; ++c) n8[c] = 16 * full::kNorm8[qp % 6][c];
@@ -311,7 +320,7 @@ __device__ __forceinline__ void idct8_quarter(const int16_t *arena, int64_t blk,
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = static_cast<int16_t>((w[j >> 1] >> ((j & 1) * 16)) & 0xffff);
-      const int ls = n8[vts_norm8_class(i, j)];
+      const int ls = ls8 ? ls8[i * 8 + j] : n8[vts_norm8_class(i, j)];
       v[j] = qp >= 36 ? (c * ls) << (sh - 6) : (c * ls + (1 << (5 - sh))) >> (6 - sh);
     }
     const int a0 = v[0] + v[4], a4 = v[0] - v[4], a2 = (v[2] >> 1) - v[6], a6 = v[2] + (v[6] >> 1);
@@ -491,11 +500,11 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
   const bool t8 = (h.modes & kModeT8) != 0;
   const int64_t lb = stored(h.blocks, h.coef, t8 ? kBlkLuma0 + 4 * ((by >> 1) * 2 + (bx >> 1)) : kBlkLuma0 + blkidx(b));
   if (lb >= 0 && t8) {
-    idct8_quarter(a.arena, lb, h.qp, bx & 1, by & 1, res);
+    idct8_quarter(a.arena, lb, h.qp, bx & 1, by & 1, a.P.scaled ? a.sct->ls8[1][h.qp % 6] : nullptr, res);
   } else if (lb >= 0) {
     int cf[16];
     load_coefs(a.arena, lb, cf);
-    full::scale_idct4(cf, h.qp, false, res);
+    full::scale_idct4(cf, h.qp, ls4_of(a, false, 0, h.qp), false, res);
   } else {
 #pragma unroll
     for (int i = 0; i < 16; ++i) res[i] = 0;
@@ -511,7 +520,8 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl) {
       int r[16];
-      chroma_res(a.arena, h.blocks, h.coef, pl, ck, full::qpc_of(h.qp, pl ? a.P.cqp_off2 : a.P.cqp_off), r);
+      const int qpc = full::qpc_of(h.qp, pl ? a.P.cqp_off2 : a.P.cqp_off);
+      chroma_res(a.arena, h.blocks, h.coef, pl, ck, qpc, ls4_of(a, false, 1 + pl, qpc), r);
 #pragma unroll
       for (int y = 0; y < 2; ++y)
 #pragma unroll
@@ -648,11 +658,12 @@ __device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraT
     }
     const int a0 = tr[bx], a1 = tr[4 + bx], a2 = tr[8 + bx], a3 = tr[12 + bx];
     const int f = by == 0 ? a0 + a1 + a2 + a3 : by == 1 ? a0 + a1 - a2 - a3 : by == 2 ? a0 - a1 - a2 + a3 : a0 - a1 + a2 - a3;
-    const int ls = full::level_scale(qp % 6, 0, 0);
+    const int32_t *ls4 = ls4_of(a, true, 0, qp);
+    const int ls = ls4[0];  // 8.5.10: LevelScale4x4(qP % 6, 0, 0) of Intra Y
     int cf[16], res[16];
     load_coefs(a.arena, stored(h.blocks, h.coef, kBlkLuma0 + blkidx(b)), cf);
     cf[0] = qp >= 36 ? (f * ls) << (qp / 6 - 6) : (f * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
-    full::scale_idct4(cf, qp, true, res);
+    full::scale_idct4(cf, qp, ls4, true, res);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       *reinterpret_cast<uint32_t *>(Y + yrow0 + static_cast<int64_t>(by * 4 + r) * pitch + bx * 4) =
@@ -714,7 +725,7 @@ __device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraT
       if (s == b8) {
         const int16_t *T = t.f8, *L = t.f8 + 17;
         int res[16];
-        if (lb >= 0) idct8_quarter(a.arena, lb, qp, qx, qy, res);
+        if (lb >= 0) idct8_quarter(a.arena, lb, qp, qx, qy, a.P.scaled ? a.sct->ls8[0][qp % 6] : nullptr, res);
         else
 #pragma unroll
           for (int i = 0; i < 16; ++i) res[i] = 0;
@@ -803,7 +814,7 @@ __device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraT
     else tr = bx < 3 && blkidx((by - 1) * 4 + bx + 1) < k;
     int cf[16], res[16];
     load_coefs(a.arena, stored(h.blocks, h.coef, kBlkLuma0 + k), cf);
-    full::scale_idct4(cf, qp, false, res);
+    full::scale_idct4(cf, qp, ls4_of(a, true, 0, qp), false, res);
     const int step = bx + 2 * by;
     for (int s = 0; s <= 9; ++s) {
       if (s == step) {
@@ -938,7 +949,8 @@ __device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraT
         for (int x = 0; x < 4; ++x) v[y * 4 + x] = c255((aa + bb * (ox + x - 3) + cc * (oy + y - 3) + 16) >> 5);
     }
     int r[16];
-    chroma_res(a.arena, h.blocks, h.coef, pl, ck, full::qpc_of(qp, pl ? a.P.cqp_off2 : a.P.cqp_off), r);
+    const int qpc = full::qpc_of(qp, pl ? a.P.cqp_off2 : a.P.cqp_off);
+    chroma_res(a.arena, h.blocks, h.coef, pl, ck, qpc, ls4_of(a, true, 1 + pl, qpc), r);
 #pragma unroll
     for (int y = 0; y < 4; ++y)
 #pragma unroll

@@ -12,6 +12,12 @@
 #pragma once
 #include <cstdint>
 
+#if defined(__HIPCC__)
+#define VTS_HD_FULL __host__ __device__
+#else
+#define VTS_HD_FULL
+#endif
+
 namespace vts {
 
 // Slice of a window, as scheduled by the host (window-relative indices).
@@ -63,7 +69,8 @@ struct FullParams {
   int32_t bframes;      // the stream has B slices: every macroblock also writes an MbRecB
   int32_t direct8x8;    // direct_8x8_inference_flag
   int32_t has_ext;      // some slice has a SliceExt (B or weighted prediction)
-  int32_t _pad[2];
+  int32_t scaled;       // scaling matrices other than Flat_16: dequantise from ScaleTab
+  int32_t _pad;
 };
 
 // Stored coefficient blocks of a macroblock, in parse order = bit order.
@@ -86,6 +93,18 @@ enum : uint8_t {
   kMbPcm = 3,
   kMbSkip = 4,
 };
+
+// 8.5.9 LevelScale4x4 / LevelScale8x8 of a stream: weightScale (Flat_16, the
+// Table 7-3 / 7-4 defaults or the stream's scaling lists after fall-back rules
+// A and B, 7.4.2.1.1 / 7.4.2.2) times normAdjust.  ls4[list][qP % 6][raster]
+// for lists 0..5 = Intra Y, Cb, Cr, Inter Y, Cb, Cr; ls8[list][qP % 6][raster
+// 8x8] for lists 0, 1 = Intra Y, Inter Y (4:2:0).
+struct ScaleTab {
+  int32_t ls4[6][6][16];
+  int32_t ls8[2][6][64];
+};
+// list of a 4x4 block: plane 0 Y, 1 Cb, 2 Cr of an intra or inter macroblock
+VTS_HD_FULL inline int scale_list4(bool intra, int plane) { return (intra ? 0 : 3) + plane; }
 
 // One decoded macroblock's syntax (128 bytes).
 struct alignas(16) MbRec {

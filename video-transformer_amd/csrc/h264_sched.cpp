@@ -6,6 +6,9 @@
 // modification), 8.2.5 (IDR, sliding window, MMCO 1-6).
 #include "h264_sched.h"
 
+#include "h264_cabac_tables.h"
+#include "h264_tables.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -90,12 +93,86 @@ bool more_rbsp(const std::vector<uint8_t> &nal, const HdrReader &r) {
   return at < stop;
 }
 
+const uint8_t kDef4[2][16] = VTS_DEFAULT_4x4_DATA;  // Tables 7-3 / 7-4 (scan order)
+const uint8_t kDef8[2][64] = VTS_DEFAULT_8x8_DATA;
+
+// 7.3.2.1.1.1 scaling_list(): n values in zig-zag order; true when
+// useDefaultScalingMatrixFlag (the first delta leaves nextScale 0)
+bool read_scaling_list(HdrReader &r, int n, uint8_t *list) {
+  int last = 8, next = 8;
+  bool use_default = false;
+  for (int j = 0; j < n; ++j) {
+    if (next != 0) {
+      const int delta = r.se();
+      next = (last + delta + 256) % 256;
+      use_default = j == 0 && next == 0;
+    }
+    list[j] = static_cast<uint8_t>(next == 0 ? last : next);
+    last = list[j];
+  }
+  return use_default;
+}
+
+// The scaling lists of one parameter set (7.4.2.1.1 / 7.4.2.2): lists 0..5
+// 4x4, 6..7 8x8 (4:2:0), present_flag per list; absent lists take the
+// fall-back of rule A (SPS: defaults and the previous list) or B (PPS:
+// the sequence-level list `seq` for lists 0, 3, 6, 7)
+void read_scaling_matrix(HdrReader &r, int n_lists, bool rule_b, const uint8_t (*seq4)[16],
+                         const uint8_t (*seq8)[64], uint8_t (*l4)[16], uint8_t (*l8)[64]) {
+  for (int i = 0; i < 8; ++i) {
+    const bool present = i < n_lists && r.u(1);
+    const int inter = (i >= 3 && i < 6) || i == 7 ? 1 : 0;
+    if (i < 6) {
+      if (present) {
+        if (read_scaling_list(r, 16, l4[i])) std::memcpy(l4[i], kDef4[inter], 16);
+      } else if (i == 0 || i == 3) {
+        std::memcpy(l4[i], rule_b ? seq4[i] : kDef4[inter], 16);
+      } else {
+        std::memcpy(l4[i], l4[i - 1], 16);
+      }
+    } else {
+      uint8_t *d = l8[i - 6];
+      if (present) {
+        if (read_scaling_list(r, 64, d)) std::memcpy(d, kDef8[inter], 64);
+      } else {
+        std::memcpy(d, rule_b ? seq8[i - 6] : kDef8[inter], 64);
+      }
+    }
+  }
+}
+
+// 4x4 / 8x8 zig-zag (frame) scan: raster position of coefficient k
+const uint8_t kZz4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+const uint8_t kZz8[64] = VTS_ZZ8_DATA;  // 8.5.7 Table 8-13
+
 }  // namespace
+
+void scale_tab_build(const uint8_t (*w4)[16], const uint8_t (*w8)[64], ScaleTab *t) {
+  static const int nv[6][3] = VTS_NORMV_DATA;  // normAdjust4x4 (8.5.9)
+  static const int n8[6][6] = VTS_NORM8_DATA;  // normAdjust8x8
+  for (int l = 0; l < 6; ++l)
+    for (int m = 0; m < 6; ++m)
+      for (int k = 0; k < 16; ++k) {
+        const int i = k >> 2, j = k & 3;
+        const int c = (!(i & 1) && !(j & 1)) ? 0 : (((i & 1) && (j & 1)) ? 1 : 2);
+        t->ls4[l][m][k] = w4[l][k] * nv[m][c];
+      }
+  for (int l = 0; l < 2; ++l)
+    for (int m = 0; m < 6; ++m)
+      for (int k = 0; k < 64; ++k) {
+        t->ls8[l][m][k] = w8[l][k] * n8[m][vts_norm8_class(k >> 3, k & 7)];
+      }
+}
 
 std::string sched_stream_facts(const std::vector<uint8_t> &sps_nal, const std::vector<uint8_t> &pps_nal,
                                const Sps &sps, const Pps &pps, SchedStream *out) {
   *out = SchedStream{};
   out->cqp_off2 = pps.chroma_qp_index_offset;
+  // scaling lists (zig-zag order): sequence level sl4 / sl8 (Flat_16 without
+  // seq_scaling_matrix_present_flag), picture level pl4 / pl8
+  uint8_t sl4[6][16], sl8[2][64], pl4[6][16], pl8[2][64];
+  std::memset(sl4, 16, sizeof(sl4));
+  std::memset(sl8, 16, sizeof(sl8));
   {  // SPS: seq_scaling_matrix_present_flag (High profiles only)
     HdrReader r(sps_nal.data() + 1, static_cast<int64_t>(sps_nal.size()) - 1);
     const int prof = static_cast<int>(r.u(8));
@@ -111,6 +188,7 @@ std::string sched_stream_facts(const std::vector<uint8_t> &sps_nal, const std::v
       r.ue();
       r.u(1);
       out->seq_scaling = static_cast<int>(r.u(1));
+      if (out->seq_scaling) read_scaling_matrix(r, cf == 3 ? 12 : 8, false, nullptr, nullptr, sl4, sl8);
     }
   }
   {  // PPS: skip to the optional tail (7.3.2.2)
@@ -128,15 +206,23 @@ std::string sched_stream_facts(const std::vector<uint8_t> &sps_nal, const std::v
     r.se();
     r.se();
     r.u(3);
+    std::memcpy(pl4, sl4, sizeof(pl4));
+    std::memcpy(pl8, sl8, sizeof(pl8));
     if (more_rbsp(pps_nal, r)) {
       out->transform_8x8 = static_cast<int>(r.u(1));
       out->pic_scaling = static_cast<int>(r.u(1));
-      if (out->pic_scaling) return "PPS scaling matrices";
+      if (out->pic_scaling) read_scaling_matrix(r, 6 + 2 * out->transform_8x8, true, sl4, sl8, pl4, pl8);
       out->cqp_off2 = r.se();
     }
     if (r.err) return "truncated PPS";
   }
-  if (out->seq_scaling) return "SPS scaling matrices";
+  // weightScale: the lists in raster order (inverse zig-zag), then LevelScale
+  uint8_t w4[6][16], w8[2][64];
+  for (int l = 0; l < 6; ++l)
+    for (int k = 0; k < 16; ++k) w4[l][kZz4[k]] = pl4[l][k];
+  for (int l = 0; l < 2; ++l)
+    for (int k = 0; k < 64; ++k) w8[l][kZz8[k]] = pl8[l][k];
+  scale_tab_build(w4, w8, &out->scale);
   if (out->transform_8x8 && !pps.entropy_coding_mode) return "8x8 transform with CAVLC (CABAC only)";
   if (pps.redundant_pic_cnt_present) return "redundant pictures";
   return "";

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "h264.h"
+#include "h264_full.h"
 
 namespace vts {
 
@@ -54,7 +55,11 @@ struct SchedStream {
   int transform_8x8 = 0;     // PPS transform_8x8_mode_flag
   int pic_scaling = 0;       // pic_scaling_matrix_present_flag
   int cqp_off2 = 0;          // second_chroma_qp_index_offset (= chroma_qp_index_offset if absent)
+  ScaleTab scale;            // LevelScale4x4 / 8x8 of the active SPS + PPS (flat without matrices)
 };
+
+// weightScale4x4 / 8x8 in raster order (w4[list][16], w8[list][64]) -> LevelScale
+void scale_tab_build(const uint8_t (*w4)[16], const uint8_t (*w8)[64], ScaleTab *t);
 
 // Parse the High-profile PPS extension (more_rbsp_data part) and the SPS
 // scaling flag; "" or the reason the general decoder cannot take the stream.

@@ -107,11 +107,13 @@ struct ReconCtx {
   int32_t mbw, mbh;
   int32_t cip, cqp_off, cqp_off2;
   uint32_t epoch;
+  const ScaleTab *sct;      // LevelScale4x4 / 8x8 (8.5.9)
 };
 
-// 8.5.12: scaling (flat) + 4x4 inverse transform; c raster (row i, col j);
-// dc_done: c[0] is an already scaled DC; r receives the residual
-VTS_HD inline void scale_idct4(const int *c, int qp, bool dc_done, int *r) {
+// 8.5.12: scaling + 4x4 inverse transform; c raster (row i, col j); ls =
+// LevelScale4x4(qP % 6, raster) of the block's list; dc_done: c[0] is an
+// already scaled DC; r receives the residual
+VTS_HD inline void scale_idct4(const int *c, int qp, const int32_t *ls, bool dc_done, int *r) {
   int d[16];
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < 4; ++j) {
@@ -120,8 +122,7 @@ VTS_HD inline void scale_idct4(const int *c, int qp, bool dc_done, int *r) {
         d[0] = c[0];
         continue;
       }
-      const int ls = level_scale(qp % 6, i, j);
-      d[k] = qp >= 24 ? (c[k] * ls) << (qp / 6 - 4) : (c[k] * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+      d[k] = qp >= 24 ? (c[k] * ls[k]) << (qp / 6 - 4) : (c[k] * ls[k] + (1 << (3 - qp / 6))) >> (4 - qp / 6);
     }
   int f[16];
   for (int i = 0; i < 4; ++i) {
@@ -142,17 +143,25 @@ VTS_HD inline void scale_idct4(const int *c, int qp, bool dc_done, int *r) {
   }
 }
 
-// 8.5.13: scaling (flat) + 8x8 inverse transform; c raster 8x8; r receives the residual
+// the same with Flat_16 (the upload encoder's own reconstruction)
+VTS_HD inline void scale_idct4(const int *c, int qp, bool dc_done, int *r) {
+  int32_t ls[16];
+  for (int k = 0; k < 16; ++k) ls[k] = level_scale(qp % 6, k >> 2, k & 3);
+  scale_idct4(c, qp, ls, dc_done, r);
+}
+
+// 8.5.13: scaling + 8x8 inverse transform; c raster 8x8; ls8 = LevelScale8x8(qP % 6,
+// raster) of the block's list; r receives the residual
 #if defined(__HIPCC__)
 __device__ __constant__ static const uint8_t kNorm8[6][6] = VTS_NORM8_DATA;
 #else
 static const uint8_t kNorm8[6][6] = VTS_NORM8_DATA;
 #endif
-VTS_HD inline void scale_idct8(const int *c, int qp, int *r) {
+VTS_HD inline void scale_idct8(const int *c, int qp, const int32_t *ls8, int *r) {
   int d[64], g[64];
   for (int i = 0; i < 8; ++i)
     for (int j = 0; j < 8; ++j) {
-      const int ls = 16 * kNorm8[qp % 6][vts_norm8_class(i, j)], k = i * 8 + j;
+      const int k = i * 8 + j, ls = ls8[k];
       d[k] = qp >= 36 ? (c[k] * ls) << (qp / 6 - 6) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     }
   for (int pass = 0; pass < 2; ++pass)
@@ -607,7 +616,7 @@ struct MbRecon {
     const int k = ((b >> 3) << 3) | (((b & 3) >> 1) << 2) | (((b >> 2) & 1) << 1) | (b & 1);  // luma4x4BlkIdx
     load_block(kBlkLuma0 + k, cf);
     if (i16) cf[0] = dcy[b];
-    scale_idct4(cf, qp, i16, res);
+    scale_idct4(cf, qp, c.sct->ls4[scale_list4(m.type != kMbInter && m.type != kMbSkip, 0)][qp % 6], i16, res);
   }
 
   VTS_HD void chroma_residual(int qpy) {
@@ -617,12 +626,12 @@ struct MbRecon {
       load_block(kBlkChromaDc0 + pl, dcl);
       const int c0 = dcl[0], c1 = dcl[1], c2 = dcl[2], c3 = dcl[3];
       const int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
-      const int ls = level_scale(qpc % 6, 0, 0);
+      const int32_t *lsc = c.sct->ls4[scale_list4(m.type != kMbInter && m.type != kMbSkip, 1 + pl)][qpc % 6];
       for (int k = 0; k < 4; ++k) {
         int cf[16], r[16];
         load_block(kBlkChromaAc0 + 4 * pl + k, cf);
-        cf[0] = ((f[k] * ls) << (qpc / 6)) >> 5;
-        scale_idct4(cf, qpc, true, r);
+        cf[0] = ((f[k] * lsc[0]) << (qpc / 6)) >> 5;  // 8.5.11.2
+        scale_idct4(cf, qpc, lsc, true, r);
         const int bx = (k & 1) * 4, by = (k >> 1) * 4;
         for (int y = 0; y < 4; ++y)
           for (int x = 0; x < 4; ++x)
@@ -665,7 +674,7 @@ struct MbRecon {
         for (int b8 = 0; b8 < 4; ++b8) {
           int cf[64], r8[64];
           load_block8(b8, cf);
-          scale_idct8(cf, qp, r8);
+          scale_idct8(cf, qp, c.sct->ls8[1][qp % 6], r8);
           put_luma8(b8, r8);
         }
       } else {
@@ -681,7 +690,7 @@ struct MbRecon {
         intra8x8(b8, (m.i4[r >> 1] >> ((r & 1) * 4)) & 15, done);
         int cf[64], r8[64];
         load_block8(b8, cf);
-        scale_idct8(cf, qp, r8);
+        scale_idct8(cf, qp, c.sct->ls8[0][qp % 6], r8);
         put_luma8(b8, r8);
         done |= (1u << r) | (1u << (r + 1)) | (1u << (r + 4)) | (1u << (r + 5));
       }
@@ -706,7 +715,7 @@ struct MbRecon {
         t[i * 4 + 2] = a0 - a1 - a2 + a3;
         t[i * 4 + 3] = a0 - a1 + a2 - a3;
       }
-      const int ls = level_scale(qp % 6, 0, 0);
+      const int ls = c.sct->ls4[0][qp % 6][0];  // LevelScale4x4(qP % 6, 0, 0) of Intra Y
       for (int j = 0; j < 4; ++j) {
         const int a0 = t[j], a1 = t[4 + j], a2 = t[8 + j], a3 = t[12 + j];
         const int f[4] = {a0 + a1 + a2 + a3, a0 + a1 - a2 - a3, a0 - a1 - a2 + a3, a0 - a1 + a2 - a3};

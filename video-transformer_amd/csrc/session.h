@@ -131,6 +131,8 @@ struct vts_ctx {
   // ---- general decoder (decode_full.hip, session_full.hip)
   bool general = false;
   vts::FullParams fprm{};
+  vts::ScaleTab scale_tab{};       // LevelScale of the stream (8.5.9; flat without scaling matrices)
+  vts::ScaleTab *d_scale = nullptr;
   std::vector<vts::FullSlice> fslices;  // every window's slices (window-relative slots, arena)
   vts::FullSlice *d_fslices = nullptr;
   vts::MbRec *d_recs[2] = {nullptr, nullptr};

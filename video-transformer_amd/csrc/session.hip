@@ -92,6 +92,8 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   HIP_TRY(hipMalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
   if (!c->fslices.empty())
     HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_scale, sizeof(ScaleTab)));
+  HIP_TRY(hipMemcpy(c->d_scale, &c->scale_tab, sizeof(ScaleTab), hipMemcpyHostToDevice));
   // the slice NALs' RBSPs, made once: the parsers read plain bits
   HIP_TRY(hipMalloc(&c->d_rbsp, static_cast<size_t>(c->es_bytes)));
   HIP_TRY(hipMalloc(&c->d_rbsp_len, sizeof(int32_t) * std::max<size_t>(1, c->fslices.size())));
@@ -1094,6 +1096,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_fslices);
   f(c->d_rbsp);
   f(c->d_rbsp_len);
+  f(c->d_scale);
   f(c->d_exts);
   f(c->d_porder);
   for (int r = 0; r < 2; ++r) {

@@ -78,6 +78,8 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   c->fprm.cqp_off2 = facts.cqp_off2;
   c->fprm.cabac = c->pps.entropy_coding_mode;
   c->fprm.t8mode = facts.transform_8x8;
+  c->fprm.scaled = facts.seq_scaling || facts.pic_scaling;
+  c->scale_tab = facts.scale;
   for (const SchedFrame &fr : frames) c->fprm.bframes |= fr.has_b ? 1 : 0;
   c->fprm.direct8x8 = c->sps.direct_8x8_inference;
   const int64_t n = c->n_frames;
@@ -373,6 +375,7 @@ int run_general(vts_ctx *c) {
     ra.epoch = epoch;
     ra.deblock = 1;
     ra.err = c->d_err;
+    ra.sct = c->d_scale;
     ra.P = c->fprm;
     if (!w.lvl_off.empty()) {  // every picture's bS at once: it needs only the parse's records
       ra.frames = c->d_levels + w.lvl_off[0];

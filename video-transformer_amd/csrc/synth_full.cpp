@@ -1704,13 +1704,50 @@ void encode_chunk_full(const vts_synth_params &P, SynthChunk *ck) {
 // Constrained Baseline SPS / PPS of the full-syntax streams: 3 reference
 // frames, frame_num wrapping at 16, POC type 2, deblocking control present,
 // two active references by default, chroma QP offset from the seed.
+
+// 7.3.2.1.1.1 scaling_list() for lists 0..n-1 (16 values each for 0..5, 64
+// for 6, 7), each chosen from the seed: absent (the fall-back rules apply),
+// useDefaultScalingMatrixFlag, a list that ends early (nextScale 0: the rest
+// repeat the last value) or a full list of values 4..64
+void write_scaling_lists(BitWriter &w, int n, uint64_t seed) {
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + 0x2545F4914F6CDD1Dull;
+  auto rnd = [&](uint32_t m) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    return static_cast<uint32_t>(x % m);
+  };
+  for (int i = 0; i < n; ++i) {
+    const uint32_t kind = rnd(4);  // 0 absent, 1 default, 2 early end, 3 full
+    w.u(1, kind ? 1 : 0);          // scaling_list_present_flag
+    if (!kind) continue;
+    if (kind == 1) {
+      w.se(-8);  // nextScale 0 at j = 0
+      continue;
+    }
+    const int size = i < 6 ? 16 : 64;
+    const int stop = kind == 2 ? 1 + static_cast<int>(rnd(static_cast<uint32_t>(size - 1))) : size;
+    int last = 8;
+    for (int j = 0; j < stop; ++j) {
+      const int next = 4 + static_cast<int>(rnd(61));
+      int delta = next - last;
+      if (delta > 127) delta -= 256;
+      if (delta < -128) delta += 256;
+      w.se(delta);
+      last = next;
+    }
+    if (stop < size) w.se(-last);  // nextScale 0: the remaining entries repeat the last
+  }
+}
 void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t> *sps_nal,
                        std::vector<uint8_t> *pps_nal) {
   const int mbw = (P.width + 15) / 16, mbh = (P.height + 15) / 16;
   const int crop_r = mbw * 16 - P.width, crop_b = mbh * 16 - P.height;
   const bool bm = (P.edge_cases & 32) != 0;
   const bool cabac = (P.edge_cases & 1024) != 0, t8 = cabac && (P.edge_cases & 2048) != 0;
-  const int profile = t8 ? 100 : ((bm || cabac) ? 77 : 66);  // High / Main / Constrained Baseline
+  // bits 12 / 13: scaling matrices in the SPS / the PPS (High profile)
+  const bool sps_scale = (P.edge_cases & 4096) != 0, pps_scale = (P.edge_cases & 8192) != 0;
+  const int profile = (t8 || sps_scale || pps_scale) ? 100 : ((bm || cabac) ? 77 : 66);  // High / Main / Constrained Baseline
   BitWriter s;
   s.u(8, static_cast<uint32_t>(profile));
   s.u(8, profile == 66 ? 0xC0 : 0x00);
@@ -1721,7 +1758,8 @@ void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t
     s.ue(0);    // bit_depth_luma_minus8
     s.ue(0);    // bit_depth_chroma_minus8
     s.u(1, 0);  // qpprime_y_zero_transform_bypass_flag
-    s.u(1, 0);  // seq_scaling_matrix_present_flag
+    s.u(1, sps_scale ? 1 : 0);  // seq_scaling_matrix_present_flag
+    if (sps_scale) write_scaling_lists(s, 8, P.seed * 2 + 1);
   }
   s.ue(kLog2MaxFrameNum - 4);
   if (bm) {
@@ -1766,9 +1804,10 @@ void make_sps_pps_full(const vts_synth_params &P, int level, std::vector<uint8_t
   p.u(1, 1);                                   // deblocking_filter_control_present_flag
   p.u(1, (P.edge_cases & 16) ? 1 : 0);         // constrained_intra_pred_flag
   p.u(1, 0);
-  if (t8) {
-    p.u(1, 1);                                 // transform_8x8_mode_flag
-    p.u(1, 0);                                 // pic_scaling_matrix_present_flag
+  if (t8 || pps_scale) {
+    p.u(1, t8 ? 1 : 0);                        // transform_8x8_mode_flag
+    p.u(1, pps_scale ? 1 : 0);                 // pic_scaling_matrix_present_flag
+    if (pps_scale) write_scaling_lists(p, 6 + (t8 ? 2 : 0), P.seed * 2 + 2);
     p.se(static_cast<int>(P.seed % 3) - 1);    // second_chroma_qp_index_offset
   }
   p.trailing();

@@ -281,7 +281,7 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 constrained_intra: bool = False, bframes: bool = False,
                 weighted: str | None = None, temporal_direct: bool = False,
                 chroma_deblock: bool = False, cabac: bool = False,
-                transform_8x8: bool = False) -> dict:
+                transform_8x8: bool = False, scaling: str | None = None) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
     and the ground-truth scene-cut frames.  coding="full" only: ``bframes`` codes
     B pictures (Main profile, POC type 0, composition offsets in the MP4),
@@ -293,7 +293,9 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     kernels must refuse).  coding="full" only: ``cabac`` writes the same syntax
     decisions with CABAC (cabac_init_idc 0, Main profile; x264's default entropy
     coder) and ``transform_8x8`` (with cabac, High profile) adds Intra_8x8 and
-    8x8-transform inter macroblocks."""
+    8x8-transform inter macroblocks.  coding="full" only: ``scaling`` =
+    "sps", "pps" or "both" writes seeded scaling matrices (High profile; lists
+    absent, default, ending early or full, exercising fall-back rules A / B)."""
     p = _lib.SynthParams()
     p.width, p.height, p.fps_num, p.fps_den = width, height, fps, 1
     p.n_frames, p.seed = n_frames, seed
@@ -312,6 +314,10 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
         if transform_8x8 and not cabac:
             raise ValueError("transform_8x8 needs cabac (8x8 CAVLC streams are refused)")
         p.edge_cases |= 1024 | (2048 if transform_8x8 else 0)
+    if scaling:
+        if coding != "full":
+            raise ValueError("scaling matrices need coding='full'")
+        p.edge_cases |= {"sps": 4096, "pps": 8192, "both": 4096 | 8192}[scaling]
     if chroma_deblock:
         if coding != "subset":
             raise ValueError("chroma_deblock is a subset-stream edge case")
