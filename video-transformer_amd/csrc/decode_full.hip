@@ -66,6 +66,7 @@ constexpr int kInterThreads = 256;   // 16 macroblocks x 16 blocks
 #endif
 constexpr int kIntraThreads = VTS_INTRA_THREADS;  // 512: 32 macroblocks in flight (256 VGPRs for the Intra_8x8 path)
 constexpr int kIntraSlots = kIntraThreads / 16;
+constexpr int kIntraLevels = 512;  // intra dependency levels bucketed in LDS (more: one scan per level)
 constexpr int kDbkThreads = VTS_DBK_THREADS;      // 1024: 16 waves = 16 row pairs in flight
 constexpr int kDbkWaves = kDbkThreads / 64;
 
@@ -969,6 +970,7 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   extern __shared__ uint16_t s_list[];  // nmb entries
   __shared__ IntraTile tiles[kIntraSlots];
   __shared__ int s_max, s_cnt;
+  __shared__ int s_lvl[kIntraLevels + 1], s_fill[kIntraLevels];
   const int nmb = a.P.mb_width * a.P.mb_height;
   const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
@@ -984,6 +986,35 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   __syncthreads();
   const int maxl = s_max;
   const int ms = tid >> 4, b = tid & 15;
+  if (maxl < kIntraLevels) {
+    // the picture's intra macroblocks bucketed by level once (a counting
+    // sort in LDS), then the levels in order: an all-intra picture has
+    // ~mbw + 2 mbh levels, and a scan of every level per level cost more
+    // than its reconstruction
+    for (int i = tid; i <= maxl + 1; i += kIntraThreads) s_lvl[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < nmb; i += kIntraThreads) {
+      const int v = lv[i];
+      if (v != kNoLevel) atomicAdd(&s_lvl[v + 1], 1);
+    }
+    __syncthreads();
+    if (tid == 0)  // s_lvl[l] = first list entry of level l (exclusive scan)
+      for (int l = 1; l <= maxl + 1; ++l) s_lvl[l] += s_lvl[l - 1];
+    __syncthreads();
+    for (int i = tid; i <= maxl; i += kIntraThreads) s_fill[i] = s_lvl[i];
+    __syncthreads();
+    for (int i = tid; i < nmb; i += kIntraThreads) {
+      const int v = lv[i];
+      if (v != kNoLevel) s_list[atomicAdd(&s_fill[v], 1)] = static_cast<uint16_t>(i);
+    }
+    __syncthreads();
+    for (int l = 0; l <= maxl; ++l) {
+      const int j0 = s_lvl[l], j1 = s_lvl[l + 1];
+      for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms]);
+      __syncthreads();
+    }
+    return;
+  }
   for (int l = 0; l <= maxl; ++l) {
     if (tid == 0) s_cnt = 0;
     __syncthreads();
