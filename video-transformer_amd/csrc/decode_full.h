@@ -24,6 +24,11 @@ struct FullParseArgs {
   int16_t *arena;            // ring's coefficient arena
   uint32_t *err;
   const int32_t *order;      // launch-relative slice of workgroup i (longest first), null = i
+  // one launch for every slice of the window (merged): a B slice waits until
+  // pdone[colocated slot] reaches pneed[colocated slot] (the picture's slice
+  // count); every slice adds 1 to pdone[its slot] when its records are out
+  uint32_t *pdone;           // per ring slot, zeroed before the launch; null = not merged
+  const int32_t *pneed;      // per ring slot
   FullParams P;
 };
 

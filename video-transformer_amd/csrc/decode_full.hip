@@ -87,10 +87,25 @@ __device__ __forceinline__ void parse_one(const FullParseArgs &a, full::FullScra
   full::BCtx bc{};
   if (P.bframes) bc.recs1 = a.recs1 + s.slot * nmb;
   if (s.ext >= 0) bc.x = a.exts + s.ext;
-  if (s.is_p == kSliceB && bc.x) {  // colocated picture: RefPicList1[0], parsed by an earlier launch
+  if (s.is_p == kSliceB && bc.x) {  // colocated picture: RefPicList1[0], parsed earlier
     const int col = bc.x->ref_slot1[0];
     bc.col = a.recs + col * nmb;
     bc.col1 = a.recs1 + col * nmb;
+    if (a.pdone) {
+      // merged launch: the colocated picture's slices have lower workgroup
+      // indices (dispatched first on every XCD), so this wait ends; bounded
+      // anyway (~3 s), then the slice reports a missing reference
+      const uint32_t need = static_cast<uint32_t>(a.pneed[col]);
+      uint32_t spins = 0;
+      while (__hip_atomic_load(&a.pdone[col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        if (++spins > (1u << 25)) {
+          atomicOr(a.err, static_cast<uint32_t>(DEC_E_NO_REF));
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the colocated records, across XCD L2s
+    }
   }
   const uint8_t *rbsp = a.rbsp + s.nal_offset + 1;
   const int32_t len = a.rbsp_len[i];
@@ -102,6 +117,10 @@ __device__ __forceinline__ void parse_one(const FullParseArgs &a, full::FullScra
     e = full::parse_slice_full(rbsp, len, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
                                a.ilvl + s.slot * nmb, a.arena, a.epoch, scratch, bc);
   if (e) atomicOr(a.err, e);
+  if (a.pdone) {  // this slice's records are out (every path, errors included)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.pdone[s.slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 // A wave of 64 lanes that all run the same (uniform) parse: the parser's state
 // is scalar, and full EXEC keeps the lane tables (LaneTab, parse_full.h) whole

@@ -37,6 +37,7 @@ struct Window {
   std::vector<int64_t> tb_off;
   std::vector<int32_t> tb_cnt, tb_L;
   int64_t fs0 = 0, fs1 = 0;        // general decoder: slices [fs0, fs1) of vts_ctx::fslices
+  int64_t pn0 = 0;                 // general decoder: the window's slot entries in vts_ctx::pneed
   std::vector<int32_t> plv_end;    // general decoder: parse launch j covers window slices
                                    // [plv_end[j-1], plv_end[j]) (B pictures after their colocated picture)
 };
@@ -141,6 +142,12 @@ struct vts_ctx {
   vts::SliceExt *d_exts = nullptr;
   std::vector<int32_t> porder;          // per fslice: parse order inside its launch (longest slice first)
   int32_t *d_porder = nullptr;
+  std::vector<int32_t> porder_m;        // per fslice: order inside the window's merged launch
+  int32_t *d_porder_m = nullptr;
+  std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
+  int32_t *d_pneed = nullptr;
+  uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
+  bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock

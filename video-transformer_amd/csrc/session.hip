@@ -103,6 +103,13 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   HIP_TRY(hipMalloc(&c->d_porder, sizeof(int32_t) * std::max<size_t>(1, c->porder.size())));
   if (!c->porder.empty())
     HIP_TRY(hipMemcpy(c->d_porder, c->porder.data(), sizeof(int32_t) * c->porder.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_porder_m, sizeof(int32_t) * std::max<size_t>(1, c->porder_m.size())));
+  if (!c->porder_m.empty())
+    HIP_TRY(hipMemcpy(c->d_porder_m, c->porder_m.data(), sizeof(int32_t) * c->porder_m.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&c->d_pneed, sizeof(int32_t) * std::max<size_t>(1, c->pneed.size())));
+  if (!c->pneed.empty())
+    HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
+  if (const char *e = std::getenv("VTS_PARSE_MERGE")) c->parse_merged = std::atoi(e) != 0;
   HIP_TRY(hipMalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
@@ -116,6 +123,7 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
     if (c->fprm.bframes)
       HIP_TRY(hipMalloc(&c->d_recs1[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRecB)));
     HIP_TRY(hipMalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
+    HIP_TRY(hipMalloc(&c->d_pdone[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
     HIP_TRY(hipMalloc(&c->d_dbk[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(DbkInfo)));
     HIP_TRY(hipMalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
     HIP_TRY(hipMalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
@@ -1099,10 +1107,13 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_scale);
   f(c->d_exts);
   f(c->d_porder);
+  f(c->d_porder_m);
+  f(c->d_pneed);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);
     f(c->d_ilvl[r]);
+    f(c->d_pdone[r]);
     f(c->d_dbk[r]);
     f(c->d_arena[r]);
   }

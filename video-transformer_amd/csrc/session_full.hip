@@ -184,6 +184,8 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   c->fslices.clear();
   c->exts.clear();
   c->porder.clear();
+  c->porder_m.clear();
+  c->pneed.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
   for (Window &w : c->windows) {
@@ -259,6 +261,17 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
       return c->fslices[static_cast<size_t>(b + x)].nal_size > c->fslices[static_cast<size_t>(b + y)].nal_size;
     });
     }
+    // merged parse launch: the levels' orders back to back (window-relative),
+    // and each picture slot's slice count
+    for (size_t j = 0; j < w.plv_end.size(); ++j) {
+      const int32_t b0 = j ? w.plv_end[j - 1] : 0;
+      for (int32_t k = b0; k < w.plv_end[j]; ++k)
+        c->porder_m.push_back(b0 + c->porder[static_cast<size_t>(w.fs0 + k)]);
+    }
+    w.pn0 = static_cast<int64_t>(c->pneed.size());
+    c->pneed.resize(c->pneed.size() + static_cast<size_t>(w.f1 - w.f0), 0);
+    for (int64_t k = w.fs0; k < static_cast<int64_t>(c->fslices.size()); ++k)
+      ++c->pneed[static_cast<size_t>(w.pn0 + c->fslices[static_cast<size_t>(k)].slot)];
     if (arena > 0xffffffffll) return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
     c->fprm.has_ext = c->exts.empty() ? 0 : 1;
     w.fs1 = static_cast<int64_t>(c->fslices.size());
@@ -348,14 +361,29 @@ int run_general(vts_ctx *c) {
     pa.arena = c->d_arena[r];
     pa.err = c->d_err;
     pa.P = c->fprm;
-    for (size_t j = 0; j < w.plv_end.size(); ++j) {  // B pictures after their colocated pictures
-      const int32_t b0 = j ? w.plv_end[j - 1] : 0;
-      pa.slices = c->d_fslices + w.fs0 + b0;
-      pa.rbsp_len = c->d_rbsp_len + w.fs0 + b0;
-      pa.n_slices = w.plv_end[j] - b0;
-      pa.slice0 = b0;
-      pa.order = c->d_porder + w.fs0 + b0;
+    if (c->parse_merged && w.plv_end.size() > 1) {
+      // one launch: B slices wait for their colocated pictures' slices, which
+      // come first in the order, so the launch ends on a full machine instead
+      // of once per colocated level on its longest slices alone
+      HIP_TRY(hipMemsetAsync(c->d_pdone[r], 0, sizeof(uint32_t) * static_cast<size_t>(w.f1 - w.f0), sp));
+      pa.slices = c->d_fslices + w.fs0;
+      pa.rbsp_len = c->d_rbsp_len + w.fs0;
+      pa.n_slices = static_cast<int32_t>(w.fs1 - w.fs0);
+      pa.slice0 = 0;
+      pa.order = c->d_porder_m + w.fs0;
+      pa.pdone = c->d_pdone[r];
+      pa.pneed = c->d_pneed + w.pn0;
       VTS_TRY(parse_full_launch(pa, sp));
+    } else {
+      for (size_t j = 0; j < w.plv_end.size(); ++j) {  // B pictures after their colocated pictures
+        const int32_t b0 = j ? w.plv_end[j - 1] : 0;
+        pa.slices = c->d_fslices + w.fs0 + b0;
+        pa.rbsp_len = c->d_rbsp_len + w.fs0 + b0;
+        pa.n_slices = w.plv_end[j] - b0;
+        pa.slice0 = b0;
+        pa.order = c->d_porder + w.fs0 + b0;
+        VTS_TRY(parse_full_launch(pa, sp));
+      }
     }
     HIP_TRY(hipEventRecord(E[1], sp));
     HIP_TRY(hipStreamWaitEvent(sd, E[1], 0));
