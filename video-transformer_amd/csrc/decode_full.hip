@@ -1071,13 +1071,14 @@ __device__ __forceinline__ int bs_dev(const MbRec *P, const MbRecB *P1, int bp, 
 }
 
 // one line of samples s[0..7] = p3 p2 p1 p0 q0 q1 q2 q3 (8.7.2.3 / 8.7.2.4)
-__device__ __forceinline__ void filt_luma(int (&s)[8], int bS, int iA, int alpha, int beta) {
+// tcs: the packed edge tables of indexA (DbkLut::at): tC0 of bS = (tcs >> 8 * bS) & 255
+__device__ __forceinline__ void filt_luma(int (&s)[8], int bS, uint32_t tcs, int alpha, int beta) {
   const int p0 = s[3], p1 = s[2], q0 = s[4], q1 = s[5];
   if (!(bS > 0 && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
   const int p2 = s[1], q2 = s[6];
   const int ap = abs(p2 - p0), aq = abs(q2 - q0);
   if (bS < 4) {
-    const int tc0 = kTc[iA][bS - 1];
+    const int tc0 = (tcs >> (8 * bS)) & 255;
     const int tc = tc0 + (ap < beta) + (aq < beta);
     const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
     s[3] = c255(p0 + delta);
@@ -1104,10 +1105,10 @@ __device__ __forceinline__ void filt_luma(int (&s)[8], int bS, int iA, int alpha
   }
 }
 // chroma line p1 p0 q0 q1
-__device__ __forceinline__ void filt_chroma(int &p1, int &p0, int &q0, int &q1, int bS, int iA, int alpha, int beta) {
+__device__ __forceinline__ void filt_chroma(int &p1, int &p0, int &q0, int &q1, int bS, uint32_t tcs, int alpha, int beta) {
   if (!(bS > 0 && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
   if (bS < 4) {
-    const int tc = kTc[iA][bS - 1] + 1;
+    const int tc = ((tcs >> (8 * bS)) & 255) + 1;
     const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
     const int np0 = c255(p0 + delta), nq0 = c255(q0 - delta);
     p0 = np0;
@@ -1124,15 +1125,33 @@ struct DbkTile {
   uint8_t c[10][20];  // chroma rows -2..7 x interleaved bytes -4..15
 };
 
-struct EdgeQ {  // alpha/beta/indexA for an edge between macroblocks of qp qpp, qpq
-  int iA, alpha, beta;
+// Table 8-16 / 8-17 and the chroma QP table (8-15) staged in LDS once per
+// workgroup: a per-lane index into __constant__ data is a vector memory load
+// on the wavefront's critical path, an LDS read is not
+struct DbkLut {
+  uint32_t at[52];  // alpha(indexA) | tC0(indexA, bS 1..3) << 8 * bS
+  uint8_t be[52];   // beta(indexB)
+  uint8_t qc[52];   // QPc(qPI)
 };
-__device__ __forceinline__ EdgeQ edge_q(int qpav, int fa, int fb) {
+__device__ __forceinline__ void dbk_lut_init(DbkLut &t) {
+  for (int i = threadIdx.x; i < 52; i += blockDim.x) {
+    t.at[i] = static_cast<uint32_t>(kAl[i]) | static_cast<uint32_t>(kTc[i][0]) << 8 |
+              static_cast<uint32_t>(kTc[i][1]) << 16 | static_cast<uint32_t>(kTc[i][2]) << 24;
+    t.be[i] = kBe[i];
+    t.qc[i] = full::qpc_of(i, 0);
+  }
+}
+__device__ __forceinline__ int dbk_qpc(const DbkLut &t, int qp, int off) { return t.qc[min(max(qp + off, 0), 51)]; }
+
+struct EdgeQ {  // alpha/beta/tC0 for an edge between macroblocks of qp qpp, qpq
+  uint32_t tcs;
+  int alpha, beta;
+};
+__device__ __forceinline__ EdgeQ edge_q(const DbkLut &t, int qpav, int fa, int fb) {
   EdgeQ e;
-  e.iA = min(max(qpav + fa, 0), 51);
-  const int iB = min(max(qpav + fb, 0), 51);
-  e.alpha = kAl[e.iA];
-  e.beta = kBe[iB];
+  e.tcs = t.at[min(max(qpav + fa, 0), 51)];
+  e.alpha = e.tcs & 255;
+  e.beta = t.be[min(max(qpav + fb, 0), 51)];
   return e;
 }
 
@@ -1221,6 +1240,7 @@ __device__ __forceinline__ DbkInfo dbk_load(const DbkInfo *p) {
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a) {
   __shared__ DbkTile tiles[kDbkWaves * 2];
   __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
+  __shared__ DbkLut lut;
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
   const int slot = a.frames[blockIdx.x].x;
   const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
@@ -1228,6 +1248,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
   uint8_t *UV = Y + a.uv_off;
   const int pitch = a.pitch;
   for (int i = threadIdx.x; i < mbh; i += kDbkThreads) prog[i] = 0;
+  dbk_lut_init(lut);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int half = lane >> 5, l = lane & 31;
@@ -1286,12 +1307,12 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
             for (int e = 0; e < 4; ++e) {
               const int bS = dbk_bs(D, 0, e, seg);
               if (!bS) continue;
-              const EdgeQ eq = edge_q(e ? qpq : (qpl + qpq + 1) >> 1, D.fa, D.fb);
+              const EdgeQ eq = edge_q(lut, e ? qpq : (qpl + qpq + 1) >> 1, D.fa, D.fb);
               if (!eq.alpha || !eq.beta) continue;
               int s[8];
 #pragma unroll
               for (int i = 0; i < 8; ++i) s[i] = r[4 * e + i];
-              filt_luma(s, bS, eq.iA, eq.alpha, eq.beta);
+              filt_luma(s, bS, eq.tcs, eq.alpha, eq.beta);
 #pragma unroll
               for (int i = 0; i < 8; ++i) r[4 * e + i] = s[i];
             }
@@ -1305,10 +1326,10 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
 #pragma unroll
               for (int pl = 0; pl < 2; ++pl) {
                 const int off = pl ? a.P.cqp_off2 : a.P.cqp_off;
-                const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, D.fa, D.fb);
+                const EdgeQ eq = edge_q(lut, (dbk_qpc(lut, qpp, off) + dbk_qpc(lut, qpq, off) + 1) >> 1, D.fa, D.fb);
                 if (!eq.alpha || !eq.beta) continue;
                 const int c0 = 4 + 2 * (2 * e) + pl;  // q0 of chroma col 2e (luma edge e)
-                filt_chroma(r[c0 - 4], r[c0 - 2], r[c0], r[c0 + 2], bS, eq.iA, eq.alpha, eq.beta);
+                filt_chroma(r[c0 - 4], r[c0 - 2], r[c0], r[c0 + 2], bS, eq.tcs, eq.alpha, eq.beta);
               }
             }
           }
@@ -1330,12 +1351,12 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
           for (int e = 0; e < 4; ++e) {
             const int bS = dbk_bs(D, 1, e, seg);
             if (!bS) continue;
-            const EdgeQ eq = edge_q(e ? qpq : (qpt + qpq + 1) >> 1, D.fa, D.fb);
+            const EdgeQ eq = edge_q(lut, e ? qpq : (qpt + qpq + 1) >> 1, D.fa, D.fb);
             if (!eq.alpha || !eq.beta) continue;
             int s[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) s[i] = r[4 * e + i];
-            filt_luma(s, bS, eq.iA, eq.alpha, eq.beta);
+            filt_luma(s, bS, eq.tcs, eq.alpha, eq.beta);
 #pragma unroll
             for (int i = 0; i < 8; ++i) r[4 * e + i] = s[i];
           }
@@ -1352,10 +1373,10 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
             const int bS = dbk_bs(D, 1, e, seg);
             if (!bS) continue;
             const int qpp = e ? qpq : qpt;
-            const EdgeQ eq = edge_q((full::qpc_of(qpp, off) + full::qpc_of(qpq, off) + 1) >> 1, D.fa, D.fb);
+            const EdgeQ eq = edge_q(lut, (dbk_qpc(lut, qpp, off) + dbk_qpc(lut, qpq, off) + 1) >> 1, D.fa, D.fb);
             if (!eq.alpha || !eq.beta) continue;
             const int q0 = 2 + 2 * e;  // chroma row 2e
-            filt_chroma(r[q0 - 2], r[q0 - 1], r[q0], r[q0 + 1], bS, eq.iA, eq.alpha, eq.beta);
+            filt_chroma(r[q0 - 2], r[q0 - 1], r[q0], r[q0 + 1], bS, eq.tcs, eq.alpha, eq.beta);
           }
 #pragma unroll
           for (int i = 1; i < 10; ++i) t.c[i][4 + j] = static_cast<uint8_t>(r[i]);

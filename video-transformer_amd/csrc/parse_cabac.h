@@ -12,7 +12,7 @@
 // neighbour facts CABAC's context selection needs come through the CAVLC
 // parser's LDS neighbour copies: coded_block_flag bits in the (CAVLC-only)
 // nzc bytes, clamped |mvd| of inter macroblocks' bottom rows in their i4
-// bytes, the previous macroblock's right-column |mvd| in FullScratch.mvdl.
+// bytes, the neighbourhood's |mvd| in FullScratch.mvx.
 #pragma once
 #include <cstdint>
 #include <type_traits>
@@ -237,27 +237,98 @@ struct CabacParser : Parser {
   }
   // Min(|mvd_lX|, 33) at luma (xN, yN) of the current macroblock's
   // neighbourhood (skipped, intra and direct blocks carry 0)
+  // (xN, yN in -1..15: A and B neighbours only; mvd_border filled the edges)
   VTS_HD VTS_INLINE int mvd_at(int addr, int xN, int yN, int comp, int l = 0) const {
-    int xw = 0, yw = 0;
-    const int n = nb_mb(addr, xN, yN, 16, &xw, &yw);
-    if (n == -1) return 0;
-    if (n == -2) return l ? sc->mvdc1[(yw / 4) * 4 + xw / 4][comp] : sc->mvdc[(yw / 4) * 4 + xw / 4][comp];
-    const MbRec &m = rec(n);
-    if (m.type != kMbInter) return 0;
-    if (n == cur_addr - 1) return l ? sc->mvdl1[yw / 4][comp] : sc->mvdl[yw / 4][comp];
-    return l ? rec1(n).mvd1[(xw / 4) * 2 + comp] : m.i4[(xw / 4) * 2 + comp];  // the row above: bottom-row values
+    return sc->mvx[l][(yN >> 2) + 1][(xN >> 2) + 1][comp];
+  }
+  // a new macroblock's mvx: the left column takes the previous macroblock's
+  // right column (when it is the left neighbour A), the top row the bottom-row
+  // |mvd| the macroblock above kept in its record (inter only), the inside 0;
+  // one cell per lane (every read is issued before any write)
+  VTS_HD VTS_INLINE void mvd_border(int A, int B) {
+    const bool top_inter = B != -1 && rec(B).type == kMbInter;
+    const MbRec *tb = top_inter ? &rec(B) : nullptr;
+    const MbRecB *tb1 = top_inter && bframes ? &rec1(B) : nullptr;
+#if defined(__HIP_DEVICE_COMPILE__)
+    VTS_LANES(50, i) {
+      const int l = i / 25, r = (i % 25) / 5, c = i % 5;
+      uint8_t v0 = 0, v1 = 0;
+      if (r > 0 && c == 0) {
+        if (A != -1) {
+          v0 = sc->mvx[l][r][4][0];
+          v1 = sc->mvx[l][r][4][1];
+        }
+      } else if (r == 0 && c > 0 && tb) {
+        const uint8_t *src = l ? (tb1 ? tb1->mvd1 : nullptr) : tb->i4;
+        if (src) {
+          v0 = src[2 * (c - 1)];
+          v1 = src[2 * (c - 1) + 1];
+        }
+      }
+      asm volatile("" ::: "memory");  // every lane's read before any lane's write
+      sc->mvx[l][r][c][0] = v0;
+      sc->mvx[l][r][c][1] = v1;
+    }
+#else
+    // host: the lanes' reads all precede their writes on the device; serially,
+    // compute the cells first
+    uint8_t nv[2][5][5][2] = {};
+    for (int l = 0; l < 2; ++l)
+      for (int r = 1; r < 5; ++r)
+        if (A != -1) {
+          nv[l][r][0][0] = sc->mvx[l][r][4][0];
+          nv[l][r][0][1] = sc->mvx[l][r][4][1];
+        }
+    if (tb)
+      for (int c = 1; c < 5; ++c) {
+        nv[0][0][c][0] = tb->i4[2 * (c - 1)];
+        nv[0][0][c][1] = tb->i4[2 * (c - 1) + 1];
+        if (tb1) {
+          nv[1][0][c][0] = tb1->mvd1[2 * (c - 1)];
+          nv[1][0][c][1] = tb1->mvd1[2 * (c - 1) + 1];
+        }
+      }
+    for (int l = 0; l < 2; ++l)
+      for (int r = 0; r < 5; ++r)
+        for (int c = 0; c < 5; ++c) {
+          sc->mvx[l][r][c][0] = nv[l][r][c][0];
+          sc->mvx[l][r][c][1] = nv[l][r][c][1];
+        }
+#endif
   }
   // condTermFlagN of ref_idx_lX (9.3.3.1.1.6): refIdxLX > 0 of an inter
   // neighbour that is neither skipped nor predicted in direct mode
+  // (xN, yN in -1..15, A and B neighbours: the left / top macroblocks' flags
+  // come from refb, which mvd_border filled)
   VTS_HD VTS_INLINE int ref_gt0_at(int addr, int xN, int yN, int l = 0) const {
-    int xw = 0, yw = 0;
-    const int n = nb_mb(addr, xN, yN, 16, &xw, &yw);
-    if (n == -1) return 0;
-    const MbRec &m = rec(n);
-    if (m.type != kMbInter) return 0;
-    const int p8 = (yw / 8) * 2 + xw / 8;
-    if (bframes && ((rec1(n).direct >> p8) & 1)) return 0;
-    return (l ? rec1(n).ref1[p8] : m.ref[p8]) > 0 ? 1 : 0;
+    if (xN < 0) return static_cast<int>((refb >> (8 * l + (yN >> 3))) & 1u);
+    if (yN < 0) return static_cast<int>((refb >> (8 * l + 4 + (xN >> 3))) & 1u);
+    const MbRec &m = cur();
+    const int p8 = (yN >> 3) * 2 + (xN >> 3);
+    if (bframes && ((cur1().direct >> p8) & 1)) return 0;
+    return (l ? cur1().ref1[p8] : m.ref[p8]) > 0 ? 1 : 0;
+  }
+  // refb bit 8 l + k: refIdxLX > 0 of the left neighbour's 8x8 row k (k 0, 1)
+  // and bit 8 l + 4 + k of the top neighbour's 8x8 column k (inter, neither
+  // skipped nor direct; 0 where unavailable)
+  uint32_t refb;
+  VTS_HD VTS_INLINE void ref_border(int A, int B) {
+    uint32_t f = 0;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int n = nb ? B : A;
+      if (n == -1 || rec(n).type != kMbInter) continue;
+      const MbRec &m = rec(n);
+      const MbRecB *m1 = bframes ? &rec1(n) : nullptr;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int p8 = nb ? 2 + k : 2 * k + 1;  // top: bottom 8x8 row; left: right 8x8 column
+        if (m1 && ((m1->direct >> p8) & 1)) continue;
+        f |= (m.ref[p8] > 0 ? 1u : 0u) << (4 * nb + k);
+        if (m1) f |= (m1->ref1[p8] > 0 ? 1u : 0u) << (8 + 4 * nb + k);
+      }
+    }
+    refb = f;
   }
   // Intra NxN mode predictor (8.3.1.1 / 8.3.2.1) of the block at (x0, y0)
   VTS_HD VTS_INLINE int mode_pred(int addr, int x0, int y0, bool is8) const {
@@ -437,11 +508,10 @@ struct CabacParser : Parser {
           sc->mvd[l][4 * k + q][1] = dy;
           const uint8_t ax = static_cast<uint8_t>(vts_min(dx < 0 ? -dx : dx, 33));
           const uint8_t ay = static_cast<uint8_t>(vts_min(dy < 0 ? -dy : dy, 33));
-          uint8_t(*mc)[2] = l ? sc->mvdc1 : sc->mvdc;
           const uint32_t bm = blk_mask(sx, sy, pw, ph);
           VTS_LANES(16, b) if ((bm >> b) & 1u) {
-            mc[b][0] = ax;
-            mc[b][1] = ay;
+            sc->mvx[l][1 + (b >> 2)][1 + (b & 3)][0] = ax;
+            sc->mvx[l][1 + (b >> 2)][1 + (b & 3)][1] = ay;
           }
         }
       }
@@ -542,10 +612,6 @@ struct CabacParser : Parser {
     int xw, yw;
     const int A = nb_mb(addr, -1, 0, 16, &xw, &yw), B = nb_mb(addr, 0, -1, 16, &xw, &yw);
     int itype, mb_type = 0;
-    VTS_LANES(32, i) {
-      if (i < 16) sc->mvdc[i][0] = sc->mvdc[i][1] = 0;
-      else if (bframes) sc->mvdc1[i - 16][0] = sc->mvdc1[i - 16][1] = 0;
-    }
     if (s->is_p == kSliceB) {
       const int t = b_type((A != -1 && !(rec1(A).direct & kDirect16) ? 1 : 0) +
                            (B != -1 && !(rec1(B).direct & kDirect16) ? 1 : 0));
@@ -690,8 +756,8 @@ struct CabacParser : Parser {
           const int rk = refs[k];
           VTS_LANES(16, b) if ((bm >> b) & 1u) {
             set_motion(b, rk, vx, vy);
-            sc->mvdc[b][0] = ax;
-            sc->mvdc[b][1] = ay;
+            sc->mvx[0][1 + (b >> 2)][1 + (b & 3)][0] = ax;
+            sc->mvx[0][1 + (b >> 2)][1 + (b & 3)][1] = ay;
           }
           done |= bm;
         }
@@ -894,22 +960,14 @@ struct CabacParser : Parser {
     MbRec &m = cur();
     if (m.type == kMbInter)
       for (int x = 0; x < 4; ++x) {
-        m.i4[2 * x] = sc->mvdc[12 + x][0];
-        m.i4[2 * x + 1] = sc->mvdc[12 + x][1];
+        m.i4[2 * x] = sc->mvx[0][4][1 + x][0];
+        m.i4[2 * x + 1] = sc->mvx[0][4][1 + x][1];
       }
-    for (int y = 0; y < 4; ++y) {
-      sc->mvdl[y][0] = sc->mvdc[y * 4 + 3][0];
-      sc->mvdl[y][1] = sc->mvdc[y * 4 + 3][1];
-    }
     if (bframes) {
       MbRecB &m1 = cur1();
       for (int x = 0; x < 4; ++x) {
-        m1.mvd1[2 * x] = sc->mvdc1[12 + x][0];
-        m1.mvd1[2 * x + 1] = sc->mvdc1[12 + x][1];
-      }
-      for (int y = 0; y < 4; ++y) {
-        sc->mvdl1[y][0] = sc->mvdc1[y * 4 + 3][0];
-        sc->mvdl1[y][1] = sc->mvdc1[y * 4 + 3][1];
+        m1.mvd1[2 * x] = sc->mvx[1][4][1 + x][0];
+        m1.mvd1[2 * x + 1] = sc->mvx[1][4][1 + x][1];
       }
     }
   }
@@ -964,7 +1022,6 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   p.cab_tables();
   p.cab_init(!s.is_p, s.qp);
   p.cab_start();
-  for (int i = 0; i < 4; ++i) sc->mvdl[i][0] = sc->mvdl[i][1] = sc->mvdl1[i][0] = sc->mvdl1[i][1] = 0;
   int addr = s.first_mb, qp = s.qp;
   for (;;) {
     if (addr >= nmb) {
@@ -978,6 +1035,9 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
     if (s.is_p) {
       int xw, yw;
       const int A = p.nb_mb(addr, -1, 0, 16, &xw, &yw), B = p.nb_mb(addr, 0, -1, 16, &xw, &yw);
+      p.mvd_border(A, B);
+      p.ref_border(A, B);
+      p.mv_border(addr);
       skip = p.dec((s.is_p == kSliceB ? 24 : 11) + (p.avail_not(A, kMbSkip) ? 1 : 0) +
                    (p.avail_not(B, kMbSkip) ? 1 : 0)) != 0;
     }
@@ -986,7 +1046,6 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
       VTS_PROF_P(p, 3);
       if (s.is_p == kSliceB) p.b_skip_body(addr, qp);
       else p.skip_body(addr, qp);
-      VTS_LANES(16, i) sc->mvdc[i][0] = sc->mvdc[i][1] = sc->mvdc1[i][0] = sc->mvdc1[i][1] = 0;
       p.prev_qpd = false;
     } else {
       ok = p.mb_cabac(addr, &qp);  // one inlined copy for every slice type

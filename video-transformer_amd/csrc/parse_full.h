@@ -362,9 +362,17 @@ struct FullScratch {
   MbRecB top1[3];             // ... of top[3]: bytes 0..31 and 112..127
   // CABAC (parse_cabac.h)
   alignas(16) int16_t blk8[64]; // 8x8 block being decoded (raster)
-  uint8_t mvdc[16][2];          // Min(|mvd|, 33) of the current macroblock's 4x4 blocks
-  uint8_t mvdl[4][2];           // ... of the previous macroblock's right column
-  uint8_t mvdc1[16][2], mvdl1[4][2];  // the same for list 1 (B slices)
+  // the motion around the current macroblock, per list, for 8.4.1.3's A / B
+  // / C / D (mv_border): entries 0..3 = the left neighbour's right column
+  // (rows 0..3), 4..7 = the top neighbour's bottom row, 8 = C (top-right),
+  // 9 = D (top-left); ref -2 = unavailable, -1 = intra / list unused
+  uint32_t nbmv[2][10];
+  int8_t nbref[2][10];
+  // Min(|mvd_lX|, 33) around the current macroblock, per list: [row][col]
+  // with row 0 = the bottom row of the macroblock above, col 0 = the right
+  // column of the one to the left (0 where unavailable / not inter), rows and
+  // cols 1..4 = the current macroblock's 4x4 blocks
+  uint8_t mvx[2][5][5][2];
 #ifdef VTS_EXP_PROF
   uint64_t pacc[8], pt;
   int32_t psec;
@@ -717,9 +725,66 @@ struct Parser {
     bool avail;
     int ref, x, y;
   };
+  // the neighbours' motion of a new macroblock (P / B slices), once: one
+  // entry (list, position) per lane
+  VTS_HD VTS_INLINE void mv_border(int addr) {
+    VTS_LANES(20, i) {
+      const int l = i / 10, e = i % 10;
+      const int xN = e < 4 ? -1 : (e < 8 ? 4 * (e - 4) : (e == 8 ? 16 : -1)), yN = e < 4 ? 4 * e : -1;
+      int xw = 0, yw = 0;
+      const int n = nb_mb(addr, xN, yN, 16, &xw, &yw);
+      int8_t r = -2;
+      uint32_t mv = 0;
+      if (n != -1) {
+        const MbRec &m = rec(n);
+        r = -1;
+        if (m.type == kMbInter || m.type == kMbSkip) {
+          const int b = (yw / 4) * 4 + xw / 4, p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+          if (l) {
+            const MbRecB &m1 = rec1(n);
+            r = m1.ref1[p8];
+            mv = static_cast<uint16_t>(m1.mv1[b][0]) | (static_cast<uint32_t>(static_cast<uint16_t>(m1.mv1[b][1])) << 16);
+          } else {
+            r = m.ref[p8];
+            mv = static_cast<uint16_t>(m.mv[b][0]) | (static_cast<uint32_t>(static_cast<uint16_t>(m.mv[b][1])) << 16);
+          }
+        }
+      }
+      sc->nbref[l][e] = r;
+      sc->nbmv[l][e] = mv;
+    }
+  }
   // list l's motion of the neighbouring 4x4 block (ref -1: unavailable, intra
-  // or list l unused, with a zero vector)
+  // or list l unused, with a zero vector); outside the macroblock from
+  // mv_border's entries
   VTS_HD VTS_INLINE Mv nb_mv(int cur, int xN, int yN, uint32_t done, int l = 0) const {
+    if (xN >= 0 && xN < 16 && yN >= 0) {  // inside: blocks already decoded
+      Mv r{false, -1, 0, 0};
+      const int b = (yN >> 2) * 4 + (xN >> 2);
+      if (yN > 15 || !((done >> b) & 1u)) return r;
+      r.avail = true;
+      const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+      if (l) {
+        const MbRecB &m1 = sc->mb1[cs];
+        r.ref = m1.ref1[p8];
+        r.x = m1.mv1[b][0];
+        r.y = m1.mv1[b][1];
+      } else {
+        const MbRec &m = sc->mb[cs];
+        r.ref = m.ref[p8];
+        r.x = m.mv[b][0];
+        r.y = m.mv[b][1];
+      }
+      return r;
+    }
+    if (yN >= 0 && xN >= 16) return Mv{false, -1, 0, 0};
+    const int e = yN < 0 ? (xN < 0 ? 9 : (xN < 16 ? 4 + (xN >> 2) : 8)) : (yN >> 2);
+    const int ref = sc->nbref[l][e];
+    if (ref == -2) return Mv{false, -1, 0, 0};
+    const uint32_t mv = sc->nbmv[l][e];
+    return Mv{true, ref, static_cast<int16_t>(mv & 0xffff), static_cast<int16_t>(mv >> 16)};
+  }
+  VTS_HD VTS_INLINE Mv nb_mv_generic(int cur, int xN, int yN, uint32_t done, int l = 0) const {
     Mv r{false, -1, 0, 0};
     int xw, yw;
     const int n = nb_mb(cur, xN, yN, 16, &xw, &yw);
@@ -942,6 +1007,7 @@ struct Parser {
 
   VTS_HD VTS_INLINE void skip_mb(int addr, int qp) {
     begin_mb(addr);
+    mv_border(addr);
     if (s->is_p == kSliceB) b_skip_body(addr, qp);
     else skip_body(addr, qp);
   }
@@ -1093,6 +1159,7 @@ struct Parser {
   // macroblock_layer(); returns false to stop the slice
   VTS_HD VTS_INLINE bool mb_layer(int addr, int *qp) {
     begin_mb(addr);
+    if (s->is_p) mv_border(addr);
     MbRec &m = cur();
     const int mb_type = static_cast<int>(br.ue());
     const int intra0 = s->is_p == kSliceB ? 23 : (s->is_p ? 5 : 0);  // Tables 7-11, 7-13, 7-14
