@@ -1253,30 +1253,38 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int half = lane >> 5, l = lane & 31;
   const bool lrow = l < 24, luma = l < 16;
-  const int row = luma ? l : l - 16;  // V phase: luma row l / chroma row l - 16
+  // V phase: luma row l / chroma row l - 16 (lanes 24..31: chroma row 7,
+  // addressed only by the clamped prefetch)
+  const int row = luma ? l : min(l - 16, 7);
+  const int ia = min(max(l - 24, 0), 5);  // rows-above lane: luma rows -4..-1, chroma rows -2..-1
   DbkTile &t = tiles[wave * 2 + half];
   const int npairs = (mbh + 1) >> 1;
   for (int p = wave; p < npairs; p += kDbkWaves) {
     const int y = 2 * p + half;
     const bool row_ok = y < mbh;
-    const int64_t yrow = static_cast<int64_t>(y * 16) * pitch, crow = static_cast<int64_t>(y * 8) * pitch;
+    // every load below is unconditional from a clamped address (its value is
+    // used only where the unclamped one was valid), so the compiler keeps it
+    // in flight across the iteration instead of waiting inside a branch
+    const int ya = row_ok ? y : mbh - 1;
+    const int64_t yrow = static_cast<int64_t>(ya * 16) * pitch, crow = static_cast<int64_t>(ya * 8) * pitch;
     uint8_t *const rowp = (luma ? Y + yrow : UV + crow) + static_cast<int64_t>(row) * pitch;
+    const DbkInfo *const drow = fdbk + ya * mbw;
+    const uint8_t *const abovep = y > 0 ? (ia < 4 ? Y + yrow + static_cast<int64_t>(ia - 4) * pitch
+                                                  : UV + crow + static_cast<int64_t>(ia - 6) * pitch)
+                                        : Y;
     uint32_t left = 0;  // carried cols 12..15 of the previous macroblock (this lane's row)
     // the macroblock of the next iteration: descriptor and this lane's row, loaded one iteration ahead
-    uint4 npx = make_uint4(0, 0, 0, 0);
-    DbkInfo nd{};
-    if (row_ok && half == 0) {
-      nd = dbk_load(fdbk + y * mbw);
-      if (lrow) npx = *reinterpret_cast<const uint4 *>(rowp);
-    }
+    DbkInfo nd = dbk_load(drow);
+    uint4 npx = *reinterpret_cast<const uint4 *>(rowp);
     for (int it = 0; it < mbw + 2; ++it) {
       const int x = it - 2 * half;
       const bool act = row_ok && x >= 0 && x < mbw;
       const DbkInfo D = nd;
       const uint4 q4 = npx;
-      if (row_ok && x + 1 >= 0 && x + 1 < mbw) {
-        nd = dbk_load(fdbk + y * mbw + x + 1);
-        if (lrow) npx = *reinterpret_cast<const uint4 *>(rowp + (x + 1) * 16);
+      {
+        const int xn = min(max(x + 1, 0), mbw - 1);
+        nd = dbk_load(drow + xn);
+        npx = *reinterpret_cast<const uint4 *>(rowp + xn * 16);
       }
       // the upper row of the pair waits for the row above (another wave)
       if (half == 0 && act && y > 0) {
@@ -1288,12 +1296,9 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
       const bool on = act && !((D.qp >> 24) & 1);  // disable_deblocking_filter_idc != 1
       const int qpq = D.qp & 255, qpl = (D.qp >> 8) & 255, qpt = (D.qp >> 16) & 255;
       const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
-      // rows above (final: the row above is two macroblocks ahead)
-      if (act && l >= 24 && l < 30 && y > 0) {
-        const int i = l - 24;
-        if (i < 4) *reinterpret_cast<uint4 *>(&t.y[i][4]) = *reinterpret_cast<const uint4 *>(Y + ybase + static_cast<int64_t>(i - 4) * pitch);
-        else *reinterpret_cast<uint4 *>(&t.c[i - 4][4]) = *reinterpret_cast<const uint4 *>(UV + cbase + static_cast<int64_t>(i - 6) * pitch);
-      }
+      // rows above (final: the row above is two macroblocks ahead), loaded
+      // here and stored to the tile after the vertical edges
+      const uint4 above = *reinterpret_cast<const uint4 *>(abovep + min(max(x, 0), mbw - 1) * 16);
       // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
       if (act && lrow) {
         const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
@@ -1339,6 +1344,8 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
         for (int i = 0; i < 5; ++i)
           *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
       }
+      if (act && l >= 24 && l < 30 && y > 0)
+        *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = above;
       lane_sync();
       // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved chroma column l - 16
       if (on) {
