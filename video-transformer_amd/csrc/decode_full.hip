@@ -570,7 +570,10 @@ __device__ __forceinline__ void lane_sync() {
 }
 
 // one intra-predicted macroblock with 16 lanes (lane = raster 4x4 block b)
-__device__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraTile &t) {
+// (inlined at its one call site: a non-inlined call takes the kernel
+// arguments' address, which copies them to scratch and turns every field read
+// into a scratch load)
+__device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraTile &t) {
   const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
   const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
   const MbRec *rec = frecs + mb;
@@ -1005,7 +1008,8 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   __syncthreads();
   const int maxl = s_max;
   const int ms = tid >> 4, b = tid & 15;
-  if (maxl < kIntraLevels) {
+  const bool bucketed = maxl < kIntraLevels;
+  if (bucketed) {
     // the picture's intra macroblocks bucketed by level once (a counting
     // sort in LDS), then the levels in order: an all-intra picture has
     // ~mbw + 2 mbh levels, and a scan of every level per level cost more
@@ -1027,21 +1031,22 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
       if (v != kNoLevel) s_list[atomicAdd(&s_fill[v], 1)] = static_cast<uint16_t>(i);
     }
     __syncthreads();
-    for (int l = 0; l <= maxl; ++l) {
-      const int j0 = s_lvl[l], j1 = s_lvl[l + 1];
-      for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms]);
-      __syncthreads();
-    }
-    return;
   }
   for (int l = 0; l <= maxl; ++l) {
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    for (int i = tid; i < nmb; i += kIntraThreads)
-      if (lv[i] == l) s_list[atomicAdd(&s_cnt, 1)] = static_cast<uint16_t>(i);
-    __syncthreads();
-    const int n = s_cnt;
-    for (int j = ms; j < n; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms]);
+    int j0, j1;
+    if (bucketed) {
+      j0 = s_lvl[l];
+      j1 = s_lvl[l + 1];
+    } else {  // more levels than buckets: this level's macroblocks by a scan
+      if (tid == 0) s_cnt = 0;
+      __syncthreads();
+      for (int i = tid; i < nmb; i += kIntraThreads)
+        if (lv[i] == l) s_list[atomicAdd(&s_cnt, 1)] = static_cast<uint16_t>(i);
+      __syncthreads();
+      j0 = 0;
+      j1 = s_cnt;
+    }
+    for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms]);
     __syncthreads();
   }
 }
@@ -1160,22 +1165,25 @@ __device__ __forceinline__ int dbk_bs(const DbkInfo &d, int dir, int e, int seg)
   return (d.bs[dir * 2 + (e >> 1)] >> (((e & 1) * 4 + seg) * 4)) & 15;
 }
 
-// grid (ceil(nmb / 256), pictures of the level): one lane per macroblock
-// derives every boundary strength of its edges (8.7.2.1) and the QPs, so the
-// wavefront below reads one 32-byte descriptor per macroblock
+// grid (ceil(nmb / 16), pictures): 16 lanes per macroblock, lane = raster
+// 4x4 block b, which derives the bS of the vertical edge on its left and of
+// the horizontal edge above it (8.7.2.1); the macroblock's 32 nibbles meet in
+// an OR butterfly over its 16 lanes, so the wavefront below reads one 32-byte
+// descriptor per macroblock.  (A lane per macroblock walking all 32 edges
+// made every load a strided 4-byte gather.)
 __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
   const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
   const int slot = a.frames[blockIdx.y].x;
-  const int mb = blockIdx.x * 256 + threadIdx.x;
-  if (mb >= nmb) return;
-  const MbRec *Q = a.recs + static_cast<int64_t>(slot) * nmb + mb;
-  const MbRecB *Q1 = a.P.bframes ? a.recs1 + static_cast<int64_t>(slot) * nmb + mb : nullptr;
+  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4), b = threadIdx.x & 15;
+  const bool ok = mb < nmb;
+  const int mbc = ok ? mb : nmb - 1;  // tail lanes: a valid macroblock, result unused (the butterfly needs them)
+  const MbRec *Q = a.recs + static_cast<int64_t>(slot) * nmb + mbc;
+  const MbRecB *Q1 = a.P.bframes ? a.recs1 + static_cast<int64_t>(slot) * nmb + mbc : nullptr;
   const MbHdr hq = load_hdr(Q);
   const FullSlice &sd = a.slices[hq.slice];
-  const int x = mb % mbw, y = mb / mbw;
+  const int x = mbc % mbw, y = mbc / mbw, bx = b & 3, by = b >> 2;
   const int idc = sd.dbk_idc, tq = hq.type;
-  DbkInfo d;
-  d.bs[0] = d.bs[1] = d.bs[2] = d.bs[3] = 0;
+  uint32_t w[4] = {0, 0, 0, 0};
   int qpl = 0, qpt = 0;
   if (idc != 1) {
     const MbRec *PL = Q - 1, *PT = Q - mbw;
@@ -1195,31 +1203,31 @@ __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
     }
     const bool t8 = (hq.modes & kModeT8) != 0;
 #pragma unroll
-    for (int dir = 0; dir < 2; ++dir)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (e == 0 && !(dir ? ft : fl)) continue;
-        if (t8 && (e & 1)) continue;  // 8x8 transform: no 4-sample internal luma edges (chroma uses e = 0, 2)
-        const MbRec *Pm = e ? Q : (dir ? PT : PL);
-        const MbRecB *Pm1 = Q1 ? Q1 - (e ? 0 : (dir ? mbw : 1)) : nullptr;
-        const int tp = e ? tq : (dir ? tt : tl);
-#pragma unroll
-        for (int seg = 0; seg < 4; ++seg) {
-          const int bq = dir ? e * 4 + seg : seg * 4 + e;
-          const int bp = dir ? (e ? bq - 4 : 12 + seg) : (e ? bq - 1 : seg * 4 + 3);
-          const int bS = bs_dev(Pm, Pm1, bp, Q, Q1, bq, tp, tq, e == 0);
-          d.bs[dir * 2 + (e >> 1)] |= static_cast<uint32_t>(bS) << (((e & 1) * 4 + seg) * 4);
-        }
-      }
+    for (int dir = 0; dir < 2; ++dir) {
+      const int e = dir ? by : bx, seg = dir ? bx : by;
+      if (e == 0 && !(dir ? ft : fl)) continue;
+      if (t8 && (e & 1)) continue;  // 8x8 transform: no 4-sample internal luma edges (chroma uses e = 0, 2)
+      const MbRec *Pm = e ? Q : (dir ? PT : PL);
+      const MbRecB *Pm1 = Q1 ? Q1 - (e ? 0 : (dir ? mbw : 1)) : nullptr;
+      const int tp = e ? tq : (dir ? tt : tl);
+      const int bp = dir ? (e ? b - 4 : 12 + seg) : (e ? b - 1 : seg * 4 + 3);
+      const int bS = bs_dev(Pm, Pm1, bp, Q, Q1, b, tp, tq, e == 0);
+      w[dir * 2 + (e >> 1)] |= static_cast<uint32_t>(bS) << (((e & 1) * 4 + seg) * 4);
+    }
   }
-  d.qp = static_cast<uint32_t>(tq == kMbPcm ? 0 : hq.qp) | (static_cast<uint32_t>(qpl) << 8) |
-         (static_cast<uint32_t>(qpt) << 16) | (idc == 1 ? 1u << 24 : 0u);
-  d.fa = sd.dbk_a;
-  d.fb = sd.dbk_b;
-  d._pad = 0;
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(w[i]), m, 16));
+  if (!ok || b > 1) return;
   DbkInfo *o = a.dbk + static_cast<int64_t>(slot) * nmb + mb;
-  reinterpret_cast<uint4 *>(o)[0] = make_uint4(d.bs[0], d.bs[1], d.bs[2], d.bs[3]);
-  reinterpret_cast<uint4 *>(o)[1] = make_uint4(d.qp, static_cast<uint32_t>(d.fa), static_cast<uint32_t>(d.fb), 0u);
+  if (b == 0) {
+    reinterpret_cast<uint4 *>(o)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    const uint32_t qp = static_cast<uint32_t>(tq == kMbPcm ? 0 : hq.qp) | (static_cast<uint32_t>(qpl) << 8) |
+                        (static_cast<uint32_t>(qpt) << 16) | (idc == 1 ? 1u << 24 : 0u);
+    reinterpret_cast<uint4 *>(o)[1] = make_uint4(qp, static_cast<uint32_t>(sd.dbk_a), static_cast<uint32_t>(sd.dbk_b), 0u);
+  }
 }
 
 __device__ __forceinline__ DbkInfo dbk_load(const DbkInfo *p) {
@@ -1447,7 +1455,7 @@ int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
   if (n_frames > 65535) return fail(VTS_E_UNSUPPORTED, "more than 65535 pictures in one bS launch");
   const int nmb = a.P.mb_width * a.P.mb_height;
-  hipLaunchKernelGGL(h264_bs_full, dim3((nmb + 255) / 256, n_frames), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(h264_bs_full, dim3((nmb + 15) / 16, n_frames), dim3(256), 0, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_bs_full launch: %s", hipGetErrorString(e));
   return VTS_OK;
