@@ -33,9 +33,11 @@ VTS_CTAB int8_t kCabInitP[VTS_CABAC_NCTX][2] = VTS_CABAC_INIT_P0_DATA;
 #undef VTS_CTAB
 
 // The engine's tables as 64 dwords each, loaded into lane tables (LaneTab) at
-// slice start: rangeTabLPS[pStateIdx][0..3] in bytes 0..3; transIdxLPS; the
-// 8x8 block's significant / last ctxIdxInc (Table 9-43, frame) and zig-zag
-// position of coefficient i in bytes 0 / 1 / 2
+// slice start: rangeTabLPS[pStateIdx][0..3] in bytes 0..3; the next state
+// byte (pStateIdx << 1 | valMPS-switch, to be XORed with valMPS) after an LPS
+// (transIdxLPS, switching valMPS at state 0) in byte 0 and after an MPS
+// (transIdxMPS) in byte 1; the 8x8 block's significant / last ctxIdxInc
+// (Table 9-43, frame) and zig-zag position of coefficient i in bytes 0 / 1 / 2
 struct CabLanes {
   uint32_t lps[64], trans[64], s8[64];
 };
@@ -48,7 +50,7 @@ constexpr CabLanes make_cab_lanes() {
   const uint8_t zz[64] = VTS_ZZ8_DATA;
   for (int i = 0; i < 64; ++i) {
     t.lps[i] = r[i][0] | (uint32_t(r[i][1]) << 8) | (uint32_t(r[i][2]) << 16) | (uint32_t(r[i][3]) << 24);
-    t.trans[i] = tr[i];
+    t.trans[i] = (uint32_t(tr[i]) << 1) | (i == 0 ? 1u : 0u) | (uint32_t(i < 62 ? i + 1 : 62) << 9);
     t.s8[i] = (i < 63 ? sig[i] | (uint32_t(last[i]) << 8) : 0u) | (uint32_t(zz[i]) << 16);
   }
   return t;
@@ -131,12 +133,12 @@ struct CabacParser : Parser {
     const uint32_t word = hi ? wb : wa;
     const uint32_t s = (word >> sh) & 127u, ps = s >> 1, mps = s & 1u;
     const uint32_t lpsr = (lps.get(ps) >> ((range >> 3) & 24u)) & 255u;
+    const uint32_t tw = trn.get(ps);  // read on both paths: no branch
     range -= lpsr;
     const uint32_t rs = range << 23;
     const bool lpsb = val >= rs;
     const uint32_t bin = mps ^ (lpsb ? 1u : 0u);
-    const uint32_t ns = lpsb ? (trn.get(ps) << 1) | (ps == 0 ? (mps ^ 1u) : mps)
-                             : ((ps < 62 ? ps + 1 : 62) << 1) | mps;
+    const uint32_t ns = ((tw >> (lpsb ? 0u : 8u)) & 127u) ^ mps;
     val -= lpsb ? rs : 0u;
     range = lpsb ? lpsr : range;
     const uint32_t nw = (word & ~(255u << sh)) | (ns << sh);
