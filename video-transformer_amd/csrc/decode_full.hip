@@ -582,40 +582,49 @@ __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int m
   const int pitch = a.pitch;
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
   uint8_t *UV = Y + a.uv_off;
-  auto nb_ok = [&](int n) -> bool {
-    if (n < 0) return false;
-    const uint4 u = reinterpret_cast<const uint4 *>(frecs + n)[0];
-    if (u.x != a.epoch || u.y != h.slice) return false;
-    if (a.P.cip) {
-      const int ty = reinterpret_cast<const uint32_t *>(frecs + n)[4] & 255;
-      if (ty == kMbInter || ty == kMbSkip) return false;
-    }
+  // Every load of the neighbourhood is issued at once, unconditionally, from
+  // clamped addresses (a neighbour's header, this lane's border samples), and
+  // the availability decides afterwards which values count: conditional
+  // loads each waited for the one before (header -> availability -> samples)
+  const int nA = mx > 0 ? mb - 1 : mb, nB = my > 0 ? mb - mbw : mb;
+  const int nC = my > 0 && mx < mbw - 1 ? mb - mbw + 1 : mb, nD = mx > 0 && my > 0 ? mb - mbw - 1 : mb;
+  const uint2 hA = *reinterpret_cast<const uint2 *>(frecs + nA), hB = *reinterpret_cast<const uint2 *>(frecs + nB);
+  const uint2 hC = *reinterpret_cast<const uint2 *>(frecs + nC), hD = *reinterpret_cast<const uint2 *>(frecs + nD);
+  const uint32_t tA = reinterpret_cast<const uint32_t *>(frecs + nA)[4], tB = reinterpret_cast<const uint32_t *>(frecs + nB)[4];
+  const uint32_t tC = reinterpret_cast<const uint32_t *>(frecs + nC)[4], tD = reinterpret_cast<const uint32_t *>(frecs + nD)[4];
+  const int64_t yrow0 = static_cast<int64_t>(my * 16) * pitch + mx * 16;
+  const int64_t crow0 = static_cast<int64_t>(my * 8) * pitch + mx * 16;
+  // row -1 (b < 7: cols -4 + 4b), col -1 (row b), chroma col -1 (b < 8: row b), chroma row -1 (8 <= b < 13)
+  const int64_t up = my > 0 ? yrow0 - pitch : yrow0;
+  const uint32_t vTop = *reinterpret_cast<const uint32_t *>(Y + max(up - 4 + 4 * min(b, 6), static_cast<int64_t>(0)));
+  const uint8_t vLeft = Y[max(yrow0 + static_cast<int64_t>(b) * pitch - 1, static_cast<int64_t>(0))];
+  const uint32_t vCl = *reinterpret_cast<const uint32_t *>(UV + crow0 + static_cast<int64_t>(min(b, 7)) * pitch - 4);
+  const uint32_t vCt = *reinterpret_cast<const uint32_t *>(UV + crow0 - pitch - 4 + 4 * min(max(b - 8, 0), 4));
+  auto nb_ok = [&](bool exists, uint2 u, uint32_t ty) -> bool {
+    if (!exists || u.x != a.epoch || u.y != h.slice) return false;
+    if (a.P.cip && ((ty & 255) == kMbInter || (ty & 255) == kMbSkip)) return false;
     return true;
   };
-  const bool A = nb_ok(mx > 0 ? mb - 1 : -1);
-  const bool B = nb_ok(my > 0 ? mb - mbw : -1);
-  const bool C = nb_ok(my > 0 && mx < mbw - 1 ? mb - mbw + 1 : -1);
-  const bool D = nb_ok(mx > 0 && my > 0 ? mb - mbw - 1 : -1);
-  // borders into the tile
-  const int64_t yrow0 = static_cast<int64_t>(my * 16) * pitch + mx * 16;
-  // unavailable neighbours read as 0 (as the oracle; conforming streams never use them)
+  const bool A = nb_ok(mx > 0, hA, tA);
+  const bool B = nb_ok(my > 0, hB, tB);
+  const bool C = nb_ok(my > 0 && mx < mbw - 1, hC, tC);
+  const bool D = nb_ok(mx > 0 && my > 0, hD, tD);
+  // borders into the tile; unavailable neighbours read as 0 (as the oracle;
+  // conforming streams never use them)
   if (b < 7) {
     const bool need = b == 0 ? D : (b < 5 ? B : C);
-    uint32_t v = 0;
-    if (need) v = *reinterpret_cast<const uint32_t *>(Y + yrow0 - pitch - 4 + 4 * b);
-    *reinterpret_cast<uint32_t *>(&t.y[0][4 * b]) = v;
+    *reinterpret_cast<uint32_t *>(&t.y[0][4 * b]) = need ? vTop : 0u;
   }
-  t.y[1 + b][3] = A ? Y[yrow0 + static_cast<int64_t>(b) * pitch - 1] : 0;
-  const int64_t crow0 = static_cast<int64_t>(my * 8) * pitch + mx * 16;
+  t.y[1 + b][3] = A ? vLeft : 0;
   if (b < 8) {
-    const uint32_t v = A ? *reinterpret_cast<const uint32_t *>(UV + crow0 + static_cast<int64_t>(b) * pitch - 4) : 0u;
+    const uint32_t v = A ? vCl : 0u;
     t.cl[0][b] = (v >> 16) & 255;
     t.cl[1][b] = v >> 24;
   }
   if (b >= 8 && b < 13) {
     const int i = b - 8;  // dword i of chroma row -1, interleaved bytes -4 + 4i
     {
-      const uint32_t v = (i == 0 ? D : B) ? *reinterpret_cast<const uint32_t *>(UV + crow0 - pitch - 4 + 4 * i) : 0u;
+      const uint32_t v = (i == 0 ? D : B) ? vCt : 0u;
       if (i == 0) {
         t.ct[0][0] = (v >> 16) & 255;
         t.ct[1][0] = v >> 24;
