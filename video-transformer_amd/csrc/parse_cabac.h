@@ -65,6 +65,26 @@ VTS_HD VTS_INLINE int cbf_off(int cat) { return static_cast<int>((0x100C080400ul
 VTS_HD VTS_INLINE int sig_off(int cat) { return static_cast<int>((0x2F2C1D0F00ull >> (8 * cat)) & 255u); }
 VTS_HD VTS_INLINE int abs_off(int cat) { return static_cast<int>((0x271E140A00ull >> (8 * cat)) & 255u); }
 
+// The engine's codIRange / codIOffset live in VGPRs: an opaque move makes
+// them divergent, so their arithmetic issues on the vector ALUs (four per
+// compute unit) instead of the one scalar unit that every wave of the compute
+// unit shares, which the parser saturates; a decision's outcome, next state
+// and renormalisation shift come back to the scalar side by readfirstlane
+// (CABAC B parse -4 % same-box, profiles/r03_cabac_vgpr_engine_ab.txt;
+// VTS_EXP_SENGINE keeps the scalar engine)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(VTS_EXP_SENGINE)
+__device__ __forceinline__ uint32_t vts_in_vgpr(uint32_t x) {
+  uint32_t r;
+  asm("; engine state in a VGPR" : "=v"(r) : "0"(x));
+  return r;
+}
+#define VTS_EV(x) vts_in_vgpr(x)
+#define VTS_EU(x) static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x)))
+#else
+#define VTS_EV(x) (x)
+#define VTS_EU(x) (x)
+#endif
+
 struct CabacParser : Parser {
   // The engine (9.3.1.2, 9.3.3.2) with codIOffset scaled: val holds the 9-bit
   // codIOffset in bits 31..23 and the next `la` bitstream bits below it, so
@@ -85,8 +105,8 @@ struct CabacParser : Parser {
 
   // ---------------------------------------------- arithmetic decoder (9.3.3.2)
   VTS_HD VTS_INLINE void cab_start() {  // 9.3.1.2: codIOffset = read_bits(9)
-    range = 510;
-    val = br.bits(32);
+    range = VTS_EV(510u);
+    val = VTS_EV(br.bits(32));
     la = 23;
   }
   // bits the engine has consumed (9.3.1.2's 9 + every renormalisation shift)
@@ -138,7 +158,7 @@ struct CabacParser : Parser {
     const uint32_t rs = range << 23;
     const bool lpsb = val >= rs;
     const uint32_t bin = mps ^ (lpsb ? 1u : 0u);
-    const uint32_t ns = ((tw >> (lpsb ? 0u : 8u)) & 127u) ^ mps;
+    const uint32_t ns = VTS_EU(((tw >> (lpsb ? 0u : 8u)) & 127u) ^ mps);
     val -= lpsb ? rs : 0u;
     range = lpsb ? lpsr : range;
     const uint32_t nw = (word & ~(255u << sh)) | (ns << sh);
@@ -149,12 +169,12 @@ struct CabacParser : Parser {
       st[0].set(ln, hi ? wa : nw);
       st[1].set(ln, hi ? nw : wb);
     }
-    const int n = __builtin_clz(range) - 23;  // RenormD as one shift (0..6)
+    const int n = static_cast<int>(VTS_EU(__builtin_clz(range) - 23));  // RenormD as one shift (0..6)
     range <<= n;
     val <<= n;
     la -= n;
     cab_fill();
-    return bin;
+    return VTS_EU(bin);
   }
   VTS_HD VTS_INLINE uint32_t bypass() {  // DecodeBypass
     VTS_PARSE_TRACE(2);
@@ -166,7 +186,7 @@ struct CabacParser : Parser {
     --la;
     cab_fill();
     const uint32_t rs = range << 23;
-    if (top || val >= rs) {
+    if (VTS_EU((top || val >= rs) ? 1u : 0u)) {
       val -= rs;
       return 1;
     }
@@ -175,8 +195,8 @@ struct CabacParser : Parser {
   VTS_HD VTS_INLINE uint32_t term() {  // DecodeTerminate: 1 ends parsing, no renormalisation
     VTS_PARSE_TRACE(3);
     range -= 2;
-    if (val >= (range << 23)) return 1;
-    if (range < 256) {
+    if (VTS_EU(val >= (range << 23) ? 1u : 0u)) return 1;
+    if (VTS_EU(range < 256 ? 1u : 0u)) {
       range <<= 1;
       val <<= 1;
       --la;
