@@ -561,7 +561,42 @@ struct IntraTile {
   uint8_t cl[2][8];    // chroma col -1, rows 0..7
   uint8_t cout[8][16]; // reconstructed chroma rows, interleaved
   int16_t f8[25];      // Intra_8x8: filtered p'[-1,-1], p'[0..15,-1] (1..16), p'[-1,0..7] (17..24)
+  // Intra_4x4, per lane: the block's reference samples E (E[0..3] = p[-1,3..0],
+  // E[4] = p[-1,-1], E[5..12] = p[0..7,-1]) at 1..13 (0 and 14 repeat the
+  // ends), their 3-tap filter F(k) = (E[k-1] + 2E[k] + E[k+1] + 2) >> 2 at
+  // 16 + k, 2-tap mean A(k) = (E[k] + E[k+1] + 1) >> 1 at 32 + k, DC at 47
+  uint8_t pe[16][48];
 };
+// Every Intra_4x4 mode (8.3.1.2.1-9) reads each predicted sample as one entry
+// of IntraTile::pe: its offset for (mode, x, y), built by the formulas below
+// once per workgroup, so lanes whose blocks use different modes run one
+// instruction stream (a per-lane switch ran the modes' bodies one after another)
+__device__ __forceinline__ int intra4_off(int mode, int x, int y) {
+  switch (mode) {
+    case 0: return 1 + 5 + x;
+    case 1: return 1 + 3 - y;
+    case 2: return 47;
+    case 3: return 16 + 6 + x + y;
+    case 4: return 16 + 4 + x - y;
+    case 5: {
+      const int z = 2 * x - y;
+      if (z >= 0) return ((z & 1) ? 16 : 32) + 4 + x - (y >> 1);
+      return z == -1 ? 16 + 4 : 16 + 5 - y;
+    }
+    case 6: {
+      const int z = 2 * y - x;
+      if (z >= 0) return (z & 1) ? 16 + 4 - y + (x >> 1) : 32 + 3 - y + (x >> 1);
+      return z == -1 ? 16 + 4 : 16 + 3 + x;
+    }
+    case 7: return (y & 1) ? 16 + 6 + x + (y >> 1) : 32 + 5 + x + (y >> 1);
+    default: {
+      const int z = x + 2 * y;
+      if (z > 5) return 1;
+      if (z == 5) return 16;
+      return ((z & 1) ? 16 : 32) + 2 - y - (x >> 1);
+    }
+  }
+}
 
 __device__ __forceinline__ void lane_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -573,7 +608,8 @@ __device__ __forceinline__ void lane_sync() {
 // (inlined at its one call site: a non-inlined call takes the kernel
 // arguments' address, which copies them to scratch and turns every field read
 // into a scratch load)
-__device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraTile &t) {
+__device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraTile &t,
+                                         const uint8_t *s_off4) {
   const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
   const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
   const MbRec *rec = frecs + mb;
@@ -859,65 +895,42 @@ __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int m
         for (int x = 4; x < 8; ++x) T[1 + x] = tr ? t.y[ty][tx + x] : T[4];
 #pragma unroll
         for (int y = 0; y < 4; ++y) L[1 + y] = left ? t.y[ty + 1 + y][tx - 1] : 0;
-#define PT(x) T[1 + (x)]
-#define PL(y) L[1 + (y)]
+        int e[15];  // pe[0..14]
+        e[0] = e[1] = L[4];
+        e[2] = L[3];
+        e[3] = L[2];
+        e[4] = L[1];
+        e[5] = T[0];
+#pragma unroll
+        for (int x = 0; x < 8; ++x) e[6 + x] = T[1 + x];
+        e[14] = e[13];
+        int dc;
+        if (top && left) dc = (T[1] + T[2] + T[3] + T[4] + L[1] + L[2] + L[3] + L[4] + 4) >> 3;
+        else if (left) dc = (L[1] + L[2] + L[3] + L[4] + 2) >> 2;
+        else if (top) dc = (T[1] + T[2] + T[3] + T[4] + 2) >> 2;
+        else dc = 128;
+        int pv[48];
+#pragma unroll
+        for (int i = 0; i < 48; ++i) pv[i] = 0;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) pv[i] = e[i];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) pv[16 + k] = (e[k] + 2 * e[k + 1] + e[k + 2] + 2) >> 2;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) pv[32 + k] = (e[1 + k] + e[2 + k] + 1) >> 1;
+        pv[47] = dc;
+        uint8_t *pe = t.pe[b];
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+          *reinterpret_cast<uint32_t *>(pe + 4 * i) = pack4(pv[4 * i], pv[4 * i + 1], pv[4 * i + 2], pv[4 * i + 3]);
+        const uint32_t *offw = reinterpret_cast<const uint32_t *>(s_off4 + 16 * min(m4, 8));  // > 8: not a mode (as mode 8)
         int o[16];
 #pragma unroll
-        for (int y = 0; y < 4; ++y)
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t ow = offw[r];
 #pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            int v;
-            switch (m4) {
-              case 0: v = PT(x); break;
-              case 1: v = PL(y); break;
-              case 2:
-                if (top && left) v = (PT(0) + PT(1) + PT(2) + PT(3) + PL(0) + PL(1) + PL(2) + PL(3) + 4) >> 3;
-                else if (left) v = (PL(0) + PL(1) + PL(2) + PL(3) + 2) >> 2;
-                else if (top) v = (PT(0) + PT(1) + PT(2) + PT(3) + 2) >> 2;
-                else v = 128;
-                break;
-              case 3:
-                v = (x == 3 && y == 3) ? (PT(6) + 3 * PT(7) + 2) >> 2
-                                       : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
-                break;
-              case 4:
-                if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
-                else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
-                else v = (PT(0) + 2 * PT(-1) + PL(0) + 2) >> 2;
-                break;
-              case 5: {
-                const int z = 2 * x - y;
-                if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
-                else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
-                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
-                else v = (PL(y - 1) + 2 * PL(y - 2) + PL(y - 3) + 2) >> 2;
-                break;
-              }
-              case 6: {
-                const int z = 2 * y - x;
-                if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
-                else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
-                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
-                else v = (PT(x - 1) + 2 * PT(x - 2) + PT(x - 3) + 2) >> 2;
-                break;
-              }
-              case 7:
-                v = (y & 1) ? (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2
-                            : (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1;
-                break;
-              default: {
-                const int z = x + 2 * y;
-                if (z == 0 || z == 2 || z == 4) v = (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
-                else if (z == 1 || z == 3) v = (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
-                else if (z == 5) v = (PL(2) + 3 * PL(3) + 2) >> 2;
-                else v = PL(3);
-                break;
-              }
-            }
-            o[y * 4 + x] = c255(v + res[y * 4 + x]);
-          }
-#undef PT
-#undef PL
+          for (int x = 0; x < 4; ++x) o[r * 4 + x] = c255(pe[(ow >> (8 * x)) & 255] + res[r * 4 + x]);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t w4 = pack4(o[r * 4], o[r * 4 + 1], o[r * 4 + 2], o[r * 4 + 3]);
@@ -1002,11 +1015,13 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   __shared__ IntraTile tiles[kIntraSlots];
   __shared__ int s_max, s_cnt;
   __shared__ int s_lvl[kIntraLevels + 1], s_fill[kIntraLevels];
+  __shared__ __attribute__((aligned(4))) uint8_t s_off4[9 * 16];
   const int nmb = a.P.mb_width * a.P.mb_height;
   const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;
   if (tid == 0) s_max = -1;
+  if (tid < 9 * 16) s_off4[tid] = static_cast<uint8_t>(intra4_off(tid >> 4, tid & 3, (tid >> 2) & 3));
   __syncthreads();
   int m = -1;
   for (int i = tid; i < nmb; i += kIntraThreads) {
@@ -1055,7 +1070,7 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
       j0 = 0;
       j1 = s_cnt;
     }
-    for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms]);
+    for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4);
     __syncthreads();
   }
 }
