@@ -555,17 +555,20 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
 }
 
 // ------------------------------------------------------------ intra blocks
-struct IntraTile {
-  uint8_t y[17][28];   // luma rows -1..15 (index + 1) x cols -4..23 (index + 4)
-  uint8_t ct[2][9];    // chroma row -1, cols -1..7 (index + 1), per plane
-  uint8_t cl[2][8];    // chroma col -1, rows 0..7
+struct alignas(16) IntraTile {  // dword / 16-byte members first, so every wide LDS access is aligned
   uint8_t cout[8][16]; // reconstructed chroma rows, interleaved
-  int16_t f8[25];      // Intra_8x8: filtered p'[-1,-1], p'[0..15,-1] (1..16), p'[-1,0..7] (17..24)
+  // Intra_8x8: the filtered reference samples p' as E (E[0..7] = p'[-1,7..0],
+  // E[8] = p'[-1,-1], E[9..24] = p'[0..15,-1]) at 1..25 (0 and 26 repeat the
+  // ends), F(k) at 32 + k, A(k) at 64 + k (as pe below), DC at 88
+  uint8_t p8[96];
   // Intra_4x4, per lane: the block's reference samples E (E[0..3] = p[-1,3..0],
   // E[4] = p[-1,-1], E[5..12] = p[0..7,-1]) at 1..13 (0 and 14 repeat the
   // ends), their 3-tap filter F(k) = (E[k-1] + 2E[k] + E[k+1] + 2) >> 2 at
   // 16 + k, 2-tap mean A(k) = (E[k] + E[k+1] + 1) >> 1 at 32 + k, DC at 47
   uint8_t pe[16][48];
+  uint8_t y[17][28];   // luma rows -1..15 (index + 1) x cols -4..23 (index + 4)
+  uint8_t ct[2][9];    // chroma row -1, cols -1..7 (index + 1), per plane
+  uint8_t cl[2][8];    // chroma col -1, rows 0..7
 };
 // Every Intra_4x4 mode (8.3.1.2.1-9) reads each predicted sample as one entry
 // of IntraTile::pe: its offset for (mode, x, y), built by the formulas below
@@ -597,6 +600,33 @@ __device__ __forceinline__ int intra4_off(int mode, int x, int y) {
     }
   }
 }
+// the same for Intra_8x8 (8.3.2.2.2-10) into IntraTile::p8
+__device__ __forceinline__ int intra8_off(int mode, int x, int y) {
+  switch (mode) {
+    case 0: return 1 + 9 + x;
+    case 1: return 1 + 7 - y;
+    case 2: return 88;
+    case 3: return 32 + 10 + x + y;
+    case 4: return 32 + 8 + x - y;
+    case 5: {
+      const int z = 2 * x - y;
+      if (z >= 0) return ((z & 1) ? 32 : 64) + 8 + x - (y >> 1);
+      return z == -1 ? 32 + 8 : 32 + 9 + 2 * x - y;
+    }
+    case 6: {
+      const int z = 2 * y - x;
+      if (z >= 0) return (z & 1) ? 32 + 8 - y + (x >> 1) : 64 + 7 - y + (x >> 1);
+      return z == -1 ? 32 + 8 : 32 + 7 + x - 2 * y;
+    }
+    case 7: return (y & 1) ? 32 + 10 + x + (y >> 1) : 64 + 9 + x + (y >> 1);
+    default: {
+      const int z = x + 2 * y;
+      if (z > 13) return 1;
+      if (z == 13) return 32;
+      return ((z & 1) ? 32 : 64) + 6 - y - (x >> 1);
+    }
+  }
+}
 
 __device__ __forceinline__ void lane_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -609,7 +639,7 @@ __device__ __forceinline__ void lane_sync() {
 // arguments' address, which copies them to scratch and turns every field read
 // into a scratch load)
 __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraTile &t,
-                                         const uint8_t *s_off4) {
+                                         const uint8_t *s_off4, const uint8_t *s_off8) {
   const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
   const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
   const MbRec *rec = frecs + mb;
@@ -784,87 +814,52 @@ __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int m
           for (int y = 1; y < 7; ++y) L[y] = (P_[16 + y] + 2 * P_[17 + y] + P_[18 + y] + 2) >> 2;
           L[7] = (P_[23] + 3 * P_[24] + 2) >> 2;
         }
+        int e[27];
 #pragma unroll
-        for (int i = 0; i < 17; ++i) t.f8[i] = static_cast<int16_t>(T[i]);
+        for (int k = 0; k < 8; ++k) e[1 + k] = L[7 - k];
+        e[0] = e[1];
+        e[9] = T[0];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) t.f8[17 + i] = static_cast<int16_t>(L[i]);
+        for (int i = 0; i < 16; ++i) e[10 + i] = T[1 + i];
+        e[26] = e[25];
+        int st = 0, sl = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          st += T[1 + i];
+          sl += L[i];
+        }
+        int pv[96];
+#pragma unroll
+        for (int i = 0; i < 96; ++i) pv[i] = 0;
+#pragma unroll
+        for (int i = 0; i < 27; ++i) pv[i] = e[i];
+#pragma unroll
+        for (int k = 0; k < 25; ++k) pv[32 + k] = (e[k] + 2 * e[k + 1] + e[k + 2] + 2) >> 2;
+#pragma unroll
+        for (int k = 0; k < 24; ++k) pv[64 + k] = (e[1 + k] + e[2 + k] + 1) >> 1;
+        pv[88] = (top && left) ? (st + sl + 8) >> 4 : (left ? (sl + 4) >> 3 : (top ? (st + 4) >> 3 : 128));
+#pragma unroll
+        for (int i = 0; i < 24; ++i)
+          *reinterpret_cast<uint32_t *>(t.p8 + 4 * i) = pack4(pv[4 * i], pv[4 * i + 1], pv[4 * i + 2], pv[4 * i + 3]);
       }
       lane_sync();
       if (s == b8) {
-        const int16_t *T = t.f8, *L = t.f8 + 17;
         int res[16];
         if (lb >= 0) idct8_quarter(a.arena, lb, qp, qx, qy, a.P.scaled ? a.sct->ls8[0][qp % 6] : nullptr, res);
         else
 #pragma unroll
           for (int i = 0; i < 16; ++i) res[i] = 0;
-#define PT(x) static_cast<int>(T[1 + (x)])
-#define PL(y) static_cast<int>((y) < 0 ? T[0] : L[(y)])
-        int dc = 128;
-        if (m8 == 2) {
-          int st = 0, sl = 0;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            st += PT(i);
-            sl += PL(i);
-          }
-          dc = (top && left) ? (st + sl + 8) >> 4 : (left ? (sl + 4) >> 3 : (top ? (st + 4) >> 3 : 128));
-        }
+        const uint8_t *offs = s_off8 + 64 * min(m8, 8);  // > 8: not a mode (as mode 8)
 #pragma unroll
         for (int yy = 0; yy < 4; ++yy) {
+          const uint32_t ow = *reinterpret_cast<const uint32_t *>(offs + (qy * 4 + yy) * 8 + qx * 4);
           int o[4];
 #pragma unroll
-          for (int xx = 0; xx < 4; ++xx) {
-            const int x = qx * 4 + xx, y = qy * 4 + yy;
-            int v;
-            switch (m8) {
-              case 0: v = PT(x); break;
-              case 1: v = PL(y); break;
-              case 2: v = dc; break;
-              case 3:
-                v = (x == 7 && y == 7) ? (PT(14) + 3 * PT(15) + 2) >> 2 : (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
-                break;
-              case 4:
-                if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + PT(x - y) + 2) >> 2;
-                else if (x < y) v = (PL(y - x - 2) + 2 * PL(y - x - 1) + PL(y - x) + 2) >> 2;
-                else v = (PT(0) + 2 * PT(-1) + PL(0) + 2) >> 2;
-                break;
-              case 5: {
-                const int z = 2 * x - y;
-                if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 1) >> 1;
-                else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + PT(x - (y >> 1)) + 2) >> 2;
-                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
-                else v = (PL(y - 2 * x - 1) + 2 * PL(y - 2 * x - 2) + PL(y - 2 * x - 3) + 2) >> 2;
-                break;
-              }
-              case 6: {
-                const int z = 2 * y - x;
-                if (z >= 0 && !(z & 1)) v = (PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 1) >> 1;
-                else if (z >= 0) v = (PL(y - (x >> 1) - 2) + 2 * PL(y - (x >> 1) - 1) + PL(y - (x >> 1)) + 2) >> 2;
-                else if (z == -1) v = (PL(0) + 2 * PL(-1) + PT(0) + 2) >> 2;
-                else v = (PT(x - 2 * y - 1) + 2 * PT(x - 2 * y - 2) + PT(x - 2 * y - 3) + 2) >> 2;
-                break;
-              }
-              case 7:
-                v = !(y & 1) ? (PT(x + (y >> 1)) + PT(x + (y >> 1) + 1) + 1) >> 1
-                             : (PT(x + (y >> 1)) + 2 * PT(x + (y >> 1) + 1) + PT(x + (y >> 1) + 2) + 2) >> 2;
-                break;
-              default: {
-                const int z = x + 2 * y;
-                if (z < 13 && !(z & 1)) v = (PL(y + (x >> 1)) + PL(y + (x >> 1) + 1) + 1) >> 1;
-                else if (z < 13) v = (PL(y + (x >> 1)) + 2 * PL(y + (x >> 1) + 1) + PL(y + (x >> 1) + 2) + 2) >> 2;
-                else if (z == 13) v = (PL(6) + 3 * PL(7) + 2) >> 2;
-                else v = PL(7);
-                break;
-              }
-            }
-            o[xx] = c255(v + res[yy * 4 + xx]);
-          }
+          for (int xx = 0; xx < 4; ++xx) o[xx] = c255(t.p8[(ow >> (8 * xx)) & 255] + res[yy * 4 + xx]);
           const uint32_t w4 = pack4(o[0], o[1], o[2], o[3]);
           *reinterpret_cast<uint32_t *>(&t.y[1 + by * 4 + yy][4 + bx * 4]) = w4;
           *reinterpret_cast<uint32_t *>(Y + yrow0 + static_cast<int64_t>(by * 4 + yy) * pitch + bx * 4) = w4;
         }
-#undef PT
-#undef PL
       }
       lane_sync();
     }
@@ -1016,12 +1011,14 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   __shared__ int s_max, s_cnt;
   __shared__ int s_lvl[kIntraLevels + 1], s_fill[kIntraLevels];
   __shared__ __attribute__((aligned(4))) uint8_t s_off4[9 * 16];
+  __shared__ __attribute__((aligned(4))) uint8_t s_off8[9 * 64];
   const int nmb = a.P.mb_width * a.P.mb_height;
   const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;
   if (tid == 0) s_max = -1;
   if (tid < 9 * 16) s_off4[tid] = static_cast<uint8_t>(intra4_off(tid >> 4, tid & 3, (tid >> 2) & 3));
+  for (int i = tid; i < 9 * 64; i += kIntraThreads) s_off8[i] = static_cast<uint8_t>(intra8_off(i >> 6, i & 7, (i >> 3) & 7));
   __syncthreads();
   int m = -1;
   for (int i = tid; i < nmb; i += kIntraThreads) {
@@ -1070,7 +1067,7 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
       j0 = 0;
       j1 = s_cnt;
     }
-    for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4);
+    for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4, s_off8);
     __syncthreads();
   }
 }
