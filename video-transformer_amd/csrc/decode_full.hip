@@ -238,61 +238,60 @@ __device__ __forceinline__ void load_win9(const uint8_t *R, int pitch, int W, in
   }
 }
 
-#define HT(r, x) t6(px(w, r, x), px(w, r, x + 1), px(w, r, x + 2), px(w, r, x + 3), px(w, r, x + 4), px(w, r, x + 5))
-#define VT(c, y) t6(px(w, y, c), px(w, y + 1, c), px(w, y + 2, c), px(w, y + 3, c), px(w, y + 4, c), px(w, y + 5, c))
-
-// 8.4.2.2.1: the 4x4 luma prediction at fractional offset (xf, yf), packed rows
+// 8.4.2.2.1 with one instruction stream for every fractional offset: every
+// intermediate a 4x4 block can need (the 6-tap rows 0..8 for j, b / s, the
+// 6-tap columns for h / m) computed once, the sample chosen by selects, so a
+// wave whose lanes sit at different offsets runs no branch bodies one after
+// another (profiles/r03_luma_unified_ab.txt); integer motion keeps its copy
 __device__ __forceinline__ void luma_pred4(const uint32_t (&w)[9][3], int xf, int yf, int (&v)[16]) {
   if (!(xf | yf)) {
 #pragma unroll
     for (int y = 0; y < 4; ++y)
 #pragma unroll
       for (int x = 0; x < 4; ++x) v[y * 4 + x] = px(w, y + 2, x + 2);
-  } else if (!yf) {
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int b = c255((HT(y + 2, x) + 16) >> 5);
-        const int o = xf == 1 ? px(w, y + 2, x + 2) : px(w, y + 2, x + 3);
-        v[y * 4 + x] = xf == 2 ? b : (b + o + 1) >> 1;
-      }
-  } else if (!xf) {
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int h = c255((VT(x + 2, y) + 16) >> 5);
-        const int o = yf == 1 ? px(w, y + 2, x + 2) : px(w, y + 3, x + 2);
-        v[y * 4 + x] = yf == 2 ? h : (h + o + 1) >> 1;
-      }
-  } else if (xf == 2 || yf == 2) {
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        int hb[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) hb[k] = HT(y + k, x);
-        const int j = c255((t6(hb[0], hb[1], hb[2], hb[3], hb[4], hb[5]) + 512) >> 10);
-        int o;
-        if (xf == 2) o = c255(((yf == 1 ? hb[2] : hb[3]) + 16) >> 5);  // b or s
-        else o = c255(((xf == 1 ? VT(x + 2, y) : VT(x + 3, y)) + 16) >> 5);  // h or m
-        v[y * 4 + x] = (xf == 2 && yf == 2) ? j : (j + o + 1) >> 1;
-      }
-  } else {
-#pragma unroll
-    for (int y = 0; y < 4; ++y)
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int bs = c255(((yf == 1 ? HT(y + 2, x) : HT(y + 3, x)) + 16) >> 5);
-        const int hm = c255(((xf == 1 ? VT(x + 2, y) : VT(x + 3, y)) + 16) >> 5);
-        v[y * 4 + x] = (bs + hm + 1) >> 1;
-      }
+    return;
   }
+  int hr[9][4], vt[4][5];
+#pragma unroll
+  for (int r = 0; r < 9; ++r)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) hr[r][x] = t6(px(w, r, x), px(w, r, x + 1), px(w, r, x + 2), px(w, r, x + 3), px(w, r, x + 4), px(w, r, x + 5));
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) vt[y][c] = t6(px(w, y, c + 2), px(w, y + 1, c + 2), px(w, y + 2, c + 2), px(w, y + 3, c + 2), px(w, y + 4, c + 2), px(w, y + 5, c + 2));
+  const bool x0 = xf == 0, y0 = yf == 0, x2 = xf == 2, y2 = yf == 2, x3 = xf == 3, y3 = yf == 3;
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int b = c255((hr[y + 2][x] + 16) >> 5), s_ = c255((hr[y + 3][x] + 16) >> 5);
+      const int h = c255((vt[y][x] + 16) >> 5), m = c255((vt[y][x + 1] + 16) >> 5);
+      const int j = c255((t6(hr[y][x], hr[y + 1][x], hr[y + 2][x], hr[y + 3][x], hr[y + 4][x], hr[y + 5][x]) + 512) >> 10);
+      const int G = px(w, y + 2, x + 2), G1 = px(w, y + 2, x + 3), G2 = px(w, y + 3, x + 2);
+      const int bs = y3 ? s_ : b, hm = x3 ? m : h;
+      int P, Q;
+      bool full;
+      if (x0) {
+        P = h;
+        Q = y3 ? G2 : G;
+        full = y2;
+      } else if (y0) {
+        P = b;
+        Q = x3 ? G1 : G;
+        full = x2;
+      } else if (x2 || y2) {
+        P = j;
+        Q = x2 ? bs : hm;
+        full = x2 && y2;
+      } else {
+        P = bs;
+        Q = hm;
+        full = false;
+      }
+      v[y * 4 + x] = full ? P : (P + Q + 1) >> 1;
+    }
 }
-#undef HT
-#undef VT
 
 // 8.5.12.1 chroma DC of chroma block ck: 2x2 Hadamard of the plane's DC levels, scaled
 __device__ __forceinline__ int chroma_dc(const int16_t *arena, uint32_t blocks, uint32_t coef, int pl, int ck,
