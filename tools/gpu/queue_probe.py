@@ -23,6 +23,11 @@ def timeit(path):
     return r
 
 
+import os  # noqa: E402
+if not os.path.exists("/tmp/gcab.mp4"):
+    scene.synth_write("/tmp/gcab.mp4", width=1280, height=720, fps=30, n_frames=18000, seed=0x5EED, coding="full",
+                      slices_per_row=0, max_motion=4, bframes=True, weighted="implicit", cabac=True,
+                      transform_8x8=True)
 scene.synth_write("/tmp/small.mp4", width=1280, height=720, fps=30, n_frames=1800, seed=7)
 print("fresh", timeit("/tmp/gcab.mp4"), flush=True)
 vs = [scene.VideoScorer("/tmp/small.mp4", device=0) for _ in range(5)]

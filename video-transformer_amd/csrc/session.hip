@@ -23,6 +23,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -44,6 +46,36 @@ namespace {
 constexpr int64_t kSingleWindowBytes = 48ll << 30;  // up to 48 GiB decoded: one window
 constexpr int64_t kMinRingBytes = 1ll << 30;        // else two rings of >= 1 GiB
 constexpr int64_t kPad = 256;
+
+// Streams outlive sessions: a process-wide free list per device, handed out
+// in a fixed role order (decode, score, parse, GOP groups) and taken back in
+// reverse, so successive sessions get the same streams in the same roles and
+// with them the same hardware queues.  Streams created afresh after other
+// sessions had come and gone could land the two GOP groups on one of the
+// process's four hardware queues and serialise them (general decoder
+// reconstruction 218 -> 288 ms, tools/gpu/queue_probe.py); sessions open at
+// the same time still get streams of their own.
+std::mutex g_stream_mu;
+std::map<int, std::vector<hipStream_t>> g_stream_pool;
+
+int stream_take(int device, hipStream_t *s) {
+  {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    auto &v = g_stream_pool[device];
+    if (!v.empty()) {
+      *s = v.back();
+      v.pop_back();
+      return VTS_OK;
+    }
+  }
+  HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+  return VTS_OK;
+}
+void stream_give(int device, hipStream_t s) {  // s idle
+  if (!s) return;
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  g_stream_pool[device].push_back(s);
+}
 
 }  // namespace
 
@@ -138,11 +170,11 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   if (!c->d_hist) HIP_TRY(hipMalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
   c->thumb_px = tw;
   if (!c->d_rgb) HIP_TRY(hipMalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
-  if (!c->s_dec) HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
-  if (!c->s_score) HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
-  if (!c->s_parse) HIP_TRY(hipStreamCreateWithFlags(&c->s_parse, hipStreamNonBlocking));
+  if (!c->s_dec) VTS_TRY(stream_take(c->device, &c->s_dec));
+  if (!c->s_score) VTS_TRY(stream_take(c->device, &c->s_score));
+  if (!c->s_parse) VTS_TRY(stream_take(c->device, &c->s_parse));
   for (int g = 0; g + 1 < vts_ctx::kMaxGroups; ++g) {
-    if (!c->s_grp[g]) HIP_TRY(hipStreamCreateWithFlags(&c->s_grp[g], hipStreamNonBlocking));
+    if (!c->s_grp[g]) VTS_TRY(stream_take(c->device, &c->s_grp[g]));
     if (!c->ev_grp[g]) HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[g], hipEventDisableTiming));
   }
   for (auto e2 : c->ev)
@@ -594,11 +626,11 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   HIP_TRY(hipMalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
   c->thumb_px = tw;
   HIP_TRY(hipMalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
-  HIP_TRY(hipStreamCreateWithFlags(&c->s_dec, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&c->s_score, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&c->s_parse, hipStreamNonBlocking));
+  VTS_TRY(stream_take(c->device, &c->s_dec));
+  VTS_TRY(stream_take(c->device, &c->s_score));
+  VTS_TRY(stream_take(c->device, &c->s_parse));
   for (int g = 1; g < c->recon_groups; ++g) {
-    HIP_TRY(hipStreamCreateWithFlags(&c->s_grp[g - 1], hipStreamNonBlocking));
+    VTS_TRY(stream_take(c->device, &c->s_grp[g - 1]));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[g - 1], hipEventDisableTiming));
   }
   c->ev.resize(c->windows.size() * 6);
@@ -1123,13 +1155,14 @@ extern "C" int vts_close(vts_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);
-  if (c->s_dec) (void)hipStreamDestroy(c->s_dec);
-  if (c->s_score) (void)hipStreamDestroy(c->s_score);
-  if (c->s_parse) (void)hipStreamDestroy(c->s_parse);
-  for (int g = 0; g < vts_ctx::kMaxGroups - 1; ++g) {
-    if (c->s_grp[g]) (void)hipStreamDestroy(c->s_grp[g]);
+  for (int g = vts_ctx::kMaxGroups - 2; g >= 0; --g) {  // back to the pool in reverse role order
+    if (c->s_grp[g]) (void)hipStreamSynchronize(c->s_grp[g]);
+    stream_give(c->device, c->s_grp[g]);
     if (c->ev_grp[g]) (void)hipEventDestroy(c->ev_grp[g]);
   }
+  stream_give(c->device, c->s_parse);
+  stream_give(c->device, c->s_score);
+  stream_give(c->device, c->s_dec);
   delete c;
   return VTS_OK;
 }
