@@ -9,5 +9,5 @@ scene.synth_write("/tmp/gcab.mp4", width=1280, height=720, fps=30, n_frames=1800
                   slices_per_row=0, max_motion=4, bframes=True, weighted="implicit", cabac=True, transform_8x8=True)
 PY
 bash tools/gpu/pmc_kernel.sh "$GRAFT_REPO_ROOT/bench.py --video /tmp/gcab.mp4 --config 720p-10min --coding full --bframes --steps 1 --warmup 0 --no-pmc --no-cpu-baseline --no-parity --extras none" \
-  "SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_WAVES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES" > gpurun_out/pmc_icache.txt 2>&1
+  "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_WAVES SQ_INSTS_SALU" > gpurun_out/pmc_icache.txt 2>&1
 rc=$?; cat gpurun_out/pmc_icache.txt; exit $rc
