@@ -3,6 +3,8 @@
 # the x264-like 10-min 720p streams (LIBS names the builds, cur = in-tree).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
+# an earlier GPU step of the same call failed or was killed: start nothing more
+[ -f gpurun_out/gpu_step_failed ] && { echo "earlier GPU step failed; not starting"; exit 1; }
 O=gpurun_out/${OUT:-r03i}
 mkdir -p $O
 cp video-transformer_amd/vtseg/libvtseg.so tools/exp/lib_cur.so

@@ -10,4 +10,4 @@ scene.synth_write("/tmp/gcab.mp4", width=1280, height=720, fps=30, n_frames=1800
 PY
 bash tools/gpu/pmc_kernel.sh "$GRAFT_REPO_ROOT/bench.py --video /tmp/gcab.mp4 --config 720p-10min --coding full --bframes --steps 1 --warmup 0 --no-pmc --no-cpu-baseline --no-parity --extras none" \
   "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_WAVES SQ_INSTS_SALU" > gpurun_out/pmc_icache.txt 2>&1
-rc=$?; cat gpurun_out/pmc_icache.txt; exit $rc
+rc=$?; cat gpurun_out/pmc_icache.txt; [ $rc -eq 0 ] || touch gpurun_out/gpu_step_failed; exit $rc

@@ -64,7 +64,7 @@ constexpr int kInterThreads = 256;   // 16 macroblocks x 16 blocks
 #ifndef VTS_DBK_THREADS
 #define VTS_DBK_THREADS 1024
 #endif
-constexpr int kIntraThreads = VTS_INTRA_THREADS;  // 512: 32 macroblocks in flight (256 VGPRs for the Intra_8x8 path)
+constexpr int kIntraThreads = VTS_INTRA_THREADS;  // 512: 32 macroblocks in flight (2 waves per SIMD, <= 256 VGPRs)
 constexpr int kIntraSlots = kIntraThreads / 16;
 constexpr int kIntraLevels = 512;  // intra dependency levels bucketed in LDS (more: one scan per level)
 constexpr int kDbkThreads = VTS_DBK_THREADS;      // 1024: 16 waves = 16 row pairs in flight
@@ -73,6 +73,11 @@ constexpr int kDbkWaves = kDbkThreads / 64;
 // One slice per wave: every value of the parse is
 // wave-uniform, so control flow never diverges and the integer work can go to
 // the scalar unit; the parallelism is the window's slices (thousands of waves).
+// 4 waves per SIMD.  Since the CABAC engine's arithmetic moved to the vector
+// ALUs, 5 (<= 102 VGPRs, a few spilled) times faster: parse -6.5 % CABAC,
+// -8.7 % CAVLC (3: +13 %; profiles/r03_parse_waves_ab.txt); it becomes the
+// default once the GPU parity suite has run on a 5-wave build
+// (-DVTS_PARSE_WAVES=5 builds it)
 #ifndef VTS_PARSE_WAVES
 #define VTS_PARSE_WAVES 4
 #endif
