@@ -4,8 +4,11 @@
                     [--config 720p-batch|720p-10min|720p-2h|1080p-2h|480p-60s]
                     [--workload decode_score|score|transcode] [--extras all|none]
 
-One process per GPU (torch.distributed.run for N > 1; RANK/LOCAL_RANK/
-WORLD_SIZE from the env, rendezvous on 127.0.0.1).  Weak scaling: every rank
+One process per GPU: under a launcher (torch.distributed.run) RANK/LOCAL_RANK/
+WORLD_SIZE come from the env and must agree with --gpus; a plain
+`bench.py --gpus N` starts the N ranks itself through torch.distributed.run
+(rendezvous on 127.0.0.1) before it touches the GPU, waits, and exits with
+their status (rank 0's JSON line is the output).  Weak scaling: every rank
 owns `videos_per_gpu` synthetic videos (video i on rank i mod N, BASELINE
 config [3]'s partition) and a step is one call of vtseg.batch.plan_batch over
 the whole batch: per local video probe + plan + device decode + score + scene
@@ -468,6 +471,69 @@ def roofline_decode_score(scorers, prof: dict | None, width: int, height: int, k
     return roof
 
 
+# ------------------------------------------------------------ rank launcher
+
+class LaunchError(ValueError):
+    """--gpus disagrees with the environment or the machine (exit status 2)."""
+
+
+def device_count() -> int:
+    """GPUs visible to this process without initialising any (on this image
+    torch.cuda.device_count() does not create a HIP context)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_plan(gpus: int, env, ndev: int, backend: str, argv: list[str],
+                     port=_free_port) -> tuple[list[str], dict] | None:
+    """How `bench.py --gpus N` becomes N rank processes (one per GPU), the
+    reference's sequential batch loop (src/pipeline.py:376-393) spread over
+    the node.  Returns None when this process is the (only) rank to run:
+    N = 1, or a launcher (torch.distributed.run) already set WORLD_SIZE to N.
+    Otherwise the torch.distributed.run command that starts N ranks of this
+    same script with the same arguments (rendezvous on 127.0.0.1) and its
+    environment; the parent only waits, so no process that touched the GPU
+    ever execs.  Raises LaunchError when --gpus disagrees with an existing
+    WORLD_SIZE, or asks for more GPUs than the machine has (NCCL = RCCL needs
+    one GPU per rank; gloo may put several ranks on one GPU as a rehearsal)."""
+    if gpus < 1:
+        raise LaunchError(f"--gpus {gpus}: at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise LaunchError(f"--gpus {gpus} disagrees with WORLD_SIZE={ws} set by the launcher")
+        return None
+    if gpus == 1:
+        return None
+    if backend == "nccl" and gpus > ndev:
+        raise LaunchError(f"--gpus {gpus} but only {ndev} GPU(s) visible; RCCL needs one GPU per "
+                          f"rank (--dist-backend gloo rehearses several ranks on one GPU)")
+    if ndev < 1:
+        raise LaunchError(f"--gpus {gpus} but no GPU visible")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port()}",
+           str(Path(__file__).resolve()), *argv]
+    child_env = dict(env)
+    child_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only (RCCL)
+    child_env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return cmd, child_env
+
+
+def placement(world: int, ndev: int) -> dict:
+    """GPUs a run occupies and ranks per GPU (rank r on GPU LOCAL_RANK % ndev):
+    a gloo rehearsal with more ranks than GPUs reports its GPUs as n_gpus,
+    never its ranks."""
+    n = max(1, min(world, max(ndev, 1)))
+    return {"n_gpus": n, "world_size": world, "ranks_per_gpu": round(world / n, 3)}
+
+
 # --------------------------------------------------------------- extras (N = 1)
 
 ROOF_RUNS = 3             # roofline_decode_score's vts_run calls per session
@@ -668,11 +734,24 @@ def main() -> None:
     ap.add_argument("--parse-chunks", type=int, default=1,
                     help="slice-parse chunks overlapped with reconstruction (1 = none, the default)")
     ap.add_argument("--level-block", type=int, default=0,
-                    help="GOP levels per reconstruct launch (0 auto = level-blocked kernel where it "
-                         "applies, 1 = one launch per level)")
+                    help="GOP levels per reconstruct launch: 0 or 1 = one launch per level (the "
+                         "default), >= 2 = the level-blocked kernel (opt-in, DESIGN 4.6)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 passes (kernel trace and --pmc) of the headline")
     args = ap.parse_args()
+
+    # --gpus N > 1 with no launcher around us: start the N ranks ourselves
+    # (before anything touches the GPU) and exit with their status
+    try:
+        plan = rank_launch_plan(args.gpus, os.environ, device_count(), args.dist_backend,
+                                sys.argv[1:], port=_free_port)
+    except LaunchError as exc:
+        print(f"bench.py: {exc}", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    if plan is not None:
+        cmd, env = plan
+        log(f"launching {args.gpus} ranks: {' '.join(cmd[:9])} ...")
+        raise SystemExit(subprocess.run(cmd, env=env).returncode)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -993,7 +1072,8 @@ def main() -> None:
 
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 1), "unit": "frames/s",
+            **placement(world, ndev),
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u8", "data": "synthetic",

@@ -331,6 +331,7 @@ typedef struct {
   int off_non_ref, off_t2b, ncycle;  /* POC type 1 (7.4.2.1.1) */
   int off_ref[256];
   uint8_t sl4[6][16], sl8[2][64];    /* sequence-level scaling lists (scan order; 16s when absent) */
+  int seq_scaling;                   /* seq_scaling_matrix_present_flag */
 } fo_sps;
 typedef struct {
   int valid, sps_id, bfpo, num_ref_l0, num_ref_l1, weighted_pred, weighted_bipred, pic_init_qp;
@@ -397,7 +398,10 @@ static int parse_sps(const uint8_t *nal, int64_t n, fo_sps *tab, char *err) {
   }
   memset(s.sl4, 16, sizeof s.sl4); /* Flat_4x4_16 / Flat_8x8_16 */
   memset(s.sl8, 16, sizeof s.sl8);
-  if (is_high(s.profile_idc) && fb_bit(&b)) fo_scaling_matrix(&b, 8, NULL, s.sl4, s.sl8);
+  if (is_high(s.profile_idc) && fb_bit(&b)) {
+    s.seq_scaling = 1;
+    fo_scaling_matrix(&b, 8, NULL, s.sl4, s.sl8);
+  }
   s.log2_max_frame_num = (int)fb_ue(&b) + 4;
   s.poc_type = (int)fb_ue(&b);
   if (s.poc_type == 0) {
@@ -468,7 +472,9 @@ static int parse_pps(const uint8_t *nal, int64_t n, fo_pps *tab, const fo_sps *s
     if (pos_bits < stop) {
       p.t8mode = (int)fb_bit(&b);
       p.pic_scaling = (int)fb_bit(&b);
-      if (p.pic_scaling) fo_scaling_matrix(&b, 6 + 2 * p.t8mode, S, l4, l8);
+      /* 7.4.2.2: rule B only when the SPS carries seq_scaling_matrix_present_flag
+         1; with Flat_16 sequence lists the PPS falls back by rule A */
+      if (p.pic_scaling) fo_scaling_matrix(&b, 6 + 2 * p.t8mode, S->seq_scaling ? S : NULL, l4, l8);
       p.cqp_off2 = fb_se(&b);
     }
     fo_tables_init(); /* ZZ8 */

@@ -30,6 +30,31 @@ extern "C" void fh_stats(unsigned long long *out) {
 
 using namespace vts;
 
+// LevelScale4x4 / 8x8 the product derives from a file's SPS / PPS
+// (sched_stream_facts, 8.5.9): ls4 = 6 x 6 x 16, ls8 = 2 x 6 x 64 int32
+extern "C" int fh_scale(const char *path, int32_t *ls4, int32_t *ls8, int *flags, char *err, int err_cap) {
+  auto bad = [&](const std::string &m) {
+    std::snprintf(err, static_cast<size_t>(err_cap), "%s", m.c_str());
+    return -1;
+  };
+  Mp4Info mp4;
+  std::string e = mp4_parse_file(path, &mp4);
+  if (!e.empty()) return bad(e);
+  const Mp4VideoTrack &t = mp4.video.front();
+  Sps sps;
+  Pps pps;
+  e = parse_sps(t.sps[0].data(), t.sps[0].size(), &sps);
+  if (e.empty()) e = parse_pps(t.pps[0].data(), t.pps[0].size(), &pps);
+  SchedStream facts;
+  if (e.empty()) e = sched_stream_facts(t.sps[0], t.pps[0], sps, pps, &facts);
+  if (!e.empty()) return bad(e);
+  std::memcpy(ls4, facts.scale.ls4, sizeof facts.scale.ls4);
+  std::memcpy(ls8, facts.scale.ls8, sizeof facts.scale.ls8);
+  flags[0] = facts.seq_scaling;
+  flags[1] = facts.pic_scaling;
+  return 0;
+}
+
 extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_cap, int64_t *n_out,
                          int *w_out, int *h_out, char *err, int err_cap) {
   auto bad = [&](const std::string &m) {

@@ -392,3 +392,51 @@ def test_scaling_matrix_streams_bit_exact(tmp_path, name, kw):
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
+
+
+@pytest.mark.parametrize("merge", ["0", "1"])
+def test_cabac_b_parse_merged_and_per_level(tmp_path, monkeypatch, merge):
+    """the merged parse launch (default; B slices wait on their
+    colocated picture's completion counter) and the per-level fallback
+    (VTS_PARSE_MERGE=0: one launch per colocated level) both equal the
+    oracle on a CABAC B stream with temporal direct in several windows."""
+    _require_gpu()
+    monkeypatch.setenv("VTS_PARSE_MERGE", merge)
+    n = 60
+    src, path = tmp_path / "src.mp4", tmp_path / "mb.mp4"
+    scene.synth_write(src, width=176, height=144, n_frames=n, coding="full", bframes=True,
+                      temporal_direct=True, weighted="implicit", cut_min_s=0.5, cut_max_s=1.2,
+                      gop_max_s=0.6, seed=21, chunks=1)
+    oracle.cabac_convert(src, path, seed=7, t8=True)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
+    for wf in (0, 24):
+        with scene.VideoScorer(path, keep_frames=wf == 0, window_frames=wf, n_streams=2) as v:
+            res = v.score()
+            if wf == 0:
+                got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+                assert _first_diff(got, frames) == []
+            assert np.array_equal(res.hist, ref["hist"])
+            assert np.array_equal(res.scores, ref["score"])
+
+
+def test_sessions_reopened_in_sequence_reuse_the_stream_pool(tmp_path):
+    """sessions take their HIP streams from a process-wide pool and
+    give them back on close; open / run / close several sessions in sequence
+    (and two at once) on the same B stream: every run equals the oracle."""
+    _require_gpu()
+    n = 48
+    path = tmp_path / "pool.mp4"
+    scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=True,
+                      weighted="implicit", cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.5, seed=23)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
+    for _ in range(4):
+        with scene.VideoScorer(path) as v:
+            res = v.score()
+            assert np.array_equal(res.scores, ref["score"]) and np.array_equal(res.hist, ref["hist"])
+    with scene.VideoScorer(path) as a, scene.VideoScorer(path) as b:
+        ra, rb = a.score(), b.score()
+        assert np.array_equal(ra.scores, ref["score"]) and np.array_equal(rb.sad, ref["sad"])
+    with scene.VideoScorer(path) as v:
+        assert np.array_equal(v.score().scores, ref["score"])

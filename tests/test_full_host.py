@@ -213,3 +213,79 @@ def test_scaling_matrix_streams_on_cpu_equal_oracle(tmp_path, harness, name, kw,
         assert got.shape == want.shape
         bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
         assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"
+
+
+def _writer_list_kinds(seed: int, n: int) -> list[int]:
+    """synth_full.cpp write_scaling_lists(): the kind of each list (0 absent,
+    1 useDefaultScalingMatrixFlag, 2 ends early, 3 full) for one seed."""
+    M = (1 << 64) - 1
+    x = (seed * 0x9E3779B97F4A7C15 + 0x2545F4914F6CDD1D) & M
+
+    def rnd(m):
+        nonlocal x
+        x ^= (x << 13) & M
+        x ^= x >> 7
+        x ^= (x << 17) & M
+        return x % m
+    kinds = []
+    for i in range(n):
+        kind = rnd(4)
+        kinds.append(kind)
+        if kind < 2:
+            continue
+        size = 16 if i < 6 else 64
+        stop = 1 + rnd(size - 1) if kind == 2 else size
+        for _ in range(stop):
+            rnd(61)
+    return kinds
+
+
+def test_pps_only_scaling_falls_back_by_rule_a(tmp_path):
+    """7.4.2.2 / Table 7-2: a PPS scaling matrix over an SPS without one
+    (seq_scaling_matrix_present_flag 0) falls back by rule A, so absent lists
+    0 (Intra Y) and 3 (Inter Y) are Default_4x4_Intra / Default_4x4_Inter
+    (Table 7-3), not the SPS's Flat_16.  LevelScale4x4 = weightScale x
+    normAdjust4x4 (8.5.9), checked by hand at three positions per list."""
+    so = tmp_path / "libfh_scale.so"
+    srcs = [ROOT / "tests" / "native" / "full_host.cpp"] + [CSRC / f for f in
+                                                             ("mp4.cpp", "h264.cpp", "h264_sched.cpp",
+                                                              "plan.cpp")]
+    subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-Wno-unknown-pragmas",
+                    f"-I{CSRC}", f"-I{ROOT / 'include'}", *map(str, srcs), "-o", str(so)], check=True)
+    lib = C.CDLL(str(so))
+    # the PPS's lists are seeded with seed * 2 + 2 (synth_full.cpp make_sps_pps_full)
+    seed = next(s for s in range(1, 4000)
+                if (lambda k: k[0] == 0 and k[3] == 0 and any(k))(_writer_list_kinds(s * 2 + 2, 6)))
+    path = tmp_path / "pps_only.mp4"
+    scene.synth_write(path, width=64, height=48, n_frames=4, coding="full", slices_per_row=0,
+                      seed=seed, scaling="pps")
+    ls4 = np.zeros((6, 6, 16), np.int32)
+    ls8 = np.zeros((2, 6, 64), np.int32)
+    flags = np.zeros(2, np.int32)
+    err = C.create_string_buffer(256)
+    assert lib.fh_scale(str(path).encode(), ls4.ctypes.data_as(C.c_void_p),
+                        ls8.ctypes.data_as(C.c_void_p), flags.ctypes.data_as(C.c_void_p), err, 256) == 0, \
+        err.value
+    assert flags.tolist() == [0, 1]
+    # raster (i, j) -> zig-zag index: (0,0) 0, (0,1) 1, (1,1) 4, (3,3) 15
+    # Default_4x4_Intra[0, 1, 4, 15] = 6, 13, 20, 42; Inter = 10, 14, 20, 34
+    # normAdjust4x4, qP % 6 = 0: v0 = 10 (i, j even), v1 = 16 (both odd), v2 = 13
+    # qP % 6 = 5: 18, 29, 23
+    assert [ls4[0, 0, 0], ls4[0, 0, 1], ls4[0, 0, 5], ls4[0, 0, 15]] == [60, 169, 320, 672]
+    assert [ls4[3, 0, 0], ls4[3, 0, 1], ls4[3, 0, 5], ls4[3, 0, 15]] == [100, 182, 320, 544]
+    assert [ls4[0, 5, 0], ls4[3, 5, 15]] == [6 * 18, 34 * 29]
+    # rule A for the lists after an absent one: list 1 / 4 copy list 0 / 3 when absent too
+    k = _writer_list_kinds(seed * 2 + 2, 6)
+    for i in (1, 2, 4, 5):
+        if k[i] == 0 and all(k[j] == 0 for j in range(3 * (i // 3), i)):
+            assert np.array_equal(ls4[i], ls4[3 * (i // 3)])
+    # and the oracle decodes the stream exactly like the product's harness
+    want, _ = oracle.decode_full(path, flags=0)
+    lib.fh_decode.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                              C.c_void_p, C.c_char_p, C.c_int]
+    cap = 4 * 64 * 48 * 3 // 2
+    out = np.zeros(cap, np.uint8)
+    n, w, h = C.c_int64(0), C.c_int(0), C.c_int(0)
+    assert lib.fh_decode(str(path).encode(), 0, out.ctypes.data, cap, C.byref(n), C.byref(w),
+                         C.byref(h), err, 256) == 0, err.value
+    assert np.array_equal(out[:want.size].reshape(want.shape), want)

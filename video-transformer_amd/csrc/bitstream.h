@@ -70,6 +70,17 @@ class BitReader {  // reads an EBSP (NAL payload) skipping emulation bytes
  public:
   BitReader(const uint8_t *p, size_t n) : p_(p), n_(n) {}
   bool ok() const { return !err_; }
+  // 7.2 more_rbsp_data(): a bit other than the rbsp_stop_one_bit remains
+  // (positions in EBSP bits; an emulation byte cannot follow the stop bit)
+  bool more_rbsp_data() const {
+    size_t last = n_;
+    while (last > 0 && p_[last - 1] == 0) --last;
+    if (last == 0) return false;
+    int tz = 0;
+    while (!((p_[last - 1] >> tz) & 1)) ++tz;
+    const size_t stop = (last - 1) * 8 + static_cast<size_t>(7 - tz);
+    return pos_ * 8 - static_cast<size_t>(bitpos_) < stop;
+  }
   uint32_t bit() {
     if (bitpos_ == 0) {
       if (pos_ >= n_) {
@@ -111,7 +122,6 @@ class BitReader {  // reads an EBSP (NAL payload) skipping emulation bytes
     const uint32_t k = ue();
     return (k & 1u) ? static_cast<int32_t>((k + 1) / 2) : -static_cast<int32_t>(k / 2);
   }
-  bool more_rbsp_data() const;  // not needed by the subset parsers
 
  private:
   const uint8_t *p_;

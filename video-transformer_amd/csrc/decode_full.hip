@@ -79,7 +79,7 @@ constexpr int kDbkWaves = kDbkThreads / 64;
 // default once the GPU parity suite has run on a 5-wave build
 // (-DVTS_PARSE_WAVES=5 builds it)
 #ifndef VTS_PARSE_WAVES
-#define VTS_PARSE_WAVES 4
+#define VTS_PARSE_WAVES 5
 #endif
 // The entropy mode is per stream, so each mode is its own kernel: a wave only
 // ever runs one parser's code, and each fits the instruction cache better.
@@ -99,12 +99,13 @@ __device__ __forceinline__ void parse_one(const FullParseArgs &a, full::FullScra
     if (a.pdone) {
       // merged launch: the colocated picture's slices have lower workgroup
       // indices (dispatched first on every XCD), so this wait ends; bounded
-      // anyway (~3 s), then the slice reports a missing reference
+      // anyway (~3 s), then DEC_E_COL_WAIT fails the run (the slice's direct
+      // prediction would read a partly written colocated record)
       const uint32_t need = static_cast<uint32_t>(a.pneed[col]);
       uint32_t spins = 0;
       while (__hip_atomic_load(&a.pdone[col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         if (++spins > (1u << 25)) {
-          atomicOr(a.err, static_cast<uint32_t>(DEC_E_NO_REF));
+          atomicOr(a.err, static_cast<uint32_t>(DEC_E_COL_WAIT));
           break;
         }
         __builtin_amdgcn_s_sleep(4);

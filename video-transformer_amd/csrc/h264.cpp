@@ -107,6 +107,7 @@ std::string parse_pps(const uint8_t *nal, size_t n, Pps *p) {
   p->constrained_intra_pred = static_cast<int>(br.u(1));
   p->redundant_pic_cnt_present = static_cast<int>(br.u(1));
   if (!br.ok()) return "truncated PPS";
+  p->has_tail = br.more_rbsp_data() ? 1 : 0;
   if (p->weighted_bipred_idc > 2) return "bad weighted_bipred_idc";
   return "";
 }
@@ -135,9 +136,10 @@ std::string describe_decode_error(uint32_t f) {
       "fractional luma motion", "multiple references", "bitstream syntax error",
       "active deblocking filter", "unknown PPS id", "macroblock not covered by any slice",
       "emulation prevention inside I_PCM samples", "reference list modification",
-      "P slice without reference frame", "adaptive reference marking (MMCO)"};
+      "P slice without reference frame", "adaptive reference marking (MMCO)",
+      "B slice's wait for its colocated picture's parse timed out"};
   std::string s;
-  for (int i = 0; i < 13; ++i)
+  for (int i = 0; i < 14; ++i)
     if (f & (1u << i)) {
       if (!s.empty()) s += ", ";
       s += names[i];

@@ -29,6 +29,9 @@ struct Pps {
   int weighted_pred = 0, weighted_bipred_idc = 0, pic_init_qp = 26;
   int chroma_qp_index_offset = 0, deblocking_filter_control_present = 0;
   int constrained_intra_pred = 0, redundant_pic_cnt_present = 0;
+  // the High-profile tail (transform_8x8_mode_flag, pic scaling matrix,
+  // second_chroma_qp_index_offset) is present: general decoder only
+  int has_tail = 0;
 };
 
 // Parse an SPS/PPS NAL unit (payload including the one-byte NAL header).
@@ -77,6 +80,7 @@ enum DecodeError : uint32_t {
   DEC_E_REFLIST = 1u << 10,       // ref_pic_list_modification / weighted pred
   DEC_E_NO_REF = 1u << 11,        // P slice without a preceding reference
   DEC_E_MMCO = 1u << 12,          // adaptive reference marking
+  DEC_E_COL_WAIT = 1u << 13,      // merged parse: a B slice's wait for its colocated picture timed out
   // not an error: a level-blocked reconstruct launch met a motion vector
   // reaching beyond its halo; the host re-runs with per-level launches
   DEC_W_LEVEL_RANGE = 1u << 31,

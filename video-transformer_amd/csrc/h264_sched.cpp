@@ -211,7 +211,10 @@ std::string sched_stream_facts(const std::vector<uint8_t> &sps_nal, const std::v
     if (more_rbsp(pps_nal, r)) {
       out->transform_8x8 = static_cast<int>(r.u(1));
       out->pic_scaling = static_cast<int>(r.u(1));
-      if (out->pic_scaling) read_scaling_matrix(r, 6 + 2 * out->transform_8x8, true, sl4, sl8, pl4, pl8);
+      // 7.4.2.2: fall-back rule B (the SPS's lists) only when the SPS has
+      // its own matrix; rule A (Table 7-3 / 7-4 defaults) otherwise
+      if (out->pic_scaling)
+        read_scaling_matrix(r, 6 + 2 * out->transform_8x8, out->seq_scaling != 0, sl4, sl8, pl4, pl8);
       out->cqp_off2 = r.se();
     }
     if (r.err) return "truncated PPS";

@@ -244,6 +244,9 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   if (!e.empty()) return fail(VTS_E_UNSUPPORTED, "PPS: %s", e.c_str());
   if (c->pps.entropy_coding_mode && c->params.decoder == 1)
     return fail(VTS_E_UNSUPPORTED, "CABAC entropy coding needs the general decoder (decoder = auto / general)");
+  if (c->pps.has_tail && c->params.decoder == 1)
+    return fail(VTS_E_UNSUPPORTED,
+                "a High-profile PPS (8x8 transform / scaling matrix / Cr QP offset) needs the general decoder");
   if (c->sps.crop_left || c->sps.crop_top)
     return fail(VTS_E_UNSUPPORTED, "left/top cropping is not supported");
   c->prm = make_dev_params(c->sps, c->pps);

@@ -37,6 +37,9 @@ constexpr int64_t kMinRingBytes = 1ll << 30;
 bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
                    const std::vector<uint32_t> &sizes, int nal_length_size) {
   if (c->pps.entropy_coding_mode) return true;  // CABAC
+  // a High-profile PPS tail (8x8 transform, scaling lists, a Cr QP offset the
+  // subset kernels' deblocking gate does not see): ADVICE r03
+  if (c->pps.has_tail) return true;
   if (c->pps.weighted_pred || c->pps.weighted_bipred_idc) return true;
   if (c->sps.max_num_ref_frames > 1 || c->pps.num_ref_idx_l0_default_active > 1) return true;
   if (!c->pps.deblocking_filter_control_present) return true;  // deblocking on, offsets 0
@@ -138,8 +141,13 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  const int64_t whole = c->es_bytes + n * (3 * tw_f + 1024 + 12) +
-                        static_cast<int64_t>(slices.size()) * static_cast<int64_t>(sizeof(FullSlice)) + (1ll << 30);
+  // whole-video buffers: the elementary stream and its RBSP copy (d_rbsp,
+  // same size), per-frame scoring outputs, the slice table with its RBSP
+  // lengths and parse order, the per-picture parse counters, 1 GiB of slack
+  const int64_t whole = 2 * c->es_bytes + n * (3 * tw_f + 1024 + 12 + 2 * 4) +
+                        static_cast<int64_t>(slices.size()) *
+                            static_cast<int64_t>(sizeof(FullSlice) + 2 * sizeof(int64_t) + 2 * sizeof(int32_t)) +
+                        (1ll << 30);
   const int64_t avail = std::max<int64_t>(0, static_cast<int64_t>(free_b) - whole);
   const int64_t ring_budget = std::min(kWindowBytes, std::max(kMinRingBytes, avail / 4));
   int64_t wcap;
