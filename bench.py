@@ -526,6 +526,22 @@ def rank_launch_plan(gpus: int, env, ndev: int, backend: str, argv: list[str],
     return cmd, child_env
 
 
+def relay_ranks(cmd: list[str], env: dict, out=None, err=None) -> int:
+    """Run the rank launcher and wait.  Its stdout carries rank 0's JSON line
+    and whatever else the ranks print there (gloo announces its peer
+    connections on stdout): the JSON line goes to our stdout, everything else
+    to stderr, so the contract's one-line output holds.  Returns the
+    launcher's exit status."""
+    out = out or sys.stdout
+    err = err or sys.stderr
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    assert proc.stdout is not None
+    for line in proc.stdout:
+        (out if line.startswith('{"metric"') else err).write(line)
+        (out if line.startswith('{"metric"') else err).flush()
+    return proc.wait()
+
+
 def placement(world: int, ndev: int) -> dict:
     """GPUs a run occupies and ranks per GPU (rank r on GPU LOCAL_RANK % ndev):
     a gloo rehearsal with more ranks than GPUs reports its GPUs as n_gpus,
@@ -751,7 +767,7 @@ def main() -> None:
     if plan is not None:
         cmd, env = plan
         log(f"launching {args.gpus} ranks: {' '.join(cmd[:9])} ...")
-        raise SystemExit(subprocess.run(cmd, env=env).returncode)
+        raise SystemExit(relay_ranks(cmd, env))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -78,3 +78,14 @@ def test_cli_refuses_more_gpus_than_visible():
                        env={k: v for k, v in __import__("os").environ.items() if k != "WORLD_SIZE"})
     assert p.returncode == 2, p.stderr[-500:]
     assert "GPU" in p.stderr and p.stdout == ""
+
+
+def test_relay_keeps_only_the_json_line_on_stdout():
+    import io
+    script = ("print('[Gloo] Rank 0 is connected to 1 peer ranks.'); "
+              "print('{\"metric\": \"m\", \"value\": 1}'); import sys; sys.exit(3)")
+    out, err = io.StringIO(), io.StringIO()
+    rc = B.relay_ranks([sys.executable, "-c", script], dict(__import__("os").environ), out, err)
+    assert rc == 3
+    assert out.getvalue() == '{"metric": "m", "value": 1}\n'
+    assert "[Gloo]" in err.getvalue()

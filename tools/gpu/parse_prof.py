@@ -13,14 +13,16 @@ NAMES = ["setup", "begin_mb", "mb_syntax", "motion", "cbp_qp", "residual", "end_
 v = scene.VideoScorer(sys.argv[1], device=0, decoder="general")
 v.run()
 torch.cuda.synchronize()
-fn = _lib.lib().vts_debug_parse_prof
+fn = getattr(_lib.lib(), "vts_debug_parse_prof", None)
+if fn is None:
+    sys.exit("this libvtseg.so is not a VTS_EXP_PROF build (tools/exp/build_full_variants.sh prof:-DVTS_EXP_PROF)")
 fn.argtypes = [C.c_void_p]
 out = (C.c_ulonglong * 8)()
 fn(out)           # reset after the first run
 v.run()
 torch.cuda.synchronize()
 fn(out)
-tot = sum(out)
+tot = sum(out) or 1  # an all-zero read: no instrumented kernel ran
 print(json.dumps({"video": sys.argv[1], "timings": v.timings(),
                   "sections": {n: [int(x), round(x / tot, 4)] for n, x in zip(NAMES, out)}}))
 v.close()

@@ -50,6 +50,32 @@ __device__ unsigned long long vts_prof_acc[8];
   } while (0)
 #endif
 #endif
+#ifdef VTS_EXP_RPROF
+// reconstruction section timing (experiment builds): per-wave s_memtime deltas
+// of h264_deblock_full [0, 8) and h264_intra_full [8, 16), summed over every
+// wave; read with vts_debug_recon_prof
+__device__ unsigned long long vts_rprof_acc[16];
+#define RPROF_DECL                                  \
+  uint64_t rp_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  uint64_t rp_t_ = __builtin_amdgcn_s_memtime()
+#define RPROF(k)                                          \
+  do {                                                    \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+    rp_acc_[k] += t_ - rp_t_;                             \
+    rp_t_ = t_;                                           \
+  } while (0)
+#define RPROF_COUNT(k, n) (rp_acc_[k] += (n))
+#define RPROF_FLUSH(base)                                                   \
+  do {                                                                      \
+    if ((threadIdx.x & 63) == 0)                                            \
+      for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&vts_rprof_acc[(base) + k_], rp_acc_[k_]); \
+  } while (0)
+#else
+#define RPROF_DECL
+#define RPROF(k)
+#define RPROF_COUNT(k, n)
+#define RPROF_FLUSH(base)
+#endif
 #include "parse_cabac.h"
 #include "parse_full.h"
 #include "recon_full.h"
@@ -1021,6 +1047,7 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;
+  RPROF_DECL;
   if (tid == 0) s_max = -1;
   if (tid < 9 * 16) s_off4[tid] = static_cast<uint8_t>(intra4_off(tid >> 4, tid & 3, (tid >> 2) & 3));
   for (int i = tid; i < 9 * 64; i += kIntraThreads) s_off8[i] = static_cast<uint8_t>(intra8_off(i >> 6, i & 7, (i >> 3) & 7));
@@ -1058,6 +1085,7 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
     }
     __syncthreads();
   }
+  RPROF(0);
   for (int l = 0; l <= maxl; ++l) {
     int j0, j1;
     if (bucketed) {
@@ -1072,9 +1100,16 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
       j0 = 0;
       j1 = s_cnt;
     }
-    for (int j = j0 + ms; j < j1; j += kIntraSlots) intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4, s_off8);
+    for (int j = j0 + ms; j < j1; j += kIntraSlots) {
+      intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4, s_off8);
+      RPROF_COUNT(7, 1);
+    }
+    RPROF(1);
     __syncthreads();
+    RPROF(2);
+    RPROF_COUNT(6, 1);
   }
+  RPROF_FLUSH(8);
 }
 
 // --------------------------------------------------------------- deblocking
@@ -1293,6 +1328,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
   const int ia = min(max(l - 24, 0), 5);  // rows-above lane: luma rows -4..-1, chroma rows -2..-1
   DbkTile &t = tiles[wave * 2 + half];
   const int npairs = (mbh + 1) >> 1;
+  RPROF_DECL;
   for (int p = wave; p < npairs; p += kDbkWaves) {
     const int y = 2 * p + half;
     const bool row_ok = y < mbh;
@@ -1327,6 +1363,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
           __builtin_amdgcn_s_sleep(1);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      RPROF(0);
       const bool on = act && !((D.qp >> 24) & 1);  // disable_deblocking_filter_idc != 1
       const int qpq = D.qp & 255, qpl = (D.qp >> 8) & 255, qpt = (D.qp >> 16) & 255;
       const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
@@ -1381,6 +1418,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
       if (act && l >= 24 && l < 30 && y > 0)
         *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = above;
       lane_sync();
+      RPROF(1);
       // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved chroma column l - 16
       if (on) {
         if (l < 16) {
@@ -1424,6 +1462,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
         }
       }
       lane_sync();
+      RPROF(2);
       // ---- write back: rows of this macroblock shifted 4 bytes left (the left
       // neighbour's last columns are final now), rows above, the row's tail
       if (act) {
@@ -1445,12 +1484,23 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
       __builtin_amdgcn_wave_barrier();
       if (act && l == 0)
         __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      RPROF(3);
+      RPROF_COUNT(7, 1);
     }
   }
+  RPROF(4);
+  RPROF_FLUSH(0);
 }
 
 }  // namespace
 
+#ifdef VTS_EXP_RPROF
+extern "C" int vts_debug_recon_prof(unsigned long long *out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_rprof_acc), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(vts_rprof_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef VTS_EXP_PROF
 extern "C" int vts_debug_parse_prof(unsigned long long *out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_prof_acc), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
