@@ -645,6 +645,7 @@ def run_single(path: Path, *, gpu: int, k: int, steps: int, threads: int, label:
         rec = {"label": label, "frames": F, "width": W, "height": H, "steps": steps,
                "value": round(F * steps / el, 1), "unit": "frames/s",
                "ms_per_step": round(el / steps * 1e3, 3), "open_s": round(open_s, 3),
+               "open_stages_ms": {k: round(x, 1) for k, x in v.open_timings().items()},
                "decoder": "general" if v.general() else "subset",
                "stage_ms": v.timings(), "recon_launches": v.recon_launches(),
                "windows": v.windows(),
@@ -685,6 +686,7 @@ def e2e_record(paths: list[Path], gpu: int) -> dict:
         t0 = time.perf_counter()
         v = scene.VideoScorer(p, device=gpu)
         t1 = time.perf_counter()
+        open_stages = {k: round(x, 1) for k, x in v.open_timings().items()}
         v.run()
         t2 = time.perf_counter()
         cuts = v.scene_cuts()
@@ -692,7 +694,8 @@ def e2e_record(paths: list[Path], gpu: int) -> dict:
         v.boundary_frames([0.0, float(v.info.duration)])
         t3 = time.perf_counter()
         v.close()
-        stages = {"open_ms": round((t1 - t0) * 1e3, 1), "decode_score_ms": round((t2 - t1) * 1e3, 1),
+        stages = {"open_ms": round((t1 - t0) * 1e3, 1), "open_stages_ms": open_stages,
+                  "decode_score_ms": round((t2 - t1) * 1e3, 1),
                   "results_ms": round((t3 - t2) * 1e3, 2), "scene_cuts": len(cuts),
                   "input_bytes": Path(p).stat().st_size,
                   "upload_inclusive_GBps": round(Path(p).stat().st_size / (t1 - t0) / 1e9, 2)}

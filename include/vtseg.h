@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTS_ABI_VERSION 5
+#define VTS_ABI_VERSION 6
 
 enum {
   VTS_OK = 0,
@@ -302,6 +302,13 @@ int vts_get_thumbnail_rgb(vts_ctx *ctx, int64_t frame, uint8_t *out,
 /* Timing of the last vts_run/vts_score, milliseconds, HIP events:
  * [0] whole, [1] parse, [2] reconstruct, [3] score. */
 int vts_last_timings(const vts_ctx *ctx, double *ms4);
+/* Host time of the vts_open that made ctx, milliseconds, by stage:
+ * [0] demux (moov) + device checks, [1] unused, [2] sample read (parallel
+ * pread), [3] host decode schedule, [4] device allocations (+ the general
+ * decoder's set-up kernels), [5] wait for the elementary-stream upload (it
+ * runs on its own thread beside [3] and [4]), [6] the rest, [7] total.
+ * Writes min(cap, 8) entries; returns 8. */
+int vts_open_timings(const vts_ctx *ctx, double *ms, int32_t cap);
 /* Decode schedule facts: what = 0 reconstruct launches per run, 1 windows,
  * 2 slices, 3 ring frames, 4 fused scoring (1/0); < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);  /* 8: general decoder in use (1/0) */

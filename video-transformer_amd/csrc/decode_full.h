@@ -39,8 +39,16 @@ struct DbkInfo {
   uint32_t qp;      // QPq | QPleft << 8 | QPtop << 16 (I_PCM: 0) | (disable_deblocking_filter_idc == 1) << 24
   int32_t fa, fb;   // FilterOffsetA / B of the macroblock's slice
   uint32_t _pad;
+  // Each edge's filter parameters (8.7.2.2, Tables 8-16 / 8-17), resolved by
+  // h264_bs_full so the deblocking wavefront reads them instead of deriving
+  // them per lane: alpha | beta << 8 | tC0(bS 1, 2, 3) << 16, 21, 26 of the
+  // edge's indexA / indexB, 0 when alpha or beta is 0 (the edge never filters).
+  uint32_t lv[4];   // luma vertical edges 0..3
+  uint32_t lh[4];   // luma horizontal edges 0..3
+  uint32_t cv[4];   // chroma vertical: (edge 0, Cb), (edge 0, Cr), (edge 2, Cb), (edge 2, Cr)
+  uint32_t ch[4];   // chroma horizontal, the same order
 };
-static_assert(sizeof(DbkInfo) == 32, "DbkInfo layout");
+static_assert(sizeof(DbkInfo) == 96, "DbkInfo layout");
 
 struct FullReconArgs {
   const int4 *frames;        // (slot, -, -, -) per picture of the launch

@@ -1226,6 +1226,15 @@ __device__ __forceinline__ int dbk_bs(const DbkInfo &d, int dir, int e, int seg)
   return (d.bs[dir * 2 + (e >> 1)] >> (((e & 1) * 4 + seg) * 4)) & 15;
 }
 
+// the packed parameters of an edge whose average QP is qpav (DbkInfo::lv)
+__device__ __forceinline__ uint32_t edge_word(int qpav, int fa, int fb) {
+  const int ia = min(max(qpav + fa, 0), 51), ib = min(max(qpav + fb, 0), 51);
+  const uint32_t alpha = kAl[ia], beta = kBe[ib];
+  if (!alpha || !beta) return 0u;
+  return alpha | beta << 8 | static_cast<uint32_t>(kTc[ia][0]) << 16 | static_cast<uint32_t>(kTc[ia][1]) << 21 |
+         static_cast<uint32_t>(kTc[ia][2]) << 26;
+}
+
 // grid (ceil(nmb / 16), pictures): 16 lanes per macroblock, lane = raster
 // 4x4 block b, which derives the bS of the vertical edge on its left and of
 // the horizontal edge above it (8.7.2.1); the macroblock's 32 nibbles meet in
@@ -1280,14 +1289,32 @@ __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
   for (int m = 1; m < 16; m <<= 1)
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(w[i]), m, 16));
-  if (!ok || b > 1) return;
+  if (!ok || b > 5) return;
   DbkInfo *o = a.dbk + static_cast<int64_t>(slot) * nmb + mb;
+  const int qpq = tq == kMbPcm ? 0 : hq.qp;
   if (b == 0) {
     reinterpret_cast<uint4 *>(o)[0] = make_uint4(w[0], w[1], w[2], w[3]);
-  } else {
-    const uint32_t qp = static_cast<uint32_t>(tq == kMbPcm ? 0 : hq.qp) | (static_cast<uint32_t>(qpl) << 8) |
+  } else if (b == 1) {
+    const uint32_t qp = static_cast<uint32_t>(qpq) | (static_cast<uint32_t>(qpl) << 8) |
                         (static_cast<uint32_t>(qpt) << 16) | (idc == 1 ? 1u << 24 : 0u);
     reinterpret_cast<uint4 *>(o)[1] = make_uint4(qp, static_cast<uint32_t>(sd.dbk_a), static_cast<uint32_t>(sd.dbk_b), 0u);
+  } else {
+    // edge parameter words: lanes 2 / 3 luma vertical / horizontal, 4 / 5 chroma
+    const bool horiz = (b & 1) != 0;
+    const int qpp = horiz ? qpt : qpl;  // the macroblock across edge 0
+    uint32_t e4[4];
+    if (b < 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) e4[e] = edge_word(e ? qpq : (qpp + qpq + 1) >> 1, sd.dbk_a, sd.dbk_b);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int off = (k & 1) ? a.P.cqp_off2 : a.P.cqp_off;
+        const int cq = full::qpc_of(qpq, off);
+        e4[k] = edge_word(k < 2 ? (full::qpc_of(qpp, off) + cq + 1) >> 1 : cq, sd.dbk_a, sd.dbk_b);
+      }
+    }
+    reinterpret_cast<uint4 *>(o)[b] = make_uint4(e4[0], e4[1], e4[2], e4[3]);
   }
 }
 
@@ -1492,6 +1519,288 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
   RPROF_FLUSH(0);
 }
 
+
+// ---- deblocking, LDS hand-off (default; VTS_DBK=1 runs h264_deblock_full)
+// The same wavefront as h264_deblock_full (a wave per macroblock-row pair,
+// the lower row two macroblocks behind), but the rows a macroblock's top edge
+// reads from the row above (luma rows 12..15, chroma rows 6..7) pass between
+// rows through a ring in LDS instead of HBM: the producer row writes them
+// while its pixels are still in the tile, the consumer row copies them into
+// its tile after the progress counter allows it.  Global memory carries no
+// hand-off, so no step waits for another wave's global stores or issues a
+// dependent global load (in h264_deblock_full the row-above load sat between
+// the progress wait and the horizontal edges of every step).  Every byte of
+// the picture has one writer: a row stores its own rows 0..12 (chroma 0..6)
+// and the row below stores rows 13..15 (chroma 7) after its top edge (the
+// picture's last row stores all of its rows).  Edge parameters come resolved
+// from h264_bs_full (DbkInfo::lv ... ch).
+// Ring: kDbkRingRows row slots (a row and the row 2 x kDbkWaves below share
+// one; the later waits for the earlier's consumer to finish) of kDbkRingCols
+// macroblock columns; a producer waits for its consumer to be within
+// kDbkRingCols - 1 columns before it overwrites one.
+constexpr int kDbkRingRows = 2 * kDbkWaves;
+constexpr int kDbkRingCols = 32;
+struct DbkLine {  // luma rows 12..15, chroma rows 6..7 (interleaved) of one macroblock
+  uint8_t y[4][16];
+  uint8_t c[2][16];
+};
+
+__device__ __forceinline__ void filt_luma_w(int (&s)[8], int bS, uint32_t w) {
+  const int alpha = w & 255, beta = (w >> 8) & 255;
+  const int p0 = s[3], p1 = s[2], q0 = s[4], q1 = s[5];
+  if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+  const int p2 = s[1], q2 = s[6];
+  const int ap = abs(p2 - p0), aq = abs(q2 - q0);
+  if (bS < 4) {
+    const int tc0 = (w >> (11 + 5 * bS)) & 31;
+    const int tc = tc0 + (ap < beta) + (aq < beta);
+    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
+    s[3] = c255(p0 + delta);
+    s[4] = c255(q0 - delta);
+    if (ap < beta) s[2] = p1 + min(max((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0), tc0);
+    if (aq < beta) s[5] = q1 + min(max((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0), tc0);
+    return;
+  }
+  const int p3 = s[0], q3 = s[7];
+  const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
+  if (ap < beta && small) {
+    s[3] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+    s[2] = (p2 + p1 + p0 + q0 + 2) >> 2;
+    s[1] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+  } else {
+    s[3] = (2 * p1 + p0 + q1 + 2) >> 2;
+  }
+  if (aq < beta && small) {
+    s[4] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+    s[5] = (p0 + q0 + q1 + q2 + 2) >> 2;
+    s[6] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+  } else {
+    s[4] = (2 * q1 + q0 + p1 + 2) >> 2;
+  }
+}
+__device__ __forceinline__ void filt_chroma_w(int &p1, int &p0, int &q0, int &q1, int bS, uint32_t w) {
+  const int alpha = w & 255, beta = (w >> 8) & 255;
+  if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+  if (bS < 4) {
+    const int tc = ((w >> (11 + 5 * bS)) & 31) + 1;
+    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
+    const int np0 = c255(p0 + delta), nq0 = c255(q0 - delta);
+    p0 = np0;
+    q0 = nq0;
+    return;
+  }
+  const int np0 = (2 * p1 + p0 + q1 + 2) >> 2, nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
+  p0 = np0;
+  q0 = nq0;
+}
+__device__ __forceinline__ uint32_t u4_at(const uint4 &v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// grid: pictures of the level
+__global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a) {
+  __shared__ DbkTile tiles[kDbkWaves * 2];
+  __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
+  __shared__ DbkLine ring[kDbkRingRows][kDbkRingCols];
+  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
+  const int slot = a.frames[blockIdx.x].x;
+  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
+  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
+  uint8_t *UV = Y + a.uv_off;
+  const int pitch = a.pitch;
+  for (int i = threadIdx.x; i < mbh; i += kDbkThreads) prog[i] = 0;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int half = lane >> 5, l = lane & 31;
+  const bool lrow = l < 24, luma = l < 16;
+  // V phase: luma row l / chroma row l - 16 (lanes 24..31: chroma row 7,
+  // addressed only by the clamped prefetch)
+  const int row = luma ? l : min(l - 16, 7);
+  const int ia = min(max(l - 24, 0), 5);  // rows-above lane: luma rows -4..-1, chroma rows -2..-1
+  DbkTile &t = tiles[wave * 2 + half];
+  // which edge-parameter quad this lane reads: vertical pass by its row kind,
+  // horizontal pass by its column kind (lanes 16..31 = chroma columns)
+  const int vq = luma ? 2 : 4, hq = l < 16 ? 3 : 5;
+  const int npairs = (mbh + 1) >> 1;
+  RPROF_DECL;
+  for (int p = wave; p < npairs; p += kDbkWaves) {
+    const int y = 2 * p + half;
+    const bool row_ok = y < mbh;
+    const int ya = row_ok ? y : mbh - 1;
+    const bool last_row = y == mbh - 1;
+    const int rs = y % kDbkRingRows, rsa = (y + kDbkRingRows - 1) % kDbkRingRows;
+    const int64_t yrow = static_cast<int64_t>(ya * 16) * pitch, crow = static_cast<int64_t>(ya * 8) * pitch;
+    uint8_t *const rowp = (luma ? Y + yrow : UV + crow) + static_cast<int64_t>(row) * pitch;
+    const DbkInfo *const drow = fdbk + ya * mbw;
+    // this row's ring slot was the row kDbkRingRows above's: its consumer must be done
+    if (row_ok && y >= kDbkRingRows) {
+      while (__hip_atomic_load(&prog[y - kDbkRingRows + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < mbw + 1)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    uint32_t left = 0;  // carried cols 12..15 of the previous macroblock (this lane's row)
+    // the next iteration's macroblock: bS words, the lane's edge parameters, its row
+    const uint4 *dq = reinterpret_cast<const uint4 *>(drow);
+    uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
+    uint4 npx = *reinterpret_cast<const uint4 *>(rowp);
+    for (int it = 0; it < mbw + 2; ++it) {
+      const int x = it - 2 * half;
+      const bool act = row_ok && x >= 0 && x < mbw;
+      const uint4 bsw = nbs, pv = nv, ph = nh, q4 = npx;
+      {
+        const int xn = min(max(x + 1, 0), mbw - 1);
+        const uint4 *dn = reinterpret_cast<const uint4 *>(drow + xn);
+        nbs = dn[0];
+        nv = dn[vq];
+        nh = dn[hq];
+        npx = *reinterpret_cast<const uint4 *>(rowp + xn * 16);
+      }
+      // the upper row of the pair waits for the row above (another wave); a
+      // row whose consumer is another wave waits until it may overwrite ring
+      // column x (the consumer read column x - kDbkRingCols)
+      if (act) {
+        const int need_up = (half == 0 && y > 0) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
+        const int need_dn = (half == 1 && y + 1 < mbh) ? x - kDbkRingCols + 1 : -(1 << 30);
+        const int *pu = &prog[y > 0 ? y - 1 : 0], *pd = &prog[y + 1 < mbh ? y + 1 : y];
+        while (__hip_atomic_load(pu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_up ||
+               __hip_atomic_load(pd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_dn)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      RPROF(0);
+      const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
+      // rows above from the ring (final: the row above is two macroblocks ahead)
+      if (act && l >= 24 && l < 30 && y > 0) {
+        const DbkLine &L = ring[rsa][x & (kDbkRingCols - 1)];
+        const uint4 v = ia < 4 ? *reinterpret_cast<const uint4 *>(&L.y[ia][0]) : *reinterpret_cast<const uint4 *>(&L.c[ia - 4][0]);
+        *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = v;
+      }
+      // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
+      if (act && lrow) {
+        const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
+        int r[20];
+#pragma unroll
+        for (int i = 0; i < 20; ++i) r[i] = (wv[i >> 2] >> ((i & 3) * 8)) & 255;
+        if (luma) {
+          const int seg = row >> 2;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int bS = (u4_at(bsw, e >> 1) >> (((e & 1) * 4 + seg) * 4)) & 15;
+            if (!bS) continue;
+            int s8[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s8[i] = r[4 * e + i];
+            filt_luma_w(s8, bS, u4_at(pv, e));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[4 * e + i] = s8[i];
+          }
+        } else {
+          const int seg = row >> 1;
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int bS = (u4_at(bsw, e >> 1) >> seg * 4) & 15;
+            if (!bS) continue;
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl) {
+              const int c0 = 4 + 2 * (2 * e) + pl;  // q0 of chroma col 2e (luma edge e)
+              filt_chroma_w(r[c0 - 4], r[c0 - 2], r[c0], r[c0 + 2], bS, u4_at(pv, e + pl));
+            }
+          }
+        }
+        uint8_t *dst = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+          *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+      }
+      lane_sync();
+      RPROF(1);
+      // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved chroma column l - 16
+      if (act) {
+        if (l < 16) {
+          const int col = l, seg = col >> 2;
+          int r[20];
+#pragma unroll
+          for (int i = 0; i < 20; ++i) r[i] = t.y[i][4 + col];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int bS = (u4_at(bsw, 2 + (e >> 1)) >> (((e & 1) * 4 + seg) * 4)) & 15;
+            if (!bS) continue;
+            int s8[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s8[i] = r[4 * e + i];
+            filt_luma_w(s8, bS, u4_at(ph, e));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[4 * e + i] = s8[i];
+          }
+#pragma unroll
+          for (int i = 1; i < 20; ++i) t.y[i][4 + col] = static_cast<uint8_t>(r[i]);
+        } else {
+          const int j = l - 16, pl = j & 1, cc = j >> 1, seg = cc >> 1;
+          int r[10];
+#pragma unroll
+          for (int i = 0; i < 10; ++i) r[i] = t.c[i][4 + j];
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int bS = (u4_at(bsw, 2 + (e >> 1)) >> seg * 4) & 15;
+            if (!bS) continue;
+            const int q0 = 2 + 2 * e;  // chroma row 2e
+            filt_chroma_w(r[q0 - 2], r[q0 - 1], r[q0], r[q0 + 1], bS, u4_at(ph, e + pl));
+          }
+#pragma unroll
+          for (int i = 1; i < 10; ++i) t.c[i][4 + j] = static_cast<uint8_t>(r[i]);
+        }
+      }
+      lane_sync();
+      RPROF(2);
+      // ---- write back: this macroblock's rows shifted 4 bytes left (the left
+      // neighbour's last columns are final now) except the ones the row below
+      // finishes (luma 13..15, chroma 7), the ring lines for the row below,
+      // the rows above this macroblock that its top edge finished
+      if (act) {
+        if (lrow) {
+          const uint8_t *src = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
+          const uint32_t w0 = *reinterpret_cast<const uint32_t *>(src), w1 = *reinterpret_cast<const uint32_t *>(src + 4);
+          const uint32_t w2 = *reinterpret_cast<const uint32_t *>(src + 8), w3 = *reinterpret_cast<const uint32_t *>(src + 12);
+          left = *reinterpret_cast<const uint32_t *>(src + 16);
+          const bool mine = last_row || (luma ? row < 13 : row < 7);
+          if (mine) {
+            uint8_t *dst = rowp + x * 16;
+            if (x > 0) *reinterpret_cast<uint32_t *>(dst - 4) = w0;
+            *reinterpret_cast<uint32_t *>(dst) = w1;
+            *reinterpret_cast<uint32_t *>(dst + 4) = w2;
+            *reinterpret_cast<uint32_t *>(dst + 8) = w3;
+            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
+          }
+          const int lr = luma ? row - 12 : row - 6;  // ring line of this lane's row
+          if (!last_row && lr >= 0) {
+            uint8_t *cur = luma ? &ring[rs][x & (kDbkRingCols - 1)].y[lr][0] : &ring[rs][x & (kDbkRingCols - 1)].c[lr][0];
+            if (x > 0) {
+              uint8_t *prv = luma ? &ring[rs][(x - 1) & (kDbkRingCols - 1)].y[lr][0]
+                                  : &ring[rs][(x - 1) & (kDbkRingCols - 1)].c[lr][0];
+              *reinterpret_cast<uint32_t *>(prv + 12) = w0;
+            }
+            *reinterpret_cast<uint32_t *>(cur) = w1;
+            *reinterpret_cast<uint32_t *>(cur + 4) = w2;
+            *reinterpret_cast<uint32_t *>(cur + 8) = w3;
+            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = left;
+          }
+        } else if (l < 28 && y > 0) {
+          const int i = l - 24;  // luma rows -3..-1, chroma row -1 of the macroblock above
+          if (i < 3) *reinterpret_cast<uint4 *>(Y + ybase + static_cast<int64_t>(i - 3) * pitch) = *reinterpret_cast<const uint4 *>(&t.y[1 + i][4]);
+          else *reinterpret_cast<uint4 *>(UV + cbase - pitch) = *reinterpret_cast<const uint4 *>(&t.c[1][4]);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      if (act && l == 0)
+        __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      RPROF(3);
+      RPROF_COUNT(7, 1);
+    }
+  }
+  RPROF(4);
+  RPROF_FLUSH(0);
+}
+
 }  // namespace
 
 #ifdef VTS_EXP_RPROF
@@ -1548,10 +1857,14 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   hipLaunchKernelGGL(h264_intra_full, dim3(n_frames), dim3(kIntraThreads), sizeof(uint16_t) * nmb, s, a);
   e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_intra_full launch: %s", hipGetErrorString(e));
-  if (a.deblock) {
+  if (a.deblock == 1) {
     hipLaunchKernelGGL(h264_deblock_full, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));
+  } else if (a.deblock) {
+    hipLaunchKernelGGL(h264_deblock_lds, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_lds launch: %s", hipGetErrorString(e));
   }
   return VTS_OK;
 }

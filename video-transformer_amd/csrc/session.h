@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -56,6 +58,31 @@ struct SmallStore {
   int32_t tl = 1, tc = 1;       // luma / chroma normalisers
 };
 
+}  // namespace vts
+
+namespace vts {
+// Host bytes without value-initialisation (a std::vector zero-fills every
+// byte of a multi-GB elementary stream before the read overwrites it)
+struct HostBytes {
+  HostBytes() = default;
+  HostBytes(const HostBytes &) = delete;
+  HostBytes &operator=(const HostBytes &) = delete;
+  ~HostBytes() { std::free(p_); }
+  bool alloc(int64_t n) {
+    std::free(p_);
+    p_ = static_cast<uint8_t *>(std::malloc(static_cast<size_t>(std::max<int64_t>(n, 1))));
+    n_ = p_ ? n : 0;
+    return p_ != nullptr;
+  }
+  uint8_t *data() { return p_; }
+  const uint8_t *data() const { return p_; }
+  size_t size() const { return static_cast<size_t>(n_); }
+  uint8_t operator[](size_t i) const { return p_[i]; }
+
+ private:
+  uint8_t *p_ = nullptr;
+  int64_t n_ = 0;
+};
 }  // namespace vts
 
 struct vts_ctx {
@@ -121,6 +148,12 @@ struct vts_ctx {
   std::vector<hipEvent_t> lev;  // per window: (start, end) per reconstruct launch, then one per parse chunk
   hipEvent_t ev_start = nullptr, ev_end = nullptr;
   double timings[4] = {0, 0, 0, 0};
+  // host time of vts_open by stage (ms, vts_open_timings): 0 demux (moov),
+  // 1 device checks, 2 sample read, 3 host schedule, 4 device allocations,
+  // 5 elementary-stream upload, 6 other uploads and set-up kernels, 7 total
+  double open_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double open_t = 0;  // seconds (steady clock) of the last lap
+  void open_lap(int k);
   int64_t last_window_done = -1;
   // command epochs: run_no counts window runs; a ring is cleared on first use
   // and again before an epoch value could repeat (h264.h kCmdEpochs)
@@ -147,6 +180,7 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
+  int dbk_kernel = 2;                   // 2: h264_deblock_lds; VTS_DBK=1: h264_deblock_full
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
@@ -166,12 +200,12 @@ int run_all(vts_ctx *c);
 int fetch_scores(vts_ctx *c);
 // general decoder: schedule + buffers from the host ES (session_full.hip);
 // `sps_nal` / `pps_nal` are the avcC parameter sets
-int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
                   const std::vector<uint32_t> &sizes, int nal_length_size, const std::vector<uint8_t> &sps_nal,
                   const std::vector<uint8_t> &pps_nal);
 int run_general(vts_ctx *c);
 // cheap look at the stream's first pictures: does it need the general decoder?
-bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+bool wants_general(const vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
                    const std::vector<uint32_t> &sizes, int nal_length_size);
 // downscale the window's frames (transcode.hip)
 int small_window(vts_ctx *c, int ring, int64_t f0, int64_t f1, hipStream_t s);

@@ -19,13 +19,19 @@
 // overlaps scoring of window i).
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "bitstream.h"
@@ -81,46 +87,155 @@ void stream_give(int device, hipStream_t s) {  // s idle
 
 namespace {
 
-// Read the sample bytes of the track into one contiguous host buffer.
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Read the sample bytes of the track into one contiguous host buffer (the
+// elementary stream, uninitialised memory: no zero-fill pass).  Consecutive
+// samples that are also consecutive in the file (a video-only mdat; the video
+// runs between audio chunks otherwise) are one file range; ranges are cut into
+// pieces of <= kReadPiece bytes that kReadThreads threads pread at once (a
+// cached file copies at memory bandwidth per thread, one sequential reader was
+// the open's largest stage).
+constexpr int64_t kReadPiece = 8ll << 20;
+constexpr int kReadThreads = 8;
+
 int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size, const char *path,
-                   std::vector<uint8_t> *es, std::vector<int64_t> *es_off) {
+                   HostBytes *es, std::vector<int64_t> *es_off) {
   int64_t total = 0;
   for (uint32_t s : t.size) total += s;
-  es->resize(static_cast<size_t>(total + kPad), 0);
+  es->alloc(total + kPad);
+  std::memset(es->data() + total, 0, kPad);
   es_off->resize(t.size.size());
-  FILE *f = nullptr;
-  if (!mem) {
-    f = std::fopen(path, "rb");
-    if (!f) return fail(VTS_E_IO, "cannot open %s", path);
-  }
+  struct Piece {
+    int64_t file, dst, n;
+  };
+  std::vector<Piece> pieces;
   int64_t pos = 0;
   for (size_t i = 0; i < t.size.size(); ++i) {
     (*es_off)[i] = pos;
     const int64_t off = t.offset[i], n = t.size[i];
-    if (mem) {
-      if (off < 0 || off + n > mem_size) return fail(VTS_E_FORMAT, "sample %zu out of file", i);
-      std::memcpy(es->data() + pos, mem + off, static_cast<size_t>(n));
-    } else {
-      if (fseeko(f, off, SEEK_SET) != 0 ||
-          std::fread(es->data() + pos, 1, static_cast<size_t>(n), f) != static_cast<size_t>(n)) {
-        std::fclose(f);
-        return fail(VTS_E_FORMAT, "cannot read sample %zu", i);
-      }
-    }
+    if (off < 0 || (mem && off + n > mem_size)) return fail(VTS_E_FORMAT, "sample %zu out of file", i);
+    if (!pieces.empty() && pieces.back().file + pieces.back().n == off && pieces.back().n + n <= kReadPiece)
+      pieces.back().n += n;
+    else
+      pieces.push_back(Piece{off, pos, n});
     pos += n;
   }
-  if (f) std::fclose(f);
+  if (pieces.empty()) return VTS_OK;
+  int fd = -1;
+  if (!mem) {
+    fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return fail(VTS_E_IO, "cannot open %s", path);
+  }
+  std::atomic<size_t> next{0};
+  std::atomic<int64_t> bad{-1};
+  auto worker = [&]() {
+    for (size_t k = next++; k < pieces.size() && bad.load() < 0; k = next++) {
+      const Piece &pc = pieces[k];
+      uint8_t *dst = es->data() + pc.dst;
+      if (mem) {
+        std::memcpy(dst, mem + pc.file, static_cast<size_t>(pc.n));
+        continue;
+      }
+      int64_t done = 0;
+      while (done < pc.n) {
+        const ssize_t r = ::pread(fd, dst + done, static_cast<size_t>(pc.n - done), pc.file + done);
+        if (r <= 0) {
+          bad = pc.dst + done;
+          break;
+        }
+        done += r;
+      }
+    }
+  };
+  const int nt = static_cast<int>(std::min<size_t>(kReadThreads, pieces.size()));
+  std::vector<std::thread> th;
+  for (int i = 1; i < nt; ++i) th.emplace_back(worker);
+  worker();
+  for (auto &x : th) x.join();
+  if (fd >= 0) ::close(fd);
+  if (bad.load() >= 0) {
+    size_t i = 0;
+    while (i + 1 < es_off->size() && (*es_off)[i + 1] <= bad.load()) ++i;
+    return fail(VTS_E_FORMAT, "cannot read sample %zu", i);
+  }
   return VTS_OK;
 }
 
+// Elementary-stream upload: host bytes -> a ring of pinned staging buffers
+// (process-wide, allocated once) -> hipMemcpyAsync into HBM, so the copy into
+// a staging slot overlaps the DMA of the previous one (a pageable hipMemcpy
+// stages internally, one small chunk at a time, synchronously).  Runs on its
+// own thread beside the host schedule (EsUpload).
+constexpr int64_t kStageBytes = 16ll << 20;
+constexpr int kStageSlots = 4;
+std::mutex g_stage_mu;
+uint8_t *g_stage[kStageSlots] = {nullptr, nullptr, nullptr, nullptr};
+
+int upload_es(int device, uint8_t *d_es, const uint8_t *host, int64_t n) {
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  HIP_TRY(hipSetDevice(device));
+  if (n <= kStageBytes) {  // small: one synchronous copy
+    HIP_TRY(hipMemcpy(d_es, host, static_cast<size_t>(n), hipMemcpyHostToDevice));
+    return VTS_OK;
+  }
+  for (int i = 0; i < kStageSlots; ++i)
+    if (!g_stage[i]) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&g_stage[i]), kStageBytes, hipHostMallocDefault));
+  hipStream_t s = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t ev[kStageSlots] = {};
+  int rc = VTS_OK;
+  for (int i = 0; i < kStageSlots && rc == VTS_OK; ++i)
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) rc = fail(VTS_E_HIP, "hipEventCreate");
+  for (int64_t off = 0, k = 0; off < n && rc == VTS_OK; off += kStageBytes, ++k) {
+    const int slot = static_cast<int>(k % kStageSlots);
+    if (k >= kStageSlots && hipEventSynchronize(ev[slot]) != hipSuccess) {
+      rc = fail(VTS_E_HIP, "staging event");
+      break;
+    }
+    const int64_t len = std::min(kStageBytes, n - off);
+    std::memcpy(g_stage[slot], host + off, static_cast<size_t>(len));
+    if (hipMemcpyAsync(d_es + off, g_stage[slot], static_cast<size_t>(len), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipEventRecord(ev[slot], s) != hipSuccess)
+      rc = fail(VTS_E_HIP, "elementary-stream upload");
+  }
+  if (hipStreamSynchronize(s) != hipSuccess && rc == VTS_OK) rc = fail(VTS_E_HIP, "elementary-stream upload");
+  for (auto e : ev)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(s);
+  return rc;
+}
+
+// upload_es on a thread of its own: started once the ES is read and its device
+// buffer allocated, joined before the first device work that reads it; the
+// host schedule runs meanwhile
+struct EsUpload {
+  std::thread th;
+  int rc = VTS_OK;
+  std::string msg;
+  void start(int device, uint8_t *d_es, const uint8_t *host, int64_t n) {
+    th = std::thread([this, device, d_es, host, n]() {
+      rc = upload_es(device, d_es, host, n);
+      if (rc != VTS_OK) msg = last_error();
+    });
+  }
+  int join() {
+    if (th.joinable()) th.join();
+    if (rc != VTS_OK) return fail(rc, "%s", msg.c_str());
+    return VTS_OK;
+  }
+  ~EsUpload() {
+    if (th.joinable()) th.join();
+  }
+};
+
 // Device buffers of the general decoder (the ES is uploaded when host_es is
 // given, else already resident).
-int alloc_general(vts_ctx *c, const uint8_t *host_es) {
+int alloc_general(vts_ctx *c) {
   HIP_TRY(hipSetDevice(c->device));
-  if (!c->d_es) {
-    HIP_TRY(hipMalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
-    HIP_TRY(hipMemcpy(c->d_es, host_es, static_cast<size_t>(c->es_bytes), hipMemcpyHostToDevice));
-  }
+  if (!c->d_es) return fail(VTS_E_INVALID, "elementary stream not resident");
   HIP_TRY(hipMalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
   if (!c->fslices.empty())
     HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
@@ -142,6 +257,7 @@ int alloc_general(vts_ctx *c, const uint8_t *host_es) {
   if (!c->pneed.empty())
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
   if (const char *e = std::getenv("VTS_PARSE_MERGE")) c->parse_merged = std::atoi(e) != 0;
+  if (const char *e = std::getenv("VTS_DBK")) c->dbk_kernel = std::atoi(e) == 1 ? 1 : 2;
   HIP_TRY(hipMalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
@@ -222,8 +338,8 @@ int switch_to_general(vts_ctx *c) {
   c->slices.clear();
   c->post_slots.clear();
   c->tb_chains.clear();
-  VTS_TRY(build_general(c, es, c->es_off, c->sample_size, c->nal_length_size, c->sps_nal, c->pps_nal));
-  return alloc_general(c, nullptr);
+  VTS_TRY(build_general(c, es.data(), c->es_off, c->sample_size, c->nal_length_size, c->sps_nal, c->pps_nal));
+  return alloc_general(c);
 }
 
 int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, const char *path) {
@@ -306,10 +422,17 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   if ((c->pps.weighted_pred || c->pps.weighted_bipred_idc) && c->params.decoder == 1)
     return fail(VTS_E_UNSUPPORTED, "weighted prediction needs the general decoder");
 
-  std::vector<uint8_t> es;
+  HostBytes es;
   std::vector<int64_t> es_off;
   VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off));
   c->es_bytes = static_cast<int64_t>(es.size());
+  c->open_lap(2);
+  // the ES goes to HBM on its own thread while the schedule below is built
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
+  EsUpload up;
+  up.start(c->device, c->d_es, es.data(), c->es_bytes);
+  c->open_lap(4);
   c->es_off = es_off;
   c->sample_size = t.size;
   c->nal_length_size = t.nal_length_size;
@@ -319,9 +442,14 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   // General CAVLC decoder (decode_full.hip) when asked, or when the headers
   // show features outside the subset kernels (deblocking, several references)
   if (c->params.decoder == 2 || reorder ||
-      (c->params.decoder == 0 && wants_general(c, es, es_off, t.size, t.nal_length_size))) {
-    VTS_TRY(build_general(c, es, es_off, t.size, t.nal_length_size, t.sps[0], t.pps[0]));
-    return alloc_general(c, es.data());
+      (c->params.decoder == 0 && wants_general(c, es.data(), es_off, t.size, t.nal_length_size))) {
+    VTS_TRY(build_general(c, es.data(), es_off, t.size, t.nal_length_size, t.sps[0], t.pps[0]));
+    c->open_lap(3);
+    VTS_TRY(up.join());
+    c->open_lap(5);
+    VTS_TRY(alloc_general(c));
+    c->open_lap(4);
+    return VTS_OK;
   }
 
   // NAL walk: slice table, intra / reference flags per frame
@@ -596,9 +724,8 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   }
 
   // ---- device allocations and uploads
+  c->open_lap(3);
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
-  HIP_TRY(hipMemcpy(c->d_es, es.data(), static_cast<size_t>(c->es_bytes), hipMemcpyHostToDevice));
   HIP_TRY(hipMalloc(&c->d_slices, sizeof(SliceDesc) * c->slices.size()));
   HIP_TRY(hipMemcpy(c->d_slices, c->slices.data(), sizeof(SliceDesc) * c->slices.size(),
                     hipMemcpyHostToDevice));
@@ -647,11 +774,14 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   for (auto &e2 : c->lev) HIP_TRY(hipEventCreate(&e2));
   HIP_TRY(hipEventCreate(&c->ev_start));
   HIP_TRY(hipEventCreate(&c->ev_end));
+  c->open_lap(4);
+  VTS_TRY(up.join());
+  c->open_lap(5);
   return VTS_OK;
 }
 
 int open_common(int device, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size,
-                const char *path, const vts_params *params, vts_ctx **out) {
+                const char *path, const vts_params *params, vts_ctx **out, double t_start) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return fail(VTS_E_NODEVICE, "no HIP device visible");
@@ -663,10 +793,14 @@ int open_common(int device, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_
     return fail(VTS_E_NODEVICE, "device %d is %s, not gfx950", device, prop.gcnArchName);
   vts_ctx *c = new vts_ctx;
   c->device = device;
+  c->open_t = t_start;
+  c->open_lap(0);
   if (params) c->params = *params;
   if (c->params.n_streams <= 0) c->params.n_streams = 2;
   if (c->params.cut_threshold <= 0) c->params.cut_threshold = 0.08f;
   const int rc = build(c, mp4, mem, mem_size, path);
+  c->open_lap(6);
+  for (int i = 0; i < 7; ++i) c->open_ms[7] += c->open_ms[i];
   if (rc != VTS_OK) {
     const std::string msg = last_error();
     vts_close(c);
@@ -949,11 +1083,12 @@ extern "C" int vts_open(int device, const char *path, const vts_params *params, 
   clear_error();
   if (!path || !out) return fail(VTS_E_INVALID, "NULL argument");
   *out = nullptr;
+  const double t0 = now_s();
   Mp4Info mp4;
   const std::string e = mp4_parse_file(path, &mp4);
   if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
   if (mp4.fragmented) return fail(VTS_E_UNSUPPORTED, "fragmented MP4 is not supported");
-  return open_common(device, mp4, nullptr, 0, path, params, out);
+  return open_common(device, mp4, nullptr, 0, path, params, out, t0);
 }
 
 extern "C" int vts_open_memory(int device, const uint8_t *data, int64_t size, const vts_params *params,
@@ -961,11 +1096,12 @@ extern "C" int vts_open_memory(int device, const uint8_t *data, int64_t size, co
   clear_error();
   if (!data || size <= 0 || !out) return fail(VTS_E_INVALID, "bad argument");
   *out = nullptr;
+  const double t0 = now_s();
   Mp4Info mp4;
   const std::string e = mp4_parse_memory(data, size, &mp4);
   if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
   if (mp4.fragmented) return fail(VTS_E_UNSUPPORTED, "fragmented MP4 is not supported");
-  return open_common(device, mp4, data, size, nullptr, params, out);
+  return open_common(device, mp4, data, size, nullptr, params, out, t0);
 }
 
 extern "C" int vts_info(const vts_ctx *c, vts_video_info *info) {
@@ -1064,6 +1200,19 @@ extern "C" int vts_get_thumbnail_rgb(vts_ctx *c, int64_t frame, uint8_t *out, in
   if (out_bytes < need) return fail(VTS_E_CAPACITY, "need %lld bytes", static_cast<long long>(need));
   HIP_TRY(hipMemcpy(out, c->d_rgb + need * frame, static_cast<size_t>(need), hipMemcpyDeviceToHost));
   return VTS_OK;
+}
+
+void vts_ctx::open_lap(int k) {
+  const double t = now_s();
+  open_ms[k] += (t - open_t) * 1e3;
+  open_t = t;
+}
+
+extern "C" int vts_open_timings(const vts_ctx *c, double *ms, int32_t cap) {
+  clear_error();
+  if (!c || !ms || cap < 0) return fail(VTS_E_INVALID, "bad argument");
+  for (int i = 0; i < std::min(cap, 8); ++i) ms[i] = c->open_ms[i];
+  return 8;
 }
 
 extern "C" int vts_last_timings(const vts_ctx *c, double *ms4) {

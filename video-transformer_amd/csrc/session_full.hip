@@ -34,7 +34,7 @@ constexpr int64_t kMinRingBytes = 1ll << 30;
 
 }  // namespace
 
-bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+bool wants_general(const vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
                    const std::vector<uint32_t> &sizes, int nal_length_size) {
   if (c->pps.entropy_coding_mode) return true;  // CABAC
   // a High-profile PPS tail (8x8 transform, scaling lists, a Cr QP offset the
@@ -49,7 +49,7 @@ bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::
   std::vector<uint32_t> sz(sizes.begin(), sizes.begin() + static_cast<int64_t>(n));
   std::vector<SchedFrame> frames;
   std::vector<SchedSlice> slices;
-  if (!sched_build(c->sps, c->pps, es.data(), off, sz, nal_length_size, &frames, &slices).empty()) return true;
+  if (!sched_build(c->sps, c->pps, es, off, sz, nal_length_size, &frames, &slices).empty()) return true;
   // 8.7.2.2: an edge is filtered only where indexA = qPav + filterOffsetA >= 16
   // (alpha is 0 below).  Chroma edges use QPc of QPY + chroma_qp_index_offset;
   // QPc(x) = x below 30 and >= 29 from there, so x + offset >= 16 is exact
@@ -60,7 +60,7 @@ bool wants_general(const vts_ctx *c, const std::vector<uint8_t> &es, const std::
   return false;
 }
 
-int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<int64_t> &es_off,
+int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
                   const std::vector<uint32_t> &sizes, int nal_length_size, const std::vector<uint8_t> &sps_nal,
                   const std::vector<uint8_t> &pps_nal) {
   SchedStream facts;
@@ -69,7 +69,7 @@ int build_general(vts_ctx *c, const std::vector<uint8_t> &es, const std::vector<
   if (c->sps.crop_left || c->sps.crop_top) return fail(VTS_E_UNSUPPORTED, "left/top cropping is not supported");
   std::vector<SchedFrame> frames;
   std::vector<SchedSlice> slices;
-  e = sched_build(c->sps, c->pps, es.data(), es_off, sizes, nal_length_size, &frames, &slices);
+  e = sched_build(c->sps, c->pps, es, es_off, sizes, nal_length_size, &frames, &slices);
   if (!e.empty()) return fail(VTS_E_UNSUPPORTED, "%s", e.c_str());
   c->general = true;
   c->fused = false;
@@ -409,7 +409,7 @@ int run_general(vts_ctx *c) {
     ra.uv_off = static_cast<int64_t>(c->pitch) * c->coded_h;
     ra.pitch = c->pitch;
     ra.epoch = epoch;
-    ra.deblock = 1;
+    ra.deblock = c->dbk_kernel;
     ra.err = c->d_err;
     ra.sct = c->d_scale;
     ra.P = c->fprm;

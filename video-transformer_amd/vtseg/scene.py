@@ -159,6 +159,15 @@ class VideoScorer:
         return {"total_ms": t[0], "parse_ms": t[1], "reconstruct_ms": t[2],
                 "score_ms": t[3]}
 
+    def open_timings(self) -> dict:
+        """Host time of this session's vts_open by stage (ms)."""
+        t = (C.c_double * 8)()
+        n = self._lib.vts_open_timings(self._ctx, t, 8)
+        if n < 0:
+            _lib.check(n)
+        return {"demux_ms": t[0], "read_ms": t[2], "schedule_ms": t[3], "alloc_ms": t[4],
+                "upload_wait_ms": t[5], "rest_ms": t[6], "total_ms": t[7]}
+
     def recon_launches(self) -> int:
         """Reconstruct launches per run (one per GOP level per window)."""
         return int(self._lib.vts_schedule_info(self._ctx, 0))
