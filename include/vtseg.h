@@ -302,6 +302,10 @@ int vts_get_thumbnail_rgb(vts_ctx *ctx, int64_t frame, uint8_t *out,
 /* Timing of the last vts_run/vts_score, milliseconds, HIP events:
  * [0] whole, [1] parse, [2] reconstruct, [3] score. */
 int vts_last_timings(const vts_ctx *ctx, double *ms4);
+/* Device memory released by closed sessions stays mapped in a process-wide
+ * cache that later sessions reuse (re-allocating released HBM waits while the
+ * driver clears it); this hands device `device`'s cache back to HIP. */
+int vts_empty_cache(int device);
 /* Host time of the vts_open that made ctx, milliseconds, by stage:
  * [0] demux (moov) + device checks, [1] unused, [2] sample read (parallel
  * pread), [3] host decode schedule, [4] device allocations (+ the general

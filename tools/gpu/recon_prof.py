@@ -12,7 +12,7 @@ import torch  # noqa: F401  (libvtseg binds to torch's HIP runtime)
 from vtseg import _lib, scene
 
 DBK = ["wait_row_above", "vertical_edges", "horizontal_edges", "write_back", "tail", "-", "-", "iterations"]
-INTRA = ["setup_bucket_sort", "intra_mbs", "level_barrier", "-", "-", "-", "wave_levels", "mbs"]
+INTRA = ["setup_bucket_sort", "level_tail", "level_barrier", "mb_loads", "mb_luma", "mb_chroma", "wave_levels", "mbs"]
 v = scene.VideoScorer(sys.argv[1], device=0, decoder="general")
 v.run()
 torch.cuda.synchronize()
@@ -32,7 +32,7 @@ res = {"video": sys.argv[1], "timings": v.timings(),
 if d[7]:
     res["deblock_cycles_per_iteration"] = {n: round(x / d[7], 1) for n, x in zip(DBK[:5], d[:5])}
 if i[7]:
-    res["intra_cycles_per_mb"] = round(i[1] / i[7], 1)
+    res["intra_cycles_per_wave_mb_step"] = {n: round(x / i[7], 1) for n, x in zip(INTRA[3:6], i[3:6])}
 if i[6]:
     res["intra_cycles_per_wave_level"] = {n: round(x / i[6], 1) for n, x in zip(INTRA[:3], i[:3])}
 print(json.dumps(res))

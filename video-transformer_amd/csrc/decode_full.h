@@ -63,7 +63,8 @@ struct FullReconArgs {
   int64_t uv_off;            // UV plane offset in a picture (pitch * coded height)
   int32_t pitch;
   uint32_t epoch;
-  int32_t deblock;           // 1: run the deblocking kernel after reconstruction
+  int32_t deblock;           // deblocking kernel after reconstruction: 0 none, 1 h264_deblock_full, 2 h264_deblock_lds
+  int32_t intra_kernel;      // 1: h264_intra_full, else h264_intra_v2 (where its LDS fits)
   int32_t _pad;
   DbkInfo *dbk;              // ring: [slot][mb] deblocking descriptors
   uint32_t *err;

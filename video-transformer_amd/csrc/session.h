@@ -5,12 +5,14 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "common.h"
 #include "decode.h"
 #include "decode_full.h"
 #include "h264.h"
+#include "devmem.h"
 #include "h264_full.h"
 
 #define HIP_TRY(expr)                                                              \
@@ -67,7 +69,12 @@ struct HostBytes {
   HostBytes() = default;
   HostBytes(const HostBytes &) = delete;
   HostBytes &operator=(const HostBytes &) = delete;
-  ~HostBytes() { std::free(p_); }
+  // a multi-GB buffer's pages take tens of ms to unmap: freed off the
+  // caller's thread (vts_open returned 50-80 ms earlier)
+  ~HostBytes() {
+    if (n_ >= (int64_t{64} << 20)) std::thread([p = p_]() { std::free(p); }).detach();
+    else std::free(p_);
+  }
   bool alloc(int64_t n) {
     std::free(p_);
     p_ = static_cast<uint8_t *>(std::malloc(static_cast<size_t>(std::max<int64_t>(n, 1))));
@@ -181,6 +188,7 @@ struct vts_ctx {
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
   int dbk_kernel = 2;                   // 2: h264_deblock_lds; VTS_DBK=1: h264_deblock_full
+  int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock

@@ -236,56 +236,57 @@ struct EsUpload {
 int alloc_general(vts_ctx *c) {
   HIP_TRY(hipSetDevice(c->device));
   if (!c->d_es) return fail(VTS_E_INVALID, "elementary stream not resident");
-  HIP_TRY(hipMalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
+  HIP_TRY(vts::dmalloc(&c->d_fslices, sizeof(FullSlice) * std::max<size_t>(1, c->fslices.size())));
   if (!c->fslices.empty())
     HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&c->d_scale, sizeof(ScaleTab)));
+  HIP_TRY(vts::dmalloc(&c->d_scale, sizeof(ScaleTab)));
   HIP_TRY(hipMemcpy(c->d_scale, &c->scale_tab, sizeof(ScaleTab), hipMemcpyHostToDevice));
   // the slice NALs' RBSPs, made once: the parsers read plain bits
-  HIP_TRY(hipMalloc(&c->d_rbsp, static_cast<size_t>(c->es_bytes)));
-  HIP_TRY(hipMalloc(&c->d_rbsp_len, sizeof(int32_t) * std::max<size_t>(1, c->fslices.size())));
+  HIP_TRY(vts::dmalloc(&c->d_rbsp, static_cast<size_t>(c->es_bytes)));
+  HIP_TRY(vts::dmalloc(&c->d_rbsp_len, sizeof(int32_t) * std::max<size_t>(1, c->fslices.size())));
   VTS_TRY(nal_unescape_launch(c->d_es, c->d_rbsp, c->d_fslices, static_cast<int32_t>(c->fslices.size()),
                               c->d_rbsp_len, nullptr));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMalloc(&c->d_porder, sizeof(int32_t) * std::max<size_t>(1, c->porder.size())));
+  HIP_TRY(vts::dmalloc(&c->d_porder, sizeof(int32_t) * std::max<size_t>(1, c->porder.size())));
   if (!c->porder.empty())
     HIP_TRY(hipMemcpy(c->d_porder, c->porder.data(), sizeof(int32_t) * c->porder.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&c->d_porder_m, sizeof(int32_t) * std::max<size_t>(1, c->porder_m.size())));
+  HIP_TRY(vts::dmalloc(&c->d_porder_m, sizeof(int32_t) * std::max<size_t>(1, c->porder_m.size())));
   if (!c->porder_m.empty())
     HIP_TRY(hipMemcpy(c->d_porder_m, c->porder_m.data(), sizeof(int32_t) * c->porder_m.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&c->d_pneed, sizeof(int32_t) * std::max<size_t>(1, c->pneed.size())));
+  HIP_TRY(vts::dmalloc(&c->d_pneed, sizeof(int32_t) * std::max<size_t>(1, c->pneed.size())));
   if (!c->pneed.empty())
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
   if (const char *e = std::getenv("VTS_PARSE_MERGE")) c->parse_merged = std::atoi(e) != 0;
   if (const char *e = std::getenv("VTS_DBK")) c->dbk_kernel = std::atoi(e) == 1 ? 1 : 2;
-  HIP_TRY(hipMalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
+  if (const char *e = std::getenv("VTS_INTRA")) c->intra_kernel = std::atoi(e) == 1 ? 1 : 2;
+  HIP_TRY(vts::dmalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&c->d_levels, sizeof(int4) * std::max<size_t>(1, c->level_frames.size())));
+  HIP_TRY(vts::dmalloc(&c->d_levels, sizeof(int4) * std::max<size_t>(1, c->level_frames.size())));
   HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(), hipMemcpyHostToDevice));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
   c->ws_bytes = score_workspace_bytes(c->width, c->height, c->k, c->ring_frames);
   const int64_t tw = (c->width / c->k) * (c->height / c->k);
   for (int r = 0; r < c->n_rings; ++r) {
-    HIP_TRY(hipMalloc(&c->d_recs[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec)));
+    HIP_TRY(vts::dmalloc(&c->d_recs[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRec)));
     if (c->fprm.bframes)
-      HIP_TRY(hipMalloc(&c->d_recs1[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRecB)));
-    HIP_TRY(hipMalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
-    HIP_TRY(hipMalloc(&c->d_pdone[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
-    HIP_TRY(hipMalloc(&c->d_dbk[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(DbkInfo)));
-    HIP_TRY(hipMalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
-    HIP_TRY(hipMalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
-    HIP_TRY(hipMalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
+      HIP_TRY(vts::dmalloc(&c->d_recs1[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRecB)));
+    HIP_TRY(vts::dmalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
+    HIP_TRY(vts::dmalloc(&c->d_pdone[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
+    HIP_TRY(vts::dmalloc(&c->d_dbk[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(DbkInfo)));
+    HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
+    HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
+    HIP_TRY(vts::dmalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
     c->ring_cleared_at[r] = -1;
   }
   if (!c->d_last[0])
-    for (int r = 0; r < 2; ++r) HIP_TRY(hipMalloc(&c->d_last[r], static_cast<size_t>(tw + kPad)));
-  if (!c->d_err) HIP_TRY(hipMalloc(&c->d_err, sizeof(uint32_t)));
-  if (!c->d_score) HIP_TRY(hipMalloc(&c->d_score, sizeof(float) * c->n_frames));
-  if (!c->d_sad) HIP_TRY(hipMalloc(&c->d_sad, sizeof(uint64_t) * c->n_frames));
-  if (!c->d_hist) HIP_TRY(hipMalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
+    for (int r = 0; r < 2; ++r) HIP_TRY(vts::dmalloc(&c->d_last[r], static_cast<size_t>(tw + kPad)));
+  if (!c->d_err) HIP_TRY(vts::dmalloc(&c->d_err, sizeof(uint32_t)));
+  if (!c->d_score) HIP_TRY(vts::dmalloc(&c->d_score, sizeof(float) * c->n_frames));
+  if (!c->d_sad) HIP_TRY(vts::dmalloc(&c->d_sad, sizeof(uint64_t) * c->n_frames));
+  if (!c->d_hist) HIP_TRY(vts::dmalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
   c->thumb_px = tw;
-  if (!c->d_rgb) HIP_TRY(hipMalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
+  if (!c->d_rgb) HIP_TRY(vts::dmalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
   if (!c->s_dec) VTS_TRY(stream_take(c->device, &c->s_dec));
   if (!c->s_score) VTS_TRY(stream_take(c->device, &c->s_score));
   if (!c->s_parse) VTS_TRY(stream_take(c->device, &c->s_parse));
@@ -310,7 +311,7 @@ int switch_to_general(vts_ctx *c) {
   std::vector<uint8_t> es(static_cast<size_t>(c->es_bytes));
   HIP_TRY(hipMemcpy(es.data(), c->d_es, es.size(), hipMemcpyDeviceToHost));
   auto f = [](void *p) {
-    if (p) (void)hipFree(p);
+    if (p) vts::dfree(p);
   };
   for (int r = 0; r < 2; ++r) {
     f(c->d_cmd[r]);
@@ -429,7 +430,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   c->open_lap(2);
   // the ES goes to HBM on its own thread while the schedule below is built
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
+  HIP_TRY(vts::dmalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
   EsUpload up;
   up.start(c->device, c->d_es, es.data(), c->es_bytes);
   c->open_lap(4);
@@ -527,7 +528,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
                             score_workspace_bytes(c->width, c->height, c->k, 1);
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  HIP_TRY(vts::dmem_free(&free_b, &total_b));
   const int64_t whole = c->es_bytes + c->n_frames * (3 * tw_f + 1024 + 12) + (1ll << 30);
   const int64_t avail = std::max<int64_t>(0, static_cast<int64_t>(free_b) - whole);
   const int64_t ring_budget = std::min(kSingleWindowBytes, std::max(kMinRingBytes, avail / 4));
@@ -726,36 +727,36 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   // ---- device allocations and uploads
   c->open_lap(3);
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMalloc(&c->d_slices, sizeof(SliceDesc) * c->slices.size()));
+  HIP_TRY(vts::dmalloc(&c->d_slices, sizeof(SliceDesc) * c->slices.size()));
   HIP_TRY(hipMemcpy(c->d_slices, c->slices.data(), sizeof(SliceDesc) * c->slices.size(),
                     hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&c->d_post, sizeof(int32_t) * std::max<size_t>(1, c->post_slots.size())));
+  HIP_TRY(vts::dmalloc(&c->d_post, sizeof(int32_t) * std::max<size_t>(1, c->post_slots.size())));
   if (!c->post_slots.empty())
     HIP_TRY(hipMemcpy(c->d_post, c->post_slots.data(), sizeof(int32_t) * c->post_slots.size(),
                       hipMemcpyHostToDevice));
   if (!c->tb_chains.empty()) {
-    HIP_TRY(hipMalloc(&c->d_tb, sizeof(int4) * c->tb_chains.size()));
+    HIP_TRY(vts::dmalloc(&c->d_tb, sizeof(int4) * c->tb_chains.size()));
     HIP_TRY(hipMemcpy(c->d_tb, c->tb_chains.data(), sizeof(int4) * c->tb_chains.size(), hipMemcpyHostToDevice));
   }
-  HIP_TRY(hipMalloc(&c->d_levels, sizeof(int4) * c->level_frames.size()));
+  HIP_TRY(vts::dmalloc(&c->d_levels, sizeof(int4) * c->level_frames.size()));
   HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(),
                     hipMemcpyHostToDevice));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
   c->ws_bytes = score_workspace_bytes(c->width, c->height, c->k, c->ring_frames);
   const int64_t tw = (c->width / c->k) * (c->height / c->k);
   for (int r = 0; r < c->n_rings; ++r) {
-    HIP_TRY(hipMalloc(&c->d_cmd[r], static_cast<size_t>(c->ring_frames * nmb * 8)));
-    HIP_TRY(hipMalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
-    HIP_TRY(hipMalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
-    if (c->fused) HIP_TRY(hipMalloc(&c->d_thumb[r], static_cast<size_t>(c->ring_frames * tw + kPad)));
+    HIP_TRY(vts::dmalloc(&c->d_cmd[r], static_cast<size_t>(c->ring_frames * nmb * 8)));
+    HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
+    HIP_TRY(vts::dmalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
+    if (c->fused) HIP_TRY(vts::dmalloc(&c->d_thumb[r], static_cast<size_t>(c->ring_frames * tw + kPad)));
   }
-  for (int r = 0; r < 2; ++r) HIP_TRY(hipMalloc(&c->d_last[r], static_cast<size_t>(tw + kPad)));
-  HIP_TRY(hipMalloc(&c->d_err, sizeof(uint32_t)));
-  HIP_TRY(hipMalloc(&c->d_score, sizeof(float) * c->n_frames));
-  HIP_TRY(hipMalloc(&c->d_sad, sizeof(uint64_t) * c->n_frames));
-  HIP_TRY(hipMalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
+  for (int r = 0; r < 2; ++r) HIP_TRY(vts::dmalloc(&c->d_last[r], static_cast<size_t>(tw + kPad)));
+  HIP_TRY(vts::dmalloc(&c->d_err, sizeof(uint32_t)));
+  HIP_TRY(vts::dmalloc(&c->d_score, sizeof(float) * c->n_frames));
+  HIP_TRY(vts::dmalloc(&c->d_sad, sizeof(uint64_t) * c->n_frames));
+  HIP_TRY(vts::dmalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
   c->thumb_px = tw;
-  HIP_TRY(hipMalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
+  HIP_TRY(vts::dmalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
   VTS_TRY(stream_take(c->device, &c->s_dec));
   VTS_TRY(stream_take(c->device, &c->s_score));
   VTS_TRY(stream_take(c->device, &c->s_parse));
@@ -1264,7 +1265,7 @@ extern "C" int vts_close(vts_ctx *c) {
   for (hipStream_t g : c->s_grp)
     if (g) (void)hipStreamSynchronize(g);
   auto f = [](void *p) {
-    if (p) (void)hipFree(p);
+    if (p) vts::dfree(p);
   };
   f(c->d_es);
   f(c->d_slices);

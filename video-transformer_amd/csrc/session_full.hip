@@ -140,7 +140,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
                             32 * ((cap_total + n - 1) / std::max<int64_t>(1, n));
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  HIP_TRY(vts::dmem_free(&free_b, &total_b));
   // whole-video buffers: the elementary stream and its RBSP copy (d_rbsp,
   // same size), per-frame scoring outputs, the slice table with its RBSP
   // lengths and parse order, the per-picture parse counters, 1 GiB of slack
@@ -410,6 +410,7 @@ int run_general(vts_ctx *c) {
     ra.pitch = c->pitch;
     ra.epoch = epoch;
     ra.deblock = c->dbk_kernel;
+    ra.intra_kernel = c->intra_kernel;
     ra.err = c->d_err;
     ra.sct = c->d_scale;
     ra.P = c->fprm;

@@ -1020,7 +1020,7 @@ std::vector<int32_t> area_taps(int64_t n, int64_t m, int coded, int *k_out, int3
 
 template <class T>
 int dev_alloc(T **p, size_t n) {
-  HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(1, n) * sizeof(T)));
+  HIP_TRY(vts::dmalloc(reinterpret_cast<void **>(p), std::max<size_t>(1, n) * sizeof(T)));
   return VTS_OK;
 }
 
@@ -1033,7 +1033,7 @@ struct DevBufs {  // transcode scratch, freed on every exit path
     return VTS_OK;
   }
   ~DevBufs() {
-    for (void *p : ptrs) (void)hipFree(p);
+    for (void *p : ptrs) vts::dfree(p);
   }
 };
 
@@ -1043,8 +1043,8 @@ int setup_small(vts_ctx *c, int sh) {
   const int sw = static_cast<int>((static_cast<int64_t>(sh) * W + H) / (2 * static_cast<int64_t>(H))) * 2;
   if (sw < 2) return fail(VTS_E_INVALID, "output width %d from %dx%d at height %d", sw, W, H, sh);
   if (S.d && S.w == sw && S.h == sh) return VTS_OK;
-  if (S.d) (void)hipFree(S.d);
-  if (S.d_taps) (void)hipFree(S.d_taps);
+  if (S.d) vts::dfree(S.d);
+  if (S.d_taps) vts::dfree(S.d_taps);
   S = SmallStore{};
   S.w = sw;
   S.h = sh;
@@ -1072,10 +1072,10 @@ int setup_small(vts_ctx *c, int sh) {
   S.off[2] = S.off[1] + static_cast<int64_t>(ty.size());
   S.off[3] = S.off[2] + static_cast<int64_t>(tcx.size());
   HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipMalloc(&S.d_taps, all.size() * sizeof(int32_t)));
+  HIP_TRY(vts::dmalloc(&S.d_taps, all.size() * sizeof(int32_t)));
   HIP_TRY(hipMemcpy(S.d_taps, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   const size_t bytes = static_cast<size_t>(S.stride * c->n_frames + 256);
-  if (hipMalloc(&S.d, bytes) != hipSuccess) {
+  if (vts::dmalloc(&S.d, bytes) != hipSuccess) {
     (void)hipGetLastError();
     S.d = nullptr;
     return fail(VTS_E_HIP, "cannot allocate %.1f GiB for the %dx%d frames", bytes / 1073741824.0, sw, sh);

@@ -161,6 +161,7 @@ SIGNATURES: dict[str, tuple] = {
     "vts_get_thumbnail_rgb": (C.c_int, [C.c_void_p, C.c_int64, _P(C.c_uint8), C.c_int64]),
     "vts_last_timings": (C.c_int, [C.c_void_p, _P(C.c_double)]),
     "vts_open_timings": (C.c_int, [C.c_void_p, _P(C.c_double), C.c_int32]),
+    "vts_empty_cache": (C.c_int, [C.c_int]),
     "vts_schedule_info": (C.c_int64, [C.c_void_p, C.c_int32]),
     "vts_close": (C.c_int, [C.c_void_p]),
     "vts_transcode": (C.c_int, [C.c_void_p, C.c_char_p, _P(TranscodeParams),
