@@ -6,7 +6,9 @@
 // memory.  TEST INFRASTRUCTURE (tests/test_full_host.py compares it with the
 // oracle); the product never runs the decoder on the CPU.
 #include <algorithm>
+#include <barrier>
 #include <cstdio>
+#include <thread>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -27,8 +29,71 @@ extern "C" void fh_stats(unsigned long long *out) {
 #include "parse_cabac.h"
 #include "parse_full.h"
 #include "recon_full.h"
+#include "intra_lanes.h"
 
 using namespace vts;
+
+// flags bit 2: intra macroblocks through the device's lane-parallel code
+// (intra_lanes.h, h264_intra_v2), 32 host threads playing the 32 lanes
+namespace {
+struct HostGroup {
+  std::barrier<> bar{32};
+  int buf[32];
+};
+struct HostLanes {
+  int t;
+  HostGroup *g;
+  void sync() const { g->bar.arrive_and_wait(); }
+  int red16(int v) const {
+    g->bar.arrive_and_wait();
+    g->buf[t] = v;
+    g->bar.arrive_and_wait();
+    int s = 0;
+    for (int i = 0; i < 16; ++i) s += g->buf[(t & 16) + i];
+    g->bar.arrive_and_wait();
+    return s;
+  }
+  int bcast(int v, int l) const {
+    g->bar.arrive_and_wait();
+    g->buf[t] = v;
+    g->bar.arrive_and_wait();
+    const int r = g->buf[l];
+    g->bar.arrive_and_wait();
+    return r;
+  }
+};
+// one picture's intra macroblocks level by level (the kernel's order; one
+// macroblock at a time), line buffers as the kernel's LDS
+void intra_lanes_picture(const i2::I2Ctx &ctx, const uint16_t *lv) {
+  const int nmb = ctx.mbw * ctx.mbh;
+  std::vector<std::pair<int, int>> order;  // (level, mb)
+  for (int i = 0; i < nmb; ++i)
+    if (lv[i] != kNoLevel) order.emplace_back(lv[i], i);
+  std::stable_sort(order.begin(), order.end());
+  std::vector<i2::I2Line> lines(static_cast<size_t>(ctx.mbw + ctx.mbh));
+  for (auto &l : lines) l.tag = -2;
+  i2::I2Line *lcol = lines.data(), *lrow = lines.data() + ctx.mbw;
+  uint8_t off4[9 * 16], off8[9 * 64];
+  for (int i = 0; i < 9 * 16; ++i) off4[i] = static_cast<uint8_t>(i2::i2_intra4_off(i >> 4, i & 3, (i >> 2) & 3));
+  for (int i = 0; i < 9 * 64; ++i) off8[i] = static_cast<uint8_t>(i2::i2_intra8_off(i >> 6, i & 7, (i >> 3) & 7));
+  auto *T = new i2::I2Tile;
+  HostGroup grp;
+  std::vector<std::thread> th;
+  for (int t = 0; t < 32; ++t)
+    th.emplace_back([&, t]() {
+      const HostLanes L{t, &grp};
+      i2::I2NoProf np;
+      for (const auto &o : order) {
+        i2::intra2_prepare(ctx, o.second, L, *T, lcol, lrow, np);
+        L.sync();
+        i2::intra2_finish(ctx, L, *T, lcol, lrow, off4, off8, np);
+        L.sync();
+      }
+    });
+  for (auto &x : th) x.join();
+  delete T;
+}
+}  // namespace
 
 // LevelScale4x4 / 8x8 the product derives from a file's SPS / PPS
 // (sched_stream_facts, 8.5.9): ls4 = 6 x 6 x 16, ls8 = 2 x 6 x 64 int32
@@ -234,6 +299,29 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
         if (r.err) return bad("recon: " + describe_decode_error(r.err));
       }
     }
+    if (flags & 2) {
+      i2::I2Ctx ic{};
+      ic.recs = fr_recs;
+      ic.arena = arena.data();
+      ic.Y = surf.data() + static_cast<int64_t>(fi) * stride;
+      ic.uv_off = static_cast<int64_t>(pitch) * ch;
+      ic.pitch = pitch;
+      ic.mbw = mbw;
+      ic.mbh = mbh;
+      ic.epoch = epoch;
+      ic.cip = P.cip;
+      ic.cqp_off = P.cqp_off;
+      ic.cqp_off2 = P.cqp_off2;
+      ic.scaled = P.scaled;
+      ic.sct = &facts.scale;
+      // I_PCM is written by the inter pass on the device; the rest by levels
+      for (int a = 0; a < nmb; ++a)
+        if (fr_recs[a].type == kMbPcm) {
+          full::MbRecon r(c, fi, a, fr_recs[a]);
+          r.run();
+        }
+      intra_lanes_picture(ic, ilvl.data() + static_cast<size_t>(fi) * nmb);
+    } else {
     for (int tt = 0; tt < mbw + 2 * mbh; ++tt)
       for (int y = 0; y < mbh; ++y) {
         const int x = tt - 2 * y;
@@ -244,6 +332,7 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
         r.run();
         if (r.err) return bad("recon: " + describe_decode_error(r.err));
       }
+    }
     if (!(flags & 1))
       for (int tt = 0; tt < mbw + 2 * mbh; ++tt)
         for (int y = 0; y < mbh; ++y) {

@@ -88,6 +88,7 @@ struct RProf {
 #include "parse_cabac.h"
 #include "parse_full.h"
 #include "recon_full.h"
+#include "intra_lanes.h"
 
 namespace vts {
 namespace {
@@ -1147,485 +1148,24 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
 //  * the macroblock leaves as whole rows at the end (dword stores).
 // h264_intra_full spent ~62 k cycles per macroblock step per wave and ~41 k
 // per wave at the level barrier (profiles/r04c_recon_sections_dbk2.json).
-// 8.5.13's 1-D 8-point inverse transform
-__device__ __forceinline__ void idct8_1d(const int (&v)[8], int (&o)[8]) {
-  const int a0 = v[0] + v[4], a4 = v[0] - v[4], a2 = (v[2] >> 1) - v[6], a6 = v[2] + (v[6] >> 1);
-  const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
-  const int a1 = -v[3] + v[5] - v[7] - (v[7] >> 1), a3 = v[1] + v[7] - v[3] - (v[3] >> 1);
-  const int a5 = -v[1] + v[7] + v[5] + (v[5] >> 1), a7 = v[3] + v[5] + v[1] + (v[1] >> 1);
-  const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
-  o[0] = b0 + b7;
-  o[1] = b2 + b5;
-  o[2] = b4 + b3;
-  o[3] = b6 + b1;
-  o[4] = b6 - b1;
-  o[5] = b4 - b3;
-  o[6] = b2 - b5;
-  o[7] = b0 - b7;
-}
 constexpr int kI2Threads = 1024;
 constexpr int kI2Groups = kI2Threads / 32;
-struct alignas(16) I2Tile {
-  int32_t lres[16][16];  // luma residual, raster (row-pass intermediates first)
-  int32_t cres[2][8][8]; // chroma residual per plane
-  int32_t dc16[16];      // Intra_16x16: each block's scaled DC
-  uint8_t y[17][28];     // luma rows -1..15 (index + 1) x cols -4..23 (index + 4)
-  uint8_t c[2][9][12];   // per plane: chroma rows -1..7 (index + 1) x cols -1..7 (index + 1)
-  uint8_t e4[2][16];     // Intra_4x4: per block slot E[0..14], DC at 15
-  uint8_t p8[96];        // Intra_8x8: E at 0..26, F(k) at 32 + k, A(k) at 64 + k, DC at 88
+using i2::I2Tile;
+// the macroblock's 32 lanes are half a wave
+struct DevLanes {
+  int t;
+  __device__ __forceinline__ void sync() const { lane_sync(); }
+  __device__ __forceinline__ int red16(int v) const {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 16);
+    return v;
+  }
+  __device__ __forceinline__ int bcast(int v, int l) const { return __shfl(v, static_cast<int>(threadIdx.x & 32) + l); }
 };
-// Intra_4x4 block steps: the raster blocks of step s (bx + 2 by = s), -1 none
-__device__ __forceinline__ int i4_step_blk(int s, int slot) {
-  // step:   0  1  2    3    4    5    6     7     8   9
-  // slot 0: 0  1  2    3    6    7    10    11    14  15
-  // slot 1: -  -  4    5    8    9    12    13    -   -
-  const uint64_t s0 = 0xFEBA763210ull;  // nibble s
-  const uint64_t s1 = 0x00DC985400ull;
-  if (slot == 0) return static_cast<int>((s0 >> (4 * s)) & 15);
-  return (s >= 2 && s <= 7) ? static_cast<int>((s1 >> (4 * s)) & 15) : -1;
-}
-__device__ __forceinline__ int red16(int v) {  // sum over the 16 lanes of v's aligned group
-#pragma unroll
-  for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 16);
-  return v;
-}
 
-__device__ __forceinline__ void intra2_mb(const FullReconArgs &a, int slot, int mb, int t, I2Tile &T,
-                                          uint8_t *lby, uint8_t *lbc, uint8_t *rcl, const uint8_t *s_off4,
-                                          const uint8_t *s_off8, RProf &rp_) {
-  const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
-  const int pitch = a.pitch;
-  const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
-  const MbRec *rec = frecs + mb;
-  const MbHdr h = load_hdr(rec);
-  const int mx = mb % mbw, my = mb / mbw;
-  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
-  uint8_t *UV = Y + a.uv_off;
-  const int qp = h.qp;
-  const bool i16 = h.type == kMbI16, t8 = !i16 && (h.modes & kModeT8);
-  // ---- residuals (8.5.12 / 8.5.13), in two passes through the tile so no lane
-  // holds a whole block: pass 1 scales and transforms rows (luma: 4x4 rows two
-  // per lane, or 8x8 rows one per lane; chroma: one 4x4 row per lane), pass 2
-  // the columns, in place (int32: a stream outside the standard's range still
-  // decodes exactly like the oracle)
-  {
-    const int32_t *ls4 = ls4_of(a, true, 0, qp);
-    if (i16 && t < 16) {  // 8.5.10: block t's entry of the Hadamard-transformed DC levels, scaled
-      const int bx = t & 3, by = t >> 2;
-      int dcl[16];
-      load_coefs(a.arena, stored(h.blocks, h.coef, kBlkI16Dc), dcl);
-      int f = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {  // row transform of DC row k at column bx; the column signs for row by
-        const int a0 = dcl[k * 4], a1 = dcl[k * 4 + 1], a2 = dcl[k * 4 + 2], a3 = dcl[k * 4 + 3];
-        const int rk = bx == 0 ? a0 + a1 + a2 + a3 : (bx == 1 ? a0 + a1 - a2 - a3 : (bx == 2 ? a0 - a1 - a2 + a3 : a0 - a1 + a2 - a3));
-        const bool pos = k == 0 || (k == 1 ? by <= 1 : (k == 2 ? (by == 0 || by == 3) : (by == 0 || by == 2)));
-        f += pos ? rk : -rk;
-      }
-      const int ls = ls4[0], sh = qp / 6;
-      T.dc16[t] = qp >= 36 ? (f * ls) << (sh - 6) : (f * ls + (1 << (5 - sh))) >> (6 - sh);
-    }
-    lane_sync();
-    if (t8) {
-      const int b8 = t >> 3, i = t & 7;
-      const int64_t lb = stored(h.blocks, h.coef, kBlkLuma0 + 4 * b8);
-      const int32_t *ls8 = a.P.scaled ? a.sct->ls8[0][qp % 6] : nullptr;
-      int v[8];
-      if (lb >= 0) {
-        const uint4 u = *reinterpret_cast<const uint4 *>(a.arena + 16 * lb + 8 * i);
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-        const int sh = qp / 6;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int c = static_cast<int16_t>((w[j >> 1] >> ((j & 1) * 16)) & 0xffff);
-          const int ls = ls8 ? ls8[i * 8 + j] : 16 * full::kNorm8[qp % 6][vts_norm8_class(i, j)];
-          v[j] = qp >= 36 ? (c * ls) << (sh - 6) : (c * ls + (1 << (5 - sh))) >> (6 - sh);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0;
-      }
-      int o[8];
-      idct8_1d(v, o);
-      int32_t *dst = &T.lres[(b8 >> 1) * 8 + i][(b8 & 1) * 8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dst[j] = o[j];
-    } else {
-      const int b = t >> 1, bx = b & 3, by = b >> 2;
-      const int64_t lb = stored(h.blocks, h.coef, kBlkLuma0 + blkidx(b));
-      const int sh = qp / 6;
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
-        const int i = (t & 1) * 2 + rr;  // row of the block
-        int c[4] = {0, 0, 0, 0};
-        if (lb >= 0) {
-          const uint2 u = *reinterpret_cast<const uint2 *>(a.arena + 16 * lb + 4 * i);
-          c[0] = static_cast<int16_t>(u.x & 0xffff);
-          c[1] = static_cast<int16_t>(u.x >> 16);
-          c[2] = static_cast<int16_t>(u.y & 0xffff);
-          c[3] = static_cast<int16_t>(u.y >> 16);
-        }
-        int d[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          d[j] = qp >= 24 ? (c[j] * ls4[i * 4 + j]) << (sh - 4) : (c[j] * ls4[i * 4 + j] + (1 << (3 - sh))) >> (4 - sh);
-        if (i16 && i == 0) d[0] = T.dc16[b];
-        const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
-        int32_t *dst = &T.lres[by * 4 + i][bx * 4];
-        dst[0] = e0 + e3;
-        dst[1] = e1 + e2;
-        dst[2] = e1 - e2;
-        dst[3] = e0 - e3;
-      }
-    }
-    {  // chroma row: plane t >> 4, block (t >> 2) & 3, row t & 3
-      const int pl = t >> 4, ck = (t >> 2) & 3, i = t & 3;
-      const int qpc = full::qpc_of(qp, pl ? a.P.cqp_off2 : a.P.cqp_off);
-      const int32_t *lsc = ls4_of(a, true, 1 + pl, qpc);
-      const int64_t cb = stored(h.blocks, h.coef, kBlkChromaAc0 + 4 * pl + ck);
-      const int sh = qpc / 6;
-      int c[4] = {0, 0, 0, 0};
-      if (cb >= 0) {
-        const uint2 u = *reinterpret_cast<const uint2 *>(a.arena + 16 * cb + 4 * i);
-        c[0] = static_cast<int16_t>(u.x & 0xffff);
-        c[1] = static_cast<int16_t>(u.x >> 16);
-        c[2] = static_cast<int16_t>(u.y & 0xffff);
-        c[3] = static_cast<int16_t>(u.y >> 16);
-      }
-      int d[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        d[j] = qpc >= 24 ? (c[j] * lsc[i * 4 + j]) << (sh - 4) : (c[j] * lsc[i * 4 + j] + (1 << (3 - sh))) >> (4 - sh);
-      if (i == 0) d[0] = chroma_dc(a.arena, h.blocks, h.coef, pl, ck, qpc, lsc);
-      const int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
-      int32_t *dst = &T.cres[pl][(ck >> 1) * 4 + i][(ck & 1) * 4];
-      dst[0] = e0 + e3;
-      dst[1] = e1 + e2;
-      dst[2] = e1 - e2;
-      dst[3] = e0 - e3;
-    }
-    lane_sync();
-    if (t8) {  // column t: 8x8 block t >> 3, column t & 7
-      const int b8 = t >> 3, j = t & 7, r0 = (b8 >> 1) * 8, c0 = (b8 & 1) * 8 + j;
-      int v[8], o[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = T.lres[r0 + i][c0];
-      idct8_1d(v, o);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) T.lres[r0 + i][c0] = (o[i] + 32) >> 6;
-    } else {  // columns 2t, 2t + 1 of the 64 4x4 columns (block b = t >> 1)
-      const int b = t >> 1, r0 = (b >> 2) * 4;
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc) {
-        const int col = (b & 3) * 4 + (t & 1) * 2 + cc;
-        const int f0 = T.lres[r0][col], f1 = T.lres[r0 + 1][col], f2 = T.lres[r0 + 2][col], f3 = T.lres[r0 + 3][col];
-        const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
-        T.lres[r0][col] = (g0 + g3 + 32) >> 6;
-        T.lres[r0 + 1][col] = (g1 + g2 + 32) >> 6;
-        T.lres[r0 + 2][col] = (g1 - g2 + 32) >> 6;
-        T.lres[r0 + 3][col] = (g0 - g3 + 32) >> 6;
-      }
-    }
-    {  // chroma column t: plane t >> 4, block (t >> 2) & 3, column t & 3
-      const int pl = t >> 4, ck = (t >> 2) & 3, r0 = (ck >> 1) * 4, col = (ck & 1) * 4 + (t & 3);
-      int32_t(*C)[8] = T.cres[pl];
-      const int f0 = C[r0][col], f1 = C[r0 + 1][col], f2 = C[r0 + 2][col], f3 = C[r0 + 3][col];
-      const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
-      C[r0][col] = (g0 + g3 + 32) >> 6;
-      C[r0 + 1][col] = (g1 + g2 + 32) >> 6;
-      C[r0 + 2][col] = (g1 - g2 + 32) >> 6;
-      C[r0 + 3][col] = (g0 - g3 + 32) >> 6;
-    }
-  }
-  // the neighbours' headers and the border samples as HBM holds them (right for
-  // inter / I_PCM neighbours), all loads at once from clamped addresses (after
-  // the residuals: their registers and these do not overlap)
-  const int nA = mx > 0 ? mb - 1 : mb, nB = my > 0 ? mb - mbw : mb;
-  const int nC = my > 0 && mx < mbw - 1 ? mb - mbw + 1 : mb, nD = mx > 0 && my > 0 ? mb - mbw - 1 : mb;
-  const uint2 hA = *reinterpret_cast<const uint2 *>(frecs + nA), hB = *reinterpret_cast<const uint2 *>(frecs + nB);
-  const uint2 hC = *reinterpret_cast<const uint2 *>(frecs + nC), hD = *reinterpret_cast<const uint2 *>(frecs + nD);
-  const uint32_t tA = reinterpret_cast<const uint32_t *>(frecs + nA)[4], tB = reinterpret_cast<const uint32_t *>(frecs + nB)[4];
-  const uint32_t tC = reinterpret_cast<const uint32_t *>(frecs + nC)[4], tD = reinterpret_cast<const uint32_t *>(frecs + nD)[4];
-  const uint32_t i4w0 = reinterpret_cast<const uint32_t *>(rec)[8], i4w1 = reinterpret_cast<const uint32_t *>(rec)[9];
-  const int64_t yrow0 = static_cast<int64_t>(my * 16) * pitch + mx * 16;
-  const int64_t crow0 = static_cast<int64_t>(my * 8) * pitch + mx * 16;
-  const int64_t up = my > 0 ? yrow0 - pitch : yrow0;
-  // lanes 0..6: row -1 dword (cols -4 + 4t); 8..23: col -1 of row t - 8;
-  // 24..31: chroma col -1 dword of row t - 24; lanes 0..4 also chroma row -1 dword t
-  const uint32_t gTop = *reinterpret_cast<const uint32_t *>(Y + max(up - 4 + 4 * min(t, 6), static_cast<int64_t>(0)));
-  const uint8_t gLeft = Y[max(yrow0 + static_cast<int64_t>(min(max(t - 8, 0), 15)) * pitch - 1, static_cast<int64_t>(0))];
-  const uint32_t gCl = *reinterpret_cast<const uint32_t *>(UV + crow0 + static_cast<int64_t>(min(max(t - 24, 0), 7)) * pitch - 4);
-  const uint32_t gCt = *reinterpret_cast<const uint32_t *>(UV + crow0 - pitch - 4 + 4 * min(t, 4));
-  // ---- neighbourhood: availability (6.4.11.1, constrained_intra_pred), then
-  // the border samples from the line buffers (neighbours this launch
-  // reconstructed) or HBM (the others); unavailable samples read as 0
-  auto nb_ok = [&](bool exists, uint2 u, uint32_t ty) -> bool {
-    if (!exists || u.x != a.epoch || u.y != h.slice) return false;
-    if (a.P.cip && ((ty & 255) == kMbInter || (ty & 255) == kMbSkip)) return false;
-    return true;
-  };
-  auto mine = [](uint32_t ty) { return (ty & 255) == kMbI4x4 || (ty & 255) == kMbI16; };
-  const bool A = nb_ok(mx > 0, hA, tA), B = nb_ok(my > 0, hB, tB);
-  const bool C = nb_ok(my > 0 && mx < mbw - 1, hC, tC), D = nb_ok(mx > 0 && my > 0, hD, tD);
-  const uint8_t *lup = lby + ((my + 1) & 1) * pitch, *lcup = lbc + ((my + 1) & 1) * pitch;  // row my - 1's parity
-  const uint8_t *rcy = rcl + my * 32;
-  if (t < 7) {  // row -1 dword t: cols -4 + 4t .. -1 + 4t (D | B | C)
-    const bool ok = t == 0 ? D : (t < 5 ? B : C);
-    const bool lds = ok && (t == 0 ? mine(tD) : (t < 5 ? mine(tB) : mine(tC)));
-    const uint32_t v = lds ? *reinterpret_cast<const uint32_t *>(lup + mx * 16 - 4 + 4 * t) : gTop;
-    *reinterpret_cast<uint32_t *>(&T.y[0][4 * t]) = ok ? v : 0u;
-  }
-  if (t >= 8 && t < 24) {
-    const int r = t - 8;
-    T.y[1 + r][3] = A ? (mine(tA) ? rcy[r] : gLeft) : 0;  // (A: the line buffer is in range)
-  }
-  if (t >= 24) {  // chroma col -1, row t - 24: bytes 2, 3 of the dword (Cb, Cr of col -1)
-    const int r = t - 24;
-    const uint32_t v = A && mine(tA) ? (static_cast<uint32_t>(rcy[16 + 2 * r]) << 16) | (static_cast<uint32_t>(rcy[17 + 2 * r]) << 24) : gCl;
-    T.c[0][1 + r][0] = A ? (v >> 16) & 255 : 0;
-    T.c[1][1 + r][0] = A ? v >> 24 : 0;
-  }
-  if (t < 5) {  // chroma row -1 dword t: interleaved bytes -4 + 4t (t = 0: D's col -1, else B)
-    const bool ok = t == 0 ? D : B;
-    const bool lds = ok && (t == 0 ? mine(tD) : mine(tB));
-    const uint32_t v0 = lds ? *reinterpret_cast<const uint32_t *>(lcup + mx * 16 - 4 + 4 * t) : gCt;
-    const uint32_t v = ok ? v0 : 0u;
-    if (t == 0) {
-      T.c[0][0][0] = (v >> 16) & 255;
-      T.c[1][0][0] = v >> 24;
-    } else {
-      const int c0 = 2 * (t - 1);
-      T.c[0][0][1 + c0] = v & 255;
-      T.c[1][0][1 + c0] = (v >> 8) & 255;
-      T.c[0][0][2 + c0] = (v >> 16) & 255;
-      T.c[1][0][2 + c0] = v >> 24;
-    }
-  }
-  lane_sync();
-  RPROF(3);
-  // ---- luma prediction + reconstruction into the tile
-  if (i16) {
-    const int mode = h.modes & 3;
-    // sums: lanes 0..15 the top row sample t / plane term, 16..31 the left column
-    const int k = t & 15;
-    const int vt = t < 16 ? T.y[0][4 + k] : T.y[1 + k][3];
-    const int s = red16(vt);
-    const int pt = k < 8 ? (k + 1) * (t < 16 ? T.y[0][4 + 8 + k] - T.y[0][4 + 6 - k] : T.y[1 + 8 + k][3] - T.y[1 + 6 - k][3]) : 0;
-    const int ps = red16(pt);
-    const int base = threadIdx.x & 32;  // the group's first lane
-    const int st = __shfl(s, base), sl = __shfl(s, base + 16);
-    const int Hh = __shfl(ps, base), Vv = __shfl(ps, base + 16);
-    const int dc = (A && B) ? (st + sl + 16) >> 5 : (A ? (sl + 8) >> 4 : (B ? (st + 8) >> 4 : 128));
-    const int aa = 16 * (T.y[16][3] + T.y[0][19]), bb = (5 * Hh + 32) >> 6, cc = (5 * Vv + 32) >> 6;
-    const int r = t >> 1, c0 = (t & 1) * 8;
-    const int left = T.y[1 + r][3];
-#pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      const int c = c0 + x;
-      const int p = mode == 0 ? T.y[0][4 + c] : (mode == 1 ? left : (mode == 2 ? dc : c255((aa + bb * (c - 7) + cc * (r - 7) + 16) >> 5)));
-      T.y[1 + r][4 + c] = static_cast<uint8_t>(c255(p + T.lres[r][c]));
-    }
-    lane_sync();
-  } else if (t8) {
-#pragma unroll 1
-    for (int b8 = 0; b8 < 4; ++b8) {
-      const int xo = (b8 & 1) * 8, yo = (b8 >> 1) * 8;
-      const int r8 = (b8 >> 1) * 8 + (b8 & 1) * 2;
-      const uint32_t i4w = (r8 >> 3) ? i4w1 : i4w0;
-      const int m8 = (i4w >> (((r8 >> 1) & 3) * 8 + (r8 & 1) * 4)) & 15;
-      const bool top = yo > 0 || B, left = xo > 0 || A;
-      const bool tl = (xo > 0 && yo > 0) || (yo == 0 && xo > 0 ? B : (xo == 0 && yo > 0 ? A : D));
-      const bool tr = b8 == 0 ? B : (b8 == 1 ? C : b8 == 2);
-      const int ty = yo, tx = 4 + xo;
-      // raw reference samples P(k): 0 = p[-1,-1], 1 + x = p[x,-1], 17 + y = p[-1,y]
-      auto P = [&](int k) -> int {
-        if (k == 0) return tl ? T.y[ty][tx - 1] : 0;
-        if (k <= 8) return top ? T.y[ty][tx + k - 1] : 0;
-        if (k <= 16) return tr ? T.y[ty][tx + k - 1] : (top ? T.y[ty][tx + 7] : 0);
-        return left ? T.y[ty + k - 16][tx - 1] : 0;
-      };
-      // 8.3.2.2.1 filtered samples, lane t: E[t] (t < 27); E[1 + j] = L'[7 - j],
-      // E[9] = T'[0] (p'[-1,-1]), E[10 + i] = T'[1 + i], E[0] = E[1], E[26] = E[25]
-      if (t < 27) {
-        int v = 0;
-        if (t <= 8) {
-          const int y = t == 0 ? 7 : 8 - t;  // L'[y]
-          if (!left) v = 0;
-          else if (y == 0) v = tl ? (P(0) + 2 * P(17) + P(18) + 2) >> 2 : (3 * P(17) + P(18) + 2) >> 2;
-          else if (y == 7) v = (P(23) + 3 * P(24) + 2) >> 2;
-          else v = (P(16 + y) + 2 * P(17 + y) + P(18 + y) + 2) >> 2;
-        } else if (t == 9) {
-          if (!tl) v = 0;
-          else if (top && left) v = (P(1) + 2 * P(0) + P(17) + 2) >> 2;
-          else if (top) v = (3 * P(0) + P(1) + 2) >> 2;
-          else if (left) v = (3 * P(0) + P(17) + 2) >> 2;
-          else v = P(0);
-        } else {
-          const int i = min(t - 10, 15);  // T'[1 + i]
-          if (!top) v = 0;
-          else if (i == 0) v = tl ? (P(0) + 2 * P(1) + P(2) + 2) >> 2 : (3 * P(1) + P(2) + 2) >> 2;
-          else if (i == 15) v = (P(15) + 3 * P(16) + 2) >> 2;
-          else v = (P(i) + 2 * P(1 + i) + P(2 + i) + 2) >> 2;
-        }
-        T.p8[t] = static_cast<uint8_t>(v);
-      }
-      lane_sync();
-      // F(k) = 3-tap of E, A(k) = mean of E[k + 1], E[k + 2]; DC (lane 31)
-      {
-        const uint8_t *e = T.p8;
-        if (t < 25) T.p8[32 + t] = static_cast<uint8_t>((e[t] + 2 * e[t + 1] + e[t + 2] + 2) >> 2);
-        if (t < 24) T.p8[64 + t] = static_cast<uint8_t>((e[1 + t] + e[2 + t] + 1) >> 1);
-        if (t == 31) {
-          int st = 0, sl = 0;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            st += e[10 + i];
-            sl += e[1 + i];
-          }
-          T.p8[88] = static_cast<uint8_t>((top && left) ? (st + sl + 8) >> 4 : (left ? (sl + 4) >> 3 : (top ? (st + 4) >> 3 : 128)));
-        }
-      }
-      lane_sync();
-      {
-        const uint8_t *offs = s_off8 + 64 * min(m8, 8);  // > 8: not a mode (as mode 8)
-        const int x = t & 7;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int y = (t >> 3) + 4 * hh;
-          T.y[1 + yo + y][4 + xo + x] = static_cast<uint8_t>(c255(T.p8[offs[y * 8 + x]] + T.lres[yo + y][xo + x]));
-        }
-      }
-      lane_sync();
-    }
-  } else {
-    const int bs = t >> 4, p = t & 15;
-#pragma unroll 1
-    for (int s = 0; s <= 9; ++s) {
-      const int blk = i4_step_blk(s, bs);
-      const int bx = blk & 3, by = blk >> 2;
-      const uint32_t i4w = blk >= 8 ? i4w1 : i4w0;
-      const int m4 = blk >= 0 ? (i4w >> (((blk >> 1) & 3) * 8 + (blk & 1) * 4)) & 15 : 0;
-      const bool top = by > 0 || B, left = bx > 0 || A;
-      const bool tl = (bx > 0 && by > 0) || (by == 0 && bx > 0 ? B : (bx == 0 && by > 0 ? A : D));
-      const bool tr = by == 0 ? (bx < 3 ? B : C) : (bx < 3 && blkidx((by - 1) * 4 + bx + 1) < blkidx(blk));
-      const int ty = by * 4, tx = 4 + bx * 4;
-      if (blk >= 0) {  // E[p] (p < 15) / DC (p = 15)
-        int v;
-        if (p <= 4) {
-          const int y = p <= 1 ? 3 : 4 - p;  // E[0] = E[1] = L[4] = p[-1,3]; E[2..4] = p[-1, 2..0]
-          v = left ? T.y[ty + 1 + y][tx - 1] : 0;
-        } else if (p == 5) {
-          v = tl ? T.y[ty][tx - 1] : 0;
-        } else if (p < 15) {
-          const int x = min(p - 6, 7);  // E[6 + x] = p[x,-1]; E[14] = E[13]
-          if (x < 4) v = top ? T.y[ty][tx + x] : 0;
-          else v = tr ? T.y[ty][tx + x] : (top ? T.y[ty][tx + 3] : 0);
-        } else {
-          int st = 0, sl = 0;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            st += T.y[ty][tx + i];
-            sl += T.y[ty + 1 + i][tx - 1];
-          }
-          v = (top && left) ? (st + sl + 4) >> 3 : (left ? (sl + 2) >> 2 : (top ? (st + 2) >> 2 : 128));
-        }
-        T.e4[bs][p] = static_cast<uint8_t>(v);
-      }
-      lane_sync();
-      if (blk >= 0) {
-        const int x = p & 3, y = p >> 2;
-        const int idx = s_off4[16 * min(m4, 8) + p];  // > 8: not a mode (as mode 8)
-        const uint8_t *e = T.e4[bs];
-        const int k = idx >= 32 ? idx - 32 : (idx >= 16 ? idx - 16 : idx);
-        const int e0 = e[min(k, 15)], e1 = e[min(k + 1, 15)], e2 = e[min(k + 2, 15)];
-        const int v = idx < 16 ? e0 : (idx < 32 ? (e0 + 2 * e1 + e2 + 2) >> 2 : (idx < 47 ? (e1 + e2 + 1) >> 1 : e[15]));
-        T.y[ty + 1 + y][tx + x] = static_cast<uint8_t>(c255(v + T.lres[by * 4 + y][bx * 4 + x]));
-      }
-      lane_sync();
-    }
-  }
-  RPROF(4);
-  // ---- chroma (8.3.4): lane t = plane t >> 4, 4x4 block (t >> 2) & 3, row t & 3
-  {
-    const int pl = t >> 4, ck = (t >> 2) & 3, yy = t & 3, ox = (ck & 1) * 4, oy = (ck >> 1) * 4;
-    const int cm = (h.modes >> 2) & 3;
-    const uint8_t(*Cp)[12] = T.c[pl];  // Cp[0][1 + x] = p[x,-1], Cp[1 + y][0] = p[-1,y], Cp[0][0] = p[-1,-1]
-    int v[4];
-    if (cm == 0) {
-      int st = 0, sl = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        st += Cp[0][1 + ox + i];
-        sl += Cp[1 + oy + i][0];
-      }
-      int dc = 128;
-      if ((ox == 0 && oy == 0) || (ox && oy)) {
-        if (B && A) dc = (st + sl + 4) >> 3;
-        else if (A) dc = (sl + 2) >> 2;
-        else if (B) dc = (st + 2) >> 2;
-      } else if (ox) {
-        if (B) dc = (st + 2) >> 2;
-        else if (A) dc = (sl + 2) >> 2;
-      } else {
-        if (A) dc = (sl + 2) >> 2;
-        else if (B) dc = (st + 2) >> 2;
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x) v[x] = dc;
-    } else if (cm == 1) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x) v[x] = Cp[1 + oy + yy][0];
-    } else if (cm == 2) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x) v[x] = Cp[0][1 + ox + x];
-    } else {
-      int Hh = 0, Vv = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        Hh += (i + 1) * (Cp[0][1 + 4 + i] - Cp[0][1 + 2 - i]);
-        Vv += (i + 1) * (Cp[1 + 4 + i][0] - (2 - i >= 0 ? Cp[1 + 2 - i][0] : Cp[0][0]));
-      }
-      const int aa = 16 * (Cp[8][0] + Cp[0][8]);
-      const int bb = (34 * Hh + 32) >> 6, cc = (34 * Vv + 32) >> 6;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) v[x] = c255((aa + bb * (ox + x - 3) + cc * (oy + yy - 3) + 16) >> 5);
-    }
-    lane_sync();  // every border read before the samples overwrite the tile's inside
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-      T.c[pl][1 + oy + yy][1 + ox + x] = static_cast<uint8_t>(c255(v[x] + T.cres[pl][oy + yy][ox + x]));
-  }
-  lane_sync();
-  RPROF(5);
-  // ---- the macroblock to HBM (whole rows) and its bottom row / right column
-  // to the line buffers
-  uint8_t *lme = lby + (my & 1) * pitch + mx * 16, *lcme = lbc + (my & 1) * pitch + mx * 16;
-  uint8_t *rcme = rcl + my * 32;
-  if (t < 16) {
-    const uint8_t *src = &T.y[1 + t][4];
-    const uint4 row = make_uint4(*reinterpret_cast<const uint32_t *>(src), *reinterpret_cast<const uint32_t *>(src + 4),
-                                 *reinterpret_cast<const uint32_t *>(src + 8), *reinterpret_cast<const uint32_t *>(src + 12));
-    *reinterpret_cast<uint4 *>(Y + yrow0 + static_cast<int64_t>(t) * pitch) = row;
-    if (t == 15) *reinterpret_cast<uint4 *>(lme) = row;
-    rcme[t] = src[15];
-  } else if (t < 24) {
-    const int r = t - 16;
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = pack4(T.c[0][1 + r][1 + 2 * i], T.c[1][1 + r][1 + 2 * i], T.c[0][1 + r][2 + 2 * i], T.c[1][1 + r][2 + 2 * i]);
-    const uint4 row = make_uint4(w[0], w[1], w[2], w[3]);
-    *reinterpret_cast<uint4 *>(UV + crow0 + static_cast<int64_t>(r) * pitch) = row;
-    if (r == 7) *reinterpret_cast<uint4 *>(lcme) = row;
-    rcme[16 + 2 * r] = T.c[0][1 + r][8];
-    rcme[17 + 2 * r] = T.c[1][1 + r][8];
-  }
-  lane_sync();
-}
-
-// grid: pictures of the level; dynamic LDS: the level lists (2 B per
-// macroblock), the bottom-row line buffers (2 x pitch luma + 2 x pitch
-// chroma) and the right columns (32 B per macroblock row)
+// grid: pictures of the level; dynamic LDS: the tagged line entries (one per
+// macroblock column and row, i2::I2Line) and the level lists (2 B per
+// macroblock)
 __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
   __shared__ I2Tile tiles[kI2Groups];
@@ -1633,10 +1173,11 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
   __shared__ int s_lvl[kIntraLevels + 1], s_fill[kIntraLevels];
   __shared__ __attribute__((aligned(4))) uint8_t s_off4[9 * 16];
   __shared__ __attribute__((aligned(4))) uint8_t s_off8[9 * 64];
-  const int mbh = a.P.mb_height, nmb = a.P.mb_width * mbh;
+  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
   const int pitch = a.pitch;
-  uint8_t *lby = s_dyn, *lbc = s_dyn + 2 * pitch, *rcl = s_dyn + 4 * pitch;
-  uint16_t *s_list = reinterpret_cast<uint16_t *>(s_dyn + 4 * pitch + 32 * mbh);
+  i2::I2Line *lcol = reinterpret_cast<i2::I2Line *>(s_dyn), *lrow = lcol + mbw;
+  uint16_t *s_list = reinterpret_cast<uint16_t *>(lrow + mbh);
+  for (int i = threadIdx.x; i < mbw + mbh; i += kI2Threads) lcol[i].tag = -2;
   const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;
@@ -1653,7 +1194,22 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
   if (m >= 0) atomicMax(&s_max, m);
   __syncthreads();
   const int maxl = s_max;
-  const int g = tid >> 5, t = tid & 31;
+  const int g = tid >> 5;
+  const DevLanes lanes{tid & 31};
+  i2::I2Ctx ctx;
+  ctx.recs = a.recs + static_cast<int64_t>(slot) * nmb;
+  ctx.arena = a.arena;
+  ctx.Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
+  ctx.uv_off = a.uv_off;
+  ctx.pitch = pitch;
+  ctx.mbw = a.P.mb_width;
+  ctx.mbh = mbh;
+  ctx.epoch = a.epoch;
+  ctx.cip = a.P.cip;
+  ctx.cqp_off = a.P.cqp_off;
+  ctx.cqp_off2 = a.P.cqp_off2;
+  ctx.scaled = a.P.scaled;
+  ctx.sct = a.sct;
   const bool bucketed = maxl < kIntraLevels;
   if (bucketed) {  // the intra macroblocks bucketed by level (counting sort), as h264_intra_full
     for (int i = tid; i <= maxl + 1; i += kI2Threads) s_lvl[i] = 0;
@@ -1689,13 +1245,22 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
       j0 = 0;
       j1 = s_cnt;
     }
-    for (int j = j0 + g; j < j1; j += kI2Groups) {
-      intra2_mb(a, slot, s_list[j], t, tiles[g], lby, lbc, rcl, s_off4, s_off8, rp_);
-      RPROF_COUNT(7, 1);
+    // rounds of 32 macroblocks: every group's reads (part 1), barrier, every
+    // group's reconstruction and writes (part 2), barrier
+    for (int base = j0; base < j1; base += kI2Groups) {
+      const int j = base + g;
+      if (j < j1) i2::intra2_prepare(ctx, s_list[j], lanes, tiles[g], lcol, lrow, rp_);
+      RPROF(1);
+      __syncthreads();
+      RPROF(2);
+      if (j < j1) {
+        i2::intra2_finish(ctx, lanes, tiles[g], lcol, lrow, s_off4, s_off8, rp_);
+        RPROF_COUNT(7, 1);
+      }
+      RPROF(1);
+      __syncthreads();
+      RPROF(2);
     }
-    RPROF(1);
-    __syncthreads();
-    RPROF(2);
     RPROF_COUNT(6, 1);
   }
   RPROF_FLUSH(8);
@@ -2444,7 +2009,7 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_inter_full launch: %s", hipGetErrorString(e));
   // lane-parallel intra (default) while its LDS fits, else the by-block kernel
-  const size_t i2_dyn = 4 * static_cast<size_t>(a.pitch) + 32 * static_cast<size_t>(a.P.mb_height) + 2 * static_cast<size_t>(nmb);
+  const size_t i2_dyn = sizeof(i2::I2Line) * static_cast<size_t>(a.P.mb_width + a.P.mb_height) + 2 * static_cast<size_t>(nmb);
   if (a.intra_kernel != 1 && i2_dyn + sizeof(I2Tile) * kI2Groups + 8 * 1024 <= 160 * 1024) {
     hipLaunchKernelGGL(h264_intra_v2, dim3(n_frames), dim3(kI2Threads), i2_dyn, s, a);
     e = hipGetLastError();
