@@ -53,6 +53,7 @@ struct HostLanes {
     g->bar.arrive_and_wait();
     return s;
   }
+  void amax(int *p, int v) const { *p = std::max(*p, v); }  // one macroblock at a time on the host
   int bcast(int v, int l) const {
     g->bar.arrive_and_wait();
     g->buf[t] = v;
@@ -71,7 +72,7 @@ void intra_lanes_picture(const i2::I2Ctx &ctx, const uint16_t *lv) {
     if (lv[i] != kNoLevel) order.emplace_back(lv[i], i);
   std::stable_sort(order.begin(), order.end());
   std::vector<i2::I2Line> lines(static_cast<size_t>(ctx.mbw + ctx.mbh));
-  for (auto &l : lines) l.tag = -2;
+  for (auto &l : lines) l.tag = l.claim = -2;
   i2::I2Line *lcol = lines.data(), *lrow = lines.data() + ctx.mbw;
   uint8_t off4[9 * 16], off8[9 * 64];
   for (int i = 0; i < 9 * 16; ++i) off4[i] = static_cast<uint8_t>(i2::i2_intra4_off(i >> 4, i & 3, (i >> 2) & 3));

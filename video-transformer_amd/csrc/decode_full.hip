@@ -1161,6 +1161,7 @@ struct DevLanes {
     return v;
   }
   __device__ __forceinline__ int bcast(int v, int l) const { return __shfl(v, static_cast<int>(threadIdx.x & 32) + l); }
+  __device__ __forceinline__ void amax(int *p, int v) const { atomicMax(p, v); }
 };
 
 // grid: pictures of the level; dynamic LDS: the tagged line entries (one per
@@ -1177,7 +1178,10 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
   const int pitch = a.pitch;
   i2::I2Line *lcol = reinterpret_cast<i2::I2Line *>(s_dyn), *lrow = lcol + mbw;
   uint16_t *s_list = reinterpret_cast<uint16_t *>(lrow + mbh);
-  for (int i = threadIdx.x; i < mbw + mbh; i += kI2Threads) lcol[i].tag = -2;
+  for (int i = threadIdx.x; i < mbw + mbh; i += kI2Threads) {
+    lcol[i].tag = -2;
+    lcol[i].claim = -2;
+  }
   const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;

@@ -239,7 +239,10 @@ VTS_I2 int i4_step_blk(int s, int slot) {
 // neighbour: a reader checks the tag and takes HBM instead (written a level
 // earlier: visible after the level barrier).
 struct alignas(16) I2Line {
-  int32_t tag, _p[3];
+  int32_t tag;    // the writer's row (column entry) / column (row entry); -2 none
+  int32_t claim;  // the largest writer of the entry so far: only it writes (a round may hold
+                  // several macroblocks of one column or row: isolated intra ones, level 0)
+  int32_t _p[2];
   uint8_t y[16];  // luma: the bottom row (column entry) / the right column (row entry)
   uint8_t c[16];  // chroma: interleaved bottom row / right column (Cb, Cr of rows 0..7)
 };
@@ -466,6 +469,10 @@ VTS_HD VTS_INLINE void intra2_prepare(const I2Ctx &a, int mb, const Lanes &L, I2
       T.c[1][0][2 + c0] = v >> 24;
     }
   }
+  if (t == 0) {  // claim this macroblock's entries (part 2 writes those it still holds)
+    L.amax(&const_cast<I2Line *>(lcol)[mx].claim, my);
+    L.amax(&const_cast<I2Line *>(lrow)[my].claim, mx);
+  }
   if (t == 31) {  // what part 2 needs of the header and the neighbourhood
     T.meta[0] = mb;
     T.meta[1] = h.type | (h.modes << 8) | (h.qp << 16);
@@ -688,12 +695,13 @@ VTS_HD VTS_INLINE void intra2_finish(const I2Ctx &a, const Lanes &L, I2Tile &T, 
   // ---- the macroblock to HBM (whole rows) and its bottom row / right column
   // to the line buffers
   I2Line &lme = lcol[mx], &rme = lrow[my];
+  const bool wcol = lme.claim == my, wrow = rme.claim == mx;  // the only writer of the entry this round
   if (t < 16) {
     const uint8_t *src = &T.y[1 + t][4];
     const I2V4 row = i2_ld4(src);
     i2_st4(Y + yrow0 + static_cast<int64_t>(t) * pitch, row);
-    if (t == 15) i2_st4(lme.y, row);
-    rme.y[t] = src[15];
+    if (t == 15 && wcol) i2_st4(lme.y, row);
+    if (wrow) rme.y[t] = src[15];
   } else if (t < 24) {
     const int r = t - 16;
     uint32_t w[4];
@@ -702,12 +710,14 @@ VTS_HD VTS_INLINE void intra2_finish(const I2Ctx &a, const Lanes &L, I2Tile &T, 
       w[i] = i2_pack4(T.c[0][1 + r][1 + 2 * i], T.c[1][1 + r][1 + 2 * i], T.c[0][1 + r][2 + 2 * i], T.c[1][1 + r][2 + 2 * i]);
     const I2V4 row = {w[0], w[1], w[2], w[3]};
     i2_st4(UV + crow0 + static_cast<int64_t>(r) * pitch, row);
-    if (r == 7) i2_st4(lme.c, row);
-    rme.c[2 * r] = T.c[0][1 + r][8];
-    rme.c[2 * r + 1] = T.c[1][1 + r][8];
+    if (r == 7 && wcol) i2_st4(lme.c, row);
+    if (wrow) {
+      rme.c[2 * r] = T.c[0][1 + r][8];
+      rme.c[2 * r + 1] = T.c[1][1 + r][8];
+    }
   } else if (t == 24) {
-    lme.tag = my;
-    rme.tag = mx;
+    if (wcol) lme.tag = my;
+    if (wrow) rme.tag = mx;
   }
   L.sync();
 }
