@@ -84,8 +84,15 @@ void intra_lanes_picture(const i2::I2Ctx &ctx, const uint16_t *lv) {
     th.emplace_back([&, t]() {
       const HostLanes L{t, &grp};
       i2::I2NoProf np;
-      for (const auto &o : order) {
-        i2::intra2_prepare(ctx, o.second, L, *T, lcol, lrow, np);
+      // every macroblock's prefetch before any reconstruction: the kernel
+      // prefetches a level ahead, so the border samples of neighbours this
+      // launch reconstructs may predate them (part 1 must not use those)
+      std::vector<i2::I2Pre> pre(order.size());
+      for (size_t k = 0; k < order.size(); ++k) pre[k] = i2::i2_prefetch(ctx, order[k].second, t);
+      L.sync();
+      for (size_t k = 0; k < order.size(); ++k) {
+        const auto &o = order[k];
+        i2::intra2_prepare(ctx, o.second, pre[k], L, *T, lcol, lrow, np);
         L.sync();
         i2::intra2_finish(ctx, L, *T, lcol, lrow, off4, off8, np);
         L.sync();

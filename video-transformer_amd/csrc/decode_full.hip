@@ -1234,6 +1234,20 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
     }
     __syncthreads();
   }
+  // the group processes s_lvl[l] + g + 32 k of every level l, in order: its
+  // first macroblock at level l0 or later (-1: none)
+  auto first_at = [&](int l0) -> int {
+    for (int l = l0; l <= maxl; ++l)
+      if (s_lvl[l] + g < s_lvl[l + 1]) return s_lvl[l] + g;
+    return -1;
+  };
+  i2::I2Pre pre{};
+  bool pv = false;  // pre holds the group's next macroblock
+  if (bucketed) {
+    const int jf = first_at(0);
+    pv = jf >= 0;
+    if (pv) pre = i2::i2_prefetch(ctx, s_list[jf], lanes.t);
+  }
   RPROF(0);
   for (int l = 0; l <= maxl; ++l) {
     int j0, j1;
@@ -1250,16 +1264,29 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
       j1 = s_cnt;
     }
     // rounds of 32 macroblocks: every group's reads (part 1), barrier, every
-    // group's reconstruction and writes (part 2), barrier
+    // group's reconstruction and writes (part 2), the group's next
+    // macroblock's records and border loads issued (in flight across the
+    // barrier), barrier
     for (int base = j0; base < j1; base += kI2Groups) {
       const int j = base + g;
-      if (j < j1) i2::intra2_prepare(ctx, s_list[j], lanes, tiles[g], lcol, lrow, rp_);
+      if (j < j1) {
+        if (!pv) pre = i2::i2_prefetch(ctx, s_list[j], lanes.t);
+        i2::intra2_prepare(ctx, s_list[j], pre, lanes, tiles[g], lcol, lrow, rp_);
+      } else {
+        // no macroblock this round: drop the prefetch (re-issued when the
+        // group has work again) rather than keep its registers across part 2
+        pre = i2::I2Pre{};
+        pv = false;
+      }
       RPROF(1);
       __syncthreads();
       RPROF(2);
       if (j < j1) {
         i2::intra2_finish(ctx, lanes, tiles[g], lcol, lrow, s_off4, s_off8, rp_);
         RPROF_COUNT(7, 1);
+        const int jn = !bucketed ? -1 : (j + kI2Groups < j1 ? j + kI2Groups : first_at(l + 1));
+        pv = jn >= 0;
+        if (pv) pre = i2::i2_prefetch(ctx, s_list[jn], lanes.t);
       }
       RPROF(1);
       __syncthreads();

@@ -247,24 +247,142 @@ struct alignas(16) I2Line {
   uint8_t c[16];  // chroma: interleaved bottom row / right column (Cb, Cr of rows 0..7)
 };
 
-// Part 1, reads only: the macroblock's residuals and its neighbourhood into
+// What part 1 reads from HBM that no reconstruction of this launch changes:
+// the macroblock's header and Intra_NxN mode words, its neighbours' headers,
+// and the border samples as HBM holds them (final for inter / I_PCM
+// neighbours; a neighbour this launch reconstructs comes from the line entries,
+// or is re-read in part 1 when its entry was overwritten).  The kernel loads
+// the next macroblock's at the end of part 2, so the loads cross the barrier
+// in flight and part 1 waits only for the coefficients.
+struct I2Pre {
+  I2Hdr h;
+  uint32_t i4w0, i4w1;
+  I2V2 hA, hB, hC, hD;
+  uint32_t tA, tB, tC, tD;
+  uint32_t gTop, gCl, gCt;
+  uint32_t gLeft;
+};
+// lane t: row -1 dword t (t < 7, cols -4 + 4t), col -1 of row t - 8 (8..23),
+// chroma col -1 dword of row t - 24 (24..31), chroma row -1 dword t (t < 5)
+VTS_I2 const uint8_t *i2_top_at(const I2Ctx &a, int mb, int t) {
+  const int mx = mb % a.mbw, my = mb / a.mbw;
+  const int64_t yrow0 = static_cast<int64_t>(my * 16) * a.pitch + mx * 16;
+  const int64_t up = my > 0 ? yrow0 - a.pitch : yrow0;
+  return a.Y + i2_max(up - 4 + 4 * i2_min(t, 6), static_cast<int64_t>(0));
+}
+VTS_I2 const uint8_t *i2_left_at(const I2Ctx &a, int mb, int t) {
+  const int mx = mb % a.mbw, my = mb / a.mbw;
+  const int64_t yrow0 = static_cast<int64_t>(my * 16) * a.pitch + mx * 16;
+  return a.Y + i2_max(yrow0 + static_cast<int64_t>(i2_min(i2_max(t - 8, 0), 15)) * a.pitch - 1, static_cast<int64_t>(0));
+}
+VTS_I2 const uint8_t *i2_cleft_at(const I2Ctx &a, int mb, int t) {
+  const int mx = mb % a.mbw, my = mb / a.mbw;
+  const int64_t crow0 = static_cast<int64_t>(my * 8) * a.pitch + mx * 16;
+  return a.Y + a.uv_off + crow0 + static_cast<int64_t>(i2_min(i2_max(t - 24, 0), 7)) * a.pitch - 4;
+}
+VTS_I2 const uint8_t *i2_ctop_at(const I2Ctx &a, int mb, int t) {
+  const int mx = mb % a.mbw, my = mb / a.mbw;
+  const int64_t crow0 = static_cast<int64_t>(my * 8) * a.pitch + mx * 16;
+  return a.Y + a.uv_off + crow0 - a.pitch - 4 + 4 * i2_min(t, 4);
+}
+VTS_I2 I2Pre i2_prefetch(const I2Ctx &a, int mb, int t) {
+  const int mbw = a.mbw, mx = mb % mbw, my = mb / mbw;
+  const MbRec *frecs = a.recs, *rec = a.recs + mb;
+  I2Pre p;
+  p.h = i2_hdr(rec);
+  p.i4w0 = reinterpret_cast<const uint32_t *>(rec)[8];
+  p.i4w1 = reinterpret_cast<const uint32_t *>(rec)[9];
+  const int nA = mx > 0 ? mb - 1 : mb, nB = my > 0 ? mb - mbw : mb;
+  const int nC = my > 0 && mx < mbw - 1 ? mb - mbw + 1 : mb, nD = mx > 0 && my > 0 ? mb - mbw - 1 : mb;
+  p.hA = i2_ld2(frecs + nA);
+  p.hB = i2_ld2(frecs + nB);
+  p.hC = i2_ld2(frecs + nC);
+  p.hD = i2_ld2(frecs + nD);
+  p.tA = reinterpret_cast<const uint32_t *>(frecs + nA)[4];
+  p.tB = reinterpret_cast<const uint32_t *>(frecs + nB)[4];
+  p.tC = reinterpret_cast<const uint32_t *>(frecs + nC)[4];
+  p.tD = reinterpret_cast<const uint32_t *>(frecs + nD)[4];
+  p.gTop = *reinterpret_cast<const uint32_t *>(i2_top_at(a, mb, t));
+  p.gLeft = *i2_left_at(a, mb, t);
+  p.gCl = *reinterpret_cast<const uint32_t *>(i2_cleft_at(a, mb, t));
+  p.gCt = *reinterpret_cast<const uint32_t *>(i2_ctop_at(a, mb, t));
+  return p;
+}
+
+// Part 1, reads only: the macroblock's neighbourhood and its residuals into
 // its tile.  Part 2 (intra2_finish) predicts, reconstructs and writes.  The
 // kernel runs part 1 of a round of macroblocks, a workgroup barrier, part 2,
 // a barrier: no line-buffer entry is read while another lane writes it.
 template <class Lanes, class Prof>
-VTS_HD VTS_INLINE void intra2_prepare(const I2Ctx &a, int mb, const Lanes &L, I2Tile &T, const I2Line *lcol,
-                                      const I2Line *lrow, Prof &rp_) {
+VTS_HD VTS_INLINE void intra2_prepare(const I2Ctx &a, int mb, const I2Pre &pre, const Lanes &L, I2Tile &T,
+                                      const I2Line *lcol, const I2Line *lrow, Prof &rp_) {
   const int t = L.t;
   const int mbw = a.mbw;
-  const int pitch = a.pitch;
-  const MbRec *frecs = a.recs;
-  const MbRec *rec = frecs + mb;
-  const I2Hdr h = i2_hdr(rec);
+  const I2Hdr h = pre.h;
   const int mx = mb % mbw, my = mb / mbw;
-  uint8_t *Y = a.Y;
-  uint8_t *UV = Y + a.uv_off;
   const int qp = h.qp;
   const bool i16 = h.type == kMbI16, t8 = !i16 && (h.modes & kModeT8);
+  const uint32_t i4w0 = pre.i4w0, i4w1 = pre.i4w1;
+  const I2V2 hA = pre.hA, hB = pre.hB, hC = pre.hC, hD = pre.hD;
+  const uint32_t tA = pre.tA, tB = pre.tB, tC = pre.tC, tD = pre.tD;
+  // ---- neighbourhood: availability (6.4.11.1, constrained_intra_pred), then
+  // the border samples from the line buffers (neighbours this launch
+  // reconstructed) or HBM (the others); unavailable samples read as 0
+  auto nb_ok = [&](bool exists, I2V2 u, uint32_t ty) -> bool {
+    if (!exists || u.x != a.epoch || u.y != h.slice) return false;
+    if (a.cip && ((ty & 255) == kMbInter || (ty & 255) == kMbSkip)) return false;
+    return true;
+  };
+  auto mine = [](uint32_t ty) { return (ty & 255) == kMbI4x4 || (ty & 255) == kMbI16; };
+  const bool A = nb_ok(mx > 0, hA, tA), B = nb_ok(my > 0, hB, tB);
+  const bool C = nb_ok(my > 0 && mx < mbw - 1, hC, tC), D = nb_ok(mx > 0 && my > 0, hD, tD);
+  // the tagged line entries this macroblock's neighbours would have written
+  const I2Line &lB = lcol[mx], &lC = lcol[i2_min(mx + 1, mbw - 1)], &lD = lcol[i2_max(mx - 1, 0)];
+  const I2Line &lA = lrow[my];
+  const bool mB = B && mine(tB) && lB.tag == my - 1, mC = C && mine(tC) && lC.tag == my - 1;
+  const bool mD = D && mine(tD) && lD.tag == my - 1, mA = A && mine(tA) && lA.tag == mx - 1;
+  // a neighbour this launch reconstructed whose entry another macroblock took
+  // over: its samples from HBM now (the prefetched ones predate them)
+  const bool sD = D && mine(tD) && !mD, sB = B && mine(tB) && !mB, sC = C && mine(tC) && !mC, sA = A && mine(tA) && !mA;
+  const uint32_t gTop = (t == 0 ? sD : (t < 5 ? sB : sC)) ? *reinterpret_cast<const uint32_t *>(i2_top_at(a, mb, t)) : pre.gTop;
+  const uint8_t gLeft = sA ? *i2_left_at(a, mb, t) : static_cast<uint8_t>(pre.gLeft);
+  const uint32_t gCl = sA ? *reinterpret_cast<const uint32_t *>(i2_cleft_at(a, mb, t)) : pre.gCl;
+  const uint32_t gCt = (t == 0 ? sD : sB) ? *reinterpret_cast<const uint32_t *>(i2_ctop_at(a, mb, t)) : pre.gCt;
+  if (t < 7) {  // row -1 dword t: cols -4 + 4t .. -1 + 4t (D | B | C)
+    const bool ok = t == 0 ? D : (t < 5 ? B : C);
+    uint32_t v = gTop;
+    if (t == 0 && mD) v = *reinterpret_cast<const uint32_t *>(&lD.y[12]);
+    if (t >= 1 && t < 5 && mB) v = *reinterpret_cast<const uint32_t *>(&lB.y[4 * (t - 1)]);
+    if (t >= 5 && mC) v = *reinterpret_cast<const uint32_t *>(&lC.y[4 * (t - 5)]);
+    *reinterpret_cast<uint32_t *>(&T.y[0][4 * t]) = ok ? v : 0u;
+  }
+  if (t >= 8 && t < 24) {
+    const int r = t - 8;
+    T.y[1 + r][3] = A ? (mA ? lA.y[r] : gLeft) : 0;
+  }
+  if (t >= 24) {  // chroma col -1, row t - 24: bytes 2, 3 of the dword (Cb, Cr of col -1)
+    const int r = t - 24;
+    const uint32_t v = mA ? (static_cast<uint32_t>(lA.c[2 * r]) << 16) | (static_cast<uint32_t>(lA.c[2 * r + 1]) << 24) : gCl;
+    T.c[0][1 + r][0] = A ? (v >> 16) & 255 : 0;
+    T.c[1][1 + r][0] = A ? v >> 24 : 0;
+  }
+  if (t < 5) {  // chroma row -1 dword t: interleaved bytes -4 + 4t (t = 0: D's col -1, else B)
+    const bool ok = t == 0 ? D : B;
+    uint32_t v0 = gCt;
+    if (t == 0 && mD) v0 = *reinterpret_cast<const uint32_t *>(&lD.c[12]);
+    if (t >= 1 && mB) v0 = *reinterpret_cast<const uint32_t *>(&lB.c[4 * (t - 1)]);
+    const uint32_t v = ok ? v0 : 0u;
+    if (t == 0) {
+      T.c[0][0][0] = (v >> 16) & 255;
+      T.c[1][0][0] = v >> 24;
+    } else {
+      const int c0 = 2 * (t - 1);
+      T.c[0][0][1 + c0] = v & 255;
+      T.c[1][0][1 + c0] = (v >> 8) & 255;
+      T.c[0][0][2 + c0] = (v >> 16) & 255;
+      T.c[1][0][2 + c0] = v >> 24;
+    }
+  }
   // ---- residuals (8.5.12 / 8.5.13), in two passes through the tile so no lane
   // holds a whole block: pass 1 scales and transforms rows (luma: 4x4 rows two
   // per lane, or 8x8 rows one per lane; chroma: one 4x4 row per lane), pass 2
@@ -397,76 +515,6 @@ VTS_HD VTS_INLINE void intra2_prepare(const I2Ctx &a, int mb, const Lanes &L, I2
       C[r0 + 1][col] = (g1 + g2 + 32) >> 6;
       C[r0 + 2][col] = (g1 - g2 + 32) >> 6;
       C[r0 + 3][col] = (g0 - g3 + 32) >> 6;
-    }
-  }
-  // the neighbours' headers and the border samples as HBM holds them (right for
-  // inter / I_PCM neighbours), all loads at once from clamped addresses (after
-  // the residuals: their registers and these do not overlap)
-  const int nA = mx > 0 ? mb - 1 : mb, nB = my > 0 ? mb - mbw : mb;
-  const int nC = my > 0 && mx < mbw - 1 ? mb - mbw + 1 : mb, nD = mx > 0 && my > 0 ? mb - mbw - 1 : mb;
-  const I2V2 hA = i2_ld2(frecs + nA), hB = i2_ld2(frecs + nB);
-  const I2V2 hC = i2_ld2(frecs + nC), hD = i2_ld2(frecs + nD);
-  const uint32_t tA = reinterpret_cast<const uint32_t *>(frecs + nA)[4], tB = reinterpret_cast<const uint32_t *>(frecs + nB)[4];
-  const uint32_t tC = reinterpret_cast<const uint32_t *>(frecs + nC)[4], tD = reinterpret_cast<const uint32_t *>(frecs + nD)[4];
-  const uint32_t i4w0 = reinterpret_cast<const uint32_t *>(rec)[8], i4w1 = reinterpret_cast<const uint32_t *>(rec)[9];
-  const int64_t yrow0 = static_cast<int64_t>(my * 16) * pitch + mx * 16;
-  const int64_t crow0 = static_cast<int64_t>(my * 8) * pitch + mx * 16;
-  const int64_t up = my > 0 ? yrow0 - pitch : yrow0;
-  // lanes 0..6: row -1 dword (cols -4 + 4t); 8..23: col -1 of row t - 8;
-  // 24..31: chroma col -1 dword of row t - 24; lanes 0..4 also chroma row -1 dword t
-  const uint32_t gTop = *reinterpret_cast<const uint32_t *>(Y + i2_max(up - 4 + 4 * i2_min(t, 6), static_cast<int64_t>(0)));
-  const uint8_t gLeft = Y[i2_max(yrow0 + static_cast<int64_t>(i2_min(i2_max(t - 8, 0), 15)) * pitch - 1, static_cast<int64_t>(0))];
-  const uint32_t gCl = *reinterpret_cast<const uint32_t *>(UV + crow0 + static_cast<int64_t>(i2_min(i2_max(t - 24, 0), 7)) * pitch - 4);
-  const uint32_t gCt = *reinterpret_cast<const uint32_t *>(UV + crow0 - pitch - 4 + 4 * i2_min(t, 4));
-  // ---- neighbourhood: availability (6.4.11.1, constrained_intra_pred), then
-  // the border samples from the line buffers (neighbours this launch
-  // reconstructed) or HBM (the others); unavailable samples read as 0
-  auto nb_ok = [&](bool exists, I2V2 u, uint32_t ty) -> bool {
-    if (!exists || u.x != a.epoch || u.y != h.slice) return false;
-    if (a.cip && ((ty & 255) == kMbInter || (ty & 255) == kMbSkip)) return false;
-    return true;
-  };
-  auto mine = [](uint32_t ty) { return (ty & 255) == kMbI4x4 || (ty & 255) == kMbI16; };
-  const bool A = nb_ok(mx > 0, hA, tA), B = nb_ok(my > 0, hB, tB);
-  const bool C = nb_ok(my > 0 && mx < mbw - 1, hC, tC), D = nb_ok(mx > 0 && my > 0, hD, tD);
-  // the tagged line entries this macroblock's neighbours would have written
-  const I2Line &lB = lcol[mx], &lC = lcol[i2_min(mx + 1, mbw - 1)], &lD = lcol[i2_max(mx - 1, 0)];
-  const I2Line &lA = lrow[my];
-  const bool mB = B && mine(tB) && lB.tag == my - 1, mC = C && mine(tC) && lC.tag == my - 1;
-  const bool mD = D && mine(tD) && lD.tag == my - 1, mA = A && mine(tA) && lA.tag == mx - 1;
-  if (t < 7) {  // row -1 dword t: cols -4 + 4t .. -1 + 4t (D | B | C)
-    const bool ok = t == 0 ? D : (t < 5 ? B : C);
-    uint32_t v = gTop;
-    if (t == 0 && mD) v = *reinterpret_cast<const uint32_t *>(&lD.y[12]);
-    if (t >= 1 && t < 5 && mB) v = *reinterpret_cast<const uint32_t *>(&lB.y[4 * (t - 1)]);
-    if (t >= 5 && mC) v = *reinterpret_cast<const uint32_t *>(&lC.y[4 * (t - 5)]);
-    *reinterpret_cast<uint32_t *>(&T.y[0][4 * t]) = ok ? v : 0u;
-  }
-  if (t >= 8 && t < 24) {
-    const int r = t - 8;
-    T.y[1 + r][3] = A ? (mA ? lA.y[r] : gLeft) : 0;
-  }
-  if (t >= 24) {  // chroma col -1, row t - 24: bytes 2, 3 of the dword (Cb, Cr of col -1)
-    const int r = t - 24;
-    const uint32_t v = mA ? (static_cast<uint32_t>(lA.c[2 * r]) << 16) | (static_cast<uint32_t>(lA.c[2 * r + 1]) << 24) : gCl;
-    T.c[0][1 + r][0] = A ? (v >> 16) & 255 : 0;
-    T.c[1][1 + r][0] = A ? v >> 24 : 0;
-  }
-  if (t < 5) {  // chroma row -1 dword t: interleaved bytes -4 + 4t (t = 0: D's col -1, else B)
-    const bool ok = t == 0 ? D : B;
-    uint32_t v0 = gCt;
-    if (t == 0 && mD) v0 = *reinterpret_cast<const uint32_t *>(&lD.c[12]);
-    if (t >= 1 && mB) v0 = *reinterpret_cast<const uint32_t *>(&lB.c[4 * (t - 1)]);
-    const uint32_t v = ok ? v0 : 0u;
-    if (t == 0) {
-      T.c[0][0][0] = (v >> 16) & 255;
-      T.c[1][0][0] = v >> 24;
-    } else {
-      const int c0 = 2 * (t - 1);
-      T.c[0][0][1 + c0] = v & 255;
-      T.c[1][0][1 + c0] = (v >> 8) & 255;
-      T.c[0][0][2 + c0] = (v >> 16) & 255;
-      T.c[1][0][2 + c0] = v >> 24;
     }
   }
   if (t == 0) {  // claim this macroblock's entries (part 2 writes those it still holds)
