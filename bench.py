@@ -45,9 +45,11 @@ Rank 0 prints ONE JSON line (contract in the task statement), including
                  score, results to the host); `long_video`: BASELINE config
                  [2], one 2-h 720p video in streamed two-ring windows;
                  `general`: the general decoder on a 10-min 720p full-syntax
-                 stream (B pictures, weighted prediction, deblocking) with
-                 per-kernel rooflines, the parse's issue rate and the
-                 stream's bits per frame.
+                 noise stream (random syntax: the worst case), and
+                 `general_content` on a 10-min 720p content stream (coded
+                 moving scenes, synth_content.h: the video-like case), each
+                 with per-kernel rooflines, the parse's issue rate, the
+                 stream's bits per frame and planted vs detected scene cuts.
 The rocprofv3 passes are child processes started before this process touches
 the GPU; --profile-dir keeps their summaries.
 """
@@ -302,7 +304,8 @@ def profile_passes(argv: list[str], out_dir: Path, keep_dir: Path | None,
 
 
 def synth_videos(jobs: list[tuple[Path, int]], width: int, height: int, frames: int,
-                 coding: str = "subset", bframes: bool = False, cabac: bool = False) -> list[dict]:
+                 coding: str = "subset", bframes: bool = False, cabac: bool = False,
+                 content: bool = False) -> list[dict]:
     """Write the synthetic H.264/MP4 inputs (vts_synth_write; ctypes releases
     the GIL, so the videos are written in parallel)."""
     from vtseg import scene
@@ -317,6 +320,10 @@ def synth_videos(jobs: list[tuple[Path, int]], width: int, height: int, frames: 
             extra = dict(bframes=True, weighted="implicit") if bframes else {}
             if cabac:
                 extra.update(cabac=True, transform_8x8=True)
+            if content:
+                # coded pictures instead of random syntax (synth_content.h);
+                # x264's default keyint 250 (~8 s) between refresh IDRs
+                extra.update(content=True, gop_max_s=8.0)
             return scene.synth_write(path, width=width, height=height, fps=FPS, n_frames=frames,
                                      seed=seed, coding="full", slices_per_row=0, max_motion=4,
                                      **extra)
@@ -621,10 +628,12 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
 
 
 def run_single(path: Path, *, gpu: int, k: int, steps: int, threads: int, label: str,
-               decoder: str = "auto", prof: dict | None = None, parity: bool = True) -> dict:
+               decoder: str = "auto", prof: dict | None = None, parity: bool = True,
+               planted: list[int] | None = None) -> dict:
     """One video through its session: `steps` timed vts_run calls (inputs
     resident), stage times, the dominant kernel's roofline and parity over
-    every frame against the oracle."""
+    every frame against the oracle; with `planted` (the writer's scene cuts)
+    the device's detected cuts beside them."""
     import torch
     from vtseg import budget_planner as bp
     from vtseg import scene
@@ -652,6 +661,12 @@ def run_single(path: Path, *, gpu: int, k: int, steps: int, threads: int, label:
                "bits_per_frame": round(Path(path).stat().st_size * 8 / F, 1)}
         if not v.general():
             rec["roofline"] = roofline_decode_score([v], prof, W, H, k, F)
+        if planted is not None:
+            det = v.scene_cuts()
+            ps = set(planted)
+            rec["cuts"] = {"planted": len(planted), "detected": len(det),
+                           "detected_at_planted": sum(1 for c in det if c in ps),
+                           "detected_within_1": sum(1 for c in det if {c - 1, c, c + 1} & ps)}
         if parity:
             duration = float(v.info.duration)
             plan = bp.plan_segments_with_budget(duration, REF_CONFIG, 0)
@@ -816,15 +831,19 @@ def main() -> None:
     local_paths = [all_paths[i] for i in local_idx]
 
     # extras' inputs, written before the profile passes (which read them)
-    gen_path = long_path = None
+    gen_path = long_path = content_path = None
+    gen_info = content_info = None
     if extras:
         t0 = time.perf_counter()
         gen_path = tmpdir / "general_720p_10min.mp4"
+        content_path = tmpdir / "general_content_720p_10min.mp4"
         long_path = tmpdir / "long_720p_2h.mp4"
-        with ThreadPoolExecutor(2) as ex:
+        with ThreadPoolExecutor(3) as ex:
             fa = ex.submit(synth_videos, [(gen_path, 0x5EED)], 1280, 720, 18000, "full", True, True)
+            fc = ex.submit(synth_videos, [(content_path, 0x5EED)], 1280, 720, 18000, "full", True, True, True)
             fb = ex.submit(synth_videos, [(long_path, 0x5EED)], 1280, 720, 216000)
-            fa.result()
+            gen_info = fa.result()[0]
+            content_info = fc.result()[0]
             fb.result()
         log(f"extras inputs written in {time.perf_counter() - t0:.1f} s")
 
@@ -846,11 +865,12 @@ def main() -> None:
         prof = profile_passes(child_argv, pdir,
                               Path(args.profile_dir) if args.profile_dir else None)
         if extras:
-            gargv = ["--config", "720p-10min", "--coding", "full", "--bframes",
-                     "--video", str(gen_path)]
-            gprof = profile_passes(gargv, pdir / "general",
-                                   Path(args.profile_dir) / "general" if args.profile_dir else None,
-                                   passes=("trace", GENERAL_PMC))
+            gprof = {}
+            for key, gp in (("general", gen_path), ("general_content", content_path)):
+                gargv = ["--config", "720p-10min", "--coding", "full", "--bframes", "--video", str(gp)]
+                gprof[key] = profile_passes(gargv, pdir / key,
+                                            Path(args.profile_dir) / key if args.profile_dir else None,
+                                            passes=("trace", GENERAL_PMC))
         shutil.rmtree(pdir, ignore_errors=True)
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1071,18 +1091,25 @@ def main() -> None:
         # the batch's sessions give their HBM back before the 2-h video's rings
         for v in sl:
             v.close()
-        for key, p, label in (("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
-                                                        "(216 000 frames), streamed two-ring decode"),
-                              ("general", gen_path, "general decoder: 10-min 720p x264-like "
-                                                    "full-syntax stream (High profile: CABAC, 8x8 "
-                                                    "transform and Intra_8x8, B pyramid with B "
-                                                    "references, spatial direct, implicit weighted "
-                                                    "bi-prediction, 3 references, deblocking, one "
-                                                    "slice per picture)")):
+        for key, p, label, info in (
+                ("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
+                                          "(216 000 frames), streamed two-ring decode", None),
+                ("general", gen_path, "general decoder, worst case: 10-min 720p x264-structured "
+                                      "full-syntax NOISE stream (random syntax decisions and residuals; "
+                                      "High profile: CABAC, 8x8 transform and Intra_8x8, B pyramid with "
+                                      "B references, spatial direct, implicit weighted bi-prediction, 3 "
+                                      "references, deblocking, one slice per picture)", gen_info),
+                ("general_content", content_path, "general decoder, video-like: 10-min 720p CONTENT "
+                                                  "stream (synth_content.h: textured scenes with planted "
+                                                  "cuts, a panning background and moving sprites coded in "
+                                                  "closed loop by SAD decisions with quantised residuals; "
+                                                  "CABAC, 8x8 transform, B pyramid, implicit weights, "
+                                                  "deblocking, keyint ~8 s)", content_info)):
             try:
-                r = run_single(p, gpu=gpu, k=4, steps=3, threads=threads, label=label)
-                if key == "general" and gprof:
-                    r["kernels"] = general_kernel_rooflines(gprof, 1280, 720, 4, r["frames"],
+                r = run_single(p, gpu=gpu, k=4, steps=3, threads=threads, label=label,
+                               planted=info["cuts"] if info else None)
+                if gprof and gprof.get(key):
+                    r["kernels"] = general_kernel_rooflines(gprof[key], 1280, 720, 4, r["frames"],
                                                             80 * 45)
                 extra[key] = r
                 log(f"{key}: {r['value']} frames/s, parity {r.get('parity', {}).get('all_equal')}")

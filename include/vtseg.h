@@ -402,7 +402,13 @@ typedef struct vts_synth_params {
                                    modification, non-reference pictures), QP
                                    changes, the deblocking filter on (idc 0/2,
                                    offsets); bit 4 of edge_cases then turns on
-                                   constrained_intra_pred                     */
+                                   constrained_intra_pred.  Further coding-1
+                                   bits: 5 B pictures, 6 / 7 explicit /
+                                   implicit weights, 8 temporal direct, 10
+                                   CABAC, 11 8x8 transforms, 12 / 13 SPS / PPS
+                                   scaling matrices, 14 content mode (with bit
+                                   5: pictures coded from textured moving
+                                   scenes instead of random syntax)           */
 } vts_synth_params;
 
 typedef struct vts_synth_info {

@@ -440,3 +440,39 @@ def test_sessions_reopened_in_sequence_reuse_the_stream_pool(tmp_path):
         assert np.array_equal(ra.scores, ref["score"]) and np.array_equal(rb.sad, ref["sad"])
     with scene.VideoScorer(path) as v:
         assert np.array_equal(v.score().scores, ref["score"])
+
+
+CONTENT = [
+    ("qvga", dict(width=320, height=240), 90),
+    ("crop_rows", dict(width=320, height=180, slices_per_row=2), 60),
+    ("hd720", dict(width=1280, height=720), 36),
+]
+
+
+@pytest.mark.parametrize("name,kw,n", CONTENT, ids=[c[0] for c in CONTENT])
+def test_content_streams_equal_the_writer_and_the_oracle(tmp_path, name, kw, n):
+    """Content-mode streams (synth_content.h: textured moving scenes coded
+    with skip / direct / 16x16 motion / intra decisions and quantised
+    residuals, x264's structure): the device's frames equal the oracle's and
+    the writer's own closed-loop reconstruction (recon_hash), and the device
+    scorer finds the planted cuts."""
+    _require_gpu()
+    kw = dict(kw)
+    spr = kw.pop("slices_per_row", 0)
+    path = tmp_path / f"content_{name}.mp4"
+    info = scene.synth_write(path, n_frames=n, coding="full", slices_per_row=spr, max_motion=4, bframes=True,
+                             weighted="implicit", cabac=True, transform_8x8=True, content=True, hash_frames=True,
+                             cut_min_s=0.5, cut_max_s=1.5, gop_max_s=1.0, seed=41, **kw)
+    frames, _ = oracle.decode_full(path)
+    assert info["recon_hash"] == oracle.recon_hash(frames)
+    W, H = kw["width"], kw["height"]
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 4)
+    with scene.VideoScorer(path, keep_frames=True) as v:
+        assert v.general()
+        res = v.score()
+        got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+        assert _first_diff(got, frames) == []
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+        assert v.scene_cuts() == sorted(info["cuts"])

@@ -45,41 +45,8 @@ struct Picture {
   }
 };
 
-// Smooth value-noise texture: two octaves of bilinear random grids + noise.
 void fill_texture(Picture &p, Pcg32 &rng, bool zero_runs) {
-  auto plane = [&](uint8_t *dst, int w, int h, int cell, int lo, int hi, int noise) {
-    const int gw = w / cell + 2, gh = h / cell + 2;
-    std::vector<int> g(size_t(gw) * gh), g2(size_t(gw * 4 + 2) * (gh * 4 + 2));
-    for (auto &x : g) x = lo + static_cast<int>(rng.below(static_cast<uint32_t>(hi - lo)));
-    const int c2 = cell / 4 > 0 ? cell / 4 : 1;
-    const int g2w = w / c2 + 2, g2h = h / c2 + 2;
-    g2.assign(size_t(g2w) * g2h, 0);
-    for (auto &x : g2) x = static_cast<int>(rng.below(41)) - 20;
-    for (int yy = 0; yy < h; ++yy) {
-      const int gy = yy / cell, fy = yy % cell;
-      const int hy = yy / c2, ey = yy % c2;
-      for (int xx = 0; xx < w; ++xx) {
-        const int gx = xx / cell, fx = xx % cell;
-        const int a = g[size_t(gy) * gw + gx], b = g[size_t(gy) * gw + gx + 1];
-        const int c = g[size_t(gy + 1) * gw + gx], d = g[size_t(gy + 1) * gw + gx + 1];
-        const int top = a * (cell - fx) + b * fx, bot = c * (cell - fx) + d * fx;
-        int val = (top * (cell - fy) + bot * fy) / (cell * cell);
-        const int hx = xx / c2, ex = xx % c2;
-        const int a2 = g2[size_t(hy) * g2w + hx], b2 = g2[size_t(hy) * g2w + hx + 1];
-        const int c2v = g2[size_t(hy + 1) * g2w + hx], d2 = g2[size_t(hy + 1) * g2w + hx + 1];
-        const int top2 = a2 * (c2 - ex) + b2 * ex, bot2 = c2v * (c2 - ex) + d2 * ex;
-        val += (top2 * (c2 - ey) + bot2 * ey) / (c2 * c2);
-        if (noise) val += static_cast<int>(rng.below(static_cast<uint32_t>(2 * noise + 1))) - noise;
-        dst[size_t(yy) * w + xx] = clamp_sample(val);
-      }
-    }
-  };
-  plane(p.y.data(), p.w, p.h, 64, 24, 232, 3);
-  if (zero_runs)  // 4 zero samples every 97 px on every 16th row: 00 00 00 00
-    for (int yy = 0; yy < p.h; yy += 16)
-      for (int xx = 0; xx + 4 <= p.w; xx += 97) std::memset(&p.y[size_t(yy) * p.w + xx], 0, 4);
-  plane(p.u.data(), p.w / 2, p.h / 2, 32, 72, 184, 1);
-  plane(p.v.data(), p.w / 2, p.h / 2, 32, 72, 184, 1);
+  synth_texture(p.y.data(), p.u.data(), p.v.data(), p.w, p.h, rng, zero_runs);
 }
 
 struct MbInfo {
@@ -217,6 +184,43 @@ void fill_sparkle(Picture &p, int mbx, int mby, Pcg32 &rng) {
 }
 
 }  // namespace
+
+// Smooth value-noise texture: two octaves of bilinear random grids + noise.
+void synth_texture(uint8_t *py, uint8_t *pu, uint8_t *pv, int pw, int ph, Pcg32 &rng, bool zero_runs) {
+  auto plane = [&](uint8_t *dst, int w, int h, int cell, int lo, int hi, int noise) {
+    const int gw = w / cell + 2, gh = h / cell + 2;
+    std::vector<int> g(size_t(gw) * gh), g2(size_t(gw * 4 + 2) * (gh * 4 + 2));
+    for (auto &x : g) x = lo + static_cast<int>(rng.below(static_cast<uint32_t>(hi - lo)));
+    const int c2 = cell / 4 > 0 ? cell / 4 : 1;
+    const int g2w = w / c2 + 2, g2h = h / c2 + 2;
+    g2.assign(size_t(g2w) * g2h, 0);
+    for (auto &x : g2) x = static_cast<int>(rng.below(41)) - 20;
+    for (int yy = 0; yy < h; ++yy) {
+      const int gy = yy / cell, fy = yy % cell;
+      const int hy = yy / c2, ey = yy % c2;
+      for (int xx = 0; xx < w; ++xx) {
+        const int gx = xx / cell, fx = xx % cell;
+        const int a = g[size_t(gy) * gw + gx], b = g[size_t(gy) * gw + gx + 1];
+        const int c = g[size_t(gy + 1) * gw + gx], d = g[size_t(gy + 1) * gw + gx + 1];
+        const int top = a * (cell - fx) + b * fx, bot = c * (cell - fx) + d * fx;
+        int val = (top * (cell - fy) + bot * fy) / (cell * cell);
+        const int hx = xx / c2, ex = xx % c2;
+        const int a2 = g2[size_t(hy) * g2w + hx], b2 = g2[size_t(hy) * g2w + hx + 1];
+        const int c2v = g2[size_t(hy + 1) * g2w + hx], d2 = g2[size_t(hy + 1) * g2w + hx + 1];
+        const int top2 = a2 * (c2 - ex) + b2 * ex, bot2 = c2v * (c2 - ex) + d2 * ex;
+        val += (top2 * (c2 - ey) + bot2 * ey) / (c2 * c2);
+        if (noise) val += static_cast<int>(rng.below(static_cast<uint32_t>(2 * noise + 1))) - noise;
+        dst[size_t(yy) * w + xx] = clamp_sample(val);
+      }
+    }
+  };
+  plane(py, pw, ph, 64, 24, 232, 3);
+  if (zero_runs)  // 4 zero samples every 97 px on every 16th row: 00 00 00 00
+    for (int yy = 0; yy < ph; yy += 16)
+      for (int xx = 0; xx + 4 <= pw; xx += 97) std::memset(&py[size_t(yy) * pw + xx], 0, 4);
+  plane(pu, pw / 2, ph / 2, 32, 72, 184, 1);
+  plane(pv, pw / 2, ph / 2, 32, 72, 184, 1);
+}
 
 void append_nal(std::vector<uint8_t> &sample, uint8_t header, std::vector<uint8_t> &rbsp) {
   std::vector<uint8_t> nal;

@@ -46,6 +46,11 @@ struct SynthChunk {
   std::string error;          // non-empty: the chunk could not be written
 };
 
+// Smooth value-noise texture (two octaves of bilinear random grids + noise)
+// of a w x h luma plane and its w/2 x h/2 chroma planes; the subset writer's
+// scenes and the full writer's content mode.
+void synth_texture(uint8_t *y, uint8_t *u, uint8_t *v, int w, int h, Pcg32 &rng, bool zero_runs);
+
 // Append one NAL unit (header byte + RBSP with emulation prevention) to an
 // AVCC sample with a 4-byte length prefix.
 void append_nal(std::vector<uint8_t> &sample, uint8_t header, std::vector<uint8_t> &rbsp);

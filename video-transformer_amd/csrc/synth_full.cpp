@@ -44,6 +44,8 @@
 #include "h264_cabac_tables.h"
 #include "h264_tables.h"
 #include "synth.h"
+#include "synth_content.h"
+#include "recon_full.h"
 
 namespace vts {
 namespace {
@@ -194,6 +196,11 @@ class FullWriter {
     cip_ = (P.edge_cases & 16) != 0;
     cabac_ = (P.edge_cases & 1024) != 0;
     t8mode_ = cabac_ && (P.edge_cases & 2048) != 0;
+    content_ = (P.edge_cases & 16384) != 0;
+    // the PPS's chroma QP offsets (make_sps_pps_full)
+    cqp_[0] = static_cast<int>(P.seed % 5) - 2;
+    cqp_[1] = (t8mode_ || (P.edge_cases & 8192)) ? static_cast<int>(P.seed % 3) - 1 : cqp_[0];
+    tex_rng_ = Pcg32(ck->seed ^ 0x9e3779b97f4a7c15ull, 0x7e47);
   }
   void run();
   void run_b();
@@ -216,6 +223,7 @@ class FullWriter {
   // B mode (edge_cases bit 5): display index of each RefPicListX entry, the
   // current picture's display index / POC, and the pictures' motion fields
   bool bmode_ = false;
+  int weighted_ = 0;  // weighted_bipred_idc
   int lst_[2][33] = {};
   int nlst_[2] = {0, 0};
   int cur_d_ = 0, cur_poc_ = 0;
@@ -223,6 +231,7 @@ class FullWriter {
   struct RefPic {
     int d, poc, fn;
     std::vector<GMb> mbs;
+    std::vector<uint8_t> rec;  // content mode: the deblocked reconstruction (NV12)
   };
   std::vector<RefPic> dpb_;
   const RefPic *col_ = nullptr;   // RefPicList1[0]
@@ -512,12 +521,15 @@ class FullWriter {
     }
   }
 
-  void write_residual(int cur, int cbp, bool i16) {
+  // L: the content mode's levels (else random ones)
+  void write_residual(int cur, int cbp, bool i16, const content::Levels *L = nullptr) {
     GMb &m = mb_[static_cast<size_t>(cur)];
     const bool intra = m.type == 1 || m.type == 2;
     int coef[64];
+    auto put = [&](const int *src, int n) { std::memcpy(coef, src, sizeof(int) * static_cast<size_t>(n)); };
     if (i16) {
-      rand_block(coef, 0, 15, 30);
+      if (L) put(L->dc16, 16);
+      else rand_block(coef, 0, 15, 30);
       if (cabac_) {
         if (cab_block(coef, 16, 0, cbf_inc_dc(cur))) m.cbf |= 1u;
       } else {
@@ -527,7 +539,8 @@ class FullWriter {
     for (int k8 = 0; k8 < 4; ++k8) {
       if (!((cbp >> k8) & 1)) continue;
       if (m.t8) {  // CABAC only (the decoders refuse CAVLC 8x8 streams)
-        rand_block8(coef);
+        if (L) put(L->l8[k8], 64);
+        else rand_block8(coef);
         const int tc = cab_block(coef, 64, 5, 0);
         for (int j = 0; j < 4; ++j) {
           const int blk = k8 * 4 + j, r = kBlkY[blk] * 4 + kBlkX[blk];
@@ -539,17 +552,20 @@ class FullWriter {
       for (int k4 = 0; k4 < 4; ++k4) {
         const int blk = k8 * 4 + k4, bx = kBlkX[blk], by = kBlkY[blk], r = by * 4 + bx;
         int tc;
+        if (L) put(L->l4[r], 16);
         if (cabac_) {
-          if (i16) rand_block(coef, 0, 14, 35);
-          else rand_block(coef, 0, 15, 30);
+          if (!L) {
+            if (i16) rand_block(coef, 0, 14, 35);
+            else rand_block(coef, 0, 15, 30);
+          }
           tc = cab_block(coef, i16 ? 15 : 16, i16 ? 1 : 2, cbf_inc_luma(cur, bx, by, intra));
         } else {
           const int n = nc(cur, bx, by, false, 0);
           if (i16) {
-            rand_block(coef, 0, 14, 35);
+            if (!L) rand_block(coef, 0, 14, 35);
             tc = write_block(coef, 0, 14, 15, n);
           } else {
-            rand_block(coef, 0, 15, 30);
+            if (!L) rand_block(coef, 0, 15, 30);
             tc = write_block(coef, 0, 15, 16, n);
           }
         }
@@ -559,7 +575,11 @@ class FullWriter {
     }
     if (cbp >> 4)
       for (int pl = 0; pl < 2; ++pl) {
-        rand_block(coef, 0, 3, 20);
+        if (L) {
+          for (int i = 0; i < 16; ++i) coef[i] = i < 4 ? L->cdc[pl][i] : 0;
+        } else {
+          rand_block(coef, 0, 3, 20);
+        }
         if (cabac_) {
           if (cab_block(coef, 4, 3, cbf_inc_chroma(cur, pl, 0, true, intra))) m.cbf |= 1u << (17 + pl);
         } else {
@@ -570,12 +590,13 @@ class FullWriter {
       for (int pl = 0; pl < 2; ++pl)
         for (int k = 0; k < 4; ++k) {
           int tc;
+          if (L) put(L->cac[pl][k], 15);
           if (cabac_) {
-            rand_block(coef, 0, 14, 40);
+            if (!L) rand_block(coef, 0, 14, 40);
             tc = cab_block(coef, 15, 4, cbf_inc_chroma(cur, pl, k, false, intra));
           } else {
             const int n = nc(cur, k & 1, k >> 1, true, pl);
-            rand_block(coef, 0, 14, 40);
+            if (!L) rand_block(coef, 0, 14, 40);
             tc = write_block(coef, 0, 14, 15, n);
           }
           m.nzc[pl][k] = tc;
@@ -585,7 +606,7 @@ class FullWriter {
 
   void write_qp_delta() {
     int dq = 0;
-    if (rng_.below(5) == 0) dq = static_cast<int>(rng_.below(9)) - 4;
+    if (!content_ && rng_.below(5) == 0) dq = static_cast<int>(rng_.below(9)) - 4;
     if (qp_ + dq < 12 || qp_ + dq > 44) dq = -dq;
     if (cabac_) {  // U binarization of the se() mapping; bin 0's context: the previous macroblock's delta
       const int k = dq > 0 ? 2 * dq - 1 : -2 * dq;
@@ -1066,8 +1087,20 @@ class FullWriter {
     qpd_cur_ = false;
     for (int a = first; a < last; ++a) {
       begin_mb(a, slice);
+      if (content_ && !is_p) {
+        content_intra(a, 0);
+        end_mb(a, last);
+        continue;
+      }
       if (is_p) {
-        const uint32_t r = rng_.below(1000);
+        const bool cskip = content_ && content_p_decide(a);
+        if (cskip) {
+          if (cabac_) put_skip(a, true, false);
+          else ++skip_run;
+          end_mb(a, last);
+          continue;
+        }
+        const uint32_t r = content_ ? 999 : rng_.below(1000);
         if (r < 450) {  // P_Skip
           GMb &m = mb_[static_cast<size_t>(a)];
           m.type = 4;
@@ -1090,7 +1123,8 @@ class FullWriter {
           bw_->ue(skip_run);
           skip_run = 0;
         }
-        if (r < 920) write_inter(a, pan_x, pan_y);
+        if (content_) content_p_write(a);
+        else if (r < 920) write_inter(a, pan_x, pan_y);
         else write_intra(a, true);
       } else {
         write_intra(a, false);
@@ -1308,6 +1342,22 @@ class FullWriter {
     qpd_cur_ = false;
     for (int a = first; a < last; ++a) {
       begin_mb(a, slice);
+      if (content_) {
+        if (content_b_decide(a)) {
+          if (cabac_) put_skip(a, true, true);
+          else ++skip_run;
+        } else {
+          if (cabac_) {
+            put_skip(a, false, true);
+          } else {
+            bw_->ue(skip_run);
+            skip_run = 0;
+          }
+          content_b_write(a);
+        }
+        end_mb(a, last);
+        continue;
+      }
       const uint32_t r = rng_.below(1000);
       if (r < 350) {  // B_Skip
         GMb &m = mb_[static_cast<size_t>(a)];
@@ -1333,6 +1383,707 @@ class FullWriter {
     if (!cabac_ && skip_run) bw_->ue(skip_run);
   }
   void write_intra_b(int a) { write_intra(a, true, 23); }
+
+
+  // ------------------------------------------------------- content mode
+  // (edge_cases bit 14, synth_content.h): decisions by SAD against the source,
+  // predictions from the writer's own reconstruction (closed loop)
+  bool content_ = false;
+  int cqp_[2] = {0, 0};                    // chroma_qp_index_offset, second_chroma_qp_index_offset
+  std::vector<content::Scene> scenes_;
+  std::vector<int> scene_of_, offx_, offy_;  // per display frame of the chunk: scene, background pan offset
+  std::vector<std::pair<int, content::Frame>> srcs_;  // rendered sources by display frame
+  Pcg32 tex_rng_{0x7e47};
+  std::vector<uint8_t> rec_;               // the current picture's reconstruction (NV12, coded size)
+  std::vector<MbRec> mrec_;                // ... its macroblocks in decoder form (deblocking)
+  std::vector<MbRecB> mrec1_;
+  int W() const { return mbw_ * 16; }
+  int H() const { return mbh_ * 16; }
+  int qpc(int pl) const { return h264::kQpc[std::clamp(qp_ + cqp_[pl], 0, 51)]; }
+  const content::Frame &src(int d) {
+    for (auto &e : srcs_)
+      if (e.first == d) return e.second;
+    srcs_.emplace_back(d, content::Frame{});
+    content::Frame &f = srcs_.back().second;
+    f.alloc(W(), H());
+    content::render(scenes_[static_cast<size_t>(scene_of_[static_cast<size_t>(d)])], d, offx_[static_cast<size_t>(d)],
+                    offy_[static_cast<size_t>(d)], &f);
+    return f;
+  }
+  // keep the sources of the current picture and the DPB
+  void prune_sources() {
+    std::vector<std::pair<int, content::Frame>> keep;
+    for (auto &e : srcs_) {
+      bool k = e.first == cur_d_;
+      for (const RefPic &r : dpb_) k |= r.d == e.first;
+      if (k) keep.push_back(std::move(e));
+    }
+    srcs_.swap(keep);
+  }
+  const uint8_t *rec_of(int d) const { return pic_of(d)->rec.data(); }
+  // 8.4.2.2 for whole-pel even motion from a reconstruction (clamped samples)
+  void predict_rec(const uint8_t *R, int mbx, int mby, int mvx, int mvy, content::MbPix *p) const {
+    const int w = W(), h = H(), dx = mvx >> 2, dy = mvy >> 2;
+    const uint8_t *UV = R + static_cast<size_t>(w) * h;
+    for (int y = 0; y < 16; ++y) {
+      const int yy = content::clampi(mby * 16 + y + dy, 0, h - 1);
+      for (int x = 0; x < 16; ++x) p->y[y * 16 + x] = R[size_t(yy) * w + content::clampi(mbx * 16 + x + dx, 0, w - 1)];
+    }
+    for (int y = 0; y < 8; ++y) {
+      const int yy = content::clampi(mby * 8 + y + dy / 2, 0, h / 2 - 1);
+      for (int x = 0; x < 8; ++x) {
+        const size_t o = size_t(yy) * w + 2 * content::clampi(mbx * 8 + x + dx / 2, 0, w / 2 - 1);
+        p->c[0][y * 8 + x] = UV[o];
+        p->c[1][y * 8 + x] = UV[o + 1];
+      }
+    }
+  }
+  // best whole-pel motion (quarter-sample units) of macroblock a from display
+  // frame r: the background's pan, a sprite's motion, or none
+  int best_mv(int a, int r, int *mvx, int *mvy, content::MbPix *pred) {
+    const int mx = a % mbw_, my = a / mbw_;
+    const content::Scene &sc = scenes_[static_cast<size_t>(scene_of_[static_cast<size_t>(cur_d_)])];
+    content::MbPix cur, p;
+    content::source_mb(src(cur_d_), mx, my, &cur);
+    const uint8_t *R = rec_of(r);
+    int cand[8][2], n = 0;
+    cand[n][0] = 4 * (offx_[static_cast<size_t>(cur_d_)] - offx_[static_cast<size_t>(r)]);
+    cand[n][1] = 4 * (offy_[static_cast<size_t>(cur_d_)] - offy_[static_cast<size_t>(r)]);
+    ++n;
+    cand[n][0] = cand[n][1] = 0;
+    ++n;
+    for (int k = 0; k < static_cast<int>(sc.spr.size()) && n < 8; ++k) {
+      int cx, cy, rx, ry;
+      content::sprite_pos(sc, k, cur_d_, &cx, &cy);
+      content::sprite_pos(sc, k, r, &rx, &ry);
+      const content::Sprite &sp = sc.spr[static_cast<size_t>(k)];
+      const int px = content::wrapi(cx, W()), py = content::wrapi(cy, H());
+      if (px > mx * 16 + 15 || px + sp.tex.w <= mx * 16 || py > my * 16 + 15 || py + sp.tex.h <= my * 16) continue;
+      cand[n][0] = 4 * (rx - cx);
+      cand[n][1] = 4 * (ry - cy);
+      ++n;
+    }
+    int best = 1 << 30;
+    for (int i = 0; i < n; ++i) {
+      predict_rec(R, mx, my, cand[i][0], cand[i][1], &p);
+      const int sd = content::sad_all(cur, p);
+      if (sd < best) {
+        best = sd;
+        *mvx = cand[i][0];
+        *mvy = cand[i][1];
+        *pred = p;
+      }
+    }
+    return best;
+  }
+  // 8.4.2.3.1 implicit bi-prediction weights of RefPicList0[r0] / RefPicList1[r1]
+  void implicit_w(int r0, int r1, int *w0, int *w1) const {
+    *w0 = *w1 = 32;
+    const RefPic *p0 = pic_of(lst_[0][r0]), *p1 = pic_of(lst_[1][r1]);
+    if (!p0 || !p1) return;
+    const int tb = std::clamp(cur_poc_ - p0->poc, -128, 127), td = std::clamp(p1->poc - p0->poc, -128, 127);
+    if (td == 0) return;
+    const int tx = (16384 + std::abs(td / 2)) / td;
+    const int dsf = std::clamp((tb * tx + 32) >> 6, -1024, 1023);
+    if ((dsf >> 2) < -64 || (dsf >> 2) > 128) return;
+    *w0 = 64 - (dsf >> 2);
+    *w1 = dsf >> 2;
+  }
+  static int bipred(int p0, int p1, int w0, int w1, bool implicit) {
+    return implicit ? std::clamp((p0 * w0 + p1 * w1 + 32) >> 6, 0, 255) : (p0 + p1 + 1) >> 1;
+  }
+  // prediction of macroblock a from its GMb's per-block references / motion
+  // (skip and direct modes); false when a motion vector is not whole-pel even
+  bool pred_from_mb(int a, content::MbPix *out) {
+    const GMb &m = mb_[static_cast<size_t>(a)];
+    const int mx = a % mbw_, my = a / mbw_;
+    // one prediction per distinct (list, reference, motion): direct
+    // modes mostly give the whole macroblock one
+    content::MbPix pl[2];
+    int have[2][3] = {{-1, 0, 0}, {-1, 0, 0}};
+    for (int b = 0; b < 16; ++b) {
+      const int rr[2] = {m.ref[0][b], m.ref[1][b]};
+      for (int l = 0; l < 2; ++l) {
+        if (rr[l] < 0) continue;
+        if ((m.mv[l][b][0] & 7) || (m.mv[l][b][1] & 7)) return false;
+        if (have[l][0] != rr[l] || have[l][1] != m.mv[l][b][0] || have[l][2] != m.mv[l][b][1]) {
+          predict_rec(rec_of(lst_[l][rr[l]]), mx, my, m.mv[l][b][0], m.mv[l][b][1], &pl[l]);
+          have[l][0] = rr[l];
+          have[l][1] = m.mv[l][b][0];
+          have[l][2] = m.mv[l][b][1];
+        }
+      }
+      if (rr[0] < 0 && rr[1] < 0) return false;
+      const bool bi = rr[0] >= 0 && rr[1] >= 0;
+      int w0 = 32, w1 = 32;
+      if (bi && weighted_ == 2) implicit_w(rr[0], rr[1], &w0, &w1);
+      const int bx = (b & 3) * 4, by = (b >> 2) * 4;
+      const content::MbPix &one = pl[rr[0] >= 0 ? 0 : 1];
+      for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) {
+          const int i = (by + y) * 16 + bx + x;
+          out->y[i] = bi ? bipred(pl[0].y[i], pl[1].y[i], w0, w1, weighted_ == 2) : one.y[i];
+        }
+      for (int c = 0; c < 2; ++c)
+        for (int y = 0; y < 2; ++y)
+          for (int x = 0; x < 2; ++x) {
+            const int i = (by / 2 + y) * 8 + bx / 2 + x;
+            out->c[c][i] = bi ? bipred(pl[0].c[c][i], pl[1].c[c][i], w0, w1, weighted_ == 2) : one.c[c][i];
+          }
+    }
+    return true;
+  }
+
+  // ---- reconstruction (8.5 with Flat_16 scaling; recon_full.h's transforms)
+  static void ls4_flat(int qp, int32_t *ls) {
+    for (int k = 0; k < 16; ++k) ls[k] = full::level_scale(qp % 6, k >> 2, k & 3);
+  }
+  void put_luma_blk(int a, int x0, int y0, int n, const int *pred16, const int *res) {
+    const int w = W(), mx = a % mbw_, my = a / mbw_;
+    for (int y = 0; y < n; ++y)
+      for (int x = 0; x < n; ++x) {
+        const int i = (y0 + y) * 16 + x0 + x;
+        rec_[size_t(my * 16 + y0 + y) * w + mx * 16 + x0 + x] = static_cast<uint8_t>(std::clamp(pred16[i] + res[y * n + x], 0, 255));
+      }
+  }
+  // luma 4x4 block b (raster) of a non-Intra_16x16 macroblock from its scan-order levels
+  void recon_luma4(int a, int b, const int *lev, const int *pred16) {
+    static const uint8_t kZ4[16] = VTS_ZZ_DATA;
+    int cf[16] = {}, res[16], any = 0;
+    int32_t ls[16];
+    for (int s = 0; s < 16; ++s) any |= cf[kZ4[s]] = lev[s];
+    if (!any) {  // no residual
+      std::memset(res, 0, sizeof res);
+      put_luma_blk(a, (b & 3) * 4, (b >> 2) * 4, 4, pred16, res);
+      return;
+    }
+    ls4_flat(qp_, ls);
+    full::scale_idct4(cf, qp_, ls, false, res);
+    put_luma_blk(a, (b & 3) * 4, (b >> 2) * 4, 4, pred16, res);
+  }
+  void recon_luma(int a, const content::MbPix &pred, const content::Levels &L, bool i16, bool t8) {
+    static const uint8_t kZ4[16] = VTS_ZZ_DATA;
+    static const uint8_t kZ8[64] = VTS_ZZ8_DATA;
+    static const uint8_t kN8[6][6] = VTS_NORM8_DATA;
+    if (t8) {
+      int32_t ls8[64];
+      for (int k = 0; k < 64; ++k) ls8[k] = 16 * kN8[qp_ % 6][vts_norm8_class(k >> 3, k & 7)];
+      for (int b8 = 0; b8 < 4; ++b8) {
+        int cf[64] = {}, r8[64];
+        for (int s = 0; s < 64; ++s) cf[kZ8[s]] = L.l8[b8][s];
+        full::scale_idct8(cf, qp_, ls8, r8);
+        put_luma_blk(a, (b8 & 1) * 8, (b8 >> 1) * 8, 8, pred.y, r8);
+      }
+      return;
+    }
+    if (!i16) {
+      for (int b = 0; b < 16; ++b) recon_luma4(a, b, L.l4[b], pred.y);
+      return;
+    }
+    // 8.5.10: Intra16x16 DC, Hadamard + scaling
+    int c[16] = {}, t[16], dcy[16];
+    for (int s = 0; s < 16; ++s) c[kZ4[s]] = L.dc16[s];
+    for (int i = 0; i < 4; ++i) {
+      const int a0 = c[i * 4], a1 = c[i * 4 + 1], a2 = c[i * 4 + 2], a3 = c[i * 4 + 3];
+      t[i * 4] = a0 + a1 + a2 + a3;
+      t[i * 4 + 1] = a0 + a1 - a2 - a3;
+      t[i * 4 + 2] = a0 - a1 - a2 + a3;
+      t[i * 4 + 3] = a0 - a1 + a2 - a3;
+    }
+    const int ls0 = full::level_scale(qp_ % 6, 0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const int a0 = t[j], a1 = t[4 + j], a2 = t[8 + j], a3 = t[12 + j];
+      const int f[4] = {a0 + a1 + a2 + a3, a0 + a1 - a2 - a3, a0 - a1 - a2 + a3, a0 - a1 + a2 - a3};
+      for (int i = 0; i < 4; ++i)
+        dcy[i * 4 + j] = qp_ >= 36 ? (f[i] * ls0) << (qp_ / 6 - 6) : (f[i] * ls0 + (1 << (5 - qp_ / 6))) >> (6 - qp_ / 6);
+    }
+    int32_t ls[16];
+    ls4_flat(qp_, ls);
+    for (int b = 0; b < 16; ++b) {
+      int cf[16] = {}, res[16];
+      for (int s = 1; s < 16; ++s) cf[kZ4[s]] = L.l4[b][s - 1];
+      cf[0] = dcy[b];
+      full::scale_idct4(cf, qp_, ls, true, res);
+      put_luma_blk(a, (b & 3) * 4, (b >> 2) * 4, 4, pred.y, res);
+    }
+  }
+  void recon_chroma(int a, const content::MbPix &pred, const content::Levels &L) {
+    static const uint8_t kZ4[16] = VTS_ZZ_DATA;
+    const int w = W(), mx = a % mbw_, my = a / mbw_;
+    uint8_t *UV = rec_.data() + static_cast<size_t>(w) * H();
+    for (int pl = 0; pl < 2; ++pl) {
+      const int q = qpc(pl);
+      const int c0 = L.cdc[pl][0], c1 = L.cdc[pl][1], c2 = L.cdc[pl][2], c3 = L.cdc[pl][3];
+      const int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+      int32_t ls[16];
+      ls4_flat(q, ls);
+      for (int k = 0; k < 4; ++k) {
+        int cf[16] = {}, r[16], any = 0;
+        for (int s = 1; s < 16; ++s) any |= cf[kZ4[s]] = L.cac[pl][k][s - 1];
+        cf[0] = ((f[k] * ls[0]) << (q / 6)) >> 5;  // 8.5.11.2
+        if (any | cf[0]) full::scale_idct4(cf, q, ls, true, r);
+        else std::memset(r, 0, sizeof r);
+        const int bx = (k & 1) * 4, by = (k >> 1) * 4;
+        for (int y = 0; y < 4; ++y)
+          for (int x = 0; x < 4; ++x)
+            UV[size_t(my * 8 + by + y) * w + 2 * (mx * 8 + bx + x) + pl] =
+                static_cast<uint8_t>(std::clamp(pred.c[pl][(by + y) * 8 + bx + x] + r[y * 4 + x], 0, 255));
+      }
+    }
+  }
+  // the decoder-form record of macroblock a (deblocking's bS inputs)
+  void set_rec(int a, int type, bool t8, const content::Levels *L) {
+    const GMb &m = mb_[static_cast<size_t>(a)];
+    MbRec &r = mrec_[static_cast<size_t>(a)];
+    MbRecB &r1 = mrec1_[static_cast<size_t>(a)];
+    r = MbRec{};
+    r1 = MbRecB{};
+    r.slice = static_cast<uint32_t>(m.slice);
+    r.type = static_cast<uint8_t>(type);
+    r.qp = static_cast<uint8_t>(qp_);
+    r.modes = t8 ? kModeT8 : 0;
+    for (int k = 0; k < 4; ++k) r.ref_slot[k] = r1.ref_slot1[k] = -1;
+    if (L)
+      for (int b = 0; b < 16; ++b) {
+        int n = 0;
+        if (t8) {
+          const int b8 = (b >> 3) * 2 + ((b & 3) >> 1);
+          for (int v : L->l8[b8]) n += v != 0;
+        } else {
+          for (int v : L->l4[b]) n += v != 0;
+        }
+        r.nz[b] = static_cast<uint8_t>(std::min(n, 255));
+      }
+    if (type != kMbInter && type != kMbSkip) return;
+    for (int b = 0; b < 16; ++b) {
+      const int p8 = (b >> 3) * 2 + ((b & 3) >> 1);
+      if (m.ref[0][b] >= 0) {
+        r.ref_slot[p8] = static_cast<int16_t>(m.refd[0][b]);
+        r.mv[b][0] = static_cast<int16_t>(m.mv[0][b][0]);
+        r.mv[b][1] = static_cast<int16_t>(m.mv[0][b][1]);
+      }
+      if (m.ref[1][b] >= 0) {
+        r1.ref_slot1[p8] = static_cast<int16_t>(m.refd[1][b]);
+        r1.mv1[b][0] = static_cast<int16_t>(m.mv[1][b][0]);
+        r1.mv1[b][1] = static_cast<int16_t>(m.mv[1][b][1]);
+      }
+    }
+  }
+  // after the picture's last macroblock: the deblocking filter (8.7), in
+  // macroblock order as a decoder runs it
+  void deblock_picture(int didc, int off_a, int off_b) {
+    std::vector<FullSlice> sl(static_cast<size_t>(mb_.back().slice + 1));
+    for (FullSlice &f : sl) {
+      f = FullSlice{};
+      f.dbk_idc = didc;
+      f.dbk_a = off_a;
+      f.dbk_b = off_b;
+    }
+    full::ReconCtx c{};
+    c.recs = mrec_.data();
+    c.recs1 = bmode_ ? mrec1_.data() : nullptr;
+    c.slices = sl.data();
+    c.surf = rec_.data();
+    c.frame_stride = 0;
+    c.pitch = W();
+    c.uv_off = static_cast<int64_t>(W()) * H();
+    c.mbw = mbw_;
+    c.mbh = mbh_;
+    c.cqp_off = cqp_[0];
+    c.cqp_off2 = cqp_[1];
+    // a macroblock whose edges all have bS 0 (inter, no levels, one motion
+    // equal to its left and top neighbours') is left alone
+    auto plain = [&](int a) {
+      const MbRec &r = mrec_[static_cast<size_t>(a)];
+      const MbRecB &r1 = mrec1_[static_cast<size_t>(a)];
+      if (r.type != kMbInter && r.type != kMbSkip) return false;
+      for (int b = 0; b < 16; ++b)
+        if (r.nz[b] || r.mv[b][0] != r.mv[0][0] || r.mv[b][1] != r.mv[0][1] || r1.mv1[b][0] != r1.mv1[0][0] ||
+            r1.mv1[b][1] != r1.mv1[0][1])
+          return false;
+      for (int k = 1; k < 4; ++k)
+        if (r.ref_slot[k] != r.ref_slot[0] || r1.ref_slot1[k] != r1.ref_slot1[0]) return false;
+      return true;
+    };
+    auto same = [&](int a, int n) {
+      const MbRec &p = mrec_[static_cast<size_t>(a)], &q = mrec_[static_cast<size_t>(n)];
+      const MbRecB &p1 = mrec1_[static_cast<size_t>(a)], &q1 = mrec1_[static_cast<size_t>(n)];
+      return p.ref_slot[0] == q.ref_slot[0] && p1.ref_slot1[0] == q1.ref_slot1[0] && p.mv[0][0] == q.mv[0][0] &&
+             p.mv[0][1] == q.mv[0][1] && p1.mv1[0][0] == q1.mv1[0][0] && p1.mv1[0][1] == q1.mv1[0][1];
+    };
+    std::vector<uint8_t> pl(static_cast<size_t>(nmb_));
+    for (int a = 0; a < nmb_; ++a) pl[static_cast<size_t>(a)] = plain(a);
+    for (int a = 0; a < nmb_; ++a) {
+      const int mx = a % mbw_;
+      if (pl[static_cast<size_t>(a)] && (mx == 0 || (pl[static_cast<size_t>(a - 1)] && same(a, a - 1))) &&
+          (a < mbw_ || (pl[static_cast<size_t>(a - mbw_)] && same(a, a - mbw_))))
+        continue;
+      full::deblock_mb(c, 0, a);
+    }
+  }
+
+  // quantise src - pred for an inter macroblock; t8 chosen by fewer levels
+  int quant_inter(const content::MbPix &cur, const content::MbPix &pred, bool allow_t8, content::Levels *L, bool *t8) {
+    const double dz = 1.0 / 6.0;
+    int cbp = content::quant_luma(cur, pred, qp_, dz, false, false, L);
+    *t8 = false;
+    if (allow_t8 && t8mode_ && (cbp & 15)) {
+      content::Levels L8 = *L;
+      const int cbp8 = content::quant_luma(cur, pred, qp_, dz, false, true, &L8);
+      if (content::nonzero(L8) < content::nonzero(*L)) {
+        *L = L8;
+        cbp = cbp8;
+        *t8 = cbp != 0;
+      }
+    }
+    return cbp | (content::quant_chroma(cur, pred, qpc(0), qpc(1), dz, L) << 4);
+  }
+  // the rest of an inter macroblock after its motion syntax: cbp, transform
+  // size, mb_qp_delta, residual; then its reconstruction
+  void put_inter_residual(int a, int cbp, bool t8, const content::Levels &L, const content::MbPix &pred) {
+    put_cbp(a, cbp, false);
+    if (t8mode_ && (cbp & 15)) put_t8(a, t8);
+    if (cbp) write_qp_delta();
+    write_residual(a, cbp, false, &L);
+    recon_luma(a, pred, L, false, t8);
+    recon_chroma(a, pred, L);
+    set_rec(a, kMbInter, t8, &L);
+  }
+  void put_skipped(int a, const content::MbPix &pred) {
+    content::Levels L{};
+    recon_luma(a, pred, L, false, false);
+    recon_chroma(a, pred, L);
+    set_rec(a, kMbSkip, false, nullptr);
+  }
+  int intra_sad_est(int a) {  // flat-prediction SAD of the source, the inter / intra switch
+    const int mx = a % mbw_, my = a / mbw_;
+    content::MbPix cur;
+    content::source_mb(src(cur_d_), mx, my, &cur);
+    int sum = 0;
+    for (int v : cur.y) sum += v;
+    const int dc = (sum + 128) >> 8;
+    int sd = 0;
+    for (int v : cur.y) sd += std::abs(v - dc);
+    return sd;
+  }
+
+  // content P macroblock; returns true for P_Skip (GMb and reconstruction
+  // done, nothing written)
+  bool content_p_decide(int a) {
+    const int mx = a % mbw_, my = a / mbw_;
+    int px, py;
+    skipmv(a, &px, &py);
+    if ((px & 7) || (py & 7)) return false;
+    content::MbPix cur, ps;
+    content::source_mb(src(cur_d_), mx, my, &cur);
+    predict_rec(rec_of(lst_[0][0]), mx, my, px, py, &ps);
+    content::Levels L;
+    bool t8;
+    if (quant_inter(cur, ps, false, &L, &t8)) return false;
+    GMb &m = mb_[static_cast<size_t>(a)];
+    m.type = 4;
+    for (int i = 0; i < 16; ++i) {
+      m.ref[0][i] = 0;
+      m.mv[0][i][0] = px;
+      m.mv[0][i][1] = py;
+      m.refd[0][i] = lst_[0][0];
+    }
+    put_skipped(a, ps);
+    return true;
+  }
+  void content_p_write(int a) {
+    const int mx = a % mbw_, my = a / mbw_;
+    content::MbPix cur, pred;
+    content::source_mb(src(cur_d_), mx, my, &cur);
+    int tx = 0, ty = 0;
+    const int sd = best_mv(a, lst_[0][0], &tx, &ty, &pred);
+    if (sd > 4096 && 2 * intra_sad_est(a) < sd) {
+      content_intra(a, 5);
+      return;
+    }
+    GMb &m = mb_[static_cast<size_t>(a)];
+    m.type = 0;
+    put_p_type(0);
+    if (nref_ > 1) put_ref(a, 0, 0, 2, 2, 0, 0, nref_);
+    int px, py;
+    mvpred(a, 0, 0, 16, 16, 0, 0, &px, &py);
+    put_mvd(a, 0, 0, 16, 16, 0, tx - px, ty - py);
+    for (int b = 0; b < 16; ++b) {
+      m.ref[0][b] = 0;
+      m.mv[0][b][0] = tx;
+      m.mv[0][b][1] = ty;
+      m.refd[0][b] = lst_[0][0];
+    }
+    content::Levels L;
+    bool t8;
+    const int cbp = quant_inter(cur, pred, true, &L, &t8);
+    put_inter_residual(a, cbp, t8, L, pred);
+  }
+
+  // content B macroblock; returns true for B_Skip (GMb and reconstruction
+  // done, nothing written)
+  bool content_b_decide(int a) {
+    const int mx = a % mbw_, my = a / mbw_;
+    GMb &m = mb_[static_cast<size_t>(a)];
+    m.type = 4;
+    m.d16 = true;
+    m.dmask = 0xf;
+    direct(a, 0xffff);
+    content::MbPix cur, pd;
+    content::source_mb(src(cur_d_), mx, my, &cur);
+    if (pred_from_mb(a, &pd)) {
+      content::Levels L;
+      bool t8;
+      if (!quant_inter(cur, pd, false, &L, &t8)) {
+        put_skipped(a, pd);
+        return true;
+      }
+    }
+    reset_mb(a, m.slice);
+    return false;
+  }
+  void content_b_write(int a) {
+    const int mx = a % mbw_, my = a / mbw_;
+    GMb &m = mb_[static_cast<size_t>(a)];
+    const int slice = m.slice;
+    content::MbPix cur, pd, p0, p1, pb;
+    content::source_mb(src(cur_d_), mx, my, &cur);
+    // direct with residual
+    m.type = 0;
+    m.d16 = true;
+    m.dmask = 0xf;
+    direct(a, 0xffff);
+    const bool dok = pred_from_mb(a, &pd);
+    const int sdd = dok ? content::sad_all(cur, pd) : (1 << 30);
+    reset_mb(a, slice);
+    int mv[2][2] = {{0, 0}, {0, 0}};
+    const int s0 = best_mv(a, lst_[0][0], &mv[0][0], &mv[0][1], &p0);
+    const int s1 = best_mv(a, lst_[1][0], &mv[1][0], &mv[1][1], &p1);
+    int w0 = 32, w1 = 32;
+    if (weighted_ == 2) implicit_w(0, 0, &w0, &w1);
+    for (int i = 0; i < 256; ++i) pb.y[i] = bipred(p0.y[i], p1.y[i], w0, w1, weighted_ == 2);
+    for (int c = 0; c < 2; ++c)
+      for (int i = 0; i < 64; ++i) pb.c[c][i] = bipred(p0.c[c][i], p1.c[c][i], w0, w1, weighted_ == 2);
+    const int sb = content::sad_all(cur, pb);
+    // mb_type 0 direct, 1 L0, 2 L1, 3 Bi (16x16); direct gets a small bias
+    int t = 0, best = sdd - 64;
+    if (s0 < best) { t = 1; best = s0; }
+    if (s1 < best) { t = 2; best = s1; }
+    if (sb < best) { t = 3; best = sb; }
+    if (best > 4096 && 2 * intra_sad_est(a) < best) {
+      content_intra(a, 23);
+      return;
+    }
+    const content::MbPix &pred = t == 0 ? pd : (t == 1 ? p0 : (t == 2 ? p1 : pb));
+    put_b_type(a, t);
+    m.type = 0;
+    if (t == 0) {
+      m.d16 = true;
+      m.dmask = 0xf;
+      direct(a, 0xffff);
+    } else {
+      const bool use[2] = {t == 1 || t == 3, t == 2 || t == 3};
+      for (int l = 0; l < 2; ++l)
+        if (use[l] && nlst_[l] >= 2) put_ref(a, 0, 0, 2, 2, l, 0, nlst_[l]);
+      int mvd[2][2] = {{0, 0}, {0, 0}};
+      for (int l = 0; l < 2; ++l) {
+        if (!use[l]) continue;
+        int px, py;
+        mvpred(a, 0, 0, 16, 16, 0, 0, &px, &py, l);
+        mvd[l][0] = mv[l][0] - px;
+        mvd[l][1] = mv[l][1] - py;
+      }
+      for (int l = 0; l < 2; ++l)
+        for (int b = 0; b < 16; ++b) set_b(m, l, b, use[l] ? 0 : -1, mv[l][0], mv[l][1]);
+      for (int l = 0; l < 2; ++l)
+        if (use[l]) put_mvd(a, 0, 0, 16, 16, l, mvd[l][0], mvd[l][1]);
+    }
+    content::Levels L;
+    bool t8;
+    const int cbp = quant_inter(cur, pred, true, &L, &t8);
+    put_inter_residual(a, cbp, t8, L, pred);
+  }
+
+  // content intra macroblock (base: mb_type offset 0 I, 5 P, 23 B):
+  // Intra_16x16 (V / H / DC / plane) or Intra_4x4 (V / H / DC), predicted
+  // from the reconstruction's neighbouring samples, chosen by SAD
+  void content_intra(int a, int base) {
+    static const uint8_t kZ4[16] = VTS_ZZ_DATA;
+    GMb &m = mb_[static_cast<size_t>(a)];
+    const int mx = a % mbw_, my = a / mbw_, w = W();
+    uint8_t *UV = rec_.data() + static_cast<size_t>(w) * H();
+    content::MbPix cur;
+    content::source_mb(src(cur_d_), mx, my, &cur);
+    const Loc A = loc(a, -1, 0, 16), B = loc(a, 0, -1, 16), D = loc(a, -1, -1, 16);
+    const bool la = intra_ok(A.mb), ta = intra_ok(B.mb), ca = intra_ok(D.mb);
+    auto ys = [&](int x, int y) { return static_cast<int>(rec_[size_t(y) * w + x]); };
+    const int x0 = mx * 16, y0 = my * 16;
+    m.type = 1;  // intra for the availability of the macroblock's own blocks
+    // ---- Intra_16x16 (8.3.3), from the samples around the macroblock
+    content::MbPix p16[4];
+    const bool ok16[4] = {ta, la, true, la && ta && ca};
+    int st = 0, sl = 0;
+    for (int i = 0; i < 16; ++i) {
+      if (ta) st += ys(x0 + i, y0 - 1);
+      if (la) sl += ys(x0 - 1, y0 + i);
+    }
+    const int dc = (ta && la) ? (st + sl + 16) >> 5 : (ta ? (st + 8) >> 4 : (la ? (sl + 8) >> 4 : 128));
+    int hp = 0, vp = 0, pa = 0;
+    if (ok16[3]) {
+      for (int k = 0; k < 8; ++k) {
+        hp += (k + 1) * (ys(x0 + 8 + k, y0 - 1) - ys(x0 + 6 - k, y0 - 1));
+        vp += (k + 1) * (ys(x0 - 1, y0 + 8 + k) - ys(x0 - 1, y0 + 6 - k));
+      }
+      pa = 16 * (ys(x0 - 1, y0 + 15) + ys(x0 + 15, y0 - 1));
+    }
+    const int pb = (5 * hp + 32) >> 6, pc = (5 * vp + 32) >> 6;
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) {
+        const int i = y * 16 + x;
+        p16[0].y[i] = ta ? ys(x0 + x, y0 - 1) : 0;
+        p16[1].y[i] = la ? ys(x0 - 1, y0 + y) : 0;
+        p16[2].y[i] = dc;
+        p16[3].y[i] = std::clamp((pa + pb * (x - 7) + pc * (y - 7) + 16) >> 5, 0, 255);
+      }
+    int pm = 2, s16 = 1 << 30;
+    for (int k = 0; k < 4; ++k) {
+      if (!ok16[k]) continue;
+      const int sd = content::sad_luma(cur, p16[k]);
+      if (sd < s16) {
+        s16 = sd;
+        pm = k;
+      }
+    }
+    // ---- Intra_4x4 (8.3.1.2 modes 0 / 1 / 2), blocks in decoding order, each
+    // reconstructed before the next predicts from it (into rec_: Intra_16x16
+    // reads only samples outside the macroblock)
+    content::Levels L{};
+    content::MbPix p4;
+    int mode4[16], s4 = 0;
+    for (int k = 0; k < 16; ++k) {
+      const int bx = kBlkX[k], by = kBlkY[k], r = by * 4 + bx;
+      const bool t = intra_ok(loc(a, bx * 4, by * 4 - 1, 16).mb), l = intra_ok(loc(a, bx * 4 - 1, by * 4, 16).mb);
+      const int X = x0 + bx * 4, Y = y0 + by * 4;
+      int cand[3][16], sums[2] = {0, 0};
+      for (int i = 0; i < 4; ++i) {
+        if (t) sums[0] += ys(X + i, Y - 1);
+        if (l) sums[1] += ys(X - 1, Y + i);
+      }
+      const int d4 = (t && l) ? (sums[0] + sums[1] + 4) >> 3 : (t ? (sums[0] + 2) >> 2 : (l ? (sums[1] + 2) >> 2 : 128));
+      for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) {
+          cand[0][y * 4 + x] = t ? ys(X + x, Y - 1) : 0;
+          cand[1][y * 4 + x] = l ? ys(X - 1, Y + y) : 0;
+          cand[2][y * 4 + x] = d4;
+        }
+      int bm = 2, bs = 1 << 30;
+      for (int md = 0; md < 3; ++md) {
+        if ((md == 0 && !t) || (md == 1 && !l)) continue;
+        int sd = 0;
+        for (int y = 0; y < 4; ++y)
+          for (int x = 0; x < 4; ++x) sd += std::abs(cur.y[(by * 4 + y) * 16 + bx * 4 + x] - cand[md][y * 4 + x]);
+        if (sd < bs) {
+          bs = sd;
+          bm = md;
+        }
+      }
+      mode4[k] = bm;
+      s4 += bs;
+      int xres[16], lv[16];
+      for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) {
+          p4.y[(by * 4 + y) * 16 + bx * 4 + x] = cand[bm][y * 4 + x];
+          xres[y * 4 + x] = cur.y[(by * 4 + y) * 16 + bx * 4 + x] - cand[bm][y * 4 + x];
+        }
+      content::quant4(xres, qp_, 1.0 / 3.0, lv);
+      for (int s = 0; s < 16; ++s) L.l4[r][s] = lv[kZ4[s]];
+      recon_luma4(a, r, L.l4[r], p4.y);
+    }
+    const bool use4 = s4 + 256 < s16;
+    // ---- chroma (8.3.4): DC / horizontal / vertical
+    auto cs = [&](int pl, int x, int y) { return static_cast<int>(UV[size_t(y) * w + 2 * x + pl]); };
+    const int cx0 = mx * 8, cy0 = my * 8;
+    content::MbPix pcm[3];
+    for (int pl = 0; pl < 2; ++pl)
+      for (int k = 0; k < 4; ++k) {
+        const int xo = (k & 1) * 4, yo = (k >> 1) * 4;
+        int stc = 0, slc = 0;
+        for (int i = 0; i < 4; ++i) {
+          if (ta) stc += cs(pl, cx0 + xo + i, cy0 - 1);
+          if (la) slc += cs(pl, cx0 - 1, cy0 + yo + i);
+        }
+        int v;
+        if ((xo == 0 && yo == 0) || (xo && yo)) {
+          v = (ta && la) ? (stc + slc + 4) >> 3 : (la ? (slc + 2) >> 2 : (ta ? (stc + 2) >> 2 : 128));
+        } else if (xo) {
+          v = ta ? (stc + 2) >> 2 : (la ? (slc + 2) >> 2 : 128);
+        } else {
+          v = la ? (slc + 2) >> 2 : (ta ? (stc + 2) >> 2 : 128);
+        }
+        for (int y = 0; y < 4; ++y)
+          for (int x = 0; x < 4; ++x) {
+            const int i = (yo + y) * 8 + xo + x;
+            pcm[0].c[pl][i] = v;
+            pcm[1].c[pl][i] = la ? cs(pl, cx0 - 1, cy0 + yo + y) : 0;
+            pcm[2].c[pl][i] = ta ? cs(pl, cx0 + xo + x, cy0 - 1) : 0;
+          }
+      }
+    int cm = 0, scm = 1 << 30;
+    for (int k = 0; k < 3; ++k) {
+      if ((k == 1 && !la) || (k == 2 && !ta)) continue;
+      int sd = 0;
+      for (int pl = 0; pl < 2; ++pl)
+        for (int i = 0; i < 64; ++i) sd += std::abs(cur.c[pl][i] - pcm[k].c[pl][i]);
+      if (sd < scm) {
+        scm = sd;
+        cm = k;
+      }
+    }
+    content::MbPix pred = use4 ? p4 : p16[pm];
+    std::memcpy(pred.c, pcm[cm].c, sizeof pred.c);
+    const int cc = content::quant_chroma(cur, pred, qpc(0), qpc(1), 1.0 / 3.0, &L);
+    if (use4) {
+      int cbp = cc << 4;
+      for (int b = 0; b < 16; ++b)
+        for (int v : L.l4[b])
+          if (v) cbp |= 1 << ((b >> 3) * 2 + ((b & 3) >> 1));
+      put_i_type(a, 0, base);
+      if (t8mode_) put_t8(a, false);
+      for (int k = 0; k < 16; ++k) {
+        const int bx = kBlkX[k], by = kBlkY[k];
+        const Loc LA = loc(a, bx * 4 - 1, by * 4, 16), LB = loc(a, bx * 4, by * 4 - 1, 16);
+        int pred_m = 2;
+        if (!(LA.mb < 0 || LB.mb < 0 || (cip_ && !intra(LA.mb)) || (cip_ && !intra(LB.mb)))) {
+          const GMb &ma = mb_[static_cast<size_t>(LA.mb)], &mb = mb_[static_cast<size_t>(LB.mb)];
+          const int pa4 = ma.type == 1 ? ma.i4[(LA.yw / 4) * 4 + LA.xw / 4] : 2;
+          const int pb4 = mb.type == 1 ? mb.i4[(LB.yw / 4) * 4 + LB.xw / 4] : 2;
+          pred_m = imin(pa4, pb4);
+        }
+        const int md = mode4[k];
+        put_pred_mode(md == pred_m, md < pred_m ? md : md - 1);
+        m.i4[by * 4 + bx] = md;
+      }
+      put_chroma_mode(a, cm);
+      put_cbp(a, cbp, true);
+      if (cbp) write_qp_delta();
+      write_residual(a, cbp, false, &L);
+      recon_chroma(a, pred, L);
+      set_rec(a, kMbI4x4, false, &L);
+      return;
+    }
+    m.type = 2;
+    for (int i = 0; i < 16; ++i) m.i4[i] = 2;
+    const int lum = content::quant_luma(cur, pred, qp_, 1.0 / 3.0, true, false, &L);
+    const int cbp = lum | (cc << 4);
+    m.cbp = cbp;
+    put_i_type(a, 1 + pm + 4 * cc + (lum ? 12 : 0), base);
+    put_chroma_mode(a, cm);
+    write_qp_delta();
+    write_residual(a, cbp, true, &L);
+    recon_luma(a, pred, L, true, false);
+    recon_chroma(a, pred, L);
+    set_rec(a, kMbI16, false, &L);
+  }
 
   // 8.2.4.2.3 list initialisation (no modification) from the writer's DPB
   void b_lists() {
@@ -1483,6 +2234,12 @@ void FullWriter::run_b() {
   const int64_t nf = ck_->nf;
   std::vector<uint8_t> cut(static_cast<size_t>(nf), 0);
   std::vector<int> pxs(static_cast<size_t>(nf)), pys(static_cast<size_t>(nf));
+  weighted_ = (ec & 64) ? 1 : ((ec & 128) ? 2 : 0);
+  if (content_) {
+    scene_of_.assign(static_cast<size_t>(nf), 0);
+    offx_.assign(static_cast<size_t>(nf), 0);
+    offy_.assign(static_cast<size_t>(nf), 0);
+  }
   {
     int64_t next_cut = scene_len();
     int pan_x = 0, pan_y = 0;
@@ -1492,13 +2249,31 @@ void FullWriter::run_b() {
       cut[static_cast<size_t>(f)] = c;
       if (c && ck_->f0 + f > 0) ck_->cuts.push_back(ck_->f0 + f);
       if (f % P_.fps_num == 0 || c) {
-        const int m = 4 * P_.max_motion;
-        pan_x = static_cast<int>(rng_.below(static_cast<uint32_t>(2 * m + 1))) - m;
-        pan_y = static_cast<int>(rng_.below(static_cast<uint32_t>(2 * m + 1))) - m;
+        if (content_) {  // whole-pel even pans (luma samples per frame x 4)
+          const int h = P_.max_motion / 2;
+          pan_x = 8 * (static_cast<int>(rng_.below(static_cast<uint32_t>(2 * h + 1))) - h);
+          pan_y = 8 * (static_cast<int>(rng_.below(static_cast<uint32_t>(2 * h + 1))) - h);
+        } else {
+          const int m = 4 * P_.max_motion;
+          pan_x = static_cast<int>(rng_.below(static_cast<uint32_t>(2 * m + 1))) - m;
+          pan_y = static_cast<int>(rng_.below(static_cast<uint32_t>(2 * m + 1))) - m;
+        }
         if (rng_.below(4) == 0) pan_x = pan_y = 0;
       }
       pxs[static_cast<size_t>(f)] = pan_x;
       pys[static_cast<size_t>(f)] = pan_y;
+      if (content_) {
+        const size_t u = static_cast<size_t>(f);
+        if (c) {
+          scenes_.emplace_back();
+          content::make_scene(&scenes_.back(), f, mbw_ * 16, mbh_ * 16, P_.max_motion, tex_rng_);
+          offx_[u] = offy_[u] = 0;
+        } else {
+          offx_[u] = offx_[u - 1] + pan_x / 4;
+          offy_[u] = offy_[u - 1] + pan_y / 4;
+        }
+        scene_of_[u] = static_cast<int>(scenes_.size()) - 1;
+      }
     }
   }
   struct Pic {
@@ -1568,7 +2343,7 @@ void FullWriter::run_b() {
     }
     col_ = is_b ? pic_of(lst_[1][0]) : nullptr;
     spatial_ = true;
-    if (is_b && (ec & 256) && rng_.below(2)) {
+    if (is_b && (ec & 256) && !content_ && rng_.below(2)) {
       // temporal direct only when every colocated reference is in RefPicList0
       bool ok = true;
       for (const GMb &cm : col_->mbs)
@@ -1582,10 +2357,16 @@ void FullWriter::run_b() {
       spatial_ = !ok;
     }
     const int slice_type = idr ? (rng_.below(2) ? 7 : 2) : (is_b ? (rng_.below(2) ? 6 : 1) : (rng_.below(2) ? 5 : 0));
-    const int pic_qp = 20 + static_cast<int>(rng_.below(17));
+    // content: x264-like QP offsets between I, P, reference B and B pictures
+    const int pic_qp = content_ ? (idr ? 24 : (is_b ? (pc.ref ? 27 : 28) : 26)) : 20 + static_cast<int>(rng_.below(17));
     const bool wp = !idr && (ec & 64) != 0;   // explicit weights (weighted_pred_flag / weighted_bipred_idc 1)
     sample.clear();
     int slice = 0;
+    if (content_) {
+      rec_.assign(static_cast<size_t>(W()) * H() * 3 / 2, 0);
+      mrec_.assign(static_cast<size_t>(nmb_), MbRec{});
+      mrec1_.assign(static_cast<size_t>(nmb_), MbRecB{});
+    }
     for (int first = 0; first < nmb_; ++slice) {
       const int row_end = spr > 0 ? ((first / mbw_) + 1) * mbw_ : nmb_;
       const int last = std::min(first + slice_mbs, row_end);
@@ -1637,12 +2418,12 @@ void FullWriter::run_b() {
       if (cabac_ && !idr) bw.ue(0);  // cabac_init_idc
       qp_ = pic_qp;
       bw.se(pic_qp - 26);
-      const uint32_t dr = rng_.below(20);
+      const uint32_t dr = content_ ? 0u : rng_.below(20);
       const int didc = dr < 16 ? 0 : (dr < 18 ? 2 : 1);
       bw.ue(static_cast<uint32_t>(didc));
       if (didc != 1) {
-        bw.se(static_cast<int>(rng_.below(7)) - 3);
-        bw.se(static_cast<int>(rng_.below(7)) - 3);
+        bw.se(content_ ? 0 : static_cast<int>(rng_.below(7)) - 3);
+        bw.se(content_ ? 0 : static_cast<int>(rng_.below(7)) - 3);
       }
       if (cabac_) {
         while (!bw.aligned()) bw.bit(1);
@@ -1657,6 +2438,19 @@ void FullWriter::run_b() {
       first = last;
     }
     bw_ = nullptr;
+    if (content_) {
+      deblock_picture(0, 0, 0);  // every content slice: idc 0, offsets 0
+      if (P_.hash_frames) {      // display-size NV12 of the reconstruction (= a decoder's output)
+        uint64_t h = 0, j = 0;
+        const int w = W();
+        for (int yy = 0; yy < P_.height; ++yy)
+          for (int xx = 0; xx < P_.width; ++xx, ++j) h += uint64_t(rec_[size_t(yy) * w + xx]) * ((j % 65521) + 1);
+        const uint8_t *UV = rec_.data() + static_cast<size_t>(w) * H();
+        for (int yy = 0; yy < P_.height / 2; ++yy)
+          for (int xx = 0; xx < P_.width; ++xx, ++j) h += uint64_t(UV[size_t(yy) * w + xx]) * ((j % 65521) + 1);
+        ck_->recon_hash += h * uint64_t(ck_->f0 + cur_d_ + 1);
+      }
+    }
     if (idr) {
       idr_id ^= 1;
       ++ck_->n_idr;
@@ -1669,9 +2463,10 @@ void FullWriter::run_b() {
           if (wrap(dpb_[i]) < wrap(dpb_[o])) o = i;
         dpb_.erase(dpb_.begin() + static_cast<int64_t>(o));
       }
-      dpb_.push_back(RefPic{cur_d_, cur_poc_, frame_num, mb_});
+      dpb_.push_back(RefPic{cur_d_, cur_poc_, frame_num, mb_, content_ ? rec_ : std::vector<uint8_t>{}});
       prev_ref_fn = frame_num;
     }
+    if (content_) prune_sources();
     ck_->data.insert(ck_->data.end(), sample.begin(), sample.end());
     ck_->size.push_back(static_cast<uint32_t>(sample.size()));
     ck_->sync.push_back(idr ? 1 : 0);
@@ -1696,6 +2491,11 @@ void FullWriter::run_b() {
 }  // namespace
 
 void encode_chunk_full(const vts_synth_params &P, SynthChunk *ck) {
+  if ((P.edge_cases & 16384) && (!(P.edge_cases & 32) || (P.edge_cases & (64 | 256 | 16)))) {
+    ck->error = "content mode (edge_cases bit 14) needs B mode (bit 5) without explicit weights, temporal direct "
+                "or constrained intra";
+    return;
+  }
   FullWriter w(P, ck);
   if (P.edge_cases & 32) w.run_b();
   else w.run();

@@ -290,7 +290,8 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
                 constrained_intra: bool = False, bframes: bool = False,
                 weighted: str | None = None, temporal_direct: bool = False,
                 chroma_deblock: bool = False, cabac: bool = False,
-                transform_8x8: bool = False, scaling: str | None = None) -> dict:
+                transform_8x8: bool = False, scaling: str | None = None,
+                content: bool = False) -> dict:
     """Write a synthetic H.264/MP4 clip (see vts_synth_write); returns its facts
     and the ground-truth scene-cut frames.  coding="full" only: ``bframes`` codes
     B pictures (Main profile, POC type 0, composition offsets in the MP4),
@@ -304,7 +305,12 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
     coder) and ``transform_8x8`` (with cabac, High profile) adds Intra_8x8 and
     8x8-transform inter macroblocks.  coding="full" only: ``scaling`` =
     "sps", "pps" or "both" writes seeded scaling matrices (High profile; lists
-    absent, default, ending early or full, exercising fall-back rules A / B)."""
+    absent, default, ending early or full, exercising fall-back rules A / B).
+    coding="full" with ``bframes`` only: ``content`` codes pictures instead of
+    random syntax (textured scenes cut at the planted frames, a panning
+    background and moving sprites; skip / direct / 16x16 motion / intra
+    decisions by SAD, residuals quantised from the source's prediction error;
+    synth_content.h)."""
     p = _lib.SynthParams()
     p.width, p.height, p.fps_num, p.fps_den = width, height, fps, 1
     p.n_frames, p.seed = n_frames, seed
@@ -336,6 +342,10 @@ def synth_write(path: str | Path, *, width: int = 1280, height: int = 720,
             raise ValueError("B pictures / weighted prediction need coding='full'")
         p.edge_cases |= 32 | {None: 0, "explicit": 64, "implicit": 128}[weighted] | \
             (256 if temporal_direct else 0)
+    if content:
+        if coding != "full" or not bframes:
+            raise ValueError("content mode needs coding='full' and bframes")
+        p.edge_cases |= 16384
     info = _lib.SynthInfo()
     cuts = (C.c_int64 * max(n_frames, 1))()
     _lib.check(_lib.lib().vts_synth_write(str(path).encode(), C.byref(p), C.byref(info),
