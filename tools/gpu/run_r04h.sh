@@ -1,0 +1,27 @@
+# Round 4: unified luma / chroma deblocking filter (parity + same-box A/B
+# against the previous build and the 512-thread variant), content-mode
+# streams on the GPU (parity against the oracle and the writer, cuts), the
+# 10-min 720p content stream's rate and stage times, deblock sections.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${TAG:-r04h}
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_full_gpu.py tests/test_transcode_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 600 python tools/gpu/content_probe.py /tmp/gcontent.mp4 3 > $O/content.json 2> $O/content.err || { tail -20 $O/content.err; exit 1; }
+cat $O/content.json
+timeout -k 10 300 python - <<'PY' || exit 1
+import sys; sys.path.insert(0, "video-transformer_amd")
+from vtseg import scene
+scene.synth_write("/tmp/gcab.mp4", width=1280, height=720, fps=30, n_frames=18000, seed=0x5EED,
+                  coding="full", slices_per_row=0, max_motion=4, bframes=True, weighted="implicit", cabac=True,
+                  transform_8x8=True)
+print("noise stream written")
+PY
+PASSES=2 bash tools/gpu/lib_ab.sh /tmp/gcab.mp4 3 $O/ab_noise cur prev dbk512 || exit 1
+PASSES=1 bash tools/gpu/lib_ab.sh /tmp/gcontent.mp4 3 $O/ab_content cur prev || exit 1
+cp video-transformer_amd/vtseg/libvtseg.so /tmp/lib_cur.so
+cp tools/exp/lib_rprof.so video-transformer_amd/vtseg/libvtseg.so
+timeout -k 10 300 python tools/gpu/recon_prof.py /tmp/gcab.mp4 > $O/rprof.json 2> $O/rprof.err || { tail -20 $O/rprof.err; cp /tmp/lib_cur.so video-transformer_amd/vtseg/libvtseg.so; exit 1; }
+cat $O/rprof.json
+cp /tmp/lib_cur.so video-transformer_amd/vtseg/libvtseg.so

@@ -1782,6 +1782,57 @@ __device__ __forceinline__ uint32_t u4_at(const uint4 &v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
+// Luma and chroma edges in one instruction stream (8.7.2.3 / 8.7.2.4): s =
+// p3 p2 p1 p0 q0 q1 q2 q3.  A chroma lane holds p1 p0 q0 q1 at s[2..5]; with
+// ap / aq < beta forced false it takes exactly the chroma filter (tC = tC0 +
+// 1, only p0 / q0 change, bS 4: p0' = (2 p1 + p0 + q1 + 2) >> 2), so a wave
+// whose lanes mix luma and chroma runs one filter, not both
+__device__ __forceinline__ void filt_w(int (&s)[8], int bS, uint32_t w, bool chroma) {
+  const int alpha = w & 255, beta = (w >> 8) & 255;
+  const int p0 = s[3], p1 = s[2], q0 = s[4], q1 = s[5];
+  if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
+  const int p2 = s[1], q2 = s[6];
+  const bool apb = !chroma && abs(p2 - p0) < beta, aqb = !chroma && abs(q2 - q0) < beta;
+  if (bS < 4) {
+    const int tc0 = (w >> (11 + 5 * bS)) & 31;
+    const int tc = tc0 + (chroma ? 1 : static_cast<int>(apb) + static_cast<int>(aqb));
+    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
+    s[3] = c255(p0 + delta);
+    s[4] = c255(q0 - delta);
+    if (apb) s[2] = p1 + min(max((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0), tc0);
+    if (aqb) s[5] = q1 + min(max((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0), tc0);
+    return;
+  }
+  const int p3 = s[0], q3 = s[7];
+  const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
+  if (apb && small) {
+    s[3] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+    s[2] = (p2 + p1 + p0 + q0 + 2) >> 2;
+    s[1] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+  } else {
+    s[3] = (2 * p1 + p0 + q1 + 2) >> 2;
+  }
+  if (aqb && small) {
+    s[4] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+    s[5] = (p0 + q0 + q1 + q2 + 2) >> 2;
+    s[6] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+  } else {
+    s[4] = (2 * q1 + q0 + p1 + 2) >> 2;
+  }
+}
+// vertical pass: a chroma lane's interleaved row (Cb Cr pairs from x = -2)
+// reordered so that slot s = (edge 2 (s >> 1), plane s & 1) has p1 p0 q0 q1
+// at u[4 s + 2 .. 4 s + 5]: u[j] = r[kDbkCPerm[j]], r[i] = u[kDbkCInv[i]]
+__device__ __constant__ static const uint8_t kDbkCPerm[20] = {18, 19, 0, 2, 4, 6, 1, 3, 5, 7,
+                                                             8, 10, 12, 14, 9, 11, 13, 15, 16, 17};
+__device__ __constant__ static const uint8_t kDbkCInv[20] = {2, 6, 3, 7, 4, 8, 5, 9, 10, 14,
+                                                            11, 15, 12, 16, 13, 17, 18, 19, 0, 1};
+// horizontal pass: chroma row of u index j (p1 p0 q0 q1 of chroma edges 0 / 4
+// at u[2..5] / u[10..13], rows 6, 7 at u[14], u[15]); -1: none
+constexpr int dbk_hrow(int j) {
+  return (j >= 2 && j <= 5) ? j - 2 : ((j >= 10 && j <= 13) ? j - 6 : (j == 14 ? 8 : (j == 15 ? 9 : -1)));
+}
+
 // grid: pictures of the level
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a) {
   __shared__ DbkTile tiles[kDbkWaves * 2];
@@ -1862,35 +1913,25 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
       if (act && lrow) {
         const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
-        int r[20];
+        int r[20], u[20];
 #pragma unroll
         for (int i = 0; i < 20; ++i) r[i] = (wv[i >> 2] >> ((i & 3) * 8)) & 255;
-        if (luma) {
-          const int seg = row >> 2;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int bS = (u4_at(bsw, e >> 1) >> (((e & 1) * 4 + seg) * 4)) & 15;
-            if (!bS) continue;
-            int s8[8];
+        for (int j = 0; j < 20; ++j) u[j] = luma ? r[j] : r[kDbkCPerm[j]];
+        const int seg = luma ? row >> 2 : row >> 1;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) s8[i] = r[4 * e + i];
-            filt_luma_w(s8, bS, u4_at(pv, e));
+        for (int e = 0; e < 4; ++e) {
+          const int bS = (u4_at(bsw, e >> 1) >> (((luma ? (e & 1) : 0) * 4 + seg) * 4)) & 15;
+          if (!bS) continue;
+          int s8[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) r[4 * e + i] = s8[i];
-          }
-        } else {
-          const int seg = row >> 1;
+          for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
+          filt_w(s8, bS, u4_at(pv, e), !luma);
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int bS = (u4_at(bsw, e >> 1) >> seg * 4) & 15;
-            if (!bS) continue;
-#pragma unroll
-            for (int pl = 0; pl < 2; ++pl) {
-              const int c0 = 4 + 2 * (2 * e) + pl;  // q0 of chroma col 2e (luma edge e)
-              filt_chroma_w(r[c0 - 4], r[c0 - 2], r[c0], r[c0 + 2], bS, u4_at(pv, e + pl));
-            }
-          }
+          for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
         }
+#pragma unroll
+        for (int i = 0; i < 20; ++i) r[i] = luma ? u[i] : u[kDbkCInv[i]];
         uint8_t *dst = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
 #pragma unroll
         for (int i = 0; i < 5; ++i)
@@ -1898,40 +1939,37 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       }
       lane_sync();
       RPROF(1);
-      // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved chroma column l - 16
+      // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved
+      // chroma column l - 16 (one plane; its edges at slots 0 and 2)
       if (act) {
-        if (l < 16) {
-          const int col = l, seg = col >> 2;
-          int r[20];
+        const int j = l - 16, pl = j & 1;
+        const int seg = luma ? l >> 2 : j >> 2;
+        uint8_t *const ycol = &t.y[0][4 + l];
+        uint8_t *const ccol = &t.c[0][4 + (j & 15)];
+        int u[20];
 #pragma unroll
-          for (int i = 0; i < 20; ++i) r[i] = t.y[i][4 + col];
+        for (int i = 0; i < 20; ++i) {  // one LDS read per sample: the lane's own column
+          const int cr = dbk_hrow(i);
+          const uint8_t *q = luma ? ycol + i * 20 : ccol + (cr >= 0 ? cr : 0) * 20;
+          u[i] = (luma || cr >= 0) ? *q : 0;
+        }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int bS = (u4_at(bsw, 2 + (e >> 1)) >> (((e & 1) * 4 + seg) * 4)) & 15;
-            if (!bS) continue;
-            int s8[8];
+        for (int e = 0; e < 4; ++e) {
+          int bS = (u4_at(bsw, 2 + (e >> 1)) >> (((luma ? (e & 1) : 0) * 4 + seg) * 4)) & 15;
+          if (!luma && (e & 1)) bS = 0;
+          if (!bS) continue;
+          int s8[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) s8[i] = r[4 * e + i];
-            filt_luma_w(s8, bS, u4_at(ph, e));
+          for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
+          filt_w(s8, bS, u4_at(ph, luma ? e : e + pl), !luma);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) r[4 * e + i] = s8[i];
-          }
+          for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
+        }
 #pragma unroll
-          for (int i = 1; i < 20; ++i) t.y[i][4 + col] = static_cast<uint8_t>(r[i]);
-        } else {
-          const int j = l - 16, pl = j & 1, cc = j >> 1, seg = cc >> 1;
-          int r[10];
-#pragma unroll
-          for (int i = 0; i < 10; ++i) r[i] = t.c[i][4 + j];
-#pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int bS = (u4_at(bsw, 2 + (e >> 1)) >> seg * 4) & 15;
-            if (!bS) continue;
-            const int q0 = 2 + 2 * e;  // chroma row 2e
-            filt_chroma_w(r[q0 - 2], r[q0 - 1], r[q0], r[q0 + 1], bS, u4_at(ph, e + pl));
-          }
-#pragma unroll
-          for (int i = 1; i < 10; ++i) t.c[i][4 + j] = static_cast<uint8_t>(r[i]);
+        for (int i = 1; i < 20; ++i) {
+          const int cr = dbk_hrow(i);
+          uint8_t *q = luma ? ycol + i * 20 : ccol + (cr >= 1 ? cr : 0) * 20;
+          if (luma || cr >= 1) *q = static_cast<uint8_t>(u[i]);
         }
       }
       lane_sync();
