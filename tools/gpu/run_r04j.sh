@@ -1,0 +1,17 @@
+# Round 4 check: full GPU parity suite, smoke, the default bench line with
+# its rocprofv3 summaries (headline, general noise and content streams).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${TAG:-r04j}
+mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
+cat $O/smoke.txt
+timeout -k 10 800 python -u bench.py --profile-dir $O/prof > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+python -c "
+import json; d=json.load(open('$O/bench.json'))
+print('bench', d['value'], d['roofline']['frac'], d['parity']['all_equal'], d['e2e']['value'])
+for k in ('general', 'general_content', 'long_video'):
+    r = d.get(k, {}); print(k, r.get('value'), r.get('stage_ms'), r.get('open_s'), r.get('cuts'), r.get('bits_per_frame'), (r.get('parity') or {}).get('all_equal'))
+"

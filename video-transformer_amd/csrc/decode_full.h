@@ -50,6 +50,14 @@ struct DbkInfo {
 };
 static_assert(sizeof(DbkInfo) == 96, "DbkInfo layout");
 
+// the rows a macroblock's top edge needs from the macroblock above (the
+// general decoder's deblocking hands them from row to row)
+struct DbkLine {  // luma rows 12..15, chroma rows 6..7 (interleaved) of one macroblock
+  uint8_t y[4][16];
+  uint8_t c[2][16];
+};
+static_assert(sizeof(DbkLine) == 96, "DbkLine layout");
+
 struct FullReconArgs {
   const int4 *frames;        // (slot, -, -, -) per picture of the launch
   const MbRec *recs;
@@ -65,8 +73,11 @@ struct FullReconArgs {
   uint32_t epoch;
   int32_t deblock;           // deblocking kernel after reconstruction: 0 none, 1 h264_deblock_full, 2 h264_deblock_lds
   int32_t intra_kernel;      // 1: h264_intra_full, else h264_intra_v2 (where its LDS fits)
-  int32_t _pad;
+  int32_t dbk_bands;         // h264_deblock_lds: workgroups per picture (bands of row pairs), 1..4
   DbkInfo *dbk;              // ring: [slot][mb] deblocking descriptors
+  uint8_t *dbkx;             // dbk_bands > 1: [slot][band boundary] a counter (64 B) + mb_width DbkLine
+                             // rows a band's last macroblock row hands to the next band
+  uint32_t *dbk_tix;         // dbk_bands > 1: this launch's ticket counter (zero before the launch)
   uint32_t *err;
   const ScaleTab *sct;       // LevelScale4x4 / 8x8 (read when P.scaled)
   FullParams P;

@@ -1725,10 +1725,6 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
 // kDbkRingCols - 1 columns before it overwrites one.
 constexpr int kDbkRingRows = 2 * kDbkWaves;
 constexpr int kDbkRingCols = 32;
-struct DbkLine {  // luma rows 12..15, chroma rows 6..7 (interleaved) of one macroblock
-  uint8_t y[4][16];
-  uint8_t c[2][16];
-};
 
 __device__ __forceinline__ void filt_luma_w(int (&s)[8], int bS, uint32_t w) {
   const int alpha = w & 255, beta = (w >> 8) & 255;
@@ -1839,7 +1835,20 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
   __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
   __shared__ DbkLine ring[kDbkRingRows][kDbkRingCols];
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
-  const int slot = a.frames[blockIdx.x].x;
+  // K workgroups per picture, each a band of row pairs; band b's first row
+  // takes the row above's ring lines from band b - 1 through global memory
+  // (an agent-scope counter per boundary, tagged with the run's epoch)
+  const int K = a.dbk_bands > 1 ? a.dbk_bands : 1;
+  // (picture, band) by ticket in start order, not by blockIdx: workgroups go
+  // to the XCDs round-robin and each XCD starts its own in order, so a band
+  // could otherwise be resident and waiting while its producer band still
+  // queues behind other waiting bands; a ticket taken at start means every
+  // lower ticket's workgroup is already running
+  __shared__ int s_ticket;
+  if (threadIdx.x == 0) s_ticket = K > 1 ? static_cast<int>(atomicAdd(a.dbk_tix, 1u)) : static_cast<int>(blockIdx.x);
+  __syncthreads();
+  const int pic = s_ticket / K, band = s_ticket - pic * K;
+  const int slot = a.frames[pic].x;
   const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
   uint8_t *UV = Y + a.uv_off;
@@ -1858,18 +1867,27 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
   // horizontal pass by its column kind (lanes 16..31 = chroma columns)
   const int vq = luma ? 2 : 4, hq = l < 16 ? 3 : 5;
   const int npairs = (mbh + 1) >> 1;
+  const int KB = min(K, npairs);  // bands of at least one row pair each
+  if (band >= KB) return;         // (before any barrier: the whole workgroup leaves)
+  const int p0 = npairs * band / KB, p1 = npairs * (band + 1) / KB;
+  const int y0 = 2 * p0, yend = min(2 * p1, mbh);
+  const int64_t xstride = static_cast<int64_t>(mbw) * static_cast<int64_t>(sizeof(DbkLine)) + 64;
+  uint8_t *const xin = band > 0 ? a.dbkx + (static_cast<int64_t>(slot) * (K - 1) + band - 1) * xstride : nullptr;
+  uint8_t *const xout = band + 1 < K ? a.dbkx + (static_cast<int64_t>(slot) * (K - 1) + band) * xstride : nullptr;
+  const uint32_t xtag = (a.epoch & 0xffffu) << 16;
   RPROF_DECL;
-  for (int p = wave; p < npairs; p += kDbkWaves) {
+  for (int p = p0 + wave; p < p1; p += kDbkWaves) {
     const int y = 2 * p + half;
     const bool row_ok = y < mbh;
     const int ya = row_ok ? y : mbh - 1;
     const bool last_row = y == mbh - 1;
+    const bool band_first = band > 0 && y == y0, band_last = band + 1 < KB && y == yend - 1;
     const int rs = y % kDbkRingRows, rsa = (y + kDbkRingRows - 1) % kDbkRingRows;
     const int64_t yrow = static_cast<int64_t>(ya * 16) * pitch, crow = static_cast<int64_t>(ya * 8) * pitch;
     uint8_t *const rowp = (luma ? Y + yrow : UV + crow) + static_cast<int64_t>(row) * pitch;
     const DbkInfo *const drow = fdbk + ya * mbw;
     // this row's ring slot was the row kDbkRingRows above's: its consumer must be done
-    if (row_ok && y >= kDbkRingRows) {
+    if (row_ok && y - kDbkRingRows >= y0) {
       while (__hip_atomic_load(&prog[y - kDbkRingRows + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < mbw + 1)
         __builtin_amdgcn_s_sleep(1);
     }
@@ -1894,19 +1912,29 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       // row whose consumer is another wave waits until it may overwrite ring
       // column x (the consumer read column x - kDbkRingCols)
       if (act) {
-        const int need_up = (half == 0 && y > 0) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
-        const int need_dn = (half == 1 && y + 1 < mbh) ? x - kDbkRingCols + 1 : -(1 << 30);
+        const int need_up = (half == 0 && y > 0 && !band_first) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
+        const int need_dn = (half == 1 && y + 1 < mbh && !band_last) ? x - kDbkRingCols + 1 : -(1 << 30);
         const int *pu = &prog[y > 0 ? y - 1 : 0], *pd = &prog[y + 1 < mbh ? y + 1 : y];
         while (__hip_atomic_load(pu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_up ||
                __hip_atomic_load(pd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_dn)
           __builtin_amdgcn_s_sleep(1);
+      }
+      if (act && band_first) {  // the previous band's last row, two macroblocks ahead
+        const uint32_t need = xtag | static_cast<uint32_t>(x + 1 < mbw ? x + 2 : mbw + 1);
+        const uint32_t *cnt = reinterpret_cast<const uint32_t *>(xin);
+        for (;;) {
+          const uint32_t v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((v & 0xffff0000u) == xtag && v >= need) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       RPROF(0);
       const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
       // rows above from the ring (final: the row above is two macroblocks ahead)
       if (act && l >= 24 && l < 30 && y > 0) {
-        const DbkLine &L = ring[rsa][x & (kDbkRingCols - 1)];
+        const DbkLine &L = band_first ? reinterpret_cast<const DbkLine *>(xin + 64)[x] : ring[rsa][x & (kDbkRingCols - 1)];
         const uint4 v = ia < 4 ? *reinterpret_cast<const uint4 *>(&L.y[ia][0]) : *reinterpret_cast<const uint4 *>(&L.c[ia - 4][0]);
         *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = v;
       }
@@ -1994,7 +2022,15 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
             if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
           }
           const int lr = luma ? row - 12 : row - 6;  // ring line of this lane's row
-          if (!last_row && lr >= 0) {
+          if (band_last && lr >= 0) {  // to the next band, through global memory
+            DbkLine *xl = reinterpret_cast<DbkLine *>(xout + 64);
+            uint8_t *cur = luma ? &xl[x].y[lr][0] : &xl[x].c[lr][0];
+            if (x > 0) *reinterpret_cast<uint32_t *>(cur - static_cast<int>(sizeof(DbkLine)) + 12) = w0;
+            *reinterpret_cast<uint32_t *>(cur) = w1;
+            *reinterpret_cast<uint32_t *>(cur + 4) = w2;
+            *reinterpret_cast<uint32_t *>(cur + 8) = w3;
+            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = left;
+          } else if (!last_row && lr >= 0) {
             uint8_t *cur = luma ? &ring[rs][x & (kDbkRingCols - 1)].y[lr][0] : &ring[rs][x & (kDbkRingCols - 1)].c[lr][0];
             if (x > 0) {
               uint8_t *prv = luma ? &ring[rs][(x - 1) & (kDbkRingCols - 1)].y[lr][0]
@@ -2016,6 +2052,12 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       __builtin_amdgcn_wave_barrier();
       if (act && l == 0)
         __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (act && band_last) {  // the lines of columns < x + 1 are final: publish to the next band
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (l == 0)
+          __hip_atomic_store(reinterpret_cast<uint32_t *>(xout), xtag | static_cast<uint32_t>(x + 1 < mbw ? x + 1 : mbw + 1),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       RPROF(3);
       RPROF_COUNT(7, 1);
     }
@@ -2093,7 +2135,8 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));
   } else if (a.deblock) {
-    hipLaunchKernelGGL(h264_deblock_lds, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
+    const int k = a.dbk_bands > 1 ? a.dbk_bands : 1;
+    hipLaunchKernelGGL(h264_deblock_lds, dim3(n_frames * k), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_lds launch: %s", hipGetErrorString(e));
   }

@@ -1,9 +1,14 @@
 // devmem.cpp — process-wide caching device allocator (devmem.h).
+//
+// Segments are hipMalloc'd blocks; a segment is cut into ranges.  A request
+// takes the smallest free range that holds it (any segment), splitting off the
+// rest as a new free range; a released range merges with its free neighbours
+// of the same segment.  Segments go back to HIP only when wholly free: on a
+// failed hipMalloc (then one retry) or vts_empty_cache().
 #include "devmem.h"
 
 #include <map>
 #include <mutex>
-#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -11,24 +16,62 @@
 namespace vts {
 namespace {
 
-constexpr size_t kCacheMin = 64 << 10;  // smaller blocks go straight back to HIP
-constexpr size_t kRound = 2 << 20;      // cached sizes rounded up to 2 MiB
+constexpr size_t kCacheMin = 64 << 10;  // smaller blocks go straight to / back to HIP
+constexpr size_t kRound = 2 << 20;      // ranges are multiples of 2 MiB (so they stay 2 MiB aligned)
 
-struct Block {
-  void *p;
+struct Range {
   size_t n;
-  int dev;
+  char *base;  // the segment's hipMalloc pointer
+  bool free;
+};
+struct Device {
+  std::map<char *, Range> ranges;             // every range of every segment, by address
+  std::multimap<size_t, char *> free_by_size;  // the free ranges
+  std::map<char *, size_t> segments;          // base -> bytes
+  size_t cached = 0;                          // bytes in free ranges
 };
 std::mutex g_mu;
-std::unordered_map<void *, Block> g_live;          // allocations handed out (cacheable sizes)
-std::map<int, std::multimap<size_t, void *>> g_free;  // per device: size -> block
-std::map<int, size_t> g_cached;
+std::map<int, Device> g_dev;
 
-void release_device_locked(int dev) {
-  auto &fm = g_free[dev];
-  for (auto &kv : fm) (void)hipFree(kv.second);
-  fm.clear();
-  g_cached[dev] = 0;
+void free_list_erase(Device &d, size_t n, char *p) {
+  auto r = d.free_by_size.equal_range(n);
+  for (auto it = r.first; it != r.second; ++it)
+    if (it->second == p) {
+      d.free_by_size.erase(it);
+      return;
+    }
+}
+
+// hand every wholly free segment back to HIP
+void release_free_segments_locked(Device &d) {
+  for (auto it = d.segments.begin(); it != d.segments.end();) {
+    auto r = d.ranges.find(it->first);
+    if (r != d.ranges.end() && r->second.free && r->second.n == it->second) {
+      free_list_erase(d, r->second.n, r->first);
+      d.cached -= r->second.n;
+      d.ranges.erase(r);
+      (void)hipFree(it->first);
+      it = d.segments.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
+// take `want` bytes from the front of free range p (splitting off the rest)
+void *take_locked(Device &d, char *p, size_t want) {
+  Range &r = d.ranges[p];
+  free_list_erase(d, r.n, p);
+  d.cached -= r.n;
+  if (r.n > want) {
+    char *rest = p + want;
+    d.ranges[rest] = Range{r.n - want, r.base, true};
+    d.free_by_size.emplace(r.n - want, rest);
+    d.cached += r.n - want;
+    r.n = want;
+  }
+  r.free = false;
+  return p;
 }
 
 }  // namespace
@@ -41,44 +84,80 @@ hipError_t dmalloc_raw(void **p, size_t n) {
   if (e != hipSuccess) return e;
   const size_t want = (n + kRound - 1) / kRound * kRound;
   std::lock_guard<std::mutex> lk(g_mu);
-  auto &fm = g_free[dev];
-  auto it = fm.lower_bound(want);
-  if (it != fm.end() && it->first <= 2 * want) {
-    *p = it->second;
-    g_live[*p] = Block{*p, it->first, dev};
-    g_cached[dev] -= it->first;
-    fm.erase(it);
+  Device &d = g_dev[dev];
+  auto it = d.free_by_size.lower_bound(want);
+  if (it != d.free_by_size.end()) {
+    *p = take_locked(d, it->second, want);
     return hipSuccess;
   }
   e = hipMalloc(p, want);
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    release_device_locked(dev);
+    release_free_segments_locked(d);
     e = hipMalloc(p, want);
     if (e != hipSuccess) return e;
   }
-  g_live[*p] = Block{*p, want, dev};
+  char *b = static_cast<char *>(*p);
+  d.segments[b] = want;
+  d.ranges[b] = Range{want, b, false};
   return hipSuccess;
 }
 
 void dfree(void *p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_live.find(p);
-  if (it == g_live.end()) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  // the range may belong to any device's segments: look in the current one first
+  Device *d = nullptr;
+  std::map<char *, Range>::iterator it;
+  auto look = [&](Device &dd) {
+    auto f = dd.ranges.find(static_cast<char *>(p));
+    if (f == dd.ranges.end() || f->second.free) return false;
+    d = &dd;
+    it = f;
+    return true;
+  };
+  if (!look(g_dev[dev]))
+    for (auto &kv : g_dev)
+      if (look(kv.second)) break;
+  if (!d) {
     (void)hipFree(p);
     return;
   }
-  const Block b = it->second;
-  g_live.erase(it);
-  g_free[b.dev].emplace(b.n, b.p);
-  g_cached[b.dev] += b.n;
+  char *q = it->first;
+  Range r = it->second;
+  r.free = true;
+  // merge with the next range of the same segment
+  auto nx = std::next(it);
+  if (nx != d->ranges.end() && nx->second.free && nx->second.base == r.base && nx->first == q + r.n) {
+    free_list_erase(*d, nx->second.n, nx->first);
+    d->cached -= nx->second.n;
+    r.n += nx->second.n;
+    d->ranges.erase(nx);
+  }
+  // ... and with the previous one
+  if (it != d->ranges.begin()) {
+    auto pv = std::prev(it);
+    if (pv->second.free && pv->second.base == r.base && pv->first + pv->second.n == q) {
+      free_list_erase(*d, pv->second.n, pv->first);
+      d->cached -= pv->second.n;
+      pv->second.n += r.n;
+      d->ranges.erase(it);
+      d->free_by_size.emplace(pv->second.n, pv->first);
+      d->cached += pv->second.n;
+      return;
+    }
+  }
+  it->second = r;
+  d->free_by_size.emplace(r.n, q);
+  d->cached += r.n;
 }
 
 size_t dmem_cached(int device) {
   std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_cached.find(device);
-  return it == g_cached.end() ? 0 : it->second;
+  auto it = g_dev.find(device);
+  return it == g_dev.end() ? 0 : it->second.cached;
 }
 
 hipError_t dmem_free(size_t *free_b, size_t *total_b) {
@@ -96,7 +175,7 @@ extern "C" int vts_empty_cache(int device) {
   int cur = 0;
   if (hipGetDevice(&cur) != hipSuccess) return vts::fail(VTS_E_HIP, "hipGetDevice");
   if (hipSetDevice(device) != hipSuccess) return vts::fail(VTS_E_NODEVICE, "device %d", device);
-  vts::release_device_locked(device);
+  vts::release_free_segments_locked(vts::g_dev[device]);
   (void)hipSetDevice(cur);
   return VTS_OK;
 }

@@ -1025,6 +1025,9 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   p.tslots = 0;
   p.lvl_prev = kNoLevel;
   p.pf_col = -1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  p.pf_col2 = -1;
+#endif
   p.todo = 0;
   p.cur_i16 = false;
   p.prev_qpd = false;

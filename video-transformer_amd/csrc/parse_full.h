@@ -409,6 +409,8 @@ struct Parser {
   int pf_col;
 #if defined(__HIP_DEVICE_COMPILE__)
   u32x4 pfl;              // lane p < 8: piece p of the prefetched column (piece_load)
+  u32x4 pfl2;             // ... and of column pf_col + 1 (two columns in flight)
+  int pf_col2;
 #else
   TopCtx pf;
   u32x4 pf1[3];           // the prefetched column's list-1 context (bframes)
@@ -534,6 +536,8 @@ struct Parser {
     const int x = addr % mbw, y = addr / mbw;
     tslots = ((x + 2) % 3) | ((x % 3) << 2) | (((x + 1) % 3) << 4);
 #if defined(__HIP_DEVICE_COMPILE__)
+    // two columns in flight: a skipped macroblock parses in less time than a
+    // global load takes, so a load issued one macroblock ahead still stalled
     if (y > 0) {
       if (!cont) {
         if (x > 0) piece_store(x - 1, piece_load(x - 1));
@@ -545,8 +549,14 @@ struct Parser {
       }
       pf_col = -1;
       if (x + 2 < mbw) {
-        pfl = piece_load(x + 2);
+        if (pf_col2 == x + 2) pfl = pfl2;
+        else pfl = piece_load(x + 2);
         pf_col = x + 2;
+      }
+      pf_col2 = -1;
+      if (x + 3 < mbw) {
+        pfl2 = piece_load(x + 3);
+        pf_col2 = x + 3;
       }
     }
 #else
@@ -938,6 +948,19 @@ struct Parser {
   // (8.4.1.2.3)
   VTS_HD VTS_INLINE void direct_pred(int addr, uint32_t mask) {
     const SliceExt &x = *bc.x;
+    const MbRec &cm = bc.col[addr];
+    const MbRecB &cm1 = bc.col1[addr];
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the colocated block's motion (global memory) requested before the
+    // neighbours' (LDS) so its latency overlaps the spatial predictor
+    const int lb = static_cast<int>(threadIdx.x) & 15;
+    const int lcb = direct8x8 ? ((lb >> 3) * 3) * 4 + ((lb & 3) >> 1) * 3 : lb;
+    const int lc8 = (lcb >> 3) * 2 + ((lcb & 3) >> 1);
+    const int8_t c_ref0 = cm.ref[lc8], c_ref1 = cm1.ref1[lc8];
+    const uint32_t c_mv0 = reinterpret_cast<const uint32_t *>(cm.mv)[lcb];
+    const uint32_t c_mv1 = reinterpret_cast<const uint32_t *>(cm1.mv1)[lcb];
+    const int16_t c_slot0 = cm.ref_slot[lc8], c_slot1 = cm1.ref_slot1[lc8];
+#endif
     int ref0 = -1, ref1 = -1, mp[2][2] = {{0, 0}, {0, 0}};
     bool zero = false;
     if (x.direct_spatial) {
@@ -960,16 +983,22 @@ struct Parser {
         if (ref1 >= 0) mv_pred(addr, 0, 0, 16, 16, ref1, 0, &mp[1][0], &mp[1][1], 1);
       }
     }
-    const MbRec &cm = bc.col[addr];
-    const MbRecB &cm1 = bc.col1[addr];
     bool bad = false;  // temporal: the colocated reference is not in RefPicList0
     VTS_LANES(16, blk) if ((mask >> blk) & 1u) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      const bool use0 = c_ref0 >= 0;
+      const int ref_col = use0 ? c_ref0 : c_ref1;  // -1: intra
+      const uint32_t cmv = use0 ? c_mv0 : c_mv1;
+      const int mcx = ref_col < 0 ? 0 : static_cast<int16_t>(cmv & 0xffff);
+      const int mcy = ref_col < 0 ? 0 : static_cast<int16_t>(cmv >> 16);
+#else
       const int cb = direct8x8 ? ((blk >> 3) * 3) * 4 + ((blk & 3) >> 1) * 3 : blk;
       const int c8 = (cb >> 3) * 2 + ((cb & 3) >> 1);
       const bool use0 = cm.ref[c8] >= 0;
       const int ref_col = use0 ? cm.ref[c8] : cm1.ref1[c8];  // -1: intra
       const int mcx = ref_col < 0 ? 0 : (use0 ? cm.mv[cb][0] : cm1.mv1[cb][0]);
       const int mcy = ref_col < 0 ? 0 : (use0 ? cm.mv[cb][1] : cm1.mv1[cb][1]);
+#endif
       if (x.direct_spatial) {
         const bool col_zero = x.col_short && ref_col == 0 && mcx >= -1 && mcx <= 1 && mcy >= -1 && mcy <= 1;
         const bool z0 = zero || ref0 < 0 || (ref0 == 0 && col_zero);
@@ -979,7 +1008,11 @@ struct Parser {
       } else {
         int r0 = 0;
         if (ref_col >= 0) {  // the lowest list-0 index naming the colocated block's reference picture
+#if defined(__HIP_DEVICE_COMPILE__)
+          const int slot = use0 ? c_slot0 : c_slot1;
+#else
           const int slot = use0 ? cm.ref_slot[c8] : cm1.ref_slot1[c8];
+#endif
           r0 = -1;
           for (int i = s->num_ref - 1; i >= 0; --i)
             if (s->ref_slot[i] == slot) r0 = i;
@@ -1396,6 +1429,9 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *rbsp, int32_t rbsp_le
   p.tslots = 0;
   p.lvl_prev = kNoLevel;
   p.pf_col = -1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  p.pf_col2 = -1;
+#endif
   p.bc = bc;
   p.bframes = P.bframes;
   p.direct8x8 = P.direct8x8;

@@ -189,10 +189,14 @@ struct vts_ctx {
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
   int dbk_kernel = 2;                   // 2: h264_deblock_lds; VTS_DBK=1: h264_deblock_full
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full
+  int dbk_bands = 1;                    // h264_deblock_lds workgroups per picture (VTS_DBK_BANDS, 1..4)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock
+  uint8_t *d_dbkx[2] = {nullptr, nullptr};       // dbk_bands > 1: rows handed between deblocking bands
+  uint32_t *d_dbk_tix = nullptr;                 // ... one ticket counter per level launch of a window
+  int64_t dbk_tix_n = 0;
   int16_t *d_arena[2] = {nullptr, nullptr};
   int64_t arena_blocks = 0;             // per ring
   // kept from open for a later switch to the general decoder (decoder = auto)

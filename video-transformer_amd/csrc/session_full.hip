@@ -29,7 +29,11 @@
 namespace vts {
 namespace {
 
-constexpr int64_t kWindowBytes = 96ll << 30;  // per ring: parse throughput grows with the slices per launch
+// per ring: parse throughput grows with the slices per launch, and every
+// window runs its own chain of reconstruction levels, so one window per
+// 10-min 720p CABAC video (~104 GB: the arena reserves 27 blocks per
+// macroblock) while HBM allows it (avail / 2 below)
+constexpr int64_t kWindowBytes = 128ll << 30;
 constexpr int64_t kMinRingBytes = 1ll << 30;
 
 }  // namespace
@@ -411,9 +415,21 @@ int run_general(vts_ctx *c) {
     ra.epoch = epoch;
     ra.deblock = c->dbk_kernel;
     ra.intra_kernel = c->intra_kernel;
+    ra.dbk_bands = c->d_dbkx[r] ? c->dbk_bands : 1;
+    ra.dbkx = c->d_dbkx[r];
     ra.err = c->d_err;
     ra.sct = c->d_scale;
     ra.P = c->fprm;
+    if (ra.dbk_bands > 1 && !w.lvl_off.empty()) {  // the deblocking launches' ticket counters, zeroed
+      const int64_t nl = static_cast<int64_t>(w.lvl_off.size());
+      if (c->dbk_tix_n < nl) {
+        vts::dfree(c->d_dbk_tix);
+        c->d_dbk_tix = nullptr;
+        HIP_TRY(vts::dmalloc(&c->d_dbk_tix, sizeof(uint32_t) * static_cast<size_t>(nl)));
+        c->dbk_tix_n = nl;
+      }
+      HIP_TRY(hipMemsetAsync(c->d_dbk_tix, 0, sizeof(uint32_t) * static_cast<size_t>(nl), sd));
+    }
     if (!w.lvl_off.empty()) {  // every picture's bS at once: it needs only the parse's records
       ra.frames = c->d_levels + w.lvl_off[0];
       VTS_TRY(bs_full_launch(ra, static_cast<int>(w.lvl_off.back() + w.lvl_cnt.back() - w.lvl_off[0]), sd));
@@ -425,6 +441,7 @@ int run_general(vts_ctx *c) {
     for (size_t l = 0; l < w.lvl_off.size(); ++l) {
       const int g = grp_of(l);
       ra.frames = c->d_levels + w.lvl_off[l];
+      ra.dbk_tix = c->d_dbk_tix ? c->d_dbk_tix + l : nullptr;
       VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], g ? c->s_grp[g - 1] : sd));
     }
     for (int g = 1; g < ng; ++g) {
