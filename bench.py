@@ -572,8 +572,8 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
     instruction-count pass.  Algorithmic bytes per picture (display-size NV12
     = 1.5*W*H):
       h264_inter_full   reference read + NV12 write          3.0*W*H
-      h264_intra_full   NV12 write (intra pictures' share)   1.5*W*H
-      h264_deblock_full NV12 read + write                    3.0*W*H
+      h264_intra_v2 / h264_intra_full      NV12 write (intra share)  1.5*W*H
+      h264_deblock_lds / h264_deblock_full NV12 read + write         3.0*W*H
       score_runs        SURVEY 8(d) bytes                     1.5*W*H + 5*w*h + 1028
     (intra and inter both count the whole picture's write; their sum
     overstates a picture that mixes them, so the sum is not reported).
@@ -583,8 +583,9 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
     divided by it (per run)."""
     nv12 = 1.5 * width * height
     w, h = width // k, height // k
-    per_pic = {"h264_inter_full": 2 * nv12, "h264_intra_full": nv12,
-               "h264_deblock_full": 2 * nv12, f"score_runs<{k}>": nv12 + 5 * w * h + 1028}
+    per_pic = {"h264_inter_full": 2 * nv12, "h264_intra_v2": nv12, "h264_intra_full": nv12,
+               "h264_deblock_lds": 2 * nv12, "h264_deblock_full": 2 * nv12,
+               f"score_runs<{k}>": nv12 + 5 * w * h + 1028}
     out = {}
     for name, b in per_pic.items():
         row = prof.get(name)
@@ -592,8 +593,10 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
             continue
         t = row["busy_ns_total"] * 1e-9 / CHILD_RUNS
         ach = b * frames / t / 1e9
+        nd = max(1, row["dispatches_traced"] // CHILD_RUNS)
         out[name] = {"bound": "hbm", "busy_ms": round(t * 1e3, 2),
-                     "dispatches": row["dispatches_traced"] // CHILD_RUNS, "bytes_per_picture": round(b),
+                     "dispatches": row["dispatches_traced"] // CHILD_RUNS,
+                     "busy_ms_per_dispatch": round(t * 1e3 / nd, 3), "bytes_per_picture": round(b),
                      "achieved": round(ach, 1), "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4)}
     pname = "h264_parse_full_cabac" if "h264_parse_full_cabac" in prof else "h264_parse_full"
@@ -1091,9 +1094,11 @@ def main() -> None:
         # the batch's sessions give their HBM back before the 2-h video's rings
         for v in sl:
             v.close()
+        # the general streams first: after the 2-h video's session its cached
+        # segments cannot host the general decoder's ~56 GB coefficient arena,
+        # and HBM released to the driver is cleared again before reuse (DESIGN
+        # §0 item 4)
         for key, p, label, info in (
-                ("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
-                                          "(216 000 frames), streamed two-ring decode", None),
                 ("general", gen_path, "general decoder, worst case: 10-min 720p x264-structured "
                                       "full-syntax NOISE stream (random syntax decisions and residuals; "
                                       "High profile: CABAC, 8x8 transform and Intra_8x8, B pyramid with "
@@ -1104,7 +1109,9 @@ def main() -> None:
                                                   "cuts, a panning background and moving sprites coded in "
                                                   "closed loop by SAD decisions with quantised residuals; "
                                                   "CABAC, 8x8 transform, B pyramid, implicit weights, "
-                                                  "deblocking, keyint ~8 s)", content_info)):
+                                                  "deblocking, keyint ~8 s)", content_info),
+                ("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
+                                          "(216 000 frames), streamed two-ring decode", None)):
             try:
                 r = run_single(p, gpu=gpu, k=4, steps=3, threads=threads, label=label,
                                planted=info["cuts"] if info else None)
