@@ -1,0 +1,26 @@
+# Round 4: general decoder GOP groups (VTS_GENERAL_GROUPS 2 / 3 / 4) with the
+# HIP runtime's default 4 hardware queues per process and with 8
+# (GPU_MAX_HW_QUEUES=8: every group's stream on its own queue beside the
+# parse and score streams), content and noise streams.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${TAG:-r04n}
+mkdir -p $O
+timeout -k 10 300 python - <<'PY' || exit 1
+import sys; sys.path.insert(0, "video-transformer_amd")
+from concurrent.futures import ThreadPoolExecutor
+from vtseg import scene
+kw = dict(width=1280, height=720, fps=30, n_frames=18000, seed=0x5EED, coding="full", slices_per_row=0, max_motion=4,
+          bframes=True, weighted="implicit", cabac=True, transform_8x8=True)
+with ThreadPoolExecutor(2) as ex:
+    a = ex.submit(scene.synth_write, "/tmp/gcab.mp4", **kw)
+    b = ex.submit(scene.synth_write, "/tmp/gcontent.mp4", content=True, gop_max_s=8.0, **kw)
+    a.result(); b.result()
+print("streams written", flush=True)
+PY
+for V in gcontent gcab; do
+timeout -k 10 400 python tools/gpu/env_ab.py /tmp/$V.mp4 3 g2=VTS_GENERAL_GROUPS=2 g4=VTS_GENERAL_GROUPS=4 > $O/q4_$V.json 2> $O/q4_$V.err || { tail -20 $O/q4_$V.err; exit 1; }
+cat $O/q4_$V.json
+GPU_MAX_HW_QUEUES=8 timeout -k 10 400 python tools/gpu/env_ab.py /tmp/$V.mp4 3 g2=VTS_GENERAL_GROUPS=2 g3=VTS_GENERAL_GROUPS=3 g4=VTS_GENERAL_GROUPS=4 > $O/q8_$V.json 2> $O/q8_$V.err || { tail -20 $O/q8_$V.err; exit 1; }
+cat $O/q8_$V.json
+done
