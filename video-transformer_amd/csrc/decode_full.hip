@@ -1932,14 +1932,20 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       RPROF(0);
       const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
-      // rows above from the ring (final: the row above is two macroblocks ahead)
+      // a macroblock none of whose edges (left, top, inside) filters keeps its
+      // samples: its step skips both passes and writes back what it loaded
+      const bool still = (bsw.x | bsw.y | bsw.z | bsw.w) == 0u;
+      // rows above from the ring (final: the row above is two macroblocks
+      // ahead); a still macroblock's lanes 24..27 take the lines they store
+      uint4 above = {0u, 0u, 0u, 0u};
       if (act && l >= 24 && l < 30 && y > 0) {
         const DbkLine &L = band_first ? reinterpret_cast<const DbkLine *>(xin + 64)[x] : ring[rsa][x & (kDbkRingCols - 1)];
-        const uint4 v = ia < 4 ? *reinterpret_cast<const uint4 *>(&L.y[ia][0]) : *reinterpret_cast<const uint4 *>(&L.c[ia - 4][0]);
-        *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = v;
+        const int il = still ? (l < 27 ? l - 23 : 5) : ia;
+        above = il < 4 ? *reinterpret_cast<const uint4 *>(&L.y[il][0]) : *reinterpret_cast<const uint4 *>(&L.c[il - 4][0]);
+        if (!still) *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = above;
       }
       // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
-      if (act && lrow) {
+      if (act && lrow && !still) {
         const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
         int r[20], u[20];
 #pragma unroll
@@ -1969,7 +1975,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       RPROF(1);
       // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved
       // chroma column l - 16 (one plane; its edges at slots 0 and 2)
-      if (act) {
+      if (act && !still) {
         const int j = l - 16, pl = j & 1;
         const int seg = luma ? l >> 2 : j >> 2;
         uint8_t *const ycol = &t.y[0][4 + l];
@@ -2008,10 +2014,21 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       // the rows above this macroblock that its top edge finished
       if (act) {
         if (lrow) {
-          const uint8_t *src = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
-          const uint32_t w0 = *reinterpret_cast<const uint32_t *>(src), w1 = *reinterpret_cast<const uint32_t *>(src + 4);
-          const uint32_t w2 = *reinterpret_cast<const uint32_t *>(src + 8), w3 = *reinterpret_cast<const uint32_t *>(src + 12);
-          left = *reinterpret_cast<const uint32_t *>(src + 16);
+          uint32_t w0, w1, w2, w3;
+          if (still) {
+            w0 = left;
+            w1 = q4.x;
+            w2 = q4.y;
+            w3 = q4.z;
+            left = q4.w;
+          } else {
+            const uint8_t *src = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
+            w0 = *reinterpret_cast<const uint32_t *>(src);
+            w1 = *reinterpret_cast<const uint32_t *>(src + 4);
+            w2 = *reinterpret_cast<const uint32_t *>(src + 8);
+            w3 = *reinterpret_cast<const uint32_t *>(src + 12);
+            left = *reinterpret_cast<const uint32_t *>(src + 16);
+          }
           const bool mine = last_row || (luma ? row < 13 : row < 7);
           if (mine) {
             uint8_t *dst = rowp + x * 16;
@@ -2044,8 +2061,10 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
           }
         } else if (l < 28 && y > 0) {
           const int i = l - 24;  // luma rows -3..-1, chroma row -1 of the macroblock above
-          if (i < 3) *reinterpret_cast<uint4 *>(Y + ybase + static_cast<int64_t>(i - 3) * pitch) = *reinterpret_cast<const uint4 *>(&t.y[1 + i][4]);
-          else *reinterpret_cast<uint4 *>(UV + cbase - pitch) = *reinterpret_cast<const uint4 *>(&t.c[1][4]);
+          const uint4 v = still ? above : (i < 3 ? *reinterpret_cast<const uint4 *>(&t.y[1 + i][4])
+                                                 : *reinterpret_cast<const uint4 *>(&t.c[1][4]));
+          if (i < 3) *reinterpret_cast<uint4 *>(Y + ybase + static_cast<int64_t>(i - 3) * pitch) = v;
+          else *reinterpret_cast<uint4 *>(UV + cbase - pitch) = v;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
