@@ -9,7 +9,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, "video-transformer_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "video-transformer_amd"))
 import numpy as np
 import torch
 from vtseg import scene

@@ -74,6 +74,7 @@ struct FullReconArgs {
   int32_t deblock;           // deblocking kernel after reconstruction: 0 none, 1 h264_deblock_full, 2 h264_deblock_lds
   int32_t intra_kernel;      // 1: h264_intra_full, else h264_intra_v2 (where its LDS fits)
   int32_t dbk_bands;         // h264_deblock_lds: workgroups per picture (bands of row pairs), 1..4
+  int32_t bs_fused;          // 1: h264_inter_full derives the level's bS (DbkInfo) after its blocks; 0: h264_bs_full does
   DbkInfo *dbk;              // ring: [slot][mb] deblocking descriptors
   uint8_t *dbkx;             // dbk_bands > 1: [slot][band boundary] a counter (64 B) + mb_width DbkLine
                              // rows a band's last macroblock row hands to the next band
@@ -94,6 +95,6 @@ int parse_full_launch(const FullParseArgs &a, hipStream_t s);
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);
 // reconstruction (+ deblocking from bs_full_launch's descriptors when
 // a.deblock) of n_frames pictures of one level
-int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);
+int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s, hipEvent_t after_inter = nullptr);
 
 }  // namespace vts

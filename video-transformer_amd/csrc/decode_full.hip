@@ -488,13 +488,12 @@ __device__ __forceinline__ void pred_ref(const FullReconArgs &a, int rs, uint32_
       }
 }
 
+__device__ void bs_mb(const FullReconArgs &a, int slot, int mb, int b);  // h264_bs_full
+
 // ------------------------------------------------------- inter / I_PCM blocks
-// grid (ceil(nmb / 16), pictures of the level); lane = (macroblock, raster 4x4 block b)
-__global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a) {
+// lane = (macroblock, raster 4x4 block b)
+__device__ __forceinline__ void inter_mb(const FullReconArgs &a, int slot, int mb, int b) {
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
-  const int slot = a.frames[blockIdx.y].x;
-  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4);
-  const int b = threadIdx.x & 15;
   if (mb >= nmb) return;
   const MbRec *rec = a.recs + static_cast<int64_t>(slot) * nmb + mb;
   const MbHdr h = load_hdr(rec);
@@ -593,6 +592,18 @@ __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a
   for (int y = 0; y < 2; ++y)
     *reinterpret_cast<uint32_t *>(UV + static_cast<int64_t>(cy + y) * pitch + 2 * cx) =
         pack4(cpred[0][y * 2], cpred[1][y * 2], cpred[0][y * 2 + 1], cpred[1][y * 2 + 1]);
+}
+// grid (ceil(nmb / 16), pictures of the level).  bs_fused (VTS_BS=1): the
+// level's bS descriptors come from the same lanes after the blocks are stored
+// (the deblocking launch after this one reads them) — measured slower than a
+// separate bS launch per level beside the chain (inter 0.31 -> 0.58 ms per
+// launch, profiles/r04r_bs_fused_ab.json), kept as an option
+__global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a) {
+  const int slot = a.frames[blockIdx.y].x;
+  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int b = threadIdx.x & 15;
+  inter_mb(a, slot, mb, b);
+  if (a.bs_fused) bs_mb(a, slot, mb, b);  // every lane (the macroblock's 16 lanes meet in a butterfly)
 }
 
 // ------------------------------------------------------------ intra blocks
@@ -1426,10 +1437,8 @@ __device__ __forceinline__ uint32_t edge_word(int qpav, int fa, int fb) {
 // an OR butterfly over its 16 lanes, so the wavefront below reads one 32-byte
 // descriptor per macroblock.  (A lane per macroblock walking all 32 edges
 // made every load a strided 4-byte gather.)
-__global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
+__device__ void bs_mb(const FullReconArgs &a, int slot, int mb, int b) {
   const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
-  const int slot = a.frames[blockIdx.y].x;
-  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4), b = threadIdx.x & 15;
   const bool ok = mb < nmb;
   const int mbc = ok ? mb : nmb - 1;  // tail lanes: a valid macroblock, result unused (the butterfly needs them)
   const MbRec *Q = a.recs + static_cast<int64_t>(slot) * nmb + mbc;
@@ -1501,6 +1510,9 @@ __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
     }
     reinterpret_cast<uint4 *>(o)[b] = make_uint4(e4[0], e4[1], e4[2], e4[3]);
   }
+}
+__global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
+  bs_mb(a, a.frames[blockIdx.y].x, blockIdx.x * 16 + (threadIdx.x >> 4), threadIdx.x & 15);
 }
 
 __device__ __forceinline__ DbkInfo dbk_load(const DbkInfo *p) {
@@ -2130,7 +2142,7 @@ int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   return VTS_OK;
 }
 
-int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
+int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s, hipEvent_t after_inter) {
   if (n_frames <= 0) return VTS_OK;
   const int nmb = a.P.mb_width * a.P.mb_height;
   if (a.P.mb_height > 1024) return fail(VTS_E_UNSUPPORTED, "picture taller than 1024 macroblock rows");
@@ -2138,6 +2150,7 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   hipLaunchKernelGGL(h264_inter_full, dim3((nmb + 15) / 16, n_frames), dim3(kInterThreads), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_inter_full launch: %s", hipGetErrorString(e));
+  if (after_inter && hipEventRecord(after_inter, s) != hipSuccess) return fail(VTS_E_HIP, "hipEventRecord after h264_inter_full");
   // lane-parallel intra (default) while its LDS fits, else the by-block kernel
   const size_t i2_dyn = sizeof(i2::I2Line) * static_cast<size_t>(a.P.mb_width + a.P.mb_height) + 2 * static_cast<size_t>(nmb);
   if (a.intra_kernel != 1 && i2_dyn + sizeof(I2Tile) * kI2Groups + 8 * 1024 <= 160 * 1024) {

@@ -191,6 +191,12 @@ struct vts_ctx {
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full
   int dbk_bands = 1;                    // h264_deblock_lds workgroups per picture (VTS_DBK_BANDS, 1..4)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
+  // where the general decoder derives bS (VTS_BS): 0 one launch for the
+  // window at the head of the level chain, 1 in each level's inter launch,
+  // 2 one launch per level on the score stream, paced by the chain (level
+  // l + 1's after level l's inter launch)
+  int bs_mode = 2;
+  std::vector<hipEvent_t> ev_bs;  // bs_mode 2: two per level launch of a window (reused window to window)
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock

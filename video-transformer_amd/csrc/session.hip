@@ -260,6 +260,7 @@ int alloc_general(vts_ctx *c) {
   if (const char *e = std::getenv("VTS_DBK")) c->dbk_kernel = std::atoi(e) == 1 ? 1 : 2;
   if (const char *e = std::getenv("VTS_INTRA")) c->intra_kernel = std::atoi(e) == 1 ? 1 : 2;
   if (const char *e = std::getenv("VTS_DBK_BANDS")) c->dbk_bands = std::min(4, std::max(1, std::atoi(e)));
+  if (const char *e = std::getenv("VTS_BS")) c->bs_mode = std::min(2, std::max(0, std::atoi(e)));
   HIP_TRY(vts::dmalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
@@ -1314,6 +1315,8 @@ extern "C" int vts_close(vts_ctx *c) {
   for (auto e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->lev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto e : c->ev_bs)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);

@@ -430,20 +430,66 @@ int run_general(vts_ctx *c) {
       }
       HIP_TRY(hipMemsetAsync(c->d_dbk_tix, 0, sizeof(uint32_t) * static_cast<size_t>(nl), sd));
     }
-    if (!w.lvl_off.empty()) {  // every picture's bS at once: it needs only the parse's records
+    // bS needs only the parse's records (vts_ctx::bs_mode)
+    const int bsm = w.lvl_off.empty() ? 0 : c->bs_mode;
+    ra.bs_fused = bsm == 1 ? 1 : 0;
+    auto bs_level = [&](size_t l, hipStream_t s) {
+      ra.frames = c->d_levels + w.lvl_off[l];
+      return bs_full_launch(ra, w.lvl_cnt[l], s);
+    };
+    if (bsm == 0 && !w.lvl_off.empty()) {
       ra.frames = c->d_levels + w.lvl_off[0];
       VTS_TRY(bs_full_launch(ra, static_cast<int>(w.lvl_off.back() + w.lvl_cnt.back() - w.lvl_off[0]), sd));
     }
-    if (ng > 1) {  // groups >= 1 on their own streams, after the bS launch
+    if (ng > 1) {  // groups >= 1 on their own streams, after the parse (and bS in mode 0)
       HIP_TRY(hipEventRecord(c->ev_grp[0], sd));
       for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], c->ev_grp[0], 0));
     }
-    for (size_t l = 0; l < w.lvl_off.size(); ++l) {
-      const int g = grp_of(l);
-      ra.frames = c->d_levels + w.lvl_off[l];
-      ra.dbk_tix = c->d_dbk_tix ? c->d_dbk_tix + l : nullptr;
-      VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], g ? c->s_grp[g - 1] : sd));
+    // the groups' level launches, interleaved (j-th level of every group, then
+    // the next): in mode 2 the score stream derives level j + 1's bS while
+    // group g runs level j's intra and deblocking launches (compute units the
+    // one-workgroup-per-picture kernels leave idle), and level j + 1 waits for it
+    // (one side stream for every group: the groups' bS on separate streams,
+    // odd groups' on the parse stream, measured slower — 188 -> 201 ms on the
+    // content stream, that stream sharing a hardware queue with a group's,
+    // profiles/r04t_bs_paced_split_ab.json)
+    auto sb_of = [&](int) { return c->s_score; };
+    std::vector<size_t> lo(static_cast<size_t>(ng)), hi(static_cast<size_t>(ng));
+    size_t jmax = 0;
+    for (int g = 0; g < ng; ++g) {
+      lo[static_cast<size_t>(g)] = g ? static_cast<size_t>(w.grp[static_cast<size_t>(g - 1)]) : 0;
+      hi[static_cast<size_t>(g)] = g + 1 < ng ? static_cast<size_t>(w.grp[static_cast<size_t>(g)]) : w.lvl_off.size();
+      jmax = std::max(jmax, hi[static_cast<size_t>(g)] - lo[static_cast<size_t>(g)]);
     }
+    if (bsm == 2) {
+      if (c->ev_bs.size() < 2 * w.lvl_off.size()) {
+        const size_t n0 = c->ev_bs.size();
+        c->ev_bs.resize(2 * w.lvl_off.size(), nullptr);
+        for (size_t k = n0; k < c->ev_bs.size(); ++k) HIP_TRY(hipEventCreateWithFlags(&c->ev_bs[k], hipEventDisableTiming));
+      }
+      HIP_TRY(hipStreamWaitEvent(c->s_score, E[1], 0));
+      for (int g = 0; g < ng; ++g) {  // every group's first level
+        if (lo[static_cast<size_t>(g)] >= hi[static_cast<size_t>(g)]) continue;
+        VTS_TRY(bs_level(lo[static_cast<size_t>(g)], sb_of(g)));
+        HIP_TRY(hipEventRecord(c->ev_bs[2 * lo[static_cast<size_t>(g)]], sb_of(g)));
+      }
+    }
+    for (size_t jj = 0; jj < jmax; ++jj)
+      for (int g = 0; g < ng; ++g) {
+        const size_t l = lo[static_cast<size_t>(g)] + jj;
+        if (l >= hi[static_cast<size_t>(g)]) continue;
+        hipStream_t s = g ? c->s_grp[g - 1] : sd;
+        if (bsm == 2) HIP_TRY(hipStreamWaitEvent(s, c->ev_bs[2 * l], 0));
+        ra.frames = c->d_levels + w.lvl_off[l];
+        ra.dbk_tix = c->d_dbk_tix ? c->d_dbk_tix + l : nullptr;
+        const bool next = bsm == 2 && l + 1 < hi[static_cast<size_t>(g)];
+        VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], s, next ? c->ev_bs[2 * l + 1] : nullptr));
+        if (next) {
+          HIP_TRY(hipStreamWaitEvent(sb_of(g), c->ev_bs[2 * l + 1], 0));
+          VTS_TRY(bs_level(l + 1, sb_of(g)));
+          HIP_TRY(hipEventRecord(c->ev_bs[2 * (l + 1)], sb_of(g)));
+        }
+      }
     for (int g = 1; g < ng; ++g) {
       HIP_TRY(hipEventRecord(c->ev_grp[g - 1], c->s_grp[g - 1]));
       HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[g - 1], 0));
