@@ -1841,7 +1841,9 @@ constexpr int dbk_hrow(int j) {
   return (j >= 2 && j <= 5) ? j - 2 : ((j >= 10 && j <= 13) ? j - 6 : (j == 14 ? 8 : (j == 15 ? 9 : -1)));
 }
 
-// grid: pictures of the level
+// grid: pictures of the level (x bands); kBands: the band hand-off compiled in
+// (VTS_DBK_BANDS > 1), else K = 1 folds it away with its registers
+template <bool kBands>
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a) {
   __shared__ DbkTile tiles[kDbkWaves * 2];
   __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
@@ -1850,7 +1852,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
   // K workgroups per picture, each a band of row pairs; band b's first row
   // takes the row above's ring lines from band b - 1 through global memory
   // (an agent-scope counter per boundary, tagged with the run's epoch)
-  const int K = a.dbk_bands > 1 ? a.dbk_bands : 1;
+  const int K = kBands && a.dbk_bands > 1 ? a.dbk_bands : 1;
   // (picture, band) by ticket in start order, not by blockIdx: workgroups go
   // to the XCDs round-robin and each XCD starts its own in order, so a band
   // could otherwise be resident and waiting while its producer band still
@@ -1863,7 +1865,10 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
   const int slot = a.frames[pic].x;
   const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
-  uint8_t *UV = Y + a.uv_off;
+  // samples addressed as 32-bit offsets from the picture (uniform base +
+  // per-lane offset: one VGPR per address instead of a pair)
+  const uint32_t uvo = static_cast<uint32_t>(a.uv_off);
+  auto at = [Y](uint32_t o) { return Y + static_cast<uint64_t>(o); };
   const int pitch = a.pitch;
   for (int i = threadIdx.x; i < mbh; i += kDbkThreads) prog[i] = 0;
   __syncthreads();
@@ -1896,7 +1901,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
     const bool band_first = band > 0 && y == y0, band_last = band + 1 < KB && y == yend - 1;
     const int rs = y % kDbkRingRows, rsa = (y + kDbkRingRows - 1) % kDbkRingRows;
     const int64_t yrow = static_cast<int64_t>(ya * 16) * pitch, crow = static_cast<int64_t>(ya * 8) * pitch;
-    uint8_t *const rowp = (luma ? Y + yrow : UV + crow) + static_cast<int64_t>(row) * pitch;
+    const uint32_t rowo = static_cast<uint32_t>((luma ? yrow : uvo + crow) + static_cast<int64_t>(row) * pitch);
     const DbkInfo *const drow = fdbk + ya * mbw;
     // this row's ring slot was the row kDbkRingRows above's: its consumer must be done
     if (row_ok && y - kDbkRingRows >= y0) {
@@ -1907,7 +1912,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
     // the next iteration's macroblock: bS words, the lane's edge parameters, its row
     const uint4 *dq = reinterpret_cast<const uint4 *>(drow);
     uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
-    uint4 npx = *reinterpret_cast<const uint4 *>(rowp);
+    uint4 npx = *reinterpret_cast<const uint4 *>(at(rowo));
     for (int it = 0; it < mbw + 2; ++it) {
       const int x = it - 2 * half;
       const bool act = row_ok && x >= 0 && x < mbw;
@@ -1918,7 +1923,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
         nbs = dn[0];
         nv = dn[vq];
         nh = dn[hq];
-        npx = *reinterpret_cast<const uint4 *>(rowp + xn * 16);
+        npx = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xn * 16)));
       }
       // the upper row of the pair waits for the row above (another wave); a
       // row whose consumer is another wave waits until it may overwrite ring
@@ -1943,18 +1948,16 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       RPROF(0);
-      const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
+      const uint32_t ybase = static_cast<uint32_t>(yrow) + static_cast<uint32_t>(x * 16);
+      const uint32_t cbase = uvo + static_cast<uint32_t>(crow) + static_cast<uint32_t>(x * 16);
       // a macroblock none of whose edges (left, top, inside) filters keeps its
       // samples: its step skips both passes and writes back what it loaded
       const bool still = (bsw.x | bsw.y | bsw.z | bsw.w) == 0u;
-      // rows above from the ring (final: the row above is two macroblocks
-      // ahead); a still macroblock's lanes 24..27 take the lines they store
-      uint4 above = {0u, 0u, 0u, 0u};
+      // rows above from the ring (final: the row above is two macroblocks ahead)
       if (act && l >= 24 && l < 30 && y > 0) {
         const DbkLine &L = band_first ? reinterpret_cast<const DbkLine *>(xin + 64)[x] : ring[rsa][x & (kDbkRingCols - 1)];
-        const int il = still ? (l < 27 ? l - 23 : 5) : ia;
-        above = il < 4 ? *reinterpret_cast<const uint4 *>(&L.y[il][0]) : *reinterpret_cast<const uint4 *>(&L.c[il - 4][0]);
-        if (!still) *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = above;
+        const uint4 v = ia < 4 ? *reinterpret_cast<const uint4 *>(&L.y[ia][0]) : *reinterpret_cast<const uint4 *>(&L.c[ia - 4][0]);
+        *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = v;
       }
       // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
       if (act && lrow && !still) {
@@ -2043,7 +2046,7 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
           }
           const bool mine = last_row || (luma ? row < 13 : row < 7);
           if (mine) {
-            uint8_t *dst = rowp + x * 16;
+            uint8_t *dst = at(rowo + static_cast<uint32_t>(x * 16));
             if (x > 0) *reinterpret_cast<uint32_t *>(dst - 4) = w0;
             *reinterpret_cast<uint32_t *>(dst) = w1;
             *reinterpret_cast<uint32_t *>(dst + 4) = w2;
@@ -2073,10 +2076,9 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
           }
         } else if (l < 28 && y > 0) {
           const int i = l - 24;  // luma rows -3..-1, chroma row -1 of the macroblock above
-          const uint4 v = still ? above : (i < 3 ? *reinterpret_cast<const uint4 *>(&t.y[1 + i][4])
-                                                 : *reinterpret_cast<const uint4 *>(&t.c[1][4]));
-          if (i < 3) *reinterpret_cast<uint4 *>(Y + ybase + static_cast<int64_t>(i - 3) * pitch) = v;
-          else *reinterpret_cast<uint4 *>(UV + cbase - pitch) = v;
+          const uint4 v = i < 3 ? *reinterpret_cast<const uint4 *>(&t.y[1 + i][4]) : *reinterpret_cast<const uint4 *>(&t.c[1][4]);
+          if (i < 3) *reinterpret_cast<uint4 *>(at(ybase + static_cast<uint32_t>((i - 3) * pitch))) = v;
+          else *reinterpret_cast<uint4 *>(at(cbase - static_cast<uint32_t>(pitch))) = v;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2168,7 +2170,8 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s, hipEv
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));
   } else if (a.deblock) {
     const int k = a.dbk_bands > 1 ? a.dbk_bands : 1;
-    hipLaunchKernelGGL(h264_deblock_lds, dim3(n_frames * k), dim3(kDbkThreads), 0, s, a);
+    if (k > 1) hipLaunchKernelGGL(h264_deblock_lds<true>, dim3(n_frames * k), dim3(kDbkThreads), 0, s, a);
+    else hipLaunchKernelGGL(h264_deblock_lds<false>, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_lds launch: %s", hipGetErrorString(e));
   }
