@@ -1210,7 +1210,7 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
   __syncthreads();
   const int maxl = s_max;
   const int g = tid >> 5;
-  const DevLanes lanes{tid & 31};
+  const DevLanes lanes0{tid & 31};
   i2::I2Ctx ctx;
   ctx.recs = a.recs + static_cast<int64_t>(slot) * nmb;
   ctx.arena = a.arena;
@@ -1257,7 +1257,7 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
   if (bucketed) {
     const int jf = first_at(0);
     pv = jf >= 0;
-    if (pv) pre = i2::i2_prefetch(ctx, s_list[jf], lanes.t);
+    if (pv) pre = i2::i2_prefetch(ctx, s_list[jf], lanes0.t);
   }
   RPROF(0);
   for (int l = 0; l <= maxl; ++l) {
@@ -1280,6 +1280,11 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
     // barrier), barrier
     for (int base = j0; base < j1; base += kI2Groups) {
       const int j = base + g;
+      // the lane index made opaque each round: what derives from it (lane
+      // masks and addresses) is recomputed per round instead of hoisted out
+      // of the loop and spilled, whose reloads waited for every load in flight
+      DevLanes lanes = lanes0;
+      asm volatile("" : "+v"(lanes.t));
       if (j < j1) {
         if (!pv) pre = i2::i2_prefetch(ctx, s_list[j], lanes.t);
         i2::intra2_prepare(ctx, s_list[j], pre, lanes, tiles[g], lcol, lrow, rp_);

@@ -1039,6 +1039,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   if (last < 0) return DEC_E_SYNTAX;
   const int64_t stop_bit = int64_t(last) * 8 + (7 - __builtin_ctz(static_cast<uint32_t>(rbsp[last])));
   p.br.init(rbsp, rbsp_len, sc->cache);
+  p.refresh_lane();
   p.br.reset_at(s.data_bit);
   // cabac_alignment_one_bit
   while (p.br.consumed() & 7)
@@ -1053,6 +1054,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
       p.err |= DEC_E_SYNTAX;
       break;
     }
+    p.refresh_lane();
     VTS_PROF_P(p, 1);
     p.begin_mb(addr);
     VTS_PROF_P(p, 2);

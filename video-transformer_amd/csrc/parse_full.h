@@ -322,7 +322,7 @@ struct RbspBitsT {
 // a loop.  Bodies are independent per l (no continue / break, no state carried
 // between elements); a per-lane condition comes back uniform through vts_any.
 #if defined(__HIP_DEVICE_COMPILE__)
-#define VTS_LANES(n, l) if (const int l = static_cast<int>(threadIdx.x); l < (n))
+#define VTS_LANES(n, l) if (const int l = lane_; l < (n))
 __device__ VTS_INLINE bool vts_any(bool b) { return __ballot(b) != 0; }
 #else
 #define VTS_LANES(n, l) for (int l = 0; l < (n); ++l)
@@ -408,10 +408,19 @@ struct Parser {
   // row above, column pf_col: prefetched during the previous macroblock
   int pf_col;
 #if defined(__HIP_DEVICE_COMPILE__)
+  // the lane index, re-read opaquely at every macroblock (refresh_lane): what
+  // derives from it is computed per macroblock instead of hoisted out of the
+  // macroblock loop and spilled (each reload waited for every load in flight)
+  int lane_;
+  __device__ VTS_INLINE void refresh_lane() {
+    lane_ = static_cast<int>(threadIdx.x);
+    asm volatile("" : "+v"(lane_));
+  }
   u32x4 pfl;              // lane p < 8: piece p of the prefetched column (piece_load)
   u32x4 pfl2;             // ... and of column pf_col + 1 (two columns in flight)
   int pf_col2;
 #else
+  void refresh_lane() {}
   TopCtx pf;
   u32x4 pf1[3];           // the prefetched column's list-1 context (bframes)
 #endif
@@ -511,7 +520,7 @@ struct Parser {
   // 2, 3, 7; the intra level; list-1 record u32x4 0, 1, 7), so the prefetch
   // lives in one VGPR quad per lane instead of 29 scalar registers
   __device__ VTS_INLINE u32x4 piece_load(int col) const {
-    const int l = static_cast<int>(threadIdx.x);
+    const int l = lane_;
     const int n = cur_addr - mbw + (col - cur_addr % mbw);
     u32x4 v = {0u, 0u, 0u, 0u};
     if (l < 4) v = reinterpret_cast<const u32x4 *>(recs + n)[l == 3 ? 7 : l + 1];
@@ -520,7 +529,7 @@ struct Parser {
     return v;
   }
   __device__ VTS_INLINE void piece_store(int col, u32x4 v) const {
-    const int l = static_cast<int>(threadIdx.x);
+    const int l = lane_;
     if (l < 4) reinterpret_cast<u32x4 *>(&sc->top[col % 3])[l == 3 ? 7 : l + 1] = v;
     else if (l == 4) sc->top[col % 3].epoch = v[0];
     else if (l < 8 && bframes) reinterpret_cast<u32x4 *>(&sc->top1[col % 3])[l == 7 ? 7 : l - 5] = v;
@@ -953,7 +962,7 @@ struct Parser {
 #if defined(__HIP_DEVICE_COMPILE__)
     // the colocated block's motion (global memory) requested before the
     // neighbours' (LDS) so its latency overlaps the spatial predictor
-    const int lb = static_cast<int>(threadIdx.x) & 15;
+    const int lb = lane_ & 15;
     const int lcb = direct8x8 ? ((lb >> 3) * 3) * 4 + ((lb & 3) >> 1) * 3 : lb;
     const int lc8 = (lcb >> 3) * 2 + ((lcb & 3) >> 1);
     const int8_t c_ref0 = cm.ref[lc8], c_ref1 = cm1.ref1[lc8];
@@ -1442,6 +1451,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *rbsp, int32_t rbsp_le
   if (last < 0) return DEC_E_SYNTAX;
   const int64_t stop_bit = int64_t(last) * 8 + (7 - __builtin_ctz(static_cast<uint32_t>(rbsp[last])));
   p.br.init(rbsp, rbsp_len, sc->cache);
+  p.refresh_lane();
   p.br.reset_at(s.data_bit);
   p.todo = 0;
   p.cur_i16 = false;
@@ -1454,6 +1464,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_full(const uint8_t *rbsp, int32_t rbsp_le
   int state = s.is_p ? kRun : kHeader;
   if (addr >= nmb) p.err |= DEC_E_SYNTAX;
   while (!p.err) {
+    p.refresh_lane();
     bool finish = false;  // the current macroblock is complete
     if (state == kBlock) {
       if (!p.block_step(addr)) break;
