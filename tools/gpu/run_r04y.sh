@@ -1,0 +1,40 @@
+# Round 4: deblocking wavefront with a one-macroblock lag between rows (kLag1:
+# a row waits for the row above's vertical pass of the macroblock above-right,
+# published mid-step).  General parity suite first; then a same-box A/B against
+# the previous kernel (tools/exp/lib_prev.so); then the full GPU suite, smoke,
+# the default bench line with its rocprofv3 summaries and a kernel trace of the
+# content stream.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${TAG:-r04y}
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_full_gpu.py tests/test_recon_groups_gpu.py > $O/pytest_general.log 2>&1 || { tail -30 $O/pytest_general.log; exit 1; }
+tail -1 $O/pytest_general.log
+timeout -k 10 300 python - <<'PY' || exit 1
+import sys; sys.path.insert(0, "video-transformer_amd")
+from concurrent.futures import ThreadPoolExecutor
+from vtseg import scene
+kw = dict(width=1280, height=720, fps=30, n_frames=18000, seed=0x5EED, coding="full", slices_per_row=0, max_motion=4,
+          bframes=True, weighted="implicit", cabac=True, transform_8x8=True)
+with ThreadPoolExecutor(2) as ex:
+    a = ex.submit(scene.synth_write, "/tmp/gcab.mp4", **kw)
+    b = ex.submit(scene.synth_write, "/tmp/gcontent.mp4", content=True, gop_max_s=8.0, **kw)
+    a.result(); b.result()
+print("streams written", flush=True)
+PY
+for V in gcontent gcab; do
+  PASSES=1 bash tools/gpu/lib_ab.sh /tmp/$V.mp4 3 $O/$V cur prev || exit 1
+done
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/kt_gcontent" -o run -- python3 "$GRAFT_REPO_ROOT/tools/gpu/env_ab.py" /tmp/gcontent.mp4 1 x= > "$GRAFT_REPO_ROOT/$O/kt_gcontent.log" 2>&1) || { tail -30 $O/kt_gcontent.log; exit 1; }
+echo traced
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
+cat $O/smoke.txt
+timeout -k 10 800 python -u bench.py --profile-dir $O/prof > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+python -c "
+import json; d=json.load(open('$O/bench.json'))
+print('bench', d['value'], d['roofline']['frac'], d['parity']['all_equal'], d['e2e']['value'])
+for k in ('general', 'general_content', 'long_video'):
+    r = d.get(k, {}); print(k, r.get('value'), r.get('stage_ms'), r.get('open_s'), r.get('windows'), r.get('cuts'), r.get('bits_per_frame'), (r.get('parity') or {}).get('all_equal'))
+"

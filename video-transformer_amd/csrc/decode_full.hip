@@ -1743,54 +1743,6 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a
 constexpr int kDbkRingRows = 2 * kDbkWaves;
 constexpr int kDbkRingCols = 32;
 
-__device__ __forceinline__ void filt_luma_w(int (&s)[8], int bS, uint32_t w) {
-  const int alpha = w & 255, beta = (w >> 8) & 255;
-  const int p0 = s[3], p1 = s[2], q0 = s[4], q1 = s[5];
-  if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-  const int p2 = s[1], q2 = s[6];
-  const int ap = abs(p2 - p0), aq = abs(q2 - q0);
-  if (bS < 4) {
-    const int tc0 = (w >> (11 + 5 * bS)) & 31;
-    const int tc = tc0 + (ap < beta) + (aq < beta);
-    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
-    s[3] = c255(p0 + delta);
-    s[4] = c255(q0 - delta);
-    if (ap < beta) s[2] = p1 + min(max((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0), tc0);
-    if (aq < beta) s[5] = q1 + min(max((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0), tc0);
-    return;
-  }
-  const int p3 = s[0], q3 = s[7];
-  const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
-  if (ap < beta && small) {
-    s[3] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
-    s[2] = (p2 + p1 + p0 + q0 + 2) >> 2;
-    s[1] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
-  } else {
-    s[3] = (2 * p1 + p0 + q1 + 2) >> 2;
-  }
-  if (aq < beta && small) {
-    s[4] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
-    s[5] = (p0 + q0 + q1 + q2 + 2) >> 2;
-    s[6] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-  } else {
-    s[4] = (2 * q1 + q0 + p1 + 2) >> 2;
-  }
-}
-__device__ __forceinline__ void filt_chroma_w(int &p1, int &p0, int &q0, int &q1, int bS, uint32_t w) {
-  const int alpha = w & 255, beta = (w >> 8) & 255;
-  if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-  if (bS < 4) {
-    const int tc = ((w >> (11 + 5 * bS)) & 31) + 1;
-    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
-    const int np0 = c255(p0 + delta), nq0 = c255(q0 - delta);
-    p0 = np0;
-    q0 = nq0;
-    return;
-  }
-  const int np0 = (2 * p1 + p0 + q1 + 2) >> 2, nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
-  p0 = np0;
-  q0 = nq0;
-}
 __device__ __forceinline__ uint32_t u4_at(const uint4 &v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
@@ -1953,8 +1905,6 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       RPROF(0);
-      const uint32_t ybase = static_cast<uint32_t>(yrow) + static_cast<uint32_t>(x * 16);
-      const uint32_t cbase = uvo + static_cast<uint32_t>(crow) + static_cast<uint32_t>(x * 16);
       // a macroblock none of whose edges (left, top, inside) filters keeps its
       // samples: its step skips both passes and writes back what it loaded
       const bool still = (bsw.x | bsw.y | bsw.z | bsw.w) == 0u;
@@ -2080,10 +2030,17 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a)
             if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = left;
           }
         } else if (l < 28 && y > 0) {
-          const int i = l - 24;  // luma rows -3..-1, chroma row -1 of the macroblock above
-          const uint4 v = i < 3 ? *reinterpret_cast<const uint4 *>(&t.y[1 + i][4]) : *reinterpret_cast<const uint4 *>(&t.c[1][4]);
-          if (i < 3) *reinterpret_cast<uint4 *>(at(ybase + static_cast<uint32_t>((i - 3) * pitch))) = v;
-          else *reinterpret_cast<uint4 *>(at(cbase - static_cast<uint32_t>(pitch))) = v;
+          // luma rows -3..-1, chroma row -1 of the macroblock above; the lane
+          // index opaque here, so the tile and row offsets are computed per
+          // step rather than kept per row (spilled, and each reload waited for
+          // every load and store in flight)
+          int lo = lane;
+          asm volatile("" : "+v"(lo));
+          const int i = (lo & 31) - 24, hf = lo >> 5, yy = min(2 * p + hf, mbh - 1);
+          const DbkTile &tt = tiles[__builtin_amdgcn_readfirstlane(wave) * 2 + hf];
+          const uint4 v = i < 3 ? *reinterpret_cast<const uint4 *>(&tt.y[1 + i][4]) : *reinterpret_cast<const uint4 *>(&tt.c[1][4]);
+          const uint32_t o = i < 3 ? static_cast<uint32_t>((yy * 16 + i - 3) * pitch) : uvo + static_cast<uint32_t>((yy * 8 - 1) * pitch);
+          *reinterpret_cast<uint4 *>(at(o + static_cast<uint32_t>(x * 16))) = v;
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
