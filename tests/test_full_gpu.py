@@ -278,6 +278,36 @@ def test_gop_groups_on_streams_equal_the_oracle(tmp_path, monkeypatch, groups, b
             assert np.array_equal(res.scores, ref["score"])
 
 
+@pytest.mark.parametrize("bs", ["0", "1", "2"], ids=["head", "inter", "paced"])
+@pytest.mark.parametrize("groups", [1, 2])
+def test_bs_schedules_equal_the_oracle(tmp_path, monkeypatch, bs, groups):
+    """Where the deblocking descriptors are derived (VTS_BS: one window-wide
+    launch at the head of the level chain, inside each level's inter launch,
+    or one launch per level on the score stream paced by the chain) does not
+    change a sample: every frame, histogram, SAD and score equals the oracle,
+    in one window and in several windows (where the score stream also scores
+    the window before)."""
+    _require_gpu()
+    monkeypatch.setenv("VTS_BS", bs)
+    monkeypatch.setenv("VTS_GENERAL_GROUPS", str(groups))
+    n = 120
+    path = tmp_path / "bs.mp4"
+    scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=True, weighted="implicit",
+                      cabac=True, transform_8x8=True, cut_min_s=0.5, cut_max_s=1.5, gop_max_s=0.4, seed=23)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
+    for wf in (0, 60):
+        with scene.VideoScorer(path, keep_frames=wf == 0, window_frames=wf, n_streams=2) as v:
+            assert v.general()
+            res = v.score()
+            if wf == 0:
+                got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+                assert _first_diff(got, frames) == []
+            assert np.array_equal(res.hist, ref["hist"])
+            assert np.array_equal(res.sad, ref["sad"])
+            assert np.array_equal(res.scores, ref["score"])
+
+
 def test_chroma_only_deblocking_goes_to_the_general_decoder(tmp_path):
     """A subset-syntax stream whose deblocking filter is active on chroma
     edges only (QPY 3, chroma_qp_index_offset 12, filter offsets +12: luma
