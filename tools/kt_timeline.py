@@ -9,7 +9,8 @@ import json
 import sys
 from collections import defaultdict
 
-RECON = ("h264_inter_full", "h264_intra_v2", "h264_intra_full", "h264_bs_full", "h264_deblock_lds", "h264_deblock_full")
+RECON = ("h264_inter_full", "h264_intra_v2", "h264_intra_full", "h264_bs_full", "h264_deblock_lds", "h264_deblock_full",
+         "h264_deblock_plane")
 
 
 def short(name):

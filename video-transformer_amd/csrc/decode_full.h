@@ -71,7 +71,8 @@ struct FullReconArgs {
   int64_t uv_off;            // UV plane offset in a picture (pitch * coded height)
   int32_t pitch;
   uint32_t epoch;
-  int32_t deblock;           // deblocking kernel after reconstruction: 0 none, 1 h264_deblock_full, 2 h264_deblock_lds
+  int32_t deblock;           // deblocking kernel after reconstruction: 0 none, 1 h264_deblock_full, 2 h264_deblock_lds,
+                             // 3 h264_deblock_plane
   int32_t intra_kernel;      // 1: h264_intra_full, else h264_intra_v2 (where its LDS fits)
   int32_t dbk_bands;         // h264_deblock_lds: workgroups per picture (bands of row pairs), 1..4
   int32_t bs_fused;          // 1: h264_inter_full derives the level's bS (DbkInfo) after its blocks; 0: h264_bs_full does

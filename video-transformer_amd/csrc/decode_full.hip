@@ -26,6 +26,8 @@
 // runs against the oracle.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "decode_full.h"
 #ifdef VTS_EXP_PROF
@@ -2096,6 +2098,286 @@ int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
   return VTS_OK;
 }
 
+// ------------------------------------------------ deblocking by plane
+// Luma and chroma deblock independently (they share only the bS words), and
+// each needs 16 lanes per macroblock row instead of 32: one workgroup per
+// (picture, plane) holds kDpGroups = 64 macroblock rows in flight (16 waves x
+// 4 groups of 16 lanes), so a 720p / 1080p picture is one pass of the
+// wavefront (h264_deblock_lds holds 32 rows: a 720p picture's rows 32..44
+// waited for the first pass to free a wave).  Same step as h264_deblock_lds
+// per plane: rows above from the ring, vertical pass (lane = sample row),
+// horizontal pass (lane = sample column), write-back (rows the row below
+// finishes excepted), ring lines for the row below; the four rows of a wave
+// run in lockstep two macroblocks apart, a wave's first row waits for the
+// previous wave's last through prog[].
+constexpr int kDpGroups = kDbkThreads / 16;
+constexpr int kDpRingCols = 16;
+struct DpTileY {
+  uint8_t s[20][20];  // rows -4..15 x cols -4..15
+};
+struct DpTileC {
+  uint8_t s[10][20];  // chroma rows -2..7 x interleaved bytes -4..15
+};
+struct DpLineY {
+  uint8_t s[4][16];  // rows 12..15
+};
+struct DpLineC {
+  uint8_t s[2][16];  // chroma rows 6..7
+};
+constexpr size_t kDpLdsY = sizeof(DpTileY) * kDpGroups + sizeof(DpLineY) * kDpGroups * kDpRingCols;
+constexpr size_t kDpLdsC = sizeof(DpTileC) * kDpGroups + sizeof(DpLineC) * kDpGroups * kDpRingCols;
+constexpr size_t kDpLds = kDpLdsY > kDpLdsC ? kDpLdsY : kDpLdsC;
+
+// kLag1: a row runs one macroblock behind the row above instead of two: its
+// horizontal pass waits only for the row above's vertical pass of the
+// macroblock above-right (the last change to the samples above it), which
+// the row above publishes mid-step in vprog[] after writing the left
+// macroblock's final cols 12..15 into its ring line
+template <bool kLuma, bool kLag1>
+__device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_t *lds, int *prog, int *vprog) {
+  using Tile = typename std::conditional<kLuma, DpTileY, DpTileC>::type;
+  using Line = typename std::conditional<kLuma, DpLineY, DpLineC>::type;
+  Tile *tiles = reinterpret_cast<Tile *>(lds);
+  Line(*ring)[kDpRingCols] = reinterpret_cast<Line(*)[kDpRingCols]>(lds + sizeof(Tile) * kDpGroups);
+  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
+  const int slot = a.frames[pic].x;
+  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
+  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
+  const uint32_t uvo = static_cast<uint32_t>(a.uv_off);
+  auto at = [Y](uint32_t o) { return Y + static_cast<uint64_t>(o); };
+  const int pitch = a.pitch;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane >> 4, l = lane & 15;
+  constexpr int kRows = kLuma ? 16 : 8;  // sample rows of a macroblock
+  constexpr int kTop = kLuma ? 4 : 2;     // tile rows above the macroblock (kept in the ring lines)
+  const bool lrow = l < kRows;           // vertical pass / write-back lane
+  const int row = kLuma ? l : min(l, 7);
+  Tile &t = tiles[wave * 4 + grp];
+  constexpr int vq = kLuma ? 2 : 4, hq = kLuma ? 3 : 5;
+  for (int p = wave; 4 * p < mbh; p += kDbkWaves) {
+    const int y = 4 * p + grp;
+    const bool row_ok = y < mbh;
+    const int ya = row_ok ? y : mbh - 1;
+    const bool last_row = y == mbh - 1;
+    const int rs = y % kDpGroups, rsa = (y + kDpGroups - 1) % kDpGroups;
+    const uint32_t rowo = kLuma ? static_cast<uint32_t>((ya * 16 + row) * pitch)
+                                : uvo + static_cast<uint32_t>((ya * 8 + row) * pitch);
+    const DbkInfo *const drow = fdbk + ya * mbw;
+    // this row's ring slot was the row kDpGroups above's: its consumer must be done
+    if (row_ok && y - kDpGroups >= 0) {
+      while (__hip_atomic_load(&prog[y - kDpGroups + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < mbw + 1)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    uint32_t left = 0;  // carried cols 12..15 of the previous macroblock (this lane's row)
+    const uint4 *dq = reinterpret_cast<const uint4 *>(drow);
+    uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
+    uint4 npx = *reinterpret_cast<const uint4 *>(at(rowo));
+    constexpr int kLag = kLag1 ? 1 : 2;
+    for (int it = 0; it < mbw + 3 * kLag; ++it) {
+      const int x = it - kLag * grp;
+      const bool act = row_ok && x >= 0 && x < mbw;
+      const uint4 bsw = nbs, pv = nv, ph = nh, q4 = npx;
+      {
+        const int xn = min(max(x + 1, 0), mbw - 1);
+        const uint4 *dn = reinterpret_cast<const uint4 *>(drow + xn);
+        nbs = dn[0];
+        nv = dn[vq];
+        nh = dn[hq];
+        npx = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xn * 16)));
+      }
+      // a wave's first row waits for the previous wave's last row; its last
+      // row waits until it may overwrite ring column x (the next wave's first
+      // row read column x - kDpRingCols)
+      if (act) {
+        const int need_up = (!kLag1 && grp == 0 && y > 0) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
+        const int need_dn = (grp == 3 && y + 1 < mbh) ? x - kDpRingCols + 1 : -(1 << 30);
+        const int *pu = &prog[y > 0 ? y - 1 : 0], *pd = &prog[y + 1 < mbh ? y + 1 : y];
+        while (__hip_atomic_load(pu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_up ||
+               __hip_atomic_load(pd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_dn)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const bool still = (bsw.x | bsw.y | bsw.z | bsw.w) == 0u;
+      constexpr int kAbove = kLuma ? 4 : 2;  // rows above from the ring
+      auto load_above = [&]() {
+        if (act && l < kAbove && y > 0) {
+          const Line &L = ring[rsa][x & (kDpRingCols - 1)];
+          *reinterpret_cast<uint4 *>(&t.s[l][4]) = *reinterpret_cast<const uint4 *>(&L.s[l][0]);
+        }
+      };
+      if (!kLag1) load_above();
+      // ---- vertical edges: lane = sample row
+      if (act && lrow && !still) {
+        const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
+        int r[20], u[20];
+#pragma unroll
+        for (int i = 0; i < 20; ++i) r[i] = (wv[i >> 2] >> ((i & 3) * 8)) & 255;
+#pragma unroll
+        for (int j = 0; j < 20; ++j) u[j] = kLuma ? r[j] : r[kDbkCPerm[j]];
+        const int seg = kLuma ? row >> 2 : row >> 1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int bS = (u4_at(bsw, e >> 1) >> (((kLuma ? (e & 1) : 0) * 4 + seg) * 4)) & 15;
+          if (!bS) continue;
+          int s8[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
+          filt_w(s8, bS, u4_at(pv, e), !kLuma);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 20; ++i) r[i] = kLuma ? u[i] : u[kDbkCInv[i]];
+        uint8_t *dst = &t.s[kTop + row][0];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+          *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+      }
+      lane_sync();
+      if constexpr (kLag1) {
+        // the left macroblock's cols 12..15 are final now: rows 12..15 (chroma
+        // 6..7) of them complete its ring line for the row below
+        const int lr = row - (kRows - kTop);
+        if (act && lrow && !last_row && x > 0 && lr >= 0) {
+          const uint32_t w0 = still ? left : *reinterpret_cast<const uint32_t *>(&t.s[kTop + row][0]);
+          *reinterpret_cast<uint32_t *>(&ring[rs][(x - 1) & (kDpRingCols - 1)].s[lr][12]) = w0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        if (act && l == 0 && !last_row)
+          __hip_atomic_store(&vprog[y], x, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // a wave's first row waits for the previous wave's last row to have
+        // filtered the vertical edges of macroblock x + 1 (the other rows'
+        // row above is the group before, one macroblock ahead in lockstep)
+        if (act && grp == 0 && y > 0) {
+          const int need = x + 1 < mbw ? x + 1 : mbw + 1;
+          while (__hip_atomic_load(&vprog[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        load_above();
+        lane_sync();
+      }
+      // ---- horizontal edges: lane = sample column (chroma: interleaved byte column)
+      if (act && !still) {
+        const int pl = l & 1, seg = l >> 2;
+        int u[20];
+        if constexpr (kLuma) {
+          const uint8_t *col = &t.s[0][4 + l];
+#pragma unroll
+          for (int i = 0; i < 20; ++i) u[i] = col[i * 20];
+        } else {
+          const uint8_t *col = &t.s[0][4 + l];
+#pragma unroll
+          for (int i = 0; i < 20; ++i) {
+            const int cr = dbk_hrow(i);
+            u[i] = cr >= 0 ? col[cr * 20] : 0;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int bS = (u4_at(bsw, 2 + (e >> 1)) >> (((kLuma ? (e & 1) : 0) * 4 + seg) * 4)) & 15;
+          if (!kLuma && (e & 1)) bS = 0;
+          if (!bS) continue;
+          int s8[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
+          filt_w(s8, bS, u4_at(ph, kLuma ? e : e + pl), !kLuma);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
+        }
+        if constexpr (kLuma) {
+          uint8_t *col = &t.s[0][4 + l];
+#pragma unroll
+          for (int i = 1; i < 20; ++i) col[i * 20] = static_cast<uint8_t>(u[i]);
+        } else {
+          uint8_t *col = &t.s[0][4 + l];
+#pragma unroll
+          for (int i = 1; i < 20; ++i) {
+            const int cr = dbk_hrow(i);
+            if (cr >= 1) col[cr * 20] = static_cast<uint8_t>(u[i]);
+          }
+        }
+      }
+      lane_sync();
+      // ---- write back: this macroblock's rows shifted 4 bytes left except the
+      // ones the row below finishes (luma 13..15, chroma 7), the ring lines for
+      // the row below, the rows above that this macroblock's top edge finished
+      if (act) {
+        if (lrow) {
+          uint32_t w0, w1, w2, w3;
+          if (still) {
+            w0 = left;
+            w1 = q4.x;
+            w2 = q4.y;
+            w3 = q4.z;
+            left = q4.w;
+          } else {
+            const uint8_t *src = &t.s[kTop + row][0];
+            w0 = *reinterpret_cast<const uint32_t *>(src);
+            w1 = *reinterpret_cast<const uint32_t *>(src + 4);
+            w2 = *reinterpret_cast<const uint32_t *>(src + 8);
+            w3 = *reinterpret_cast<const uint32_t *>(src + 12);
+            left = *reinterpret_cast<const uint32_t *>(src + 16);
+          }
+          if (last_row || row < (kLuma ? 13 : 7)) {
+            uint8_t *dst = at(rowo + static_cast<uint32_t>(x * 16));
+            if (x > 0) *reinterpret_cast<uint32_t *>(dst - 4) = w0;
+            *reinterpret_cast<uint32_t *>(dst) = w1;
+            *reinterpret_cast<uint32_t *>(dst + 4) = w2;
+            *reinterpret_cast<uint32_t *>(dst + 8) = w3;
+            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
+          }
+          const int lr = row - (kRows - kTop);  // ring line of this lane's row (luma 12..15, chroma 6..7)
+          if (!last_row && lr >= 0) {
+            Line &C = ring[rs][x & (kDpRingCols - 1)];
+            uint8_t *cur = &C.s[lr][0];
+            if (!kLag1 && x > 0) *reinterpret_cast<uint32_t *>(&ring[rs][(x - 1) & (kDpRingCols - 1)].s[lr][12]) = w0;
+            *reinterpret_cast<uint32_t *>(cur) = w1;
+            *reinterpret_cast<uint32_t *>(cur + 4) = w2;
+            *reinterpret_cast<uint32_t *>(cur + 8) = w3;
+            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = left;
+          }
+        }
+        // luma rows -3..-1 / chroma row -1 of the macroblock above (lane index
+        // opaque: the offsets computed per step, not kept per row)
+        if (l < (kLuma ? 3 : 1) && y > 0) {
+          int lo = lane;
+          asm volatile("" : "+v"(lo));
+          const int i = lo & 15, g = lo >> 4, yy = min(4 * p + g, mbh - 1);
+          const Tile &tt = tiles[__builtin_amdgcn_readfirstlane(wave) * 4 + g];
+          // luma: tile row 1 + i (rows -3..-1); chroma: tile row 1 (row -1)
+          const uint4 v = *reinterpret_cast<const uint4 *>(&tt.s[1 + i][4]);
+          const uint32_t o = kLuma ? static_cast<uint32_t>((yy * 16 + i - 3) * pitch)
+                                   : uvo + static_cast<uint32_t>((yy * 8 - 1) * pitch);
+          *reinterpret_cast<uint4 *>(at(o + static_cast<uint32_t>(x * 16))) = v;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      if (act && l == 0) {
+        __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (kLag1 && x == mbw - 1 && !last_row)  // the last macroblock's line is whole after the write-back
+          __hip_atomic_store(&vprog[y], mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+}
+// grid: 2 x pictures of the level (even blocks luma, odd chroma)
+template <bool kLag1>
+__global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kDpLds];
+  __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
+  __shared__ int vprog[kLag1 ? 1024 : 1];  // kLag1: per row, the macroblock whose vertical pass is done
+  for (int i = threadIdx.x; i < a.P.mb_height; i += kDbkThreads) {
+    prog[i] = 0;
+    if (kLag1) vprog[i] = 0;
+  }
+  __syncthreads();
+  if ((blockIdx.x & 1) == 0) dp_plane<true, kLag1>(a, static_cast<int>(blockIdx.x >> 1), lds, prog, vprog);
+  else dp_plane<false, kLag1>(a, static_cast<int>(blockIdx.x >> 1), lds, prog, vprog);
+}
+
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
   if (n_frames > 65535) return fail(VTS_E_UNSUPPORTED, "more than 65535 pictures in one bS launch");
@@ -2126,7 +2408,12 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s, hipEv
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_intra_full launch: %s", hipGetErrorString(e));
   }
-  if (a.deblock == 1) {
+  if (a.deblock >= 3) {
+    if (a.deblock == 4) hipLaunchKernelGGL(h264_deblock_plane<true>, dim3(2 * n_frames), dim3(kDbkThreads), 0, s, a);
+    else hipLaunchKernelGGL(h264_deblock_plane<false>, dim3(2 * n_frames), dim3(kDbkThreads), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_plane launch: %s", hipGetErrorString(e));
+  } else if (a.deblock == 1) {
     hipLaunchKernelGGL(h264_deblock_full, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));

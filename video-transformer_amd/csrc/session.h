@@ -187,7 +187,7 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
-  int dbk_kernel = 2;                   // 2: h264_deblock_lds; VTS_DBK=1: h264_deblock_full
+  int dbk_kernel = 3;                   // 3: h264_deblock_plane; VTS_DBK=2: h264_deblock_lds, 1: h264_deblock_full
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full
   int dbk_bands = 1;                    // h264_deblock_lds workgroups per picture (VTS_DBK_BANDS, 1..4)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level

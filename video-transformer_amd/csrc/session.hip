@@ -257,7 +257,7 @@ int alloc_general(vts_ctx *c) {
   if (!c->pneed.empty())
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
   if (const char *e = std::getenv("VTS_PARSE_MERGE")) c->parse_merged = std::atoi(e) != 0;
-  if (const char *e = std::getenv("VTS_DBK")) c->dbk_kernel = std::atoi(e) == 1 ? 1 : 2;
+  if (const char *e = std::getenv("VTS_DBK")) c->dbk_kernel = std::min(4, std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("VTS_INTRA")) c->intra_kernel = std::atoi(e) == 1 ? 1 : 2;
   if (const char *e = std::getenv("VTS_DBK_BANDS")) c->dbk_bands = std::min(4, std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("VTS_BS")) c->bs_mode = std::min(2, std::max(0, std::atoi(e)));
