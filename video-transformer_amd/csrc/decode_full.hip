@@ -2168,7 +2168,8 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
       while (__hip_atomic_load(&prog[y - kDpGroups + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < mbw + 1)
         __builtin_amdgcn_s_sleep(1);
     }
-    uint32_t left = 0;  // carried cols 12..15 of the previous macroblock (this lane's row)
+    uint32_t left = 0;   // carried cols 12..15 of the previous macroblock (this lane's row)
+    bool ldirty = false;  // ... and they differ from what HBM holds (that macroblock was filtered)
     const uint4 *dq = reinterpret_cast<const uint4 *>(drow);
     uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
     uint4 npx = *reinterpret_cast<const uint4 *>(at(rowo));
@@ -2320,14 +2321,20 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
             w3 = *reinterpret_cast<const uint32_t *>(src + 12);
             left = *reinterpret_cast<const uint32_t *>(src + 16);
           }
+          // a still macroblock's own samples are what HBM holds (only this
+          // step writes its rows 0..12 / 0..6): stored are the left
+          // neighbour's last columns when that one was filtered
           if (last_row || row < (kLuma ? 13 : 7)) {
             uint8_t *dst = at(rowo + static_cast<uint32_t>(x * 16));
-            if (x > 0) *reinterpret_cast<uint32_t *>(dst - 4) = w0;
-            *reinterpret_cast<uint32_t *>(dst) = w1;
-            *reinterpret_cast<uint32_t *>(dst + 4) = w2;
-            *reinterpret_cast<uint32_t *>(dst + 8) = w3;
-            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
+            if (x > 0 && (!still || ldirty)) *reinterpret_cast<uint32_t *>(dst - 4) = w0;
+            if (!still) {
+              *reinterpret_cast<uint32_t *>(dst) = w1;
+              *reinterpret_cast<uint32_t *>(dst + 4) = w2;
+              *reinterpret_cast<uint32_t *>(dst + 8) = w3;
+              if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
+            }
           }
+          ldirty = !still;
           const int lr = row - (kRows - kTop);  // ring line of this lane's row (luma 12..15, chroma 6..7)
           if (!last_row && lr >= 0) {
             Line &C = ring[rs][x & (kDpRingCols - 1)];
