@@ -93,6 +93,7 @@ CONFIGS = {
     "480p-60s": (640, 480, 1800, 1, "BASELINE config [0] clip (60-s 480p) on the GPU path"),
 }
 FPS = 30
+HD_FRAMES = 54000  # the N = 1 line's 1080p record: a 30-min sample of config [4]'s 2-h video
 METRIC = "720p frames/sec decoded+scored per node; segment-index exact-match vs CPU"
 # the reference's default analyzer config (config/config.yaml:84-96)
 REF_CONFIG = {"analyzer": {"max_continuations": 3, "retry_times": 5,
@@ -135,6 +136,23 @@ def tb_bytes_per_launch(width: int, height: int, k: int, frames: int, chains: in
     per_chain = nv12 + (0 if keep else nv12) + w * h
     per_frame = 3 * w * h + w * h + 1024 + 8 + (nv12 if keep else 0)
     return (chains * per_chain + frames * per_frame) / launches
+
+
+def host_cores() -> dict:
+    """The host cores this process may use: the scheduler affinity set
+    (os.sched_getaffinity) and, when the cgroup caps CPU time (cgroup v2
+    cpu.max "quota period"), that cap in whole cores.  The CPU baseline runs
+    one oracle thread per usable core: all affinity cores, unless the cgroup
+    quota grants fewer (more threads than the quota only time-slice)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        quota = None
+    return {"affinity": aff, "cgroup_quota": quota, "usable": min(aff, quota) if quota else aff}
 
 
 def smooth_frames_host(rng, n, width, height):
@@ -804,8 +822,10 @@ def main() -> None:
     k = 4 if height <= 720 else 6
     w, h = width // k, height // k
     stride = width * height * 3 // 2
-    aff = len(os.sched_getaffinity(0))
-    threads = max(1, min(16, aff // max(1, world)))
+    hc = host_cores()
+    # N = 1: the oracle (parity pass = CPU baseline) on every usable host core;
+    # N > 1: each rank's share of them (the parity pass only, no baseline)
+    threads = max(1, hc["usable"] // max(1, world))
     extras = args.extras == "all" and world == 1 and args.workload == "decode_score" and \
         not args.no_parity
 
@@ -834,20 +854,23 @@ def main() -> None:
     local_paths = [all_paths[i] for i in local_idx]
 
     # extras' inputs, written before the profile passes (which read them)
-    gen_path = long_path = content_path = None
+    gen_path = long_path = content_path = hd_path = None
     gen_info = content_info = None
     if extras:
         t0 = time.perf_counter()
         gen_path = tmpdir / "general_720p_10min.mp4"
         content_path = tmpdir / "general_content_720p_10min.mp4"
         long_path = tmpdir / "long_720p_2h.mp4"
-        with ThreadPoolExecutor(3) as ex:
+        hd_path = tmpdir / "hd_1080p_30min.mp4"
+        with ThreadPoolExecutor(4) as ex:
             fa = ex.submit(synth_videos, [(gen_path, 0x5EED)], 1280, 720, 18000, "full", True, True)
             fc = ex.submit(synth_videos, [(content_path, 0x5EED)], 1280, 720, 18000, "full", True, True, True)
             fb = ex.submit(synth_videos, [(long_path, 0x5EED)], 1280, 720, 216000)
+            fd = ex.submit(synth_videos, [(hd_path, 0x5EED)], 1920, 1080, HD_FRAMES)
             gen_info = fa.result()[0]
             content_info = fc.result()[0]
             fb.result()
+            fd.result()
         log(f"extras inputs written in {time.perf_counter() - t0:.1f} s")
 
     prof = gprof = None
@@ -1070,12 +1093,14 @@ def main() -> None:
             parity["checked_on_each_rank"] = f"{len(per_video)} videos x {nfr // max(1, len(per_video))} frames"
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = {"value": round(nfr / secs, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+                   "host_cores": hc,
                    "sample": f"the parity pass: {nfr} frames ({width}x{height}, {len(per_video)} "
                              f"videos) of the benchmark batch decoded by " +
                              ("oracle/h264_full_oracle.c fo_decode" if dec == "full" else
                               "oracle/vtseg_oracle.c or_decode_samples") +
                              f" + scored by or_score_frames, GOP-parallel on {threads} "
-                             f"threads, {secs:.1f} s"}
+                             f"threads = every usable host core (affinity {hc['affinity']}, cgroup "
+                             f"quota {hc['cgroup_quota'] or 'none'}), {secs:.1f} s"}
         log(f"rank {rank}: parity all_equal={parity['all_equal']}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu is None:
         if args.workload == "score":
@@ -1111,10 +1136,14 @@ def main() -> None:
                                                   "CABAC, 8x8 transform, B pyramid, implicit weights, "
                                                   "deblocking, keyint ~8 s)", content_info),
                 ("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
-                                          "(216 000 frames), streamed two-ring decode", None)):
+                                          "(216 000 frames), streamed two-ring decode", None),
+                ("hd_1080p", hd_path, f"BASELINE config [4] per-GPU share, sampled: one 1080p video of "
+                                      f"{HD_FRAMES / FPS / 60:.0f} min ({HD_FRAMES} frames; config [4] is 2 h "
+                                      f"per GPU), coded 1920x1088 with display crop, thumbnails k=6, "
+                                      f"streamed decode", None)):
             try:
-                r = run_single(p, gpu=gpu, k=4, steps=3, threads=threads, label=label,
-                               planted=info["cuts"] if info else None)
+                r = run_single(p, gpu=gpu, k=6 if key == "hd_1080p" else 4, steps=3, threads=threads,
+                               label=label, planted=info["cuts"] if info else None)
                 if gprof and gprof.get(key):
                     r["kernels"] = general_kernel_rooflines(gprof[key], 1280, 720, 4, r["frames"],
                                                             80 * 45)
@@ -1166,7 +1195,7 @@ def main() -> None:
     if not args.video:
         shutil.rmtree(tmpdir, ignore_errors=True)
     else:
-        for p in (gen_path, long_path):
+        for p in (gen_path, long_path, content_path, hd_path):
             if p is not None:
                 Path(p).unlink(missing_ok=True)
     if world > 1:

@@ -278,17 +278,14 @@ def test_gop_groups_on_streams_equal_the_oracle(tmp_path, monkeypatch, groups, b
             assert np.array_equal(res.scores, ref["score"])
 
 
-@pytest.mark.parametrize("bs", ["0", "1", "2"], ids=["head", "inter", "paced"])
 @pytest.mark.parametrize("groups", [1, 2])
-def test_bs_schedules_equal_the_oracle(tmp_path, monkeypatch, bs, groups):
-    """Where the deblocking descriptors are derived (VTS_BS: one window-wide
-    launch at the head of the level chain, inside each level's inter launch,
-    or one launch per level on the score stream paced by the chain) does not
-    change a sample: every frame, histogram, SAD and score equals the oracle,
+def test_paced_bs_equals_the_oracle(tmp_path, monkeypatch, groups):
+    """The deblocking descriptors are derived one level launch at a time on
+    the score stream, paced by the reconstruction chain: every frame,
+    histogram, SAD and score equals the oracle, with one and two GOP groups,
     in one window and in several windows (where the score stream also scores
     the window before)."""
     _require_gpu()
-    monkeypatch.setenv("VTS_BS", bs)
     monkeypatch.setenv("VTS_GENERAL_GROUPS", str(groups))
     n = 120
     path = tmp_path / "bs.mp4"

@@ -354,9 +354,6 @@ __device__ __forceinline__ uint4 finish_row(bool chroma, bool pcm, uint4 lo, uin
 // from them), or the Cb and Cr 8-byte runs of an I_PCM chroma row (3 + 3).
 // shf = byte shift | mode << 8: 0 funnel, 1 / 2 left / right edge, 3 I_PCM
 // chroma.
-#ifndef VTS_K4_ROW6
-#define VTS_K4_ROW6 0  // 1: h264_recon_score<K> rows in flight as <= 6 dwords (measured -1 %)
-#endif
 typedef uint4 uint4_a4 __attribute__((aligned(4)));
 typedef uint32_t u32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
 struct Row6 {
@@ -591,38 +588,6 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       // every aligned load is issued before any is used: 16-byte pairs for
       // luma / NV12 rows, 8-byte pairs of the planar Cb and Cr rows of I_PCM
       const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
-#if VTS_K4_ROW6
-      // rows in flight as <= 6 dwords (issue_row6: a 4-byte-aligned 16-byte
-      // load + one dword; LDS-staged I_PCM rows pass through with shift 0)
-      Row6 src[KK + HK];
-      const uint4 *blk = pcm_lds + (threadIdx.x % MB_PER_WG) * 24;
-      const bool staged = kStage && stage && pcm;
-#pragma unroll
-      for (int i = 0; i < KK + HK; ++i) {
-        if (staged) {
-          if (i < KK) {
-            const uint4 v = blk[q * KK + i];
-            src[i].w0 = v.x, src[i].w1 = v.y, src[i].w2 = v.z, src[i].w3 = v.w, src[i].w4 = 0, src[i].w5 = 0;
-            src[i].shf = 0;
-          } else {
-            const int r = q * HK + (i - KK);
-            const uint4 u = blk[16 + (r >> 1)], v = blk[20 + (r >> 1)];
-            src[i].w0 = (r & 1) ? u.z : u.x, src[i].w1 = (r & 1) ? u.w : u.y, src[i].w2 = 0;
-            src[i].w3 = (r & 1) ? v.z : v.x, src[i].w4 = (r & 1) ? v.w : v.y, src[i].w5 = 0;
-            src[i].shf = 3 << 8;
-          }
-        } else {
-          const bool ch = i >= KK;
-          issue_row6(F, pcmb, pcm, ch, ch ? q * HK + (i - KK) : q * KK + i, m, mby, mvx, mvy, src[i]);
-        }
-      }
-      uint32_t zero = 0;
-#pragma unroll
-      for (int i = 0; i < KK + HK; ++i) {
-        const uint4 v = finish_row6(i >= KK, pcm, src[i], zero);
-        if (i < KK) yr[i] = v; else cr[i - KK] = v;
-      }
-#else
       uint4 lo[KK + HK], hi[KK + HK];
       int shf[KK + HK];  // funnel shift | edge mode << 8 (1 left, 2 right)
       // LDS-staged I_PCM block (I pictures): luma row r = chunk r, Cb row r =
@@ -723,7 +688,6 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
         }
         if (i < KK) yr[i] = v; else cr[i - KK] = v;
       }
-#endif
       if (pcm && zero) errs |= pcm_rows_epb(pcmb, q, KK, HK);
     } else {
 #pragma unroll
@@ -802,197 +766,6 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
   if (errs) atomicOr(a.err, errs);
 }
 
-// h264_recon_score6: fused reconstruct + scoring for k = 6 (1080p: coded
-// 1920x1088, display 1920x1080, 320x180 thumbnails).  Six-row thumbnail
-// bands do not tile 16-row macroblocks, but 2-row pairs tile both, so a lane
-// owns two row pairs of one macroblock (luma rows 2p, 2p+1, 2p+8, 2p+9 and
-// chroma rows p, p+4; one command, 6 rows in flight like the k = 4 kernel)
-// and each pair lies in one band.  A workgroup covers 3 macroblock rows (48
-// rows = 8 bands) x 21 macroblock columns (336 pixels = 56 thumbnail
-// pixels); lanes add their partial box sums into LDS (Y, and U | V << 16),
-// then 112 threads turn the 8 x 56 pixel sums into RGB, thumbnail luma,
-// histogram and SAD.  Coded rows past the display height (1080..1087) are
-// reconstructed but not scored.
-constexpr int kK6Cols = 21, kK6Rows = 3;                 // macroblocks per workgroup
-constexpr int kK6Threads = 256;
-constexpr int kK6Lanes = kK6Cols * kK6Rows * 4;          // 252 lanes used
-constexpr int kK6Px = kK6Cols * 16 / 6;                  // thumbnail pixels per band row
-constexpr int kK6Bands = kK6Rows * 16 / 6;               // 8 bands
-
-__device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int w) {
-  // bytes [lo, hi) of a 16-byte chunk that fall in its 32-bit word w
-  const int a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
-  const uint32_t upto_b = b >= 4 ? 0xffffffffu : ((1u << (8 * b)) - 1u);
-  const uint32_t upto_a = a >= 4 ? 0xffffffffu : ((1u << (8 * a)) - 1u);
-  return upto_b & ~upto_a;
-}
-
-#ifndef VTS_K6_WAVES
-#define VTS_K6_WAVES 0
-#endif
-#ifndef VTS_K6_BAND
-#define VTS_K6_BAND 1  // h264_recon_score6b (one wave per band); 0: the LDS-sum layout
-#endif
-#if VTS_K6_WAVES
-#define VTS_K6_OCC __attribute__((amdgpu_waves_per_eu(VTS_K6_WAVES)))
-#else
-#define VTS_K6_OCC
-#endif
-__global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC __attribute__((unused)) h264_recon_score6(FusedArgs fa) {
-  constexpr int K = 6, HK = 3;
-  __shared__ uint32_t lds_y[kK6Bands * kK6Px], lds_uv[kK6Bands * kK6Px];
-  __shared__ uint32_t lds_hist[256];
-  __shared__ uint32_t red[kK6Threads / 64];
-  const ReconArgs &a = fa.r;
-  const int mbw = a.mb_width, mbh = a.mb_height, nmb = mbw * mbh;
-  const int cblocks = (mbw + kK6Cols - 1) / kK6Cols;
-  const int bid = xcd_block(blockIdx.x, gridDim.x);
-  const int fi = bid / fa.wgs_per_frame;
-  const int wb = bid - fi * fa.wgs_per_frame;
-  const int rb = wb / cblocks, cb = wb - rb * cblocks;   // 3-MB-row block, 21-MB-column block
-  const int t = threadIdx.x;
-  // (a 768-thread layout with one wave per row group on 60 consecutive
-  // macroblocks measured 34% slower: one workgroup per CU, profiles/r01_k6_layout_ab.txt)
-  const int cib = t % kK6Cols, rg = t / kK6Cols;          // column in block, row group 0..11
-  const bool lane_ok = t < kK6Lanes;
-  const int m = cb * kK6Cols + cib, mby = rb * kK6Rows + rg / 4, pp = rg % 4;
-  const bool active = lane_ok && m < mbw && mby < mbh;
-  const int4 fr = a.frames[fi];
-  const FrameRefs F = frame_refs(a, fr.y);
-  const int64_t gframe = fa.frame0 + fr.x;
-  const int64_t npx = static_cast<int64_t>(fa.w) * fa.h;
-  // command, and (finishing threads) the predecessor's thumbnail: in flight
-  // across the barrier that clears the LDS sums
-  const uint64_t c =
-      active ? current_cmd(a.cmd[static_cast<int64_t>(fr.x) * nmb + static_cast<int64_t>(mby) * mbw + m], a.epoch) : 0;
-  constexpr int kFin = kK6Px / 4;                         // finishing threads per band
-  const int fband = rb * kK6Bands + t / kFin, fpx = cb * kK6Px + (t % kFin) * 4;
-  const bool fin = t < kK6Bands * kFin && fband < fa.h && fpx < fa.w;
-  uint32_t prevw = 0;
-  if (fin && fr.z >= 0)
-    prevw = *reinterpret_cast<const uint32_t *>(fa.thumb + static_cast<int64_t>(fr.z) * npx +
-                                                static_cast<int64_t>(fband) * fa.w + fpx);
-  for (int i = t; i < kK6Bands * kK6Px; i += kK6Threads) lds_y[i] = lds_uv[i] = 0;
-  if (t < 256) lds_hist[t] = 0;
-  __syncthreads();
-  uint32_t errs = 0;
-  if (active) {
-    uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
-    uint8_t *dst_uv = dst + F.pitch * F.H;
-    // rows: 0,1 = luma 2pp, 2pp+1; 2,3 = luma 2pp+8, 2pp+9; 4,5 = chroma pp, pp+4
-    uint4 rows[6];
-    const bool pcm = (c >> 62) == 1;
-    if (fast_cmd(F, c)) {
-      const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
-      const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
-      uint4 lo[6], hi[6];
-      int shf[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-        issue_row(F, pcmb, pcm, i >= 4, i < 4 ? 2 * pp + (i & 1) + 8 * (i >> 1) : pp + 4 * (i - 4), m, mby,
-                  mvx, mvy, lo[i], hi[i], shf[i]);
-      uint32_t zero = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) rows[i] = finish_row(i >= 4, pcm, lo[i], hi[i], shf[i], zero);
-      if (pcm && zero) errs |= pcm_rows_epb(pcmb, pp, 2, 1) | pcm_rows_epb(pcmb, pp + 4, 2, 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        st_row(dst + static_cast<int64_t>(mby * 16 + 2 * pp + (i & 1) + 8 * (i >> 1)) * F.pitch + m * 16, rows[i]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        st_row(dst_uv + static_cast<int64_t>(mby * 8 + pp + 4 * i) * F.pitch + m * 16, rows[4 + i]);
-    } else {
-      // general path (sub-pel chroma, errors): rare; one row at a time
-      // (unrolled six times it cost 40 VGPRs and SGPR spills for the whole
-      // kernel), stored, then read back for scoring
-#pragma unroll 1
-      for (int i = 0; i < 6; ++i) {
-        const bool chroma = i >= 4;
-        const int r = chroma ? pp + 4 * (i - 4) : 2 * pp + (i & 1) + 8 * (i >> 1);
-        uint8_t *o = (chroma ? dst_uv + static_cast<int64_t>(mby * 8 + r) * F.pitch
-                             : dst + static_cast<int64_t>(mby * 16 + r) * F.pitch) + m * 16;
-        *reinterpret_cast<uint4 *>(o) = fetch_row(F, c, chroma ? 16 + r : r, m, mby, errs);
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const bool chroma = i >= 4;
-        const int r = chroma ? pp + 4 * (i - 4) : 2 * pp + (i & 1) + 8 * (i >> 1);
-        const uint8_t *o = (chroma ? dst_uv + static_cast<int64_t>(mby * 8 + r) * F.pitch
-                                   : dst + static_cast<int64_t>(mby * 16 + r) * F.pitch) + m * 16;
-        rows[i] = *reinterpret_cast<const uint4 *>(o);
-      }
-    }
-    // partial box sums of the (up to 4) thumbnail pixels over this lane's 16
-    // columns, per row pair: pixel p of a 48-column triple covers bytes
-    // [6p, 6p + 6) of it, luma and NV12 chroma alike
-    const int j = m % 3, p0 = j == 0 ? 0 : (j == 1 ? 2 : 5);
-    const int pcol = (cib / 3) * 8;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int band = (mby * 8 + pp + 4 * h) / 3;       // = its luma rows' band
-      if (band >= fa.h) continue;
-      const int pbase = pcol + (band - rb * kK6Bands) * kK6Px;
-      const uint32_t l0[4] = {rows[2 * h].x, rows[2 * h].y, rows[2 * h].z, rows[2 * h].w};
-      const uint32_t l1[4] = {rows[2 * h + 1].x, rows[2 * h + 1].y, rows[2 * h + 1].z, rows[2 * h + 1].w};
-      const uint32_t ch[4] = {rows[4 + h].x, rows[4 + h].y, rows[4 + h].z, rows[4 + h].w};
-#pragma unroll
-      for (int sl = 0; sl < 4; ++sl) {
-        const int p = p0 + sl;
-        if (p >= 8 || (j != 1 && sl == 3)) continue;
-        const int lo_b = 6 * p - 16 * j, hi_b = lo_b + 6;
-        uint32_t ys = 0, us = 0, vs = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const uint32_t mk = byte_mask(lo_b, hi_b, w);
-          ys = sad_u8(l0[w] & mk, 0u, sad_u8(l1[w] & mk, 0u, ys));
-          us = sad_u8(ch[w] & mk & 0x00ff00ffu, 0u, us);
-          vs = sad_u8(ch[w] & mk & 0xff00ff00u, 0u, vs);
-        }
-        atomicAdd(&lds_y[pbase + p], ys);
-        atomicAdd(&lds_uv[pbase + p], us | (vs << 16));
-      }
-    }
-  }
-  __syncthreads();
-  uint32_t sad = 0;
-  if (fin) {
-    const int li = (fband - rb * kK6Bands) * kK6Px + (t % kFin) * 4;
-    uint32_t rgb24[4], packed = 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const uint32_t uv = lds_uv[li + p];
-      const uint32_t y = (lds_y[li + p] + K * K / 2) / (K * K);
-      const uint32_t u = ((uv & 0xffffu) + HK * HK / 2) / (HK * HK), v = ((uv >> 16) + HK * HK / 2) / (HK * HK);
-      rgb24[p] = bt709_rgb24(y, u, v);
-      packed |= y << (8 * p);
-      atomicAdd(&lds_hist[y], 1u);
-    }
-    const int64_t tpx = static_cast<int64_t>(fband) * fa.w + fpx;
-    store_rgb<4>(fa.rgb + (gframe * npx + tpx) * 3, rgb24);
-    *reinterpret_cast<uint32_t *>(fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx) = packed;
-    if (fr.z >= 0) sad = sad_u8(packed, prevw, 0u);
-  }
-  if (fr.z >= 0) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sad += __shfl_xor(sad, off, 64);
-    if ((t & 63) == 0) red[t >> 6] = sad;
-  }
-  __syncthreads();
-  if (fr.z >= 0 && t == 0) {
-    uint64_t s = 0;
-#pragma unroll
-    for (int i = 0; i < kK6Threads / 64; ++i) s += red[i];
-    atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(s));
-  }
-  if (t < 128) {
-    const uint64_t lo = lds_hist[2 * t], hi = lds_hist[2 * t + 1];
-    if (lo | hi)
-      atomicAdd(reinterpret_cast<unsigned long long *>(fa.hist + gframe * 256) + t,
-                static_cast<unsigned long long>(lo | (hi << 32)));
-  }
-  if (errs) atomicOr(a.err, errs);
-}
-
 // h264_recon_score6b: the k = 6 kernel with one WAVE per (thumbnail band,
 // 63 consecutive macroblock columns).  A band is 6 luma + 3 chroma rows, so
 // it spans at most two macroblock rows (two commands); lanes of a wave take
@@ -1005,9 +778,6 @@ __global__ void __launch_bounds__(kK6Threads) VTS_K6_OCC __attribute__((unused))
 // LDS atomics except the histogram.  4 waves (4 bands) per workgroup.
 constexpr int kK6bCols = 63;
 constexpr int kK6bPx = kK6bCols * 16 / 6;  // thumbnail pixels per wave segment (168)
-#ifndef VTS_K6B_STAGE
-#define VTS_K6B_STAGE 1  // RGB / thumbnail bytes staged in LDS, stored as dwords
-#endif
 
 // DEC_E_EPB_IN_PCM if an emulation-prevention byte falls in row `rin` of an
 // I_PCM block (a luma row, or the Cb and Cr rows of chroma row rin)
@@ -1017,13 +787,13 @@ __device__ __noinline__ uint32_t pcm_row_epb(const uint8_t *pcm, bool chroma, in
   return bad ? DEC_E_EPB_IN_PCM : 0u;
 }
 
-#ifndef VTS_K6B_WAVES
-#define VTS_K6B_WAVES 0
-#endif
-#ifndef VTS_K6B_ROW6
-#define VTS_K6B_ROW6 1  // rows in flight as <= 6 dwords (issue_row6), each finished,
-                        // stored and box-summed as it lands (no 9-row array)
-#endif
+__device__ __forceinline__ uint32_t byte_mask(int lo, int hi, int w) {
+  // bytes [lo, hi) of a 16-byte chunk that fall in its 32-bit word w
+  const int a = min(max(lo - 4 * w, 0), 4), b = min(max(hi - 4 * w, 0), 4);
+  const uint32_t upto_b = b >= 4 ? 0xffffffffu : ((1u << (8 * b)) - 1u);
+  const uint32_t upto_a = a >= 4 ? 0xffffffffu : ((1u << (8 * a)) - 1u);
+  return upto_b & ~upto_a;
+}
 
 // add row i of a band (0..5 luma, 6..8 NV12 chroma) into the lane's segment
 // box sums: [0] = the left partial [0, b0), [1..3] = the owned pixels
@@ -1047,18 +817,11 @@ __device__ __forceinline__ void k6_acc_row(int i, int b0, const uint4 row, uint3
     }
   }
 }
-#if VTS_K6B_WAVES
-#define VTS_K6B_OCC __attribute__((amdgpu_waves_per_eu(VTS_K6B_WAVES)))
-#else
-#define VTS_K6B_OCC
-#endif
-__global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs fa) {
+__global__ void __launch_bounds__(256) h264_recon_score6b(FusedArgs fa) {
   constexpr int K = 6, HK = 3;
   __shared__ uint32_t lds_hist[256];
   __shared__ uint32_t red[4];
-#if VTS_K6B_STAGE
   __shared__ __attribute__((aligned(16))) uint8_t stage_rgb[4][3 * kK6bPx], stage_th[4][kK6bPx];
-#endif
   const ReconArgs &a = fa.r;
   const int mbw = a.mb_width, nmb = mbw * a.mb_height;
   const int segs = (mbw + kK6bCols - 1) / kK6bCols;
@@ -1104,7 +867,6 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
     uint8_t *dst = a.surf + static_cast<int64_t>(fr.x) * a.frame_stride;
     uint8_t *dst_uv = dst + F.pitch * F.H;
     if (fast_cmd(F, c0) && fast_cmd(F, c1)) {
-#if VTS_K6B_ROW6
       Row6 src[K + HK];  // <= 6 dwords per row in flight (48 VGPRs for the 9 rows, not 72)
 #pragma unroll
       for (int i = 0; i < K + HK; ++i) {
@@ -1133,32 +895,6 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
         if (scored) k6_acc_row(i, b0, row, ys, us, vs);
       }
       summed = true;
-#else
-      uint4 lo[K + HK], hi[K + HK];
-      int shf[K + HK];
-#pragma unroll
-      for (int i = 0; i < K + HK; ++i) {
-        const bool chroma = i >= K;
-        const int r = chroma ? HK * band + (i - K) : r0 + i;  // luma row / chroma row
-        const int mbr = chroma ? r >> 3 : r >> 4;
-        const uint64_t c = mbr == mby0 ? c0 : c1;
-        const bool pcm = (c >> 62) == 1;
-        const uint8_t *pcmb = F.es + static_cast<int64_t>(c & 0xffffffffffffull);
-        const int mvx = static_cast<int16_t>(c & 0xffff), mvy = static_cast<int16_t>((c >> 16) & 0xffff);
-        if (r < (chroma ? F.CH : F.H))
-          issue_row(F, pcmb, pcm, chroma, chroma ? (r & 7) : (r & 15), m, mbr, mvx, mvy, lo[i], hi[i], shf[i]);
-        else
-          lo[i] = hi[i] = make_uint4(0, 0, 0, 0), shf[i] = 0;
-      }
-      uint32_t zero = 0;
-#pragma unroll
-      for (int i = 0; i < K + HK; ++i) {
-        const bool chroma = i >= K;
-        const int r = chroma ? HK * band + (i - K) : r0 + i;
-        const uint64_t c = (chroma ? r >> 3 : r >> 4) == mby0 ? c0 : c1;
-        rows[i] = finish_row(chroma, (c >> 62) == 1, lo[i], hi[i], shf[i], zero);
-      }
-#endif
       if (zero) {  // a zero byte in I_PCM samples: check for emulation prevention exactly
         for (int i = 0; i < K + HK; ++i) {
           const bool chroma = i >= K;
@@ -1168,15 +904,6 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
             errs |= pcm_row_epb(F.es + static_cast<int64_t>(c & 0xffffffffffffull), chroma, chroma ? (r & 7) : (r & 15));
         }
       }
-#if !VTS_K6B_ROW6
-#pragma unroll
-      for (int i = 0; i < K + HK; ++i) {
-        const bool chroma = i >= K;
-        const int r = chroma ? HK * band + (i - K) : r0 + i;
-        if (r < (chroma ? F.CH : F.H))
-          st_row((chroma ? dst_uv : dst) + static_cast<int64_t>(r) * F.pitch + m * 16, rows[i]);
-      }
-#endif
     } else {
       // general path (sub-pel chroma, errors): rare; one row at a time,
       // stored, then read back for scoring (no runtime-indexed register array)
@@ -1238,15 +965,9 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
       us[3] += un;
       vs[3] += vn;
     }
-#if VTS_K6B_STAGE
     // the wave's RGB / thumbnail bytes go through LDS and leave as dwords
     uint8_t *rgb = stage_rgb[threadIdx.x >> 6] + 3 * (pix0 - kK6bPx * seg);
     uint8_t *thumb = stage_th[threadIdx.x >> 6] + (pix0 - kK6bPx * seg);
-#else
-    const int64_t tpx = static_cast<int64_t>(band) * fa.w + pix0;
-    uint8_t *rgb = fa.rgb + (gframe * npx + tpx) * 3;
-    uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx;
-#endif
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (i >= nown || pix0 + i >= fa.w) continue;
@@ -1267,7 +988,6 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
     if (lane == 0) red[threadIdx.x >> 6] = sad;
   }
   __syncthreads();
-#if VTS_K6B_STAGE
   if (band < fa.h && r0 < F.H) {
     // this wave's segment: pixels [kK6bPx * seg, + np) of thumbnail row `band`
     // (w % 8 == 0, so every row and segment starts on a dword)
@@ -1280,7 +1000,6 @@ __global__ void __launch_bounds__(256) VTS_K6B_OCC h264_recon_score6b(FusedArgs 
     for (int d = lane; d < 3 * np / 4; d += 64) grgb[d] = srgb[d];
     if (lane < np / 4) gth[lane] = sth[lane];
   }
-#endif
   if (fr.z >= 0 && threadIdx.x == 0) {
     const uint64_t t = uint64_t(red[0]) + red[1] + red[2] + red[3];
     if (t) atomicAdd(reinterpret_cast<unsigned long long *>(fa.sad + gframe), static_cast<unsigned long long>(t));
@@ -1709,17 +1428,12 @@ int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s) {
   if (n_frames <= 0) return VTS_OK;
   if (k == 6) {
     FusedArgs b = a;
-#if VTS_K6_BAND
     // one wave per (band, 63 macroblock columns), 4 bands per workgroup
     const int bands = (a.r.mb_height * 16 + 5) / 6;
     b.wgs_per_frame = ((a.r.mb_width + kK6bCols - 1) / kK6bCols) * ((bands + 3) / 4);
     hipLaunchKernelGGL(h264_recon_score6b, dim3(n_frames * b.wgs_per_frame), dim3(256), 0, s, b);
-#else
-    b.wgs_per_frame = ((a.r.mb_width + kK6Cols - 1) / kK6Cols) * ((a.r.mb_height + kK6Rows - 1) / kK6Rows);
-    hipLaunchKernelGGL(h264_recon_score6, dim3(n_frames * b.wgs_per_frame), dim3(kK6Threads), 0, s, b);
-#endif
     const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score6 launch: %s", hipGetErrorString(e));
+    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_score6b launch: %s", hipGetErrorString(e));
     return VTS_OK;
   }
   const int q = (k == 0) ? 4 : 16 / k;

@@ -32,7 +32,7 @@ struct FullParseArgs {
   FullParams P;
 };
 
-// per macroblock deblocking descriptor (h264_bs_full -> h264_deblock_full)
+// per macroblock deblocking descriptor (h264_bs_full -> h264_deblock_plane)
 struct DbkInfo {
   uint32_t bs[4];   // bS of edge e (0 = the macroblock edge; 0 when it is not filtered) of direction
                     // dir (0 vertical), 4-sample segment seg: nibble (e & 1) * 4 + seg of word dir * 2 + e / 2
@@ -50,14 +50,6 @@ struct DbkInfo {
 };
 static_assert(sizeof(DbkInfo) == 96, "DbkInfo layout");
 
-// the rows a macroblock's top edge needs from the macroblock above (the
-// general decoder's deblocking hands them from row to row)
-struct DbkLine {  // luma rows 12..15, chroma rows 6..7 (interleaved) of one macroblock
-  uint8_t y[4][16];
-  uint8_t c[2][16];
-};
-static_assert(sizeof(DbkLine) == 96, "DbkLine layout");
-
 struct FullReconArgs {
   const int4 *frames;        // (slot, -, -, -) per picture of the launch
   const MbRec *recs;
@@ -71,15 +63,9 @@ struct FullReconArgs {
   int64_t uv_off;            // UV plane offset in a picture (pitch * coded height)
   int32_t pitch;
   uint32_t epoch;
-  int32_t deblock;           // deblocking kernel after reconstruction: 0 none, 1 h264_deblock_full, 2 h264_deblock_lds,
-                             // 3 h264_deblock_plane
+  int32_t deblock;           // 1: h264_deblock_plane after reconstruction (0: none)
   int32_t intra_kernel;      // 1: h264_intra_full, else h264_intra_v2 (where its LDS fits)
-  int32_t dbk_bands;         // h264_deblock_lds: workgroups per picture (bands of row pairs), 1..4
-  int32_t bs_fused;          // 1: h264_inter_full derives the level's bS (DbkInfo) after its blocks; 0: h264_bs_full does
   DbkInfo *dbk;              // ring: [slot][mb] deblocking descriptors
-  uint8_t *dbkx;             // dbk_bands > 1: [slot][band boundary] a counter (64 B) + mb_width DbkLine
-                             // rows a band's last macroblock row hands to the next band
-  uint32_t *dbk_tix;         // dbk_bands > 1: this launch's ticket counter (zero before the launch)
   uint32_t *err;
   const ScaleTab *sct;       // LevelScale4x4 / 8x8 (read when P.scaled)
   FullParams P;

@@ -14,13 +14,11 @@
 //                     1 + the highest level among the intra neighbours it
 //                     reads; an all-intra picture gives the x + 2y wavefront),
 //                     16 lanes per macroblock, its borders and 4x4 blocks in LDS
-//   h264_deblock_full one workgroup per picture, one wave per pair of
-//                     macroblock rows (the lower row two macroblocks behind the
-//                     upper, the pair behind the pair above through LDS
-//                     progress counters): the standard's raster order (8.7) as
-//                     a wavefront; a lane filters one row across the vertical
-//                     edges in registers, then one column across the
-//                     horizontal edges out of an LDS tile
+//   h264_bs_full      16 lanes per macroblock: bS of every edge + the edge
+//                     filter parameters into a 96-byte descriptor
+//   h264_deblock_plane one workgroup per (picture, plane), 16 lanes per
+//                     macroblock row, the rows two macroblocks apart (8.7's
+//                     raster order as a wavefront), rows above through LDS
 // Per-macroblock arithmetic (transforms, interpolation, intra modes, edge
 // filters) follows the same clauses as recon_full.h, which the CPU harness
 // runs against the oracle.
@@ -490,7 +488,6 @@ __device__ __forceinline__ void pred_ref(const FullReconArgs &a, int rs, uint32_
       }
 }
 
-__device__ void bs_mb(const FullReconArgs &a, int slot, int mb, int b);  // h264_bs_full
 
 // ------------------------------------------------------- inter / I_PCM blocks
 // lane = (macroblock, raster 4x4 block b)
@@ -595,17 +592,9 @@ __device__ __forceinline__ void inter_mb(const FullReconArgs &a, int slot, int m
     *reinterpret_cast<uint32_t *>(UV + static_cast<int64_t>(cy + y) * pitch + 2 * cx) =
         pack4(cpred[0][y * 2], cpred[1][y * 2], cpred[0][y * 2 + 1], cpred[1][y * 2 + 1]);
 }
-// grid (ceil(nmb / 16), pictures of the level).  bs_fused (VTS_BS=1): the
-// level's bS descriptors come from the same lanes after the blocks are stored
-// (the deblocking launch after this one reads them) — measured slower than a
-// separate bS launch per level beside the chain (inter 0.31 -> 0.58 ms per
-// launch, profiles/r04r_bs_fused_ab.json), kept as an option
+// grid (ceil(nmb / 16), pictures of the level)
 __global__ void __launch_bounds__(kInterThreads) h264_inter_full(FullReconArgs a) {
-  const int slot = a.frames[blockIdx.y].x;
-  const int mb = blockIdx.x * 16 + (threadIdx.x >> 4);
-  const int b = threadIdx.x & 15;
-  inter_mb(a, slot, mb, b);
-  if (a.bs_fused) bs_mb(a, slot, mb, b);  // every lane (the macroblock's 16 lanes meet in a butterfly)
+  inter_mb(a, a.frames[blockIdx.y].x, blockIdx.x * 16 + (threadIdx.x >> 4), threadIdx.x & 15);
 }
 
 // ------------------------------------------------------------ intra blocks
@@ -1339,96 +1328,6 @@ __device__ __forceinline__ int bs_dev(const MbRec *P, const MbRecB *P1, int bp, 
   return (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
 }
 
-// one line of samples s[0..7] = p3 p2 p1 p0 q0 q1 q2 q3 (8.7.2.3 / 8.7.2.4)
-// tcs: the packed edge tables of indexA (DbkLut::at): tC0 of bS = (tcs >> 8 * bS) & 255
-__device__ __forceinline__ void filt_luma(int (&s)[8], int bS, uint32_t tcs, int alpha, int beta) {
-  const int p0 = s[3], p1 = s[2], q0 = s[4], q1 = s[5];
-  if (!(bS > 0 && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-  const int p2 = s[1], q2 = s[6];
-  const int ap = abs(p2 - p0), aq = abs(q2 - q0);
-  if (bS < 4) {
-    const int tc0 = (tcs >> (8 * bS)) & 255;
-    const int tc = tc0 + (ap < beta) + (aq < beta);
-    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
-    s[3] = c255(p0 + delta);
-    s[4] = c255(q0 - delta);
-    if (ap < beta) s[2] = p1 + min(max((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0), tc0);
-    if (aq < beta) s[5] = q1 + min(max((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0), tc0);
-    return;
-  }
-  const int p3 = s[0], q3 = s[7];
-  const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
-  if (ap < beta && small) {
-    s[3] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
-    s[2] = (p2 + p1 + p0 + q0 + 2) >> 2;
-    s[1] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
-  } else {
-    s[3] = (2 * p1 + p0 + q1 + 2) >> 2;
-  }
-  if (aq < beta && small) {
-    s[4] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
-    s[5] = (p0 + q0 + q1 + q2 + 2) >> 2;
-    s[6] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-  } else {
-    s[4] = (2 * q1 + q0 + p1 + 2) >> 2;
-  }
-}
-// chroma line p1 p0 q0 q1
-__device__ __forceinline__ void filt_chroma(int &p1, int &p0, int &q0, int &q1, int bS, uint32_t tcs, int alpha, int beta) {
-  if (!(bS > 0 && abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-  if (bS < 4) {
-    const int tc = ((tcs >> (8 * bS)) & 255) + 1;
-    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
-    const int np0 = c255(p0 + delta), nq0 = c255(q0 - delta);
-    p0 = np0;
-    q0 = nq0;
-    return;
-  }
-  const int np0 = (2 * p1 + p0 + q1 + 2) >> 2, nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
-  p0 = np0;
-  q0 = nq0;
-}
-
-struct DbkTile {
-  uint8_t y[20][20];  // luma rows -4..15 x cols -4..15
-  uint8_t c[10][20];  // chroma rows -2..7 x interleaved bytes -4..15
-};
-
-// Table 8-16 / 8-17 and the chroma QP table (8-15) staged in LDS once per
-// workgroup: a per-lane index into __constant__ data is a vector memory load
-// on the wavefront's critical path, an LDS read is not
-struct DbkLut {
-  uint32_t at[52];  // alpha(indexA) | tC0(indexA, bS 1..3) << 8 * bS
-  uint8_t be[52];   // beta(indexB)
-  uint8_t qc[52];   // QPc(qPI)
-};
-__device__ __forceinline__ void dbk_lut_init(DbkLut &t) {
-  for (int i = threadIdx.x; i < 52; i += blockDim.x) {
-    t.at[i] = static_cast<uint32_t>(kAl[i]) | static_cast<uint32_t>(kTc[i][0]) << 8 |
-              static_cast<uint32_t>(kTc[i][1]) << 16 | static_cast<uint32_t>(kTc[i][2]) << 24;
-    t.be[i] = kBe[i];
-    t.qc[i] = full::qpc_of(i, 0);
-  }
-}
-__device__ __forceinline__ int dbk_qpc(const DbkLut &t, int qp, int off) { return t.qc[min(max(qp + off, 0), 51)]; }
-
-struct EdgeQ {  // alpha/beta/tC0 for an edge between macroblocks of qp qpp, qpq
-  uint32_t tcs;
-  int alpha, beta;
-};
-__device__ __forceinline__ EdgeQ edge_q(const DbkLut &t, int qpav, int fa, int fb) {
-  EdgeQ e;
-  e.tcs = t.at[min(max(qpav + fa, 0), 51)];
-  e.alpha = e.tcs & 255;
-  e.beta = t.be[min(max(qpav + fb, 0), 51)];
-  return e;
-}
-
-// bS of edge e (0 = the macroblock edge) of direction dir, 4-sample segment seg
-__device__ __forceinline__ int dbk_bs(const DbkInfo &d, int dir, int e, int seg) {
-  return (d.bs[dir * 2 + (e >> 1)] >> (((e & 1) * 4 + seg) * 4)) & 15;
-}
-
 // the packed parameters of an edge whose average QP is qpav (DbkInfo::lv)
 __device__ __forceinline__ uint32_t edge_word(int qpav, int fa, int fb) {
   const int ia = min(max(qpav + fa, 0), 51), ib = min(max(qpav + fb, 0), 51);
@@ -1522,228 +1421,6 @@ __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
   bs_mb(a, a.frames[blockIdx.y].x, blockIdx.x * 16 + (threadIdx.x >> 4), threadIdx.x & 15);
 }
 
-__device__ __forceinline__ DbkInfo dbk_load(const DbkInfo *p) {
-  const uint4 u0 = reinterpret_cast<const uint4 *>(p)[0], u1 = reinterpret_cast<const uint4 *>(p)[1];
-  DbkInfo d;
-  d.bs[0] = u0.x;
-  d.bs[1] = u0.y;
-  d.bs[2] = u0.z;
-  d.bs[3] = u0.w;
-  d.qp = u1.x;
-  d.fa = static_cast<int32_t>(u1.y);
-  d.fb = static_cast<int32_t>(u1.z);
-  d._pad = 0;
-  return d;
-}
-
-// grid: pictures of the level
-__global__ void __launch_bounds__(kDbkThreads) h264_deblock_full(FullReconArgs a) {
-  __shared__ DbkTile tiles[kDbkWaves * 2];
-  __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
-  __shared__ DbkLut lut;
-  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
-  const int slot = a.frames[blockIdx.x].x;
-  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
-  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
-  uint8_t *UV = Y + a.uv_off;
-  const int pitch = a.pitch;
-  for (int i = threadIdx.x; i < mbh; i += kDbkThreads) prog[i] = 0;
-  dbk_lut_init(lut);
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int half = lane >> 5, l = lane & 31;
-  const bool lrow = l < 24, luma = l < 16;
-  // V phase: luma row l / chroma row l - 16 (lanes 24..31: chroma row 7,
-  // addressed only by the clamped prefetch)
-  const int row = luma ? l : min(l - 16, 7);
-  const int ia = min(max(l - 24, 0), 5);  // rows-above lane: luma rows -4..-1, chroma rows -2..-1
-  DbkTile &t = tiles[wave * 2 + half];
-  const int npairs = (mbh + 1) >> 1;
-  RPROF_DECL;
-  for (int p = wave; p < npairs; p += kDbkWaves) {
-    const int y = 2 * p + half;
-    const bool row_ok = y < mbh;
-    // every load below is unconditional from a clamped address (its value is
-    // used only where the unclamped one was valid), so the compiler keeps it
-    // in flight across the iteration instead of waiting inside a branch
-    const int ya = row_ok ? y : mbh - 1;
-    const int64_t yrow = static_cast<int64_t>(ya * 16) * pitch, crow = static_cast<int64_t>(ya * 8) * pitch;
-    uint8_t *const rowp = (luma ? Y + yrow : UV + crow) + static_cast<int64_t>(row) * pitch;
-    const DbkInfo *const drow = fdbk + ya * mbw;
-    const uint8_t *const abovep = y > 0 ? (ia < 4 ? Y + yrow + static_cast<int64_t>(ia - 4) * pitch
-                                                  : UV + crow + static_cast<int64_t>(ia - 6) * pitch)
-                                        : Y;
-    uint32_t left = 0;  // carried cols 12..15 of the previous macroblock (this lane's row)
-    // the macroblock of the next iteration: descriptor and this lane's row, loaded one iteration ahead
-    DbkInfo nd = dbk_load(drow);
-    uint4 npx = *reinterpret_cast<const uint4 *>(rowp);
-    for (int it = 0; it < mbw + 2; ++it) {
-      const int x = it - 2 * half;
-      const bool act = row_ok && x >= 0 && x < mbw;
-      const DbkInfo D = nd;
-      const uint4 q4 = npx;
-      {
-        const int xn = min(max(x + 1, 0), mbw - 1);
-        nd = dbk_load(drow + xn);
-        npx = *reinterpret_cast<const uint4 *>(rowp + xn * 16);
-      }
-      // the upper row of the pair waits for the row above (another wave)
-      if (half == 0 && act && y > 0) {
-        const int need = x + 1 < mbw ? x + 2 : mbw + 1;
-        while (__hip_atomic_load(&prog[y - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-          __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      RPROF(0);
-      const bool on = act && !((D.qp >> 24) & 1);  // disable_deblocking_filter_idc != 1
-      const int qpq = D.qp & 255, qpl = (D.qp >> 8) & 255, qpt = (D.qp >> 16) & 255;
-      const int64_t ybase = yrow + x * 16, cbase = crow + x * 16;
-      // rows above (final: the row above is two macroblocks ahead), loaded
-      // here and stored to the tile after the vertical edges
-      const uint4 above = *reinterpret_cast<const uint4 *>(abovep + min(max(x, 0), mbw - 1) * 16);
-      // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
-      if (act && lrow) {
-        const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
-        int r[20];
-#pragma unroll
-        for (int i = 0; i < 20; ++i) r[i] = (wv[i >> 2] >> ((i & 3) * 8)) & 255;
-        if (on) {
-          if (luma) {
-            const int seg = row >> 2;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int bS = dbk_bs(D, 0, e, seg);
-              if (!bS) continue;
-              const EdgeQ eq = edge_q(lut, e ? qpq : (qpl + qpq + 1) >> 1, D.fa, D.fb);
-              if (!eq.alpha || !eq.beta) continue;
-              int s[8];
-#pragma unroll
-              for (int i = 0; i < 8; ++i) s[i] = r[4 * e + i];
-              filt_luma(s, bS, eq.tcs, eq.alpha, eq.beta);
-#pragma unroll
-              for (int i = 0; i < 8; ++i) r[4 * e + i] = s[i];
-            }
-          } else {
-            const int seg = row >> 1;
-#pragma unroll
-            for (int e = 0; e < 4; e += 2) {
-              const int bS = dbk_bs(D, 0, e, seg);
-              if (!bS) continue;
-              const int qpp = e ? qpq : qpl;
-#pragma unroll
-              for (int pl = 0; pl < 2; ++pl) {
-                const int off = pl ? a.P.cqp_off2 : a.P.cqp_off;
-                const EdgeQ eq = edge_q(lut, (dbk_qpc(lut, qpp, off) + dbk_qpc(lut, qpq, off) + 1) >> 1, D.fa, D.fb);
-                if (!eq.alpha || !eq.beta) continue;
-                const int c0 = 4 + 2 * (2 * e) + pl;  // q0 of chroma col 2e (luma edge e)
-                filt_chroma(r[c0 - 4], r[c0 - 2], r[c0], r[c0 + 2], bS, eq.tcs, eq.alpha, eq.beta);
-              }
-            }
-          }
-        }
-        uint8_t *dst = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-          *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
-      }
-      if (act && l >= 24 && l < 30 && y > 0)
-        *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = above;
-      lane_sync();
-      RPROF(1);
-      // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved chroma column l - 16
-      if (on) {
-        if (l < 16) {
-          const int col = l, seg = col >> 2;
-          int r[20];
-#pragma unroll
-          for (int i = 0; i < 20; ++i) r[i] = t.y[i][4 + col];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int bS = dbk_bs(D, 1, e, seg);
-            if (!bS) continue;
-            const EdgeQ eq = edge_q(lut, e ? qpq : (qpt + qpq + 1) >> 1, D.fa, D.fb);
-            if (!eq.alpha || !eq.beta) continue;
-            int s[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) s[i] = r[4 * e + i];
-            filt_luma(s, bS, eq.tcs, eq.alpha, eq.beta);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) r[4 * e + i] = s[i];
-          }
-#pragma unroll
-          for (int i = 1; i < 20; ++i) t.y[i][4 + col] = static_cast<uint8_t>(r[i]);
-        } else {
-          const int j = l - 16, pl = j & 1, cc = j >> 1, seg = cc >> 1;
-          const int off = pl ? a.P.cqp_off2 : a.P.cqp_off;
-          int r[10];
-#pragma unroll
-          for (int i = 0; i < 10; ++i) r[i] = t.c[i][4 + j];
-#pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const int bS = dbk_bs(D, 1, e, seg);
-            if (!bS) continue;
-            const int qpp = e ? qpq : qpt;
-            const EdgeQ eq = edge_q(lut, (dbk_qpc(lut, qpp, off) + dbk_qpc(lut, qpq, off) + 1) >> 1, D.fa, D.fb);
-            if (!eq.alpha || !eq.beta) continue;
-            const int q0 = 2 + 2 * e;  // chroma row 2e
-            filt_chroma(r[q0 - 2], r[q0 - 1], r[q0], r[q0 + 1], bS, eq.tcs, eq.alpha, eq.beta);
-          }
-#pragma unroll
-          for (int i = 1; i < 10; ++i) t.c[i][4 + j] = static_cast<uint8_t>(r[i]);
-        }
-      }
-      lane_sync();
-      RPROF(2);
-      // ---- write back: rows of this macroblock shifted 4 bytes left (the left
-      // neighbour's last columns are final now), rows above, the row's tail
-      if (act) {
-        if (lrow) {
-          const uint8_t *src = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
-          uint8_t *dst = rowp + x * 16;
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (x > 0 || i > 0) *reinterpret_cast<uint32_t *>(dst - 4 + 4 * i) = *reinterpret_cast<const uint32_t *>(src + 4 * i);
-          left = *reinterpret_cast<const uint32_t *>(src + 16);
-          if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
-        } else if (l < 28 && y > 0 && on && dbk_bs(D, 1, 0, 0) + dbk_bs(D, 1, 0, 1) + dbk_bs(D, 1, 0, 2) + dbk_bs(D, 1, 0, 3)) {
-          const int i = l - 24;  // luma rows -3..-1, chroma row -1
-          if (i < 3) *reinterpret_cast<uint4 *>(Y + ybase + static_cast<int64_t>(i - 3) * pitch) = *reinterpret_cast<const uint4 *>(&t.y[1 + i][4]);
-          else *reinterpret_cast<uint4 *>(UV + cbase - pitch) = *reinterpret_cast<const uint4 *>(&t.c[1][4]);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      if (act && l == 0)
-        __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      RPROF(3);
-      RPROF_COUNT(7, 1);
-    }
-  }
-  RPROF(4);
-  RPROF_FLUSH(0);
-}
-
-
-// ---- deblocking, LDS hand-off (default; VTS_DBK=1 runs h264_deblock_full)
-// The same wavefront as h264_deblock_full (a wave per macroblock-row pair,
-// the lower row two macroblocks behind), but the rows a macroblock's top edge
-// reads from the row above (luma rows 12..15, chroma rows 6..7) pass between
-// rows through a ring in LDS instead of HBM: the producer row writes them
-// while its pixels are still in the tile, the consumer row copies them into
-// its tile after the progress counter allows it.  Global memory carries no
-// hand-off, so no step waits for another wave's global stores or issues a
-// dependent global load (in h264_deblock_full the row-above load sat between
-// the progress wait and the horizontal edges of every step).  Every byte of
-// the picture has one writer: a row stores its own rows 0..12 (chroma 0..6)
-// and the row below stores rows 13..15 (chroma 7) after its top edge (the
-// picture's last row stores all of its rows).  Edge parameters come resolved
-// from h264_bs_full (DbkInfo::lv ... ch).
-// Ring: kDbkRingRows row slots (a row and the row 2 x kDbkWaves below share
-// one; the later waits for the earlier's consumer to finish) of kDbkRingCols
-// macroblock columns; a producer waits for its consumer to be within
-// kDbkRingCols - 1 columns before it overwrites one.
-constexpr int kDbkRingRows = 2 * kDbkWaves;
-constexpr int kDbkRingCols = 32;
 
 __device__ __forceinline__ uint32_t u4_at(const uint4 &v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
@@ -1800,269 +1477,6 @@ constexpr int dbk_hrow(int j) {
   return (j >= 2 && j <= 5) ? j - 2 : ((j >= 10 && j <= 13) ? j - 6 : (j == 14 ? 8 : (j == 15 ? 9 : -1)));
 }
 
-// grid: pictures of the level (x bands); kBands: the band hand-off compiled in
-// (VTS_DBK_BANDS > 1), else K = 1 folds it away with its registers
-template <bool kBands>
-__global__ void __launch_bounds__(kDbkThreads) h264_deblock_lds(FullReconArgs a) {
-  __shared__ DbkTile tiles[kDbkWaves * 2];
-  __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
-  __shared__ DbkLine ring[kDbkRingRows][kDbkRingCols];
-  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
-  // K workgroups per picture, each a band of row pairs; band b's first row
-  // takes the row above's ring lines from band b - 1 through global memory
-  // (an agent-scope counter per boundary, tagged with the run's epoch)
-  const int K = kBands && a.dbk_bands > 1 ? a.dbk_bands : 1;
-  // (picture, band) by ticket in start order, not by blockIdx: workgroups go
-  // to the XCDs round-robin and each XCD starts its own in order, so a band
-  // could otherwise be resident and waiting while its producer band still
-  // queues behind other waiting bands; a ticket taken at start means every
-  // lower ticket's workgroup is already running
-  __shared__ int s_ticket;
-  if (threadIdx.x == 0) s_ticket = K > 1 ? static_cast<int>(atomicAdd(a.dbk_tix, 1u)) : static_cast<int>(blockIdx.x);
-  __syncthreads();
-  const int pic = s_ticket / K, band = s_ticket - pic * K;
-  const int slot = a.frames[pic].x;
-  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
-  uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
-  // samples addressed as 32-bit offsets from the picture (uniform base +
-  // per-lane offset: one VGPR per address instead of a pair)
-  const uint32_t uvo = static_cast<uint32_t>(a.uv_off);
-  auto at = [Y](uint32_t o) { return Y + static_cast<uint64_t>(o); };
-  const int pitch = a.pitch;
-  for (int i = threadIdx.x; i < mbh; i += kDbkThreads) prog[i] = 0;
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int half = lane >> 5, l = lane & 31;
-  const bool lrow = l < 24, luma = l < 16;
-  // V phase: luma row l / chroma row l - 16 (lanes 24..31: chroma row 7,
-  // addressed only by the clamped prefetch)
-  const int row = luma ? l : min(l - 16, 7);
-  const int ia = min(max(l - 24, 0), 5);  // rows-above lane: luma rows -4..-1, chroma rows -2..-1
-  DbkTile &t = tiles[wave * 2 + half];
-  // which edge-parameter quad this lane reads: vertical pass by its row kind,
-  // horizontal pass by its column kind (lanes 16..31 = chroma columns)
-  const int vq = luma ? 2 : 4, hq = l < 16 ? 3 : 5;
-  const int npairs = (mbh + 1) >> 1;
-  const int KB = min(K, npairs);  // bands of at least one row pair each
-  if (band >= KB) return;         // (before any barrier: the whole workgroup leaves)
-  const int p0 = npairs * band / KB, p1 = npairs * (band + 1) / KB;
-  const int y0 = 2 * p0, yend = min(2 * p1, mbh);
-  const int64_t xstride = static_cast<int64_t>(mbw) * static_cast<int64_t>(sizeof(DbkLine)) + 64;
-  uint8_t *const xin = band > 0 ? a.dbkx + (static_cast<int64_t>(slot) * (K - 1) + band - 1) * xstride : nullptr;
-  uint8_t *const xout = band + 1 < K ? a.dbkx + (static_cast<int64_t>(slot) * (K - 1) + band) * xstride : nullptr;
-  const uint32_t xtag = (a.epoch & 0xffffu) << 16;
-  RPROF_DECL;
-  for (int p = p0 + wave; p < p1; p += kDbkWaves) {
-    const int y = 2 * p + half;
-    const bool row_ok = y < mbh;
-    const int ya = row_ok ? y : mbh - 1;
-    const bool last_row = y == mbh - 1;
-    const bool band_first = band > 0 && y == y0, band_last = band + 1 < KB && y == yend - 1;
-    const int rs = y % kDbkRingRows, rsa = (y + kDbkRingRows - 1) % kDbkRingRows;
-    const int64_t yrow = static_cast<int64_t>(ya * 16) * pitch, crow = static_cast<int64_t>(ya * 8) * pitch;
-    const uint32_t rowo = static_cast<uint32_t>((luma ? yrow : uvo + crow) + static_cast<int64_t>(row) * pitch);
-    const DbkInfo *const drow = fdbk + ya * mbw;
-    // this row's ring slot was the row kDbkRingRows above's: its consumer must be done
-    if (row_ok && y - kDbkRingRows >= y0) {
-      while (__hip_atomic_load(&prog[y - kDbkRingRows + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < mbw + 1)
-        __builtin_amdgcn_s_sleep(1);
-    }
-    uint32_t left = 0;  // carried cols 12..15 of the previous macroblock (this lane's row)
-    // the next iteration's macroblock: bS words, the lane's edge parameters, its row
-    const uint4 *dq = reinterpret_cast<const uint4 *>(drow);
-    uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
-    uint4 npx = *reinterpret_cast<const uint4 *>(at(rowo));
-    for (int it = 0; it < mbw + 2; ++it) {
-      const int x = it - 2 * half;
-      const bool act = row_ok && x >= 0 && x < mbw;
-      const uint4 bsw = nbs, pv = nv, ph = nh, q4 = npx;
-      {
-        const int xn = min(max(x + 1, 0), mbw - 1);
-        const uint4 *dn = reinterpret_cast<const uint4 *>(drow + xn);
-        nbs = dn[0];
-        nv = dn[vq];
-        nh = dn[hq];
-        npx = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xn * 16)));
-      }
-      // the upper row of the pair waits for the row above (another wave); a
-      // row whose consumer is another wave waits until it may overwrite ring
-      // column x (the consumer read column x - kDbkRingCols)
-      if (act) {
-        const int need_up = (half == 0 && y > 0 && !band_first) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
-        const int need_dn = (half == 1 && y + 1 < mbh && !band_last) ? x - kDbkRingCols + 1 : -(1 << 30);
-        const int *pu = &prog[y > 0 ? y - 1 : 0], *pd = &prog[y + 1 < mbh ? y + 1 : y];
-        while (__hip_atomic_load(pu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_up ||
-               __hip_atomic_load(pd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_dn)
-          __builtin_amdgcn_s_sleep(1);
-      }
-      if (act && band_first) {  // the previous band's last row, two macroblocks ahead
-        const uint32_t need = xtag | static_cast<uint32_t>(x + 1 < mbw ? x + 2 : mbw + 1);
-        const uint32_t *cnt = reinterpret_cast<const uint32_t *>(xin);
-        for (;;) {
-          const uint32_t v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((v & 0xffff0000u) == xtag && v >= need) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      RPROF(0);
-      // a macroblock none of whose edges (left, top, inside) filters keeps its
-      // samples: its step skips both passes and writes back what it loaded
-      const bool still = (bsw.x | bsw.y | bsw.z | bsw.w) == 0u;
-      // rows above from the ring (final: the row above is two macroblocks ahead)
-      if (act && l >= 24 && l < 30 && y > 0) {
-        const DbkLine &L = band_first ? reinterpret_cast<const DbkLine *>(xin + 64)[x] : ring[rsa][x & (kDbkRingCols - 1)];
-        const uint4 v = ia < 4 ? *reinterpret_cast<const uint4 *>(&L.y[ia][0]) : *reinterpret_cast<const uint4 *>(&L.c[ia - 4][0]);
-        *reinterpret_cast<uint4 *>(ia < 4 ? &t.y[ia][4] : &t.c[ia - 4][4]) = v;
-      }
-      // ---- vertical edges: lane l < 16 = luma row l, 16..23 = chroma row l - 16
-      if (act && lrow && !still) {
-        const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
-        int r[20], u[20];
-#pragma unroll
-        for (int i = 0; i < 20; ++i) r[i] = (wv[i >> 2] >> ((i & 3) * 8)) & 255;
-#pragma unroll
-        for (int j = 0; j < 20; ++j) u[j] = luma ? r[j] : r[kDbkCPerm[j]];
-        const int seg = luma ? row >> 2 : row >> 1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int bS = (u4_at(bsw, e >> 1) >> (((luma ? (e & 1) : 0) * 4 + seg) * 4)) & 15;
-          if (!bS) continue;
-          int s8[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
-          filt_w(s8, bS, u4_at(pv, e), !luma);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 20; ++i) r[i] = luma ? u[i] : u[kDbkCInv[i]];
-        uint8_t *dst = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-          *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
-      }
-      lane_sync();
-      RPROF(1);
-      // ---- horizontal edges: lane l < 16 = luma column l, 16..31 = interleaved
-      // chroma column l - 16 (one plane; its edges at slots 0 and 2)
-      if (act && !still) {
-        const int j = l - 16, pl = j & 1;
-        const int seg = luma ? l >> 2 : j >> 2;
-        uint8_t *const ycol = &t.y[0][4 + l];
-        uint8_t *const ccol = &t.c[0][4 + (j & 15)];
-        int u[20];
-#pragma unroll
-        for (int i = 0; i < 20; ++i) {  // one LDS read per sample: the lane's own column
-          const int cr = dbk_hrow(i);
-          const uint8_t *q = luma ? ycol + i * 20 : ccol + (cr >= 0 ? cr : 0) * 20;
-          u[i] = (luma || cr >= 0) ? *q : 0;
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int bS = (u4_at(bsw, 2 + (e >> 1)) >> (((luma ? (e & 1) : 0) * 4 + seg) * 4)) & 15;
-          if (!luma && (e & 1)) bS = 0;
-          if (!bS) continue;
-          int s8[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
-          filt_w(s8, bS, u4_at(ph, luma ? e : e + pl), !luma);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
-        }
-#pragma unroll
-        for (int i = 1; i < 20; ++i) {
-          const int cr = dbk_hrow(i);
-          uint8_t *q = luma ? ycol + i * 20 : ccol + (cr >= 1 ? cr : 0) * 20;
-          if (luma || cr >= 1) *q = static_cast<uint8_t>(u[i]);
-        }
-      }
-      lane_sync();
-      RPROF(2);
-      // ---- write back: this macroblock's rows shifted 4 bytes left (the left
-      // neighbour's last columns are final now) except the ones the row below
-      // finishes (luma 13..15, chroma 7), the ring lines for the row below,
-      // the rows above this macroblock that its top edge finished
-      if (act) {
-        if (lrow) {
-          uint32_t w0, w1, w2, w3;
-          if (still) {
-            w0 = left;
-            w1 = q4.x;
-            w2 = q4.y;
-            w3 = q4.z;
-            left = q4.w;
-          } else {
-            const uint8_t *src = luma ? &t.y[4 + row][0] : &t.c[2 + row][0];
-            w0 = *reinterpret_cast<const uint32_t *>(src);
-            w1 = *reinterpret_cast<const uint32_t *>(src + 4);
-            w2 = *reinterpret_cast<const uint32_t *>(src + 8);
-            w3 = *reinterpret_cast<const uint32_t *>(src + 12);
-            left = *reinterpret_cast<const uint32_t *>(src + 16);
-          }
-          const bool mine = last_row || (luma ? row < 13 : row < 7);
-          if (mine) {
-            uint8_t *dst = at(rowo + static_cast<uint32_t>(x * 16));
-            if (x > 0) *reinterpret_cast<uint32_t *>(dst - 4) = w0;
-            *reinterpret_cast<uint32_t *>(dst) = w1;
-            *reinterpret_cast<uint32_t *>(dst + 4) = w2;
-            *reinterpret_cast<uint32_t *>(dst + 8) = w3;
-            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(dst + 12) = left;
-          }
-          const int lr = luma ? row - 12 : row - 6;  // ring line of this lane's row
-          if (band_last && lr >= 0) {  // to the next band, through global memory
-            DbkLine *xl = reinterpret_cast<DbkLine *>(xout + 64);
-            uint8_t *cur = luma ? &xl[x].y[lr][0] : &xl[x].c[lr][0];
-            if (x > 0) *reinterpret_cast<uint32_t *>(cur - static_cast<int>(sizeof(DbkLine)) + 12) = w0;
-            *reinterpret_cast<uint32_t *>(cur) = w1;
-            *reinterpret_cast<uint32_t *>(cur + 4) = w2;
-            *reinterpret_cast<uint32_t *>(cur + 8) = w3;
-            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = left;
-          } else if (!last_row && lr >= 0) {
-            uint8_t *cur = luma ? &ring[rs][x & (kDbkRingCols - 1)].y[lr][0] : &ring[rs][x & (kDbkRingCols - 1)].c[lr][0];
-            if (x > 0) {
-              uint8_t *prv = luma ? &ring[rs][(x - 1) & (kDbkRingCols - 1)].y[lr][0]
-                                  : &ring[rs][(x - 1) & (kDbkRingCols - 1)].c[lr][0];
-              *reinterpret_cast<uint32_t *>(prv + 12) = w0;
-            }
-            *reinterpret_cast<uint32_t *>(cur) = w1;
-            *reinterpret_cast<uint32_t *>(cur + 4) = w2;
-            *reinterpret_cast<uint32_t *>(cur + 8) = w3;
-            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = left;
-          }
-        } else if (l < 28 && y > 0) {
-          // luma rows -3..-1, chroma row -1 of the macroblock above; the lane
-          // index opaque here, so the tile and row offsets are computed per
-          // step rather than kept per row (spilled, and each reload waited for
-          // every load and store in flight)
-          int lo = lane;
-          asm volatile("" : "+v"(lo));
-          const int i = (lo & 31) - 24, hf = lo >> 5, yy = min(2 * p + hf, mbh - 1);
-          const DbkTile &tt = tiles[__builtin_amdgcn_readfirstlane(wave) * 2 + hf];
-          const uint4 v = i < 3 ? *reinterpret_cast<const uint4 *>(&tt.y[1 + i][4]) : *reinterpret_cast<const uint4 *>(&tt.c[1][4]);
-          const uint32_t o = i < 3 ? static_cast<uint32_t>((yy * 16 + i - 3) * pitch) : uvo + static_cast<uint32_t>((yy * 8 - 1) * pitch);
-          *reinterpret_cast<uint4 *>(at(o + static_cast<uint32_t>(x * 16))) = v;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      if (act && l == 0)
-        __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (act && band_last) {  // the lines of columns < x + 1 are final: publish to the next band
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (l == 0)
-          __hip_atomic_store(reinterpret_cast<uint32_t *>(xout), xtag | static_cast<uint32_t>(x + 1 < mbw ? x + 1 : mbw + 1),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      RPROF(3);
-      RPROF_COUNT(7, 1);
-    }
-  }
-  RPROF(4);
-  RPROF_FLUSH(0);
-}
-
 }  // namespace
 
 #ifdef VTS_EXP_RPROF
@@ -2103,9 +1517,9 @@ int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
 // each needs 16 lanes per macroblock row instead of 32: one workgroup per
 // (picture, plane) holds kDpGroups = 64 macroblock rows in flight (16 waves x
 // 4 groups of 16 lanes), so a 720p / 1080p picture is one pass of the
-// wavefront (h264_deblock_lds holds 32 rows: a 720p picture's rows 32..44
-// waited for the first pass to free a wave).  Same step as h264_deblock_lds
-// per plane: rows above from the ring, vertical pass (lane = sample row),
+// wavefront.  Per plane and step: rows above from an LDS ring (the rows a
+// macroblock's top edge needs pass from row to row in LDS, never through
+// HBM), vertical pass (lane = sample row),
 // horizontal pass (lane = sample column), write-back (rows the row below
 // finishes excepted), ring lines for the row below; the four rows of a wave
 // run in lockstep two macroblocks apart, a wave's first row waits for the
@@ -2128,13 +1542,10 @@ constexpr size_t kDpLdsY = sizeof(DpTileY) * kDpGroups + sizeof(DpLineY) * kDpGr
 constexpr size_t kDpLdsC = sizeof(DpTileC) * kDpGroups + sizeof(DpLineC) * kDpGroups * kDpRingCols;
 constexpr size_t kDpLds = kDpLdsY > kDpLdsC ? kDpLdsY : kDpLdsC;
 
-// kLag1: a row runs one macroblock behind the row above instead of two: its
-// horizontal pass waits only for the row above's vertical pass of the
-// macroblock above-right (the last change to the samples above it), which
-// the row above publishes mid-step in vprog[] after writing the left
-// macroblock's final cols 12..15 into its ring line
-template <bool kLuma, bool kLag1>
-__device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_t *lds, int *prog, int *vprog) {
+// (A row one macroblock behind the row above instead of two was bit-exact
+// and no faster)
+template <bool kLuma>
+__device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_t *lds, int *prog) {
   using Tile = typename std::conditional<kLuma, DpTileY, DpTileC>::type;
   using Line = typename std::conditional<kLuma, DpLineY, DpLineC>::type;
   Tile *tiles = reinterpret_cast<Tile *>(lds);
@@ -2173,7 +1584,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
     const uint4 *dq = reinterpret_cast<const uint4 *>(drow);
     uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
     uint4 npx = *reinterpret_cast<const uint4 *>(at(rowo));
-    constexpr int kLag = kLag1 ? 1 : 2;
+    constexpr int kLag = 2;
     for (int it = 0; it < mbw + 3 * kLag; ++it) {
       const int x = it - kLag * grp;
       const bool act = row_ok && x >= 0 && x < mbw;
@@ -2190,7 +1601,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
       // row waits until it may overwrite ring column x (the next wave's first
       // row read column x - kDpRingCols)
       if (act) {
-        const int need_up = (!kLag1 && grp == 0 && y > 0) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
+        const int need_up = (grp == 0 && y > 0) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
         const int need_dn = (grp == 3 && y + 1 < mbh) ? x - kDpRingCols + 1 : -(1 << 30);
         const int *pu = &prog[y > 0 ? y - 1 : 0], *pd = &prog[y + 1 < mbh ? y + 1 : y];
         while (__hip_atomic_load(pu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need_up ||
@@ -2206,7 +1617,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
           *reinterpret_cast<uint4 *>(&t.s[l][4]) = *reinterpret_cast<const uint4 *>(&L.s[l][0]);
         }
       };
-      if (!kLag1) load_above();
+      load_above();
       // ---- vertical edges: lane = sample row
       if (act && lrow && !still) {
         const uint32_t wv[5] = {x > 0 ? left : 0u, q4.x, q4.y, q4.z, q4.w};
@@ -2235,30 +1646,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
           *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
       }
       lane_sync();
-      if constexpr (kLag1) {
-        // the left macroblock's cols 12..15 are final now: rows 12..15 (chroma
-        // 6..7) of them complete its ring line for the row below
-        const int lr = row - (kRows - kTop);
-        if (act && lrow && !last_row && x > 0 && lr >= 0) {
-          const uint32_t w0 = still ? left : *reinterpret_cast<const uint32_t *>(&t.s[kTop + row][0]);
-          *reinterpret_cast<uint32_t *>(&ring[rs][(x - 1) & (kDpRingCols - 1)].s[lr][12]) = w0;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        if (act && l == 0 && !last_row)
-          __hip_atomic_store(&vprog[y], x, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // a wave's first row waits for the previous wave's last row to have
-        // filtered the vertical edges of macroblock x + 1 (the other rows'
-        // row above is the group before, one macroblock ahead in lockstep)
-        if (act && grp == 0 && y > 0) {
-          const int need = x + 1 < mbw ? x + 1 : mbw + 1;
-          while (__hip_atomic_load(&vprog[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        load_above();
-        lane_sync();
-      }
       // ---- horizontal edges: lane = sample column (chroma: interleaved byte column)
       if (act && !still) {
         const int pl = l & 1, seg = l >> 2;
@@ -2339,7 +1726,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
           if (!last_row && lr >= 0) {
             Line &C = ring[rs][x & (kDpRingCols - 1)];
             uint8_t *cur = &C.s[lr][0];
-            if (!kLag1 && x > 0) *reinterpret_cast<uint32_t *>(&ring[rs][(x - 1) & (kDpRingCols - 1)].s[lr][12]) = w0;
+            if (x > 0) *reinterpret_cast<uint32_t *>(&ring[rs][(x - 1) & (kDpRingCols - 1)].s[lr][12]) = w0;
             *reinterpret_cast<uint32_t *>(cur) = w1;
             *reinterpret_cast<uint32_t *>(cur + 4) = w2;
             *reinterpret_cast<uint32_t *>(cur + 8) = w3;
@@ -2364,25 +1751,18 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
       __builtin_amdgcn_wave_barrier();
       if (act && l == 0) {
         __hip_atomic_store(&prog[y], x + 1 < mbw ? x + 1 : mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (kLag1 && x == mbw - 1 && !last_row)  // the last macroblock's line is whole after the write-back
-          __hip_atomic_store(&vprog[y], mbw + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
   }
 }
 // grid: 2 x pictures of the level (even blocks luma, odd chroma)
-template <bool kLag1>
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kDpLds];
   __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
-  __shared__ int vprog[kLag1 ? 1024 : 1];  // kLag1: per row, the macroblock whose vertical pass is done
-  for (int i = threadIdx.x; i < a.P.mb_height; i += kDbkThreads) {
-    prog[i] = 0;
-    if (kLag1) vprog[i] = 0;
-  }
+  for (int i = threadIdx.x; i < a.P.mb_height; i += kDbkThreads) prog[i] = 0;
   __syncthreads();
-  if ((blockIdx.x & 1) == 0) dp_plane<true, kLag1>(a, static_cast<int>(blockIdx.x >> 1), lds, prog, vprog);
-  else dp_plane<false, kLag1>(a, static_cast<int>(blockIdx.x >> 1), lds, prog, vprog);
+  if ((blockIdx.x & 1) == 0) dp_plane<true>(a, static_cast<int>(blockIdx.x >> 1), lds, prog);
+  else dp_plane<false>(a, static_cast<int>(blockIdx.x >> 1), lds, prog);
 }
 
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
@@ -2415,21 +1795,10 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s, hipEv
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_intra_full launch: %s", hipGetErrorString(e));
   }
-  if (a.deblock >= 3) {
-    if (a.deblock == 4) hipLaunchKernelGGL(h264_deblock_plane<true>, dim3(2 * n_frames), dim3(kDbkThreads), 0, s, a);
-    else hipLaunchKernelGGL(h264_deblock_plane<false>, dim3(2 * n_frames), dim3(kDbkThreads), 0, s, a);
+  if (a.deblock) {
+    hipLaunchKernelGGL(h264_deblock_plane, dim3(2 * n_frames), dim3(kDbkThreads), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_plane launch: %s", hipGetErrorString(e));
-  } else if (a.deblock == 1) {
-    hipLaunchKernelGGL(h264_deblock_full, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_full launch: %s", hipGetErrorString(e));
-  } else if (a.deblock) {
-    const int k = a.dbk_bands > 1 ? a.dbk_bands : 1;
-    if (k > 1) hipLaunchKernelGGL(h264_deblock_lds<true>, dim3(n_frames * k), dim3(kDbkThreads), 0, s, a);
-    else hipLaunchKernelGGL(h264_deblock_lds<false>, dim3(n_frames), dim3(kDbkThreads), 0, s, a);
-    e = hipGetLastError();
-    if (e != hipSuccess) return fail(VTS_E_HIP, "h264_deblock_lds launch: %s", hipGetErrorString(e));
   }
   return VTS_OK;
 }

@@ -1,9 +1,10 @@
 // devmem.cpp — process-wide caching device allocator (devmem.h).
 //
 // Segments are hipMalloc'd blocks; a segment is cut into ranges.  A request
-// takes the smallest free range that holds it (any segment), splitting off the
-// rest as a new free range; a released range merges with its free neighbours
-// of the same segment.  Segments go back to HIP only when wholly free: on a
+// takes the smallest free range that holds it (any segment) when that range is
+// a close fit or the request is large (devmem.h), splitting off the rest as a
+// new free range; a released range merges with its free neighbours of the
+// same segment.  Segments go back to HIP only when wholly free: on a
 // failed hipMalloc (then one retry) or vts_empty_cache().
 #include "devmem.h"
 
@@ -18,6 +19,7 @@ namespace {
 
 constexpr size_t kCacheMin = 64 << 10;  // smaller blocks go straight to / back to HIP
 constexpr size_t kRound = 2 << 20;      // ranges are multiples of 2 MiB (so they stay 2 MiB aligned)
+constexpr size_t kCarveMin = size_t(256) << 20;  // requests this large may be cut from any larger free range
 
 struct Range {
   size_t n;
@@ -86,13 +88,19 @@ hipError_t dmalloc_raw(void **p, size_t n) {
   std::lock_guard<std::mutex> lk(g_mu);
   Device &d = g_dev[dev];
   auto it = d.free_by_size.lower_bound(want);
-  if (it != d.free_by_size.end()) {
+  // a close fit, or a large request (a fresh hipMalloc of recycled memory
+  // waits for the driver's clear): take it from the cache
+  if (it != d.free_by_size.end() && (it->first <= 2 * want || it->first <= want + (64u << 20) || want >= kCarveMin)) {
     *p = take_locked(d, it->second, want);
     return hipSuccess;
   }
   e = hipMalloc(p, want);
   if (e != hipSuccess) {
     (void)hipGetLastError();
+    if (it != d.free_by_size.end()) {  // no fresh memory: carve the large range after all
+      *p = take_locked(d, it->second, want);
+      return hipSuccess;
+    }
     release_free_segments_locked(d);
     e = hipMalloc(p, want);
     if (e != hipSuccess) return e;

@@ -5,10 +5,15 @@
 // waits while the driver clears it (vts_open of the general decoder after a
 // closed session: 4-6 s in the allocation stage, against 7 ms on fresh
 // memory; profiles/r04c_open_stages.json), so released blocks of >= 64 KiB
-// stay mapped in a per-device cache and the next session takes them back
-// (best fit, at most twice the size asked for).  A failed hipMalloc empties
-// the device's cache and tries once more.  Window sizing counts cached bytes
-// as free (vts::dmem_free).  vts_empty_cache() hands the cache back.
+// stay mapped in a per-device cache and the next session takes them back.
+// Placement: the smallest free range that holds the request; a range more
+// than twice the request (and 64 MiB over it) is carved only for requests of
+// >= 256 MiB, or when a fresh hipMalloc fails, so small buffers do not pin a
+// large cached segment (a segment goes back to HIP only when wholly free).  A
+// failed hipMalloc empties the device's wholly free segments and tries once
+// more.  Window sizing counts cached bytes as free (vts::dmem_free: the free
+// ranges, which large requests may carve).  vts_empty_cache() hands the
+// cache back.
 #pragma once
 #include <hip/hip_runtime_api.h>
 

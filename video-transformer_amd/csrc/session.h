@@ -187,22 +187,12 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
-  int dbk_kernel = 3;                   // 3: h264_deblock_plane; VTS_DBK=2: h264_deblock_lds, 1: h264_deblock_full
-  int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full
-  int dbk_bands = 1;                    // h264_deblock_lds workgroups per picture (VTS_DBK_BANDS, 1..4)
+  int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full (its LDS fallback)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
-  // where the general decoder derives bS (VTS_BS): 0 one launch for the
-  // window at the head of the level chain, 1 in each level's inter launch,
-  // 2 one launch per level on the score stream, paced by the chain (level
-  // l + 1's after level l's inter launch)
-  int bs_mode = 2;
-  std::vector<hipEvent_t> ev_bs;  // bs_mode 2: two per level launch of a window (reused window to window)
+  std::vector<hipEvent_t> ev_bs;  // paced bS: two per level launch of a window (reused window to window)
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock
-  uint8_t *d_dbkx[2] = {nullptr, nullptr};       // dbk_bands > 1: rows handed between deblocking bands
-  uint32_t *d_dbk_tix = nullptr;                 // ... one ticket counter per level launch of a window
-  int64_t dbk_tix_n = 0;
   int16_t *d_arena[2] = {nullptr, nullptr};
   int64_t arena_blocks = 0;             // per ring
   // kept from open for a later switch to the general decoder (decoder = auto)

@@ -257,10 +257,7 @@ int alloc_general(vts_ctx *c) {
   if (!c->pneed.empty())
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
   if (const char *e = std::getenv("VTS_PARSE_MERGE")) c->parse_merged = std::atoi(e) != 0;
-  if (const char *e = std::getenv("VTS_DBK")) c->dbk_kernel = std::min(4, std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("VTS_INTRA")) c->intra_kernel = std::atoi(e) == 1 ? 1 : 2;
-  if (const char *e = std::getenv("VTS_DBK_BANDS")) c->dbk_bands = std::min(4, std::max(1, std::atoi(e)));
-  if (const char *e = std::getenv("VTS_BS")) c->bs_mode = std::min(2, std::max(0, std::atoi(e)));
   HIP_TRY(vts::dmalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
@@ -276,12 +273,6 @@ int alloc_general(vts_ctx *c) {
     HIP_TRY(vts::dmalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
     HIP_TRY(vts::dmalloc(&c->d_pdone[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
     HIP_TRY(vts::dmalloc(&c->d_dbk[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(DbkInfo)));
-    if (c->dbk_bands > 1) {  // [slot][boundary]: a 64-byte counter + one DbkLine per column
-      const size_t xb = static_cast<size_t>(c->ring_frames) * (c->dbk_bands - 1) *
-                        (static_cast<size_t>(c->sps.mb_width) * sizeof(DbkLine) + 64);
-      HIP_TRY(vts::dmalloc(&c->d_dbkx[r], xb));
-      HIP_TRY(hipMemset(c->d_dbkx[r], 0, xb));
-    }
     HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
     HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
     HIP_TRY(vts::dmalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
@@ -384,7 +375,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   c->k = c->params.k > 0 ? c->params.k : (c->height <= 720 ? 4 : 6);
   {
     // h264_recon_score<k>: k in {2,4,8}, display = coded size;
-    // h264_recon_score6: k = 6, any cropping, thumbnail width % 8 == 0
+    // h264_recon_score6b: k = 6, any cropping, thumbnail width % 8 == 0
     const bool can_fuse = ((c->k == 2 || c->k == 4 || c->k == 8) && c->width == c->coded_w &&
                            c->height == c->coded_h) ||
                           (c->k == 6 && (c->width / 6) % 8 == 0);
@@ -1302,14 +1293,12 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_porder);
   f(c->d_porder_m);
   f(c->d_pneed);
-  f(c->d_dbk_tix);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);
     f(c->d_ilvl[r]);
     f(c->d_pdone[r]);
     f(c->d_dbk[r]);
-    f(c->d_dbkx[r]);
     f(c->d_arena[r]);
   }
   for (auto e : c->ev)

@@ -413,40 +413,28 @@ int run_general(vts_ctx *c) {
     ra.uv_off = static_cast<int64_t>(c->pitch) * c->coded_h;
     ra.pitch = c->pitch;
     ra.epoch = epoch;
-    ra.deblock = c->dbk_kernel;
+    ra.deblock = 1;
     ra.intra_kernel = c->intra_kernel;
-    ra.dbk_bands = c->d_dbkx[r] ? c->dbk_bands : 1;
-    ra.dbkx = c->d_dbkx[r];
     ra.err = c->d_err;
     ra.sct = c->d_scale;
     ra.P = c->fprm;
-    if (ra.dbk_bands > 1 && !w.lvl_off.empty()) {  // the deblocking launches' ticket counters, zeroed
-      const int64_t nl = static_cast<int64_t>(w.lvl_off.size());
-      if (c->dbk_tix_n < nl) {
-        vts::dfree(c->d_dbk_tix);
-        c->d_dbk_tix = nullptr;
-        HIP_TRY(vts::dmalloc(&c->d_dbk_tix, sizeof(uint32_t) * static_cast<size_t>(nl)));
-        c->dbk_tix_n = nl;
-      }
-      HIP_TRY(hipMemsetAsync(c->d_dbk_tix, 0, sizeof(uint32_t) * static_cast<size_t>(nl), sd));
-    }
-    // bS needs only the parse's records (vts_ctx::bs_mode)
-    const int bsm = w.lvl_off.empty() ? 0 : c->bs_mode;
-    ra.bs_fused = bsm == 1 ? 1 : 0;
+    // bS needs only the parse's records: one launch per level on the score
+    // stream, paced by the chain (level l + 1's after level l's inter launch),
+    // beside the intra and deblocking launches that leave most compute units
+    // idle.  (Measured and dropped, DESIGN.md §9: one window-wide launch at the
+    // head of the chain that both GOP groups waited for; bS inside each inter
+    // launch.)
+    const bool paced = !w.lvl_off.empty();
     auto bs_level = [&](size_t l, hipStream_t s) {
       ra.frames = c->d_levels + w.lvl_off[l];
       return bs_full_launch(ra, w.lvl_cnt[l], s);
     };
-    if (bsm == 0 && !w.lvl_off.empty()) {
-      ra.frames = c->d_levels + w.lvl_off[0];
-      VTS_TRY(bs_full_launch(ra, static_cast<int>(w.lvl_off.back() + w.lvl_cnt.back() - w.lvl_off[0]), sd));
-    }
-    if (ng > 1) {  // groups >= 1 on their own streams, after the parse (and bS in mode 0)
+    if (ng > 1) {  // groups >= 1 on their own streams, after the parse
       HIP_TRY(hipEventRecord(c->ev_grp[0], sd));
       for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], c->ev_grp[0], 0));
     }
     // the groups' level launches, interleaved (j-th level of every group, then
-    // the next): in mode 2 the score stream derives level j + 1's bS while
+    // the next): the score stream derives level j + 1's bS while
     // group g runs level j's intra and deblocking launches (compute units the
     // one-workgroup-per-picture kernels leave idle), and level j + 1 waits for it
     // (one side stream for every group: the groups' bS on separate streams,
@@ -461,7 +449,7 @@ int run_general(vts_ctx *c) {
       hi[static_cast<size_t>(g)] = g + 1 < ng ? static_cast<size_t>(w.grp[static_cast<size_t>(g)]) : w.lvl_off.size();
       jmax = std::max(jmax, hi[static_cast<size_t>(g)] - lo[static_cast<size_t>(g)]);
     }
-    if (bsm == 2) {
+    if (paced) {
       if (c->ev_bs.size() < 2 * w.lvl_off.size()) {
         const size_t n0 = c->ev_bs.size();
         c->ev_bs.resize(2 * w.lvl_off.size(), nullptr);
@@ -479,10 +467,9 @@ int run_general(vts_ctx *c) {
         const size_t l = lo[static_cast<size_t>(g)] + jj;
         if (l >= hi[static_cast<size_t>(g)]) continue;
         hipStream_t s = g ? c->s_grp[g - 1] : sd;
-        if (bsm == 2) HIP_TRY(hipStreamWaitEvent(s, c->ev_bs[2 * l], 0));
+        if (paced) HIP_TRY(hipStreamWaitEvent(s, c->ev_bs[2 * l], 0));
         ra.frames = c->d_levels + w.lvl_off[l];
-        ra.dbk_tix = c->d_dbk_tix ? c->d_dbk_tix + l : nullptr;
-        const bool next = bsm == 2 && l + 1 < hi[static_cast<size_t>(g)];
+        const bool next = paced && l + 1 < hi[static_cast<size_t>(g)];
         VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], s, next ? c->ev_bs[2 * l + 1] : nullptr));
         if (next) {
           HIP_TRY(hipStreamWaitEvent(sb_of(g), c->ev_bs[2 * l + 1], 0));

@@ -1024,8 +1024,14 @@ int dev_alloc(T **p, size_t n) {
   return VTS_OK;
 }
 
-struct DevBufs {  // transcode scratch, freed on every exit path
+// Transcode scratch, freed on every exit path.  vts::dfree hands a range
+// straight back to the process-wide cache (no implicit device synchronisation
+// as with hipFree), so the streams whose kernels may still use the buffers
+// are drained first: an early return after the searches were queued must not
+// let a later allocation reuse memory those kernels still write.
+struct DevBufs {
   std::vector<void *> ptrs;
+  std::vector<hipStream_t> streams;  // synchronised before anything is freed
   template <class T>
   int get(T **p, size_t n) {
     VTS_TRY(dev_alloc(p, n));
@@ -1033,6 +1039,7 @@ struct DevBufs {  // transcode scratch, freed on every exit path
     return VTS_OK;
   }
   ~DevBufs() {
+    for (hipStream_t s : streams) (void)hipStreamSynchronize(s);
     for (void *p : ptrs) vts::dfree(p);
   }
 };
@@ -1248,6 +1255,7 @@ extern "C" int vts_transcode(vts_ctx *c, const char *out_path, const vts_transco
   // drain to the host) runs on s2 behind the chunk's last search event,
   // overlapping the searches of later chunks.
   hipStream_t s1 = c->s_dec, s2 = c->s_score;
+  B.streams = {s1, s2};
   HIP_TRY(hipMemcpy(d_sent, sent.data(), sent.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(d_went, went.data(), went.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_TRY(hipMemsetAsync(d_stats, 0, 3 * sizeof(unsigned long long), s2));
