@@ -1,7 +1,8 @@
 // CPU harness of the general device decoder: the product's host scheduler
-// (h264_sched.cpp) and the very per-slice parser / per-macroblock
-// reconstruction and deblocking code the GPU kernels run (parse_full.h,
-// recon_full.h), driven in the kernels' order — inter macroblocks first,
+// (h264_sched.cpp) and the very per-slice parser / per-picture derivation /
+// per-macroblock reconstruction and deblocking code the GPU kernels run
+// (parse_full.h, parse_cabac.h, derive_full.h, recon_full.h), driven in the
+// kernels' order — inter macroblocks first,
 // intra macroblocks and deblocking along the x + 2y wavefront — on host
 // memory.  TEST INFRASTRUCTURE (tests/test_full_host.py compares it with the
 // oracle); the product never runs the decoder on the CPU.
@@ -28,6 +29,7 @@ extern "C" void fh_stats(unsigned long long *out) {
 #include "mp4.h"
 #include "parse_cabac.h"
 #include "parse_full.h"
+#include "derive_full.h"
 #include "recon_full.h"
 #include "intra_lanes.h"
 
@@ -258,28 +260,63 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
     const SchedFrame &fr = frames[static_cast<size_t>(fi)];
     MbRec *fr_recs = recs.data() + static_cast<size_t>(fi) * nmb;
     uint32_t errs = 0;
+    MbRecB *fr_recs1 = bframes ? recs1.data() + static_cast<size_t>(fi) * nmb : nullptr;
+    uint16_t *fr_ilvl = ilvl.data() + static_cast<size_t>(fi) * nmb;
     for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
-      full::FullScratch sc;
       const FullSlice &fsl = fs[static_cast<size_t>(si)];
-      full::BCtx bc{};
-      bc.recs1 = bframes ? recs1.data() + static_cast<size_t>(fi) * nmb : nullptr;
-      bc.x = fsl.ext >= 0 ? &exts[static_cast<size_t>(fsl.ext)] : nullptr;
-      if (fsl.is_p == kSliceB) {
-        const int col = exts[static_cast<size_t>(fsl.ext)].ref_slot1[0];
-        bc.col = recs.data() + static_cast<size_t>(col) * nmb;
-        bc.col1 = recs1.data() + static_cast<size_t>(col) * nmb;
-      }
+      const SliceExt *x = fsl.ext >= 0 ? &exts[static_cast<size_t>(fsl.ext)] : nullptr;
       // the device's nal_unescape, serially: the payload's RBSP (+ zero padding)
       std::vector<uint8_t> rbsp(static_cast<size_t>(fsl.nal_size) + 128, 0);
       const int32_t rlen = full::unescape_nal(es.data() + fsl.nal_offset + 1, fsl.nal_size - 1, rbsp.data());
-      errs |= P.cabac ? full::parse_slice_cabac(rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, fr_recs,
-                                                ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(), epoch, &sc,
-                                                bc)
-                      : full::parse_slice_full(rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, fr_recs,
-                                               ilvl.data() + static_cast<size_t>(fi) * nmb, arena.data(), epoch, &sc,
-                                               bc);
+      if (P.cabac) {
+        // the kernel's LDS: scratch + one SynEdge per macroblock column
+        std::vector<uint64_t> lds((full::syn_lds_bytes(mbw) + 7) / 8);
+        errs |= full::parse_slice_cabac(rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, fr_recs, fr_recs1, x,
+                                        arena.data(), epoch, reinterpret_cast<full::SynScratch *>(lds.data()));
+      } else {
+        full::FullScratch sc;
+        full::BCtx bc{};
+        bc.recs1 = fr_recs1;
+        bc.x = x;
+        if (fsl.is_p == kSliceB) {
+          const int col = exts[static_cast<size_t>(fsl.ext)].ref_slot1[0];
+          bc.col = recs.data() + static_cast<size_t>(col) * nmb;
+          bc.col1 = recs1.data() + static_cast<size_t>(col) * nmb;
+        }
+        errs |= full::parse_slice_full(rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, fr_recs, fr_ilvl,
+                                       arena.data(), epoch, &sc, bc);
+      }
     }
     if (errs) return bad("frame " + std::to_string(fi) + ": parse: " + describe_decode_error(errs));
+    if (P.cabac) {
+      // h264_derive's per-macroblock work in raster order (every neighbour
+      // precedes), the colocated pictures derived earlier (decoding order)
+      full::DeriveCtx dc{};
+      dc.recs = fr_recs;
+      dc.recs1 = fr_recs1;
+      dc.ilvl = fr_ilvl;
+      dc.ring = recs.data();
+      dc.ring1 = bframes ? recs1.data() : nullptr;
+      dc.slices = fs.data();
+      dc.exts = exts.data();
+      dc.mbw = mbw;
+      dc.mbh = mbh;
+      dc.epoch = epoch;
+      dc.cip = P.cip;
+      dc.direct8x8 = P.direct8x8;
+      dc.bframes = P.bframes;
+      std::vector<full::DEdge> er(static_cast<size_t>(nmb)), eb(static_cast<size_t>(nmb));
+      full::DWork w;
+      for (int a = 0; a < nmb; ++a) {
+        const int x = a % mbw, y = a / mbw;
+        const full::DEdge *A = x > 0 ? &er[static_cast<size_t>(a - 1)] : nullptr;
+        const full::DEdge *B = y > 0 ? &eb[static_cast<size_t>(a - mbw)] : nullptr;
+        const full::DEdge *C = y > 0 && x + 1 < mbw ? &eb[static_cast<size_t>(a - mbw + 1)] : nullptr;
+        const full::DEdge *D = y > 0 && x > 0 ? &eb[static_cast<size_t>(a - mbw - 1)] : nullptr;
+        errs |= full::derive_mb(dc, a, A, B, C, D, w, &er[static_cast<size_t>(a)], &eb[static_cast<size_t>(a)]);
+      }
+      if (errs) return bad("frame " + std::to_string(fi) + ": derive: " + describe_decode_error(errs));
+    }
     full::ReconCtx c{};
     c.recs = fr_recs;
     c.recs1 = bframes ? recs1.data() + static_cast<size_t>(fi) * nmb : nullptr;

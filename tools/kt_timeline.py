@@ -14,7 +14,7 @@ RECON = ("h264_inter_full", "h264_intra_v2", "h264_intra_full", "h264_bs_full", 
 
 
 def short(name):
-    for k in RECON + ("h264_parse_full_cabac", "h264_parse_full", "nal_unescape"):
+    for k in RECON + ("h264_parse_full_cabac", "h264_parse_full", "h264_derive", "nal_unescape"):
         if k in name:
             return k
     return name.split("(")[0][-40:]

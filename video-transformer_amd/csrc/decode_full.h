@@ -32,6 +32,21 @@ struct FullParseArgs {
   FullParams P;
 };
 
+// h264_derive: complete the CABAC parse's syntax records of n pictures (their
+// colocated pictures completed by an earlier launch)
+struct DeriveArgs {
+  const int32_t *slots;      // ring slot of picture i of the launch
+  MbRec *recs;               // ring: [slot][mb]
+  MbRecB *recs1;             // ring: [slot][mb] list-1 halves (P.bframes), else null
+  uint16_t *ilvl;            // ring: [slot][mb] intra dependency levels (written)
+  const FullSlice *slices;   // the window's slices (MbRec.slice)
+  const SliceExt *exts;      // the window's SliceExt records
+  uint32_t *err;
+  uint32_t epoch;
+  int32_t _pad;
+  FullParams P;
+};
+
 // per macroblock deblocking descriptor (h264_bs_full -> h264_deblock_plane)
 struct DbkInfo {
   uint32_t bs[4];   // bS of edge e (0 = the macroblock edge; 0 when it is not filtered) of direction
@@ -77,6 +92,7 @@ struct FullReconArgs {
 int nal_unescape_launch(const uint8_t *es, uint8_t *rbsp, const FullSlice *slices, int32_t n_slices,
                         int32_t *rbsp_len, hipStream_t s);
 int parse_full_launch(const FullParseArgs &a, hipStream_t s);
+int derive_launch(const DeriveArgs &a, int n_pictures, hipStream_t s);
 // deblocking descriptors (bS, QPs) of n_frames pictures: reads only the
 // parse's records, so one launch covers a whole window
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);

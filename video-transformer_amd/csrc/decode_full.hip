@@ -2,9 +2,13 @@
 // 4x4 / 16x16 / chroma prediction, residuals, quarter-sample motion over up to
 // 16 references, the deblocking filter).  DESIGN.md §5b.
 //
-//   h264_parse_full   one lane per slice: slice_data() -> MbRec + coefficient
-//   h264_parse_full_cabac  blocks + intra dependency level (parse_full.h,
-//                     parse_cabac.h), one kernel per entropy mode
+//   h264_parse_full   one wave per slice: slice_data() -> MbRec + coefficient
+//                     blocks + intra dependency level (CAVLC, parse_full.h)
+//   h264_parse_full_cabac  one wave per slice: CABAC slice_data() -> syntax
+//                     records + coefficient blocks (parse_cabac.h)
+//   h264_derive       one workgroup per picture, one lane per macroblock row
+//                     on the x + 2y wavefront: motion, intra modes and
+//                     levels from the syntax records (derive_full.h)
 //   h264_inter_full   one lane per 4x4 luma block (+ its 2x2 Cb/Cr) of every
 //                     inter / skip / I_PCM macroblock of every picture of the
 //                     level: 6-tap / bilinear prediction from dword windows,
@@ -87,6 +91,7 @@ struct RProf {
 #define RPROF_FLUSH(base) rp_.flush(base)
 #include "parse_cabac.h"
 #include "parse_full.h"
+#include "derive_full.h"
 #include "recon_full.h"
 #include "intra_lanes.h"
 
@@ -119,8 +124,11 @@ constexpr int kDbkWaves = kDbkThreads / 64;
 #endif
 // The entropy mode is per stream, so each mode is its own kernel: a wave only
 // ever runs one parser's code, and each fits the instruction cache better.
-template <bool kCabac>
-__device__ __forceinline__ void parse_one(const FullParseArgs &a, full::FullScratch *scratch) {
+// CAVLC (parse_full.h) derives motion, modes and levels inline and a B slice
+// waits for its colocated picture's records; CABAC (parse_cabac.h) writes
+// syntax records only, completed per picture by h264_derive, so its slices
+// are independent.
+__device__ __forceinline__ void parse_one_cavlc(const FullParseArgs &a, full::FullScratch *scratch) {
   const int i = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
@@ -149,15 +157,9 @@ __device__ __forceinline__ void parse_one(const FullParseArgs &a, full::FullScra
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the colocated records, across XCD L2s
     }
   }
-  const uint8_t *rbsp = a.rbsp + s.nal_offset + 1;
-  const int32_t len = a.rbsp_len[i];
-  uint32_t e;
-  if constexpr (kCabac)
-    e = full::parse_slice_cabac(rbsp, len, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
-                                a.ilvl + s.slot * nmb, a.arena, a.epoch, scratch, bc);
-  else
-    e = full::parse_slice_full(rbsp, len, s, static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
-                               a.ilvl + s.slot * nmb, a.arena, a.epoch, scratch, bc);
+  const uint32_t e = full::parse_slice_full(a.rbsp + s.nal_offset + 1, a.rbsp_len[i], s,
+                                            static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
+                                            a.ilvl + s.slot * nmb, a.arena, a.epoch, scratch, bc);
   if (e) atomicOr(a.err, e);
   if (a.pdone) {  // this slice's records are out (every path, errors included)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -172,12 +174,67 @@ __device__ __forceinline__ void parse_one(const FullParseArgs &a, full::FullScra
 __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full(FullParseArgs a) {
   __shared__ full::FullScratch scratch;
-  parse_one<false>(a, &scratch);
+  parse_one_cavlc(a, &scratch);
 }
+// dynamic LDS: full::syn_lds_bytes(mb_width) (SynScratch + the row of top edges)
 __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full_cabac(FullParseArgs a) {
-  __shared__ full::FullScratch scratch;
-  parse_one<true>(a, &scratch);
+  extern __shared__ __attribute__((aligned(16))) uint8_t syn_lds[];
+  const int i = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
+  const FullSlice &s = a.slices[i];
+  const FullParams P = a.P;
+  const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
+  const uint32_t e = full::parse_slice_cabac(a.rbsp + s.nal_offset + 1, a.rbsp_len[i], s,
+                                             static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
+                                             P.bframes ? a.recs1 + s.slot * nmb : nullptr,
+                                             s.ext >= 0 ? a.exts + s.ext : nullptr, a.arena, a.epoch,
+                                             reinterpret_cast<full::SynScratch *>(syn_lds));
+  if (e) atomicOr(a.err, e);
+}
+
+// One workgroup per picture, one lane per macroblock row: at step t row y
+// derives macroblock x = t - 2y (derive_full.h), so the row above has
+// finished x - 1, x and x + 1 (its bottom edges in an LDS ring of four
+// columns per row) and the lane's own previous macroblock is its left edge;
+// a barrier per step.  Dynamic LDS: derive_lds_bytes.
+__global__ void __launch_bounds__(256) h264_derive(DeriveArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
+  const int mbw = a.P.mb_width, mbh = a.P.mb_height;
+  const int64_t nmb = static_cast<int64_t>(mbw) * mbh;
+  const int slot = a.slots[blockIdx.x];
+  full::DWork *work = reinterpret_cast<full::DWork *>(dlds);                   // [blockDim]
+  full::DEdge *ring = reinterpret_cast<full::DEdge *>(work + blockDim.x);      // [mbh][4]
+  full::DEdge *left = ring + 4 * mbh;                                          // [mbh]
+  full::DeriveCtx c;
+  c.recs = a.recs + slot * nmb;
+  c.recs1 = a.P.bframes ? a.recs1 + slot * nmb : nullptr;
+  c.ilvl = a.ilvl + slot * nmb;
+  c.ring = a.recs;
+  c.ring1 = a.recs1;
+  c.slices = a.slices;
+  c.exts = a.exts;
+  c.mbw = mbw;
+  c.mbh = mbh;
+  c.epoch = a.epoch;
+  c.cip = a.P.cip;
+  c.direct8x8 = a.P.direct8x8;
+  c.bframes = a.P.bframes;
+  const int y = static_cast<int>(threadIdx.x);
+  uint32_t err = 0;
+  const int steps = mbw + 2 * (mbh - 1);
+  for (int t = 0; t < steps; ++t) {
+    const int x = t - 2 * y;
+    if (y < mbh && x >= 0 && x < mbw) {
+      const full::DEdge *A = x > 0 ? &left[y] : nullptr;
+      const full::DEdge *B = y > 0 ? &ring[4 * (y - 1) + (x & 3)] : nullptr;
+      const full::DEdge *C = y > 0 && x + 1 < mbw ? &ring[4 * (y - 1) + ((x + 1) & 3)] : nullptr;
+      const full::DEdge *D = y > 0 && x > 0 ? &ring[4 * (y - 1) + ((x - 1) & 3)] : nullptr;
+      // the right edge replaces the left one (derive_mb writes its edges last)
+      err |= full::derive_mb(c, y * mbw + x, A, B, C, D, work[y], &left[y], &ring[4 * y + (x & 3)]);
+    }
+    __syncthreads();
+  }
+  if (err) atomicOr(a.err, err);
 }
 
 // 7.4.1: one workgroup per slice NAL, 256 payload bytes per step; a byte is
@@ -1505,10 +1562,30 @@ int nal_unescape_launch(const uint8_t *es, uint8_t *rbsp, const FullSlice *slice
 
 int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
   if (a.n_slices <= 0) return VTS_OK;
-  if (a.P.cabac) hipLaunchKernelGGL(h264_parse_full_cabac, dim3(a.n_slices), dim3(64), 0, s, a);
-  else hipLaunchKernelGGL(h264_parse_full, dim3(a.n_slices), dim3(64), 0, s, a);
+  if (a.P.cabac) {
+    const size_t lds = full::syn_lds_bytes(a.P.mb_width);
+    if (lds > 60 * 1024) return fail(VTS_E_UNSUPPORTED, "picture wider than the CABAC parser's LDS row allows");
+    hipLaunchKernelGGL(h264_parse_full_cabac, dim3(a.n_slices), dim3(64), lds, s, a);
+  } else {
+    hipLaunchKernelGGL(h264_parse_full, dim3(a.n_slices), dim3(64), 0, s, a);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_parse_full launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
+size_t derive_lds_bytes(int mb_height) {
+  const int threads = 64 * ((mb_height + 63) / 64);
+  return sizeof(full::DWork) * static_cast<size_t>(threads) + sizeof(full::DEdge) * 5 * static_cast<size_t>(mb_height);
+}
+
+int derive_launch(const DeriveArgs &a, int n_pictures, hipStream_t s) {
+  if (n_pictures <= 0) return VTS_OK;
+  if (a.P.mb_height > 256) return fail(VTS_E_UNSUPPORTED, "picture taller than 256 macroblock rows (h264_derive)");
+  const int threads = 64 * ((a.P.mb_height + 63) / 64);
+  hipLaunchKernelGGL(h264_derive, dim3(n_pictures), dim3(threads), derive_lds_bytes(a.P.mb_height), s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_derive launch: %s", hipGetErrorString(e));
   return VTS_OK;
 }
 

@@ -137,9 +137,10 @@ std::string describe_decode_error(uint32_t f) {
       "active deblocking filter", "unknown PPS id", "macroblock not covered by any slice",
       "emulation prevention inside I_PCM samples", "reference list modification",
       "P slice without reference frame", "adaptive reference marking (MMCO)",
-      "B slice's wait for its colocated picture's parse timed out"};
+      "B slice's wait for its colocated picture's parse timed out",
+      "coefficient arena range of a slice exceeded"};
   std::string s;
-  for (int i = 0; i < 14; ++i)
+  for (int i = 0; i < 15; ++i)
     if (f & (1u << i)) {
       if (!s.empty()) s += ", ";
       s += names[i];

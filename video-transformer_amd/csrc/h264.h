@@ -81,6 +81,8 @@ enum DecodeError : uint32_t {
   DEC_E_NO_REF = 1u << 11,        // P slice without a preceding reference
   DEC_E_MMCO = 1u << 12,          // adaptive reference marking
   DEC_E_COL_WAIT = 1u << 13,      // merged parse: a B slice's wait for its colocated picture timed out
+  DEC_E_ARENA = 1u << 14,         // a slice's coefficient blocks overflowed its arena range (the host
+                                  // re-runs the window with the provable bound)
   // not an error: a level-blocked reconstruct launch met a motion vector
   // reaching beyond its halo; the host re-runs with per-level launches
   DEC_W_LEVEL_RANGE = 1u << 31,

@@ -1,18 +1,38 @@
-// parse_cabac.h — CABAC slice_data() parser of the general device decoder
-// (ITU-T H.264 9.3): High-profile I, P and B slices with 8x8 transforms.  The
-// kernel (h264_parse_full) runs one slice per single-lane wave, so the whole
-// arithmetic decoder is wave-uniform scalar code; the CPU harness compiles the
-// same header.  It produces exactly what the CAVLC parser produces (MbRec,
-// coefficient blocks, intra dependency level) plus, for the reconstruction,
-// transform_size_8x8_flag (MbRec.modes bit 4) and 8x8 coefficient blocks.
+// parse_cabac.h — CABAC slice_data() SYNTAX parser of the general device
+// decoder (ITU-T H.264 9.3): High-profile I, P and B slices with 8x8
+// transforms.  The kernel (h264_parse_full_cabac) runs one slice per wave;
+// the whole arithmetic decoder is wave-uniform scalar code, and the CPU
+// harness compiles the same header.
 //
-// Context states and the engine's tables live in lane tables (LaneTab: the
-// idle lanes of a few VGPRs, read and written with v_readlane / v_writelane),
-// so a bin costs no memory access.  The
-// neighbour facts CABAC's context selection needs come through the CAVLC
-// parser's LDS neighbour copies: coded_block_flag bits in the (CAVLC-only)
-// nzc bytes, clamped |mvd| of inter macroblocks' bottom rows in their i4
-// bytes, the neighbourhood's |mvd| in FullScratch.mvx.
+// The serial per-slice wave decodes bins and nothing else: the syntax
+// elements, the coefficient blocks, and the few neighbour facts CABAC's
+// context selection reads (9.3.3.1.1: mb types, cbp, coded_block_flag bits,
+// |mvd|, refIdx > 0, transform / chroma-mode flags of the macroblocks to the
+// left and above).  Those facts cross macroblock edges as 20-byte SynEdge
+// records in LDS: the left one from the previous macroblock, the top ones in
+// a per-column row of the wave's LDS that the slice itself fills — no record
+// of another macroblock is ever read back from global memory.  Everything
+// the standard derives from syntax plus decoded neighbours — motion-vector
+// prediction (8.4.1.3), P_Skip (8.4.1.1), direct prediction (8.4.1.2),
+// Intra4x4 / 8x8 prediction modes (8.3.1.1 / 8.3.2.1), reference slots, the
+// intra dependency level — is left to the per-picture wavefront kernel
+// h264_derive (derive_full.h), so a B slice no longer waits for its
+// colocated picture's parse either.
+//
+// What the parse writes per macroblock, in the MbRec / MbRecB layout that
+// h264_derive completes in place (the "syntax record"):
+//   type, qp, cbp, modes, coef / blocks, nz, nzc (coded_block_flag bits) —
+//     final;
+//   ref[4] / ref1[4]: ref_idx_l0 / l1 per 8x8 quadrant as coded (-1 where the
+//     partition does not use the list; direct quadrants -1); direct (MbRecB);
+//   mv[16] / mv1[16]: mvd_l0 / l1 of the (sub-)partition covering each 4x4
+//     block (0 for skipped / direct / intra blocks);
+//   i4[8]: I_NxN — per 4x4 block (Intra_8x8: at the 8x8's top-left 4x4) the
+//     nibble 8 | 0 for prev_intra_pred_mode_flag = 1, else rem_intra_pred_mode;
+//     inter — i4[0] the partition shape (0 16x16, 1 16x8, 2 8x16, 3 8x8),
+//     i4[1] the partitions' prediction (2 bits each: 0 direct, 1 L0, 2 L1,
+//     3 Bi), i4[2] the sub-partition shapes (2 bits per 8x8: 0 8x8, 1 8x4,
+//     2 4x8, 3 4x4).
 #pragma once
 #include <cstdint>
 #include <type_traits>
@@ -70,9 +90,8 @@ VTS_HD VTS_INLINE int abs_off(int cat) { return static_cast<int>((0x271E140A00ul
 // compute unit) instead of the one scalar unit that every wave of the compute
 // unit shares, which the parser saturates; a decision's outcome, next state
 // and renormalisation shift come back to the scalar side by readfirstlane
-// (CABAC B parse -4 % same-box, profiles/r03_cabac_vgpr_engine_ab.txt;
-// VTS_EXP_SENGINE keeps the scalar engine)
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(VTS_EXP_SENGINE)
+// (CABAC B parse -4 % same-box, profiles/r03_cabac_vgpr_engine_ab.txt)
+#if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint32_t vts_in_vgpr(uint32_t x) {
   uint32_t r;
   asm("; engine state in a VGPR" : "=v"(r) : "0"(x));
@@ -85,7 +104,77 @@ __device__ __forceinline__ uint32_t vts_in_vgpr(uint32_t x) {
 #define VTS_EU(x) (x)
 #endif
 
-struct CabacParser : Parser {
+// ------------------------------------------------------- neighbour facts
+// What the macroblock to the right (its left edge) or below (its top edge)
+// reads of a macroblock for context selection, as bit fields of SynEdge::f.
+// "Along the edge" = the 4x4 blocks / 8x8 quadrants touching it: the right
+// column (raster 3, 7, 11, 15; quadrants 1, 3; chroma blocks 1, 3) or the
+// bottom row (raster 12..15; quadrants 2, 3; chroma blocks 2, 3), index k in
+// order.  I_PCM is stored as cbp luma 15 / chroma 2 and every
+// coded_block_flag set, which gives exactly the standard's I_PCM rules below.
+enum : uint32_t {
+  kEType = 7u,          // bits 0-2: kMb* type
+  kECbpSh = 3,          // bits 3-8: coded_block_pattern
+  kET8 = 1u << 9,       // transform_size_8x8_flag
+  kEChroma = 1u << 10,  // I_NxN / Intra_16x16 with intra_chroma_pred_mode != 0
+  kEDirect16 = 1u << 11,  // B_Skip / B_Direct_16x16
+  kERefSh = 12,         // bits 12 + 2 l + k: refIdxLX > 0 of edge quadrant k (explicitly coded only)
+  kECbfSh = 16,         // bits 16 + k: luma 4x4 coded_block_flag along the edge
+  kECbfDc = 1u << 20,   // Intra16x16DCLevel coded_block_flag
+  kECdcSh = 21,         // bits 21 + iCbCr: chroma DC coded_block_flag
+  kECacSh = 23,         // bits 23 + 2 iCbCr + k: chroma AC coded_block_flag along the edge
+};
+struct SynEdge {
+  uint32_t f;
+  uint8_t mvd[2][4][2];  // Min(|mvd_lX|, 33) of the edge's 4x4 blocks [list][k][component]
+};
+static_assert(sizeof(SynEdge) == 20, "SynEdge layout");
+
+// Per-wave scratch (LDS on the device); SynEdge top[mb_width] follows it.
+struct SynScratch {
+  MbRec m;                      // the macroblock being parsed (its syntax record)
+  MbRecB m1;                    // ... its list-1 half (streams with B slices)
+  alignas(16) int16_t blk[16];  // coefficient block being decoded (raster)
+  alignas(16) int16_t blk8[64]; // 8x8 block being decoded (raster)
+  uint32_t cache[kCacheWords];  // bit reader
+  // Min(|mvd_lX|, 33) around the current macroblock, per list: [row][col],
+  // row 0 = the bottom row of the macroblock above, col 0 = the right column
+  // of the one to the left (0 where unavailable / not coded), rows and cols
+  // 1..4 = the current macroblock's 4x4 blocks
+  uint8_t mvx[2][5][5][2];
+  SynEdge left;                 // the previous macroblock's right edge
+#ifdef VTS_EXP_PROF
+  uint64_t pacc[8], pt;
+  int32_t psec;
+#endif
+};
+VTS_HD VTS_INLINE size_t syn_lds_bytes(int mb_width) {
+  return (sizeof(SynScratch) + 15) / 16 * 16 + sizeof(SynEdge) * static_cast<size_t>(mb_width);
+}
+
+struct CabacSyn {
+  RbspBitsT<kCacheWords> br;
+  const FullSlice *s;     // global (the ref_slot table is indexed at run time)
+  const SliceExt *x;      // B slices: the slice's SliceExt
+  MbRec *recs;            // the frame's records (global)
+  MbRecB *recs1;          // ... list-1 halves (streams with B slices), else null
+  int16_t *arena;         // window coefficient arena, 16 int16 per block
+  SynScratch *sc;
+  SynEdge *top;           // per macroblock column: the bottom edge of the slice's last macroblock there
+  uint32_t used;          // blocks stored so far in the slice
+  uint32_t slice_index;
+  uint32_t epoch;
+  int mbw;
+  int first_mb;
+  uint32_t err;
+  bool bframes;           // write the list-1 halves
+  bool direct8x8;         // direct_8x8_inference_flag
+  bool t8mode;            // transform_8x8_mode_flag
+  bool prev_qpd;          // the previous macroblock of the slice has mb_qp_delta != 0
+  // the current macroblock's neighbours A (left) and B (above): their edge
+  // facts (0 when unavailable) and availability
+  uint32_t fa, fb;
+  bool av_a, av_b;
   // The engine (9.3.1.2, 9.3.3.2) with codIOffset scaled: val holds the 9-bit
   // codIOffset in bits 31..23 and the next `la` bitstream bits below it, so
   // renormalisation is a shift of val and the bit reader is touched once per
@@ -93,15 +182,34 @@ struct CabacParser : Parser {
   // val >= codIRange << 23.
   uint32_t range, val;
   int32_t la;
-  bool prev_qpd;  // the previous macroblock of the slice has mb_qp_delta != 0
   // context states (pStateIdx << 1 | valMPS), four per dword.  The residual
   // contexts of 4x4 blocks (ctxIdx 85..275) fill st[0] (slot c - 85); all
   // others (0..84, and 399..459 at 85..145) st[1], so every decode's table is
   // known at compile time (slot q: lane q >> 2, byte q & 3)
   LaneTab st[2];
+  LaneTab lps, trn, s8;  // kCabLanes
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the lane index, re-read opaquely at every macroblock (refresh_lane): what
+  // derives from it is computed per macroblock instead of hoisted out of the
+  // macroblock loop and spilled
+  int lane_;
+  __device__ VTS_INLINE void refresh_lane() {
+    lane_ = static_cast<int>(threadIdx.x);
+    asm volatile("" : "+v"(lane_));
+  }
+#else
+  void refresh_lane() {}
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(VTS_EXP_PROF)
+  __device__ VTS_INLINE void prof_mark(int k) const {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    sc->pacc[sc->psec] += t - sc->pt;
+    sc->pt = t;
+    sc->psec = k;
+  }
+#endif
   static VTS_HD VTS_INLINE int ctx_tab(int c) { return (c >= 85 && c <= 275) ? 0 : 1; }
   static VTS_HD VTS_INLINE int ctx_slot(int c) { return c >= 399 ? c - 314 : (c >= 85 ? c - 85 : c); }
-  LaneTab lps, trn, s8;  // kCabLanes
 
   // ---------------------------------------------- arithmetic decoder (9.3.3.2)
   VTS_HD VTS_INLINE void cab_start() {  // 9.3.1.2: codIOffset = read_bits(9)
@@ -181,12 +289,12 @@ struct CabacParser : Parser {
     // the doubled codIOffset needs 10 bits: its top bit leaves val, and then
     // the offset is >= codIRange whatever val holds (val - rs wraps to the
     // right difference)
-    const uint32_t top = val >> 31;
+    const uint32_t top_bit = val >> 31;
     val <<= 1;
     --la;
     cab_fill();
     const uint32_t rs = range << 23;
-    if (VTS_EU((top || val >= rs) ? 1u : 0u)) {
+    if (VTS_EU((top_bit || val >= rs) ? 1u : 0u)) {
       val -= rs;
       return 1;
     }
@@ -205,181 +313,190 @@ struct CabacParser : Parser {
     return 0;
   }
 
-  // ------------------------------------------------------ neighbour facts
-  VTS_HD VTS_INLINE uint32_t cbf_of(const MbRec &m) const {
-    return static_cast<uint32_t>(m.nzc[0]) | (static_cast<uint32_t>(m.nzc[1]) << 8) |
-           (static_cast<uint32_t>(m.nzc[2]) << 16) | (static_cast<uint32_t>(m.nzc[3]) << 24);
+  // ------------------------------------------------------ macroblock frame
+  VTS_HD VTS_INLINE MbRec &cur() const { return sc->m; }
+  VTS_HD VTS_INLINE MbRecB &cur1() const { return sc->m1; }
+  VTS_HD VTS_INLINE static int etype(uint32_t f) { return static_cast<int>(f & kEType); }
+  VTS_HD VTS_INLINE static int ecbp(uint32_t f) { return static_cast<int>((f >> kECbpSh) & 63u); }
+
+  // a new macroblock: its neighbours' edge facts, the record image reset,
+  // the |mvd| grid's borders from the neighbours' edges (one cell per lane)
+  VTS_HD VTS_INLINE void begin_mb(int addr) {
+    VTS_PARSE_TRACE(0);
+    const int xcol = addr % mbw;
+    av_a = xcol > 0 && addr - 1 >= first_mb;
+    av_b = addr - mbw >= first_mb;
+    fa = av_a ? sc->left.f : 0u;
+    fb = av_b ? top[xcol].f : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the record's initial dwords, one per lane: epoch, slice, 0 coef / blocks
+    // / type..modes, ref -1, ref_slot -1, i4 DC (2), then zeros; list 1: ref1
+    // -1, ref_slot1 -1, then zeros
+    VTS_LANES(64, l) {
+      if (l < 32) {
+        const uint32_t v = l == 0 ? epoch : (l == 1 ? slice_index : ((l >= 5 && l <= 7) ? ~0u : ((l == 8 || l == 9) ? 0x22222222u : 0u)));
+        reinterpret_cast<uint32_t *>(&cur())[l] = v;
+      } else if (bframes) {
+        reinterpret_cast<uint32_t *>(&cur1())[l - 32] = l - 32 < 3 ? ~0u : 0u;
+      }
+    }
+    const SynEdge *te = &top[xcol];
+    VTS_LANES(50, i) {
+      const int l = i / 25, r = (i % 25) / 5, c = i % 5;
+      uint8_t v0 = 0, v1 = 0;
+      if (r > 0 && c == 0 && av_a) {
+        v0 = sc->left.mvd[l][r - 1][0];
+        v1 = sc->left.mvd[l][r - 1][1];
+      } else if (r == 0 && c > 0 && av_b) {
+        v0 = te->mvd[l][c - 1][0];
+        v1 = te->mvd[l][c - 1][1];
+      }
+      sc->mvx[l][r][c][0] = v0;
+      sc->mvx[l][r][c][1] = v1;
+    }
+#else
+    MbRec &m = cur();
+    m.epoch = epoch;
+    m.slice = slice_index;
+    m.coef = 0;
+    m.blocks = 0;
+    m.type = 0;
+    m.qp = 0;
+    m.cbp = 0;
+    m.modes = 0;
+    for (int i = 0; i < 4; ++i) {
+      m.ref[i] = -1;
+      m.ref_slot[i] = -1;
+    }
+    for (int i = 0; i < 8; ++i) m.i4[i] = 0x22;  // DC
+    for (int i = 0; i < 16; ++i) {
+      m.nz[i] = 0;
+      m.mv[i][0] = m.mv[i][1] = 0;
+    }
+    for (int i = 0; i < 8; ++i) m.nzc[i] = 0;
+    if (bframes) {
+      MbRecB &m1 = cur1();
+      for (int i = 0; i < 4; ++i) {
+        m1.ref1[i] = -1;
+        m1.ref_slot1[i] = -1;
+      }
+      m1.direct = 0;
+      for (int i = 0; i < 3; ++i) m1._p[i] = 0;
+      for (int i = 0; i < 8; ++i) m1.mvd1[i] = 0;
+      for (int i = 0; i < 40; ++i) m1._q[i] = 0;
+      for (int i = 0; i < 16; ++i) m1.mv1[i][0] = m1.mv1[i][1] = 0;
+    }
+    for (int l = 0; l < 2; ++l)
+      for (int r = 0; r < 5; ++r)
+        for (int c = 0; c < 5; ++c)
+          for (int k = 0; k < 2; ++k) {
+            uint8_t v = 0;
+            if (r > 0 && c == 0 && av_a) v = sc->left.mvd[l][r - 1][k];
+            else if (r == 0 && c > 0 && av_b) v = top[xcol].mvd[l][c - 1][k];
+            sc->mvx[l][r][c][k] = v;
+          }
+#endif
+  }
+
+  // the current macroblock's edge facts (right: true = its right edge for
+  // the next macroblock, false = its bottom edge for the one below)
+  VTS_HD VTS_INLINE SynEdge edge_of(bool right) const {
+    const MbRec &m = cur();
+    const int ty = m.type;
+    uint32_t f = static_cast<uint32_t>(ty);
+    const bool pcm = ty == kMbPcm;
+    const uint32_t cbp = pcm ? 0x2fu : m.cbp;
+    f |= cbp << kECbpSh;
+    if (m.modes & kModeT8) f |= kET8;
+    if ((ty == kMbI4x4 || ty == kMbI16) && ((m.modes >> 2) & 3)) f |= kEChroma;
+    const uint8_t dir = bframes ? cur1().direct : 0;
+    if (dir & kDirect16) f |= kEDirect16;
+    const uint32_t cbf = static_cast<uint32_t>(m.nzc[0]) | (static_cast<uint32_t>(m.nzc[1]) << 8) |
+                         (static_cast<uint32_t>(m.nzc[2]) << 16) | (static_cast<uint32_t>(m.nzc[3]) << 24);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rr = right ? 4 * k + 3 : 12 + k;  // raster luma block along the edge
+      if (pcm || ((cbf >> (1 + rr)) & 1u)) f |= 1u << (kECbfSh + k);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int p8 = right ? 2 * k + 1 : 2 + k;
+      if (ty == kMbInter && !((dir >> p8) & 1)) {
+        if (m.ref[p8] > 0) f |= 1u << (kERefSh + k);
+        if (bframes && cur1().ref1[p8] > 0) f |= 1u << (kERefSh + 2 + k);
+      }
+      const int cb = right ? 2 * k + 1 : 2 + k;  // chroma 4x4 block along the edge
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+        if (pcm || ((cbf >> (kBlkChromaAc0 + 4 * pl + cb)) & 1u)) f |= 1u << (kECacSh + 2 * pl + k);
+    }
+    if (pcm || (cbf & 1u)) f |= kECbfDc;
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+      if (pcm || ((cbf >> (kBlkChromaDc0 + pl)) & 1u)) f |= 1u << (kECdcSh + pl);
+    SynEdge e;
+    e.f = f;
+#pragma unroll
+    for (int l = 0; l < 2; ++l)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) e.mvd[l][k][c] = right ? sc->mvx[l][1 + k][4][c] : sc->mvx[l][4][1 + k][c];
+    return e;
+  }
+  // after a macroblock: its record to global memory (16 bytes per lane), its
+  // edges for the neighbours to the right and below
+  VTS_HD VTS_INLINE void end_mb(int addr) {
+    const SynEdge er = edge_of(true), eb = edge_of(false);
+#if defined(__HIP_DEVICE_COMPILE__)
+    VTS_LANES(16, l) {
+      if (l < 8) reinterpret_cast<u32x4 *>(&recs[addr])[l] = reinterpret_cast<const u32x4 *>(&cur())[l];
+      else if (bframes && (l < 10 || l >= 12))
+        reinterpret_cast<u32x4 *>(&recs1[addr])[l - 8] = reinterpret_cast<const u32x4 *>(&cur1())[l - 8];
+    }
+#else
+    recs[addr] = cur();
+    if (bframes) recs1[addr] = cur1();
+#endif
+    sc->left = er;
+    top[addr % mbw] = eb;
+  }
+
+  // store sc->blk (or src) as the next arena block; bit = kBlk* index
+  VTS_HD VTS_INLINE bool store_block(uint32_t bit, const int16_t *src) {
+    VTS_PARSE_TRACE(7);
+    if (used >= s->arena_cap) return false;
+    int16_t *dst = arena + 16 * static_cast<int64_t>(s->arena + used);
+#if defined(__HIPCC__)
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(dst);
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src);
+    d4[0] = s4[0];
+    d4[1] = s4[1];
+#else
+    for (int i = 0; i < 16; ++i) dst[i] = src[i];
+#endif
+    if (cur().blocks == 0) cur().coef = s->arena + used;
+    cur().blocks |= 1u << bit;
+    ++used;
+    return true;
   }
   VTS_HD VTS_INLINE void set_cbf(uint32_t bit) {
     MbRec &m = cur();
     m.nzc[bit >> 3] = static_cast<uint8_t>(m.nzc[bit >> 3] | (1u << (bit & 7)));
   }
-  VTS_HD VTS_INLINE bool avail_not(int n, int type) const { return n != -1 && rec(n).type != type; }
-  // condTermFlagN of coded_block_flag (9.3.3.1.1.9)
-  VTS_HD VTS_INLINE int cbf_cond(int n, bool cur_intra, bool tb, uint32_t bit) const {
-    if (n == -1) return cur_intra ? 1 : 0;
-    const MbRec &m = rec(n);
-    if (m.type == kMbPcm) return 1;
-    if (!tb || m.type == kMbSkip) return 0;
-    return static_cast<int>((cbf_of(m) >> bit) & 1u);
-  }
-  VTS_HD VTS_INLINE int cbf_luma_inc(int addr, int bx, int by, bool intra) const {
-    int inc = 0;
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      int xw = 0, yw = 0;
-      const int n = nb_mb(addr, nb ? bx * 4 : bx * 4 - 1, nb ? by * 4 - 1 : by * 4, 16, &xw, &yw);
-      bool tb = false;
-      uint32_t bit = 0;
-      if (n != -1) {
-        tb = (rec(n).cbp >> ((yw / 8) * 2 + xw / 8)) & 1;
-        bit = 1u + static_cast<uint32_t>((yw / 4) * 4 + xw / 4);
-      }
-      inc += cbf_cond(n, intra, tb, bit) << nb;
-    }
-    return inc;
-  }
-  VTS_HD VTS_INLINE int cbf_chroma_inc(int addr, int pl, int blk, bool dc, bool intra) const {
-    int inc = 0;
-    const int x = dc ? 0 : (blk & 1) * 4, y = dc ? 0 : (blk >> 1) * 4;
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      int xw = 0, yw = 0;
-      const int n = nb_mb(addr, nb ? x : x - 1, nb ? y - 1 : y, 8, &xw, &yw);
-      bool tb = false;
-      uint32_t bit = 0;
-      if (n != -1) {
-        const int cc = rec(n).cbp >> 4;
-        tb = dc ? cc != 0 : cc == 2;
-        bit = dc ? 17u + static_cast<uint32_t>(pl) : 19u + static_cast<uint32_t>(4 * pl + (yw / 4) * 2 + xw / 4);
-      }
-      inc += cbf_cond(n, intra, tb, bit) << nb;
-    }
-    return inc;
-  }
-  // Min(|mvd_lX|, 33) at luma (xN, yN) of the current macroblock's
-  // neighbourhood (skipped, intra and direct blocks carry 0)
-  // (xN, yN in -1..15: A and B neighbours only; mvd_border filled the edges)
-  VTS_HD VTS_INLINE int mvd_at(int addr, int xN, int yN, int comp, int l = 0) const {
-    return sc->mvx[l][(yN >> 2) + 1][(xN >> 2) + 1][comp];
-  }
-  // a new macroblock's mvx: the left column takes the previous macroblock's
-  // right column (when it is the left neighbour A), the top row the bottom-row
-  // |mvd| the macroblock above kept in its record (inter only), the inside 0;
-  // one cell per lane (every read is issued before any write)
-  VTS_HD VTS_INLINE void mvd_border(int A, int B) {
-    const bool top_inter = B != -1 && rec(B).type == kMbInter;
-    const MbRec *tb = top_inter ? &rec(B) : nullptr;
-    const MbRecB *tb1 = top_inter && bframes ? &rec1(B) : nullptr;
-#if defined(__HIP_DEVICE_COMPILE__)
-    VTS_LANES(50, i) {
-      const int l = i / 25, r = (i % 25) / 5, c = i % 5;
-      uint8_t v0 = 0, v1 = 0;
-      if (r > 0 && c == 0) {
-        if (A != -1) {
-          v0 = sc->mvx[l][r][4][0];
-          v1 = sc->mvx[l][r][4][1];
-        }
-      } else if (r == 0 && c > 0 && tb) {
-        const uint8_t *src = l ? (tb1 ? tb1->mvd1 : nullptr) : tb->i4;
-        if (src) {
-          v0 = src[2 * (c - 1)];
-          v1 = src[2 * (c - 1) + 1];
-        }
-      }
-      asm volatile("" ::: "memory");  // every lane's read before any lane's write
-      sc->mvx[l][r][c][0] = v0;
-      sc->mvx[l][r][c][1] = v1;
-    }
-#else
-    // host: the lanes' reads all precede their writes on the device; serially,
-    // compute the cells first
-    uint8_t nv[2][5][5][2] = {};
-    for (int l = 0; l < 2; ++l)
-      for (int r = 1; r < 5; ++r)
-        if (A != -1) {
-          nv[l][r][0][0] = sc->mvx[l][r][4][0];
-          nv[l][r][0][1] = sc->mvx[l][r][4][1];
-        }
-    if (tb)
-      for (int c = 1; c < 5; ++c) {
-        nv[0][0][c][0] = tb->i4[2 * (c - 1)];
-        nv[0][0][c][1] = tb->i4[2 * (c - 1) + 1];
-        if (tb1) {
-          nv[1][0][c][0] = tb1->mvd1[2 * (c - 1)];
-          nv[1][0][c][1] = tb1->mvd1[2 * (c - 1) + 1];
-        }
-      }
-    for (int l = 0; l < 2; ++l)
-      for (int r = 0; r < 5; ++r)
-        for (int c = 0; c < 5; ++c) {
-          sc->mvx[l][r][c][0] = nv[l][r][c][0];
-          sc->mvx[l][r][c][1] = nv[l][r][c][1];
-        }
-#endif
-  }
+
   // condTermFlagN of ref_idx_lX (9.3.3.1.1.6): refIdxLX > 0 of an inter
-  // neighbour that is neither skipped nor predicted in direct mode
-  // (xN, yN in -1..15, A and B neighbours: the left / top macroblocks' flags
-  // come from refb, which mvd_border filled)
-  VTS_HD VTS_INLINE int ref_gt0_at(int addr, int xN, int yN, int l = 0) const {
-    if (xN < 0) return static_cast<int>((refb >> (8 * l + (yN >> 3))) & 1u);
-    if (yN < 0) return static_cast<int>((refb >> (8 * l + 4 + (xN >> 3))) & 1u);
-    const MbRec &m = cur();
+  // neighbour partition that is neither skipped nor predicted in direct mode
+  // (xN, yN in -1..15: A and B neighbours only)
+  VTS_HD VTS_INLINE int ref_gt0_at(int xN, int yN, int l) const {
+    if (xN < 0) return static_cast<int>((fa >> (kERefSh + 2 * l + (yN >> 3))) & 1u);
+    if (yN < 0) return static_cast<int>((fb >> (kERefSh + 2 * l + (xN >> 3))) & 1u);
     const int p8 = (yN >> 3) * 2 + (xN >> 3);
     if (bframes && ((cur1().direct >> p8) & 1)) return 0;
-    return (l ? cur1().ref1[p8] : m.ref[p8]) > 0 ? 1 : 0;
+    return (l ? cur1().ref1[p8] : cur().ref[p8]) > 0 ? 1 : 0;
   }
-  // refb bit 8 l + k: refIdxLX > 0 of the left neighbour's 8x8 row k (k 0, 1)
-  // and bit 8 l + 4 + k of the top neighbour's 8x8 column k (inter, neither
-  // skipped nor direct; 0 where unavailable)
-  uint32_t refb;
-  VTS_HD VTS_INLINE void ref_border(int A, int B) {
-    uint32_t f = 0;
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int n = nb ? B : A;
-      if (n == -1 || rec(n).type != kMbInter) continue;
-      const MbRec &m = rec(n);
-      const MbRecB *m1 = bframes ? &rec1(n) : nullptr;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int p8 = nb ? 2 + k : 2 * k + 1;  // top: bottom 8x8 row; left: right 8x8 column
-        if (m1 && ((m1->direct >> p8) & 1)) continue;
-        f |= (m.ref[p8] > 0 ? 1u : 0u) << (4 * nb + k);
-        if (m1) f |= (m1->ref1[p8] > 0 ? 1u : 0u) << (8 + 4 * nb + k);
-      }
-    }
-    refb = f;
-  }
-  // Intra NxN mode predictor (8.3.1.1 / 8.3.2.1) of the block at (x0, y0)
-  VTS_HD VTS_INLINE int mode_pred(int addr, int x0, int y0, bool is8) const {
-    int xa = 0, ya = 0, xb = 0, yb = 0;
-    const int a = nb_mb(addr, x0 - 1, y0, 16, &xa, &ya), b = nb_mb(addr, x0, y0 - 1, 16, &xb, &yb);
-    if (a == -1 || b == -1) return 2;
-    const MbRec &ma = rec(a), &mb = rec(b);
-    if (cip && (ma.type == kMbInter || ma.type == kMbSkip || mb.type == kMbInter || mb.type == kMbSkip)) return 2;
-    int md[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const MbRec &m = i ? mb : ma;
-      const int xw = i ? xb : xa, yw = i ? yb : ya;
-      if (m.type != kMbI4x4) {
-        md[i] = 2;
-        continue;
-      }
-      int r = (yw / 4) * 4 + xw / 4;
-      if (is8 && !(m.modes & kModeT8)) {  // Intra4x4PredMode[luma8x8BlkIdxN * 4 + (A ? 1 : 2)]
-        const int k = ((yw / 8) * 2 + xw / 8) * 4 + (i ? 2 : 1);
-        r = blk_y(k) * 4 + blk_x(k);
-      }
-      md[i] = (m.i4[r >> 1] >> ((r & 1) * 4)) & 15;
-    }
-    return vts_min(md[0], md[1]);
-  }
-  VTS_HD VTS_INLINE void set_i4(int r, int mode) {
-    MbRec &m = cur();
-    m.i4[r >> 1] = static_cast<uint8_t>((m.i4[r >> 1] & (0xf0 >> ((r & 1) * 4))) | (mode << ((r & 1) * 4)));
+  VTS_HD VTS_INLINE int mvd_at(int xN, int yN, int comp, int l) const {
+    return sc->mvx[l][(yN >> 2) + 1][(xN >> 2) + 1][comp];
   }
 
   // ------------------------------------------------------- syntax elements
@@ -425,9 +542,9 @@ struct CabacParser : Parser {
     return t;
   }
   // ref_idx_lX (U binarization, ctxIdx 54..59)
-  VTS_HD VTS_INLINE int ref_idx(int addr, int x0, int y0, int l) {
+  VTS_HD VTS_INLINE int ref_idx(int x0, int y0, int l) {
     int v = 0;
-    if (dec(54 + ref_gt0_at(addr, x0 - 1, y0, l) + 2 * ref_gt0_at(addr, x0, y0 - 1, l))) {
+    if (dec(54 + ref_gt0_at(x0 - 1, y0, l) + 2 * ref_gt0_at(x0, y0 - 1, l))) {
       v = 1;
       if (dec(58)) {
         v = 2;
@@ -437,63 +554,45 @@ struct CabacParser : Parser {
     }
     return v;
   }
-  // mb_pred / sub_mb_pred of a B macroblock (7.3.5.1-2): mb_type 0..22;
-  // *small: a partition below 8x8 (or a direct one without
-  // direct_8x8_inference) rules out transform_size_8x8_flag
-  VTS_HD VTS_INLINE bool b_inter_cabac(int addr, int mb_type, bool *small) {
-    uint8_t *pm = sc->pm;
-    int8_t *sub = sc->sub, *r0 = sc->refs, *r1 = sc->refs1;
-    for (int k = 0; k < 4; ++k) {
-      pm[k] = 0;
-      sub[k] = 0;
-      r0[k] = r1[k] = -1;
-    }
-    if (mb_type == 0) {  // B_Direct_16x16
-      VTS_PARSE_TRACE(6);
-      cur1().direct = 0x0f | kDirect16;
-      if (!direct8x8) *small = true;
-      direct_pred(addr, 0xffffu);
-      return !err;
-    }
-    int shape;
-    if (mb_type <= 3) {
-      shape = 0;
-      pm[0] = static_cast<uint8_t>(mb_type);
-    } else if (mb_type < 22) {
-      shape = (mb_type & 1) ? 2 : 1;
-      pm[0] = kBPart[mb_type] & 3;
-      pm[1] = kBPart[mb_type] >> 2;
-    } else {
-      shape = 3;
-      for (int k = 0; k < 4; ++k) {
-        const int v = b_sub();
-        pm[k] = kBSub[v] & 3;
-        sub[k] = static_cast<int8_t>(kBSub[v] >> 2);
-        if (pm[k] == 0) {
-          cur1().direct |= static_cast<uint8_t>(1u << k);
-          if (!direct8x8) *small = true;
-        } else if (sub[k]) {
-          *small = true;
+  VTS_HD VTS_INLINE int mvd(int base, int sum) {  // U prefix cMax 9 + UEG3 + sign
+    if (!dec(base + (sum < 3 ? 0 : (sum > 32 ? 2 : 1)))) return 0;
+    int v = 1;
+    while (v < 9 && dec(base + vts_min(v + 2, 6))) ++v;  // ctxIdxInc 3, 4, 5, 6, 6, ...
+    if (v >= 9) {
+      int k = 3;
+      while (bypass()) {
+        v += 1 << k;
+        if (++k > 24) {
+          err |= DEC_E_SYNTAX;
+          return 0;
         }
       }
+      while (k--) v += static_cast<int>(bypass()) << k;
     }
+    return bypass() ? -v : v;
+  }
+
+  // mb_pred / sub_mb_pred of an inter macroblock (7.3.5.1-2) as syntax:
+  // shape 0..3 (16x16, 16x8, 8x16, 8x8), pm[k] the prediction of partition k
+  // (bit 0 L0, bit 1 L1; 0 direct), sub[k] the sub-partition shape of 8x8 k.
+  // ref_idx into ref / ref1 per quadrant, mvd into mv / mv1 per 4x4 block and
+  // into the |mvd| grid.  false (err set) on a reference index outside the list.
+  VTS_HD VTS_INLINE bool inter_syntax(int shape, const uint8_t (&pm)[4], const uint8_t (&sub)[4]) {
     const int nparts = shape == 0 ? 1 : (shape < 3 ? 2 : 4);
     MbRec &m = cur();
     MbRecB &m1 = cur1();
     for (int l = 0; l < 2; ++l) {
-      const int nref = l ? bc.x->num_ref1 : s->num_ref;
-      int8_t *rr = l ? r1 : r0;
+      const int nref = l ? (x ? x->num_ref1 : 0) : s->num_ref;
       for (int k = 0; k < nparts; ++k) {
         if (!((pm[k] >> l) & 1)) continue;
         const int x0 = (shape == 2 || shape == 3) ? 8 * (k & 1) : 0;
         const int y0 = shape == 1 ? 8 * k : (shape == 3 ? 8 * (k >> 1) : 0);
-        const int v = nref > 1 ? ref_idx(addr, x0, y0, l) : 0;
-        if (v >= nref || (l ? bc.x->ref_slot1[v & 31] : s->ref_slot[v & 31]) < 0) {
+        const int v = nref > 1 ? ref_idx(x0, y0, l) : 0;
+        if (v >= nref || (l ? x->ref_slot1[v & 31] : s->ref_slot[v & 31]) < 0) {
           err |= DEC_E_NO_REF;
           return false;
         }
-        rr[k] = static_cast<int8_t>(v);
-        // the partition's 8x8 quarters carry the index for later contexts
+        // the partition's 8x8 quarters carry the index (later contexts, h264_derive)
         const int pw = (shape == 0 || shape == 1) ? 2 : 1, ph = (shape == 0 || shape == 2) ? 2 : 1;
         for (int qy = 0; qy < ph; ++qy)
           for (int qx = 0; qx < pw; ++qx) {
@@ -524,43 +623,36 @@ struct CabacParser : Parser {
             else if (sub[k] == 2) sx += 4 * q;
             else if (sub[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
           }
-          const int dx = mvd(40, mvd_at(addr, sx - 1, sy, 0, l) + mvd_at(addr, sx, sy - 1, 0, l));
-          const int dy = mvd(47, mvd_at(addr, sx - 1, sy, 1, l) + mvd_at(addr, sx, sy - 1, 1, l));
-          sc->mvd[l][4 * k + q][0] = dx;
-          sc->mvd[l][4 * k + q][1] = dy;
+          const int dx = mvd(40, mvd_at(sx - 1, sy, 0, l) + mvd_at(sx, sy - 1, 0, l));
+          const int dy = mvd(47, mvd_at(sx - 1, sy, 1, l) + mvd_at(sx, sy - 1, 1, l));
           const uint8_t ax = static_cast<uint8_t>(vts_min(dx < 0 ? -dx : dx, 33));
           const uint8_t ay = static_cast<uint8_t>(vts_min(dy < 0 ? -dy : dy, 33));
           const uint32_t bm = blk_mask(sx, sy, pw, ph);
+          // mvd_lX lies in [-8192, 8191.75] samples (Annex A): the record's int16
+          if (dx < -32768 || dx > 32767 || dy < -32768 || dy > 32767) {
+            err |= DEC_E_SYNTAX;
+            return false;
+          }
+          const int16_t cx = static_cast<int16_t>(dx), cy = static_cast<int16_t>(dy);
           VTS_LANES(16, b) if ((bm >> b) & 1u) {
             sc->mvx[l][1 + (b >> 2)][1 + (b & 3)][0] = ax;
             sc->mvx[l][1 + (b >> 2)][1 + (b & 3)][1] = ay;
+            if (l) {
+              m1.mv1[b][0] = cx;
+              m1.mv1[b][1] = cy;
+            } else {
+              m.mv[b][0] = cx;
+              m.mv[b][1] = cy;
+            }
           }
         }
       }
-    // the references the parse recorded are set again by the motion below
-    for (int k = 0; k < 4; ++k) {
-      m.ref[k] = -1;
-      m1.ref1[k] = -1;
-    }
-    return b_motion(addr, shape);
+    m.i4[0] = static_cast<uint8_t>(shape);
+    m.i4[1] = static_cast<uint8_t>(pm[0] | (pm[1] << 2) | (pm[2] << 4) | (pm[3] << 6));
+    m.i4[2] = static_cast<uint8_t>(sub[0] | (sub[1] << 2) | (sub[2] << 4) | (sub[3] << 6));
+    return !err;
   }
-  VTS_HD VTS_INLINE int mvd(int base, int sum) {  // U prefix cMax 9 + UEG3 + sign
-    if (!dec(base + (sum < 3 ? 0 : (sum > 32 ? 2 : 1)))) return 0;
-    int v = 1;
-    while (v < 9 && dec(base + vts_min(v + 2, 6))) ++v;  // ctxIdxInc 3, 4, 5, 6, 6, ...
-    if (v >= 9) {
-      int k = 3;
-      while (bypass()) {
-        v += 1 << k;
-        if (++k > 24) {
-          err |= DEC_E_SYNTAX;
-          return 0;
-        }
-      }
-      while (k--) v += static_cast<int>(bypass()) << k;
-    }
-    return bypass() ? -v : v;
-  }
+
   // residual_block_cabac (7.3.5.3.3): each level goes straight to its raster
   // position in dst, which the caller has zeroed (4x4 blocks: zig-zag position
   // of coefficient start + i; 8x8: the 8x8 zig-zag; chroma DC: list order);
@@ -628,15 +720,13 @@ struct CabacParser : Parser {
 
   // ------------------------------------------------------ macroblock_layer
   // (begin_mb done by the caller); returns false to stop the slice
-  VTS_HD VTS_INLINE bool mb_cabac(int addr, int *qp) {
+  VTS_HD VTS_INLINE bool mb_cabac(int *qp) {
     VTS_PROF(2);
     MbRec &m = cur();
-    int xw, yw;
-    const int A = nb_mb(addr, -1, 0, 16, &xw, &yw), B = nb_mb(addr, 0, -1, 16, &xw, &yw);
+    const bool is_b = s->is_p == kSliceB;
     int itype, mb_type = 0;
-    if (s->is_p == kSliceB) {
-      const int t = b_type((A != -1 && !(rec1(A).direct & kDirect16) ? 1 : 0) +
-                           (B != -1 && !(rec1(B).direct & kDirect16) ? 1 : 0));
+    if (is_b) {
+      const int t = b_type((av_a && !(fa & kEDirect16) ? 1 : 0) + (av_b && !(fb & kEDirect16) ? 1 : 0));
       itype = t >= 23 ? t - 23 : -1;
       mb_type = t;
     } else if (s->is_p) {
@@ -648,7 +738,7 @@ struct CabacParser : Parser {
         else mb_type = dec(17) ? 1 : 2;
       }
     } else {
-      itype = i_type(0, (avail_not(A, kMbI4x4) ? 1 : 0) + (avail_not(B, kMbI4x4) ? 1 : 0));
+      itype = i_type(0, (av_a && etype(fa) != kMbI4x4 ? 1 : 0) + (av_b && etype(fb) != kMbI4x4 ? 1 : 0));
     }
     if (itype == 25) {  // I_PCM: alignment, 384 samples through the RBSP reader, engine restart
       m.type = kMbPcm;
@@ -661,8 +751,8 @@ struct CabacParser : Parser {
           const uint32_t lo = br.bits(8), hi = br.bits(8);
           sc->blk[i] = static_cast<int16_t>(lo | (hi << 8));
         }
-        if (!store_block(k)) {
-          err |= DEC_E_SYNTAX;
+        if (!store_block(k, sc->blk)) {
+          err |= DEC_E_ARENA;
           return false;
         }
       }
@@ -673,130 +763,77 @@ struct CabacParser : Parser {
     }
     int cbp = 0;
     bool small = false;
-    if (itype == 0) {  // I_NxN
+    if (itype == 0) {  // I_NxN: the modes' syntax (h264_derive predicts them)
       m.type = kMbI4x4;
       bool t8 = false;
-      if (P_t8mode) {
-        const int inc = (A != -1 && (rec(A).modes & kModeT8) ? 1 : 0) + (B != -1 && (rec(B).modes & kModeT8) ? 1 : 0);
-        t8 = dec(399 + inc) != 0;
-      }
+      if (t8mode) t8 = dec(399 + ((fa & kET8) ? 1 : 0) + ((fb & kET8) ? 1 : 0)) != 0;
       const int nb = t8 ? 4 : 16;
       if (t8) m.modes = kModeT8;
-      uint8_t *pflag = sc->prev, *rem = sc->rem;
       for (int i = 0; i < nb; ++i) {
-        pflag[i] = static_cast<uint8_t>(dec(68));
-        if (!pflag[i]) {
-          uint32_t r = dec(69);
-          r |= dec(69) << 1;
-          r |= dec(69) << 2;
-          rem[i] = static_cast<uint8_t>(r);
+        uint32_t v = 8;
+        if (!dec(68)) {
+          v = dec(69);
+          v |= dec(69) << 1;
+          v |= dec(69) << 2;
         }
-      }
-      for (int i = 0; i < nb; ++i) {
-        const int x0 = t8 ? (i & 1) * 8 : blk_x(i) * 4, y0 = t8 ? (i >> 1) * 8 : blk_y(i) * 4;
-        const int pm = mode_pred(addr, x0, y0, t8);
-        const int mode = pflag[i] ? pm : (rem[i] < pm ? rem[i] : rem[i] + 1);
-        const int r = (y0 / 4) * 4 + x0 / 4;
-        set_i4(r, mode);
-        if (t8) {
-          set_i4(r + 1, mode);
-          set_i4(r + 4, mode);
-          set_i4(r + 5, mode);
-        }
+        const int r = t8 ? (i >> 1) * 8 + (i & 1) * 2 : blk_y(i) * 4 + blk_x(i);
+        m.i4[r >> 1] = static_cast<uint8_t>((m.i4[r >> 1] & (0xf0 >> ((r & 1) * 4))) | (v << ((r & 1) * 4)));
       }
     } else if (itype > 0) {  // I_16x16
       m.type = kMbI16;
       cbp = ((((itype - 1) / 4) % 3) << 4) | (itype >= 13 ? 15 : 0);
       m.modes = static_cast<uint8_t>((itype - 1) % 4);
-    } else if (s->is_p == kSliceB) {  // Table 7-14
-      m.type = kMbInter;
-      VTS_PROF(3);
-      if (!b_inter_cabac(addr, mb_type, &small)) return false;
-    } else {  // inter (Table 7-13)
+    } else {  // inter (Tables 7-13, 7-14, 7-17, 7-18)
       VTS_PROF(3);
       m.type = kMbInter;
-      const int nparts = mb_type == 0 ? 1 : (mb_type <= 2 ? 2 : 4);
-      int8_t *sub = sc->sub, *refs = sc->refs;
-      for (int k = 0; k < 4; ++k) sub[k] = refs[k] = 0;
-      if (mb_type == 3)
-        for (int k = 0; k < 4; ++k) {
-          int v;
-          if (dec(21)) v = 0;
-          else if (!dec(22)) v = 1;
-          else v = dec(23) ? 2 : 3;
-          sub[k] = static_cast<int8_t>(v);
-          if (v) small = true;
+      uint8_t pm[4] = {0, 0, 0, 0}, sub[4] = {0, 0, 0, 0};
+      int shape;
+      if (is_b) {
+        if (mb_type == 0) {  // B_Direct_16x16
+          VTS_PARSE_TRACE(6);
+          cur1().direct = 0x0f | kDirect16;
+          if (!direct8x8) small = true;
+          shape = -1;
+        } else if (mb_type <= 3) {
+          shape = 0;
+          pm[0] = static_cast<uint8_t>(mb_type);
+        } else if (mb_type < 22) {
+          shape = (mb_type & 1) ? 2 : 1;
+          pm[0] = kBPart[mb_type] & 3;
+          pm[1] = kBPart[mb_type] >> 2;
+        } else {
+          shape = 3;
+          for (int k = 0; k < 4; ++k) {
+            const int v = b_sub();
+            pm[k] = kBSub[v] & 3;
+            sub[k] = static_cast<uint8_t>(kBSub[v] >> 2);
+            if (pm[k] == 0) {
+              cur1().direct |= static_cast<uint8_t>(1u << k);
+              if (!direct8x8) small = true;
+            } else if (sub[k]) {
+              small = true;
+            }
+          }
         }
-      const int nref = s->num_ref;
-      for (int k = 0; k < nparts; ++k) {
-        const int x0 = (mb_type == 2 || mb_type == 3) ? 8 * (k & 1) : 0;
-        const int y0 = mb_type == 1 ? 8 * k : (mb_type == 3 ? 8 * (k >> 1) : 0);
-        int v = 0;
-        if (nref > 1) v = ref_idx(addr, x0, y0, 0);
-        if (v >= nref || s->ref_slot[v & 31] < 0) {
-          err |= DEC_E_NO_REF;
-          return false;
-        }
-        refs[k] = static_cast<int8_t>(v);
-        // the partition's 8x8 quarters carry the index for later contexts
-        const int pw = (mb_type == 0 || mb_type == 1) ? 2 : 1, ph = (mb_type == 0 || mb_type == 2) ? 2 : 1;
-        for (int qy = 0; qy < ph; ++qy)
-          for (int qx = 0; qx < pw; ++qx) m.ref[(y0 / 8 + qy) * 2 + x0 / 8 + qx] = static_cast<int8_t>(v);
+      } else {
+        shape = mb_type;
+        for (int k = 0; k < 4; ++k) pm[k] = 1;
+        if (mb_type == 3)
+          for (int k = 0; k < 4; ++k) {
+            int v;
+            if (dec(21)) v = 0;
+            else if (!dec(22)) v = 1;
+            else v = dec(23) ? 2 : 3;
+            sub[k] = static_cast<uint8_t>(v);
+            if (v) small = true;
+          }
       }
-      uint32_t done = 0;
-      for (int k = 0; k < nparts; ++k) {
-        int nsub = 1, pw, ph, x0, y0;
-        if (mb_type == 0) { pw = ph = 16; x0 = y0 = 0; }
-        else if (mb_type == 1) { pw = 16; ph = 8; x0 = 0; y0 = 8 * k; }
-        else if (mb_type == 2) { pw = 8; ph = 16; x0 = 8 * k; y0 = 0; }
-        else {
-          x0 = 8 * (k & 1);
-          y0 = 8 * (k >> 1);
-          nsub = sub[k] == 0 ? 1 : (sub[k] == 3 ? 4 : 2);
-          pw = (sub[k] == 0 || sub[k] == 1) ? 8 : 4;
-          ph = (sub[k] == 0 || sub[k] == 2) ? 8 : 4;
-        }
-        for (int q = 0; q < nsub; ++q) {
-          int sx = x0, sy = y0;
-          if (mb_type == 3) {
-            if (sub[k] == 1) sy += 4 * q;
-            else if (sub[k] == 2) sx += 4 * q;
-            else if (sub[k] == 3) { sx += 4 * (q & 1); sy += 4 * (q >> 1); }
-          }
-          const int dx = mvd(40, mvd_at(addr, sx - 1, sy, 0) + mvd_at(addr, sx, sy - 1, 0));
-          const int dy = mvd(47, mvd_at(addr, sx - 1, sy, 1) + mvd_at(addr, sx, sy - 1, 1));
-          int px, py;
-          mv_pred(addr, sx, sy, pw, ph, refs[k], done, &px, &py);
-          const int vx = px + dx, vy = py + dy;
-          if (vx < -32768 || vx > 32767 || vy < -32768 || vy > 32767) {
-            err |= DEC_E_SYNTAX;
-            return false;
-          }
-          const uint8_t ax = static_cast<uint8_t>(vts_min(dx < 0 ? -dx : dx, 33));
-          const uint8_t ay = static_cast<uint8_t>(vts_min(dy < 0 ? -dy : dy, 33));
-          const uint32_t bm = blk_mask(sx, sy, pw, ph);
-          const int rk = refs[k];
-          VTS_LANES(16, b) if ((bm >> b) & 1u) {
-            set_motion(b, rk, vx, vy);
-            sc->mvx[0][1 + (b >> 2)][1 + (b & 3)][0] = ax;
-            sc->mvx[0][1 + (b >> 2)][1 + (b & 3)][1] = ay;
-          }
-          done |= bm;
-        }
-      }
+      if (shape >= 0 && !inter_syntax(shape, pm, sub)) return false;
     }
     VTS_PROF(2);
     if (m.type == kMbI4x4 || m.type == kMbI16) {  // intra_chroma_pred_mode, TU cMax 3
-      int inc = 0;
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const int n = nb ? B : A;
-        if (n == -1) continue;
-        const MbRec &r = rec(n);
-        inc += ((r.type == kMbI4x4 || r.type == kMbI16) && ((r.modes >> 2) & 3)) ? 1 : 0;
-      }
       int cm = 0;
-      if (dec(64 + inc)) {
+      if (dec(64 + ((fa & kEChroma) ? 1 : 0) + ((fb & kEChroma) ? 1 : 0))) {
         cm = 1;
         if (dec(67)) {
           cm = 2;
@@ -807,39 +844,20 @@ struct CabacParser : Parser {
     }
     VTS_PROF(4);
     if (m.type != kMbI16) {  // coded_block_pattern (9.3.3.1.1.4)
+      const int ca_cbp = ecbp(fa), cb_cbp = ecbp(fb);
       for (int b8 = 0; b8 < 4; ++b8) {
-        const int bx = (b8 & 1) * 8, by = (b8 >> 1) * 8;
-        int cond[2];
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-          int x2 = 0, y2 = 0;
-          const int n = nb_mb(addr, nb ? bx : bx - 1, nb ? by - 1 : by, 16, &x2, &y2);
-          const int b8n = (y2 / 8) * 2 + x2 / 8;
-          if (n == -1) cond[nb] = 0;
-          else if (n == -2) cond[nb] = ((cbp >> b8n) & 1) ? 0 : 1;
-          else {
-            const MbRec &r = rec(n);
-            cond[nb] = r.type == kMbPcm ? 0 : (r.type == kMbSkip ? 1 : (((r.cbp >> b8n) & 1) ? 0 : 1));
-          }
-        }
-        cbp |= static_cast<int>(dec(73 + cond[0] + 2 * cond[1])) << b8;
+        // A: the left 8x8 (inside, or the left macroblock's right column);
+        // B: the 8x8 above (inside, or the top macroblock's bottom row)
+        const int condA = (b8 & 1) ? !((cbp >> (b8 - 1)) & 1) : (av_a ? !((ca_cbp >> (b8 + 1)) & 1) : 0);
+        const int condB = (b8 & 2) ? !((cbp >> (b8 - 2)) & 1) : (av_b ? !((cb_cbp >> (b8 + 2)) & 1) : 0);
+        cbp |= static_cast<int>(dec(73 + condA + 2 * condB)) << b8;
       }
-      int ca[2] = {0, 0}, c2[2] = {0, 0};
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const int n = nb ? B : A;
-        if (n == -1) continue;
-        const MbRec &r = rec(n);
-        const int cc = r.type == kMbPcm ? 2 : (r.type == kMbSkip ? 0 : r.cbp >> 4);
-        ca[nb] = cc != 0;
-        c2[nb] = cc == 2;
-      }
-      if (dec(77 + ca[0] + 2 * ca[1])) cbp |= (1 + static_cast<int>(dec(81 + c2[0] + 2 * c2[1]))) << 4;
+      const int ccA = av_a ? ca_cbp >> 4 : 0, ccB = av_b ? cb_cbp >> 4 : 0;
+      if (dec(77 + (ccA != 0) + 2 * (ccB != 0))) cbp |= (1 + static_cast<int>(dec(81 + (ccA == 2) + 2 * (ccB == 2)))) << 4;
     }
     m.cbp = static_cast<uint8_t>(cbp);
-    if (m.type == kMbInter && (cbp & 15) && P_t8mode && !small) {
-      const int inc = (A != -1 && (rec(A).modes & kModeT8) ? 1 : 0) + (B != -1 && (rec(B).modes & kModeT8) ? 1 : 0);
-      if (dec(399 + inc)) m.modes = static_cast<uint8_t>(m.modes | kModeT8);
+    if (m.type == kMbInter && (cbp & 15) && t8mode && !small) {
+      if (dec(399 + ((fa & kET8) ? 1 : 0) + ((fb & kET8) ? 1 : 0))) m.modes = static_cast<uint8_t>(m.modes | kModeT8);
     }
     bool qpd = false;
     if (cbp || m.type == kMbI16) {  // mb_qp_delta: U of the se() mapping
@@ -868,38 +886,11 @@ struct CabacParser : Parser {
     // ---- residual (7.3.5.3), blocks in bitstream order
     const bool intra = m.type == kMbI4x4 || m.type == kMbI16;
     const bool t8 = (m.modes & kModeT8) != 0;
-    // the blocks present, in bitstream order = kBlk* bit order; an 8x8 block
-    // is its quarter's first 4x4 bit.  One residual() site for all of them.
-    // condTermFlagN (9.3.3.1.1.9) of the luma 4x4 blocks on the macroblock's
-    // left / top edge, from the neighbours' records once: bits 0-3 = A of
-    // rows 0-3, bits 4-7 = B of columns 0-3; inside the macroblock the
-    // neighbour's flag is its coded_block_flag (cbfc)
-    uint32_t nbl = 0, cbfc = 0;
-    if ((cbp & 15) && !t8) {
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const int n = nb ? B : A;
-        uint32_t f = 0;
-        if (n == -1) {
-          f = intra ? 15u : 0u;
-        } else {
-          const MbRec &r = rec(n);
-          if (r.type == kMbPcm) {
-            f = 15u;
-          } else if (r.type != kMbSkip) {
-            const uint32_t cb = cbf_of(r);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              // A: row k, right column (raster 4k + 3) in 8x8 (k / 2) * 2 + 1;
-              // B: column k, bottom row (raster 12 + k) in 8x8 2 + k / 2
-              const int b8 = nb ? 2 + (k >> 1) : (k >> 1) * 2 + 1, rr = nb ? 12 + k : 4 * k + 3;
-              f |= (((r.cbp >> b8) & 1) ? (cb >> (1 + rr)) & 1u : 0u) << k;
-            }
-          }
-        }
-        nbl |= f << (4 * nb);
-      }
-    }
+    // condTermFlagN (9.3.3.1.1.9) of coded_block_flag across the edges: an
+    // unavailable neighbour counts as the current macroblock's intra-ness
+    const uint32_t un = intra ? 0xffffffffu : 0u;
+    const uint32_t ea = av_a ? fa : un, eb = av_b ? fb : un;
+    uint32_t cbfc = 0;  // inside the macroblock: the luma 4x4 blocks' coded_block_flag, raster
     uint32_t todo = m.type == kMbI16 ? 1u << kBlkI16Dc : 0u;
     for (int q = 0; q < 4; ++q)
       if ((cbp >> q) & 1) todo |= (t8 ? 1u : 15u) << (kBlkLuma0 + 4 * q);
@@ -912,12 +903,9 @@ struct CabacParser : Parser {
       int cat, inc = 0, maxNum = 16, start = 0, r = 0;
       int16_t *dst = sc->blk;
       if (bt == kBlkI16Dc) {
+        // an available neighbour's Intra16x16DCLevel flag (I_PCM: 1, other types 0)
         cat = 0;
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-          const int n = nb ? B : A;
-          inc += cbf_cond(n, true, n != -1 && rec(n).type == kMbI16, 0) << nb;
-        }
+        inc = static_cast<int>(((av_a ? fa : ~0u) & kECbfDc) ? 1 : 0) + 2 * static_cast<int>(((av_b ? fb : ~0u) & kECbfDc) ? 1 : 0);
       } else if (bt < kBlkChromaDc0) {
         const int k = static_cast<int>(bt) - kBlkLuma0, bx = blk_x(k), by = blk_y(k);
         r = by * 4 + bx;
@@ -931,20 +919,24 @@ struct CabacParser : Parser {
             maxNum = 15;
             start = 1;
           }
-          const uint32_t ca = bx ? (cbfc >> (r - 1)) & 1u : (nbl >> by) & 1u;
-          const uint32_t cb = by ? (cbfc >> (r - 4)) & 1u : (nbl >> (4 + bx)) & 1u;
+          const uint32_t ca = bx ? (cbfc >> (r - 1)) & 1u : (ea >> (kECbfSh + by)) & 1u;
+          const uint32_t cb = by ? (cbfc >> (r - 4)) & 1u : (eb >> (kECbfSh + bx)) & 1u;
           inc = static_cast<int>(ca + 2 * cb);
         }
       } else if (bt < kBlkChromaAc0) {
         cat = 3;
         maxNum = 4;
-        inc = cbf_chroma_inc(addr, static_cast<int>(bt) - kBlkChromaDc0, 0, true, intra);
+        const int pl = static_cast<int>(bt) - kBlkChromaDc0;
+        inc = static_cast<int>((ea >> (kECdcSh + pl)) & 1u) + 2 * static_cast<int>((eb >> (kECdcSh + pl)) & 1u);
       } else {
-        const int j = static_cast<int>(bt) - kBlkChromaAc0;
+        const int j = static_cast<int>(bt) - kBlkChromaAc0, pl = j >> 2, cx = j & 1, cy = (j >> 1) & 1;
         cat = 4;
         maxNum = 15;
         start = 1;
-        inc = cbf_chroma_inc(addr, j >> 2, j & 3, false, intra);
+        const uint32_t cbf = static_cast<uint32_t>(m.nzc[2]) | (static_cast<uint32_t>(m.nzc[3]) << 8);  // bits 16..31
+        const uint32_t ca = cx ? (cbf >> (kBlkChromaAc0 - 16 + 4 * pl + cy * 2)) & 1u : (ea >> (kECacSh + 2 * pl + cy)) & 1u;
+        const uint32_t cb = cy ? (cbf >> (kBlkChromaAc0 - 16 + 4 * pl + cx)) & 1u : (eb >> (kECacSh + 2 * pl + cx)) & 1u;
+        inc = static_cast<int>(ca + 2 * cb);
       }
       zero16x(dst, cat == 5 ? 64 : 16);
       const int nc = cat == 5 ? residual_t<true>(5, 0, 64, dst, 0) : residual_t<false>(cat, inc, maxNum, dst, start);
@@ -957,7 +949,7 @@ struct CabacParser : Parser {
         }
         if (nc)
           for (int j = 0; j < 4; ++j)
-            if (!store_block(bt + j, sc->blk8 + 16 * j)) { err |= DEC_E_SYNTAX; return false; }
+            if (!store_block(bt + j, sc->blk8 + 16 * j)) { err |= DEC_E_ARENA; return false; }
         continue;
       }
       if (cat == 1 || cat == 2) {
@@ -966,7 +958,7 @@ struct CabacParser : Parser {
       }
       if (nc) {
         set_cbf(bt == kBlkI16Dc ? 0u : (cat <= 2 ? 1u + static_cast<uint32_t>(r) : bt));
-        if (!store_block(bt)) { err |= DEC_E_SYNTAX; return false; }
+        if (!store_block(bt, sc->blk)) { err |= DEC_E_ARENA; return false; }
       }
     }
     VTS_PROF(6);
@@ -976,60 +968,33 @@ struct CabacParser : Parser {
     }
     return true;
   }
-
-  // after a macroblock: its clamped |mvd| for the neighbours below / right
-  VTS_HD VTS_INLINE void finish_mvd() {
-    MbRec &m = cur();
-    if (m.type == kMbInter)
-      for (int x = 0; x < 4; ++x) {
-        m.i4[2 * x] = sc->mvx[0][4][1 + x][0];
-        m.i4[2 * x + 1] = sc->mvx[0][4][1 + x][1];
-      }
-    if (bframes) {
-      MbRecB &m1 = cur1();
-      for (int x = 0; x < 4; ++x) {
-        m1.mvd1[2 * x] = sc->mvx[1][4][1 + x][0];
-        m1.mvd1[2 * x + 1] = sc->mvx[1][4][1 + x][1];
-      }
-    }
-  }
-
-  bool P_t8mode;
 };
 
 // Parse CABAC slice `s` (window slice index si) from its RBSP (rbsp_len
-// bytes, emulation-prevention bytes removed).  Returns DEC_E_* bits.
+// bytes, emulation-prevention bytes removed) into syntax records (above);
+// sc is the wave's scratch with SynEdge[P.mb_width] behind it.  Returns
+// DEC_E_* bits.
 VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_len, const FullSlice &s, uint32_t si,
-                                         const FullParams P, MbRec *frame_recs, uint16_t *frame_ilvl, int16_t *arena,
-                                         uint32_t epoch, FullScratch *sc, const BCtx &bc) {
-  CabacParser p;
-  p.bc = bc;
-  p.bframes = P.bframes;
-  p.direct8x8 = P.direct8x8;
-  if (s.is_p == kSliceB && (!bc.x || !bc.col || !P.bframes)) return DEC_E_NO_REF;
+                                             const FullParams P, MbRec *frame_recs, MbRecB *frame_recs1,
+                                             const SliceExt *x, int16_t *arena, uint32_t epoch, SynScratch *sc) {
+  CabacSyn p;
+  p.bframes = P.bframes != 0;
+  p.direct8x8 = P.direct8x8 != 0;
+  p.t8mode = P.t8mode != 0;
+  if (s.is_p == kSliceB && (!x || !P.bframes)) return DEC_E_NO_REF;
   p.s = &s;
-  p.cip = P.cip;
-  p.P_t8mode = P.t8mode != 0;
+  p.x = x;
   p.recs = frame_recs;
-  p.ilvl = frame_ilvl;
+  p.recs1 = frame_recs1;
   p.arena = arena;
   p.sc = sc;
+  p.top = reinterpret_cast<SynEdge *>(reinterpret_cast<uint8_t *>(sc) + (sizeof(SynScratch) + 15) / 16 * 16);
   p.used = 0;
   p.slice_index = si;
   p.epoch = epoch;
   p.mbw = P.mb_width;
   p.first_mb = s.first_mb;
   p.err = 0;
-  p.cur_addr = -2;
-  p.cs = 0;
-  p.tslots = 0;
-  p.lvl_prev = kNoLevel;
-  p.pf_col = -1;
-#if defined(__HIP_DEVICE_COMPILE__)
-  p.pf_col2 = -1;
-#endif
-  p.todo = 0;
-  p.cur_i16 = false;
   p.prev_qpd = false;
   const int nmb = P.mb_width * P.mb_height;
   // the RBSP stop bit, past any trailing cabac_zero_words (zero bytes once
@@ -1059,27 +1024,22 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
     p.begin_mb(addr);
     VTS_PROF_P(p, 2);
     bool ok = true, skip = false;
-    if (s.is_p) {
-      int xw, yw;
-      const int A = p.nb_mb(addr, -1, 0, 16, &xw, &yw), B = p.nb_mb(addr, 0, -1, 16, &xw, &yw);
-      p.mvd_border(A, B);
-      p.ref_border(A, B);
-      p.mv_border(addr);
-      skip = p.dec((s.is_p == kSliceB ? 24 : 11) + (p.avail_not(A, kMbSkip) ? 1 : 0) +
-                   (p.avail_not(B, kMbSkip) ? 1 : 0)) != 0;
-    }
+    if (s.is_p)
+      skip = p.dec((s.is_p == kSliceB ? 24 : 11) + (p.av_a && CabacSyn::etype(p.fa) != kMbSkip ? 1 : 0) +
+                   (p.av_b && CabacSyn::etype(p.fb) != kMbSkip ? 1 : 0)) != 0;
     if (skip) {
       VTS_PARSE_TRACE(s.is_p == kSliceB ? 4 : 5);
       VTS_PROF_P(p, 3);
-      if (s.is_p == kSliceB) p.b_skip_body(addr, qp);
-      else p.skip_body(addr, qp);
+      MbRec &m = p.cur();
+      m.type = kMbSkip;
+      m.qp = static_cast<uint8_t>(qp);
+      if (s.is_p == kSliceB) p.cur1().direct = 0x0f | kDirect16;
       p.prev_qpd = false;
     } else {
-      ok = p.mb_cabac(addr, &qp);  // one inlined copy for every slice type
+      ok = p.mb_cabac(&qp);  // one inlined copy for every slice type
     }
     if (!ok || p.err) break;
     VTS_PROF_P(p, 6);
-    p.finish_mvd();
     p.end_mb(addr);
     ++addr;
     if (p.term()) break;  // end_of_slice_flag

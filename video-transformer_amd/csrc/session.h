@@ -44,6 +44,8 @@ struct Window {
   int64_t pn0 = 0;                 // general decoder: the window's slot entries in vts_ctx::pneed
   std::vector<int32_t> plv_end;    // general decoder: parse launch j covers window slices
                                    // [plv_end[j-1], plv_end[j]) (B pictures after their colocated picture)
+  int64_t ds0 = 0;                 // general decoder, CABAC: the window's entries in vts_ctx::dslots
+  std::vector<int32_t> dlv_end;    // ... h264_derive launch j covers entries [dlv_end[j-1], dlv_end[j])
 };
 
 // Downscaled copy of every decoded frame (transcode.hip), filled by run_all
@@ -187,6 +189,8 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
+  std::vector<int32_t> dslots;          // CABAC: ring slots of the windows' pictures by parse level (h264_derive)
+  int32_t *d_dslots = nullptr;
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full (its LDS fallback)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<hipEvent_t> ev_bs;  // paced bS: two per level launch of a window (reused window to window)

@@ -253,6 +253,9 @@ int alloc_general(vts_ctx *c) {
   HIP_TRY(vts::dmalloc(&c->d_porder_m, sizeof(int32_t) * std::max<size_t>(1, c->porder_m.size())));
   if (!c->porder_m.empty())
     HIP_TRY(hipMemcpy(c->d_porder_m, c->porder_m.data(), sizeof(int32_t) * c->porder_m.size(), hipMemcpyHostToDevice));
+  HIP_TRY(vts::dmalloc(&c->d_dslots, sizeof(int32_t) * std::max<size_t>(1, c->dslots.size())));
+  if (!c->dslots.empty())
+    HIP_TRY(hipMemcpy(c->d_dslots, c->dslots.data(), sizeof(int32_t) * c->dslots.size(), hipMemcpyHostToDevice));
   HIP_TRY(vts::dmalloc(&c->d_pneed, sizeof(int32_t) * std::max<size_t>(1, c->pneed.size())));
   if (!c->pneed.empty())
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
@@ -1293,6 +1296,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_porder);
   f(c->d_porder_m);
   f(c->d_pneed);
+  f(c->d_dslots);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);

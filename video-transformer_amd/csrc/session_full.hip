@@ -198,6 +198,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   c->porder.clear();
   c->porder_m.clear();
   c->pneed.clear();
+  c->dslots.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
   for (Window &w : c->windows) {
@@ -273,12 +274,32 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       return c->fslices[static_cast<size_t>(b + x)].nal_size > c->fslices[static_cast<size_t>(b + y)].nal_size;
     });
     }
-    // merged parse launch: the levels' orders back to back (window-relative),
-    // and each picture slot's slice count
-    for (size_t j = 0; j < w.plv_end.size(); ++j) {
-      const int32_t b0 = j ? w.plv_end[j - 1] : 0;
-      for (int32_t k = b0; k < w.plv_end[j]; ++k)
-        c->porder_m.push_back(b0 + c->porder[static_cast<size_t>(w.fs0 + k)]);
+    // merged parse launch (window-relative): CAVLC, the levels' orders back
+    // to back (a B slice waits for its colocated picture's slices, which
+    // therefore come first); CABAC, every slice of the window longest first
+    // (its slices are independent: h264_derive does the colocated reads)
+    if (c->fprm.cabac) {
+      const int64_t nws = static_cast<int64_t>(c->fslices.size()) - w.fs0;
+      const size_t o0 = c->porder_m.size();
+      for (int64_t k = 0; k < nws; ++k) c->porder_m.push_back(static_cast<int32_t>(k));
+      std::stable_sort(c->porder_m.begin() + static_cast<int64_t>(o0), c->porder_m.end(), [&](int32_t a, int32_t b) {
+        return c->fslices[static_cast<size_t>(w.fs0 + a)].nal_size > c->fslices[static_cast<size_t>(w.fs0 + b)].nal_size;
+      });
+    } else {
+      for (size_t j = 0; j < w.plv_end.size(); ++j) {
+        const int32_t b0 = j ? w.plv_end[j - 1] : 0;
+        for (int32_t k = b0; k < w.plv_end[j]; ++k)
+          c->porder_m.push_back(b0 + c->porder[static_cast<size_t>(w.fs0 + k)]);
+      }
+    }
+    // h264_derive launches (CABAC): the window's pictures by parse level, so a
+    // B picture's colocated picture is complete before it
+    w.ds0 = static_cast<int64_t>(c->dslots.size());
+    w.dlv_end.clear();
+    for (int32_t pl = 0; pl <= maxp; ++pl) {
+      for (int64_t f = w.f0; f < w.f1; ++f)
+        if (plevel[static_cast<size_t>(f)] == pl) c->dslots.push_back(slot_of(f));
+      w.dlv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->dslots.size()) - w.ds0));
     }
     w.pn0 = static_cast<int64_t>(c->pneed.size());
     c->pneed.resize(c->pneed.size() + static_cast<size_t>(w.f1 - w.f0), 0);
@@ -373,7 +394,32 @@ int run_general(vts_ctx *c) {
     pa.arena = c->d_arena[r];
     pa.err = c->d_err;
     pa.P = c->fprm;
-    if (c->parse_merged && w.plv_end.size() > 1) {
+    if (c->fprm.cabac) {
+      // syntax records of every slice (no waits), then the per-picture
+      // derivation by parse level
+      pa.slices = c->d_fslices + w.fs0;
+      pa.rbsp_len = c->d_rbsp_len + w.fs0;
+      pa.n_slices = static_cast<int32_t>(w.fs1 - w.fs0);
+      pa.slice0 = 0;
+      pa.order = c->d_porder_m + w.fs0;
+      pa.pdone = nullptr;
+      pa.pneed = nullptr;
+      VTS_TRY(parse_full_launch(pa, sp));
+      DeriveArgs da{};
+      da.recs = c->d_recs[r];
+      da.recs1 = c->d_recs1[r];
+      da.ilvl = c->d_ilvl[r];
+      da.slices = c->d_fslices + w.fs0;
+      da.exts = c->d_exts;
+      da.err = c->d_err;
+      da.epoch = epoch;
+      da.P = c->fprm;
+      for (size_t j = 0; j < w.dlv_end.size(); ++j) {
+        const int32_t b0 = j ? w.dlv_end[j - 1] : 0;
+        da.slots = c->d_dslots + w.ds0 + b0;
+        VTS_TRY(derive_launch(da, w.dlv_end[j] - b0, sp));
+      }
+    } else if (c->parse_merged && w.plv_end.size() > 1) {
       // one launch: B slices wait for their colocated pictures' slices, which
       // come first in the order, so the launch ends on a full machine instead
       // of once per colocated level on its longest slices alone
