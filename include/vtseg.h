@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VTS_ABI_VERSION 6
+#define VTS_ABI_VERSION 7
 
 enum {
   VTS_OK = 0,
@@ -280,6 +280,13 @@ int vts_score(vts_ctx *ctx, float *scores, uint32_t *hist, uint64_t *sad,
  * results stay on the device; returns after the work is enqueued and
  * finished (synchronous). */
 int vts_run(vts_ctx *ctx);
+/* vts_run split in two: vts_run_async enqueues the run on the session's HIP
+ * streams and returns; vts_wait blocks until it is done (errors, timings and
+ * any re-run as in vts_run).  Several sessions submitted before any waits
+ * share the device (plan_batch).  Entry points that read results wait
+ * themselves; vts_close waits for a run nobody waited for. */
+int vts_run_async(vts_ctx *ctx);
+int vts_wait(vts_ctx *ctx);
 /* Scene cut frame indices (score > threshold) of the last vts_score/vts_run. */
 int vts_scene_cuts(vts_ctx *ctx, int64_t *frame_idx, int64_t cap,
                    int64_t *n_out);
@@ -306,6 +313,9 @@ int vts_last_timings(const vts_ctx *ctx, double *ms4);
  * cache that later sessions reuse (re-allocating released HBM waits while the
  * driver clears it); this hands device `device`'s cache back to HIP. */
 int vts_empty_cache(int device);
+/* Bytes of device memory the sessions' allocator has handed out on `device`
+ * (open sessions' buffers; the cache's free ranges excluded). */
+int64_t vts_device_bytes(int device);
 /* Host time of the vts_open that made ctx, milliseconds, by stage:
  * [0] demux (moov) + device checks, [1] unused, [2] sample read (parallel
  * pread), [3] host decode schedule, [4] device allocations (+ the general
@@ -314,7 +324,10 @@ int vts_empty_cache(int device);
  * Writes min(cap, 8) entries; returns 8. */
 int vts_open_timings(const vts_ctx *ctx, double *ms, int32_t cap);
 /* Decode schedule facts: what = 0 reconstruct launches per run, 1 windows,
- * 2 slices, 3 ring frames, 4 fused scoring (1/0); < 0 on error. */
+ * 2 slices, 3 ring frames, 4 fused scoring (1/0), 5 / 6 level-blocked
+ * launches / chains, 7 chain slots, 8 general decoder (1/0), 9 runs repeated
+ * with the bound's CABAC coefficient arena, 10 coefficient blocks per ring;
+ * < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);  /* 8: general decoder in use (1/0) */
 int vts_close(vts_ctx *ctx);
 

@@ -305,6 +305,14 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
       dc.cip = P.cip;
       dc.direct8x8 = P.direct8x8;
       dc.bframes = P.bframes;
+      dc.col = -2;  // the colocated picture the frame's B slices share, else -1 (per macroblock)
+      for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
+        const FullSlice &fsl = fs[static_cast<size_t>(si)];
+        if (fsl.is_p != kSliceB) continue;
+        const int cs = exts[static_cast<size_t>(fsl.ext)].ref_slot1[0];
+        dc.col = (dc.col == -2 || dc.col == cs) ? cs : -1;
+      }
+      if (dc.col < 0) dc.col = -1;
       std::vector<full::DEdge> er(static_cast<size_t>(nmb)), eb(static_cast<size_t>(nmb));
       full::DWork w;
       for (int a = 0; a < nmb; ++a) {
@@ -313,7 +321,9 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
         const full::DEdge *B = y > 0 ? &eb[static_cast<size_t>(a - mbw)] : nullptr;
         const full::DEdge *C = y > 0 && x + 1 < mbw ? &eb[static_cast<size_t>(a - mbw + 1)] : nullptr;
         const full::DEdge *D = y > 0 && x > 0 ? &eb[static_cast<size_t>(a - mbw - 1)] : nullptr;
-        errs |= full::derive_mb(dc, a, A, B, C, D, w, &er[static_cast<size_t>(a)], &eb[static_cast<size_t>(a)]);
+        full::DIn in;
+        full::derive_load(dc, a, in);
+        errs |= full::derive_mb(dc, a, in, A, B, C, D, w, &er[static_cast<size_t>(a)], &eb[static_cast<size_t>(a)]);
       }
       if (errs) return bad("frame " + std::to_string(fi) + ": derive: " + describe_decode_error(errs));
     }

@@ -422,15 +422,45 @@ def test_scaling_matrix_streams_bit_exact(tmp_path, name, kw):
 
 
 @pytest.mark.parametrize("merge", ["0", "1"])
-def test_cabac_b_parse_merged_and_per_level(tmp_path, monkeypatch, merge):
-    """the merged parse launch (default; B slices wait on their
-    colocated picture's completion counter) and the per-level fallback
-    (VTS_PARSE_MERGE=0: one launch per colocated level) both equal the
-    oracle on a CABAC B stream with temporal direct in several windows."""
+def test_cavlc_b_parse_merged_and_per_level(tmp_path, monkeypatch, merge):
+    """the CAVLC parser's merged launch (default; B slices wait on
+    their colocated picture's completion counter) and the per-level fallback
+    (VTS_PARSE_MERGE=0: one launch per colocated level) both equal the oracle
+    on a B stream with temporal direct in several windows.  (The CABAC parser
+    has no such wait: h264_derive reads the colocated records, by parse
+    level, test_cabac_temporal_direct_windows_and_arena_rerun.)"""
     _require_gpu()
     monkeypatch.setenv("VTS_PARSE_MERGE", merge)
     n = 60
-    src, path = tmp_path / "src.mp4", tmp_path / "mb.mp4"
+    path = tmp_path / "mb.mp4"
+    scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=True,
+                      temporal_direct=True, weighted="implicit", cut_min_s=0.5, cut_max_s=1.2,
+                      gop_max_s=0.6, seed=21, chunks=1)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
+    for wf in (0, 24):
+        with scene.VideoScorer(path, keep_frames=wf == 0, window_frames=wf, n_streams=2) as v:
+            assert v.general()
+            res = v.score()
+            if wf == 0:
+                got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
+                assert _first_diff(got, frames) == []
+            assert np.array_equal(res.hist, ref["hist"])
+            assert np.array_equal(res.scores, ref["score"])
+
+
+@pytest.mark.parametrize("per_byte", ["4", "0"], ids=["estimate", "overflow_rerun"])
+def test_cabac_temporal_direct_windows_and_arena_rerun(tmp_path, monkeypatch, per_byte):
+    """The CABAC syntax parse + h264_derive (colocated records read by parse
+    level) on a B stream with temporal direct, in one window and in several
+    windows on two rings; with VTS_ARENA_PER_BYTE=0 every slice's estimated
+    coefficient range (64 blocks) overflows, the run reports DEC_E_ARENA to
+    the host, which sizes the ranges from the bound and runs again: every
+    frame, histogram and score equals the oracle either way."""
+    _require_gpu()
+    monkeypatch.setenv("VTS_ARENA_PER_BYTE", per_byte)
+    n = 60
+    src, path = tmp_path / "src.mp4", tmp_path / "td.mp4"
     scene.synth_write(src, width=176, height=144, n_frames=n, coding="full", bframes=True,
                       temporal_direct=True, weighted="implicit", cut_min_s=0.5, cut_max_s=1.2,
                       gop_max_s=0.6, seed=21, chunks=1)
@@ -439,12 +469,54 @@ def test_cabac_b_parse_merged_and_per_level(tmp_path, monkeypatch, merge):
     ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
     for wf in (0, 24):
         with scene.VideoScorer(path, keep_frames=wf == 0, window_frames=wf, n_streams=2) as v:
+            assert v.general()
             res = v.score()
+            res2 = v.score()  # a second run on the re-sized arena
             if wf == 0:
                 got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
                 assert _first_diff(got, frames) == []
-            assert np.array_equal(res.hist, ref["hist"])
-            assert np.array_equal(res.scores, ref["score"])
+            for r in (res, res2):
+                assert np.array_equal(r.hist, ref["hist"])
+                assert np.array_equal(r.scores, ref["score"])
+            assert v.arena_reruns() == (1 if per_byte == "0" else 0)
+
+
+def test_async_runs_of_several_sessions_equal_the_oracle(tmp_path):
+    """vts_run_async on three sessions (a CABAC B, a CAVLC B and a subset
+    stream) before any vts_wait: the device overlaps them and every result
+    equals the oracle; results read without an explicit wait complete the
+    run first; a session closed with a run still pending waits for it."""
+    _require_gpu()
+    n = 48
+    paths = [tmp_path / f"a{i}.mp4" for i in range(3)]
+    src = tmp_path / "src.mp4"
+    scene.synth_write(src, width=176, height=144, n_frames=n, coding="full", bframes=True, weighted="implicit",
+                      cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.5, seed=29, chunks=1)
+    oracle.cabac_convert(src, paths[0], seed=9, t8=True)
+    scene.synth_write(paths[1], width=176, height=144, n_frames=n, coding="full", bframes=True,
+                      weighted="implicit", cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.5, seed=31)
+    scene.synth_write(paths[2], width=176, height=144, n_frames=n, cut_min_s=0.5, cut_max_s=1.2, seed=37)
+    refs = []
+    for i, p in enumerate(paths):
+        frames, _ = (oracle.decode_full(p) if i < 2 else oracle.decode_file(p))
+        refs.append(oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4))
+    vs = [scene.VideoScorer(p) for p in paths]
+    try:
+        for _ in range(2):
+            for v in vs:
+                v.run_async()
+            for i, v in enumerate(vs):
+                if i != 1:
+                    v.wait()      # session 1: scene_cuts() below waits itself
+                cuts = v.scene_cuts()
+                assert cuts == np.nonzero(refs[i]["score"] > 0.08)[0].tolist()
+                res = v.score()
+                assert np.array_equal(res.scores, refs[i]["score"])
+                assert np.array_equal(res.hist, refs[i]["hist"])
+        vs[0].run_async()  # left pending: close waits
+    finally:
+        for v in vs:
+            v.close()
 
 
 def test_sessions_reopened_in_sequence_reuse_the_stream_pool(tmp_path):

@@ -16,7 +16,7 @@ struct FullParseArgs {
   int32_t n_slices;
   int32_t slice0;            // window index of slices[0] (MbRec.slice)
   uint32_t epoch;
-  int32_t _pad;
+  int32_t n_long;            // CABAC: the first n_long workgroups (longest slices) raise their wave priority
   MbRec *recs;               // ring: [slot][mb]
   MbRecB *recs1;             // ring: [slot][mb] list-1 halves (P.bframes), else null
   const SliceExt *exts;      // the window's SliceExt records
@@ -35,7 +35,8 @@ struct FullParseArgs {
 // h264_derive: complete the CABAC parse's syntax records of n pictures (their
 // colocated pictures completed by an earlier launch)
 struct DeriveArgs {
-  const int32_t *slots;      // ring slot of picture i of the launch
+  const int2 *pics;          // picture i of the launch: (ring slot, its B slices' common colocated
+                             // slot RefPicList1[0], or -1: none / they differ)
   MbRec *recs;               // ring: [slot][mb]
   MbRecB *recs1;             // ring: [slot][mb] list-1 halves (P.bframes), else null
   uint16_t *ilvl;            // ring: [slot][mb] intra dependency levels (written)
@@ -66,7 +67,7 @@ struct DbkInfo {
 static_assert(sizeof(DbkInfo) == 96, "DbkInfo layout");
 
 struct FullReconArgs {
-  const int4 *frames;        // (slot, -, -, -) per picture of the launch
+  const int4 *frames;        // (ring slot, descriptor slot in dbk, -, -) per picture of the launch
   const MbRec *recs;
   const MbRecB *recs1;       // list-1 halves (P.bframes), else null
   const SliceExt *exts;      // the window's SliceExt records (FullSlice.ext)
@@ -80,7 +81,8 @@ struct FullReconArgs {
   uint32_t epoch;
   int32_t deblock;           // 1: h264_deblock_plane after reconstruction (0: none)
   int32_t intra_kernel;      // 1: h264_intra_full, else h264_intra_v2 (where its LDS fits)
-  DbkInfo *dbk;              // ring: [slot][mb] deblocking descriptors
+  DbkInfo *dbk;              // [descriptor slot][mb] deblocking descriptors: a ring of two levels per GOP
+                             // group (bS of level l + 1 is derived while level l deblocks)
   uint32_t *err;
   const ScaleTab *sct;       // LevelScale4x4 / 8x8 (read when P.scaled)
   FullParams P;

@@ -36,6 +36,10 @@
 // parse section timing (experiment builds): s_memtime deltas per section,
 // summed over all slices; read with vts_debug_parse_prof
 __device__ unsigned long long vts_prof_acc[8];
+// per workgroup of the last CABAC parse launch: start / end s_memtime and the
+// hardware id (s_getreg HW_ID: wave, SIMD, CU, SE / XCC bits), read with
+// vts_debug_parse_waves
+__device__ unsigned long long vts_wave_t[3 * 65536];
 #if !defined(__HIP_DEVICE_COMPILE__)
 #define VTS_PROF(k)
 #define VTS_PROF_P(p, k)
@@ -180,7 +184,15 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
 __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full_cabac(FullParseArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t syn_lds[];
+#ifdef VTS_EXP_PROF
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
   const int i = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
+#ifndef VTS_EXP_NOPRIO
+  // the launch's longest slices (first in the order) bound it: their waves
+  // win the issue arbitration against the short slices' waves beside them
+  if (static_cast<int>(blockIdx.x) < a.n_long) __builtin_amdgcn_s_setprio(3);
+#endif
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
   const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
@@ -190,6 +202,14 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
                                              s.ext >= 0 ? a.exts + s.ext : nullptr, a.arena, a.epoch,
                                              reinterpret_cast<full::SynScratch *>(syn_lds));
   if (e) atomicOr(a.err, e);
+#ifdef VTS_EXP_PROF
+  if (threadIdx.x == 0 && blockIdx.x < 65536) {
+    vts_wave_t[3 * blockIdx.x] = t_start;
+    vts_wave_t[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime();
+    vts_wave_t[3 * blockIdx.x + 2] = static_cast<unsigned long long>(i) |
+                                     (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) << 32);
+  }
+#endif
 }
 
 // One workgroup per picture, one lane per macroblock row: at step t row y
@@ -201,7 +221,8 @@ __global__ void __launch_bounds__(256) h264_derive(DeriveArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dlds[];
   const int mbw = a.P.mb_width, mbh = a.P.mb_height;
   const int64_t nmb = static_cast<int64_t>(mbw) * mbh;
-  const int slot = a.slots[blockIdx.x];
+  const int2 pic = a.pics[blockIdx.x];
+  const int slot = pic.x;
   full::DWork *work = reinterpret_cast<full::DWork *>(dlds);                   // [blockDim]
   full::DEdge *ring = reinterpret_cast<full::DEdge *>(work + blockDim.x);      // [mbh][4]
   full::DEdge *left = ring + 4 * mbh;                                          // [mbh]
@@ -219,18 +240,24 @@ __global__ void __launch_bounds__(256) h264_derive(DeriveArgs a) {
   c.cip = a.P.cip;
   c.direct8x8 = a.P.direct8x8;
   c.bframes = a.P.bframes;
+  c.col = pic.y;
   const int y = static_cast<int>(threadIdx.x);
   uint32_t err = 0;
   const int steps = mbw + 2 * (mbh - 1);
+  full::DIn nxt;  // the lane's next macroblock's words, loaded one step ahead
   for (int t = 0; t < steps; ++t) {
     const int x = t - 2 * y;
     if (y < mbh && x >= 0 && x < mbw) {
+      full::DIn in;
+      if (x == 0) full::derive_load(c, y * mbw, in);
+      else in = nxt;
+      if (x + 1 < mbw) full::derive_load(c, y * mbw + x + 1, nxt);
       const full::DEdge *A = x > 0 ? &left[y] : nullptr;
       const full::DEdge *B = y > 0 ? &ring[4 * (y - 1) + (x & 3)] : nullptr;
       const full::DEdge *C = y > 0 && x + 1 < mbw ? &ring[4 * (y - 1) + ((x + 1) & 3)] : nullptr;
       const full::DEdge *D = y > 0 && x > 0 ? &ring[4 * (y - 1) + ((x - 1) & 3)] : nullptr;
       // the right edge replaces the left one (derive_mb writes its edges last)
-      err |= full::derive_mb(c, y * mbw + x, A, B, C, D, work[y], &left[y], &ring[4 * y + (x & 3)]);
+      err |= full::derive_mb(c, y * mbw + x, in, A, B, C, D, work[y], &left[y], &ring[4 * y + (x & 3)]);
     }
     __syncthreads();
   }
@@ -1400,7 +1427,7 @@ __device__ __forceinline__ uint32_t edge_word(int qpav, int fa, int fb) {
 // an OR butterfly over its 16 lanes, so the wavefront below reads one 32-byte
 // descriptor per macroblock.  (A lane per macroblock walking all 32 edges
 // made every load a strided 4-byte gather.)
-__device__ void bs_mb(const FullReconArgs &a, int slot, int mb, int b) {
+__device__ void bs_mb(const FullReconArgs &a, int slot, int di, int mb, int b) {
   const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
   const bool ok = mb < nmb;
   const int mbc = ok ? mb : nmb - 1;  // tail lanes: a valid macroblock, result unused (the butterfly needs them)
@@ -1447,7 +1474,7 @@ __device__ void bs_mb(const FullReconArgs &a, int slot, int mb, int b) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(w[i]), m, 16));
   if (!ok || b > 5) return;
-  DbkInfo *o = a.dbk + static_cast<int64_t>(slot) * nmb + mb;
+  DbkInfo *o = a.dbk + static_cast<int64_t>(di) * nmb + mb;
   const int qpq = tq == kMbPcm ? 0 : hq.qp;
   if (b == 0) {
     reinterpret_cast<uint4 *>(o)[0] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -1475,7 +1502,8 @@ __device__ void bs_mb(const FullReconArgs &a, int slot, int mb, int b) {
   }
 }
 __global__ void __launch_bounds__(256) h264_bs_full(FullReconArgs a) {
-  bs_mb(a, a.frames[blockIdx.y].x, blockIdx.x * 16 + (threadIdx.x >> 4), threadIdx.x & 15);
+  const int4 f = a.frames[blockIdx.y];
+  bs_mb(a, f.x, f.y, blockIdx.x * 16 + (threadIdx.x >> 4), threadIdx.x & 15);
 }
 
 
@@ -1544,6 +1572,10 @@ extern "C" int vts_debug_recon_prof(unsigned long long *out) {
 }
 #endif
 #ifdef VTS_EXP_PROF
+extern "C" int vts_debug_parse_waves(unsigned long long *out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_wave_t), sizeof(unsigned long long) * 3 * static_cast<size_t>(n)) == hipSuccess
+             ? 0 : -1;
+}
 extern "C" int vts_debug_parse_prof(unsigned long long *out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_prof_acc), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
   unsigned long long z[8] = {};
@@ -1629,7 +1661,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_
   Line(*ring)[kDpRingCols] = reinterpret_cast<Line(*)[kDpRingCols]>(lds + sizeof(Tile) * kDpGroups);
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
   const int slot = a.frames[pic].x;
-  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(slot) * nmb;
+  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(a.frames[pic].y) * nmb;
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
   const uint32_t uvo = static_cast<uint32_t>(a.uv_off);
   auto at = [Y](uint32_t o) { return Y + static_cast<uint64_t>(o); };

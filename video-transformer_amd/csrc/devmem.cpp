@@ -31,6 +31,7 @@ struct Device {
   std::multimap<size_t, char *> free_by_size;  // the free ranges
   std::map<char *, size_t> segments;          // base -> bytes
   size_t cached = 0;                          // bytes in free ranges
+  size_t in_use = 0;                          // bytes handed out (ranges not free)
 };
 std::mutex g_mu;
 std::map<int, Device> g_dev;
@@ -73,6 +74,7 @@ void *take_locked(Device &d, char *p, size_t want) {
     r.n = want;
   }
   r.free = false;
+  d.in_use += want;
   return p;
 }
 
@@ -108,6 +110,7 @@ hipError_t dmalloc_raw(void **p, size_t n) {
   char *b = static_cast<char *>(*p);
   d.segments[b] = want;
   d.ranges[b] = Range{want, b, false};
+  d.in_use += want;
   return hipSuccess;
 }
 
@@ -136,6 +139,7 @@ void dfree(void *p) {
   char *q = it->first;
   Range r = it->second;
   r.free = true;
+  d->in_use -= r.n;
   // merge with the next range of the same segment
   auto nx = std::next(it);
   if (nx != d->ranges.end() && nx->second.free && nx->second.base == r.base && nx->first == q + r.n) {
@@ -168,6 +172,12 @@ size_t dmem_cached(int device) {
   return it == g_dev.end() ? 0 : it->second.cached;
 }
 
+size_t dmem_in_use(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_dev.find(device);
+  return it == g_dev.end() ? 0 : it->second.in_use;
+}
+
 hipError_t dmem_free(size_t *free_b, size_t *total_b) {
   const hipError_t e = hipMemGetInfo(free_b, total_b);
   if (e != hipSuccess) return e;
@@ -177,6 +187,8 @@ hipError_t dmem_free(size_t *free_b, size_t *total_b) {
 }
 
 }  // namespace vts
+
+extern "C" int64_t vts_device_bytes(int device) { return static_cast<int64_t>(vts::dmem_in_use(device)); }
 
 extern "C" int vts_empty_cache(int device) {
   std::lock_guard<std::mutex> lk(vts::g_mu);

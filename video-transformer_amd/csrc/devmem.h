@@ -28,6 +28,7 @@ inline hipError_t dmalloc(T **p, size_t n) {
 }
 void dfree(void *p);                 // null-safe; the block's stream work must be finished
 size_t dmem_cached(int device);      // bytes held in the device's cache
+size_t dmem_in_use(int device);      // bytes of the device's cached ranges handed out (sessions' buffers)
 hipError_t dmem_free(size_t *free_b, size_t *total_b);  // hipMemGetInfo + the cache
 
 }  // namespace vts

@@ -319,8 +319,7 @@ struct CabacSyn {
   VTS_HD VTS_INLINE static int etype(uint32_t f) { return static_cast<int>(f & kEType); }
   VTS_HD VTS_INLINE static int ecbp(uint32_t f) { return static_cast<int>((f >> kECbpSh) & 63u); }
 
-  // a new macroblock: its neighbours' edge facts, the record image reset,
-  // the |mvd| grid's borders from the neighbours' edges (one cell per lane)
+  // a new macroblock: its neighbours' availability and edge facts
   VTS_HD VTS_INLINE void begin_mb(int addr) {
     VTS_PARSE_TRACE(0);
     const int xcol = addr % mbw;
@@ -328,6 +327,62 @@ struct CabacSyn {
     av_b = addr - mbw >= first_mb;
     fa = av_a ? sc->left.f : 0u;
     fb = av_b ? top[xcol].f : 0u;
+  }
+  // a skipped macroblock (P_Skip / B_Skip): its record and both edges are
+  // constants but for the QP, so they go out from registers, one 16-byte
+  // piece (record) or dword (edges) per lane, without a record image
+  VTS_HD VTS_INLINE void emit_skip(int addr, int qp, bool is_b) {
+    const uint32_t w4 = kMbSkip | (static_cast<uint32_t>(qp) << 8);
+    const uint32_t ef = kMbSkip | (is_b ? kEDirect16 : 0u);
+    SynEdge *te = &top[addr % mbw];
+#if defined(__HIP_DEVICE_COMPILE__)
+    VTS_LANES(26, l) {
+      if (l < 16) {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (l == 0) v = u32x4{epoch, slice_index, 0u, 0u};
+        else if (l == 1) v = u32x4{w4, ~0u, ~0u, ~0u};
+        else if (l == 2) v = u32x4{0x22222222u, 0x22222222u, 0u, 0u};
+        else if (l == 8) v = u32x4{~0u, ~0u, ~0u, is_b ? 0x1fu : 0u};
+        if (l < 8) reinterpret_cast<u32x4 *>(&recs[addr])[l] = v;
+        else if (bframes && (l < 10 || l >= 12)) reinterpret_cast<u32x4 *>(&recs1[addr])[l - 8] = v;
+      } else {
+        // the edges: dword 0 the flags, 1..4 the (zero) |mvd| bytes
+        const int e = l - 16, k = e % 5;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(e < 5 ? &sc->left : te);
+        dst[k] = k == 0 ? ef : 0u;
+      }
+    }
+#else
+    MbRec m{};
+    m.epoch = epoch;
+    m.slice = slice_index;
+    m.type = kMbSkip;
+    m.qp = static_cast<uint8_t>(qp);
+    for (int i = 0; i < 4; ++i) {
+      m.ref[i] = -1;
+      m.ref_slot[i] = -1;
+    }
+    for (int i = 0; i < 8; ++i) m.i4[i] = 0x22;
+    recs[addr] = m;
+    if (bframes) {
+      MbRecB m1{};
+      for (int i = 0; i < 4; ++i) {
+        m1.ref1[i] = -1;
+        m1.ref_slot1[i] = -1;
+      }
+      m1.direct = is_b ? 0x0f | kDirect16 : 0;
+      recs1[addr] = m1;
+    }
+    SynEdge e{};
+    e.f = ef;
+    sc->left = e;
+    *te = e;
+#endif
+  }
+  // a coded macroblock: the record image reset, the |mvd| grid's borders from
+  // the neighbours' edges (one cell per lane)
+  VTS_HD VTS_INLINE void init_mb(int addr) {
+    const int xcol = addr % mbw;
 #if defined(__HIP_DEVICE_COMPILE__)
     // the record's initial dwords, one per lane: epoch, slice, 0 coef / blocks
     // / type..modes, ref -1, ref_slot -1, i4 DC (2), then zeros; list 1: ref1
@@ -398,9 +453,9 @@ struct CabacSyn {
 #endif
   }
 
-  // the current macroblock's edge facts (right: true = its right edge for
+  // the current macroblock's edge flags (right: true = its right edge for
   // the next macroblock, false = its bottom edge for the one below)
-  VTS_HD VTS_INLINE SynEdge edge_of(bool right) const {
+  VTS_HD VTS_INLINE uint32_t edge_flags(bool right) const {
     const MbRec &m = cur();
     const int ty = m.type;
     uint32_t f = static_cast<uint32_t>(ty);
@@ -434,32 +489,39 @@ struct CabacSyn {
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl)
       if (pcm || ((cbf >> (kBlkChromaDc0 + pl)) & 1u)) f |= 1u << (kECdcSh + pl);
-    SynEdge e;
-    e.f = f;
-#pragma unroll
-    for (int l = 0; l < 2; ++l)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) e.mvd[l][k][c] = right ? sc->mvx[l][1 + k][4][c] : sc->mvx[l][4][1 + k][c];
-    return e;
+    return f;
   }
-  // after a macroblock: its record to global memory (16 bytes per lane), its
-  // edges for the neighbours to the right and below
+  // after a coded macroblock: its record to global memory (16 bytes per
+  // lane), its edges for the neighbours to the right and below (the flags
+  // scalar, the |mvd| bytes one per lane)
   VTS_HD VTS_INLINE void end_mb(int addr) {
-    const SynEdge er = edge_of(true), eb = edge_of(false);
+    const uint32_t fr = edge_flags(true), fbm = edge_flags(false);
+    SynEdge *te = &top[addr % mbw];
 #if defined(__HIP_DEVICE_COMPILE__)
-    VTS_LANES(16, l) {
-      if (l < 8) reinterpret_cast<u32x4 *>(&recs[addr])[l] = reinterpret_cast<const u32x4 *>(&cur())[l];
-      else if (bframes && (l < 10 || l >= 12))
-        reinterpret_cast<u32x4 *>(&recs1[addr])[l - 8] = reinterpret_cast<const u32x4 *>(&cur1())[l - 8];
+    VTS_LANES(64, l) {
+      if (l < 16) {
+        if (l < 8) reinterpret_cast<u32x4 *>(&recs[addr])[l] = reinterpret_cast<const u32x4 *>(&cur())[l];
+        else if (bframes && (l < 10 || l >= 12))
+          reinterpret_cast<u32x4 *>(&recs1[addr])[l - 8] = reinterpret_cast<const u32x4 *>(&cur1())[l - 8];
+      } else if (l < 48) {
+        // byte (list, k, component) of the right (lanes 16..31) / bottom (32..47) edge
+        const int e = l - 16, bot = e >> 4, li = (e >> 3) & 1, k = (e >> 1) & 3, cc = e & 1;
+        const uint8_t v = bot ? sc->mvx[li][4][1 + k][cc] : sc->mvx[li][1 + k][4][cc];
+        (bot ? te : &sc->left)->mvd[li][k][cc] = v;
+      }
     }
 #else
     recs[addr] = cur();
     if (bframes) recs1[addr] = cur1();
+    for (int li = 0; li < 2; ++li)
+      for (int k = 0; k < 4; ++k)
+        for (int cc = 0; cc < 2; ++cc) {
+          sc->left.mvd[li][k][cc] = sc->mvx[li][1 + k][4][cc];
+          te->mvd[li][k][cc] = sc->mvx[li][4][1 + k][cc];
+        }
 #endif
-    sc->left = er;
-    top[addr % mbw] = eb;
+    sc->left.f = fr;
+    te->f = fbm;
   }
 
   // store sc->blk (or src) as the next arena block; bit = kBlk* index
@@ -1023,24 +1085,21 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
     VTS_PROF_P(p, 1);
     p.begin_mb(addr);
     VTS_PROF_P(p, 2);
-    bool ok = true, skip = false;
+    bool skip = false;
     if (s.is_p)
       skip = p.dec((s.is_p == kSliceB ? 24 : 11) + (p.av_a && CabacSyn::etype(p.fa) != kMbSkip ? 1 : 0) +
                    (p.av_b && CabacSyn::etype(p.fb) != kMbSkip ? 1 : 0)) != 0;
     if (skip) {
       VTS_PARSE_TRACE(s.is_p == kSliceB ? 4 : 5);
       VTS_PROF_P(p, 3);
-      MbRec &m = p.cur();
-      m.type = kMbSkip;
-      m.qp = static_cast<uint8_t>(qp);
-      if (s.is_p == kSliceB) p.cur1().direct = 0x0f | kDirect16;
+      p.emit_skip(addr, qp, s.is_p == kSliceB);
       p.prev_qpd = false;
     } else {
-      ok = p.mb_cabac(&qp);  // one inlined copy for every slice type
+      p.init_mb(addr);
+      if (!p.mb_cabac(&qp) || p.err) break;  // one inlined copy for every slice type
+      VTS_PROF_P(p, 6);
+      p.end_mb(addr);
     }
-    if (!ok || p.err) break;
-    VTS_PROF_P(p, 6);
-    p.end_mb(addr);
     ++addr;
     if (p.term()) break;  // end_of_slice_flag
   }

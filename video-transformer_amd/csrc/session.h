@@ -45,6 +45,7 @@ struct Window {
   std::vector<int32_t> plv_end;    // general decoder: parse launch j covers window slices
                                    // [plv_end[j-1], plv_end[j]) (B pictures after their colocated picture)
   int64_t ds0 = 0;                 // general decoder, CABAC: the window's entries in vts_ctx::dslots
+  int32_t n_long = 0;              // ... its long slices (first in the parse order, wave priority raised)
   std::vector<int32_t> dlv_end;    // ... h264_derive launch j covers entries [dlv_end[j-1], dlv_end[j])
 };
 
@@ -169,6 +170,8 @@ struct vts_ctx {
   int64_t run_no = 0;
   int64_t ring_cleared_at[2] = {-1, -1};
   bool have_results = false;
+  bool pending = false;            // a run is submitted (vts_run_async) and not yet waited for
+  uint32_t *h_err = nullptr;       // pinned: the run's error word, copied back at its end
   std::vector<float> host_scores;
   vts::SmallStore small;       // transcode: downscaled frames (off unless vts_transcode ran)
   // ---- general decoder (decode_full.hip, session_full.hip)
@@ -189,8 +192,9 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
-  std::vector<int32_t> dslots;          // CABAC: ring slots of the windows' pictures by parse level (h264_derive)
-  int32_t *d_dslots = nullptr;
+  std::vector<int2> dslots;             // CABAC: the windows' pictures by parse level (h264_derive): ring slot,
+                                        // common colocated slot
+  int2 *d_dslots = nullptr;
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full (its LDS fallback)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<hipEvent_t> ev_bs;  // paced bS: two per level launch of a window (reused window to window)
@@ -199,6 +203,11 @@ struct vts_ctx {
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock
   int16_t *d_arena[2] = {nullptr, nullptr};
   int64_t arena_blocks = 0;             // per ring
+  std::vector<int32_t> fslice_nmbs;     // per fslice: its macroblocks (arena ranges)
+  bool arena_safe = false;              // CABAC arena ranges from the bound (after a DEC_E_ARENA run)
+  int arena_per_byte = 4;               // CABAC arena estimate: blocks per NAL byte (VTS_ARENA_PER_BYTE)
+  int64_t arena_reruns = 0;             // runs repeated for that
+  int64_t dbk_pics = 0;                 // descriptor slots of d_dbk (a ring of two levels per GOP group)
   // kept from open for a later switch to the general decoder (decoder = auto)
   std::vector<int64_t> es_off;          // sample offsets in the ES buffer
   std::vector<uint32_t> sample_size;
@@ -207,8 +216,13 @@ struct vts_ctx {
 };
 
 namespace vts {
-// Decode + score every window (and downscale when ctx->small.on).
+// Decode + score every window (and downscale when ctx->small.on):
+// submit_all enqueues a run, finish_all waits for it (errors, timings, the
+// re-runs the device asks for); run_all = both.
 int run_all(vts_ctx *c);
+int submit_all(vts_ctx *c);
+int finish_all(vts_ctx *c);
+int finish_subset(vts_ctx *c);
 int fetch_scores(vts_ctx *c);
 // general decoder: schedule + buffers from the host ES (session_full.hip);
 // `sps_nal` / `pps_nal` are the avcC parameter sets
@@ -216,6 +230,9 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
                   const std::vector<uint32_t> &sizes, int nal_length_size, const std::vector<uint8_t> &sps_nal,
                   const std::vector<uint8_t> &pps_nal);
 int run_general(vts_ctx *c);
+int submit_general(vts_ctx *c);
+int finish_general(vts_ctx *c);
+void assign_arena(vts_ctx *c);
 // cheap look at the stream's first pictures: does it need the general decoder?
 bool wants_general(const vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
                    const std::vector<uint32_t> &sizes, int nal_length_size);

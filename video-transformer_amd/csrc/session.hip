@@ -253,9 +253,9 @@ int alloc_general(vts_ctx *c) {
   HIP_TRY(vts::dmalloc(&c->d_porder_m, sizeof(int32_t) * std::max<size_t>(1, c->porder_m.size())));
   if (!c->porder_m.empty())
     HIP_TRY(hipMemcpy(c->d_porder_m, c->porder_m.data(), sizeof(int32_t) * c->porder_m.size(), hipMemcpyHostToDevice));
-  HIP_TRY(vts::dmalloc(&c->d_dslots, sizeof(int32_t) * std::max<size_t>(1, c->dslots.size())));
+  HIP_TRY(vts::dmalloc(&c->d_dslots, sizeof(int2) * std::max<size_t>(1, c->dslots.size())));
   if (!c->dslots.empty())
-    HIP_TRY(hipMemcpy(c->d_dslots, c->dslots.data(), sizeof(int32_t) * c->dslots.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_dslots, c->dslots.data(), sizeof(int2) * c->dslots.size(), hipMemcpyHostToDevice));
   HIP_TRY(vts::dmalloc(&c->d_pneed, sizeof(int32_t) * std::max<size_t>(1, c->pneed.size())));
   if (!c->pneed.empty())
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
@@ -275,7 +275,7 @@ int alloc_general(vts_ctx *c) {
       HIP_TRY(vts::dmalloc(&c->d_recs1[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRecB)));
     HIP_TRY(vts::dmalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
     HIP_TRY(vts::dmalloc(&c->d_pdone[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
-    HIP_TRY(vts::dmalloc(&c->d_dbk[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(DbkInfo)));
+    HIP_TRY(vts::dmalloc(&c->d_dbk[r], static_cast<size_t>(c->dbk_pics * nmb) * sizeof(DbkInfo)));
     HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
     HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
     HIP_TRY(vts::dmalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
@@ -817,8 +817,28 @@ int open_common(int device, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_
 }  // namespace
 
 int vts::run_all(vts_ctx *c) {
-  if (c->general) return run_general(c);
+  VTS_TRY(submit_all(c));
+  return finish_all(c);
+}
+
+int vts::finish_all(vts_ctx *c) {
+  if (!c->pending) return VTS_OK;
+  c->pending = false;
+  return c->general ? finish_general(c) : finish_subset(c);
+}
+
+// Enqueue one run (every window's decode + score) on the session's streams;
+// finish_all waits for it, reads the error word and the timings, and re-runs
+// where the device asked for it (level-blocking halo, general decoder, arena).
+int vts::submit_all(vts_ctx *c) {
+  if (c->pending) VTS_TRY(finish_all(c));
+  if (c->general) {
+    VTS_TRY(submit_general(c));
+    c->pending = true;
+    return VTS_OK;
+  }
   HIP_TRY(hipSetDevice(c->device));
+  if (!c->h_err) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_err), sizeof(uint32_t)));
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
   HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
   HIP_TRY(hipStreamWaitEvent(c->s_score, c->ev_start, 0));
@@ -1012,10 +1032,17 @@ int vts::run_all(vts_ctx *c) {
     HIP_TRY(hipEventRecord(E[4], ss));
   }
   HIP_TRY(hipStreamWaitEvent(sd, c->ev[(nw - 1) * 6 + 4], 0));
+  HIP_TRY(hipMemcpyAsync(c->h_err, c->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, sd));
   HIP_TRY(hipEventRecord(c->ev_end, sd));
+  c->pending = true;
+  return VTS_OK;
+}
+
+int vts::finish_subset(vts_ctx *c) {
+  const size_t nw = c->windows.size();
+  const bool keep = c->params.keep_frames > 0 || c->small.on;
   HIP_TRY(hipEventSynchronize(c->ev_end));
-  uint32_t err = 0;
-  HIP_TRY(hipMemcpy(&err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
+  const uint32_t err = *c->h_err;
   // timings
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, c->ev_start, c->ev_end));
@@ -1057,7 +1084,7 @@ int vts::run_all(vts_ctx *c) {
                                    DEC_E_DEBLOCK | DEC_E_REFLIST | DEC_E_MMCO | DEC_E_EPB_IN_PCM;
   if ((err & kSubsetMiss) && c->params.decoder == 0) {  // small.on too: run_general downscales
     VTS_TRY(switch_to_general(c));
-    return run_general(c);
+    return run_all(c);
   }
   if (err) {
     c->have_results = false;
@@ -1069,6 +1096,7 @@ int vts::run_all(vts_ctx *c) {
 }
 
 int vts::fetch_scores(vts_ctx *c) {
+  VTS_TRY(finish_all(c));  // a submitted run first
   if (!c->host_scores.empty()) return VTS_OK;
   c->host_scores.resize(static_cast<size_t>(c->n_frames));
   HIP_TRY(hipMemcpy(c->host_scores.data(), c->d_score, sizeof(float) * c->n_frames,
@@ -1120,6 +1148,18 @@ extern "C" int vts_run(vts_ctx *c) {
   return run_all(c);
 }
 
+extern "C" int vts_run_async(vts_ctx *c) {
+  clear_error();
+  if (!c) return fail(VTS_E_INVALID, "NULL ctx");
+  return submit_all(c);
+}
+
+extern "C" int vts_wait(vts_ctx *c) {
+  clear_error();
+  if (!c) return fail(VTS_E_INVALID, "NULL ctx");
+  return finish_all(c);
+}
+
 extern "C" int vts_score(vts_ctx *c, float *scores, uint32_t *hist, uint64_t *sad, int64_t *pts,
                          int64_t cap, int64_t *n_frames) {
   clear_error();
@@ -1140,6 +1180,7 @@ extern "C" int vts_score(vts_ctx *c, float *scores, uint32_t *hist, uint64_t *sa
 extern "C" int vts_scene_cuts(vts_ctx *c, int64_t *frame_idx, int64_t cap, int64_t *n_out) {
   clear_error();
   if (!c || !n_out) return fail(VTS_E_INVALID, "NULL argument");
+  VTS_TRY(finish_all(c));  // a submitted run completes first
   if (!c->have_results) return fail(VTS_E_INVALID, "run vts_score/vts_run first");
   VTS_TRY(fetch_scores(c));
   int64_t n = 0;
@@ -1172,6 +1213,7 @@ extern "C" int vts_frame_pts(const vts_ctx *c, int64_t *pts, int64_t cap, int64_
 extern "C" int vts_get_frame_nv12(vts_ctx *c, int64_t frame, uint8_t *out, int64_t out_bytes) {
   clear_error();
   if (!c || !out) return fail(VTS_E_INVALID, "NULL argument");
+  VTS_TRY(finish_all(c));
   const int64_t need = static_cast<int64_t>(c->width) * c->height * 3 / 2;
   if (out_bytes < need) return fail(VTS_E_CAPACITY, "need %lld bytes", static_cast<long long>(need));
   if (c->last_window_done < 0) return fail(VTS_E_INVALID, "nothing decoded yet");
@@ -1197,6 +1239,8 @@ extern "C" int vts_get_frame_nv12(vts_ctx *c, int64_t frame, uint8_t *out, int64
 extern "C" int vts_get_thumbnail_rgb(vts_ctx *c, int64_t frame, uint8_t *out, int64_t out_bytes) {
   clear_error();
   if (!c || !out) return fail(VTS_E_INVALID, "NULL argument");
+  VTS_TRY(finish_all(c));
+  VTS_TRY(finish_all(c));  // a submitted run completes first
   if (!c->have_results) return fail(VTS_E_INVALID, "run vts_score/vts_run first");
   if (frame < 0 || frame >= c->n_frames) return fail(VTS_E_INVALID, "frame out of range");
   const int64_t need = 3 * c->thumb_px;
@@ -1254,6 +1298,8 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
     }
     case 7: return c->tb_off ? 0 : static_cast<int64_t>(c->tb_chains.size());  // chain slots (levels x chains)
     case 8: return c->general ? 1 : 0;
+    case 9: return c->arena_reruns;                 // runs repeated with the bound's coefficient arena
+    case 10: return c->arena_blocks;                // coefficient blocks per ring (general decoder)
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
   }
 }
@@ -1261,6 +1307,8 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
 extern "C" int vts_close(vts_ctx *c) {
   if (!c) return VTS_OK;
   (void)hipSetDevice(c->device);
+  if (c->pending && c->ev_end) (void)hipEventSynchronize(c->ev_end);  // a submitted run nobody waited for
+  if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->s_dec) (void)hipStreamSynchronize(c->s_dec);
   if (c->s_score) (void)hipStreamSynchronize(c->s_score);
   if (c->s_parse) (void)hipStreamSynchronize(c->s_parse);

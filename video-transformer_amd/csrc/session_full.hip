@@ -29,6 +29,22 @@
 namespace vts {
 namespace {
 
+// Coefficient blocks a slice may store.  CAVLC: a stored block costs >= 3
+// bits.  CABAC: every stored 4x4 block holds a non-zero level, whose sign is
+// one bypass bin = one bit the arithmetic decoder reads (an 8x8 block stores
+// four 4x4 blocks per such bit), so 32 x the NAL bytes is a bound too; it is
+// ~37x what real CABAC streams store (x264-like content: ~0.9 blocks per
+// byte), so the arena is first sized from 4 blocks per byte and a slice that
+// overflows its range (DEC_E_ARENA) makes the host re-run with the bound.
+// Either way never more than the 27 blocks a macroblock can hold.
+// (VTS_ARENA_PER_BYTE overrides the estimate's 4: the tests' way to force
+// the overflow path.)
+int64_t slice_arena_cap(bool cabac, bool safe, int64_t n_mbs, int64_t nal_size, int64_t per_byte) {
+  const int64_t per_mb = 27ll * n_mbs;
+  if (!cabac) return std::min<int64_t>(per_mb, 3ll * nal_size + 27);
+  return std::min<int64_t>(per_mb, safe ? 32ll * nal_size + 64 : per_byte * nal_size + 64);
+}
+
 // per ring: parse throughput grows with the slices per launch, and every
 // window runs its own chain of reconstruction levels, so one window per
 // 10-min 720p CABAC video (~104 GB: the arena reserves 27 blocks per
@@ -126,13 +142,14 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   for (int64_t f = 0; f < n; ++f)
     for (int64_t col : frames[static_cast<size_t>(f)].cols)
       plevel[static_cast<size_t>(f)] = std::max(plevel[static_cast<size_t>(f)], plevel[static_cast<size_t>(col)] + 1);
-  // coefficient blocks each slice may need (CAVLC bound, h264_full.h)
+  // coefficient blocks each slice may need (slice_arena_cap)
+  c->arena_safe = false;
+  c->arena_per_byte = 4;
+  if (const char *ev = std::getenv("VTS_ARENA_PER_BYTE")) c->arena_per_byte = std::max(0, std::atoi(ev));
   std::vector<int64_t> cap(slices.size());
   int64_t cap_total = 0;
   for (size_t i = 0; i < slices.size(); ++i) {
-    // CAVLC stores a block for >= 3 bits; CABAC can code one in less, so it gets the per-macroblock bound
-    cap[i] = c->pps.entropy_coding_mode ? 27ll * slices[i].n_mbs
-                                        : std::min<int64_t>(27ll * slices[i].n_mbs, 3ll * slices[i].nal_size + 27);
+    cap[i] = slice_arena_cap(c->pps.entropy_coding_mode, false, slices[i].n_mbs, slices[i].nal_size, c->arena_per_byte);
     cap_total += cap[i];
   }
   // windows
@@ -194,6 +211,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
 
   // per window: device slices (window-relative slots and arena), level lists
   c->fslices.clear();
+  c->fslice_nmbs.clear();
   c->exts.clear();
   c->porder.clear();
   c->porder_m.clear();
@@ -231,6 +249,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
         d.arena = static_cast<uint32_t>(arena);
         d.arena_cap = static_cast<uint32_t>(cap[static_cast<size_t>(si)]);
         arena += cap[static_cast<size_t>(si)];
+        c->fslice_nmbs.push_back(static_cast<int32_t>(s.n_mbs));
         d.ext = -1;
         for (int i = 0; i < 32; ++i) {
           const int64_t r = s.ref[i];
@@ -285,6 +304,15 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       std::stable_sort(c->porder_m.begin() + static_cast<int64_t>(o0), c->porder_m.end(), [&](int32_t a, int32_t b) {
         return c->fslices[static_cast<size_t>(w.fs0 + a)].nal_size > c->fslices[static_cast<size_t>(w.fs0 + b)].nal_size;
       });
+      // "long" slices, >= 8 x the window's median (x264-like content: the I
+      // pictures, ~50x the median B slice): first in the order, prioritised
+      w.n_long = 0;
+      if (nws > 0) {
+        const int32_t med = c->fslices[static_cast<size_t>(w.fs0 + c->porder_m[o0 + static_cast<size_t>(nws / 2)])].nal_size;
+        while (w.n_long < nws &&
+               c->fslices[static_cast<size_t>(w.fs0 + c->porder_m[o0 + static_cast<size_t>(w.n_long)])].nal_size >= 8ll * med)
+          ++w.n_long;
+      }
     } else {
       for (size_t j = 0; j < w.plv_end.size(); ++j) {
         const int32_t b0 = j ? w.plv_end[j - 1] : 0;
@@ -294,11 +322,23 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
     }
     // h264_derive launches (CABAC): the window's pictures by parse level, so a
     // B picture's colocated picture is complete before it
+    // (with the colocated slot its B slices share, so each macroblock's
+    // colocated words load with its own, or -1)
     w.ds0 = static_cast<int64_t>(c->dslots.size());
     w.dlv_end.clear();
     for (int32_t pl = 0; pl <= maxp; ++pl) {
-      for (int64_t f = w.f0; f < w.f1; ++f)
-        if (plevel[static_cast<size_t>(f)] == pl) c->dslots.push_back(slot_of(f));
+      for (int64_t f = w.f0; f < w.f1; ++f) {
+        if (plevel[static_cast<size_t>(f)] != pl) continue;
+        const SchedFrame &fr = frames[static_cast<size_t>(f)];
+        int64_t col = -2;  // -2: no B slice yet
+        for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
+          const SchedSlice &sl = slices[static_cast<size_t>(si)];
+          if (sl.is_p != kSliceB) continue;
+          const int64_t cs = sl.ref1[0] >= 0 ? disp[static_cast<size_t>(sl.ref1[0])] - w.f0 : -1;
+          col = (col == -2 || col == cs) ? cs : -1;
+        }
+        c->dslots.push_back(make_int2(slot_of(f), static_cast<int32_t>(col < 0 ? -1 : col)));
+      }
       w.dlv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->dslots.size()) - w.ds0));
     }
     w.pn0 = static_cast<int64_t>(c->pneed.size());
@@ -346,11 +386,69 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       }
     }
   }
+  // Deblocking descriptors (h264_bs_full -> h264_deblock_plane) live in a
+  // ring of two level slots per GOP group: level l + 1's bS is derived while
+  // level l deblocks, and level l + 2's only after level l + 1's inter launch,
+  // which follows level l's deblocking on the group's stream (run_general).
+  // Slot (2 g + (j & 1)) x the most pictures of a level, j the level's index
+  // in its group; int4.y of each level entry is its picture's descriptor slot.
+  // (When that ring would not be smaller than one slot per picture — few,
+  // wide levels, e.g. all-intra — each picture keeps its own slot.)
+  int64_t maxcnt = 1, maxg = 1;
+  for (const Window &w : c->windows) {
+    for (int32_t n2 : w.lvl_cnt) maxcnt = std::max<int64_t>(maxcnt, n2);
+    maxg = std::max<int64_t>(maxg, 1 + static_cast<int64_t>(w.grp.size()));
+  }
+  if (2 * maxg * maxcnt >= c->ring_frames) {
+    for (int4 &f : c->level_frames) f.y = f.x;
+    c->dbk_pics = c->ring_frames;
+    return VTS_OK;
+  }
+  for (const Window &w : c->windows) {
+    int g = 0;
+    size_t lo = 0;
+    for (size_t l = 0; l < w.lvl_off.size(); ++l) {
+      while (g < static_cast<int>(w.grp.size()) && l >= static_cast<size_t>(w.grp[static_cast<size_t>(g)])) {
+        lo = static_cast<size_t>(w.grp[static_cast<size_t>(g)]);
+        ++g;
+      }
+      const int64_t base = (2 * g + static_cast<int64_t>((l - lo) & 1)) * maxcnt;
+      for (int32_t i = 0; i < w.lvl_cnt[l]; ++i)
+        c->level_frames[static_cast<size_t>(w.lvl_off[l] + i)].y = static_cast<int32_t>(base + i);
+    }
+  }
+  c->dbk_pics = 2 * maxg * maxcnt;
   return VTS_OK;
 }
 
+// The slices' coefficient arena ranges (FullSlice::arena / arena_cap, each
+// window from 0) and the ring's block count, from the estimate or, once a
+// slice overflowed (c->arena_safe), the bound (slice_arena_cap).
+void assign_arena(vts_ctx *c) {
+  c->arena_blocks = 0;
+  for (const Window &w : c->windows) {
+    int64_t arena = 0;
+    for (int64_t k = w.fs0; k < w.fs1; ++k) {
+      FullSlice &d = c->fslices[static_cast<size_t>(k)];
+      const int64_t cap = slice_arena_cap(c->fprm.cabac, c->arena_safe, c->fslice_nmbs[static_cast<size_t>(k)], d.nal_size,
+                                          c->arena_per_byte);
+      d.arena = static_cast<uint32_t>(arena);
+      d.arena_cap = static_cast<uint32_t>(cap);
+      arena += cap;
+    }
+    c->arena_blocks = std::max(c->arena_blocks, arena);
+  }
+}
+
 int run_general(vts_ctx *c) {
+  VTS_TRY(submit_general(c));
+  c->pending = true;
+  return finish_all(c);
+}
+
+int submit_general(vts_ctx *c) {
   HIP_TRY(hipSetDevice(c->device));
+  if (!c->h_err) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_err), sizeof(uint32_t)));
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
   HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
   HIP_TRY(hipStreamWaitEvent(c->s_score, c->ev_start, 0));
@@ -404,6 +502,7 @@ int run_general(vts_ctx *c) {
       pa.order = c->d_porder_m + w.fs0;
       pa.pdone = nullptr;
       pa.pneed = nullptr;
+      pa.n_long = w.n_long;
       VTS_TRY(parse_full_launch(pa, sp));
       DeriveArgs da{};
       da.recs = c->d_recs[r];
@@ -416,7 +515,7 @@ int run_general(vts_ctx *c) {
       da.P = c->fprm;
       for (size_t j = 0; j < w.dlv_end.size(); ++j) {
         const int32_t b0 = j ? w.dlv_end[j - 1] : 0;
-        da.slots = c->d_dslots + w.ds0 + b0;
+        da.pics = c->d_dslots + w.ds0 + b0;
         VTS_TRY(derive_launch(da, w.dlv_end[j] - b0, sp));
       }
     } else if (c->parse_merged && w.plv_end.size() > 1) {
@@ -552,10 +651,15 @@ int run_general(vts_ctx *c) {
     HIP_TRY(hipEventRecord(E[4], ss));
   }
   HIP_TRY(hipStreamWaitEvent(sd, c->ev[(nw - 1) * 6 + 4], 0));
+  HIP_TRY(hipMemcpyAsync(c->h_err, c->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, sd));
   HIP_TRY(hipEventRecord(c->ev_end, sd));
+  return VTS_OK;
+}
+
+int finish_general(vts_ctx *c) {
+  const size_t nw = c->windows.size();
   HIP_TRY(hipEventSynchronize(c->ev_end));
-  uint32_t err = 0;
-  HIP_TRY(hipMemcpy(&err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
+  const uint32_t err = *c->h_err;
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, c->ev_start, c->ev_end));
   c->timings[0] = ms;
@@ -571,6 +675,20 @@ int run_general(vts_ctx *c) {
     c->timings[3] += s;
   }
   c->last_window_done = static_cast<int64_t>(nw) - 1;
+  if ((err & DEC_E_ARENA) && !c->arena_safe) {
+    // a slice stored more coefficient blocks than its estimated range:
+    // ranges from the bound, a larger arena, and the run again
+    c->arena_safe = true;
+    ++c->arena_reruns;
+    assign_arena(c);
+    HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
+    for (int r = 0; r < c->n_rings; ++r) {
+      vts::dfree(c->d_arena[r]);
+      c->d_arena[r] = nullptr;
+      HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + 256));  // + kPad (session.hip)
+    }
+    return run_all(c);
+  }
   if (err) {
     c->have_results = false;
     return fail(VTS_E_DECODE, "device decoder: %s", describe_decode_error(err).c_str());

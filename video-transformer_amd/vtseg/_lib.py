@@ -12,7 +12,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libvtseg.so"
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 VTS_OK = 0
 VTS_E_INVALID = -1
@@ -153,6 +153,8 @@ SIGNATURES: dict[str, tuple] = {
     "vts_score": (C.c_int, [C.c_void_p, _P(C.c_float), _P(C.c_uint32), _P(C.c_uint64),
                             _P(C.c_int64), C.c_int64, _P(C.c_int64)]),
     "vts_run": (C.c_int, [C.c_void_p]),
+    "vts_run_async": (C.c_int, [C.c_void_p]),
+    "vts_wait": (C.c_int, [C.c_void_p]),
     "vts_scene_cuts": (C.c_int, [C.c_void_p, _P(C.c_int64), C.c_int64, _P(C.c_int64)]),
     "vts_frame_pts": (C.c_int, [C.c_void_p, _P(C.c_int64), C.c_int64, _P(C.c_int64)]),
     "vts_boundary_frames": (C.c_int, [C.c_void_p, _P(C.c_double), C.c_int64,
@@ -162,6 +164,7 @@ SIGNATURES: dict[str, tuple] = {
     "vts_last_timings": (C.c_int, [C.c_void_p, _P(C.c_double)]),
     "vts_open_timings": (C.c_int, [C.c_void_p, _P(C.c_double), C.c_int32]),
     "vts_empty_cache": (C.c_int, [C.c_int]),
+    "vts_device_bytes": (C.c_int64, [C.c_int]),
     "vts_schedule_info": (C.c_int64, [C.c_void_p, C.c_int32]),
     "vts_close": (C.c_int, [C.c_void_p]),
     "vts_transcode": (C.c_int, [C.c_void_p, C.c_char_p, _P(TranscodeParams),

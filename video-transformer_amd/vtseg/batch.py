@@ -78,42 +78,63 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
     cut_frames: list[list[int]] = [[] for _ in range(per)]
     cut_times: list[list[float]] = [[] for _ in range(per)]
     errors: dict[int, str] = {}
-    for j, i in enumerate(range(rank, n, world)):
+    mine = list(enumerate(range(rank, n, world)))
+    segs_of: dict[int, list] = {}
+    durations: dict[int, float] = {}
+    for j, i in mine:
         p = str(paths[i])
-        duration = probe_duration(p)
-        segs = _segments(duration, config, current_api_count)
-        n_cuts = -1
-        if score:
-            # A failure on one video must not keep this rank from the
-            # collectives below (the other ranks would wait forever): record
-            # it in the video's record and carry on.
+        durations[i] = probe_duration(p)
+        segs_of[i] = _segments(durations[i], config, current_api_count)
+    if score:
+        # Every local session's run is submitted before any is waited for, so
+        # the device overlaps them (one video's serial parse tail or
+        # reconstruction chain leaves compute units another's fills).  A
+        # failure on one video must not keep this rank from the collectives
+        # below (the other ranks would wait forever): it is recorded in the
+        # video's record.
+        from .scene import VideoScorer
+        running: dict[int, tuple] = {}
+        for j, i in mine:
+            v, own = (sessions or {}).get(i), False
             try:
-                from .scene import VideoScorer
-                v = (sessions or {}).get(i)
-                own = v is None
-                if own:
+                if v is None:
+                    own = True
                     dev_id = torch.cuda.current_device() if device is None else device
-                    v = VideoScorer(p, device=dev_id)
-                try:
-                    v.run()                  # decode + score; per-frame results stay on the device
-                    cuts = v.scene_cuts()    # only the scores come back to find the cuts
-                    pts = v.frame_pts()
-                    times = [t for sg in segs for t in (sg.start, sg.end)]
-                    sf = v.boundary_frames(times) if times else []
-                    ts = int(v.info.track_timescale)
-                finally:
-                    if own:
-                        v.close()
-                n_cuts = len(cuts)
-                seg_frames[j] = sf
-                cut_frames[j] = list(cuts)
-                cut_times[j] = [float(pts[c]) / ts for c in cuts]
+                    v = VideoScorer(str(paths[i]), device=dev_id)
+                v.run_async()            # decode + score; per-frame results stay on the device
+                running[i] = (v, own)
             except Exception as exc:  # noqa: BLE001 - reported per video
                 errors[i] = f"{type(exc).__name__}: {exc}"
                 local[j, 3] = 1
-        local[j, 0] = len(segs)
-        local[j, 1] = n_cuts
-        local[j, 2] = round(duration * 1_000_000)
+                if own and v is not None:
+                    v.close()
+        for j, i in mine:
+            if i not in running:
+                continue
+            v, own = running[i]
+            try:
+                v.wait()
+                cuts = v.scene_cuts()    # only the scores come back to find the cuts
+                pts = v.frame_pts()
+                times = [t for sg in segs_of[i] for t in (sg.start, sg.end)]
+                sf = v.boundary_frames(times) if times else []
+                ts = int(v.info.track_timescale)
+                seg_frames[j] = sf
+                cut_frames[j] = list(cuts)
+                cut_times[j] = [float(pts[c]) / ts for c in cuts]
+                local[j, 1] = len(cuts)
+            except Exception as exc:  # noqa: BLE001 - reported per video
+                errors[i] = f"{type(exc).__name__}: {exc}"
+                local[j, 3] = 1
+                local[j, 1] = -1
+            finally:
+                if own:
+                    v.close()
+    for j, i in mine:
+        local[j, 0] = len(segs_of[i])
+        if not score or i in errors:
+            local[j, 1] = -1
+        local[j, 2] = round(durations[i] * 1_000_000)
     g = _all_gather(local, world, group, dev).view(world, per, REC)
     arrays = (exchange_boundaries(g, seg_frames, cut_frames, cut_times, group=group, device=dev)
               if score else None)

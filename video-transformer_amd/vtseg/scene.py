@@ -153,6 +153,21 @@ class VideoScorer:
         """Decode + score with results left on the device (benchmark step)."""
         _lib.check(self._lib.vts_run(self._ctx))
 
+    def run_async(self) -> None:
+        """Enqueue a run (decode + score) and return; wait() (or any call that
+        reads results) completes it.  Runs of several sessions submitted
+        before any wait share the device."""
+        _lib.check(self._lib.vts_run_async(self._ctx))
+
+    def wait(self) -> None:
+        """Complete a run_async() (errors and re-runs as in run())."""
+        _lib.check(self._lib.vts_wait(self._ctx))
+
+    def arena_reruns(self) -> int:
+        """Runs repeated because a CABAC slice overflowed its estimated
+        coefficient range (the session then keeps the bound's ranges)."""
+        return int(self._lib.vts_schedule_info(self._ctx, 9))
+
     def timings(self) -> dict:
         t = (C.c_double * 4)()
         _lib.check(self._lib.vts_last_timings(self._ctx, t))
