@@ -809,7 +809,18 @@ def e2e_record(paths: list[Path], gpu: int) -> dict:
                         "boundary frames, close; files in the page cache (just written)"}
 
 
+# HIP hardware queues per process (read once, when HIP initialises): a
+# session drives up to six streams (parse, decode / GOP groups, score), and
+# plan_batch overlaps several sessions' runs; on HIP's default 4 queues their
+# launches share queues in submission order and the runs serialise (4 content
+# sessions: 3.99x one session's step; 16 queues: 2.76x, profiles/r05f_*).
+# The documented deployment setting; set before anything
+# initialises HIP, inherited by the profiler children and the ranks.
+HW_QUEUES = "16"
+
+
 def main() -> None:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", HW_QUEUES)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)

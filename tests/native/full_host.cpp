@@ -115,6 +115,8 @@ extern "C" int fh_scale(const char *path, int32_t *ls4, int32_t *ls8, int *flags
   Mp4Info mp4;
   std::string e = mp4_parse_file(path, &mp4);
   if (!e.empty()) return bad(e);
+  if (mp4.video.empty() || mp4.video.front().sps.empty() || mp4.video.front().pps.empty())
+    return bad("no video track / parameter sets");
   const Mp4VideoTrack &t = mp4.video.front();
   Sps sps;
   Pps pps;
@@ -139,7 +141,9 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   Mp4Info mp4;
   std::string e = mp4_parse_file(path, &mp4);
   if (!e.empty()) return bad(e);
+  if (mp4.video.empty()) return bad("no video track");
   const Mp4VideoTrack &t = mp4.video.front();
+  if (t.sps.empty() || t.pps.empty()) return bad("no parameter sets");
   Sps sps;
   Pps pps;
   e = parse_sps(t.sps[0].data(), t.sps[0].size(), &sps);

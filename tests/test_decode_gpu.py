@@ -136,6 +136,39 @@ def test_emulation_prevention_inside_pcm_fails_loudly(tmp_path):
     assert np.array_equal(got, frames)
 
 
+@pytest.mark.parametrize("coding", ["cabac", "cavlc"])
+def test_corrupted_slice_data_fails_loudly(tmp_path, coding):
+    """a stream whose slice data was damaged after its
+    headers (so vts_open accepts it) fails its run with VTS_E_DECODE — the
+    parse ends away from the RBSP stop bit or meets impossible syntax — and
+    the session stays usable: closing it and decoding the intact stream
+    again equals the oracle."""
+    _require_gpu()
+    from vtseg import _lib
+    n = 24
+    path, bad = tmp_path / "ok.mp4", tmp_path / "bad.mp4"
+    extra = dict(cabac=True, transform_8x8=True) if coding == "cabac" else {}
+    scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=True, weighted="implicit",
+                      cut_min_s=0.5, cut_max_s=1.0, gop_max_s=0.5, seed=17, **extra)
+    m = oracle.read_mp4(path)
+    data = bytearray(path.read_bytes())
+    rng = np.random.default_rng(5)
+    for i in range(0, n, 3):  # every third picture: a few bytes past its slice header
+        off, size = int(m["offsets"][i]), int(m["sizes"][i])
+        for _ in range(3):
+            j = off + int(rng.integers(size // 3, size))
+            data[j] ^= 0xA5
+    bad.write_bytes(bytes(data))
+    with scene.VideoScorer(bad) as v:
+        with pytest.raises(VtsegError) as ei:
+            v.score()
+        assert ei.value.code == _lib.VTS_E_DECODE, ei.value
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
+    with scene.VideoScorer(path) as v:
+        assert np.array_equal(v.score().scores, ref["score"])
+
+
 def test_open_rejects_non_mp4(tmp_path):
     _require_gpu()
     bad = tmp_path / "x.mp4"

@@ -90,8 +90,9 @@ VTS_HD VTS_INLINE int abs_off(int cat) { return static_cast<int>((0x271E140A00ul
 // compute unit) instead of the one scalar unit that every wave of the compute
 // unit shares, which the parser saturates; a decision's outcome, next state
 // and renormalisation shift come back to the scalar side by readfirstlane
-// (CABAC B parse -4 % same-box, profiles/r03_cabac_vgpr_engine_ab.txt)
-#if defined(__HIP_DEVICE_COMPILE__)
+// (CABAC B parse -4 % same-box, profiles/r03_cabac_vgpr_engine_ab.txt;
+// VTS_EXP_SENGINE keeps the scalar engine)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(VTS_EXP_SENGINE)
 __device__ __forceinline__ uint32_t vts_in_vgpr(uint32_t x) {
   uint32_t r;
   asm("; engine state in a VGPR" : "=v"(r) : "0"(x));
