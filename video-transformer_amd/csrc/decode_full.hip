@@ -188,11 +188,6 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
   const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
   const int i = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
-#ifndef VTS_EXP_NOPRIO
-  // the launch's longest slices (first in the order) bound it: their waves
-  // win the issue arbitration against the short slices' waves beside them
-  if (static_cast<int>(blockIdx.x) < a.n_long) __builtin_amdgcn_s_setprio(3);
-#endif
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
   const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
@@ -377,22 +372,27 @@ __device__ __forceinline__ void luma_pred4(const uint32_t (&w)[9][3], int xf, in
       for (int x = 0; x < 4; ++x) v[y * 4 + x] = px(w, y + 2, x + 2);
     return;
   }
-  int hr[9][4], vt[4][5];
-#pragma unroll
-  for (int r = 0; r < 9; ++r)
+  // one output row at a time, so only six rows of horizontal intermediates
+  // (and the row's vertical ones) are live at once: 6-tap row r is made just
+  // before output row r - 5 first needs it
+  int hr[9][4];
+  auto hrow = [&](int r) {
 #pragma unroll
     for (int x = 0; x < 4; ++x) hr[r][x] = t6(px(w, r, x), px(w, r, x + 1), px(w, r, x + 2), px(w, r, x + 3), px(w, r, x + 4), px(w, r, x + 5));
+  };
 #pragma unroll
-  for (int y = 0; y < 4; ++y)
-#pragma unroll
-    for (int c = 0; c < 5; ++c) vt[y][c] = t6(px(w, y, c + 2), px(w, y + 1, c + 2), px(w, y + 2, c + 2), px(w, y + 3, c + 2), px(w, y + 4, c + 2), px(w, y + 5, c + 2));
+  for (int r = 0; r < 5; ++r) hrow(r);
   const bool x0 = xf == 0, y0 = yf == 0, x2 = xf == 2, y2 = yf == 2, x3 = xf == 3, y3 = yf == 3;
 #pragma unroll
-  for (int y = 0; y < 4; ++y)
+  for (int y = 0; y < 4; ++y) {
+    hrow(y + 5);
+    int vt[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) vt[c] = t6(px(w, y, c + 2), px(w, y + 1, c + 2), px(w, y + 2, c + 2), px(w, y + 3, c + 2), px(w, y + 4, c + 2), px(w, y + 5, c + 2));
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int b = c255((hr[y + 2][x] + 16) >> 5), s_ = c255((hr[y + 3][x] + 16) >> 5);
-      const int h = c255((vt[y][x] + 16) >> 5), m = c255((vt[y][x + 1] + 16) >> 5);
+      const int h = c255((vt[x] + 16) >> 5), m = c255((vt[x + 1] + 16) >> 5);
       const int j = c255((t6(hr[y][x], hr[y + 1][x], hr[y + 2][x], hr[y + 3][x], hr[y + 4][x], hr[y + 5][x]) + 512) >> 10);
       const int G = px(w, y + 2, x + 2), G1 = px(w, y + 2, x + 3), G2 = px(w, y + 3, x + 2);
       const int bs = y3 ? s_ : b, hm = x3 ? m : h;
@@ -417,6 +417,7 @@ __device__ __forceinline__ void luma_pred4(const uint32_t (&w)[9][3], int xf, in
       }
       v[y * 4 + x] = full ? P : (P + Q + 1) >> 1;
     }
+  }
 }
 
 // 8.5.12.1 chroma DC of chroma block ck: 2x2 Hadamard of the plane's DC levels, scaled
@@ -1250,16 +1251,28 @@ struct DevLanes {
   __device__ __forceinline__ void amax(int *p, int v) const { atomicMax(p, v); }
 };
 
-// grid: pictures of the level; dynamic LDS: the tagged line entries (one per
-// macroblock column and row, i2::I2Line) and the level lists (2 B per
-// macroblock)
-__global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
-  __shared__ I2Tile tiles[kI2Groups];
-  __shared__ int s_max, s_cnt;
-  __shared__ int s_lvl[kIntraLevels + 1], s_fill[kIntraLevels];
-  __shared__ __attribute__((aligned(4))) uint8_t s_off4[9 * 16];
-  __shared__ __attribute__((aligned(4))) uint8_t s_off8[9 * 64];
+// The intra phase's LDS: the groups' tiles, the level buckets and offset
+// tables, then (dynamic) the tagged line entries (one per macroblock column
+// and row, i2::I2Line) and the level lists (2 B per macroblock)
+struct I2Lds {
+  I2Tile tiles[kI2Groups];
+  int s_max, s_cnt;
+  int s_lvl[kIntraLevels + 1], s_fill[kIntraLevels];
+  uint8_t s_off4[9 * 16];
+  uint8_t s_off8[9 * 64];
+};
+__host__ __device__ constexpr size_t i2_lds_bytes(int mbw, int mbh) {
+  return (sizeof(I2Lds) + 15) / 16 * 16 + sizeof(i2::I2Line) * static_cast<size_t>(mbw + mbh) +
+         2 * static_cast<size_t>(mbw) * static_cast<size_t>(mbh);
+}
+// one picture's intra macroblocks by dependency level (1024 threads)
+__device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slot, uint8_t *lds) {
+  I2Lds &L0 = *reinterpret_cast<I2Lds *>(lds);
+  I2Tile *tiles = L0.tiles;
+  int &s_max = L0.s_max, &s_cnt = L0.s_cnt;
+  int *s_lvl = L0.s_lvl, *s_fill = L0.s_fill;
+  uint8_t *s_off4 = L0.s_off4, *s_off8 = L0.s_off8;
+  uint8_t *s_dyn = lds + (sizeof(I2Lds) + 15) / 16 * 16;
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
   const int pitch = a.pitch;
   i2::I2Line *lcol = reinterpret_cast<i2::I2Line *>(s_dyn), *lrow = lcol + mbw;
@@ -1268,7 +1281,6 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
     lcol[i].tag = -2;
     lcol[i].claim = -2;
   }
-  const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;
   RPROF_DECL;
@@ -1386,6 +1398,11 @@ __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
     RPROF_COUNT(6, 1);
   }
   RPROF_FLUSH(8);
+}
+// grid: pictures of the level; dynamic LDS: i2_lds_bytes
+__global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_i2[];
+  intra_v2_picture(a, a.frames[blockIdx.x].x, s_i2);
 }
 
 // --------------------------------------------------------------- deblocking
@@ -1654,14 +1671,13 @@ constexpr size_t kDpLds = kDpLdsY > kDpLdsC ? kDpLdsY : kDpLdsC;
 // (A row one macroblock behind the row above instead of two was bit-exact
 // and no faster)
 template <bool kLuma>
-__device__ __forceinline__ void dp_plane(const FullReconArgs &a, int pic, uint8_t *lds, int *prog) {
+__device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int di, uint8_t *lds, int *prog) {
   using Tile = typename std::conditional<kLuma, DpTileY, DpTileC>::type;
   using Line = typename std::conditional<kLuma, DpLineY, DpLineC>::type;
   Tile *tiles = reinterpret_cast<Tile *>(lds);
   Line(*ring)[kDpRingCols] = reinterpret_cast<Line(*)[kDpRingCols]>(lds + sizeof(Tile) * kDpGroups);
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
-  const int slot = a.frames[pic].x;
-  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(a.frames[pic].y) * nmb;
+  const DbkInfo *fdbk = a.dbk + static_cast<int64_t>(di) * nmb;
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
   const uint32_t uvo = static_cast<uint32_t>(a.uv_off);
   auto at = [Y](uint32_t o) { return Y + static_cast<uint64_t>(o); };
@@ -1870,8 +1886,110 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs 
   __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
   for (int i = threadIdx.x; i < a.P.mb_height; i += kDbkThreads) prog[i] = 0;
   __syncthreads();
-  if ((blockIdx.x & 1) == 0) dp_plane<true>(a, static_cast<int>(blockIdx.x >> 1), lds, prog);
-  else dp_plane<false>(a, static_cast<int>(blockIdx.x >> 1), lds, prog);
+  const int4 f = a.frames[blockIdx.x >> 1];
+  if ((blockIdx.x & 1) == 0) dp_plane<true>(a, f.x, f.y, lds, prog);
+  else dp_plane<false>(a, f.x, f.y, lds, prog);
+}
+
+// ------------------------------------------------ per-picture scheduler
+// One launch per window instead of three launches per reconstruction level:
+// a persistent grid (one 1024-thread workgroup per compute unit) whose
+// workgroups take the window's pictures by ticket in decoding order, wait
+// for that picture's reference pictures to be finished (per-slot flags set
+// to the run's epoch with agent-scope release / acquire), then run the whole
+// picture: inter prediction + residuals and its deblocking descriptors (16
+// lanes per macroblock, h264_inter_full / h264_bs_full's code), the intra
+// macroblocks by dependency level (h264_intra_v2's), the deblocking of luma
+// then chroma (h264_deblock_plane's), and flag it.  A picture starts as soon
+// as its own references are done, not when a whole level of every GOP is.
+// Deadlock-free: a workgroup takes a ticket only when it runs, and waits only
+// on lower tickets, so the lowest unfinished ticket never waits.  A wait that
+// does not end in ~2^26 polls (a bug, not a schedule) flags DEC_E_SCHED and
+// goes on, so the grid always drains.
+constexpr int kRsThreads = 1024;
+static_assert(kRsThreads == kI2Threads && kRsThreads == kDbkThreads, "the phases share the workgroup");
+__host__ __device__ constexpr size_t rs_dbk_lds_bytes() { return (kDpLds + 15) / 16 * 16 + sizeof(int) * 1024; }
+// The phases are calls, not inlined: register allocation then stays per
+// phase (inlined into the one ticket loop, each phase's per-lane constants
+// were hoisted out of it and live across all of them: 241 VGPRs spilled).
+__device__ __attribute__((noinline)) void rs_inter(const FullReconArgs &a, int slot, int di, int nmb) {
+  for (int base = 0; base < nmb * 16; base += kRsThreads) {
+    const int idx = base + static_cast<int>(threadIdx.x);
+    inter_mb(a, slot, idx >> 4, idx & 15);
+  }
+}
+__device__ __attribute__((noinline)) void rs_bs(const FullReconArgs &a, int slot, int di, int nmb) {
+  for (int base = 0; base < nmb * 16; base += kRsThreads) {  // every lane (a macroblock's 16 meet in a butterfly)
+    const int idx = base + static_cast<int>(threadIdx.x);
+    bs_mb(a, slot, di, idx >> 4, idx & 15);
+  }
+}
+__device__ __attribute__((noinline)) void rs_intra(const FullReconArgs &a, int slot, uint8_t *lds) {
+  intra_v2_picture(a, slot, lds);
+}
+template <bool kLuma>
+__device__ __attribute__((noinline)) void rs_deblock(const FullReconArgs &a, int slot, int di, uint8_t *lds, int *prog) {
+  dp_plane<kLuma>(a, slot, di, lds, prog);
+}
+__global__ void __launch_bounds__(kRsThreads) h264_recon_sched(FullReconArgs a, SchedArgs sa) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t rlds[];
+  __shared__ int s_t;
+  const int tid = static_cast<int>(threadIdx.x);
+  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
+  int *prog = reinterpret_cast<int *>(rlds + (kDpLds + 15) / 16 * 16);
+  const int di = static_cast<int>(blockIdx.x);  // this workgroup's descriptor slot in a.dbk
+  for (;;) {
+    if (tid == 0) s_t = static_cast<int>(atomicAdd(sa.next, 1u));
+    __syncthreads();
+    const int t = s_t;
+    if (t >= sa.n_pics) break;
+    const int4 pic = sa.pics[t];
+    const int slot = pic.x;
+    if (tid < pic.z) {  // the reference pictures (lower tickets)
+      const int r = sa.refs[pic.y + tid];
+      uint32_t spins = 0;
+      while (__hip_atomic_load(&sa.done[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) {
+        if (++spins > (1u << 26)) {
+          atomicOr(a.err, static_cast<uint32_t>(DEC_E_SCHED));
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // their samples, across XCD L2s
+    rs_inter(a, slot, di, nmb);
+    rs_bs(a, slot, di, nmb);
+    __syncthreads();
+    rs_intra(a, slot, rlds);
+    __syncthreads();
+    for (int i = tid; i < mbh; i += kRsThreads) prog[i] = 0;
+    __syncthreads();
+    rs_deblock<true>(a, slot, di, rlds, prog);
+    __syncthreads();
+    for (int i = tid; i < mbh; i += kRsThreads) prog[i] = 0;
+    __syncthreads();
+    rs_deblock<false>(a, slot, di, rlds, prog);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave's samples out before the flag
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&sa.done[slot], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+size_t recon_sched_lds_bytes(int mb_width, int mb_height) {
+  const size_t a = i2_lds_bytes(mb_width, mb_height), b = rs_dbk_lds_bytes();
+  return a > b ? a : b;
+}
+
+int recon_sched_launch(const FullReconArgs &a, const SchedArgs &sa, int n_wg, hipStream_t s) {
+  if (sa.n_pics <= 0) return VTS_OK;
+  if (a.P.mb_height > 1024) return fail(VTS_E_UNSUPPORTED, "picture taller than 1024 macroblock rows");
+  const size_t lds = recon_sched_lds_bytes(a.P.mb_width, a.P.mb_height);
+  if (lds > 160 * 1024) return fail(VTS_E_UNSUPPORTED, "picture too large for the per-picture scheduler's LDS");
+  hipLaunchKernelGGL(h264_recon_sched, dim3(static_cast<unsigned>(n_wg)), dim3(kRsThreads), lds, s, a, sa);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_sched launch: %s", hipGetErrorString(e));
+  return VTS_OK;
 }
 
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
@@ -1894,9 +2012,9 @@ int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s, hipEv
   if (e != hipSuccess) return fail(VTS_E_HIP, "h264_inter_full launch: %s", hipGetErrorString(e));
   if (after_inter && hipEventRecord(after_inter, s) != hipSuccess) return fail(VTS_E_HIP, "hipEventRecord after h264_inter_full");
   // lane-parallel intra (default) while its LDS fits, else the by-block kernel
-  const size_t i2_dyn = sizeof(i2::I2Line) * static_cast<size_t>(a.P.mb_width + a.P.mb_height) + 2 * static_cast<size_t>(nmb);
-  if (a.intra_kernel != 1 && i2_dyn + sizeof(I2Tile) * kI2Groups + 8 * 1024 <= 160 * 1024) {
-    hipLaunchKernelGGL(h264_intra_v2, dim3(n_frames), dim3(kI2Threads), i2_dyn, s, a);
+  const size_t i2_lds = i2_lds_bytes(a.P.mb_width, a.P.mb_height);
+  if (a.intra_kernel != 1 && i2_lds <= 160 * 1024) {
+    hipLaunchKernelGGL(h264_intra_v2, dim3(n_frames), dim3(kI2Threads), i2_lds, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "h264_intra_v2 launch: %s", hipGetErrorString(e));
   } else {

@@ -138,9 +138,10 @@ std::string describe_decode_error(uint32_t f) {
       "emulation prevention inside I_PCM samples", "reference list modification",
       "P slice without reference frame", "adaptive reference marking (MMCO)",
       "B slice's wait for its colocated picture's parse timed out",
-      "coefficient arena range of a slice exceeded"};
+      "coefficient arena range of a slice exceeded",
+      "per-picture reconstruction scheduler: a reference picture never finished"};
   std::string s;
-  for (int i = 0; i < 15; ++i)
+  for (int i = 0; i < 16; ++i)
     if (f & (1u << i)) {
       if (!s.empty()) s += ", ";
       s += names[i];

@@ -83,6 +83,7 @@ enum DecodeError : uint32_t {
   DEC_E_COL_WAIT = 1u << 13,      // merged parse: a B slice's wait for its colocated picture timed out
   DEC_E_ARENA = 1u << 14,         // a slice's coefficient blocks overflowed its arena range (the host
                                   // re-runs the window with the provable bound)
+  DEC_E_SCHED = 1u << 15,         // h264_recon_sched: a wait for a reference picture never ended
   // not an error: a level-blocked reconstruct launch met a motion vector
   // reaching beyond its halo; the host re-runs with per-level launches
   DEC_W_LEVEL_RANGE = 1u << 31,

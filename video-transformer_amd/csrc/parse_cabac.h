@@ -336,6 +336,7 @@ struct CabacSyn {
     const uint32_t w4 = kMbSkip | (static_cast<uint32_t>(qp) << 8);
     const uint32_t ef = kMbSkip | (is_b ? kEDirect16 : 0u);
     SynEdge *te = &top[addr % mbw];
+    (void)w4;
 #if defined(__HIP_DEVICE_COMPILE__)
     VTS_LANES(26, l) {
       if (l < 16) {

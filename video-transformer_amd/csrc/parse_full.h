@@ -685,6 +685,7 @@ struct Parser {
       if (!e) return -1;
       br.skip(e >> 4);
       zeros = e & 15;
+      if (zeros + tc > maxNum) return -1;  // total_zeros beyond the block (a corrupt slice)
     }
     int pos = zeros + tc - 1;  // list index of the highest coefficient
     for (int i = 0; i < tc; ++i) {

@@ -45,7 +45,7 @@ struct Window {
   std::vector<int32_t> plv_end;    // general decoder: parse launch j covers window slices
                                    // [plv_end[j-1], plv_end[j]) (B pictures after their colocated picture)
   int64_t ds0 = 0;                 // general decoder, CABAC: the window's entries in vts_ctx::dslots
-  int32_t n_long = 0;              // ... its long slices (first in the parse order, wave priority raised)
+  int64_t rs0 = 0;                 // general decoder: the window's pictures in vts_ctx::rs_pics
   std::vector<int32_t> dlv_end;    // ... h264_derive launch j covers entries [dlv_end[j-1], dlv_end[j])
 };
 
@@ -192,6 +192,18 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
+  // per-picture reconstruction scheduler (h264_recon_sched; VTS_RECON_SCHED=0:
+  // the per-level launch chain): pictures in decoding order (slot, first ref,
+  // ref count), their reference pictures' slots, the launch's ticket counter,
+  // per ring slot the epoch of the run that finished it, workgroups per launch
+  bool recon_sched = true;
+  std::vector<int4> rs_pics;
+  std::vector<int32_t> rs_refs;
+  int4 *d_rs_pics = nullptr;
+  int32_t *d_rs_refs = nullptr;
+  uint32_t *d_rs_next = nullptr;
+  uint32_t *d_rs_done[2] = {nullptr, nullptr};
+  int rs_wg = 0;
   std::vector<int2> dslots;             // CABAC: the windows' pictures by parse level (h264_derive): ring slot,
                                         // common colocated slot
   int2 *d_dslots = nullptr;

@@ -267,6 +267,28 @@ int alloc_general(vts_ctx *c) {
   HIP_TRY(vts::dmalloc(&c->d_levels, sizeof(int4) * std::max<size_t>(1, c->level_frames.size())));
   HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(), hipMemcpyHostToDevice));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
+  // the per-picture reconstruction scheduler where its LDS fits (else the
+  // per-level launch chain): one workgroup per compute unit it can hold
+  // (capped at the ring), each with its own deblocking descriptors
+  if (const char *e = std::getenv("VTS_RECON_SCHED")) c->recon_sched = std::atoi(e) != 0;
+  if (recon_sched_lds_bytes(c->sps.mb_width, c->sps.mb_height) > 160 * 1024 || c->sps.mb_height > 1024)
+    c->recon_sched = false;
+  if (c->recon_sched) {
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
+    c->rs_wg = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, c->ring_frames)));
+    c->dbk_pics = c->rs_wg;
+    auto up = [](void **d, const void *h, size_t n) -> hipError_t {
+      if (*d) vts::dfree(*d);
+      *d = nullptr;
+      hipError_t e = vts::dmalloc(d, std::max<size_t>(4, n));
+      if (e == hipSuccess && n) e = hipMemcpy(*d, h, n, hipMemcpyHostToDevice);
+      return e;
+    };
+    HIP_TRY(up(reinterpret_cast<void **>(&c->d_rs_pics), c->rs_pics.data(), sizeof(int4) * c->rs_pics.size()));
+    HIP_TRY(up(reinterpret_cast<void **>(&c->d_rs_refs), c->rs_refs.data(), sizeof(int32_t) * c->rs_refs.size()));
+    HIP_TRY(up(reinterpret_cast<void **>(&c->d_rs_next), nullptr, 0));
+  }
   c->ws_bytes = score_workspace_bytes(c->width, c->height, c->k, c->ring_frames);
   const int64_t tw = (c->width / c->k) * (c->height / c->k);
   for (int r = 0; r < c->n_rings; ++r) {
@@ -275,6 +297,10 @@ int alloc_general(vts_ctx *c) {
       HIP_TRY(vts::dmalloc(&c->d_recs1[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRecB)));
     HIP_TRY(vts::dmalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
     HIP_TRY(vts::dmalloc(&c->d_pdone[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
+    if (c->recon_sched) {  // done flags: zero, never an epoch (runs count from 1)
+      HIP_TRY(vts::dmalloc(&c->d_rs_done[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
+      HIP_TRY(hipMemset(c->d_rs_done[r], 0, sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
+    }
     HIP_TRY(vts::dmalloc(&c->d_dbk[r], static_cast<size_t>(c->dbk_pics * nmb) * sizeof(DbkInfo)));
     HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
     HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
@@ -1345,11 +1371,15 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_porder_m);
   f(c->d_pneed);
   f(c->d_dslots);
+  f(c->d_rs_pics);
+  f(c->d_rs_refs);
+  f(c->d_rs_next);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);
     f(c->d_ilvl[r]);
     f(c->d_pdone[r]);
+    f(c->d_rs_done[r]);
     f(c->d_dbk[r]);
     f(c->d_arena[r]);
   }

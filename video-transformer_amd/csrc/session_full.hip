@@ -217,6 +217,8 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   c->porder_m.clear();
   c->pneed.clear();
   c->dslots.clear();
+  c->rs_pics.clear();
+  c->rs_refs.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
   for (Window &w : c->windows) {
@@ -304,15 +306,6 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       std::stable_sort(c->porder_m.begin() + static_cast<int64_t>(o0), c->porder_m.end(), [&](int32_t a, int32_t b) {
         return c->fslices[static_cast<size_t>(w.fs0 + a)].nal_size > c->fslices[static_cast<size_t>(w.fs0 + b)].nal_size;
       });
-      // "long" slices, >= 8 x the window's median (x264-like content: the I
-      // pictures, ~50x the median B slice): first in the order, prioritised
-      w.n_long = 0;
-      if (nws > 0) {
-        const int32_t med = c->fslices[static_cast<size_t>(w.fs0 + c->porder_m[o0 + static_cast<size_t>(nws / 2)])].nal_size;
-        while (w.n_long < nws &&
-               c->fslices[static_cast<size_t>(w.fs0 + c->porder_m[o0 + static_cast<size_t>(w.n_long)])].nal_size >= 8ll * med)
-          ++w.n_long;
-      }
     } else {
       for (size_t j = 0; j < w.plv_end.size(); ++j) {
         const int32_t b0 = j ? w.plv_end[j - 1] : 0;
@@ -340,6 +333,20 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
         c->dslots.push_back(make_int2(slot_of(f), static_cast<int32_t>(col < 0 ? -1 : col)));
       }
       w.dlv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->dslots.size()) - w.ds0));
+    }
+    // the per-picture scheduler's list: the window's pictures in decoding
+    // order with their reference pictures' slots
+    w.rs0 = static_cast<int64_t>(c->rs_pics.size());
+    for (int64_t f = w.f0; f < w.f1; ++f) {
+      const SchedFrame &fr = frames[static_cast<size_t>(f)];
+      const int32_t r0 = static_cast<int32_t>(c->rs_refs.size());
+      std::vector<int32_t> rs;
+      for (int64_t rf : fr.refs) {
+        const int32_t sl = slot_of(rf);
+        if (std::find(rs.begin(), rs.end(), sl) == rs.end()) rs.push_back(sl);
+      }
+      c->rs_refs.insert(c->rs_refs.end(), rs.begin(), rs.end());
+      c->rs_pics.push_back(make_int4(slot_of(f), r0, static_cast<int32_t>(rs.size()), 0));
     }
     w.pn0 = static_cast<int64_t>(c->pneed.size());
     c->pneed.resize(c->pneed.size() + static_cast<size_t>(w.f1 - w.f0), 0);
@@ -502,7 +509,6 @@ int submit_general(vts_ctx *c) {
       pa.order = c->d_porder_m + w.fs0;
       pa.pdone = nullptr;
       pa.pneed = nullptr;
-      pa.n_long = w.n_long;
       VTS_TRY(parse_full_launch(pa, sp));
       DeriveArgs da{};
       da.recs = c->d_recs[r];
@@ -563,68 +569,80 @@ int submit_general(vts_ctx *c) {
     ra.err = c->d_err;
     ra.sct = c->d_scale;
     ra.P = c->fprm;
-    // bS needs only the parse's records: one launch per level on the score
-    // stream, paced by the chain (level l + 1's after level l's inter launch),
-    // beside the intra and deblocking launches that leave most compute units
-    // idle.  (Measured and dropped, DESIGN.md §9: one window-wide launch at the
-    // head of the chain that both GOP groups waited for; bS inside each inter
-    // launch.)
-    const bool paced = !w.lvl_off.empty();
-    auto bs_level = [&](size_t l, hipStream_t s) {
-      ra.frames = c->d_levels + w.lvl_off[l];
-      return bs_full_launch(ra, w.lvl_cnt[l], s);
-    };
-    if (ng > 1) {  // groups >= 1 on their own streams, after the parse
-      HIP_TRY(hipEventRecord(c->ev_grp[0], sd));
-      for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], c->ev_grp[0], 0));
-    }
-    // the groups' level launches, interleaved (j-th level of every group, then
-    // the next): the score stream derives level j + 1's bS while
-    // group g runs level j's intra and deblocking launches (compute units the
-    // one-workgroup-per-picture kernels leave idle), and level j + 1 waits for it
-    // (one side stream for every group: the groups' bS on separate streams,
-    // odd groups' on the parse stream, measured slower — 188 -> 201 ms on the
-    // content stream, that stream sharing a hardware queue with a group's,
-    // profiles/r04t_bs_paced_split_ab.json)
-    auto sb_of = [&](int) { return c->s_score; };
-    std::vector<size_t> lo(static_cast<size_t>(ng)), hi(static_cast<size_t>(ng));
-    size_t jmax = 0;
-    for (int g = 0; g < ng; ++g) {
-      lo[static_cast<size_t>(g)] = g ? static_cast<size_t>(w.grp[static_cast<size_t>(g - 1)]) : 0;
-      hi[static_cast<size_t>(g)] = g + 1 < ng ? static_cast<size_t>(w.grp[static_cast<size_t>(g)]) : w.lvl_off.size();
-      jmax = std::max(jmax, hi[static_cast<size_t>(g)] - lo[static_cast<size_t>(g)]);
-    }
-    if (paced) {
-      if (c->ev_bs.size() < 2 * w.lvl_off.size()) {
-        const size_t n0 = c->ev_bs.size();
-        c->ev_bs.resize(2 * w.lvl_off.size(), nullptr);
-        for (size_t k = n0; k < c->ev_bs.size(); ++k) HIP_TRY(hipEventCreateWithFlags(&c->ev_bs[k], hipEventDisableTiming));
-      }
-      HIP_TRY(hipStreamWaitEvent(c->s_score, E[1], 0));
-      for (int g = 0; g < ng; ++g) {  // every group's first level
-        if (lo[static_cast<size_t>(g)] >= hi[static_cast<size_t>(g)]) continue;
-        VTS_TRY(bs_level(lo[static_cast<size_t>(g)], sb_of(g)));
-        HIP_TRY(hipEventRecord(c->ev_bs[2 * lo[static_cast<size_t>(g)]], sb_of(g)));
-      }
-    }
-    for (size_t jj = 0; jj < jmax; ++jj)
-      for (int g = 0; g < ng; ++g) {
-        const size_t l = lo[static_cast<size_t>(g)] + jj;
-        if (l >= hi[static_cast<size_t>(g)]) continue;
-        hipStream_t s = g ? c->s_grp[g - 1] : sd;
-        if (paced) HIP_TRY(hipStreamWaitEvent(s, c->ev_bs[2 * l], 0));
+    if (c->recon_sched) {
+      // every picture of the window by per-picture readiness, one launch
+      SchedArgs sa{};
+      sa.pics = c->d_rs_pics + w.rs0;
+      sa.refs = c->d_rs_refs;
+      sa.n_pics = static_cast<int32_t>(w.f1 - w.f0);
+      sa.next = c->d_rs_next;
+      sa.done = c->d_rs_done[r];
+      HIP_TRY(hipMemsetAsync(c->d_rs_next, 0, sizeof(uint32_t), sd));
+      VTS_TRY(recon_sched_launch(ra, sa, c->rs_wg, sd));
+    } else {
+      // bS needs only the parse's records: one launch per level on the score
+      // stream, paced by the chain (level l + 1's after level l's inter launch),
+      // beside the intra and deblocking launches that leave most compute units
+      // idle.  (Measured and dropped, DESIGN.md §9: one window-wide launch at the
+      // head of the chain that both GOP groups waited for; bS inside each inter
+      // launch.)
+      const bool paced = !w.lvl_off.empty();
+      auto bs_level = [&](size_t l, hipStream_t s) {
         ra.frames = c->d_levels + w.lvl_off[l];
-        const bool next = paced && l + 1 < hi[static_cast<size_t>(g)];
-        VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], s, next ? c->ev_bs[2 * l + 1] : nullptr));
-        if (next) {
-          HIP_TRY(hipStreamWaitEvent(sb_of(g), c->ev_bs[2 * l + 1], 0));
-          VTS_TRY(bs_level(l + 1, sb_of(g)));
-          HIP_TRY(hipEventRecord(c->ev_bs[2 * (l + 1)], sb_of(g)));
+        return bs_full_launch(ra, w.lvl_cnt[l], s);
+      };
+      if (ng > 1) {  // groups >= 1 on their own streams, after the parse
+        HIP_TRY(hipEventRecord(c->ev_grp[0], sd));
+        for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], c->ev_grp[0], 0));
+      }
+      // the groups' level launches, interleaved (j-th level of every group, then
+      // the next): the score stream derives level j + 1's bS while
+      // group g runs level j's intra and deblocking launches (compute units the
+      // one-workgroup-per-picture kernels leave idle), and level j + 1 waits for it
+      // (one side stream for every group: the groups' bS on separate streams,
+      // odd groups' on the parse stream, measured slower — 188 -> 201 ms on the
+      // content stream, that stream sharing a hardware queue with a group's,
+      // profiles/r04t_bs_paced_split_ab.json)
+      auto sb_of = [&](int) { return c->s_score; };
+      std::vector<size_t> lo(static_cast<size_t>(ng)), hi(static_cast<size_t>(ng));
+      size_t jmax = 0;
+      for (int g = 0; g < ng; ++g) {
+        lo[static_cast<size_t>(g)] = g ? static_cast<size_t>(w.grp[static_cast<size_t>(g - 1)]) : 0;
+        hi[static_cast<size_t>(g)] = g + 1 < ng ? static_cast<size_t>(w.grp[static_cast<size_t>(g)]) : w.lvl_off.size();
+        jmax = std::max(jmax, hi[static_cast<size_t>(g)] - lo[static_cast<size_t>(g)]);
+      }
+      if (paced) {
+        if (c->ev_bs.size() < 2 * w.lvl_off.size()) {
+          const size_t n0 = c->ev_bs.size();
+          c->ev_bs.resize(2 * w.lvl_off.size(), nullptr);
+          for (size_t k = n0; k < c->ev_bs.size(); ++k) HIP_TRY(hipEventCreateWithFlags(&c->ev_bs[k], hipEventDisableTiming));
+        }
+        HIP_TRY(hipStreamWaitEvent(c->s_score, E[1], 0));
+        for (int g = 0; g < ng; ++g) {  // every group's first level
+          if (lo[static_cast<size_t>(g)] >= hi[static_cast<size_t>(g)]) continue;
+          VTS_TRY(bs_level(lo[static_cast<size_t>(g)], sb_of(g)));
+          HIP_TRY(hipEventRecord(c->ev_bs[2 * lo[static_cast<size_t>(g)]], sb_of(g)));
         }
       }
-    for (int g = 1; g < ng; ++g) {
-      HIP_TRY(hipEventRecord(c->ev_grp[g - 1], c->s_grp[g - 1]));
-      HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[g - 1], 0));
+      for (size_t jj = 0; jj < jmax; ++jj)
+        for (int g = 0; g < ng; ++g) {
+          const size_t l = lo[static_cast<size_t>(g)] + jj;
+          if (l >= hi[static_cast<size_t>(g)]) continue;
+          hipStream_t s = g ? c->s_grp[g - 1] : sd;
+          if (paced) HIP_TRY(hipStreamWaitEvent(s, c->ev_bs[2 * l], 0));
+          ra.frames = c->d_levels + w.lvl_off[l];
+          const bool next = paced && l + 1 < hi[static_cast<size_t>(g)];
+          VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], s, next ? c->ev_bs[2 * l + 1] : nullptr));
+          if (next) {
+            HIP_TRY(hipStreamWaitEvent(sb_of(g), c->ev_bs[2 * l + 1], 0));
+            VTS_TRY(bs_level(l + 1, sb_of(g)));
+            HIP_TRY(hipEventRecord(c->ev_bs[2 * (l + 1)], sb_of(g)));
+          }
+        }
+      for (int g = 1; g < ng; ++g) {
+        HIP_TRY(hipEventRecord(c->ev_grp[g - 1], c->s_grp[g - 1]));
+        HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[g - 1], 0));
+      }
     }
     if (c->small.on) VTS_TRY(small_window(c, r, w.f0, w.f1, sd));
     HIP_TRY(hipEventRecord(E[2], sd));
