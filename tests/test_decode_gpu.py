@@ -148,8 +148,11 @@ def test_corrupted_slice_data_fails_loudly(tmp_path, coding):
     n = 24
     path, bad = tmp_path / "ok.mp4", tmp_path / "bad.mp4"
     extra = dict(cabac=True, transform_8x8=True) if coding == "cabac" else {}
+    # one slice per picture: the damage (past the first third of the sample)
+    # lands in slice data, never in another slice's header, which vts_open
+    # would refuse instead
     scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=True, weighted="implicit",
-                      cut_min_s=0.5, cut_max_s=1.0, gop_max_s=0.5, seed=17, **extra)
+                      cut_min_s=0.5, cut_max_s=1.0, gop_max_s=0.5, seed=17, slices_per_row=0, **extra)
     m = oracle.read_mp4(path)
     data = bytearray(path.read_bytes())
     rng = np.random.default_rng(5)

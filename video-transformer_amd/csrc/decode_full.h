@@ -90,7 +90,7 @@ struct FullReconArgs {
 
 // h264_recon_sched: every picture of a window, one persistent launch
 struct SchedArgs {
-  const int4 *pics;          // the window's pictures in decoding order: (ring slot, first entry in refs,
+  const int4 *pics;          // the window's pictures by dependency level: (ring slot, first entry in refs,
                              // reference pictures, -)
   const int32_t *refs;       // their reference pictures' ring slots (distinct per picture)
   int32_t n_pics;

@@ -1159,7 +1159,7 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   }
   if (m >= 0) atomicMax(&s_max, m);
   __syncthreads();
-  const int maxl = s_max;
+  const int maxl = __builtin_amdgcn_readfirstlane(s_max);  // uniform: the loops below hold barriers
   const int ms = tid >> 4, b = tid & 15;
   const bool bucketed = maxl < kIntraLevels;
   if (bucketed) {
@@ -1189,8 +1189,8 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   for (int l = 0; l <= maxl; ++l) {
     int j0, j1;
     if (bucketed) {
-      j0 = s_lvl[l];
-      j1 = s_lvl[l + 1];
+      j0 = __builtin_amdgcn_readfirstlane(s_lvl[l]);
+      j1 = __builtin_amdgcn_readfirstlane(s_lvl[l + 1]);
     } else {  // more levels than buckets: this level's macroblocks by a scan
       if (tid == 0) s_cnt = 0;
       __syncthreads();
@@ -1198,7 +1198,7 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
         if (lv[i] == l) s_list[atomicAdd(&s_cnt, 1)] = static_cast<uint16_t>(i);
       __syncthreads();
       j0 = 0;
-      j1 = s_cnt;
+      j1 = __builtin_amdgcn_readfirstlane(s_cnt);
     }
     for (int j = j0 + ms; j < j1; j += kIntraSlots) {
       intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4, s_off8, rp_);
@@ -1295,7 +1295,7 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
   }
   if (m >= 0) atomicMax(&s_max, m);
   __syncthreads();
-  const int maxl = s_max;
+  const int maxl = __builtin_amdgcn_readfirstlane(s_max);  // uniform: the loops below hold barriers
   const int g = tid >> 5;
   const DevLanes lanes0{tid & 31};
   i2::I2Ctx ctx;
@@ -1350,8 +1350,8 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
   for (int l = 0; l <= maxl; ++l) {
     int j0, j1;
     if (bucketed) {
-      j0 = s_lvl[l];
-      j1 = s_lvl[l + 1];
+      j0 = __builtin_amdgcn_readfirstlane(s_lvl[l]);
+      j1 = __builtin_amdgcn_readfirstlane(s_lvl[l + 1]);
     } else {
       if (tid == 0) s_cnt = 0;
       __syncthreads();
@@ -1359,7 +1359,7 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
         if (lv[i] == l) s_list[atomicAdd(&s_cnt, 1)] = static_cast<uint16_t>(i);
       __syncthreads();
       j0 = 0;
-      j1 = s_cnt;
+      j1 = __builtin_amdgcn_readfirstlane(s_cnt);
     }
     // rounds of 32 macroblocks: every group's reads (part 1), barrier, every
     // group's reconstruction and writes (part 2), the group's next
@@ -1681,6 +1681,11 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
   const uint32_t uvo = static_cast<uint32_t>(a.uv_off);
   auto at = [Y](uint32_t o) { return Y + static_cast<uint64_t>(o); };
+#if defined(VTS_EXP_DBK_BUF)
+  typedef uint32_t bv3 __attribute__((ext_vector_type(3)));
+  typedef uint32_t bv4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t srsc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, static_cast<int>(a.frame_stride), 0x00020000);
+#endif
   const int pitch = a.pitch;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = lane >> 4, l = lane & 15;
@@ -1710,10 +1715,31 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
     uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
     uint4 npx = *reinterpret_cast<const uint4 *>(at(rowo));
     constexpr int kLag = 2;
+#if defined(VTS_EXP_DBK_PF2)
+    // a second stage: the macroblock after next in flight too
+    const int xs1 = min(max(1 - kLag * grp, 0), mbw - 1);
+    const uint4 *dq1 = reinterpret_cast<const uint4 *>(drow + xs1);
+    uint4 nbs2 = dq1[0], nv2 = dq1[vq], nh2 = dq1[hq];
+    uint4 npx2 = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xs1 * 16)));
+#endif
     for (int it = 0; it < mbw + 3 * kLag; ++it) {
       const int x = it - kLag * grp;
       const bool act = row_ok && x >= 0 && x < mbw;
       const uint4 bsw = nbs, pv = nv, ph = nh, q4 = npx;
+#if defined(VTS_EXP_DBK_PF2)
+      {
+        nbs = nbs2;
+        nv = nv2;
+        nh = nh2;
+        npx = npx2;
+        const int xn = min(max(x + 2, 0), mbw - 1);
+        const uint4 *dn = reinterpret_cast<const uint4 *>(drow + xn);
+        nbs2 = dn[0];
+        nv2 = dn[vq];
+        nh2 = dn[hq];
+        npx2 = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xn * 16)));
+      }
+#else
       {
         const int xn = min(max(x + 1, 0), mbw - 1);
         const uint4 *dn = reinterpret_cast<const uint4 *>(drow + xn);
@@ -1722,6 +1748,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
         nh = dn[hq];
         npx = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xn * 16)));
       }
+#endif
       // a wave's first row waits for the previous wave's last row; its last
       // row waits until it may overwrite ring column x (the next wave's first
       // row read column x - kDpRingCols)
@@ -1813,6 +1840,61 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
         }
       }
       lane_sync();
+#if defined(VTS_EXP_DBK_BUF)
+      // ---- write back, every store issued by every lane at every step (the
+      // ones a lane must not make at an offset past the frame, which the
+      // buffer's range check drops): a constant count of stores per step lets
+      // the compiler wait for the prefetched loads only, not for the step
+      // before's stores as well (vmcnt counts both, in order)
+      {
+        uint32_t w0, w1, w2, w3, nleft;
+        if (still) {
+          w0 = left;
+          w1 = q4.x;
+          w2 = q4.y;
+          w3 = q4.z;
+          nleft = q4.w;
+        } else {
+          const uint8_t *src = &t.s[kTop + row][0];
+          w0 = *reinterpret_cast<const uint32_t *>(src);
+          w1 = *reinterpret_cast<const uint32_t *>(src + 4);
+          w2 = *reinterpret_cast<const uint32_t *>(src + 8);
+          w3 = *reinterpret_cast<const uint32_t *>(src + 12);
+          nleft = *reinterpret_cast<const uint32_t *>(src + 16);
+        }
+        constexpr uint32_t kOob = 0x80000000u;
+        const bool wr = act && lrow && (last_row || row < (kLuma ? 13 : 7));
+        const uint32_t o = rowo + static_cast<uint32_t>(x * 16);
+        __builtin_amdgcn_raw_buffer_store_b32(w0, srsc, (wr && x > 0 && (!still || ldirty)) ? o - 4 : kOob, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b96(bv3{w1, w2, w3}, srsc, (wr && !still) ? o : kOob, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(nleft, srsc, (wr && !still && x == mbw - 1) ? o + 12 : kOob, 0, 0);
+        if (act && lrow) {
+          left = nleft;
+          ldirty = !still;
+          const int lr = row - (kRows - kTop);  // ring line of this lane's row (luma 12..15, chroma 6..7)
+          if (!last_row && lr >= 0) {
+            Line &C = ring[rs][x & (kDpRingCols - 1)];
+            uint8_t *cur = &C.s[lr][0];
+            if (x > 0) *reinterpret_cast<uint32_t *>(&ring[rs][(x - 1) & (kDpRingCols - 1)].s[lr][12]) = w0;
+            *reinterpret_cast<uint32_t *>(cur) = w1;
+            *reinterpret_cast<uint32_t *>(cur + 4) = w2;
+            *reinterpret_cast<uint32_t *>(cur + 8) = w3;
+            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = nleft;
+          }
+        }
+        // luma rows -3..-1 / chroma row -1 of the macroblock above
+        int lo = lane;
+        asm volatile("" : "+v"(lo));
+        const int i = lo & 15, g = lo >> 4, yy = min(4 * p + g, mbh - 1);
+        const Tile &tt = tiles[__builtin_amdgcn_readfirstlane(wave) * 4 + g];
+        const uint4 v = *reinterpret_cast<const uint4 *>(&tt.s[1 + (kLuma ? min(i, 2) : 0)][4]);
+        const uint32_t oa = kLuma ? static_cast<uint32_t>((yy * 16 + i - 3) * pitch)
+                                  : uvo + static_cast<uint32_t>((yy * 8 - 1) * pitch);
+        const bool wa = act && l < (kLuma ? 3 : 1) && y > 0;
+        __builtin_amdgcn_raw_buffer_store_b128(bv4{v.x, v.y, v.z, v.w}, srsc,
+                                               wa ? oa + static_cast<uint32_t>(x * 16) : kOob, 0, 0);
+      }
+#else
       // ---- write back: this macroblock's rows shifted 4 bytes left except the
       // ones the row below finishes (luma 13..15, chroma 7), the ring lines for
       // the row below, the rows above that this macroblock's top edge finished
@@ -1872,6 +1954,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           *reinterpret_cast<uint4 *>(at(o + static_cast<uint32_t>(x * 16))) = v;
         }
       }
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       if (act && l == 0) {
@@ -1892,13 +1975,14 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs 
 }
 
 // ------------------------------------------------ per-picture scheduler
+// (VTS_RECON_SCHED=1; measured slower than the level launches)
 // One launch per window instead of three launches per reconstruction level:
 // a persistent grid (one 1024-thread workgroup per compute unit) whose
-// workgroups take the window's pictures by ticket in decoding order, wait
-// for that picture's reference pictures to be finished (per-slot flags set
-// to the run's epoch with agent-scope release / acquire), then run the whole
-// picture: inter prediction + residuals and its deblocking descriptors (16
-// lanes per macroblock, h264_inter_full / h264_bs_full's code), the intra
+// workgroups take the window's pictures by ticket in dependency-level order,
+// wait for that picture's reference pictures to be finished (per-slot flags
+// set to the run's epoch with agent-scope release / acquire), then run the
+// whole picture: inter prediction + residuals and its deblocking descriptors
+// (16 lanes per macroblock, h264_inter_full / h264_bs_full's code), the intra
 // macroblocks by dependency level (h264_intra_v2's), the deblocking of luma
 // then chroma (h264_deblock_plane's), and flag it.  A picture starts as soon
 // as its own references are done, not when a whole level of every GOP is.
@@ -1912,23 +1996,24 @@ __host__ __device__ constexpr size_t rs_dbk_lds_bytes() { return (kDpLds + 15) /
 // The phases are calls, not inlined: register allocation then stays per
 // phase (inlined into the one ticket loop, each phase's per-lane constants
 // were hoisted out of it and live across all of them: 241 VGPRs spilled).
-__device__ __attribute__((noinline)) void rs_inter(const FullReconArgs &a, int slot, int di, int nmb) {
+#define VTS_RS_PHASE __device__ __attribute__((noinline))
+VTS_RS_PHASE void rs_inter(const FullReconArgs &a, int slot, int di, int nmb) {
   for (int base = 0; base < nmb * 16; base += kRsThreads) {
     const int idx = base + static_cast<int>(threadIdx.x);
     inter_mb(a, slot, idx >> 4, idx & 15);
   }
 }
-__device__ __attribute__((noinline)) void rs_bs(const FullReconArgs &a, int slot, int di, int nmb) {
+VTS_RS_PHASE void rs_bs(const FullReconArgs &a, int slot, int di, int nmb) {
   for (int base = 0; base < nmb * 16; base += kRsThreads) {  // every lane (a macroblock's 16 meet in a butterfly)
     const int idx = base + static_cast<int>(threadIdx.x);
     bs_mb(a, slot, di, idx >> 4, idx & 15);
   }
 }
-__device__ __attribute__((noinline)) void rs_intra(const FullReconArgs &a, int slot, uint8_t *lds) {
+VTS_RS_PHASE void rs_intra(const FullReconArgs &a, int slot, uint8_t *lds) {
   intra_v2_picture(a, slot, lds);
 }
 template <bool kLuma>
-__device__ __attribute__((noinline)) void rs_deblock(const FullReconArgs &a, int slot, int di, uint8_t *lds, int *prog) {
+VTS_RS_PHASE void rs_deblock(const FullReconArgs &a, int slot, int di, uint8_t *lds, int *prog) {
   dp_plane<kLuma>(a, slot, di, lds, prog);
 }
 __global__ void __launch_bounds__(kRsThreads) h264_recon_sched(FullReconArgs a, SchedArgs sa) {
@@ -1938,11 +2023,15 @@ __global__ void __launch_bounds__(kRsThreads) h264_recon_sched(FullReconArgs a, 
   const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
   int *prog = reinterpret_cast<int *>(rlds + (kDpLds + 15) / 16 * 16);
   const int di = static_cast<int>(blockIdx.x);  // this workgroup's descriptor slot in a.dbk
-  for (;;) {
-    if (tid == 0) s_t = static_cast<int>(atomicAdd(sa.next, 1u));
-    __syncthreads();
-    const int t = s_t;
-    if (t >= sa.n_pics) break;
+  // The ticket: fetched by lane 0, broadcast through LDS, read as a uniform
+  // value, and the loop tested at its head only.  (With the fetch at the head
+  // and a break after it, the compiler made the loop exit divergent and,
+  // in its exec-mask bookkeeping, retired lane 0 after the first picture:
+  // the other lanes went on with a ticket nobody fetched any more.)
+  if (tid == 0) s_t = static_cast<int>(atomicAdd(sa.next, 1u));
+  __syncthreads();
+  int t = __builtin_amdgcn_readfirstlane(s_t);
+  while (t < sa.n_pics) {
     const int4 pic = sa.pics[t];
     const int slot = pic.x;
     if (tid < pic.z) {  // the reference pictures (lower tickets)
@@ -1972,7 +2061,12 @@ __global__ void __launch_bounds__(kRsThreads) h264_recon_sched(FullReconArgs a, 
     rs_deblock<false>(a, slot, di, rlds, prog);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave's samples out before the flag
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(&sa.done[slot], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __hip_atomic_store(&sa.done[slot], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_t = static_cast<int>(atomicAdd(sa.next, 1u));
+    }
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane(s_t);
   }
 }
 

@@ -192,11 +192,12 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
-  // per-picture reconstruction scheduler (h264_recon_sched; VTS_RECON_SCHED=0:
-  // the per-level launch chain): pictures in decoding order (slot, first ref,
-  // ref count), their reference pictures' slots, the launch's ticket counter,
-  // per ring slot the epoch of the run that finished it, workgroups per launch
-  bool recon_sched = true;
+  // per-picture reconstruction scheduler (h264_recon_sched, VTS_RECON_SCHED=1;
+  // measured slower than the per-level launch chain, the default — DESIGN.md
+  // §9): pictures by dependency level (slot, first ref, ref count), their
+  // reference pictures' slots, the launch's ticket counter, per ring slot the
+  // epoch of the run that finished it, workgroups per launch
+  bool recon_sched = false;
   std::vector<int4> rs_pics;
   std::vector<int32_t> rs_refs;
   int4 *d_rs_pics = nullptr;

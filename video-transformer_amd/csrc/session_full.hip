@@ -334,10 +334,18 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       }
       w.dlv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->dslots.size()) - w.ds0));
     }
-    // the per-picture scheduler's list: the window's pictures in decoding
-    // order with their reference pictures' slots
+    // the per-picture scheduler's list: the window's pictures by dependency
+    // level (then decoding order), each with its reference pictures' slots.
+    // Level order, not decoding order: a GOP is a chain, and tickets in
+    // decoding order would hand the grid one GOP's chain at a time (measured:
+    // 40x slower than the level launches); by level, the GOPs' chains advance
+    // side by side and a reference always holds a lower ticket.
     w.rs0 = static_cast<int64_t>(c->rs_pics.size());
-    for (int64_t f = w.f0; f < w.f1; ++f) {
+    std::vector<int64_t> by_level;
+    for (int64_t f = w.f0; f < w.f1; ++f) by_level.push_back(f);
+    std::stable_sort(by_level.begin(), by_level.end(),
+                     [&](int64_t x, int64_t y) { return level[static_cast<size_t>(x)] < level[static_cast<size_t>(y)]; });
+    for (int64_t f : by_level) {
       const SchedFrame &fr = frames[static_cast<size_t>(f)];
       const int32_t r0 = static_cast<int32_t>(c->rs_refs.size());
       std::vector<int32_t> rs;
@@ -477,11 +485,6 @@ int submit_general(vts_ctx *c) {
       HIP_TRY(hipStreamWaitEvent(sd, c->ev[(wi - c->n_rings) * 6 + 4], 0));
     }
     const int ng = 1 + static_cast<int>(w.grp.size());
-    auto grp_of = [&](size_t l) {  // group of reconstruct launch l
-      int g = 0;
-      while (g + 1 < ng && l >= static_cast<size_t>(w.grp[static_cast<size_t>(g)])) ++g;
-      return g;
-    };
     const int64_t run = c->run_no++;
     const uint32_t epoch = 1u + static_cast<uint32_t>(run % 0x7fffffff);
     if (c->ring_cleared_at[r] < 0) {  // records of another run read as absent (their epoch)
