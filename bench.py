@@ -1197,13 +1197,6 @@ def main() -> None:
         # the batch's sessions give their HBM back before the 2-h video's rings
         for v in sl:
             v.close()
-        try:
-            extra["general_batch"] = general_batch_record(gb_paths, gpu, threads, [x["cuts"] for x in gb_infos])
-            log(f"general_batch: {extra['general_batch']['value']} frames/s, "
-                f"x{extra['general_batch']['batch_over_single']} of one video's step, "
-                f"parity {extra['general_batch']['parity']['all_equal']}")
-        except Exception as exc:  # noqa: BLE001 - reported in the line
-            extra["general_batch"] = {"error": f"{type(exc).__name__}: {exc}"}
         # the general streams first: after the 2-h video's session its cached
         # segments cannot host the general decoder's ~56 GB coefficient arena,
         # and HBM released to the driver is cleared again before reuse (DESIGN
@@ -1236,6 +1229,19 @@ def main() -> None:
                 log(f"{key}: {r['value']} frames/s, parity {r.get('parity', {}).get('all_equal')}")
             except Exception as exc:  # noqa: BLE001 - reported in the line
                 extra[key] = {"error": f"{type(exc).__name__}: {exc}"}
+        # config [3]'s four general sessions last: their ~196 GB fit beside what
+        # the 2-h video's session left cached (carved from its segments, the
+        # rest fresh), while before it the 2-h video's 45 GB rings found no
+        # cached segment that large, HIP memory ran out and the cache went back
+        # to the driver, whose clear then cost the open ~6 s (r05d: alloc_ms
+        # 6 230)
+        try:
+            extra["general_batch"] = general_batch_record(gb_paths, gpu, threads, [x["cuts"] for x in gb_infos])
+            log(f"general_batch: {extra['general_batch']['value']} frames/s, "
+                f"x{extra['general_batch']['batch_over_single']} of one video's step, "
+                f"parity {extra['general_batch']['parity']['all_equal']}")
+        except Exception as exc:  # noqa: BLE001 - reported in the line
+            extra["general_batch"] = {"error": f"{type(exc).__name__}: {exc}"}
 
     if rank == 0:
         line = {

@@ -1681,11 +1681,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
   uint8_t *Y = a.surf + static_cast<int64_t>(slot) * a.frame_stride;
   const uint32_t uvo = static_cast<uint32_t>(a.uv_off);
   auto at = [Y](uint32_t o) { return Y + static_cast<uint64_t>(o); };
-#if defined(VTS_EXP_DBK_BUF)
-  typedef uint32_t bv3 __attribute__((ext_vector_type(3)));
-  typedef uint32_t bv4 __attribute__((ext_vector_type(4)));
-  const __amdgpu_buffer_rsrc_t srsc = __builtin_amdgcn_make_buffer_rsrc(Y, 0, static_cast<int>(a.frame_stride), 0x00020000);
-#endif
   const int pitch = a.pitch;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = lane >> 4, l = lane & 15;
@@ -1715,31 +1710,10 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
     uint4 nbs = dq[0], nv = dq[vq], nh = dq[hq];
     uint4 npx = *reinterpret_cast<const uint4 *>(at(rowo));
     constexpr int kLag = 2;
-#if defined(VTS_EXP_DBK_PF2)
-    // a second stage: the macroblock after next in flight too
-    const int xs1 = min(max(1 - kLag * grp, 0), mbw - 1);
-    const uint4 *dq1 = reinterpret_cast<const uint4 *>(drow + xs1);
-    uint4 nbs2 = dq1[0], nv2 = dq1[vq], nh2 = dq1[hq];
-    uint4 npx2 = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xs1 * 16)));
-#endif
     for (int it = 0; it < mbw + 3 * kLag; ++it) {
       const int x = it - kLag * grp;
       const bool act = row_ok && x >= 0 && x < mbw;
       const uint4 bsw = nbs, pv = nv, ph = nh, q4 = npx;
-#if defined(VTS_EXP_DBK_PF2)
-      {
-        nbs = nbs2;
-        nv = nv2;
-        nh = nh2;
-        npx = npx2;
-        const int xn = min(max(x + 2, 0), mbw - 1);
-        const uint4 *dn = reinterpret_cast<const uint4 *>(drow + xn);
-        nbs2 = dn[0];
-        nv2 = dn[vq];
-        nh2 = dn[hq];
-        npx2 = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xn * 16)));
-      }
-#else
       {
         const int xn = min(max(x + 1, 0), mbw - 1);
         const uint4 *dn = reinterpret_cast<const uint4 *>(drow + xn);
@@ -1748,7 +1722,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
         nh = dn[hq];
         npx = *reinterpret_cast<const uint4 *>(at(rowo + static_cast<uint32_t>(xn * 16)));
       }
-#endif
       // a wave's first row waits for the previous wave's last row; its last
       // row waits until it may overwrite ring column x (the next wave's first
       // row read column x - kDpRingCols)
@@ -1840,61 +1813,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
         }
       }
       lane_sync();
-#if defined(VTS_EXP_DBK_BUF)
-      // ---- write back, every store issued by every lane at every step (the
-      // ones a lane must not make at an offset past the frame, which the
-      // buffer's range check drops): a constant count of stores per step lets
-      // the compiler wait for the prefetched loads only, not for the step
-      // before's stores as well (vmcnt counts both, in order)
-      {
-        uint32_t w0, w1, w2, w3, nleft;
-        if (still) {
-          w0 = left;
-          w1 = q4.x;
-          w2 = q4.y;
-          w3 = q4.z;
-          nleft = q4.w;
-        } else {
-          const uint8_t *src = &t.s[kTop + row][0];
-          w0 = *reinterpret_cast<const uint32_t *>(src);
-          w1 = *reinterpret_cast<const uint32_t *>(src + 4);
-          w2 = *reinterpret_cast<const uint32_t *>(src + 8);
-          w3 = *reinterpret_cast<const uint32_t *>(src + 12);
-          nleft = *reinterpret_cast<const uint32_t *>(src + 16);
-        }
-        constexpr uint32_t kOob = 0x80000000u;
-        const bool wr = act && lrow && (last_row || row < (kLuma ? 13 : 7));
-        const uint32_t o = rowo + static_cast<uint32_t>(x * 16);
-        __builtin_amdgcn_raw_buffer_store_b32(w0, srsc, (wr && x > 0 && (!still || ldirty)) ? o - 4 : kOob, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b96(bv3{w1, w2, w3}, srsc, (wr && !still) ? o : kOob, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(nleft, srsc, (wr && !still && x == mbw - 1) ? o + 12 : kOob, 0, 0);
-        if (act && lrow) {
-          left = nleft;
-          ldirty = !still;
-          const int lr = row - (kRows - kTop);  // ring line of this lane's row (luma 12..15, chroma 6..7)
-          if (!last_row && lr >= 0) {
-            Line &C = ring[rs][x & (kDpRingCols - 1)];
-            uint8_t *cur = &C.s[lr][0];
-            if (x > 0) *reinterpret_cast<uint32_t *>(&ring[rs][(x - 1) & (kDpRingCols - 1)].s[lr][12]) = w0;
-            *reinterpret_cast<uint32_t *>(cur) = w1;
-            *reinterpret_cast<uint32_t *>(cur + 4) = w2;
-            *reinterpret_cast<uint32_t *>(cur + 8) = w3;
-            if (x == mbw - 1) *reinterpret_cast<uint32_t *>(cur + 12) = nleft;
-          }
-        }
-        // luma rows -3..-1 / chroma row -1 of the macroblock above
-        int lo = lane;
-        asm volatile("" : "+v"(lo));
-        const int i = lo & 15, g = lo >> 4, yy = min(4 * p + g, mbh - 1);
-        const Tile &tt = tiles[__builtin_amdgcn_readfirstlane(wave) * 4 + g];
-        const uint4 v = *reinterpret_cast<const uint4 *>(&tt.s[1 + (kLuma ? min(i, 2) : 0)][4]);
-        const uint32_t oa = kLuma ? static_cast<uint32_t>((yy * 16 + i - 3) * pitch)
-                                  : uvo + static_cast<uint32_t>((yy * 8 - 1) * pitch);
-        const bool wa = act && l < (kLuma ? 3 : 1) && y > 0;
-        __builtin_amdgcn_raw_buffer_store_b128(bv4{v.x, v.y, v.z, v.w}, srsc,
-                                               wa ? oa + static_cast<uint32_t>(x * 16) : kOob, 0, 0);
-      }
-#else
       // ---- write back: this macroblock's rows shifted 4 bytes left except the
       // ones the row below finishes (luma 13..15, chroma 7), the ring lines for
       // the row below, the rows above that this macroblock's top edge finished
@@ -1954,7 +1872,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           *reinterpret_cast<uint4 *>(at(o + static_cast<uint32_t>(x * 16))) = v;
         }
       }
-#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       if (act && l == 0) {

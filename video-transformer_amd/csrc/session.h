@@ -247,6 +247,8 @@ int submit_general(vts_ctx *c);
 int finish_general(vts_ctx *c);
 void assign_arena(vts_ctx *c);
 // cheap look at the stream's first pictures: does it need the general decoder?
+// the parameter sets alone send the stream to the general decoder
+bool general_by_headers(const vts_ctx *c);
 bool wants_general(const vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
                    const std::vector<uint32_t> &sizes, int nal_length_size);
 // downscale the window's frames (transcode.hip)

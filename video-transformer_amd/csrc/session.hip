@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -97,19 +98,33 @@ double now_s() {
 // runs between audio chunks otherwise) are one file range; ranges are cut into
 // pieces of <= kReadPiece bytes that kReadThreads threads pread at once (a
 // cached file copies at memory bandwidth per thread, one sequential reader was
-// the open's largest stage).
+// the open's largest stage).  A piece holds whole samples; `on_piece(k, s0,
+// s1)`, when given, runs on the reading thread as soon as piece k (samples
+// [s0, s1)) is in memory, after `on_plan(n)` announced the n pieces.
 constexpr int64_t kReadPiece = 8ll << 20;
-constexpr int kReadThreads = 8;
+int read_threads() {  // 8; VTS_READ_THREADS: 1..64 (measurement)
+  static const int n = [] {
+    const char *e = std::getenv("VTS_READ_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }();
+  return n;
+}
+
+struct PieceHooks {
+  std::function<void(size_t)> on_plan;
+  std::function<void(size_t, int64_t, int64_t)> on_piece;
+};
 
 int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size, const char *path,
-                   HostBytes *es, std::vector<int64_t> *es_off) {
+                   HostBytes *es, std::vector<int64_t> *es_off, const PieceHooks *hooks = nullptr) {
   int64_t total = 0;
   for (uint32_t s : t.size) total += s;
   es->alloc(total + kPad);
   std::memset(es->data() + total, 0, kPad);
   es_off->resize(t.size.size());
   struct Piece {
-    int64_t file, dst, n;
+    int64_t file, dst, n, s0, s1;
   };
   std::vector<Piece> pieces;
   int64_t pos = 0;
@@ -117,12 +132,15 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
     (*es_off)[i] = pos;
     const int64_t off = t.offset[i], n = t.size[i];
     if (off < 0 || (mem && off + n > mem_size)) return fail(VTS_E_FORMAT, "sample %zu out of file", i);
-    if (!pieces.empty() && pieces.back().file + pieces.back().n == off && pieces.back().n + n <= kReadPiece)
+    if (!pieces.empty() && pieces.back().file + pieces.back().n == off && pieces.back().n + n <= kReadPiece) {
       pieces.back().n += n;
-    else
-      pieces.push_back(Piece{off, pos, n});
+      pieces.back().s1 = static_cast<int64_t>(i) + 1;
+    } else {
+      pieces.push_back(Piece{off, pos, n, static_cast<int64_t>(i), static_cast<int64_t>(i) + 1});
+    }
     pos += n;
   }
+  if (hooks && hooks->on_plan) hooks->on_plan(pieces.size());
   if (pieces.empty()) return VTS_OK;
   int fd = -1;
   if (!mem) {
@@ -137,20 +155,22 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
       uint8_t *dst = es->data() + pc.dst;
       if (mem) {
         std::memcpy(dst, mem + pc.file, static_cast<size_t>(pc.n));
-        continue;
-      }
-      int64_t done = 0;
-      while (done < pc.n) {
-        const ssize_t r = ::pread(fd, dst + done, static_cast<size_t>(pc.n - done), pc.file + done);
-        if (r <= 0) {
-          bad = pc.dst + done;
-          break;
+      } else {
+        int64_t done = 0;
+        while (done < pc.n) {
+          const ssize_t r = ::pread(fd, dst + done, static_cast<size_t>(pc.n - done), pc.file + done);
+          if (r <= 0) {
+            bad = pc.dst + done;
+            break;
+          }
+          done += r;
         }
-        done += r;
+        if (done < pc.n) break;
       }
+      if (hooks && hooks->on_piece) hooks->on_piece(k, pc.s0, pc.s1);
     }
   };
-  const int nt = static_cast<int>(std::min<size_t>(kReadThreads, pieces.size()));
+  const int nt = static_cast<int>(std::min<size_t>(static_cast<size_t>(read_threads()), pieces.size()));
   std::vector<std::thread> th;
   for (int i = 1; i < nt; ++i) th.emplace_back(worker);
   worker();
@@ -451,9 +471,83 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   if ((c->pps.weighted_pred || c->pps.weighted_bipred_idc) && c->params.decoder == 1)
     return fail(VTS_E_UNSUPPORTED, "weighted prediction needs the general decoder");
 
+  // The subset decoder's NAL walk (slice table, intra / reference flags per
+  // frame) runs on the reading threads, piece by piece as each is read, into
+  // per-piece tables joined in frame order below (a 2-h 720p video is ~10 M
+  // slices: walked after the read on one thread it was the open's longest
+  // stage).  Skipped when the headers already ask for the general decoder.
+  struct Run {
+    std::vector<SliceDesc> sl;
+    int rc = VTS_OK;
+    std::string msg;
+    int64_t s0 = 0, s1 = 0;
+  };
+  std::vector<Run> runs;
+  const int L = t.nal_length_size;
+  std::vector<int64_t> first_slice(c->n_frames), n_slices(c->n_frames);
+  std::vector<uint8_t> intra(c->n_frames, 1), is_ref(c->n_frames, 0);
   HostBytes es;
   std::vector<int64_t> es_off;
-  VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off));
+  auto walk = [&](Run &R, int64_t f0, int64_t f1) {
+    const uint8_t *E = es.data();
+    R.s0 = f0;
+    R.s1 = f1;
+    R.sl.reserve(static_cast<size_t>(f1 - f0) * 2);
+    for (int64_t f = f0; f < f1; ++f) {
+      int64_t p = es_off[f];
+      const int64_t end = p + t.size[f];
+      first_slice[f] = static_cast<int64_t>(R.sl.size());  // within the piece, rebased below
+      while (p + L <= end) {
+        uint32_t len = 0;
+        for (int i = 0; i < L; ++i) len = (len << 8) | E[p + i];
+        p += L;
+        if (len == 0 || p + len > end) {
+          R.rc = VTS_E_FORMAT;
+          R.msg = "bad NAL length in frame " + std::to_string(f);
+          return;
+        }
+        const uint8_t hdr = E[p];
+        const int type = hdr & 0x1f;
+        if (type == 1 || type == 5) {
+          BitReader br(E + p + 1, len - 1);
+          br.ue();  // first_mb_in_slice
+          uint32_t st = br.ue();
+          if (st > 4) st -= 5;
+          if (st != 2) intra[f] = 0;
+          if ((hdr >> 5) & 3) is_ref[f] = 1;
+          SliceDesc sd{};
+          sd.nal_offset = p;
+          sd.nal_size = static_cast<int32_t>(len);
+          R.sl.push_back(sd);
+        } else if (type == 7 || type == 8) {
+          const std::vector<uint8_t> &ps = (type == 7) ? t.sps[0] : t.pps[0];
+          if (ps.size() != len || std::memcmp(ps.data(), E + p, len) != 0) {
+            R.rc = VTS_E_UNSUPPORTED;
+            R.msg = "in-band parameter set differs from avcC";
+            return;
+          }
+        } else if (type >= 2 && type <= 4) {
+          R.rc = VTS_E_UNSUPPORTED;
+          R.msg = "data partitioning is not supported";
+          return;
+        }
+        p += len;
+      }
+      n_slices[f] = static_cast<int64_t>(R.sl.size()) - first_slice[f];
+      if (n_slices[f] == 0) {
+        R.rc = VTS_E_FORMAT;
+        R.msg = "frame " + std::to_string(f) + " has no slices";
+        return;
+      }
+    }
+  };
+  PieceHooks hooks;
+  hooks.on_plan = [&](size_t n) { runs.resize(n); };
+  hooks.on_piece = [&](size_t k, int64_t s0, int64_t s1) { walk(runs[k], s0, s1); };
+  // (subset only, or auto unless reordering or the parameter sets already
+  // send the stream to the general decoder: wants_general's first checks)
+  const bool may_subset = c->params.decoder == 1 || (c->params.decoder == 0 && !reorder && !general_by_headers(c));
+  VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off, may_subset ? &hooks : nullptr));
   c->es_bytes = static_cast<int64_t>(es.size());
   c->open_lap(2);
   // the ES goes to HBM on its own thread while the schedule below is built
@@ -481,43 +575,27 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
     return VTS_OK;
   }
 
-  // NAL walk: slice table, intra / reference flags per frame
-  const int L = t.nal_length_size;
-  std::vector<int64_t> first_slice(c->n_frames), n_slices(c->n_frames);
-  std::vector<uint8_t> intra(c->n_frames, 1), is_ref(c->n_frames, 0);
-  for (int64_t f = 0; f < c->n_frames; ++f) {
-    int64_t p = es_off[f];
-    const int64_t end = p + t.size[f];
-    first_slice[f] = static_cast<int64_t>(c->slices.size());
-    while (p + L <= end) {
-      uint32_t len = 0;
-      for (int i = 0; i < L; ++i) len = (len << 8) | es[p + i];
-      p += L;
-      if (len == 0 || p + len > end) return fail(VTS_E_FORMAT, "bad NAL length in frame %lld", (long long)f);
-      const uint8_t hdr = es[p];
-      const int type = hdr & 0x1f;
-      if (type == 1 || type == 5) {
-        BitReader br(es.data() + p + 1, len - 1);
-        br.ue();  // first_mb_in_slice
-        uint32_t st = br.ue();
-        if (st > 4) st -= 5;
-        if (st != 2) intra[f] = 0;
-        if ((hdr >> 5) & 3) is_ref[f] = 1;
-        SliceDesc sd{};
-        sd.nal_offset = p;
-        sd.nal_size = static_cast<int32_t>(len);
-        c->slices.push_back(sd);
-      } else if (type == 7 || type == 8) {
-        const std::vector<uint8_t> &ps = (type == 7) ? t.sps[0] : t.pps[0];
-        if (ps.size() != len || std::memcmp(ps.data(), es.data() + p, len) != 0)
-          return fail(VTS_E_UNSUPPORTED, "in-band parameter set differs from avcC");
-      } else if (type >= 2 && type <= 4) {
-        return fail(VTS_E_UNSUPPORTED, "data partitioning is not supported");
+  // the pieces' slice tables, joined in frame order (the first failing
+  // piece in frame order reports, as one walk would)
+  if (!may_subset) return fail(VTS_E_INVALID, "decoder %d: no subset schedule", c->params.decoder);
+  {
+    for (const Run &R : runs)
+      if (R.rc != VTS_OK) return fail(R.rc, "%s", R.msg.c_str());
+    const size_t nr = runs.size();
+    std::vector<int64_t> base(nr + 1, 0);
+    for (size_t r = 0; r < nr; ++r) base[r + 1] = base[r] + static_cast<int64_t>(runs[r].sl.size());
+    c->slices.resize(static_cast<size_t>(base[nr]));
+    std::atomic<size_t> next{0};
+    auto join = [&]() {
+      for (size_t r = next++; r < nr; r = next++) {
+        for (int64_t f = runs[r].s0; f < runs[r].s1; ++f) first_slice[f] += base[r];
+        std::copy(runs[r].sl.begin(), runs[r].sl.end(), c->slices.begin() + base[r]);
       }
-      p += len;
-    }
-    n_slices[f] = static_cast<int64_t>(c->slices.size()) - first_slice[f];
-    if (n_slices[f] == 0) return fail(VTS_E_FORMAT, "frame %lld has no slices", (long long)f);
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < read_threads() && static_cast<size_t>(i) < nr; ++i) th.emplace_back(join);
+    join();
+    for (auto &x : th) x.join();
   }
 
   // references and levels (single reference: the latest reference picture)

@@ -54,15 +54,19 @@ constexpr int64_t kMinRingBytes = 1ll << 30;
 
 }  // namespace
 
-bool wants_general(const vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
-                   const std::vector<uint32_t> &sizes, int nal_length_size) {
+bool general_by_headers(const vts_ctx *c) {
   if (c->pps.entropy_coding_mode) return true;  // CABAC
   // a High-profile PPS tail (8x8 transform, scaling lists, a Cr QP offset the
   // subset kernels' deblocking gate does not see): ADVICE r03
   if (c->pps.has_tail) return true;
   if (c->pps.weighted_pred || c->pps.weighted_bipred_idc) return true;
   if (c->sps.max_num_ref_frames > 1 || c->pps.num_ref_idx_l0_default_active > 1) return true;
-  if (!c->pps.deblocking_filter_control_present) return true;  // deblocking on, offsets 0
+  return !c->pps.deblocking_filter_control_present;  // deblocking on, offsets 0
+}
+
+bool wants_general(const vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_off,
+                   const std::vector<uint32_t> &sizes, int nal_length_size) {
+  if (general_by_headers(c)) return true;
   // the first pictures' slice headers: an active deblocking filter or several references
   const size_t n = std::min<size_t>(sizes.size(), 3);
   std::vector<int64_t> off(es_off.begin(), es_off.begin() + static_cast<int64_t>(n));
