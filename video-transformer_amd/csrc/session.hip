@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -188,66 +189,87 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
 // (process-wide, allocated once) -> hipMemcpyAsync into HBM, so the copy into
 // a staging slot overlaps the DMA of the previous one (a pageable hipMemcpy
 // stages internally, one small chunk at a time, synchronously).  Runs on its
-// own thread beside the host schedule (EsUpload).
+// own thread and takes byte ranges as they become ready: the reading threads
+// push each piece as it lands, so the upload runs beside the read and the
+// schedule instead of after the read.
 constexpr int64_t kStageBytes = 16ll << 20;
 constexpr int kStageSlots = 4;
 std::mutex g_stage_mu;
 uint8_t *g_stage[kStageSlots] = {nullptr, nullptr, nullptr, nullptr};
 
-int upload_es(int device, uint8_t *d_es, const uint8_t *host, int64_t n) {
-  std::lock_guard<std::mutex> lk(g_stage_mu);
-  HIP_TRY(hipSetDevice(device));
-  if (n <= kStageBytes) {  // small: one synchronous copy
-    HIP_TRY(hipMemcpy(d_es, host, static_cast<size_t>(n), hipMemcpyHostToDevice));
-    return VTS_OK;
-  }
-  for (int i = 0; i < kStageSlots; ++i)
-    if (!g_stage[i]) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&g_stage[i]), kStageBytes, hipHostMallocDefault));
-  hipStream_t s = nullptr;
-  HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  hipEvent_t ev[kStageSlots] = {};
-  int rc = VTS_OK;
-  for (int i = 0; i < kStageSlots && rc == VTS_OK; ++i)
-    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) rc = fail(VTS_E_HIP, "hipEventCreate");
-  for (int64_t off = 0, k = 0; off < n && rc == VTS_OK; off += kStageBytes, ++k) {
-    const int slot = static_cast<int>(k % kStageSlots);
-    if (k >= kStageSlots && hipEventSynchronize(ev[slot]) != hipSuccess) {
-      rc = fail(VTS_E_HIP, "staging event");
-      break;
-    }
-    const int64_t len = std::min(kStageBytes, n - off);
-    std::memcpy(g_stage[slot], host + off, static_cast<size_t>(len));
-    if (hipMemcpyAsync(d_es + off, g_stage[slot], static_cast<size_t>(len), hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipEventRecord(ev[slot], s) != hipSuccess)
-      rc = fail(VTS_E_HIP, "elementary-stream upload");
-  }
-  if (hipStreamSynchronize(s) != hipSuccess && rc == VTS_OK) rc = fail(VTS_E_HIP, "elementary-stream upload");
-  for (auto e : ev)
-    if (e) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(s);
-  return rc;
-}
-
-// upload_es on a thread of its own: started once the ES is read and its device
-// buffer allocated, joined before the first device work that reads it; the
-// host schedule runs meanwhile
 struct EsUpload {
   std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::pair<int64_t, int64_t>> q;  // (offset, bytes) ready in host memory
+  bool closed = false;
   int rc = VTS_OK;
   std::string msg;
-  void start(int device, uint8_t *d_es, const uint8_t *host, int64_t n) {
-    th = std::thread([this, device, d_es, host, n]() {
-      rc = upload_es(device, d_es, host, n);
+  void start(int device, uint8_t *d_es, const uint8_t *host) {
+    th = std::thread([this, device, d_es, host]() {
+      rc = run(device, d_es, host);
       if (rc != VTS_OK) msg = last_error();
     });
   }
+  void push(int64_t off, int64_t n) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      q.emplace_back(off, n);
+    }
+    cv.notify_one();
+  }
   int join() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      closed = true;
+    }
+    cv.notify_one();
     if (th.joinable()) th.join();
     if (rc != VTS_OK) return fail(rc, "%s", msg.c_str());
     return VTS_OK;
   }
-  ~EsUpload() {
-    if (th.joinable()) th.join();
+  ~EsUpload() { (void)join(); }
+
+ private:
+  int run(int device, uint8_t *d_es, const uint8_t *host) {
+    std::lock_guard<std::mutex> slk(g_stage_mu);
+    HIP_TRY(hipSetDevice(device));
+    for (int i = 0; i < kStageSlots; ++i)
+      if (!g_stage[i]) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&g_stage[i]), kStageBytes, hipHostMallocDefault));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t ev[kStageSlots] = {};
+    int r = VTS_OK;
+    for (int i = 0; i < kStageSlots && r == VTS_OK; ++i)
+      if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) r = fail(VTS_E_HIP, "hipEventCreate");
+    int64_t k = 0;  // staging copies so far
+    for (;;) {
+      std::pair<int64_t, int64_t> item;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !q.empty() || closed; });
+        if (q.empty()) break;
+        item = q.back();
+        q.pop_back();
+      }
+      for (int64_t off = item.first, end = item.first + item.second; off < end && r == VTS_OK; off += kStageBytes, ++k) {
+        const int slot = static_cast<int>(k % kStageSlots);
+        if (k >= kStageSlots && hipEventSynchronize(ev[slot]) != hipSuccess) {
+          r = fail(VTS_E_HIP, "staging event");
+          break;
+        }
+        const int64_t len = std::min(kStageBytes, end - off);
+        std::memcpy(g_stage[slot], host + off, static_cast<size_t>(len));
+        if (hipMemcpyAsync(d_es + off, g_stage[slot], static_cast<size_t>(len), hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipEventRecord(ev[slot], s) != hipSuccess)
+          r = fail(VTS_E_HIP, "elementary-stream upload");
+      }
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && r == VTS_OK) r = fail(VTS_E_HIP, "elementary-stream upload");
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(s);
+    return r;
   }
 };
 
@@ -541,21 +563,33 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
       }
     }
   };
-  PieceHooks hooks;
-  hooks.on_plan = [&](size_t n) { runs.resize(n); };
-  hooks.on_piece = [&](size_t k, int64_t s0, int64_t s1) { walk(runs[k], s0, s1); };
   // (subset only, or auto unless reordering or the parameter sets already
   // send the stream to the general decoder: wants_general's first checks)
   const bool may_subset = c->params.decoder == 1 || (c->params.decoder == 0 && !reorder && !general_by_headers(c));
-  VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off, may_subset ? &hooks : nullptr));
-  c->es_bytes = static_cast<int64_t>(es.size());
-  c->open_lap(2);
-  // the ES goes to HBM on its own thread while the schedule below is built
+  // the ES's device buffer first: each piece goes up as soon as it is read
+  {
+    int64_t total = 0;
+    for (uint32_t n : t.size) total += n;
+    c->es_bytes = total + kPad;
+  }
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(vts::dmalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
-  EsUpload up;
-  up.start(c->device, c->d_es, es.data(), c->es_bytes);
   c->open_lap(4);
+  EsUpload up;
+  PieceHooks hooks;
+  hooks.on_plan = [&](size_t n) {
+    runs.resize(n);
+    up.start(c->device, c->d_es, es.data());
+  };
+  hooks.on_piece = [&](size_t k, int64_t s0, int64_t s1) {
+    const int64_t off = es_off[s0], end = s1 < c->n_frames ? es_off[s1] : es_off[s1 - 1] + t.size[s1 - 1];
+    up.push(off, end - off);
+    if (may_subset) walk(runs[k], s0, s1);
+  };
+  VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off, &hooks));
+  if (static_cast<int64_t>(es.size()) != c->es_bytes) return fail(VTS_E_FORMAT, "elementary stream size");
+  up.push(c->es_bytes - kPad, kPad);  // the zero padding after the last sample
+  c->open_lap(2);
   c->es_off = es_off;
   c->sample_size = t.size;
   c->nal_length_size = t.nal_length_size;
@@ -676,7 +710,11 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   }
   // slice slots / ref slots and per-level frame lists
   std::vector<int32_t> launch_of(static_cast<size_t>(c->n_frames), 0);  // launch index within its window
-  for (Window &w : c->windows) {
+  // per window: the slices' first index per level launch (the slice pass
+  // below, on threads: slots and the launch-order sort touch every slice)
+  std::vector<std::vector<int64_t>> wcnt(c->windows.size());
+  for (size_t wi = 0; wi < c->windows.size(); ++wi) {
+    Window &w = c->windows[wi];
     w.s0 = first_slice[w.f0];
     w.s1 = (w.f1 < c->n_frames) ? first_slice[w.f1] : static_cast<int64_t>(c->slices.size());
     int64_t maxl = 0;
@@ -684,10 +722,6 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
       if (ref[x] >= 0 && ref[x] < w.f0)
         return fail(VTS_E_UNSUPPORTED, "reference crosses a window boundary");
       maxl = std::max(maxl, level[x]);
-      for (int64_t s = first_slice[x]; s < first_slice[x] + n_slices[x]; ++s) {
-        c->slices[s].slot = static_cast<int32_t>(x - w.f0);
-        c->slices[s].ref_slot = ref[x] >= 0 ? static_cast<int32_t>(ref[x] - w.f0) : -1;
-      }
     }
     // GOPs (runs starting at an intra frame) of this window.  Default: every
     // GOP of the window in each level launch.  Grouping GOPs so a launch's
@@ -745,12 +779,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
       for (int64_t l = 0; l < nl; ++l) cnt[l + 1] += cnt[l];
       w.lvl_s0.resize(static_cast<size_t>(nl));
       for (int64_t l = 0; l < nl; ++l) w.lvl_s0[l] = w.s0 + cnt[l];
-      std::vector<SliceDesc> sorted(static_cast<size_t>(w.s1 - w.s0));
-      std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
-      for (int64_t x = w.f0; x < w.f1; ++x)
-        for (int64_t sl = first_slice[x]; sl < first_slice[x] + n_slices[x]; ++sl)
-          sorted[static_cast<size_t>(fill[launch_of[x]]++)] = c->slices[sl];
-      std::copy(sorted.begin(), sorted.end(), c->slices.begin() + w.s0);
+      wcnt[wi] = cnt;
       // Parse chunks: the first covers launch 0 alone (reconstruction starts
       // as soon as the intra pictures are parsed), the rest split the other
       // launches into runs of about equal slice counts.
@@ -828,6 +857,33 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
         }
       }
     }
+  }
+
+  // the slice pass, one window per thread: frame slots, reference slots and
+  // the launch-order sort (stable: decode order within a launch), so the
+  // slices of launches [a, b) are one contiguous range
+  {
+    std::atomic<size_t> next{0};
+    auto pass = [&]() {
+      for (size_t wi = next++; wi < c->windows.size(); wi = next++) {
+        const Window &w = c->windows[wi];
+        std::vector<SliceDesc> sorted(static_cast<size_t>(w.s1 - w.s0));
+        std::vector<int64_t> fill(wcnt[wi].begin(), wcnt[wi].end() - 1);
+        for (int64_t x = w.f0; x < w.f1; ++x)
+          for (int64_t sl = first_slice[x]; sl < first_slice[x] + n_slices[x]; ++sl) {
+            SliceDesc d = c->slices[sl];
+            d.slot = static_cast<int32_t>(x - w.f0);
+            d.ref_slot = ref[x] >= 0 ? static_cast<int32_t>(ref[x] - w.f0) : -1;
+            sorted[static_cast<size_t>(fill[launch_of[x]]++)] = d;
+          }
+        std::copy(sorted.begin(), sorted.end(), c->slices.begin() + w.s0);
+      }
+    };
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < std::min<size_t>(static_cast<size_t>(read_threads()), c->windows.size()); ++i)
+      th.emplace_back(pass);
+    pass();
+    for (auto &x : th) x.join();
   }
 
   // ---- device allocations and uploads
