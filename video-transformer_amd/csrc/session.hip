@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -100,8 +102,10 @@ double now_s() {
 // pieces of <= kReadPiece bytes that kReadThreads threads pread at once (a
 // cached file copies at memory bandwidth per thread, one sequential reader was
 // the open's largest stage).  A piece holds whole samples; `on_piece(k, s0,
-// s1)`, when given, runs on the reading thread as soon as piece k (samples
-// [s0, s1)) is in memory, after `on_plan(n)` announced the n pieces.
+// s1, src)`, when given, runs on the reading thread as soon as piece k
+// (samples [s0, s1), their bytes back to back at src) is in memory, after
+// `on_plan(n)` announced the n pieces.  With `es` null and `mem` given
+// (a mapped file) nothing is copied: src points into `mem`.
 constexpr int64_t kReadPiece = 8ll << 20;
 int read_threads() {  // 8; VTS_READ_THREADS: 1..64 (measurement)
   static const int n = [] {
@@ -112,17 +116,50 @@ int read_threads() {  // 8; VTS_READ_THREADS: 1..64 (measurement)
   return n;
 }
 
+// a read-only private mapping of a whole file (munmap on a detached thread
+// for large ones, like HostBytes)
+struct FileMap {
+  const uint8_t *p = nullptr;
+  int64_t n = 0;
+  int open(const char *path) {
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return fail(VTS_E_IO, "cannot open %s", path);
+    struct stat st {};
+    if (::fstat(fd, &st) != 0 || st.st_size <= 0) {
+      ::close(fd);
+      return fail(VTS_E_IO, "cannot stat %s", path);
+    }
+    void *m = ::mmap(nullptr, static_cast<size_t>(st.st_size), PROT_READ, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (m == MAP_FAILED) return fail(VTS_E_IO, "cannot map %s", path);
+    (void)::madvise(m, static_cast<size_t>(st.st_size), MADV_WILLNEED);
+    p = static_cast<const uint8_t *>(m);
+    n = st.st_size;
+    return VTS_OK;
+  }
+  ~FileMap() {
+    if (!p) return;
+    void *m = const_cast<uint8_t *>(p);
+    const size_t len = static_cast<size_t>(n);
+    if (n >= (int64_t{64} << 20)) std::thread([m, len]() { ::munmap(m, len); }).detach();
+    else ::munmap(m, len);
+  }
+};
+
 struct PieceHooks {
   std::function<void(size_t)> on_plan;
-  std::function<void(size_t, int64_t, int64_t)> on_piece;
+  std::function<void(size_t, int64_t, int64_t, const uint8_t *)> on_piece;
 };
 
 int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size, const char *path,
                    HostBytes *es, std::vector<int64_t> *es_off, const PieceHooks *hooks = nullptr) {
   int64_t total = 0;
   for (uint32_t s : t.size) total += s;
-  es->alloc(total + kPad);
-  std::memset(es->data() + total, 0, kPad);
+  if (!es && !mem) return fail(VTS_E_INVALID, "gather_samples: nowhere to read to");
+  if (es) {
+    es->alloc(total + kPad);
+    std::memset(es->data() + total, 0, kPad);
+  }
   es_off->resize(t.size.size());
   struct Piece {
     int64_t file, dst, n, s0, s1;
@@ -153,6 +190,10 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
   auto worker = [&]() {
     for (size_t k = next++; k < pieces.size() && bad.load() < 0; k = next++) {
       const Piece &pc = pieces[k];
+      if (!es) {  // mapped: the piece is where it lies
+        if (hooks && hooks->on_piece) hooks->on_piece(k, pc.s0, pc.s1, mem + pc.file);
+        continue;
+      }
       uint8_t *dst = es->data() + pc.dst;
       if (mem) {
         std::memcpy(dst, mem + pc.file, static_cast<size_t>(pc.n));
@@ -168,7 +209,7 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
         }
         if (done < pc.n) break;
       }
-      if (hooks && hooks->on_piece) hooks->on_piece(k, pc.s0, pc.s1);
+      if (hooks && hooks->on_piece) hooks->on_piece(k, pc.s0, pc.s1, dst);
     }
   };
   const int nt = static_cast<int>(std::min<size_t>(static_cast<size_t>(read_threads()), pieces.size()));
@@ -201,20 +242,24 @@ struct EsUpload {
   std::thread th;
   std::mutex mu;
   std::condition_variable cv;
-  std::vector<std::pair<int64_t, int64_t>> q;  // (offset, bytes) ready in host memory
+  struct Item {
+    const uint8_t *src;
+    int64_t dst, n;
+  };
+  std::vector<Item> q;  // host bytes ready, and where they go in the device ES
   bool closed = false;
   int rc = VTS_OK;
   std::string msg;
-  void start(int device, uint8_t *d_es, const uint8_t *host) {
-    th = std::thread([this, device, d_es, host]() {
-      rc = run(device, d_es, host);
+  void start(int device, uint8_t *d_es) {
+    th = std::thread([this, device, d_es]() {
+      rc = run(device, d_es);
       if (rc != VTS_OK) msg = last_error();
     });
   }
-  void push(int64_t off, int64_t n) {
+  void push(const uint8_t *src, int64_t dst, int64_t n) {
     {
       std::lock_guard<std::mutex> lk(mu);
-      q.emplace_back(off, n);
+      q.push_back(Item{src, dst, n});
     }
     cv.notify_one();
   }
@@ -231,7 +276,7 @@ struct EsUpload {
   ~EsUpload() { (void)join(); }
 
  private:
-  int run(int device, uint8_t *d_es, const uint8_t *host) {
+  int run(int device, uint8_t *d_es) {
     std::lock_guard<std::mutex> slk(g_stage_mu);
     HIP_TRY(hipSetDevice(device));
     for (int i = 0; i < kStageSlots; ++i)
@@ -244,7 +289,7 @@ struct EsUpload {
       if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) r = fail(VTS_E_HIP, "hipEventCreate");
     int64_t k = 0;  // staging copies so far
     for (;;) {
-      std::pair<int64_t, int64_t> item;
+      Item item;
       {
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return !q.empty() || closed; });
@@ -252,15 +297,15 @@ struct EsUpload {
         item = q.back();
         q.pop_back();
       }
-      for (int64_t off = item.first, end = item.first + item.second; off < end && r == VTS_OK; off += kStageBytes, ++k) {
+      for (int64_t off = 0; off < item.n && r == VTS_OK; off += kStageBytes, ++k) {
         const int slot = static_cast<int>(k % kStageSlots);
         if (k >= kStageSlots && hipEventSynchronize(ev[slot]) != hipSuccess) {
           r = fail(VTS_E_HIP, "staging event");
           break;
         }
-        const int64_t len = std::min(kStageBytes, end - off);
-        std::memcpy(g_stage[slot], host + off, static_cast<size_t>(len));
-        if (hipMemcpyAsync(d_es + off, g_stage[slot], static_cast<size_t>(len), hipMemcpyHostToDevice, s) != hipSuccess ||
+        const int64_t len = std::min(kStageBytes, item.n - off);
+        std::memcpy(g_stage[slot], item.src + off, static_cast<size_t>(len));
+        if (hipMemcpyAsync(d_es + item.dst + off, g_stage[slot], static_cast<size_t>(len), hipMemcpyHostToDevice, s) != hipSuccess ||
             hipEventRecord(ev[slot], s) != hipSuccess)
           r = fail(VTS_E_HIP, "elementary-stream upload");
       }
@@ -510,8 +555,9 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   std::vector<uint8_t> intra(c->n_frames, 1), is_ref(c->n_frames, 0);
   HostBytes es;
   std::vector<int64_t> es_off;
-  auto walk = [&](Run &R, int64_t f0, int64_t f1) {
-    const uint8_t *E = es.data();
+  // walk samples [f0, f1), whose bytes lie back to back from src
+  auto walk = [&](Run &R, int64_t f0, int64_t f1, const uint8_t *src) {
+    const uint8_t *E = src - es_off[f0];  // E + es_off[f]: sample f (device ES offsets)
     R.s0 = f0;
     R.s1 = f1;
     R.sl.reserve(static_cast<size_t>(f1 - f0) * 2);
@@ -575,20 +621,41 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(vts::dmalloc(&c->d_es, static_cast<size_t>(c->es_bytes)));
   c->open_lap(4);
+  FileMap fmap;  // before `up`: unmapped only after the upload thread has been joined
   EsUpload up;
   PieceHooks hooks;
   hooks.on_plan = [&](size_t n) {
     runs.resize(n);
-    up.start(c->device, c->d_es, es.data());
+    up.start(c->device, c->d_es);
   };
-  hooks.on_piece = [&](size_t k, int64_t s0, int64_t s1) {
-    const int64_t off = es_off[s0], end = s1 < c->n_frames ? es_off[s1] : es_off[s1 - 1] + t.size[s1 - 1];
-    up.push(off, end - off);
-    if (may_subset) walk(runs[k], s0, s1);
+  hooks.on_piece = [&](size_t k, int64_t s0, int64_t s1, const uint8_t *src) {
+    const int64_t end = s1 < c->n_frames ? es_off[s1] : es_off[s1 - 1] + t.size[s1 - 1];
+    up.push(src, es_off[s0], end - es_off[s0]);
+    if (may_subset) walk(runs[k], s0, s1, src);
   };
-  VTS_TRY(gather_samples(t, mem, mem_size, path, &es, &es_off, &hooks));
-  if (static_cast<int64_t>(es.size()) != c->es_bytes) return fail(VTS_E_FORMAT, "elementary stream size");
-  up.push(c->es_bytes - kPad, kPad);  // the zero padding after the last sample
+  // The subset decoder keeps no host copy of the ES: a file is mapped, the
+  // pieces are walked and uploaded where they lie (the copy into a host
+  // buffer — 7 GB for a 2-h 720p video, its pages faulted in fresh — was
+  // most of the read).  The general decoder's host schedule reads the whole
+  // ES, so it gets the host copy (made from the mapping if the first slices
+  // send an auto stream there after all).
+  if (may_subset && !mem && !std::getenv("VTS_OPEN_COPY")) VTS_TRY(fmap.open(path));
+  const uint8_t *src_mem = fmap.p ? fmap.p : mem;
+  const int64_t src_size = fmap.p ? fmap.n : mem_size;
+  VTS_TRY(gather_samples(t, src_mem, src_size, path, fmap.p ? nullptr : &es, &es_off, &hooks));
+  static const uint8_t kZeroPad[kPad] = {};
+  up.push(kZeroPad, c->es_bytes - kPad, kPad);  // the zero padding after the last sample
+  if (fmap.p && c->params.decoder == 0) {
+    // wants_general reads the first pictures' slice headers: a host copy of those
+    const size_t n3 = std::min<size_t>(t.size.size(), 3);
+    int64_t b3 = 0;
+    for (size_t i = 0; i < n3; ++i) b3 += t.size[i];
+    es.alloc(b3 + kPad);
+    for (size_t i = 0; i < n3; ++i) std::memcpy(es.data() + es_off[i], fmap.p + t.offset[i], t.size[i]);
+    std::memset(es.data() + b3, 0, kPad);
+  } else if (!fmap.p && static_cast<int64_t>(es.size()) != c->es_bytes) {
+    return fail(VTS_E_FORMAT, "elementary stream size");
+  }
   c->open_lap(2);
   c->es_off = es_off;
   c->sample_size = t.size;
@@ -600,6 +667,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   // show features outside the subset kernels (deblocking, several references)
   if (c->params.decoder == 2 || reorder ||
       (c->params.decoder == 0 && wants_general(c, es.data(), es_off, t.size, t.nal_length_size))) {
+    if (fmap.p) VTS_TRY(gather_samples(t, fmap.p, fmap.n, path, &es, &es_off));  // the whole ES on the host after all
     VTS_TRY(build_general(c, es.data(), es_off, t.size, t.nal_length_size, t.sps[0], t.pps[0]));
     c->open_lap(3);
     VTS_TRY(up.join());
