@@ -815,12 +815,15 @@ def e2e_record(paths: list[Path], gpu: int) -> dict:
 # launches share queues in submission order and the runs serialise (4 content
 # sessions: 3.99x one session's step; 16 queues: 2.76x, profiles/r05f_*).
 # The documented deployment setting; set before anything
-# initialises HIP, inherited by the profiler children and the ranks.
+# initialises HIP, inherited by the profiler children and the ranks.  Set,
+# not defaulted: the GPU box exports HIP's default (4) itself, which a
+# setdefault kept (r05n: 4.25x).  32 queues: batch 2.0x but one session's
+# step 311 -> 383 ms (profiles/r05o_batch_queues_after_sessions.json).
 HW_QUEUES = "16"
 
 
 def main() -> None:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", HW_QUEUES)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("VTS_BENCH_HW_QUEUES", HW_QUEUES)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)

@@ -8,6 +8,9 @@
 // failed hipMalloc (then one retry) or vts_empty_cache().
 #include "devmem.h"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -36,6 +39,19 @@ struct Device {
 std::mutex g_mu;
 std::map<int, Device> g_dev;
 
+// VTS_DEVMEM_LOG=1: every fresh hipMalloc and every release of cached
+// segments to HIP on stderr, with its time (measurement)
+bool log_on() {
+  static const bool on = [] {
+    const char *e = std::getenv("VTS_DEVMEM_LOG");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 void free_list_erase(Device &d, size_t n, char *p) {
   auto r = d.free_by_size.equal_range(n);
   for (auto it = r.first; it != r.second; ++it)
@@ -47,6 +63,8 @@ void free_list_erase(Device &d, size_t n, char *p) {
 
 // hand every wholly free segment back to HIP
 void release_free_segments_locked(Device &d) {
+  const auto t0 = std::chrono::steady_clock::now();
+  size_t nseg = 0, bytes = 0;
   for (auto it = d.segments.begin(); it != d.segments.end();) {
     auto r = d.ranges.find(it->first);
     if (r != d.ranges.end() && r->second.free && r->second.n == it->second) {
@@ -54,11 +72,16 @@ void release_free_segments_locked(Device &d) {
       d.cached -= r->second.n;
       d.ranges.erase(r);
       (void)hipFree(it->first);
+      ++nseg;
+      bytes += it->second;
       it = d.segments.erase(it);
     } else {
       ++it;
     }
   }
+  if (log_on())
+    std::fprintf(stderr, "[devmem] released %zu segments, %.2f GB to HIP in %.1f ms (cached %.2f GB, in use %.2f GB)\n",
+                 nseg, bytes / 1e9, ms_since(t0), d.cached / 1e9, d.in_use / 1e9);
 }
 
 // take `want` bytes from the front of free range p (splitting off the rest)
@@ -96,7 +119,11 @@ hipError_t dmalloc_raw(void **p, size_t n) {
     *p = take_locked(d, it->second, want);
     return hipSuccess;
   }
+  const auto t0 = std::chrono::steady_clock::now();
   e = hipMalloc(p, want);
+  if (log_on())
+    std::fprintf(stderr, "[devmem] hipMalloc %.3f GB: %s in %.1f ms (cached %.2f GB, in use %.2f GB)\n", want / 1e9,
+                 e == hipSuccess ? "ok" : "failed", ms_since(t0), d.cached / 1e9, d.in_use / 1e9);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     if (it != d.free_by_size.end()) {  // no fresh memory: carve the large range after all
