@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -1 $O/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
 tail -1 $O/smoke.txt
-timeout -k 10 900 python -u bench.py --profile-dir $O/prof > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+VTS_DEVMEM_LOG=1 timeout -k 10 900 python -u bench.py --profile-dir $O/prof > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
 python -c "
 import json; d=json.load(open('$O/bench.json'))
 print('bench', d['value'], d['roofline']['frac'], d['parity']['all_equal'], d['e2e'].get('value'), d['cpu_baseline']['value'])

@@ -57,34 +57,51 @@ constexpr int64_t kSingleWindowBytes = 48ll << 30;  // up to 48 GiB decoded: one
 constexpr int64_t kMinRingBytes = 1ll << 30;        // else two rings of >= 1 GiB
 constexpr int64_t kPad = 256;
 
-// Streams outlive sessions: a process-wide free list per device, handed out
-// in a fixed role order (decode, score, parse, GOP groups) and taken back in
-// reverse, so successive sessions get the same streams in the same roles and
-// with them the same hardware queues.  Streams created afresh after other
-// sessions had come and gone could land the two GOP groups on one of the
-// process's four hardware queues and serialise them (general decoder
-// reconstruction 218 -> 288 ms, tools/gpu/queue_probe.py); sessions open at
-// the same time still get streams of their own.
+// Streams outlive sessions, as whole sets: a session's six streams (decode,
+// score, parse, three GOP groups) are created one after another — HIP gives
+// each new stream the least-used of the process's hardware queues, so the
+// six land on six different queues — and go back to a process-wide free list
+// per device together, so every later session again gets six streams on six
+// queues.  Single streams pooled one by one came back mixed after many
+// sessions: two of one session's GOP-group / parse streams could share a
+// queue and serialise (general decoder reconstruction 145 -> 239 ms in the
+// bench after eight concurrent sessions on 16 queues; 218 -> 288 ms on 4,
+// tools/gpu/queue_probe.py).  Sessions open at the same time never share one.
 std::mutex g_stream_mu;
-std::map<int, std::vector<hipStream_t>> g_stream_pool;
+std::map<int, std::vector<std::vector<hipStream_t>>> g_stream_sets;
+constexpr int kSessionStreams = 3 + (vts_ctx::kMaxGroups - 1);
 
-int stream_take(int device, hipStream_t *s) {
+int streams_take(vts_ctx *c) {
+  std::vector<hipStream_t> set;
   {
     std::lock_guard<std::mutex> lk(g_stream_mu);
-    auto &v = g_stream_pool[device];
+    auto &v = g_stream_sets[c->device];
     if (!v.empty()) {
-      *s = v.back();
+      set = v.back();
       v.pop_back();
-      return VTS_OK;
+    } else {
+      set.assign(kSessionStreams, nullptr);
+      for (auto &x : set) {
+        if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) {
+          for (auto &y : set)
+            if (y) (void)hipStreamDestroy(y);
+          return fail(VTS_E_HIP, "hipStreamCreate");
+        }
+      }
     }
   }
-  HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+  c->s_dec = set[0];
+  c->s_score = set[1];
+  c->s_parse = set[2];
+  for (int g = 0; g + 1 < vts_ctx::kMaxGroups; ++g) c->s_grp[g] = set[static_cast<size_t>(3 + g)];
   return VTS_OK;
 }
-void stream_give(int device, hipStream_t s) {  // s idle
-  if (!s) return;
+void streams_give(vts_ctx *c) {  // every stream idle
+  if (!c->s_dec) return;
+  std::vector<hipStream_t> set = {c->s_dec, c->s_score, c->s_parse};
+  for (int g = 0; g + 1 < vts_ctx::kMaxGroups; ++g) set.push_back(c->s_grp[g]);
   std::lock_guard<std::mutex> lk(g_stream_mu);
-  g_stream_pool[device].push_back(s);
+  g_stream_sets[c->device].push_back(set);
 }
 
 }  // namespace
@@ -402,13 +419,9 @@ int alloc_general(vts_ctx *c) {
   if (!c->d_hist) HIP_TRY(vts::dmalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
   c->thumb_px = tw;
   if (!c->d_rgb) HIP_TRY(vts::dmalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
-  if (!c->s_dec) VTS_TRY(stream_take(c->device, &c->s_dec));
-  if (!c->s_score) VTS_TRY(stream_take(c->device, &c->s_score));
-  if (!c->s_parse) VTS_TRY(stream_take(c->device, &c->s_parse));
-  for (int g = 0; g + 1 < vts_ctx::kMaxGroups; ++g) {
-    if (!c->s_grp[g]) VTS_TRY(stream_take(c->device, &c->s_grp[g]));
+  if (!c->s_dec) VTS_TRY(streams_take(c));
+  for (int g = 0; g + 1 < vts_ctx::kMaxGroups; ++g)
     if (!c->ev_grp[g]) HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[g], hipEventDisableTiming));
-  }
   for (auto e2 : c->ev)
     if (e2) (void)hipEventDestroy(e2);
   c->ev.assign(c->windows.size() * 6, nullptr);
@@ -987,13 +1000,8 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   HIP_TRY(vts::dmalloc(&c->d_hist, sizeof(uint32_t) * 256 * c->n_frames));
   c->thumb_px = tw;
   HIP_TRY(vts::dmalloc(&c->d_rgb, static_cast<size_t>(3 * tw * c->n_frames + kPad)));
-  VTS_TRY(stream_take(c->device, &c->s_dec));
-  VTS_TRY(stream_take(c->device, &c->s_score));
-  VTS_TRY(stream_take(c->device, &c->s_parse));
-  for (int g = 1; g < c->recon_groups; ++g) {
-    VTS_TRY(stream_take(c->device, &c->s_grp[g - 1]));
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[g - 1], hipEventDisableTiming));
-  }
+  VTS_TRY(streams_take(c));
+  for (int g = 1; g < c->recon_groups; ++g) HIP_TRY(hipEventCreateWithFlags(&c->ev_grp[g - 1], hipEventDisableTiming));
   c->ev.resize(c->windows.size() * 6);
   for (auto &e2 : c->ev) HIP_TRY(hipEventCreate(&e2));
   int64_t nlev = 0;
@@ -1593,14 +1601,11 @@ extern "C" int vts_close(vts_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);
-  for (int g = vts_ctx::kMaxGroups - 2; g >= 0; --g) {  // back to the pool in reverse role order
+  for (int g = vts_ctx::kMaxGroups - 2; g >= 0; --g) {
     if (c->s_grp[g]) (void)hipStreamSynchronize(c->s_grp[g]);
-    stream_give(c->device, c->s_grp[g]);
     if (c->ev_grp[g]) (void)hipEventDestroy(c->ev_grp[g]);
   }
-  stream_give(c->device, c->s_parse);
-  stream_give(c->device, c->s_score);
-  stream_give(c->device, c->s_dec);
+  streams_give(c);  // back to the pool as the set it came as
   delete c;
   return VTS_OK;
 }
