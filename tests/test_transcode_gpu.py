@@ -149,6 +149,27 @@ def test_transcode_twice_and_after_score(tmp_path):
     assert np.array_equal(r0.scores, r1.scores)
 
 
+def test_transcode_to_unwritable_path_then_normal(tmp_path):
+    """a transcode whose output cannot be opened fails (after the
+    encoder's device work was queued) with its streams drained before the
+    buffers go back to the allocator; the next transcode in the same session
+    — whose buffers come from that same cache — writes the same bytes as a
+    fresh session."""
+    _require_gpu()
+    from vtseg import VtsegError
+    src = tmp_path / "in.mp4"
+    scene.synth_write(src, width=320, height=192, n_frames=60, cut_min_s=0.7, cut_max_s=1.5,
+                      gop_max_s=0.5)
+    with scene.VideoScorer(src) as v:
+        ref = v.transcode(tmp_path / "ref.mp4", height=96)
+    with scene.VideoScorer(src) as v:
+        with pytest.raises(VtsegError):
+            v.transcode(tmp_path / "no_such_dir" / "x.mp4", height=96)
+        got = v.transcode(tmp_path / "ok.mp4", height=96)
+    assert got["bytes_written"] == ref["bytes_written"]
+    assert (tmp_path / "ok.mp4").read_bytes() == (tmp_path / "ref.mp4").read_bytes()
+
+
 def test_compress_video_for_upload_gpu(tmp_path):
     """The drop-in method: > max size -> compressed_<name> next to the input,
     a valid H.264 MP4 at 360 lines; a second call reuses it."""

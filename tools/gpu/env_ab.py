@@ -26,7 +26,7 @@ for order in (variants, variants[::-1]):
     for name, env in order:
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        v = scene.VideoScorer(path, device=0)
+        v = scene.VideoScorer(path, device=0, window_frames=int(os.environ.get("AB_WINDOW_FRAMES", "0")))
         for k, x in old.items():
             if x is None:
                 os.environ.pop(k, None)

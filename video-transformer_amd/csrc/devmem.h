@@ -1,19 +1,23 @@
 // devmem.h — the sessions' device memory: a process-wide caching allocator.
 //
 // A session allocates tens of GB (decoded-surface rings, macroblock records,
-// the coefficient arena).  hipMalloc of memory another allocation released
-// waits while the driver clears it (vts_open of the general decoder after a
-// closed session: 4-6 s in the allocation stage, against 7 ms on fresh
-// memory; profiles/r04c_open_stages.json), so released blocks of >= 64 KiB
-// stay mapped in a per-device cache and the next session takes them back.
-// Placement: the smallest free range that holds the request; a range more
-// than twice the request (and 64 MiB over it) is carved only for requests of
-// >= 256 MiB, or when a fresh hipMalloc fails, so small buffers do not pin a
-// large cached segment (a segment goes back to HIP only when wholly free).  A
-// failed hipMalloc empties the device's wholly free segments and tries once
-// more.  Window sizing counts cached bytes as free (vts::dmem_free: the free
-// ranges, which large requests may carve).  vts_empty_cache() hands the
-// cache back.
+// the coefficient arena).  HBM handed back to HIP is cleared by the driver
+// before it is handed out again (~45 GB/s; vts_open of a session after
+// differently shaped ones: seconds in the allocation stage), so nothing goes
+// back between sessions:
+//  - requests of >= 256 MiB are physical 128 MiB chunks (hipMemCreate)
+//    mapped back to back into a fresh virtual range; on release the range is
+//    unmapped and the chunks kept, and any later request maps whichever are
+//    idle — no fragmentation, whatever the sessions' shapes (devmem.cpp);
+//  - smaller blocks of >= 64 KiB stay in a per-device cache of hipMalloc
+//    segments: the smallest free range that holds the request, a range more
+//    than twice the request (and 64 MiB over it) carved only when a fresh
+//    hipMalloc fails; a segment goes back to HIP only when wholly free, and
+//    a failed allocation gives back only as much as it needs, smallest idle
+//    segments / chunks first.
+// Window sizing counts cached bytes as free (vts::dmem_free).
+// vts_empty_cache() hands everything idle back; VTS_DEVMEM_LOG=1 logs every
+// fresh allocation and give-back, VTS_DEVMEM_VMM=0 turns the mapped path off.
 #pragma once
 #include <hip/hip_runtime_api.h>
 

@@ -478,6 +478,16 @@ int submit_general(vts_ctx *c) {
   // picture of a level, which leaves most compute units idle)
   hipStream_t sp = c->s_parse;
   hipStream_t ss = (c->params.n_streams >= 2 && c->windows.size() > 1) ? c->s_score : c->s_dec;
+  // the paced bS launches: on the score stream when scoring is not on it (one
+  // window, or one stream); with several windows scored on s_score, on a
+  // group stream of their own (else window i + 1's bS, and with it its first
+  // level, would queue behind window i's scoring; VTS_BS_STREAM=0:
+  // the score stream regardless)
+  hipStream_t sbs = c->s_score;
+  if (ss == c->s_score && c->general_groups < vts_ctx::kMaxGroups) {
+    const char *e = std::getenv("VTS_BS_STREAM");
+    if (!e || std::atoi(e) != 0) sbs = c->s_grp[vts_ctx::kMaxGroups - 2];
+  }
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
   const size_t nw = c->windows.size();
   for (size_t wi = 0; wi < nw; ++wi) {
@@ -610,7 +620,7 @@ int submit_general(vts_ctx *c) {
       // odd groups' on the parse stream, measured slower — 188 -> 201 ms on the
       // content stream, that stream sharing a hardware queue with a group's,
       // profiles/r04t_bs_paced_split_ab.json)
-      auto sb_of = [&](int) { return c->s_score; };
+      auto sb_of = [&](int) { return sbs; };
       std::vector<size_t> lo(static_cast<size_t>(ng)), hi(static_cast<size_t>(ng));
       size_t jmax = 0;
       for (int g = 0; g < ng; ++g) {
@@ -624,7 +634,7 @@ int submit_general(vts_ctx *c) {
           c->ev_bs.resize(2 * w.lvl_off.size(), nullptr);
           for (size_t k = n0; k < c->ev_bs.size(); ++k) HIP_TRY(hipEventCreateWithFlags(&c->ev_bs[k], hipEventDisableTiming));
         }
-        HIP_TRY(hipStreamWaitEvent(c->s_score, E[1], 0));
+        HIP_TRY(hipStreamWaitEvent(sbs, E[1], 0));
         for (int g = 0; g < ng; ++g) {  // every group's first level
           if (lo[static_cast<size_t>(g)] >= hi[static_cast<size_t>(g)]) continue;
           VTS_TRY(bs_level(lo[static_cast<size_t>(g)], sb_of(g)));
