@@ -1533,39 +1533,61 @@ __device__ __forceinline__ uint32_t u4_at(const uint4 &v, int i) {
 // ap / aq < beta forced false it takes exactly the chroma filter (tC = tC0 +
 // 1, only p0 / q0 change, bS 4: p0' = (2 p1 + p0 + q1 + 2) >> 2), so a wave
 // whose lanes mix luma and chroma runs one filter, not both
-__device__ __forceinline__ void filt_w(int (&s)[8], int bS, uint32_t w, bool chroma) {
+// The p and q sides of the edge sit in the two 16-bit halves of one register
+// (p low, q high): the standard's p-side and q-side formulas mirror each
+// other, so one packed instruction computes both (v_pk_* on gfx950), with the
+// half-swapped registers (q, p) for the mirrored terms (round 5: content /
+// noise reconstruction -3 % / -2 %, 103 -> 85 VGPRs, bit-exact;
+// profiles/r05u_deblock_packed_filter_ab.json).
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 pk_swap(u16x2 v) { return u16x2{v.y, v.x}; }
+__device__ __forceinline__ u16x2 pk_pair(int p, int q) {
+  return u16x2{static_cast<uint16_t>(p), static_cast<uint16_t>(q)};
+}
+__device__ __forceinline__ i16x2 pk_abs(i16x2 v) { return __builtin_elementwise_max(v, -v); }
+__device__ __forceinline__ void filt_pk(int (&s)[8], int bS, uint32_t w, bool chroma) {
   const int alpha = w & 255, beta = (w >> 8) & 255;
-  const int p0 = s[3], p1 = s[2], q0 = s[4], q1 = s[5];
-  if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-  const int p2 = s[1], q2 = s[6];
-  const bool apb = !chroma && abs(p2 - p0) < beta, aqb = !chroma && abs(q2 - q0) < beta;
+  const u16x2 A = pk_pair(s[3], s[4]), B = pk_pair(s[2], s[5]), C = pk_pair(s[1], s[6]), D = pk_pair(s[0], s[7]);
+  const u16x2 As = pk_swap(A), Bs = pk_swap(B);
+  const i16x2 d1 = pk_abs(__builtin_bit_cast(i16x2, B) - __builtin_bit_cast(i16x2, A));
+  const int d0 = abs(s[3] - s[4]);
+  if (!(d0 < alpha && d1.x < beta && d1.y < beta)) return;
+  const i16x2 d2 = pk_abs(__builtin_bit_cast(i16x2, C) - __builtin_bit_cast(i16x2, A));
+  const bool apb = !chroma && d2.x < beta, aqb = !chroma && d2.y < beta;
+  u16x2 nA, nB = B, nC = C;
   if (bS < 4) {
     const int tc0 = (w >> (11 + 5 * bS)) & 31;
     const int tc = tc0 + (chroma ? 1 : static_cast<int>(apb) + static_cast<int>(aqb));
-    const int delta = min(max((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc), tc);
-    s[3] = c255(p0 + delta);
-    s[4] = c255(q0 - delta);
-    if (apb) s[2] = p1 + min(max((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0), tc0);
-    if (aqb) s[5] = q1 + min(max((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0), tc0);
-    return;
-  }
-  const int p3 = s[0], q3 = s[7];
-  const bool small = abs(p0 - q0) < ((alpha >> 2) + 2);
-  if (apb && small) {
-    s[3] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
-    s[2] = (p2 + p1 + p0 + q0 + 2) >> 2;
-    s[1] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+    const int delta = min(max((((s[4] - s[3]) << 2) + (s[2] - s[5]) + 4) >> 3, -tc), tc);
+    const i16x2 a2 = __builtin_bit_cast(i16x2, A) + i16x2{static_cast<int16_t>(delta), static_cast<int16_t>(-delta)};
+    nA = __builtin_bit_cast(u16x2, __builtin_elementwise_min(__builtin_elementwise_max(a2, i16x2{0, 0}), i16x2{255, 255}));
+    const u16x2 avg = (A + As + u16x2{1, 1}) >> 1;  // (p0 + q0 + 1) >> 1 in both halves
+    i16x2 h = (__builtin_bit_cast(i16x2, C + avg) - __builtin_bit_cast(i16x2, B << 1)) >> 1;
+    const int16_t t0 = static_cast<int16_t>(tc0);
+    h = __builtin_elementwise_min(__builtin_elementwise_max(h, i16x2{static_cast<int16_t>(-t0), static_cast<int16_t>(-t0)}),
+                                  i16x2{t0, t0});
+    const u16x2 b2 = B + __builtin_bit_cast(u16x2, h);
+    nB = u16x2{apb ? b2.x : B.x, aqb ? b2.y : B.y};
   } else {
-    s[3] = (2 * p1 + p0 + q1 + 2) >> 2;
+    const bool small = d0 < ((alpha >> 2) + 2);
+    const u16x2 s0 = (C + (B << 1) + (A << 1) + (As << 1) + Bs + u16x2{4, 4}) >> 3;
+    const u16x2 s1 = (C + B + A + As + u16x2{2, 2}) >> 2;
+    const u16x2 s2 = ((D << 1) + C + (C << 1) + B + A + As + u16x2{4, 4}) >> 3;
+    const u16x2 w0 = ((B << 1) + A + Bs + u16x2{2, 2}) >> 2;
+    const bool sp = apb && small, sq = aqb && small;
+    nA = u16x2{sp ? s0.x : w0.x, sq ? s0.y : w0.y};
+    nB = u16x2{sp ? s1.x : B.x, sq ? s1.y : B.y};
+    nC = u16x2{sp ? s2.x : C.x, sq ? s2.y : C.y};
   }
-  if (aqb && small) {
-    s[4] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
-    s[5] = (p0 + q0 + q1 + q2 + 2) >> 2;
-    s[6] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-  } else {
-    s[4] = (2 * q1 + q0 + p1 + 2) >> 2;
-  }
+  s[3] = nA.x;
+  s[4] = nA.y;
+  s[2] = nB.x;
+  s[5] = nB.y;
+  s[1] = nC.x;
+  s[6] = nC.y;
 }
+
 // vertical pass: a chroma lane's interleaved row (Cb Cr pairs from x = -2)
 // reordered so that slot s = (edge 2 (s >> 1), plane s & 1) has p1 p0 q0 q1
 // at u[4 s + 2 .. 4 s + 5]: u[j] = r[kDbkCPerm[j]], r[i] = u[kDbkCInv[i]]
@@ -1759,7 +1781,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           int s8[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
-          filt_w(s8, bS, u4_at(pv, e), !kLuma);
+          filt_pk(s8, bS, u4_at(pv, e), !kLuma);
 #pragma unroll
           for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
         }
@@ -1795,7 +1817,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           int s8[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) s8[i] = u[4 * e + i];
-          filt_w(s8, bS, u4_at(ph, kLuma ? e : e + pl), !kLuma);
+          filt_pk(s8, bS, u4_at(ph, kLuma ? e : e + pl), !kLuma);
 #pragma unroll
           for (int i = 0; i < 8; ++i) u[4 * e + i] = s8[i];
         }
