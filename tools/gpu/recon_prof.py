@@ -1,8 +1,8 @@
 """Reconstruction section times of a VTS_EXP_RPROF build (tools/exp/lib_rprof.so
 copied over vtseg/libvtseg.so): one decode of the given video, then the
-s_memtime totals per section of h264_deblock_full and h264_intra_full, summed
-over every wave, and per step (deblock: one macroblock iteration of a wave;
-intra: one level of a workgroup's waves)."""
+s_memtime totals per section of h264_deblock_plane (dp_plane) and
+h264_intra_v2, summed over every wave, and per step (deblock: one macroblock
+step of a wave's row groups; intra: one level of a workgroup's waves)."""
 import ctypes as C
 import json
 import sys
@@ -11,7 +11,7 @@ sys.path.insert(0, "video-transformer_amd")
 import torch  # noqa: F401  (libvtseg binds to torch's HIP runtime)
 from vtseg import _lib, scene
 
-DBK = ["wait_row_above", "vertical_edges", "horizontal_edges", "write_back", "tail", "-", "-", "iterations"]
+DBK = ["wait_rows", "ring_in_vertical", "horizontal", "write_back", "loop_head_loads", "-", "still_steps", "steps"]
 INTRA = ["setup_bucket_sort", "level_tail", "level_barrier", "mb_loads", "mb_luma", "mb_chroma", "wave_levels", "mbs"]
 v = scene.VideoScorer(sys.argv[1], device=0, decoder="general")
 v.run()

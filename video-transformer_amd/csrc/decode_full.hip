@@ -1712,6 +1712,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
   const int row = kLuma ? l : min(l, 7);
   Tile &t = tiles[wave * 4 + grp];
   constexpr int vq = kLuma ? 2 : 4, hq = kLuma ? 3 : 5;
+  RPROF_DECL;
   for (int p = wave; 4 * p < mbh; p += kDbkWaves) {
     const int y = 4 * p + grp;
     const bool row_ok = y < mbh;
@@ -1747,6 +1748,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
       // a wave's first row waits for the previous wave's last row; its last
       // row waits until it may overwrite ring column x (the next wave's first
       // row read column x - kDpRingCols)
+      RPROF(4);  // loop head + next macroblock's loads issued
       if (act) {
         const int need_up = (grp == 0 && y > 0) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
         const int need_dn = (grp == 3 && y + 1 < mbh) ? x - kDpRingCols + 1 : -(1 << 30);
@@ -1756,7 +1758,10 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           __builtin_amdgcn_s_sleep(1);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      RPROF(0);  // waits on the rows above / below
       const bool still = (bsw.x | bsw.y | bsw.z | bsw.w) == 0u;
+      RPROF_COUNT(7, 1);
+      RPROF_COUNT(6, still ? 1 : 0);
       constexpr int kAbove = kLuma ? 4 : 2;  // rows above from the ring
       auto load_above = [&]() {
         if (act && l < kAbove && y > 0) {
@@ -1793,6 +1798,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
       }
       lane_sync();
+      RPROF(1);  // ring lines in, vertical edges (and this step's loads' latency)
       // ---- horizontal edges: lane = sample column (chroma: interleaved byte column)
       if (act && !still) {
         const int pl = l & 1, seg = l >> 2;
@@ -1835,6 +1841,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
         }
       }
       lane_sync();
+      RPROF(2);  // horizontal edges
       // ---- write back: this macroblock's rows shifted 4 bytes left except the
       // ones the row below finishes (luma 13..15, chroma 7), the ring lines for
       // the row below, the rows above that this macroblock's top edge finished
@@ -1894,6 +1901,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           *reinterpret_cast<uint4 *>(at(o + static_cast<uint32_t>(x * 16))) = v;
         }
       }
+      RPROF(3);  // write back, ring lines out, rows above
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       if (act && l == 0) {
@@ -1901,6 +1909,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
       }
     }
   }
+  RPROF_FLUSH(0);
 }
 // grid: 2 x pictures of the level (even blocks luma, odd chroma)
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs a) {
