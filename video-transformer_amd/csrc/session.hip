@@ -243,50 +243,91 @@ int gather_samples(const Mp4VideoTrack &t, const uint8_t *mem, int64_t mem_size,
   return VTS_OK;
 }
 
-// Elementary-stream upload: host bytes -> a ring of pinned staging buffers
-// (process-wide, allocated once) -> hipMemcpyAsync into HBM, so the copy into
-// a staging slot overlaps the DMA of the previous one (a pageable hipMemcpy
-// stages internally, one small chunk at a time, synchronously).  Runs on its
-// own thread and takes byte ranges as they become ready: the reading threads
-// push each piece as it lands, so the upload runs beside the read and the
-// schedule instead of after the read.
-constexpr int64_t kStageBytes = 16ll << 20;
-constexpr int kStageSlots = 4;
+// Elementary-stream upload: host bytes -> pinned staging slots (a
+// process-wide pool, allocated once) -> hipMemcpyAsync into HBM (a pageable
+// hipMemcpy stages internally, one small chunk at a time, synchronously).
+// The threads that push byte ranges copy them into free slots themselves —
+// the reading threads, each as its piece lands, so the host copies run eight
+// at a time beside the read — and one thread issues the DMA of every filled
+// slot and frees slots as their copies complete.  The pool belongs to one
+// upload at a time.
+constexpr int64_t kStageBytes = 8ll << 20;
+constexpr int kStageSlots = 24;
 std::mutex g_stage_mu;
-uint8_t *g_stage[kStageSlots] = {nullptr, nullptr, nullptr, nullptr};
+uint8_t *g_stage[kStageSlots] = {};
 
 struct EsUpload {
   std::thread th;
   std::mutex mu;
-  std::condition_variable cv;
-  struct Item {
-    const uint8_t *src;
+  std::condition_variable cv_dma, cv_slot;
+  std::vector<int> free_slots;
+  struct Filled {
+    int slot;
     int64_t dst, n;
   };
-  std::vector<Item> q;  // host bytes ready, and where they go in the device ES
-  bool closed = false;
+  std::vector<Filled> filled;  // copied into staging, DMA not yet issued
+  int pushers = 0;             // push() calls in progress
+  bool closed = false, started = false;
   int rc = VTS_OK;
   std::string msg;
-  void start(int device, uint8_t *d_es) {
+  std::unique_lock<std::mutex> pool;  // g_stage_mu while this upload runs
+
+  int start(int device, uint8_t *d_es) {
+    pool = std::unique_lock<std::mutex>(g_stage_mu);
+    HIP_TRY(hipSetDevice(device));
+    for (int i = 0; i < kStageSlots; ++i) {
+      if (!g_stage[i]) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&g_stage[i]), kStageBytes, hipHostMallocDefault));
+      free_slots.push_back(i);
+    }
+    started = true;
     th = std::thread([this, device, d_es]() {
       rc = run(device, d_es);
       if (rc != VTS_OK) msg = last_error();
     });
+    return VTS_OK;
   }
+  // copy [src, src + n) to device offset dst (on the caller's thread, into
+  // staging slots as they come free)
   void push(const uint8_t *src, int64_t dst, int64_t n) {
+    if (!started) return;
     {
       std::lock_guard<std::mutex> lk(mu);
-      q.push_back(Item{src, dst, n});
+      ++pushers;
     }
-    cv.notify_one();
+    for (int64_t off = 0; off < n; off += kStageBytes) {
+      int slot;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_slot.wait(lk, [&] { return !free_slots.empty() || rc != VTS_OK; });
+        if (rc != VTS_OK) break;
+        slot = free_slots.back();
+        free_slots.pop_back();
+      }
+      const int64_t len = std::min(kStageBytes, n - off);
+      std::memcpy(g_stage[slot], src + off, static_cast<size_t>(len));
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        filled.push_back(Filled{slot, dst + off, len});
+      }
+      cv_dma.notify_one();
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      --pushers;
+    }
+    cv_dma.notify_one();
   }
   int join() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      closed = true;
+    if (started) {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        closed = true;
+      }
+      cv_dma.notify_one();
+      if (th.joinable()) th.join();
+      started = false;
+      if (pool.owns_lock()) pool.unlock();
     }
-    cv.notify_one();
-    if (th.joinable()) th.join();
     if (rc != VTS_OK) return fail(rc, "%s", msg.c_str());
     return VTS_OK;
   }
@@ -294,43 +335,65 @@ struct EsUpload {
 
  private:
   int run(int device, uint8_t *d_es) {
-    std::lock_guard<std::mutex> slk(g_stage_mu);
-    HIP_TRY(hipSetDevice(device));
-    for (int i = 0; i < kStageSlots; ++i)
-      if (!g_stage[i]) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&g_stage[i]), kStageBytes, hipHostMallocDefault));
+    if (hipSetDevice(device) != hipSuccess) return fail(VTS_E_HIP, "hipSetDevice");
     hipStream_t s = nullptr;
-    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return fail(VTS_E_HIP, "hipStreamCreate");
     hipEvent_t ev[kStageSlots] = {};
     int r = VTS_OK;
     for (int i = 0; i < kStageSlots && r == VTS_OK; ++i)
       if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) r = fail(VTS_E_HIP, "hipEventCreate");
-    int64_t k = 0;  // staging copies so far
+    std::vector<int> inflight;  // slots whose DMA was issued, oldest first
+    auto retire_oldest = [&]() {
+      const int slot = inflight.front();
+      inflight.erase(inflight.begin());
+      if (hipEventSynchronize(ev[slot]) != hipSuccess && r == VTS_OK) r = fail(VTS_E_HIP, "staging event");
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        free_slots.push_back(slot);
+      }
+      cv_slot.notify_all();
+    };
     for (;;) {
-      Item item;
+      std::vector<Filled> work;
+      bool done = false;
       {
         std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return !q.empty() || closed; });
-        if (q.empty()) break;
-        item = q.back();
-        q.pop_back();
+        // wake for filled slots, for the end, or (with copies in flight) to
+        // hand slots back to waiting pushers
+        cv_dma.wait_for(lk, std::chrono::microseconds(200), [&] {
+          return !filled.empty() || (closed && pushers == 0) || (!inflight.empty() && free_slots.empty());
+        });
+        work.swap(filled);
+        done = closed && pushers == 0 && work.empty();
+        if (r != VTS_OK) rc = r;
       }
-      for (int64_t off = 0; off < item.n && r == VTS_OK; off += kStageBytes, ++k) {
-        const int slot = static_cast<int>(k % kStageSlots);
-        if (k >= kStageSlots && hipEventSynchronize(ev[slot]) != hipSuccess) {
-          r = fail(VTS_E_HIP, "staging event");
-          break;
-        }
-        const int64_t len = std::min(kStageBytes, item.n - off);
-        std::memcpy(g_stage[slot], item.src + off, static_cast<size_t>(len));
-        if (hipMemcpyAsync(d_es + item.dst + off, g_stage[slot], static_cast<size_t>(len), hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipEventRecord(ev[slot], s) != hipSuccess)
+      for (const Filled &f : work) {
+        if (r == VTS_OK && (hipMemcpyAsync(d_es + f.dst, g_stage[f.slot], static_cast<size_t>(f.n), hipMemcpyHostToDevice, s) != hipSuccess ||
+                            hipEventRecord(ev[f.slot], s) != hipSuccess))
           r = fail(VTS_E_HIP, "elementary-stream upload");
+        inflight.push_back(f.slot);
       }
+      // keep slots coming back: retire the copies that are done, and the
+      // oldest when every slot is taken
+      while (!inflight.empty() && hipEventQuery(ev[inflight.front()]) == hipSuccess) retire_oldest();
+      bool starved;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        starved = free_slots.empty();
+      }
+      if (starved && !inflight.empty()) retire_oldest();
+      if (done) break;
     }
+    while (!inflight.empty()) retire_oldest();
     if (hipStreamSynchronize(s) != hipSuccess && r == VTS_OK) r = fail(VTS_E_HIP, "elementary-stream upload");
-    for (auto e : ev)
-      if (e) (void)hipEventDestroy(e);
+    for (auto x : ev)
+      if (x) (void)hipEventDestroy(x);
     (void)hipStreamDestroy(s);
+    if (r != VTS_OK) {
+      std::lock_guard<std::mutex> lk(mu);
+      rc = r;
+      cv_slot.notify_all();
+    }
     return r;
   }
 };
@@ -637,9 +700,10 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   FileMap fmap;  // before `up`: unmapped only after the upload thread has been joined
   EsUpload up;
   PieceHooks hooks;
+  int up_rc = VTS_OK;
   hooks.on_plan = [&](size_t n) {
     runs.resize(n);
-    up.start(c->device, c->d_es);
+    up_rc = up.start(c->device, c->d_es);
   };
   hooks.on_piece = [&](size_t k, int64_t s0, int64_t s1, const uint8_t *src) {
     const int64_t end = s1 < c->n_frames ? es_off[s1] : es_off[s1 - 1] + t.size[s1 - 1];
@@ -656,6 +720,7 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   const uint8_t *src_mem = fmap.p ? fmap.p : mem;
   const int64_t src_size = fmap.p ? fmap.n : mem_size;
   VTS_TRY(gather_samples(t, src_mem, src_size, path, fmap.p ? nullptr : &es, &es_off, &hooks));
+  VTS_TRY(up_rc);
   static const uint8_t kZeroPad[kPad] = {};
   up.push(kZeroPad, c->es_bytes - kPad, kPad);  // the zero padding after the last sample
   if (fmap.p && c->params.decoder == 0) {
