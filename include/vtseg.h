@@ -249,9 +249,12 @@ typedef struct vts_params {
                               n >= 2 = up to n levels per launch with the
                               levels between in LDS */
   int32_t keep_frames;     /* level-blocked launches keep only each block's
-                              last frame in HBM (the next block's reference);
-                              1 = store every decoded frame (vts_get_frame_nv12
-                              of any frame; the transcoder sets it itself)  */
+                              last frame in HBM (the next block's reference),
+                              and the general decoder recycles a picture's
+                              surface once it is scored and no longer
+                              referenced; 1 = store every decoded frame
+                              (vts_get_frame_nv12 of any frame; the
+                              transcoder sets it itself)                     */
   int32_t decoder;         /* 0 auto: the I_PCM / integer-motion subset kernels
                               when the stream's headers allow, else (or when
                               the device parser meets syntax outside the
@@ -326,8 +329,9 @@ int vts_open_timings(const vts_ctx *ctx, double *ms, int32_t cap);
 /* Decode schedule facts: what = 0 reconstruct launches per run, 1 windows,
  * 2 slices, 3 ring frames, 4 fused scoring (1/0), 5 / 6 level-blocked
  * launches / chains, 7 chain slots, 8 general decoder (1/0), 9 runs repeated
- * with the bound's CABAC coefficient arena, 10 coefficient blocks per ring;
- * < 0 on error. */
+ * with the bound's CABAC coefficient arena, 10 coefficient blocks per ring,
+ * 11 decoded-picture surfaces per ring when the general decoder recycles them
+ * (0: one per window frame); < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);  /* 8: general decoder in use (1/0) */
 int vts_close(vts_ctx *ctx);
 

@@ -77,7 +77,7 @@ def test_general_decoder_windows_and_rings(tmp_path):
                       gop_max_s=0.5, coding="full", seed=5)
     frames, _ = oracle.decode_full(path)
     ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 320, 240, 320, 240, 4)
-    with scene.VideoScorer(path, window_frames=30, n_streams=2) as v:
+    with scene.VideoScorer(path, window_frames=30, n_streams=2, keep_frames=True) as v:
         assert v.general() and v.windows() >= 4
         res = v.score()
         assert np.array_equal(res.hist, ref["hist"])
@@ -198,7 +198,7 @@ def test_b_pictures_windows_and_rings(tmp_path):
                       weighted="explicit", chunks=4, cut_min_s=0.5, cut_max_s=1.5, gop_max_s=0.6, seed=9)
     frames, _ = oracle.decode_full(path)
     ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 160, 96, 160, 96, 4)
-    with scene.VideoScorer(path, window_frames=30, n_streams=2) as v:
+    with scene.VideoScorer(path, window_frames=30, n_streams=2, keep_frames=True) as v:
         assert v.general() and v.windows() >= 3
         res = v.score()
         assert np.array_equal(res.hist, ref["hist"])
@@ -307,6 +307,46 @@ def test_per_picture_scheduler_equals_the_oracle(tmp_path, monkeypatch, bframes)
                 assert np.array_equal(res.hist, ref["hist"])
                 assert np.array_equal(res.sad, ref["sad"])
                 assert np.array_equal(res.scores, ref["score"])
+
+
+@pytest.mark.parametrize("groups", [1, 2])
+def test_recycled_surfaces_equal_the_oracle(tmp_path, monkeypatch, groups):
+    """Without keep_frames the general decoder recycles decoded-picture
+    surfaces: a per-GOP-group liveness plan maps window slots to surfaces,
+    each level launch is thumbnailed on a side stream and the window's SADs
+    come from the thumbnail ring.  Histograms, SADs, scores and RGB
+    thumbnails equal the oracle in one window and in several windows on two
+    rings, on a second run too; the session holds fewer surfaces than window
+    frames and refuses to hand a frame back."""
+    _require_gpu()
+    monkeypatch.setenv("VTS_GENERAL_GROUPS", str(groups))
+    n = 240
+    path = tmp_path / "pool.mp4"
+    scene.synth_write(path, width=320, height=240, n_frames=n, coding="full", bframes=True, weighted="implicit",
+                      cabac=True, transform_8x8=True, cut_min_s=0.5, cut_max_s=1.5, gop_max_s=0.5, seed=41)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 320, 240, 320, 240, 4)
+    for wf in (0, 80):
+        with scene.VideoScorer(path, window_frames=wf, n_streams=2) as v:
+            assert v.general()
+            surfs = v._lib.vts_schedule_info(v._ctx, 11)
+            ring = v._lib.vts_schedule_info(v._ctx, 3)
+            assert 0 < surfs < ring, (surfs, ring)
+            for _ in range(2):
+                res = v.score()
+                assert np.array_equal(res.hist, ref["hist"])
+                assert np.array_equal(res.sad, ref["sad"])
+                assert np.array_equal(res.scores, ref["score"])
+            rgb = np.stack([v.thumbnail_rgb(i, 4) for i in range(n)]).reshape(-1)
+            assert np.array_equal(rgb, ref["rgb"])
+            with pytest.raises(VtsegError, match="not kept"):
+                v.frame_nv12(n - 1)
+    monkeypatch.setenv("VTS_SURF_POOL", "0")  # the knob: one surface per window slot again
+    with scene.VideoScorer(path, window_frames=80, n_streams=2) as v:
+        assert v._lib.vts_schedule_info(v._ctx, 11) == 0
+        res = v.score()
+        assert np.array_equal(res.scores, ref["score"])
+        assert np.array_equal(v.frame_nv12(n - 1).reshape(frames[-1].shape), frames[-1])
 
 
 @pytest.mark.parametrize("groups", [1, 2])

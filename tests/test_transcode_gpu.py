@@ -86,7 +86,7 @@ def test_transcode_bytes_match_oracle(tmp_path, name, sk, tk):
     # the device decoder reads it back to the encoder's reconstruction
     sw, sh, ch = ref["width"], ref["height"], ref["coded_height"]
     rec = ref["recon"]
-    with scene.VideoScorer(out) as d:
+    with scene.VideoScorer(out, keep_frames=True) as d:
         d.score()
         last = d.frame_nv12(d.n_frames - 1).reshape(sh * 3 // 2, sw)
     want = np.concatenate([rec[-1, :sh, :sw], rec[-1, ch:ch + sh // 2, :sw]])
@@ -269,7 +269,7 @@ def test_transcode_of_general_decoder_inputs(tmp_path, name, sk, mode):
     assert m["dts"] == [p - info["pts"][0] for p in info["pts"]] or m["dts"] == list(info["pts"])
     sw, sh, ch = ref["width"], ref["height"], ref["coded_height"]
     rec = ref["recon"]
-    with scene.VideoScorer(out) as d:
+    with scene.VideoScorer(out, keep_frames=True) as d:
         d.score()
         last = d.frame_nv12(d.n_frames - 1).reshape(sh * 3 // 2, sw)
     want = np.concatenate([rec[-1, :sh, :sw], rec[-1, ch:ch + sh // 2, :sw]])

@@ -77,6 +77,24 @@ struct ThumbSadArgs {
   float *score;
 };
 
+// Thumbnails of one list of pictures (general decoder with recycled surfaces):
+// thumbnail luma per window slot, RGB and histogram per frame.
+struct PicThumbArgs {
+  const uint8_t *surf;     // surface pool
+  int64_t frame_stride;
+  const int32_t *surf_of;  // window slot -> surface (null: the slot)
+  const int4 *pics;        // .x = window slot
+  int32_t n_pics;
+  int32_t w, h;            // thumbnail size
+  int32_t pitch, uv_row_offset;
+  int32_t chunks_per_row;  // w / G (G = 16 / k bytes, 48 / 6 for k = 6)
+  int32_t n_chunks;        // chunks_per_row * h
+  int64_t f0;              // frame of window slot 0
+  uint8_t *thumb;          // [slot][h][w]
+  uint8_t *rgb;            // [frame][h][w][3] (may be null)
+  uint32_t *hist;          // [frame][256], zero before (bands add into it; may be null)
+};
+
 int parse_launch(const ParseArgs &a, hipStream_t s);
 int fused_launch(const FusedArgs &a, int k, int n_frames, hipStream_t s);
 int thumb_sad_launch(const ThumbSadArgs &t, hipStream_t s);
@@ -91,6 +109,7 @@ int tb_max_tasks(int mb_width, int mb_height, int L);
 // hist[0 .. 256 n) = 0, sad[0 .. n) = 0 (hist 16-byte aligned)
 int clear_accum_launch(uint32_t *hist, uint64_t *sad, int64_t n_frames, hipStream_t s);
 int score_launch(const vts_score_desc *d, hipStream_t stream);
+int thumb_pics_launch(const PicThumbArgs &a, int k, hipStream_t s);
 int64_t score_workspace_bytes(int32_t width, int32_t height, int32_t k, int64_t n_frames);
 
 }  // namespace vts

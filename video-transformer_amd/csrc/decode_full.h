@@ -75,6 +75,7 @@ struct FullReconArgs {
   const int16_t *arena;
   const FullSlice *slices;   // the window's slices (MbRec.slice indexes them)
   uint8_t *surf;             // ring of NV12 pictures
+  const int32_t *surf_of;    // window slot -> surface index in surf (null: the slot; recycled surfaces)
   int64_t frame_stride;
   int64_t uv_off;            // UV plane offset in a picture (pitch * coded height)
   int32_t pitch;

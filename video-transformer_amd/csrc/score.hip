@@ -26,9 +26,11 @@
 //     run's tail thumbnail.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "common.h"
+#include "decode.h"
 #include "pixel.h"
 
 namespace vts {
@@ -73,6 +75,95 @@ __device__ __forceinline__ void load_row(const uint8_t *p, uint32_t *w) {
     w[4 * i + 1] = v.y;
     w[4 * i + 2] = v.z;
     w[4 * i + 3] = v.w;
+  }
+}
+
+// One chunk of a thumbnail (G pixels of thumbnail row ty, from byte column
+// col): luma box means yq and packed RGB (r | g << 8 | b << 16), each pixel
+// counted into the LDS histogram as it is made; thumb_pics' form of
+// score_runs' inner loop (kept inline there: sharing this function cost
+// score_runs<6> 36 VGPRs and spills)
+template <int K>
+__device__ __forceinline__ void thumb_chunk(const uint8_t *yplane, const uint8_t *uvplane, int pitch, int ty,
+                                            int64_t col, uint32_t *lds_hist, uint32_t (&yq)[Geo<K>::kG],
+                                            uint32_t (&rgb24)[Geo<K>::kG]) {
+  using G = Geo<K>;
+  // --- luma box sums: G pixels, K rows
+  uint32_t ys[G::kG];
+#pragma unroll
+  for (int p = 0; p < G::kG; ++p) ys[p] = 0;
+#pragma unroll
+  for (int r = 0; r < K; ++r) {
+    uint32_t w[G::kWords];
+    load_row<G::kWords>(yplane + static_cast<int64_t>(ty * K + r) * pitch + col, w);
+#pragma unroll
+    for (int p = 0; p < G::kG; ++p) {
+      if constexpr (K == 6) {
+        // compile-time byte ranges [6p, 6p+6)
+        switch (p) {
+          case 0: ys[0] = byte_sum<0, 6>(w, ys[0]); break;
+          case 1: ys[1] = byte_sum<6, 12>(w, ys[1]); break;
+          case 2: ys[2] = byte_sum<12, 18>(w, ys[2]); break;
+          case 3: ys[3] = byte_sum<18, 24>(w, ys[3]); break;
+          case 4: ys[4] = byte_sum<24, 30>(w, ys[4]); break;
+          case 5: ys[5] = byte_sum<30, 36>(w, ys[5]); break;
+          case 6: ys[6] = byte_sum<36, 42>(w, ys[6]); break;
+          default: ys[7] = byte_sum<42, 48>(w, ys[7]); break;
+        }
+      } else if constexpr (K == 2) {
+        ys[p] = sad_u8(w[p / 2] & ((p & 1) ? 0xffff0000u : 0x0000ffffu), 0u, ys[p]);
+      } else if constexpr (K == 4) {
+        ys[p] = sad_u8(w[p], 0u, ys[p]);
+      } else {  // K == 8
+        ys[p] = sad_u8(w[2 * p + 1], 0u, sad_u8(w[2 * p], 0u, ys[p]));
+      }
+    }
+  }
+  // --- chroma box sums: interleaved UV, K/2 rows, same byte columns
+  uint32_t us[G::kG], vs[G::kG];
+#pragma unroll
+  for (int p = 0; p < G::kG; ++p) us[p] = vs[p] = 0;
+#pragma unroll
+  for (int r = 0; r < G::kH; ++r) {
+    uint32_t w[G::kWords];
+    load_row<G::kWords>(uvplane + static_cast<int64_t>(ty * G::kH + r) * pitch + col, w);
+#pragma unroll
+    for (int p = 0; p < G::kG; ++p) {
+      if constexpr (K == 6) {
+        switch (p) {
+          case 0: us[0] = byte_sum<0, 6, 2>(w, us[0]); vs[0] = byte_sum<1, 6, 2>(w, vs[0]); break;
+          case 1: us[1] = byte_sum<6, 12, 2>(w, us[1]); vs[1] = byte_sum<7, 12, 2>(w, vs[1]); break;
+          case 2: us[2] = byte_sum<12, 18, 2>(w, us[2]); vs[2] = byte_sum<13, 18, 2>(w, vs[2]); break;
+          case 3: us[3] = byte_sum<18, 24, 2>(w, us[3]); vs[3] = byte_sum<19, 24, 2>(w, vs[3]); break;
+          case 4: us[4] = byte_sum<24, 30, 2>(w, us[4]); vs[4] = byte_sum<25, 30, 2>(w, vs[4]); break;
+          case 5: us[5] = byte_sum<30, 36, 2>(w, us[5]); vs[5] = byte_sum<31, 36, 2>(w, vs[5]); break;
+          case 6: us[6] = byte_sum<36, 42, 2>(w, us[6]); vs[6] = byte_sum<37, 42, 2>(w, vs[6]); break;
+          default: us[7] = byte_sum<42, 48, 2>(w, us[7]); vs[7] = byte_sum<43, 48, 2>(w, vs[7]); break;
+        }
+      } else if constexpr (K == 2) {
+        // one UV pair per thumbnail px: bytes 2p, 2p+1
+        const uint32_t word = w[p / 2] >> ((p & 1) * 16);
+        us[p] += word & 0xffu;
+        vs[p] += (word >> 8) & 0xffu;
+      } else if constexpr (K == 4) {
+        us[p] = sad_u8(w[p] & 0x00ff00ffu, 0u, us[p]);
+        vs[p] = sad_u8((w[p] >> 8) & 0x00ff00ffu, 0u, vs[p]);
+      } else {  // K == 8: 4 UV pairs = 8 bytes = 2 words
+        us[p] = sad_u8(w[2 * p + 1] & 0x00ff00ffu, 0u, sad_u8(w[2 * p] & 0x00ff00ffu, 0u, us[p]));
+        vs[p] = sad_u8((w[2 * p + 1] >> 8) & 0x00ff00ffu, 0u,
+                       sad_u8((w[2 * p] >> 8) & 0x00ff00ffu, 0u, vs[p]));
+      }
+    }
+  }
+  // --- thumbnail pixels: round, convert, histogram
+#pragma unroll
+  for (int p = 0; p < G::kG; ++p) {
+    const uint32_t y = (ys[p] + G::kYDiv / 2) / G::kYDiv;
+    const uint32_t u = (us[p] + G::kCDiv / 2) / G::kCDiv;
+    const uint32_t v = (vs[p] + G::kCDiv / 2) / G::kCDiv;
+    yq[p] = y;
+    rgb24[p] = bt709_rgb24(y, u, v);
+    atomicAdd(&lds_hist[y], 1u);
   }
 }
 
@@ -299,6 +390,49 @@ __global__ void __launch_bounds__(256) score_seams(RunArgs a) {
   }
 }
 
+// Thumbnails of a list of pictures (one reconstruction level of the general
+// decoder, so a surface can be reused once its level is thumbnailed): luma
+// thumbnail into the window's thumbnail ring, RGB, histogram by frame.  The
+// launch sits on the level chain, so each picture is split over
+// blockIdx.y bands of thumbnail rows (a few chunks per thread, not one
+// workgroup's long loop); a band adds its LDS histogram into the frame's
+// (zeroed per window, integer adds: deterministic).  thumb_sad then scores the
+// window from the ring.
+constexpr int kThumbThreads = 256;
+template <int K>
+__global__ void __launch_bounds__(kThumbThreads) thumb_pics(PicThumbArgs a) {
+  using G = Geo<K>;
+  __shared__ uint32_t lds_hist[256];
+  const int tid = threadIdx.x;
+  const int slot = a.pics[blockIdx.x].x;
+  const int64_t f = a.f0 + slot;
+  const uint8_t *yplane = a.surf + static_cast<int64_t>(a.surf_of ? a.surf_of[slot] : slot) * a.frame_stride;
+  const uint8_t *uvplane = yplane + static_cast<int64_t>(a.pitch) * a.uv_row_offset;
+  const int64_t npx = static_cast<int64_t>(a.w) * a.h;
+  lds_hist[tid] = 0;
+  __syncthreads();
+  uint8_t *thumb = a.thumb + static_cast<int64_t>(slot) * npx;
+  const int r0 = static_cast<int>((static_cast<int64_t>(a.h) * blockIdx.y) / gridDim.y);
+  const int r1 = static_cast<int>((static_cast<int64_t>(a.h) * (blockIdx.y + 1)) / gridDim.y);
+  for (int c = r0 * a.chunks_per_row + tid; c < r1 * a.chunks_per_row; c += kThumbThreads) {
+    const int ty = c / a.chunks_per_row;
+    const int tx = c - ty * a.chunks_per_row;
+    uint32_t yq[G::kG], rgb24[G::kG];
+    thumb_chunk<K>(yplane, uvplane, a.pitch, ty, static_cast<int64_t>(tx) * G::kRowBytes, lds_hist, yq, rgb24);
+    const int64_t tpx = static_cast<int64_t>(ty) * a.w + static_cast<int64_t>(tx) * G::kG;
+    if constexpr (G::kG >= 4) {
+#pragma unroll
+      for (int q = 0; q < G::kG / 4; ++q)
+        reinterpret_cast<uint32_t *>(thumb + tpx)[q] = yq[4 * q] | yq[4 * q + 1] << 8 | yq[4 * q + 2] << 16 | yq[4 * q + 3] << 24;
+    } else {
+      *reinterpret_cast<uint16_t *>(thumb + tpx) = static_cast<uint16_t>(yq[0] | yq[1] << 8);
+    }
+    if (a.rgb) store_rgb<G::kG>(a.rgb + f * npx * 3 + tpx * 3, rgb24);
+  }
+  __syncthreads();
+  if (a.hist && lds_hist[tid]) atomicAdd(&a.hist[f * 256 + tid], lds_hist[tid]);
+}
+
 int row_bytes_for(int k) { return k == 6 ? 48 : 16; }
 
 }  // namespace
@@ -379,6 +513,25 @@ int score_launch(const vts_score_desc *d, hipStream_t stream) {
     e = hipGetLastError();
     if (e != hipSuccess) return fail(VTS_E_HIP, "score_seams launch: %s", hipGetErrorString(e));
   }
+  return VTS_OK;
+}
+
+int thumb_pics_launch(const PicThumbArgs &a, int k, hipStream_t s) {
+  if (a.n_pics <= 0) return VTS_OK;
+  if (a.w * k > a.pitch || a.chunks_per_row * row_bytes_for(k) != a.w * k || a.n_chunks != a.chunks_per_row * a.h)
+    return fail(VTS_E_INVALID, "thumb_pics: thumbnail geometry does not match k=%d", k);
+  // bands of rows: about four chunks per thread
+  const int bands = std::max(1, std::min(a.h, (a.n_chunks + 4 * kThumbThreads - 1) / (4 * kThumbThreads)));
+  const dim3 grid(static_cast<unsigned>(a.n_pics), static_cast<unsigned>(bands));
+  switch (k) {
+    case 2: hipLaunchKernelGGL(thumb_pics<2>, grid, dim3(kThumbThreads), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(thumb_pics<4>, grid, dim3(kThumbThreads), 0, s, a); break;
+    case 6: hipLaunchKernelGGL(thumb_pics<6>, grid, dim3(kThumbThreads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(thumb_pics<8>, grid, dim3(kThumbThreads), 0, s, a); break;
+    default: return fail(VTS_E_INVALID, "thumb_pics: k must be 2, 4, 6 or 8");
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "thumb_pics launch: %s", hipGetErrorString(e));
   return VTS_OK;
 }
 

@@ -211,6 +211,21 @@ struct vts_ctx {
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full (its LDS fallback)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<hipEvent_t> ev_bs;  // paced bS: two per level launch of a window (reused window to window)
+  // recycled surfaces (keep_frames 0, no transcode, per-level launches, at most
+  // two GOP groups): a picture's surface goes back to its group's pool once
+  // the last picture predicting from it is reconstructed and its own level is
+  // thumbnailed: thumb_pics right after the level on the group's own stream
+  // (surf_inline), or on s_grp[kSurfThumbStream] with the group surf_lag
+  // levels behind it (VTS_SURF_THUMB=side, VTS_SURF_LAG);
+  // surf_of[frame] = surface of the frame's window slot, surf_count per ring
+  static constexpr int kSurfThumbStream = 1;
+  bool surf_pool = false;
+  bool surf_inline = true;
+  int surf_lag = 0;
+  std::vector<int32_t> surf_of;
+  int32_t *d_surf_of = nullptr;
+  int64_t surf_count = 0;
+  std::vector<hipEvent_t> ev_th;  // per level launch: (reconstructed, thumbnailed), + window end
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock

@@ -440,6 +440,11 @@ int alloc_general(vts_ctx *c) {
   if (const char *e = std::getenv("VTS_RECON_SCHED")) c->recon_sched = std::atoi(e) != 0;
   if (recon_sched_lds_bytes(c->sps.mb_width, c->sps.mb_height) > 160 * 1024 || c->sps.mb_height > 1024)
     c->recon_sched = false;
+  if (c->recon_sched && c->surf_pool) return fail(VTS_E_INVALID, "recycled surfaces planned with the per-picture scheduler");
+  if (c->surf_pool) {
+    HIP_TRY(vts::dmalloc(&c->d_surf_of, sizeof(int32_t) * c->surf_of.size()));
+    HIP_TRY(hipMemcpy(c->d_surf_of, c->surf_of.data(), sizeof(int32_t) * c->surf_of.size(), hipMemcpyHostToDevice));
+  }
   if (c->recon_sched) {
     int ncu = 0;
     HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -470,7 +475,8 @@ int alloc_general(vts_ctx *c) {
     }
     HIP_TRY(vts::dmalloc(&c->d_dbk[r], static_cast<size_t>(c->dbk_pics * nmb) * sizeof(DbkInfo)));
     HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
-    HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + kPad)));
+    HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>((c->surf_pool ? c->surf_count : c->ring_frames) * c->frame_stride + kPad)));
+    if (c->surf_pool) HIP_TRY(vts::dmalloc(&c->d_thumb[r], static_cast<size_t>(c->ring_frames * tw + kPad)));
     HIP_TRY(vts::dmalloc(&c->d_ws[r], static_cast<size_t>(c->ws_bytes)));
     c->ring_cleared_at[r] = -1;
   }
@@ -1522,6 +1528,11 @@ extern "C" int vts_get_frame_nv12(vts_ctx *c, int64_t frame, uint8_t *out, int64
   for (int64_t wi = first_resident; wi <= c->last_window_done; ++wi) {
     const Window &w = c->windows[static_cast<size_t>(wi)];
     if (frame < w.f0 || frame >= w.f1) continue;
+    if (c->surf_pool)
+      return fail(VTS_E_INVALID,
+                  "frame %lld is not kept: the general decoder recycles surfaces once a picture is scored "
+                  "(open with vts_params.keep_frames = 1, or VTS_SURF_POOL=0)",
+                  static_cast<long long>(frame));
     if (c->tb_ran_sparse && w.tb && !c->tb_last[static_cast<size_t>(frame)])
       return fail(VTS_E_INVALID,
                   "frame %lld was decoded in LDS only (level-blocked launches keep each block's last "
@@ -1601,6 +1612,7 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
     case 8: return c->general ? 1 : 0;
     case 9: return c->arena_reruns;                 // runs repeated with the bound's coefficient arena
     case 10: return c->arena_blocks;                // coefficient blocks per ring (general decoder)
+    case 11: return c->surf_pool ? c->surf_count : 0;  // recycled surfaces per ring (general decoder)
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
   }
 }
@@ -1649,6 +1661,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_rs_pics);
   f(c->d_rs_refs);
   f(c->d_rs_next);
+  f(c->d_surf_of);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);
@@ -1663,6 +1676,8 @@ extern "C" int vts_close(vts_ctx *c) {
   for (auto e : c->lev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->ev_bs)
+    if (e) (void)hipEventDestroy(e);
+  for (auto e : c->ev_th)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);

@@ -225,6 +225,20 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   c->rs_refs.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
+  // recycled surfaces: only where no caller reads a decoded frame back (no
+  // keep_frames, no transcode yet) and the reconstruction is the per-level
+  // chain of at most two GOP groups (the thumbnail stream is s_grp[1])
+  {
+    const char *sp = std::getenv("VTS_SURF_POOL"), *rs = std::getenv("VTS_RECON_SCHED");
+    const char *th = std::getenv("VTS_SURF_THUMB"), *lg = std::getenv("VTS_SURF_LAG");
+    c->surf_inline = !(th && std::strcmp(th, "side") == 0);
+    c->surf_lag = c->surf_inline ? 0 : (lg ? std::max(0, std::atoi(lg)) : 3);
+    c->surf_pool = c->params.keep_frames == 0 && !c->small.on &&
+                   (c->surf_inline || c->general_groups <= vts_ctx::kSurfThumbStream + 1) &&
+                   !(sp && std::atoi(sp) == 0) && !(rs && std::atoi(rs) != 0);
+  }
+  c->surf_of.assign(static_cast<size_t>(c->surf_pool ? n : 0), 0);
+  c->surf_count = 0;
   for (Window &w : c->windows) {
     w.fs0 = static_cast<int64_t>(c->fslices.size());
     int64_t arena = 0, maxl = 0;
@@ -404,6 +418,58 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
         c->level_frames.insert(c->level_frames.end(), l.begin(), l.end());
       }
     }
+    if (c->surf_pool) {
+      // j: a picture's launch index in its group.  A surface is free for the
+      // group's launches after max(last reader's j, own j + surf_lag): its
+      // readers ran earlier on the group's stream, and so did its thumbnails
+      // (inline), or launch j waits for the thumbnails of launch
+      // j - surf_lag - 1 (side stream, run_general).  Each group its own
+      // pool: the groups' launches are not ordered against each other.
+      std::vector<int32_t> jof(static_cast<size_t>(wn), 0), last(static_cast<size_t>(wn), -1);
+      const size_t nl = w.lvl_off.size();
+      std::vector<size_t> glo(static_cast<size_t>(ngrp) + 1, nl);
+      glo[0] = 0;
+      for (int g = 1; g < ngrp; ++g) glo[static_cast<size_t>(g)] = static_cast<size_t>(w.grp[static_cast<size_t>(g - 1)]);
+      for (int g = 0; g < ngrp; ++g)
+        for (size_t l = glo[static_cast<size_t>(g)]; l < glo[static_cast<size_t>(g) + 1]; ++l)
+          for (int32_t i = 0; i < w.lvl_cnt[l]; ++i)
+            jof[static_cast<size_t>(c->level_frames[static_cast<size_t>(w.lvl_off[l] + i)].x)] =
+                static_cast<int32_t>(l - glo[static_cast<size_t>(g)]);
+      for (int64_t f = w.f0; f < w.f1; ++f)
+        for (int64_t rf : frames[static_cast<size_t>(f)].refs) {
+          int32_t &lr = last[static_cast<size_t>(slot_of(rf))];
+          lr = std::max(lr, jof[static_cast<size_t>(slot_of(f))]);
+        }
+      int64_t base = 0;
+      for (int g = 0; g < ngrp; ++g) {
+        const size_t l0 = glo[static_cast<size_t>(g)], l1 = glo[static_cast<size_t>(g) + 1];
+        std::vector<std::vector<int32_t>> freed(l1 - l0);
+        std::vector<int32_t> pool;
+        int32_t made = 0;
+        for (size_t l = l0; l < l1; ++l) {
+          const size_t j = l - l0;
+          if (j > 0) {
+            for (int32_t s : freed[j - 1]) pool.push_back(s);
+            freed[j - 1].clear();
+          }
+          for (int32_t i = 0; i < w.lvl_cnt[l]; ++i) {
+            const int32_t slot = c->level_frames[static_cast<size_t>(w.lvl_off[l] + i)].x;
+            int32_t s;
+            if (pool.empty()) s = made++;
+            else {
+              s = pool.back();
+              pool.pop_back();
+            }
+            c->surf_of[static_cast<size_t>(w.f0 + slot)] = static_cast<int32_t>(base + s);
+            const size_t fa = static_cast<size_t>(
+                std::max<int64_t>(last[static_cast<size_t>(slot)], static_cast<int64_t>(j) + c->surf_lag));
+            if (fa < freed.size()) freed[fa].push_back(s);
+          }
+        }
+        base += made;
+      }
+      c->surf_count = std::max(c->surf_count, base);
+    }
   }
   // Deblocking descriptors (h264_bs_full -> h264_deblock_plane) live in a
   // ring of two level slots per GOP group: level l + 1's bS is derived while
@@ -467,6 +533,17 @@ int run_general(vts_ctx *c) {
 
 int submit_general(vts_ctx *c) {
   HIP_TRY(hipSetDevice(c->device));
+  if (c->surf_pool && c->small.on) {
+    // a transcode (after open) reads every decoded frame of a window: one
+    // surface per window slot from now on
+    HIP_TRY(hipDeviceSynchronize());
+    for (int r = 0; r < c->n_rings; ++r) {
+      vts::dfree(c->d_surf[r]);
+      c->d_surf[r] = nullptr;
+      HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>(c->ring_frames * c->frame_stride + 256)));  // + kPad (session.hip)
+    }
+    c->surf_pool = false;
+  }
   if (!c->h_err) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_err), sizeof(uint32_t)));
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(uint32_t), c->s_dec));
   HIP_TRY(hipEventRecord(c->ev_start, c->s_dec));
@@ -577,6 +654,7 @@ int submit_general(vts_ctx *c) {
     ra.arena = c->d_arena[r];
     ra.slices = c->d_fslices + w.fs0;
     ra.surf = c->d_surf[r];
+    ra.surf_of = c->surf_pool ? c->d_surf_of + w.f0 : nullptr;
     ra.frame_stride = c->frame_stride;
     ra.uv_off = static_cast<int64_t>(c->pitch) * c->coded_h;
     ra.pitch = c->pitch;
@@ -608,6 +686,8 @@ int submit_general(vts_ctx *c) {
         ra.frames = c->d_levels + w.lvl_off[l];
         return bs_full_launch(ra, w.lvl_cnt[l], s);
       };
+      if (c->surf_pool)  // thumb_pics' bands add into the window's histograms
+        HIP_TRY(hipMemsetAsync(c->d_hist + w.f0 * 256, 0, sizeof(uint32_t) * 256 * static_cast<size_t>(w.f1 - w.f0), sd));
       if (ng > 1) {  // groups >= 1 on their own streams, after the parse
         HIP_TRY(hipEventRecord(c->ev_grp[0], sd));
         for (int g = 1; g < ng; ++g) HIP_TRY(hipStreamWaitEvent(c->s_grp[g - 1], c->ev_grp[0], 0));
@@ -621,6 +701,35 @@ int submit_general(vts_ctx *c) {
       // content stream, that stream sharing a hardware queue with a group's,
       // profiles/r04t_bs_paced_split_ab.json)
       auto sb_of = [&](int) { return sbs; };
+      // recycled surfaces: each level's thumbnails after its reconstruction,
+      // on the group's stream (inline) or on the thumbnail stream, where a
+      // group's launch j waits for the thumbnails of its launch
+      // j - surf_lag - 1 (the liveness plan's promise)
+      const bool side = c->surf_pool && !c->surf_inline;
+      hipStream_t st = c->s_grp[vts_ctx::kSurfThumbStream];
+      PicThumbArgs ta{};
+      if (c->surf_pool) {
+        const size_t need = 2 * w.lvl_off.size() + 1;
+        if (c->ev_th.size() < need) {
+          const size_t n0 = c->ev_th.size();
+          c->ev_th.resize(need, nullptr);
+          for (size_t k = n0; k < need; ++k) HIP_TRY(hipEventCreateWithFlags(&c->ev_th[k], hipEventDisableTiming));
+        }
+        const int rb = c->k == 6 ? 48 : 16;
+        ta.surf = c->d_surf[r];
+        ta.frame_stride = c->frame_stride;
+        ta.surf_of = c->d_surf_of + w.f0;
+        ta.w = c->width / c->k;
+        ta.h = c->height / c->k;
+        ta.pitch = c->pitch;
+        ta.uv_row_offset = c->coded_h;
+        ta.chunks_per_row = c->width / rb;
+        ta.n_chunks = ta.chunks_per_row * ta.h;
+        ta.f0 = w.f0;
+        ta.thumb = c->d_thumb[r];
+        ta.rgb = c->d_rgb;
+        ta.hist = c->d_hist;
+      }
       std::vector<size_t> lo(static_cast<size_t>(ng)), hi(static_cast<size_t>(ng));
       size_t jmax = 0;
       for (int g = 0; g < ng; ++g) {
@@ -647,9 +756,23 @@ int submit_general(vts_ctx *c) {
           if (l >= hi[static_cast<size_t>(g)]) continue;
           hipStream_t s = g ? c->s_grp[g - 1] : sd;
           if (paced) HIP_TRY(hipStreamWaitEvent(s, c->ev_bs[2 * l], 0));
+          if (side && jj > static_cast<size_t>(c->surf_lag))
+            HIP_TRY(hipStreamWaitEvent(s, c->ev_th[2 * (l - static_cast<size_t>(c->surf_lag) - 1) + 1], 0));
           ra.frames = c->d_levels + w.lvl_off[l];
           const bool next = paced && l + 1 < hi[static_cast<size_t>(g)];
           VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], s, next ? c->ev_bs[2 * l + 1] : nullptr));
+          if (c->surf_pool && !side) {
+            ta.pics = c->d_levels + w.lvl_off[l];
+            ta.n_pics = w.lvl_cnt[l];
+            VTS_TRY(thumb_pics_launch(ta, c->k, s));
+          } else if (side) {
+            HIP_TRY(hipEventRecord(c->ev_th[2 * l], s));
+            HIP_TRY(hipStreamWaitEvent(st, c->ev_th[2 * l], 0));
+            ta.pics = c->d_levels + w.lvl_off[l];
+            ta.n_pics = w.lvl_cnt[l];
+            VTS_TRY(thumb_pics_launch(ta, c->k, st));
+            HIP_TRY(hipEventRecord(c->ev_th[2 * l + 1], st));
+          }
           if (next) {
             HIP_TRY(hipStreamWaitEvent(sb_of(g), c->ev_bs[2 * l + 1], 0));
             VTS_TRY(bs_level(l + 1, sb_of(g)));
@@ -660,11 +783,30 @@ int submit_general(vts_ctx *c) {
         HIP_TRY(hipEventRecord(c->ev_grp[g - 1], c->s_grp[g - 1]));
         HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[g - 1], 0));
       }
+      if (side) {  // the window's thumbnails before its scoring
+        HIP_TRY(hipEventRecord(c->ev_th[2 * w.lvl_off.size()], st));
+        HIP_TRY(hipStreamWaitEvent(ss, c->ev_th[2 * w.lvl_off.size()], 0));
+      }
     }
     if (c->small.on) VTS_TRY(small_window(c, r, w.f0, w.f1, sd));
     HIP_TRY(hipEventRecord(E[2], sd));
     HIP_TRY(hipStreamWaitEvent(ss, E[2], 0));
     HIP_TRY(hipEventRecord(E[3], ss));
+    if (c->surf_pool) {  // SAD and score from the thumbnail ring
+      ThumbSadArgs t{};
+      t.thumb = c->d_thumb[r];
+      t.prev_luma = wi > 0 ? c->d_last[(wi - 1) & 1] : nullptr;
+      t.last_luma = c->d_last[wi & 1];
+      t.frame0 = w.f0;
+      t.n_frames = w.f1 - w.f0;
+      t.w = c->width / c->k;
+      t.h = c->height / c->k;
+      t.sad = c->d_sad;
+      t.score = c->d_score;
+      VTS_TRY(thumb_sad_launch(t, ss));
+      HIP_TRY(hipEventRecord(E[4], ss));
+      continue;
+    }
     vts_score_desc d{};
     d.nv12 = c->d_surf[r];
     d.frame_stride = c->frame_stride;
