@@ -9,9 +9,11 @@
 // across (as in the subset path), sized to a ring budget of decoded surfaces,
 // macroblock records and coefficient arena.
 // Run, per window (two rings, decode of window i+1 overlapping scoring of
-// window i): h264_parse_full over the window's slices, then per level
-// h264_recon_full + h264_deblock_full over that level's pictures, then the
-// scoring kernels on the finished pictures (score.hip).
+// window i): the slice parse (+ h264_derive for CABAC), then per level and
+// GOP group the inter, intra and deblocking launches over that level's
+// pictures (recon_full_launch; the level's bS on a paced side stream), then
+// scoring: per level thumb_pics + the window's thumb_sad when surfaces are
+// recycled (keep_frames 0), else score.hip's pass over the finished pictures.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
