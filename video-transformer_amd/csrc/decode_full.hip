@@ -1289,7 +1289,8 @@ struct DevLanes {
 
 // The intra phase's LDS: the groups' tiles, the level buckets and offset
 // tables, then (dynamic) the tagged line entries (one per macroblock column
-// and row, i2::I2Line) and the level lists (2 B per macroblock)
+// and row, i2::I2Line), the level lists and the round table (2 B per
+// macroblock each)
 struct I2Lds {
   I2Tile tiles[kI2Groups];
   int s_max, s_cnt;
@@ -1299,7 +1300,12 @@ struct I2Lds {
 };
 __host__ __device__ constexpr size_t i2_lds_bytes(int mbw, int mbh) {
   return (sizeof(I2Lds) + 15) / 16 * 16 + sizeof(i2::I2Line) * static_cast<size_t>(mbw + mbh) +
-         2 * static_cast<size_t>(mbw) * static_cast<size_t>(mbh);
+         4 * static_cast<size_t>(mbw) * static_cast<size_t>(mbh);
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+  return v;
 }
 // one picture's intra macroblocks by dependency level (1024 threads)
 __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slot, uint8_t *lds) {
@@ -1313,6 +1319,7 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
   const int pitch = a.pitch;
   i2::I2Line *lcol = reinterpret_cast<i2::I2Line *>(s_dyn), *lrow = lcol + mbw;
   uint16_t *s_list = reinterpret_cast<uint16_t *>(lrow + mbh);
+  uint16_t *s_rnd = s_list + nmb;  // per macroblock: its level, then 0x8000 | its round
   for (int i = threadIdx.x; i < mbw + mbh; i += kI2Threads) {
     lcol[i].tag = -2;
     lcol[i].claim = -2;
@@ -1331,7 +1338,7 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
   }
   if (m >= 0) atomicMax(&s_max, m);
   __syncthreads();
-  const int maxl = __builtin_amdgcn_readfirstlane(s_max);  // uniform: the loops below hold barriers
+  int maxl = __builtin_amdgcn_readfirstlane(s_max);  // uniform: the loops below hold barriers
   const int g = tid >> 5;
   const DevLanes lanes0{tid & 31};
   i2::I2Ctx ctx;
@@ -1365,8 +1372,93 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
     for (int i = tid; i < nmb; i += kI2Threads) {
       const int v = lv[i];
       if (v != kNoLevel) s_list[atomicAdd(&s_fill[v], 1)] = static_cast<uint16_t>(i);
+      s_rnd[i] = static_cast<uint16_t>(v == kNoLevel ? 0x7fff : v);
+    }
+    if (tid == 0) {
+      int widest = 0;
+      for (int l = 0; l <= maxl; ++l) widest = max(widest, s_lvl[l + 1] - s_lvl[l]);
+      s_cnt = widest;
     }
     __syncthreads();
+    // Rounds instead of levels where a level holds more macroblocks than a
+    // round (an x + 2y diagonal of 33..40 at 720p took two rounds): each
+    // macroblock in the earliest round after its intra neighbours' (A, B, C,
+    // D at lower levels: a superset of what it predicts from) with room.  An
+    // all-intra 720p picture: 208 -> 175 rounds (1080p 380 -> 317).  The
+    // line entries' tags make any such order safe (a neighbour whose entry
+    // was taken over is read from HBM).  Wave 0 assigns, level by level.
+    if (__builtin_amdgcn_readfirstlane(s_cnt) > kI2Groups) {
+      for (int i = tid; i < kIntraLevels; i += kI2Threads) s_fill[i] = 0;  // per round: macroblocks
+      __syncthreads();
+      if (tid < 64) {
+        int rmax = -1;
+        bool over = false;
+        for (int l = 0; l <= maxl && !over; ++l) {
+          const int j0 = __builtin_amdgcn_readfirstlane(s_lvl[l]), j1 = __builtin_amdgcn_readfirstlane(s_lvl[l + 1]);
+          for (int c0 = j0; c0 < j1 && !over; c0 += 64) {
+            const int i = c0 + tid;
+            const bool valid = i < j1;
+            int r0 = 0, mb = 0;
+            if (valid) {
+              mb = s_list[i];
+              const int mx = mb % mbw, my = mb / mbw;
+              auto dep = [&](bool ok, int n) {
+                if (ok) {
+                  const int e = s_rnd[n];
+                  if (e & 0x8000) r0 = max(r0, (e & 0x7fff) + 1);  // assigned: a lower level
+                }
+              };
+              dep(mx > 0, mb - 1);
+              dep(my > 0, mb - mbw);
+              dep(my > 0 && mx + 1 < mbw, mb - mbw + 1);
+              dep(my > 0 && mx > 0, mb - mbw - 1);
+            }
+            bool un = valid;
+            int r = wave_min(un ? r0 : 0x7fffffff);
+            while (__ballot(un) != 0) {
+              if (r >= kIntraLevels) {
+                over = true;
+                break;
+              }
+              const uint64_t el = __ballot(un && r0 <= r);
+              if (el == 0) {
+                r = wave_min(un ? r0 : 0x7fffffff);
+                continue;
+              }
+              const int fill = s_fill[r];
+              const int room = kI2Groups - fill;
+              const int before = __popcll(el & ((1ull << tid) - 1ull));
+              if (un && r0 <= r && before < room) {
+                s_rnd[mb] = static_cast<uint16_t>(0x8000 | r);
+                un = false;
+              }
+              const int taken = min(room, __popcll(el));
+              s_fill[r] = fill + taken;  // every lane the same value
+              if (taken > 0) rmax = max(rmax, r);
+              ++r;
+            }
+          }
+        }
+        if (tid == 0) s_cnt = over ? -1 : rmax;
+      }
+      __syncthreads();
+      const int nr = __builtin_amdgcn_readfirstlane(s_cnt) + 1;
+      if (nr > 0) {  // the lists by round (else they stay by level)
+        if (tid == 0) {
+          s_lvl[0] = 0;
+          for (int r = 0; r < nr; ++r) s_lvl[r + 1] = s_lvl[r] + s_fill[r];
+        }
+        __syncthreads();
+        for (int i = tid; i < nr; i += kI2Threads) s_fill[i] = s_lvl[i];
+        __syncthreads();
+        for (int i = tid; i < nmb; i += kI2Threads) {
+          const int e = s_rnd[i];
+          if (e & 0x8000) s_list[atomicAdd(&s_fill[e & 0x7fff], 1)] = static_cast<uint16_t>(i);
+        }
+        maxl = nr - 1;
+        __syncthreads();
+      }
+    }
   }
   // the group processes s_lvl[l] + g + 32 k of every level l, in order: its
   // first macroblock at level l0 or later (-1: none)
