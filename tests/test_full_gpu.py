@@ -32,6 +32,21 @@ def _first_diff(a, b):
     return bad[:8].tolist()
 
 
+def _recycled_equal(path, ref, k=4):
+    """The same stream opened without keep_frames: decoded surfaces recycled
+    (thumb_pics per level launch, thumb_sad per window), so only the scoring
+    outputs can be compared, and they must equal the oracle's."""
+    with scene.VideoScorer(path, k=k) as v:
+        assert v.general() and v._lib.vts_schedule_info(v._ctx, 11) > 0
+        res = v.score()
+        assert np.array_equal(res.hist, ref["hist"])
+        assert np.array_equal(res.sad, ref["sad"])
+        assert np.array_equal(res.scores, ref["score"])
+        n = res.scores.shape[0]
+        rgb = np.stack([v.thumbnail_rgb(i, k) for i in range(n)]).reshape(-1)
+        assert np.array_equal(rgb, ref["rgb"])
+
+
 FULL = [
     ("tiny", dict(width=48, height=32, max_motion=2)),
     ("qvga", dict(width=320, height=240, max_motion=3)),
@@ -66,6 +81,7 @@ def test_general_decoder_bit_exact(tmp_path, name, kw):
         assert np.array_equal(res.scores, ref["score"])
         res2 = v.score()   # a second run over the same rings (record epochs)
         assert np.array_equal(res2.scores, res.scores)
+    _recycled_equal(path, ref, k)
 
 
 def test_general_decoder_windows_and_rings(tmp_path):
@@ -186,6 +202,7 @@ def test_b_pictures_bit_exact(tmp_path, name, kw):
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
+    _recycled_equal(path, ref, k)
 
 
 def test_b_pictures_windows_and_rings(tmp_path):
@@ -249,6 +266,7 @@ def test_cabac_b_streams_bit_exact(tmp_path, name, kw, t8):
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
+    _recycled_equal(path, ref)
 
 
 @pytest.mark.parametrize("groups", [1, 2, 3, 4])
@@ -457,6 +475,7 @@ def test_writer_cabac_streams_bit_exact(tmp_path, name, kw):
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
+    _recycled_equal(path, ref)
 
 
 SCALING = [
@@ -490,6 +509,7 @@ def test_scaling_matrix_streams_bit_exact(tmp_path, name, kw):
         assert np.array_equal(res.hist, ref["hist"])
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
+    _recycled_equal(path, ref)
 
 
 @pytest.mark.parametrize("merge", ["0", "1"])
@@ -646,3 +666,4 @@ def test_content_streams_equal_the_writer_and_the_oracle(tmp_path, name, kw, n):
         assert np.array_equal(res.sad, ref["sad"])
         assert np.array_equal(res.scores, ref["score"])
         assert v.scene_cuts() == sorted(info["cuts"])
+    _recycled_equal(path, ref)
