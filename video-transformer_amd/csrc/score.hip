@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.h"
 #include "decode.h"
@@ -394,7 +395,7 @@ __global__ void __launch_bounds__(256) score_seams(RunArgs a) {
 // decoder, so a surface can be reused once its level is thumbnailed): luma
 // thumbnail into the window's thumbnail ring, RGB, histogram by frame.  The
 // launch sits on the level chain, so each picture is split over
-// blockIdx.y bands of thumbnail rows (a few chunks per thread, not one
+// blockIdx.y bands of thumbnail rows (a chunk per thread, not one
 // workgroup's long loop); a band adds its LDS histogram into the frame's
 // (zeroed per window, integer adds: deterministic).  thumb_sad then scores the
 // window from the ring.
@@ -520,8 +521,13 @@ int thumb_pics_launch(const PicThumbArgs &a, int k, hipStream_t s) {
   if (a.n_pics <= 0) return VTS_OK;
   if (a.w * k > a.pitch || a.chunks_per_row * row_bytes_for(k) != a.w * k || a.n_chunks != a.chunks_per_row * a.h)
     return fail(VTS_E_INVALID, "thumb_pics: thumbnail geometry does not match k=%d", k);
-  // bands of rows: about four chunks per thread
-  const int bands = std::max(1, std::min(a.h, (a.n_chunks + 4 * kThumbThreads - 1) / (4 * kThumbThreads)));
+  // bands of rows: one chunk per thread (VTS_THUMB_CHUNKS; 1 / 2 / 4 / 8
+  // measured, 1 the shortest level chain: profiles/r05am_thumb_bands_ab.json)
+  static const int per_thread = [] {
+    const char *e = std::getenv("VTS_THUMB_CHUNKS");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  const int bands = std::max(1, std::min(a.h, (a.n_chunks + per_thread * kThumbThreads - 1) / (per_thread * kThumbThreads)));
   const dim3 grid(static_cast<unsigned>(a.n_pics), static_cast<unsigned>(bands));
   switch (k) {
     case 2: hipLaunchKernelGGL(thumb_pics<2>, grid, dim3(kThumbThreads), 0, s, a); break;
