@@ -191,12 +191,14 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
   const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
+  uint32_t used = 0;
   const uint32_t e = full::parse_slice_cabac(a.rbsp + s.nal_offset + 1, a.rbsp_len[i], s,
                                              static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
                                              P.bframes ? a.recs1 + s.slot * nmb : nullptr,
                                              s.ext >= 0 ? a.exts + s.ext : nullptr, a.arena, a.epoch,
-                                             reinterpret_cast<full::SynScratch *>(syn_lds));
+                                             reinterpret_cast<full::SynScratch *>(syn_lds), &used);
   if (e) atomicOr(a.err, e);
+  if (a.arena_used && threadIdx.x == 0) a.arena_used[i] = used;
 #ifdef VTS_EXP_PROF
   if (threadIdx.x == 0 && blockIdx.x < 65536) {
     vts_wave_t[3 * blockIdx.x] = t_start;

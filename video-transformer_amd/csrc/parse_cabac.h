@@ -1040,7 +1040,8 @@ struct CabacSyn {
 // DEC_E_* bits.
 VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_len, const FullSlice &s, uint32_t si,
                                              const FullParams P, MbRec *frame_recs, MbRecB *frame_recs1,
-                                             const SliceExt *x, int16_t *arena, uint32_t epoch, SynScratch *sc) {
+                                             const SliceExt *x, int16_t *arena, uint32_t epoch, SynScratch *sc,
+                                             uint32_t *used_out = nullptr) {
   CabacSyn p;
   p.bframes = P.bframes != 0;
   p.direct8x8 = P.direct8x8 != 0;
@@ -1109,6 +1110,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   VTS_PROF_FLUSH(p);
   // the arithmetic decoder has read through the stop bit
   if (!p.err && (p.br.err || p.cab_consumed() != stop_bit + 1)) p.err |= DEC_E_SYNTAX;
+  if (used_out) *used_out = p.used;  // the coefficient blocks the slice stored
   return p.err;
 }
 

@@ -235,6 +235,9 @@ struct vts_ctx {
   bool arena_safe = false;              // CABAC arena ranges from the bound (after a DEC_E_ARENA run)
   int arena_per_byte = 4;               // CABAC arena estimate: blocks per NAL byte (VTS_ARENA_PER_BYTE)
   int64_t arena_reruns = 0;             // runs repeated for that
+  uint32_t *d_arena_used = nullptr;     // CABAC: per fslice, the coefficient blocks its last parse stored
+  bool arena_tight = false;             // CABAC: ranges cut to what the first clean run stored (same stream,
+                                        // same parse: the same blocks every run)
   int64_t dbk_pics = 0;                 // descriptor slots of d_dbk (a ring of two levels per GOP group)
   // kept from open for a later switch to the general decoder (decoder = auto)
   std::vector<int64_t> es_off;          // sample offsets in the ES buffer

@@ -428,6 +428,7 @@ int alloc_general(vts_ctx *c) {
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
   if (const char *e = std::getenv("VTS_PARSE_MERGE")) c->parse_merged = std::atoi(e) != 0;
   if (const char *e = std::getenv("VTS_INTRA")) c->intra_kernel = std::atoi(e) == 1 ? 1 : 2;
+  if (c->fprm.cabac) HIP_TRY(vts::dmalloc(&c->d_arena_used, sizeof(uint32_t) * std::max<size_t>(1, c->fslices.size())));
   HIP_TRY(vts::dmalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
@@ -1662,6 +1663,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_rs_refs);
   f(c->d_rs_next);
   f(c->d_surf_of);
+  f(c->d_arena_used);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);

@@ -594,6 +594,7 @@ int submit_general(vts_ctx *c) {
     pa.ilvl = c->d_ilvl[r];
     pa.arena = c->d_arena[r];
     pa.err = c->d_err;
+    pa.arena_used = (c->fprm.cabac && !c->arena_tight && c->d_arena_used) ? c->d_arena_used + w.fs0 : nullptr;
     pa.P = c->fprm;
     if (c->fprm.cabac) {
       // syntax records of every slice (no waits), then the per-picture
@@ -871,6 +872,37 @@ int finish_general(vts_ctx *c) {
   if (err) {
     c->have_results = false;
     return fail(VTS_E_DECODE, "device decoder: %s", describe_decode_error(err).c_str());
+  }
+  static const bool tighten = [] {
+    const char *e = std::getenv("VTS_ARENA_TIGHT");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (tighten && c->fprm.cabac && !c->arena_tight && c->d_arena_used) {
+    // the first clean run: each slice's range cut to the blocks it stored
+    // (the estimate reserves 4 per slice byte; the streams here store
+    // 0.46-0.87), the arena reallocated to that; later runs parse the same
+    // blocks (a slice that still overflowed would re-run with the bound)
+    std::vector<uint32_t> used(c->fslices.size());
+    HIP_TRY(hipMemcpy(used.data(), c->d_arena_used, sizeof(uint32_t) * used.size(), hipMemcpyDeviceToHost));
+    int64_t blocks = 0;
+    for (const Window &w : c->windows) {
+      int64_t arena = 0;
+      for (int64_t k = w.fs0; k < w.fs1; ++k) {
+        FullSlice &d = c->fslices[static_cast<size_t>(k)];
+        d.arena = static_cast<uint32_t>(arena);
+        d.arena_cap = used[static_cast<size_t>(k)];
+        arena += used[static_cast<size_t>(k)];
+      }
+      blocks = std::max(blocks, arena);
+    }
+    HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
+    for (int r = 0; r < c->n_rings; ++r) {
+      vts::dfree(c->d_arena[r]);
+      c->d_arena[r] = nullptr;
+      HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, blocks)) * 32 + 256));  // + kPad (session.hip)
+    }
+    c->arena_blocks = blocks;
+    c->arena_tight = true;
   }
   c->have_results = true;
   c->host_scores.clear();
