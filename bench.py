@@ -710,13 +710,15 @@ def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: lis
     sessions, then plan_batch every step — every session's run submitted
     before any is waited for (vts_run_async), so the device overlaps them —
     against one video's step alone; each session's HBM (the allocator's bytes
-    handed out by its vts_open) and full parity of every video."""
+    handed out by its vts_open; and the sessions' mean after the runs) and
+    full parity of every video."""
     import torch
     from vtseg import _lib, batch, scene
     from vtseg import budget_planner as bp
     from vtseg import video_segmenter as vs
     L = _lib.lib()
     sessions, hbm = {}, []
+    base = int(L.vts_device_bytes(gpu))
     try:
         for i, p in enumerate(paths):
             before = int(L.vts_device_bytes(gpu))
@@ -739,6 +741,8 @@ def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: lis
             items = batch.plan_batch(strs, REF_CONFIG, score=True, sessions=sessions)
         torch.cuda.synchronize()
         batch_ms = (time.perf_counter() - t0) / 3 * 1e3
+        # after the runs (the CABAC arena is cut to what each slice stored after a session's first run)
+        hbm_after = int(L.vts_device_bytes(gpu)) - base
         per_video, ok = [], True
         for i, p in enumerate(paths):
             v = sessions[i]
@@ -760,6 +764,7 @@ def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: lis
                 "ms_per_step": round(batch_ms, 2), "single_video_ms": round(single_ms, 2),
                 "batch_over_single": round(batch_ms / single_ms, 3),
                 "hbm_gb_per_session": [round(b / 1e9, 2) for b in hbm],
+                "hbm_gb_per_session_after_runs": round(hbm_after / len(paths) / 1e9, 2),
                 "arena_reruns": [sessions[i].arena_reruns() for i in range(len(paths))],
                 "parity": {"all_equal": bool(ok), "videos": per_video}}
     finally:
