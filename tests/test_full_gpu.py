@@ -547,9 +547,7 @@ def test_cabac_temporal_direct_windows_and_arena_rerun(tmp_path, monkeypatch, pe
     windows on two rings; with VTS_ARENA_PER_BYTE=0 every slice's estimated
     coefficient range (64 blocks) overflows, the run reports DEC_E_ARENA to
     the host, which sizes the ranges from the bound and runs again: every
-    frame, histogram and score equals the oracle either way.  After the first
-    clean run the ranges are cut to the blocks each slice stored, and the
-    second run on that arena equals the oracle too."""
+    frame, histogram and score equals the oracle either way."""
     _require_gpu()
     monkeypatch.setenv("VTS_ARENA_PER_BYTE", per_byte)
     n = 60
@@ -563,11 +561,7 @@ def test_cabac_temporal_direct_windows_and_arena_rerun(tmp_path, monkeypatch, pe
     for wf in (0, 24):
         with scene.VideoScorer(path, keep_frames=wf == 0, window_frames=wf, n_streams=2) as v:
             assert v.general()
-            blocks0 = v._lib.vts_schedule_info(v._ctx, 10)
             res = v.score()
-            # the first clean run cuts each slice's range to the blocks it stored
-            blocks1 = v._lib.vts_schedule_info(v._ctx, 10)
-            assert 0 < blocks1 < blocks0 or (per_byte == "0" and blocks1 <= blocks0), (blocks0, blocks1)
             res2 = v.score()  # a second run on the re-sized arena
             if wf == 0:
                 got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
