@@ -13,5 +13,5 @@ python -c "
 import json; d=json.load(open('$O/bench.json'))
 print('bench', d['value'], d['roofline']['frac'], d['parity']['all_equal'], d['e2e'].get('value'), d['cpu_baseline']['value'])
 for k in ('general_batch', 'general', 'general_content', 'long_video', 'hd_1080p'):
-    r = d.get(k, {}); print(k, r.get('value'), r.get('ms_per_step'), r.get('batch_over_single'), r.get('hbm_gb_per_session'), r.get('stage_ms'), r.get('open_s'), r.get('open_stages_ms'), (r.get('parity') or {}).get('all_equal'), r.get('error'))
+    r = d.get(k, {}); print(k, r.get('value'), r.get('ms_per_step'), r.get('batch_over_single'), r.get('hbm_gb_per_session'), r.get('hbm_gb_per_session_after_runs'), r.get('stage_ms'), r.get('open_s'), r.get('open_stages_ms'), (r.get('parity') or {}).get('all_equal'), r.get('error'))
 "
