@@ -246,7 +246,16 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
       exts.push_back(x);
     }
   }
+  // CABAC: the session's window arena (session_full.hip cabac_window_blocks)
+  if (pps.entropy_coding_mode) arena_blocks += arena_blocks / 8 + kArenaChunk * static_cast<uint32_t>(slices.size());
   std::vector<int16_t> arena(static_cast<size_t>(arena_blocks) * 16 + 16);
+  // the kernel's LDS holds whatever the CU's last workgroup left there: the
+  // harness fills it with a poison byte, never zeros
+  auto poisoned_lds = [&]() {
+    std::vector<uint64_t> lds((full::syn_lds_bytes(mbw) + 7) / 8);
+    std::memset(lds.data(), 0xA5, lds.size() * sizeof(uint64_t));
+    return lds;
+  };
   FullParams P{};
   P.mb_width = mbw;
   P.mb_height = mbh;
@@ -260,6 +269,34 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
   P.has_ext = exts.empty() ? 0 : 1;
   P.direct8x8 = sps.direct_8x8_inference;
   const uint32_t epoch = 7;
+  // CABAC: the window arena's block counter (kArenaChunk at a time; the
+  // host decodes the whole stream as one window).  flags bit 3: the arena cut
+  // to exactly what the slices ask for — a first parse of every slice counts
+  // the blocks handed out, the decode below runs with that capacity (the same
+  // requests in the same order on the host), then a canary region after it
+  // must be untouched (no store past the blocks handed out)
+  constexpr int16_t kCanary = 0x5a5b;
+  uint32_t arena_top = 0, arena_cap = arena_blocks;
+  if ((flags & 8) && pps.entropy_coding_mode) {
+    for (int fi = 0; fi < n; ++fi) {
+      const SchedFrame &fr = frames[static_cast<size_t>(fi)];
+      for (int64_t si = fr.s0; si < fr.s0 + fr.ns; ++si) {
+        const FullSlice &fsl = fs[static_cast<size_t>(si)];
+        const SliceExt *x = fsl.ext >= 0 ? &exts[static_cast<size_t>(fsl.ext)] : nullptr;
+        std::vector<uint8_t> rbsp(static_cast<size_t>(fsl.nal_size) + 128, 0);
+        const int32_t rlen = full::unescape_nal(es.data() + fsl.nal_offset + 1, fsl.nal_size - 1, rbsp.data());
+        std::vector<uint64_t> lds = poisoned_lds();
+        const uint32_t e = full::parse_slice_cabac(
+            rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, recs.data() + static_cast<size_t>(fi) * nmb,
+            bframes ? recs1.data() + static_cast<size_t>(fi) * nmb : nullptr, x, arena.data(), &arena_top, arena_cap,
+            epoch, reinterpret_cast<full::SynScratch *>(lds.data()));
+        if (e) return bad("counting parse: " + describe_decode_error(e));
+      }
+    }
+    arena_cap = arena_top;
+    arena_top = 0;
+    arena.assign(static_cast<size_t>(arena_cap) * 16 + 16 * 16, kCanary);
+  }
   for (int fi = 0; fi < n; ++fi) {
     const SchedFrame &fr = frames[static_cast<size_t>(fi)];
     MbRec *fr_recs = recs.data() + static_cast<size_t>(fi) * nmb;
@@ -274,9 +311,10 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
       const int32_t rlen = full::unescape_nal(es.data() + fsl.nal_offset + 1, fsl.nal_size - 1, rbsp.data());
       if (P.cabac) {
         // the kernel's LDS: scratch + one SynEdge per macroblock column
-        std::vector<uint64_t> lds((full::syn_lds_bytes(mbw) + 7) / 8);
+        std::vector<uint64_t> lds = poisoned_lds();
         errs |= full::parse_slice_cabac(rbsp.data(), rlen, fsl, static_cast<uint32_t>(si), P, fr_recs, fr_recs1, x,
-                                        arena.data(), epoch, reinterpret_cast<full::SynScratch *>(lds.data()));
+                                        arena.data(), &arena_top, arena_cap, epoch,
+                                        reinterpret_cast<full::SynScratch *>(lds.data()));
       } else {
         full::FullScratch sc;
         full::BCtx bc{};
@@ -406,5 +444,8 @@ extern "C" int fh_decode(const char *path, int flags, uint8_t *out, int64_t out_
       std::memcpy(o + static_cast<int64_t>(W) * H + static_cast<int64_t>(y) * W,
                   Y + static_cast<int64_t>(pitch) * ch + static_cast<int64_t>(y) * pitch, W);
   }
+  if ((flags & 8) && pps.entropy_coding_mode)
+    for (size_t k = static_cast<size_t>(arena_cap) * 16; k < arena.size(); ++k)
+      if (arena[k] != kCanary) return bad("a slice stored past the blocks handed out");
   return 0;
 }

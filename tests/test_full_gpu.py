@@ -544,10 +544,10 @@ def test_cavlc_b_parse_merged_and_per_level(tmp_path, monkeypatch, merge):
 def test_cabac_temporal_direct_windows_and_arena_rerun(tmp_path, monkeypatch, per_byte):
     """The CABAC syntax parse + h264_derive (colocated records read by parse
     level) on a B stream with temporal direct, in one window and in several
-    windows on two rings; with VTS_ARENA_PER_BYTE=0 every slice's estimated
-    coefficient range (64 blocks) overflows, the run reports DEC_E_ARENA to
-    the host, which sizes the ranges from the bound and runs again: every
-    frame, histogram and score equals the oracle either way."""
+    windows on two rings; with VTS_ARENA_PER_BYTE=0 the windows' arenas (64
+    blocks per slice + a chunk each) overflow, the run reports DEC_E_ARENA to
+    the host, which grows the arena from what the windows asked for and runs
+    again: every frame, histogram and score equals the oracle either way."""
     _require_gpu()
     monkeypatch.setenv("VTS_ARENA_PER_BYTE", per_byte)
     n = 60
@@ -569,7 +569,41 @@ def test_cabac_temporal_direct_windows_and_arena_rerun(tmp_path, monkeypatch, pe
             for r in (res, res2):
                 assert np.array_equal(r.hist, ref["hist"])
                 assert np.array_equal(r.scores, ref["score"])
-            assert v.arena_reruns() == (1 if per_byte == "0" else 0)
+            assert (v.arena_reruns() >= 1) if per_byte == "0" else (v.arena_reruns() == 0)
+
+
+def test_cabac_arena_growth_and_reruns_after_another_session(tmp_path, monkeypatch):
+    """the bench line whose 10-min 720p content stream
+    differed from the oracle ran a noise-stream session first and re-mapped
+    the content session's arena after its first run.  Here, at 720p: a noise
+    stream's session whose arena overflows and grows (re-mapped HBM) is run
+    three times and closed; then a content stream's session on the recycled
+    HBM overflows and grows too, and every one of its three runs — the first
+    after the growth, then two on the grown arena — equals the oracle in
+    histograms, SADs and scores (the chunk counters give every run a
+    different block layout)."""
+    _require_gpu()
+    W, H = 1280, 720
+    x264ish = dict(coding="full", slices_per_row=0, max_motion=4, bframes=True, weighted="implicit",
+                   cabac=True, transform_8x8=True)
+    noise, content = tmp_path / "noise.mp4", tmp_path / "content.mp4"
+    scene.synth_write(noise, width=W, height=H, fps=30, n_frames=240, seed=5, cut_min_s=1.0,
+                      cut_max_s=3.0, gop_max_s=4.0, **x264ish)
+    scene.synth_write(content, width=W, height=H, fps=30, n_frames=900, seed=3, cut_min_s=2.0,
+                      cut_max_s=6.0, gop_max_s=8.0, content=True, **x264ish)
+    monkeypatch.setenv("VTS_ARENA_PER_BYTE", "0")
+    for path, n in ((noise, 240), (content, 900)):
+        frames, _ = oracle.decode_full(path)
+        ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, W, H, W, H, 4)
+        del frames
+        with scene.VideoScorer(path, k=4) as v:
+            assert v.general()
+            for run in range(3):
+                res = v.score()
+                assert np.array_equal(res.hist, ref["hist"]), (path.name, run)
+                assert np.array_equal(res.sad, ref["sad"]), (path.name, run)
+                assert np.array_equal(res.scores, ref["score"]), (path.name, run)
+            assert v.arena_reruns() >= 1
 
 
 def test_async_runs_of_several_sessions_equal_the_oracle(tmp_path):

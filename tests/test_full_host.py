@@ -315,3 +315,38 @@ def test_lane_parallel_intra_on_cpu_equals_oracle(tmp_path, harness, name, kw):
         got = harness(path, flags)
         bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
         assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"
+
+
+TIGHT = [
+    ("content_qvga", dict(width=320, height=240, n_frames=72, seed=7, content=True)),
+    ("content_720p", dict(width=1280, height=720, n_frames=24, seed=3, content=True)),
+    ("noise_b_t8", dict(width=320, height=240, n_frames=36, seed=9, content=False)),
+]
+
+
+@pytest.mark.parametrize("name,kw", TIGHT, ids=[x[0] for x in TIGHT])
+def test_exact_cabac_arena_on_cpu_equals_oracle(tmp_path, harness, name, kw):
+    """The CABAC arena at exactly the blocks the slices ask for (chunked
+    allocation from the window's counter, h264_full.h kArenaChunk): a counting
+    parse, then the decode with that capacity, a canary region after it and
+    the parser's LDS poisoned (0xA5): the canaries stay (no store past the
+    blocks handed out) and every frame equals the oracle before and after
+    deblocking (suspect (a))."""
+    kw = dict(kw)
+    path = tmp_path / f"tight_{name}.mp4"
+    scene.synth_write(path, fps=30, cut_min_s=0.3, cut_max_s=0.8, gop_max_s=0.5, chunks=1,
+                      coding="full", slices_per_row=0, max_motion=4, bframes=True, weighted="implicit",
+                      cabac=True, transform_8x8=True, **kw)
+    for flags in (9, 8):
+        want, _ = oracle.decode_full(path, flags=flags & 1)
+        got = harness(path, flags)
+        bad = np.nonzero((got != want).reshape(got.shape[0], -1).any(1))[0]
+        assert bad.size == 0, f"flags {flags}: frames {bad[:8].tolist()} differ"
+
+
+def test_exact_cabac_arena_real_stream(harness):
+    """The same exact arena on the real High-profile CABAC clip (realshort.mp4)."""
+    path = ROOT / "tests" / "golden" / "real" / "realshort.mp4"
+    want, _ = oracle.decode_full(path)
+    got = harness(path, 8)
+    assert np.array_equal(got, want)

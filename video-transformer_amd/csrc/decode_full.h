@@ -29,7 +29,9 @@ struct FullParseArgs {
   // count); every slice adds 1 to pdone[its slot] when its records are out
   uint32_t *pdone;           // per ring slot, zeroed before the launch; null = not merged
   const int32_t *pneed;      // per ring slot
-  uint32_t *arena_used;      // CABAC: per launch slice, the coefficient blocks it stored (null: not kept)
+  uint32_t *arena_top;       // CABAC: the window's count of arena blocks handed out (zeroed before the launch)
+  uint32_t arena_blocks;     // CABAC: the arena's capacity in blocks
+  int32_t _pad2;
   FullParams P;
 };
 

@@ -181,11 +181,7 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
   parse_one_cavlc(a, &scratch);
 }
 // dynamic LDS: full::syn_lds_bytes(mb_width) (SynScratch + the row of top
-// edges).  kUsed: also store each slice's coefficient-block count
-// (a.arena_used; only until the session's arena is cut to it) — a separate
-// instance, since taking the count changed the parse's code and cost the
-// content stream's parse 3 % (profiles/r05at_parse_used_output_ab.json)
-template <bool kUsed>
+// edges)
 __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full_cabac(FullParseArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t syn_lds[];
@@ -196,14 +192,12 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
   const int64_t nmb = static_cast<int64_t>(P.mb_width) * P.mb_height;
-  uint32_t used = 0;
   const uint32_t e = full::parse_slice_cabac(a.rbsp + s.nal_offset + 1, a.rbsp_len[i], s,
                                              static_cast<uint32_t>(a.slice0 + i), P, a.recs + s.slot * nmb,
                                              P.bframes ? a.recs1 + s.slot * nmb : nullptr,
-                                             s.ext >= 0 ? a.exts + s.ext : nullptr, a.arena, a.epoch,
-                                             reinterpret_cast<full::SynScratch *>(syn_lds), kUsed ? &used : nullptr);
+                                             s.ext >= 0 ? a.exts + s.ext : nullptr, a.arena, a.arena_top,
+                                             a.arena_blocks, a.epoch, reinterpret_cast<full::SynScratch *>(syn_lds));
   if (e) atomicOr(a.err, e);
-  if (kUsed && threadIdx.x == 0) a.arena_used[i] = used;
 #ifdef VTS_EXP_PROF
   if (threadIdx.x == 0 && blockIdx.x < 65536) {
     vts_wave_t[3 * blockIdx.x] = t_start;
@@ -1771,10 +1765,8 @@ int parse_full_launch(const FullParseArgs &a, hipStream_t s) {
   if (a.P.cabac) {
     const size_t lds = full::syn_lds_bytes(a.P.mb_width);
     if (lds > 60 * 1024) return fail(VTS_E_UNSUPPORTED, "picture wider than the CABAC parser's LDS row allows");
-    if (a.arena_used)
-      hipLaunchKernelGGL(h264_parse_full_cabac<true>, dim3(a.n_slices), dim3(64), lds, s, a);
-    else
-      hipLaunchKernelGGL(h264_parse_full_cabac<false>, dim3(a.n_slices), dim3(64), lds, s, a);
+    if (!a.arena_top) return fail(VTS_E_INVALID, "CABAC parse launch without its arena counter");
+    hipLaunchKernelGGL(h264_parse_full_cabac, dim3(a.n_slices), dim3(64), lds, s, a);
   } else {
     hipLaunchKernelGGL(h264_parse_full, dim3(a.n_slices), dim3(64), 0, s, a);
   }

@@ -33,9 +33,11 @@ struct FullSlice {
   int32_t num_ref;      // num_ref_idx_l0_active (P, B)
   int32_t dbk_idc;      // disable_deblocking_filter_idc
   int32_t dbk_a, dbk_b; // FilterOffsetA / FilterOffsetB
-  uint32_t arena;       // first coefficient block reserved for the slice
-  uint32_t arena_cap;   // blocks reserved: min(27 x MBs, 3 x NAL bytes + 27) bounds
-                        // what CAVLC can code (a stored block costs >= 3 bits)
+  uint32_t arena;       // CAVLC: first coefficient block reserved for the slice
+  uint32_t arena_cap;   // CAVLC: blocks reserved: min(27 x MBs, 3 x NAL bytes + 27) bounds
+                        // what CAVLC can code (a stored block costs >= 3 bits).  CABAC
+                        // slices take their blocks from the window's arena in chunks
+                        // (kArenaChunk) and ignore both fields
   int32_t ext;          // SliceExt of a B slice or a weighted P slice, -1: none
   int16_t ref_slot[32]; // RefPicList0[i] -> ring slot (-1: no reference picture)
 };
@@ -81,6 +83,13 @@ enum : uint32_t {
   kBlkChromaAc0 = 19,   // + 4 * iCbCr + chroma4x4BlkIdx
   kPcmBlocks = 12,      // I_PCM: 384 samples in 12 blocks (256 luma, 64 Cb, 64 Cr)
 };
+
+// CABAC: a slice takes coefficient blocks from its window's arena kArenaChunk
+// at a time (one atomic add on the window's counter); a macroblock's blocks
+// stay in one chunk (MbRec.coef + the popcount of MbRec.blocks below a block's
+// bit addresses it), so a chunk with fewer than kMbMaxBlocks left is abandoned
+constexpr uint32_t kArenaChunk = 256;
+constexpr uint32_t kMbMaxBlocks = 27;  // 16 luma + Intra16x16 DC + 2 chroma DC + 8 chroma AC
 
 // MbRec-parallel intra dependency level of a macroblock that is not intra-predicted
 constexpr uint16_t kNoLevel = 0xffff;

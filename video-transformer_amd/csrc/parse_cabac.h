@@ -162,7 +162,9 @@ struct CabacSyn {
   int16_t *arena;         // window coefficient arena, 16 int16 per block
   SynScratch *sc;
   SynEdge *top;           // per macroblock column: the bottom edge of the slice's last macroblock there
-  uint32_t used;          // blocks stored so far in the slice
+  uint32_t *arena_top;    // the window's counter of blocks handed out (kArenaChunk at a time)
+  uint32_t arena_blocks;  // the window arena's capacity in blocks
+  uint32_t blk_at, blk_end;  // the slice's current chunk: next free block, end
   uint32_t slice_index;
   uint32_t epoch;
   int mbw;
@@ -526,11 +528,32 @@ struct CabacSyn {
     te->f = fbm;
   }
 
-  // store sc->blk (or src) as the next arena block; bit = kBlk* index
-  VTS_HD VTS_INLINE bool store_block(uint32_t bit, const int16_t *src) {
+  // room for n blocks of one macroblock in the slice's current chunk, else a
+  // new chunk from the window's counter (one lane adds; the wave reads lane
+  // 0's result); false (DEC_E_ARENA) when the window arena is exhausted —
+  // the counter keeps counting, so the host sees what the window asked for
+  VTS_HD VTS_INLINE bool reserve(uint32_t n) {
+    if (blk_end - blk_at >= n) return true;
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t b = 0;
+    if (lane_ == 0) b = atomicAdd(arena_top, kArenaChunk);
+    b = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(b)));
+#else
+    const uint32_t b = __atomic_fetch_add(arena_top, kArenaChunk, __ATOMIC_RELAXED);
+#endif
+    if (b > arena_blocks - kArenaChunk || arena_blocks < kArenaChunk) {
+      err |= DEC_E_ARENA;
+      return false;
+    }
+    blk_at = b;
+    blk_end = b + kArenaChunk;
+    return true;
+  }
+  // store sc->blk (or src) as the next arena block; bit = kBlk* index (the
+  // macroblock reserved its room first)
+  VTS_HD VTS_INLINE void store_block(uint32_t bit, const int16_t *src) {
     VTS_PARSE_TRACE(7);
-    if (used >= s->arena_cap) return false;
-    int16_t *dst = arena + 16 * static_cast<int64_t>(s->arena + used);
+    int16_t *dst = arena + 16 * static_cast<int64_t>(blk_at);
 #if defined(__HIPCC__)
     u32x4 *d4 = reinterpret_cast<u32x4 *>(dst);
     const u32x4 *s4 = reinterpret_cast<const u32x4 *>(src);
@@ -539,10 +562,9 @@ struct CabacSyn {
 #else
     for (int i = 0; i < 16; ++i) dst[i] = src[i];
 #endif
-    if (cur().blocks == 0) cur().coef = s->arena + used;
+    if (cur().blocks == 0) cur().coef = blk_at;
     cur().blocks |= 1u << bit;
-    ++used;
-    return true;
+    ++blk_at;
   }
   VTS_HD VTS_INLINE void set_cbf(uint32_t bit) {
     MbRec &m = cur();
@@ -810,15 +832,13 @@ struct CabacSyn {
       br.reset_at(cab_consumed());  // the engine's lookahead goes back to the bit reader
       br.align();
       for (int j = 0; j < 16; ++j) m.nz[j] = 16;
+      if (!reserve(kPcmBlocks)) return false;
       for (int k = 0; k < 12; ++k) {
         for (int i = 0; i < 16; ++i) {
           const uint32_t lo = br.bits(8), hi = br.bits(8);
           sc->blk[i] = static_cast<int16_t>(lo | (hi << 8));
         }
-        if (!store_block(k, sc->blk)) {
-          err |= DEC_E_ARENA;
-          return false;
-        }
+        store_block(k, sc->blk);
       }
       m.blocks = 0;
       prev_qpd = false;
@@ -960,6 +980,7 @@ struct CabacSyn {
       if ((cbp >> q) & 1) todo |= (t8 ? 1u : 15u) << (kBlkLuma0 + 4 * q);
     if (cbp >> 4) todo |= 3u << kBlkChromaDc0;
     if ((cbp >> 4) == 2) todo |= 255u << kBlkChromaAc0;
+    if (todo && !reserve(kMbMaxBlocks)) return false;
     VTS_PROF(5);
     while (todo) {
       const uint32_t bt = static_cast<uint32_t>(__builtin_ctz(todo));
@@ -1012,8 +1033,7 @@ struct CabacSyn {
           set_cbf(1u + static_cast<uint32_t>(rs[j]));
         }
         if (nc)
-          for (int j = 0; j < 4; ++j)
-            if (!store_block(bt + j, sc->blk8 + 16 * j)) { err |= DEC_E_ARENA; return false; }
+          for (int j = 0; j < 4; ++j) store_block(bt + j, sc->blk8 + 16 * j);
         continue;
       }
       if (cat == 1 || cat == 2) {
@@ -1022,7 +1042,7 @@ struct CabacSyn {
       }
       if (nc) {
         set_cbf(bt == kBlkI16Dc ? 0u : (cat <= 2 ? 1u + static_cast<uint32_t>(r) : bt));
-        if (!store_block(bt, sc->blk)) { err |= DEC_E_ARENA; return false; }
+        store_block(bt, sc->blk);
       }
     }
     VTS_PROF(6);
@@ -1040,8 +1060,8 @@ struct CabacSyn {
 // DEC_E_* bits.
 VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_len, const FullSlice &s, uint32_t si,
                                              const FullParams P, MbRec *frame_recs, MbRecB *frame_recs1,
-                                             const SliceExt *x, int16_t *arena, uint32_t epoch, SynScratch *sc,
-                                             uint32_t *used_out = nullptr) {
+                                             const SliceExt *x, int16_t *arena, uint32_t *arena_top,
+                                             uint32_t arena_blocks, uint32_t epoch, SynScratch *sc) {
   CabacSyn p;
   p.bframes = P.bframes != 0;
   p.direct8x8 = P.direct8x8 != 0;
@@ -1054,7 +1074,9 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   p.arena = arena;
   p.sc = sc;
   p.top = reinterpret_cast<SynEdge *>(reinterpret_cast<uint8_t *>(sc) + (sizeof(SynScratch) + 15) / 16 * 16);
-  p.used = 0;
+  p.arena_top = arena_top;
+  p.arena_blocks = arena_blocks;
+  p.blk_at = p.blk_end = 0;
   p.slice_index = si;
   p.epoch = epoch;
   p.mbw = P.mb_width;
@@ -1110,7 +1132,6 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   VTS_PROF_FLUSH(p);
   // the arithmetic decoder has read through the stop bit
   if (!p.err && (p.br.err || p.cab_consumed() != stop_bit + 1)) p.err |= DEC_E_SYNTAX;
-  if (used_out) *used_out = p.used;  // the coefficient blocks the slice stored
   return p.err;
 }
 

@@ -230,14 +230,18 @@ struct vts_ctx {
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock
   int16_t *d_arena[2] = {nullptr, nullptr};
-  int64_t arena_blocks = 0;             // per ring
+  int64_t arena_blocks = 0;             // per ring (CABAC: the capacity the windows share)
   std::vector<int32_t> fslice_nmbs;     // per fslice: its macroblocks (arena ranges)
-  bool arena_safe = false;              // CABAC arena ranges from the bound (after a DEC_E_ARENA run)
-  int arena_per_byte = 4;               // CABAC arena estimate: blocks per NAL byte (VTS_ARENA_PER_BYTE)
-  int64_t arena_reruns = 0;             // runs repeated for that
-  uint32_t *d_arena_used = nullptr;     // CABAC: per fslice, the coefficient blocks its last parse stored
-  bool arena_tight = false;             // CABAC: ranges cut to what the first clean run stored (same stream,
-                                        // same parse: the same blocks every run)
+  // CABAC: slices take blocks from their window's arena in chunks (h264_full.h
+  // kArenaChunk, one counter per window).  The capacity starts at an estimate
+  // (arena_per_byte blocks per slice byte, VTS_ARENA_PER_BYTE; the streams
+  // here store 0.46-0.87) and grows, up to arena_bound (32 per byte: every
+  // stored block costs at least one bypass bin), when a run reports
+  // DEC_E_ARENA, which re-runs it (arena_reruns)
+  int arena_per_byte = 1;
+  int64_t arena_bound = 0;              // per ring: the capacity no valid stream exceeds
+  int64_t arena_reruns = 0;
+  uint32_t *d_arena_top = nullptr;      // per window: blocks its parse handed out (asked for)
   int64_t dbk_pics = 0;                 // descriptor slots of d_dbk (a ring of two levels per GOP group)
   // kept from open for a later switch to the general decoder (decoder = auto)
   std::vector<int64_t> es_off;          // sample offsets in the ES buffer
@@ -263,7 +267,6 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
 int run_general(vts_ctx *c);
 int submit_general(vts_ctx *c);
 int finish_general(vts_ctx *c);
-void assign_arena(vts_ctx *c);
 // cheap look at the stream's first pictures: does it need the general decoder?
 // the parameter sets alone send the stream to the general decoder
 bool general_by_headers(const vts_ctx *c);

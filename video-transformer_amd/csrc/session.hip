@@ -428,7 +428,7 @@ int alloc_general(vts_ctx *c) {
     HIP_TRY(hipMemcpy(c->d_pneed, c->pneed.data(), sizeof(int32_t) * c->pneed.size(), hipMemcpyHostToDevice));
   if (const char *e = std::getenv("VTS_PARSE_MERGE")) c->parse_merged = std::atoi(e) != 0;
   if (const char *e = std::getenv("VTS_INTRA")) c->intra_kernel = std::atoi(e) == 1 ? 1 : 2;
-  if (c->fprm.cabac) HIP_TRY(vts::dmalloc(&c->d_arena_used, sizeof(uint32_t) * std::max<size_t>(1, c->fslices.size())));
+  if (c->fprm.cabac) HIP_TRY(vts::dmalloc(&c->d_arena_top, sizeof(uint32_t) * std::max<size_t>(1, c->windows.size())));
   HIP_TRY(vts::dmalloc(&c->d_exts, sizeof(SliceExt) * std::max<size_t>(1, c->exts.size())));
   if (!c->exts.empty())
     HIP_TRY(hipMemcpy(c->d_exts, c->exts.data(), sizeof(SliceExt) * c->exts.size(), hipMemcpyHostToDevice));
@@ -1611,7 +1611,7 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
     }
     case 7: return c->tb_off ? 0 : static_cast<int64_t>(c->tb_chains.size());  // chain slots (levels x chains)
     case 8: return c->general ? 1 : 0;
-    case 9: return c->arena_reruns;                 // runs repeated with the bound's coefficient arena
+    case 9: return c->arena_reruns;                 // runs repeated with a larger coefficient arena
     case 10: return c->arena_blocks;                // coefficient blocks per ring (general decoder)
     case 11: return c->surf_pool ? c->surf_count : 0;  // recycled surfaces per ring (general decoder)
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
@@ -1663,7 +1663,7 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_rs_refs);
   f(c->d_rs_next);
   f(c->d_surf_of);
-  f(c->d_arena_used);
+  f(c->d_arena_top);
   for (int r = 0; r < 2; ++r) {
     f(c->d_recs[r]);
     f(c->d_recs1[r]);

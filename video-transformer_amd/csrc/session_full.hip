@@ -32,19 +32,23 @@ namespace vts {
 namespace {
 
 // Coefficient blocks a slice may store.  CAVLC: a stored block costs >= 3
-// bits.  CABAC: every stored 4x4 block holds a non-zero level, whose sign is
-// one bypass bin = one bit the arithmetic decoder reads (an 8x8 block stores
-// four 4x4 blocks per such bit), so 32 x the NAL bytes is a bound too; it is
-// ~37x what real CABAC streams store (x264-like content: ~0.9 blocks per
-// byte), so the arena is first sized from 4 blocks per byte and a slice that
-// overflows its range (DEC_E_ARENA) makes the host re-run with the bound.
-// Either way never more than the 27 blocks a macroblock can hold.
-// (VTS_ARENA_PER_BYTE overrides the estimate's 4: the tests' way to force
-// the overflow path.)
-int64_t slice_arena_cap(bool cabac, bool safe, int64_t n_mbs, int64_t nal_size, int64_t per_byte) {
-  const int64_t per_mb = 27ll * n_mbs;
+// bits, and each slice gets that bound as its own range.  CABAC: every stored
+// 4x4 block holds a non-zero level, whose sign is one bypass bin = one bit the
+// arithmetic decoder reads (an 8x8 block stores four 4x4 blocks per such bit),
+// so 32 x the NAL bytes is a bound too — ~37x what real CABAC streams store
+// (x264-like content: ~0.9 blocks per byte); the window's arena is sized from
+// `per_byte` blocks per byte instead (cabac_window_blocks) and grows when a run
+// overflows it.  Either way never more than the 27 blocks a macroblock holds.
+int64_t slice_arena_cap(bool cabac, int64_t n_mbs, int64_t nal_size, int64_t per_byte) {
+  const int64_t per_mb = static_cast<int64_t>(kMbMaxBlocks) * n_mbs;
   if (!cabac) return std::min<int64_t>(per_mb, 3ll * nal_size + 27);
-  return std::min<int64_t>(per_mb, safe ? 32ll * nal_size + 64 : per_byte * nal_size + 64);
+  return std::min<int64_t>(per_mb, per_byte * nal_size + 64);
+}
+// CABAC: a window's arena for `blocks` stored blocks over `n_slices` slices:
+// each slice leaves its last chunk partly unused and a chunk switch abandons
+// fewer than kMbMaxBlocks of kArenaChunk (< 1/9)
+int64_t cabac_window_blocks(int64_t blocks, int64_t n_slices) {
+  return blocks + blocks / 8 + static_cast<int64_t>(kArenaChunk) * n_slices;
 }
 
 // per ring: parse throughput grows with the slices per launch, and every
@@ -148,14 +152,14 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   for (int64_t f = 0; f < n; ++f)
     for (int64_t col : frames[static_cast<size_t>(f)].cols)
       plevel[static_cast<size_t>(f)] = std::max(plevel[static_cast<size_t>(f)], plevel[static_cast<size_t>(col)] + 1);
-  // coefficient blocks each slice may need (slice_arena_cap)
-  c->arena_safe = false;
-  c->arena_per_byte = 4;
+  // coefficient blocks each slice may need (slice_arena_cap): CAVLC its
+  // range, CABAC its share of the window's arena estimate
+  c->arena_per_byte = 1;
   if (const char *ev = std::getenv("VTS_ARENA_PER_BYTE")) c->arena_per_byte = std::max(0, std::atoi(ev));
   std::vector<int64_t> cap(slices.size());
   int64_t cap_total = 0;
   for (size_t i = 0; i < slices.size(); ++i) {
-    cap[i] = slice_arena_cap(c->pps.entropy_coding_mode, false, slices[i].n_mbs, slices[i].nal_size, c->arena_per_byte);
+    cap[i] = slice_arena_cap(c->pps.entropy_coding_mode, slices[i].n_mbs, slices[i].nal_size, c->arena_per_byte);
     cap_total += cap[i];
   }
   // windows
@@ -227,6 +231,8 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   c->rs_refs.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
+  c->arena_bound = 0;
+  c->arena_reruns = 0;
   // recycled surfaces: only where no caller reads a decoded frame back (no
   // keep_frames, no transcode yet) and the reconstruction is the per-level
   // chain of at most two GOP groups (the thumbnail stream is s_grp[1])
@@ -243,7 +249,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   c->surf_count = 0;
   for (Window &w : c->windows) {
     w.fs0 = static_cast<int64_t>(c->fslices.size());
-    int64_t arena = 0, maxl = 0;
+    int64_t arena = 0, abound = 0, maxl = 0;
     int32_t maxp = 0;
     for (int64_t f = w.f0; f < w.f1; ++f) maxp = std::max(maxp, plevel[static_cast<size_t>(f)]);
     w.plv_end.clear();
@@ -268,9 +274,12 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
         d.dbk_idc = s.dbk_idc;
         d.dbk_a = s.dbk_a;
         d.dbk_b = s.dbk_b;
-        d.arena = static_cast<uint32_t>(arena);
-        d.arena_cap = static_cast<uint32_t>(cap[static_cast<size_t>(si)]);
+        if (!c->fprm.cabac) {
+          d.arena = static_cast<uint32_t>(arena);
+          d.arena_cap = static_cast<uint32_t>(cap[static_cast<size_t>(si)]);
+        }
         arena += cap[static_cast<size_t>(si)];
+        abound += slice_arena_cap(true, s.n_mbs, s.nal_size, 32);
         c->fslice_nmbs.push_back(static_cast<int32_t>(s.n_mbs));
         d.ext = -1;
         for (int i = 0; i < 32; ++i) {
@@ -380,9 +389,19 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
     c->pneed.resize(c->pneed.size() + static_cast<size_t>(w.f1 - w.f0), 0);
     for (int64_t k = w.fs0; k < static_cast<int64_t>(c->fslices.size()); ++k)
       ++c->pneed[static_cast<size_t>(w.pn0 + c->fslices[static_cast<size_t>(k)].slot)];
-    if (arena > 0xffffffffll) return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
     c->fprm.has_ext = c->exts.empty() ? 0 : 1;
     w.fs1 = static_cast<int64_t>(c->fslices.size());
+    if (c->fprm.cabac) {
+      arena = cabac_window_blocks(arena, w.fs1 - w.fs0);
+      abound = cabac_window_blocks(abound, w.fs1 - w.fs0);
+      // the chunk counter and block indices are 32-bit: the bound stays below
+      // 2^32 with a chunk per slice of headroom for requests past the end
+      const int64_t lim = 0xffffffffll - static_cast<int64_t>(kArenaChunk) * (w.fs1 - w.fs0 + 1);
+      if (arena > lim) return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
+      c->arena_bound = std::max(c->arena_bound, std::min(abound, lim));
+    } else if (arena > 0xffffffffll) {
+      return fail(VTS_E_UNSUPPORTED, "window coefficient arena beyond 32-bit indices");
+    }
     c->arena_blocks = std::max(c->arena_blocks, arena);
     // two interleaved groups of GOPs reconstruct on two streams: a level's
     // pictures are one workgroup each, and two unsynchronised level sequences
@@ -508,36 +527,6 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   return VTS_OK;
 }
 
-// The slices' coefficient arena ranges (FullSlice::arena / arena_cap, each
-// window from 0) and the ring's block count, from the estimate or, once a
-// slice overflowed (c->arena_safe), the bound (slice_arena_cap).
-void assign_arena(vts_ctx *c) {
-  c->arena_blocks = 0;
-  for (const Window &w : c->windows) {
-    int64_t arena = 0;
-    for (int64_t k = w.fs0; k < w.fs1; ++k) {
-      FullSlice &d = c->fslices[static_cast<size_t>(k)];
-      const int64_t cap = slice_arena_cap(c->fprm.cabac, c->arena_safe, c->fslice_nmbs[static_cast<size_t>(k)], d.nal_size,
-                                          c->arena_per_byte);
-      d.arena = static_cast<uint32_t>(arena);
-      d.arena_cap = static_cast<uint32_t>(cap);
-      arena += cap;
-    }
-    c->arena_blocks = std::max(c->arena_blocks, arena);
-  }
-}
-
-// VTS_ARENA_TIGHT=1: cut the CABAC arena to each slice's stored blocks after
-// the first clean run.  Opt-in: the round-5 final bench line saw the content
-// stream's scores differ from the oracle with it on
-static bool arena_tighten() {
-  static const bool on = [] {
-    const char *e = std::getenv("VTS_ARENA_TIGHT");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
 int run_general(vts_ctx *c) {
   VTS_TRY(submit_general(c));
   c->pending = true;
@@ -605,10 +594,11 @@ int submit_general(vts_ctx *c) {
     pa.ilvl = c->d_ilvl[r];
     pa.arena = c->d_arena[r];
     pa.err = c->d_err;
-    pa.arena_used = (arena_tighten() && c->fprm.cabac && !c->arena_tight && c->d_arena_used) ? c->d_arena_used + w.fs0
-                                                                                                : nullptr;
     pa.P = c->fprm;
     if (c->fprm.cabac) {
+      pa.arena_top = c->d_arena_top + wi;
+      pa.arena_blocks = static_cast<uint32_t>(c->arena_blocks);
+      HIP_TRY(hipMemsetAsync(pa.arena_top, 0, sizeof(uint32_t), sp));
       // syntax records of every slice (no waits), then the per-picture
       // derivation by parse level
       pa.slices = c->d_fslices + w.fs0;
@@ -867,13 +857,16 @@ int finish_general(vts_ctx *c) {
     c->timings[3] += s;
   }
   c->last_window_done = static_cast<int64_t>(nw) - 1;
-  if ((err & DEC_E_ARENA) && !c->arena_safe) {
-    // a slice stored more coefficient blocks than its estimated range:
-    // ranges from the bound, a larger arena, and the run again
-    c->arena_safe = true;
+  if ((err & DEC_E_ARENA) && c->fprm.cabac && c->arena_blocks < c->arena_bound) {
+    // a window's slices asked for more coefficient blocks than its arena
+    // holds: the largest request (the counters keep counting past the end)
+    // with a quarter more, at least twice the arena, at most the bound; the
+    // run again
+    std::vector<uint32_t> top(nw);
+    HIP_TRY(hipMemcpy(top.data(), c->d_arena_top, sizeof(uint32_t) * nw, hipMemcpyDeviceToHost));
+    const int64_t need = *std::max_element(top.begin(), top.end());
+    c->arena_blocks = std::min(c->arena_bound, std::max(2 * c->arena_blocks, need + need / 4));
     ++c->arena_reruns;
-    assign_arena(c);
-    HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
     for (int r = 0; r < c->n_rings; ++r) {
       vts::dfree(c->d_arena[r]);
       c->d_arena[r] = nullptr;
@@ -884,33 +877,6 @@ int finish_general(vts_ctx *c) {
   if (err) {
     c->have_results = false;
     return fail(VTS_E_DECODE, "device decoder: %s", describe_decode_error(err).c_str());
-  }
-  if (arena_tighten() && c->fprm.cabac && !c->arena_tight && c->d_arena_used) {
-    // the first clean run: each slice's range cut to the blocks it stored
-    // (the estimate reserves 4 per slice byte; the streams here store
-    // 0.46-0.87), the arena reallocated to that; later runs parse the same
-    // blocks (a slice that still overflowed would re-run with the bound)
-    std::vector<uint32_t> used(c->fslices.size());
-    HIP_TRY(hipMemcpy(used.data(), c->d_arena_used, sizeof(uint32_t) * used.size(), hipMemcpyDeviceToHost));
-    int64_t blocks = 0;
-    for (const Window &w : c->windows) {
-      int64_t arena = 0;
-      for (int64_t k = w.fs0; k < w.fs1; ++k) {
-        FullSlice &d = c->fslices[static_cast<size_t>(k)];
-        d.arena = static_cast<uint32_t>(arena);
-        d.arena_cap = used[static_cast<size_t>(k)];
-        arena += used[static_cast<size_t>(k)];
-      }
-      blocks = std::max(blocks, arena);
-    }
-    HIP_TRY(hipMemcpy(c->d_fslices, c->fslices.data(), sizeof(FullSlice) * c->fslices.size(), hipMemcpyHostToDevice));
-    for (int r = 0; r < c->n_rings; ++r) {
-      vts::dfree(c->d_arena[r]);
-      c->d_arena[r] = nullptr;
-      HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, blocks)) * 32 + 256));  // + kPad (session.hip)
-    }
-    c->arena_blocks = blocks;
-    c->arena_tight = true;
   }
   c->have_results = true;
   c->host_scores.clear();

@@ -164,8 +164,9 @@ class VideoScorer:
         _lib.check(self._lib.vts_wait(self._ctx))
 
     def arena_reruns(self) -> int:
-        """Runs repeated because a CABAC slice overflowed its estimated
-        coefficient range (the session then keeps the bound's ranges)."""
+        """Runs repeated because a CABAC window's slices asked for more
+        coefficient blocks than its arena held (the session keeps the grown
+        arena)."""
         return int(self._lib.vts_schedule_info(self._ctx, 9))
 
     def timings(self) -> dict:
