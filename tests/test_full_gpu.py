@@ -296,42 +296,11 @@ def test_gop_groups_on_streams_equal_the_oracle(tmp_path, monkeypatch, groups, b
             assert np.array_equal(res.scores, ref["score"])
 
 
-@pytest.mark.parametrize("bframes", [False, True], ids=["ip", "b"])
-def test_per_picture_scheduler_equals_the_oracle(tmp_path, monkeypatch, bframes):
-    """The opt-in per-picture reconstruction scheduler (VTS_RECON_SCHED=1,
-    h264_recon_sched: one persistent launch per window, pictures by ticket,
-    each started when its reference pictures are done) equals the oracle, in
-    one window and in several windows on two rings, and on a second run
-    (per-slot done flags of an earlier epoch never read as done)."""
-    _require_gpu()
-    monkeypatch.setenv("VTS_RECON_SCHED", "1")
-    n = 120
-    path = tmp_path / "rs.mp4"
-    scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=bframes,
-                      weighted="implicit" if bframes else None, cabac=bframes, transform_8x8=bframes,
-                      cut_min_s=0.5, cut_max_s=1.5, gop_max_s=0.4, seed=29)
-    frames, _ = oracle.decode_full(path)
-    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
-    for wf in (0, 60):
-        with scene.VideoScorer(path, keep_frames=wf == 0, window_frames=wf, n_streams=2) as v:
-            assert v.general()
-            for second in (False, True):
-                if second:
-                    v.run()
-                res = v.score()
-                if wf == 0:
-                    got = np.stack([v.frame_nv12(i).reshape(frames[i].shape) for i in range(n)])
-                    assert _first_diff(got, frames) == []
-                assert np.array_equal(res.hist, ref["hist"])
-                assert np.array_equal(res.sad, ref["sad"])
-                assert np.array_equal(res.scores, ref["score"])
-
-
 @pytest.mark.parametrize("groups", [1, 2])
 def test_recycled_surfaces_equal_the_oracle(tmp_path, monkeypatch, groups):
     """Without keep_frames the general decoder recycles decoded-picture
     surfaces: a per-GOP-group liveness plan maps window slots to surfaces,
-    each level launch is thumbnailed on a side stream and the window's SADs
+    each level launch is thumbnailed right after it and the window's SADs
     come from the thumbnail ring.  Histograms, SADs, scores and RGB
     thumbnails equal the oracle in one window and in several windows on two
     rings, on a second run too; the session holds fewer surfaces than window

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build libvtseg variants that differ only in decode_full.hip compile-time
-# switches (VTS_EXP_*), for A/B timing on the GPU box: tools/exp/lib_<name>.so.
+# switches (-D flags of an experiment), for same-box A/B timing: tools/exp/lib_<name>.so.
 #   bash tools/exp/build_full_variants.sh name:-DFLAG ...
 set -e
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)

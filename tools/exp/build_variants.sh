@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build libvtseg variants that differ only in decode.hip compile-time switches
-# (VTS_EXP_*), for A/B timing on the GPU box: tools/exp/lib_<name>.so.
+# (-D flags of an experiment), for same-box A/B timing: tools/exp/lib_<name>.so.
 set -e
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 PKG=$ROOT/video-transformer_amd

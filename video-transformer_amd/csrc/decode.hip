@@ -110,11 +110,6 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 constexpr int kReconThreads = 256;
 
-// timing-only experiment switches (tools/exp): 1 no histogram, 2 no RGB
-// store, 4 no thumbnail scoring at all, 8 no BT.709 arithmetic
-#ifndef VTS_EXP_SKIP
-#define VTS_EXP_SKIP 0
-#endif
 #ifndef VTS_NT_LOAD
 #define VTS_NT_LOAD 0
 #endif
@@ -538,7 +533,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       pcm_src[threadIdx.x] = (mb < nmb && (c >> 62) == 1) ? (c & 0xffffffffffffull) : ~0ull;
   }
   if constexpr (K != 0) {
-    if constexpr (!(VTS_EXP_SKIP & 1)) lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
+    lds_hist[threadIdx.x] = 0;  // kReconThreads == 256
     __syncthreads();
   }
   if constexpr (kStage) {
@@ -699,7 +694,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
     for (int rr = 0; rr < KK; ++rr) st_row(dst + (mby * 16 + q * KK + rr) * F.pitch + m * 16, yr[rr]);
 #pragma unroll
     for (int rr = 0; rr < HK; ++rr) st_row(dst_uv + (mby * 8 + q * HK + rr) * F.pitch + m * 16, cr[rr]);
-    if constexpr (K != 0 && !(VTS_EXP_SKIP & 4)) {
+    if constexpr (K != 0) {
       uint32_t ys[G], us[G], vs[G];
 #pragma unroll
       for (int p = 0; p < G; ++p) ys[p] = us[p] = vs[p] = 0;
@@ -715,12 +710,12 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
         const uint32_t y = (ys[p] + K * K / 2) / (K * K);
         const uint32_t u = (us[p] + HK * HK / 2) / (HK * HK);
         const uint32_t v = (vs[p] + HK * HK / 2) / (HK * HK);
-        rgb24[p] = (VTS_EXP_SKIP & 8) ? (y | u << 8 | v << 16) : bt709_rgb24(y, u, v);
+        rgb24[p] = bt709_rgb24(y, u, v);
         packed[p / 4] |= y << (8 * (p & 3));
-        if (!(VTS_EXP_SKIP & 1)) atomicAdd(&lds_hist[y], 1u);
+        atomicAdd(&lds_hist[y], 1u);
       }
       const int64_t tpx = static_cast<int64_t>(mby * Q + q) * fa.w + m * G;
-      if (!(VTS_EXP_SKIP & 2)) store_rgb<G>(fa.rgb + (gframe * fa.w * fa.h + tpx) * 3, rgb24);
+      store_rgb<G>(fa.rgb + (gframe * fa.w * fa.h + tpx) * 3, rgb24);
       const int64_t npx = static_cast<int64_t>(fa.w) * fa.h;
       uint8_t *thumb = fa.thumb + static_cast<int64_t>(fr.x) * npx + tpx;
       if constexpr (G >= 4) {
@@ -752,7 +747,7 @@ __global__ void __launch_bounds__(kReconThreads) VTS_OCCUPANCY h264_recon_score(
       }
     }
   }
-  if constexpr (K != 0 && !(VTS_EXP_SKIP & 1)) {
+  if constexpr (K != 0) {
     __syncthreads();
     // two bins per 64-bit atomic (a frame's bin total stays below 2^32, so
     // the low count never carries into the high one): half the L2 atomics

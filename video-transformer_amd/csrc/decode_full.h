@@ -92,17 +92,6 @@ struct FullReconArgs {
   FullParams P;
 };
 
-// h264_recon_sched: every picture of a window, one persistent launch
-struct SchedArgs {
-  const int4 *pics;          // the window's pictures by dependency level: (ring slot, first entry in refs,
-                             // reference pictures, -)
-  const int32_t *refs;       // their reference pictures' ring slots (distinct per picture)
-  int32_t n_pics;
-  int32_t _pad;
-  uint32_t *next;            // ticket counter, zero before the launch
-  uint32_t *done;            // per ring slot: the run's epoch once the picture is reconstructed + deblocked
-};
-
 // 7.4.1 per slice NAL: the payload (after the header byte) without its
 // emulation-prevention bytes, at the same offset of rbsp; rbsp_len[i] = its
 // length.  Once per session: the parsers then read plain RBSP bits.
@@ -116,9 +105,5 @@ int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);
 // reconstruction (+ deblocking from bs_full_launch's descriptors when
 // a.deblock) of n_frames pictures of one level
 int recon_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s, hipEvent_t after_inter = nullptr);
-// every picture of a window by per-picture readiness (n_wg workgroups; a.dbk
-// holds n_wg descriptor slots); LDS it needs (<= 160 KiB or the launch fails)
-int recon_sched_launch(const FullReconArgs &a, const SchedArgs &sa, int n_wg, hipStream_t s);
-size_t recon_sched_lds_bytes(int mb_width, int mb_height);
 
 }  // namespace vts

@@ -32,67 +32,8 @@
 
 #include "common.h"
 #include "decode_full.h"
-#ifdef VTS_EXP_PROF
-// parse section timing (experiment builds): s_memtime deltas per section,
-// summed over all slices; read with vts_debug_parse_prof
-__device__ unsigned long long vts_prof_acc[8];
-// per workgroup of the last CABAC parse launch: start / end s_memtime and the
-// hardware id (s_getreg HW_ID: wave, SIMD, CU, SE / XCC bits), read with
-// vts_debug_parse_waves
-__device__ unsigned long long vts_wave_t[3 * 65536];
 #if !defined(__HIP_DEVICE_COMPILE__)
-#define VTS_PROF(k)
-#define VTS_PROF_P(p, k)
-#define VTS_PROF_FLUSH(p)
-#define VTS_PROF_START(p)
-#else
-#define VTS_PROF(k) prof_mark(k)
-#define VTS_PROF_P(p, k) (p).prof_mark(k)
-#define VTS_PROF_FLUSH(p)                                               \
-  for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&vts_prof_acc[k_], (p).sc->pacc[k_])
-#define VTS_PROF_START(p)                                               \
-  do {                                                                  \
-    for (int k_ = 0; k_ < 8; ++k_) (p).sc->pacc[k_] = 0;                \
-    (p).sc->pt = __builtin_amdgcn_s_memtime();                          \
-    (p).sc->psec = 0;                                                   \
-  } while (0)
 #endif
-#endif
-// Reconstruction section timing (VTS_EXP_RPROF experiment builds): per-wave
-// s_memtime deltas of h264_deblock_* [0, 8) and h264_intra_full [8, 16),
-// summed over every wave; read with vts_debug_recon_prof.  Other builds get
-// the no-op RProf.
-#ifdef VTS_EXP_RPROF
-__device__ unsigned long long vts_rprof_acc[16];
-struct RProf {
-  uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t t = 0;
-  __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
-  __device__ __forceinline__ void mark(int k) {
-    const uint64_t n = __builtin_amdgcn_s_memtime();
-    acc[k] += n - t;
-    t = n;
-  }
-  __device__ __forceinline__ void count(int k, int n) { acc[k] += static_cast<uint64_t>(n); }
-  __device__ __forceinline__ void flush(int base) {
-    if ((threadIdx.x & 63) == 0)
-      for (int k = 0; k < 8; ++k) atomicAdd(&vts_rprof_acc[base + k], acc[k]);
-  }
-};
-#else
-struct RProf {
-  __device__ __forceinline__ void start() {}
-  __device__ __forceinline__ void mark(int) {}
-  __device__ __forceinline__ void count(int, int) {}
-  __device__ __forceinline__ void flush(int) {}
-};
-#endif
-#define RPROF_DECL \
-  RProf rp_;       \
-  rp_.start()
-#define RPROF(k) rp_.mark(k)
-#define RPROF_COUNT(k, n) rp_.count(k, n)
-#define RPROF_FLUSH(base) rp_.flush(base)
 #include "parse_cabac.h"
 #include "parse_full.h"
 #include "derive_full.h"
@@ -185,9 +126,6 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
 __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_parse_full_cabac(FullParseArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t syn_lds[];
-#ifdef VTS_EXP_PROF
-  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-#endif
   const int i = a.order ? a.order[blockIdx.x] : static_cast<int>(blockIdx.x);
   const FullSlice &s = a.slices[i];
   const FullParams P = a.P;
@@ -198,14 +136,6 @@ __attribute__((amdgpu_waves_per_eu(VTS_PARSE_WAVES, VTS_PARSE_WAVES))) h264_pars
                                              s.ext >= 0 ? a.exts + s.ext : nullptr, a.arena, a.arena_top,
                                              a.arena_blocks, a.epoch, reinterpret_cast<full::SynScratch *>(syn_lds));
   if (e) atomicOr(a.err, e);
-#ifdef VTS_EXP_PROF
-  if (threadIdx.x == 0 && blockIdx.x < 65536) {
-    vts_wave_t[3 * blockIdx.x] = t_start;
-    vts_wave_t[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime();
-    vts_wave_t[3 * blockIdx.x + 2] = static_cast<unsigned long long>(i) |
-                                     (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))) << 32);
-  }
-#endif
 }
 
 // One workgroup per picture, one lane per macroblock row: at step t row y
@@ -804,7 +734,7 @@ __device__ __forceinline__ void lane_sync() {
 // arguments' address, which copies them to scratch and turns every field read
 // into a scratch load)
 __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int mb, int b, IntraTile &t,
-                                         const uint8_t *s_off4, const uint8_t *s_off8, RProf &rp_) {
+                                         const uint8_t *s_off4, const uint8_t *s_off8) {
   const int mbw = a.P.mb_width, nmb = mbw * a.P.mb_height;
   const MbRec *frecs = a.recs + static_cast<int64_t>(slot) * nmb;
   const MbRec *rec = frecs + mb;
@@ -869,7 +799,6 @@ __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int m
     }
   }
   lane_sync();
-  RPROF(3);
   const int qp = h.qp;
   if (h.type == kMbI16) {
     const int mode = h.modes & 3;
@@ -1102,7 +1031,6 @@ __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int m
       lane_sync();
     }
   }
-  RPROF(4);
   // chroma (8.3.4): lanes 0..7 = (plane, 4x4 block)
   if (b < 8) {
     const int pl = b >> 2, ck = b & 3, ox = (ck & 1) * 4, oy = (ck >> 1) * 4;
@@ -1169,7 +1097,6 @@ __device__ __forceinline__ void intra_mb(const FullReconArgs &a, int slot, int m
     *reinterpret_cast<uint4 *>(UV + crow0 + static_cast<int64_t>(b) * pitch) = row;
   }
   lane_sync();
-  RPROF(5);
 }
 
 // grid: pictures of the level; the intra-predicted macroblocks by dependency level
@@ -1184,7 +1111,6 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
   const int slot = a.frames[blockIdx.x].x;
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;
-  RPROF_DECL;
   if (tid == 0) s_max = -1;
   if (tid < 9 * 16) s_off4[tid] = static_cast<uint8_t>(intra4_off(tid >> 4, tid & 3, (tid >> 2) & 3));
   for (int i = tid; i < 9 * 64; i += kIntraThreads) s_off8[i] = static_cast<uint8_t>(intra8_off(i >> 6, i & 7, (i >> 3) & 7));
@@ -1222,7 +1148,6 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
     }
     __syncthreads();
   }
-  RPROF(0);
   for (int l = 0; l <= maxl; ++l) {
     int j0, j1;
     if (bucketed) {
@@ -1238,15 +1163,10 @@ __global__ void __launch_bounds__(kIntraThreads) h264_intra_full(FullReconArgs a
       j1 = __builtin_amdgcn_readfirstlane(s_cnt);
     }
     for (int j = j0 + ms; j < j1; j += kIntraSlots) {
-      intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4, s_off8, rp_);
-      RPROF_COUNT(7, 1);
+      intra_mb(a, slot, s_list[j], b, tiles[ms], s_off4, s_off8);
     }
-    RPROF(1);
     __syncthreads();
-    RPROF(2);
-    RPROF_COUNT(6, 1);
   }
-  RPROF_FLUSH(8);
 }
 
 // ---- intra, lane-parallel (default; VTS_INTRA=1 runs h264_intra_full)
@@ -1327,7 +1247,6 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
   }
   const uint16_t *lv = a.ilvl + static_cast<int64_t>(slot) * nmb;
   const int tid = threadIdx.x;
-  RPROF_DECL;
   if (tid == 0) s_max = -1;
   if (tid < 9 * 16) s_off4[tid] = static_cast<uint8_t>(intra4_off(tid >> 4, tid & 3, (tid >> 2) & 3));
   for (int i = tid; i < 9 * 64; i += kI2Threads) s_off8[i] = static_cast<uint8_t>(intra8_off(i >> 6, i & 7, (i >> 3) & 7));
@@ -1342,6 +1261,7 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
   int maxl = __builtin_amdgcn_readfirstlane(s_max);  // uniform: the loops below hold barriers
   const int g = tid >> 5;
   const DevLanes lanes0{tid & 31};
+  i2::I2NoProf rp_;
   i2::I2Ctx ctx;
   ctx.recs = a.recs + static_cast<int64_t>(slot) * nmb;
   ctx.arena = a.arena;
@@ -1475,7 +1395,6 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
     pv = jf >= 0;
     if (pv) pre = i2::i2_prefetch(ctx, s_list[jf], lanes0.t);
   }
-  RPROF(0);
   for (int l = 0; l <= maxl; ++l) {
     int j0, j1;
     if (bucketed) {
@@ -1510,23 +1429,16 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
         pre = i2::I2Pre{};
         pv = false;
       }
-      RPROF(1);
       __syncthreads();
-      RPROF(2);
       if (j < j1) {
         i2::intra2_finish(ctx, lanes, tiles[g], lcol, lrow, s_off4, s_off8, rp_);
-        RPROF_COUNT(7, 1);
         const int jn = !bucketed ? -1 : (j + kI2Groups < j1 ? j + kI2Groups : first_at(l + 1));
         pv = jn >= 0;
         if (pv) pre = i2::i2_prefetch(ctx, s_list[jn], lanes.t);
       }
-      RPROF(1);
       __syncthreads();
-      RPROF(2);
     }
-    RPROF_COUNT(6, 1);
   }
-  RPROF_FLUSH(8);
 }
 // grid: pictures of the level; dynamic LDS: i2_lds_bytes
 __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
@@ -1732,24 +1644,6 @@ constexpr int dbk_hrow(int j) {
 
 }  // namespace
 
-#ifdef VTS_EXP_RPROF
-extern "C" int vts_debug_recon_prof(unsigned long long *out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_rprof_acc), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
-  unsigned long long z[16] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(vts_rprof_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif
-#ifdef VTS_EXP_PROF
-extern "C" int vts_debug_parse_waves(unsigned long long *out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_wave_t), sizeof(unsigned long long) * 3 * static_cast<size_t>(n)) == hipSuccess
-             ? 0 : -1;
-}
-extern "C" int vts_debug_parse_prof(unsigned long long *out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vts_prof_acc), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
-  unsigned long long z[8] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(vts_prof_acc), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 int nal_unescape_launch(const uint8_t *es, uint8_t *rbsp, const FullSlice *slices, int32_t n_slices,
                         int32_t *rbsp_len, hipStream_t s) {
@@ -1842,7 +1736,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
   const int row = kLuma ? l : min(l, 7);
   Tile &t = tiles[wave * 4 + grp];
   constexpr int vq = kLuma ? 2 : 4, hq = kLuma ? 3 : 5;
-  RPROF_DECL;
   for (int p = wave; 4 * p < mbh; p += kDbkWaves) {
     const int y = 4 * p + grp;
     const bool row_ok = y < mbh;
@@ -1878,7 +1771,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
       // a wave's first row waits for the previous wave's last row; its last
       // row waits until it may overwrite ring column x (the next wave's first
       // row read column x - kDpRingCols)
-      RPROF(4);  // loop head + next macroblock's loads issued
       if (act) {
         const int need_up = (grp == 0 && y > 0) ? (x + 1 < mbw ? x + 2 : mbw + 1) : -(1 << 30);
         const int need_dn = (grp == 3 && y + 1 < mbh) ? x - kDpRingCols + 1 : -(1 << 30);
@@ -1888,10 +1780,7 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           __builtin_amdgcn_s_sleep(1);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      RPROF(0);  // waits on the rows above / below
       const bool still = (bsw.x | bsw.y | bsw.z | bsw.w) == 0u;
-      RPROF_COUNT(7, 1);
-      RPROF_COUNT(6, still ? 1 : 0);
       constexpr int kAbove = kLuma ? 4 : 2;  // rows above from the ring
       auto load_above = [&]() {
         if (act && l < kAbove && y > 0) {
@@ -1928,7 +1817,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           *reinterpret_cast<uint32_t *>(dst + 4 * i) = pack4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
       }
       lane_sync();
-      RPROF(1);  // ring lines in, vertical edges (and this step's loads' latency)
       // ---- horizontal edges: lane = sample column (chroma: interleaved byte column)
       if (act && !still) {
         const int pl = l & 1, seg = l >> 2;
@@ -1971,7 +1859,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
         }
       }
       lane_sync();
-      RPROF(2);  // horizontal edges
       // ---- write back: this macroblock's rows shifted 4 bytes left except the
       // ones the row below finishes (luma 13..15, chroma 7), the ring lines for
       // the row below, the rows above that this macroblock's top edge finished
@@ -2031,7 +1918,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
           *reinterpret_cast<uint4 *>(at(o + static_cast<uint32_t>(x * 16))) = v;
         }
       }
-      RPROF(3);  // write back, ring lines out, rows above
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_wave_barrier();
       if (act && l == 0) {
@@ -2039,7 +1925,6 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
       }
     }
   }
-  RPROF_FLUSH(0);
 }
 // grid: 2 x pictures of the level (even blocks luma, odd chroma)
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs a) {
@@ -2050,118 +1935,6 @@ __global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs 
   const int4 f = a.frames[blockIdx.x >> 1];
   if ((blockIdx.x & 1) == 0) dp_plane<true>(a, f.x, f.y, lds, prog);
   else dp_plane<false>(a, f.x, f.y, lds, prog);
-}
-
-// ------------------------------------------------ per-picture scheduler
-// (VTS_RECON_SCHED=1; measured slower than the level launches)
-// One launch per window instead of three launches per reconstruction level:
-// a persistent grid (one 1024-thread workgroup per compute unit) whose
-// workgroups take the window's pictures by ticket in dependency-level order,
-// wait for that picture's reference pictures to be finished (per-slot flags
-// set to the run's epoch with agent-scope release / acquire), then run the
-// whole picture: inter prediction + residuals and its deblocking descriptors
-// (16 lanes per macroblock, h264_inter_full / h264_bs_full's code), the intra
-// macroblocks by dependency level (h264_intra_v2's), the deblocking of luma
-// then chroma (h264_deblock_plane's), and flag it.  A picture starts as soon
-// as its own references are done, not when a whole level of every GOP is.
-// Deadlock-free: a workgroup takes a ticket only when it runs, and waits only
-// on lower tickets, so the lowest unfinished ticket never waits.  A wait that
-// does not end in ~2^26 polls (a bug, not a schedule) flags DEC_E_SCHED and
-// goes on, so the grid always drains.
-constexpr int kRsThreads = 1024;
-static_assert(kRsThreads == kI2Threads && kRsThreads == kDbkThreads, "the phases share the workgroup");
-__host__ __device__ constexpr size_t rs_dbk_lds_bytes() { return (kDpLds + 15) / 16 * 16 + sizeof(int) * 1024; }
-// The phases are calls, not inlined: register allocation then stays per
-// phase (inlined into the one ticket loop, each phase's per-lane constants
-// were hoisted out of it and live across all of them: 241 VGPRs spilled).
-#define VTS_RS_PHASE __device__ __attribute__((noinline))
-VTS_RS_PHASE void rs_inter(const FullReconArgs &a, int slot, int di, int nmb) {
-  for (int base = 0; base < nmb * 16; base += kRsThreads) {
-    const int idx = base + static_cast<int>(threadIdx.x);
-    inter_mb(a, slot, idx >> 4, idx & 15);
-  }
-}
-VTS_RS_PHASE void rs_bs(const FullReconArgs &a, int slot, int di, int nmb) {
-  for (int base = 0; base < nmb * 16; base += kRsThreads) {  // every lane (a macroblock's 16 meet in a butterfly)
-    const int idx = base + static_cast<int>(threadIdx.x);
-    bs_mb(a, slot, di, idx >> 4, idx & 15);
-  }
-}
-VTS_RS_PHASE void rs_intra(const FullReconArgs &a, int slot, uint8_t *lds) {
-  intra_v2_picture(a, slot, lds);
-}
-template <bool kLuma>
-VTS_RS_PHASE void rs_deblock(const FullReconArgs &a, int slot, int di, uint8_t *lds, int *prog) {
-  dp_plane<kLuma>(a, slot, di, lds, prog);
-}
-__global__ void __launch_bounds__(kRsThreads) h264_recon_sched(FullReconArgs a, SchedArgs sa) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t rlds[];
-  __shared__ int s_t;
-  const int tid = static_cast<int>(threadIdx.x);
-  const int mbw = a.P.mb_width, mbh = a.P.mb_height, nmb = mbw * mbh;
-  int *prog = reinterpret_cast<int *>(rlds + (kDpLds + 15) / 16 * 16);
-  const int di = static_cast<int>(blockIdx.x);  // this workgroup's descriptor slot in a.dbk
-  // The ticket: fetched by lane 0, broadcast through LDS, read as a uniform
-  // value, and the loop tested at its head only.  (With the fetch at the head
-  // and a break after it, the compiler made the loop exit divergent and,
-  // in its exec-mask bookkeeping, retired lane 0 after the first picture:
-  // the other lanes went on with a ticket nobody fetched any more.)
-  if (tid == 0) s_t = static_cast<int>(atomicAdd(sa.next, 1u));
-  __syncthreads();
-  int t = __builtin_amdgcn_readfirstlane(s_t);
-  while (t < sa.n_pics) {
-    const int4 pic = sa.pics[t];
-    const int slot = pic.x;
-    if (tid < pic.z) {  // the reference pictures (lower tickets)
-      const int r = sa.refs[pic.y + tid];
-      uint32_t spins = 0;
-      while (__hip_atomic_load(&sa.done[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) {
-        if (++spins > (1u << 26)) {
-          atomicOr(a.err, static_cast<uint32_t>(DEC_E_SCHED));
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // their samples, across XCD L2s
-    rs_inter(a, slot, di, nmb);
-    rs_bs(a, slot, di, nmb);
-    __syncthreads();
-    rs_intra(a, slot, rlds);
-    __syncthreads();
-    for (int i = tid; i < mbh; i += kRsThreads) prog[i] = 0;
-    __syncthreads();
-    rs_deblock<true>(a, slot, di, rlds, prog);
-    __syncthreads();
-    for (int i = tid; i < mbh; i += kRsThreads) prog[i] = 0;
-    __syncthreads();
-    rs_deblock<false>(a, slot, di, rlds, prog);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // every wave's samples out before the flag
-    __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_store(&sa.done[slot], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_t = static_cast<int>(atomicAdd(sa.next, 1u));
-    }
-    __syncthreads();
-    t = __builtin_amdgcn_readfirstlane(s_t);
-  }
-}
-
-size_t recon_sched_lds_bytes(int mb_width, int mb_height) {
-  const size_t a = i2_lds_bytes(mb_width, mb_height), b = rs_dbk_lds_bytes();
-  return a > b ? a : b;
-}
-
-int recon_sched_launch(const FullReconArgs &a, const SchedArgs &sa, int n_wg, hipStream_t s) {
-  if (sa.n_pics <= 0) return VTS_OK;
-  if (a.P.mb_height > 1024) return fail(VTS_E_UNSUPPORTED, "picture taller than 1024 macroblock rows");
-  const size_t lds = recon_sched_lds_bytes(a.P.mb_width, a.P.mb_height);
-  if (lds > 160 * 1024) return fail(VTS_E_UNSUPPORTED, "picture too large for the per-picture scheduler's LDS");
-  hipLaunchKernelGGL(h264_recon_sched, dim3(static_cast<unsigned>(n_wg)), dim3(kRsThreads), lds, s, a, sa);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(VTS_E_HIP, "h264_recon_sched launch: %s", hipGetErrorString(e));
-  return VTS_OK;
 }
 
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {

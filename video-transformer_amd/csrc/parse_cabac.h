@@ -90,9 +90,8 @@ VTS_HD VTS_INLINE int abs_off(int cat) { return static_cast<int>((0x271E140A00ul
 // compute unit) instead of the one scalar unit that every wave of the compute
 // unit shares, which the parser saturates; a decision's outcome, next state
 // and renormalisation shift come back to the scalar side by readfirstlane
-// (CABAC B parse -4 % same-box, profiles/r03_cabac_vgpr_engine_ab.txt;
-// VTS_EXP_SENGINE keeps the scalar engine)
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(VTS_EXP_SENGINE)
+// (CABAC B parse -4 % same-box, profiles/r03_cabac_vgpr_engine_ab.txt)
+#if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint32_t vts_in_vgpr(uint32_t x) {
   uint32_t r;
   asm("; engine state in a VGPR" : "=v"(r) : "0"(x));
@@ -144,10 +143,6 @@ struct SynScratch {
   // 1..4 = the current macroblock's 4x4 blocks
   uint8_t mvx[2][5][5][2];
   SynEdge left;                 // the previous macroblock's right edge
-#ifdef VTS_EXP_PROF
-  uint64_t pacc[8], pt;
-  int32_t psec;
-#endif
 };
 VTS_HD VTS_INLINE size_t syn_lds_bytes(int mb_width) {
   return (sizeof(SynScratch) + 15) / 16 * 16 + sizeof(SynEdge) * static_cast<size_t>(mb_width);
@@ -202,14 +197,6 @@ struct CabacSyn {
   }
 #else
   void refresh_lane() {}
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && defined(VTS_EXP_PROF)
-  __device__ VTS_INLINE void prof_mark(int k) const {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    sc->pacc[sc->psec] += t - sc->pt;
-    sc->pt = t;
-    sc->psec = k;
-  }
 #endif
   static VTS_HD VTS_INLINE int ctx_tab(int c) { return (c >= 85 && c <= 275) ? 0 : 1; }
   static VTS_HD VTS_INLINE int ctx_slot(int c) { return c >= 399 ? c - 314 : (c >= 85 ? c - 85 : c); }
@@ -807,7 +794,6 @@ struct CabacSyn {
   // ------------------------------------------------------ macroblock_layer
   // (begin_mb done by the caller); returns false to stop the slice
   VTS_HD VTS_INLINE bool mb_cabac(int *qp) {
-    VTS_PROF(2);
     MbRec &m = cur();
     const bool is_b = s->is_p == kSliceB;
     int itype, mb_type = 0;
@@ -868,7 +854,6 @@ struct CabacSyn {
       cbp = ((((itype - 1) / 4) % 3) << 4) | (itype >= 13 ? 15 : 0);
       m.modes = static_cast<uint8_t>((itype - 1) % 4);
     } else {  // inter (Tables 7-13, 7-14, 7-17, 7-18)
-      VTS_PROF(3);
       m.type = kMbInter;
       uint8_t pm[4] = {0, 0, 0, 0}, sub[4] = {0, 0, 0, 0};
       int shape;
@@ -914,7 +899,6 @@ struct CabacSyn {
       }
       if (shape >= 0 && !inter_syntax(shape, pm, sub)) return false;
     }
-    VTS_PROF(2);
     if (m.type == kMbI4x4 || m.type == kMbI16) {  // intra_chroma_pred_mode, TU cMax 3
       int cm = 0;
       if (dec(64 + ((fa & kEChroma) ? 1 : 0) + ((fb & kEChroma) ? 1 : 0))) {
@@ -926,7 +910,6 @@ struct CabacSyn {
       }
       m.modes = static_cast<uint8_t>(m.modes | (cm << 2));
     }
-    VTS_PROF(4);
     if (m.type != kMbI16) {  // coded_block_pattern (9.3.3.1.1.4)
       const int ca_cbp = ecbp(fa), cb_cbp = ecbp(fb);
       for (int b8 = 0; b8 < 4; ++b8) {
@@ -981,7 +964,6 @@ struct CabacSyn {
     if (cbp >> 4) todo |= 3u << kBlkChromaDc0;
     if ((cbp >> 4) == 2) todo |= 255u << kBlkChromaAc0;
     if (todo && !reserve(kMbMaxBlocks)) return false;
-    VTS_PROF(5);
     while (todo) {
       const uint32_t bt = static_cast<uint32_t>(__builtin_ctz(todo));
       todo &= todo - 1u;
@@ -1045,7 +1027,6 @@ struct CabacSyn {
         store_block(bt, sc->blk);
       }
     }
-    VTS_PROF(6);
     if (br.err || cab_consumed() > 8 * br.size) {
       err |= DEC_E_SYNTAX;
       return false;
@@ -1096,7 +1077,6 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   // cabac_alignment_one_bit
   while (p.br.consumed() & 7)
     if (!p.br.bit()) return DEC_E_SYNTAX;
-  VTS_PROF_START(p);
   p.cab_tables();
   p.cab_init(!s.is_p, s.qp);
   p.cab_start();
@@ -1107,29 +1087,23 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
       break;
     }
     p.refresh_lane();
-    VTS_PROF_P(p, 1);
     p.begin_mb(addr);
-    VTS_PROF_P(p, 2);
     bool skip = false;
     if (s.is_p)
       skip = p.dec((s.is_p == kSliceB ? 24 : 11) + (p.av_a && CabacSyn::etype(p.fa) != kMbSkip ? 1 : 0) +
                    (p.av_b && CabacSyn::etype(p.fb) != kMbSkip ? 1 : 0)) != 0;
     if (skip) {
       VTS_PARSE_TRACE(s.is_p == kSliceB ? 4 : 5);
-      VTS_PROF_P(p, 3);
       p.emit_skip(addr, qp, s.is_p == kSliceB);
       p.prev_qpd = false;
     } else {
       p.init_mb(addr);
       if (!p.mb_cabac(&qp) || p.err) break;  // one inlined copy for every slice type
-      VTS_PROF_P(p, 6);
       p.end_mb(addr);
     }
     ++addr;
     if (p.term()) break;  // end_of_slice_flag
   }
-  VTS_PROF_P(p, 7);
-  VTS_PROF_FLUSH(p);
   // the arithmetic decoder has read through the stop bit
   if (!p.err && (p.br.err || p.cab_consumed() != stop_bit + 1)) p.err |= DEC_E_SYNTAX;
   return p.err;

@@ -23,13 +23,6 @@
 #ifndef VTS_PARSE_TRACE
 #define VTS_PARSE_TRACE(...)
 #endif
-// section markers of the parse (VTS_EXP_PROF builds time them: decode_full.hip)
-#ifndef VTS_PROF
-#define VTS_PROF(k)
-#define VTS_PROF_P(p, k)
-#define VTS_PROF_FLUSH(p)
-#define VTS_PROF_START(p)
-#endif
 
 namespace vts {
 namespace full {
@@ -373,10 +366,6 @@ struct FullScratch {
   // column of the one to the left (0 where unavailable / not inter), rows and
   // cols 1..4 = the current macroblock's 4x4 blocks
   uint8_t mvx[2][5][5][2];
-#ifdef VTS_EXP_PROF
-  uint64_t pacc[8], pt;
-  int32_t psec;
-#endif
 };
 
 typedef uint32_t u32x4 __attribute__((vector_size(16)));  // SROA-friendly (uint4 copies are memmoves)
@@ -429,14 +418,6 @@ struct Parser {
   int direct8x8;          // direct_8x8_inference_flag
   uint32_t todo;          // residual blocks of the current macroblock still to decode (kBlk* bits)
   bool cur_i16;           // the current macroblock is Intra_16x16
-#if defined(__HIP_DEVICE_COMPILE__) && defined(VTS_EXP_PROF)
-  __device__ VTS_INLINE void prof_mark(int k) const {
-    const uint64_t t = __builtin_amdgcn_s_memtime();
-    sc->pacc[sc->psec] += t - sc->pt;
-    sc->pt = t;
-    sc->psec = k;
-  }
-#endif
 
   // --- neighbour access (6.4.12): mb -1 unavailable, -2 the current MB
   VTS_HD VTS_INLINE int nb_mb(int cur, int xN, int yN, int maxW, int *xw, int *yw) const {

@@ -84,12 +84,7 @@ struct WinBitsT {
         // scalar loads from `pb - sh` the compiler once formed an SMEM base of
         // (aligned - 1) + offset 1, which reads the wrong dword; volatile
         // loads, the earlier cure, waited for memory one dword at a time)
-#if defined(__HIP_DEVICE_COMPILE__) && defined(VTS_EXP_BITS_GLOBAL)
-        typedef const __attribute__((address_space(1))) uint32_t gu32;  // global, not flat
-#else
-        typedef const uint32_t gu32;
-#endif
-        gu32 *w = reinterpret_cast<gu32 *>(reinterpret_cast<uintptr_t>(pb) & ~uintptr_t(3));
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(pb) & ~uintptr_t(3));
 #pragma unroll
         for (int k = 0; k <= kW; ++k) t[k] = w[k];
       } else {

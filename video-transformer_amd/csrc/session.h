@@ -45,7 +45,6 @@ struct Window {
   std::vector<int32_t> plv_end;    // general decoder: parse launch j covers window slices
                                    // [plv_end[j-1], plv_end[j]) (B pictures after their colocated picture)
   int64_t ds0 = 0;                 // general decoder, CABAC: the window's entries in vts_ctx::dslots
-  int64_t rs0 = 0;                 // general decoder: the window's pictures in vts_ctx::rs_pics
   std::vector<int32_t> dlv_end;    // ... h264_derive launch j covers entries [dlv_end[j-1], dlv_end[j])
 };
 
@@ -192,40 +191,21 @@ struct vts_ctx {
   std::vector<int32_t> pneed;           // per window frame (ring slot): slices of the picture
   int32_t *d_pneed = nullptr;
   uint32_t *d_pdone[2] = {nullptr, nullptr};  // per ring: slices done per slot (merged parse)
-  // per-picture reconstruction scheduler (h264_recon_sched, VTS_RECON_SCHED=1;
-  // measured slower than the per-level launch chain, the default — DESIGN.md
-  // §9): pictures by dependency level (slot, first ref, ref count), their
-  // reference pictures' slots, the launch's ticket counter, per ring slot the
-  // epoch of the run that finished it, workgroups per launch
-  bool recon_sched = false;
-  std::vector<int4> rs_pics;
-  std::vector<int32_t> rs_refs;
-  int4 *d_rs_pics = nullptr;
-  int32_t *d_rs_refs = nullptr;
-  uint32_t *d_rs_next = nullptr;
-  uint32_t *d_rs_done[2] = {nullptr, nullptr};
-  int rs_wg = 0;
   std::vector<int2> dslots;             // CABAC: the windows' pictures by parse level (h264_derive): ring slot,
                                         // common colocated slot
   int2 *d_dslots = nullptr;
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full (its LDS fallback)
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<hipEvent_t> ev_bs;  // paced bS: two per level launch of a window (reused window to window)
-  // recycled surfaces (keep_frames 0, no transcode, per-level launches, at most
-  // two GOP groups): a picture's surface goes back to its group's pool once
-  // the last picture predicting from it is reconstructed and its own level is
-  // thumbnailed: thumb_pics right after the level on the group's own stream
-  // (surf_inline), or on s_grp[kSurfThumbStream] with the group surf_lag
-  // levels behind it (VTS_SURF_THUMB=side, VTS_SURF_LAG);
-  // surf_of[frame] = surface of the frame's window slot, surf_count per ring
-  static constexpr int kSurfThumbStream = 1;
+  // recycled surfaces (keep_frames 0, no transcode): a picture's surface
+  // goes back to its GOP group's pool once the last picture predicting from it
+  // is reconstructed and its own level is thumbnailed (thumb_pics right after
+  // the level on the group's own stream); surf_of[frame] = surface of the
+  // frame's window slot, surf_count per ring
   bool surf_pool = false;
-  bool surf_inline = true;
-  int surf_lag = 0;
   std::vector<int32_t> surf_of;
   int32_t *d_surf_of = nullptr;
   int64_t surf_count = 0;
-  std::vector<hipEvent_t> ev_th;  // per level launch: (reconstructed, thumbnailed), + window end
   std::vector<int64_t> disp;            // presentation rank of each sample (decode order)
   uint16_t *d_ilvl[2] = {nullptr, nullptr};  // intra dependency level per macroblock
   vts::DbkInfo *d_dbk[2] = {nullptr, nullptr};  // deblocking descriptor per macroblock

@@ -138,13 +138,18 @@ int read_threads() {  // 8; VTS_READ_THREADS: 1..64 (measurement)
 struct FileMap {
   const uint8_t *p = nullptr;
   int64_t n = 0;
+  // VTS_OK with p null: not a regular file (the caller reads it instead)
   int open(const char *path) {
     const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return fail(VTS_E_IO, "cannot open %s", path);
     struct stat st {};
-    if (::fstat(fd, &st) != 0 || st.st_size <= 0) {
+    if (::fstat(fd, &st) != 0) {
       ::close(fd);
       return fail(VTS_E_IO, "cannot stat %s", path);
+    }
+    if (!S_ISREG(st.st_mode) || st.st_size <= 0) {
+      ::close(fd);
+      return VTS_OK;
     }
     void *m = ::mmap(nullptr, static_cast<size_t>(st.st_size), PROT_READ, MAP_PRIVATE, fd, 0);
     ::close(fd);
@@ -435,32 +440,9 @@ int alloc_general(vts_ctx *c) {
   HIP_TRY(vts::dmalloc(&c->d_levels, sizeof(int4) * std::max<size_t>(1, c->level_frames.size())));
   HIP_TRY(hipMemcpy(c->d_levels, c->level_frames.data(), sizeof(int4) * c->level_frames.size(), hipMemcpyHostToDevice));
   const int64_t nmb = static_cast<int64_t>(c->sps.mb_width) * c->sps.mb_height;
-  // the per-picture reconstruction scheduler where its LDS fits (else the
-  // per-level launch chain): one workgroup per compute unit it can hold
-  // (capped at the ring), each with its own deblocking descriptors
-  if (const char *e = std::getenv("VTS_RECON_SCHED")) c->recon_sched = std::atoi(e) != 0;
-  if (recon_sched_lds_bytes(c->sps.mb_width, c->sps.mb_height) > 160 * 1024 || c->sps.mb_height > 1024)
-    c->recon_sched = false;
-  if (c->recon_sched && c->surf_pool) return fail(VTS_E_INVALID, "recycled surfaces planned with the per-picture scheduler");
   if (c->surf_pool) {
     HIP_TRY(vts::dmalloc(&c->d_surf_of, sizeof(int32_t) * c->surf_of.size()));
     HIP_TRY(hipMemcpy(c->d_surf_of, c->surf_of.data(), sizeof(int32_t) * c->surf_of.size(), hipMemcpyHostToDevice));
-  }
-  if (c->recon_sched) {
-    int ncu = 0;
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-    c->rs_wg = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ncu, c->ring_frames)));
-    c->dbk_pics = c->rs_wg;
-    auto up = [](void **d, const void *h, size_t n) -> hipError_t {
-      if (*d) vts::dfree(*d);
-      *d = nullptr;
-      hipError_t e = vts::dmalloc(d, std::max<size_t>(4, n));
-      if (e == hipSuccess && n) e = hipMemcpy(*d, h, n, hipMemcpyHostToDevice);
-      return e;
-    };
-    HIP_TRY(up(reinterpret_cast<void **>(&c->d_rs_pics), c->rs_pics.data(), sizeof(int4) * c->rs_pics.size()));
-    HIP_TRY(up(reinterpret_cast<void **>(&c->d_rs_refs), c->rs_refs.data(), sizeof(int32_t) * c->rs_refs.size()));
-    HIP_TRY(up(reinterpret_cast<void **>(&c->d_rs_next), nullptr, 0));
   }
   c->ws_bytes = score_workspace_bytes(c->width, c->height, c->k, c->ring_frames);
   const int64_t tw = (c->width / c->k) * (c->height / c->k);
@@ -470,10 +452,6 @@ int alloc_general(vts_ctx *c) {
       HIP_TRY(vts::dmalloc(&c->d_recs1[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(MbRecB)));
     HIP_TRY(vts::dmalloc(&c->d_ilvl[r], static_cast<size_t>(c->ring_frames * nmb) * sizeof(uint16_t)));
     HIP_TRY(vts::dmalloc(&c->d_pdone[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
-    if (c->recon_sched) {  // done flags: zero, never an epoch (runs count from 1)
-      HIP_TRY(vts::dmalloc(&c->d_rs_done[r], sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
-      HIP_TRY(hipMemset(c->d_rs_done[r], 0, sizeof(uint32_t) * static_cast<size_t>(std::max<int64_t>(1, c->ring_frames))));
-    }
     HIP_TRY(vts::dmalloc(&c->d_dbk[r], static_cast<size_t>(c->dbk_pics * nmb) * sizeof(DbkInfo)));
     HIP_TRY(vts::dmalloc(&c->d_arena[r], static_cast<size_t>(std::max<int64_t>(1, c->arena_blocks)) * 32 + kPad));
     HIP_TRY(vts::dmalloc(&c->d_surf[r], static_cast<size_t>((c->surf_pool ? c->surf_count : c->ring_frames) * c->frame_stride + kPad)));
@@ -722,8 +700,10 @@ int build(vts_ctx *c, const Mp4Info &mp4, const uint8_t *mem, int64_t mem_size, 
   // buffer — 7 GB for a 2-h 720p video, its pages faulted in fresh — was
   // most of the read).  The general decoder's host schedule reads the whole
   // ES, so it gets the host copy (made from the mapping if the first slices
-  // send an auto stream there after all).
-  if (may_subset && !mem && !std::getenv("VTS_OPEN_COPY")) VTS_TRY(fmap.open(path));
+  // send an auto stream there after all).  Only regular files are mapped (a
+  // pipe or device is read with pread), and the file must not shrink while
+  // vts_open runs (a mapped page past a new end faults).
+  if (may_subset && !mem) VTS_TRY(fmap.open(path));
   const uint8_t *src_mem = fmap.p ? fmap.p : mem;
   const int64_t src_size = fmap.p ? fmap.n : mem_size;
   VTS_TRY(gather_samples(t, src_mem, src_size, path, fmap.p ? nullptr : &es, &es_off, &hooks));
@@ -1659,9 +1639,6 @@ extern "C" int vts_close(vts_ctx *c) {
   f(c->d_porder_m);
   f(c->d_pneed);
   f(c->d_dslots);
-  f(c->d_rs_pics);
-  f(c->d_rs_refs);
-  f(c->d_rs_next);
   f(c->d_surf_of);
   f(c->d_arena_top);
   for (int r = 0; r < 2; ++r) {
@@ -1669,7 +1646,6 @@ extern "C" int vts_close(vts_ctx *c) {
     f(c->d_recs1[r]);
     f(c->d_ilvl[r]);
     f(c->d_pdone[r]);
-    f(c->d_rs_done[r]);
     f(c->d_dbk[r]);
     f(c->d_arena[r]);
   }
@@ -1678,8 +1654,6 @@ extern "C" int vts_close(vts_ctx *c) {
   for (auto e : c->lev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->ev_bs)
-    if (e) (void)hipEventDestroy(e);
-  for (auto e : c->ev_th)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);

@@ -227,23 +227,15 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
   c->porder_m.clear();
   c->pneed.clear();
   c->dslots.clear();
-  c->rs_pics.clear();
-  c->rs_refs.clear();
   c->level_frames.clear();
   c->arena_blocks = 0;
   c->arena_bound = 0;
   c->arena_reruns = 0;
   // recycled surfaces: only where no caller reads a decoded frame back (no
-  // keep_frames, no transcode yet) and the reconstruction is the per-level
-  // chain of at most two GOP groups (the thumbnail stream is s_grp[1])
+  // keep_frames, no transcode yet); VTS_SURF_POOL=0 keeps one surface per slot
   {
-    const char *sp = std::getenv("VTS_SURF_POOL"), *rs = std::getenv("VTS_RECON_SCHED");
-    const char *th = std::getenv("VTS_SURF_THUMB"), *lg = std::getenv("VTS_SURF_LAG");
-    c->surf_inline = !(th && std::strcmp(th, "side") == 0);
-    c->surf_lag = c->surf_inline ? 0 : (lg ? std::max(0, std::atoi(lg)) : 3);
-    c->surf_pool = c->params.keep_frames == 0 && !c->small.on &&
-                   (c->surf_inline || c->general_groups <= vts_ctx::kSurfThumbStream + 1) &&
-                   !(sp && std::atoi(sp) == 0) && !(rs && std::atoi(rs) != 0);
+    const char *sp = std::getenv("VTS_SURF_POOL");
+    c->surf_pool = c->params.keep_frames == 0 && !c->small.on && !(sp && std::atoi(sp) == 0);
   }
   c->surf_of.assign(static_cast<size_t>(c->surf_pool ? n : 0), 0);
   c->surf_count = 0;
@@ -363,28 +355,6 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       }
       w.dlv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->dslots.size()) - w.ds0));
     }
-    // the per-picture scheduler's list: the window's pictures by dependency
-    // level (then decoding order), each with its reference pictures' slots.
-    // Level order, not decoding order: a GOP is a chain, and tickets in
-    // decoding order would hand the grid one GOP's chain at a time (measured:
-    // 40x slower than the level launches); by level, the GOPs' chains advance
-    // side by side and a reference always holds a lower ticket.
-    w.rs0 = static_cast<int64_t>(c->rs_pics.size());
-    std::vector<int64_t> by_level;
-    for (int64_t f = w.f0; f < w.f1; ++f) by_level.push_back(f);
-    std::stable_sort(by_level.begin(), by_level.end(),
-                     [&](int64_t x, int64_t y) { return level[static_cast<size_t>(x)] < level[static_cast<size_t>(y)]; });
-    for (int64_t f : by_level) {
-      const SchedFrame &fr = frames[static_cast<size_t>(f)];
-      const int32_t r0 = static_cast<int32_t>(c->rs_refs.size());
-      std::vector<int32_t> rs;
-      for (int64_t rf : fr.refs) {
-        const int32_t sl = slot_of(rf);
-        if (std::find(rs.begin(), rs.end(), sl) == rs.end()) rs.push_back(sl);
-      }
-      c->rs_refs.insert(c->rs_refs.end(), rs.begin(), rs.end());
-      c->rs_pics.push_back(make_int4(slot_of(f), r0, static_cast<int32_t>(rs.size()), 0));
-    }
     w.pn0 = static_cast<int64_t>(c->pneed.size());
     c->pneed.resize(c->pneed.size() + static_cast<size_t>(w.f1 - w.f0), 0);
     for (int64_t k = w.fs0; k < static_cast<int64_t>(c->fslices.size()); ++k)
@@ -441,11 +411,10 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
     }
     if (c->surf_pool) {
       // j: a picture's launch index in its group.  A surface is free for the
-      // group's launches after max(last reader's j, own j + surf_lag): its
-      // readers ran earlier on the group's stream, and so did its thumbnails
-      // (inline), or launch j waits for the thumbnails of launch
-      // j - surf_lag - 1 (side stream, run_general).  Each group its own
-      // pool: the groups' launches are not ordered against each other.
+      // group's launches after max(last reader's j, own j): its readers and
+      // its thumbnails (thumb_pics right after each level launch) ran earlier
+      // on the group's stream.  Each group its own pool: the groups' launches
+      // are not ordered against each other.
       std::vector<int32_t> jof(static_cast<size_t>(wn), 0), last(static_cast<size_t>(wn), -1);
       const size_t nl = w.lvl_off.size();
       std::vector<size_t> glo(static_cast<size_t>(ngrp) + 1, nl);
@@ -482,8 +451,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
               pool.pop_back();
             }
             c->surf_of[static_cast<size_t>(w.f0 + slot)] = static_cast<int32_t>(base + s);
-            const size_t fa = static_cast<size_t>(
-                std::max<int64_t>(last[static_cast<size_t>(slot)], static_cast<int64_t>(j) + c->surf_lag));
+            const size_t fa = static_cast<size_t>(std::max<int64_t>(last[static_cast<size_t>(slot)], static_cast<int64_t>(j)));
             if (fa < freed.size()) freed[fa].push_back(s);
           }
         }
@@ -669,17 +637,7 @@ int submit_general(vts_ctx *c) {
     ra.err = c->d_err;
     ra.sct = c->d_scale;
     ra.P = c->fprm;
-    if (c->recon_sched) {
-      // every picture of the window by per-picture readiness, one launch
-      SchedArgs sa{};
-      sa.pics = c->d_rs_pics + w.rs0;
-      sa.refs = c->d_rs_refs;
-      sa.n_pics = static_cast<int32_t>(w.f1 - w.f0);
-      sa.next = c->d_rs_next;
-      sa.done = c->d_rs_done[r];
-      HIP_TRY(hipMemsetAsync(c->d_rs_next, 0, sizeof(uint32_t), sd));
-      VTS_TRY(recon_sched_launch(ra, sa, c->rs_wg, sd));
-    } else {
+    {
       // bS needs only the parse's records: one launch per level on the score
       // stream, paced by the chain (level l + 1's after level l's inter launch),
       // beside the intra and deblocking launches that leave most compute units
@@ -706,20 +664,10 @@ int submit_general(vts_ctx *c) {
       // content stream, that stream sharing a hardware queue with a group's,
       // profiles/r04t_bs_paced_split_ab.json)
       auto sb_of = [&](int) { return sbs; };
-      // recycled surfaces: each level's thumbnails after its reconstruction,
-      // on the group's stream (inline) or on the thumbnail stream, where a
-      // group's launch j waits for the thumbnails of its launch
-      // j - surf_lag - 1 (the liveness plan's promise)
-      const bool side = c->surf_pool && !c->surf_inline;
-      hipStream_t st = c->s_grp[vts_ctx::kSurfThumbStream];
+      // recycled surfaces: each level's thumbnails right after its
+      // reconstruction, on the group's stream (the liveness plan's promise)
       PicThumbArgs ta{};
       if (c->surf_pool) {
-        const size_t need = 2 * w.lvl_off.size() + 1;
-        if (c->ev_th.size() < need) {
-          const size_t n0 = c->ev_th.size();
-          c->ev_th.resize(need, nullptr);
-          for (size_t k = n0; k < need; ++k) HIP_TRY(hipEventCreateWithFlags(&c->ev_th[k], hipEventDisableTiming));
-        }
         const int rb = c->k == 6 ? 48 : 16;
         ta.surf = c->d_surf[r];
         ta.frame_stride = c->frame_stride;
@@ -761,22 +709,13 @@ int submit_general(vts_ctx *c) {
           if (l >= hi[static_cast<size_t>(g)]) continue;
           hipStream_t s = g ? c->s_grp[g - 1] : sd;
           if (paced) HIP_TRY(hipStreamWaitEvent(s, c->ev_bs[2 * l], 0));
-          if (side && jj > static_cast<size_t>(c->surf_lag))
-            HIP_TRY(hipStreamWaitEvent(s, c->ev_th[2 * (l - static_cast<size_t>(c->surf_lag) - 1) + 1], 0));
           ra.frames = c->d_levels + w.lvl_off[l];
           const bool next = paced && l + 1 < hi[static_cast<size_t>(g)];
           VTS_TRY(recon_full_launch(ra, w.lvl_cnt[l], s, next ? c->ev_bs[2 * l + 1] : nullptr));
-          if (c->surf_pool && !side) {
+          if (c->surf_pool) {
             ta.pics = c->d_levels + w.lvl_off[l];
             ta.n_pics = w.lvl_cnt[l];
             VTS_TRY(thumb_pics_launch(ta, c->k, s));
-          } else if (side) {
-            HIP_TRY(hipEventRecord(c->ev_th[2 * l], s));
-            HIP_TRY(hipStreamWaitEvent(st, c->ev_th[2 * l], 0));
-            ta.pics = c->d_levels + w.lvl_off[l];
-            ta.n_pics = w.lvl_cnt[l];
-            VTS_TRY(thumb_pics_launch(ta, c->k, st));
-            HIP_TRY(hipEventRecord(c->ev_th[2 * l + 1], st));
           }
           if (next) {
             HIP_TRY(hipStreamWaitEvent(sb_of(g), c->ev_bs[2 * l + 1], 0));
@@ -787,10 +726,6 @@ int submit_general(vts_ctx *c) {
       for (int g = 1; g < ng; ++g) {
         HIP_TRY(hipEventRecord(c->ev_grp[g - 1], c->s_grp[g - 1]));
         HIP_TRY(hipStreamWaitEvent(sd, c->ev_grp[g - 1], 0));
-      }
-      if (side) {  // the window's thumbnails before its scoring
-        HIP_TRY(hipEventRecord(c->ev_th[2 * w.lvl_off.size()], st));
-        HIP_TRY(hipStreamWaitEvent(ss, c->ev_th[2 * w.lvl_off.size()], 0));
       }
     }
     if (c->small.on) VTS_TRY(small_window(c, r, w.f0, w.f1, sd));
