@@ -998,6 +998,20 @@ def main() -> None:
     device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
     coll_dev = device if args.dist_backend == "nccl" else torch.device("cpu")
+    # N = 1: the step's all-gathers still go through RCCL — a world-size-1
+    # NCCL group and plan_batch(always_gather=True) — so the line measures the
+    # same collective path every rank of an N > 1 run takes (not the
+    # profiler's child passes, which time the kernels only)
+    one_rank_group = None
+    if world == 1 and args.dist_backend == "nccl" and args.workload == "decode_score" and not args.video:
+        try:
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                                    world_size=1, device_id=device)
+            one_rank_group = "rccl"
+        except Exception as exc:  # noqa: BLE001 - reported in the line
+            one_rank_group = f"none (RCCL world-size-1 group failed: {type(exc).__name__}: {exc})"
+            log(f"RCCL at N=1 unavailable: {exc}")
+    gather_always = one_rank_group == "rccl"
 
     from vtseg import batch
     from vtseg import budget_planner as bp
@@ -1042,7 +1056,7 @@ def main() -> None:
 
             def step():
                 outs["items"] = batch.plan_batch(str_paths, REF_CONFIG, score=True,
-                                                 sessions=scorers)
+                                                 sessions=scorers, always_gather=gather_always)
 
     def barrier():
         if world > 1:
@@ -1268,9 +1282,11 @@ def main() -> None:
                        "frames_per_video": F, "frames_per_gpu": F * vpg,
                        "width": width, "height": height, "k": k,
                        "parallelism": f"video-per-gpu x{world} (video i on rank i mod {world})",
-                       "collectives": ("plan_batch: all_gather of per-video records + padded "
-                                       "boundary arrays, " + (args.dist_backend if world > 1
-                                                              else "none at N=1")),
+                       "collectives": ("plan_batch: all_gather_into_tensor of per-video records + "
+                                       "padded boundary arrays, " +
+                                       (args.dist_backend if world > 1 else
+                                        ("rccl (world-size-1 NCCL group, always_gather) at N=1"
+                                         if gather_always else (one_rank_group or "none at N=1")))),
                        "segment_counts": counts},
             "roofline": roof,
             "roofline_decode": roof_decode,
@@ -1299,6 +1315,8 @@ def main() -> None:
                 Path(p).unlink(missing_ok=True)
     if world > 1:
         dist.barrier()
+        dist.destroy_process_group()
+    elif gather_always:
         dist.destroy_process_group()
 
 

@@ -159,3 +159,99 @@ def test_two_rank_boundary_exchange(tmp_path):
             assert sf == tuple((seg[2 * s], seg[2 * s + 1]) for s in range(ns))
             assert cf == tuple(1000 * r + 7 * j + t for t in range(nc))
             assert ct == tuple(0.5 * r + j + t / 3 for t in range(nc))
+
+
+def _one_rank_group(backend: str):
+    import torch
+    import torch.distributed as dist
+    kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, **kw)
+
+
+def test_world_one_forced_gather_equals_plain_run(tmp_path):
+    """always_gather=True at world size 1 (gloo on CPU): the records and the
+    boundary arrays go through dist.all_gather_into_tensor and come back equal
+    to the collective-free run."""
+    import torch.distributed as dist
+    from vtseg import scene
+    from vtseg.batch import exchange_boundaries, plan_batch
+    paths = []
+    for i in range(3):
+        p = tmp_path / f"v{i}.mp4"
+        scene.synth_write(p, width=64, height=48, n_frames=300 + 150 * i, seed=i)
+        paths.append(str(p))
+    plain = plan_batch(paths, CONFIG)
+    _one_rank_group("gloo")
+    try:
+        forced = plan_batch(paths, CONFIG, always_gather=True)
+        import torch
+        recs = torch.tensor([[[2, 3, 0, 0], [1, 0, 0, 0]]], dtype=torch.int64)
+        x = exchange_boundaries(recs, [[0, 10, 8, 20], [0, 5]], [[3, 9, 15], []],
+                                [[0.1, 0.3, 0.5], []], always_gather=True)
+    finally:
+        dist.destroy_process_group()
+    assert forced == plain
+    assert x == [[(((0, 10), (8, 20)), (3, 9, 15), (0.1, 0.3, 0.5)), (((0, 5),), (), ())]]
+
+
+@pytest.mark.gpu
+def test_rccl_world_one_batch_equals_serial(tmp_path):
+    """the RCCL branch of plan_batch on an MI355X.  A
+    world-size-1 NCCL (= RCCL) process group; plan_batch with
+    always_gather=True sends the per-video records and the padded boundary
+    arrays through dist.all_gather_into_tensor on the GPU, and every item
+    (segments, scene cuts, segment frame ranges, cut times) equals the
+    collective-free serial run; exchange_boundaries alone too."""
+    import torch
+    import torch.distributed as dist
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test requires an MI355X")
+    from vtseg import scene
+    from vtseg.batch import exchange_boundaries, plan_batch
+    paths = []
+    for i in range(3):
+        p = tmp_path / f"v{i}.mp4"
+        scene.synth_write(p, width=320, height=240, n_frames=600 + 300 * i, seed=7 + i,
+                          cut_min_s=2, cut_max_s=6)
+        paths.append(str(p))
+    serial = plan_batch(paths, CONFIG, score=True, device=0)
+    assert all(it.n_cuts > 0 and not it.score_failed for it in serial)
+    torch.cuda.set_device(0)
+    _one_rank_group("nccl")
+    try:
+        assert dist.get_backend() == "nccl"
+        got = plan_batch(paths, CONFIG, score=True, device=0, always_gather=True)
+        recs = torch.tensor([[[2, 3, 0, 0], [1, 0, 0, 0]]], dtype=torch.int64)
+        x = exchange_boundaries(recs, [[0, 10, 8, 20], [0, 5]], [[3, 9, 15], []],
+                                [[0.1, 0.3, 0.5], []], device=torch.device("cuda", 0),
+                                always_gather=True)
+    finally:
+        dist.destroy_process_group()
+    assert got == serial
+    assert x == [[(((0, 10), (8, 20)), (3, 9, 15), (0.1, 0.3, 0.5)), (((0, 5),), (), ())]]
+
+
+@pytest.mark.gpu
+def test_bounded_in_flight_sessions_equal_serial(tmp_path):
+    """plan_batch opens at most max_in_flight sessions at once
+    (finishing and closing the oldest first): with more videos than that —
+    five CABAC B videos, one or two in flight — every record succeeds and
+    equals the default run's."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test requires an MI355X")
+    from vtseg import scene
+    from vtseg.batch import plan_batch
+    paths = []
+    for i in range(5):
+        p = tmp_path / f"c{i}.mp4"
+        scene.synth_write(p, width=320, height=240, n_frames=240 + 60 * i, seed=11 + i, coding="full",
+                          slices_per_row=0, bframes=True, weighted="implicit", cabac=True,
+                          transform_8x8=True, cut_min_s=1, cut_max_s=3, gop_max_s=2)
+        paths.append(str(p))
+    ref = plan_batch(paths, CONFIG, score=True, device=0)
+    assert all(not it.score_failed and it.n_cuts >= 0 for it in ref)
+    for k in (1, 2):
+        got = plan_batch(paths, CONFIG, score=True, device=0, max_in_flight=k)
+        assert got == ref

@@ -53,20 +53,30 @@ def _segments(duration: float, config: dict, current_api_count: int):
 
 def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int = 0,
                score: bool = False, device: int | None = None, group=None,
-               sessions: dict | None = None) -> list[BatchItem]:
+               sessions: dict | None = None, max_in_flight: int = 4,
+               always_gather: bool = False) -> list[BatchItem]:
     """Plan (and with score=True decode + score) a batch of videos, video i on
     rank i % world, and all-gather the results (module docstring).
 
     sessions: optional {video index: open scene.VideoScorer} for this rank's
     videos, kept open by the caller (their elementary streams stay resident in
     HBM across calls; the benchmark's timed step).  Videos without one are
-    opened from their file and closed again (demux + upload included)."""
+    opened from their file and closed again (demux + upload included); at
+    most `max_in_flight` of those are open at once (a general-decoder session
+    holds tens of GB of HBM), the oldest finished and closed before the next
+    opens, and an open that fails while others are in flight is retried once
+    after they are drained.
+
+    always_gather: run the all-gathers through the initialised process group
+    even at world size 1 (the RCCL path of an N=1 run; otherwise a single
+    rank keeps its own records without a collective)."""
     import torch
     import torch.distributed as dist
 
     distributed = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size(group) if distributed else 1
     rank = dist.get_rank(group) if distributed else 0
+    force = always_gather and distributed
     n = len(paths)
     per = (n + world - 1) // world
     backend = dist.get_backend(group) if distributed else "none"
@@ -86,32 +96,24 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
         durations[i] = probe_duration(p)
         segs_of[i] = _segments(durations[i], config, current_api_count)
     if score:
-        # Every local session's run is submitted before any is waited for, so
-        # the device overlaps them (one video's serial parse tail or
+        # Local sessions' runs are submitted before earlier ones are waited
+        # for, so the device overlaps them (one video's serial parse tail or
         # reconstruction chain leaves compute units another's fills).  A
         # failure on one video must not keep this rank from the collectives
         # below (the other ranks would wait forever): it is recorded in the
         # video's record.
+        from collections import deque
+
         from .scene import VideoScorer
-        running: dict[int, tuple] = {}
-        for j, i in mine:
-            v, own = (sessions or {}).get(i), False
-            try:
-                if v is None:
-                    own = True
-                    dev_id = torch.cuda.current_device() if device is None else device
-                    v = VideoScorer(str(paths[i]), device=dev_id)
-                v.run_async()            # decode + score; per-frame results stay on the device
-                running[i] = (v, own)
-            except Exception as exc:  # noqa: BLE001 - reported per video
-                errors[i] = f"{type(exc).__name__}: {exc}"
-                local[j, 3] = 1
-                if own and v is not None:
-                    v.close()
-        for j, i in mine:
-            if i not in running:
-                continue
-            v, own = running[i]
+        running: deque = deque()  # (j, i, session, opened here), in submission order
+
+        def fail(j, i, exc):
+            errors[i] = f"{type(exc).__name__}: {exc}"
+            local[j, 3] = 1
+            local[j, 1] = -1
+
+        def finish_oldest():
+            j, i, v, own = running.popleft()
             try:
                 v.wait()
                 cuts = v.scene_cuts()    # only the scores come back to find the cuts
@@ -124,19 +126,45 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
                 cut_times[j] = [float(pts[c]) / ts for c in cuts]
                 local[j, 1] = len(cuts)
             except Exception as exc:  # noqa: BLE001 - reported per video
-                errors[i] = f"{type(exc).__name__}: {exc}"
-                local[j, 3] = 1
-                local[j, 1] = -1
+                fail(j, i, exc)
             finally:
                 if own:
                     v.close()
+
+        dev_id = device
+        for j, i in mine:
+            v, own = (sessions or {}).get(i), False
+            try:
+                if v is None:
+                    own = True
+                    while sum(1 for x in running if x[3]) >= max(1, max_in_flight):
+                        finish_oldest()
+                    if dev_id is None:
+                        dev_id = torch.cuda.current_device()
+                    try:
+                        v = VideoScorer(str(paths[i]), device=dev_id)
+                    except Exception:  # noqa: BLE001 - HBM held by the runs in flight: drain, retry once
+                        if not running:
+                            raise
+                        while running:
+                            finish_oldest()
+                        v = VideoScorer(str(paths[i]), device=dev_id)
+                v.run_async()            # decode + score; per-frame results stay on the device
+                running.append((j, i, v, own))
+            except Exception as exc:  # noqa: BLE001 - reported per video
+                fail(j, i, exc)
+                if own and v is not None:
+                    v.close()
+        while running:
+            finish_oldest()
     for j, i in mine:
         local[j, 0] = len(segs_of[i])
         if not score or i in errors:
             local[j, 1] = -1
         local[j, 2] = round(durations[i] * 1_000_000)
-    g = _all_gather(local, world, group, dev).view(world, per, REC)
-    arrays = (exchange_boundaries(g, seg_frames, cut_frames, cut_times, group=group, device=dev)
+    g = _all_gather(local, world, group, dev, force).view(world, per, REC)
+    arrays = (exchange_boundaries(g, seg_frames, cut_frames, cut_times, group=group, device=dev,
+                                  always_gather=force)
               if score else None)
     items = []
     for i in range(n):
@@ -153,14 +181,15 @@ def plan_batch(paths: list[str | Path], config: dict, *, current_api_count: int 
 
 
 def exchange_boundaries(records, seg_frames, cut_frames, cut_times, *, group=None,
-                        device=None):
+                        device=None, always_gather: bool = False):
     """Second all-gather of the batch: per-video boundary arrays.
 
     records: the gathered [world, per, REC] int64 (n_segments, n_cuts, ...) of
     the first exchange, identical on every rank, so every rank pads to the
     same widths.  seg_frames[j] (2 per segment), cut_frames[j], cut_times[j]:
     this rank's j-th video.  Returns [world][per] of (segment_frames pairs,
-    cut_frames, cut_times) tuples.
+    cut_frames, cut_times) tuples.  always_gather: through the process group
+    even at world size 1 (plan_batch).
     """
     import torch
     import torch.distributed as dist
@@ -180,8 +209,9 @@ def exchange_boundaries(records, seg_frames, cut_frames, cut_times, *, group=Non
             li[j, :len(row)] = torch.tensor(row, dtype=torch.int64)
         if len(cut_times[j]):
             lf[j, :len(cut_times[j])] = torch.tensor(list(cut_times[j]), dtype=torch.float64)
-    gi = _all_gather(li, world, group, dev).view(world, per, width_i)
-    gf = _all_gather(lf, world, group, dev).view(world, per, width_f)
+    force = always_gather and distributed
+    gi = _all_gather(li, world, group, dev, force).view(world, per, width_i)
+    gf = _all_gather(lf, world, group, dev, force).view(world, per, width_f)
     out = []
     for r in range(world):
         row_r = []
@@ -197,12 +227,13 @@ def exchange_boundaries(records, seg_frames, cut_frames, cut_times, *, group=Non
     return out
 
 
-def _all_gather(local, world: int, group, dev):
-    """[per, ...] on every rank -> [world * per, ...] on the CPU."""
+def _all_gather(local, world: int, group, dev, force: bool = False):
+    """[per, ...] on every rank -> [world * per, ...] on the CPU (at world
+    size 1 the rank's own tensor, unless `force`: then through the group)."""
     import torch
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not force:
         return local
     t = local.to(dev)
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
