@@ -513,8 +513,8 @@ def test_cavlc_b_parse_merged_and_per_level(tmp_path, monkeypatch, merge):
 def test_cabac_temporal_direct_windows_and_arena_rerun(tmp_path, monkeypatch, per_byte):
     """The CABAC syntax parse + h264_derive (colocated records read by parse
     level) on a B stream with temporal direct, in one window and in several
-    windows on two rings; with VTS_ARENA_PER_BYTE=0 the windows' arenas (64
-    blocks per slice + a chunk each) overflow, the run reports DEC_E_ARENA to
+    windows on two rings; with VTS_ARENA_PER_BYTE=0 the windows' arenas (one
+    256-block chunk) overflow, the run reports DEC_E_ARENA to
     the host, which grows the arena from what the windows asked for and runs
     again: every frame, histogram and score equals the oracle either way."""
     _require_gpu()

@@ -362,7 +362,9 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
     c->fprm.has_ext = c->exts.empty() ? 0 : 1;
     w.fs1 = static_cast<int64_t>(c->fslices.size());
     if (c->fprm.cabac) {
-      arena = cabac_window_blocks(arena, w.fs1 - w.fs0);
+      // (VTS_ARENA_PER_BYTE=0: one chunk, the tests' way to make every run
+      // outgrow its first arena)
+      arena = c->arena_per_byte == 0 ? static_cast<int64_t>(kArenaChunk) : cabac_window_blocks(arena, w.fs1 - w.fs0);
       abound = cabac_window_blocks(abound, w.fs1 - w.fs0);
       // the chunk counter and block indices are 32-bit: the bound stays below
       // 2^32 with a chunk per slice of headroom for requests past the end
