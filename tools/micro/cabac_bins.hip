@@ -30,6 +30,7 @@ struct Run {
   int32_t len;
   int32_t n;
   int32_t mode;
+  uint32_t *bits;  // modes 0-2: every bin, 32 per word (device: lane 0 stores)
 };
 
 VTS_HD VTS_INLINE uint32_t run_bins(const Run &r, SynScratch *sc) {
@@ -41,14 +42,20 @@ VTS_HD VTS_INLINE uint32_t run_bins(const Run &r, SynScratch *sc) {
   p.cab_tables();
   p.cab_init(true, 26);
   p.cab_start();
-  uint32_t acc = 0;
+  uint32_t acc = 0, word = 0;
   for (int i = 0; i < r.n; ++i) {
-    if (r.mode == 0) {
-      acc += p.dec(105 + (i % 15));
-    } else if (r.mode == 1) {
-      acc += p.dec(60);
-    } else if (r.mode == 2) {
-      acc += p.bypass();
+    if (r.mode <= 2) {
+      const uint32_t b = r.mode == 0 ? p.dec(105 + (i % 15)) : (r.mode == 1 ? p.dec(60) : p.bypass());
+      acc += b;
+      word |= b << (i & 31);
+      if ((i & 31) == 31 || i + 1 == r.n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (threadIdx.x == 0) r.bits[i >> 5] = word;
+#else
+        r.bits[i >> 5] = word;
+#endif
+        word = 0;
+      }
     } else if (r.mode == 3) {
       for (int k = 0; k < 16; ++k) sc->blk[k] = 0;
       acc += static_cast<uint32_t>(p.residual_t<false>(2, i & 3, 16, sc->blk, 0));
@@ -93,10 +100,13 @@ int main(int argc, char **argv) {
     // bins on the host (same bytes, same calls)
     for (auto &t : g_trace) t = 0;
     std::vector<uint8_t> lds(sizeof(SynScratch) + 64);
-    Run hr{h.data(), len, nn, mode};
+    std::vector<uint32_t> hbits(static_cast<size_t>(nn) / 32 + 1, 0), dbits(hbits.size(), 0);
+    uint32_t *dbits_d = nullptr;
+    (void)hipMalloc(&dbits_d, dbits.size() * 4);
+    Run hr{h.data(), len, nn, mode, hbits.data()};
     const uint32_t hacc = run_bins(hr, reinterpret_cast<SynScratch *>(lds.data()));
     const unsigned long long bins = g_trace[1] + g_trace[2] + g_trace[3];
-    Run r{d, len, nn, mode};
+    Run r{d, len, nn, mode, dbits_d};
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -111,6 +121,13 @@ int main(int argc, char **argv) {
     unsigned long long cyc = 0;
     (void)hipMemcpy(&acc, dout, 4, hipMemcpyDeviceToHost);
     (void)hipMemcpy(&cyc, dcyc, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(dbits.data(), dbits_d, dbits.size() * 4, hipMemcpyDeviceToHost);
+    long first_diff = -1;
+    if (mode <= 2)
+      for (int i = 0; i < nn && first_diff < 0; ++i)
+        if (((hbits[i >> 5] >> (i & 31)) & 1) != ((dbits[i >> 5] >> (i & 31)) & 1)) first_diff = i;
+    std::printf("{\"mode\": \"%s\", \"first_diff_bin\": %ld, \"host_acc\": %u, \"dev_acc\": %u}\n", names[mode],
+                first_diff, hacc, acc);
     std::printf("{\"mode\": \"%s\", \"calls\": %d, \"bins\": %llu, \"equal\": %s, \"ms\": %.3f, \"ns_per_bin\": %.2f, "
                 "\"memtime_per_bin\": %.1f}\n",
                 names[mode], nn, bins, acc == hacc ? "true" : "false", ms, ms * 1e6 / static_cast<double>(bins),
