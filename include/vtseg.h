@@ -21,6 +21,8 @@
  *                          is the identity stub this feeds)  segment time -> frame index
  *   vts_open/vts_score/... (no reference code; north_star)   decode + NV12 scene scoring
  *   vts_score_nv12_dev     (no reference code)               the scoring kernel on device NV12
+ *   vts_batch_run          pipeline.py:376-393 (the batch loop over analyze_video), as
+ *                          vtseg.batch.plan_batch: video i on rank i % world, RCCL exchange
  *   vts_synth_write        (no reference code; tests/test_video_segmenter.py:147-178 builds
  *                          its only synthetic clip with `ffmpeg -f lavfi`, absent here)
  *
@@ -36,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VTS_ABI_VERSION 7
+#define VTS_ABI_VERSION 8
 
 enum {
   VTS_OK = 0,
@@ -334,6 +336,58 @@ int vts_open_timings(const vts_ctx *ctx, double *ms, int32_t cap);
  * (0: one per window frame); < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);  /* 8: general decoder in use (1/0) */
 int vts_close(vts_ctx *ctx);
+
+/* ------------------------------------------------------------ batch
+ * One call per process plans (and with score = 1 decodes + scores) a batch
+ * of videos: video i belongs to rank i % world, this process runs its own
+ * (at most max_in_flight sessions open at once, every run submitted before
+ * earlier ones are waited for), and two all-gathers over RCCL give every
+ * rank the whole batch: the per-video records, then the boundary arrays
+ * padded to the batch's widths.  Replaces the reference's sequential loop
+ * (src/pipeline.py:376-393 -> ContentAnalyzer.analyze_video per URL); the
+ * same records and rules as vtseg.batch.plan_batch (a video whose scoring
+ * fails is marked and the batch goes on; a planning error fails the call
+ * on the rank that meets it, before any exchange).
+ *
+ * The communicator: vts_rccl_unique_id on one rank, its 128 bytes sent to
+ * the others by the host's own means, then vts_rccl_comm_init on every
+ * rank (its device, the world size, its rank).  NULL: this process is the
+ * whole batch (rank 0 of 1) and nothing is exchanged.  RCCL (librccl.so.1)
+ * is loaded on first use. */
+#define VTS_RCCL_ID_BYTES 128
+int vts_rccl_unique_id(uint8_t *id /* VTS_RCCL_ID_BYTES */);
+int vts_rccl_comm_init(int32_t device, int32_t world, int32_t rank, const uint8_t *id, void **comm);
+int vts_rccl_comm_destroy(void *comm);
+
+typedef struct vts_batch vts_batch;
+typedef struct vts_batch_params {
+  int32_t score;             /* 1: decode + score every video (scene cuts, segment frames)  */
+  int32_t device;            /* HIP device of this rank                                     */
+  int32_t max_in_flight;     /* sessions open at once on this rank; 0 = 4                   */
+  int32_t _pad;
+  int64_t current_api_count; /* plan_segments_with_budget's current_api_count               */
+  void *rccl_comm;           /* vts_rccl_comm_init's, or NULL (one process, no exchange)    */
+} vts_batch_params;
+/* BatchItem (vtseg/batch.py) without its arrays */
+typedef struct vts_batch_record {
+  double duration;           /* probe_duration, through the exchange in microseconds      */
+  int64_t n_segments;        /* plan_segments windows                                     */
+  int64_t n_cuts;            /* scene cuts; -1 when not scored or scoring failed          */
+  int32_t rank;              /* rank that processed the video                             */
+  int32_t score_failed;      /* 1: scoring failed (vts_batch_error on that rank says why) */
+} vts_batch_record;
+int vts_batch_run(const char *const *paths, int64_t n, const vts_budget_cfg *cfg,
+                  const vts_batch_params *params, vts_batch **out);
+int vts_batch_get(const vts_batch *b, int64_t i, vts_batch_record *rec);
+/* video i's arrays (score = 1): segment_frames 2 x n_segments ([start, end)
+ * frame of each segment's extract window), cut_frames / cut_times n_cuts
+ * (presentation time in seconds); each may be NULL */
+int vts_batch_arrays(const vts_batch *b, int64_t i, int64_t *segment_frames,
+                     int64_t *cut_frames, double *cut_times);
+/* the scoring failure of one of this rank's videos ("" otherwise); two-call
+ * size query through *len */
+int vts_batch_error(const vts_batch *b, int64_t i, char *msg, int64_t cap, int64_t *len);
+void vts_batch_free(vts_batch *b);
 
 /* ------------------------------- upload transcode (360p)
  * Replaces the pixel half of ContentAnalyzer._compress_video_for_upload

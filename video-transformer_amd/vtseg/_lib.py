@@ -12,7 +12,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libvtseg.so"
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 VTS_OK = 0
 VTS_E_INVALID = -1
@@ -129,6 +129,16 @@ class ManifestArgs(C.Structure):
                 ("overlap_seconds_int", C.c_char_p)]
 
 
+class BatchParams(C.Structure):
+    _fields_ = [("score", C.c_int32), ("device", C.c_int32), ("max_in_flight", C.c_int32),
+                ("_pad", C.c_int32), ("current_api_count", C.c_int64), ("rccl_comm", C.c_void_p)]
+
+
+class BatchRecord(C.Structure):
+    _fields_ = [("duration", C.c_double), ("n_segments", C.c_int64), ("n_cuts", C.c_int64),
+                ("rank", C.c_int32), ("score_failed", C.c_int32)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/vtseg.h
 _P = C.POINTER
 SIGNATURES: dict[str, tuple] = {
@@ -171,6 +181,16 @@ SIGNATURES: dict[str, tuple] = {
                                 _P(TranscodeInfo)]),
     "vts_synth_write": (C.c_int, [C.c_char_p, _P(SynthParams), _P(SynthInfo),
                                   _P(C.c_int64), C.c_int64]),
+    "vts_rccl_unique_id": (C.c_int, [_P(C.c_uint8)]),
+    "vts_rccl_comm_init": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _P(C.c_uint8), _P(C.c_void_p)]),
+    "vts_rccl_comm_destroy": (C.c_int, [C.c_void_p]),
+    "vts_batch_run": (C.c_int, [_P(C.c_char_p), C.c_int64, _P(BudgetCfg), _P(BatchParams),
+                                _P(C.c_void_p)]),
+    "vts_batch_get": (C.c_int, [C.c_void_p, C.c_int64, _P(BatchRecord)]),
+    "vts_batch_arrays": (C.c_int, [C.c_void_p, C.c_int64, _P(C.c_int64), _P(C.c_int64),
+                                   _P(C.c_double)]),
+    "vts_batch_error": (C.c_int, [C.c_void_p, C.c_int64, C.c_char_p, C.c_int64, _P(C.c_int64)]),
+    "vts_batch_free": (None, [C.c_void_p]),
     "vts_last_error": (C.c_char_p, []),
     "vts_abi_version": (C.c_int, []),
     "vts_device_count": (C.c_int, []),

@@ -239,3 +239,94 @@ def _all_gather(local, world: int, group, dev, force: bool = False):
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
     dist.all_gather_into_tensor(out, t, group=group)
     return out.cpu()
+
+
+class RcclComm:
+    """An RCCL communicator made by libvtseg (vts_rccl_comm_init) for
+    plan_batch_native: the id from `unique_id()` on one rank, sent to the
+    others by the caller's own means."""
+
+    def __init__(self, device: int, world: int, rank: int, uid: bytes):
+        import ctypes as C
+
+        from . import _lib
+        if len(uid) != 128:
+            raise ValueError("an RCCL unique id is 128 bytes")
+        self._lib = _lib.lib()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _lib.check(self._lib.vts_rccl_comm_init(device, world, rank, buf, C.byref(h)))
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+
+        from . import _lib
+        buf = (C.c_uint8 * 128)()
+        _lib.check(_lib.lib().vts_rccl_unique_id(buf))
+        return bytes(buf)
+
+    def close(self) -> None:
+        if self.handle:
+            self._lib.vts_rccl_comm_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def plan_batch_native(paths: list[str | Path], config: dict, *, current_api_count: int = 0,
+                      score: bool = False, device: int = 0, max_in_flight: int = 4,
+                      comm: RcclComm | None = None) -> list[BatchItem]:
+    """plan_batch through the C ABI's vts_batch_run (one native call: probe,
+    plan, decode + score, and the two all-gathers over RCCL when `comm` is
+    given) — what a host without torch.distributed calls; the same BatchItems."""
+    import ctypes as C
+
+    from . import _lib
+    from .budget_planner import _i64, budget_cfg
+    L = _lib.lib()
+    n = len(paths)
+    arr = (C.c_char_p * max(n, 1))(*[str(p).encode() for p in paths])
+    prm = _lib.BatchParams()
+    prm.score = 1 if score else 0
+    prm.device = int(device)
+    prm.max_in_flight = int(max_in_flight)
+    prm.current_api_count = _i64("current_api_count", int(current_api_count))
+    prm.rccl_comm = comm.handle if comm is not None else None
+    cfg = budget_cfg(config)
+    h = C.c_void_p()
+    _lib.check(L.vts_batch_run(arr, n, C.byref(cfg), C.byref(prm), C.byref(h)))
+    try:
+        items = []
+        for i in range(n):
+            rec = _lib.BatchRecord()
+            _lib.check(L.vts_batch_get(h, i, C.byref(rec)))
+            extra = {}
+            if score and not rec.score_failed:
+                ns, nc = int(rec.n_segments), max(0, int(rec.n_cuts))
+                sf = (C.c_int64 * max(1, 2 * ns))()
+                cf = (C.c_int64 * max(1, nc))()
+                ct = (C.c_double * max(1, nc))()
+                _lib.check(L.vts_batch_arrays(h, i, sf, cf, ct))
+                extra = {"segment_frames": tuple((sf[2 * s], sf[2 * s + 1]) for s in range(ns)),
+                         "cut_frames": tuple(cf[:nc]), "cut_times": tuple(ct[:nc])}
+            err = None
+            if rec.score_failed:
+                ln = C.c_int64(0)
+                L.vts_batch_error(h, i, None, 0, C.byref(ln))
+                if ln.value:
+                    buf = C.create_string_buffer(ln.value + 1)
+                    L.vts_batch_error(h, i, buf, ln.value + 1, C.byref(ln))
+                    err = buf.value.decode("utf-8", "replace")
+            items.append(BatchItem(index=i, path=str(paths[i]), duration=float(rec.duration),
+                                   n_segments=int(rec.n_segments), n_cuts=int(rec.n_cuts),
+                                   rank=int(rec.rank), score_failed=bool(rec.score_failed),
+                                   score_error=err, **extra))
+        return items
+    finally:
+        L.vts_batch_free(h)

@@ -68,11 +68,9 @@ _ERRORS = {
 }
 
 
-def plan_segments_with_budget(
-    duration: float,
-    config: Mapping[str, object],
-    current_api_count: int,
-) -> SegmentPlan:
+def budget_cfg(config: Mapping[str, object]) -> "_lib.BudgetCfg":
+    """The reference's config coercion (budget_planner.py:95-103) as the C
+    ABI's vts_budget_cfg (also vts_batch_run's planning input)."""
     analyzer_raw = config.get("analyzer")
     analyzer = cast(dict[str, object], analyzer_raw) if isinstance(analyzer_raw, dict) else {}
     lv_raw = analyzer.get("long_video")
@@ -92,7 +90,6 @@ def plan_segments_with_budget(
     threshold_raw = lv.get("duration_threshold_seconds")
     cfg.consolidate = 1 if _coerce_bool(lv.get("consolidate"), True) else 0
 
-    duration_f = float(duration)  # reference: max(float(duration), 0.0) at :104
     threshold = None
     if isinstance(threshold_raw, (int, float, str)):
         try:
@@ -101,6 +98,16 @@ def plan_segments_with_budget(
             threshold = None
     cfg.has_threshold = 0 if threshold is None else 1
     cfg.duration_threshold_seconds = 0.0 if threshold is None else threshold
+    return cfg
+
+
+def plan_segments_with_budget(
+    duration: float,
+    config: Mapping[str, object],
+    current_api_count: int,
+) -> SegmentPlan:
+    cfg = budget_cfg(config)
+    duration_f = float(duration)  # reference: max(float(duration), 0.0) at :104
     count = _i64("current_api_count", int(current_api_count))
 
     out = _lib.Plan()
@@ -119,4 +126,4 @@ def plan_segments_with_budget(
     )
 
 
-__all__ = ["SegmentPlan", "plan_segments_with_budget", "_coerce_int", "_coerce_bool"]
+__all__ = ["SegmentPlan", "plan_segments_with_budget", "budget_cfg", "_coerce_int", "_coerce_bool"]
