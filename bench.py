@@ -650,18 +650,24 @@ def general_kernel_rooflines(prof: dict, width: int, height: int, k: int, frames
 
 def run_single(path: Path, *, gpu: int, k: int, steps: int, threads: int, label: str,
                decoder: str = "auto", prof: dict | None = None, parity: bool = True,
-               planted: list[int] | None = None) -> dict:
+               planted: list[int] | None = None, window_frames: int = 0) -> dict:
     """One video through its session: `steps` timed vts_run calls (inputs
-    resident), stage times, the dominant kernel's roofline and parity over
-    every frame against the oracle; with `planted` (the writer's scene cuts)
-    the device's detected cuts beside them."""
+    resident), stage times, the session's HBM (the allocator's bytes handed
+    out by its vts_open, and after the runs: a CABAC arena that overflowed
+    grew), the dominant kernel's roofline and parity over every frame against
+    the oracle; with `planted` (the writer's scene cuts) the device's detected
+    cuts beside them."""
     import torch
+    from vtseg import _lib
     from vtseg import budget_planner as bp
     from vtseg import scene
     from vtseg import video_segmenter as vs
+    L = _lib.lib()
+    before = int(L.vts_device_bytes(gpu))
     t0 = time.perf_counter()
-    v = scene.VideoScorer(path, device=gpu, decoder=decoder)
+    v = scene.VideoScorer(path, device=gpu, decoder=decoder, window_frames=window_frames)
     open_s = time.perf_counter() - t0
+    hbm_open = int(L.vts_device_bytes(gpu)) - before
     try:
         F = v.n_frames
         W, H = int(v.info.width), int(v.info.height)
@@ -679,7 +685,13 @@ def run_single(path: Path, *, gpu: int, k: int, steps: int, threads: int, label:
                "decoder": "general" if v.general() else "subset",
                "stage_ms": v.timings(), "recon_launches": v.recon_launches(),
                "windows": v.windows(),
+               "hbm_gb_at_open": round(hbm_open / 1e9, 2),
+               "hbm_gb_after_runs": round((int(L.vts_device_bytes(gpu)) - before) / 1e9, 2),
                "bits_per_frame": round(Path(path).stat().st_size * 8 / F, 1)}
+        if v.general():
+            rec["arena_reruns"] = v.arena_reruns()
+        if window_frames:
+            rec["window_frames"] = window_frames
         if not v.general():
             rec["roofline"] = roofline_decode_score([v], prof, W, H, k, F)
         if planted is not None:
@@ -704,14 +716,17 @@ def run_single(path: Path, *, gpu: int, k: int, steps: int, threads: int, label:
         v.close()
 
 
-def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: list[list[int]]) -> dict:
-    """BATCH config [3]'s per-GPU share on real-syntax streams: the video-like
-    CABAC B content streams (one per local video) opened as resident
-    sessions, then plan_batch every step — every session's run submitted
-    before any is waited for (vts_run_async), so the device overlaps them —
-    against one video's step alone; each session's HBM (the allocator's bytes
-    handed out by its vts_open; and the sessions' mean after the runs) and
-    full parity of every video."""
+def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: list[list[int]],
+                         n_content: int) -> dict:
+    """BATCH config [3]'s per-GPU share on real-syntax streams, resident
+    sessions through plan_batch (every session's run submitted before any is
+    waited for, vts_run_async): the first n_content paths are video-like CABAC
+    B content streams — their batch against one of them alone is the overlap
+    figure (`batch_over_single`, HIP's default hardware queues) — the rest
+    full-syntax noise streams, run as a mixed batch with half of the content
+    sessions (`mixed`: the worst case beside the typical).  Each session's HBM
+    (the allocator's bytes handed out by its vts_open, and the mean after the
+    runs) and full parity of every video."""
     import torch
     from vtseg import _lib, batch, scene
     from vtseg import budget_planner as bp
@@ -719,6 +734,18 @@ def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: lis
     L = _lib.lib()
     sessions, hbm = {}, []
     base = int(L.vts_device_bytes(gpu))
+
+    def timed(idx: list[int]) -> tuple[float, list]:
+        strs = [str(paths[i]) for i in idx]
+        ses = {j: sessions[i] for j, i in enumerate(idx)}
+        batch.plan_batch(strs, REF_CONFIG, score=True, sessions=ses)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            items = batch.plan_batch(strs, REF_CONFIG, score=True, sessions=ses)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / 3 * 1e3, items
+
     try:
         for i, p in enumerate(paths):
             before = int(L.vts_device_bytes(gpu))
@@ -733,15 +760,12 @@ def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: lis
             v0.run()
         torch.cuda.synchronize()
         single_ms = (time.perf_counter() - t0) / 3 * 1e3
-        strs = [str(p) for p in paths]
-        batch.plan_batch(strs, REF_CONFIG, score=True, sessions=sessions)  # warm-up
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(3):
-            items = batch.plan_batch(strs, REF_CONFIG, score=True, sessions=sessions)
-        torch.cuda.synchronize()
-        batch_ms = (time.perf_counter() - t0) / 3 * 1e3
-        # after the runs (the CABAC arena is cut to what each slice stored after a session's first run)
+        content = list(range(n_content))
+        batch_ms, items_c = timed(content)
+        mixed = list(range(max(1, n_content // 2))) + list(range(n_content, len(paths)))
+        mixed_ms, items_m = timed(mixed)
+        items = {i: it for i, it in zip(content, items_c)}
+        items.update({i: it for i, it in zip(mixed, items_m)})
         hbm_after = int(L.vts_device_bytes(gpu)) - base
         per_video, ok = [], True
         for i, p in enumerate(paths):
@@ -751,18 +775,26 @@ def general_batch_record(paths: list[Path], gpu: int, threads: int, planted: lis
             segs = vs.plan_segments(duration, plan.segment_duration, plan.overlap)
             par, ct = parity_check(v, p, 4, segs, threads, None, "full")
             par["batch_record_equal"] = batch_record_check(items[i], segs, ct, True)
+            par["stream"] = "content" if i < n_content else "noise"
             det = set(items[i].cut_frames)
             par["planted_cuts"] = len(planted[i])
             par["planted_cuts_detected"] = sum(1 for c in planted[i] if c in det)
             per_video.append(par)
             ok &= par["all_equal"] and par["batch_record_equal"]
-        return {"label": f"BASELINE config [3] per-GPU share on real syntax: {len(paths)} x 10-min 720p CONTENT "
+        return {"label": f"BASELINE config [3] per-GPU share on real syntax: {n_content} x 10-min 720p CONTENT "
                          "streams (CABAC, 8x8, B pyramid, implicit weights, deblocking) as resident sessions "
-                         "through vtseg.batch.plan_batch, every session's run submitted before any wait",
-                "videos": len(paths), "frames_per_video": F, "steps": 3,
-                "value": round(len(paths) * F / (batch_ms / 1e3), 1), "unit": "frames/s",
+                         "through vtseg.batch.plan_batch, every session's run submitted before any wait, on the "
+                         "process's HIP hardware queues as inherited; `mixed`: "
+                         f"{len(mixed) - (len(paths) - n_content)} of them with {len(paths) - n_content} "
+                         "full-syntax NOISE streams (the worst case for HBM and parse)",
+                "videos": n_content, "frames_per_video": F, "steps": 3,
+                "value": round(n_content * F / (batch_ms / 1e3), 1), "unit": "frames/s",
                 "ms_per_step": round(batch_ms, 2), "single_video_ms": round(single_ms, 2),
                 "batch_over_single": round(batch_ms / single_ms, 3),
+                "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),
+                "mixed": {"videos": [("content" if i < n_content else "noise") for i in mixed],
+                          "ms_per_step": round(mixed_ms, 2),
+                          "value": round(len(mixed) * F / (mixed_ms / 1e3), 1), "unit": "frames/s"},
                 "hbm_gb_per_session": [round(b / 1e9, 2) for b in hbm],
                 "hbm_gb_per_session_after_runs": round(hbm_after / len(paths) / 1e9, 2),
                 "arena_reruns": [sessions[i].arena_reruns() for i in range(len(paths))],
@@ -814,21 +846,21 @@ def e2e_record(paths: list[Path], gpu: int) -> dict:
                         "boundary frames, close; files in the page cache (just written)"}
 
 
-# HIP hardware queues per process (read once, when HIP initialises): a
-# session drives up to six streams (parse, decode / GOP groups, score), and
-# plan_batch overlaps several sessions' runs; on HIP's default 4 queues their
-# launches share queues in submission order and the runs serialise (4 content
-# sessions: 3.99x one session's step; 16 queues: 2.76x, profiles/r05f_*).
-# The documented deployment setting; set before anything
-# initialises HIP, inherited by the profiler children and the ranks.  Set,
-# not defaulted: the GPU box exports HIP's default (4) itself, which a
-# setdefault kept (r05n: 4.25x).  32 queues: batch 2.0x but one session's
-# step 311 -> 383 ms (profiles/r05o_batch_queues_after_sessions.json).
-HW_QUEUES = "16"
+# HIP hardware queues: the bench runs on whatever the process inherits (HIP's
+# default 4, which the GPU box exports); sessions opened beside others take
+# streams with hardware queues of their own (session.hip streams_take), so
+# concurrent sessions overlap without GPU_MAX_HW_QUEUES (round 5 forced 16
+# here).  VTS_BENCH_HW_QUEUES sets it for a measurement.
+# general-decoder records beyond 10 min: config [2]'s path (a 30-min content
+# stream in three windows) and config [4]'s resolution (a 5-min 1080p one)
+GLONG_FRAMES = 54000
+GLONG_WINDOW = 18000
+GHD_FRAMES = 9000
 
 
 def main() -> None:
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("VTS_BENCH_HW_QUEUES", HW_QUEUES)
+    if os.environ.get("VTS_BENCH_HW_QUEUES"):
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ["VTS_BENCH_HW_QUEUES"]
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -936,8 +968,8 @@ def main() -> None:
     local_paths = [all_paths[i] for i in local_idx]
 
     # extras' inputs, written before the profile passes (which read them)
-    gen_path = long_path = content_path = hd_path = None
-    gen_info = content_info = None
+    gen_path = long_path = content_path = hd_path = glong_path = ghd_path = None
+    gen_info = content_info = glong_info = ghd_info = None
     gb_paths, gb_infos = [], []
     if extras:
         t0 = time.perf_counter()
@@ -945,18 +977,35 @@ def main() -> None:
         content_path = tmpdir / "general_content_720p_10min.mp4"
         long_path = tmpdir / "long_720p_2h.mp4"
         hd_path = tmpdir / "hd_1080p_30min.mp4"
+        glong_path = tmpdir / "general_content_720p_30min.mp4"
+        ghd_path = tmpdir / "general_content_1080p_5min.mp4"
+        # config [3]'s share on real syntax: vpg content streams, and the worst
+        # case beside them — half of a mixed batch noise streams (VERDICT r05
+        # item 4)
+        n_noise = max(1, vpg // 2)
         gb_paths = [content_path] + [tmpdir / f"general_content_720p_10min_{i}.mp4" for i in range(1, vpg)]
-        with ThreadPoolExecutor(8) as ex:
-            fa = ex.submit(synth_videos, [(gen_path, 0x5EED)], 1280, 720, 18000, "full", True, True)
+        gb_noise = [gen_path] + [tmpdir / f"general_720p_10min_{i}.mp4" for i in range(1, n_noise)]
+        with ThreadPoolExecutor(12) as ex:
+            fa = [ex.submit(synth_videos, [(p, 0x5EED + i)], 1280, 720, 18000, "full", True, True)
+                  for i, p in enumerate(gb_noise)]
             fc = [ex.submit(synth_videos, [(p, 0x5EED + i)], 1280, 720, 18000, "full", True, True, True)
                   for i, p in enumerate(gb_paths)]
+            fl = ex.submit(synth_videos, [(glong_path, 0x5EED + 100)], 1280, 720, GLONG_FRAMES, "full", True,
+                           True, True)
+            fh = ex.submit(synth_videos, [(ghd_path, 0x5EED + 200)], 1920, 1080, GHD_FRAMES, "full", True,
+                           True, True)
             fb = ex.submit(synth_videos, [(long_path, 0x5EED)], 1280, 720, 216000)
             fd = ex.submit(synth_videos, [(hd_path, 0x5EED)], 1920, 1080, HD_FRAMES)
-            gen_info = fa.result()[0]
+            noise_infos = [f.result()[0] for f in fa]
+            gen_info = noise_infos[0]
             gb_infos = [f.result()[0] for f in fc]
             content_info = gb_infos[0]
+            glong_info = fl.result()[0]
+            ghd_info = fh.result()[0]
             fb.result()
             fd.result()
+        gb_infos = gb_infos + noise_infos
+        gb_paths = gb_paths + gb_noise
         log(f"extras inputs written in {time.perf_counter() - t0:.1f} s")
 
     prof = gprof = None
@@ -1235,6 +1284,15 @@ def main() -> None:
                                                   "closed loop by SAD decisions with quantised residuals; "
                                                   "CABAC, 8x8 transform, B pyramid, implicit weights, "
                                                   "deblocking, keyint ~8 s)", content_info),
+                ("general_long", glong_path, f"BASELINE config [2]'s path on real syntax: one "
+                                             f"{GLONG_FRAMES / FPS / 60:.0f}-min 720p CONTENT stream "
+                                             f"({GLONG_FRAMES} frames, the general decoder in windows of "
+                                             f"{GLONG_WINDOW} frames on two rings: parse of window i + 1 "
+                                             f"beside the reconstruction of window i)", glong_info),
+                ("general_hd", ghd_path, f"BASELINE config [4]'s resolution on real syntax: one "
+                                         f"{GHD_FRAMES / FPS / 60:.0f}-min 1080p CONTENT stream "
+                                         f"({GHD_FRAMES} frames, coded 1920x1088 with display crop, "
+                                         f"thumbnails k=6, general decoder)", ghd_info),
                 ("long_video", long_path, "BASELINE config [2]: one 2-h 720p video "
                                           "(216 000 frames), streamed two-ring decode", None),
                 ("hd_1080p", hd_path, f"BASELINE config [4] per-GPU share, sampled: one 1080p video of "
@@ -1242,8 +1300,9 @@ def main() -> None:
                                       f"per GPU), coded 1920x1088 with display crop, thumbnails k=6, "
                                       f"streamed decode", None)):
             try:
-                r = run_single(p, gpu=gpu, k=6 if key == "hd_1080p" else 4, steps=3, threads=threads,
-                               label=label, planted=info["cuts"] if info else None)
+                r = run_single(p, gpu=gpu, k=6 if key in ("hd_1080p", "general_hd") else 4, steps=3,
+                               threads=threads, label=label, planted=info["cuts"] if info else None,
+                               window_frames=GLONG_WINDOW if key == "general_long" else 0)
                 if gprof and gprof.get(key):
                     r["kernels"] = general_kernel_rooflines(gprof[key], 1280, 720, 4, r["frames"],
                                                             80 * 45)
@@ -1258,9 +1317,11 @@ def main() -> None:
         # to the driver, whose clear then cost the open ~6 s (r05d: alloc_ms
         # 6 230)
         try:
-            extra["general_batch"] = general_batch_record(gb_paths, gpu, threads, [x["cuts"] for x in gb_infos])
+            extra["general_batch"] = general_batch_record(gb_paths, gpu, threads, [x["cuts"] for x in gb_infos],
+                                                          n_content=vpg)
             log(f"general_batch: {extra['general_batch']['value']} frames/s, "
                 f"x{extra['general_batch']['batch_over_single']} of one video's step, "
+                f"mixed {extra['general_batch']['mixed']['value']} frames/s, "
                 f"parity {extra['general_batch']['parity']['all_equal']}")
         except Exception as exc:  # noqa: BLE001 - reported in the line
             extra["general_batch"] = {"error": f"{type(exc).__name__}: {exc}"}
@@ -1287,7 +1348,8 @@ def main() -> None:
                                        (args.dist_backend if world > 1 else
                                         ("rccl (world-size-1 NCCL group, always_gather) at N=1"
                                          if gather_always else (one_rank_group or "none at N=1")))),
-                       "segment_counts": counts},
+                       "segment_counts": counts,
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)")},
             "roofline": roof,
             "roofline_decode": roof_decode,
             "parity": parity,
@@ -1310,7 +1372,7 @@ def main() -> None:
     if not args.video:
         shutil.rmtree(tmpdir, ignore_errors=True)
     else:
-        for p in (gen_path, long_path, hd_path, *gb_paths):
+        for p in (gen_path, long_path, hd_path, glong_path, ghd_path, *gb_paths):
             if p is not None:
                 Path(p).unlink(missing_ok=True)
     if world > 1:

@@ -17,7 +17,7 @@
 // -DVTS_STATS: count the parser's trace points (VTS_PARSE_TRACE: 0 macroblock,
 // 1 context-coded bin, 2 bypass bin, 3 terminate bin) for fh_stats()
 #ifdef VTS_STATS
-static unsigned long long g_trace[8];
+static unsigned long long g_trace[32];
 #define VTS_PARSE_TRACE(k) (++g_trace[(k)])
 extern "C" void fh_stats(unsigned long long *out) {
   for (int i = 0; i < 8; ++i) out[i] = g_trace[i];

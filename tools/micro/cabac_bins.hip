@@ -16,7 +16,7 @@
 #include <cstdlib>
 #include <vector>
 
-static unsigned long long g_trace[8];
+static unsigned long long g_trace[32];
 #if !defined(__HIP_DEVICE_COMPILE__)
 #define VTS_PARSE_TRACE(k) (++g_trace[(k)])
 #endif

@@ -146,7 +146,23 @@ __global__ void __launch_bounds__(64) engine_kernel(Run r, uint32_t *out, unsign
   p.cab_init(true, 26);
   unsigned long long t0 = 0, t1 = 0;
   uint32_t acc = 0;
-  if (r.engine == 0) {
+  if (r.engine == 0 && r.mode == 3) {  // 16 decisions per loop trip, nothing else in the loop
+    p.cab_start();
+    t0 = __builtin_amdgcn_s_memtime();
+    for (int b = 0; b < r.n; b += 16) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc += p.dec(60);
+    }
+    t1 = __builtin_amdgcn_s_memtime();
+  } else if (r.engine == 0 && r.mode == 4) {  // 16 bypass bins per trip
+    p.cab_start();
+    t0 = __builtin_amdgcn_s_memtime();
+    for (int b = 0; b < r.n; b += 16) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc += p.bypass();
+    }
+    t1 = __builtin_amdgcn_s_memtime();
+  } else if (r.engine == 0) {
     p.cab_start();
     t0 = __builtin_amdgcn_s_memtime();
     acc = loop([&](int c) { return p.dec(c); }, r, r.bits);
@@ -202,11 +218,11 @@ int main(int argc, char **argv) {
   (void)hipMalloc(&dcyc, 8);
   (void)hipMalloc(&dbits, words * 4);
   (void)hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice);
-  const char *modes[] = {"const", "var", "pair"};
+  const char *modes[] = {"const", "var", "pair", "const_unrolled16", "bypass_unrolled16"};
   const char *engines[] = {"prod", "sdword", "sdwordc", "vdword"};
-  for (int mode = 0; mode < 3; ++mode) {
+  for (int mode = 0; mode < 5; ++mode) {
     std::vector<uint32_t> ref(words), got(words);
-    for (int eng = 0; eng < 4; ++eng) {
+    for (int eng = 0; eng < (mode >= 3 ? 1 : 4); ++eng) {
       Run r{d, len, n, mode, eng, dbits};
       hipLaunchKernelGGL(engine_kernel, dim3(1), dim3(64), 0, 0, r, dout, dcyc);  // warm-up
       hipEvent_t e0, e1;

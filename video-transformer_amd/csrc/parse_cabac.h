@@ -210,7 +210,7 @@ struct CabacSyn {
   // bits the engine has consumed (9.3.1.2's 9 + every renormalisation shift)
   VTS_HD VTS_INLINE int32_t cab_consumed() const { return br.consumed() - la; }
   VTS_HD VTS_INLINE void cab_fill() {
-    if (la < 8) {
+    if (VTS_UNLIKELY(la < 8)) {
       val |= br.bits(16) << (7 - la);
       la += 16;
     }
@@ -240,15 +240,13 @@ struct CabacSyn {
         st[t].set(w, word);
       }
   }
-  VTS_HD VTS_INLINE uint32_t dec(int ctx) {  // DecodeDecision
+  // DecodeDecision on slot q of lane table kTab (ctx_slot / ctx_tab): the
+  // table known at compile time, so only its lane is read and written
+  template <int kTab>
+  VTS_HD VTS_INLINE uint32_t dec_slot(uint32_t q) {
     VTS_PARSE_TRACE(1);
-    const int q = ctx_slot(ctx);
-    const uint32_t ln = static_cast<uint32_t>(q >> 2) & 63u, sh = static_cast<uint32_t>(q & 3) * 8u;
-    // which of the two lane tables: folded where it is a constant (every call
-    // site), else both are read and written with selects (no branch)
-    const bool fixed = __builtin_constant_p(ctx_tab(ctx)), hi = ctx_tab(ctx) != 0;
-    const uint32_t wa = fixed && hi ? 0u : st[0].get(ln), wb = fixed && !hi ? 0u : st[1].get(ln);
-    const uint32_t word = hi ? wb : wa;
+    const uint32_t ln = (q >> 2) & 63u, sh = (q & 3u) * 8u;
+    const uint32_t word = st[kTab].get(ln);
     const uint32_t s = (word >> sh) & 127u, ps = s >> 1, mps = s & 1u;
     const uint32_t lpsr = (lps.get(ps) >> ((range >> 3) & 24u)) & 255u;
     const uint32_t tw = trn.get(ps);  // read on both paths: no branch
@@ -259,15 +257,42 @@ struct CabacSyn {
     const uint32_t ns = VTS_EU(((tw >> (lpsb ? 0u : 8u)) & 127u) ^ mps);
     val -= lpsb ? rs : 0u;
     range = lpsb ? lpsr : range;
-    const uint32_t nw = (word & ~(255u << sh)) | (ns << sh);
-    if (fixed) {
-      if (hi) st[1].set(ln, nw);
-      else st[0].set(ln, nw);
-    } else {
-      st[0].set(ln, hi ? wa : nw);
-      st[1].set(ln, hi ? nw : wb);
-    }
+    st[kTab].set(ln, (word & ~(255u << sh)) | (ns << sh));
     const int n = static_cast<int>(VTS_EU(__builtin_clz(range) - 23));  // RenormD as one shift (0..6)
+    range <<= n;
+    val <<= n;
+    la -= n;
+    cab_fill();
+    VTS_PARSE_TRACE(10);
+    return VTS_EU(bin);
+  }
+  VTS_HD VTS_INLINE uint32_t dec(int ctx) {  // DecodeDecision
+    // which of the two lane tables: folded where it is a constant (every call
+    // site but the residual loops, which call dec_slot), else both are read
+    // and written with selects (no branch)
+    if (__builtin_constant_p(ctx_tab(ctx)))
+      return ctx_tab(ctx) ? dec_slot<1>(static_cast<uint32_t>(ctx_slot(ctx)))
+                          : dec_slot<0>(static_cast<uint32_t>(ctx_slot(ctx)));
+    VTS_PARSE_TRACE(1);
+    const int q = ctx_slot(ctx);
+    const uint32_t ln = static_cast<uint32_t>(q >> 2) & 63u, sh = static_cast<uint32_t>(q & 3) * 8u;
+    const bool hi = ctx_tab(ctx) != 0;
+    const uint32_t wa = st[0].get(ln), wb = st[1].get(ln);
+    const uint32_t word = hi ? wb : wa;
+    const uint32_t s = (word >> sh) & 127u, ps = s >> 1, mps = s & 1u;
+    const uint32_t lpsr = (lps.get(ps) >> ((range >> 3) & 24u)) & 255u;
+    const uint32_t tw = trn.get(ps);
+    range -= lpsr;
+    const uint32_t rs = range << 23;
+    const bool lpsb = val >= rs;
+    const uint32_t bin = mps ^ (lpsb ? 1u : 0u);
+    const uint32_t ns = VTS_EU(((tw >> (lpsb ? 0u : 8u)) & 127u) ^ mps);
+    val -= lpsb ? rs : 0u;
+    range = lpsb ? lpsr : range;
+    const uint32_t nw = (word & ~(255u << sh)) | (ns << sh);
+    st[0].set(ln, hi ? wa : nw);
+    st[1].set(ln, hi ? nw : wb);
+    const int n = static_cast<int>(VTS_EU(__builtin_clz(range) - 23));
     range <<= n;
     val <<= n;
     la -= n;
@@ -284,11 +309,10 @@ struct CabacSyn {
     --la;
     cab_fill();
     const uint32_t rs = range << 23;
-    if (VTS_EU((top_bit || val >= rs) ? 1u : 0u)) {
-      val -= rs;
-      return 1;
-    }
-    return 0;
+    const uint32_t b = VTS_EU((top_bit || val >= rs) ? 1u : 0u);  // no branch: the bin selects
+    val -= b ? rs : 0u;
+    VTS_PARSE_TRACE(11);
+    return b;
   }
   VTS_HD VTS_INLINE uint32_t term() {  // DecodeTerminate: 1 ends parsing, no renormalisation
     VTS_PARSE_TRACE(3);
@@ -373,6 +397,7 @@ struct CabacSyn {
   // a coded macroblock: the record image reset, the |mvd| grid's borders from
   // the neighbours' edges (one cell per lane)
   VTS_HD VTS_INLINE void init_mb(int addr) {
+    VTS_PARSE_TRACE(9);
     const int xcol = addr % mbw;
 #if defined(__HIP_DEVICE_COMPILE__)
     // the record's initial dwords, one per lane: epoch, slice, 0 coef / blocks
@@ -486,6 +511,7 @@ struct CabacSyn {
   // lane), its edges for the neighbours to the right and below (the flags
   // scalar, the |mvd| bytes one per lane)
   VTS_HD VTS_INLINE void end_mb(int addr) {
+    VTS_PARSE_TRACE(8);
     const uint32_t fr = edge_flags(true), fbm = edge_flags(false);
     SynEdge *te = &top[addr % mbw];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -552,6 +578,35 @@ struct CabacSyn {
     if (cur().blocks == 0) cur().coef = blk_at;
     cur().blocks |= 1u << bit;
     ++blk_at;
+  }
+  // The block being decoded by residual_t: on the device coefficient j
+  // (raster position; an 8x8 block's 64 in raster order, its four stored
+  // blocks lanes 16k..16k+15) lives in lane j of cv, so a level is one select
+  // and the store one 2-byte write per lane, with no LDS round trip (the
+  // scratch copy, sc->blk / blk8, stays the host's, and I_PCM's)
+#if defined(__HIP_DEVICE_COMPILE__)
+  int32_t cv;
+  VTS_HD VTS_INLINE void coef_clear(int16_t *, int) { cv = 0; }
+  VTS_HD VTS_INLINE void coef_set(int16_t *, int pos, int v) { cv = lane_ == pos ? v : cv; }
+#else
+  VTS_HD VTS_INLINE void coef_clear(int16_t *dst, int n) { zero16x(dst, n); }
+  VTS_HD VTS_INLINE void coef_set(int16_t *dst, int pos, int v) { dst[pos] = static_cast<int16_t>(v); }
+#endif
+  // store nblk (1 or 4) consecutive blocks of the decoded block as the next
+  // arena blocks; bit = the first's kBlk* index (room reserved by the caller)
+  VTS_HD VTS_INLINE void store_coefs(uint32_t bit, int nblk, const int16_t *src) {
+    VTS_PARSE_TRACE(7);
+    int16_t *dst = arena + 16 * static_cast<int64_t>(blk_at);
+#if defined(__HIP_DEVICE_COMPILE__)
+    (void)src;
+    if (lane_ < 16 * nblk) dst[lane_] = static_cast<int16_t>(cv);
+#else
+    for (int i = 0; i < 16 * nblk; ++i) dst[i] = src[i];
+#endif
+    MbRec &m = cur();
+    if (m.blocks == 0) m.coef = blk_at;
+    m.blocks |= ((1u << nblk) - 1u) << bit;
+    blk_at += static_cast<uint32_t>(nblk);
   }
   VTS_HD VTS_INLINE void set_cbf(uint32_t bit) {
     MbRec &m = cur();
@@ -734,42 +789,48 @@ struct CabacSyn {
   template <bool kT8>
   VTS_HD VTS_INLINE int residual_t(int cat, int cbf_inc, int maxNum, int16_t *dst, int start) {
     typedef typename std::conditional<kT8, uint64_t, uint32_t>::type Mask;
-    if (!kT8 && !dec(85 + cbf_off(cat) + cbf_inc)) return 0;
+    // every context of a 4x4 block (ctxIdx 85..275) lies in lane table 0 at
+    // slot ctxIdx - 85, every one of an 8x8 block (402..459) in table 1 at
+    // ctxIdx - 314: the slots from their bases, no table select per bin
+    constexpr int kTab = kT8 ? 1 : 0;
+    VTS_PARSE_TRACE(13);
+    if (!kT8 && !dec_slot<0>(static_cast<uint32_t>(cbf_off(cat) + cbf_inc))) return 0;
     Mask sig = 0;
     int numc = maxNum;
-    const int sig_base = kT8 ? 402 : 105 + sig_off(cat), last_base = kT8 ? 417 : 166 + sig_off(cat);
+    const int sig_q = kT8 ? 402 - 314 : 105 - 85 + sig_off(cat), last_q = kT8 ? 417 - 314 : 166 - 85 + sig_off(cat);
     for (int i = 0; i < numc - 1; ++i) {
-      int inc_s, inc_l;
+      int qs, ql;
       if (kT8) {
         const uint32_t e = s8.get(static_cast<uint32_t>(i));
-        inc_s = static_cast<int>(e & 255u);
-        inc_l = static_cast<int>((e >> 8) & 255u);
+        qs = sig_q + static_cast<int>(e & 15u);
+        ql = last_q + static_cast<int>((e >> 8) & 15u);
       } else {
-        inc_s = inc_l = cat == 3 ? vts_min(i, 2) : i;
+        const int inc = cat == 3 ? vts_min(i, 2) : i;
+        qs = vts_min(sig_q + inc, 165 - 85);
+        ql = vts_min(last_q + inc, 226 - 85);
       }
-      if (dec(kT8 ? 402 + (inc_s & 15) : vts_min(sig_base + inc_s, 165))) {
+      if (dec_slot<kTab>(static_cast<uint32_t>(qs))) {
         sig |= Mask(1) << i;
-        if (dec(kT8 ? 417 + (inc_l & 15) : vts_min(last_base + inc_l, 226))) {
+        if (dec_slot<kTab>(static_cast<uint32_t>(ql))) {
           numc = i + 1;
           break;
         }
       }
     }
-    (void)sig_base;
-    (void)last_base;
     sig |= Mask(1) << (numc - 1);
+    VTS_PARSE_TRACE(14);
     int eq1 = 0, gt1 = 0, n = 0;
-    const int base = kT8 ? 426 : 227 + abs_off(cat);
+    const int base = kT8 ? 426 - 314 : 227 - 85 + abs_off(cat);
     while (sig) {  // the significant coefficients, highest first
       const int i = kT8 ? 63 - static_cast<int>(__builtin_clzll(static_cast<uint64_t>(sig)))
                         : 31 - static_cast<int>(__builtin_clz(static_cast<uint32_t>(sig)));
       sig &= ~(Mask(1) << i);
       int v = 0;
-      if (dec(base + (gt1 ? 0 : vts_min(4, 1 + eq1)))) {
+      if (dec_slot<kTab>(static_cast<uint32_t>(base + (gt1 ? 0 : vts_min(4, 1 + eq1))))) {
         v = 1;
-        const int inc = 5 + vts_min(4 - (cat == 3 ? 1 : 0), gt1);
-        while (v < 14 && dec(base + inc)) ++v;
-        if (v >= 14) {  // UEG0 suffix
+        const uint32_t qg = static_cast<uint32_t>(base + 5 + vts_min(4 - (cat == 3 ? 1 : 0), gt1));
+        while (v < 14 && dec_slot<kTab>(qg)) ++v;
+        if (VTS_UNLIKELY(v >= 14)) {  // UEG0 suffix
           int k = 0;
           while (bypass()) {
             v += 1 << k;
@@ -778,12 +839,12 @@ struct CabacSyn {
           while (k--) v += static_cast<int>(bypass()) << k;
         }
       }
-      int lvl = v + 1;
-      if (bypass()) lvl = -lvl;
-      if (lvl > 32767 || lvl < -32768) return -1;
+      const int mag = v + 1;
+      const int lvl = bypass() ? -mag : mag;
+      if (VTS_UNLIKELY(mag > 32768 || lvl > 32767)) return -1;
       const int pos = kT8 ? static_cast<int>((s8.get(static_cast<uint32_t>(i)) >> 16) & 63u)
                           : (cat == 3 ? i : zz4(i + start));
-      dst[pos] = static_cast<int16_t>(lvl);
+      coef_set(dst, pos, lvl);
       if (v == 0) ++eq1;
       else ++gt1;
       ++n;
@@ -951,6 +1012,7 @@ struct CabacSyn {
     prev_qpd = qpd;
     m.qp = static_cast<uint8_t>(*qp);
     // ---- residual (7.3.5.3), blocks in bitstream order
+    VTS_PARSE_TRACE(12);
     const bool intra = m.type == kMbI4x4 || m.type == kMbI16;
     const bool t8 = (m.modes & kModeT8) != 0;
     // condTermFlagN (9.3.3.1.1.9) of coded_block_flag across the edges: an
@@ -1005,7 +1067,7 @@ struct CabacSyn {
         const uint32_t cb = cy ? (cbf >> (kBlkChromaAc0 - 16 + 4 * pl + cx)) & 1u : (eb >> (kECacSh + 2 * pl + cx)) & 1u;
         inc = static_cast<int>(ca + 2 * cb);
       }
-      zero16x(dst, cat == 5 ? 64 : 16);
+      coef_clear(dst, cat == 5 ? 64 : 16);
       const int nc = cat == 5 ? residual_t<true>(5, 0, 64, dst, 0) : residual_t<false>(cat, inc, maxNum, dst, start);
       if (nc < 0) { err |= DEC_E_SYNTAX; return false; }
       if (cat == 5) {  // the quarter's 4 blocks: raster 8x8 rows 2j, 2j + 1
@@ -1014,8 +1076,7 @@ struct CabacSyn {
           m.nz[rs[j]] = static_cast<uint8_t>(nc > 255 ? 255 : nc);
           set_cbf(1u + static_cast<uint32_t>(rs[j]));
         }
-        if (nc)
-          for (int j = 0; j < 4; ++j) store_block(bt + j, sc->blk8 + 16 * j);
+        if (nc) store_coefs(bt, 4, sc->blk8);
         continue;
       }
       if (cat == 1 || cat == 2) {
@@ -1024,7 +1085,7 @@ struct CabacSyn {
       }
       if (nc) {
         set_cbf(bt == kBlkI16Dc ? 0u : (cat <= 2 ? 1u + static_cast<uint32_t>(r) : bt));
-        store_block(bt, sc->blk);
+        store_coefs(bt, 1, sc->blk);
       }
     }
     if (br.err || cab_consumed() > 8 * br.size) {
@@ -1080,6 +1141,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   p.cab_tables();
   p.cab_init(!s.is_p, s.qp);
   p.cab_start();
+  VTS_PARSE_TRACE(15);
   int addr = s.first_mb, qp = s.qp;
   for (;;) {
     if (addr >= nmb) {
@@ -1106,6 +1168,7 @@ VTS_HD VTS_INLINE uint32_t parse_slice_cabac(const uint8_t *rbsp, int32_t rbsp_l
   }
   // the arithmetic decoder has read through the stop bit
   if (!p.err && (p.br.err || p.cab_consumed() != stop_bit + 1)) p.err |= DEC_E_SYNTAX;
+  VTS_PARSE_TRACE(16);
   return p.err;
 }
 

@@ -232,7 +232,7 @@ struct RbspBitsT {
   VTS_HD VTS_INLINE uint32_t load4(int32_t i) {
     constexpr int32_t kBlk = 4 * (kW - 1);
     const int32_t blk = i - (i % kBlk);
-    if (blk != cache_at) {
+    if (VTS_UNLIKELY(blk != cache_at)) {
       const uint8_t *pb = base + blk;
       const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(pb) & 3);
       // plain loads from a base the compiler can see is dword aligned, all in
@@ -258,7 +258,7 @@ struct RbspBitsT {
     pos += 4;
   }
   VTS_HD VTS_INLINE void ensure(int n) {  // n <= 32
-    if (nb < n) refill();
+    if (VTS_UNLIKELY(nb < n)) refill();
   }
   VTS_HD VTS_INLINE void skip(int n) {  // n < 64, n <= nb
     win <<= n;

@@ -18,6 +18,10 @@
 #define VTS_HD
 #endif
 #define VTS_INLINE inline __attribute__((always_inline))
+// A lone parse wave pays ~16-20 cycles for every taken branch and ~2 for a
+// fall-through (profiles/r06i_single_wave_issue_latencies.jsonl): rare paths
+// (bit-reader refills) are laid out off the common path
+#define VTS_UNLIKELY(x) __builtin_expect(!!(x), 0)
 
 namespace vts {
 

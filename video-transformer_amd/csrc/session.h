@@ -152,6 +152,7 @@ struct vts_ctx {
   int general_groups = 2;  // general decoder: GOP groups reconstructing on s_dec / s_grp[g - 1]
                            // (DESIGN.md §5b); VTS_GENERAL_GROUPS (1..4) overrides
   hipStream_t s_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};
+  int stream_kind = 0;     // the pool its stream set came from (session.hip streams_take)
   hipEvent_t ev_grp[kMaxGroups - 1] = {nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> ev;  // per window: dec start, parsed, decoded, score start, scored, spare
   std::vector<hipEvent_t> lev;  // per window: (start, end) per reconstruct launch, then one per parse chunk
@@ -214,11 +215,12 @@ struct vts_ctx {
   std::vector<int32_t> fslice_nmbs;     // per fslice: its macroblocks (arena ranges)
   // CABAC: slices take blocks from their window's arena in chunks (h264_full.h
   // kArenaChunk, one counter per window).  The capacity starts at an estimate
-  // (arena_per_byte blocks per slice byte, VTS_ARENA_PER_BYTE; the streams
-  // here store 0.46-0.87) and grows, up to arena_bound (32 per byte: every
-  // stored block costs at least one bypass bin), when a run reports
-  // DEC_E_ARENA, which re-runs it (arena_reruns)
-  int arena_per_byte = 1;
+  // (arena_q4 quarter blocks per slice byte: 0.75, + 1/8 and a chunk per
+  // slice of slack; VTS_ARENA_PER_BYTE = whole blocks per byte, 0 forces the
+  // growth; the streams here store 0.46-0.87) and grows, up to arena_bound
+  // (32 per byte: every stored block costs at least one bypass bin), when a
+  // run reports DEC_E_ARENA, which re-runs it (arena_reruns)
+  int arena_q4 = 3;
   int64_t arena_bound = 0;              // per ring: the capacity no valid stream exceeds
   int64_t arena_reruns = 0;
   uint32_t *d_arena_top = nullptr;      // per window: blocks its parse handed out (asked for)

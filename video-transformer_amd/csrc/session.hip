@@ -68,27 +68,68 @@ constexpr int64_t kPad = 256;
 // bench after eight concurrent sessions on 16 queues; 218 -> 288 ms on 4,
 // tools/gpu/queue_probe.py).  Sessions open at the same time never share one.
 std::mutex g_stream_mu;
-std::map<int, std::vector<std::vector<hipStream_t>>> g_stream_sets;
+// free sets per (device, kind); sets handed out per device
+std::map<std::pair<int, int>, std::vector<std::vector<hipStream_t>>> g_stream_sets;
+std::map<int, int> g_sets_in_use;
+std::map<int, int> g_own_sets;  // CU-masked sets created per device (in use or pooled)
 constexpr int kSessionStreams = 3 + (vts_ctx::kMaxGroups - 1);
+// at most this many CU-masked sets per device: every one holds six hardware
+// queues for good, and a process with many more queues than the GPU maps at
+// once is time-sliced across all of them — after the bench's batches had
+// left 7 such sets (42 queues) pooled, single sessions ran 2x slower
+// (profiles/r06j_bench_default_720p_batch.json); 3 sets, 18 queues, measured
+// without a slowdown (r06i)
+constexpr int kMaxOwnSets = 3;
+
+// Which kind of stream set a session gets: 0 plain non-blocking streams
+// (HIP spreads a process's streams over its GPU_MAX_HW_QUEUES shared hardware
+// queues, 4 by default), 1 streams created with a CU mask naming every
+// compute unit (HIP backs each with a hardware queue of its own).  A session
+// opened while no other holds a set gets plain streams; one opened beside
+// others gets its own queues, so concurrent sessions' launches never wait
+// behind each other's event barriers in a shared queue.  Measured on 4 queues
+// (profiles/r06i_batch_stream_policies.json, 4 content sessions through
+// plan_batch): all plain 3.99x one session's step, this policy 2.35x (on 16
+// plain queues 2.82x); every set CU-masked also overlaps (1.95x of its own
+// step) but one session alone on its own queues is 31 % slower (392 vs 300 ms).
+// Beyond kMaxOwnSets CU-masked sets, sessions take plain streams again.
+int stream_kind_for(int in_use, bool own_free) { return in_use > 0 && own_free ? 1 : 0; }
 
 int streams_take(vts_ctx *c) {
   std::vector<hipStream_t> set;
   {
     std::lock_guard<std::mutex> lk(g_stream_mu);
-    auto &v = g_stream_sets[c->device];
+    int &in_use = g_sets_in_use[c->device];
+    const bool own_free = !g_stream_sets[{c->device, 1}].empty() || g_own_sets[c->device] < kMaxOwnSets;
+    const int kind = stream_kind_for(in_use, own_free);
+    auto &v = g_stream_sets[{c->device, kind}];
     if (!v.empty()) {
       set = v.back();
       v.pop_back();
     } else {
       set.assign(kSessionStreams, nullptr);
+      std::vector<uint32_t> mask;
+      if (kind == 1) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
+          return fail(VTS_E_HIP, "hipDeviceGetAttribute(multiProcessorCount)");
+        mask.assign(static_cast<size_t>((cus + 31) / 32), 0u);
+        for (int i = 0; i < cus; ++i) mask[static_cast<size_t>(i >> 5)] |= 1u << (i & 31);
+      }
       for (auto &x : set) {
-        if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) {
+        const hipError_t e = kind == 1
+                                 ? hipExtStreamCreateWithCUMask(&x, static_cast<uint32_t>(mask.size()), mask.data())
+                                 : hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+        if (e != hipSuccess) {
           for (auto &y : set)
             if (y) (void)hipStreamDestroy(y);
           return fail(VTS_E_HIP, "hipStreamCreate");
         }
       }
+      if (kind == 1) ++g_own_sets[c->device];
     }
+    ++in_use;
+    c->stream_kind = kind;
   }
   c->s_dec = set[0];
   c->s_score = set[1];
@@ -101,7 +142,8 @@ void streams_give(vts_ctx *c) {  // every stream idle
   std::vector<hipStream_t> set = {c->s_dec, c->s_score, c->s_parse};
   for (int g = 0; g + 1 < vts_ctx::kMaxGroups; ++g) set.push_back(c->s_grp[g]);
   std::lock_guard<std::mutex> lk(g_stream_mu);
-  g_stream_sets[c->device].push_back(set);
+  g_stream_sets[{c->device, c->stream_kind}].push_back(set);
+  --g_sets_in_use[c->device];
 }
 
 }  // namespace

@@ -39,10 +39,11 @@ namespace {
 // (x264-like content: ~0.9 blocks per byte); the window's arena is sized from
 // `per_byte` blocks per byte instead (cabac_window_blocks) and grows when a run
 // overflows it.  Either way never more than the 27 blocks a macroblock holds.
-int64_t slice_arena_cap(bool cabac, int64_t n_mbs, int64_t nal_size, int64_t per_byte) {
+// (per_byte_q4: quarter blocks per byte)
+int64_t slice_arena_cap(bool cabac, int64_t n_mbs, int64_t nal_size, int64_t per_byte_q4) {
   const int64_t per_mb = static_cast<int64_t>(kMbMaxBlocks) * n_mbs;
   if (!cabac) return std::min<int64_t>(per_mb, 3ll * nal_size + 27);
-  return std::min<int64_t>(per_mb, per_byte * nal_size + 64);
+  return std::min<int64_t>(per_mb, per_byte_q4 * nal_size / 4 + 64);
 }
 // CABAC: a window's arena for `blocks` stored blocks over `n_slices` slices:
 // each slice leaves its last chunk partly unused and a chunk switch abandons
@@ -154,12 +155,12 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       plevel[static_cast<size_t>(f)] = std::max(plevel[static_cast<size_t>(f)], plevel[static_cast<size_t>(col)] + 1);
   // coefficient blocks each slice may need (slice_arena_cap): CAVLC its
   // range, CABAC its share of the window's arena estimate
-  c->arena_per_byte = 1;
-  if (const char *ev = std::getenv("VTS_ARENA_PER_BYTE")) c->arena_per_byte = std::max(0, std::atoi(ev));
+  c->arena_q4 = 3;  // 0.75 blocks per byte
+  if (const char *ev = std::getenv("VTS_ARENA_PER_BYTE")) c->arena_q4 = 4 * std::max(0, std::atoi(ev));
   std::vector<int64_t> cap(slices.size());
   int64_t cap_total = 0;
   for (size_t i = 0; i < slices.size(); ++i) {
-    cap[i] = slice_arena_cap(c->pps.entropy_coding_mode, slices[i].n_mbs, slices[i].nal_size, c->arena_per_byte);
+    cap[i] = slice_arena_cap(c->pps.entropy_coding_mode, slices[i].n_mbs, slices[i].nal_size, c->arena_q4);
     cap_total += cap[i];
   }
   // windows
@@ -271,7 +272,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
           d.arena_cap = static_cast<uint32_t>(cap[static_cast<size_t>(si)]);
         }
         arena += cap[static_cast<size_t>(si)];
-        abound += slice_arena_cap(true, s.n_mbs, s.nal_size, 32);
+        abound += slice_arena_cap(true, s.n_mbs, s.nal_size, 4 * 32);
         c->fslice_nmbs.push_back(static_cast<int32_t>(s.n_mbs));
         d.ext = -1;
         for (int i = 0; i < 32; ++i) {
@@ -364,7 +365,7 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
     if (c->fprm.cabac) {
       // (VTS_ARENA_PER_BYTE=0: one chunk, the tests' way to make every run
       // outgrow its first arena)
-      arena = c->arena_per_byte == 0 ? static_cast<int64_t>(kArenaChunk) : cabac_window_blocks(arena, w.fs1 - w.fs0);
+      arena = c->arena_q4 == 0 ? static_cast<int64_t>(kArenaChunk) : cabac_window_blocks(arena, w.fs1 - w.fs0);
       abound = cabac_window_blocks(abound, w.fs1 - w.fs0);
       // the chunk counter and block indices are 32-bit: the bound stays below
       // 2^32 with a chunk per slice of headroom for requests past the end
