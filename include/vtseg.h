@@ -333,7 +333,10 @@ int vts_open_timings(const vts_ctx *ctx, double *ms, int32_t cap);
  * launches / chains, 7 chain slots, 8 general decoder (1/0), 9 runs repeated
  * with the bound's CABAC coefficient arena, 10 coefficient blocks per ring,
  * 11 decoded-picture surfaces per ring when the general decoder recycles them
- * (0: one per window frame); < 0 on error. */
+ * (0: one per window frame), 12 the session's HIP stream set (0 plain
+ * streams on the process's shared hardware queues, 1 streams with hardware
+ * queues of their own: sessions opened beside others, at most 3 such sets
+ * per device); < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);  /* 8: general decoder in use (1/0) */
 int vts_close(vts_ctx *ctx);
 

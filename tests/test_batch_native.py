@@ -109,3 +109,43 @@ def test_native_batch_over_a_one_rank_rccl_communicator(tmp_path):
     assert _rows(got) == _rows(want)
     assert _rows(got2) == _rows(plan_batch(paths, CONFIG))
     assert all(i.rank == 0 for i in got)
+
+
+@pytest.mark.gpu
+def test_concurrent_sessions_take_their_own_hardware_queues(tmp_path):
+    """The stream-set policy (session.hip streams_take): the first of several
+    open sessions on plain streams, the next three on CU-masked streams with
+    hardware queues of their own, any further one on plain streams again (at
+    most 3 such sets per device); every session's scores equal a lone
+    session's, runs submitted together or one by one; a session opened after
+    all closed is plain again."""
+    import numpy as np
+    import torch
+    assert torch.cuda.is_available()
+    paths = _videos(tmp_path, 5, frames=(600,))
+    with scene.VideoScorer(paths[0], device=0) as v:
+        assert not v.own_queues()
+        ref = v.score().scores.copy()
+    vs = [scene.VideoScorer(p, device=0) for p in paths]
+    try:
+        assert [v.own_queues() for v in vs] == [False, True, True, True, False]
+        for v in vs:
+            v.run_async()
+        for v in vs:
+            v.wait()
+        for i, v in enumerate(vs):
+            want = ref if i == 0 else None
+            got = v.score().scores
+            if want is not None:
+                assert np.array_equal(got, want)
+        alone = []
+        for p in paths:
+            with scene.VideoScorer(p, device=0) as w:
+                alone.append(w.score().scores.copy())
+        for v, a in zip(vs, alone):
+            assert np.array_equal(v.score().scores, a)
+    finally:
+        for v in vs:
+            v.close()
+    with scene.VideoScorer(paths[1], device=0) as v:
+        assert not v.own_queues()

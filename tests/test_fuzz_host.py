@@ -22,6 +22,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+import fmp4
 import oracle
 from vtseg import scene
 from vtseg.video_utils import probe_duration
@@ -68,6 +69,9 @@ def _seeds(d: Path) -> list[Path]:
     p = d / "content.mp4"
     scene.synth_write(p, seed=11, coding="full", bframes=True, weighted="implicit", cabac=True,
                       transform_8x8=True, content=True, **kw)
+    out.append(p)
+    p = d / "fragmented.mp4"  # movie fragments (tfhd / tfdt / trun) of the CABAC B stream
+    fmp4.fragment(out[2], p, per_fragment=3)
     out.append(p)
     out.append(REAL)
     return out

@@ -303,11 +303,161 @@ std::string parse_trak(const Box &trak, Mp4Info *info) {
   return "";
 }
 
+// ISO/IEC 14496-12 §8.8: the samples of the movie fragments appended to the
+// tracks' tables.  trex gives each track's defaults, tfhd a fragment's
+// (track, base data offset, defaults), tfdt its first decode time, trun its
+// samples (duration, size, flags, composition offset, each present or
+// defaulted; data_offset from the base, else on from the previous run).
+// Sync = sample_is_non_sync_sample (flags bit 16) clear.
+struct Moof {
+  int64_t start;                 // file offset of the moof box
+  std::vector<uint8_t> payload;
+};
+struct Trex {
+  uint32_t duration = 0, size = 0, flags = 0;
+};
+
+std::string apply_fragments(const Box &moov, const std::vector<Moof> &moofs, Mp4Info *info) {
+  std::vector<std::pair<uint32_t, Trex>> trex;
+  Box mvex;
+  if (find_child(moov, fourcc("mvex"), &mvex)) {
+    const uint8_t *cur = mvex.p, *end = mvex.p + mvex.n;
+    Box b;
+    while (next_box(cur, end, &b)) {
+      if (b.type == fourcc("trex") && b.n >= 24) {
+        Trex t;
+        t.duration = rd32(b.p + 12);
+        t.size = rd32(b.p + 16);
+        t.flags = rd32(b.p + 20);
+        trex.emplace_back(rd32(b.p + 4), t);
+      } else if (b.type == fourcc("mehd") && b.n >= 8) {
+        info->fragment_duration = b.p[0] == 1 ? (b.n >= 12 ? static_cast<int64_t>(rd64(b.p + 4)) : 0) : rd32(b.p + 4);
+      }
+    }
+  }
+  auto track_of = [&](uint32_t id) -> Mp4VideoTrack * {
+    for (Mp4VideoTrack &t : info->tracks)
+      if (t.track_id == id) return &t;
+    return nullptr;
+  };
+  std::vector<int64_t> next_dts(info->tracks.size(), -1);  // decode time after each track's last sample
+  for (size_t k = 0; k < info->tracks.size(); ++k) {
+    const Mp4VideoTrack &t = info->tracks[k];
+    if (!t.dts.empty()) next_dts[k] = t.dts.back();  // (the moov's last sample's duration is unknown here)
+  }
+  for (const Moof &mf : moofs) {
+    Box root{fourcc("moof"), mf.payload.data(), mf.payload.size()};
+    const uint8_t *cur = root.p, *end = root.p + root.n;
+    Box traf;
+    int64_t prev_end = mf.start;  // base of a traf without an explicit / moof base: the previous traf's data end
+    bool first_traf = true;
+    while (next_box(cur, end, &traf)) {
+      if (traf.type != fourcc("traf")) continue;
+      Box tfhd;
+      if (!find_child(traf, fourcc("tfhd"), &tfhd) || tfhd.n < 8) return "traf without tfhd";
+      const uint32_t tf = rd32(tfhd.p) & 0xffffff, id = rd32(tfhd.p + 4);
+      Mp4VideoTrack *t = track_of(id);
+      if (!t) return "movie fragment of an unknown track";
+      const size_t ti = static_cast<size_t>(t - info->tracks.data());
+      Trex d;
+      for (const auto &x : trex)
+        if (x.first == id) d = x.second;
+      size_t q = 8;
+      int64_t base;
+      auto need = [&](size_t n) { return q + n <= tfhd.n; };
+      if (tf & 0x1) {
+        if (!need(8)) return "truncated tfhd";
+        base = static_cast<int64_t>(rd64(tfhd.p + q));
+        q += 8;
+      } else {
+        base = (tf & 0x20000) || first_traf ? mf.start : prev_end;
+      }
+      if (tf & 0x2) q += 4;  // sample_description_index
+      if (tf & 0x8) {
+        if (!need(4)) return "truncated tfhd";
+        d.duration = rd32(tfhd.p + q);
+        q += 4;
+      }
+      if (tf & 0x10) {
+        if (!need(4)) return "truncated tfhd";
+        d.size = rd32(tfhd.p + q);
+        q += 4;
+      }
+      if (tf & 0x20) {
+        if (!need(4)) return "truncated tfhd";
+        d.flags = rd32(tfhd.p + q);
+        q += 4;
+      }
+      Box tfdt;
+      int64_t dts = next_dts[ti] < 0 ? 0 : next_dts[ti];
+      if (find_child(traf, fourcc("tfdt"), &tfdt) && tfdt.n >= 8)
+        dts = tfdt.p[0] == 1 ? (tfdt.n >= 12 ? static_cast<int64_t>(rd64(tfdt.p + 4)) : dts) : rd32(tfdt.p + 4);
+      int64_t pos = base;
+      const uint8_t *tc = traf.p, *te = traf.p + traf.n;
+      Box trun;
+      while (next_box(tc, te, &trun)) {
+        if (trun.type != fourcc("trun")) continue;
+        if (trun.n < 8) return "truncated trun";
+        const int ver = trun.p[0];
+        const uint32_t rf = rd32(trun.p) & 0xffffff, count = rd32(trun.p + 4);
+        size_t r = 8;
+        if (rf & 0x1) {
+          if (r + 4 > trun.n) return "truncated trun";
+          pos = base + static_cast<int32_t>(rd32(trun.p + r));
+          r += 4;
+        }
+        uint32_t first_flags = 0;
+        const bool has_first = (rf & 0x4) != 0;
+        if (has_first) {
+          if (r + 4 > trun.n) return "truncated trun";
+          first_flags = rd32(trun.p + r);
+          r += 4;
+        }
+        const size_t per = 4u * (((rf >> 8) & 1) + ((rf >> 9) & 1) + ((rf >> 10) & 1) + ((rf >> 11) & 1));
+        if (r + per * count > trun.n) return "truncated trun";
+        for (uint32_t i = 0; i < count; ++i) {
+          uint32_t dur = d.duration, sz = d.size, fl = (i == 0 && has_first) ? first_flags : d.flags;
+          int32_t cto = 0;
+          if (rf & 0x100) { dur = rd32(trun.p + r); r += 4; }
+          if (rf & 0x200) { sz = rd32(trun.p + r); r += 4; }
+          if (rf & 0x400) { fl = rd32(trun.p + r); r += 4; }
+          if (rf & 0x800) {
+            const uint32_t c = rd32(trun.p + r);
+            cto = ver == 0 && c > 0x7fffffffu ? 0x7fffffff : static_cast<int32_t>(c);
+            r += 4;
+          }
+          if (pos < 0 || pos + static_cast<int64_t>(sz) > info->file_size) return "fragment sample outside the file";
+          t->offset.push_back(pos);
+          t->size.push_back(sz);
+          t->dts.push_back(dts);
+          t->cts_offset.push_back(cto);
+          t->sync.push_back(((fl >> 16) & 1) ? 0 : 1);
+          if (cto) t->has_ctts = true;
+          pos += sz;
+          dts += dur;
+        }
+      }
+      t->has_stss = true;  // every fragment sample's sync flag is explicit
+      next_dts[ti] = dts;
+      prev_end = pos;
+      first_traf = false;
+    }
+  }
+  // the track's media duration: its fragments' end (track timescale)
+  for (size_t k = 0; k < info->tracks.size(); ++k)
+    if (next_dts[k] > info->tracks[k].duration && !moofs.empty()) info->tracks[k].duration = next_dts[k];
+  info->video.clear();
+  for (const Mp4VideoTrack &t : info->tracks)
+    if (t.handler == fourcc("vide")) info->video.push_back(t);
+  return "";
+}
+
 std::string parse_source(const Source &src, Mp4Info *info) {
   *info = Mp4Info{};
   info->file_size = src.size();
   int64_t pos = 0;
   std::vector<uint8_t> moov;
+  std::vector<Moof> moofs;
   bool have_moov = false;
   while (pos + 8 <= src.size()) {
     uint8_t h[16];
@@ -333,6 +483,12 @@ std::string parse_source(const Source &src, Mp4Info *info) {
       have_moov = true;
     } else if (type == fourcc("moof")) {
       info->fragmented = true;
+      if (size > (64ull << 20)) return "moof too large";
+      Moof m;
+      m.start = pos;
+      m.payload.resize(static_cast<size_t>(size - hdr));
+      if (!src.read(pos + hdr, m.payload.data(), m.payload.size())) return "read error";
+      moofs.push_back(std::move(m));
     }
     pos += static_cast<int64_t>(size);
   }
@@ -359,6 +515,7 @@ std::string parse_source(const Source &src, Mp4Info *info) {
       if (!e.empty()) return e;
     }
   }
+  if (info->fragmented) return apply_fragments(root, moofs, info);
   return "";
 }
 
@@ -429,6 +586,20 @@ int64_t mvhd_duration_us(const Mp4Info &info) {
   const __int128 half = ts / 2;
   const __int128 q = (num >= 0) ? (num + half) / ts : -((-num + half) / ts);
   return static_cast<int64_t>(q);
+}
+
+int64_t container_duration_us(const Mp4Info &info) {
+  if (!info.has_mvhd) return -1;
+  if (info.movie_duration > 0 || !info.fragmented) return mvhd_duration_us(info);
+  int64_t best = -1;
+  for (const Mp4VideoTrack &t : info.tracks) {
+    if (t.dts.empty()) continue;
+    Mp4Info one;  // the track's own timescale through the same rounding
+    one.movie_timescale = t.timescale;
+    one.movie_duration = t.duration - t.dts.front();
+    best = std::max(best, mvhd_duration_us(one));
+  }
+  return best;
 }
 
 // ------------------------------------------------------------------ writer

@@ -46,7 +46,10 @@ struct Mp4Info {
   int64_t movie_timescale = 0;
   int64_t movie_duration = 0;
   bool has_mvhd = false;
-  bool fragmented = false;   // moof/mvex present
+  bool fragmented = false;   // moof/mvex present: the tracks' sample tables hold
+                             // the moov's samples followed by every movie
+                             // fragment's (moof/traf/trun), in file order
+  int64_t fragment_duration = 0;  // mehd (movie timescale), 0 when absent
   int64_t file_size = 0;
   std::vector<Mp4VideoTrack> video;
   std::vector<Mp4VideoTrack> tracks;  // every track with a sample table, file order
@@ -59,6 +62,11 @@ std::string mp4_parse_memory(const uint8_t *data, int64_t size, Mp4Info *out);
 // libavformat: s->duration = av_rescale(mvhd.duration, AV_TIME_BASE, timescale)
 // (round to nearest, ties away from zero); a timescale <= 0 reads as 1.
 int64_t mvhd_duration_us(const Mp4Info &info);
+// The container duration ffprobe's format=duration reports, microseconds:
+// mvhd's when it is set; for a fragmented file whose mvhd says 0, the
+// longest track's samples (first decode time to the last sample's end, each
+// track in its own timescale, rounded as above).  -1: none.
+int64_t container_duration_us(const Mp4Info &info);
 
 // Stream-copy [start, end) seconds of every track into a new MP4 with moov
 // first (ffmpeg -ss S -i IN -t D -c copy -movflags +faststart):

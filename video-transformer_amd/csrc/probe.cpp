@@ -12,9 +12,12 @@ int fill_video_info(const Mp4Info &mp4, vts_video_info *info) {
   std::memset(info, 0, sizeof *info);
   info->movie_timescale = mp4.movie_timescale;
   info->movie_duration = mp4.movie_duration;
-  if (mp4.has_mvhd && !mp4.fragmented) {
-    info->duration_us = mvhd_duration_us(mp4);
-    info->duration = static_cast<double>(info->duration_us) / 1e6;
+  if (mp4.has_mvhd) {
+    const int64_t us = container_duration_us(mp4);
+    if (us >= 0) {
+      info->duration_us = us;
+      info->duration = static_cast<double>(us) / 1e6;
+    }
   }
   if (mp4.video.empty()) return fail(VTS_E_FORMAT, "no video track");
   const Mp4VideoTrack &t = mp4.video.front();
@@ -72,12 +75,13 @@ extern "C" int vts_probe_duration(const char *path, double *seconds) {
     fail(VTS_E_FORMAT, "no mvhd");
     return VTS_OK;
   }
-  if (mp4.fragmented) {
-    fail(VTS_E_FORMAT, "fragmented MP4: duration needs the fragment index");
+  // ffprobe prints 0 duration as "N/A" -> the reference's float() fails -> 0.0
+  const int64_t us = container_duration_us(mp4);
+  if (us < 0) {
+    fail(VTS_E_FORMAT, "fragmented MP4 without samples");
     return VTS_OK;
   }
-  // ffprobe prints 0 duration as "N/A" -> the reference's float() fails -> 0.0
-  *seconds = static_cast<double>(mvhd_duration_us(mp4)) / 1e6;
+  *seconds = static_cast<double>(us) / 1e6;
   return VTS_OK;
 }
 

@@ -366,7 +366,6 @@ std::string mp4_add_tracks(const char *video_path, const char *src_path, const c
   if (!e.empty()) return e;
   e = mp4_parse_file(src_path, &b);
   if (!e.empty()) return e;
-  if (a.fragmented || b.fragmented) return "fragmented MP4 is not supported";
   const double inf = 1e300;  // finite: ceil_ticks saturates it (frexp of inf is not a number)
   std::vector<Cut> cuts;
   for (const Mp4VideoTrack &t : a.tracks) {
@@ -392,7 +391,6 @@ std::string mp4_remux_segment(const char *in_path, double start, double end,
   Mp4Info mp4;
   std::string e = mp4_parse_file(in_path, &mp4);
   if (!e.empty()) return e;
-  if (mp4.fragmented) return "fragmented MP4 is not supported";
   if (mp4.video.empty()) return "no video track";
   std::vector<Cut> cuts;
   for (const Mp4VideoTrack &t : mp4.tracks) {

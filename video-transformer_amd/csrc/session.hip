@@ -1448,7 +1448,6 @@ extern "C" int vts_open(int device, const char *path, const vts_params *params, 
   Mp4Info mp4;
   const std::string e = mp4_parse_file(path, &mp4);
   if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
-  if (mp4.fragmented) return fail(VTS_E_UNSUPPORTED, "fragmented MP4 is not supported");
   return open_common(device, mp4, nullptr, 0, path, params, out, t0);
 }
 
@@ -1461,7 +1460,6 @@ extern "C" int vts_open_memory(int device, const uint8_t *data, int64_t size, co
   Mp4Info mp4;
   const std::string e = mp4_parse_memory(data, size, &mp4);
   if (!e.empty()) return fail(VTS_E_FORMAT, "%s", e.c_str());
-  if (mp4.fragmented) return fail(VTS_E_UNSUPPORTED, "fragmented MP4 is not supported");
   return open_common(device, mp4, data, size, nullptr, params, out, t0);
 }
 
@@ -1636,6 +1634,7 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
     case 9: return c->arena_reruns;                 // runs repeated with a larger coefficient arena
     case 10: return c->arena_blocks;                // coefficient blocks per ring (general decoder)
     case 11: return c->surf_pool ? c->surf_count : 0;  // recycled surfaces per ring (general decoder)
+    case 12: return c->s_dec ? c->stream_kind : -1;   // stream set: 0 plain, 1 own hardware queues
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
   }
 }

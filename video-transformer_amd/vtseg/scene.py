@@ -193,6 +193,11 @@ class VideoScorer:
         subset kernels)."""
         return bool(self._lib.vts_schedule_info(self._ctx, 8))
 
+    def own_queues(self) -> bool:
+        """The session's HIP streams have hardware queues of their own (it was
+        opened beside other sessions; session.hip streams_take)."""
+        return int(self._lib.vts_schedule_info(self._ctx, 12)) == 1
+
     def windows(self) -> int:
         """Decode windows per run (1 = the whole video at once; more = the
         streamed two-ring schedule)."""

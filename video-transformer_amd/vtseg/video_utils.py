@@ -3,12 +3,13 @@
 ``probe_duration`` reads the ISO-BMFF ``moov`` box natively (libvtseg
 ``vts_probe_duration``) and returns the value ffprobe prints for
 ``-show_entries format=duration`` on such files:
-``av_rescale(mvhd.duration, 1_000_000, mvhd.timescale) / 1e6``.  For any other
-container it keeps the reference behaviour exactly: run ffprobe with the
-reference's arguments and 15 s timeout.  Where the native parser has no
-answer for an ISO-BMFF file (fragmented MP4, no ``mvhd``, a parse error, a
-zero duration) it also falls back to that ffprobe command, so such files get
-ffprobe's value as in the reference.  Like the reference it never raises and
+``av_rescale(mvhd.duration, 1_000_000, mvhd.timescale) / 1e6`` (a fragmented
+MP4 whose mvhd says 0: the longest track's fragment samples, same rounding).
+For any other container it keeps the reference behaviour exactly: run ffprobe
+with the reference's arguments and 15 s timeout.  Where the native parser has
+no answer for an ISO-BMFF file (no ``mvhd``, a parse error, a zero duration)
+it also falls back to that ffprobe command, so such files get ffprobe's value
+as in the reference.  Like the reference it never raises and
 returns 0.0 on any failure (video_utils.py:28-38).
 """
 from __future__ import annotations
