@@ -1243,6 +1243,10 @@ def main() -> None:
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             cpu = {"value": round(nfr / secs, 2), "unit": "frames/s", "cores": threads, "kind": "port",
                    "host_cores": hc,
+                   "note": "the oracle: an unoptimised scalar C restatement of the decoder and scorer used as "
+                           "the parity checker, not an ffmpeg-class CPU decoder (ffmpeg, the reference's own "
+                           "path, is absent from the image); a GPU / CPU ratio from it says nothing about "
+                           "kernel quality",
                    "sample": f"the parity pass: {nfr} frames ({width}x{height}, {len(per_video)} "
                              f"videos) of the benchmark batch decoded by " +
                              ("oracle/h264_full_oracle.c fo_decode" if dec == "full" else

@@ -252,6 +252,12 @@ struct CabacSyn {
     const uint32_t tw = trn.get(ps);  // read on both paths: no branch
     range -= lpsr;
     const uint32_t rs = range << 23;
+    // (the LPS test as a scalar condition from the compare's lane mask, with
+    // bin and next state on the scalar unit: all-intra / content parse -2 %,
+    // noise +5 %: the scalar unit is what many parse waves share;
+    // profiles/r06o_cabac_uniform_decision_ab.json.  One state per dword in
+    // six lane tables, no byte fields: bit-exact on the CPU harness, the
+    // device parse of the real clip desynchronised; not kept)
     const bool lpsb = val >= rs;
     const uint32_t bin = mps ^ (lpsb ? 1u : 0u);
     const uint32_t ns = VTS_EU(((tw >> (lpsb ? 0u : 8u)) & 127u) ^ mps);
@@ -805,9 +811,10 @@ struct CabacSyn {
         qs = sig_q + static_cast<int>(e & 15u);
         ql = last_q + static_cast<int>((e >> 8) & 15u);
       } else {
-        const int inc = cat == 3 ? vts_min(i, 2) : i;
-        qs = vts_min(sig_q + inc, 165 - 85);
-        ql = vts_min(last_q + inc, 226 - 85);
+        // ctxIdxInc = i: Min(i, 2) of chroma DC (cat 3) is i too, its i <= 2
+        // (4 levels); the largest slots are 80 / 141 (cat 4, i = 13)
+        qs = sig_q + i;
+        ql = last_q + i;
       }
       if (dec_slot<kTab>(static_cast<uint32_t>(qs))) {
         sig |= Mask(1) << i;
