@@ -321,6 +321,11 @@ int vts_empty_cache(int device);
 /* Bytes of device memory the sessions' allocator has handed out on `device`
  * (open sessions' buffers; the cache's free ranges excluded). */
 int64_t vts_device_bytes(int device);
+/* Destroy the idle pooled HIP stream sets of `device` (< 0: every device);
+ * sets held by open sessions stay.  Returns the number of sets destroyed.
+ * Call before process exit when streams should not outlive the library
+ * (the Python loader does, at interpreter exit). */
+int vts_release_streams(int device);
 /* Host time of the vts_open that made ctx, milliseconds, by stage:
  * [0] demux (moov) + device checks, [1] unused, [2] sample read (parallel
  * pread), [3] host decode schedule, [4] device allocations (+ the general

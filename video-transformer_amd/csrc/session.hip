@@ -148,6 +148,28 @@ void streams_give(vts_ctx *c) {  // every stream idle
 
 }  // namespace
 
+// Destroy the idle pooled stream sets (device < 0: every device).  Sets held
+// by open sessions stay.  The library's Python loader calls it at interpreter
+// exit: streams left to the HIP runtime's own teardown crashed rocprofv3
+// --pmc runs at exit once CU-masked sets existed (__cxa_finalize, rc 139; the
+// counter files of the pass were lost — profiles/r06j..r06s bench lines).
+extern "C" int vts_release_streams(int device) {
+  clear_error();
+  std::lock_guard<std::mutex> lk(g_stream_mu);
+  int n = 0;
+  for (auto &kv : g_stream_sets) {
+    if (device >= 0 && kv.first.first != device) continue;
+    for (auto &set : kv.second) {
+      for (hipStream_t s : set)
+        if (s) (void)hipStreamDestroy(s);
+      ++n;
+      if (kv.first.second == 1) --g_own_sets[kv.first.first];
+    }
+    kv.second.clear();
+  }
+  return n;
+}
+
 namespace {
 
 double now_s() {

@@ -7,6 +7,7 @@ library is missing or stale every entry point raises ``VtsegLibraryError``.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 from pathlib import Path
@@ -174,6 +175,7 @@ SIGNATURES: dict[str, tuple] = {
     "vts_last_timings": (C.c_int, [C.c_void_p, _P(C.c_double)]),
     "vts_open_timings": (C.c_int, [C.c_void_p, _P(C.c_double), C.c_int32]),
     "vts_empty_cache": (C.c_int, [C.c_int]),
+    "vts_release_streams": (C.c_int, [C.c_int]),
     "vts_device_bytes": (C.c_int64, [C.c_int]),
     "vts_schedule_info": (C.c_int64, [C.c_void_p, C.c_int32]),
     "vts_close": (C.c_int, [C.c_void_p]),
@@ -222,6 +224,9 @@ def lib() -> C.CDLL:
     if handle.vts_abi_version() != ABI_VERSION:
         raise VtsegLibraryError("libvtseg ABI version mismatch; rebuild")
     _lib = handle
+    # pooled stream sets go before the HIP runtime's own teardown (rocprofv3
+    # --pmc runs crashed at exit otherwise; session.hip vts_release_streams)
+    atexit.register(handle.vts_release_streams, -1)
     return handle
 
 
