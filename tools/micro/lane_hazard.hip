@@ -5,7 +5,7 @@
 // with one wait state (s_nop 0) between, and another writelane between.  Each
 // runs 100 000 dependent rounds on one wave and counts rounds whose read
 // differs from the value written.  Inline asm, so the compiler's hazard
-// recognizer adds nothing.  Measured (profiles/r06t_lane_hazard.json): back
+// recognizer adds nothing.  Measured (profiles/r06u_lane_hazard.json): back
 // to back with constant lanes reads the stale lane (90 000 of 100 000; the
 // loop's tenth copy has other instructions between); one wait state, or any
 // instruction between, reads the new value.  The compiler puts that s_nop 0
