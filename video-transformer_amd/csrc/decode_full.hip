@@ -55,6 +55,11 @@ constexpr int kIntraSlots = kIntraThreads / 16;
 constexpr int kIntraLevels = 512;  // intra dependency levels bucketed in LDS (more: one scan per level)
 constexpr int kDbkThreads = VTS_DBK_THREADS;      // 1024: 16 waves = 16 row pairs in flight
 constexpr int kDbkWaves = kDbkThreads / 64;
+// experiment hook: per-workgroup start / end of the one-workgroup-per-picture
+// kernels (tools/exp/wg_trace.h); nothing in the product build
+#ifndef VTS_WG_TRACE
+#define VTS_WG_TRACE(kernel, end, key) ((void)0)
+#endif
 
 // One slice per wave: every value of the parse is
 // wave-uniform, so control flow never diverges and the integer work can go to
@@ -1443,7 +1448,9 @@ __device__ __forceinline__ void intra_v2_picture(const FullReconArgs &a, int slo
 // grid: pictures of the level; dynamic LDS: i2_lds_bytes
 __global__ void __launch_bounds__(kI2Threads) h264_intra_v2(FullReconArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_i2[];
+  VTS_WG_TRACE(1, 0, a.frames);
   intra_v2_picture(a, a.frames[blockIdx.x].x, s_i2);
+  VTS_WG_TRACE(1, 1, a.frames);
 }
 
 // --------------------------------------------------------------- deblocking
@@ -1930,11 +1937,13 @@ __device__ __forceinline__ void dp_plane(const FullReconArgs &a, int slot, int d
 __global__ void __launch_bounds__(kDbkThreads) h264_deblock_plane(FullReconArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kDpLds];
   __shared__ int prog[1024];  // per macroblock row: macroblocks finished (mbw + 1: row flushed)
+  VTS_WG_TRACE(0, 0, a.frames);
   for (int i = threadIdx.x; i < a.P.mb_height; i += kDbkThreads) prog[i] = 0;
   __syncthreads();
   const int4 f = a.frames[blockIdx.x >> 1];
   if ((blockIdx.x & 1) == 0) dp_plane<true>(a, f.x, f.y, lds, prog);
   else dp_plane<false>(a, f.x, f.y, lds, prog);
+  VTS_WG_TRACE(0, 1, a.frames);
 }
 
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s) {
