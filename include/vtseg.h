@@ -341,7 +341,8 @@ int vts_open_timings(const vts_ctx *ctx, double *ms, int32_t cap);
  * (0: one per window frame), 12 the session's HIP stream set (0 plain
  * streams on the process's shared hardware queues, 1 streams with hardware
  * queues of their own: sessions opened beside others, at most 3 such sets
- * per device); < 0 on error. */
+ * per device), 13 CABAC slices parsed in the windows' long-slice launches
+ * (0: every window one parse launch); < 0 on error. */
 int64_t vts_schedule_info(const vts_ctx *ctx, int32_t what);  /* 8: general decoder in use (1/0) */
 int vts_close(vts_ctx *ctx);
 

@@ -46,6 +46,12 @@ struct Window {
                                    // [plv_end[j-1], plv_end[j]) (B pictures after their colocated picture)
   int64_t ds0 = 0;                 // general decoder, CABAC: the window's entries in vts_ctx::dslots
   std::vector<int32_t> dlv_end;    // ... h264_derive launch j covers entries [dlv_end[j-1], dlv_end[j])
+  // CABAC: the window's plong longest slices (porder_m's first entries) parse
+  // in a launch of their own, the rest in one beside it, with the derivation
+  // of every picture that needs none of the long ones (the first dlv_early[j]
+  // entries of derive launch j); 0: one parse launch
+  int32_t plong = 0;
+  std::vector<int32_t> dlv_early;
 };
 
 // Downscaled copy of every decoded frame (transcode.hip), filled by run_all
@@ -196,6 +202,9 @@ struct vts_ctx {
                                         // common colocated slot
   int2 *d_dslots = nullptr;
   int intra_kernel = 2;                 // 2: h264_intra_v2; VTS_INTRA=1: h264_intra_full (its LDS fallback)
+  int parse_split = 1;                  // CABAC: long slices in a parse launch of their own (VTS_PARSE_SPLIT:
+                                        // 0 one launch, 2 the longest eighth whatever the sizes, a test mode)
+  std::vector<hipEvent_t> ev_px;        // per window: arena reset done, short parse + early derives done
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<hipEvent_t> ev_bs;  // paced bS: two per level launch of a window (reused window to window)
   // recycled surfaces (keep_frames 0, no transcode): a picture's surface

@@ -1657,6 +1657,11 @@ extern "C" int64_t vts_schedule_info(const vts_ctx *c, int32_t what) {
     case 10: return c->arena_blocks;                // coefficient blocks per ring (general decoder)
     case 11: return c->surf_pool ? c->surf_count : 0;  // recycled surfaces per ring (general decoder)
     case 12: return c->s_dec ? c->stream_kind : -1;   // stream set: 0 plain, 1 own hardware queues
+    case 13: {  // CABAC: slices parsed in the windows' long-slice launches (0: one launch per window)
+      int64_t n = 0;
+      for (const Window &w : c->windows) n += w.plong;
+      return n;
+    }
     default: return fail(VTS_E_INVALID, "unknown schedule field %d", what);
   }
 }
@@ -1717,6 +1722,8 @@ extern "C" int vts_close(vts_ctx *c) {
   for (auto e : c->lev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->ev_bs)
+    if (e) (void)hipEventDestroy(e);
+  for (auto e : c->ev_px)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);

@@ -321,6 +321,10 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
     // to back (a B slice waits for its colocated picture's slices, which
     // therefore come first); CABAC, every slice of the window longest first
     // (its slices are independent: h264_derive does the colocated reads)
+    // (CABAC) late[slot]: the picture has one of the window's long slices, or
+    // its colocated picture is late — its derivation waits for the long parse
+    std::vector<uint8_t> late(static_cast<size_t>(w.f1 - w.f0), 0);
+    w.plong = 0;
     if (c->fprm.cabac) {
       const int64_t nws = static_cast<int64_t>(c->fslices.size()) - w.fs0;
       const size_t o0 = c->porder_m.size();
@@ -328,6 +332,29 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
       std::stable_sort(c->porder_m.begin() + static_cast<int64_t>(o0), c->porder_m.end(), [&](int32_t a, int32_t b) {
         return c->fslices[static_cast<size_t>(w.fs0 + a)].nal_size > c->fslices[static_cast<size_t>(w.fs0 + b)].nal_size;
       });
+      // The launch ends on its longest slices (an x264 stream's intra
+      // pictures: one wave's serial bin chain each, several times the others'
+      // time).  Those of at least a quarter of the longest's size parse in a
+      // launch of their own when they are at most 1/8 of the window's slices;
+      // the rest parse beside them, and every picture that needs none of them
+      // (its slices all short, its colocated pictures early) is derived
+      // while the long ones still parse.
+      // (VTS_PARSE_SPLIT=0: one launch; 2, a test mode: the longest eighth,
+      // whatever the sizes)
+      const char *ps = std::getenv("VTS_PARSE_SPLIT");
+      c->parse_split = ps ? std::min(std::max(std::atoi(ps), 0), 2) : 1;
+      if (c->parse_split && nws > 1) {
+        auto size_at = [&](int64_t k) { return c->fslices[static_cast<size_t>(w.fs0 + c->porder_m[o0 + static_cast<size_t>(k)])].nal_size; };
+        const int64_t mx = size_at(0);
+        int64_t k = 0;
+        while (k < nws && 4 * static_cast<int64_t>(size_at(k)) >= mx) ++k;
+        if (c->parse_split == 2) k = std::max<int64_t>(1, nws / 8);
+        if (k < nws && 8 * k <= nws) {
+          w.plong = static_cast<int32_t>(k);
+          for (int64_t j = 0; j < k; ++j)
+            late[static_cast<size_t>(c->fslices[static_cast<size_t>(w.fs0 + c->porder_m[o0 + static_cast<size_t>(j)])].slot)] = 1;
+        }
+      }
     } else {
       for (size_t j = 0; j < w.plv_end.size(); ++j) {
         const int32_t b0 = j ? w.plv_end[j - 1] : 0;
@@ -341,7 +368,9 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
     // colocated words load with its own, or -1)
     w.ds0 = static_cast<int64_t>(c->dslots.size());
     w.dlv_end.clear();
+    w.dlv_early.clear();
     for (int32_t pl = 0; pl <= maxp; ++pl) {
+      std::vector<int2> early, lat;
       for (int64_t f = w.f0; f < w.f1; ++f) {
         if (plevel[static_cast<size_t>(f)] != pl) continue;
         const SchedFrame &fr = frames[static_cast<size_t>(f)];
@@ -352,8 +381,16 @@ int build_general(vts_ctx *c, const uint8_t *es, const std::vector<int64_t> &es_
           const int64_t cs = sl.ref1[0] >= 0 ? disp[static_cast<size_t>(sl.ref1[0])] - w.f0 : -1;
           col = (col == -2 || col == cs) ? cs : -1;
         }
-        c->dslots.push_back(make_int2(slot_of(f), static_cast<int32_t>(col < 0 ? -1 : col)));
+        const int16_t sf = slot_of(f);
+        for (int64_t cf : fr.cols) {  // (colocated pictures: lower parse levels, flags final)
+          const int64_t cslot = disp[static_cast<size_t>(cf)] - w.f0;
+          if (cslot < 0 || cslot >= w.f1 - w.f0 || late[static_cast<size_t>(cslot)]) late[static_cast<size_t>(sf)] = 1;
+        }
+        (late[static_cast<size_t>(sf)] ? lat : early).push_back(make_int2(sf, static_cast<int32_t>(col < 0 ? -1 : col)));
       }
+      c->dslots.insert(c->dslots.end(), early.begin(), early.end());
+      c->dslots.insert(c->dslots.end(), lat.begin(), lat.end());
+      w.dlv_early.push_back(static_cast<int32_t>(early.size()));
       w.dlv_end.push_back(static_cast<int32_t>(static_cast<int64_t>(c->dslots.size()) - w.ds0));
     }
     w.pn0 = static_cast<int64_t>(c->pneed.size());
@@ -579,7 +616,6 @@ int submit_general(vts_ctx *c) {
       pa.order = c->d_porder_m + w.fs0;
       pa.pdone = nullptr;
       pa.pneed = nullptr;
-      VTS_TRY(parse_full_launch(pa, sp));
       DeriveArgs da{};
       da.recs = c->d_recs[r];
       da.recs1 = c->d_recs1[r];
@@ -589,10 +625,43 @@ int submit_general(vts_ctx *c) {
       da.err = c->d_err;
       da.epoch = epoch;
       da.P = c->fprm;
-      for (size_t j = 0; j < w.dlv_end.size(); ++j) {
-        const int32_t b0 = j ? w.dlv_end[j - 1] : 0;
-        da.pics = c->d_dslots + w.ds0 + b0;
-        VTS_TRY(derive_launch(da, w.dlv_end[j] - b0, sp));
+      // the long slices on the parse stream; the others, then the early
+      // pictures' derivation, on a stream the reconstruction leaves idle (a
+      // third GOP group's, unused at two groups)
+      hipStream_t sx = w.plong > 0 && c->general_groups <= 2 ? c->s_grp[1] : nullptr;
+      if (sx) {
+        if (c->ev_px.size() < 2 * nw) {
+          const size_t n0 = c->ev_px.size();
+          c->ev_px.resize(2 * nw, nullptr);
+          for (size_t k = n0; k < c->ev_px.size(); ++k) HIP_TRY(hipEventCreateWithFlags(&c->ev_px[k], hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(c->ev_px[2 * wi], sp));  // the ring's records and the arena counter are reset
+        HIP_TRY(hipStreamWaitEvent(sx, c->ev_px[2 * wi], 0));
+        FullParseArgs ps = pa;
+        ps.order = c->d_porder_m + w.fs0 + w.plong;
+        ps.n_slices = pa.n_slices - w.plong;
+        VTS_TRY(parse_full_launch(ps, sx));
+        pa.n_slices = w.plong;
+        VTS_TRY(parse_full_launch(pa, sp));
+        for (size_t j = 0; j < w.dlv_end.size(); ++j) {
+          const int32_t b0 = j ? w.dlv_end[j - 1] : 0;
+          da.pics = c->d_dslots + w.ds0 + b0;
+          VTS_TRY(derive_launch(da, w.dlv_early[j], sx));
+        }
+        HIP_TRY(hipEventRecord(c->ev_px[2 * wi + 1], sx));
+        HIP_TRY(hipStreamWaitEvent(sp, c->ev_px[2 * wi + 1], 0));
+        for (size_t j = 0; j < w.dlv_end.size(); ++j) {
+          const int32_t b0 = (j ? w.dlv_end[j - 1] : 0) + w.dlv_early[j];
+          da.pics = c->d_dslots + w.ds0 + b0;
+          VTS_TRY(derive_launch(da, w.dlv_end[j] - b0, sp));
+        }
+      } else {
+        VTS_TRY(parse_full_launch(pa, sp));
+        for (size_t j = 0; j < w.dlv_end.size(); ++j) {
+          const int32_t b0 = j ? w.dlv_end[j - 1] : 0;
+          da.pics = c->d_dslots + w.ds0 + b0;
+          VTS_TRY(derive_launch(da, w.dlv_end[j] - b0, sp));
+        }
       }
     } else if (c->parse_merged && w.plv_end.size() > 1) {
       // one launch: B slices wait for their colocated pictures' slices, which
