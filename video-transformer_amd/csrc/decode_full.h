@@ -99,6 +99,8 @@ int nal_unescape_launch(const uint8_t *es, uint8_t *rbsp, const FullSlice *slice
                         int32_t *rbsp_len, hipStream_t s);
 int parse_full_launch(const FullParseArgs &a, hipStream_t s);
 int derive_launch(const DeriveArgs &a, int n_pictures, hipStream_t s);
+// a one-wave kernel that returns after `us` microseconds (stream_delay)
+int delay_launch(uint32_t us, hipStream_t s);
 // deblocking descriptors (bS, QPs) of n_frames pictures: reads only the
 // parse's records, so one launch covers a whole window
 int bs_full_launch(const FullReconArgs &a, int n_frames, hipStream_t s);

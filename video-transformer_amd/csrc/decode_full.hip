@@ -1681,6 +1681,20 @@ size_t derive_lds_bytes(int mb_height) {
   return sizeof(full::DWork) * static_cast<size_t>(threads) + sizeof(full::DEdge) * 5 * static_cast<size_t>(mb_height);
 }
 
+// one wave that returns after `us` microseconds (the 100 MHz real-time
+// counter): what a stream runs before a launch that must not be dispatched
+// ahead of another queue's
+__global__ void __launch_bounds__(64) stream_delay(uint32_t us) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), n = 100ull * us;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < n) __builtin_amdgcn_s_sleep(8);
+}
+int delay_launch(uint32_t us, hipStream_t s) {
+  hipLaunchKernelGGL(stream_delay, dim3(1), dim3(64), 0, s, us);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(VTS_E_HIP, "stream_delay launch: %s", hipGetErrorString(e));
+  return VTS_OK;
+}
+
 int derive_launch(const DeriveArgs &a, int n_pictures, hipStream_t s) {
   if (n_pictures <= 0) return VTS_OK;
   if (a.P.mb_height > 256) return fail(VTS_E_UNSUPPORTED, "picture taller than 256 macroblock rows (h264_derive)");

@@ -205,6 +205,9 @@ struct vts_ctx {
   int parse_split = 1;                  // CABAC: long slices in a parse launch of their own (VTS_PARSE_SPLIT:
                                         // 0 one launch, 2 the longest eighth whatever the sizes, a test mode)
   std::vector<hipEvent_t> ev_px;        // per window: arena reset done, short parse + early derives done
+  hipStream_t s_px = nullptr;           // the short parse's stream: a hardware queue of its own (CU mask of every
+                                        // compute unit), made on first use; a stream sharing the parse stream's
+                                        // queue would run after the long launch
   bool parse_merged = true;             // VTS_PARSE_MERGE=0: one launch per colocated level
   std::vector<hipEvent_t> ev_bs;  // paced bS: two per level launch of a window (reused window to window)
   // recycled surfaces (keep_frames 0, no transcode): a picture's surface

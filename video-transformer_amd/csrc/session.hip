@@ -1725,6 +1725,10 @@ extern "C" int vts_close(vts_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->ev_px)
     if (e) (void)hipEventDestroy(e);
+  if (c->s_px) {
+    (void)hipStreamSynchronize(c->s_px);
+    (void)hipStreamDestroy(c->s_px);
+  }
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_end) (void)hipEventDestroy(c->ev_end);
   for (int g = vts_ctx::kMaxGroups - 2; g >= 0; --g) {

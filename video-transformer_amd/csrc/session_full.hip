@@ -626,9 +626,23 @@ int submit_general(vts_ctx *c) {
       da.epoch = epoch;
       da.P = c->fprm;
       // the long slices on the parse stream; the others, then the early
-      // pictures' derivation, on a stream the reconstruction leaves idle (a
-      // third GOP group's, unused at two groups)
-      hipStream_t sx = w.plong > 0 && c->general_groups <= 2 ? c->s_grp[1] : nullptr;
+      // pictures' derivation, on a stream with a hardware queue of its own
+      // (HIP puts plain streams on its few queues in turn, and two streams on
+      // one queue run one after the other: the short launch would wait for
+      // the long one): a session on CU-masked streams (own queues) uses its
+      // third GOP group's, idle at two groups; one on plain streams makes one
+      // (each stream on a queue of its own was measured: four content
+      // sessions through plan_batch 2.34x -> 2.72x one session's step, the
+      // process's queues being time-sliced)
+      const bool own_q = c->stream_kind == 1 && c->general_groups <= 2;
+      if (w.plong > 0 && !own_q && !c->s_px) {
+        int cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+        std::vector<uint32_t> mask(static_cast<size_t>((cus + 31) / 32), 0u);
+        for (int i = 0; i < cus; ++i) mask[static_cast<size_t>(i >> 5)] |= 1u << (i & 31);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&c->s_px, static_cast<uint32_t>(mask.size()), mask.data()));
+      }
+      hipStream_t sx = w.plong > 0 ? (own_q ? c->s_grp[1] : c->s_px) : nullptr;
       if (sx) {
         if (c->ev_px.size() < 2 * nw) {
           const size_t n0 = c->ev_px.size();
@@ -637,12 +651,17 @@ int submit_general(vts_ctx *c) {
         }
         HIP_TRY(hipEventRecord(c->ev_px[2 * wi], sp));  // the ring's records and the arena counter are reset
         HIP_TRY(hipStreamWaitEvent(sx, c->ev_px[2 * wi], 0));
+        pa.n_slices = w.plong;
         FullParseArgs ps = pa;
         ps.order = c->d_porder_m + w.fs0 + w.plong;
-        ps.n_slices = pa.n_slices - w.plong;
-        VTS_TRY(parse_full_launch(ps, sx));
-        pa.n_slices = w.plong;
+        ps.n_slices = static_cast<int32_t>(w.fs1 - w.fs0) - w.plong;
         VTS_TRY(parse_full_launch(pa, sp));
+        // the long slices' waves are the window's critical path: their launch
+        // is dispatched before the short one's thousands of waves fill the
+        // compute units (two queues' launches start in either order; without
+        // this the content parse measured 130 or 157 ms run to run)
+        VTS_TRY(delay_launch(50, sx));
+        VTS_TRY(parse_full_launch(ps, sx));
         for (size_t j = 0; j < w.dlv_end.size(); ++j) {
           const int32_t b0 = j ? w.dlv_end[j - 1] : 0;
           da.pics = c->d_dslots + w.ds0 + b0;
