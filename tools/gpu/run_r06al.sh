@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 6 (al): the significance / last flags' context words held in
+# registers across a block's positions — the GPU suite, then A/B against the
+# previous build (tools/exp/lib_base.so) on the all-intra, content and noise
+# streams
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r06al
+mkdir -p $O
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/gpu/write_streams.py content 18000 /tmp/c0.mp4 || exit $?
+PASSES=2 bash tools/gpu/lib_ab.sh /tmp/c0.mp4 3 $O/content base cur || exit $?
+timeout -k 10 300 python -u tools/gpu/write_streams.py noise 18000 /tmp/n0.mp4 || exit $?
+PASSES=1 bash tools/gpu/lib_ab.sh /tmp/n0.mp4 2 $O/noise base cur || exit $?
