@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 6 (am): the round's final tree — the GPU suite, smoke(), then the
+# default bench line with its profiler passes (kernel-trace stats and the PMC
+# HBM-traffic passes)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r06am
+mkdir -p $O
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+rc=$?; tail -2 $O/smoke.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python -u bench.py --profile-dir $O/prof > $O/bench.json 2> $O/bench.err
+rc=$?
+tail -12 $O/bench.err
+exit $rc
