@@ -812,6 +812,13 @@ def e2e_record(paths: list[Path], gpu: int) -> dict:
     stages timed one by one on the first video."""
     import torch
     from vtseg import batch, scene
+    # the record's inputs are page-cache resident, as it says: read once before
+    # the clock starts (the box may have evicted the files since they were
+    # written; from disk the same call measured 0.18 -> 1.49 s)
+    for p in paths:
+        with open(p, "rb") as fh:
+            while fh.read(1 << 24):
+                pass
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     items = batch.plan_batch([str(p) for p in paths], REF_CONFIG, score=True, device=gpu)
