@@ -55,6 +55,10 @@ constexpr int kIntraSlots = kIntraThreads / 16;
 constexpr int kIntraLevels = 512;  // intra dependency levels bucketed in LDS (more: one scan per level)
 constexpr int kDbkThreads = VTS_DBK_THREADS;      // 1024: 16 waves = 16 row pairs in flight
 constexpr int kDbkWaves = kDbkThreads / 64;
+// (a 256-thread build, 16 rows in flight, hung on the noise stream: its ring
+// hand-off between waves needs more rows in flight than one pass of 4 waves;
+// 512 ran, no faster: profiles/r06ar_*)
+static_assert(kDbkThreads >= 512 && kDbkThreads <= 1024 && kDbkThreads % 64 == 0, "deblocking workgroup size");
 // experiment hook: per-workgroup start / end of the one-workgroup-per-picture
 // kernels (tools/exp/wg_trace.h); nothing in the product build
 #ifndef VTS_WG_TRACE
