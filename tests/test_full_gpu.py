@@ -635,6 +635,30 @@ def test_sessions_reopened_in_sequence_reuse_the_stream_pool(tmp_path):
         assert np.array_equal(v.score().scores, ref["score"])
 
 
+def test_released_stream_sets_are_made_again(tmp_path):
+    """vts_release_streams destroys the idle pooled stream sets (a session's
+    stays while it is open); sessions opened afterwards make new sets and
+    still equal the oracle (the loader calls it at interpreter exit)."""
+    _require_gpu()
+    from vtseg import _lib
+    n = 36
+    path = tmp_path / "rel.mp4"
+    scene.synth_write(path, width=176, height=144, n_frames=n, coding="full", bframes=True, cabac=True,
+                      weighted="implicit", cut_min_s=0.5, cut_max_s=1.2, gop_max_s=0.5, seed=29)
+    frames, _ = oracle.decode_full(path)
+    ref = oracle.score_frames(frames.reshape(-1), frames[0].size, n, 176, 144, 176, 144, 4)
+    L = _lib.lib()
+    with scene.VideoScorer(path) as a, scene.VideoScorer(path) as b:
+        assert np.array_equal(a.score().scores, ref["score"]) and np.array_equal(b.score().sad, ref["sad"])
+        assert L.vts_release_streams(0) >= 0  # the open sessions' sets are not idle: kept
+        assert np.array_equal(a.score().hist, ref["hist"])
+    assert L.vts_release_streams(-1) >= 2  # both sets idle now
+    assert L.vts_release_streams(-1) == 0
+    for _ in range(2):
+        with scene.VideoScorer(path) as v:
+            assert np.array_equal(v.score().scores, ref["score"])
+
+
 CONTENT = [
     ("qvga", dict(width=320, height=240), 90),
     ("crop_rows", dict(width=320, height=180, slices_per_row=2), 60),
